@@ -1,0 +1,134 @@
+"""The training driver: models, flat params, Adam, DP, scenario sampling, logging, ckpt.
+
+Reference: ``train.py:26-105`` (one env, one process, host scenario sampling, two Adams,
+tqdm, no logging/ckpt). Here one ``train_step`` is::
+
+    sample B envs (rank-sharded, counter-based RNG)      -> s0 (B,N,4), g (B,N,2)
+    engine.step(s0, g)  # rollout + losses + grads into the flat grad buffer
+    DP all-reduce(flat grad)                              (one RCCL call)
+    Adam on the controller / CBF ranges                   (joint, or alternating)
+    engine.after_update()                                 (repack bf16 MFMA fragments)
+
+``engine`` is the HIP engine on a GPU (native kernels, no autograd) or the pure-torch
+oracle engine on CPU.
+"""
+from __future__ import annotations
+
+import time
+from typing import Optional
+
+import numpy as np
+import torch
+
+from .. import config as C
+from .. import env as E
+from ..models import CBF, Controller
+from ..parallel import DP
+from ..utils.params import FlatParams, FlatAdam
+from ..utils.metrics import MetricsLogger
+from ..utils import ckpt
+
+
+def resolve_device(name: str, local_rank: int = 0) -> torch.device:
+    if name in ("auto", None):
+        name = "hip" if torch.cuda.is_available() else "cpu"
+    if name in ("hip", "cuda", "gpu"):
+        if not torch.cuda.is_available():
+            raise RuntimeError("HIP device requested but torch.cuda.is_available() is False")
+        return torch.device("cuda", local_rank % max(torch.cuda.device_count(), 1))
+    return torch.device("cpu")
+
+
+class Trainer:
+    def __init__(self, cfg: C.TrainConfig, device: Optional[torch.device] = None, dp: Optional[DP] = None):
+        self.cfg = cfg
+        if dp is None:
+            from ..parallel import env_world
+            _, _, lr_ = env_world()
+            device = device or resolve_device(cfg.device, lr_)
+            if device.type == "cuda":
+                torch.cuda.set_device(device)
+            dp = DP(device=device)
+        self.dp = dp
+        self.device = device or resolve_device(cfg.device, dp.local_rank)
+        torch.manual_seed(cfg.seed)
+        self.controller = Controller(4).to(self.device)
+        self.cbf = CBF(4).to(self.device)
+        self.fp = FlatParams({"controller": self.controller, "cbf": self.cbf}, device=self.device)
+        dp.broadcast_(self.fp.flat)
+        self.opt = FlatAdam(self.fp, lr=cfg.lr, weight_decay=cfg.weight_decay)
+        self.step_count = 0
+        self.torch_gen = torch.Generator(device=self.device)
+        self.torch_gen.manual_seed(cfg.seed * 1000003 + dp.rank)
+        self.logger = MetricsLogger(dp, cfg.log_path)
+        if self.device.type == "cuda":
+            from .hip_engine import HipEngine
+            self.engine = HipEngine(self)
+        else:
+            from .oracle_engine import OracleEngine
+            self.engine = OracleEngine(self)
+        if cfg.model_path and _exists(cfg.model_path):
+            ckpt.load(self, cfg.model_path)
+
+    # ------------------------------------------------------------------ data
+    def sample(self, it: Optional[int] = None):
+        """B scenarios for this rank. HIP: on-device parallel sampler; CPU: host reference."""
+        it = self.step_count if it is None else it
+        B, N = self.cfg.num_envs, self.cfg.num_agents
+        if self.device.type == "cuda":
+            from ..ops import scenario
+            return scenario.generate(B, N, seed=self.cfg.seed, iteration=it, rank=self.dp.rank,
+                                     device=self.device)
+        seed = (self.cfg.seed * 1_000_003 + it) * 4099 + self.dp.rank
+        return E.generate_batch(B, N, C.DIST_MIN_THRES, seed=seed)
+
+    def on_params_loaded(self):
+        self.fp.rebind()
+        self.engine.after_update()
+
+    # ------------------------------------------------------------------ step
+    def groups_to_step(self):
+        k = self.cfg.alternate_every
+        if k <= 0:
+            return ["controller", "cbf"]
+        return ["controller"] if (self.step_count // k) % 2 == 0 else ["cbf"]
+
+    def train_step(self, s0=None, g=None):
+        if s0 is None:
+            s0, g = self.sample()
+        s0 = s0.to(self.device)
+        g = g.to(self.device)
+        stats = self.engine.step(s0, g)
+        self.dp.all_reduce_(self.fp.grad)
+        self.opt.step(self.groups_to_step())
+        self.engine.after_update()
+        self.step_count += 1
+        return stats
+
+    def fit(self, steps: Optional[int] = None, progress: bool = False):
+        steps = self.cfg.train_steps if steps is None else steps
+        it = range(steps)
+        if progress and self.dp.rank == 0:
+            try:
+                from tqdm import tqdm
+                it = tqdm(it)
+            except ImportError:
+                pass
+        last = None
+        for _ in it:
+            stats = self.train_step()
+            self.logger.update(stats)
+            if (self.step_count % max(self.cfg.display_steps, 1)) == 0:
+                last = self.logger.emit(self.step_count)
+            if self.cfg.model_path and (self.step_count % max(self.cfg.save_steps, 1)) == 0:
+                ckpt.save(self, self.cfg.model_path)
+                self.dp.barrier()
+        return last
+
+    def save(self, path):
+        ckpt.save(self, path)
+
+
+def _exists(p):
+    import os
+    return os.path.exists(p)

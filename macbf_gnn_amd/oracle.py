@@ -1,0 +1,288 @@
+"""Pure-PyTorch oracle of the *intended* MACBF semantics, batched over environments.
+
+This is the CPU reference path (BASELINE config #1) and the correctness oracle for every
+HIP kernel in ``csrc/``. It implements the reference with the fixes of the SURVEY.md
+section 2.4 defect register:
+
+* kNN keeps self at slot 0 and always returns indices (D3); K_eff = min(N, TOP_K).
+* per-edge features use the (N, K, C) -> per-edge layout, not the channel-scrambling
+  reshape (D12); the controller max-pools the *values* (D13).
+* the trajectory is a batch of per-timestep graphs (B, T, N, K), not one T*N scene (D14);
+  loss means are pooled over all valid (env, t, i, k) entries as in the reference's single
+  masked mean.
+* h' = CBF(s') on the time-t neighbour set (D10, ``reuse_nbr_idx``).
+
+Shapes: B envs, T steps, N agents, K neighbour slots. Functions accept any leading batch
+dims ``...`` in front of (N, ·).
+Reference cites: kNN ``core.py:234-250``; controller ``controller.py:31-63``; CBF
+``cbf.py:21-45``; TTC ``core.py:187-231``; losses ``core.py:89-184``; loop ``train.py:48-105``.
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, Optional
+
+import torch
+import torch.nn.functional as F
+
+from . import config as C
+
+
+# ----------------------------------------------------------------------------- graph
+def knn_idx(s: torch.Tensor, k: int) -> torch.Tensor:
+    """Indices of the k nearest agents (positions = s[..., :2]), nearest first.
+
+    Ties are broken by the lower agent index (stable sort), which is also what the HIP
+    kernel's strict-< insertion over ascending candidates produces. Self is slot 0.
+    """
+    p = s[..., :2]
+    d = p.unsqueeze(-2) - p.unsqueeze(-3)            # (..., N, N, 2): p_i - p_j
+    d2 = d[..., 0] * d[..., 0] + d[..., 1] * d[..., 1]
+    k = min(k, s.shape[-2])
+    return torch.sort(d2, dim=-1, stable=True).indices[..., :k]
+
+
+def gather_nbrs(s: torch.Tensor, idx: torch.Tensor) -> torch.Tensor:
+    """s (..., N, C), idx (..., N, K) -> s_j (..., N, K, C)."""
+    lead = s.shape[:-2]
+    N, Cc = s.shape[-2:]
+    K = idx.shape[-1]
+    sf = s.reshape(-1, N, Cc)
+    ix = idx.reshape(-1, N * K, 1).expand(-1, -1, Cc)
+    return torch.gather(sf, 1, ix).reshape(*lead, N, K, Cc)
+
+
+def edge_rel(s: torch.Tensor, idx: torch.Tensor):
+    """Relative state s_i - s_j (..., N, K, 4) and the self indicator (..., N, K)."""
+    sj = gather_nbrs(s, idx)
+    rel = s.unsqueeze(-2) - sj
+    ar = torch.arange(s.shape[-2], device=s.device).view(*([1] * (idx.dim() - 2)), -1, 1)
+    eye = (idx == ar).to(s.dtype)
+    return rel, eye
+
+
+# ----------------------------------------------------------------------------- safety
+def ttc_dangerous(rel: torch.Tensor, eye: torch.Tensor, r: float, ttc: float) -> torch.Tensor:
+    """Time-to-collision danger test on relative states (core.py:187-209 / 212-231).
+
+    Self pairs are shifted to p=(1,1) via ``eye`` (core.py:193-194). fp32 throughout.
+    """
+    x = rel[..., 0] + eye
+    y = rel[..., 1] + eye
+    vx = rel[..., 2]
+    vy = rel[..., 3]
+    alpha = vx * vx + vy * vy
+    beta = 2.0 * (x * vx + y * vy)
+    gamma = x * x + y * y - r * r
+    disc = beta * beta - 4.0 * alpha * gamma
+    dist_dang = gamma < 0
+    two_pos = (disc > 0) & (gamma > 0) & (beta < 0)
+    lt = (-beta - 2.0 * alpha * ttc < 0) | ((beta + 2.0 * alpha * ttc) ** 2 < disc)
+    return dist_dang | (two_pos & lt)
+
+
+def ttc_mask_knn(s: torch.Tensor, idx: torch.Tensor) -> torch.Tensor:
+    """Training danger mask on the top-K pairs, r=DIST_MIN_THRES, ttc=TIME_TO_COLLISION."""
+    rel, eye = edge_rel(s, idx)
+    return ttc_dangerous(rel, eye, C.DIST_MIN_THRES, C.TIME_TO_COLLISION)
+
+
+def ttc_mask_all_pairs(s: torch.Tensor) -> torch.Tensor:
+    """Check mask on all pairs (core.py:212-231) -> (..., N, N) bool."""
+    rel = s.unsqueeze(-2) - s.unsqueeze(-3)
+    N = s.shape[-2]
+    eye = torch.eye(N, dtype=s.dtype, device=s.device).expand(rel.shape[:-1])
+    return ttc_dangerous(rel, eye, C.DIST_MIN_CHECK, C.TIME_TO_COLLISION_CHECK)
+
+
+def safe_agent_count(s: torch.Tensor) -> torch.Tensor:
+    """Number of agents with no dangerous pair, per leading index (train.py:74-75)."""
+    return (~ttc_mask_all_pairs(s).any(-1)).sum(-1)
+
+
+# ----------------------------------------------------------------------------- networks
+def _lin(x, w, b):
+    if w.dim() == 3:          # Conv1d(k=1) weight (out, in, 1)
+        w = w[..., 0]
+    return F.linear(x, w, b)
+
+
+def controller_forward(p: Dict[str, torch.Tensor], s, g, idx, return_aux=False):
+    """Gain-scheduled GNN controller (controller.py:31-63), intended semantics.
+
+    ``p`` is the controller ``state_dict`` (or named parameters) keyed like the reference.
+    """
+    rel, eye = edge_rel(s, idx)
+    x = torch.cat([rel, eye.unsqueeze(-1)], dim=-1)                     # (...,N,K,5)
+    dist = torch.sqrt(rel[..., 0] ** 2 + rel[..., 1] ** 2)
+    mask = (dist < C.OBS_RADIUS).to(s.dtype)                            # strict, no eps
+    h = F.relu(_lin(x, p["controller_centr_net.0.weight"], p["controller_centr_net.0.bias"]))
+    h = F.relu(_lin(h, p["controller_centr_net.2.weight"], p["controller_centr_net.2.bias"]))
+    pooled = (h * mask.unsqueeze(-1)).max(dim=-2).values                # (...,N,128)
+    z = torch.cat([pooled, s[..., :2] - g, s[..., 2:4]], dim=-1)
+    for i, act in ((0, True), (2, True), (4, True), (6, False)):
+        z = _lin(z, p[f"controller_dec_net.{i}.weight"], p[f"controller_dec_net.{i}.bias"])
+        if act:
+            z = F.relu(z)
+    k = 2.0 * torch.sigmoid(z) + 0.2
+    ex = s[..., 0] - g[..., 0]
+    ey = s[..., 1] - g[..., 1]
+    ax = -(k[..., 0] * ex + k[..., 1] * s[..., 2])
+    ay = -(k[..., 2] * ey + k[..., 3] * s[..., 3])
+    a = torch.stack([ax, ay], dim=-1)
+    if return_aux:
+        return a, {"gains": k, "pooled": pooled, "mask": mask}
+    return a
+
+
+def cbf_features(s, idx):
+    rel, eye = edge_rel(s, idx)
+    d = torch.sqrt(rel[..., 0] ** 2 + rel[..., 1] ** 2 + C.CBF_DIST_EPS)
+    x = torch.cat([rel, eye.unsqueeze(-1), (d - C.DIST_MIN_THRES).unsqueeze(-1)], dim=-1)
+    mask = (d <= C.OBS_RADIUS).to(s.dtype)
+    return x, mask
+
+
+def cbf_forward(p: Dict[str, torch.Tensor], s, idx):
+    """Per-edge barrier h(x_i, x_j) (cbf.py:21-45) -> (..., N, K); masked by radius."""
+    x, mask = cbf_features(s, idx)
+    z = x
+    for i, act in ((0, True), (2, True), (4, True), (6, False)):
+        z = _lin(z, p[f"cbf_net.{i}.weight"], p[f"cbf_net.{i}.bias"])
+        if act:
+            z = F.relu(z)
+    return z[..., 0] * mask
+
+
+# ----------------------------------------------------------------------------- losses
+def action_ref(s, g):
+    """a_ref = [p-g, v] K_ref^T with K_ref = -[[1,0,sqrt3,0],[0,1,0,sqrt3]] (core.py:175-178)."""
+    return torch.stack([-((s[..., 0] - g[..., 0]) + C.SQRT3 * s[..., 2]),
+                        -((s[..., 1] - g[..., 1]) + C.SQRT3 * s[..., 3])], dim=-1)
+
+
+def action_loss_terms(s, g, a):
+    """|‖a‖² − ‖a_ref‖²| per agent (core.py:174-184 before the mean)."""
+    ar = action_ref(s, g)
+    return ((a * a).sum(-1) - (ar * ar).sum(-1)).abs()
+
+
+def cbf_loss_sums(h, h_next, dang, valid):
+    """Raw sums of the 8 barrier/derivative terms + 2 counts (no normalisation).
+
+    h, h_next, dang: (B,T,N,K); valid: (B,T) bool. Returns dict of 0-d tensors.
+    """
+    w = valid.to(h.dtype)[..., None, None]
+    dm = dang.to(h.dtype) * w
+    sm = (1.0 - dang.to(h.dtype)) * w
+    deriv = h_next - h + C.TIME_STEP * C.ALPHA_CBF * h
+    return {
+        "n_dang": dm.sum(), "n_safe": sm.sum(),
+        "loss_dang": (F.relu(h + C.LOSS_EPS_DANG) * dm).sum(),
+        "loss_safe": (F.relu(-h) * sm).sum(),
+        "acc_dang": ((h <= 0).to(h.dtype) * dm).sum(),
+        "acc_safe": ((h > 0).to(h.dtype) * sm).sum(),
+        "loss_dang_deriv": (F.relu(-deriv + C.LOSS_EPS_DANG) * dm).sum(),
+        "loss_safe_deriv": (F.relu(-deriv) * sm).sum(),
+        "acc_dang_deriv": ((deriv >= 0).to(h.dtype) * dm).sum(),
+        "acc_safe_deriv": ((deriv > 0).to(h.dtype) * sm).sum(),
+    }
+
+
+def finalize_losses(sums, n_act_sum, n_act):
+    """Normalise pooled sums like core.py:113-127 / 155-169 and weight like train.py:93-98."""
+    nd = 1e-5 + sums["n_dang"]
+    ns = 1e-5 + sums["n_safe"]
+    out = {
+        "loss_dang": sums["loss_dang"] / nd,
+        "loss_safe": sums["loss_safe"] / ns,
+        "loss_dang_deriv": sums["loss_dang_deriv"] / nd,
+        "loss_safe_deriv": sums["loss_safe_deriv"] / ns,
+        "loss_action": n_act_sum / max(float(n_act), 1.0),
+    }
+    neg = torch.tensor(-1.0, dtype=nd.dtype, device=nd.device)
+    has_d = sums["n_dang"] > 0
+    has_s = sums["n_safe"] > 0
+    out["acc_dang"] = torch.where(has_d, sums["acc_dang"] / nd, neg)
+    out["acc_safe"] = torch.where(has_s, sums["acc_safe"] / ns, neg)
+    out["acc_dang_deriv"] = torch.where(has_d, sums["acc_dang_deriv"] / nd, neg)
+    out["acc_safe_deriv"] = torch.where(has_s, sums["acc_safe_deriv"] / ns, neg)
+    w = C.LOSS_WEIGHTS
+    out["total"] = C.LOSS_SCALE * (w[0] * out["loss_dang"] + w[1] * out["loss_safe"]
+                                   + w[2] * out["loss_dang_deriv"] + w[3] * out["loss_safe_deriv"]
+                                   + w[4] * out["loss_action"])
+    return out
+
+
+# ----------------------------------------------------------------------------- rollout
+def rollout(ctrl_params, s0, g, *, top_k=C.TOP_K, inner_loops=C.INNER_LOOPS, bptt=True,
+            early_stop=True, noise_prob=0.0, noise_scale=C.NOISE_SCALE, generator=None,
+            compute_safety=False):
+    """Batched rollout with per-env done masks (train.py:58-81).
+
+    Returns dict with S (B,T+1,N,4), A (B,T,N,2), idx (B,T,N,K), valid (B,T) bool,
+    dist (B,T) mean goal distance after each step, safe (B,T) safe-agent counts of s_{t+1}.
+    """
+    B = s0.shape[0]
+    s = s0
+    active = torch.ones(B, dtype=torch.bool, device=s0.device)
+    S, A, I, V, D, SF = [s0], [], [], [], [], []
+    for _ in range(inner_loops):
+        idx = knn_idx(s.detach(), top_k)
+        a = controller_forward(ctrl_params, s, g, idx)
+        if noise_prob > 0:
+            coin = torch.rand(B, generator=generator, device=s.device) < noise_prob
+            nz = torch.randn(a.shape, generator=generator, device=s.device) * noise_scale
+            a = a + nz * coin[:, None, None].to(a.dtype)
+        s_next = s + torch.cat([s[..., 2:], a], -1) * C.TIME_STEP
+        dist = torch.linalg.norm(s_next[..., :2] - g, dim=-1).mean(-1)
+        V.append(active.clone())
+        A.append(a)
+        I.append(idx)
+        D.append(dist.detach())
+        if compute_safety:
+            SF.append(safe_agent_count(s_next.detach()))
+        S.append(s_next)
+        active = active & ~(dist.detach() < C.DIST_MIN_CHECK)
+        s = s_next if bptt else s_next.detach()
+        if early_stop and not bool(active.any()):
+            break
+    out = {"S": torch.stack(S, 1), "A": torch.stack(A, 1), "idx": torch.stack(I, 1),
+           "valid": torch.stack(V, 1), "dist": torch.stack(D, 1)}
+    if compute_safety:
+        out["safe"] = torch.stack(SF, 1)
+    if not bptt:
+        # keep s_{t+1} connected to a_t for h' but detach s_t inputs (upstream-MACBF mode)
+        out["S_in"] = torch.stack([S[0]] + [x.detach() for x in S[1:]], 1)
+    return out
+
+
+def train_losses(ctrl_params, cbf_params, traj, g, *, n_counts: Optional[Dict] = None,
+                 reuse_nbr_idx=True, top_k=C.TOP_K):
+    """All losses of one iteration from a rollout (train.py:83-98, intended semantics).
+
+    ``n_counts`` overrides the pooled counts (n_dang, n_safe, n_act) -- used by DP so that
+    every rank normalises by the global counts and the summed gradient equals the
+    single-process gradient on the concatenated env batch.
+    """
+    S, A, idx, valid = traj["S"], traj["A"], traj["idx"], traj["valid"]
+    T = A.shape[1]
+    S_in = traj.get("S_in", S)
+    s_t = S_in[:, :T]
+    s_n = S[:, 1:T + 1]
+    h = cbf_forward(cbf_params, s_t, idx)
+    idx_n = idx if reuse_nbr_idx else knn_idx(s_n.detach(), top_k)
+    hn = cbf_forward(cbf_params, s_n, idx_n)
+    dang = ttc_mask_knn(S[:, :T].detach(), idx)
+    sums = cbf_loss_sums(h, hn, dang, valid)
+    gg = g.unsqueeze(1).expand(-1, T, -1, -1)
+    act = action_loss_terms(s_t, gg, A)
+    vf = valid.to(act.dtype)[..., None]
+    act_sum = (act * vf).sum()
+    n_act = float(vf.sum().item()) * S.shape[2]
+    if n_counts is not None:
+        sums = dict(sums)
+        sums["n_dang"] = torch.as_tensor(n_counts["n_dang"], dtype=h.dtype)
+        sums["n_safe"] = torch.as_tensor(n_counts["n_safe"], dtype=h.dtype)
+        n_act = float(n_counts["n_act"])
+    return finalize_losses(sums, act_sum, n_act), sums, act_sum

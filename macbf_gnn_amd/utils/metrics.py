@@ -1,0 +1,79 @@
+"""Metrics accumulation and JSONL logging.
+
+The reference collects loss/acc lists and never emits them (``train.py:43-45,93-96``) and
+has the safety rate commented out (``train.py:74-76``). Here every ``DISPLAY_STEPS`` the
+per-rank sums are all-reduced (one small collective) and rank 0 prints one JSON line:
+the 5 weighted losses, 4 accuracies, safety rate (fraction of agents with no dangerous
+pair under the ``core.py:212-231`` check, averaged over valid steps) and agent-steps/s.
+"""
+from __future__ import annotations
+
+import json
+import sys
+import time
+
+import torch
+
+from .. import config as C
+
+KEYS = ["loss_total", "loss_dang", "loss_safe", "loss_dang_deriv", "loss_safe_deriv", "loss_action",
+        "acc_dang_sum", "acc_safe_sum", "acc_dang_deriv_sum", "acc_safe_deriv_sum",
+        "n_dang", "n_safe", "agent_steps", "safe_agents", "T", "iters"]
+# keys whose per-rank values are already normalised by global counts (sum over ranks);
+# n_dang/n_safe are global already (divide by world after the sum)
+GLOBAL_KEYS = {"n_dang", "n_safe"}
+
+
+class MetricsLogger:
+    def __init__(self, dp, path=None, stream=sys.stdout):
+        self.dp = dp
+        self.path = path
+        self.stream = stream
+        self.reset()
+
+    def reset(self):
+        self.acc = {k: 0.0 for k in KEYS}
+        self.t0 = time.perf_counter()
+
+    def update(self, stats):
+        for k in KEYS:
+            if k == "iters":
+                self.acc[k] += 1
+            elif k in stats:
+                self.acc[k] += float(stats[k])
+
+    def summary(self, step):
+        vec = torch.tensor([self.acc[k] for k in KEYS], dtype=torch.float64)
+        if self.dp.enabled:
+            dev = self.dp.device if (self.dp.device is not None and self.dp.device.type == "cuda") else "cpu"
+            vec = vec.to(dev)
+            self.dp.all_reduce_(vec)
+            vec = vec.cpu()
+        d = dict(zip(KEYS, vec.tolist()))
+        w = max(self.dp.world, 1)
+        it = max(d["iters"] / w, 1.0)
+        dt = time.perf_counter() - self.t0
+        nd = d["n_dang"] / w
+        ns = d["n_safe"] / w
+        out = {"step": step, "iters": int(it)}
+        for k in ["loss_total", "loss_dang", "loss_safe", "loss_dang_deriv", "loss_safe_deriv", "loss_action"]:
+            out[k] = d[k] / it
+        out["acc_dang"] = d["acc_dang_sum"] / nd if nd > 0 else -1.0
+        out["acc_safe"] = d["acc_safe_sum"] / ns if ns > 0 else -1.0
+        out["acc_dang_deriv"] = d["acc_dang_deriv_sum"] / nd if nd > 0 else -1.0
+        out["acc_safe_deriv"] = d["acc_safe_deriv_sum"] / ns if ns > 0 else -1.0
+        out["safety_rate"] = d["safe_agents"] / d["agent_steps"] if d["agent_steps"] > 0 else 1.0
+        out["mean_T"] = d["T"] / (it * w)
+        out["agent_steps_per_s"] = d["agent_steps"] / max(dt, 1e-9)
+        return out
+
+    def emit(self, step):
+        out = self.summary(step)
+        if self.dp.rank == 0:
+            line = json.dumps(out)
+            print(line, file=self.stream, flush=True)
+            if self.path:
+                with open(self.path, "a") as f:
+                    f.write(line + "\n")
+        self.reset()
+        return out

@@ -1,0 +1,155 @@
+"""Flat fp32 parameter / gradient buffers and a flat Adam.
+
+All 51,141 trainable parameters (controller 34,052 + CBF 17,089) live in ONE
+contiguous fp32 buffer; the ``nn.Module`` parameters are views into it, so ``state_dict``
+keeps the reference keys while the native kernels, the single RCCL all-reduce and the fused
+Adam all work on one flat tensor (one 204.6 KB bucket, no DDP hooks).
+
+The two reference optimizers (``train.py:36-37``: Adam(lr=1e-4, weight_decay=1e-8) on the
+controller and on the CBF) are one flat Adam over two contiguous ranges with their own
+step counters; the math is ``torch.optim.Adam`` (L2 weight decay added to the gradient).
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Tuple
+
+import torch
+import torch.nn as nn
+
+
+class FlatParams:
+    """Owns the flat master buffer; module parameters become views into it."""
+
+    def __init__(self, modules: Dict[str, nn.Module], device=None):
+        self.modules = modules
+        self.specs: List[Tuple[str, str, torch.Size, int, int]] = []
+        self.ranges: Dict[str, Tuple[int, int]] = {}
+        off = 0
+        for mname, mod in modules.items():
+            start = off
+            for pname, p in mod.named_parameters():
+                self.specs.append((mname, pname, p.shape, off, p.numel()))
+                off += p.numel()
+            self.ranges[mname] = (start, off)
+        self.numel = off
+        dev = device if device is not None else next(iter(modules.values())).parameters().__next__().device
+        self.flat = torch.zeros(self.numel, dtype=torch.float32, device=dev)
+        self.grad = torch.zeros_like(self.flat)
+        with torch.no_grad():
+            for (mname, pname, shape, o, n), p in zip(self.specs, self._params()):
+                self.flat[o:o + n].copy_(p.detach().reshape(-1))
+        self.rebind()
+
+    def _params(self):
+        for mod in self.modules.values():
+            for _, p in mod.named_parameters():
+                yield p
+
+    def rebind(self):
+        """(Re)point every module parameter and its .grad at views of the flat buffers."""
+        for (mname, pname, shape, o, n), p in zip(self.specs, self._params()):
+            p.data = self.flat[o:o + n].view(shape)
+            p.grad = self.grad[o:o + n].view(shape)
+
+    def offset(self, mname: str, pname: str) -> int:
+        for m, pn, shape, o, n in self.specs:
+            if m == mname and pn == pname:
+                return o
+        raise KeyError((mname, pname))
+
+    def view(self, mname: str, pname: str) -> torch.Tensor:
+        for m, pn, shape, o, n in self.specs:
+            if m == mname and pn == pname:
+                return self.flat[o:o + n].view(shape)
+        raise KeyError((mname, pname))
+
+    def zero_grad(self):
+        self.grad.zero_()
+        self.rebind()
+
+    def sync_grads_from_modules(self):
+        """Autograd may replace a ``.grad`` view by a fresh tensor; fold those back in."""
+        for (mname, pname, shape, o, n), p in zip(self.specs, self._params()):
+            gv = self.grad[o:o + n]
+            if p.grad is None:
+                continue
+            if p.grad.data_ptr() != gv.data_ptr():
+                gv.copy_(p.grad.reshape(-1))
+        self.rebind()
+
+
+class FlatAdam:
+    """torch.optim.Adam semantics over contiguous ranges of a flat buffer.
+
+    ``step(group)`` updates one named range (or all). On a HIP device the update runs in
+    the fused ``adam`` kernel (``csrc/adam.hip``); on CPU in torch ops.
+    """
+
+    def __init__(self, fp: FlatParams, lr=1e-4, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0):
+        self.fp = fp
+        self.lr, self.betas, self.eps, self.wd = lr, betas, eps, weight_decay
+        self.exp_avg = torch.zeros_like(fp.flat)
+        self.exp_avg_sq = torch.zeros_like(fp.flat)
+        self.steps = {name: 0 for name in fp.ranges}
+
+    def step(self, groups=None):
+        groups = list(self.fp.ranges) if groups is None else list(groups)
+        for name in groups:
+            a, b = self.fp.ranges[name]
+            self.steps[name] += 1
+            t = self.steps[name]
+            if self.fp.flat.device.type != "cpu":
+                from ..ops import native
+                native.adam(self.fp.flat, self.fp.grad, self.exp_avg, self.exp_avg_sq, a, b,
+                            self.lr, self.betas[0], self.betas[1], self.eps, self.wd, t)
+            else:
+                self._step_torch(a, b, t)
+
+    def _step_torch(self, a, b, t):
+        b1, b2 = self.betas
+        p = self.fp.flat[a:b]
+        g = self.fp.grad[a:b]
+        if self.wd != 0:
+            g = g + self.wd * p
+        m = self.exp_avg[a:b]
+        v = self.exp_avg_sq[a:b]
+        m.mul_(b1).add_(g, alpha=1 - b1)
+        v.mul_(b2).addcmul_(g, g, value=1 - b2)
+        bc1 = 1 - b1 ** t
+        bc2 = 1 - b2 ** t
+        denom = (v.sqrt() / (bc2 ** 0.5)).add_(self.eps)
+        p.addcdiv_(m, denom, value=-self.lr / bc1)
+
+    # -- torch.optim.Adam-compatible state dicts (one per reference optimizer) ------------
+    def torch_state_dict(self, name: str) -> dict:
+        a, _ = self.fp.ranges[name]
+        state, ids = {}, []
+        i = 0
+        for m, pn, shape, o, n in self.fp.specs:
+            if m != name:
+                continue
+            if self.steps[name] > 0:
+                state[i] = {"step": torch.tensor(float(self.steps[name])),
+                            "exp_avg": self.exp_avg[o:o + n].view(shape).detach().cpu().clone(),
+                            "exp_avg_sq": self.exp_avg_sq[o:o + n].view(shape).detach().cpu().clone()}
+            ids.append(i)
+            i += 1
+        group = {"lr": self.lr, "betas": self.betas, "eps": self.eps, "weight_decay": self.wd,
+                 "amsgrad": False, "maximize": False, "foreach": None, "capturable": False,
+                 "differentiable": False, "fused": None, "decoupled_weight_decay": False,
+                 "params": ids}
+        return {"state": state, "param_groups": [group]}
+
+    def load_torch_state_dict(self, name: str, sd: dict):
+        i = 0
+        step = 0
+        for m, pn, shape, o, n in self.fp.specs:
+            if m != name:
+                continue
+            st = sd["state"].get(i, sd["state"].get(str(i)))
+            if st is not None:
+                self.exp_avg[o:o + n].copy_(st["exp_avg"].reshape(-1))
+                self.exp_avg_sq[o:o + n].copy_(st["exp_avg_sq"].reshape(-1))
+                step = int(float(st["step"]))
+            i += 1
+        self.steps[name] = step
