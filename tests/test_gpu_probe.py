@@ -1,0 +1,52 @@
+"""Device checks of the hardware layouts every fused kernel relies on (MI355X only):
+v_mfma_f32_32x32x16_bf16 operand/accumulator maps and ds_read_b64_tr_b16 semantics."""
+import numpy as np
+import pytest
+import torch
+
+from macbf_gnn_amd.ops import layout as L
+from macbf_gnn_amd.ops import native
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda")
+
+
+def test_mfma_layout_exact():
+    rng = np.random.default_rng(0)
+    A = rng.integers(-4, 5, size=(32, 16)).astype(np.float32)
+    B = rng.integers(-4, 5, size=(16, 32)).astype(np.float32)   # asymmetric
+    a = np.zeros((64, 8), np.float32)
+    b = np.zeros((64, 8), np.float32)
+    for l in range(64):
+        r, h = l & 31, l >> 5
+        a[l] = A[r, 8 * h:8 * h + 8]
+        b[l] = B[8 * h:8 * h + 8, r]
+    ta = torch.tensor(a, dtype=torch.bfloat16, device=DEV).contiguous()
+    tb = torch.tensor(b, dtype=torch.bfloat16, device=DEV).contiguous()
+    d = torch.zeros(64, 16, dtype=torch.float32, device=DEV)
+    assert native.lib().probe_mfma(ta.data_ptr(), tb.data_ptr(), d.data_ptr(), native.stream_handle()) == 0
+    torch.cuda.synchronize()
+    d = d.cpu().numpy()
+    D = np.zeros((32, 32), np.float32)
+    for l in range(64):
+        r, h = l & 31, l >> 5
+        for reg in range(16):
+            D[L.acc_row(reg, h), r] = d[l, reg]
+    np.testing.assert_array_equal(D, A @ B)
+
+
+@pytest.mark.parametrize("stride,e0,m0", [(64, 0, 0), (64, 16, 32), (72, 8, 0), (128, 0, 96)])
+def test_tr16_transposed_fragment(stride, e0, m0):
+    rows = 32 if stride <= 72 else 40
+    img = (np.arange(rows * stride) % 251).astype(np.float32).reshape(rows, stride)
+    t = torch.tensor(img, dtype=torch.bfloat16, device=DEV).contiguous()
+    out = torch.zeros(64, 8, dtype=torch.bfloat16, device=DEV)
+    assert native.lib().probe_tr(t.data_ptr(), rows, stride, e0, m0, out.data_ptr(), native.stream_handle()) == 0
+    torch.cuda.synchronize()
+    got = out.float().cpu().numpy()
+    exp = np.zeros((64, 8), np.float32)
+    for l in range(64):
+        r, h = l & 31, l >> 5
+        for j in range(8):
+            exp[l, j] = img[e0 + 8 * h + j, m0 + r]
+    np.testing.assert_array_equal(got, exp)

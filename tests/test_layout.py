@@ -1,0 +1,155 @@
+"""CPU checks of the MFMA fragment packing with a lane-level emulator of
+v_mfma_f32_32x32x16_bf16 (layouts from the CDNA4 guide). If these pass, the index
+arithmetic the HIP kernels rely on is consistent; the GPU tests then check the kernels."""
+import numpy as np
+import torch
+
+from macbf_gnn_amd.models import CBF, Controller
+from macbf_gnn_amd.ops import layout as L
+from macbf_gnn_amd.utils.params import FlatParams
+
+
+def _setup():
+    torch.manual_seed(0)
+    ctrl, cbf = Controller(4), CBF(4)
+    fp = FlatParams({"controller": ctrl, "cbf": cbf})
+    offs = {pn: o for (m, pn, shape, o, n) in fp.specs}
+    src = np.concatenate([fp.flat.numpy().astype(np.float64), [0.0, 1.0]])
+    return ctrl, cbf, fp, offs, src
+
+
+def _vals(packer, src, nflat):
+    return src[L.resolve(packer.index(), nflat)]
+
+
+def acc_to_mat(c):
+    """(64,16) accumulator regs -> (32,32) matrix D[row][col]."""
+    D = np.zeros((32, 32))
+    for l in range(64):
+        r, h = l & 31, l >> 5
+        for reg in range(16):
+            D[L.acc_row(reg, h), r] = c[l, reg]
+    return D
+
+
+def bias_init(b, mt):
+    c = np.zeros((64, 16))
+    for l in range(64):
+        h = l >> 5
+        for reg in range(16):
+            c[l, reg] = b[32 * mt + L.acc_row(reg, h)]
+    return c
+
+
+def test_emulated_cbf_chain_matches_mlp():
+    ctrl, cbf, fp, offs, src = _setup()
+    pk = L.cbf_packer(offs)
+    vals = _vals(pk, src, fp.numel)
+    fo = pk.offsets()
+    rng = np.random.default_rng(1)
+    X = rng.normal(size=(32, 6))          # 32 edges x 6 features
+    # B operand of layer 1: lane (edge r, h): hi features in h=0 (+const 1 at k=6), zeros in h=1
+    Fb = np.zeros((64, 8))
+    for l in range(64):
+        r, h = l & 31, l >> 5
+        if h == 0:
+            Fb[l, :6] = X[r]
+            Fb[l, 6] = 1.0
+    H1 = [np.maximum(L.emu_mfma(L.emu_frag(vals, fo["w1f"] + mt), Fb, np.zeros((64, 16))), 0) for mt in range(2)]
+    W2b = cbf.cbf_net[2].bias.detach().numpy()
+    H2 = []
+    for mt in range(4):
+        c = bias_init(W2b, mt)
+        for kk in range(4):
+            c = L.emu_mfma(L.emu_frag(vals, fo["w2"] + mt * 4 + kk), L.emu_acc_frag(H1[kk >> 1], kk & 1), c)
+        H2.append(np.maximum(c, 0))
+    b3 = cbf.cbf_net[4].bias.detach().numpy()
+    H3 = []
+    for mt in range(2):
+        c = bias_init(b3, mt)
+        for kk in range(8):
+            c = L.emu_mfma(L.emu_frag(vals, fo["w3"] + mt * 8 + kk), L.emu_acc_frag(H2[kk >> 1], kk & 1), c)
+        H3.append(np.maximum(c, 0))
+    got = np.concatenate([acc_to_mat(H3[0]), acc_to_mat(H3[1])], 0)     # (64, 32)
+    net = cbf.cbf_net
+    with torch.no_grad():
+        x = torch.tensor(X, dtype=torch.float32)
+        ref = torch.relu(torch.nn.functional.linear(x, net[0].weight[..., 0], net[0].bias))
+        ref = torch.relu(torch.nn.functional.linear(ref, net[2].weight[..., 0], net[2].bias))
+        ref = torch.relu(torch.nn.functional.linear(ref, net[4].weight[..., 0], net[4].bias))
+    np.testing.assert_allclose(got, ref.numpy().T, rtol=1e-4, atol=1e-5)
+
+    # backward data chain: dH2 = W3^T dH3 with w3t packed, dH1 = W2^T dH2 with w2t
+    dH3 = [rng.normal(size=(64, 16)) for _ in range(2)]
+    dH2 = []
+    for mt in range(4):
+        c = np.zeros((64, 16))
+        for kk in range(4):
+            c = L.emu_mfma(L.emu_frag(vals, fo["w3t"] + mt * 4 + kk), L.emu_acc_frag(dH3[kk >> 1], kk & 1), c)
+        dH2.append(c)
+    W3 = net[4].weight.detach().numpy()[..., 0]
+    ref2 = W3.T @ np.concatenate([acc_to_mat(d) for d in dH3], 0)
+    np.testing.assert_allclose(np.concatenate([acc_to_mat(d) for d in dH2], 0), ref2, rtol=1e-6, atol=1e-6)
+    dH1 = []
+    for mt in range(2):
+        c = np.zeros((64, 16))
+        for kk in range(8):
+            c = L.emu_mfma(L.emu_frag(vals, fo["w2t"] + mt * 8 + kk), L.emu_acc_frag(dH2[kk >> 1], kk & 1), c)
+        dH1.append(c)
+    W2 = net[2].weight.detach().numpy()[..., 0]
+    ref1 = W2.T @ ref2
+    np.testing.assert_allclose(np.concatenate([acc_to_mat(d) for d in dH1], 0), ref1, rtol=1e-6, atol=1e-6)
+    c = np.zeros((64, 16))
+    for kk in range(4):
+        c = L.emu_mfma(L.emu_frag(vals, fo["w1ft"] + kk), L.emu_acc_frag(dH1[kk >> 1], kk & 1), c)
+    W1 = net[0].weight.detach().numpy()[..., 0]
+    np.testing.assert_allclose(acc_to_mat(c)[:6], W1.T @ ref1, rtol=1e-6, atol=1e-6)
+
+
+def test_emulated_transposed_orientation():
+    """Z = H1^T W2^T with H1 (accumulator) as the A operand and ew2 as B fragments."""
+    ctrl, cbf, fp, offs, src = _setup()
+    pk = L.ctrl_packer(offs)
+    vals = _vals(pk, src, fp.numel)
+    fo = pk.offsets()
+    rng = np.random.default_rng(2)
+    H1 = rng.normal(size=(64, 32))     # 64 features x 32 edges (standard orientation)
+    acc = [np.zeros((64, 16)) for _ in range(2)]
+    for t in range(2):
+        for l in range(64):
+            r, h = l & 31, l >> 5
+            for reg in range(16):
+                acc[t][l, reg] = H1[32 * t + L.acc_row(reg, h), r]
+    W2 = ctrl.controller_centr_net[2].weight.detach().numpy()[..., 0]   # (128, 64)
+    for nt in range(4):
+        c = np.zeros((64, 16))
+        for kk in range(4):
+            # A = accumulator regs (Z = X^T B), B = packed ew2 fragment for column tile nt
+            c = L.emu_mfma(L.emu_acc_frag(acc[kk >> 1], kk & 1), L.emu_frag(vals, fo["ew2"] + nt * 4 + kk), c)
+        Z = acc_to_mat(c)                  # rows = edges, cols = features 32nt..
+        np.testing.assert_allclose(Z, (W2 @ H1).T[:, 32 * nt:32 * nt + 32], rtol=1e-6, atol=1e-6)
+
+
+def test_emulated_node_w1_natural():
+    ctrl, cbf, fp, offs, src = _setup()
+    pk = L.ctrl_packer(offs)
+    vals = _vals(pk, src, fp.numel)
+    fo = pk.offsets()
+    rng = np.random.default_rng(3)
+    P = rng.normal(size=(132, 32))          # node input: pooled 128 + state 4, 32 agents
+    Pb = np.zeros((144, 32))
+    Pb[:132] = P
+    Pb[132] = 1.0
+    out = []
+    for mt in range(2):
+        c = np.zeros((64, 16))
+        for kk in range(9):
+            b = np.zeros((64, 8))
+            for l in range(64):
+                r, h = l & 31, l >> 5
+                b[l] = Pb[16 * kk + 8 * h: 16 * kk + 8 * h + 8, r]
+            c = L.emu_mfma(L.emu_frag(vals, fo["nw1f"] + mt * 9 + kk), b, c)
+        out.append(acc_to_mat(c))
+    lin = ctrl.controller_dec_net[0]
+    ref = lin.weight.detach().numpy() @ P + lin.bias.detach().numpy()[:, None]
+    np.testing.assert_allclose(np.concatenate(out, 0), ref, rtol=1e-5, atol=1e-6)
