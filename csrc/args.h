@@ -43,6 +43,8 @@ struct CtrlArgs {
   float* act_sum;   long ac_env;      // per-env sum of |‖a‖² - ‖a_ref‖²| (may be null)
   const float2* noise; long n_env;    // additive action noise (may be null)
   float dt, obs_r, sqrt3;
+  bf16* pooled;     long p_env;       // (b,i,128) max-pooled edge features out (bf16), or null
+  uint8_t* argmax;  long am_env;      // (b,i,128) winning slot per feature (0xFF: no grad), or null
 };
 
 struct LossConsts {
@@ -51,9 +53,9 @@ struct LossConsts {
 
 struct CbfFwdArgs {
   const float4* S;  long s_env, s_step;   // state of (b,t,i): S[b*s_env + t*s_step + i]
-  const int* idx;                          // (B,T,N,K) contiguous
-  const uint8_t* dang;                     // (B,T,N,K) or null (all safe)
-  const uint8_t* valid;                    // (B,T) or null (all valid)
+  const int* idx;                          // (T,B,N,K) contiguous (time-major)
+  const uint8_t* dang;                     // (T,B,N,K) or null (all safe)
+  const uint8_t* valid;                    // (T,B) or null (all valid)
   int B, T, N, K;
   int two;                                 // also evaluate h' on s_{t+1}
   const bf16* wpack; int f_fwd;            // fragment offset of w1f (w2, w3 follow)
@@ -67,6 +69,79 @@ struct CbfFwdArgs {
   float obs_r, dist_thr, dist_eps;
 };
 
+struct CbfBwdArgs {
+  const float4* S;  long s_env, s_step;   // state of (b,t,i): S[b*s_env + t*s_step + i]
+  const int* idx;                          // (T,B,N,K) time-major
+  int B, T, N, K;
+  int passes;                              // evaluations = passes*E; pass p reads states at t+p
+  const float* dh;                         // (passes, E) upstream dL/dh (radius mask folded in)
+  const bf16* wpack; int f_bwd;            // fragment offset of w1f (w2,w3,w3t,w2t,w1ft follow)
+  const float* wvec;
+  float4* dE;                              // (passes, E) dL/d(s_i - s_j) per evaluation, or null
+  float* partial;                          // (gridDim.x, CBF_PARTIAL) per-workgroup dW slabs
+  float obs_r, dist_thr, dist_eps;
+};
+
+struct CtrlNodeBwdArgs {
+  const bf16* pooled;  long p_env;     // (b,i,128) pooled edge features of step t (rollout)
+  const float4* S;     long s_env;     // states s_t
+  const float2* G;                     // goals (B,N)
+  const float2* A;     long a_env;     // actions a_t as applied (incl. noise)
+  const float4* Gn;    long gn_env;    // G_{t+1} = dL/ds_{t+1} (or null)
+  const uint8_t* valid; long v_env;    // valid[b*v_env] for this step (or null = all valid)
+  int B, N;
+  const bf16* wrm;                     // row-major node images
+  int o_w1, o_w2, o_w3, o_w4;          // element offsets (strides 168/72/136/72)
+  const float* wvec;                   // controller side vector (eb2|nb2|nb3|nb4)
+  float act_coef, dt, sqrt3;
+  bf16* dP;            long dp_env;    // (b,i,128) dL/dpooled out
+  float4* ego;                         // (B,N) dL/ds_t from the node path + gain law + action loss
+  float* partial;                      // (gridDim.x, CTRL_NODE_PARTIAL) slabs, accumulated
+};
+
+struct CtrlEdgeBwdArgs {
+  const float4* S;     long s_env;
+  const int* idx;      long i_env;
+  const uint8_t* argmax; long am_env;  // (b,i,128) winning slot per pooled feature
+  const bf16* dP;      long dp_env;    // (b,i,128)
+  int B, N, K;
+  const bf16* wpack;   int f_ew1f, f_ew2tn;   // packed fragments (ew2tn followed by ew1ft)
+  float4* dEc;         long de_env;    // (b,i,K) dL/d(s_i - s_j) out
+  float* partial;                      // (gridDim.x, CTRL_EDGE_PARTIAL) slabs, accumulated
+};
+
+struct CsrArgs {
+  const int* idx;      // (G, N, K) neighbour indices of G = B*T graphs
+  int G, N, K;
+  int* ptr;            // (G, N+1) incoming-edge offsets
+  int* edges;          // (G, N*K) incoming edge ids (i*K + k), self edges excluded
+};
+
+struct NodeRedArgs {
+  const float4* dE;    // (passes, T, B, N, K) per-edge dL/d(s_i - s_j)
+  const int* ptr; const int* edges;   // reverse CSR of the B*T graphs
+  int B, T, N, K, passes, accumulate;
+  float4* out;         // (T+1, B, N)
+};
+
+struct CombineArgs {
+  const float4* dS;   long ds_env;    // direct grads at step t (B,N) view
+  const float4* ego;                  // (B,N) contiguous or null
+  const float4* dEc;                  // (B,N,K) controller edge grads at step t or null
+  const int* ptr;     long ptr_env;   // reverse CSR of graph t (per env strides)
+  const int* edges;   long edges_env;
+  const float4* Gn;   long gn_env;    // G_{t+1} (B,N) view, or null (no BPTT / last step)
+  float4* Gout;       long go_env;    // G_t (B,N) view
+  int B, N, K;
+  float dt;
+};
+
+struct AdamArgs {
+  float* param; const float* grad; float* m; float* v;
+  int lo, hi;
+  float b1, b2, eps, wd, step_size, bc2_sqrt;
+};
+
 }  // namespace mb
 
 extern "C" {
@@ -74,6 +149,14 @@ int mb_scan(const mb::ScanArgs* a, hipStream_t st);
 int mb_scenario(const mb::ScenArgs* a, hipStream_t st);
 int mb_ctrl_fwd(const mb::CtrlArgs* a, int num_cu, hipStream_t st);
 int mb_cbf_fwd(const mb::CbfFwdArgs* a, int num_blocks, hipStream_t st);
+int mb_cbf_bwd(const mb::CbfBwdArgs* a, int num_blocks, hipStream_t st);
+int mb_ctrl_node_bwd(const mb::CtrlNodeBwdArgs* a, int num_blocks, hipStream_t st);
+int mb_ctrl_edge_bwd(const mb::CtrlEdgeBwdArgs* a, int num_blocks, hipStream_t st);
+int mb_rev_csr(const mb::CsrArgs* a, hipStream_t st);
+int mb_node_reduce(const mb::NodeRedArgs* a, hipStream_t st);
+int mb_node_combine(const mb::CombineArgs* a, hipStream_t st);
+int mb_reduce_rows(const float* partial, int rows, int cols, float* out, int accumulate, hipStream_t st);
+int mb_adam(const mb::AdamArgs* a, hipStream_t st);
 int mb_probe_mfma(const void* a, const void* b, float* d, hipStream_t st);
 int mb_probe_tr(const void* img, int rows, int stride, int e0, int m0, void* out, hipStream_t st);
 }

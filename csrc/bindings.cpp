@@ -39,13 +39,14 @@ static int scenario(u64 S, u64 G, int B, int N, float L, float r, float spread, 
 static int ctrl_fwd(u64 S, long s_env, u64 G, u64 idx, long i_env, int B, int N, int K, u64 wpack, int f_edge,
                     int f_node, u64 wvec, u64 A, long a_env, u64 Sn, long sn_env, u64 dist_sum, long d_env,
                     u64 act_sum, long ac_env, u64 noise, long n_env, float dt, float obs_r, float sqrt3,
-                    int num_cu, u64 stream) {
+                    u64 pooled, long p_env, u64 argmax, long am_env, int num_cu, u64 stream) {
   mb::CtrlArgs a{};
   a.S = P<const float4>(S); a.s_env = s_env; a.G = P<const float2>(G); a.idx = P<const int>(idx); a.i_env = i_env;
   a.B = B; a.N = N; a.K = K; a.wpack = P<const bf16>(wpack); a.f_edge = f_edge; a.f_node = f_node;
   a.wvec = P<const float>(wvec); a.A = P<float2>(A); a.a_env = a_env; a.Snext = P<float4>(Sn); a.sn_env = sn_env;
   a.dist_sum = P<float>(dist_sum); a.d_env = d_env; a.act_sum = P<float>(act_sum); a.ac_env = ac_env;
   a.noise = P<const float2>(noise); a.n_env = n_env; a.dt = dt; a.obs_r = obs_r; a.sqrt3 = sqrt3;
+  a.pooled = P<bf16>(pooled); a.p_env = p_env; a.argmax = P<uint8_t>(argmax); a.am_env = am_env;
   return mb_ctrl_fwd(&a, num_cu, ST(stream));
 }
 
@@ -65,6 +66,79 @@ static int cbf_fwd(u64 S, long s_env, long s_step, u64 idx, u64 dang, u64 valid,
   a.lc.scale = lc[6].cast<float>();
   a.obs_r = obs_r; a.dist_thr = dist_thr; a.dist_eps = dist_eps;
   return mb_cbf_fwd(&a, num_blocks, ST(stream));
+}
+
+static int cbf_bwd(u64 S, long s_env, long s_step, u64 idx, int B, int T, int N, int K, int passes, u64 dh,
+                   u64 wpack, int f_bwd, u64 wvec, u64 dE, u64 partial, float obs_r, float dist_thr,
+                   float dist_eps, int num_blocks, u64 stream) {
+  mb::CbfBwdArgs a{};
+  a.S = P<const float4>(S); a.s_env = s_env; a.s_step = s_step; a.idx = P<const int>(idx);
+  a.B = B; a.T = T; a.N = N; a.K = K; a.passes = passes; a.dh = P<const float>(dh);
+  a.wpack = P<const bf16>(wpack); a.f_bwd = f_bwd; a.wvec = P<const float>(wvec);
+  a.dE = P<float4>(dE); a.partial = P<float>(partial);
+  a.obs_r = obs_r; a.dist_thr = dist_thr; a.dist_eps = dist_eps;
+  return mb_cbf_bwd(&a, num_blocks, ST(stream));
+}
+
+static int rev_csr(u64 idx, int G, int N, int K, u64 ptr, u64 edges, u64 stream) {
+  mb::CsrArgs a{};
+  a.idx = P<const int>(idx); a.G = G; a.N = N; a.K = K; a.ptr = P<int>(ptr); a.edges = P<int>(edges);
+  return mb_rev_csr(&a, ST(stream));
+}
+
+static int node_reduce(u64 dE, u64 ptr, u64 edges, int B, int T, int N, int K, int passes, int accumulate, u64 out,
+                       u64 stream) {
+  mb::NodeRedArgs a{};
+  a.dE = P<const float4>(dE); a.ptr = P<const int>(ptr); a.edges = P<const int>(edges);
+  a.B = B; a.T = T; a.N = N; a.K = K; a.passes = passes; a.accumulate = accumulate; a.out = P<float4>(out);
+  return mb_node_reduce(&a, ST(stream));
+}
+
+static int node_combine(u64 dS, long ds_env, u64 ego, u64 dEc, u64 ptr, long ptr_env, u64 edges, long edges_env,
+                        u64 Gn, long gn_env, u64 Gout, long go_env, int B, int N, int K, float dt, u64 stream) {
+  mb::CombineArgs a{};
+  a.dS = P<const float4>(dS); a.ds_env = ds_env; a.ego = P<const float4>(ego); a.dEc = P<const float4>(dEc);
+  a.ptr = P<const int>(ptr); a.ptr_env = ptr_env; a.edges = P<const int>(edges); a.edges_env = edges_env;
+  a.Gn = P<const float4>(Gn); a.gn_env = gn_env; a.Gout = P<float4>(Gout); a.go_env = go_env;
+  a.B = B; a.N = N; a.K = K; a.dt = dt;
+  return mb_node_combine(&a, ST(stream));
+}
+
+static int reduce_rows(u64 partial, int rows, int cols, u64 out, int accumulate, u64 stream) {
+  return mb_reduce_rows(P<const float>(partial), rows, cols, P<float>(out), accumulate, ST(stream));
+}
+
+static int adam(u64 param, u64 grad, u64 m, u64 v, int lo, int hi, float b1, float b2, float eps, float wd,
+                float step_size, float bc2_sqrt, u64 stream) {
+  mb::AdamArgs a{};
+  a.param = P<float>(param); a.grad = P<const float>(grad); a.m = P<float>(m); a.v = P<float>(v);
+  a.lo = lo; a.hi = hi; a.b1 = b1; a.b2 = b2; a.eps = eps; a.wd = wd; a.step_size = step_size; a.bc2_sqrt = bc2_sqrt;
+  return mb_adam(&a, ST(stream));
+}
+
+static int ctrl_node_bwd(u64 pooled, long p_env, u64 S, long s_env, u64 G, u64 A, long a_env, u64 Gn, long gn_env,
+                         u64 valid, long v_env, int B, int N, u64 wrm, int o1, int o2, int o3, int o4, u64 wvec,
+                         float act_coef, float dt, float sqrt3, u64 dP, long dp_env, u64 ego, u64 partial,
+                         int num_blocks, u64 stream) {
+  mb::CtrlNodeBwdArgs a{};
+  a.pooled = P<const bf16>(pooled); a.p_env = p_env; a.S = P<const float4>(S); a.s_env = s_env;
+  a.G = P<const float2>(G); a.A = P<const float2>(A); a.a_env = a_env; a.Gn = P<const float4>(Gn); a.gn_env = gn_env;
+  a.valid = P<const uint8_t>(valid); a.v_env = v_env; a.B = B; a.N = N; a.wrm = P<const bf16>(wrm);
+  a.o_w1 = o1; a.o_w2 = o2; a.o_w3 = o3; a.o_w4 = o4; a.wvec = P<const float>(wvec);
+  a.act_coef = act_coef; a.dt = dt; a.sqrt3 = sqrt3; a.dP = P<bf16>(dP); a.dp_env = dp_env;
+  a.ego = P<float4>(ego); a.partial = P<float>(partial);
+  return mb_ctrl_node_bwd(&a, num_blocks, ST(stream));
+}
+
+static int ctrl_edge_bwd(u64 S, long s_env, u64 idx, long i_env, u64 argmax, long am_env, u64 dP, long dp_env,
+                         int B, int N, int K, u64 wpack, int f_ew1f, int f_ew2tn, u64 dEc, long de_env, u64 partial,
+                         int num_blocks, u64 stream) {
+  mb::CtrlEdgeBwdArgs a{};
+  a.S = P<const float4>(S); a.s_env = s_env; a.idx = P<const int>(idx); a.i_env = i_env;
+  a.argmax = P<const uint8_t>(argmax); a.am_env = am_env; a.dP = P<const bf16>(dP); a.dp_env = dp_env;
+  a.B = B; a.N = N; a.K = K; a.wpack = P<const bf16>(wpack); a.f_ew1f = f_ew1f; a.f_ew2tn = f_ew2tn;
+  a.dEc = P<float4>(dEc); a.de_env = de_env; a.partial = P<float>(partial);
+  return mb_ctrl_edge_bwd(&a, num_blocks, ST(stream));
 }
 
 static int probe_mfma(u64 a, u64 b, u64 d, u64 stream) {
@@ -94,6 +168,14 @@ PYBIND11_MODULE(_C, m) {
   m.def("scenario", &scenario);
   m.def("ctrl_fwd", &ctrl_fwd);
   m.def("cbf_fwd", &cbf_fwd);
+  m.def("cbf_bwd", &cbf_bwd);
+  m.def("ctrl_node_bwd", &ctrl_node_bwd);
+  m.def("ctrl_edge_bwd", &ctrl_edge_bwd);
+  m.def("rev_csr", &rev_csr);
+  m.def("node_reduce", &node_reduce);
+  m.def("node_combine", &node_combine);
+  m.def("reduce_rows", &reduce_rows);
+  m.def("adam", &adam);
   m.def("probe_mfma", &probe_mfma);
   m.def("probe_tr", &probe_tr);
   m.def("device_info", &device_info);

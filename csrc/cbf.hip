@@ -95,19 +95,20 @@ struct EdgeCtx {
   bool mask;
 };
 
-DEV void cbf_edge(const float4* S, long s_env, long s_step, const int* idx, int T, int N, int K,
+DEV void cbf_edge(const float4* S, long s_env, long s_step, const int* idx, int B, int N, int K,
                   long e, long E, int tstep_off, float obs_r, float dist_thr, float dist_eps, EdgeCtx& c) {
   c.ok = e < E;
   c.rel = make_float4(0.f, 0.f, 0.f, 0.f);
   c.eye = 0.f; c.d = 0.f; c.dfeat = 0.f; c.mask = false;
   c.b = c.t = c.i = c.j = 0;
   if (!c.ok) return;
+  // time-major edge order: e = ((t*B + b)*N + i)*K + k
   const long NK = (long)N * K;
-  const long bt = e / NK;
-  const long rem = e - bt * NK;
+  const long tb = e / NK;
+  const long rem = e - tb * NK;
   c.i = (int)(rem / K);
-  c.b = (int)(bt / T);
-  c.t = (int)(bt - (long)c.b * T);
+  c.t = (int)(tb / B);
+  c.b = (int)(tb - (long)c.t * B);
   c.j = idx[e];
   const float4* Sb = S + (long)c.b * s_env + (long)(c.t + tstep_off) * s_step;
   const float4 si = Sb[c.i];
@@ -147,7 +148,7 @@ __global__ __launch_bounds__(WAVES * 64) void cbf_fwd_kernel(CbfFwdArgs a) {
       const bf16* wt = wl + opaque_zero();
       const float* vt = vl + opaque_zero();
       EdgeCtx c;
-      cbf_edge(a.S, a.s_env, a.s_step, a.idx, a.T, a.N, a.K, e, E, pass, a.obs_r, a.dist_thr, a.dist_eps, c);
+      cbf_edge(a.S, a.s_env, a.s_step, a.idx, a.B, a.N, a.K, e, E, pass, a.obs_r, a.dist_thr, a.dist_eps, c);
       const float hp = cbf_mlp(cbf_edge_frag(c.rel, c.eye, c.dfeat, c.ok, h), wt, vt, lane, act);
       if (pass == 0) { c0 = c; hv = c.mask ? hp : 0.f; }
       else { hnv = c.mask ? hp : 0.f; mask1 = c.mask; }
@@ -155,7 +156,7 @@ __global__ __launch_bounds__(WAVES * 64) void cbf_fwd_kernel(CbfFwdArgs a) {
     if (!c0.ok || h != 0) continue;
     if (a.h_out) a.h_out[e] = hv;
     if (a.hn_out) a.hn_out[e] = hnv;
-    const bool vld = a.valid ? (a.valid[(long)c0.b * a.T + c0.t] != 0) : true;
+    const bool vld = a.valid ? (a.valid[(long)c0.t * a.B + c0.b] != 0) : true;
     const bool dg = a.dang ? (a.dang[e] != 0) : false;
     float gh = 0.f, ghn = 0.f;
     if (vld && a.two) {
@@ -217,5 +218,240 @@ extern "C" int mb_cbf_fwd(const mb::CbfFwdArgs* a, int num_blocks, hipStream_t s
   const size_t lds = (size_t)CBF_FWD_FRAGS * FRAG_BYTES + CBF_VEC * 4;
   (void)hipFuncSetAttribute((const void*)cbf_fwd_kernel<CBF_FWD_WAVES>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   hipLaunchKernelGGL(cbf_fwd_kernel<CBF_FWD_WAVES>, dim3(num_blocks), dim3(CBF_FWD_WAVES * 64), lds, st, *a);
+  return (int)hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------
+// cbf_bwd_kernel: hand-written backward of the CBF edge MLP for `passes`*E evaluations.
+// Workgroup = 4 waves sharing a 128-evaluation chunk (32 per wave):
+//   data path (per wave, registers only): recompute H1,H2,H3 -> dH3 = w4*dh*relu'
+//     -> dH2 = W3^T dH3 .relu' (16 MFMA) -> dH1 = W2^T dH2 .relu' (16) -> dF = W1^T dH1 (4)
+//     -> dL/d(s_i - s_j) incl. the |dp|_eps feature; written per evaluation (self edges 0)
+//   weight gradients (workgroup-shared): activations / deltas of the chunk are staged as
+//     edge-major bf16 LDS images; each wave owns a fixed subset of the 32x32 output tiles of
+//     dW3 (64x128), dW2 (128x64), dW1f (64x32) and contracts over the chunk's 128 edges with
+//     ds_read_b64_tr_b16 fragments -> MFMA; bias grads are row sums of the A fragments; the
+//     64->1 head (w4, b4) accumulates per lane. Fixed ownership -> deterministic per-WG slabs,
+//     reduced by a separate deterministic pass (no float atomics).
+// ---------------------------------------------------------------------------------------
+namespace mb {
+
+constexpr int CBF_BWD_WAVES = 4;
+constexpr int CBF_CH = CBF_BWD_WAVES * 32;    // evaluations per chunk
+constexpr int SA128 = 136, SA64 = 72, SA32 = 40;
+constexpr int CBF_BWD_FRAGS = 70;
+// per-WG partial slab layout (floats)
+constexpr int P_W3 = 0, P_B3 = 8192, P_W2 = 8256, P_B2 = 16448, P_W1 = 16576, P_W4 = 18624, P_B4 = 18688;
+constexpr int CBF_PARTIAL = 18696;
+// stage A/B: (128 + 64)-wide images; stage C+D: dH1|F|dh|relu(H3) = 64+32+32+64 wide
+constexpr size_t CBF_STAGE_BYTES = (size_t)(SA64 + SA32 + SA32 + SA64) * CBF_CH * 2;
+
+size_t cbf_bwd_lds() { return (size_t)CBF_BWD_FRAGS * FRAG_BYTES + CBF_VEC * 4 + CBF_STAGE_BYTES; }
+
+__global__ __launch_bounds__(CBF_BWD_WAVES * 64, 1) void cbf_bwd_kernel(CbfBwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  bf16* wl = reinterpret_cast<bf16*>(smem);
+  float* vl = reinterpret_cast<float*>(smem + CBF_BWD_FRAGS * FRAG_BYTES);
+  bf16* stg = reinterpret_cast<bf16*>(smem + CBF_BWD_FRAGS * FRAG_BYTES + CBF_VEC * 4);
+  block_copy16(wl, a.wpack + (size_t)a.f_bwd * 512, CBF_BWD_FRAGS * FRAG_BYTES);
+  block_copy16(vl, a.wvec, CBF_VEC * 4);
+  __syncthreads();
+  const int wave = threadIdx.x / WAVE, lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
+  const long E = (long)a.B * a.T * a.N * a.K;
+  const long EV = E * a.passes;
+  const long nchunks = (EV + CBF_CH - 1) / CBF_CH;
+  const int erow = wave * 32 + r;
+
+  f32x16 accA[2], accB[2], accC;
+  accA[0] = accA[1] = accB[0] = accB[1] = accC = zero16();
+  float bA[2] = {0.f, 0.f}, bB[2] = {0.f, 0.f};
+  float bD = 0.f;   // db4 (row-sum of the dh image, waves 2/3 tile 0)
+  // owned tiles
+  const int tA0 = wave, tA1 = wave + 4;       // dW3: (mt = t/4, nt = t%4)
+  const int tB0 = wave, tB1 = wave + 4;       // dW2: (mt = t/2, nt = t%2)
+
+  for (long chunk = blockIdx.x; chunk < nchunks; chunk += gridDim.x) {
+    const long ev = chunk * CBF_CH + wave * 32 + r;
+    const bool in = ev < EV;
+    const int pass = (in && ev >= E) ? 1 : 0;
+    const long e = ev - (long)pass * E;
+    EdgeCtx c;
+    cbf_edge(a.S, a.s_env, a.s_step, a.idx, a.B, a.N, a.K, e, in ? E : 0, pass, a.obs_r, a.dist_thr, a.dist_eps, c);
+    const float dhv = in ? a.dh[ev] : 0.f;
+    const bf16x8 F = cbf_edge_frag(c.rel, c.eye, c.dfeat, c.ok, h);
+    const bf16* wt = wl + opaque_zero();
+    const float* b2 = vl;
+    const float* b3 = vl + 128;
+    const float* w4 = vl + 192;
+    // ---- forward recompute
+    bf16x16 H1b[2], H2b[4];
+    f32x16 H3p[2];
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt) {
+      f32x16 t1 = mfma(frag_ld(wt, mt, lane), F, zero16());
+      relu_(t1);
+      H1b[mt] = to_bf16x16(t1);
+    }
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+      f32x16 t2 = bias_rows(b2, 32 * mt, h);
+      static_for<4>([&](auto kk_) {
+        constexpr int kk = decltype(kk_)::value;
+        t2 = mfma(frag_ld(wt, 2 + mt * 4 + kk, lane), bacc_frag<kk & 1>(H1b[kk >> 1]), t2);
+      });
+      relu_(t2);
+      H2b[mt] = to_bf16x16(t2);
+    }
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt) {
+      f32x16 t3 = bias_rows(b3, 32 * mt, h);
+      static_for<8>([&](auto kk_) {
+        constexpr int kk = decltype(kk_)::value;
+        t3 = mfma(frag_ld(wt, 18 + mt * 8 + kk, lane), bacc_frag<kk & 1>(H2b[kk >> 1]), t3);
+      });
+      H3p[mt] = t3;
+    }
+    // ---- head backward: dH3pre = w4 * dh * relu'(H3pre); dw4 += dh * relu(H3pre)
+    bf16x16 d3b[2], H3b[2];
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt) {
+      f32x16 d3;
+#pragma unroll
+      for (int reg = 0; reg < 16; ++reg) {
+        const float x = H3p[mt][reg];
+        d3[reg] = x > 0.f ? w4[32 * mt + acc_row(reg, h)] * dhv : 0.f;
+        H3p[mt][reg] = fmaxf(x, 0.f);
+      }
+      d3b[mt] = to_bf16x16(d3);
+      H3b[mt] = to_bf16x16(H3p[mt]);
+    }
+    // ---- dH2pre = (W3^T dH3pre) . relu'(H2)
+    bf16x16 d2b[4];
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+      f32x16 t = zero16();
+      static_for<4>([&](auto kk_) {
+        constexpr int kk = decltype(kk_)::value;
+        t = mfma(frag_ld(wt, 34 + mt * 4 + kk, lane), bacc_frag<kk & 1>(d3b[kk >> 1]), t);
+      });
+#pragma unroll
+      for (int q = 0; q < 16; ++q) t[q] = ((float)H2b[mt][q] > 0.f) ? t[q] : 0.f;
+      d2b[mt] = to_bf16x16(t);
+    }
+    // ---- dH1pre = (W2^T dH2pre) . relu'(H1)
+    bf16x16 d1b[2];
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt) {
+      f32x16 t = zero16();
+      static_for<8>([&](auto kk_) {
+        constexpr int kk = decltype(kk_)::value;
+        t = mfma(frag_ld(wt, 50 + mt * 8 + kk, lane), bacc_frag<kk & 1>(d2b[kk >> 1]), t);
+      });
+#pragma unroll
+      for (int q = 0; q < 16; ++q) t[q] = ((float)H1b[mt][q] > 0.f) ? t[q] : 0.f;
+      d1b[mt] = to_bf16x16(t);
+    }
+    // ---- dF = W1^T dH1pre (rows: dx dy dvx dvy eye dist)
+    {
+      f32x16 t = zero16();
+      static_for<4>([&](auto kk_) {
+        constexpr int kk = decltype(kk_)::value;
+        t = mfma(frag_ld(wt, 66 + kk, lane), bacc_frag<kk & 1>(d1b[kk >> 1]), t);
+      });
+      const float ddist = shfl_xor32(t[1]);   // row 5 lives in lane r+32, reg 1
+      if (a.dE && in && h == 0) {
+        float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (c.ok && c.j != c.i) {
+          const float inv = 1.f / c.d;
+          g = make_float4(t[0] + ddist * c.rel.x * inv, t[1] + ddist * c.rel.y * inv,
+                          t[2], t[3]);
+        }
+        a.dE[ev] = g;
+      }
+    }
+    // ---- stage A: dW3 (64x128) += dH3pre . H2^T ; db3
+    bf16* imA = stg;
+    bf16* imB = stg + CBF_CH * SA64;
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt) store_tile(imA, SA64, erow, 32 * mt, d3b[mt], h);
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) store_tile(imB, SA128, erow, 32 * mt, H2b[mt], h);
+    __syncthreads();
+    bA[0] += stage_mma(imA, SA64, imB, SA128, tA0 / 4, tA0 % 4, CBF_CH / 16, lane, accA[0], tA0 % 4 == 0);
+    bA[1] += stage_mma(imA, SA64, imB, SA128, tA1 / 4, tA1 % 4, CBF_CH / 16, lane, accA[1], tA1 % 4 == 0);
+    __syncthreads();
+    // ---- stage B: dW2 (128x64) += dH2pre . H1^T ; db2
+    imA = stg;
+    imB = stg + CBF_CH * SA128;
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) store_tile(imA, SA128, erow, 32 * mt, d2b[mt], h);
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt) store_tile(imB, SA64, erow, 32 * mt, H1b[mt], h);
+    __syncthreads();
+    bB[0] += stage_mma(imA, SA128, imB, SA64, tB0 / 2, tB0 % 2, CBF_CH / 16, lane, accB[0], tB0 % 2 == 0);
+    bB[1] += stage_mma(imA, SA128, imB, SA64, tB1 / 2, tB1 % 2, CBF_CH / 16, lane, accB[1], tB1 % 2 == 0);
+    __syncthreads();
+    // ---- stage C+D: dW1f (64x32) += dH1pre . F^T (waves 0,1);
+    //      dW4pad (32x64) += [dh;0] . relu(H3)^T -> row 0 = dw4, row-sum = db4 (waves 2,3)
+    bf16* imC = stg;
+    bf16* imF = imC + CBF_CH * SA64;
+    bf16* imD = imF + CBF_CH * SA32;
+    bf16* imH = imD + CBF_CH * SA32;
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt) store_tile(imC, SA64, erow, 32 * mt, d1b[mt], h);
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt) store_tile(imH, SA64, erow, 32 * mt, H3b[mt], h);
+    {
+      bf16x8 z, dv;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { z[j] = (bf16)0.f; dv[j] = (bf16)0.f; }
+      if (h == 0) dv[0] = (bf16)dhv;
+      *reinterpret_cast<bf16x8*>(imF + erow * SA32 + 8 * h) = F;
+      *reinterpret_cast<bf16x8*>(imF + erow * SA32 + 16 + 8 * h) = z;
+      *reinterpret_cast<bf16x8*>(imD + erow * SA32 + 8 * h) = dv;
+      *reinterpret_cast<bf16x8*>(imD + erow * SA32 + 16 + 8 * h) = z;
+    }
+    __syncthreads();
+    if (wave < 2) stage_mma(imC, SA64, imF, SA32, wave, 0, CBF_CH / 16, lane, accC, false);
+    else bD += stage_mma(imD, SA32, imH, SA64, 0, wave - 2, CBF_CH / 16, lane, accC, wave == 2);
+    __syncthreads();
+  }
+
+  // ---- per-workgroup slab
+  float* P = a.partial + (long)blockIdx.x * CBF_PARTIAL;
+  write_tile(P + P_W3, 128, tA0 / 4, tA0 % 4, accA[0], lane);
+  write_tile(P + P_W3, 128, tA1 / 4, tA1 % 4, accA[1], lane);
+  write_tile(P + P_W2, 64, tB0 / 2, tB0 % 2, accB[0], lane);
+  write_tile(P + P_W2, 64, tB1 / 2, tB1 % 2, accB[1], lane);
+  if (wave < 2) {
+    write_tile(P + P_W1, 32, wave, 0, accC, lane);
+  } else {
+    // dW4pad row 0 (= dw4 for columns 32*(wave-2) + r): reg 0 of lanes h == 0
+    if (h == 0) P[P_W4 + 32 * (wave - 2) + r] = accC[0];
+    if (wave == 2) {
+      const float s4 = bD + shfl_xor32(bD);
+      if (lane == 0) P[P_B4] = s4;
+    }
+  }
+  {
+    const float s0 = bA[0] + shfl_xor32(bA[0]);
+    const float s1 = bA[1] + shfl_xor32(bA[1]);
+    if (h == 0 && tA0 % 4 == 0) P[P_B3 + 32 * (tA0 / 4) + r] = s0;
+    if (h == 0 && tA1 % 4 == 0) P[P_B3 + 32 * (tA1 / 4) + r] = s1;
+    const float u0 = bB[0] + shfl_xor32(bB[0]);
+    const float u1 = bB[1] + shfl_xor32(bB[1]);
+    if (h == 0 && tB0 % 2 == 0) P[P_B2 + 32 * (tB0 / 2) + r] = u0;
+    if (h == 0 && tB1 % 2 == 0) P[P_B2 + 32 * (tB1 / 2) + r] = u1;
+  }
+}
+
+}  // namespace mb
+
+extern "C" int mb_cbf_bwd(const mb::CbfBwdArgs* a, int num_blocks, hipStream_t st) {
+  using namespace mb;
+  if (a->K > 16 || a->K < 1 || a->passes < 1 || a->passes > 2) return -1;
+  const size_t lds = cbf_bwd_lds();
+  (void)hipFuncSetAttribute((const void*)cbf_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipLaunchKernelGGL(cbf_bwd_kernel, dim3(num_blocks), dim3(CBF_BWD_WAVES * 64), lds, st, *a);
   return (int)hipGetLastError();
 }

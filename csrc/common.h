@@ -124,3 +124,140 @@ DEV uint64_t mix64(uint64_t z) {
 DEV float u01(uint64_t key) { return (float)(mix64(key) >> 40) * (1.0f / 16777216.0f); }
 
 }  // namespace mb
+
+namespace mb {
+
+typedef __bf16 bf16x16 __attribute__((ext_vector_type(16)));
+
+// f32x16 accumulator -> packed bf16 copy (8 VGPRs), element q = reg q
+DEV bf16x16 to_bf16x16(const f32x16& c) {
+  bf16x16 r;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) r[q] = (bf16)c[q];
+  return r;
+}
+
+template <int S>
+DEV bf16x8 bacc_frag(const bf16x16& c) {
+  bf16x8 r;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = c[8 * S + j];
+  return r;
+}
+
+// store one standard-orientation tile (lane = edge row `erow` of the image, regs = features
+// col0 + acc_row(reg,h)) into an edge-major bf16 LDS image: 4 x 8-byte writes per lane
+DEV void store_tile(bf16* img, int stride, int erow, int col0, const bf16x16& v, int h) {
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    bf16x4 q;
+    q[0] = v[4 * g]; q[1] = v[4 * g + 1]; q[2] = v[4 * g + 2]; q[3] = v[4 * g + 3];
+    *reinterpret_cast<bf16x4*>(img + erow * stride + col0 + 8 * g + 4 * h) = q;
+  }
+}
+
+// Transposed operand fragment from an edge-major LDS image img[e][m] (row stride `stride`
+// elements, 8-byte aligned): lane (r, h) receives img[e0 + 8h + j][m0 + r], j = 0..7, via two
+// ds_read_b64_tr_b16. Used as A (rows = m, k = e) or B (k = e, cols = m) of a contraction over
+// edges (the weight-gradient GEMMs). Requires EXEC = all 64 lanes.
+DEV bf16x8 tr_frag(const bf16* img, int stride, int e0, int m0, int lane) {
+  const int q = (lane & 15) >> 2, p = lane & 3, gg = (lane >> 4) & 1, h = lane >> 5;
+  const bf16* a1 = img + (e0 + 8 * h + q) * stride + m0 + 16 * gg + 4 * p;
+  const bf16* a2 = a1 + 4 * stride;
+  const s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4*)(a1));
+  const s16x4 v2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4*)(a2));
+  const bf16x4 b1 = __builtin_bit_cast(bf16x4, v1);
+  const bf16x4 b2 = __builtin_bit_cast(bf16x4, v2);
+  bf16x8 r;
+  r[0] = b1[0]; r[1] = b1[1]; r[2] = b1[2]; r[3] = b1[3];
+  r[4] = b2[0]; r[5] = b2[1]; r[6] = b2[2]; r[7] = b2[3];
+  return r;
+}
+
+// acc += A_img[rows 32mt.., k = e] . B_img[k = e, cols 32nt..] over `esteps` x 16 edges;
+// returns the row sums of A (bias gradient; per lane: row 32mt + r over half h) if `bsum`
+DEV float stage_mma(const bf16* imgA, int sA, const bf16* imgB, int sB, int mt, int nt, int esteps, int lane,
+                    f32x16& acc, bool bsum) {
+  float s = 0.f;
+#pragma unroll 2
+  for (int ks = 0; ks < esteps; ++ks) {
+    const bf16x8 a = tr_frag(imgA, sA, 16 * ks, 32 * mt, lane);
+    const bf16x8 b = tr_frag(imgB, sB, 16 * ks, 32 * nt, lane);
+    acc = mfma(a, b, acc);
+    if (bsum) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s += (float)a[j];
+    }
+  }
+  return s;
+}
+
+// write an owned dW tile (rows 32mt.., cols 32nt..) of a row-major (ncols) fp32 slab
+DEV void write_tile(float* dst, int ncols, int mt, int nt, const f32x16& c, int lane) {
+  const int r = lane & 31, h = lane >> 5;
+#pragma unroll
+  for (int reg = 0; reg < 16; ++reg) dst[(32 * mt + acc_row(reg, h)) * ncols + 32 * nt + r] = c[reg];
+}
+
+DEV float sum32(float v) {   // sum over the 32 lanes of this lane's half
+#pragma unroll
+  for (int o = 16; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+}  // namespace mb
+
+namespace mb {
+
+// ---- MFMA operand readers for row-major bf16 weight images W[rows][stride] in LDS.
+// One copy of a weight matrix serves the forward (W) and the backward (W^T) chains.
+
+// A = W, natural k:  elem j = W[m0 + r][16kk + 8h + j]        (one 16-byte read)
+DEV bf16x8 wrm_nat(const bf16* W, int stride, int m0, int kk, int lane) {
+  const int r = lane & 31, h = lane >> 5;
+  return *reinterpret_cast<const bf16x8*>(W + (m0 + r) * stride + 16 * kk + 8 * h);
+}
+
+// A = W, accumulator k: elem j = W[m0 + r][32t + 16s + 8(j>>2) + 4h + (j&3)], kk = 2t + s
+DEV bf16x8 wrm_acc(const bf16* W, int stride, int m0, int kk, int lane) {
+  const int r = lane & 31, h = lane >> 5;
+  const bf16* p = W + (m0 + r) * stride + 16 * kk + 4 * h;
+  const bf16x4 lo = *reinterpret_cast<const bf16x4*>(p);
+  const bf16x4 hi = *reinterpret_cast<const bf16x4*>(p + 8);
+  bf16x8 f;
+  f[0] = lo[0]; f[1] = lo[1]; f[2] = lo[2]; f[3] = lo[3];
+  f[4] = hi[0]; f[5] = hi[1]; f[6] = hi[2]; f[7] = hi[3];
+  return f;
+}
+
+// two ds_read_b64_tr_b16: lane (r = 16gg + i, h) receives img[rb1 + j][c0 + r] (j<4) and
+// img[rb2 + j-4][c0 + r] (j>=4); rb1/rb2 may depend on h only (uniform per 16-lane group)
+DEV bf16x8 tr_pair(const bf16* img, int stride, int rb1, int rb2, int c0, int lane) {
+  const int q = (lane & 15) >> 2, p = lane & 3, gg = (lane >> 4) & 1;
+  const bf16* a1 = img + (rb1 + q) * stride + c0 + 16 * gg + 4 * p;
+  const bf16* a2 = img + (rb2 + q) * stride + c0 + 16 * gg + 4 * p;
+  const s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4*)(a1));
+  const s16x4 v2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4*)(a2));
+  const bf16x4 b1 = __builtin_bit_cast(bf16x4, v1);
+  const bf16x4 b2 = __builtin_bit_cast(bf16x4, v2);
+  bf16x8 r;
+  r[0] = b1[0]; r[1] = b1[1]; r[2] = b1[2]; r[3] = b1[3];
+  r[4] = b2[0]; r[5] = b2[1]; r[6] = b2[2]; r[7] = b2[3];
+  return r;
+}
+
+// A = W^T, accumulator k: elem j = W[32t + 16s + 8(j>>2) + 4h + (j&3)][m0 + r]
+DEV bf16x8 wrmT_acc(const bf16* W, int stride, int m0, int kk, int lane) {
+  const int h = lane >> 5;
+  const int rb = 16 * kk + 4 * h;
+  return tr_pair(W, stride, rb, rb + 8, m0, lane);
+}
+
+// A = W^T, natural k: elem j = W[16kk + 8h + j][m0 + r]
+DEV bf16x8 wrmT_nat(const bf16* W, int stride, int m0, int kk, int lane) {
+  const int h = lane >> 5;
+  const int rb = 16 * kk + 8 * h;
+  return tr_pair(W, stride, rb, rb + 4, m0, lane);
+}
+
+}  // namespace mb

@@ -180,26 +180,50 @@ __global__ __launch_bounds__(WAVES * 64) void ctrl_fwd_kernel(CtrlArgs a) {
       const unsigned mask32 = (unsigned)(__ballot(m) & 0xffffffffull);
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt) {
+        // masked max over each agent's 16 rows + first-occurrence argmax (row order = slot)
         float p0 = 0.f, p1 = 0.f;
+        int r0 = 255, r1 = 255;
 #pragma unroll
         for (int reg = 0; reg < 8; ++reg) {
           const int e = acc_row(reg, h);
           const float v = ((mask32 >> e) & 1u) ? fmaxf(Z[nt][reg], 0.f) : 0.f;
-          p0 = fmaxf(p0, v);
+          if (v > p0 || (v == p0 && v > 0.f && e < r0)) { p0 = v; r0 = e; }
         }
 #pragma unroll
         for (int reg = 8; reg < 16; ++reg) {
           const int e = acc_row(reg, h);
           const float v = ((mask32 >> e) & 1u) ? fmaxf(Z[nt][reg], 0.f) : 0.f;
-          p1 = fmaxf(p1, v);
+          if (v > p1 || (v == p1 && v > 0.f && e < r1)) { p1 = v; r1 = e; }
         }
-        p0 = fmaxf(p0, shfl_xor32(p0));
-        p1 = fmaxf(p1, shfl_xor32(p1));
+        const float q0 = shfl_xor32(p0), q1 = shfl_xor32(p1);
+        const int s0 = __shfl_xor(r0, 32), s1 = __shfl_xor(r1, 32);
+        if (q0 > p0 || (q0 == p0 && s0 < r0)) { p0 = q0; r0 = s0; }
+        if (q1 > p1 || (q1 == p1 && s1 < r1)) { p1 = q1; r1 = s1; }
         const int arow = 2 * q + h;   // h==0 writes agent 2q, h==1 agent 2q+1
-        pool[arow * PSTR + 32 * nt + r] = (bf16)(h == 0 ? p0 : p1);
+        const float pv = (h == 0) ? p0 : p1;
+        pool[arow * PSTR + 32 * nt + r] = (bf16)pv;
+        if (a.argmax) {
+          const int ga = g0 + arow;
+          if (ga < total) {
+            const int bb = ga / N, ii = ga - bb * N;
+            const int rr = (h == 0) ? r0 : r1 - 16;
+            a.argmax[(long)bb * a.am_env + (long)ii * 128 + 32 * nt + r] = (pv > 0.f) ? (uint8_t)rr : (uint8_t)0xFF;
+          }
+        }
       }
     }
     lds_wave_sync();
+    if (a.pooled) {   // 32 agents x 256 B, 16 B per lane
+      for (int u = lane; u < 32 * 16; u += 64) {
+        const int ag = u >> 4, ch = u & 15;
+        const int ga = g0 + ag;
+        if (ga < total) {
+          const int bb = ga / N, ii = ga - bb * N;
+          *reinterpret_cast<bf16x8*>(a.pooled + (long)bb * a.p_env + (long)ii * 128 + ch * 8) =
+              *reinterpret_cast<const bf16x8*>(pool + ag * PSTR + ch * 8);
+        }
+      }
+    }
     // ---------------- node phase: lane column r = agent g0 + r
     const int gi = g0 + r;
     const bool ok = gi < total;
@@ -273,5 +297,473 @@ extern "C" int mb_ctrl_fwd(const mb::CtrlArgs* a, int num_cu, hipStream_t st) {
   const size_t lds = ctrl_fwd_lds();
   (void)hipFuncSetAttribute((const void*)ctrl_fwd_kernel<CTRL_WAVES>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   hipLaunchKernelGGL(ctrl_fwd_kernel<CTRL_WAVES>, dim3(blocks), dim3(CTRL_WAVES * 64), lds, st, *a);
+  return (int)hipGetLastError();
+}
+
+// =======================================================================================
+// Controller backward for one timestep of the BPTT recursion (reference: autograd through
+// controller.py:31-63 inside train.py:103). Two kernels, because the node MLP (4 layers,
+// forward + transposed weights) and the edge MLP (recompute + backward) do not fit one
+// workgroup's LDS together with the weight-gradient staging:
+//   ctrl_node_bwd: pooled features (stored by the rollout) -> node MLP recompute -> gain law
+//     backward (dA = dt*G_{t+1}[v] + action-loss grad) -> dY4..dY1 -> dL/dpooled (to
+//     global, bf16) + dL/ds_t of the ego terms; node weight grads (WG-shared, 4 stages).
+//   ctrl_edge_bwd: edge MLP recompute, max-pool backward via the stored argmax slots,
+//     dH1 = W2^T dZ, dF = W1^T dH1 -> per-edge dL/d(s_i - s_j); edge weight grads.
+// Weight gradients accumulate into a fixed per-workgroup slab across all timesteps
+// (slab += partial, deterministic) and are reduced once after the recursion.
+// =======================================================================================
+namespace mb {
+
+constexpr int NB_WAVES = 4;
+constexpr int NB_CH = NB_WAVES * 32;                  // agents per chunk
+constexpr int NS1 = 168, NS2 = 72, NS3 = 136, NS4 = 72;   // row-major image strides
+constexpr int NODE_RM_ELEMS = 64 * NS1 + 128 * NS2 + 64 * NS3 + 32 * NS4;
+constexpr int NP_W1 = 0, NP_W2 = 10240, NP_B2 = 18432, NP_W3 = 18560, NP_B3 = 26752, NP_W4 = 26816, NP_B4 = 28864;
+constexpr int CTRL_NODE_PARTIAL = 28896;
+constexpr size_t NB_STAGE = (size_t)(72 + 168) * NB_CH * 2;
+
+size_t ctrl_node_bwd_lds() { return (size_t)NODE_RM_ELEMS * 2 + CTRL_VEC * 4 + NB_STAGE; }
+
+DEV float sigm(float x) { return 1.f / (1.f + __expf(-x)); }
+
+DEV void add_tile(float* dst, int ncols, int mt, int nt, const f32x16& c, int lane) {
+  const int r = lane & 31, h = lane >> 5;
+#pragma unroll
+  for (int reg = 0; reg < 16; ++reg) dst[(32 * mt + acc_row(reg, h)) * ncols + 32 * nt + r] += c[reg];
+}
+
+__global__ __launch_bounds__(NB_WAVES * 64, 1) void ctrl_node_bwd_kernel(CtrlNodeBwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  bf16* wr = reinterpret_cast<bf16*>(smem);
+  float* vl = reinterpret_cast<float*>(smem + NODE_RM_ELEMS * 2);
+  bf16* stg = reinterpret_cast<bf16*>(smem + NODE_RM_ELEMS * 2 + CTRL_VEC * 4);
+  block_copy16(wr, a.wrm, NODE_RM_ELEMS * 2);
+  block_copy16(vl, a.wvec, CTRL_VEC * 4);
+  __syncthreads();
+  const float* nb2 = vl + 128;
+  const float* nb3 = vl + 256;
+  const float* nb4 = vl + 320;
+  const int wave = threadIdx.x / WAVE, lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
+  const int N = a.N;
+  const int total = a.B * N;
+  const long nchunks = (total + NB_CH - 1) / NB_CH;
+  const int erow = wave * 32 + r;
+
+  f32x16 acc1[3], acc2[2], acc3[2], acc4;
+#pragma unroll
+  for (int q = 0; q < 3; ++q) acc1[q] = zero16();
+  acc2[0] = acc2[1] = acc3[0] = acc3[1] = acc4 = zero16();
+  float bs2[2] = {0.f, 0.f}, bs3[2] = {0.f, 0.f}, bs4 = 0.f;
+  const int n1 = (wave < 2) ? 3 : 2;
+
+  for (long chunk = blockIdx.x; chunk < nchunks; chunk += gridDim.x) {
+    const int ga = (int)(chunk * NB_CH) + erow;
+    const bool ok = ga < total;
+    int b = 0, i = 0;
+    float4 si = make_float4(0.f, 0.f, 0.f, 0.f);
+    float2 gg = make_float2(0.f, 0.f), av = make_float2(0.f, 0.f);
+    float4 gn = make_float4(0.f, 0.f, 0.f, 0.f);
+    bool vld = false;
+    bf16x8 Pf[9];
+    const bf16 z = (bf16)0.f;   // Pf is dead after Y1; S1 re-reads the pooled rows
+    if (ok) {
+      b = ga / N; i = ga - b * N;
+      si = a.S[(long)b * a.s_env + i];
+      gg = a.G[(long)b * N + i];
+      av = a.A[(long)b * a.a_env + i];
+      if (a.Gn) gn = a.Gn[(long)b * a.gn_env + i];
+      vld = a.valid ? (a.valid[(long)b * a.v_env] != 0) : true;
+      const bf16* prow = a.pooled + (long)b * a.p_env + (long)i * 128;
+#pragma unroll
+      for (int kk = 0; kk < 8; ++kk) Pf[kk] = *reinterpret_cast<const bf16x8*>(prow + 16 * kk + 8 * h);
+    } else {
+#pragma unroll
+      for (int kk = 0; kk < 8; ++kk)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) Pf[kk][j] = z;
+    }
+    const float ex = si.x - gg.x, ey = si.y - gg.y;
+    Pf[8] = node_state_frag(ex, ey, si.z, si.w, ok, h);
+    const bf16* W1 = wr + opaque_zero();
+    const bf16* W2 = W1 + 64 * NS1;
+    const bf16* W3 = W2 + 128 * NS2;
+    const bf16* W4 = W3 + 64 * NS3;
+    // ---- forward recompute
+    bf16x16 Y1b[2], Y2b[4], Y3b[2];
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt) {
+      f32x16 c = zero16();
+#pragma unroll
+      for (int kk = 0; kk < 9; ++kk) c = mfma(wrm_nat(W1 + opaque_zero(), NS1, 32 * mt, kk, lane), Pf[kk], c);
+      relu_(c);
+      Y1b[mt] = to_bf16x16(c);
+    }
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+      f32x16 c = bias_rows(nb2, 32 * mt, h);
+      static_for<4>([&](auto kk_) {
+        constexpr int kk = decltype(kk_)::value;
+        c = mfma(wrm_acc(W2 + opaque_zero(), NS2, 32 * mt, kk, lane), bacc_frag<kk & 1>(Y1b[kk >> 1]), c);
+      });
+      relu_(c);
+      Y2b[mt] = to_bf16x16(c);
+    }
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt) {
+      f32x16 c = bias_rows(nb3, 32 * mt, h);
+      static_for<8>([&](auto kk_) {
+        constexpr int kk = decltype(kk_)::value;
+        c = mfma(wrm_acc(W3 + opaque_zero(), NS3, 32 * mt, kk, lane), bacc_frag<kk & 1>(Y2b[kk >> 1]), c);
+      });
+      relu_(c);
+      Y3b[mt] = to_bf16x16(c);
+    }
+    f32x16 y4 = bias_rows(nb4, 0, h);
+    static_for<4>([&](auto kk_) {
+      constexpr int kk = decltype(kk_)::value;
+      y4 = mfma(wrm_acc(W4 + opaque_zero(), NS4, 0, kk, lane), bacc_frag<kk & 1>(Y3b[kk >> 1]), y4);
+    });
+    // ---- gain law + action loss backward (lanes h == 0 own agent r; rows 0..3 = regs 0..3)
+    f32x16 d4 = zero16();
+    float4 egod = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (ok && h == 0) {
+      const float s0 = sigm(y4[0]), s1 = sigm(y4[1]), s2 = sigm(y4[2]), s3 = sigm(y4[3]);
+      const float k0 = 2.f * s0 + 0.2f, k1 = 2.f * s1 + 0.2f, k2 = 2.f * s2 + 0.2f, k3 = 2.f * s3 + 0.2f;
+      float dax = a.dt * gn.z, day = a.dt * gn.w;
+      if (vld && a.act_coef != 0.f) {
+        const float rx = -(ex + a.sqrt3 * si.z), ry = -(ey + a.sqrt3 * si.w);
+        const float diff = (av.x * av.x + av.y * av.y) - (rx * rx + ry * ry);
+        const float sg = diff > 0.f ? 1.f : (diff < 0.f ? -1.f : 0.f);
+        const float c = a.act_coef * sg;
+        dax += c * 2.f * av.x;
+        day += c * 2.f * av.y;
+        egod.x += c * 2.f * rx;
+        egod.y += c * 2.f * ry;
+        egod.z += c * 2.f * a.sqrt3 * rx;
+        egod.w += c * 2.f * a.sqrt3 * ry;
+      }
+      // a_x = -(k0 ex + k1 vx), a_y = -(k2 ey + k3 vy)
+      egod.x += -k0 * dax;
+      egod.z += -k1 * dax;
+      egod.y += -k2 * day;
+      egod.w += -k3 * day;
+      d4[0] = -dax * ex * 2.f * s0 * (1.f - s0);
+      d4[1] = -dax * si.z * 2.f * s1 * (1.f - s1);
+      d4[2] = -day * ey * 2.f * s2 * (1.f - s2);
+      d4[3] = -day * si.w * 2.f * s3 * (1.f - s3);
+    }
+    const bf16x16 d4b = to_bf16x16(d4);
+    // Backward chain interleaved with the WG-shared weight-gradient stages so that each
+    // activation dies right after its last use (register pressure).
+    // ---- dY3 = W4^T dY4 (K = 32) . relu'(Y3)
+    bf16x16 d3b[2];
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt) {
+      f32x16 c = zero16();
+      static_for<2>([&](auto kk_) {
+        constexpr int kk = decltype(kk_)::value;
+        c = mfma(wrmT_acc(W4 + opaque_zero(), NS4, 32 * mt, kk, lane), bacc_frag<kk & 1>(d4b), c);
+      });
+#pragma unroll
+      for (int q = 0; q < 16; ++q) c[q] = ((float)Y3b[mt][q] > 0.f) ? c[q] : 0.f;
+      d3b[mt] = to_bf16x16(c);
+    }
+    {   // S4: dWn4pad (32x64) += dY4 . Y3^T ; nb4
+      bf16* imA = stg;
+      bf16* imB = stg + NB_CH * 40;
+      store_tile(imA, 40, erow, 0, d4b, h);
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt) store_tile(imB, 72, erow, 32 * mt, Y3b[mt], h);
+      __syncthreads();
+      if (wave < 2) bs4 += stage_mma(imA, 40, imB, 72, 0, wave, NB_CH / 16, lane, acc4, wave == 0);
+      __syncthreads();
+    }
+    // ---- dY2 = W3^T dY3 . relu'(Y2)
+    bf16x16 d2b[4];
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+      f32x16 c = zero16();
+      static_for<4>([&](auto kk_) {
+        constexpr int kk = decltype(kk_)::value;
+        c = mfma(wrmT_acc(W3 + opaque_zero(), NS3, 32 * mt, kk, lane), bacc_frag<kk & 1>(d3b[kk >> 1]), c);
+      });
+#pragma unroll
+      for (int q = 0; q < 16; ++q) c[q] = ((float)Y2b[mt][q] > 0.f) ? c[q] : 0.f;
+      d2b[mt] = to_bf16x16(c);
+    }
+    {   // S3: dWn3 (64x128) += dY3 . Y2^T ; nb3
+      bf16* imA = stg;
+      bf16* imB = stg + NB_CH * 72;
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt) store_tile(imA, 72, erow, 32 * mt, d3b[mt], h);
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) store_tile(imB, 136, erow, 32 * mt, Y2b[mt], h);
+      __syncthreads();
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int t = wave + 4 * u;
+        bs3[u] += stage_mma(imA, 72, imB, 136, t / 4, t % 4, NB_CH / 16, lane, acc3[u], t % 4 == 0);
+      }
+      __syncthreads();
+    }
+    // ---- dY1 = W2^T dY2 . relu'(Y1)
+    bf16x16 d1b[2];
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt) {
+      f32x16 c = zero16();
+      static_for<8>([&](auto kk_) {
+        constexpr int kk = decltype(kk_)::value;
+        c = mfma(wrmT_acc(W2 + opaque_zero(), NS2, 32 * mt, kk, lane), bacc_frag<kk & 1>(d2b[kk >> 1]), c);
+      });
+#pragma unroll
+      for (int q = 0; q < 16; ++q) c[q] = ((float)Y1b[mt][q] > 0.f) ? c[q] : 0.f;
+      d1b[mt] = to_bf16x16(c);
+    }
+    {   // S2: dWn2 (128x64) += dY2 . Y1^T ; nb2
+      bf16* imA = stg;
+      bf16* imB = stg + NB_CH * 136;
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) store_tile(imA, 136, erow, 32 * mt, d2b[mt], h);
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt) store_tile(imB, 72, erow, 32 * mt, Y1b[mt], h);
+      __syncthreads();
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int t = wave + 4 * u;
+        bs2[u] += stage_mma(imA, 136, imB, 72, t / 2, t % 2, NB_CH / 16, lane, acc2[u], t % 2 == 0);
+      }
+      __syncthreads();
+    }
+    // ---- dP = W1f^T dY1 : rows 0..127 pooled grads -> global; rows 128..131 state grads
+#pragma unroll
+    for (int mt = 0; mt < 5; ++mt) {
+      f32x16 c = zero16();
+      static_for<4>([&](auto kk_) {
+        constexpr int kk = decltype(kk_)::value;
+        c = mfma(wrmT_acc(W1 + opaque_zero(), NS1, 32 * mt, kk, lane), bacc_frag<kk & 1>(d1b[kk >> 1]), c);
+      });
+      if (mt < 4) {
+        if (ok) {
+          bf16* drow = a.dP + (long)b * a.dp_env + (long)i * 128 + 32 * mt;
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            bf16x4 v;
+            v[0] = (bf16)c[4 * g]; v[1] = (bf16)c[4 * g + 1]; v[2] = (bf16)c[4 * g + 2]; v[3] = (bf16)c[4 * g + 3];
+            *reinterpret_cast<bf16x4*>(drow + 8 * g + 4 * h) = v;
+          }
+        }
+      } else if (ok && h == 0) {
+        egod.x += c[0];   // d/d(ex) -> x
+        egod.y += c[1];   // d/d(ey) -> y
+        egod.z += c[2];   // vx
+        egod.w += c[3];   // vy
+        a.ego[(long)b * N + i] = egod;
+      }
+    }
+    {   // S1: dWn1f (64x160) += dY1 . P^T  (P re-read from the pooled rows: L2-hot)
+      bf16* imA = stg;
+      bf16* imB = stg + NB_CH * 72;
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt) store_tile(imA, 72, erow, 32 * mt, d1b[mt], h);
+      const bf16x8 sf = node_state_frag(ex, ey, si.z, si.w, ok, h);
+      const bf16* prow = a.pooled + (long)b * a.p_env + (long)i * 128;
+      bf16x8 zz;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) zz[j] = z;
+#pragma unroll
+      for (int kk = 0; kk < 8; ++kk) {
+        const bf16x8 pv = ok ? *reinterpret_cast<const bf16x8*>(prow + 16 * kk + 8 * h) : zz;
+        *reinterpret_cast<bf16x8*>(imB + erow * NS1 + 16 * kk + 8 * h) = pv;
+      }
+      *reinterpret_cast<bf16x8*>(imB + erow * NS1 + 128 + 8 * h) = sf;
+      *reinterpret_cast<bf16x8*>(imB + erow * NS1 + 144 + 8 * h) = zz;
+      __syncthreads();
+#pragma unroll
+      for (int u = 0; u < 3; ++u) {
+        const int t = wave + 4 * u;
+        if (u < n1) stage_mma(imA, 72, imB, NS1, t / 5, t % 5, NB_CH / 16, lane, acc1[u], false);
+      }
+      __syncthreads();
+    }
+  }
+  // ---- slab += this workgroup's partial (fixed WG -> slab map: deterministic)
+  float* P = a.partial + (long)blockIdx.x * CTRL_NODE_PARTIAL;
+#pragma unroll
+  for (int u = 0; u < 3; ++u) {
+    const int t = wave + 4 * u;
+    if (u < n1) add_tile(P + NP_W1, 160, t / 5, t % 5, acc1[u], lane);
+  }
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int t2 = wave + 4 * u;
+    add_tile(P + NP_W2, 64, t2 / 2, t2 % 2, acc2[u], lane);
+    const float s2 = bs2[u] + shfl_xor32(bs2[u]);
+    if (t2 % 2 == 0 && h == 0) P[NP_B2 + 32 * (t2 / 2) + r] += s2;
+    const int t3 = wave + 4 * u;
+    add_tile(P + NP_W3, 128, t3 / 4, t3 % 4, acc3[u], lane);
+    const float s3 = bs3[u] + shfl_xor32(bs3[u]);
+    if (t3 % 4 == 0 && h == 0) P[NP_B3 + 32 * (t3 / 4) + r] += s3;
+  }
+  if (wave < 2) {
+    add_tile(P + NP_W4, 64, 0, wave, acc4, lane);
+    if (wave == 0) {
+      const float s4 = bs4 + shfl_xor32(bs4);
+      if (h == 0) P[NP_B4 + r] += s4;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+constexpr int EB_WAVES = 4;
+constexpr int EB_CH = EB_WAVES * 32;     // agents per chunk (each round: 128 edges)
+constexpr int EP_W2 = 0, EP_B2 = 8192, EP_W1 = 8320;
+constexpr int CTRL_EDGE_PARTIAL = 10368;
+constexpr size_t EB_STAGE = (size_t)(136 + 72) * EB_CH * 2;
+
+size_t ctrl_edge_bwd_lds() { return (size_t)22 * FRAG_BYTES + EB_STAGE; }
+
+__global__ __launch_bounds__(EB_WAVES * 64, 2) void ctrl_edge_bwd_kernel(CtrlEdgeBwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  bf16* wf = reinterpret_cast<bf16*>(smem);                 // ew1f (2) | ew2tn (16) | ew1ft (4)
+  bf16* stg = reinterpret_cast<bf16*>(smem + 22 * FRAG_BYTES);
+  block_copy16(wf, a.wpack + (size_t)a.f_ew1f * 512, 2 * FRAG_BYTES);
+  block_copy16(wf + 2 * 512, a.wpack + (size_t)a.f_ew2tn * 512, 20 * FRAG_BYTES);
+  __syncthreads();
+  const int wave = threadIdx.x / WAVE, lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
+  const int N = a.N, K = a.K;
+  const int total = a.B * N;
+  const long nchunks = (total + EB_CH - 1) / EB_CH;
+  const int erow = wave * 32 + r;
+  f32x16 accW2[2], accW1;
+  accW2[0] = accW2[1] = accW1 = zero16();
+  float bs[2] = {0.f, 0.f};
+  const bf16 z = (bf16)0.f;
+
+  for (long chunk = blockIdx.x; chunk < nchunks; chunk += gridDim.x) {
+    for (int q = 0; q < 16; ++q) {
+      const int al = 2 * q + (r >> 4);
+      const int slot = r & 15;
+      const int ga = (int)(chunk * EB_CH) + wave * 32 + al;
+      const bool ok = (ga < total) && (slot < K);
+      int b = 0, i = 0, j = 0;
+      float4 rel = make_float4(0.f, 0.f, 0.f, 0.f);
+      float eye = 0.f;
+      if (ok) {
+        b = ga / N; i = ga - b * N;
+        j = a.idx[(long)b * a.i_env + (long)i * K + slot];
+        const float4 si = a.S[(long)b * a.s_env + i];
+        const float4 sj = a.S[(long)b * a.s_env + j];
+        rel = make_float4(si.x - sj.x, si.y - sj.y, si.z - sj.z, si.w - sj.w);
+        eye = (j == i) ? 1.f : 0.f;
+      }
+      const bf16x8 F = ctrl_edge_frag(rel, eye, ok, h);
+      const bf16* wt = wf + opaque_zero();
+      bf16x16 H1b[2];
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt) {
+        f32x16 c = mfma(frag_ld(wt, mt, lane), F, zero16());
+        relu_(c);
+        H1b[mt] = to_bf16x16(c);
+      }
+      // max-pool backward: this edge receives dP[f] where it was the argmax slot
+      bf16x8 dz[8];
+#pragma unroll
+      for (int kk = 0; kk < 8; ++kk) {
+        bf16x8 v;
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj) v[jj] = z;
+        if (ok) {
+          const int f0 = 16 * kk + 8 * h;
+          const uint64_t am = *reinterpret_cast<const uint64_t*>(a.argmax + (long)b * a.am_env + (long)i * 128 + f0);
+          const bf16x8 dp = *reinterpret_cast<const bf16x8*>(a.dP + (long)b * a.dp_env + (long)i * 128 + f0);
+#pragma unroll
+          for (int jj = 0; jj < 8; ++jj) v[jj] = (((am >> (8 * jj)) & 0xFFull) == (uint64_t)slot) ? dp[jj] : z;
+        }
+        dz[kk] = v;
+      }
+      // dH1 = W2^T dZ (natural k) . relu'(H1)
+      bf16x16 d1b[2];
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt) {
+        f32x16 c = zero16();
+#pragma unroll
+        for (int kk = 0; kk < 8; ++kk) c = mfma(frag_ld(wt, 2 + mt * 8 + kk, lane), dz[kk], c);
+#pragma unroll
+        for (int qq = 0; qq < 16; ++qq) c[qq] = ((float)H1b[mt][qq] > 0.f) ? c[qq] : 0.f;
+        d1b[mt] = to_bf16x16(c);
+      }
+      // dF = W1^T dH1 -> rows dx dy dvx dvy (lanes h == 0, regs 0..3)
+      {
+        f32x16 c = zero16();
+        static_for<4>([&](auto kk_) {
+          constexpr int kk = decltype(kk_)::value;
+          c = mfma(frag_ld(wt, 18 + kk, lane), bacc_frag<kk & 1>(d1b[kk >> 1]), c);
+        });
+        if (ok && h == 0) {
+          const float4 g = (j != i) ? make_float4(c[0], c[1], c[2], c[3]) : make_float4(0.f, 0.f, 0.f, 0.f);
+          a.dEc[(long)b * a.de_env + (long)i * K + slot] = g;
+        }
+      }
+      // S1: dW2 (128x64) += dZ . H1^T ; eb2
+      {
+        bf16* imA = stg;
+        bf16* imB = stg + EB_CH * 136;
+#pragma unroll
+        for (int kk = 0; kk < 8; ++kk) *reinterpret_cast<bf16x8*>(imA + erow * 136 + 16 * kk + 8 * h) = dz[kk];
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt) store_tile(imB, 72, erow, 32 * mt, H1b[mt], h);
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const int t = wave + 4 * u;
+          bs[u] += stage_mma(imA, 136, imB, 72, t / 2, t % 2, EB_CH / 16, lane, accW2[u], t % 2 == 0);
+        }
+        __syncthreads();
+      }
+      // S2: dW1f (64x32) += dH1 . F^T
+      {
+        bf16* imA = stg;
+        bf16* imB = stg + EB_CH * 72;
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt) store_tile(imA, 72, erow, 32 * mt, d1b[mt], h);
+        bf16x8 zz;
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj) zz[jj] = z;
+        *reinterpret_cast<bf16x8*>(imB + erow * 40 + 8 * h) = F;
+        *reinterpret_cast<bf16x8*>(imB + erow * 40 + 16 + 8 * h) = zz;
+        __syncthreads();
+        if (wave < 2) stage_mma(imA, 72, imB, 40, wave, 0, EB_CH / 16, lane, accW1, false);
+        __syncthreads();
+      }
+    }
+  }
+  float* P = a.partial + (long)blockIdx.x * CTRL_EDGE_PARTIAL;
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int t = wave + 4 * u;
+    add_tile(P + EP_W2, 64, t / 2, t % 2, accW2[u], lane);
+    const float s = bs[u] + shfl_xor32(bs[u]);
+    if (t % 2 == 0 && h == 0) P[EP_B2 + 32 * (t / 2) + r] += s;
+  }
+  if (wave < 2) add_tile(P + EP_W1, 32, wave, 0, accW1, lane);
+}
+
+}  // namespace mb
+
+extern "C" int mb_ctrl_node_bwd(const mb::CtrlNodeBwdArgs* a, int num_blocks, hipStream_t st) {
+  using namespace mb;
+  const size_t lds = ctrl_node_bwd_lds();
+  (void)hipFuncSetAttribute((const void*)ctrl_node_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipLaunchKernelGGL(ctrl_node_bwd_kernel, dim3(num_blocks), dim3(NB_WAVES * 64), lds, st, *a);
+  return (int)hipGetLastError();
+}
+
+extern "C" int mb_ctrl_edge_bwd(const mb::CtrlEdgeBwdArgs* a, int num_blocks, hipStream_t st) {
+  using namespace mb;
+  if (a->K > 16 || a->K < 1) return -1;
+  const size_t lds = ctrl_edge_bwd_lds();
+  (void)hipFuncSetAttribute((const void*)ctrl_edge_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipLaunchKernelGGL(ctrl_edge_bwd_kernel, dim3(num_blocks), dim3(EB_WAVES * 64), lds, st, *a);
   return (int)hipGetLastError();
 }

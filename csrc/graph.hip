@@ -1,0 +1,169 @@
+// Edge -> node gradient reduction without float atomics (deterministic), gfx950.
+//
+// A kNN graph is not symmetric, so dL/d(s_i - s_j) of edge (i -> slot k -> j) must be added
+// to s_i and subtracted from s_j. Instead of per-edge atomics (64 lanes hitting 64 random
+// rows = the slowest atomic shape on CDNA4), each timestep graph gets a reverse CSR (incoming
+// edges per target, sorted by edge id), and one thread per agent gathers
+//   G_i = sum_k dE[i,k] - sum_{e in in(i)} dE[e]
+// in a fixed order. rev_csr_kernel builds the CSR for all B*T graphs in one launch
+// (one workgroup per graph, LDS counting sort).
+#include "common.h"
+#include "args.h"
+
+namespace mb {
+
+constexpr int CSR_BLOCK = 256;
+
+__global__ __launch_bounds__(CSR_BLOCK) void rev_csr_kernel(CsrArgs a) {
+  extern __shared__ __attribute__((aligned(16))) int sm[];
+  int* cnt = sm;                 // N + 1
+  int* fill = sm + a.N + 1;      // N
+  __shared__ int wsum[CSR_BLOCK];
+  const long g = blockIdx.x;
+  const int N = a.N, K = a.K, NK = N * K;
+  const int* idx = a.idx + g * NK;
+  for (int q = threadIdx.x; q <= N; q += CSR_BLOCK) cnt[q] = 0;
+  for (int q = threadIdx.x; q < N; q += CSR_BLOCK) fill[q] = 0;
+  __syncthreads();
+  for (int e = threadIdx.x; e < NK; e += CSR_BLOCK) {
+    const int j = idx[e];
+    if (j != e / K) atomicAdd(&cnt[j + 1], 1);
+  }
+  __syncthreads();
+  // exclusive scan of cnt[1..N] into cnt[0..N] (two-level: per-thread segment, then totals)
+  const int seg = (N + CSR_BLOCK - 1) / CSR_BLOCK;
+  const int lo = threadIdx.x * seg + 1, hi = min(lo + seg, N + 1);
+  int run = 0;
+  for (int q = lo; q < hi; ++q) { run += cnt[q]; cnt[q] = run; }
+  wsum[threadIdx.x] = run;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int acc = 0;
+    for (int w = 0; w < CSR_BLOCK; ++w) { const int v = wsum[w]; wsum[w] = acc; acc += v; }
+  }
+  __syncthreads();
+  const int off = wsum[threadIdx.x];
+  for (int q = lo; q < hi; ++q) cnt[q] += off;
+  __syncthreads();
+  int* ptr = a.ptr + g * (N + 1);
+  for (int q = threadIdx.x; q <= N; q += CSR_BLOCK) ptr[q] = cnt[q];
+  int* out = a.edges + g * NK;
+  for (int e = threadIdx.x; e < NK; e += CSR_BLOCK) {
+    const int j = idx[e];
+    if (j != e / K) {
+      const int p = atomicAdd(&fill[j], 1);
+      out[cnt[j] + p] = e;
+    }
+  }
+  __threadfence();     // fill writes visible before other threads of the block sort them
+  __syncthreads();
+  // deterministic order inside each bucket: insertion sort by edge id
+  for (int j = threadIdx.x; j < N; j += CSR_BLOCK) {
+    const int b0 = cnt[j], b1 = cnt[j + 1];
+    for (int x = b0 + 1; x < b1; ++x) {
+      const int v = out[x];
+      int y = x - 1;
+      while (y >= b0 && out[y] > v) { out[y + 1] = out[y]; --y; }
+      out[y + 1] = v;
+    }
+  }
+}
+
+// dS[b, t', i] (+)= reduce of pass-0 edges of graph (b,t') and pass-1 edges of graph (b,t'-1)
+__global__ __launch_bounds__(256) void node_reduce_kernel(NodeRedArgs a) {
+  const long tid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long total = (long)a.B * (a.T + 1) * a.N;
+  if (tid >= total) return;
+  // time-major: out[(t'*B + b)*N + i], graphs g = t*B + b
+  const int i = (int)(tid % a.N);
+  const long tb = tid / a.N;
+  const int tp = (int)(tb / a.B);
+  const int b = (int)(tb - (long)tp * a.B);
+  const int N = a.N, K = a.K;
+  const long E = (long)a.B * a.T * N * K;
+  float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int pass = 0; pass < a.passes; ++pass) {
+    const int t = tp - pass;
+    if (t < 0 || t >= a.T) continue;
+    const long gi = (long)t * a.B + b;
+    const float4* dE = a.dE + (long)pass * E + gi * N * K;
+    for (int k = 0; k < K; ++k) {
+      const float4 v = dE[(long)i * K + k];
+      g.x += v.x; g.y += v.y; g.z += v.z; g.w += v.w;
+    }
+    const int* ptr = a.ptr + gi * (N + 1);
+    const int* edges = a.edges + gi * (long)N * K;
+    for (int q = ptr[i]; q < ptr[i + 1]; ++q) {
+      const float4 v = dE[edges[q]];
+      g.x -= v.x; g.y -= v.y; g.z -= v.z; g.w -= v.w;
+    }
+  }
+  float4* o = a.out + ((long)tp * a.B + b) * N + i;
+  if (a.accumulate) {
+    const float4 p = *o;
+    g.x += p.x; g.y += p.y; g.z += p.z; g.w += p.w;
+  }
+  *o = g;
+}
+
+// One reverse-time step of the BPTT recursion (train.py:58-103 through autograd in the
+// reference; hand-derived here):
+//   G_t = dS_direct[t] + ego_t + sum_k dEc[i,k] - sum_in dEc[e]
+//         + Euler adjoint of s_{t+1} = s_t + dt [v_t, a_t]  (if bptt)
+__global__ __launch_bounds__(256) void node_combine_kernel(CombineArgs a) {
+  const long tid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (tid >= (long)a.B * a.N) return;
+  const int b = (int)(tid / a.N), i = (int)(tid % a.N);
+  const int N = a.N, K = a.K;
+  float4 g = a.dS[(long)b * a.ds_env + i];
+  if (a.ego) {
+    const float4 v = a.ego[(long)b * N + i];
+    g.x += v.x; g.y += v.y; g.z += v.z; g.w += v.w;
+  }
+  if (a.dEc) {
+    const float4* dE = a.dEc + (long)b * N * K;
+    for (int k = 0; k < K; ++k) {
+      const float4 v = dE[(long)i * K + k];
+      g.x += v.x; g.y += v.y; g.z += v.z; g.w += v.w;
+    }
+    const int* ptr = a.ptr + (long)b * a.ptr_env;
+    const int* edges = a.edges + (long)b * a.edges_env;
+    for (int q = ptr[i]; q < ptr[i + 1]; ++q) {
+      const float4 v = dE[edges[q]];
+      g.x -= v.x; g.y -= v.y; g.z -= v.z; g.w -= v.w;
+    }
+  }
+  if (a.Gn) {
+    const float4 n = a.Gn[(long)b * a.gn_env + i];
+    g.x += n.x;
+    g.y += n.y;
+    g.z += n.z + a.dt * n.x;
+    g.w += n.w + a.dt * n.y;
+  }
+  a.Gout[(long)b * a.go_env + i] = g;
+}
+
+}  // namespace mb
+
+extern "C" int mb_rev_csr(const mb::CsrArgs* a, hipStream_t st) {
+  using namespace mb;
+  const size_t lds = (size_t)(2 * a->N + 1) * 4;
+  if (lds > 150 * 1024) return -1;
+  (void)hipFuncSetAttribute((const void*)rev_csr_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipLaunchKernelGGL(rev_csr_kernel, dim3(a->G), dim3(CSR_BLOCK), lds, st, *a);
+  return (int)hipGetLastError();
+}
+
+extern "C" int mb_node_reduce(const mb::NodeRedArgs* a, hipStream_t st) {
+  using namespace mb;
+  const long total = (long)a->B * (a->T + 1) * a->N;
+  hipLaunchKernelGGL(node_reduce_kernel, dim3((total + 255) / 256), dim3(256), 0, st, *a);
+  return (int)hipGetLastError();
+}
+
+extern "C" int mb_node_combine(const mb::CombineArgs* a, hipStream_t st) {
+  using namespace mb;
+  const long total = (long)a->B * a->N;
+  hipLaunchKernelGGL(node_combine_kernel, dim3((total + 255) / 256), dim3(256), 0, st, *a);
+  return (int)hipGetLastError();
+}

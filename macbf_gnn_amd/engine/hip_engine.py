@@ -1,0 +1,221 @@
+"""The MI355X training step: native kernels end to end, no autograd.
+
+Per iteration (reference ``train.py:48-105``, intended semantics; all buffers time-major
+(T, B, N, ...) so the first T steps of a rollout are one contiguous block):
+
+rollout, t = 0.. (stops when every env is done; per-env done masks)
+    scan(s_t)      -> kNN idx, TTC danger bits + counts, all-pairs safety of s_t
+    ctrl_fwd(s_t)  -> a_t, s_{t+1}, pooled features + argmax slots (saved for backward),
+                      per-env goal distance / action-loss sums
+losses
+    counts all-reduced over DP ranks (global pooled normalisation)
+    cbf_fwd        -> h(s_t), h'(s_{t+1}) on the same slots, loss sums, dL/dh, dL/dh'
+backward
+    cbf_bwd        -> dL/d(s_i - s_j) per edge (h and h' paths) + CBF dW slabs
+    rev_csr + node_reduce -> direct dL/ds_t (edge -> node, deterministic, no atomics)
+    for t = T-1..0 (BPTT):  ctrl_node_bwd -> ctrl_edge_bwd -> node_combine
+                      (dA_t = dt*G_{t+1}[v] + action-loss grad; G_t = dL/ds_t)
+    slab reductions -> the flat gradient buffer (then RCCL all-reduce + fused Adam).
+"""
+from __future__ import annotations
+
+import torch
+
+from .. import config as C
+from ..ops import layout as L
+from ..ops import native
+from ..ops.weights import PackedWeights
+
+
+class HipEngine:
+    name = "hip"
+
+    def __init__(self, trainer):
+        self.tr = trainer
+        cfg = trainer.cfg
+        if not cfg.bptt:
+            raise NotImplementedError("HIP engine: --no_bptt is not implemented yet (oracle engine only)")
+        if not cfg.reuse_nbr_idx:
+            raise NotImplementedError("HIP engine requires reuse_nbr_idx (oracle engine supports recompute)")
+        native.lib()
+        self.dev = trainer.device
+        self.B, self.N = cfg.num_envs, cfg.num_agents
+        self.K = min(self.N, cfg.top_k)
+        if self.K > C.MAX_TOP_K:
+            raise ValueError(f"top_k <= {C.MAX_TOP_K} supported by the native kernels")
+        self.Tmax = cfg.inner_loops
+        self.pw = PackedWeights(trainer.fp)
+        offs = {pn: o for (m, pn, shape, o, n) in trainer.fp.specs}
+        mk = lambda a: torch.as_tensor(a, dtype=torch.long, device=self.dev)
+        self.maps = {}
+        for name, fn in (("cbf", L.cbf_grad_map), ("node", L.ctrl_node_grad_map), ("edge", L.ctrl_edge_grad_map)):
+            s, d = fn(offs)
+            self.maps[name] = (mk(s), mk(d))
+        self._alloc()
+
+    # ------------------------------------------------------------------ buffers
+    def _alloc(self):
+        B, N, K, T, dev = self.B, self.N, self.K, self.Tmax, self.dev
+        f32, i32, u8, bf = torch.float32, torch.int32, torch.uint8, torch.bfloat16
+        self.S = torch.zeros(T + 1, B, N, 4, dtype=f32, device=dev)
+        self.G = torch.zeros(B, N, 2, dtype=f32, device=dev)
+        self.A = torch.zeros(T, B, N, 2, dtype=f32, device=dev)
+        self.idx = torch.zeros(T, B, N, K, dtype=i32, device=dev)
+        self.dang = torch.zeros(T, B, N, K, dtype=u8, device=dev)
+        self.cnt = torch.zeros(T, B, 2, dtype=f32, device=dev)
+        self.safe = torch.zeros(T + 1, B, dtype=f32, device=dev)
+        self.dist = torch.zeros(T, B, dtype=f32, device=dev)
+        self.act = torch.zeros(T, B, dtype=f32, device=dev)
+        self.pooled = torch.zeros(T, B, N, 128, dtype=bf, device=dev)
+        self.argmax = torch.zeros(T, B, N, 128, dtype=u8, device=dev)
+        self.dh = torch.zeros(2 * T * B * N * K, dtype=f32, device=dev)
+        self.dE = torch.zeros(2 * T * B * N * K * 4, dtype=f32, device=dev)
+        self.rptr = torch.zeros(T * B, N + 1, dtype=i32, device=dev)
+        self.redges = torch.zeros(T * B, N * K, dtype=i32, device=dev)
+        self.dS = torch.zeros(T + 1, B, N, 4, dtype=f32, device=dev)
+        self.Gb = torch.zeros(T + 1, B, N, 4, dtype=f32, device=dev)
+        self.dP = torch.zeros(B, N, 128, dtype=bf, device=dev)
+        self.ego = torch.zeros(B, N, 4, dtype=f32, device=dev)
+        self.dEc = torch.zeros(B, N, K, 4, dtype=f32, device=dev)
+        self.counts = torch.zeros(3, dtype=f32, device=dev)
+        self.nb_node, self.nb_edge = native.ctrl_bwd_grids(B * N, dev)
+        self.part_node = torch.zeros(self.nb_node, native.CTRL_NODE_PARTIAL, dtype=f32, device=dev)
+        self.part_edge = torch.zeros(self.nb_edge, native.CTRL_EDGE_PARTIAL, dtype=f32, device=dev)
+        self.red_cbf = torch.zeros(native.CBF_PARTIAL, dtype=f32, device=dev)
+        self.red_node = torch.zeros(native.CTRL_NODE_PARTIAL, dtype=f32, device=dev)
+        self.red_edge = torch.zeros(native.CTRL_EDGE_PARTIAL, dtype=f32, device=dev)
+        self.host_dist = torch.zeros(T, B, dtype=f32, pin_memory=True)
+        self._part_cbf = {}
+        self._part_fwd = {}
+
+    def after_update(self):
+        self.pw.update()
+
+    # ------------------------------------------------------------------ rollout
+    def rollout(self, s0, g):
+        cfg = self.tr.cfg
+        B, N, K = self.B, self.N, self.K
+        pw = self.pw
+        self.S[0].copy_(s0)
+        self.G.copy_(g)
+        self.cnt.zero_()
+        self.safe.zero_()
+        self.dist.zero_()
+        self.act.zero_()
+        events = []
+        T = self.Tmax
+        for t in range(self.Tmax):
+            native.scan(self.S[t], self.idx[t], self.dang[t], self.cnt[t], self.safe[t], K=K,
+                        do_knn=True, do_safety=cfg.compute_safety)
+            noise = None
+            if cfg.add_noise_prob > 0:
+                coin = (torch.rand(B, 1, 1, device=self.dev, generator=self.tr.torch_gen) < cfg.add_noise_prob)
+                noise = (torch.randn(B, N, 2, device=self.dev, generator=self.tr.torch_gen) * cfg.noise_scale
+                         * coin.to(torch.float32)).contiguous()
+            native.ctrl_fwd(self.S[t], self.G, self.idx[t], pw.ctrl_w, pw.ctrl_off["ew1f"], pw.ctrl_off["nw1f"],
+                            pw.ctrl_v, self.A[t], self.S[t + 1], self.dist[t], self.act[t], noise=noise,
+                            pooled=self.pooled[t], argmax=self.argmax[t])
+            if cfg.early_stop:
+                self.host_dist[t].copy_(self.dist[t], non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record()
+                events.append(ev)
+                # 1-step-lagged host check: never stalls the queue on the step just issued
+                if t >= 1:
+                    events[t - 1].synchronize()
+                    if self._all_done(t - 1):
+                        T = t + 1   # step t was already issued; its envs are masked out
+                        break
+        if cfg.compute_safety:
+            native.scan(self.S[T], None, None, None, self.safe[T], K=K, do_knn=False, do_safety=True)
+        return T
+
+    def _all_done(self, t):
+        d = self.host_dist[: t + 1] / self.N < C.DIST_MIN_CHECK      # (t+1, B)
+        return bool(d.any(0).all())
+
+    # ------------------------------------------------------------------ step
+    def step(self, s0, g):
+        tr = self.tr
+        cfg = tr.cfg
+        B, N, K = self.B, self.N, self.K
+        pw = self.pw
+        T = self.rollout(s0, g)
+        # validity: step t of env b counts iff the env was not done before t
+        done = (self.dist[:T] / N) < C.DIST_MIN_CHECK                 # (T, B)
+        di = done.to(torch.int32)
+        valid = ((torch.cumsum(di, 0) - di) == 0)
+        valid_u8 = valid.to(torch.uint8).contiguous()
+        vf = valid.to(torch.float32)
+        # pooled counts (global over DP ranks)
+        self.counts[0] = (self.cnt[:T, :, 0] * vf).sum()
+        self.counts[1] = (self.cnt[:T, :, 1] * vf).sum()
+        self.counts[2] = vf.sum() * N
+        tr.dp.all_reduce_(self.counts)
+        n_act = self.counts[2].clamp_min(1.0)
+        E = T * B * N * K
+        # ---- CBF forward: h, h', loss sums, upstream grads
+        S = self.S[: T + 1]
+        idx = self.idx[:T]
+        nbf = native.cbf_fwd_grid(E, self.dev)
+        part_fwd = self._buf(self._part_fwd, nbf, 10)
+        dh = self.dh[: 2 * E].view(2, T, B, N, K)
+        native.cbf_fwd(S, idx, pw.cbf_w, pw.cbf_off["w1f"], pw.cbf_v, dang=self.dang[:T], valid=valid_u8, two=True,
+                       dh_out=dh, counts=self.counts, partial=part_fwd, num_blocks=nbf)
+        # ---- CBF backward (both paths) -> per-edge feature grads + dW slabs
+        nbb = native.cbf_bwd_grid(2 * E, self.dev)
+        part_cbf = self._buf(self._part_cbf, nbb, native.CBF_PARTIAL)
+        dE = self.dE[: 2 * E * 4].view(2, T, B, N, K, 4)
+        native.cbf_bwd(S, idx, dh, pw.cbf_w, pw.cbf_off["w1f"], pw.cbf_v, passes=2, dE=dE, partial=part_cbf,
+                       num_blocks=nbb)
+        rptr = self.rptr[: T * B]
+        redges = self.redges[: T * B]
+        native.rev_csr(idx.view(T * B, N, K), rptr, redges)
+        native.node_reduce(dE, rptr, redges, self.dS, T=T, B=B, N=N, K=K, passes=2)
+        # ---- BPTT through the rollout
+        self.part_node.zero_()
+        self.part_edge.zero_()
+        act_coef = (C.LOSS_SCALE * C.LOSS_WEIGHTS[4]) / n_act
+        act_coef_f = float(act_coef)   # one host read per step (counts already reduced)
+        self.Gb[T].copy_(self.dS[T])
+        rptr3 = rptr.view(T, B, N + 1)
+        redges3 = redges.view(T, B, N * K)
+        for t in range(T - 1, -1, -1):
+            native.ctrl_node_bwd(self.pooled[t], self.S[t], self.G, self.A[t], self.Gb[t + 1], valid_u8[t],
+                                 pw.ctrl_rm, pw.node_rm_off, pw.ctrl_v, act_coef_f, self.dP, self.ego,
+                                 self.part_node, self.nb_node)
+            native.ctrl_edge_bwd(self.S[t], self.idx[t], self.argmax[t], self.dP, pw.ctrl_w, pw.ctrl_off["ew1f"],
+                                 pw.ctrl_off["ew2tn"], self.dEc, self.part_edge, self.nb_edge)
+            native.node_combine(self.dS[t], self.ego, self.dEc, rptr3[t], redges3[t], self.Gb[t + 1], self.Gb[t], K=K)
+        # ---- weight-gradient slabs -> flat grad
+        fg = tr.fp.grad
+        fg.zero_()
+        for name, part, red in (("cbf", part_cbf, self.red_cbf), ("node", self.part_node, self.red_node),
+                                ("edge", self.part_edge, self.red_edge)):
+            native.reduce_rows(part, red)
+            src, dst = self.maps[name]
+            fg.index_add_(0, dst, red.index_select(0, src))
+        # ---- stats (device tensors; converted lazily by the logger)
+        sums = part_fwd.to(torch.float64).sum(0)
+        nd = 1e-5 + self.counts[0].double()
+        ns = 1e-5 + self.counts[1].double()
+        act_sum = (self.act[:T].double() * valid.double()).sum()
+        w = C.LOSS_WEIGHTS
+        ld, ls, ldd, lsd = sums[2] / nd, sums[3] / ns, sums[6] / nd, sums[7] / ns
+        la = act_sum / n_act.double()
+        total = C.LOSS_SCALE * (w[0] * ld + w[1] * ls + w[2] * ldd + w[3] * lsd + w[4] * la)
+        safe_next = self.safe[1: T + 1]                               # safety of s_{t+1}
+        return {
+            "loss_total": total, "loss_dang": ld, "loss_safe": ls, "loss_dang_deriv": ldd,
+            "loss_safe_deriv": lsd, "loss_action": la,
+            "acc_dang_sum": sums[4], "acc_safe_sum": sums[5], "acc_dang_deriv_sum": sums[8],
+            "acc_safe_deriv_sum": sums[9], "n_dang": self.counts[0], "n_safe": self.counts[1],
+            "agent_steps": vf.sum() * N, "safe_agents": (safe_next * vf).sum(), "T": T,
+        }
+
+    def _buf(self, cache, rows, cols):
+        b = cache.get(rows)
+        if b is None:
+            b = torch.zeros(rows, cols, dtype=torch.float32, device=self.dev)
+            cache[rows] = b
+        return b

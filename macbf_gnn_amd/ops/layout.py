@@ -267,3 +267,170 @@ def emu_acc_frag(c: np.ndarray, s: int) -> np.ndarray:
 
 def emu_frag(packed_vals: np.ndarray, frag: int) -> np.ndarray:
     return packed_vals[frag * 512:(frag + 1) * 512].reshape(64, 8)
+
+
+# ------------------------------------------------------------------ row-major LDS images
+# One padded row-major bf16 copy per weight matrix; the kernels read W fragments with
+# ds_read_b64/b128 (wrm_*) and W^T fragments with ds_read_b64_tr_b16 (wrmT_*), so the
+# forward and backward chains share one LDS image (csrc/common.h).
+@dataclass
+class RMImage:
+    name: str
+    offset: int     # elements
+    rows: int
+    stride: int
+
+
+class RMPacker:
+    def __init__(self):
+        self.images: List[RMImage] = []
+        self.parts: List[np.ndarray] = []
+        self.size = 0
+
+    def add(self, name, vm, rows, cols, stride):
+        assert stride % 8 == 0 and stride >= cols
+        idx = np.full((rows, stride), ZERO, dtype=np.int64)
+        for r in range(rows):
+            for c in range(cols):
+                idx[r, c] = vm(r, c)
+        self.images.append(RMImage(name, self.size, rows, stride))
+        self.parts.append(idx.reshape(-1))
+        self.size += rows * stride
+        return self
+
+    def index(self):
+        return np.concatenate(self.parts)
+
+    def offsets(self):
+        return {im.name: im.offset for im in self.images}
+
+
+NODE_STRIDES = {"w1": 168, "w2": 72, "w3": 136, "w4": 72}
+
+
+def ctrl_node_rm(fp_offsets) -> RMPacker:
+    """Row-major node-MLP images for the controller backward kernel (csrc/ctrl.hip)."""
+    nW1, nb1 = fp_offsets["controller_dec_net.0.weight"], fp_offsets["controller_dec_net.0.bias"]
+    nW2 = fp_offsets["controller_dec_net.2.weight"]
+    nW3 = fp_offsets["controller_dec_net.4.weight"]
+    nW4 = fp_offsets["controller_dec_net.6.weight"]
+
+    def w1f(o, k):   # same virtual matrix as ctrl_packer's nw1f, 160 columns (144.. zero)
+        if k < 132:
+            return nW1 + o * 132 + k
+        if k == 132:
+            return nb1 + o
+        if 136 <= k < 140:
+            return nW1 + o * 132 + 128 + (k - 136)
+        return ZERO
+
+    p = RMPacker()
+    p.add("w1", w1f, 64, 160, NODE_STRIDES["w1"])
+    p.add("w2", _mat(nW2, 128, 64), 128, 64, NODE_STRIDES["w2"])
+    p.add("w3", _mat(nW3, 64, 128), 64, 128, NODE_STRIDES["w3"])
+    p.add("w4", _mat(nW4, 4, 64), 32, 64, NODE_STRIDES["w4"])
+    return p
+
+
+def emu_tr_pair(img, rb1, rb2, c0):
+    """ds_read_b64_tr_b16 pair as used by tr_pair(): rb1/rb2 are arrays over h (2,)."""
+    out = np.zeros((64, 8))
+    for l in range(64):
+        r, h = l & 31, l >> 5
+        for j in range(4):
+            out[l, j] = img[rb1[h] + j, c0 + r]
+            out[l, 4 + j] = img[rb2[h] + j, c0 + r]
+    return out
+
+
+def emu_wrm_nat(img, m0, kk):
+    out = np.zeros((64, 8))
+    for l in range(64):
+        r, h = l & 31, l >> 5
+        out[l] = img[m0 + r, 16 * kk + 8 * h: 16 * kk + 8 * h + 8]
+    return out
+
+
+def emu_wrm_acc(img, m0, kk):
+    out = np.zeros((64, 8))
+    for l in range(64):
+        r, h = l & 31, l >> 5
+        base = 16 * kk + 4 * h
+        out[l, :4] = img[m0 + r, base:base + 4]
+        out[l, 4:] = img[m0 + r, base + 8:base + 12]
+    return out
+
+
+def emu_wrmT_acc(img, m0, kk):
+    rb = [16 * kk + 4 * h for h in range(2)]
+    return emu_tr_pair(img, rb, [x + 8 for x in rb], m0)
+
+
+def emu_wrmT_nat(img, m0, kk):
+    rb = [16 * kk + 8 * h for h in range(2)]
+    return emu_tr_pair(img, rb, [x + 4 for x in rb], m0)
+
+
+# ------------------------------------------------------------------ gradient slab -> flat maps
+def _pairs_rowmajor(base_slab, ncols_slab, param_off, rows, cols):
+    src, dst = [], []
+    for r in range(rows):
+        for c in range(cols):
+            src.append(base_slab + r * ncols_slab + c)
+            dst.append(param_off + r * cols + c)
+    return src, dst
+
+
+def cbf_grad_map(fp_offsets):
+    """(src in the reduced CBF slab, dst in the flat grad) pairs; src may repeat dst (hi/lo)."""
+    W1, b1 = fp_offsets["cbf_net.0.weight"], fp_offsets["cbf_net.0.bias"]
+    W2, b2 = fp_offsets["cbf_net.2.weight"], fp_offsets["cbf_net.2.bias"]
+    W3, b3 = fp_offsets["cbf_net.4.weight"], fp_offsets["cbf_net.4.bias"]
+    W4, b4 = fp_offsets["cbf_net.6.weight"], fp_offsets["cbf_net.6.bias"]
+    S, D = [], []
+    for s_, d_ in (_pairs_rowmajor(0, 128, W3, 64, 128), _pairs_rowmajor(8256, 64, W2, 128, 64)):
+        S += s_; D += d_
+    S += [8192 + m for m in range(64)]; D += [b3 + m for m in range(64)]
+    S += [16448 + m for m in range(128)]; D += [b2 + m for m in range(128)]
+    for o in range(64):
+        for k in range(6):
+            S += [16576 + o * 32 + k, 16576 + o * 32 + 8 + k]; D += [W1 + o * 6 + k] * 2
+        S.append(16576 + o * 32 + 6); D.append(b1 + o)
+    S += [18624 + n for n in range(64)]; D += [W4 + n for n in range(64)]
+    S.append(18688); D.append(b4)
+    return np.asarray(S, np.int64), np.asarray(D, np.int64)
+
+
+def ctrl_node_grad_map(fp_offsets):
+    nW1, nb1 = fp_offsets["controller_dec_net.0.weight"], fp_offsets["controller_dec_net.0.bias"]
+    nW2, nb2 = fp_offsets["controller_dec_net.2.weight"], fp_offsets["controller_dec_net.2.bias"]
+    nW3, nb3 = fp_offsets["controller_dec_net.4.weight"], fp_offsets["controller_dec_net.4.bias"]
+    nW4, nb4 = fp_offsets["controller_dec_net.6.weight"], fp_offsets["controller_dec_net.6.bias"]
+    S, D = [], []
+    for o in range(64):
+        for k in range(132):
+            S.append(o * 160 + k); D.append(nW1 + o * 132 + k)
+        S.append(o * 160 + 132); D.append(nb1 + o)
+        for k in range(4):
+            S.append(o * 160 + 136 + k); D.append(nW1 + o * 132 + 128 + k)
+    for s_, d_ in (_pairs_rowmajor(10240, 64, nW2, 128, 64), _pairs_rowmajor(18560, 128, nW3, 64, 128),
+                   _pairs_rowmajor(26816, 64, nW4, 4, 64)):
+        S += s_; D += d_
+    S += [18432 + m for m in range(128)]; D += [nb2 + m for m in range(128)]
+    S += [26752 + m for m in range(64)]; D += [nb3 + m for m in range(64)]
+    S += [28864 + m for m in range(4)]; D += [nb4 + m for m in range(4)]
+    return np.asarray(S, np.int64), np.asarray(D, np.int64)
+
+
+def ctrl_edge_grad_map(fp_offsets):
+    eW1, eb1 = fp_offsets["controller_centr_net.0.weight"], fp_offsets["controller_centr_net.0.bias"]
+    eW2, eb2 = fp_offsets["controller_centr_net.2.weight"], fp_offsets["controller_centr_net.2.bias"]
+    S, D = _pairs_rowmajor(0, 64, eW2, 128, 64)
+    S += [8192 + m for m in range(128)]; D += [eb2 + m for m in range(128)]
+    for o in range(64):
+        for k in range(5):
+            S.append(8320 + o * 32 + k); D.append(eW1 + o * 5 + k)
+        for k in range(4):
+            S.append(8320 + o * 32 + 8 + k); D.append(eW1 + o * 5 + k)
+        S.append(8320 + o * 32 + 5); D.append(eb1 + o)
+    return np.asarray(S, np.int64), np.asarray(D, np.int64)

@@ -120,19 +120,27 @@ def scenario(S, G, *, seed, L, r=C.DIST_MIN_THRES, spread=C.GOAL_SPREAD, max_rou
     _ok(rc, "scenario")
 
 
-def ctrl_fwd(S, G, idx, wpack, f_edge, f_node, wvec, A, Sn, dist_sum, act_sum, noise=None):
-    """Fused controller step. S (B,N,4) view (row-contiguous), G (B,N,2) contiguous,
-    idx (B,N,K) view, A (B,N,2) view, Sn (B,N,4) view, dist_sum/act_sum (B,) views."""
+def _rows(t, last, name, lead):
+    """t is a float/bf16 view whose trailing dims are contiguous rows of width `last`."""
+    if t is None:
+        return
+    if tuple(t.shape[:len(lead)]) != tuple(lead) or t.shape[-1] != last or t.stride(-1) != 1 \
+            or t.stride(-2) != last:
+        raise NativeError(f"{name}: expected {lead}x{last} with contiguous rows, got {tuple(t.shape)} {t.stride()}")
+
+
+def ctrl_fwd(S, G, idx, wpack, f_edge, f_node, wvec, A, Sn, dist_sum, act_sum, noise=None, pooled=None, argmax=None):
+    """Fused controller step on per-step views: S/Sn (B,N,4), G (B,N,2), idx (B,N,K),
+    A (B,N,2), dist_sum/act_sum (B,), pooled (B,N,128) bf16, argmax (B,N,128) uint8."""
     B, N = S.shape[0], S.shape[1]
     K = idx.shape[2]
     if K < 1 or K > C.MAX_TOP_K:
         raise NativeError("K out of range")
-    for t, n, last in ((S, "S", 4), (Sn, "Sn", 4), (A, "A", 2)):
-        if t is not None and (t.dtype != torch.float32 or t.shape[:2] != (B, N) or t.shape[2] != last
-                              or t.stride(2) != 1 or t.stride(1) != last):
-            raise NativeError(f"{n} must be float32 (B,N,{last}) with contiguous rows")
+    _rows(S, 4, "S", (B, N))
+    _rows(Sn, 4, "Sn", (B, N))
+    _rows(A, 2, "A", (B, N))
     check(G, torch.float32, (B, N, 2), "G")
-    if idx.dtype != torch.int32 or idx.stride(2) != 1 or idx.stride(1) != K or idx.shape[:2] != (B, N):
+    if idx.dtype != torch.int32 or idx.stride(2) != 1 or idx.stride(1) != K or tuple(idx.shape[:2]) != (B, N):
         raise NativeError("idx must be int32 (B,N,K)")
     check(wpack, torch.bfloat16, None, "wpack")
     check(wvec, torch.float32, None, "wvec")
@@ -141,8 +149,15 @@ def ctrl_fwd(S, G, idx, wpack, f_edge, f_node, wvec, A, Sn, dist_sum, act_sum, n
     for t, n in ((dist_sum, "dist_sum"), (act_sum, "act_sum")):
         if t is not None and (t.dtype != torch.float32 or tuple(t.shape) != (B,)):
             raise NativeError(f"{n} must be float32 (B,)")
-    if noise is not None and (noise.dtype != torch.float32 or noise.shape[:2] != (B, N) or noise.stride(1) != 2):
-        raise NativeError("noise must be float32 (B,N,2)")
+    _rows(noise, 2, "noise", (B, N))
+    if pooled is not None:
+        _rows(pooled, 128, "pooled", (B, N))
+        if pooled.dtype != torch.bfloat16:
+            raise NativeError("pooled must be bf16")
+    if argmax is not None:
+        _rows(argmax, 128, "argmax", (B, N))
+        if argmax.dtype != torch.uint8:
+            raise NativeError("argmax must be uint8")
     rc = lib().ctrl_fwd(ptr(S), S.stride(0) // 4, ptr(G), ptr(idx), idx.stride(0), B, N, K,
                         ptr(wpack), int(f_edge), int(f_node), ptr(wvec),
                         ptr(A), A.stride(0) // 2 if A is not None else 0,
@@ -151,6 +166,8 @@ def ctrl_fwd(S, G, idx, wpack, f_edge, f_node, wvec, A, Sn, dist_sum, act_sum, n
                         ptr(act_sum), act_sum.stride(0) if act_sum is not None else 0,
                         ptr(noise), noise.stride(0) // 2 if noise is not None else 0,
                         float(C.TIME_STEP), float(C.OBS_RADIUS), float(C.SQRT3),
+                        ptr(pooled), pooled.stride(0) if pooled is not None else 0,
+                        ptr(argmax), argmax.stride(0) if argmax is not None else 0,
                         num_cu(S.device), stream_handle())
     _ok(rc, "ctrl_fwd")
 
@@ -158,36 +175,174 @@ def ctrl_fwd(S, G, idx, wpack, f_edge, f_node, wvec, A, Sn, dist_sum, act_sum, n
 LOSS_CONSTS = (C.LOSS_EPS_DANG, C.TIME_STEP * C.ALPHA_CBF, C.LOSS_WEIGHTS[0], C.LOSS_WEIGHTS[1],
                C.LOSS_WEIGHTS[2], C.LOSS_WEIGHTS[3], C.LOSS_SCALE)
 CBF_FWD_WAVES = 4
+CBF_PARTIAL = 18696
+CTRL_NODE_PARTIAL = 28896
+CTRL_EDGE_PARTIAL = 10368
 
 
 def cbf_fwd_grid(E: int, device) -> int:
     tiles = (E + 31) // 32
-    return max(1, min((tiles + CBF_FWD_WAVES - 1) // CBF_FWD_WAVES, num_cu(device) * 2))
+    return max(1, min((tiles + CBF_FWD_WAVES - 1) // CBF_FWD_WAVES, num_cu(device) * 4))
+
+
+def _time_major_S(S, T, B, N, need):
+    if S.dtype != torch.float32 or S.dim() != 4 or S.shape[0] < T + need or S.shape[1] != B \
+            or S.shape[2] != N or S.shape[3] != 4 or S.stride(3) != 1 or S.stride(2) != 4:
+        raise NativeError(f"S must be float32 (>=T+{need}, B, N, 4) with contiguous rows")
 
 
 def cbf_fwd(S, idx, wpack, f_fwd, wvec, *, dang=None, valid=None, two=True, h_out=None, hn_out=None,
             dh_out=None, counts=None, partial=None, num_blocks=None):
-    """S: (B, T', N, 4) contiguous with T' >= T + two; idx (B,T,N,K) int32 contiguous."""
-    B, T, N, K = idx.shape
+    """Time-major: S (>=T+two, B, N, 4); idx/dang/h (T, B, N, K); valid (T, B); dh (2, T, B, N, K)."""
+    T, B, N, K = idx.shape
     check(idx, torch.int32, None, "idx")
-    if S.dtype != torch.float32 or not S.is_contiguous() or S.shape[0] != B or S.shape[2] != N \
-            or S.shape[1] < T + (1 if two else 0):
-        raise NativeError("S must be contiguous float32 (B, >=T+1, N, 4)")
+    _time_major_S(S, T, B, N, 1 if two else 0)
     E = B * T * N * K
-    check(dang, torch.uint8, (B, T, N, K), "dang")
-    check(valid, torch.uint8, (B, T), "valid")
-    check(h_out, torch.float32, (B, T, N, K), "h_out")
-    check(hn_out, torch.float32, (B, T, N, K), "hn_out")
-    check(dh_out, torch.float32, (2, B, T, N, K), "dh_out")
+    check(dang, torch.uint8, (T, B, N, K), "dang")
+    check(valid, torch.uint8, (T, B), "valid")
+    check(h_out, torch.float32, (T, B, N, K), "h_out")
+    check(hn_out, torch.float32, (T, B, N, K), "hn_out")
+    check(dh_out, torch.float32, (2, T, B, N, K), "dh_out")
     if dh_out is not None:
         check(counts, torch.float32, None, "counts")
     check(wpack, torch.bfloat16, None, "wpack")
     check(wvec, torch.float32, None, "wvec")
     nb = num_blocks or cbf_fwd_grid(E, S.device)
     check(partial, torch.float32, (nb, 10), "partial")
-    rc = lib().cbf_fwd(ptr(S), S.stride(0) // 4, S.stride(1) // 4, ptr(idx), ptr(dang), ptr(valid),
+    rc = lib().cbf_fwd(ptr(S), S.stride(1) // 4, S.stride(0) // 4, ptr(idx), ptr(dang), ptr(valid),
                        B, T, N, K, int(two), ptr(wpack), int(f_fwd), ptr(wvec), ptr(h_out), ptr(hn_out),
                        ptr(dh_out), ptr(counts), ptr(partial), LOSS_CONSTS,
                        float(C.OBS_RADIUS), float(C.DIST_MIN_THRES), float(C.CBF_DIST_EPS), nb, stream_handle())
     _ok(rc, "cbf_fwd")
     return nb
+
+
+def cbf_bwd_grid(EV: int, device) -> int:
+    return max(1, min((EV + 127) // 128, num_cu(device)))
+
+
+def cbf_bwd(S, idx, dh, wpack, f_bwd, wvec, *, passes=2, dE=None, partial=None, num_blocks=None):
+    """dh (passes, T, B, N, K) -> dE (passes, T, B, N, K, 4), per-WG dW slabs (nb, CBF_PARTIAL)."""
+    T, B, N, K = idx.shape
+    check(idx, torch.int32, None, "idx")
+    _time_major_S(S, T, B, N, passes - 1)
+    check(dh, torch.float32, (passes, T, B, N, K), "dh")
+    check(dE, torch.float32, (passes, T, B, N, K, 4), "dE")
+    check(wpack, torch.bfloat16, None, "wpack")
+    check(wvec, torch.float32, None, "wvec")
+    if wpack.numel() < (f_bwd + 70) * 512:
+        raise NativeError("packed CBF weights too small")
+    E = B * T * N * K
+    nb = num_blocks or cbf_bwd_grid(E * passes, S.device)
+    check(partial, torch.float32, (nb, CBF_PARTIAL), "partial")
+    rc = lib().cbf_bwd(ptr(S), S.stride(1) // 4, S.stride(0) // 4, ptr(idx), B, T, N, K, int(passes), ptr(dh),
+                       ptr(wpack), int(f_bwd), ptr(wvec), ptr(dE), ptr(partial), float(C.OBS_RADIUS),
+                       float(C.DIST_MIN_THRES), float(C.CBF_DIST_EPS), nb, stream_handle())
+    _ok(rc, "cbf_bwd")
+    return nb
+
+
+def rev_csr(idx, rptr, redges):
+    """idx (G, N, K) int32 contiguous -> rptr (G, N+1), redges (G, N*K)."""
+    Gn, N, K = idx.shape
+    check(idx, torch.int32, (Gn, N, K), "idx")
+    check(rptr, torch.int32, (Gn, N + 1), "rptr")
+    check(redges, torch.int32, (Gn, N * K), "redges")
+    _ok(lib().rev_csr(ptr(idx), Gn, N, K, ptr(rptr), ptr(redges), stream_handle()), "rev_csr")
+
+
+def node_reduce(dE, rptr, redges, out, *, T, B, N, K, passes=2, accumulate=False):
+    check(dE, torch.float32, (passes, T, B, N, K, 4), "dE")
+    check(rptr, torch.int32, None, "rptr")
+    check(redges, torch.int32, None, "redges")
+    if rptr.shape[0] < T * B or redges.shape[0] < T * B:
+        raise NativeError("reverse CSR too small")
+    if out.dtype != torch.float32 or not out.is_contiguous() or out.shape[0] < T + 1 or \
+            tuple(out.shape[1:]) != (B, N, 4):
+        raise NativeError("out must be float32 (>=T+1, B, N, 4)")
+    _ok(lib().node_reduce(ptr(dE), ptr(rptr), ptr(redges), B, T, N, K, passes, int(accumulate), ptr(out),
+                          stream_handle()), "node_reduce")
+
+
+def node_combine(dS_t, ego, dEc, rptr_t, redges_t, Gn, Gout, *, K, dt=C.TIME_STEP):
+    """All (B,N,4) views; dEc (B,N,K,4); rptr_t (B, N+1) / redges_t (B, N*K) of graph t."""
+    B, N = dS_t.shape[:2]
+    _rows(dS_t, 4, "dS_t", (B, N))
+    _rows(Gout, 4, "Gout", (B, N))
+    _rows(Gn, 4, "Gn", (B, N))
+    check(ego, torch.float32, (B, N, 4), "ego")
+    check(dEc, torch.float32, (B, N, K, 4), "dEc")
+    if dEc is not None:
+        if rptr_t.dtype != torch.int32 or tuple(rptr_t.shape) != (B, N + 1) or rptr_t.stride(1) != 1:
+            raise NativeError("rptr_t must be int32 (B, N+1)")
+        if redges_t.dtype != torch.int32 or tuple(redges_t.shape) != (B, N * K) or redges_t.stride(1) != 1:
+            raise NativeError("redges_t must be int32 (B, N*K)")
+    _ok(lib().node_combine(ptr(dS_t), dS_t.stride(0) // 4, ptr(ego), ptr(dEc),
+                           ptr(rptr_t), rptr_t.stride(0) if dEc is not None else 0,
+                           ptr(redges_t), redges_t.stride(0) if dEc is not None else 0,
+                           ptr(Gn), Gn.stride(0) // 4 if Gn is not None else 0,
+                           ptr(Gout), Gout.stride(0) // 4, B, N, K, float(dt), stream_handle()), "node_combine")
+
+
+def ctrl_bwd_grids(total_agents: int, device):
+    ch = (total_agents + 127) // 128
+    cu = num_cu(device)
+    return max(1, min(ch, cu)), max(1, min(ch, 2 * cu))
+
+
+def ctrl_node_bwd(pooled, S, G, A, Gn, valid_t, wrm, offs, wvec, act_coef, dP, ego, partial, num_blocks):
+    B, N = S.shape[:2]
+    _rows(pooled, 128, "pooled", (B, N))
+    _rows(S, 4, "S", (B, N))
+    check(G, torch.float32, (B, N, 2), "G")
+    _rows(A, 2, "A", (B, N))
+    _rows(Gn, 4, "Gn", (B, N))
+    if valid_t is not None and (valid_t.dtype != torch.uint8 or tuple(valid_t.shape) != (B,)):
+        raise NativeError("valid_t must be uint8 (B,)")
+    check(wrm, torch.bfloat16, None, "wrm")
+    check(dP, torch.bfloat16, (B, N, 128), "dP")
+    check(ego, torch.float32, (B, N, 4), "ego")
+    check(partial, torch.float32, (num_blocks, CTRL_NODE_PARTIAL), "partial")
+    rc = lib().ctrl_node_bwd(ptr(pooled), pooled.stride(0), ptr(S), S.stride(0) // 4, ptr(G), ptr(A), A.stride(0) // 2,
+                             ptr(Gn), Gn.stride(0) // 4 if Gn is not None else 0,
+                             ptr(valid_t), valid_t.stride(0) if valid_t is not None else 0, B, N,
+                             ptr(wrm), offs["w1"], offs["w2"], offs["w3"], offs["w4"], ptr(wvec),
+                             float(act_coef), float(C.TIME_STEP), float(C.SQRT3), ptr(dP), dP.stride(0),
+                             ptr(ego), ptr(partial), int(num_blocks), stream_handle())
+    _ok(rc, "ctrl_node_bwd")
+
+
+def ctrl_edge_bwd(S, idx, argmax, dP, wpack, f_ew1f, f_ew2tn, dEc, partial, num_blocks):
+    B, N = S.shape[:2]
+    K = idx.shape[2]
+    _rows(S, 4, "S", (B, N))
+    if idx.dtype != torch.int32 or idx.stride(2) != 1 or idx.stride(1) != K or tuple(idx.shape[:2]) != (B, N):
+        raise NativeError("idx must be int32 (B,N,K)")
+    _rows(argmax, 128, "argmax", (B, N))
+    check(dP, torch.bfloat16, (B, N, 128), "dP")
+    check(dEc, torch.float32, (B, N, K, 4), "dEc")
+    check(partial, torch.float32, (num_blocks, CTRL_EDGE_PARTIAL), "partial")
+    rc = lib().ctrl_edge_bwd(ptr(S), S.stride(0) // 4, ptr(idx), idx.stride(0), ptr(argmax), argmax.stride(0),
+                             ptr(dP), dP.stride(0), B, N, K, ptr(wpack), int(f_ew1f), int(f_ew2tn), ptr(dEc),
+                             dEc.stride(0) // 4, ptr(partial), int(num_blocks), stream_handle())
+    _ok(rc, "ctrl_edge_bwd")
+
+
+def reduce_rows(partial, out, accumulate=False):
+    rows, cols = partial.shape
+    check(partial, torch.float32, None, "partial")
+    check(out, torch.float32, (cols,), "out")
+    if cols % 4:
+        raise NativeError("cols must be a multiple of 4")
+    _ok(lib().reduce_rows(ptr(partial), rows, cols, ptr(out), int(accumulate), stream_handle()), "reduce_rows")
+
+
+def adam(param, grad, m, v, lo, hi, lr, b1, b2, eps, wd, step):
+    for t, n in ((param, "param"), (grad, "grad"), (m, "m"), (v, "v")):
+        check(t, torch.float32, (param.numel(),), n)
+    if not (0 <= lo <= hi <= param.numel()):
+        raise NativeError("bad Adam range")
+    bc1 = 1.0 - b1 ** step
+    bc2 = 1.0 - b2 ** step
+    _ok(lib().adam(ptr(param), ptr(grad), ptr(m), ptr(v), int(lo), int(hi), float(b1), float(b2), float(eps),
+                   float(wd), float(lr / bc1), float(bc2 ** 0.5), stream_handle()), "adam")

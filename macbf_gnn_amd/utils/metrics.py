@@ -36,14 +36,18 @@ class MetricsLogger:
         self.t0 = time.perf_counter()
 
     def update(self, stats):
+        """Accumulate; device tensors stay on device (no host sync until emit)."""
         for k in KEYS:
             if k == "iters":
                 self.acc[k] += 1
             elif k in stats:
-                self.acc[k] += float(stats[k])
+                v = stats[k]
+                if isinstance(v, torch.Tensor):
+                    v = v.detach().to(torch.float64)
+                self.acc[k] = self.acc[k] + v
 
     def summary(self, step):
-        vec = torch.tensor([self.acc[k] for k in KEYS], dtype=torch.float64)
+        vec = torch.tensor([float(self.acc[k]) for k in KEYS], dtype=torch.float64)
         if self.dp.enabled:
             dev = self.dp.device if (self.dp.device is not None and self.dp.device.type == "cuda") else "cpu"
             vec = vec.to(dev)

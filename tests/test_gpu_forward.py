@@ -100,15 +100,16 @@ def test_ctrl_fwd_matches_oracle(B, N):
 def test_cbf_fwd_h_losses_grads(B, T, N):
     ctrl, cbf, fp, pw = _nets(1)
     K = min(N, C.TOP_K)
-    S = torch.stack([_states(B, N, seed=10 + t, vscale=1.0)[0] for t in range(T + 1)], 1).contiguous()
+    # time-major (T+1, B, N, 4)
+    S = torch.stack([_states(B, N, seed=10 + t, vscale=1.0)[0] for t in range(T + 1)], 0).contiguous()
     S[..., :2] *= 0.5          # denser -> more dangerous pairs
-    idx = torch.stack([O.knn_idx(S[:, t], K) for t in range(T)], 1).to(torch.int32).contiguous()
-    dang = torch.stack([O.ttc_mask_knn(S[:, t], idx[:, t].long()) for t in range(T)], 1).to(torch.uint8).contiguous()
-    valid = torch.ones(B, T, dtype=torch.uint8, device=DEV)
-    valid[0, -1] = 0
-    h = torch.empty(B, T, N, K, device=DEV)
+    idx = torch.stack([O.knn_idx(S[t], K) for t in range(T)], 0).to(torch.int32).contiguous()
+    dang = torch.stack([O.ttc_mask_knn(S[t], idx[t].long()) for t in range(T)], 0).to(torch.uint8).contiguous()
+    valid = torch.ones(T, B, dtype=torch.uint8, device=DEV)
+    valid[-1, 0] = 0
+    h = torch.empty(T, B, N, K, device=DEV)
     hn = torch.empty_like(h)
-    dh = torch.empty(2, B, T, N, K, device=DEV)
+    dh = torch.empty(2, T, B, N, K, device=DEV)
     vb = valid.bool()[..., None, None]
     nd = (dang.bool() & vb).sum().float()
     ns = (~dang.bool() & vb).sum().float()
@@ -119,8 +120,8 @@ def test_cbf_fwd_h_losses_grads(B, T, N):
                    h_out=h, hn_out=hn, dh_out=dh, counts=counts, partial=partial, num_blocks=nb)
     torch.cuda.synchronize()
     with torch.no_grad():
-        href = O.cbf_forward(cbf.params_dict(), S[:, :T], idx.long())
-        hnref = O.cbf_forward(cbf.params_dict(), S[:, 1:], idx.long())
+        href = O.cbf_forward(cbf.params_dict(), S[:T], idx.long())
+        hnref = O.cbf_forward(cbf.params_dict(), S[1:], idx.long())
     scale = href.abs().max().item() + 1e-6
     assert (h - href).abs().max().item() <= 2e-2 * scale + 2e-3
     assert (hn - hnref).abs().max().item() <= 2e-2 * scale + 2e-3
@@ -138,8 +139,8 @@ def test_cbf_fwd_h_losses_grads(B, T, N):
     s2["n_dang"], s2["n_safe"] = nd, ns
     out = O.finalize_losses(s2, torch.zeros((), device=DEV), 1.0)
     gh, ghn = torch.autograd.grad(out["total"], [hh, hhn])
-    m0 = O.cbf_features(S[:, :T], idx.long())[1]
-    m1 = O.cbf_features(S[:, 1:], idx.long())[1]
+    m0 = O.cbf_features(S[:T], idx.long())[1]
+    m1 = O.cbf_features(S[1:], idx.long())[1]
     torch.testing.assert_close(dh[0], gh * m0, rtol=1e-4, atol=1e-6)
     torch.testing.assert_close(dh[1], ghn * m1, rtol=1e-4, atol=1e-6)
 

@@ -153,3 +153,81 @@ def test_emulated_node_w1_natural():
     lin = ctrl.controller_dec_net[0]
     ref = lin.weight.detach().numpy() @ P + lin.bias.detach().numpy()[:, None]
     np.testing.assert_allclose(np.concatenate(out, 0), ref, rtol=1e-5, atol=1e-6)
+
+
+def _rm_images(fp, offs, src):
+    pk = L.ctrl_node_rm(offs)
+    vals = src[L.resolve(pk.index(), fp.numel)]
+    imgs = {}
+    for im in pk.images:
+        imgs[im.name] = vals[im.offset: im.offset + im.rows * im.stride].reshape(im.rows, im.stride)
+    return imgs
+
+
+def test_emulated_rowmajor_node_forward_backward():
+    ctrl, cbf, fp, offs, src = _setup()
+    im = _rm_images(fp, offs, src)
+    rng = np.random.default_rng(5)
+    Pin = np.zeros((160, 32))
+    Pin[:132] = rng.normal(size=(132, 32))
+    Pin[132] = 1.0
+    # forward Y1 = W1f P (natural B from data)
+    Y1 = []
+    for mt in range(2):
+        c = np.zeros((64, 16))
+        for kk in range(9):
+            b = np.stack([Pin[16 * kk + 8 * (l >> 5): 16 * kk + 8 * (l >> 5) + 8, l & 31] for l in range(64)])
+            c = L.emu_mfma(L.emu_wrm_nat(im["w1"], 32 * mt, kk), b, c)
+        Y1.append(np.maximum(c, 0))
+    net = ctrl.controller_dec_net
+    W = [net[i].weight.detach().numpy().astype(np.float64) for i in (0, 2, 4, 6)]
+    bb = [net[i].bias.detach().numpy().astype(np.float64) for i in (0, 2, 4, 6)]
+    ref1 = np.maximum(W[0] @ Pin[:132] + bb[0][:, None], 0)
+    np.testing.assert_allclose(np.concatenate([acc_to_mat(y) for y in Y1]), ref1, rtol=1e-5, atol=1e-6)
+    # Y2 = W2 Y1 (accumulator B)
+    Y2 = []
+    for mt in range(4):
+        c = bias_init(bb[1], mt)
+        for kk in range(4):
+            c = L.emu_mfma(L.emu_wrm_acc(im["w2"], 32 * mt, kk), L.emu_acc_frag(Y1[kk >> 1], kk & 1), c)
+        Y2.append(c)
+    ref2 = W[1] @ ref1 + bb[1][:, None]
+    np.testing.assert_allclose(np.concatenate([acc_to_mat(y) for y in Y2]), ref2, rtol=1e-5, atol=1e-6)
+    # backward: dY3 = W4^T dY4 (K=32 from a 32-row accumulator), dY1 = W2^T dY2, dP = W1f^T dY1
+    dY4 = np.zeros((64, 16))
+    for l in range(32):
+        dY4[l, :4] = rng.normal(size=4)       # rows 0..3 live in lanes h=0, regs 0..3
+    dY3 = []
+    for mt in range(2):
+        c = np.zeros((64, 16))
+        for kk in range(2):
+            c = L.emu_mfma(L.emu_wrmT_acc(im["w4"], 32 * mt, kk), L.emu_acc_frag(dY4, kk & 1), c)
+        dY3.append(c)
+    D4 = acc_to_mat(dY4)[:4]
+    np.testing.assert_allclose(np.concatenate([acc_to_mat(y) for y in dY3]), W[3].T @ D4, rtol=1e-6, atol=1e-7)
+    dY2 = [rng.normal(size=(64, 16)) for _ in range(4)]
+    dY1 = []
+    for mt in range(2):
+        c = np.zeros((64, 16))
+        for kk in range(8):
+            c = L.emu_mfma(L.emu_wrmT_acc(im["w2"], 32 * mt, kk), L.emu_acc_frag(dY2[kk >> 1], kk & 1), c)
+        dY1.append(c)
+    D2 = np.concatenate([acc_to_mat(d) for d in dY2])
+    np.testing.assert_allclose(np.concatenate([acc_to_mat(y) for y in dY1]), W[1].T @ D2, rtol=1e-6, atol=1e-6)
+    dP = []
+    for mt in range(5):
+        c = np.zeros((64, 16))
+        for kk in range(4):
+            c = L.emu_mfma(L.emu_wrmT_acc(im["w1"], 32 * mt, kk), L.emu_acc_frag(dY1[kk >> 1], kk & 1), c)
+        dP.append(c)
+    D1 = np.concatenate([acc_to_mat(d) for d in dY1])
+    got = np.concatenate([acc_to_mat(d) for d in dP])
+    np.testing.assert_allclose(got[:132], W[0].T @ D1, rtol=1e-6, atol=1e-6)
+    # natural transposed reader: A = W2^T with natural-k B
+    Bn = rng.normal(size=(128, 32))
+    for mt in range(2):
+        c = np.zeros((64, 16))
+        for kk in range(8):
+            b = np.stack([Bn[16 * kk + 8 * (l >> 5): 16 * kk + 8 * (l >> 5) + 8, l & 31] for l in range(64)])
+            c = L.emu_mfma(L.emu_wrmT_nat(im["w2"], 32 * mt, kk), b, c)
+        np.testing.assert_allclose(acc_to_mat(c), (W[1].T @ Bn)[32 * mt:32 * mt + 32], rtol=1e-6, atol=1e-6)
