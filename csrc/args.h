@@ -7,8 +7,16 @@ typedef __bf16 bf16;
 
 namespace mb {
 
+struct CellSortArgs {
+  const float4* S;  long s_env;      // agent (b,i) state at S[b*s_env + i]
+  int B, N;
+  float L;                           // scenario side length (Morton grid spans [0, L]^2)
+  int* perm;                         // (B, N) position on the curve -> agent id
+};
+
 struct ScanArgs {
   const float4* S;  long s_env;      // agent (b,i) state at S[b*s_env + i]
+  const int* perm;                   // (B, N) Morton order from cell_sort
   int B, N, K;
   int* idx;         long i_env;      // (b,i,k) at idx[b*i_env + i*K + k]
   uint8_t* dang;                     // same indexing as idx (may be null)
@@ -76,6 +84,7 @@ struct CbfBwdArgs {
   int passes;                              // evaluations = passes*E; pass p reads states at t+p
   const float* dh;                         // (passes, E) upstream dL/dh (radius mask folded in)
   const bf16* wpack; int f_bwd;            // fragment offset of w1f (w2,w3,w3t,w2t,w1ft follow)
+  const bf16* wrm;                         // row-major W2 [128][72] | W3 [64][136] images
   const float* wvec;
   float4* dE;                              // (passes, E) dL/d(s_i - s_j) per evaluation, or null
   float* partial;                          // (gridDim.x, CBF_PARTIAL) per-workgroup dW slabs
@@ -146,6 +155,7 @@ struct AdamArgs {
 
 extern "C" {
 int mb_scan(const mb::ScanArgs* a, hipStream_t st);
+int mb_cell_sort(const mb::CellSortArgs* a, hipStream_t st);
 int mb_scenario(const mb::ScenArgs* a, hipStream_t st);
 int mb_ctrl_fwd(const mb::CtrlArgs* a, int num_cu, hipStream_t st);
 int mb_cbf_fwd(const mb::CbfFwdArgs* a, int num_blocks, hipStream_t st);

@@ -16,11 +16,17 @@ template <typename T>
 static T* P(u64 p) { return reinterpret_cast<T*>(static_cast<uintptr_t>(p)); }
 static hipStream_t ST(u64 s) { return reinterpret_cast<hipStream_t>(static_cast<uintptr_t>(s)); }
 
-static int scan(u64 S, long s_env, int B, int N, int K, u64 idx, long i_env, u64 dang, u64 cnt, long c_env,
+static int cell_sort(u64 S, long s_env, int B, int N, float L, u64 perm, u64 stream) {
+  mb::CellSortArgs a{};
+  a.S = P<const float4>(S); a.s_env = s_env; a.B = B; a.N = N; a.L = L; a.perm = P<int>(perm);
+  return mb_cell_sort(&a, ST(stream));
+}
+
+static int scan(u64 S, long s_env, u64 perm, int B, int N, int K, u64 idx, long i_env, u64 dang, u64 cnt, long c_env,
                 u64 safe, long sf_env, float r2_train, float ttc_train, float r2_check, float ttc_check,
                 int do_knn, int do_safety, u64 stream) {
   mb::ScanArgs a{};
-  a.S = P<const float4>(S); a.s_env = s_env; a.B = B; a.N = N; a.K = K;
+  a.S = P<const float4>(S); a.s_env = s_env; a.perm = P<const int>(perm); a.B = B; a.N = N; a.K = K;
   a.idx = P<int>(idx); a.i_env = i_env; a.dang = P<uint8_t>(dang);
   a.cnt = P<float>(cnt); a.c_env = c_env; a.safe = P<float>(safe); a.sf_env = sf_env;
   a.r2_train = r2_train; a.ttc_train = ttc_train; a.r2_check = r2_check; a.ttc_check = ttc_check;
@@ -69,12 +75,12 @@ static int cbf_fwd(u64 S, long s_env, long s_step, u64 idx, u64 dang, u64 valid,
 }
 
 static int cbf_bwd(u64 S, long s_env, long s_step, u64 idx, int B, int T, int N, int K, int passes, u64 dh,
-                   u64 wpack, int f_bwd, u64 wvec, u64 dE, u64 partial, float obs_r, float dist_thr,
+                   u64 wpack, int f_bwd, u64 wrm, u64 wvec, u64 dE, u64 partial, float obs_r, float dist_thr,
                    float dist_eps, int num_blocks, u64 stream) {
   mb::CbfBwdArgs a{};
   a.S = P<const float4>(S); a.s_env = s_env; a.s_step = s_step; a.idx = P<const int>(idx);
   a.B = B; a.T = T; a.N = N; a.K = K; a.passes = passes; a.dh = P<const float>(dh);
-  a.wpack = P<const bf16>(wpack); a.f_bwd = f_bwd; a.wvec = P<const float>(wvec);
+  a.wpack = P<const bf16>(wpack); a.f_bwd = f_bwd; a.wrm = P<const bf16>(wrm); a.wvec = P<const float>(wvec);
   a.dE = P<float4>(dE); a.partial = P<float>(partial);
   a.obs_r = obs_r; a.dist_thr = dist_thr; a.dist_eps = dist_eps;
   return mb_cbf_bwd(&a, num_blocks, ST(stream));
@@ -165,6 +171,7 @@ static std::string err_str(int e) { return hipGetErrorString((hipError_t)e); }
 PYBIND11_MODULE(_C, m) {
   m.doc() = "macbf_gnn_amd native gfx950 kernels";
   m.def("scan", &scan);
+  m.def("cell_sort", &cell_sort);
   m.def("scenario", &scenario);
   m.def("ctrl_fwd", &ctrl_fwd);
   m.def("cbf_fwd", &cbf_fwd);

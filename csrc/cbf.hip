@@ -95,22 +95,24 @@ struct EdgeCtx {
   bool mask;
 };
 
+// 32-bit index math throughout (host asserts passes*E < 2^31): 64-bit divisions/multiplies
+// here cost dozens of VGPRs and instructions per edge.
 DEV void cbf_edge(const float4* S, long s_env, long s_step, const int* idx, int B, int N, int K,
-                  long e, long E, int tstep_off, float obs_r, float dist_thr, float dist_eps, EdgeCtx& c) {
-  c.ok = e < E;
+                  long e_, long E_, int tstep_off, float obs_r, float dist_thr, float dist_eps, EdgeCtx& c) {
+  const unsigned e = (unsigned)e_;
+  c.ok = e_ < E_;
   c.rel = make_float4(0.f, 0.f, 0.f, 0.f);
   c.eye = 0.f; c.d = 0.f; c.dfeat = 0.f; c.mask = false;
   c.b = c.t = c.i = c.j = 0;
   if (!c.ok) return;
   // time-major edge order: e = ((t*B + b)*N + i)*K + k
-  const long NK = (long)N * K;
-  const long tb = e / NK;
-  const long rem = e - tb * NK;
-  c.i = (int)(rem / K);
-  c.t = (int)(tb / B);
-  c.b = (int)(tb - (long)c.t * B);
+  const unsigned ik = e / (unsigned)K;
+  const unsigned tb = ik / (unsigned)N;
+  c.i = (int)(ik - tb * (unsigned)N);
+  c.t = (int)(tb / (unsigned)B);
+  c.b = (int)(tb - (unsigned)c.t * (unsigned)B);
   c.j = idx[e];
-  const float4* Sb = S + (long)c.b * s_env + (long)(c.t + tstep_off) * s_step;
+  const float4* Sb = S + ((unsigned)c.b * (unsigned)s_env + (unsigned)(c.t + tstep_off) * (unsigned)s_step);
   const float4 si = Sb[c.i];
   const float4 sj = Sb[c.j];
   c.rel = make_float4(si.x - sj.x, si.y - sj.y, si.z - sj.z, si.w - sj.w);
@@ -239,21 +241,41 @@ namespace mb {
 constexpr int CBF_BWD_WAVES = 4;
 constexpr int CBF_CH = CBF_BWD_WAVES * 32;    // evaluations per chunk
 constexpr int SA128 = 136, SA64 = 72, SA32 = 40;
-constexpr int CBF_BWD_FRAGS = 70;
+constexpr int RM_W2 = 128 * 72, RM_W3 = 64 * 136;   // row-major image sizes (elements)
 // per-WG partial slab layout (floats)
 constexpr int P_W3 = 0, P_B3 = 8192, P_W2 = 8256, P_B2 = 16448, P_W1 = 16576, P_W4 = 18624, P_B4 = 18688;
 constexpr int CBF_PARTIAL = 18696;
 // stage A/B: (128 + 64)-wide images; stage C+D: dH1|F|dh|relu(H3) = 64+32+32+64 wide
 constexpr size_t CBF_STAGE_BYTES = (size_t)(SA64 + SA32 + SA32 + SA64) * CBF_CH * 2;
+constexpr size_t CBF_BWD_W_BYTES = (size_t)(RM_W2 + RM_W3) * 2 + 6 * FRAG_BYTES;
 
-size_t cbf_bwd_lds() { return (size_t)CBF_BWD_FRAGS * FRAG_BYTES + CBF_VEC * 4 + CBF_STAGE_BYTES; }
+size_t cbf_bwd_lds() { return CBF_BWD_W_BYTES + CBF_VEC * 4 + CBF_STAGE_BYTES; }
+
+struct CbfIn {
+  EdgeCtx c;
+  float dh;
+  bool in;
+};
+
+DEV void cbf_load(const CbfBwdArgs& a, long chunk, int wave, int r, long E, long EV, CbfIn& x) {
+  const unsigned ev = (unsigned)chunk * CBF_CH + wave * 32 + r;
+  x.in = ev < (unsigned)EV;
+  const int pass = (x.in && ev >= (unsigned)E) ? 1 : 0;
+  const unsigned e = ev - (unsigned)pass * (unsigned)E;
+  cbf_edge(a.S, a.s_env, a.s_step, a.idx, a.B, a.N, a.K, e, x.in ? E : 0, pass, a.obs_r, a.dist_thr, a.dist_eps, x.c);
+  x.dh = x.in ? a.dh[ev] : 0.f;
+}
 
 __global__ __launch_bounds__(CBF_BWD_WAVES * 64, 1) void cbf_bwd_kernel(CbfBwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  bf16* wl = reinterpret_cast<bf16*>(smem);
-  float* vl = reinterpret_cast<float*>(smem + CBF_BWD_FRAGS * FRAG_BYTES);
-  bf16* stg = reinterpret_cast<bf16*>(smem + CBF_BWD_FRAGS * FRAG_BYTES + CBF_VEC * 4);
-  block_copy16(wl, a.wpack + (size_t)a.f_bwd * 512, CBF_BWD_FRAGS * FRAG_BYTES);
+  bf16* W2 = reinterpret_cast<bf16*>(smem);
+  bf16* W3 = W2 + RM_W2;
+  bf16* wf = W3 + RM_W3;                       // w1f (2 frags) | w1ft (4 frags)
+  float* vl = reinterpret_cast<float*>(smem + CBF_BWD_W_BYTES);
+  bf16* stg = reinterpret_cast<bf16*>(smem + CBF_BWD_W_BYTES + CBF_VEC * 4);
+  block_copy16(W2, a.wrm, (RM_W2 + RM_W3) * 2);
+  block_copy16(wf, a.wpack + (size_t)a.f_bwd * 512, 2 * FRAG_BYTES);
+  block_copy16(wf + 2 * 512, a.wpack + (size_t)(a.f_bwd + 66) * 512, 4 * FRAG_BYTES);
   block_copy16(vl, a.wvec, CBF_VEC * 4);
   __syncthreads();
   const int wave = threadIdx.x / WAVE, lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
@@ -261,28 +283,27 @@ __global__ __launch_bounds__(CBF_BWD_WAVES * 64, 1) void cbf_bwd_kernel(CbfBwdAr
   const long EV = E * a.passes;
   const long nchunks = (EV + CBF_CH - 1) / CBF_CH;
   const int erow = wave * 32 + r;
+  // owned weight-gradient tiles: tiles wave and wave+4 of dW3 (64x128, (t/4, t%4)) and of
+  // dW2 (128x64, (t/2, t%2)); one tile of dW1f (waves 0,1) or dW4pad (waves 2,3)
+  f32x16 accA[2], accB[2], accC = zero16();
+  accA[0] = accA[1] = accB[0] = accB[1] = zero16();
+  float bA[2] = {0.f, 0.f}, bB[2] = {0.f, 0.f}, db4 = 0.f;
 
-  f32x16 accA[2], accB[2], accC;
-  accA[0] = accA[1] = accB[0] = accB[1] = accC = zero16();
-  float bA[2] = {0.f, 0.f}, bB[2] = {0.f, 0.f};
-  float bD = 0.f;   // db4 (row-sum of the dh image, waves 2/3 tile 0)
-  // owned tiles
-  const int tA0 = wave, tA1 = wave + 4;       // dW3: (mt = t/4, nt = t%4)
-  const int tB0 = wave, tB1 = wave + 4;       // dW2: (mt = t/2, nt = t%2)
-
+  CbfIn nx;
+  if ((long)blockIdx.x < nchunks) cbf_load(a, blockIdx.x, wave, r, E, EV, nx);
   for (long chunk = blockIdx.x; chunk < nchunks; chunk += gridDim.x) {
-    const long ev = chunk * CBF_CH + wave * 32 + r;
-    const bool in = ev < EV;
-    const int pass = (in && ev >= E) ? 1 : 0;
-    const long e = ev - (long)pass * E;
-    EdgeCtx c;
-    cbf_edge(a.S, a.s_env, a.s_step, a.idx, a.B, a.N, a.K, e, in ? E : 0, pass, a.obs_r, a.dist_thr, a.dist_eps, c);
-    const float dhv = in ? a.dh[ev] : 0.f;
+    const CbfIn cur = nx;
+    if (chunk + gridDim.x < nchunks) cbf_load(a, chunk + gridDim.x, wave, r, E, EV, nx);   // prefetch
+    const EdgeCtx& c = cur.c;
+    const float dhv = cur.dh;
+    if (h == 0) db4 += dhv;
     const bf16x8 F = cbf_edge_frag(c.rel, c.eye, c.dfeat, c.ok, h);
-    const bf16* wt = wl + opaque_zero();
-    const float* b2 = vl;
-    const float* b3 = vl + 128;
-    const float* w4 = vl + 192;
+    const bf16* wt = wf + opaque_zero();
+    // loop-invariant LDS vectors behind an opaque offset: otherwise the compiler hoists
+    // ~128 bias/head values into registers for the whole kernel
+    const float* b2 = vl + opaque_zero();
+    const float* b3 = vl + 128 + opaque_zero();
+    const float* w4 = vl + 192 + opaque_zero();
     // ---- forward recompute
     bf16x16 H1b[2], H2b[4];
     f32x16 H3p[2];
@@ -297,7 +318,7 @@ __global__ __launch_bounds__(CBF_BWD_WAVES * 64, 1) void cbf_bwd_kernel(CbfBwdAr
       f32x16 t2 = bias_rows(b2, 32 * mt, h);
       static_for<4>([&](auto kk_) {
         constexpr int kk = decltype(kk_)::value;
-        t2 = mfma(frag_ld(wt, 2 + mt * 4 + kk, lane), bacc_frag<kk & 1>(H1b[kk >> 1]), t2);
+        t2 = mfma(wrm_acc(W2 + opaque_zero(), SA64, 32 * mt, kk, lane), bacc_frag<kk & 1>(H1b[kk >> 1]), t2);
       });
       relu_(t2);
       H2b[mt] = to_bf16x16(t2);
@@ -307,11 +328,11 @@ __global__ __launch_bounds__(CBF_BWD_WAVES * 64, 1) void cbf_bwd_kernel(CbfBwdAr
       f32x16 t3 = bias_rows(b3, 32 * mt, h);
       static_for<8>([&](auto kk_) {
         constexpr int kk = decltype(kk_)::value;
-        t3 = mfma(frag_ld(wt, 18 + mt * 8 + kk, lane), bacc_frag<kk & 1>(H2b[kk >> 1]), t3);
+        t3 = mfma(wrm_acc(W3 + opaque_zero(), SA128, 32 * mt, kk, lane), bacc_frag<kk & 1>(H2b[kk >> 1]), t3);
       });
       H3p[mt] = t3;
     }
-    // ---- head backward: dH3pre = w4 * dh * relu'(H3pre); dw4 += dh * relu(H3pre)
+    // ---- head backward
     bf16x16 d3b[2], H3b[2];
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt) {
@@ -325,6 +346,22 @@ __global__ __launch_bounds__(CBF_BWD_WAVES * 64, 1) void cbf_bwd_kernel(CbfBwdAr
       d3b[mt] = to_bf16x16(d3);
       H3b[mt] = to_bf16x16(H3p[mt]);
     }
+    // ---- stage A: dW3 (64x128) += dH3pre . H2^T ; db3   (one tile per wave)
+    {
+      bf16* imA = stg;
+      bf16* imB = stg + CBF_CH * SA64;
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt) store_tile(imA, SA64, erow, 32 * mt, d3b[mt], h);
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) store_tile(imB, SA128, erow, 32 * mt, H2b[mt], h);
+      __syncthreads();
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int t = wave + 4 * u;
+        bA[u] += stage_mma(imA, SA64, imB, SA128, t / 4, t % 4, CBF_CH / 16, lane, accA[u], t % 4 == 0);
+      }
+      __syncthreads();
+    }
     // ---- dH2pre = (W3^T dH3pre) . relu'(H2)
     bf16x16 d2b[4];
 #pragma unroll
@@ -332,11 +369,27 @@ __global__ __launch_bounds__(CBF_BWD_WAVES * 64, 1) void cbf_bwd_kernel(CbfBwdAr
       f32x16 t = zero16();
       static_for<4>([&](auto kk_) {
         constexpr int kk = decltype(kk_)::value;
-        t = mfma(frag_ld(wt, 34 + mt * 4 + kk, lane), bacc_frag<kk & 1>(d3b[kk >> 1]), t);
+        t = mfma(wrmT_acc(W3 + opaque_zero(), SA128, 32 * mt, kk, lane), bacc_frag<kk & 1>(d3b[kk >> 1]), t);
       });
 #pragma unroll
       for (int q = 0; q < 16; ++q) t[q] = ((float)H2b[mt][q] > 0.f) ? t[q] : 0.f;
       d2b[mt] = to_bf16x16(t);
+    }
+    // ---- stage B: dW2 (128x64) += dH2pre . H1^T ; db2
+    {
+      bf16* imA = stg;
+      bf16* imB = stg + CBF_CH * SA128;
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) store_tile(imA, SA128, erow, 32 * mt, d2b[mt], h);
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt) store_tile(imB, SA64, erow, 32 * mt, H1b[mt], h);
+      __syncthreads();
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int t = wave + 4 * u;
+        bB[u] += stage_mma(imA, SA128, imB, SA64, t / 2, t % 2, CBF_CH / 16, lane, accB[u], t % 2 == 0);
+      }
+      __syncthreads();
     }
     // ---- dH1pre = (W2^T dH2pre) . relu'(H1)
     bf16x16 d1b[2];
@@ -345,63 +398,41 @@ __global__ __launch_bounds__(CBF_BWD_WAVES * 64, 1) void cbf_bwd_kernel(CbfBwdAr
       f32x16 t = zero16();
       static_for<8>([&](auto kk_) {
         constexpr int kk = decltype(kk_)::value;
-        t = mfma(frag_ld(wt, 50 + mt * 8 + kk, lane), bacc_frag<kk & 1>(d2b[kk >> 1]), t);
+        t = mfma(wrmT_acc(W2 + opaque_zero(), SA64, 32 * mt, kk, lane), bacc_frag<kk & 1>(d2b[kk >> 1]), t);
       });
 #pragma unroll
       for (int q = 0; q < 16; ++q) t[q] = ((float)H1b[mt][q] > 0.f) ? t[q] : 0.f;
       d1b[mt] = to_bf16x16(t);
     }
-    // ---- dF = W1^T dH1pre (rows: dx dy dvx dvy eye dist)
+    // ---- dF = W1^T dH1pre (rows: dx dy dvx dvy eye dist) -> dL/d(s_i - s_j)
     {
       f32x16 t = zero16();
       static_for<4>([&](auto kk_) {
         constexpr int kk = decltype(kk_)::value;
-        t = mfma(frag_ld(wt, 66 + kk, lane), bacc_frag<kk & 1>(d1b[kk >> 1]), t);
+        t = mfma(frag_ld(wt, 2 + kk, lane), bacc_frag<kk & 1>(d1b[kk >> 1]), t);
       });
       const float ddist = shfl_xor32(t[1]);   // row 5 lives in lane r+32, reg 1
-      if (a.dE && in && h == 0) {
+      if (a.dE && cur.in && h == 0) {
+        const unsigned ev = (unsigned)chunk * CBF_CH + wave * 32 + r;
         float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
         if (c.ok && c.j != c.i) {
           const float inv = 1.f / c.d;
-          g = make_float4(t[0] + ddist * c.rel.x * inv, t[1] + ddist * c.rel.y * inv,
-                          t[2], t[3]);
+          g = make_float4(t[0] + ddist * c.rel.x * inv, t[1] + ddist * c.rel.y * inv, t[2], t[3]);
         }
         a.dE[ev] = g;
       }
     }
-    // ---- stage A: dW3 (64x128) += dH3pre . H2^T ; db3
-    bf16* imA = stg;
-    bf16* imB = stg + CBF_CH * SA64;
-#pragma unroll
-    for (int mt = 0; mt < 2; ++mt) store_tile(imA, SA64, erow, 32 * mt, d3b[mt], h);
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt) store_tile(imB, SA128, erow, 32 * mt, H2b[mt], h);
-    __syncthreads();
-    bA[0] += stage_mma(imA, SA64, imB, SA128, tA0 / 4, tA0 % 4, CBF_CH / 16, lane, accA[0], tA0 % 4 == 0);
-    bA[1] += stage_mma(imA, SA64, imB, SA128, tA1 / 4, tA1 % 4, CBF_CH / 16, lane, accA[1], tA1 % 4 == 0);
-    __syncthreads();
-    // ---- stage B: dW2 (128x64) += dH2pre . H1^T ; db2
-    imA = stg;
-    imB = stg + CBF_CH * SA128;
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt) store_tile(imA, SA128, erow, 32 * mt, d2b[mt], h);
-#pragma unroll
-    for (int mt = 0; mt < 2; ++mt) store_tile(imB, SA64, erow, 32 * mt, H1b[mt], h);
-    __syncthreads();
-    bB[0] += stage_mma(imA, SA128, imB, SA64, tB0 / 2, tB0 % 2, CBF_CH / 16, lane, accB[0], tB0 % 2 == 0);
-    bB[1] += stage_mma(imA, SA128, imB, SA64, tB1 / 2, tB1 % 2, CBF_CH / 16, lane, accB[1], tB1 % 2 == 0);
-    __syncthreads();
     // ---- stage C+D: dW1f (64x32) += dH1pre . F^T (waves 0,1);
-    //      dW4pad (32x64) += [dh;0] . relu(H3)^T -> row 0 = dw4, row-sum = db4 (waves 2,3)
-    bf16* imC = stg;
-    bf16* imF = imC + CBF_CH * SA64;
-    bf16* imD = imF + CBF_CH * SA32;
-    bf16* imH = imD + CBF_CH * SA32;
-#pragma unroll
-    for (int mt = 0; mt < 2; ++mt) store_tile(imC, SA64, erow, 32 * mt, d1b[mt], h);
-#pragma unroll
-    for (int mt = 0; mt < 2; ++mt) store_tile(imH, SA64, erow, 32 * mt, H3b[mt], h);
+    //      dW4pad (32x64) += [dh;0] . relu(H3)^T -> row 0 = dw4 (waves 2,3)
     {
+      bf16* imC = stg;
+      bf16* imF = imC + CBF_CH * SA64;
+      bf16* imD = imF + CBF_CH * SA32;
+      bf16* imH = imD + CBF_CH * SA32;
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt) store_tile(imC, SA64, erow, 32 * mt, d1b[mt], h);
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt) store_tile(imH, SA64, erow, 32 * mt, H3b[mt], h);
       bf16x8 z, dv;
 #pragma unroll
       for (int j = 0; j < 8; ++j) { z[j] = (bf16)0.f; dv[j] = (bf16)0.f; }
@@ -410,38 +441,39 @@ __global__ __launch_bounds__(CBF_BWD_WAVES * 64, 1) void cbf_bwd_kernel(CbfBwdAr
       *reinterpret_cast<bf16x8*>(imF + erow * SA32 + 16 + 8 * h) = z;
       *reinterpret_cast<bf16x8*>(imD + erow * SA32 + 8 * h) = dv;
       *reinterpret_cast<bf16x8*>(imD + erow * SA32 + 16 + 8 * h) = z;
+      __syncthreads();
+      if (wave < 2) stage_mma(imC, SA64, imF, SA32, wave, 0, CBF_CH / 16, lane, accC, false);
+      else if (wave < 4) stage_mma(imD, SA32, imH, SA64, 0, wave - 2, CBF_CH / 16, lane, accC, false);
+      __syncthreads();
     }
-    __syncthreads();
-    if (wave < 2) stage_mma(imC, SA64, imF, SA32, wave, 0, CBF_CH / 16, lane, accC, false);
-    else bD += stage_mma(imD, SA32, imH, SA64, 0, wave - 2, CBF_CH / 16, lane, accC, wave == 2);
-    __syncthreads();
   }
 
   // ---- per-workgroup slab
   float* P = a.partial + (long)blockIdx.x * CBF_PARTIAL;
-  write_tile(P + P_W3, 128, tA0 / 4, tA0 % 4, accA[0], lane);
-  write_tile(P + P_W3, 128, tA1 / 4, tA1 % 4, accA[1], lane);
-  write_tile(P + P_W2, 64, tB0 / 2, tB0 % 2, accB[0], lane);
-  write_tile(P + P_W2, 64, tB1 / 2, tB1 % 2, accB[1], lane);
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int t = wave + 4 * u;
+    write_tile(P + P_W3, 128, t / 4, t % 4, accA[u], lane);
+    write_tile(P + P_W2, 64, t / 2, t % 2, accB[u], lane);
+    const float s3 = bA[u] + shfl_xor32(bA[u]);
+    if (h == 0 && t % 4 == 0) P[P_B3 + 32 * (t / 4) + r] = s3;
+    const float s2 = bB[u] + shfl_xor32(bB[u]);
+    if (h == 0 && t % 2 == 0) P[P_B2 + 32 * (t / 2) + r] = s2;
+  }
   if (wave < 2) {
     write_tile(P + P_W1, 32, wave, 0, accC, lane);
-  } else {
-    // dW4pad row 0 (= dw4 for columns 32*(wave-2) + r): reg 0 of lanes h == 0
-    if (h == 0) P[P_W4 + 32 * (wave - 2) + r] = accC[0];
-    if (wave == 2) {
-      const float s4 = bD + shfl_xor32(bD);
-      if (lane == 0) P[P_B4] = s4;
-    }
+  } else if (wave < 4) {
+    if (h == 0) P[P_W4 + 32 * (wave - 2) + r] = accC[0];   // dW4pad row 0 = dw4
   }
-  {
-    const float s0 = bA[0] + shfl_xor32(bA[0]);
-    const float s1 = bA[1] + shfl_xor32(bA[1]);
-    if (h == 0 && tA0 % 4 == 0) P[P_B3 + 32 * (tA0 / 4) + r] = s0;
-    if (h == 0 && tA1 % 4 == 0) P[P_B3 + 32 * (tA1 / 4) + r] = s1;
-    const float u0 = bB[0] + shfl_xor32(bB[0]);
-    const float u1 = bB[1] + shfl_xor32(bB[1]);
-    if (h == 0 && tB0 % 2 == 0) P[P_B2 + 32 * (tB0 / 2) + r] = u0;
-    if (h == 0 && tB1 % 2 == 0) P[P_B2 + 32 * (tB1 / 2) + r] = u1;
+  // db4: exact fp32 per-wave partials, summed through LDS
+  __shared__ float red4[CBF_BWD_WAVES];
+  const float s4 = wave_sum(db4);
+  if (lane == 0) red4[wave] = s4;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float t4 = 0.f;
+    for (int w = 0; w < CBF_BWD_WAVES; ++w) t4 += red4[w];
+    P[P_B4] = t4;
   }
 }
 

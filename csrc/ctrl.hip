@@ -132,6 +132,37 @@ DEV void node_forward(const bf16* pool, const bf16x8& sfrag, const bf16* wn, con
   }
 }
 
+// Two-stage software pipeline for the per-edge gathers (idx -> s_j are dependent global
+// loads): at tile q the kernel issues the idx load of tile q+2 and the state loads of tile
+// q+1, then computes tile q, so every load has a full tile of MFMA work to land under.
+struct EdgeIdx { int j, b, i; bool ok; };
+struct EdgeSt { float4 si, sj; int j, i; bool ok; };
+
+DEV void ctrl_idx_load(const int* idx, long i_env, int N, int K, int g0, int q, int r, int total, EdgeIdx& o) {
+  const int al = 2 * q + (r >> 4);
+  const int slot = r & 15;
+  const int gi = g0 + al;
+  o.ok = (q < 16) && (gi < total) && (slot < K);
+  o.b = 0; o.i = 0; o.j = 0;
+  if (o.ok) {
+    o.b = gi / N;
+    o.i = gi - o.b * N;
+    o.j = idx[o.b * (int)i_env + o.i * K + slot];
+  }
+}
+
+DEV void ctrl_st_load(const float4* S, long s_env, const EdgeIdx& x, EdgeSt& o) {
+  o.ok = x.ok;
+  o.j = x.j;
+  o.i = x.i;
+  if (x.ok) {
+    o.si = S[x.b * (int)s_env + x.i];
+    o.sj = S[x.b * (int)s_env + x.j];
+  } else {
+    o.si = o.sj = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+}
+
 template <int WAVES>
 __global__ __launch_bounds__(WAVES * 64) void ctrl_fwd_kernel(CtrlArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -155,25 +186,24 @@ __global__ __launch_bounds__(WAVES * 64) void ctrl_fwd_kernel(CtrlArgs a) {
 
   for (int grp = blockIdx.x * WAVES + wave; grp * 32 < total; grp += gridDim.x * WAVES) {
     const int g0 = grp * 32;
-    // ---------------- edge phase: 16 tiles x (2 agents x 16 slots)
+    // ---------------- edge phase: 16 tiles x (2 agents x 16 slots); the gathers of tile q+1
+    // (idx -> s_j, dependent global loads) are issued before tile q's MFMA chain
+    EdgeIdx xi1;
+    EdgeSt xs0;
+    {
+      EdgeIdx xi0;
+      ctrl_idx_load(a.idx, a.i_env, N, K, g0, 0, r, total, xi0);
+      ctrl_st_load(a.S, a.s_env, xi0, xs0);
+      ctrl_idx_load(a.idx, a.i_env, N, K, g0, 1, r, total, xi1);
+    }
     for (int q = 0; q < 16; ++q) {
-      const int al = 2 * q + (r >> 4);
-      const int slot = r & 15;
-      const int gi = g0 + al;
-      const bool ok = (gi < total) && (slot < K);
-      float4 rel = make_float4(0.f, 0.f, 0.f, 0.f);
-      float eye = 0.f;
-      bool m = false;
-      if (ok) {
-        const int b = gi / N, i = gi - b * N;
-        const int j = a.idx[(long)b * a.i_env + (long)i * K + slot];
-        const float4 si = a.S[(long)b * a.s_env + i];
-        const float4 sj = a.S[(long)b * a.s_env + j];
-        rel = make_float4(si.x - sj.x, si.y - sj.y, si.z - sj.z, si.w - sj.w);
-        eye = (j == i) ? 1.f : 0.f;
-        // strict < on the un-eps'd norm (controller.py:38-39)
-        m = sqrtf(rel.x * rel.x + rel.y * rel.y) < a.obs_r;
-      }
+      const EdgeSt cur = xs0;
+      ctrl_st_load(a.S, a.s_env, xi1, xs0);                       // states of tile q+1
+      ctrl_idx_load(a.idx, a.i_env, N, K, g0, q + 2, r, total, xi1);   // idx of tile q+2
+      const bool ok = cur.ok;
+      const float4 rel = make_float4(cur.si.x - cur.sj.x, cur.si.y - cur.sj.y, cur.si.z - cur.sj.z, cur.si.w - cur.sj.w);
+      const float eye = (cur.j == cur.i) ? 1.f : 0.f;
+      const bool m = ok && (sqrtf(rel.x * rel.x + rel.y * rel.y) < a.obs_r);   // strict, un-eps'd (controller.py:38-39)
       const bf16x8 F = ctrl_edge_frag(rel, eye, ok, h);
       f32x16 Z[4];
       ctrl_edge_tile(F, wl + opaque_zero(), eb2, lane, Z);
@@ -641,22 +671,26 @@ __global__ __launch_bounds__(EB_WAVES * 64, 2) void ctrl_edge_bwd_kernel(CtrlEdg
   const bf16 z = (bf16)0.f;
 
   for (long chunk = blockIdx.x; chunk < nchunks; chunk += gridDim.x) {
+    EdgeIdx xi1;
+    EdgeSt xs0;
+    const int g0 = (int)(chunk * EB_CH) + wave * 32;
+    {
+      EdgeIdx xi0;
+      ctrl_idx_load(a.idx, a.i_env, N, K, g0, 0, r, total, xi0);
+      ctrl_st_load(a.S, a.s_env, xi0, xs0);
+      ctrl_idx_load(a.idx, a.i_env, N, K, g0, 1, r, total, xi1);
+    }
     for (int q = 0; q < 16; ++q) {
-      const int al = 2 * q + (r >> 4);
+      const EdgeSt cur = xs0;
+      ctrl_st_load(a.S, a.s_env, xi1, xs0);
+      ctrl_idx_load(a.idx, a.i_env, N, K, g0, q + 2, r, total, xi1);
       const int slot = r & 15;
-      const int ga = (int)(chunk * EB_CH) + wave * 32 + al;
-      const bool ok = (ga < total) && (slot < K);
-      int b = 0, i = 0, j = 0;
-      float4 rel = make_float4(0.f, 0.f, 0.f, 0.f);
-      float eye = 0.f;
-      if (ok) {
-        b = ga / N; i = ga - b * N;
-        j = a.idx[(long)b * a.i_env + (long)i * K + slot];
-        const float4 si = a.S[(long)b * a.s_env + i];
-        const float4 sj = a.S[(long)b * a.s_env + j];
-        rel = make_float4(si.x - sj.x, si.y - sj.y, si.z - sj.z, si.w - sj.w);
-        eye = (j == i) ? 1.f : 0.f;
-      }
+      const bool ok = cur.ok;
+      const int ga = g0 + 2 * q + (r >> 4);
+      const int b = ok ? ga / N : 0;
+      const int i = cur.i, j = cur.j;
+      const float4 rel = make_float4(cur.si.x - cur.sj.x, cur.si.y - cur.sj.y, cur.si.z - cur.sj.z, cur.si.w - cur.sj.w);
+      const float eye = (j == i) ? 1.f : 0.f;
       const bf16x8 F = ctrl_edge_frag(rel, eye, ok, h);
       const bf16* wt = wf + opaque_zero();
       bf16x16 H1b[2];
@@ -667,20 +701,26 @@ __global__ __launch_bounds__(EB_WAVES * 64, 2) void ctrl_edge_bwd_kernel(CtrlEdg
         H1b[mt] = to_bf16x16(c);
       }
       // max-pool backward: this edge receives dP[f] where it was the argmax slot
+      // (all 16 loads of the agent's argmax/dP rows issued back to back)
       bf16x8 dz[8];
+      {
+        uint64_t amv[8];
+        bf16x8 dpv[8];
+        const uint8_t* arow = a.argmax + b * (int)a.am_env + i * 128;
+        const bf16* prow = a.dP + b * (int)a.dp_env + i * 128;
 #pragma unroll
-      for (int kk = 0; kk < 8; ++kk) {
-        bf16x8 v;
-#pragma unroll
-        for (int jj = 0; jj < 8; ++jj) v[jj] = z;
-        if (ok) {
+        for (int kk = 0; kk < 8; ++kk) {
           const int f0 = 16 * kk + 8 * h;
-          const uint64_t am = *reinterpret_cast<const uint64_t*>(a.argmax + (long)b * a.am_env + (long)i * 128 + f0);
-          const bf16x8 dp = *reinterpret_cast<const bf16x8*>(a.dP + (long)b * a.dp_env + (long)i * 128 + f0);
-#pragma unroll
-          for (int jj = 0; jj < 8; ++jj) v[jj] = (((am >> (8 * jj)) & 0xFFull) == (uint64_t)slot) ? dp[jj] : z;
+          amv[kk] = ok ? *reinterpret_cast<const uint64_t*>(arow + f0) : ~0ull;
+          dpv[kk] = *reinterpret_cast<const bf16x8*>(prow + f0);
         }
-        dz[kk] = v;
+#pragma unroll
+        for (int kk = 0; kk < 8; ++kk) {
+          bf16x8 v;
+#pragma unroll
+          for (int jj = 0; jj < 8; ++jj) v[jj] = (((amv[kk] >> (8 * jj)) & 0xFFull) == (uint64_t)slot) ? dpv[kk][jj] : z;
+          dz[kk] = v;
+        }
       }
       // dH1 = W2^T dZ (natural k) . relu'(H1)
       bf16x16 d1b[2];
@@ -702,7 +742,7 @@ __global__ __launch_bounds__(EB_WAVES * 64, 2) void ctrl_edge_bwd_kernel(CtrlEdg
         });
         if (ok && h == 0) {
           const float4 g = (j != i) ? make_float4(c[0], c[1], c[2], c[3]) : make_float4(0.f, 0.f, 0.f, 0.f);
-          a.dEc[(long)b * a.de_env + (long)i * K + slot] = g;
+          a.dEc[b * (int)a.de_env + i * K + slot] = g;
         }
       }
       // S1: dW2 (128x64) += dZ . H1^T ; eb2

@@ -166,7 +166,7 @@ class HipEngine:
         nbb = native.cbf_bwd_grid(2 * E, self.dev)
         part_cbf = self._buf(self._part_cbf, nbb, native.CBF_PARTIAL)
         dE = self.dE[: 2 * E * 4].view(2, T, B, N, K, 4)
-        native.cbf_bwd(S, idx, dh, pw.cbf_w, pw.cbf_off["w1f"], pw.cbf_v, passes=2, dE=dE, partial=part_cbf,
+        native.cbf_bwd(S, idx, dh, pw.cbf_w, pw.cbf_off["w1f"], pw.cbf_rm, pw.cbf_v, passes=2, dE=dE, partial=part_cbf,
                        num_blocks=nbb)
         rptr = self.rptr[: T * B]
         redges = self.redges[: T * B]

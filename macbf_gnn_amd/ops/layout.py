@@ -434,3 +434,16 @@ def ctrl_edge_grad_map(fp_offsets):
             S.append(8320 + o * 32 + 8 + k); D.append(eW1 + o * 5 + k)
         S.append(8320 + o * 32 + 5); D.append(eb1 + o)
     return np.asarray(S, np.int64), np.asarray(D, np.int64)
+
+
+CBF_RM_STRIDES = {"w2": 72, "w3": 136}
+
+
+def cbf_rm(fp_offsets) -> RMPacker:
+    """Row-major CBF images for the backward kernel: W2 (128x64) and W3 (64x128)."""
+    W2 = fp_offsets["cbf_net.2.weight"]
+    W3 = fp_offsets["cbf_net.4.weight"]
+    p = RMPacker()
+    p.add("w2", _mat(W2, 128, 64), 128, 64, CBF_RM_STRIDES["w2"])
+    p.add("w3", _mat(W3, 64, 128), 64, 128, CBF_RM_STRIDES["w3"])
+    return p

@@ -9,6 +9,7 @@ so shapes are never trusted implicitly).
 from __future__ import annotations
 
 import functools
+import math
 import os
 
 import torch
@@ -80,10 +81,29 @@ def _ok(rc, what):
 
 
 # ----------------------------------------------------------------------------- kernels
-def scan(S, idx, dang, cnt, safe, *, K, do_knn=True, do_safety=True):
+SCAN_MAX_N = 4096
+_perm_cache = {}
+
+
+def _perm_buf(B, N, device):
+    key = (B, N, str(device))
+    t = _perm_cache.get(key)
+    if t is None:
+        t = torch.empty(B, N, dtype=torch.int32, device=device)
+        _perm_cache[key] = t
+    return t
+
+
+def scan(S, idx, dang, cnt, safe, *, K, do_knn=True, do_safety=True, perm=None):
     """K1 over one timestep. S: (B, N, 4) view with env stride (may be a slice of a (B,T+1,N,4)
-    buffer); idx/dang: (B, N, K) views; cnt: (B, 2) view; safe: (B,) view."""
+    buffer); idx/dang: (B, N, K) views; cnt: (B, 2) view; safe: (B,) view.
+
+    Two launches: cell_sort orders each env's agents along a Morton curve, then the scan walks
+    candidates outward along it (results are order independent; the order only keeps the
+    wave-divergent top-K insertion rare)."""
     B, N = S.shape[0], S.shape[1]
+    if N > SCAN_MAX_N:
+        raise NativeError(f"scan stages one env in LDS: N <= {SCAN_MAX_N} (got {N})")
     if S.dtype != torch.float32 or S.stride(2) != 1 or S.stride(1) != 4:
         raise NativeError("S must be float32 with contiguous (N,4) rows")
     if K < 1 or K > C.MAX_TOP_K or K > N:
@@ -98,7 +118,12 @@ def scan(S, idx, dang, cnt, safe, *, K, do_knn=True, do_safety=True):
             raise NativeError("cnt must be float32 (B,2)")
     if do_safety and safe is not None and (safe.dtype != torch.float32 or tuple(safe.shape) != (B,)):
         raise NativeError("safe must be float32 (B,)")
-    rc = lib().scan(ptr(S), S.stride(0) // 4, B, N, K, ptr(idx) if do_knn else 0,
+    if perm is None:
+        perm = _perm_buf(B, N, S.device)
+    rc = lib().cell_sort(ptr(S), S.stride(0) // 4, B, N, float(math.sqrt(max(1.0, N / C.AGENT_DENSITY))),
+                         ptr(perm), stream_handle())
+    _ok(rc, "cell_sort")
+    rc = lib().scan(ptr(S), S.stride(0) // 4, ptr(perm), B, N, K, ptr(idx) if do_knn else 0,
                     idx.stride(0) if do_knn else 0, ptr(dang) if do_knn else 0,
                     ptr(cnt) if do_knn else 0, cnt.stride(0) if (do_knn and cnt is not None) else 0,
                     ptr(safe) if do_safety else 0, safe.stride(0) if (do_safety and safe is not None) else 0,
@@ -221,7 +246,7 @@ def cbf_bwd_grid(EV: int, device) -> int:
     return max(1, min((EV + 127) // 128, num_cu(device)))
 
 
-def cbf_bwd(S, idx, dh, wpack, f_bwd, wvec, *, passes=2, dE=None, partial=None, num_blocks=None):
+def cbf_bwd(S, idx, dh, wpack, f_bwd, wrm, wvec, *, passes=2, dE=None, partial=None, num_blocks=None):
     """dh (passes, T, B, N, K) -> dE (passes, T, B, N, K, 4), per-WG dW slabs (nb, CBF_PARTIAL)."""
     T, B, N, K = idx.shape
     check(idx, torch.int32, None, "idx")
@@ -232,11 +257,14 @@ def cbf_bwd(S, idx, dh, wpack, f_bwd, wvec, *, passes=2, dE=None, partial=None, 
     check(wvec, torch.float32, None, "wvec")
     if wpack.numel() < (f_bwd + 70) * 512:
         raise NativeError("packed CBF weights too small")
+    check(wrm, torch.bfloat16, (128 * 72 + 64 * 136,), "wrm")
     E = B * T * N * K
+    if E * passes >= 2 ** 31:
+        raise NativeError("too many edge evaluations for 32-bit indexing")
     nb = num_blocks or cbf_bwd_grid(E * passes, S.device)
     check(partial, torch.float32, (nb, CBF_PARTIAL), "partial")
     rc = lib().cbf_bwd(ptr(S), S.stride(1) // 4, S.stride(0) // 4, ptr(idx), B, T, N, K, int(passes), ptr(dh),
-                       ptr(wpack), int(f_bwd), ptr(wvec), ptr(dE), ptr(partial), float(C.OBS_RADIUS),
+                       ptr(wpack), int(f_bwd), ptr(wrm), ptr(wvec), ptr(dE), ptr(partial), float(C.OBS_RADIUS),
                        float(C.DIST_MIN_THRES), float(C.CBF_DIST_EPS), nb, stream_handle())
     _ok(rc, "cbf_bwd")
     return nb

@@ -27,6 +27,8 @@ class PackedWeights:
         self.node_rm = L.ctrl_node_rm(offs)
         self.node_rm_off = self.node_rm.offsets()
         self._irm = mk(self.node_rm.index())
+        self.cbf_rmp = L.cbf_rm(offs)
+        self._icrm = mk(self.cbf_rmp.index())
         self._src = torch.zeros(n + 2, dtype=torch.float32, device=dev)
         self._src[n + 1] = 1.0
         self.ctrl_w = torch.empty(self._ictrl.numel(), dtype=torch.bfloat16, device=dev)
@@ -34,6 +36,7 @@ class PackedWeights:
         self.ctrl_v = torch.empty(self._vctrl.numel(), dtype=torch.float32, device=dev)
         self.cbf_v = torch.empty(self._vcbf.numel(), dtype=torch.float32, device=dev)
         self.ctrl_rm = torch.empty(self._irm.numel(), dtype=torch.bfloat16, device=dev)
+        self.cbf_rm = torch.empty(self._icrm.numel(), dtype=torch.bfloat16, device=dev)
         self.update()
 
     @torch.no_grad()
@@ -45,3 +48,4 @@ class PackedWeights:
         torch.index_select(self._src, 0, self._vctrl, out=self.ctrl_v)
         torch.index_select(self._src, 0, self._vcbf, out=self.cbf_v)
         self.ctrl_rm.copy_(self._src.index_select(0, self._irm))
+        self.cbf_rm.copy_(self._src.index_select(0, self._icrm))

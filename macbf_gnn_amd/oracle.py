@@ -32,8 +32,9 @@ from . import config as C
 def knn_idx(s: torch.Tensor, k: int) -> torch.Tensor:
     """Indices of the k nearest agents (positions = s[..., :2]), nearest first.
 
-    Ties are broken by the lower agent index (stable sort), which is also what the HIP
-    kernel's strict-< insertion over ascending candidates produces. Self is slot 0.
+    Ties are broken by the lower agent index (stable sort); the HIP scan compares (d2, index)
+    lexicographically, so it produces the same lists in any candidate order. Self is slot 0
+    unless another agent sits exactly on it with a lower index.
     """
     p = s[..., :2]
     d = p.unsqueeze(-2) - p.unsqueeze(-3)            # (..., N, N, 2): p_i - p_j

@@ -86,7 +86,7 @@ def test_cbf_bwd_matches_autograd(T, B, N):
     dE = torch.zeros(2, T, B, N, K, 4, device=DEV)
     nb = native.cbf_bwd_grid(2 * T * B * N * K, DEV)
     part = torch.zeros(nb, native.CBF_PARTIAL, device=DEV)
-    native.cbf_bwd(S, idx, dh, pw.cbf_w, pw.cbf_off["w1f"], pw.cbf_v, passes=2, dE=dE, partial=part, num_blocks=nb)
+    native.cbf_bwd(S, idx, dh, pw.cbf_w, pw.cbf_off["w1f"], pw.cbf_rm, pw.cbf_v, passes=2, dE=dE, partial=part, num_blocks=nb)
     rptr = torch.zeros(T * B, N + 1, dtype=torch.int32, device=DEV)
     red_e = torch.zeros(T * B, N * K, dtype=torch.int32, device=DEV)
     native.rev_csr(idx.view(T * B, N, K), rptr, red_e)

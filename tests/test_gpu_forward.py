@@ -52,6 +52,28 @@ def test_scan_knn_ttc_safety(B, N):
     assert torch.equal(safe, O.safe_agent_count(s).float())
 
 
+@pytest.mark.parametrize("B,N", [(2, 300), (1, 4096)])
+def test_scan_ties_and_out_of_domain(B, N):
+    """Morton-ordered scan: exact (d2, index) tie-breaks on a lattice with duplicates, agents
+    outside the nominal square (clamped cells), result independent of the visit order."""
+    s, _ = _states(B, N, seed=5)
+    L = math.sqrt(max(1.0, N / 8.0))
+    s[..., :2] = torch.round(s[..., :2] * 4) / 4             # lattice -> many equal distances
+    s[:, : N // 10, :2] += 1.5 * L                             # far outside the square
+    s[:, N // 10: N // 5, :2] -= 0.7 * L
+    K = min(N, C.TOP_K)
+    idx = torch.empty(B, N, K, dtype=torch.int32, device=DEV)
+    dang = torch.empty(B, N, K, dtype=torch.uint8, device=DEV)
+    cnt = torch.zeros(B, 2, device=DEV)
+    safe = torch.zeros(B, device=DEV)
+    native.scan(s.contiguous(), idx, dang, cnt, safe, K=K)
+    torch.cuda.synchronize()
+    ref = O.knn_idx(s, K)
+    assert torch.equal(idx.long(), ref)
+    assert torch.equal(dang.bool(), O.ttc_mask_knn(s, ref))
+    assert torch.equal(safe, O.safe_agent_count(s).float())
+
+
 def test_scan_strided_views():
     """Writes into a (B, T, N, K) trajectory buffer through per-step views."""
     B, T, N = 2, 3, 40
