@@ -10,13 +10,13 @@ namespace mb {
 struct CellSortArgs {
   const float4* S;  long s_env;      // agent (b,i) state at S[b*s_env + i]
   int B, N;
-  float L;                           // scenario side length (Morton grid spans [0, L]^2)
+  float L;                           // scenario side length (curve grid spans [0, L]^2)
   int* perm;                         // (B, N) position on the curve -> agent id
 };
 
 struct ScanArgs {
   const float4* S;  long s_env;      // agent (b,i) state at S[b*s_env + i]
-  const int* perm;                   // (B, N) Morton order from cell_sort
+  const int* perm;                   // (B, N) Hilbert order from cell_sort
   int B, N, K;
   int* idx;         long i_env;      // (b,i,k) at idx[b*i_env + i*K + k]
   uint8_t* dang;                     // same indexing as idx (may be null)

@@ -35,37 +35,45 @@ DEV bool ttc_danger(float x, float y, float vx, float vy, float r2, float ttc) {
 // Spatial ordering. The top-K insertion is wave-divergent: a wave pays for the 12-step
 // insertion whenever ANY of its 64 lanes inserts. With agents in random order every
 // candidate is an insertion for some lane. cell_sort_kernel orders each env's agents along a
-// Morton curve (32x32 grid over the scenario square), so a wave's 64 agents are spatial
+// Hilbert curve (32x32 grid over the scenario square), so a wave's 64 agents are spatial
 // neighbours; scan_kernel then visits candidates outward from the wave's own position on
 // the curve, the lists converge within the first ~100 candidates and later candidates
 // almost never insert. Results do not depend on the order: (d2, index) is compared
 // lexicographically, so idx/dang/counts/safety are exactly those of the plain all-pairs scan.
 // ---------------------------------------------------------------------------------------
 constexpr int SORT_BLOCK = 1024;
-constexpr int MORTON_BINS = 1024;
+constexpr int CURVE_BINS = 1024;
 
-DEV unsigned spread5(unsigned v) {   // 5 bits -> every other bit
-  v &= 31u;
-  v = (v | (v << 8)) & 0x00FF00FFu;
-  v = (v | (v << 4)) & 0x0F0F0F0Fu;
-  v = (v | (v << 2)) & 0x33333333u;
-  v = (v | (v << 1)) & 0x55555555u;
-  return v;
+// Hilbert index on the 32x32 cell grid: consecutive indices are edge-adjacent cells, so any
+// 64 consecutive agents cover a compact patch (a Morton range can jump across the square).
+DEV int hilbert32(int x, int y) {
+  int d = 0;
+#pragma unroll
+  for (int s = 16; s > 0; s >>= 1) {
+    const int rx = (x & s) ? 1 : 0;
+    const int ry = (y & s) ? 1 : 0;
+    d += s * s * ((3 * rx) ^ ry);
+    if (ry == 0) {
+      if (rx == 1) { x = 31 - x; y = 31 - y; }
+      const int t = x; x = y; y = t;
+    }
+  }
+  return d;
 }
 
 __global__ __launch_bounds__(SORT_BLOCK) void cell_sort_kernel(CellSortArgs a) {
-  __shared__ int hist[MORTON_BINS];
+  __shared__ int hist[CURVE_BINS];
   __shared__ int wsum[SORT_BLOCK / WAVE];
   const int b = blockIdx.x;
   const float4* Sb = a.S + (long)b * a.s_env;
-  for (int q = threadIdx.x; q < MORTON_BINS; q += SORT_BLOCK) hist[q] = 0;
+  for (int q = threadIdx.x; q < CURVE_BINS; q += SORT_BLOCK) hist[q] = 0;
   __syncthreads();
   const float inv = 32.f / a.L;
   for (int i = threadIdx.x; i < a.N; i += SORT_BLOCK) {
     const float4 s = Sb[i];
     const int cx = min(31, max(0, (int)(s.x * inv)));
     const int cy = min(31, max(0, (int)(s.y * inv)));
-    atomicAdd(&hist[spread5(cx) | (spread5(cy) << 1)], 1);
+    atomicAdd(&hist[hilbert32(cx, cy)], 1);
   }
   __syncthreads();
   // exclusive scan of 1024 bins with 1024 threads: wave scan + wave totals
@@ -91,97 +99,169 @@ __global__ __launch_bounds__(SORT_BLOCK) void cell_sort_kernel(CellSortArgs a) {
     const float4 s = Sb[i];
     const int cx = min(31, max(0, (int)(s.x * inv)));
     const int cy = min(31, max(0, (int)(s.y * inv)));
-    const int p = atomicAdd(&hist[spread5(cx) | (spread5(cy) << 1)], 1);
+    const int p = atomicAdd(&hist[hilbert32(cx, cy)], 1);
     perm[p] = i;
   }
 }
 
-constexpr int SCAN_BLOCK = 256;      // 4 waves x 64 agents (consecutive on the Morton curve)
-constexpr int SCAN_MAXN = 4096;      // whole env staged in LDS (24 B per agent)
+constexpr int SCAN_BLOCK = 256;      // 4 waves x 64 agents (consecutive on the curve)
+constexpr int SCAN_MAXN = 4096;      // whole env staged in LDS
+constexpr int SCH = 8;               // candidates per chunk (one bounding box each)
 
-template <int K>
-DEV void topk_insert(float (&bd)[K], int (&bi)[K], float d2, int j) {
-  // caller guarantees (d2, j) < (bd[K-1], bi[K-1]) lexicographically
-#pragma unroll
-  for (int q = K - 1; q >= 1; --q) {
-    const bool sh = (d2 < bd[q - 1]) || (d2 == bd[q - 1] && j < bi[q - 1]);
-    const bool here = !sh && ((d2 < bd[q]) || (d2 == bd[q] && j < bi[q]));
-    const float nd = sh ? bd[q - 1] : (here ? d2 : bd[q]);
-    const int ni = sh ? bi[q - 1] : (here ? j : bi[q]);
-    bd[q] = nd;
-    bi[q] = ni;
-  }
-  if ((d2 < bd[0]) || (d2 == bd[0] && j < bi[0])) { bd[0] = d2; bi[0] = j; }
+static inline size_t scan_lds_bytes(int N) {
+  const int Np = (N + SCH - 1) / SCH * SCH;
+  return (size_t)Np * 24 + (size_t)(Np / SCH) * 20;
 }
 
+// (d2, index) packed into one 64-bit key: d2 >= 0, so its IEEE bits order like the values and
+// a single unsigned compare is the lexicographic (distance, lower index) order.
+DEV uint64_t knn_key(float d2, unsigned j) { return ((uint64_t)__float_as_uint(d2) << 32) | j; }
+constexpr uint64_t KEY_EMPTY = (0x7f800000ull << 32) | 0xffffffffull;   // (+inf, max index)
+
+template <int K>
+DEV void topk_insert(uint64_t (&bk)[K], uint64_t x) {
+  // caller guarantees x < bk[K-1]; bk is sorted ascending, so c[] is monotone
+  bool c[K];
+#pragma unroll
+  for (int q = 0; q < K; ++q) c[q] = x < bk[q];
+#pragma unroll
+  for (int q = K - 1; q >= 1; --q) bk[q] = c[q - 1] ? bk[q - 1] : (c[q] ? x : bk[q]);
+  bk[0] = c[0] ? x : bk[0];
+}
+
+DEV float wave_min(float v) { return -wave_max(-v); }
+
+// Chunked scan with conservative culling. The env's agents are staged in curve order in LDS
+// with a bounding box (+ max speed) per chunk of 8. A wave compares the box gap to its own
+// 64-agent box: the whole chunk is skipped for kNN when the gap exceeds every lane's current
+// K-th distance (strictly, so ties are never skipped), and for the safety check when it
+// exceeds the reachable distance r + ttc*(vmax_wave + vmax_chunk) (x1.01 + 1e-4 margin). Both
+// decisions are wave-uniform branches; after the local neighbourhood has filled the lists
+// almost every far chunk costs one box test instead of 8 pair evaluations.
 template <int K>
 __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanArgs a) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  float4* tp = reinterpret_cast<float4*>(smem);               // sorted: x, y, |v|, agent id (bits)
-  float2* tv = reinterpret_cast<float2*>(tp + a.N);           // sorted: vx, vy
+  extern __shared__ float4 smem4[];
+  const int N = a.N;
+  const int Np = (N + SCH - 1) / SCH * SCH;
+  const int nch = Np / SCH;
+  float4* tp = smem4;                                          // [Np] x, y, vx, vy
+  float2* tq = reinterpret_cast<float2*>(tp + Np);             // [Np] |v|, agent id (bits)
+  float4* cb = reinterpret_cast<float4*>(tq + Np);             // [nch] minx, miny, maxx, maxy
+  float* cv = reinterpret_cast<float*>(cb + nch);              // [nch] max |v|
   __shared__ float red[3][SCAN_BLOCK / WAVE];
   const int b = blockIdx.y;
-  const int N = a.N;
   const float4* Sb = a.S + (long)b * a.s_env;
   const int* perm = a.perm + (long)b * N;
-  for (int q = threadIdx.x; q < N; q += SCAN_BLOCK) {
-    const int id = perm[q];
-    const float4 s = Sb[id];
-    tp[q] = make_float4(s.x, s.y, sqrtf(s.z * s.z + s.w * s.w), __int_as_float(id));
-    tv[q] = make_float2(s.z, s.w);
+  for (int q = threadIdx.x; q < Np; q += SCAN_BLOCK) {
+    if (q < N) {
+      const int id = perm[q];
+      const float4 s = Sb[id];
+      tp[q] = s;
+      tq[q] = make_float2(sqrtf(s.z * s.z + s.w * s.w), __int_as_float(id));
+    } else {
+      tp[q] = make_float4(INFINITY, INFINITY, 0.f, 0.f);      // key == KEY_EMPTY: never selected
+      tq[q] = make_float2(0.f, __int_as_float(-1));
+    }
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < nch; c += SCAN_BLOCK) {
+    float4 bx = make_float4(INFINITY, INFINITY, -INFINITY, -INFINITY);
+    float vm = 0.f;
+#pragma unroll
+    for (int u = 0; u < SCH; ++u) {
+      const int q = c * SCH + u;
+      if (q < N) {
+        const float4 s = tp[q];
+        bx.x = fminf(bx.x, s.x); bx.y = fminf(bx.y, s.y);
+        bx.z = fmaxf(bx.z, s.x); bx.w = fmaxf(bx.w, s.y);
+        vm = fmaxf(vm, tq[q].x);
+      }
+    }
+    cb[c] = bx;
+    cv[c] = vm;
   }
   __syncthreads();
   const int wave = threadIdx.x / WAVE, lane = threadIdx.x & 63;
   const int pos = blockIdx.x * SCAN_BLOCK + threadIdx.x;      // my position on the curve
   const bool act = pos < N;
   float4 me = make_float4(0.f, 0.f, 0.f, 0.f);
-  float2 mv = make_float2(0.f, 0.f);
+  float myv = 0.f;
   int i = 0;
   if (act) {
     me = tp[pos];
-    mv = tv[pos];
-    i = __float_as_int(me.w);
+    const float2 mq = tq[pos];
+    myv = mq.x;
+    i = __float_as_int(mq.y);
   }
   const float rc = sqrtf(a.r2_check);
-  // geometric pre-test for the safety check: dangerous => |p| < r + ttc*|v_i - v_j| <= r + ttc*(|v_i|+|v_j|)
-  const float base_i = rc + a.ttc_check * me.z;
-  float bd[K];
-  int bi[K];
+  // per-pair pre-test of the safety check: dangerous => |p| < r + ttc*|v_i - v_j| <= r + ttc*(|v_i|+|v_j|)
+  const float base_i = rc + a.ttc_check * myv;
+  uint64_t bk[K];
 #pragma unroll
-  for (int q = 0; q < K; ++q) { bd[q] = INFINITY; bi[q] = 0x7fffffff; }
+  for (int q = 0; q < K; ++q) bk[q] = KEY_EMPTY;
   bool danger = false;
-  // outward walk along the curve from the centre of this wave's 64 positions
-  int c0 = blockIdx.x * SCAN_BLOCK + wave * WAVE + 32;
-  if (c0 >= N) c0 = N - 1;
-  if (act) {
-    for (int d = 0; d < N; ++d) {
-      const int off = (d + 1) >> 1;
-      int p = (d & 1) ? c0 + off : c0 - off;
-      if (p >= N) p -= N;
-      if (p < 0) p += N;
-      const float4 c = tp[p];
-      const int j = __float_as_int(c.w);
-      const float dx = me.x - c.x;
-      const float dy = me.y - c.y;
-      const float d2 = dx * dx + dy * dy;
-      if (a.do_knn && ((d2 < bd[K - 1]) || (d2 == bd[K - 1] && j < bi[K - 1]))) topk_insert<K>(bd, bi, d2, j);
-      if (a.do_safety && !danger) {
-        const float lim = 1.01f * (base_i + a.ttc_check * c.z) + 1e-4f;
-        if (d2 < lim * lim && j != i) {
-          const float2 v = tv[p];
-          danger = ttc_danger(dx, dy, mv.x - v.x, mv.y - v.y, a.r2_check, a.ttc_check);
+  const float wminx = wave_min(act ? me.x : INFINITY), wmaxx = wave_max(act ? me.x : -INFINITY);
+  const float wminy = wave_min(act ? me.y : INFINITY), wmaxy = wave_max(act ? me.y : -INFINITY);
+  const float wvmax = wave_max(act ? myv : 0.f);
+  const bool wave_live = __any(act);
+  int cc0 = (blockIdx.x * SCAN_BLOCK + wave * WAVE + 32) / SCH;
+  if (cc0 >= nch) cc0 = nch - 1;
+  float thr = INFINITY;                 // max over active lanes of the current K-th distance
+  bool all_danger = false;
+  if (wave_live) {
+    // chunk metadata is read one step ahead of the (deterministic) walk to hide LDS latency
+    int ch = cc0;
+    float4 bx = cb[ch];
+    float cvm = cv[ch];
+    for (int m = 0; m < nch; ++m) {
+      const int cur = ch;
+      const float4 cbx = bx;
+      const float ccv = cvm;
+      {
+        const int k = (m + 2) >> 1;
+        int nx = ((m + 1) & 1) ? cc0 - k : cc0 + k;
+        if (nx >= nch) nx -= nch;
+        if (nx < 0) nx += nch;
+        ch = nx;
+        if (m + 1 < nch) { bx = cb[ch]; cvm = cv[ch]; }
+      }
+      const float gx = fmaxf(0.f, fmaxf(cbx.x - wmaxx, wminx - cbx.z));
+      const float gy = fmaxf(0.f, fmaxf(cbx.y - wmaxy, wminy - cbx.w));
+      const float bd2 = (gx * gx + gy * gy) * 0.999f;
+      const bool nk = a.do_knn && !(bd2 > thr);
+      const float lb = 1.01f * (rc + a.ttc_check * (wvmax + ccv)) + 1e-4f;
+      const bool ns = a.do_safety && !all_danger && !(bd2 > lb * lb);
+      if (!nk && !ns) continue;
+      float4 c[SCH];
+      float2 cq[SCH];
+#pragma unroll
+      for (int u = 0; u < SCH; ++u) { c[u] = tp[cur * SCH + u]; cq[u] = tq[cur * SCH + u]; }
+#pragma unroll
+      for (int u = 0; u < SCH; ++u) {
+        const int j = __float_as_int(cq[u].y);
+        const float dx = me.x - c[u].x;
+        const float dy = me.y - c[u].y;
+        const float d2 = dx * dx + dy * dy;
+        const uint64_t key = knn_key(d2, (unsigned)j);
+        if (nk && act && key < bk[K - 1]) topk_insert<K>(bk, key);
+        if (ns && act && !danger) {
+          const float lim = 1.01f * (base_i + a.ttc_check * cq[u].x) + 1e-4f;
+          if (d2 < lim * lim && j != i)
+            danger = ttc_danger(dx, dy, me.z - c[u].z, me.w - c[u].w, a.r2_check, a.ttc_check);
         }
       }
+      if (nk) thr = wave_max(act ? __uint_as_float((unsigned)(bk[K - 1] >> 32)) : -INFINITY);
+      if (ns) all_danger = !__any(act && !danger);
     }
   }
   float ndang = 0.f, nsafe_e = 0.f, safe_ag = 0.f;
   if (act && a.do_knn) {
     int* out = a.idx + (long)b * a.i_env + (long)i * K;
     uint8_t* dout = a.dang ? a.dang + (long)b * a.i_env + (long)i * K : nullptr;
-    const float4 si = Sb[i];
+    const float4 si = me;
 #pragma unroll
     for (int q = 0; q < K; ++q) {
-      const int j = bi[q];
+      const int j = (int)(unsigned)bk[q];
       out[q] = j;
       const float4 sj = Sb[j];
       const float eye = (j == i) ? 1.f : 0.f;
@@ -212,7 +292,7 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanArgs a) {
 template <int K>
 static void launch_k(const ScanArgs& a, hipStream_t st) {
   dim3 grid((a.N + SCAN_BLOCK - 1) / SCAN_BLOCK, a.B);
-  const size_t lds = (size_t)a.N * 24;
+  const size_t lds = scan_lds_bytes(a.N);
   (void)hipFuncSetAttribute((const void*)scan_kernel<K>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   hipLaunchKernelGGL(scan_kernel<K>, grid, dim3(SCAN_BLOCK), lds, st, a);
 }

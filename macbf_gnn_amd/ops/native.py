@@ -98,7 +98,7 @@ def scan(S, idx, dang, cnt, safe, *, K, do_knn=True, do_safety=True, perm=None):
     """K1 over one timestep. S: (B, N, 4) view with env stride (may be a slice of a (B,T+1,N,4)
     buffer); idx/dang: (B, N, K) views; cnt: (B, 2) view; safe: (B,) view.
 
-    Two launches: cell_sort orders each env's agents along a Morton curve, then the scan walks
+    Two launches: cell_sort orders each env's agents along a Hilbert curve, then the scan walks
     candidates outward along it (results are order independent; the order only keeps the
     wave-divergent top-K insertion rare)."""
     B, N = S.shape[0], S.shape[1]
