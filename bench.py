@@ -39,7 +39,9 @@ def main():
     ap.add_argument("--envs", type=int, default=64, help="environments per rank (weak scaling)")
     ap.add_argument("--inner_loops", type=int, default=50)
     ap.add_argument("--seed", type=int, default=0)
-    ap.add_argument("--no_early_stop", action="store_true")
+    ap.add_argument("--no_early_stop", action="store_true", help="fixed-T (=inner_loops) throughput")
+    ap.add_argument("--phases", action="store_true",
+                    help="after the timed loop, 2 extra steps with per-phase device-event timings")
     args = ap.parse_args()
 
     import torch
@@ -75,6 +77,15 @@ def main():
     elapsed = dp.max_scalar(elapsed)
     dp.all_reduce_(acc)
     agent_steps, safe_agents, t_sum = acc.tolist()
+    phases = None
+    if args.phases:          # outside the timed region
+        tr.timer.enabled = True
+        tot = {}
+        for _ in range(2):
+            for k, v in tr.train_step().get("phases_ms", {}).items():
+                tot[k] = tot.get(k, 0.0) + v / 2
+        tr.timer.enabled = False
+        phases = {k: round(v, 3) for k, v in tot.items()}
     value = agent_steps / elapsed
     out = {
         "metric": "agent-steps/sec (train loop) + safety-rate, 1024 agents",
@@ -94,10 +105,13 @@ def main():
                    "seq_len": args.inner_loops, "parallelism": f"dp{world}"},
         "safety_rate": safe_agents / agent_steps if agent_steps > 0 else None,
         "mean_T": t_sum / (args.steps * world),
+        "early_stop": not args.no_early_stop,
         "baseline": {"value": BASELINE_AGENT_STEPS_PER_S,
                      "source": "BASELINE.md: reference rollout-only loop @ N=1024, CPU x8 (upper bound of its "
                                "train loop, which does not run at N=1024)"},
     }
+    if phases is not None:
+        out["phases_ms"] = phases
     if rank == 0:
         print(json.dumps(out), flush=True)
     dp.shutdown()

@@ -40,6 +40,9 @@ def remove_distant_agents(x: torch.Tensor, k: int):
 
 
 def _knn(states):
+    if states.is_cuda:
+        from macbf_gnn_amd.ops import graph
+        return graph.knn(states.detach().unsqueeze(0), TOP_K)[0].long()
     return _O.knn_idx(states.detach().unsqueeze(0), TOP_K)[0]
 
 

@@ -84,6 +84,8 @@ class TrainConfig:
     model_path: Optional[str] = None
     log_path: Optional[str] = None
     compute_safety: bool = True
+    nan_guard: bool = True            # skip the optimizer step when the reduced gradient is not finite
+    phase_timing: bool = False        # per-phase device-event timings in the step stats
 
     def k_eff(self) -> int:
         return min(self.num_agents, self.top_k)

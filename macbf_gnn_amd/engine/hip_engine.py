@@ -140,7 +140,9 @@ class HipEngine:
         cfg = tr.cfg
         B, N, K = self.B, self.N, self.K
         pw = self.pw
+        tm = tr.timer
         T = self.rollout(s0, g)
+        tm.mark("rollout")
         # validity: step t of env b counts iff the env was not done before t
         done = (self.dist[:T] / N) < C.DIST_MIN_CHECK                 # (T, B)
         di = done.to(torch.int32)
@@ -162,6 +164,7 @@ class HipEngine:
         dh = self.dh[: 2 * E].view(2, T, B, N, K)
         native.cbf_fwd(S, idx, pw.cbf_w, pw.cbf_off["w1f"], pw.cbf_v, dang=self.dang[:T], valid=valid_u8, two=True,
                        dh_out=dh, counts=self.counts, partial=part_fwd, num_blocks=nbf)
+        tm.mark("cbf_loss")
         # ---- CBF backward (both paths) -> per-edge feature grads + dW slabs
         nbb = native.cbf_bwd_grid(2 * E, self.dev)
         part_cbf = self._buf(self._part_cbf, nbb, native.CBF_PARTIAL)
@@ -172,6 +175,7 @@ class HipEngine:
         redges = self.redges[: T * B]
         native.rev_csr(idx.view(T * B, N, K), rptr, redges)
         native.node_reduce(dE, rptr, redges, self.dS, T=T, B=B, N=N, K=K, passes=2)
+        tm.mark("cbf_backward")
         # ---- BPTT through the rollout
         self.part_node.zero_()
         self.part_edge.zero_()
@@ -187,6 +191,7 @@ class HipEngine:
             native.ctrl_edge_bwd(self.S[t], self.idx[t], self.argmax[t], self.dP, pw.ctrl_w, pw.ctrl_off["ew1f"],
                                  pw.ctrl_off["ew2tn"], self.dEc, self.part_edge, self.nb_edge)
             native.node_combine(self.dS[t], self.ego, self.dEc, rptr3[t], redges3[t], self.Gb[t + 1], self.Gb[t], K=K)
+        tm.mark("bptt")
         # ---- weight-gradient slabs -> flat grad
         fg = tr.fp.grad
         fg.zero_()
@@ -195,6 +200,7 @@ class HipEngine:
             native.reduce_rows(part, red)
             src, dst = self.maps[name]
             fg.index_add_(0, dst, red.index_select(0, src))
+        tm.mark("grad_reduce")
         # ---- stats (device tensors; converted lazily by the logger)
         sums = part_fwd.to(torch.float64).sum(0)
         nd = 1e-5 + self.counts[0].double()

@@ -30,6 +30,7 @@ class OracleEngine:
                               bptt=cfg.bptt, early_stop=cfg.early_stop,
                               noise_prob=cfg.add_noise_prob, noise_scale=cfg.noise_scale,
                               generator=tr.torch_gen, compute_safety=cfg.compute_safety)
+        tr.timer.mark("rollout")
         T = traj["A"].shape[1]
         valid = traj["valid"]
         dang = oracle.ttc_mask_knn(traj["S"][:, :T].detach(), traj["idx"])
@@ -41,9 +42,11 @@ class OracleEngine:
         ncounts = {"n_dang": float(counts[0]), "n_safe": float(counts[1]), "n_act": float(counts[2])}
         losses, sums, act_sum = oracle.train_losses(cp, bp, traj, g, n_counts=ncounts,
                                                     reuse_nbr_idx=cfg.reuse_nbr_idx, top_k=cfg.top_k)
+        tr.timer.mark("losses")
         tr.fp.zero_grad()
         losses["total"].backward()
         tr.fp.sync_grads_from_modules()
+        tr.timer.mark("backward")
         agent_steps = int(valid.sum().item()) * N
         safe = float((traj["safe"].to(torch.float64) * valid).sum().item()) if "safe" in traj else 0.0
         stats = {

@@ -26,6 +26,7 @@ from ..models import CBF, Controller
 from ..parallel import DP
 from ..utils.params import FlatParams, FlatAdam
 from ..utils.metrics import MetricsLogger
+from ..utils.timing import PhaseTimer
 from ..utils import ckpt
 
 
@@ -61,6 +62,8 @@ class Trainer:
         self.torch_gen = torch.Generator(device=self.device)
         self.torch_gen.manual_seed(cfg.seed * 1000003 + dp.rank)
         self.logger = MetricsLogger(dp, cfg.log_path)
+        self.timer = PhaseTimer(self.device, enabled=cfg.phase_timing)
+        self.skipped_steps = 0
         if self.device.type == "cuda":
             from .hip_engine import HipEngine
             self.engine = HipEngine(self)
@@ -94,15 +97,31 @@ class Trainer:
         return ["controller"] if (self.step_count // k) % 2 == 0 else ["cbf"]
 
     def train_step(self, s0=None, g=None):
+        tm = self.timer
+        tm.start()
         if s0 is None:
             s0, g = self.sample()
         s0 = s0.to(self.device)
         g = g.to(self.device)
+        tm.mark("sample")
         stats = self.engine.step(s0, g)
         self.dp.all_reduce_(self.fp.grad)
-        self.opt.step(self.groups_to_step())
-        self.engine.after_update()
+        tm.mark("allreduce")
+        # failure detection: a non-finite reduced gradient is identical on every
+        # rank, so every rank skips the same step; parameters and Adam state stay untouched
+        if self.cfg.nan_guard and not bool(torch.isfinite(self.fp.grad).all()):
+            self.skipped_steps += 1
+            stats["skipped"] = 1
+            if self.dp.rank == 0:
+                print(f"[macbf] step {self.step_count}: non-finite gradient, optimizer step skipped "
+                      f"({self.skipped_steps} so far)", flush=True)
+        else:
+            self.opt.step(self.groups_to_step())
+            self.engine.after_update()
+        tm.mark("optimizer")
         self.step_count += 1
+        if tm.enabled:
+            stats["phases_ms"] = tm.results()
         return stats
 
     def fit(self, steps: Optional[int] = None, progress: bool = False):

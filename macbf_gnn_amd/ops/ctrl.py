@@ -1,0 +1,84 @@
+"""GNN controller forward/backward on the HIP device as a ``torch.autograd.Function``.
+
+Used by ``models.Controller.forward`` on gfx950 (reference ``controller.py:31-63``).
+Forward: ``ctrl_fwd`` (edge MLP + masked max-pool with saved argmax slots + node MLP + gain
+law), no Euler step. Backward: ``ctrl_node_bwd`` (node MLP + gain law; the upstream dL/da is
+fed as the velocity adjoint of s_{t+1} = s_t + dt [v, a], i.e. G = (0, 0, dL/da / dt)),
+``ctrl_edge_bwd`` (max-pool routing via argmax, edge MLP), ``node_combine`` (edge -> node,
+reverse CSR, no Euler term) and the slab reductions for the parameter gradients.
+"""
+from __future__ import annotations
+
+import torch
+
+from .. import config as C
+from . import graph, native
+from .packing import module_pack
+
+
+class _CtrlFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, s, g, idx, mp, *params):
+        B, N, K = idx.shape
+        dev = s.device
+        w, v, rm = mp.pack(params)
+        S = s.detach().float().contiguous()
+        G = g.detach().float().contiguous()
+        A = torch.empty(B, N, 2, dtype=torch.float32, device=dev)
+        pooled = torch.empty(B, N, 128, dtype=torch.bfloat16, device=dev)
+        am = torch.empty(B, N, 128, dtype=torch.uint8, device=dev)
+        native.ctrl_fwd(S, G, idx, w, mp.off["ew1f"], mp.off["nw1f"], v, A, None, None, None,
+                        pooled=pooled, argmax=am)
+        ctx.mp = mp
+        ctx.packed = (w, v, rm)
+        ctx.save_for_backward(S, G, idx, A, pooled, am)
+        return A
+
+    @staticmethod
+    def backward(ctx, gA):
+        S, G, idx, A, pooled, am = ctx.saved_tensors
+        mp = ctx.mp
+        w, v, rm = ctx.packed
+        B, N, K = idx.shape
+        dev = S.device
+        Gn = torch.zeros(B, N, 4, dtype=torch.float32, device=dev)
+        Gn[..., 2:] = gA.float() / C.TIME_STEP
+        nbn, nbe = native.ctrl_bwd_grids(B * N, dev)
+        # the controller kernels accumulate into their slabs (BPTT sums over steps): start at 0
+        pn = torch.zeros(nbn, native.CTRL_NODE_PARTIAL, dtype=torch.float32, device=dev)
+        pe = torch.zeros(nbe, native.CTRL_EDGE_PARTIAL, dtype=torch.float32, device=dev)
+        dP = torch.empty(B, N, 128, dtype=torch.bfloat16, device=dev)
+        ego = torch.empty(B, N, 4, dtype=torch.float32, device=dev)
+        dEc = torch.empty(B, N, K, 4, dtype=torch.float32, device=dev)
+        native.ctrl_node_bwd(pooled, S, G, A, Gn, None, rm, mp.rm_off, v, 0.0, dP, ego, pn, nbn)
+        native.ctrl_edge_bwd(S, idx, am, dP, w, mp.off["ew1f"], mp.off["ew2tn"], dEc, pe, nbe)
+        gs = gg = None
+        if ctx.needs_input_grad[0]:
+            rptr = torch.empty(B, N + 1, dtype=torch.int32, device=dev)
+            red_e = torch.empty(B, N * K, dtype=torch.int32, device=dev)
+            native.rev_csr(idx, rptr, red_e)
+            gs = torch.empty(B, N, 4, dtype=torch.float32, device=dev)
+            native.node_combine(torch.zeros(B, N, 4, device=dev), ego, dEc, rptr, red_e, None, gs, K=K)
+        rn = torch.empty(native.CTRL_NODE_PARTIAL, dtype=torch.float32, device=dev)
+        re = torch.empty(native.CTRL_EDGE_PARTIAL, dtype=torch.float32, device=dev)
+        native.reduce_rows(pn, rn)
+        native.reduce_rows(pe, re)
+        pgrads = mp.unpack_grads({"node": rn, "edge": re})
+        return (gs, gg, None, None, *pgrads)
+
+
+def controller_apply(module, s: torch.Tensor, g: torch.Tensor, idx: torch.Tensor | None,
+                     top_k: int = C.TOP_K) -> torch.Tensor:
+    """s (B, N, 4), g (B, N, 2) on the HIP device -> a (B, N, 2); differentiable in s and in the
+    module's parameters (goals are treated as constants)."""
+    lead = s.shape[:-2]
+    N = s.shape[-2]
+    s3 = s.reshape(-1, N, 4)
+    g3 = g.reshape(-1, N, 2)
+    if idx is None:
+        idx3 = graph.knn(s3, top_k)
+    else:
+        idx3 = idx.reshape(-1, N, idx.shape[-1]).to(torch.int32).contiguous()
+    mp = module_pack("ctrl", module, s.device)
+    a = _CtrlFn.apply(s3.float(), g3.float(), idx3, mp, *module.parameters())
+    return a.reshape(*lead, N, 2)

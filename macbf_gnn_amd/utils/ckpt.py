@@ -75,3 +75,20 @@ def _load_module(mod, sd, strict):
         for k, p in own.items():
             if k in sd:
                 p.copy_(sd[k].to(p.dtype).reshape(p.shape))
+
+
+def load_models(path: str, controller, cbf, strict: bool = True):
+    """Load only the network weights of a checkpoint (any format ``load`` accepts) into bare
+    modules, e.g. for evaluation without a trainer."""
+    ck = torch.load(path, map_location="cpu", weights_only=True)
+    if "controller" in ck or "cbf" in ck:
+        if "controller" in ck and controller is not None:
+            _load_module(controller, ck["controller"], strict)
+        if "cbf" in ck and cbf is not None:
+            _load_module(cbf, ck["cbf"], strict)
+        return
+    keys = list(ck.keys())
+    if any(k.startswith("controller_") for k in keys) and controller is not None:
+        _load_module(controller, ck, strict)
+    elif any(k.startswith("cbf_net") for k in keys) and cbf is not None:
+        _load_module(cbf, ck, strict)

@@ -10,7 +10,7 @@ echo "pytest rc=$rc" >> gpurun_out/${TAG}_tests.log
 tail -8 gpurun_out/${TAG}_tests.log
 # 0 = pass, 1 = test failures: the GPU is healthy, continue. Anything else (crash/timeout): stop.
 if [ $rc -gt 1 ]; then exit $rc; fi
-timeout -k 10 600 python bench.py --steps 5 --warmup 2 > gpurun_out/${TAG}_bench.log 2>&1
+timeout -k 10 600 python bench.py --steps 5 --warmup 2 --phases > gpurun_out/${TAG}_bench.log 2>&1
 rc=$?
 echo "bench rc=$rc" >> gpurun_out/${TAG}_bench.log
 tail -2 gpurun_out/${TAG}_bench.log

@@ -100,3 +100,31 @@ def test_alternating_updates_only_touch_one_network():
     c1 = torch.cat([p.detach().reshape(-1) for p in t.controller.parameters()])
     b1 = torch.cat([p.detach().reshape(-1) for p in t.cbf.parameters()])
     assert not torch.equal(c0, c1) and torch.equal(b0, b1)
+
+
+def test_nan_guard_skips_optimizer_step():
+    t = _tr()
+    s, g = E.generate_batch(1, 8, seed=2)
+    before = t.fp.flat.clone()
+    real_step = t.engine.step
+
+    def poisoned(s0, g0):
+        st = real_step(s0, g0)
+        t.fp.grad[3] = float("nan")
+        return st
+
+    t.engine.step = poisoned
+    st = t.train_step(s, g)
+    assert st.get("skipped") == 1 and t.skipped_steps == 1
+    assert torch.equal(before, t.fp.flat)
+    t.engine.step = real_step
+    t.train_step(s, g)
+    assert not torch.equal(before, t.fp.flat)
+
+
+def test_phase_timing_reports_phases():
+    t = _tr(phase_timing=True)
+    st = t.train_step(*E.generate_batch(1, 8, seed=4))
+    ph = st["phases_ms"]
+    for k in ("sample", "rollout", "losses", "backward", "allreduce", "optimizer"):
+        assert k in ph and ph[k] >= 0.0
