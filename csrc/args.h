@@ -89,6 +89,14 @@ struct CbfBwdArgs {
   float4* dE;                              // (passes, E) dL/d(s_i - s_j) per evaluation, or null
   float* partial;                          // (gridDim.x, CBF_PARTIAL) per-workgroup dW slabs
   float obs_r, dist_thr, dist_eps;
+  // fused training mode (passes == 2): dh is computed in-kernel from h(s_t), h'(s_{t+1}) of the
+  // same edge, the danger bit, env-step validity and the global pooled counts; the 10 loss
+  // partial sums go to the slab at P_LOSS (dh is then not read)
+  int fused;
+  const uint8_t* dang;                     // (T,B,N,K)
+  const uint8_t* valid;                    // (T,B) or null
+  const float* counts;                     // [n_dang, n_safe] global
+  LossConsts lc;
 };
 
 struct CtrlNodeBwdArgs {

@@ -76,8 +76,14 @@ static int cbf_fwd(u64 S, long s_env, long s_step, u64 idx, u64 dang, u64 valid,
 
 static int cbf_bwd(u64 S, long s_env, long s_step, u64 idx, int B, int T, int N, int K, int passes, u64 dh,
                    u64 wpack, int f_bwd, u64 wrm, u64 wvec, u64 dE, u64 partial, float obs_r, float dist_thr,
-                   float dist_eps, int num_blocks, u64 stream) {
+                   float dist_eps, int fused, u64 dang, u64 valid, u64 counts, py::tuple lc, int num_blocks,
+                   u64 stream) {
   mb::CbfBwdArgs a{};
+  a.fused = fused; a.dang = P<const uint8_t>(dang); a.valid = P<const uint8_t>(valid);
+  a.counts = P<const float>(counts);
+  a.lc.eps_dang = lc[0].cast<float>(); a.lc.dt_alpha = lc[1].cast<float>(); a.lc.w_dang = lc[2].cast<float>();
+  a.lc.w_safe = lc[3].cast<float>(); a.lc.w_dang_d = lc[4].cast<float>(); a.lc.w_safe_d = lc[5].cast<float>();
+  a.lc.scale = lc[6].cast<float>();
   a.S = P<const float4>(S); a.s_env = s_env; a.s_step = s_step; a.idx = P<const int>(idx);
   a.B = B; a.T = T; a.N = N; a.K = K; a.passes = passes; a.dh = P<const float>(dh);
   a.wpack = P<const bf16>(wpack); a.f_bwd = f_bwd; a.wrm = P<const bf16>(wrm); a.wvec = P<const float>(wvec);

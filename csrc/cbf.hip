@@ -224,17 +224,22 @@ extern "C" int mb_cbf_fwd(const mb::CbfFwdArgs* a, int num_blocks, hipStream_t s
 }
 
 // ---------------------------------------------------------------------------------------
-// cbf_bwd_kernel: hand-written backward of the CBF edge MLP for `passes`*E evaluations.
-// Workgroup = 4 waves sharing a 128-evaluation chunk (32 per wave):
+// cbf_bwd_kernel<FUSED>: hand-written backward of the CBF edge MLP.
+// Workgroup = 4 waves sharing a chunk of 128 evaluations (32 per wave):
 //   data path (per wave, registers only): recompute H1,H2,H3 -> dH3 = w4*dh*relu'
 //     -> dH2 = W3^T dH3 .relu' (16 MFMA) -> dH1 = W2^T dH2 .relu' (16) -> dF = W1^T dH1 (4)
 //     -> dL/d(s_i - s_j) incl. the |dp|_eps feature; written per evaluation (self edges 0)
 //   weight gradients (workgroup-shared): activations / deltas of the chunk are staged as
 //     edge-major bf16 LDS images; each wave owns a fixed subset of the 32x32 output tiles of
 //     dW3 (64x128), dW2 (128x64), dW1f (64x32) and contracts over the chunk's 128 edges with
-//     ds_read_b64_tr_b16 fragments -> MFMA; bias grads are row sums of the A fragments; the
-//     64->1 head (w4, b4) accumulates per lane. Fixed ownership -> deterministic per-WG slabs,
-//     reduced by a separate deterministic pass (no float atomics).
+//     ds_read_b64_tr_b16 fragments -> MFMA; bias grads are row sums of the A fragments, split
+//     over the waves that read the same row block; the 64->1 head (w4, b4) accumulates per
+//     lane. Fixed ownership -> deterministic per-WG slabs, reduced by a separate pass.
+// FUSED (training): the chunk is 64 edges x {h(s_t) (waves 0,1), h'(s_{t+1}) (waves 2,3)}. The
+//   forward recompute includes the 64->1 head; h and h' of each edge meet in LDS, every wave
+//   forms its upstream dL/dh locally (barrier + derivative hinge losses with the danger bit,
+//   step validity and the global pooled counts) and the loss partial sums go to the slab. This
+//   replaces the separate forward/loss kernel and the dh round trip through HBM.
 // ---------------------------------------------------------------------------------------
 namespace mb {
 
@@ -244,7 +249,8 @@ constexpr int SA128 = 136, SA64 = 72, SA32 = 40;
 constexpr int RM_W2 = 128 * 72, RM_W3 = 64 * 136;   // row-major image sizes (elements)
 // per-WG partial slab layout (floats)
 constexpr int P_W3 = 0, P_B3 = 8192, P_W2 = 8256, P_B2 = 16448, P_W1 = 16576, P_W4 = 18624, P_B4 = 18688;
-constexpr int CBF_PARTIAL = 18696;
+constexpr int P_LOSS = 18692;                 // 10 loss partial sums (fused mode)
+constexpr int CBF_PARTIAL = 18704;
 // stage A/B: (128 + 64)-wide images; stage C+D: dH1|F|dh|relu(H3) = 64+32+32+64 wide
 constexpr size_t CBF_STAGE_BYTES = (size_t)(SA64 + SA32 + SA32 + SA64) * CBF_CH * 2;
 constexpr size_t CBF_BWD_W_BYTES = (size_t)(RM_W2 + RM_W3) * 2 + 6 * FRAG_BYTES;
@@ -253,19 +259,41 @@ size_t cbf_bwd_lds() { return CBF_BWD_W_BYTES + CBF_VEC * 4 + CBF_STAGE_BYTES; }
 
 struct CbfIn {
   EdgeCtx c;
-  float dh;
+  float dh;       // upstream gradient (non-fused)
   bool in;
+  bool dg, vld;   // fused: danger bit, env-step validity
+  unsigned ev;    // evaluation index (pass*E + e)
 };
 
+template <bool FUSED>
 DEV void cbf_load(const CbfBwdArgs& a, long chunk, int wave, int r, long E, long EV, CbfIn& x) {
-  const unsigned ev = (unsigned)chunk * CBF_CH + wave * 32 + r;
-  x.in = ev < (unsigned)EV;
-  const int pass = (x.in && ev >= (unsigned)E) ? 1 : 0;
-  const unsigned e = ev - (unsigned)pass * (unsigned)E;
+  int pass;
+  unsigned e;
+  if constexpr (FUSED) {
+    pass = wave >> 1;
+    e = (unsigned)chunk * (CBF_CH / 2) + (wave & 1) * 32 + r;
+    x.in = e < (unsigned)E;
+    x.ev = (unsigned)pass * (unsigned)E + e;
+  } else {
+    const unsigned ev = (unsigned)chunk * CBF_CH + wave * 32 + r;
+    x.in = ev < (unsigned)EV;
+    pass = (x.in && ev >= (unsigned)E) ? 1 : 0;
+    e = ev - (unsigned)pass * (unsigned)E;
+    x.ev = ev;
+  }
   cbf_edge(a.S, a.s_env, a.s_step, a.idx, a.B, a.N, a.K, e, x.in ? E : 0, pass, a.obs_r, a.dist_thr, a.dist_eps, x.c);
-  x.dh = x.in ? a.dh[ev] : 0.f;
+  if constexpr (FUSED) {
+    x.dh = 0.f;
+    x.dg = x.in && a.dang[e] != 0;
+    x.vld = x.in && (a.valid ? (a.valid[(unsigned)x.c.t * (unsigned)a.B + (unsigned)x.c.b] != 0) : true);
+  } else {
+    x.dh = x.in ? a.dh[x.ev] : 0.f;
+    x.dg = false;
+    x.vld = false;
+  }
 }
 
+template <bool FUSED>
 __global__ __launch_bounds__(CBF_BWD_WAVES * 64, 1) void cbf_bwd_kernel(CbfBwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   bf16* W2 = reinterpret_cast<bf16*>(smem);
@@ -273,37 +301,51 @@ __global__ __launch_bounds__(CBF_BWD_WAVES * 64, 1) void cbf_bwd_kernel(CbfBwdAr
   bf16* wf = W3 + RM_W3;                       // w1f (2 frags) | w1ft (4 frags)
   float* vl = reinterpret_cast<float*>(smem + CBF_BWD_W_BYTES);
   bf16* stg = reinterpret_cast<bf16*>(smem + CBF_BWD_W_BYTES + CBF_VEC * 4);
+  __shared__ float hx[CBF_CH];                 // fused: h / h' exchange
+  __shared__ float bred[CBF_BWD_WAVES][192];   // bias partials: b3 (64) | b2 (128)
+  __shared__ float lred[CBF_BWD_WAVES][10];
+  __shared__ float red4[CBF_BWD_WAVES];
   block_copy16(W2, a.wrm, (RM_W2 + RM_W3) * 2);
   block_copy16(wf, a.wpack + (size_t)a.f_bwd * 512, 2 * FRAG_BYTES);
   block_copy16(wf + 2 * 512, a.wpack + (size_t)(a.f_bwd + 66) * 512, 4 * FRAG_BYTES);
   block_copy16(vl, a.wvec, CBF_VEC * 4);
+  for (int q = threadIdx.x; q < CBF_BWD_WAVES * 192; q += blockDim.x) (&bred[0][0])[q] = 0.f;
   __syncthreads();
   const int wave = threadIdx.x / WAVE, lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
   const long E = (long)a.B * a.T * a.N * a.K;
   const long EV = E * a.passes;
-  const long nchunks = (EV + CBF_CH - 1) / CBF_CH;
+  const long nchunks = FUSED ? (E + CBF_CH / 2 - 1) / (CBF_CH / 2) : (EV + CBF_CH - 1) / CBF_CH;
   const int erow = wave * 32 + r;
+  const int pass_w = wave >> 1;                // fused: this wave's pass
+  float nd = 1.f, ns = 1.f;
+  if constexpr (FUSED) { nd = 1e-5f + a.counts[0]; ns = 1e-5f + a.counts[1]; }
+  float lacc[10];
+#pragma unroll
+  for (int q = 0; q < 10; ++q) lacc[q] = 0.f;
   // owned weight-gradient tiles: tiles wave and wave+4 of dW3 (64x128, (t/4, t%4)) and of
   // dW2 (128x64, (t/2, t%2)); one tile of dW1f (waves 0,1) or dW4pad (waves 2,3)
   f32x16 accA[2], accB[2], accC = zero16();
   accA[0] = accA[1] = accB[0] = accB[1] = zero16();
   float bA[2] = {0.f, 0.f}, bB[2] = {0.f, 0.f}, db4 = 0.f;
+  const int bsA = 2 * wave, bsB = 4 * (wave & 1);   // bias-sum edge steps of this wave
 
   CbfIn nx;
-  if ((long)blockIdx.x < nchunks) cbf_load(a, blockIdx.x, wave, r, E, EV, nx);
+  if ((long)blockIdx.x < nchunks) cbf_load<FUSED>(a, blockIdx.x, wave, r, E, EV, nx);
   for (long chunk = blockIdx.x; chunk < nchunks; chunk += gridDim.x) {
     const CbfIn cur = nx;
-    if (chunk + gridDim.x < nchunks) cbf_load(a, chunk + gridDim.x, wave, r, E, EV, nx);   // prefetch
+    if (chunk + gridDim.x < nchunks) cbf_load<FUSED>(a, chunk + gridDim.x, wave, r, E, EV, nx);   // prefetch
     const EdgeCtx& c = cur.c;
-    const float dhv = cur.dh;
-    if (h == 0) db4 += dhv;
     const bf16x8 F = cbf_edge_frag(c.rel, c.eye, c.dfeat, c.ok, h);
+    // one opaque base per LDS image per chunk: the per-lane address math is computed once and
+    // shared by all fragment reads (immediate offsets), while the loads themselves cannot be
+    // hoisted out of the chunk loop (~100 weight VGPRs otherwise)
     const bf16* wt = wf + opaque_zero();
-    // loop-invariant LDS vectors behind an opaque offset: otherwise the compiler hoists
-    // ~128 bias/head values into registers for the whole kernel
-    const float* b2 = vl + opaque_zero();
-    const float* b3 = vl + 128 + opaque_zero();
-    const float* w4 = vl + 192 + opaque_zero();
+    const bf16* W2c = W2 + opaque_zero();
+    const bf16* W3c = W3 + opaque_zero();
+    const float* vlc = vl + opaque_zero();
+    const float* b2 = vlc;
+    const float* b3 = vlc + 128;
+    const float* w4 = vlc + 192;
     // ---- forward recompute
     bf16x16 H1b[2], H2b[4];
     f32x16 H3p[2];
@@ -315,38 +357,98 @@ __global__ __launch_bounds__(CBF_BWD_WAVES * 64, 1) void cbf_bwd_kernel(CbfBwdAr
     }
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt) {
-      f32x16 t2 = bias_rows(b2, 32 * mt, h);
+      f32x16 t2 = bias_rows4(b2, 32 * mt, h);
       static_for<4>([&](auto kk_) {
         constexpr int kk = decltype(kk_)::value;
-        t2 = mfma(wrm_acc(W2 + opaque_zero(), SA64, 32 * mt, kk, lane), bacc_frag<kk & 1>(H1b[kk >> 1]), t2);
+        t2 = mfma(wrm_acc(W2c, SA64, 32 * mt, kk, lane), bacc_frag<kk & 1>(H1b[kk >> 1]), t2);
       });
       relu_(t2);
       H2b[mt] = to_bf16x16(t2);
     }
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt) {
-      f32x16 t3 = bias_rows(b3, 32 * mt, h);
+      f32x16 t3 = bias_rows4(b3, 32 * mt, h);
       static_for<8>([&](auto kk_) {
         constexpr int kk = decltype(kk_)::value;
-        t3 = mfma(wrm_acc(W3 + opaque_zero(), SA128, 32 * mt, kk, lane), bacc_frag<kk & 1>(H2b[kk >> 1]), t3);
+        t3 = mfma(wrm_acc(W3c, SA128, 32 * mt, kk, lane), bacc_frag<kk & 1>(H2b[kk >> 1]), t3);
       });
       H3p[mt] = t3;
     }
+    float dhv = cur.dh;
+    if constexpr (FUSED) {
+      // ---- head, h/h' exchange, local loss + upstream gradient
+      float hs = 0.f;
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const float4 w = *reinterpret_cast<const float4*>(w4 + 32 * mt + 8 * g + 4 * h);
+          hs += w.x * fmaxf(H3p[mt][4 * g], 0.f) + w.y * fmaxf(H3p[mt][4 * g + 1], 0.f) +
+                w.z * fmaxf(H3p[mt][4 * g + 2], 0.f) + w.w * fmaxf(H3p[mt][4 * g + 3], 0.f);
+        }
+      hs += shfl_xor32(hs);
+      const float hm = (cur.in && c.mask) ? hs + vlc[256] : 0.f;
+      if (h == 0) hx[erow] = hm;
+      __syncthreads();
+      const float other = hx[(wave ^ 2) * 32 + r];
+      const float hv = pass_w == 0 ? hm : other;
+      const float hnv = pass_w == 0 ? other : hm;
+      float gh = 0.f, ghn = 0.f;
+      if (cur.vld) {
+        const float deriv = hnv - hv + a.lc.dt_alpha * hv;
+        const bool acc_here = (pass_w == 0) && (h == 0);
+        if (cur.dg) {
+          const float cc = a.lc.scale / nd;
+          const float ind_b = (hv + a.lc.eps_dang > 0.f) ? 1.f : 0.f;
+          const float ind_d = (-deriv + a.lc.eps_dang > 0.f) ? 1.f : 0.f;
+          gh = cc * (a.lc.w_dang * ind_b + a.lc.w_dang_d * ind_d * (1.f - a.lc.dt_alpha));
+          ghn = -cc * a.lc.w_dang_d * ind_d;
+          if (acc_here) {
+            lacc[0] += 1.f;
+            lacc[2] += fmaxf(hv + a.lc.eps_dang, 0.f);
+            lacc[4] += (hv <= 0.f) ? 1.f : 0.f;
+            lacc[6] += fmaxf(-deriv + a.lc.eps_dang, 0.f);
+            lacc[8] += (deriv >= 0.f) ? 1.f : 0.f;
+          }
+        } else {
+          const float cc = a.lc.scale / ns;
+          const float ind_b = (-hv > 0.f) ? 1.f : 0.f;
+          const float ind_d = (-deriv > 0.f) ? 1.f : 0.f;
+          gh = cc * (-a.lc.w_safe * ind_b + a.lc.w_safe_d * ind_d * (1.f - a.lc.dt_alpha));
+          ghn = -cc * a.lc.w_safe_d * ind_d;
+          if (acc_here) {
+            lacc[1] += 1.f;
+            lacc[3] += fmaxf(-hv, 0.f);
+            lacc[5] += (hv > 0.f) ? 1.f : 0.f;
+            lacc[7] += fmaxf(-deriv, 0.f);
+            lacc[9] += (deriv > 0.f) ? 1.f : 0.f;
+          }
+        }
+      }
+      dhv = (cur.in && c.mask) ? (pass_w == 0 ? gh : ghn) : 0.f;
+    }
+    if (h == 0) db4 += dhv;
     // ---- head backward
     bf16x16 d3b[2], H3b[2];
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt) {
       f32x16 d3;
 #pragma unroll
-      for (int reg = 0; reg < 16; ++reg) {
-        const float x = H3p[mt][reg];
-        d3[reg] = x > 0.f ? w4[32 * mt + acc_row(reg, h)] * dhv : 0.f;
-        H3p[mt][reg] = fmaxf(x, 0.f);
+      for (int g = 0; g < 4; ++g) {
+        const float4 w = *reinterpret_cast<const float4*>(w4 + 32 * mt + 8 * g + 4 * h);
+        const float wv[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int reg = 4 * g + i;
+          const float x = H3p[mt][reg];
+          d3[reg] = x > 0.f ? wv[i] * dhv : 0.f;
+          H3p[mt][reg] = fmaxf(x, 0.f);
+        }
       }
       d3b[mt] = to_bf16x16(d3);
       H3b[mt] = to_bf16x16(H3p[mt]);
     }
-    // ---- stage A: dW3 (64x128) += dH3pre . H2^T ; db3   (one tile per wave)
+    // ---- stage A: dW3 (64x128) += dH3pre . H2^T ; db3   (tiles (u, wave))
     {
       bf16* imA = stg;
       bf16* imB = stg + CBF_CH * SA64;
@@ -356,10 +458,8 @@ __global__ __launch_bounds__(CBF_BWD_WAVES * 64, 1) void cbf_bwd_kernel(CbfBwdAr
       for (int mt = 0; mt < 4; ++mt) store_tile(imB, SA128, erow, 32 * mt, H2b[mt], h);
       __syncthreads();
 #pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const int t = wave + 4 * u;
-        bA[u] += stage_mma(imA, SA64, imB, SA128, t / 4, t % 4, CBF_CH / 16, lane, accA[u], t % 4 == 0);
-      }
+      for (int u = 0; u < 2; ++u)
+        bA[u] += stage_mma(imA, SA64, imB, SA128, u, wave, CBF_CH / 16, lane, accA[u], bsA, bsA + 2);
       __syncthreads();
     }
     // ---- dH2pre = (W3^T dH3pre) . relu'(H2)
@@ -369,13 +469,12 @@ __global__ __launch_bounds__(CBF_BWD_WAVES * 64, 1) void cbf_bwd_kernel(CbfBwdAr
       f32x16 t = zero16();
       static_for<4>([&](auto kk_) {
         constexpr int kk = decltype(kk_)::value;
-        t = mfma(wrmT_acc(W3 + opaque_zero(), SA128, 32 * mt, kk, lane), bacc_frag<kk & 1>(d3b[kk >> 1]), t);
+        t = mfma(wrmT_acc(W3c, SA128, 32 * mt, kk, lane), bacc_frag<kk & 1>(d3b[kk >> 1]), t);
       });
-#pragma unroll
-      for (int q = 0; q < 16; ++q) t[q] = ((float)H2b[mt][q] > 0.f) ? t[q] : 0.f;
       d2b[mt] = to_bf16x16(t);
+      mask_by_nonzero(d2b[mt], H2b[mt]);
     }
-    // ---- stage B: dW2 (128x64) += dH2pre . H1^T ; db2
+    // ---- stage B: dW2 (128x64) += dH2pre . H1^T ; db2   (tiles ((wave>>1) + 2u, wave&1))
     {
       bf16* imA = stg;
       bf16* imB = stg + CBF_CH * SA128;
@@ -385,10 +484,9 @@ __global__ __launch_bounds__(CBF_BWD_WAVES * 64, 1) void cbf_bwd_kernel(CbfBwdAr
       for (int mt = 0; mt < 2; ++mt) store_tile(imB, SA64, erow, 32 * mt, H1b[mt], h);
       __syncthreads();
 #pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const int t = wave + 4 * u;
-        bB[u] += stage_mma(imA, SA128, imB, SA64, t / 2, t % 2, CBF_CH / 16, lane, accB[u], t % 2 == 0);
-      }
+      for (int u = 0; u < 2; ++u)
+        bB[u] += stage_mma(imA, SA128, imB, SA64, (wave >> 1) + 2 * u, wave & 1, CBF_CH / 16, lane, accB[u],
+                           bsB, bsB + 4);
       __syncthreads();
     }
     // ---- dH1pre = (W2^T dH2pre) . relu'(H1)
@@ -398,11 +496,10 @@ __global__ __launch_bounds__(CBF_BWD_WAVES * 64, 1) void cbf_bwd_kernel(CbfBwdAr
       f32x16 t = zero16();
       static_for<8>([&](auto kk_) {
         constexpr int kk = decltype(kk_)::value;
-        t = mfma(wrmT_acc(W2 + opaque_zero(), SA64, 32 * mt, kk, lane), bacc_frag<kk & 1>(d2b[kk >> 1]), t);
+        t = mfma(wrmT_acc(W2c, SA64, 32 * mt, kk, lane), bacc_frag<kk & 1>(d2b[kk >> 1]), t);
       });
-#pragma unroll
-      for (int q = 0; q < 16; ++q) t[q] = ((float)H1b[mt][q] > 0.f) ? t[q] : 0.f;
       d1b[mt] = to_bf16x16(t);
+      mask_by_nonzero(d1b[mt], H1b[mt]);
     }
     // ---- dF = W1^T dH1pre (rows: dx dy dvx dvy eye dist) -> dL/d(s_i - s_j)
     {
@@ -413,13 +510,12 @@ __global__ __launch_bounds__(CBF_BWD_WAVES * 64, 1) void cbf_bwd_kernel(CbfBwdAr
       });
       const float ddist = shfl_xor32(t[1]);   // row 5 lives in lane r+32, reg 1
       if (a.dE && cur.in && h == 0) {
-        const unsigned ev = (unsigned)chunk * CBF_CH + wave * 32 + r;
         float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
         if (c.ok && c.j != c.i) {
           const float inv = 1.f / c.d;
           g = make_float4(t[0] + ddist * c.rel.x * inv, t[1] + ddist * c.rel.y * inv, t[2], t[3]);
         }
-        a.dE[ev] = g;
+        a.dE[cur.ev] = g;
       }
     }
     // ---- stage C+D: dW1f (64x32) += dH1pre . F^T (waves 0,1);
@@ -442,8 +538,8 @@ __global__ __launch_bounds__(CBF_BWD_WAVES * 64, 1) void cbf_bwd_kernel(CbfBwdAr
       *reinterpret_cast<bf16x8*>(imD + erow * SA32 + 8 * h) = dv;
       *reinterpret_cast<bf16x8*>(imD + erow * SA32 + 16 + 8 * h) = z;
       __syncthreads();
-      if (wave < 2) stage_mma(imC, SA64, imF, SA32, wave, 0, CBF_CH / 16, lane, accC, false);
-      else if (wave < 4) stage_mma(imD, SA32, imH, SA64, 0, wave - 2, CBF_CH / 16, lane, accC, false);
+      if (wave < 2) stage_mma(imC, SA64, imF, SA32, wave, 0, CBF_CH / 16, lane, accC);
+      else stage_mma(imD, SA32, imH, SA64, 0, wave - 2, CBF_CH / 16, lane, accC);
       __syncthreads();
     }
   }
@@ -452,28 +548,48 @@ __global__ __launch_bounds__(CBF_BWD_WAVES * 64, 1) void cbf_bwd_kernel(CbfBwdAr
   float* P = a.partial + (long)blockIdx.x * CBF_PARTIAL;
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
-    const int t = wave + 4 * u;
-    write_tile(P + P_W3, 128, t / 4, t % 4, accA[u], lane);
-    write_tile(P + P_W2, 64, t / 2, t % 2, accB[u], lane);
+    write_tile(P + P_W3, 128, u, wave, accA[u], lane);
+    write_tile(P + P_W2, 64, (wave >> 1) + 2 * u, wave & 1, accB[u], lane);
     const float s3 = bA[u] + shfl_xor32(bA[u]);
-    if (h == 0 && t % 4 == 0) P[P_B3 + 32 * (t / 4) + r] = s3;
     const float s2 = bB[u] + shfl_xor32(bB[u]);
-    if (h == 0 && t % 2 == 0) P[P_B2 + 32 * (t / 2) + r] = s2;
+    if (h == 0) {
+      bred[wave][32 * u + r] = s3;
+      bred[wave][64 + 32 * ((wave >> 1) + 2 * u) + r] = s2;
+    }
   }
   if (wave < 2) {
     write_tile(P + P_W1, 32, wave, 0, accC, lane);
-  } else if (wave < 4) {
+  } else {
     if (h == 0) P[P_W4 + 32 * (wave - 2) + r] = accC[0];   // dW4pad row 0 = dw4
   }
-  // db4: exact fp32 per-wave partials, summed through LDS
-  __shared__ float red4[CBF_BWD_WAVES];
+  // db4 (exact fp32) and loss sums: per-wave partials, fixed-order sums through LDS
   const float s4 = wave_sum(db4);
   if (lane == 0) red4[wave] = s4;
+  if constexpr (FUSED) {
+#pragma unroll
+    for (int q = 0; q < 10; ++q) {
+      const float v = wave_sum(lacc[q]);
+      if (lane == 0) lred[wave][q] = v;
+    }
+  }
   __syncthreads();
+  if (threadIdx.x < 192) {
+    float t = 0.f;
+    for (int w = 0; w < CBF_BWD_WAVES; ++w) t += bred[w][threadIdx.x];
+    if (threadIdx.x < 64) P[P_B3 + threadIdx.x] = t;
+    else P[P_B2 + threadIdx.x - 64] = t;
+  }
   if (threadIdx.x == 0) {
     float t4 = 0.f;
     for (int w = 0; w < CBF_BWD_WAVES; ++w) t4 += red4[w];
     P[P_B4] = t4;
+  }
+  if (threadIdx.x >= 192 && threadIdx.x < 202) {
+    const int q = threadIdx.x - 192;
+    float t = 0.f;
+    if constexpr (FUSED)
+      for (int w = 0; w < CBF_BWD_WAVES; ++w) t += lred[w][q];
+    P[P_LOSS + q] = t;
   }
 }
 
@@ -482,8 +598,14 @@ __global__ __launch_bounds__(CBF_BWD_WAVES * 64, 1) void cbf_bwd_kernel(CbfBwdAr
 extern "C" int mb_cbf_bwd(const mb::CbfBwdArgs* a, int num_blocks, hipStream_t st) {
   using namespace mb;
   if (a->K > 16 || a->K < 1 || a->passes < 1 || a->passes > 2) return -1;
+  if (a->fused && (a->passes != 2 || !a->dang || !a->counts)) return -2;
   const size_t lds = cbf_bwd_lds();
-  (void)hipFuncSetAttribute((const void*)cbf_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL(cbf_bwd_kernel, dim3(num_blocks), dim3(CBF_BWD_WAVES * 64), lds, st, *a);
+  if (a->fused) {
+    (void)hipFuncSetAttribute((const void*)cbf_bwd_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(cbf_bwd_kernel<true>, dim3(num_blocks), dim3(CBF_BWD_WAVES * 64), lds, st, *a);
+  } else {
+    (void)hipFuncSetAttribute((const void*)cbf_bwd_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(cbf_bwd_kernel<false>, dim3(num_blocks), dim3(CBF_BWD_WAVES * 64), lds, st, *a);
+  }
   return (int)hipGetLastError();
 }

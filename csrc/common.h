@@ -175,21 +175,53 @@ DEV bf16x8 tr_frag(const bf16* img, int stride, int e0, int m0, int lane) {
 }
 
 // acc += A_img[rows 32mt.., k = e] . B_img[k = e, cols 32nt..] over `esteps` x 16 edges;
-// returns the row sums of A (bias gradient; per lane: row 32mt + r over half h) if `bsum`
+// returns the row sums of A over the edge steps [bs_lo, bs_hi) (bias gradient partial; per
+// lane: row 32mt + r over half h). Callers split the steps between the waves that read the
+// same row block, so the VALU cost of the bias sums is spread evenly.
 DEV float stage_mma(const bf16* imgA, int sA, const bf16* imgB, int sB, int mt, int nt, int esteps, int lane,
-                    f32x16& acc, bool bsum) {
+                    f32x16& acc, int bs_lo = 0, int bs_hi = 0) {
   float s = 0.f;
 #pragma unroll 2
   for (int ks = 0; ks < esteps; ++ks) {
     const bf16x8 a = tr_frag(imgA, sA, 16 * ks, 32 * mt, lane);
     const bf16x8 b = tr_frag(imgB, sB, 16 * ks, 32 * nt, lane);
     acc = mfma(a, b, acc);
-    if (bsum) {
+    if (ks >= bs_lo && ks < bs_hi) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) s += (float)a[j];
     }
   }
   return s;
+}
+
+// accumulator init with bias rows, 4 x 16-byte loads (rows acc_row(4g..4g+3, h) are contiguous)
+DEV f32x16 bias_rows4(const float* b, int row0, int h) {
+  f32x16 c;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const float4 v = *reinterpret_cast<const float4*>(b + row0 + 8 * g + 4 * h);
+    c[4 * g] = v.x; c[4 * g + 1] = v.y; c[4 * g + 2] = v.z; c[4 * g + 3] = v.w;
+  }
+  return c;
+}
+
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x8 __attribute__((ext_vector_type(8)));
+
+// d *= relu'(pre) given the bf16 post-activation H = relu(pre) (>= +0): per 16-bit element,
+// mask = 0 - min(H, 1) (0xFFFF where H != 0) with packed u16 ops -> 3 ops per element pair
+DEV void mask_by_nonzero(bf16x16& d, const bf16x16& H) {
+  u32x8 dv = __builtin_bit_cast(u32x8, d);
+  const u32x8 hv = __builtin_bit_cast(u32x8, H);
+#pragma unroll
+  for (int p = 0; p < 8; ++p) {
+    const u16x2 x = __builtin_bit_cast(u16x2, hv[p]);
+    const u16x2 one = {1, 1};
+    const u16x2 zero = {0, 0};
+    const u16x2 m = zero - __builtin_elementwise_min(x, one);
+    dv[p] &= __builtin_bit_cast(unsigned int, m);
+  }
+  d = __builtin_bit_cast(bf16x16, dv);
 }
 
 // write an owned dW tile (rows 32mt.., cols 32nt..) of a row-major (ncols) fp32 slab

@@ -9,9 +9,9 @@ rollout, t = 0.. (stops when every env is done; per-env done masks)
                       per-env goal distance / action-loss sums
 losses
     counts all-reduced over DP ranks (global pooled normalisation)
-    cbf_fwd        -> h(s_t), h'(s_{t+1}) on the same slots, loss sums, dL/dh, dL/dh'
 backward
-    cbf_bwd        -> dL/d(s_i - s_j) per edge (h and h' paths) + CBF dW slabs
+    cbf_bwd (fused) -> h(s_t), h'(s_{t+1}) on the same slots, loss sums, dL/dh, dL/dh' formed
+                      in-kernel, dL/d(s_i - s_j) per edge (h and h' paths) + CBF dW slabs
     rev_csr + node_reduce -> direct dL/ds_t (edge -> node, deterministic, no atomics)
     for t = T-1..0 (BPTT):  ctrl_node_bwd -> ctrl_edge_bwd -> node_combine
                       (dA_t = dt*G_{t+1}[v] + action-loss grad; G_t = dL/ds_t)
@@ -68,7 +68,6 @@ class HipEngine:
         self.act = torch.zeros(T, B, dtype=f32, device=dev)
         self.pooled = torch.zeros(T, B, N, 128, dtype=bf, device=dev)
         self.argmax = torch.zeros(T, B, N, 128, dtype=u8, device=dev)
-        self.dh = torch.zeros(2 * T * B * N * K, dtype=f32, device=dev)
         self.dE = torch.zeros(2 * T * B * N * K * 4, dtype=f32, device=dev)
         self.rptr = torch.zeros(T * B, N + 1, dtype=i32, device=dev)
         self.redges = torch.zeros(T * B, N * K, dtype=i32, device=dev)
@@ -86,7 +85,6 @@ class HipEngine:
         self.red_edge = torch.zeros(native.CTRL_EDGE_PARTIAL, dtype=f32, device=dev)
         self.host_dist = torch.zeros(T, B, dtype=f32, pin_memory=True)
         self._part_cbf = {}
-        self._part_fwd = {}
 
     def after_update(self):
         self.pw.update()
@@ -156,26 +154,21 @@ class HipEngine:
         tr.dp.all_reduce_(self.counts)
         n_act = self.counts[2].clamp_min(1.0)
         E = T * B * N * K
-        # ---- CBF forward: h, h', loss sums, upstream grads
+        # ---- CBF: h, h', hinge losses, upstream grads and the full backward in ONE kernel
         S = self.S[: T + 1]
         idx = self.idx[:T]
-        nbf = native.cbf_fwd_grid(E, self.dev)
-        part_fwd = self._buf(self._part_fwd, nbf, 10)
-        dh = self.dh[: 2 * E].view(2, T, B, N, K)
-        native.cbf_fwd(S, idx, pw.cbf_w, pw.cbf_off["w1f"], pw.cbf_v, dang=self.dang[:T], valid=valid_u8, two=True,
-                       dh_out=dh, counts=self.counts, partial=part_fwd, num_blocks=nbf)
-        tm.mark("cbf_loss")
-        # ---- CBF backward (both paths) -> per-edge feature grads + dW slabs
+        tm.mark("counts")
         nbb = native.cbf_bwd_grid(2 * E, self.dev)
         part_cbf = self._buf(self._part_cbf, nbb, native.CBF_PARTIAL)
         dE = self.dE[: 2 * E * 4].view(2, T, B, N, K, 4)
-        native.cbf_bwd(S, idx, dh, pw.cbf_w, pw.cbf_off["w1f"], pw.cbf_rm, pw.cbf_v, passes=2, dE=dE, partial=part_cbf,
-                       num_blocks=nbb)
+        native.cbf_bwd(S, idx, None, pw.cbf_w, pw.cbf_off["w1f"], pw.cbf_rm, pw.cbf_v, passes=2, dE=dE,
+                       partial=part_cbf, num_blocks=nbb, fused=True, dang=self.dang[:T], valid=valid_u8,
+                       counts=self.counts)
         rptr = self.rptr[: T * B]
         redges = self.redges[: T * B]
         native.rev_csr(idx.view(T * B, N, K), rptr, redges)
         native.node_reduce(dE, rptr, redges, self.dS, T=T, B=B, N=N, K=K, passes=2)
-        tm.mark("cbf_backward")
+        tm.mark("cbf")
         # ---- BPTT through the rollout
         self.part_node.zero_()
         self.part_edge.zero_()
@@ -202,7 +195,7 @@ class HipEngine:
             fg.index_add_(0, dst, red.index_select(0, src))
         tm.mark("grad_reduce")
         # ---- stats (device tensors; converted lazily by the logger)
-        sums = part_fwd.to(torch.float64).sum(0)
+        sums = self.red_cbf[native.CBF_P_LOSS: native.CBF_P_LOSS + 10].to(torch.float64)
         nd = 1e-5 + self.counts[0].double()
         ns = 1e-5 + self.counts[1].double()
         act_sum = (self.act[:T].double() * valid.double()).sum()

@@ -200,7 +200,8 @@ def ctrl_fwd(S, G, idx, wpack, f_edge, f_node, wvec, A, Sn, dist_sum, act_sum, n
 LOSS_CONSTS = (C.LOSS_EPS_DANG, C.TIME_STEP * C.ALPHA_CBF, C.LOSS_WEIGHTS[0], C.LOSS_WEIGHTS[1],
                C.LOSS_WEIGHTS[2], C.LOSS_WEIGHTS[3], C.LOSS_SCALE)
 CBF_FWD_WAVES = 4
-CBF_PARTIAL = 18696
+CBF_PARTIAL = 18704
+CBF_P_LOSS = 18692          # 10 loss partial sums in the CBF slab (fused mode)
 CTRL_NODE_PARTIAL = 28896
 CTRL_EDGE_PARTIAL = 10368
 
@@ -246,12 +247,26 @@ def cbf_bwd_grid(EV: int, device) -> int:
     return max(1, min((EV + 127) // 128, num_cu(device)))
 
 
-def cbf_bwd(S, idx, dh, wpack, f_bwd, wrm, wvec, *, passes=2, dE=None, partial=None, num_blocks=None):
-    """dh (passes, T, B, N, K) -> dE (passes, T, B, N, K, 4), per-WG dW slabs (nb, CBF_PARTIAL)."""
+def cbf_bwd(S, idx, dh, wpack, f_bwd, wrm, wvec, *, passes=2, dE=None, partial=None, num_blocks=None,
+            fused=False, dang=None, valid=None, counts=None):
+    """dh (passes, T, B, N, K) -> dE (passes, T, B, N, K, 4), per-WG dW slabs (nb, CBF_PARTIAL).
+
+    fused=True (training, passes=2): dh is not read; the kernel evaluates h and h' of every
+    edge, forms the hinge-loss upstream gradients from dang (T,B,N,K), valid (T,B) and the
+    global counts [n_dang, n_safe], and writes the 10 loss partial sums at CBF_P_LOSS."""
     T, B, N, K = idx.shape
     check(idx, torch.int32, None, "idx")
     _time_major_S(S, T, B, N, passes - 1)
-    check(dh, torch.float32, (passes, T, B, N, K), "dh")
+    if fused:
+        if passes != 2:
+            raise NativeError("fused CBF backward needs passes=2")
+        check(dang, torch.uint8, (T, B, N, K), "dang")
+        check(valid, torch.uint8, (T, B), "valid")
+        check(counts, torch.float32, None, "counts")
+        if dang is None or counts is None or counts.numel() < 2:
+            raise NativeError("fused CBF backward needs dang and counts")
+    else:
+        check(dh, torch.float32, (passes, T, B, N, K), "dh")
     check(dE, torch.float32, (passes, T, B, N, K, 4), "dE")
     check(wpack, torch.bfloat16, None, "wpack")
     check(wvec, torch.float32, None, "wvec")
@@ -263,9 +278,11 @@ def cbf_bwd(S, idx, dh, wpack, f_bwd, wrm, wvec, *, passes=2, dE=None, partial=N
         raise NativeError("too many edge evaluations for 32-bit indexing")
     nb = num_blocks or cbf_bwd_grid(E * passes, S.device)
     check(partial, torch.float32, (nb, CBF_PARTIAL), "partial")
-    rc = lib().cbf_bwd(ptr(S), S.stride(1) // 4, S.stride(0) // 4, ptr(idx), B, T, N, K, int(passes), ptr(dh),
+    rc = lib().cbf_bwd(ptr(S), S.stride(1) // 4, S.stride(0) // 4, ptr(idx), B, T, N, K, int(passes),
+                       0 if fused else ptr(dh),
                        ptr(wpack), int(f_bwd), ptr(wrm), ptr(wvec), ptr(dE), ptr(partial), float(C.OBS_RADIUS),
-                       float(C.DIST_MIN_THRES), float(C.CBF_DIST_EPS), nb, stream_handle())
+                       float(C.DIST_MIN_THRES), float(C.CBF_DIST_EPS), int(fused), ptr(dang) if fused else 0,
+                       ptr(valid) if fused else 0, ptr(counts) if fused else 0, LOSS_CONSTS, nb, stream_handle())
     _ok(rc, "cbf_bwd")
     return nb
 

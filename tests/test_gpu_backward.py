@@ -197,3 +197,45 @@ def test_train_steps_hip():
     assert torch.isfinite(tr.fp.flat).all()
     assert not torch.equal(before, tr.fp.flat)
     assert 1 <= st["T"] <= 20
+
+
+def test_fused_cbf_train_kernel_matches_two_kernel_path():
+    """cbf_bwd(fused=True) == cbf_fwd (losses + dL/dh) followed by cbf_bwd(dh)."""
+    ctrl, cbf, fp, pw = _nets(5)
+    T, B, N = 3, 2, 96
+    K = C.TOP_K
+    S = _states((T + 1, B), N, seed=9, dens=0.5).contiguous()
+    idx = torch.stack([O.knn_idx(S[t], K) for t in range(T)]).to(torch.int32).contiguous()
+    dang = torch.stack([O.ttc_mask_knn(S[t], idx[t].long()) for t in range(T)]).to(torch.uint8).contiguous()
+    valid = torch.ones(T, B, dtype=torch.uint8, device=DEV)
+    valid[2, 1] = 0
+    counts = torch.tensor([float(dang.sum()), float((1 - dang).sum()), 0.0], device=DEV)
+    E = T * B * N * K
+    # two-kernel reference
+    nbf = native.cbf_fwd_grid(E, DEV)
+    pf = torch.zeros(nbf, 10, device=DEV)
+    dh = torch.zeros(2, T, B, N, K, device=DEV)
+    native.cbf_fwd(S, idx, pw.cbf_w, pw.cbf_off["w1f"], pw.cbf_v, dang=dang, valid=valid, two=True, dh_out=dh,
+                   counts=counts, partial=pf, num_blocks=nbf)
+    nb = native.cbf_bwd_grid(2 * E, DEV)
+    p1 = torch.zeros(nb, native.CBF_PARTIAL, device=DEV)
+    dE1 = torch.zeros(2, T, B, N, K, 4, device=DEV)
+    native.cbf_bwd(S, idx, dh, pw.cbf_w, pw.cbf_off["w1f"], pw.cbf_rm, pw.cbf_v, passes=2, dE=dE1, partial=p1,
+                   num_blocks=nb)
+    # fused
+    p2 = torch.zeros(nb, native.CBF_PARTIAL, device=DEV)
+    dE2 = torch.zeros(2, T, B, N, K, 4, device=DEV)
+    native.cbf_bwd(S, idx, None, pw.cbf_w, pw.cbf_off["w1f"], pw.cbf_rm, pw.cbf_v, passes=2, dE=dE2, partial=p2,
+                   num_blocks=nb, fused=True, dang=dang, valid=valid, counts=counts)
+    r1 = torch.zeros(native.CBF_PARTIAL, device=DEV)
+    r2 = torch.zeros(native.CBF_PARTIAL, device=DEV)
+    native.reduce_rows(p1, r1)
+    native.reduce_rows(p2, r2)
+    torch.cuda.synchronize()
+    L = native.CBF_P_LOSS
+    ref_sums = pf.double().sum(0)
+    got = r2[L:L + 10].double()
+    assert torch.equal(got[[0, 1]], ref_sums[[0, 1]])                 # counts: exact
+    _cmp(got[2:], ref_sums[2:], "loss sums", rel=2e-2, cos=0.999)
+    _cmp(dE2, dE1, "dE", rel=5e-2, cos=0.998)
+    _cmp(r2[:L], r1[:L], "dW slab", rel=5e-2, cos=0.998)

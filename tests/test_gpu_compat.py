@@ -82,8 +82,9 @@ def test_controller_module_forward_backward(B, N):
     gr = torch.autograd.grad((aref * w).sum(), [s2] + list(p.values()))
     _cmp(a.detach(), aref.detach(), "a", rel=3e-2, cos=0.999)
     _cmp(sx.grad, gr[0], "dL/ds")
+    tol = 0.15 if B * N < 100 else 0.1
     for (k, prm), ref in zip(ctrl.named_parameters(), gr[1:]):
-        _cmp(prm.grad, ref, k)
+        _cmp(prm.grad, ref, k, rel=tol)
 
 
 def test_core_api_on_device():
