@@ -209,18 +209,21 @@ typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 typedef unsigned int u32x8 __attribute__((ext_vector_type(8)));
 
 // d *= relu'(pre) given the bf16 post-activation H = relu(pre) (>= +0): per 16-bit element,
-// mask = 0 - min(H, 1) (0xFFFF where H != 0) with packed u16 ops -> 3 ops per element pair
+// mask = 0 - min(H, 1) (0xFFFF where H != 0) with packed u16 ops, 3 ops per element pair.
+// (inline asm: the ext_vector u16x2 formulation of this was miscompiled by hipcc 7.2 into a
+// mask taken from only one register of H)
+DEV unsigned nz_mask16x2(unsigned x) {
+  unsigned m;
+  const unsigned ones = 0x00010001u, zero = 0u;
+  asm volatile("v_pk_min_u16 %0, %1, %2\n\tv_pk_sub_u16 %0, %3, %0" : "=&v"(m) : "v"(x), "v"(ones), "v"(zero));
+  return m;
+}
+
 DEV void mask_by_nonzero(bf16x16& d, const bf16x16& H) {
   u32x8 dv = __builtin_bit_cast(u32x8, d);
   const u32x8 hv = __builtin_bit_cast(u32x8, H);
 #pragma unroll
-  for (int p = 0; p < 8; ++p) {
-    const u16x2 x = __builtin_bit_cast(u16x2, hv[p]);
-    const u16x2 one = {1, 1};
-    const u16x2 zero = {0, 0};
-    const u16x2 m = zero - __builtin_elementwise_min(x, one);
-    dv[p] &= __builtin_bit_cast(unsigned int, m);
-  }
+  for (int p = 0; p < 8; ++p) dv[p] &= nz_mask16x2(hv[p]);
   d = __builtin_bit_cast(bf16x16, dv);
 }
 

@@ -506,7 +506,7 @@ __global__ __launch_bounds__(NB_WAVES * 64, 1) void ctrl_node_bwd_kernel(CtrlNod
 #pragma unroll
       for (int mt = 0; mt < 2; ++mt) store_tile(imB, 72, erow, 32 * mt, Y3b[mt], h);
       __syncthreads();
-      if (wave < 2) bs4 += stage_mma(imA, 40, imB, 72, 0, wave, NB_CH / 16, lane, acc4, wave == 0);
+      if (wave < 2) bs4 += stage_mma(imA, 40, imB, 72, 0, wave, NB_CH / 16, lane, acc4, 0, wave == 0 ? NB_CH / 16 : 0);
       __syncthreads();
     }
     // ---- dY2 = W3^T dY3 . relu'(Y2)
@@ -533,7 +533,7 @@ __global__ __launch_bounds__(NB_WAVES * 64, 1) void ctrl_node_bwd_kernel(CtrlNod
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         const int t = wave + 4 * u;
-        bs3[u] += stage_mma(imA, 72, imB, 136, t / 4, t % 4, NB_CH / 16, lane, acc3[u], t % 4 == 0);
+        bs3[u] += stage_mma(imA, 72, imB, 136, t / 4, t % 4, NB_CH / 16, lane, acc3[u], 0, t % 4 == 0 ? NB_CH / 16 : 0);
       }
       __syncthreads();
     }
@@ -561,7 +561,7 @@ __global__ __launch_bounds__(NB_WAVES * 64, 1) void ctrl_node_bwd_kernel(CtrlNod
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         const int t = wave + 4 * u;
-        bs2[u] += stage_mma(imA, 136, imB, 72, t / 2, t % 2, NB_CH / 16, lane, acc2[u], t % 2 == 0);
+        bs2[u] += stage_mma(imA, 136, imB, 72, t / 2, t % 2, NB_CH / 16, lane, acc2[u], 0, t % 2 == 0 ? NB_CH / 16 : 0);
       }
       __syncthreads();
     }
@@ -612,7 +612,7 @@ __global__ __launch_bounds__(NB_WAVES * 64, 1) void ctrl_node_bwd_kernel(CtrlNod
 #pragma unroll
       for (int u = 0; u < 3; ++u) {
         const int t = wave + 4 * u;
-        if (u < n1) stage_mma(imA, 72, imB, NS1, t / 5, t % 5, NB_CH / 16, lane, acc1[u], false);
+        if (u < n1) stage_mma(imA, 72, imB, NS1, t / 5, t % 5, NB_CH / 16, lane, acc1[u]);
       }
       __syncthreads();
     }
@@ -757,7 +757,7 @@ __global__ __launch_bounds__(EB_WAVES * 64, 2) void ctrl_edge_bwd_kernel(CtrlEdg
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
           const int t = wave + 4 * u;
-          bs[u] += stage_mma(imA, 136, imB, 72, t / 2, t % 2, EB_CH / 16, lane, accW2[u], t % 2 == 0);
+          bs[u] += stage_mma(imA, 136, imB, 72, t / 2, t % 2, EB_CH / 16, lane, accW2[u], 0, t % 2 == 0 ? EB_CH / 16 : 0);
         }
         __syncthreads();
       }
@@ -773,7 +773,7 @@ __global__ __launch_bounds__(EB_WAVES * 64, 2) void ctrl_edge_bwd_kernel(CtrlEdg
         *reinterpret_cast<bf16x8*>(imB + erow * 40 + 8 * h) = F;
         *reinterpret_cast<bf16x8*>(imB + erow * 40 + 16 + 8 * h) = zz;
         __syncthreads();
-        if (wave < 2) stage_mma(imA, 72, imB, 40, wave, 0, EB_CH / 16, lane, accW1, false);
+        if (wave < 2) stage_mma(imA, 72, imB, 40, wave, 0, EB_CH / 16, lane, accW1);
         __syncthreads();
       }
     }
