@@ -80,6 +80,7 @@ struct CbfFwdArgs {
 struct CbfBwdArgs {
   const float4* S;  long s_env, s_step;   // state of (b,t,i): S[b*s_env + t*s_step + i]
   const int* idx;                          // (T,B,N,K) time-major
+  const int* idx1;                         // neighbour slots of pass 1 (null = idx: reuse_nbr_idx)
   int B, T, N, K;
   int passes;                              // evaluations = passes*E; pass p reads states at t+p
   const float* dh;                         // (passes, E) upstream dL/dh (radius mask folded in)
@@ -139,6 +140,8 @@ struct NodeRedArgs {
   const int* ptr; const int* edges;   // reverse CSR of the B*T graphs
   int B, T, N, K, passes, accumulate;
   float4* out;         // (T+1, B, N)
+  int pass_mask;       // bit p: include pass p (0 -> all passes)
+  int shift1;          // pass 1 edges belong to graph t + shift1 (1: h' on recomputed kNN of s_{t+1})
 };
 
 struct CombineArgs {

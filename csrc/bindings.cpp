@@ -76,9 +76,10 @@ static int cbf_fwd(u64 S, long s_env, long s_step, u64 idx, u64 dang, u64 valid,
 
 static int cbf_bwd(u64 S, long s_env, long s_step, u64 idx, int B, int T, int N, int K, int passes, u64 dh,
                    u64 wpack, int f_bwd, u64 wrm, u64 wvec, u64 dE, u64 partial, float obs_r, float dist_thr,
-                   float dist_eps, int fused, u64 dang, u64 valid, u64 counts, py::tuple lc, int num_blocks,
-                   u64 stream) {
+                   float dist_eps, int fused, u64 dang, u64 valid, u64 counts, py::tuple lc, u64 idx1,
+                   int num_blocks, u64 stream) {
   mb::CbfBwdArgs a{};
+  a.idx1 = P<const int>(idx1);
   a.fused = fused; a.dang = P<const uint8_t>(dang); a.valid = P<const uint8_t>(valid);
   a.counts = P<const float>(counts);
   a.lc.eps_dang = lc[0].cast<float>(); a.lc.dt_alpha = lc[1].cast<float>(); a.lc.w_dang = lc[2].cast<float>();
@@ -99,8 +100,9 @@ static int rev_csr(u64 idx, int G, int N, int K, u64 ptr, u64 edges, u64 stream)
 }
 
 static int node_reduce(u64 dE, u64 ptr, u64 edges, int B, int T, int N, int K, int passes, int accumulate, u64 out,
-                       u64 stream) {
+                       int pass_mask, int shift1, u64 stream) {
   mb::NodeRedArgs a{};
+  a.pass_mask = pass_mask; a.shift1 = shift1;
   a.dE = P<const float4>(dE); a.ptr = P<const int>(ptr); a.edges = P<const int>(edges);
   a.B = B; a.T = T; a.N = N; a.K = K; a.passes = passes; a.accumulate = accumulate; a.out = P<float4>(out);
   return mb_node_reduce(&a, ST(stream));

@@ -281,7 +281,8 @@ DEV void cbf_load(const CbfBwdArgs& a, long chunk, int wave, int r, long E, long
     e = ev - (unsigned)pass * (unsigned)E;
     x.ev = ev;
   }
-  cbf_edge(a.S, a.s_env, a.s_step, a.idx, a.B, a.N, a.K, e, x.in ? E : 0, pass, a.obs_r, a.dist_thr, a.dist_eps, x.c);
+  const int* idxp = (pass == 1 && a.idx1) ? a.idx1 : a.idx;
+  cbf_edge(a.S, a.s_env, a.s_step, idxp, a.B, a.N, a.K, e, x.in ? E : 0, pass, a.obs_r, a.dist_thr, a.dist_eps, x.c);
   if constexpr (FUSED) {
     x.dh = 0.f;
     x.dg = x.in && a.dang[e] != 0;

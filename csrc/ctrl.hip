@@ -588,7 +588,7 @@ __global__ __launch_bounds__(NB_WAVES * 64, 1) void ctrl_node_bwd_kernel(CtrlNod
         egod.y += c[1];   // d/d(ey) -> y
         egod.z += c[2];   // vx
         egod.w += c[3];   // vy
-        a.ego[(long)b * N + i] = egod;
+        if (a.ego) a.ego[(long)b * N + i] = egod;
       }
     }
     {   // S1: dWn1f (64x160) += dY1 . P^T  (P re-read from the pooled rows: L2-hot)
@@ -740,7 +740,7 @@ __global__ __launch_bounds__(EB_WAVES * 64, 2) void ctrl_edge_bwd_kernel(CtrlEdg
           constexpr int kk = decltype(kk_)::value;
           c = mfma(frag_ld(wt, 18 + kk, lane), bacc_frag<kk & 1>(d1b[kk >> 1]), c);
         });
-        if (ok && h == 0) {
+        if (ok && h == 0 && a.dEc) {
           const float4 g = (j != i) ? make_float4(c[0], c[1], c[2], c[3]) : make_float4(0.f, 0.f, 0.f, 0.f);
           a.dEc[b * (int)a.de_env + i * K + slot] = g;
         }

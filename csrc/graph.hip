@@ -83,10 +83,12 @@ __global__ __launch_bounds__(256) void node_reduce_kernel(NodeRedArgs a) {
   const long E = (long)a.B * a.T * N * K;
   float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
   for (int pass = 0; pass < a.passes; ++pass) {
+    if (a.pass_mask && !((a.pass_mask >> pass) & 1)) continue;
     const int t = tp - pass;
     if (t < 0 || t >= a.T) continue;
-    const long gi = (long)t * a.B + b;
-    const float4* dE = a.dE + (long)pass * E + gi * N * K;
+    const long ge = (long)t * a.B + b;                          // edge block of step t
+    const long gi = ge + (pass == 1 ? (long)a.shift1 * a.B : 0);  // graph (CSR) the edges live in
+    const float4* dE = a.dE + (long)pass * E + ge * N * K;
     for (int k = 0; k < K; ++k) {
       const float4 v = dE[(long)i * K + k];
       g.x += v.x; g.y += v.y; g.z += v.z; g.w += v.w;

@@ -86,6 +86,7 @@ class TrainConfig:
     compute_safety: bool = True
     nan_guard: bool = True            # skip the optimizer step when the reduced gradient is not finite
     phase_timing: bool = False        # per-phase device-event timings in the step stats
+    prefetch_data: bool = True        # HIP: sample iteration i+1 on a side stream during iteration i
 
     def k_eff(self) -> int:
         return min(self.num_agents, self.top_k)

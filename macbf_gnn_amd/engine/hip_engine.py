@@ -33,10 +33,8 @@ class HipEngine:
     def __init__(self, trainer):
         self.tr = trainer
         cfg = trainer.cfg
-        if not cfg.bptt:
-            raise NotImplementedError("HIP engine: --no_bptt is not implemented yet (oracle engine only)")
-        if not cfg.reuse_nbr_idx:
-            raise NotImplementedError("HIP engine requires reuse_nbr_idx (oracle engine supports recompute)")
+        self.bptt = cfg.bptt
+        self.reuse = cfg.reuse_nbr_idx
         native.lib()
         self.dev = trainer.device
         self.B, self.N = cfg.num_envs, cfg.num_agents
@@ -60,7 +58,9 @@ class HipEngine:
         self.S = torch.zeros(T + 1, B, N, 4, dtype=f32, device=dev)
         self.G = torch.zeros(B, N, 2, dtype=f32, device=dev)
         self.A = torch.zeros(T, B, N, 2, dtype=f32, device=dev)
-        self.idx = torch.zeros(T, B, N, K, dtype=i32, device=dev)
+        # one extra graph when h' uses the recomputed kNN of s_{t+1} (reuse_nbr_idx=False)
+        G1 = 0 if self.reuse else 1
+        self.idx = torch.zeros(T + G1, B, N, K, dtype=i32, device=dev)
         self.dang = torch.zeros(T, B, N, K, dtype=u8, device=dev)
         self.cnt = torch.zeros(T, B, 2, dtype=f32, device=dev)
         self.safe = torch.zeros(T + 1, B, dtype=f32, device=dev)
@@ -69,8 +69,8 @@ class HipEngine:
         self.pooled = torch.zeros(T, B, N, 128, dtype=bf, device=dev)
         self.argmax = torch.zeros(T, B, N, 128, dtype=u8, device=dev)
         self.dE = torch.zeros(2 * T * B * N * K * 4, dtype=f32, device=dev)
-        self.rptr = torch.zeros(T * B, N + 1, dtype=i32, device=dev)
-        self.redges = torch.zeros(T * B, N * K, dtype=i32, device=dev)
+        self.rptr = torch.zeros((T + G1) * B, N + 1, dtype=i32, device=dev)
+        self.redges = torch.zeros((T + G1) * B, N * K, dtype=i32, device=dev)
         self.dS = torch.zeros(T + 1, B, N, 4, dtype=f32, device=dev)
         self.Gb = torch.zeros(T + 1, B, N, 4, dtype=f32, device=dev)
         self.dP = torch.zeros(B, N, 128, dtype=bf, device=dev)
@@ -84,7 +84,9 @@ class HipEngine:
         self.red_node = torch.zeros(native.CTRL_NODE_PARTIAL, dtype=f32, device=dev)
         self.red_edge = torch.zeros(native.CTRL_EDGE_PARTIAL, dtype=f32, device=dev)
         self.host_dist = torch.zeros(T, B, dtype=f32, pin_memory=True)
+        self._nobptt = {}     # lazily sized (T*B)-batched controller-backward buffers
         self._part_cbf = {}
+        self._part_cbf_nb = {}
 
     def after_update(self):
         self.pw.update()
@@ -124,8 +126,11 @@ class HipEngine:
                     if self._all_done(t - 1):
                         T = t + 1   # step t was already issued; its envs are masked out
                         break
-        if cfg.compute_safety:
-            native.scan(self.S[T], None, None, None, self.safe[T], K=K, do_knn=False, do_safety=True)
+        if cfg.compute_safety or not self.reuse:
+            # safety of the final state; with reuse_nbr_idx=False also the kNN graph of s_T (for h')
+            native.scan(self.S[T], self.idx[T] if not self.reuse else None, None, None,
+                        self.safe[T] if cfg.compute_safety else None, K=K, do_knn=not self.reuse,
+                        do_safety=cfg.compute_safety)
         return T
 
     def _all_done(self, t):
@@ -161,35 +166,59 @@ class HipEngine:
         nbb = native.cbf_bwd_grid(2 * E, self.dev)
         part_cbf = self._buf(self._part_cbf, nbb, native.CBF_PARTIAL)
         dE = self.dE[: 2 * E * 4].view(2, T, B, N, K, 4)
+        idx1 = None if self.reuse else self.idx[1: T + 1]
         native.cbf_bwd(S, idx, None, pw.cbf_w, pw.cbf_off["w1f"], pw.cbf_rm, pw.cbf_v, passes=2, dE=dE,
                        partial=part_cbf, num_blocks=nbb, fused=True, dang=self.dang[:T], valid=valid_u8,
-                       counts=self.counts)
-        rptr = self.rptr[: T * B]
-        redges = self.redges[: T * B]
-        native.rev_csr(idx.view(T * B, N, K), rptr, redges)
-        native.node_reduce(dE, rptr, redges, self.dS, T=T, B=B, N=N, K=K, passes=2)
+                       counts=self.counts, idx1=idx1)
+        G1 = 0 if self.reuse else 1
+        rptr = self.rptr[: (T + G1) * B]
+        redges = self.redges[: (T + G1) * B]
+        native.rev_csr(self.idx[: T + G1].view((T + G1) * B, N, K), rptr, redges)
+        # no-BPTT: s_t is a detached input, only h'(s_{t+1}) gradients reach a_t
+        native.node_reduce(dE, rptr, redges, self.dS, T=T, B=B, N=N, K=K, passes=2,
+                           pass_mask=0 if self.bptt else 2, shift1=G1)
         tm.mark("cbf")
-        # ---- BPTT through the rollout
+        # ---- controller backward
         self.part_node.zero_()
         self.part_edge.zero_()
         act_coef = (C.LOSS_SCALE * C.LOSS_WEIGHTS[4]) / n_act
         act_coef_f = float(act_coef)   # one host read per step (counts already reduced)
-        self.Gb[T].copy_(self.dS[T])
-        rptr3 = rptr.view(T, B, N + 1)
-        redges3 = redges.view(T, B, N * K)
-        for t in range(T - 1, -1, -1):
-            native.ctrl_node_bwd(self.pooled[t], self.S[t], self.G, self.A[t], self.Gb[t + 1], valid_u8[t],
-                                 pw.ctrl_rm, pw.node_rm_off, pw.ctrl_v, act_coef_f, self.dP, self.ego,
-                                 self.part_node, self.nb_node)
-            native.ctrl_edge_bwd(self.S[t], self.idx[t], self.argmax[t], self.dP, pw.ctrl_w, pw.ctrl_off["ew1f"],
-                                 pw.ctrl_off["ew2tn"], self.dEc, self.part_edge, self.nb_edge)
-            native.node_combine(self.dS[t], self.ego, self.dEc, rptr3[t], redges3[t], self.Gb[t + 1], self.Gb[t], K=K)
+        if self.bptt:
+            # BPTT through the rollout: G_t = dL/ds_t, reverse time
+            self.Gb[T].copy_(self.dS[T])
+            rptr3 = rptr[: T * B].view(T, B, N + 1)
+            redges3 = redges[: T * B].view(T, B, N * K)
+            for t in range(T - 1, -1, -1):
+                native.ctrl_node_bwd(self.pooled[t], self.S[t], self.G, self.A[t], self.Gb[t + 1], valid_u8[t],
+                                     pw.ctrl_rm, pw.node_rm_off, pw.ctrl_v, act_coef_f, self.dP, self.ego,
+                                     self.part_node, self.nb_node)
+                native.ctrl_edge_bwd(self.S[t], self.idx[t], self.argmax[t], self.dP, pw.ctrl_w, pw.ctrl_off["ew1f"],
+                                     pw.ctrl_off["ew2tn"], self.dEc, self.part_edge, self.nb_edge)
+                native.node_combine(self.dS[t], self.ego, self.dEc, rptr3[t], redges3[t], self.Gb[t + 1],
+                                    self.Gb[t], K=K)
+        else:
+            # no BPTT: the steps are independent -> ONE node + ONE edge backward launch over all
+            # T*B (step, env) pairs, with dL/da_t = dt * dL/dv_{t+1} from h'(s_{t+1}) + action loss
+            TB = T * B
+            nb_n, nb_e, Gr, dP = self._nobptt_bufs(TB)
+            Gr[:TB].view(T, B, N, 2).copy_(self.G.unsqueeze(0).expand(T, B, N, 2))
+            pn = self._buf(self._part_cbf_nb, ("n", nb_n), native.CTRL_NODE_PARTIAL)
+            pe = self._buf(self._part_cbf_nb, ("e", nb_e), native.CTRL_EDGE_PARTIAL)
+            pn.zero_()
+            pe.zero_()
+            native.ctrl_node_bwd(self.pooled[:T].view(TB, N, 128), self.S[:T].view(TB, N, 4), Gr[:TB],
+                                 self.A[:T].view(TB, N, 2), self.dS[1: T + 1].view(TB, N, 4), valid_u8.view(TB),
+                                 pw.ctrl_rm, pw.node_rm_off, pw.ctrl_v, act_coef_f, dP[:TB], None, pn, nb_n)
+            native.ctrl_edge_bwd(self.S[:T].view(TB, N, 4), self.idx[:T].view(TB, N, K), self.argmax[:T].view(TB, N, 128),
+                                 dP[:TB], pw.ctrl_w, pw.ctrl_off["ew1f"], pw.ctrl_off["ew2tn"], None, pe, nb_e)
+            self._nb_parts = (pn, pe)
         tm.mark("bptt")
         # ---- weight-gradient slabs -> flat grad
         fg = tr.fp.grad
         fg.zero_()
-        for name, part, red in (("cbf", part_cbf, self.red_cbf), ("node", self.part_node, self.red_node),
-                                ("edge", self.part_edge, self.red_edge)):
+        pnode, pedge = (self.part_node, self.part_edge) if self.bptt else self._nb_parts
+        for name, part, red in (("cbf", part_cbf, self.red_cbf), ("node", pnode, self.red_node),
+                                ("edge", pedge, self.red_edge)):
             native.reduce_rows(part, red)
             src, dst = self.maps[name]
             fg.index_add_(0, dst, red.index_select(0, src))
@@ -212,9 +241,23 @@ class HipEngine:
             "agent_steps": vf.sum() * N, "safe_agents": (safe_next * vf).sum(), "T": T,
         }
 
-    def _buf(self, cache, rows, cols):
-        b = cache.get(rows)
+    def _buf(self, cache, key, cols):
+        b = cache.get(key)
         if b is None:
+            rows = key[1] if isinstance(key, tuple) else key
             b = torch.zeros(rows, cols, dtype=torch.float32, device=self.dev)
-            cache[rows] = b
+            cache[key] = b
         return b
+
+    def _nobptt_bufs(self, TB):
+        """(T*B)-batched buffers for the no-BPTT controller backward (sized for Tmax)."""
+        if "dP" not in self._nobptt:
+            TBm = self.Tmax * self.B
+            nb_n, nb_e = native.ctrl_bwd_grids(TBm * self.N, self.dev)
+            self._nobptt = {
+                "grids": (nb_n, nb_e),
+                "G": torch.zeros(TBm, self.N, 2, dtype=torch.float32, device=self.dev),
+                "dP": torch.zeros(TBm, self.N, 128, dtype=torch.bfloat16, device=self.dev),
+            }
+        nb_n, nb_e = self._nobptt["grids"]
+        return nb_n, nb_e, self._nobptt["G"], self._nobptt["dP"]

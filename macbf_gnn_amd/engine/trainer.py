@@ -64,6 +64,9 @@ class Trainer:
         self.logger = MetricsLogger(dp, cfg.log_path)
         self.timer = PhaseTimer(self.device, enabled=cfg.phase_timing)
         self.skipped_steps = 0
+        self._next = None
+        self._side = torch.cuda.Stream(device=self.device) if (self.device.type == "cuda" and cfg.prefetch_data) \
+            else None
         if self.device.type == "cuda":
             from .hip_engine import HipEngine
             self.engine = HipEngine(self)
@@ -85,6 +88,30 @@ class Trainer:
         seed = (self.cfg.seed * 1_000_003 + it) * 4099 + self.dp.rank
         return E.generate_batch(B, N, C.DIST_MIN_THRES, seed=seed)
 
+    def _sample_async(self, it: int):
+        """Launch the (parameter-independent) scenario sampler for iteration ``it`` on a side
+        stream: it overlaps the current iteration's rollout instead of serialising with it."""
+        with torch.cuda.stream(self._side):
+            s, g = self.sample(it)
+            ev = torch.cuda.Event()
+            ev.record(self._side)
+        return it, s, g, ev
+
+    def _take_sample(self):
+        if self._side is None:
+            return self.sample()
+        nx = self._next
+        if nx is not None and nx[0] == self.step_count:
+            _, s0, g, ev = nx
+            cur = torch.cuda.current_stream(self.device)
+            cur.wait_event(ev)
+            s0.record_stream(cur)
+            g.record_stream(cur)
+        else:
+            s0, g = self.sample()
+        self._next = self._sample_async(self.step_count + 1)
+        return s0, g
+
     def on_params_loaded(self):
         self.fp.rebind()
         self.engine.after_update()
@@ -100,7 +127,7 @@ class Trainer:
         tm = self.timer
         tm.start()
         if s0 is None:
-            s0, g = self.sample()
+            s0, g = self._take_sample()
         s0 = s0.to(self.device)
         g = g.to(self.device)
         tm.mark("sample")

@@ -248,7 +248,7 @@ def cbf_bwd_grid(EV: int, device) -> int:
 
 
 def cbf_bwd(S, idx, dh, wpack, f_bwd, wrm, wvec, *, passes=2, dE=None, partial=None, num_blocks=None,
-            fused=False, dang=None, valid=None, counts=None):
+            fused=False, dang=None, valid=None, counts=None, idx1=None):
     """dh (passes, T, B, N, K) -> dE (passes, T, B, N, K, 4), per-WG dW slabs (nb, CBF_PARTIAL).
 
     fused=True (training, passes=2): dh is not read; the kernel evaluates h and h' of every
@@ -273,6 +273,8 @@ def cbf_bwd(S, idx, dh, wpack, f_bwd, wrm, wvec, *, passes=2, dE=None, partial=N
     if wpack.numel() < (f_bwd + 70) * 512:
         raise NativeError("packed CBF weights too small")
     check(wrm, torch.bfloat16, (128 * 72 + 64 * 136,), "wrm")
+    if idx1 is not None:
+        check(idx1, torch.int32, (T, B, N, K), "idx1")
     E = B * T * N * K
     if E * passes >= 2 ** 31:
         raise NativeError("too many edge evaluations for 32-bit indexing")
@@ -282,7 +284,8 @@ def cbf_bwd(S, idx, dh, wpack, f_bwd, wrm, wvec, *, passes=2, dE=None, partial=N
                        0 if fused else ptr(dh),
                        ptr(wpack), int(f_bwd), ptr(wrm), ptr(wvec), ptr(dE), ptr(partial), float(C.OBS_RADIUS),
                        float(C.DIST_MIN_THRES), float(C.CBF_DIST_EPS), int(fused), ptr(dang) if fused else 0,
-                       ptr(valid) if fused else 0, ptr(counts) if fused else 0, LOSS_CONSTS, nb, stream_handle())
+                       ptr(valid) if fused else 0, ptr(counts) if fused else 0, LOSS_CONSTS, ptr(idx1), nb,
+                       stream_handle())
     _ok(rc, "cbf_bwd")
     return nb
 
@@ -296,17 +299,20 @@ def rev_csr(idx, rptr, redges):
     _ok(lib().rev_csr(ptr(idx), Gn, N, K, ptr(rptr), ptr(redges), stream_handle()), "rev_csr")
 
 
-def node_reduce(dE, rptr, redges, out, *, T, B, N, K, passes=2, accumulate=False):
+def node_reduce(dE, rptr, redges, out, *, T, B, N, K, passes=2, accumulate=False, pass_mask=0, shift1=0):
+    """dE (passes, T, B, N, K, 4) -> out[t'] (+)= sum over passes p of the edge->node reduction of
+    step t' - p. pass_mask selects passes (0 = all); shift1=1: pass-1 edges live in graph t+1
+    (h' on the recomputed kNN of s_{t+1}), so the CSR arrays must hold T+1 graphs."""
     check(dE, torch.float32, (passes, T, B, N, K, 4), "dE")
     check(rptr, torch.int32, None, "rptr")
     check(redges, torch.int32, None, "redges")
-    if rptr.shape[0] < T * B or redges.shape[0] < T * B:
+    if rptr.shape[0] < (T + shift1) * B or redges.shape[0] < (T + shift1) * B:
         raise NativeError("reverse CSR too small")
     if out.dtype != torch.float32 or not out.is_contiguous() or out.shape[0] < T + 1 or \
             tuple(out.shape[1:]) != (B, N, 4):
         raise NativeError("out must be float32 (>=T+1, B, N, 4)")
     _ok(lib().node_reduce(ptr(dE), ptr(rptr), ptr(redges), B, T, N, K, passes, int(accumulate), ptr(out),
-                          stream_handle()), "node_reduce")
+                          int(pass_mask), int(shift1), stream_handle()), "node_reduce")
 
 
 def node_combine(dS_t, ego, dEc, rptr_t, redges_t, Gn, Gout, *, K, dt=C.TIME_STEP):
@@ -369,7 +375,8 @@ def ctrl_edge_bwd(S, idx, argmax, dP, wpack, f_ew1f, f_ew2tn, dEc, partial, num_
     check(partial, torch.float32, (num_blocks, CTRL_EDGE_PARTIAL), "partial")
     rc = lib().ctrl_edge_bwd(ptr(S), S.stride(0) // 4, ptr(idx), idx.stride(0), ptr(argmax), argmax.stride(0),
                              ptr(dP), dP.stride(0), B, N, K, ptr(wpack), int(f_ew1f), int(f_ew2tn), ptr(dEc),
-                             dEc.stride(0) // 4, ptr(partial), int(num_blocks), stream_handle())
+                             dEc.stride(0) // 4 if dEc is not None else 0, ptr(partial), int(num_blocks),
+                             stream_handle())
     _ok(rc, "ctrl_edge_bwd")
 
 

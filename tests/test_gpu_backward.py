@@ -162,10 +162,12 @@ def _trainer(device, **kw):
     return Trainer(cfg, device=device, dp=DP(device=device))
 
 
-def test_full_step_grad_matches_oracle():
-    """One full training step: HIP engine gradient vs autograd through the oracle engine."""
+@pytest.mark.parametrize("bptt,reuse", [(True, True), (False, True), (True, False), (False, False)])
+def test_full_step_grad_matches_oracle(bptt, reuse):
+    """One full training step: HIP engine gradient vs autograd through the oracle engine, for
+    BPTT / no-BPTT and h' on the time-t or on the recomputed time-(t+1) neighbour slots."""
     from macbf_gnn_amd.engine.oracle_engine import OracleEngine
-    tr = _trainer(DEV)
+    tr = _trainer(DEV, bptt=bptt, reuse_nbr_idx=reuse)
     s0, g = tr.sample()
     stats = tr.engine.step(s0, g)
     g_hip = tr.fp.grad.clone()
@@ -239,3 +241,15 @@ def test_fused_cbf_train_kernel_matches_two_kernel_path():
     _cmp(got[2:], ref_sums[2:], "loss sums", rel=2e-2, cos=0.999)
     _cmp(dE2, dE1, "dE", rel=5e-2, cos=0.998)
     _cmp(r2[:L], r1[:L], "dW slab", rel=5e-2, cos=0.998)
+
+
+def test_prefetched_sampling_is_identical():
+    """Side-stream prefetch of the next scenario batch changes timing only, not the data."""
+    a = _trainer(DEV, N=64, B=2, T=6)
+    b = _trainer(DEV, N=64, B=2, T=6)
+    b._side = None                       # synchronous sampling
+    for _ in range(3):
+        a.train_step()
+        b.train_step()
+    torch.cuda.synchronize()
+    assert torch.equal(a.fp.flat, b.fp.flat)
