@@ -84,7 +84,13 @@ DEV int opaque_zero() {
   return z;
 }
 
-DEV float shfl_xor32(float v) { return __shfl_xor(v, 32); }
+// lane l <- lane l^32 with v_permlane32_swap (CDNA4, VALU) instead of ds_bpermute (LDS path)
+DEV unsigned xor32u(unsigned u) {
+  const auto r = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+  return (threadIdx.x & 32) ? r[0] : r[1];
+}
+DEV float shfl_xor32(float v) { return __uint_as_float(xor32u(__float_as_uint(v))); }
+DEV int shfl_xor32i(int v) { return (int)xor32u((unsigned)v); }
 
 // hi/lo bf16 split of an fp32 value: x ~= hi + lo with ~16 significant bits
 DEV void split_bf16(float x, bf16& hi, bf16& lo) {

@@ -208,25 +208,33 @@ __global__ __launch_bounds__(WAVES * 64) void ctrl_fwd_kernel(CtrlArgs a) {
       f32x16 Z[4];
       ctrl_edge_tile(F, wl + opaque_zero(), eb2, lane, Z);
       const unsigned mask32 = (unsigned)(__ballot(m) & 0xffffffffull);
+      // per-register edge mask (rows acc_row(reg, h)), shared by the 4 feature tiles
+      bool mk[16];
+#pragma unroll
+      for (int reg = 0; reg < 16; ++reg) mk[reg] = (mask32 >> acc_row(reg, h)) & 1u;
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt) {
-        // masked max over each agent's 16 rows + first-occurrence argmax (row order = slot)
+        // masked max-pool of relu(Z) over each agent's 16 rows + first-occurrence argmax.
+        // Pooled values start at 0 with a strict '>' so masked rows (0), negative Z (relu -> 0)
+        // and later equal values never win; rows are visited in increasing slot order.
         float p0 = 0.f, p1 = 0.f;
         int r0 = 255, r1 = 255;
 #pragma unroll
         for (int reg = 0; reg < 8; ++reg) {
-          const int e = acc_row(reg, h);
-          const float v = ((mask32 >> e) & 1u) ? fmaxf(Z[nt][reg], 0.f) : 0.f;
-          if (v > p0 || (v == p0 && v > 0.f && e < r0)) { p0 = v; r0 = e; }
+          const float v = mk[reg] ? Z[nt][reg] : 0.f;
+          const bool gt = v > p0;
+          p0 = gt ? v : p0;
+          r0 = gt ? acc_row(reg, h) : r0;
         }
 #pragma unroll
         for (int reg = 8; reg < 16; ++reg) {
-          const int e = acc_row(reg, h);
-          const float v = ((mask32 >> e) & 1u) ? fmaxf(Z[nt][reg], 0.f) : 0.f;
-          if (v > p1 || (v == p1 && v > 0.f && e < r1)) { p1 = v; r1 = e; }
+          const float v = mk[reg] ? Z[nt][reg] : 0.f;
+          const bool gt = v > p1;
+          p1 = gt ? v : p1;
+          r1 = gt ? acc_row(reg, h) : r1;
         }
         const float q0 = shfl_xor32(p0), q1 = shfl_xor32(p1);
-        const int s0 = __shfl_xor(r0, 32), s1 = __shfl_xor(r1, 32);
+        const int s0 = shfl_xor32i(r0), s1 = shfl_xor32i(r1);
         if (q0 > p0 || (q0 == p0 && s0 < r0)) { p0 = q0; r0 = s0; }
         if (q1 > p1 || (q1 == p1 && s1 < r1)) { p1 = q1; r1 = s1; }
         const int arow = 2 * q + h;   // h==0 writes agent 2q, h==1 agent 2q+1

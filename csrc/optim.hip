@@ -7,22 +7,40 @@
 
 namespace mb {
 
-// out[c] (+)= sum_r partial[r * cols + c], fixed row order (bitwise reproducible)
-__global__ __launch_bounds__(256) void reduce_rows_kernel(const float* partial, int rows, int cols, float* out,
-                                                          int accumulate) {
-  const int c4 = blockIdx.x * blockDim.x + threadIdx.x;   // one float4 column group per thread
-  if (c4 * 4 >= cols) return;
+// out[c] (+)= sum_r partial[r * cols + c] in a fixed order (bitwise reproducible).
+// Block = 16 float4-column groups x 16 row slices: slice y sums rows y, y+16, ... in order, then
+// the 16 slice sums are added in slice order through LDS. ~300 workgroups for the CBF slab
+// instead of 19 with one serial thread per column.
+constexpr int RR_COLS = 16, RR_SLICES = 16;
+__global__ __launch_bounds__(RR_COLS * RR_SLICES) void reduce_rows_kernel(const float* partial, int rows, int cols,
+                                                                          float* out, int accumulate) {
+  __shared__ float4 red[RR_SLICES][RR_COLS];
+  const int cx = threadIdx.x % RR_COLS, sy = threadIdx.x / RR_COLS;
+  const int c4 = blockIdx.x * RR_COLS + cx;
+  const bool ok = c4 * 4 < cols;
   float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
-  for (int r = 0; r < rows; ++r) {
-    const float4 v = *reinterpret_cast<const float4*>(partial + (long)r * cols + c4 * 4);
-    s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+  if (ok) {
+#pragma unroll 4
+    for (int r = sy; r < rows; r += RR_SLICES) {
+      const float4 v = *reinterpret_cast<const float4*>(partial + (long)r * cols + c4 * 4);
+      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
   }
-  float4* o = reinterpret_cast<float4*>(out + c4 * 4);
-  if (accumulate) {
-    const float4 p = *o;
-    s.x += p.x; s.y += p.y; s.z += p.z; s.w += p.w;
+  red[sy][cx] = s;
+  __syncthreads();
+  if (sy == 0 && ok) {
+    float4 t = red[0][cx];
+    for (int y = 1; y < RR_SLICES; ++y) {
+      const float4 v = red[y][cx];
+      t.x += v.x; t.y += v.y; t.z += v.z; t.w += v.w;
+    }
+    float4* o = reinterpret_cast<float4*>(out + c4 * 4);
+    if (accumulate) {
+      const float4 p = *o;
+      t.x += p.x; t.y += p.y; t.z += p.z; t.w += p.w;
+    }
+    *o = t;
   }
-  *o = s;
 }
 
 __global__ __launch_bounds__(256) void adam_kernel(AdamArgs a) {
@@ -45,8 +63,8 @@ __global__ __launch_bounds__(256) void adam_kernel(AdamArgs a) {
 extern "C" int mb_reduce_rows(const float* partial, int rows, int cols, float* out, int accumulate, hipStream_t st) {
   if (cols % 4) return -1;
   const int groups = cols / 4;
-  hipLaunchKernelGGL(mb::reduce_rows_kernel, dim3((groups + 255) / 256), dim3(256), 0, st, partial, rows, cols, out,
-                     accumulate);
+  hipLaunchKernelGGL(mb::reduce_rows_kernel, dim3((groups + mb::RR_COLS - 1) / mb::RR_COLS),
+                     dim3(mb::RR_COLS * mb::RR_SLICES), 0, st, partial, rows, cols, out, accumulate);
   return (int)hipGetLastError();
 }
 

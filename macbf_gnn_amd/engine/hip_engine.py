@@ -84,6 +84,7 @@ class HipEngine:
         self.red_node = torch.zeros(native.CTRL_NODE_PARTIAL, dtype=f32, device=dev)
         self.red_edge = torch.zeros(native.CTRL_EDGE_PARTIAL, dtype=f32, device=dev)
         self.host_dist = torch.zeros(T, B, dtype=f32, pin_memory=True)
+        self.aux = torch.cuda.Stream(device=dev)      # reverse-CSR build overlaps the CBF kernel
         self._nobptt = {}     # lazily sized (T*B)-batched controller-backward buffers
         self._part_cbf = {}
         self._part_cbf_nb = {}
@@ -159,6 +160,16 @@ class HipEngine:
         tr.dp.all_reduce_(self.counts)
         n_act = self.counts[2].clamp_min(1.0)
         E = T * B * N * K
+        # ---- reverse CSR of the step graphs (needs only idx): on the aux stream, concurrent with
+        #      the CBF kernel below
+        G1 = 0 if self.reuse else 1
+        rptr = self.rptr[: (T + G1) * B]
+        redges = self.redges[: (T + G1) * B]
+        self.aux.wait_stream(torch.cuda.current_stream(self.dev))
+        with torch.cuda.stream(self.aux):
+            native.rev_csr(self.idx[: T + G1].view((T + G1) * B, N, K), rptr, redges)
+            csr_done = torch.cuda.Event()
+            csr_done.record(self.aux)
         # ---- CBF: h, h', hinge losses, upstream grads and the full backward in ONE kernel
         S = self.S[: T + 1]
         idx = self.idx[:T]
@@ -170,10 +181,8 @@ class HipEngine:
         native.cbf_bwd(S, idx, None, pw.cbf_w, pw.cbf_off["w1f"], pw.cbf_rm, pw.cbf_v, passes=2, dE=dE,
                        partial=part_cbf, num_blocks=nbb, fused=True, dang=self.dang[:T], valid=valid_u8,
                        counts=self.counts, idx1=idx1)
-        G1 = 0 if self.reuse else 1
-        rptr = self.rptr[: (T + G1) * B]
-        redges = self.redges[: (T + G1) * B]
-        native.rev_csr(self.idx[: T + G1].view((T + G1) * B, N, K), rptr, redges)
+        cur = torch.cuda.current_stream(self.dev)
+        cur.wait_event(csr_done)
         # no-BPTT: s_t is a detached input, only h'(s_{t+1}) gradients reach a_t
         native.node_reduce(dE, rptr, redges, self.dS, T=T, B=B, N=N, K=K, passes=2,
                            pass_mask=0 if self.bptt else 2, shift1=G1)

@@ -3,7 +3,7 @@
 TAG=${1:-run}; shift
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
-TESTS=${@:-tests/test_gpu_probe.py tests/test_gpu_forward.py tests/test_gpu_backward.py}
+TESTS=${@:-tests/test_gpu_probe.py tests/test_gpu_forward.py tests/test_gpu_backward.py tests/test_gpu_compat.py}
 timeout -k 10 900 python -m pytest $TESTS -q -m gpu -p no:cacheprovider > gpurun_out/${TAG}_tests.log 2>&1
 rc=$?
 echo "pytest rc=$rc" >> gpurun_out/${TAG}_tests.log
