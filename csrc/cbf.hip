@@ -17,6 +17,10 @@
 #include "common.h"
 #include "args.h"
 
+#ifndef CBF_NW
+#define CBF_NW 8   // waves per CBF-backward workgroup (4: one per SIMD, 8: two per SIMD)
+#endif
+
 namespace mb {
 
 constexpr int CBF_FWD_FRAGS = 34;  // w1f 2 + w2 16 + w3 16
@@ -243,19 +247,26 @@ extern "C" int mb_cbf_fwd(const mb::CbfFwdArgs* a, int num_blocks, hipStream_t s
 // ---------------------------------------------------------------------------------------
 namespace mb {
 
-constexpr int CBF_BWD_WAVES = 4;
-constexpr int CBF_CH = CBF_BWD_WAVES * 32;    // evaluations per chunk
 constexpr int SA128 = 136, SA64 = 72, SA32 = 40;
 constexpr int RM_W2 = 128 * 72, RM_W3 = 64 * 136;   // row-major image sizes (elements)
 // per-WG partial slab layout (floats)
 constexpr int P_W3 = 0, P_B3 = 8192, P_W2 = 8256, P_B2 = 16448, P_W1 = 16576, P_W4 = 18624, P_B4 = 18688;
 constexpr int P_LOSS = 18692;                 // 10 loss partial sums (fused mode)
 constexpr int CBF_PARTIAL = 18704;
-// stage A/B: (128 + 64)-wide images; stage C+D: dH1|F|dh|relu(H3) = 64+32+32+64 wide
-constexpr size_t CBF_STAGE_BYTES = (size_t)(SA64 + SA32 + SA32 + SA64) * CBF_CH * 2;
 constexpr size_t CBF_BWD_W_BYTES = (size_t)(RM_W2 + RM_W3) * 2 + 6 * FRAG_BYTES;
 
-size_t cbf_bwd_lds() { return CBF_BWD_W_BYTES + CBF_VEC * 4 + CBF_STAGE_BYTES; }
+// Stage regions. NW = 4 waves (one per SIMD): two regions used alternately (stage k of the
+// running sequence A,B,C,A,B,C,... writes region k&1): a region is rewritten only after every
+// wave has passed the NEXT stage's barrier, i.e. finished reading it -> one barrier per stage.
+// NW = 8 waves (two per SIMD, chunk of 256): one region (LDS), two barriers per stage.
+// Stage A/B: (128 + 64)-wide images; stage C+D: dH1 | [F, dh, 0] | relu(H3) = 64+32+64 wide.
+template <int NW> struct CbfCfg {
+  static constexpr int CH = NW * 32;                          // evaluations per chunk
+  static constexpr int KS = CH / 16;                          // edge steps per stage contraction
+  static constexpr int NREG = NW == 4 ? 2 : 1;
+  static constexpr int REGION = (SA64 + SA128) * CH;          // elements per region
+  static constexpr size_t LDS = CBF_BWD_W_BYTES + CBF_VEC * 4 + (size_t)NREG * REGION * 2;
+};
 
 struct CbfIn {
   EdgeCtx c;
@@ -265,17 +276,18 @@ struct CbfIn {
   unsigned ev;    // evaluation index (pass*E + e)
 };
 
-template <bool FUSED>
+template <bool FUSED, int NW>
 DEV void cbf_load(const CbfBwdArgs& a, long chunk, int wave, int r, long E, long EV, CbfIn& x) {
+  constexpr int CH = CbfCfg<NW>::CH;
   int pass;
   unsigned e;
   if constexpr (FUSED) {
-    pass = wave >> 1;
-    e = (unsigned)chunk * (CBF_CH / 2) + (wave & 1) * 32 + r;
+    pass = wave / (NW / 2);
+    e = (unsigned)chunk * (CH / 2) + (wave % (NW / 2)) * 32 + r;
     x.in = e < (unsigned)E;
     x.ev = (unsigned)pass * (unsigned)E + e;
   } else {
-    const unsigned ev = (unsigned)chunk * CBF_CH + wave * 32 + r;
+    const unsigned ev = (unsigned)chunk * CH + wave * 32 + r;
     x.in = ev < (unsigned)EV;
     pass = (x.in && ev >= (unsigned)E) ? 1 : 0;
     e = ev - (unsigned)pass * (unsigned)E;
@@ -294,47 +306,66 @@ DEV void cbf_load(const CbfBwdArgs& a, long chunk, int wave, int r, long E, long
   }
 }
 
-template <bool FUSED>
-__global__ __launch_bounds__(CBF_BWD_WAVES * 64, 1) void cbf_bwd_kernel(CbfBwdArgs a) {
+// ---------------------------------------------------------------------------------------
+// cbf_bwd_kernel<FUSED, NW>: hand-written backward of the CBF edge MLP.
+// Workgroup = NW waves sharing a chunk of 32*NW evaluations (32 per wave):
+//   data path (per wave, registers only): recompute H1,H2,H3 -> dH3 = w4*dh*relu'
+//     -> dH2 = W3^T dH3 .relu' (16 MFMA) -> dH1 = W2^T dH2 .relu' (16) -> dF = W1^T dH1 (4)
+//     -> dL/d(s_i - s_j) incl. the |dp|_eps feature; written per evaluation (self edges 0)
+//   weight gradients (workgroup-shared): activations / deltas of the chunk are staged as
+//     edge-major bf16 LDS images; each wave owns a fixed subset of the 8 + 8 + 2 + 2 32x32
+//     output tiles of dW3 (64x128), dW2 (128x64), dW1f (64x32), dW4pad (32x64) and contracts
+//     over the chunk's edges with ds_read_b64_tr_b16 fragments -> MFMA; bias grads are row
+//     sums of the A fragments, split over the waves that read the same row block; fixed
+//     ownership -> deterministic per-WG slabs, reduced by a separate pass (no float atomics).
+// FUSED (training): the chunk is CH/2 edges x {h(s_t) (waves < NW/2), h'(s_{t+1}) (the rest)}.
+//   The forward recompute includes the 64->1 head; h and h' of each edge meet in LDS, every
+//   wave forms its upstream dL/dh locally (barrier + derivative hinge losses with the danger
+//   bit, step validity and the global pooled counts) and the loss partial sums go to the slab.
+// ---------------------------------------------------------------------------------------
+template <bool FUSED, int NW>
+__global__ __launch_bounds__(NW * 64, 1) void cbf_bwd_kernel(CbfBwdArgs a) {
+  using Cfg = CbfCfg<NW>;
+  constexpr int CH = Cfg::CH, KS = Cfg::KS;
+  constexpr int TA = 8 / NW;                   // owned dW3 tiles (and dW2 tiles) per wave
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   bf16* W2 = reinterpret_cast<bf16*>(smem);
   bf16* W3 = W2 + RM_W2;
   bf16* wf = W3 + RM_W3;                       // w1f (2 frags) | w1ft (4 frags)
   float* vl = reinterpret_cast<float*>(smem + CBF_BWD_W_BYTES);
   bf16* stg = reinterpret_cast<bf16*>(smem + CBF_BWD_W_BYTES + CBF_VEC * 4);
-  __shared__ float hx[CBF_CH];                 // fused: h / h' exchange
-  __shared__ float bred[CBF_BWD_WAVES][192];   // bias partials: b3 (64) | b2 (128)
-  __shared__ float lred[CBF_BWD_WAVES][10];
-  __shared__ float red4[CBF_BWD_WAVES];
+  __shared__ float hx[CH];                     // fused: h / h' exchange
+  __shared__ float lacc[8][FUSED ? CH / 2 : 1];  // fused: per-lane loss partial sums (pass-0 lanes)
+  __shared__ float lred[NW][10];
+  __shared__ float red4[NW];
   block_copy16(W2, a.wrm, (RM_W2 + RM_W3) * 2);
   block_copy16(wf, a.wpack + (size_t)a.f_bwd * 512, 2 * FRAG_BYTES);
   block_copy16(wf + 2 * 512, a.wpack + (size_t)(a.f_bwd + 66) * 512, 4 * FRAG_BYTES);
   block_copy16(vl, a.wvec, CBF_VEC * 4);
-  for (int q = threadIdx.x; q < CBF_BWD_WAVES * 192; q += blockDim.x) (&bred[0][0])[q] = 0.f;
+  if constexpr (FUSED)
+    for (int q = threadIdx.x; q < 8 * CH / 2; q += blockDim.x) (&lacc[0][0])[q] = 0.f;
   __syncthreads();
   const int wave = threadIdx.x / WAVE, lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
   const long E = (long)a.B * a.T * a.N * a.K;
   const long EV = E * a.passes;
-  const long nchunks = FUSED ? (E + CBF_CH / 2 - 1) / (CBF_CH / 2) : (EV + CBF_CH - 1) / CBF_CH;
+  const long nchunks = FUSED ? (E + CH / 2 - 1) / (CH / 2) : (EV + CH - 1) / CH;
   const int erow = wave * 32 + r;
-  const int pass_w = wave >> 1;                // fused: this wave's pass
+  const int pass_w = wave / (NW / 2);          // fused: this wave's pass
   float nd = 1.f, ns = 1.f;
   if constexpr (FUSED) { nd = 1e-5f + a.counts[0]; ns = 1e-5f + a.counts[1]; }
-  float lacc[10];
+  f32x16 accA[TA], accB[TA], accC = zero16();
+  float bA[TA], bB[TA], db4 = 0.f;
 #pragma unroll
-  for (int q = 0; q < 10; ++q) lacc[q] = 0.f;
-  // owned weight-gradient tiles: tiles wave and wave+4 of dW3 (64x128, (t/4, t%4)) and of
-  // dW2 (128x64, (t/2, t%2)); one tile of dW1f (waves 0,1) or dW4pad (waves 2,3)
-  f32x16 accA[2], accB[2], accC = zero16();
-  accA[0] = accA[1] = accB[0] = accB[1] = zero16();
-  float bA[2] = {0.f, 0.f}, bB[2] = {0.f, 0.f}, db4 = 0.f;
-  const int bsA = 2 * wave, bsB = 4 * (wave & 1);   // bias-sum edge steps of this wave
+  for (int u = 0; u < TA; ++u) { accA[u] = accB[u] = zero16(); bA[u] = bB[u] = 0.f; }
+  // bias-sum edge steps: 4 waves read each dW3 row block, 2 waves each dW2 row block
+  const int bsA = (KS / 4) * (wave % 4), bsB = (KS / 2) * (wave % 2);
+  int par = 0;                                 // stage region parity (NREG == 2)
 
   CbfIn nx;
-  if ((long)blockIdx.x < nchunks) cbf_load<FUSED>(a, blockIdx.x, wave, r, E, EV, nx);
+  if ((long)blockIdx.x < nchunks) cbf_load<FUSED, NW>(a, blockIdx.x, wave, r, E, EV, nx);
   for (long chunk = blockIdx.x; chunk < nchunks; chunk += gridDim.x) {
     const CbfIn cur = nx;
-    if (chunk + gridDim.x < nchunks) cbf_load<FUSED>(a, chunk + gridDim.x, wave, r, E, EV, nx);   // prefetch
+    if (chunk + gridDim.x < nchunks) cbf_load<FUSED, NW>(a, chunk + gridDim.x, wave, r, E, EV, nx);   // prefetch
     const EdgeCtx& c = cur.c;
     const bf16x8 F = cbf_edge_frag(c.rel, c.eye, c.dfeat, c.ok, h);
     // one opaque base per LDS image per chunk: the per-lane address math is computed once and
@@ -391,7 +422,7 @@ __global__ __launch_bounds__(CBF_BWD_WAVES * 64, 1) void cbf_bwd_kernel(CbfBwdAr
       const float hm = (cur.in && c.mask) ? hs + vlc[256] : 0.f;
       if (h == 0) hx[erow] = hm;
       __syncthreads();
-      const float other = hx[(wave ^ 2) * 32 + r];
+      const float other = hx[(wave ^ (NW / 2)) * 32 + r];
       const float hv = pass_w == 0 ? hm : other;
       const float hnv = pass_w == 0 ? other : hm;
       float gh = 0.f, ghn = 0.f;
@@ -404,12 +435,11 @@ __global__ __launch_bounds__(CBF_BWD_WAVES * 64, 1) void cbf_bwd_kernel(CbfBwdAr
           const float ind_d = (-deriv + a.lc.eps_dang > 0.f) ? 1.f : 0.f;
           gh = cc * (a.lc.w_dang * ind_b + a.lc.w_dang_d * ind_d * (1.f - a.lc.dt_alpha));
           ghn = -cc * a.lc.w_dang_d * ind_d;
-          if (acc_here) {
-            lacc[0] += 1.f;
-            lacc[2] += fmaxf(hv + a.lc.eps_dang, 0.f);
-            lacc[4] += (hv <= 0.f) ? 1.f : 0.f;
-            lacc[6] += fmaxf(-deriv + a.lc.eps_dang, 0.f);
-            lacc[8] += (deriv >= 0.f) ? 1.f : 0.f;
+          if (acc_here) {   // loss sums live in LDS (registers are the limit at 2 waves/SIMD)
+            lacc[0][erow] += fmaxf(hv + a.lc.eps_dang, 0.f);
+            lacc[2][erow] += (hv <= 0.f) ? 1.f : 0.f;
+            lacc[4][erow] += fmaxf(-deriv + a.lc.eps_dang, 0.f);
+            lacc[6][erow] += (deriv >= 0.f) ? 1.f : 0.f;
           }
         } else {
           const float cc = a.lc.scale / ns;
@@ -418,11 +448,10 @@ __global__ __launch_bounds__(CBF_BWD_WAVES * 64, 1) void cbf_bwd_kernel(CbfBwdAr
           gh = cc * (-a.lc.w_safe * ind_b + a.lc.w_safe_d * ind_d * (1.f - a.lc.dt_alpha));
           ghn = -cc * a.lc.w_safe_d * ind_d;
           if (acc_here) {
-            lacc[1] += 1.f;
-            lacc[3] += fmaxf(-hv, 0.f);
-            lacc[5] += (hv > 0.f) ? 1.f : 0.f;
-            lacc[7] += fmaxf(-deriv, 0.f);
-            lacc[9] += (deriv > 0.f) ? 1.f : 0.f;
+            lacc[1][erow] += fmaxf(-hv, 0.f);
+            lacc[3][erow] += (hv > 0.f) ? 1.f : 0.f;
+            lacc[5][erow] += fmaxf(-deriv, 0.f);
+            lacc[7][erow] += (deriv > 0.f) ? 1.f : 0.f;
           }
         }
       }
@@ -449,19 +478,21 @@ __global__ __launch_bounds__(CBF_BWD_WAVES * 64, 1) void cbf_bwd_kernel(CbfBwdAr
       d3b[mt] = to_bf16x16(d3);
       H3b[mt] = to_bf16x16(H3p[mt]);
     }
-    // ---- stage A: dW3 (64x128) += dH3pre . H2^T ; db3   (tiles (u, wave))
+    // ---- stage A: dW3 (64x128) += dH3pre . H2^T ; db3   (tiles t = wave + NW u -> (t/4, t%4))
     {
-      bf16* imA = stg;
-      bf16* imB = stg + CBF_CH * SA64;
+      bf16* imA = stg + par * Cfg::REGION;
+      bf16* imB = imA + CH * SA64;
 #pragma unroll
       for (int mt = 0; mt < 2; ++mt) store_tile(imA, SA64, erow, 32 * mt, d3b[mt], h);
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt) store_tile(imB, SA128, erow, 32 * mt, H2b[mt], h);
       __syncthreads();
 #pragma unroll
-      for (int u = 0; u < 2; ++u)
-        bA[u] += stage_mma(imA, SA64, imB, SA128, u, wave, CBF_CH / 16, lane, accA[u], bsA, bsA + 2);
-      __syncthreads();
+      for (int u = 0; u < TA; ++u) {
+        const int t = wave + NW * u;
+        bA[u] += stage_mma(imA, SA64, imB, SA128, t / 4, t % 4, KS, lane, accA[u], bsA, bsA + KS / 4);
+      }
+      if constexpr (Cfg::NREG == 2) par ^= 1; else __syncthreads();
     }
     // ---- dH2pre = (W3^T dH3pre) . relu'(H2)
     bf16x16 d2b[4];
@@ -475,20 +506,21 @@ __global__ __launch_bounds__(CBF_BWD_WAVES * 64, 1) void cbf_bwd_kernel(CbfBwdAr
       d2b[mt] = to_bf16x16(t);
       mask_by_nonzero(d2b[mt], H2b[mt]);
     }
-    // ---- stage B: dW2 (128x64) += dH2pre . H1^T ; db2   (tiles ((wave>>1) + 2u, wave&1))
+    // ---- stage B: dW2 (128x64) += dH2pre . H1^T ; db2   (tiles t = wave + NW u -> (t/2, t%2))
     {
-      bf16* imA = stg;
-      bf16* imB = stg + CBF_CH * SA128;
+      bf16* imA = stg + par * Cfg::REGION;
+      bf16* imB = imA + CH * SA128;
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt) store_tile(imA, SA128, erow, 32 * mt, d2b[mt], h);
 #pragma unroll
       for (int mt = 0; mt < 2; ++mt) store_tile(imB, SA64, erow, 32 * mt, H1b[mt], h);
       __syncthreads();
 #pragma unroll
-      for (int u = 0; u < 2; ++u)
-        bB[u] += stage_mma(imA, SA128, imB, SA64, (wave >> 1) + 2 * u, wave & 1, CBF_CH / 16, lane, accB[u],
-                           bsB, bsB + 4);
-      __syncthreads();
+      for (int u = 0; u < TA; ++u) {
+        const int t = wave + NW * u;
+        bB[u] += stage_mma(imA, SA128, imB, SA64, t / 2, t % 2, KS, lane, accB[u], bsB, bsB + KS / 2);
+      }
+      if constexpr (Cfg::NREG == 2) par ^= 1; else __syncthreads();
     }
     // ---- dH1pre = (W2^T dH2pre) . relu'(H1)
     bf16x16 d1b[2];
@@ -519,79 +551,95 @@ __global__ __launch_bounds__(CBF_BWD_WAVES * 64, 1) void cbf_bwd_kernel(CbfBwdAr
         a.dE[cur.ev] = g;
       }
     }
-    // ---- stage C+D: dW1f (64x32) += dH1pre . F^T (waves 0,1);
-    //      dW4pad (32x64) += [dh;0] . relu(H3)^T -> row 0 = dw4 (waves 2,3)
+    // ---- stage C+D: dW1f (64x32) += dH1pre . [F|dh|0]^T (waves 0,1; cols >= 16 unused);
+    //      dW4pad (32x64) += [dh;0..] . relu(H3)^T, A = image cols 16..47 -> row 0 = dw4 (waves 2,3;
+    //      rows >= 1 read padding / the next row and are discarded: MFMA rows are independent)
     {
-      bf16* imC = stg;
-      bf16* imF = imC + CBF_CH * SA64;
-      bf16* imD = imF + CBF_CH * SA32;
-      bf16* imH = imD + CBF_CH * SA32;
+      bf16* imC = stg + par * Cfg::REGION;
+      bf16* imF = imC + CH * SA64;
+      bf16* imH = imF + CH * SA32;
 #pragma unroll
       for (int mt = 0; mt < 2; ++mt) store_tile(imC, SA64, erow, 32 * mt, d1b[mt], h);
 #pragma unroll
       for (int mt = 0; mt < 2; ++mt) store_tile(imH, SA64, erow, 32 * mt, H3b[mt], h);
-      bf16x8 z, dv;
+      bf16x8 dv;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) { z[j] = (bf16)0.f; dv[j] = (bf16)0.f; }
+      for (int j = 0; j < 8; ++j) dv[j] = (bf16)0.f;
       if (h == 0) dv[0] = (bf16)dhv;
       *reinterpret_cast<bf16x8*>(imF + erow * SA32 + 8 * h) = F;
-      *reinterpret_cast<bf16x8*>(imF + erow * SA32 + 16 + 8 * h) = z;
-      *reinterpret_cast<bf16x8*>(imD + erow * SA32 + 8 * h) = dv;
-      *reinterpret_cast<bf16x8*>(imD + erow * SA32 + 16 + 8 * h) = z;
+      *reinterpret_cast<bf16x8*>(imF + erow * SA32 + 16 + 8 * h) = dv;
       __syncthreads();
-      if (wave < 2) stage_mma(imC, SA64, imF, SA32, wave, 0, CBF_CH / 16, lane, accC);
-      else stage_mma(imD, SA32, imH, SA64, 0, wave - 2, CBF_CH / 16, lane, accC);
-      __syncthreads();
+      if (wave < 2) stage_mma(imC, SA64, imF, SA32, wave, 0, KS, lane, accC);
+      else if (wave < 4) stage_mma(imF + 16, SA32, imH, SA64, 0, wave - 2, KS, lane, accC);
+      if constexpr (Cfg::NREG == 2) par ^= 1; else __syncthreads();
     }
   }
+  __syncthreads();   // all stage reads done: the stage region is reused below
+  float* bred = reinterpret_cast<float*>(stg);        // [NW][192] bias partials: b3 (64) | b2 (128)
+  for (int q = threadIdx.x; q < NW * 192; q += blockDim.x) bred[q] = 0.f;
+  __syncthreads();
 
   // ---- per-workgroup slab
   float* P = a.partial + (long)blockIdx.x * CBF_PARTIAL;
 #pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    write_tile(P + P_W3, 128, u, wave, accA[u], lane);
-    write_tile(P + P_W2, 64, (wave >> 1) + 2 * u, wave & 1, accB[u], lane);
+  for (int u = 0; u < TA; ++u) {
+    const int t = wave + NW * u;
+    write_tile(P + P_W3, 128, t / 4, t % 4, accA[u], lane);
+    write_tile(P + P_W2, 64, t / 2, t % 2, accB[u], lane);
     const float s3 = bA[u] + shfl_xor32(bA[u]);
     const float s2 = bB[u] + shfl_xor32(bB[u]);
     if (h == 0) {
-      bred[wave][32 * u + r] = s3;
-      bred[wave][64 + 32 * ((wave >> 1) + 2 * u) + r] = s2;
+      bred[wave * 192 + 32 * (t / 4) + r] = s3;
+      bred[wave * 192 + 64 + 32 * (t / 2) + r] = s2;
     }
   }
   if (wave < 2) {
     write_tile(P + P_W1, 32, wave, 0, accC, lane);
-  } else {
+  } else if (wave < 4) {
     if (h == 0) P[P_W4 + 32 * (wave - 2) + r] = accC[0];   // dW4pad row 0 = dw4
   }
   // db4 (exact fp32) and loss sums: per-wave partials, fixed-order sums through LDS
   const float s4 = wave_sum(db4);
   if (lane == 0) red4[wave] = s4;
   if constexpr (FUSED) {
+    if (wave < NW / 2) {
 #pragma unroll
-    for (int q = 0; q < 10; ++q) {
-      const float v = wave_sum(lacc[q]);
-      if (lane == 0) lred[wave][q] = v;
+      for (int q = 0; q < 8; ++q) {
+        const float v = wave_sum(h == 0 ? lacc[q][erow] : 0.f);
+        if (lane == 0) lred[wave][2 + q] = v;
+      }
     }
   }
   __syncthreads();
   if (threadIdx.x < 192) {
     float t = 0.f;
-    for (int w = 0; w < CBF_BWD_WAVES; ++w) t += bred[w][threadIdx.x];
+    for (int w = 0; w < NW; ++w) t += bred[w * 192 + threadIdx.x];
     if (threadIdx.x < 64) P[P_B3 + threadIdx.x] = t;
     else P[P_B2 + threadIdx.x - 64] = t;
   }
   if (threadIdx.x == 0) {
     float t4 = 0.f;
-    for (int w = 0; w < CBF_BWD_WAVES; ++w) t4 += red4[w];
+    for (int w = 0; w < NW; ++w) t4 += red4[w];
     P[P_B4] = t4;
   }
   if (threadIdx.x >= 192 && threadIdx.x < 202) {
     const int q = threadIdx.x - 192;
     float t = 0.f;
-    if constexpr (FUSED)
-      for (int w = 0; w < CBF_BWD_WAVES; ++w) t += lred[w][q];
+    if constexpr (FUSED) {
+      if (q >= 2)
+        for (int w = 0; w < NW / 2; ++w) t += lred[w][q];
+      else if (blockIdx.x == 0)
+        t = a.counts[q];     // global pooled counts (slot layout kept for the two-kernel path)
+    }
     P[P_LOSS + q] = t;
   }
+}
+
+template <bool FUSED, int NW>
+static void launch_cbf_bwd(const CbfBwdArgs& a, int num_blocks, hipStream_t st) {
+  const size_t lds = CbfCfg<NW>::LDS;
+  (void)hipFuncSetAttribute((const void*)cbf_bwd_kernel<FUSED, NW>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipLaunchKernelGGL((cbf_bwd_kernel<FUSED, NW>), dim3(num_blocks), dim3(NW * 64), lds, st, a);
 }
 
 }  // namespace mb
@@ -600,13 +648,7 @@ extern "C" int mb_cbf_bwd(const mb::CbfBwdArgs* a, int num_blocks, hipStream_t s
   using namespace mb;
   if (a->K > 16 || a->K < 1 || a->passes < 1 || a->passes > 2) return -1;
   if (a->fused && (a->passes != 2 || !a->dang || !a->counts)) return -2;
-  const size_t lds = cbf_bwd_lds();
-  if (a->fused) {
-    (void)hipFuncSetAttribute((const void*)cbf_bwd_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL(cbf_bwd_kernel<true>, dim3(num_blocks), dim3(CBF_BWD_WAVES * 64), lds, st, *a);
-  } else {
-    (void)hipFuncSetAttribute((const void*)cbf_bwd_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL(cbf_bwd_kernel<false>, dim3(num_blocks), dim3(CBF_BWD_WAVES * 64), lds, st, *a);
-  }
+  if (a->fused) launch_cbf_bwd<true, CBF_NW>(*a, num_blocks, st);
+  else launch_cbf_bwd<false, CBF_NW>(*a, num_blocks, st);
   return (int)hipGetLastError();
 }
