@@ -503,9 +503,8 @@ __global__ __launch_bounds__(NB_WAVES * 64, 1) void ctrl_node_bwd_kernel(CtrlNod
         constexpr int kk = decltype(kk_)::value;
         c = mfma(wrmT_acc(W4 + opaque_zero(), NS4, 32 * mt, kk, lane), bacc_frag<kk & 1>(d4b), c);
       });
-#pragma unroll
-      for (int q = 0; q < 16; ++q) c[q] = ((float)Y3b[mt][q] > 0.f) ? c[q] : 0.f;
-      d3b[mt] = to_bf16x16(c);
+d3b[mt] = to_bf16x16(c);
+      mask_by_nonzero(d3b[mt], Y3b[mt]);
     }
     {   // S4: dWn4pad (32x64) += dY4 . Y3^T ; nb4
       bf16* imA = stg;
@@ -526,9 +525,8 @@ __global__ __launch_bounds__(NB_WAVES * 64, 1) void ctrl_node_bwd_kernel(CtrlNod
         constexpr int kk = decltype(kk_)::value;
         c = mfma(wrmT_acc(W3 + opaque_zero(), NS3, 32 * mt, kk, lane), bacc_frag<kk & 1>(d3b[kk >> 1]), c);
       });
-#pragma unroll
-      for (int q = 0; q < 16; ++q) c[q] = ((float)Y2b[mt][q] > 0.f) ? c[q] : 0.f;
-      d2b[mt] = to_bf16x16(c);
+d2b[mt] = to_bf16x16(c);
+      mask_by_nonzero(d2b[mt], Y2b[mt]);
     }
     {   // S3: dWn3 (64x128) += dY3 . Y2^T ; nb3
       bf16* imA = stg;
@@ -554,9 +552,8 @@ __global__ __launch_bounds__(NB_WAVES * 64, 1) void ctrl_node_bwd_kernel(CtrlNod
         constexpr int kk = decltype(kk_)::value;
         c = mfma(wrmT_acc(W2 + opaque_zero(), NS2, 32 * mt, kk, lane), bacc_frag<kk & 1>(d2b[kk >> 1]), c);
       });
-#pragma unroll
-      for (int q = 0; q < 16; ++q) c[q] = ((float)Y1b[mt][q] > 0.f) ? c[q] : 0.f;
-      d1b[mt] = to_bf16x16(c);
+d1b[mt] = to_bf16x16(c);
+      mask_by_nonzero(d1b[mt], Y1b[mt]);
     }
     {   // S2: dWn2 (128x64) += dY2 . Y1^T ; nb2
       bf16* imA = stg;
@@ -708,28 +705,32 @@ __global__ __launch_bounds__(EB_WAVES * 64, 2) void ctrl_edge_bwd_kernel(CtrlEdg
         relu_(c);
         H1b[mt] = to_bf16x16(c);
       }
-      // max-pool backward: this edge receives dP[f] where it was the argmax slot
-      // (all 16 loads of the agent's argmax/dP rows issued back to back)
-      bf16x8 dz[8];
+      // max-pool backward as an LDS scatter into the S1 image (rows = this wave's 32 edges =
+      // agents 2q, 2q+1 x 16 slots): zero the rows, then lane (r, h) routes dP[f] of agent 2q+h,
+      // f = 4r..4r+3, to row (h, argmax slot). One coalesced argmax/dP load per lane instead of
+      // 16 redundant row loads + 64 compare/selects per edge lane.
+      bf16* imS = stg;                                           // S1 dZ image, stride 136
       {
-        uint64_t amv[8];
-        bf16x8 dpv[8];
-        const uint8_t* arow = a.argmax + b * (int)a.am_env + i * 128;
-        const bf16* prow = a.dP + b * (int)a.dp_env + i * 128;
+        const u32x4 zero4 = {0u, 0u, 0u, 0u};
 #pragma unroll
-        for (int kk = 0; kk < 8; ++kk) {
-          const int f0 = 16 * kk + 8 * h;
-          amv[kk] = ok ? *reinterpret_cast<const uint64_t*>(arow + f0) : ~0ull;
-          dpv[kk] = *reinterpret_cast<const bf16x8*>(prow + f0);
+        for (int c8 = 0; c8 < 8; ++c8)
+          *reinterpret_cast<u32x4*>(imS + (wave * 32 + (lane >> 1)) * 136 + 64 * (lane & 1) + 8 * c8) = zero4;
+        const int ag = g0 + 2 * q + h;                          // agent of this half
+        if (ag < total) {
+          const int bb = ag / N, ii = ag - bb * N;
+          const unsigned am4 = *reinterpret_cast<const unsigned*>(a.argmax + bb * (int)a.am_env + ii * 128 + 4 * r);
+          const bf16x4 dp4 = *reinterpret_cast<const bf16x4*>(a.dP + bb * (int)a.dp_env + ii * 128 + 4 * r);
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj) {
+            const unsigned sl = (am4 >> (8 * jj)) & 0xFFu;
+            if (sl < 16u) imS[(wave * 32 + 16 * h + (int)sl) * 136 + 4 * r + jj] = dp4[jj];
+          }
         }
-#pragma unroll
-        for (int kk = 0; kk < 8; ++kk) {
-          bf16x8 v;
-#pragma unroll
-          for (int jj = 0; jj < 8; ++jj) v[jj] = (((amv[kk] >> (8 * jj)) & 0xFFull) == (uint64_t)slot) ? dpv[kk][jj] : z;
-          dz[kk] = v;
-        }
+        lds_wave_sync();
       }
+      bf16x8 dz[8];
+#pragma unroll
+      for (int kk = 0; kk < 8; ++kk) dz[kk] = *reinterpret_cast<const bf16x8*>(imS + erow * 136 + 16 * kk + 8 * h);
       // dH1 = W2^T dZ (natural k) . relu'(H1)
       bf16x16 d1b[2];
 #pragma unroll
@@ -737,9 +738,8 @@ __global__ __launch_bounds__(EB_WAVES * 64, 2) void ctrl_edge_bwd_kernel(CtrlEdg
         f32x16 c = zero16();
 #pragma unroll
         for (int kk = 0; kk < 8; ++kk) c = mfma(frag_ld(wt, 2 + mt * 8 + kk, lane), dz[kk], c);
-#pragma unroll
-        for (int qq = 0; qq < 16; ++qq) c[qq] = ((float)H1b[mt][qq] > 0.f) ? c[qq] : 0.f;
         d1b[mt] = to_bf16x16(c);
+        mask_by_nonzero(d1b[mt], H1b[mt]);
       }
       // dF = W1^T dH1 -> rows dx dy dvx dvy (lanes h == 0, regs 0..3)
       {
@@ -753,19 +753,19 @@ __global__ __launch_bounds__(EB_WAVES * 64, 2) void ctrl_edge_bwd_kernel(CtrlEdg
           a.dEc[b * (int)a.de_env + i * K + slot] = g;
         }
       }
-      // S1: dW2 (128x64) += dZ . H1^T ; eb2
+      // S1: dW2 (128x64) += dZ . H1^T ; eb2 (dZ is already in the image; bias-sum steps split
+      //     between the two waves that read each row block)
       {
         bf16* imA = stg;
         bf16* imB = stg + EB_CH * 136;
-#pragma unroll
-        for (int kk = 0; kk < 8; ++kk) *reinterpret_cast<bf16x8*>(imA + erow * 136 + 16 * kk + 8 * h) = dz[kk];
 #pragma unroll
         for (int mt = 0; mt < 2; ++mt) store_tile(imB, 72, erow, 32 * mt, H1b[mt], h);
         __syncthreads();
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
           const int t = wave + 4 * u;
-          bs[u] += stage_mma(imA, 136, imB, 72, t / 2, t % 2, EB_CH / 16, lane, accW2[u], 0, t % 2 == 0 ? EB_CH / 16 : 0);
+          bs[u] += stage_mma(imA, 136, imB, 72, t / 2, t % 2, EB_CH / 16, lane, accW2[u], 4 * (wave & 1),
+                             4 * (wave & 1) + 4);
         }
         __syncthreads();
       }
@@ -787,14 +787,22 @@ __global__ __launch_bounds__(EB_WAVES * 64, 2) void ctrl_edge_bwd_kernel(CtrlEdg
     }
   }
   float* P = a.partial + (long)blockIdx.x * CTRL_EDGE_PARTIAL;
+  __shared__ float ebred[EB_WAVES][2][32];
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
     const int t = wave + 4 * u;
     add_tile(P + EP_W2, 64, t / 2, t % 2, accW2[u], lane);
     const float s = bs[u] + shfl_xor32(bs[u]);
-    if (t % 2 == 0 && h == 0) P[EP_B2 + 32 * (t / 2) + r] += s;
+    if (h == 0) ebred[wave][u][r] = s;
   }
   if (wave < 2) add_tile(P + EP_W1, 32, wave, 0, accW1, lane);
+  __syncthreads();
+  // eb2 row block (wave>>1) + 2u was summed half by wave w and half by w^1: add in fixed order
+  if (threadIdx.x < 128) {
+    const int mt = threadIdx.x >> 5, rr = threadIdx.x & 31;    // row block 0..3
+    const int w0 = 2 * (mt & 1), u = mt >> 1;                   // waves w0, w0+1 own it
+    P[EP_B2 + 32 * mt + rr] += ebred[w0][u][rr] + ebred[w0 + 1][u][rr];
+  }
 }
 
 }  // namespace mb
