@@ -253,3 +253,18 @@ def test_prefetched_sampling_is_identical():
         b.train_step()
     torch.cuda.synchronize()
     assert torch.equal(a.fp.flat, b.fp.flat)
+
+
+def test_full_step_4096_agents_matches_oracle():
+    """BASELINE config #4 scale (4096 agents / env, LDS neighbour-tile stress) on a short horizon."""
+    from macbf_gnn_amd.engine.oracle_engine import OracleEngine
+    tr = _trainer(DEV, N=4096, B=2, T=3)
+    s0, g = tr.sample()
+    stats = tr.engine.step(s0, g)
+    g_hip = tr.fp.grad.clone()
+    OracleEngine(tr).step(s0, g)
+    g_ref = tr.fp.grad.clone()
+    for name in ("controller", "cbf"):
+        a_, b_ = tr.fp.ranges[name]
+        _cmp(g_hip[a_:b_], g_ref[a_:b_], name, rel=0.12, cos=0.99)
+    assert torch.isfinite(torch.as_tensor(float(stats["loss_total"])))
