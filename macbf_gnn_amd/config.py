@@ -44,6 +44,7 @@ NOISE_SCALE = 0.3
 # --- derived / fixed-by-reference constants -----------------------------------
 # eps inside the CBF distance feature: sqrt(sum(x^2 + 1e-4)) over 2 coords (cbf.py:24-25)
 CBF_DIST_EPS = 2e-4
+CBF_DIST_EPS_COORD = 1e-4          # per coordinate (D = 3: 3e-4)
 # loss margins (core.py:113, 155)
 LOSS_EPS_DANG = 1e-3
 # loss weights (train.py:93) and global scale (train.py:98)
@@ -87,6 +88,9 @@ class TrainConfig:
     nan_guard: bool = True            # skip the optimizer step when the reduced gradient is not finite
     phase_timing: bool = False        # per-phase device-event timings in the step stats
     prefetch_data: bool = True        # HIP: sample iteration i+1 on a side stream during iteration i
+    dim: int = 2                      # spatial dimension of the double integrator (2: reference, 3)
+    num_obstacles: int = 0            # static point-set obstacles per env (12 points each)
+    obstacle_points: int = 12
 
     def k_eff(self) -> int:
         return min(self.num_agents, self.top_k)

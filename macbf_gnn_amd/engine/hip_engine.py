@@ -35,6 +35,8 @@ class HipEngine:
         cfg = trainer.cfg
         self.bptt = cfg.bptt
         self.reuse = cfg.reuse_nbr_idx
+        if cfg.dim != 2 or cfg.num_obstacles:
+            raise NotImplementedError("HIP engine: 3-D / obstacle kernels not built yet")
         native.lib()
         self.dev = trainer.device
         self.B, self.N = cfg.num_envs, cfg.num_agents
@@ -139,7 +141,7 @@ class HipEngine:
         return bool(d.any(0).all())
 
     # ------------------------------------------------------------------ step
-    def step(self, s0, g):
+    def step(self, s0, g, obs=None):
         tr = self.tr
         cfg = tr.cfg
         B, N, K = self.B, self.N, self.K

@@ -21,7 +21,7 @@ class OracleEngine:
     def after_update(self):
         pass
 
-    def step(self, s0, g):
+    def step(self, s0, g, obs=None):
         tr = self.tr
         cfg = tr.cfg
         cp = tr.controller.params_dict()
@@ -29,11 +29,12 @@ class OracleEngine:
         traj = oracle.rollout(cp, s0, g, top_k=cfg.top_k, inner_loops=cfg.inner_loops,
                               bptt=cfg.bptt, early_stop=cfg.early_stop,
                               noise_prob=cfg.add_noise_prob, noise_scale=cfg.noise_scale,
-                              generator=tr.torch_gen, compute_safety=cfg.compute_safety)
+                              generator=tr.torch_gen, compute_safety=cfg.compute_safety, obs=obs)
         tr.timer.mark("rollout")
         T = traj["A"].shape[1]
         valid = traj["valid"]
-        dang = oracle.ttc_mask_knn(traj["S"][:, :T].detach(), traj["idx"])
+        s_d = traj["S"][:, :T].detach()
+        dang = oracle.ttc_mask_knn(s_d, traj["idx"], oracle.with_obstacles(s_d, obs))
         vmask = valid[..., None, None]
         N = s0.shape[1]
         counts = torch.stack([(dang & vmask).sum(), (~dang & vmask).sum(),
@@ -41,7 +42,7 @@ class OracleEngine:
         tr.dp.all_reduce_(counts)
         ncounts = {"n_dang": float(counts[0]), "n_safe": float(counts[1]), "n_act": float(counts[2])}
         losses, sums, act_sum = oracle.train_losses(cp, bp, traj, g, n_counts=ncounts,
-                                                    reuse_nbr_idx=cfg.reuse_nbr_idx, top_k=cfg.top_k)
+                                                    reuse_nbr_idx=cfg.reuse_nbr_idx, top_k=cfg.top_k, obs=obs)
         tr.timer.mark("losses")
         tr.fp.zero_grad()
         losses["total"].backward()

@@ -53,8 +53,10 @@ class Trainer:
         self.dp = dp
         self.device = device or resolve_device(cfg.device, dp.local_rank)
         torch.manual_seed(cfg.seed)
-        self.controller = Controller(4).to(self.device)
-        self.cbf = CBF(4).to(self.device)
+        if cfg.dim not in (2, 3):
+            raise ValueError("dim must be 2 or 3")
+        self.controller = Controller(2 * cfg.dim).to(self.device)
+        self.cbf = CBF(2 * cfg.dim).to(self.device)
         self.fp = FlatParams({"controller": self.controller, "cbf": self.cbf}, device=self.device)
         dp.broadcast_(self.fp.flat)
         self.opt = FlatAdam(self.fp, lr=cfg.lr, weight_decay=cfg.weight_decay)
@@ -78,39 +80,42 @@ class Trainer:
 
     # ------------------------------------------------------------------ data
     def sample(self, it: Optional[int] = None):
-        """B scenarios for this rank. HIP: on-device parallel sampler; CPU: host reference."""
+        """B scenarios for this rank -> (s0, g, obstacles or None). HIP: on-device parallel
+        sampler; CPU: host reference."""
         it = self.step_count if it is None else it
-        B, N = self.cfg.num_envs, self.cfg.num_agents
+        cfg = self.cfg
+        B, N = cfg.num_envs, cfg.num_agents
         if self.device.type == "cuda":
             from ..ops import scenario
-            return scenario.generate(B, N, seed=self.cfg.seed, iteration=it, rank=self.dp.rank,
-                                     device=self.device)
-        seed = (self.cfg.seed * 1_000_003 + it) * 4099 + self.dp.rank
-        return E.generate_batch(B, N, C.DIST_MIN_THRES, seed=seed)
+            return scenario.generate(B, N, seed=cfg.seed, iteration=it, rank=self.dp.rank, device=self.device,
+                                     dim=cfg.dim, num_obstacles=cfg.num_obstacles, obstacle_points=cfg.obstacle_points)
+        seed = (cfg.seed * 1_000_003 + it) * 4099 + self.dp.rank
+        return E.generate_scenarios(B, N, cfg.dim, cfg.num_obstacles, seed=seed)
 
     def _sample_async(self, it: int):
         """Launch the (parameter-independent) scenario sampler for iteration ``it`` on a side
         stream: it overlaps the current iteration's rollout instead of serialising with it."""
         with torch.cuda.stream(self._side):
-            s, g = self.sample(it)
+            data = self.sample(it)
             ev = torch.cuda.Event()
             ev.record(self._side)
-        return it, s, g, ev
+        return it, data, ev
 
     def _take_sample(self):
         if self._side is None:
             return self.sample()
         nx = self._next
         if nx is not None and nx[0] == self.step_count:
-            _, s0, g, ev = nx
+            _, data, ev = nx
             cur = torch.cuda.current_stream(self.device)
             cur.wait_event(ev)
-            s0.record_stream(cur)
-            g.record_stream(cur)
+            for t in data:
+                if t is not None:
+                    t.record_stream(cur)
         else:
-            s0, g = self.sample()
+            data = self.sample()
         self._next = self._sample_async(self.step_count + 1)
-        return s0, g
+        return data
 
     def on_params_loaded(self):
         self.fp.rebind()
@@ -123,15 +128,16 @@ class Trainer:
             return ["controller", "cbf"]
         return ["controller"] if (self.step_count // k) % 2 == 0 else ["cbf"]
 
-    def train_step(self, s0=None, g=None):
+    def train_step(self, s0=None, g=None, obs=None):
         tm = self.timer
         tm.start()
         if s0 is None:
-            s0, g = self._take_sample()
+            s0, g, obs = self._take_sample()
         s0 = s0.to(self.device)
         g = g.to(self.device)
+        obs = obs.to(self.device) if obs is not None else None
         tm.mark("sample")
-        stats = self.engine.step(s0, g)
+        stats = self.engine.step(s0, g, obs)
         self.dp.all_reduce_(self.fp.grad)
         tm.mark("allreduce")
         # failure detection: a non-finite reduced gradient is identical on every

@@ -40,8 +40,85 @@ def generate_obstacle_rectangle(center, sides, num=12):
     return rect + np.asarray(center, dtype=np.float64)
 
 
-def side_length(num_agents: int) -> float:
-    return float(np.sqrt(max(1.0, num_agents / C.AGENT_DENSITY)))
+def side_length(num_agents: int, dim: int = 2) -> float:
+    """Side of the square (D=2, core.py:46) / cube (D=3) holding AGENT_DENSITY agents per unit."""
+    return float(max(1.0, num_agents / C.AGENT_DENSITY) ** (1.0 / dim))
+
+
+def generate_obstacle_sphere(center, radius, num=12):
+    """``num`` points spread over a sphere (Fibonacci lattice): the 3-D point-set obstacle."""
+    k = np.arange(num) + 0.5
+    phi = np.arccos(1.0 - 2.0 * k / num)
+    th = np.pi * (1.0 + 5 ** 0.5) * k
+    pts = np.stack([np.cos(th) * np.sin(phi), np.sin(th) * np.sin(phi), np.cos(phi)], 1) * radius
+    return np.asarray(center, dtype=np.float64) + pts
+
+
+def generate_obstacles(num_obstacles, L, dim=2, rng: np.random.Generator | None = None, points=12):
+    """``num_obstacles`` static point-set obstacles inside the arena -> (num_obstacles*points, D).
+    D = 2: alternating circles / rectangles (the reference generators, core.py:7-42);
+    D = 3: spheres."""
+    rng = rng or np.random.default_rng()
+    out = []
+    for q in range(num_obstacles):
+        c = rng.uniform(0.0, L, size=(dim,))
+        if dim == 3:
+            out.append(generate_obstacle_sphere(c, rng.uniform(0.1, 0.3), points))
+        elif q % 2 == 0:
+            out.append(generate_obstacle_circle(c, rng.uniform(0.1, 0.3), points))
+        else:
+            out.append(generate_obstacle_rectangle(c, rng.uniform(0.2, 0.6, size=(2,)), points))
+    if not out:
+        return np.zeros((0, dim), dtype=np.float32)
+    return np.concatenate(out, 0).astype(np.float32)
+
+
+def _rsa(n, dim, thres, sample, rng, fixed=None):
+    """Sequential rejection sampling of n points, each > thres from every earlier point and
+    from the fixed points (obstacles)."""
+    pts = np.zeros((n, dim), dtype=np.float32)
+    fixed = np.zeros((0, dim), dtype=np.float32) if fixed is None else fixed
+    i = 0
+    tries = 0
+    while i < n:
+        cand = sample(i)
+        tries += 1
+        prev = np.concatenate([pts[:i], fixed], 0)
+        if prev.shape[0] and np.min(np.linalg.norm(prev - cand, axis=1)) <= thres:
+            if tries > 1000 * n:
+                raise RuntimeError("scenario sampler: arena too crowded")
+            continue
+        pts[i] = cand
+        i += 1
+    return pts
+
+
+def generate_data_nd(num_agents, dim=2, dist_min_thres=C.DIST_MIN_THRES, rng=None, obstacles=None):
+    """D-dimensional scenario (starts at rest, goals within GOAL_SPREAD per coordinate), with
+    starts and goals kept > dist_min_thres from each other and from the obstacle points."""
+    rng = rng or np.random.default_rng()
+    L = side_length(num_agents, dim)
+    st = _rsa(num_agents, dim, dist_min_thres, lambda i: rng.uniform(size=(dim,)) * L, rng, obstacles)
+    gl = _rsa(num_agents, dim, dist_min_thres,
+              lambda i: rng.uniform(-C.GOAL_SPREAD, C.GOAL_SPREAD, size=(dim,)) + st[i], rng, obstacles)
+    states = np.concatenate([st, np.zeros_like(st)], 1).astype(np.float32)
+    return states, gl.astype(np.float32)
+
+
+def generate_scenarios(num_envs, num_agents, dim=2, num_obstacles=0, seed=0, dist_min_thres=C.DIST_MIN_THRES):
+    """Host sampler for batched D-dimensional scenarios with obstacles ->
+    (s (B,N,2D), g (B,N,D), obs (B,M,D) or None). D = 2 without obstacles is ``generate_batch``."""
+    if dim == 2 and num_obstacles == 0:
+        s, g = generate_batch(num_envs, num_agents, dist_min_thres, seed)
+        return s, g, None
+    rng = np.random.default_rng(seed)
+    S, G, O = [], [], []
+    for _ in range(num_envs):
+        obs = generate_obstacles(num_obstacles, side_length(num_agents, dim), dim, rng)
+        s_, g_ = generate_data_nd(num_agents, dim, dist_min_thres, rng, obs if num_obstacles else None)
+        S.append(s_); G.append(g_); O.append(obs)
+    obs_t = torch.from_numpy(np.stack(O)) if num_obstacles else None
+    return torch.from_numpy(np.stack(S)), torch.from_numpy(np.stack(G)), obs_t
 
 
 def generate_data(num_agents, dist_min_thres, rng: np.random.Generator | None = None):

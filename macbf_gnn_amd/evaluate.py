@@ -120,7 +120,7 @@ def evaluate(controller, cbf, cfg: EvalConfig, device: Optional[torch.device] = 
     for ep in range(cfg.episodes):
         if device.type == "cuda":
             from .ops import scenario
-            s0, g = scenario.generate(cfg.num_envs, cfg.num_agents, seed=cfg.seed + 7919, iteration=ep, rank=0,
+            s0, g, _ = scenario.generate(cfg.num_envs, cfg.num_agents, seed=cfg.seed + 7919, iteration=ep, rank=0,
                                       device=device)
         else:
             s0, g = E.generate_batch(cfg.num_envs, cfg.num_agents, C.DIST_MIN_THRES, seed=cfg.seed * 7919 + ep)

@@ -21,8 +21,8 @@ from .. import oracle
 class CBF(nn.Module):
     def __init__(self, in_dim: int = 4):
         super().__init__()
-        if in_dim != 4:
-            raise NotImplementedError("2-D double integrator only (in_dim=4); see SURVEY 2.5")
+        if in_dim not in (4, 6):
+            raise NotImplementedError("double integrator in 2-D (in_dim=4) or 3-D (in_dim=6)")
         self.in_dim = in_dim
         self.cbf_net = nn.Sequential(
             nn.Conv1d(in_dim + 2, 64, (1,)), nn.ReLU(),
@@ -34,17 +34,20 @@ class CBF(nn.Module):
     def params_dict(self):
         return dict(self.named_parameters())
 
-    def forward(self, states: torch.Tensor, idx: torch.Tensor | None = None, top_k: int = C.TOP_K):
-        """states (N,4) -> h (N,1,K) [reference layout]; states (...,N,4) -> h (...,N,K)."""
+    def forward(self, states: torch.Tensor, idx: torch.Tensor | None = None, top_k: int = C.TOP_K,
+                obstacles: torch.Tensor | None = None):
+        """states (N,2D) -> h (N,1,K) [reference layout]; states (...,N,2D) -> h (...,N,K).
+        ``obstacles`` (M,D) / (B,M,D): static points that join the neighbour graph."""
         single = states.dim() == 2
         s = states.unsqueeze(0) if single else states
-        if idx is None:
-            idx = oracle.knn_idx(s.detach(), top_k) if s.device.type == "cpu" else None
         if s.device.type == "cpu":
-            h = oracle.cbf_forward(self.params_dict(), s, idx)
+            nodes = oracle.with_obstacles(s, obstacles)
+            if idx is None:
+                idx = oracle.knn_idx(s.detach(), top_k, nodes.detach())
+            h = oracle.cbf_forward(self.params_dict(), s, idx, nodes=nodes)
         else:
             from ..ops import cbf as cbf_ops
-            h = cbf_ops.cbf_apply(self, s, idx, top_k)
+            h = cbf_ops.cbf_apply(self, s, idx, top_k, obstacles=obstacles)
         if single:
             return h[0].unsqueeze(1)          # (N, 1, K)
         return h

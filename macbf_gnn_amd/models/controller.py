@@ -19,34 +19,36 @@ from .. import oracle
 class Controller(nn.Module):
     def __init__(self, in_dim: int = 4):
         super().__init__()
-        if in_dim != 4:
-            raise NotImplementedError("2-D double integrator only (in_dim=4); see SURVEY 2.5")
+        if in_dim not in (4, 6):
+            raise NotImplementedError("double integrator in 2-D (in_dim=4) or 3-D (in_dim=6)")
         self.in_dim = in_dim
         self.controller_centr_net = nn.Sequential(
             nn.Conv1d(in_dim + 1, 64, (1,)), nn.ReLU(),
             nn.Conv1d(64, 128, (1,)), nn.ReLU(),
         )
         self.controller_dec_net = nn.Sequential(
-            nn.Linear(128 + 4, 64), nn.ReLU(),
+            nn.Linear(128 + in_dim, 64), nn.ReLU(),
             nn.Linear(64, 128), nn.ReLU(),
             nn.Linear(128, 64), nn.ReLU(),
-            nn.Linear(64, 4),
+            nn.Linear(64, in_dim),
         )
 
     def params_dict(self):
         return dict(self.named_parameters())
 
     def forward(self, states: torch.Tensor, goals: torch.Tensor, idx: torch.Tensor | None = None,
-                top_k: int = C.TOP_K):
-        """states (N,4), goals (N,2) -> a (N,2); batched (...,N,4),(...,N,2) -> (...,N,2)."""
+                top_k: int = C.TOP_K, obstacles: torch.Tensor | None = None):
+        """states (N,2D), goals (N,D) -> a (N,D); batched (...,N,2D),(...,N,D) -> (...,N,D).
+        ``obstacles`` (M,D) / (B,M,D): static points that join the neighbour graph."""
         single = states.dim() == 2
         s = states.unsqueeze(0) if single else states
         g = goals.unsqueeze(0) if single else goals
         if s.device.type == "cpu":
+            nodes = oracle.with_obstacles(s, obstacles)
             if idx is None:
-                idx = oracle.knn_idx(s.detach(), top_k)
-            a = oracle.controller_forward(self.params_dict(), s, g, idx)
+                idx = oracle.knn_idx(s.detach(), top_k, nodes.detach())
+            a = oracle.controller_forward(self.params_dict(), s, g, idx, nodes=nodes)
         else:
             from ..ops import ctrl as ctrl_ops
-            a = ctrl_ops.controller_apply(self, s, g, idx, top_k)
+            a = ctrl_ops.controller_apply(self, s, g, idx, top_k, obstacles=obstacles)
         return a[0] if single else a

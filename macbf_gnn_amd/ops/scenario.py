@@ -20,8 +20,12 @@ def _mix(*xs) -> int:
     return h
 
 
-def generate(B, N, *, seed=0, iteration=0, rank=0, device=None, out=None):
+def generate(B, N, *, seed=0, iteration=0, rank=0, device=None, out=None, dim=2, num_obstacles=0,
+             obstacle_points=12):
+    """-> (s0 (B,N,2D), g (B,N,D), obstacles (B,M,D) or None)."""
     device = device or torch.device("cuda")
+    if dim != 2 or num_obstacles:
+        raise NotImplementedError("on-device sampler: 2-D without obstacles (3-D / obstacles: see generate_nd)")
     if out is None:
         S = torch.empty(B, N, 4, dtype=torch.float32, device=device)
         G = torch.empty(B, N, 2, dtype=torch.float32, device=device)
@@ -29,4 +33,4 @@ def generate(B, N, *, seed=0, iteration=0, rank=0, device=None, out=None):
         S, G = out
     native.scenario(S, G, seed=_mix(seed, iteration, rank), L=E.side_length(N), r=C.DIST_MIN_THRES,
                     spread=C.GOAL_SPREAD)
-    return S, G
+    return S, G, None

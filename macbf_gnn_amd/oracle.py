@@ -12,8 +12,11 @@ section 2.4 defect register:
   masked mean.
 * h' = CBF(s') on the time-t neighbour set (D10, ``reuse_nbr_idx``).
 
-Shapes: B envs, T steps, N agents, K neighbour slots. Functions accept any leading batch
-dims ``...`` in front of (N, ·).
+Shapes: B envs, T steps, N agents, K neighbour slots; state dim 2D = (position D, velocity D)
+for the D-dimensional double integrator (D = 2: the reference; D = 3: BASELINE config #5).
+Functions accept any leading batch dims ``...`` in front of (N, ·). Static obstacles
+ enter as extra non-controlled graph nodes: ``nodes = cat(s, [o, 0])``; agents
+are the first N nodes, so agent i is node i and self stays at kNN slot 0.
 Reference cites: kNN ``core.py:234-250``; controller ``controller.py:31-63``; CBF
 ``cbf.py:21-45``; TTC ``core.py:187-231``; losses ``core.py:89-184``; loop ``train.py:48-105``.
 """
@@ -29,33 +32,60 @@ from . import config as C
 
 
 # ----------------------------------------------------------------------------- graph
-def knn_idx(s: torch.Tensor, k: int) -> torch.Tensor:
-    """Indices of the k nearest agents (positions = s[..., :2]), nearest first.
+def sdim(s: torch.Tensor) -> int:
+    """Spatial dimension D of a (..., 2D) double-integrator state."""
+    return s.shape[-1] // 2
 
-    Ties are broken by the lower agent index (stable sort); the HIP scan compares (d2, index)
+
+def with_obstacles(s: torch.Tensor, obs: Optional[torch.Tensor]) -> torch.Tensor:
+    """Graph nodes: the N agents followed by the M static obstacle points (velocity 0)."""
+    if obs is None:
+        return s
+    # obs is (B, M, D) (or (M, D)); s is (B, ..., N, 2D): broadcast over the middle dims
+    if obs.dim() == 2:
+        obs = obs.unsqueeze(0)
+    o = obs.reshape(obs.shape[0], *([1] * (s.dim() - obs.dim())), *obs.shape[1:])
+    o = o.expand(*s.shape[:-2], *obs.shape[-2:])
+    return torch.cat([s, torch.cat([o.to(s.dtype), torch.zeros_like(o, dtype=s.dtype)], -1)], -2)
+
+
+def sq_dist(d: torch.Tensor, D: int) -> torch.Tensor:
+    """sum_d d_d^2 accumulated in coordinate order (matches the kernels' fp32 order)."""
+    out = d[..., 0] * d[..., 0]
+    for q in range(1, D):
+        out = out + d[..., q] * d[..., q]
+    return out
+
+
+def knn_idx(s: torch.Tensor, k: int, nodes: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Indices (into ``nodes``, default the agents) of the k nearest nodes of every agent,
+    nearest first.
+
+    Ties are broken by the lower node index (stable sort); the HIP scan compares (d2, index)
     lexicographically, so it produces the same lists in any candidate order. Self is slot 0
-    unless another agent sits exactly on it with a lower index.
+    unless another node sits exactly on it with a lower index.
     """
-    p = s[..., :2]
-    d = p.unsqueeze(-2) - p.unsqueeze(-3)            # (..., N, N, 2): p_i - p_j
-    d2 = d[..., 0] * d[..., 0] + d[..., 1] * d[..., 1]
-    k = min(k, s.shape[-2])
+    nodes = s if nodes is None else nodes
+    D = sdim(s)
+    d = s[..., :D].unsqueeze(-2) - nodes[..., :D].unsqueeze(-3)      # (..., N, Nn, D): p_i - p_j
+    d2 = sq_dist(d, D)
+    k = min(k, nodes.shape[-2])
     return torch.sort(d2, dim=-1, stable=True).indices[..., :k]
 
 
 def gather_nbrs(s: torch.Tensor, idx: torch.Tensor) -> torch.Tensor:
-    """s (..., N, C), idx (..., N, K) -> s_j (..., N, K, C)."""
+    """s (..., Nn, C) nodes, idx (..., N, K) into them -> s_j (..., N, K, C)."""
     lead = s.shape[:-2]
-    N, Cc = s.shape[-2:]
-    K = idx.shape[-1]
-    sf = s.reshape(-1, N, Cc)
+    Nn, Cc = s.shape[-2:]
+    N, K = idx.shape[-2:]
+    sf = s.reshape(-1, Nn, Cc)
     ix = idx.reshape(-1, N * K, 1).expand(-1, -1, Cc)
     return torch.gather(sf, 1, ix).reshape(*lead, N, K, Cc)
 
 
-def edge_rel(s: torch.Tensor, idx: torch.Tensor):
-    """Relative state s_i - s_j (..., N, K, 4) and the self indicator (..., N, K)."""
-    sj = gather_nbrs(s, idx)
+def edge_rel(s: torch.Tensor, idx: torch.Tensor, nodes: Optional[torch.Tensor] = None):
+    """Relative state s_i - s_j (..., N, K, 2D) and the self indicator (..., N, K)."""
+    sj = gather_nbrs(s if nodes is None else nodes, idx)
     rel = s.unsqueeze(-2) - sj
     ar = torch.arange(s.shape[-2], device=s.device).view(*([1] * (idx.dim() - 2)), -1, 1)
     eye = (idx == ar).to(s.dtype)
@@ -66,15 +96,20 @@ def edge_rel(s: torch.Tensor, idx: torch.Tensor):
 def ttc_dangerous(rel: torch.Tensor, eye: torch.Tensor, r: float, ttc: float) -> torch.Tensor:
     """Time-to-collision danger test on relative states (core.py:187-209 / 212-231).
 
-    Self pairs are shifted to p=(1,1) via ``eye`` (core.py:193-194). fp32 throughout.
+    Self pairs are shifted to p=(1,..,1) via ``eye`` (core.py:193-194). fp32 throughout.
     """
-    x = rel[..., 0] + eye
-    y = rel[..., 1] + eye
-    vx = rel[..., 2]
-    vy = rel[..., 3]
-    alpha = vx * vx + vy * vy
-    beta = 2.0 * (x * vx + y * vy)
-    gamma = x * x + y * y - r * r
+    D = rel.shape[-1] // 2
+    p = [rel[..., q] + eye for q in range(D)]
+    v = [rel[..., D + q] for q in range(D)]
+    alpha = v[0] * v[0]
+    pv = p[0] * v[0]
+    pp = p[0] * p[0]
+    for q in range(1, D):
+        alpha = alpha + v[q] * v[q]
+        pv = pv + p[q] * v[q]
+        pp = pp + p[q] * p[q]
+    beta = 2.0 * pv
+    gamma = pp - r * r
     disc = beta * beta - 4.0 * alpha * gamma
     dist_dang = gamma < 0
     two_pos = (disc > 0) & (gamma > 0) & (beta < 0)
@@ -82,23 +117,24 @@ def ttc_dangerous(rel: torch.Tensor, eye: torch.Tensor, r: float, ttc: float) ->
     return dist_dang | (two_pos & lt)
 
 
-def ttc_mask_knn(s: torch.Tensor, idx: torch.Tensor) -> torch.Tensor:
+def ttc_mask_knn(s: torch.Tensor, idx: torch.Tensor, nodes: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Training danger mask on the top-K pairs, r=DIST_MIN_THRES, ttc=TIME_TO_COLLISION."""
-    rel, eye = edge_rel(s, idx)
+    rel, eye = edge_rel(s, idx, nodes)
     return ttc_dangerous(rel, eye, C.DIST_MIN_THRES, C.TIME_TO_COLLISION)
 
 
-def ttc_mask_all_pairs(s: torch.Tensor) -> torch.Tensor:
-    """Check mask on all pairs (core.py:212-231) -> (..., N, N) bool."""
-    rel = s.unsqueeze(-2) - s.unsqueeze(-3)
-    N = s.shape[-2]
-    eye = torch.eye(N, dtype=s.dtype, device=s.device).expand(rel.shape[:-1])
+def ttc_mask_all_pairs(s: torch.Tensor, nodes: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Check mask of every agent against every node (core.py:212-231) -> (..., N, Nn) bool."""
+    nodes = s if nodes is None else nodes
+    rel = s.unsqueeze(-2) - nodes.unsqueeze(-3)
+    N, Nn = s.shape[-2], nodes.shape[-2]
+    eye = torch.eye(N, Nn, dtype=s.dtype, device=s.device).expand(rel.shape[:-1])
     return ttc_dangerous(rel, eye, C.DIST_MIN_CHECK, C.TIME_TO_COLLISION_CHECK)
 
 
-def safe_agent_count(s: torch.Tensor) -> torch.Tensor:
+def safe_agent_count(s: torch.Tensor, nodes: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Number of agents with no dangerous pair, per leading index (train.py:74-75)."""
-    return (~ttc_mask_all_pairs(s).any(-1)).sum(-1)
+    return (~ttc_mask_all_pairs(s, nodes).any(-1)).sum(-1)
 
 
 # ----------------------------------------------------------------------------- networks
@@ -108,45 +144,47 @@ def _lin(x, w, b):
     return F.linear(x, w, b)
 
 
-def controller_forward(p: Dict[str, torch.Tensor], s, g, idx, return_aux=False):
+def controller_forward(p: Dict[str, torch.Tensor], s, g, idx, return_aux=False, nodes=None):
     """Gain-scheduled GNN controller (controller.py:31-63), intended semantics.
 
     ``p`` is the controller ``state_dict`` (or named parameters) keyed like the reference.
+    D-dimensional: edge input [s_i - s_j, eye] (2D+1), node input [pooled, p - g, v] (128+2D),
+    2D gains, a_d = -(k_{2d} (p_d - g_d) + k_{2d+1} v_d) (D = 2: the reference law).
     """
-    rel, eye = edge_rel(s, idx)
-    x = torch.cat([rel, eye.unsqueeze(-1)], dim=-1)                     # (...,N,K,5)
-    dist = torch.sqrt(rel[..., 0] ** 2 + rel[..., 1] ** 2)
+    D = sdim(s)
+    rel, eye = edge_rel(s, idx, nodes)
+    x = torch.cat([rel, eye.unsqueeze(-1)], dim=-1)                     # (...,N,K,2D+1)
+    dist = torch.sqrt(sq_dist(rel, D))
     mask = (dist < C.OBS_RADIUS).to(s.dtype)                            # strict, no eps
     h = F.relu(_lin(x, p["controller_centr_net.0.weight"], p["controller_centr_net.0.bias"]))
     h = F.relu(_lin(h, p["controller_centr_net.2.weight"], p["controller_centr_net.2.bias"]))
     pooled = (h * mask.unsqueeze(-1)).max(dim=-2).values                # (...,N,128)
-    z = torch.cat([pooled, s[..., :2] - g, s[..., 2:4]], dim=-1)
+    z = torch.cat([pooled, s[..., :D] - g, s[..., D:2 * D]], dim=-1)
     for i, act in ((0, True), (2, True), (4, True), (6, False)):
         z = _lin(z, p[f"controller_dec_net.{i}.weight"], p[f"controller_dec_net.{i}.bias"])
         if act:
             z = F.relu(z)
     k = 2.0 * torch.sigmoid(z) + 0.2
-    ex = s[..., 0] - g[..., 0]
-    ey = s[..., 1] - g[..., 1]
-    ax = -(k[..., 0] * ex + k[..., 1] * s[..., 2])
-    ay = -(k[..., 2] * ey + k[..., 3] * s[..., 3])
-    a = torch.stack([ax, ay], dim=-1)
+    a = torch.stack([-(k[..., 2 * q] * (s[..., q] - g[..., q]) + k[..., 2 * q + 1] * s[..., D + q])
+                     for q in range(D)], dim=-1)
     if return_aux:
         return a, {"gains": k, "pooled": pooled, "mask": mask}
     return a
 
 
-def cbf_features(s, idx):
-    rel, eye = edge_rel(s, idx)
-    d = torch.sqrt(rel[..., 0] ** 2 + rel[..., 1] ** 2 + C.CBF_DIST_EPS)
+def cbf_features(s, idx, nodes=None):
+    D = sdim(s)
+    rel, eye = edge_rel(s, idx, nodes)
+    d = torch.sqrt(sq_dist(rel, D) + C.CBF_DIST_EPS_COORD * D)
     x = torch.cat([rel, eye.unsqueeze(-1), (d - C.DIST_MIN_THRES).unsqueeze(-1)], dim=-1)
     mask = (d <= C.OBS_RADIUS).to(s.dtype)
     return x, mask
 
 
-def cbf_forward(p: Dict[str, torch.Tensor], s, idx):
-    """Per-edge barrier h(x_i, x_j) (cbf.py:21-45) -> (..., N, K); masked by radius."""
-    x, mask = cbf_features(s, idx)
+def cbf_forward(p: Dict[str, torch.Tensor], s, idx, nodes=None):
+    """Per-edge barrier h(x_i, x_j) (cbf.py:21-45) -> (..., N, K); masked by radius.
+    Edge input [s_i - s_j, eye, |p_i - p_j|_eps - r] (2D + 2 channels)."""
+    x, mask = cbf_features(s, idx, nodes)
     z = x
     for i, act in ((0, True), (2, True), (4, True), (6, False)):
         z = _lin(z, p[f"cbf_net.{i}.weight"], p[f"cbf_net.{i}.bias"])
@@ -157,9 +195,9 @@ def cbf_forward(p: Dict[str, torch.Tensor], s, idx):
 
 # ----------------------------------------------------------------------------- losses
 def action_ref(s, g):
-    """a_ref = [p-g, v] K_ref^T with K_ref = -[[1,0,sqrt3,0],[0,1,0,sqrt3]] (core.py:175-178)."""
-    return torch.stack([-((s[..., 0] - g[..., 0]) + C.SQRT3 * s[..., 2]),
-                        -((s[..., 1] - g[..., 1]) + C.SQRT3 * s[..., 3])], dim=-1)
+    """a_ref = [p-g, v] K_ref^T with K_ref = -[I, sqrt3 I] (core.py:175-178; D = 2 there)."""
+    D = sdim(s)
+    return torch.stack([-((s[..., q] - g[..., q]) + C.SQRT3 * s[..., D + q]) for q in range(D)], dim=-1)
 
 
 def action_loss_terms(s, g, a):
@@ -218,7 +256,7 @@ def finalize_losses(sums, n_act_sum, n_act):
 # ----------------------------------------------------------------------------- rollout
 def rollout(ctrl_params, s0, g, *, top_k=C.TOP_K, inner_loops=C.INNER_LOOPS, bptt=True,
             early_stop=True, noise_prob=0.0, noise_scale=C.NOISE_SCALE, generator=None,
-            compute_safety=False):
+            compute_safety=False, obs=None):
     """Batched rollout with per-env done masks (train.py:58-81).
 
     Returns dict with S (B,T+1,N,4), A (B,T,N,2), idx (B,T,N,K), valid (B,T) bool,
@@ -228,21 +266,24 @@ def rollout(ctrl_params, s0, g, *, top_k=C.TOP_K, inner_loops=C.INNER_LOOPS, bpt
     s = s0
     active = torch.ones(B, dtype=torch.bool, device=s0.device)
     S, A, I, V, D, SF = [s0], [], [], [], [], []
+    dim = sdim(s0)
     for _ in range(inner_loops):
-        idx = knn_idx(s.detach(), top_k)
-        a = controller_forward(ctrl_params, s, g, idx)
+        nodes = with_obstacles(s, obs)
+        idx = knn_idx(s.detach(), top_k, nodes.detach())
+        a = controller_forward(ctrl_params, s, g, idx, nodes=nodes)
         if noise_prob > 0:
             coin = torch.rand(B, generator=generator, device=s.device) < noise_prob
             nz = torch.randn(a.shape, generator=generator, device=s.device) * noise_scale
             a = a + nz * coin[:, None, None].to(a.dtype)
-        s_next = s + torch.cat([s[..., 2:], a], -1) * C.TIME_STEP
-        dist = torch.linalg.norm(s_next[..., :2] - g, dim=-1).mean(-1)
+        s_next = s + torch.cat([s[..., dim:], a], -1) * C.TIME_STEP
+        dist = torch.linalg.norm(s_next[..., :dim] - g, dim=-1).mean(-1)
         V.append(active.clone())
         A.append(a)
         I.append(idx)
         D.append(dist.detach())
         if compute_safety:
-            SF.append(safe_agent_count(s_next.detach()))
+            sn = s_next.detach()
+            SF.append(safe_agent_count(sn, with_obstacles(sn, obs)))
         S.append(s_next)
         active = active & ~(dist.detach() < C.DIST_MIN_CHECK)
         s = s_next if bptt else s_next.detach()
@@ -259,7 +300,7 @@ def rollout(ctrl_params, s0, g, *, top_k=C.TOP_K, inner_loops=C.INNER_LOOPS, bpt
 
 
 def train_losses(ctrl_params, cbf_params, traj, g, *, n_counts: Optional[Dict] = None,
-                 reuse_nbr_idx=True, top_k=C.TOP_K):
+                 reuse_nbr_idx=True, top_k=C.TOP_K, obs=None):
     """All losses of one iteration from a rollout (train.py:83-98, intended semantics).
 
     ``n_counts`` overrides the pooled counts (n_dang, n_safe, n_act) -- used by DP so that
@@ -271,10 +312,12 @@ def train_losses(ctrl_params, cbf_params, traj, g, *, n_counts: Optional[Dict] =
     S_in = traj.get("S_in", S)
     s_t = S_in[:, :T]
     s_n = S[:, 1:T + 1]
-    h = cbf_forward(cbf_params, s_t, idx)
-    idx_n = idx if reuse_nbr_idx else knn_idx(s_n.detach(), top_k)
-    hn = cbf_forward(cbf_params, s_n, idx_n)
-    dang = ttc_mask_knn(S[:, :T].detach(), idx)
+    h = cbf_forward(cbf_params, s_t, idx, nodes=with_obstacles(s_t, obs))
+    nodes_n = with_obstacles(s_n, obs)
+    idx_n = idx if reuse_nbr_idx else knn_idx(s_n.detach(), top_k, nodes_n.detach())
+    hn = cbf_forward(cbf_params, s_n, idx_n, nodes=nodes_n)
+    s_d = S[:, :T].detach()
+    dang = ttc_mask_knn(s_d, idx, with_obstacles(s_d, obs))
     sums = cbf_loss_sums(h, hn, dang, valid)
     gg = g.unsqueeze(1).expand(-1, T, -1, -1)
     act = action_loss_terms(s_t, gg, A)

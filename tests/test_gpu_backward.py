@@ -168,7 +168,7 @@ def test_full_step_grad_matches_oracle(bptt, reuse):
     BPTT / no-BPTT and h' on the time-t or on the recomputed time-(t+1) neighbour slots."""
     from macbf_gnn_amd.engine.oracle_engine import OracleEngine
     tr = _trainer(DEV, bptt=bptt, reuse_nbr_idx=reuse)
-    s0, g = tr.sample()
+    s0, g, _ = tr.sample()
     stats = tr.engine.step(s0, g)
     g_hip = tr.fp.grad.clone()
     orc = OracleEngine(tr)
@@ -182,7 +182,7 @@ def test_full_step_grad_matches_oracle(bptt, reuse):
 
 def test_full_step_deterministic():
     tr = _trainer(DEV, N=64, B=3, T=4)
-    s0, g = tr.sample()
+    s0, g, _ = tr.sample()
     tr.engine.step(s0, g)
     g1 = tr.fp.grad.clone()
     tr.engine.step(s0, g)
@@ -259,7 +259,7 @@ def test_full_step_4096_agents_matches_oracle():
     """BASELINE config #4 scale (4096 agents / env, LDS neighbour-tile stress) on a short horizon."""
     from macbf_gnn_amd.engine.oracle_engine import OracleEngine
     tr = _trainer(DEV, N=4096, B=2, T=3)
-    s0, g = tr.sample()
+    s0, g, _ = tr.sample()
     stats = tr.engine.step(s0, g)
     g_hip = tr.fp.grad.clone()
     OracleEngine(tr).step(s0, g)

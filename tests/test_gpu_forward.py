@@ -170,7 +170,7 @@ def test_cbf_fwd_h_losses_grads(B, T, N):
 def test_scenario_invariants():
     from macbf_gnn_amd.ops import scenario
     for N in (8, 32, 1024):
-        S, G = scenario.generate(4, N, seed=3, device=DEV)
+        S, G, _ = scenario.generate(4, N, seed=3, device=DEV)
         torch.cuda.synchronize()
         L = math.sqrt(max(1.0, N / 8.0))
         p = S[..., :2]

@@ -108,8 +108,8 @@ def test_nan_guard_skips_optimizer_step():
     before = t.fp.flat.clone()
     real_step = t.engine.step
 
-    def poisoned(s0, g0):
-        st = real_step(s0, g0)
+    def poisoned(s0, g0, obs=None):
+        st = real_step(s0, g0, obs)
         t.fp.grad[3] = float("nan")
         return st
 
