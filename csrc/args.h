@@ -8,16 +8,19 @@ typedef __bf16 bf16;
 namespace mb {
 
 struct CellSortArgs {
-  const float4* S;  long s_env;      // agent (b,i) state at S[b*s_env + i]
-  int B, N;
+  const float4* S;  long s_env;      // node (b,i) record at S[(b*s_env + i) * rec]
+  int B, N;                          // N = graph nodes (agents + obstacle points)
+  int rec;                           // float4s per node record (1: 2-D, 2: 3-D)
   float L;                           // scenario side length (curve grid spans [0, L]^2)
   int* perm;                         // (B, N) position on the curve -> agent id
 };
 
 struct ScanArgs {
-  const float4* S;  long s_env;      // agent (b,i) state at S[b*s_env + i]
-  const int* perm;                   // (B, N) Hilbert order from cell_sort
-  int B, N, K;
+  const float4* S;  long s_env;      // node (b,i) record at S[(b*s_env + i) * REC<dim>]
+  const int* perm;                   // (B, Nn) Hilbert order from cell_sort
+  int B, N, K;                       // N agents (centres; the first N nodes)
+  int Nn;                            // graph nodes: agents + static obstacle points
+  int dim;
   int* idx;         long i_env;      // (b,i,k) at idx[b*i_env + i*K + k]
   uint8_t* dang;                     // same indexing as idx (may be null)
   float* cnt;       long c_env;      // cnt[b*c_env + {0: dangerous edges, 1: safe edges}]
@@ -27,8 +30,10 @@ struct ScanArgs {
 };
 
 struct ScenArgs {
-  float4* S;      // (B, N) states out (x, y, 0, 0)
-  float2* G;      // (B, N) goals out
+  float4* S;      long s_env;     // node records out (agents only; velocity 0), strides in records
+  float* G;       // (B, N, D) goals out
+  const float* obs; int M;        // (B, M, D) static obstacle points (conflict points) or M = 0
+  int dim;
   int B, N;
   float L, r, spread;
   unsigned long long seed;
@@ -37,19 +42,20 @@ struct ScenArgs {
 };
 
 struct CtrlArgs {
-  const float4* S;  long s_env;       // states at step t: (b,i) -> S[b*s_env + i]
-  const float2* G;                    // goals (b,i) -> G[b*N + i]
+  const float4* S;  long s_env;       // node records at step t: (b,i) -> S[(b*s_env + i) * REC]
+  int dim;                            // 2 or 3; vectors below hold D floats per agent
+  const float* G;                     // goals (b,i,d) -> G[(b*N + i)*D + d]
   const int* idx;   long i_env;       // (b,i,k) -> idx[b*i_env + i*K + k]
   int B, N, K;
   const bf16* wpack;                  // packed ctrl fragments
   int f_edge;                         // fragment offset of ew1f (ew2 follows)
   int f_node;                         // fragment offset of nw1f (nw2, nw3, nw4 follow)
   const float* wvec;                  // eb2|nb2|nb3|nb4 (CTRL_VEC floats)
-  float2* A;        long a_env;       // actions out (may be null)
-  float4* Snext;    long sn_env;      // next states out (may be null)
+  float* A;         long a_env;       // actions out (b,i,d) -> A[(b*a_env + i)*D + d] (may be null)
+  float4* Snext;    long sn_env;      // next-state records out (may be null)
   float* dist_sum;  long d_env;       // per-env sum of |p' - g| (may be null)
   float* act_sum;   long ac_env;      // per-env sum of |‖a‖² - ‖a_ref‖²| (may be null)
-  const float2* noise; long n_env;    // additive action noise (may be null)
+  const float* noise; long n_env;     // additive action noise (b,i,d) (may be null)
   float dt, obs_r, sqrt3;
   bf16* pooled;     long p_env;       // (b,i,128) max-pooled edge features out (bf16), or null
   uint8_t* argmax;  long am_env;      // (b,i,128) winning slot per feature (0xFF: no grad), or null
@@ -60,7 +66,8 @@ struct LossConsts {
 };
 
 struct CbfFwdArgs {
-  const float4* S;  long s_env, s_step;   // state of (b,t,i): S[b*s_env + t*s_step + i]
+  const float4* S;  long s_env, s_step;   // node record of (b,t,i): S[(b*s_env + t*s_step + i) * REC]
+  int dim;                                 // 2 or 3
   const int* idx;                          // (T,B,N,K) contiguous (time-major)
   const uint8_t* dang;                     // (T,B,N,K) or null (all safe)
   const uint8_t* valid;                    // (T,B) or null (all valid)
@@ -78,7 +85,8 @@ struct CbfFwdArgs {
 };
 
 struct CbfBwdArgs {
-  const float4* S;  long s_env, s_step;   // state of (b,t,i): S[b*s_env + t*s_step + i]
+  const float4* S;  long s_env, s_step;   // node record of (b,t,i): S[(b*s_env + t*s_step + i) * REC]
+  int dim;                                 // 2 or 3
   const int* idx;                          // (T,B,N,K) time-major
   const int* idx1;                         // neighbour slots of pass 1 (null = idx: reuse_nbr_idx)
   int B, T, N, K;
@@ -87,7 +95,7 @@ struct CbfBwdArgs {
   const bf16* wpack; int f_bwd;            // fragment offset of w1f (w2,w3,w3t,w2t,w1ft follow)
   const bf16* wrm;                         // row-major W2 [128][72] | W3 [64][136] images
   const float* wvec;
-  float4* dE;                              // (passes, E) dL/d(s_i - s_j) per evaluation, or null
+  float4* dE;                              // (passes, E) records of dL/d(s_i - s_j), or null
   float* partial;                          // (gridDim.x, CBF_PARTIAL) per-workgroup dW slabs
   float obs_r, dist_thr, dist_eps;
   // fused training mode (passes == 2): dh is computed in-kernel from h(s_t), h'(s_{t+1}) of the
@@ -102,10 +110,11 @@ struct CbfBwdArgs {
 
 struct CtrlNodeBwdArgs {
   const bf16* pooled;  long p_env;     // (b,i,128) pooled edge features of step t (rollout)
-  const float4* S;     long s_env;     // states s_t
-  const float2* G;                     // goals (B,N)
-  const float2* A;     long a_env;     // actions a_t as applied (incl. noise)
-  const float4* Gn;    long gn_env;    // G_{t+1} = dL/ds_{t+1} (or null)
+  const float4* S;     long s_env;     // node records s_t
+  int dim;
+  const float* G;                      // goals (B,N,D)
+  const float* A;      long a_env;     // actions a_t as applied (incl. noise), D per agent
+  const float4* Gn;    long gn_env;    // G_{t+1} = dL/ds_{t+1} records (or null)
   const uint8_t* valid; long v_env;    // valid[b*v_env] for this step (or null = all valid)
   int B, N;
   const bf16* wrm;                     // row-major node images
@@ -113,25 +122,27 @@ struct CtrlNodeBwdArgs {
   const float* wvec;                   // controller side vector (eb2|nb2|nb3|nb4)
   float act_coef, dt, sqrt3;
   bf16* dP;            long dp_env;    // (b,i,128) dL/dpooled out
-  float4* ego;                         // (B,N) dL/ds_t from the node path + gain law + action loss
+  float4* ego;                         // (B,N) records: dL/ds_t from the node path + gain law + action loss
   float* partial;                      // (gridDim.x, CTRL_NODE_PARTIAL) slabs, accumulated
 };
 
 struct CtrlEdgeBwdArgs {
-  const float4* S;     long s_env;
+  const float4* S;     long s_env;     // node records (strides in records)
+  int dim;
   const int* idx;      long i_env;
   const uint8_t* argmax; long am_env;  // (b,i,128) winning slot per pooled feature
   const bf16* dP;      long dp_env;    // (b,i,128)
   int B, N, K;
   const bf16* wpack;   int f_ew1f, f_ew2tn;   // packed fragments (ew2tn followed by ew1ft)
-  float4* dEc;         long de_env;    // (b,i,K) dL/d(s_i - s_j) out
+  float4* dEc;         long de_env;    // (b,i,K) records of dL/d(s_i - s_j) out
   float* partial;                      // (gridDim.x, CTRL_EDGE_PARTIAL) slabs, accumulated
 };
 
 struct CsrArgs {
-  const int* idx;      // (G, N, K) neighbour indices of G = B*T graphs
+  const int* idx;      // (G, N, K) neighbour indices of G = B*T graphs (N centres)
   int G, N, K;
-  int* ptr;            // (G, N+1) incoming-edge offsets
+  int Nn;              // target nodes (agents + obstacle points); 0 = N
+  int* ptr;            // (G, Nn+1) incoming-edge offsets
   int* edges;          // (G, N*K) incoming edge ids (i*K + k), self edges excluded
 };
 
@@ -141,10 +152,13 @@ struct NodeRedArgs {
   int B, T, N, K, passes, accumulate;
   float4* out;         // (T+1, B, N)
   int pass_mask;       // bit p: include pass p (0 -> all passes)
+  int Nn;              // CSR target nodes per graph (0 = N)
+  int dim;
   int shift1;          // pass 1 edges belong to graph t + shift1 (1: h' on recomputed kNN of s_{t+1})
 };
 
 struct CombineArgs {
+  int dim;                            // records of REC<dim> float4s; strides in records
   const float4* dS;   long ds_env;    // direct grads at step t (B,N) view
   const float4* ego;                  // (B,N) contiguous or null
   const float4* dEc;                  // (B,N,K) controller edge grads at step t or null

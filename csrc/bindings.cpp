@@ -16,16 +16,18 @@ template <typename T>
 static T* P(u64 p) { return reinterpret_cast<T*>(static_cast<uintptr_t>(p)); }
 static hipStream_t ST(u64 s) { return reinterpret_cast<hipStream_t>(static_cast<uintptr_t>(s)); }
 
-static int cell_sort(u64 S, long s_env, int B, int N, float L, u64 perm, u64 stream) {
+static int cell_sort(u64 S, long s_env, int B, int N, float L, u64 perm, int rec, u64 stream) {
   mb::CellSortArgs a{};
+  a.rec = rec;
   a.S = P<const float4>(S); a.s_env = s_env; a.B = B; a.N = N; a.L = L; a.perm = P<int>(perm);
   return mb_cell_sort(&a, ST(stream));
 }
 
 static int scan(u64 S, long s_env, u64 perm, int B, int N, int K, u64 idx, long i_env, u64 dang, u64 cnt, long c_env,
                 u64 safe, long sf_env, float r2_train, float ttc_train, float r2_check, float ttc_check,
-                int do_knn, int do_safety, u64 stream) {
+                int do_knn, int do_safety, int Nn, int dim, u64 stream) {
   mb::ScanArgs a{};
+  a.Nn = Nn; a.dim = dim;
   a.S = P<const float4>(S); a.s_env = s_env; a.perm = P<const int>(perm); a.B = B; a.N = N; a.K = K;
   a.idx = P<int>(idx); a.i_env = i_env; a.dang = P<uint8_t>(dang);
   a.cnt = P<float>(cnt); a.c_env = c_env; a.safe = P<float>(safe); a.sf_env = sf_env;
@@ -34,10 +36,11 @@ static int scan(u64 S, long s_env, u64 perm, int B, int N, int K, u64 idx, long 
   return mb_scan(&a, ST(stream));
 }
 
-static int scenario(u64 S, u64 G, int B, int N, float L, float r, float spread, u64 seed, int max_rounds,
-                    u64 status, u64 stream) {
+static int scenario(u64 S, long s_env, u64 G, u64 obs, int M, int dim, int B, int N, float L, float r, float spread,
+                    u64 seed, int max_rounds, u64 status, u64 stream) {
   mb::ScenArgs a{};
-  a.S = P<float4>(S); a.G = P<float2>(G); a.B = B; a.N = N; a.L = L; a.r = r; a.spread = spread;
+  a.S = P<float4>(S); a.s_env = s_env; a.G = P<float>(G); a.obs = P<const float>(obs); a.M = M; a.dim = dim;
+  a.B = B; a.N = N; a.L = L; a.r = r; a.spread = spread;
   a.seed = seed; a.max_rounds = max_rounds; a.status = P<int>(status);
   return mb_scenario(&a, ST(stream));
 }
@@ -45,22 +48,24 @@ static int scenario(u64 S, u64 G, int B, int N, float L, float r, float spread, 
 static int ctrl_fwd(u64 S, long s_env, u64 G, u64 idx, long i_env, int B, int N, int K, u64 wpack, int f_edge,
                     int f_node, u64 wvec, u64 A, long a_env, u64 Sn, long sn_env, u64 dist_sum, long d_env,
                     u64 act_sum, long ac_env, u64 noise, long n_env, float dt, float obs_r, float sqrt3,
-                    u64 pooled, long p_env, u64 argmax, long am_env, int num_cu, u64 stream) {
+                    u64 pooled, long p_env, u64 argmax, long am_env, int dim, int num_cu, u64 stream) {
   mb::CtrlArgs a{};
-  a.S = P<const float4>(S); a.s_env = s_env; a.G = P<const float2>(G); a.idx = P<const int>(idx); a.i_env = i_env;
+  a.dim = dim;
+  a.S = P<const float4>(S); a.s_env = s_env; a.G = P<const float>(G); a.idx = P<const int>(idx); a.i_env = i_env;
   a.B = B; a.N = N; a.K = K; a.wpack = P<const bf16>(wpack); a.f_edge = f_edge; a.f_node = f_node;
-  a.wvec = P<const float>(wvec); a.A = P<float2>(A); a.a_env = a_env; a.Snext = P<float4>(Sn); a.sn_env = sn_env;
+  a.wvec = P<const float>(wvec); a.A = P<float>(A); a.a_env = a_env; a.Snext = P<float4>(Sn); a.sn_env = sn_env;
   a.dist_sum = P<float>(dist_sum); a.d_env = d_env; a.act_sum = P<float>(act_sum); a.ac_env = ac_env;
-  a.noise = P<const float2>(noise); a.n_env = n_env; a.dt = dt; a.obs_r = obs_r; a.sqrt3 = sqrt3;
+  a.noise = P<const float>(noise); a.n_env = n_env; a.dt = dt; a.obs_r = obs_r; a.sqrt3 = sqrt3;
   a.pooled = P<bf16>(pooled); a.p_env = p_env; a.argmax = P<uint8_t>(argmax); a.am_env = am_env;
   return mb_ctrl_fwd(&a, num_cu, ST(stream));
 }
 
 static int cbf_fwd(u64 S, long s_env, long s_step, u64 idx, u64 dang, u64 valid, int B, int T, int N, int K,
                    int two, u64 wpack, int f_fwd, u64 wvec, u64 h_out, u64 hn_out, u64 dh_out, u64 counts,
-                   u64 partial, py::tuple lc, float obs_r, float dist_thr, float dist_eps, int num_blocks,
+                   u64 partial, py::tuple lc, float obs_r, float dist_thr, float dist_eps, int dim, int num_blocks,
                    u64 stream) {
   mb::CbfFwdArgs a{};
+  a.dim = dim;
   a.S = P<const float4>(S); a.s_env = s_env; a.s_step = s_step; a.idx = P<const int>(idx);
   a.dang = P<const uint8_t>(dang); a.valid = P<const uint8_t>(valid);
   a.B = B; a.T = T; a.N = N; a.K = K; a.two = two;
@@ -77,8 +82,9 @@ static int cbf_fwd(u64 S, long s_env, long s_step, u64 idx, u64 dang, u64 valid,
 static int cbf_bwd(u64 S, long s_env, long s_step, u64 idx, int B, int T, int N, int K, int passes, u64 dh,
                    u64 wpack, int f_bwd, u64 wrm, u64 wvec, u64 dE, u64 partial, float obs_r, float dist_thr,
                    float dist_eps, int fused, u64 dang, u64 valid, u64 counts, py::tuple lc, u64 idx1,
-                   int num_blocks, u64 stream) {
+                   int dim, int num_blocks, u64 stream) {
   mb::CbfBwdArgs a{};
+  a.dim = dim;
   a.idx1 = P<const int>(idx1);
   a.fused = fused; a.dang = P<const uint8_t>(dang); a.valid = P<const uint8_t>(valid);
   a.counts = P<const float>(counts);
@@ -93,24 +99,27 @@ static int cbf_bwd(u64 S, long s_env, long s_step, u64 idx, int B, int T, int N,
   return mb_cbf_bwd(&a, num_blocks, ST(stream));
 }
 
-static int rev_csr(u64 idx, int G, int N, int K, u64 ptr, u64 edges, u64 stream) {
+static int rev_csr(u64 idx, int G, int N, int K, u64 ptr, u64 edges, int Nn, u64 stream) {
   mb::CsrArgs a{};
+  a.Nn = Nn;
   a.idx = P<const int>(idx); a.G = G; a.N = N; a.K = K; a.ptr = P<int>(ptr); a.edges = P<int>(edges);
   return mb_rev_csr(&a, ST(stream));
 }
 
 static int node_reduce(u64 dE, u64 ptr, u64 edges, int B, int T, int N, int K, int passes, int accumulate, u64 out,
-                       int pass_mask, int shift1, u64 stream) {
+                       int pass_mask, int shift1, int Nn, int dim, u64 stream) {
   mb::NodeRedArgs a{};
-  a.pass_mask = pass_mask; a.shift1 = shift1;
+  a.pass_mask = pass_mask; a.shift1 = shift1; a.Nn = Nn; a.dim = dim;
   a.dE = P<const float4>(dE); a.ptr = P<const int>(ptr); a.edges = P<const int>(edges);
   a.B = B; a.T = T; a.N = N; a.K = K; a.passes = passes; a.accumulate = accumulate; a.out = P<float4>(out);
   return mb_node_reduce(&a, ST(stream));
 }
 
 static int node_combine(u64 dS, long ds_env, u64 ego, u64 dEc, u64 ptr, long ptr_env, u64 edges, long edges_env,
-                        u64 Gn, long gn_env, u64 Gout, long go_env, int B, int N, int K, float dt, u64 stream) {
+                        u64 Gn, long gn_env, u64 Gout, long go_env, int B, int N, int K, float dt, int dim,
+                        u64 stream) {
   mb::CombineArgs a{};
+  a.dim = dim;
   a.dS = P<const float4>(dS); a.ds_env = ds_env; a.ego = P<const float4>(ego); a.dEc = P<const float4>(dEc);
   a.ptr = P<const int>(ptr); a.ptr_env = ptr_env; a.edges = P<const int>(edges); a.edges_env = edges_env;
   a.Gn = P<const float4>(Gn); a.gn_env = gn_env; a.Gout = P<float4>(Gout); a.go_env = go_env;
@@ -133,10 +142,11 @@ static int adam(u64 param, u64 grad, u64 m, u64 v, int lo, int hi, float b1, flo
 static int ctrl_node_bwd(u64 pooled, long p_env, u64 S, long s_env, u64 G, u64 A, long a_env, u64 Gn, long gn_env,
                          u64 valid, long v_env, int B, int N, u64 wrm, int o1, int o2, int o3, int o4, u64 wvec,
                          float act_coef, float dt, float sqrt3, u64 dP, long dp_env, u64 ego, u64 partial,
-                         int num_blocks, u64 stream) {
+                         int dim, int num_blocks, u64 stream) {
   mb::CtrlNodeBwdArgs a{};
+  a.dim = dim;
   a.pooled = P<const bf16>(pooled); a.p_env = p_env; a.S = P<const float4>(S); a.s_env = s_env;
-  a.G = P<const float2>(G); a.A = P<const float2>(A); a.a_env = a_env; a.Gn = P<const float4>(Gn); a.gn_env = gn_env;
+  a.G = P<const float>(G); a.A = P<const float>(A); a.a_env = a_env; a.Gn = P<const float4>(Gn); a.gn_env = gn_env;
   a.valid = P<const uint8_t>(valid); a.v_env = v_env; a.B = B; a.N = N; a.wrm = P<const bf16>(wrm);
   a.o_w1 = o1; a.o_w2 = o2; a.o_w3 = o3; a.o_w4 = o4; a.wvec = P<const float>(wvec);
   a.act_coef = act_coef; a.dt = dt; a.sqrt3 = sqrt3; a.dP = P<bf16>(dP); a.dp_env = dp_env;
@@ -146,8 +156,9 @@ static int ctrl_node_bwd(u64 pooled, long p_env, u64 S, long s_env, u64 G, u64 A
 
 static int ctrl_edge_bwd(u64 S, long s_env, u64 idx, long i_env, u64 argmax, long am_env, u64 dP, long dp_env,
                          int B, int N, int K, u64 wpack, int f_ew1f, int f_ew2tn, u64 dEc, long de_env, u64 partial,
-                         int num_blocks, u64 stream) {
+                         int dim, int num_blocks, u64 stream) {
   mb::CtrlEdgeBwdArgs a{};
+  a.dim = dim;
   a.S = P<const float4>(S); a.s_env = s_env; a.idx = P<const int>(idx); a.i_env = i_env;
   a.argmax = P<const uint8_t>(argmax); a.am_env = am_env; a.dP = P<const bf16>(dP); a.dp_env = dp_env;
   a.B = B; a.N = N; a.K = K; a.wpack = P<const bf16>(wpack); a.f_ew1f = f_ew1f; a.f_ew2tn = f_ew2tn;

@@ -16,6 +16,7 @@
 #pragma clang fp contract(off)
 #include "common.h"
 #include "args.h"
+#include "state.h"
 
 #ifndef CBF_NW
 #define CBF_NW 8   // waves per CBF-backward workgroup (4: one per SIMD, 8: two per SIMD)
@@ -28,22 +29,38 @@ constexpr int CBF_VEC = 260;       // b2 128 | b3 64 | w4 64 | b4 1 (+3 pad)
 
 
 
-DEV bf16x8 cbf_edge_frag(float4 rel, float eye, float dfeat, bool ok, int h) {
+// Layer-1 B fragment of one edge (K slots: see layout.cbf_w1_slot): fp32 features split into
+// bf16 hi (lanes h = 0) and residual lo (lanes h = 1) parts.
+template <int D>
+DEV bf16x8 cbf_edge_frag(const float (&rp)[D], const float (&rv)[D], float eye, float dfeat, bool ok, int h) {
   bf16x8 f;
   const bf16 z = (bf16)0.f;
 #pragma unroll
   for (int j = 0; j < 8; ++j) f[j] = z;
   if (!ok) return f;
-  bf16 hx, lx, hy, ly, hvx, lvx, hvy, lvy, hd, ld;
-  split_bf16(rel.x, hx, lx);
-  split_bf16(rel.y, hy, ly);
-  split_bf16(rel.z, hvx, lvx);
-  split_bf16(rel.w, hvy, lvy);
-  split_bf16(dfeat, hd, ld);
-  if (h == 0) {
-    f[0] = hx; f[1] = hy; f[2] = hvx; f[3] = hvy; f[4] = (bf16)eye; f[5] = hd; f[6] = (bf16)1.f;
+  bf16 hi[2 * D + 1], lo[2 * D + 1];
+#pragma unroll
+  for (int q = 0; q < D; ++q) {
+    split_bf16(rp[q], hi[q], lo[q]);
+    split_bf16(rv[q], hi[D + q], lo[D + q]);
+  }
+  split_bf16(dfeat, hi[2 * D], lo[2 * D]);
+  if constexpr (D == 2) {
+    if (h == 0) {
+      f[0] = hi[0]; f[1] = hi[1]; f[2] = hi[2]; f[3] = hi[3]; f[4] = (bf16)eye; f[5] = hi[4]; f[6] = (bf16)1.f;
+    } else {
+      f[0] = lo[0]; f[1] = lo[1]; f[2] = lo[2]; f[3] = lo[3]; f[5] = lo[4];
+    }
   } else {
-    f[0] = lx; f[1] = ly; f[2] = lvx; f[3] = lvy; f[5] = ld;
+    if (h == 0) {
+#pragma unroll
+      for (int q = 0; q < 7; ++q) f[q] = hi[q];
+      f[7] = (bf16)1.f;
+    } else {
+#pragma unroll
+      for (int q = 0; q < 7; ++q) f[q] = lo[q];
+      f[7] = (bf16)eye;
+    }
   }
   return f;
 }
@@ -91,21 +108,24 @@ DEV float cbf_mlp(const bf16x8& F, const bf16* wl, const float* vl, int lane, Cb
   return s + b4;
 }
 
+template <int D>
 struct EdgeCtx {
   bool ok;
   int b, t, i, j;
-  float4 rel;
+  float rp[D], rv[D];     // s_i - s_j: positions, velocities
   float eye, d, dfeat;
   bool mask;
 };
 
 // 32-bit index math throughout (host asserts passes*E < 2^31): 64-bit divisions/multiplies
-// here cost dozens of VGPRs and instructions per edge.
+// here cost dozens of VGPRs and instructions per edge. Strides are in node records.
+template <int D>
 DEV void cbf_edge(const float4* S, long s_env, long s_step, const int* idx, int B, int N, int K,
-                  long e_, long E_, int tstep_off, float obs_r, float dist_thr, float dist_eps, EdgeCtx& c) {
+                  long e_, long E_, int tstep_off, float obs_r, float dist_thr, float dist_eps, EdgeCtx<D>& c) {
   const unsigned e = (unsigned)e_;
   c.ok = e_ < E_;
-  c.rel = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+  for (int q = 0; q < D; ++q) { c.rp[q] = 0.f; c.rv[q] = 0.f; }
   c.eye = 0.f; c.d = 0.f; c.dfeat = 0.f; c.mask = false;
   c.b = c.t = c.i = c.j = 0;
   if (!c.ok) return;
@@ -116,17 +136,19 @@ DEV void cbf_edge(const float4* S, long s_env, long s_step, const int* idx, int 
   c.t = (int)(tb / (unsigned)B);
   c.b = (int)(tb - (unsigned)c.t * (unsigned)B);
   c.j = idx[e];
-  const float4* Sb = S + ((unsigned)c.b * (unsigned)s_env + (unsigned)(c.t + tstep_off) * (unsigned)s_step);
-  const float4 si = Sb[c.i];
-  const float4 sj = Sb[c.j];
-  c.rel = make_float4(si.x - sj.x, si.y - sj.y, si.z - sj.z, si.w - sj.w);
+  const float4* Sb = S + ((unsigned)c.b * (unsigned)s_env + (unsigned)(c.t + tstep_off) * (unsigned)s_step) * REC<D>;
+  float pi[D], vi[D], pj[D], vj[D];
+  load_rec<D>(Sb, (unsigned)c.i, pi, vi);
+  load_rec<D>(Sb, (unsigned)c.j, pj, vj);
+#pragma unroll
+  for (int q = 0; q < D; ++q) { c.rp[q] = pi[q] - pj[q]; c.rv[q] = vi[q] - vj[q]; }
   c.eye = (c.j == c.i) ? 1.f : 0.f;
-  c.d = sqrtf(c.rel.x * c.rel.x + c.rel.y * c.rel.y + dist_eps);
+  c.d = sqrtf(sqsum<D>(c.rp) + dist_eps);
   c.dfeat = c.d - dist_thr;
   c.mask = c.d <= obs_r;
 }
 
-template <int WAVES>
+template <int WAVES, int D>
 __global__ __launch_bounds__(WAVES * 64) void cbf_fwd_kernel(CbfFwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   bf16* wl = reinterpret_cast<bf16*>(smem);
@@ -146,16 +168,16 @@ __global__ __launch_bounds__(WAVES * 64) void cbf_fwd_kernel(CbfFwdArgs a) {
   CbfActs act;
   for (long tile = (long)blockIdx.x * WAVES + wave; tile < ntiles; tile += (long)gridDim.x * WAVES) {
     const long e = tile * 32 + r;
-    EdgeCtx c0;
+    EdgeCtx<D> c0;
     float hv = 0.f, hnv = 0.f;
     bool mask1 = false;
 #pragma unroll 1
     for (int pass = 0; pass < 1 + a.two; ++pass) {
       const bf16* wt = wl + opaque_zero();
       const float* vt = vl + opaque_zero();
-      EdgeCtx c;
-      cbf_edge(a.S, a.s_env, a.s_step, a.idx, a.B, a.N, a.K, e, E, pass, a.obs_r, a.dist_thr, a.dist_eps, c);
-      const float hp = cbf_mlp(cbf_edge_frag(c.rel, c.eye, c.dfeat, c.ok, h), wt, vt, lane, act);
+      EdgeCtx<D> c;
+      cbf_edge<D>(a.S, a.s_env, a.s_step, a.idx, a.B, a.N, a.K, e, E, pass, a.obs_r, a.dist_thr, a.dist_eps, c);
+      const float hp = cbf_mlp(cbf_edge_frag<D>(c.rp, c.rv, c.eye, c.dfeat, c.ok, h), wt, vt, lane, act);
       if (pass == 0) { c0 = c; hv = c.mask ? hp : 0.f; }
       else { hnv = c.mask ? hp : 0.f; mask1 = c.mask; }
     }
@@ -222,8 +244,13 @@ extern "C" int mb_cbf_fwd(const mb::CbfFwdArgs* a, int num_blocks, hipStream_t s
   using namespace mb;
   if (a->K > 16 || a->K < 1) return -1;
   const size_t lds = (size_t)CBF_FWD_FRAGS * FRAG_BYTES + CBF_VEC * 4;
-  (void)hipFuncSetAttribute((const void*)cbf_fwd_kernel<CBF_FWD_WAVES>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL(cbf_fwd_kernel<CBF_FWD_WAVES>, dim3(num_blocks), dim3(CBF_FWD_WAVES * 64), lds, st, *a);
+  if (a->dim == 3) {
+    (void)hipFuncSetAttribute((const void*)cbf_fwd_kernel<CBF_FWD_WAVES, 3>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL((cbf_fwd_kernel<CBF_FWD_WAVES, 3>), dim3(num_blocks), dim3(CBF_FWD_WAVES * 64), lds, st, *a);
+  } else {
+    (void)hipFuncSetAttribute((const void*)cbf_fwd_kernel<CBF_FWD_WAVES, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL((cbf_fwd_kernel<CBF_FWD_WAVES, 2>), dim3(num_blocks), dim3(CBF_FWD_WAVES * 64), lds, st, *a);
+  }
   return (int)hipGetLastError();
 }
 
@@ -268,16 +295,17 @@ template <int NW> struct CbfCfg {
   static constexpr size_t LDS = CBF_BWD_W_BYTES + CBF_VEC * 4 + (size_t)NREG * REGION * 2;
 };
 
+template <int D>
 struct CbfIn {
-  EdgeCtx c;
+  EdgeCtx<D> c;
   float dh;       // upstream gradient (non-fused)
   bool in;
   bool dg, vld;   // fused: danger bit, env-step validity
   unsigned ev;    // evaluation index (pass*E + e)
 };
 
-template <bool FUSED, int NW>
-DEV void cbf_load(const CbfBwdArgs& a, long chunk, int wave, int r, long E, long EV, CbfIn& x) {
+template <bool FUSED, int NW, int D>
+DEV void cbf_load(const CbfBwdArgs& a, long chunk, int wave, int r, long E, long EV, CbfIn<D>& x) {
   constexpr int CH = CbfCfg<NW>::CH;
   int pass;
   unsigned e;
@@ -294,7 +322,7 @@ DEV void cbf_load(const CbfBwdArgs& a, long chunk, int wave, int r, long E, long
     x.ev = ev;
   }
   const int* idxp = (pass == 1 && a.idx1) ? a.idx1 : a.idx;
-  cbf_edge(a.S, a.s_env, a.s_step, idxp, a.B, a.N, a.K, e, x.in ? E : 0, pass, a.obs_r, a.dist_thr, a.dist_eps, x.c);
+  cbf_edge<D>(a.S, a.s_env, a.s_step, idxp, a.B, a.N, a.K, e, x.in ? E : 0, pass, a.obs_r, a.dist_thr, a.dist_eps, x.c);
   if constexpr (FUSED) {
     x.dh = 0.f;
     x.dg = x.in && a.dang[e] != 0;
@@ -323,7 +351,7 @@ DEV void cbf_load(const CbfBwdArgs& a, long chunk, int wave, int r, long E, long
 //   wave forms its upstream dL/dh locally (barrier + derivative hinge losses with the danger
 //   bit, step validity and the global pooled counts) and the loss partial sums go to the slab.
 // ---------------------------------------------------------------------------------------
-template <bool FUSED, int NW>
+template <bool FUSED, int NW, int D>
 __global__ __launch_bounds__(NW * 64, 1) void cbf_bwd_kernel(CbfBwdArgs a) {
   using Cfg = CbfCfg<NW>;
   constexpr int CH = Cfg::CH, KS = Cfg::KS;
@@ -361,13 +389,13 @@ __global__ __launch_bounds__(NW * 64, 1) void cbf_bwd_kernel(CbfBwdArgs a) {
   const int bsA = (KS / 4) * (wave % 4), bsB = (KS / 2) * (wave % 2);
   int par = 0;                                 // stage region parity (NREG == 2)
 
-  CbfIn nx;
-  if ((long)blockIdx.x < nchunks) cbf_load<FUSED, NW>(a, blockIdx.x, wave, r, E, EV, nx);
+  CbfIn<D> nx;
+  if ((long)blockIdx.x < nchunks) cbf_load<FUSED, NW, D>(a, blockIdx.x, wave, r, E, EV, nx);
   for (long chunk = blockIdx.x; chunk < nchunks; chunk += gridDim.x) {
-    const CbfIn cur = nx;
-    if (chunk + gridDim.x < nchunks) cbf_load<FUSED, NW>(a, chunk + gridDim.x, wave, r, E, EV, nx);   // prefetch
-    const EdgeCtx& c = cur.c;
-    const bf16x8 F = cbf_edge_frag(c.rel, c.eye, c.dfeat, c.ok, h);
+    const CbfIn<D> cur = nx;
+    if (chunk + gridDim.x < nchunks) cbf_load<FUSED, NW, D>(a, chunk + gridDim.x, wave, r, E, EV, nx);   // prefetch
+    const EdgeCtx<D>& c = cur.c;
+    const bf16x8 F = cbf_edge_frag<D>(c.rp, c.rv, c.eye, c.dfeat, c.ok, h);
     // one opaque base per LDS image per chunk: the per-lane address math is computed once and
     // shared by all fragment reads (immediate offsets), while the loads themselves cannot be
     // hoisted out of the chunk loop (~100 weight VGPRs otherwise)
@@ -541,14 +569,21 @@ __global__ __launch_bounds__(NW * 64, 1) void cbf_bwd_kernel(CbfBwdArgs a) {
         constexpr int kk = decltype(kk_)::value;
         t = mfma(frag_ld(wt, 2 + kk, lane), bacc_frag<kk & 1>(d1b[kk >> 1]), t);
       });
-      const float ddist = shfl_xor32(t[1]);   // row 5 lives in lane r+32, reg 1
+      // rows = feature columns: s_i - s_j (0..2D-1), eye (2D), dist (2D+1); lane h = 0 holds rows
+      // 0..3 in regs 0..3, lane h = 1 rows 4..7
+      float g4[8];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) { g4[q] = t[q]; g4[4 + q] = shfl_xor32(t[q]); }
       if (a.dE && cur.in && h == 0) {
-        float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
+        float dp[D], dv[D];
+#pragma unroll
+        for (int q = 0; q < D; ++q) { dp[q] = 0.f; dv[q] = 0.f; }
         if (c.ok && c.j != c.i) {
-          const float inv = 1.f / c.d;
-          g = make_float4(t[0] + ddist * c.rel.x * inv, t[1] + ddist * c.rel.y * inv, t[2], t[3]);
+          const float ddist = g4[2 * D + 1] * (1.f / c.d);
+#pragma unroll
+          for (int q = 0; q < D; ++q) { dp[q] = g4[q] + ddist * c.rp[q]; dv[q] = g4[D + q]; }
         }
-        a.dE[cur.ev] = g;
+        store_rec<D>(a.dE, cur.ev, dp, dv);
       }
     }
     // ---- stage C+D: dW1f (64x32) += dH1pre . [F|dh|0]^T (waves 0,1; cols >= 16 unused);
@@ -635,11 +670,11 @@ __global__ __launch_bounds__(NW * 64, 1) void cbf_bwd_kernel(CbfBwdArgs a) {
   }
 }
 
-template <bool FUSED, int NW>
+template <bool FUSED, int NW, int D>
 static void launch_cbf_bwd(const CbfBwdArgs& a, int num_blocks, hipStream_t st) {
   const size_t lds = CbfCfg<NW>::LDS;
-  (void)hipFuncSetAttribute((const void*)cbf_bwd_kernel<FUSED, NW>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL((cbf_bwd_kernel<FUSED, NW>), dim3(num_blocks), dim3(NW * 64), lds, st, a);
+  (void)hipFuncSetAttribute((const void*)cbf_bwd_kernel<FUSED, NW, D>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipLaunchKernelGGL((cbf_bwd_kernel<FUSED, NW, D>), dim3(num_blocks), dim3(NW * 64), lds, st, a);
 }
 
 }  // namespace mb
@@ -648,7 +683,12 @@ extern "C" int mb_cbf_bwd(const mb::CbfBwdArgs* a, int num_blocks, hipStream_t s
   using namespace mb;
   if (a->K > 16 || a->K < 1 || a->passes < 1 || a->passes > 2) return -1;
   if (a->fused && (a->passes != 2 || !a->dang || !a->counts)) return -2;
-  if (a->fused) launch_cbf_bwd<true, CBF_NW>(*a, num_blocks, st);
-  else launch_cbf_bwd<false, CBF_NW>(*a, num_blocks, st);
+  if (a->dim == 3) {
+    if (a->fused) launch_cbf_bwd<true, CBF_NW, 3>(*a, num_blocks, st);
+    else launch_cbf_bwd<false, CBF_NW, 3>(*a, num_blocks, st);
+  } else {
+    if (a->fused) launch_cbf_bwd<true, CBF_NW, 2>(*a, num_blocks, st);
+    else launch_cbf_bwd<false, CBF_NW, 2>(*a, num_blocks, st);
+  }
   return (int)hipGetLastError();
 }

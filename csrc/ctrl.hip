@@ -16,6 +16,7 @@
 #pragma clang fp contract(off)
 #include "common.h"
 #include "args.h"
+#include "state.h"
 
 namespace mb {
 
@@ -24,41 +25,62 @@ constexpr int CTRL_FWD_FRAGS = 72;   // ew1f 2 + ew2 16 | nw1f 18 + nw2 16 + nw3
 constexpr int CTRL_VEC = 352;        // eb2 128 | nb2 128 | nb3 64 | nb4 32 (padded)
 
 
-DEV bf16x8 ctrl_edge_frag(float4 rel, float eye, bool ok, int h) {
+// edge layer-1 B fragment (layout.ctrl_edge_slot): hi [s_i - s_j (2D), eye, 1], lo [s_i - s_j]
+template <int D>
+DEV bf16x8 ctrl_edge_frag(const float (&rp)[D], const float (&rv)[D], float eye, bool ok, int h) {
   bf16x8 f;
-  bf16 hx, lx, hy, ly, hvx, lvx, hvy, lvy;
-  split_bf16(rel.x, hx, lx);
-  split_bf16(rel.y, hy, ly);
-  split_bf16(rel.z, hvx, lvx);
-  split_bf16(rel.w, hvy, lvy);
-  const bf16 z = (bf16)0.f;
-  if (!ok) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) f[j] = z;
-    return f;
-  }
-  if (h == 0) {
-    f[0] = hx; f[1] = hy; f[2] = hvx; f[3] = hvy; f[4] = (bf16)eye; f[5] = (bf16)1.f; f[6] = z; f[7] = z;
-  } else {
-    f[0] = lx; f[1] = ly; f[2] = lvx; f[3] = lvy; f[4] = z; f[5] = z; f[6] = z; f[7] = z;
-  }
-  return f;
-}
-
-DEV bf16x8 node_state_frag(float ex, float ey, float vx, float vy, bool ok, int h) {
-  bf16x8 f;
-  bf16 a0, a1, b0, b1, c0, c1, d0, d1;
-  split_bf16(ex, a0, a1);
-  split_bf16(ey, b0, b1);
-  split_bf16(vx, c0, c1);
-  split_bf16(vy, d0, d1);
   const bf16 z = (bf16)0.f;
 #pragma unroll
   for (int j = 0; j < 8; ++j) f[j] = z;
   if (!ok) return f;
-  if (h == 0) { f[0] = a0; f[1] = b0; f[2] = c0; f[3] = d0; f[4] = (bf16)1.f; }
-  else        { f[0] = a1; f[1] = b1; f[2] = c1; f[3] = d1; }
+  bf16 hi[2 * D], lo[2 * D];
+#pragma unroll
+  for (int q = 0; q < D; ++q) {
+    split_bf16(rp[q], hi[q], lo[q]);
+    split_bf16(rv[q], hi[D + q], lo[D + q]);
+  }
+  if (h == 0) {
+#pragma unroll
+    for (int q = 0; q < 2 * D; ++q) f[q] = hi[q];
+    f[2 * D] = (bf16)eye;
+    f[2 * D + 1] = (bf16)1.f;
+  } else {
+#pragma unroll
+    for (int q = 0; q < 2 * D; ++q) f[q] = lo[q];
+  }
   return f;
+}
+
+// node layer-1 state fragment (layout.ctrl_node_slot): hi [p - g, v, 1], lo [p - g, v]
+template <int D>
+DEV bf16x8 node_state_frag(const float (&e)[D], const float (&v)[D], bool ok, int h) {
+  bf16x8 f;
+  const bf16 z = (bf16)0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) f[j] = z;
+  if (!ok) return f;
+  bf16 hi[2 * D], lo[2 * D];
+#pragma unroll
+  for (int q = 0; q < D; ++q) {
+    split_bf16(e[q], hi[q], lo[q]);
+    split_bf16(v[q], hi[D + q], lo[D + q]);
+  }
+  if (h == 0) {
+#pragma unroll
+    for (int q = 0; q < 2 * D; ++q) f[q] = hi[q];
+    f[2 * D] = (bf16)1.f;
+  } else {
+#pragma unroll
+    for (int q = 0; q < 2 * D; ++q) f[q] = lo[q];
+  }
+  return f;
+}
+
+// rows 0..2D-1 of an accumulator tile for lanes h == 0: rows 0..3 are regs 0..3 of this lane,
+// rows 4..7 regs 0..3 of lane r + 32 (all lanes must call: lane swap)
+DEV void acc_rows8(const f32x16& c, float (&o)[8]) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) { o[q] = c[q]; o[4 + q] = shfl_xor32(c[q]); }
 }
 
 // One edge tile in the transposed orientation: returns Z^T (4 column tiles) for 32 edges.
@@ -136,7 +158,7 @@ DEV void node_forward(const bf16* pool, const bf16x8& sfrag, const bf16* wn, con
 // loads): at tile q the kernel issues the idx load of tile q+2 and the state loads of tile
 // q+1, then computes tile q, so every load has a full tile of MFMA work to land under.
 struct EdgeIdx { int j, b, i; bool ok; };
-struct EdgeSt { float4 si, sj; int j, i; bool ok; };
+template <int D> struct EdgeSt { float rp[D], rv[D]; int j, i; bool ok; };
 
 DEV void ctrl_idx_load(const int* idx, long i_env, int N, int K, int g0, int q, int r, int total, EdgeIdx& o) {
   const int al = 2 * q + (r >> 4);
@@ -151,19 +173,24 @@ DEV void ctrl_idx_load(const int* idx, long i_env, int N, int K, int g0, int q, 
   }
 }
 
-DEV void ctrl_st_load(const float4* S, long s_env, const EdgeIdx& x, EdgeSt& o) {
+template <int D>
+DEV void ctrl_st_load(const float4* S, long s_env, const EdgeIdx& x, EdgeSt<D>& o) {
   o.ok = x.ok;
   o.j = x.j;
   o.i = x.i;
+#pragma unroll
+  for (int q = 0; q < D; ++q) { o.rp[q] = 0.f; o.rv[q] = 0.f; }
   if (x.ok) {
-    o.si = S[x.b * (int)s_env + x.i];
-    o.sj = S[x.b * (int)s_env + x.j];
-  } else {
-    o.si = o.sj = make_float4(0.f, 0.f, 0.f, 0.f);
+    const float4* Sb = S + (x.b * (int)s_env) * REC<D>;
+    float pi[D], vi[D], pj[D], vj[D];
+    load_rec<D>(Sb, (unsigned)x.i, pi, vi);
+    load_rec<D>(Sb, (unsigned)x.j, pj, vj);
+#pragma unroll
+    for (int q = 0; q < D; ++q) { o.rp[q] = pi[q] - pj[q]; o.rv[q] = vi[q] - vj[q]; }
   }
 }
 
-template <int WAVES>
+template <int WAVES, int D>
 __global__ __launch_bounds__(WAVES * 64) void ctrl_fwd_kernel(CtrlArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   bf16* wl = reinterpret_cast<bf16*>(smem);                            // ew1f, ew2 (18 frags)
@@ -189,22 +216,21 @@ __global__ __launch_bounds__(WAVES * 64) void ctrl_fwd_kernel(CtrlArgs a) {
     // ---------------- edge phase: 16 tiles x (2 agents x 16 slots); the gathers of tile q+1
     // (idx -> s_j, dependent global loads) are issued before tile q's MFMA chain
     EdgeIdx xi1;
-    EdgeSt xs0;
+    EdgeSt<D> xs0;
     {
       EdgeIdx xi0;
       ctrl_idx_load(a.idx, a.i_env, N, K, g0, 0, r, total, xi0);
-      ctrl_st_load(a.S, a.s_env, xi0, xs0);
+      ctrl_st_load<D>(a.S, a.s_env, xi0, xs0);
       ctrl_idx_load(a.idx, a.i_env, N, K, g0, 1, r, total, xi1);
     }
     for (int q = 0; q < 16; ++q) {
-      const EdgeSt cur = xs0;
-      ctrl_st_load(a.S, a.s_env, xi1, xs0);                       // states of tile q+1
+      const EdgeSt<D> cur = xs0;
+      ctrl_st_load<D>(a.S, a.s_env, xi1, xs0);                    // states of tile q+1
       ctrl_idx_load(a.idx, a.i_env, N, K, g0, q + 2, r, total, xi1);   // idx of tile q+2
       const bool ok = cur.ok;
-      const float4 rel = make_float4(cur.si.x - cur.sj.x, cur.si.y - cur.sj.y, cur.si.z - cur.sj.z, cur.si.w - cur.sj.w);
       const float eye = (cur.j == cur.i) ? 1.f : 0.f;
-      const bool m = ok && (sqrtf(rel.x * rel.x + rel.y * rel.y) < a.obs_r);   // strict, un-eps'd (controller.py:38-39)
-      const bf16x8 F = ctrl_edge_frag(rel, eye, ok, h);
+      const bool m = ok && (sqrtf(sqsum<D>(cur.rp)) < a.obs_r);   // strict, un-eps'd (controller.py:38-39)
+      const bf16x8 F = ctrl_edge_frag<D>(cur.rp, cur.rv, eye, ok, h);
       f32x16 Z[4];
       ctrl_edge_tile(F, wl + opaque_zero(), eb2, lane, Z);
       const unsigned mask32 = (unsigned)(__ballot(m) & 0xffffffffull);
@@ -266,37 +292,49 @@ __global__ __launch_bounds__(WAVES * 64) void ctrl_fwd_kernel(CtrlArgs a) {
     const int gi = g0 + r;
     const bool ok = gi < total;
     int b = 0, i = 0;
-    float4 si = make_float4(0.f, 0.f, 0.f, 0.f);
-    float2 gg = make_float2(0.f, 0.f);
+    float sp[D], sv[D], gg[D];
+#pragma unroll
+    for (int q = 0; q < D; ++q) { sp[q] = 0.f; sv[q] = 0.f; gg[q] = 0.f; }
     if (ok) {
       b = gi / N; i = gi - b * N;
-      si = a.S[(long)b * a.s_env + i];
-      gg = a.G[(long)b * N + i];
+      load_rec<D>(a.S + (long)b * a.s_env * REC<D>, (unsigned)i, sp, sv);
+#pragma unroll
+      for (int q = 0; q < D; ++q) gg[q] = a.G[((long)b * N + i) * D + q];
     }
-    const float ex = si.x - gg.x, ey = si.y - gg.y;
-    const bf16x8 sf = node_state_frag(ex, ey, si.z, si.w, ok, h);
+    float ex[D];
+#pragma unroll
+    for (int q = 0; q < D; ++q) ex[q] = sp[q] - gg[q];
+    const bf16x8 sf = node_state_frag<D>(ex, sv, ok, h);
     NodeActs na;
     node_forward(pool, sf, wn + opaque_zero(), nb2, nb3, nb4, lane, na);
+    float y4r[8];
+    acc_rows8(na.Y4, y4r);                                     // gain pre-activations 0..2D-1
     float dsum = 0.f, asum = 0.f;
     if (ok && h == 0) {
-      const float k0 = 2.f / (1.f + __expf(-na.Y4[0])) + 0.2f;
-      const float k1 = 2.f / (1.f + __expf(-na.Y4[1])) + 0.2f;
-      const float k2 = 2.f / (1.f + __expf(-na.Y4[2])) + 0.2f;
-      const float k3 = 2.f / (1.f + __expf(-na.Y4[3])) + 0.2f;
-      float ax = -(k0 * ex + k1 * si.z);
-      float ay = -(k2 * ey + k3 * si.w);
-      if (a.noise) {
-        const float2 nz = a.noise[(long)b * a.n_env + i];
-        ax += nz.x;
-        ay += nz.y;
+      float av[D], snp[D], snv[D], ar[D];
+#pragma unroll
+      for (int q = 0; q < D; ++q) {
+        const float kp = 2.f / (1.f + __expf(-y4r[2 * q])) + 0.2f;
+        const float kv = 2.f / (1.f + __expf(-y4r[2 * q + 1])) + 0.2f;
+        av[q] = -(kp * ex[q] + kv * sv[q]);
+        if (a.noise) av[q] += a.noise[((long)b * a.n_env + i) * D + q];
       }
-      if (a.A) a.A[(long)b * a.a_env + i] = make_float2(ax, ay);
-      const float4 sn = make_float4(si.x + si.z * a.dt, si.y + si.w * a.dt, si.z + ax * a.dt, si.w + ay * a.dt);
-      if (a.Snext) a.Snext[(long)b * a.sn_env + i] = sn;
-      const float dx = sn.x - gg.x, dy = sn.y - gg.y;
-      dsum = sqrtf(dx * dx + dy * dy);
-      const float rx = -(ex + a.sqrt3 * si.z), ry = -(ey + a.sqrt3 * si.w);
-      asum = fabsf((ax * ax + ay * ay) - (rx * rx + ry * ry));
+      if (a.A) {
+#pragma unroll
+        for (int q = 0; q < D; ++q) a.A[((long)b * a.a_env + i) * D + q] = av[q];
+      }
+#pragma unroll
+      for (int q = 0; q < D; ++q) {
+        snp[q] = sp[q] + sv[q] * a.dt;
+        snv[q] = sv[q] + av[q] * a.dt;
+        ar[q] = -(ex[q] + a.sqrt3 * sv[q]);
+      }
+      if (a.Snext) store_rec<D>(a.Snext + (long)b * a.sn_env * REC<D>, (unsigned)i, snp, snv);
+      float dd[D];
+#pragma unroll
+      for (int q = 0; q < D; ++q) dd[q] = snp[q] - gg[q];
+      dsum = sqrtf(sqsum<D>(dd));
+      asum = fabsf(sqsum<D>(av) - sqsum<D>(ar));
     }
     // per-env sums: one atomic per wave when its 32 agents share an env
     const int last = min(g0 + 31, total - 1);
@@ -333,8 +371,13 @@ extern "C" int mb_ctrl_fwd(const mb::CtrlArgs* a, int num_cu, hipStream_t st) {
   const int maxb = num_cu > 0 ? num_cu * 2 : blocks;
   if (blocks > maxb) blocks = maxb;
   const size_t lds = ctrl_fwd_lds();
-  (void)hipFuncSetAttribute((const void*)ctrl_fwd_kernel<CTRL_WAVES>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL(ctrl_fwd_kernel<CTRL_WAVES>, dim3(blocks), dim3(CTRL_WAVES * 64), lds, st, *a);
+  if (a->dim == 3) {
+    (void)hipFuncSetAttribute((const void*)ctrl_fwd_kernel<CTRL_WAVES, 3>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL((ctrl_fwd_kernel<CTRL_WAVES, 3>), dim3(blocks), dim3(CTRL_WAVES * 64), lds, st, *a);
+  } else {
+    (void)hipFuncSetAttribute((const void*)ctrl_fwd_kernel<CTRL_WAVES, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL((ctrl_fwd_kernel<CTRL_WAVES, 2>), dim3(blocks), dim3(CTRL_WAVES * 64), lds, st, *a);
+  }
   return (int)hipGetLastError();
 }
 
@@ -371,6 +414,7 @@ DEV void add_tile(float* dst, int ncols, int mt, int nt, const f32x16& c, int la
   for (int reg = 0; reg < 16; ++reg) dst[(32 * mt + acc_row(reg, h)) * ncols + 32 * nt + r] += c[reg];
 }
 
+template <int D>
 __global__ __launch_bounds__(NB_WAVES * 64, 1) void ctrl_node_bwd_kernel(CtrlNodeBwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   bf16* wr = reinterpret_cast<bf16*>(smem);
@@ -399,18 +443,21 @@ __global__ __launch_bounds__(NB_WAVES * 64, 1) void ctrl_node_bwd_kernel(CtrlNod
     const int ga = (int)(chunk * NB_CH) + erow;
     const bool ok = ga < total;
     int b = 0, i = 0;
-    float4 si = make_float4(0.f, 0.f, 0.f, 0.f);
-    float2 gg = make_float2(0.f, 0.f), av = make_float2(0.f, 0.f);
-    float4 gn = make_float4(0.f, 0.f, 0.f, 0.f);
+    float sp[D], sv[D], gg[D], av[D], gnp[D], gnv[D];
+#pragma unroll
+    for (int q = 0; q < D; ++q) { sp[q] = sv[q] = gg[q] = av[q] = gnp[q] = gnv[q] = 0.f; }
     bool vld = false;
     bf16x8 Pf[9];
     const bf16 z = (bf16)0.f;   // Pf is dead after Y1; S1 re-reads the pooled rows
     if (ok) {
       b = ga / N; i = ga - b * N;
-      si = a.S[(long)b * a.s_env + i];
-      gg = a.G[(long)b * N + i];
-      av = a.A[(long)b * a.a_env + i];
-      if (a.Gn) gn = a.Gn[(long)b * a.gn_env + i];
+      load_rec<D>(a.S + (long)b * a.s_env * REC<D>, (unsigned)i, sp, sv);
+#pragma unroll
+      for (int q = 0; q < D; ++q) {
+        gg[q] = a.G[((long)b * N + i) * D + q];
+        av[q] = a.A[((long)b * a.a_env + i) * D + q];
+      }
+      if (a.Gn) load_rec<D>(a.Gn + (long)b * a.gn_env * REC<D>, (unsigned)i, gnp, gnv);
       vld = a.valid ? (a.valid[(long)b * a.v_env] != 0) : true;
       const bf16* prow = a.pooled + (long)b * a.p_env + (long)i * 128;
 #pragma unroll
@@ -421,8 +468,10 @@ __global__ __launch_bounds__(NB_WAVES * 64, 1) void ctrl_node_bwd_kernel(CtrlNod
 #pragma unroll
         for (int j = 0; j < 8; ++j) Pf[kk][j] = z;
     }
-    const float ex = si.x - gg.x, ey = si.y - gg.y;
-    Pf[8] = node_state_frag(ex, ey, si.z, si.w, ok, h);
+    float ex[D];
+#pragma unroll
+    for (int q = 0; q < D; ++q) ex[q] = sp[q] - gg[q];
+    Pf[8] = node_state_frag<D>(ex, sv, ok, h);
     const bf16* W1 = wr + opaque_zero();
     const bf16* W2 = W1 + 64 * NS1;
     const bf16* W3 = W2 + 128 * NS2;
@@ -462,34 +511,48 @@ __global__ __launch_bounds__(NB_WAVES * 64, 1) void ctrl_node_bwd_kernel(CtrlNod
       constexpr int kk = decltype(kk_)::value;
       y4 = mfma(wrm_acc(W4 + opaque_zero(), NS4, 0, kk, lane), bacc_frag<kk & 1>(Y3b[kk >> 1]), y4);
     });
-    // ---- gain law + action loss backward (lanes h == 0 own agent r; rows 0..3 = regs 0..3)
-    f32x16 d4 = zero16();
-    float4 egod = make_float4(0.f, 0.f, 0.f, 0.f);
+    // ---- gain law + action loss backward (lanes h == 0 own agent r; gain rows 0..2D-1 are
+    //      regs 0..3 of lane r and (D = 3) regs 0,1 of lane r + 32)
+    float y4r[8];
+    acc_rows8(y4, y4r);
+    float d4r[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) d4r[q] = 0.f;
+    float egp[D], egv[D];                         // dL/d(p - g), dL/dv of the ego terms
+#pragma unroll
+    for (int q = 0; q < D; ++q) { egp[q] = 0.f; egv[q] = 0.f; }
     if (ok && h == 0) {
-      const float s0 = sigm(y4[0]), s1 = sigm(y4[1]), s2 = sigm(y4[2]), s3 = sigm(y4[3]);
-      const float k0 = 2.f * s0 + 0.2f, k1 = 2.f * s1 + 0.2f, k2 = 2.f * s2 + 0.2f, k3 = 2.f * s3 + 0.2f;
-      float dax = a.dt * gn.z, day = a.dt * gn.w;
+      float da[D], ar[D];
+#pragma unroll
+      for (int q = 0; q < D; ++q) { da[q] = a.dt * gnv[q]; ar[q] = -(ex[q] + a.sqrt3 * sv[q]); }
       if (vld && a.act_coef != 0.f) {
-        const float rx = -(ex + a.sqrt3 * si.z), ry = -(ey + a.sqrt3 * si.w);
-        const float diff = (av.x * av.x + av.y * av.y) - (rx * rx + ry * ry);
+        const float diff = sqsum<D>(av) - sqsum<D>(ar);
         const float sg = diff > 0.f ? 1.f : (diff < 0.f ? -1.f : 0.f);
         const float c = a.act_coef * sg;
-        dax += c * 2.f * av.x;
-        day += c * 2.f * av.y;
-        egod.x += c * 2.f * rx;
-        egod.y += c * 2.f * ry;
-        egod.z += c * 2.f * a.sqrt3 * rx;
-        egod.w += c * 2.f * a.sqrt3 * ry;
+#pragma unroll
+        for (int q = 0; q < D; ++q) {
+          da[q] += c * 2.f * av[q];
+          egp[q] += c * 2.f * ar[q];
+          egv[q] += c * 2.f * a.sqrt3 * ar[q];
+        }
       }
-      // a_x = -(k0 ex + k1 vx), a_y = -(k2 ey + k3 vy)
-      egod.x += -k0 * dax;
-      egod.z += -k1 * dax;
-      egod.y += -k2 * day;
-      egod.w += -k3 * day;
-      d4[0] = -dax * ex * 2.f * s0 * (1.f - s0);
-      d4[1] = -dax * si.z * 2.f * s1 * (1.f - s1);
-      d4[2] = -day * ey * 2.f * s2 * (1.f - s2);
-      d4[3] = -day * si.w * 2.f * s3 * (1.f - s3);
+      // a_d = -(k_{2d} e_d + k_{2d+1} v_d), k = 2 sigmoid(y) + 0.2
+#pragma unroll
+      for (int q = 0; q < D; ++q) {
+        const float s0 = sigm(y4r[2 * q]), s1 = sigm(y4r[2 * q + 1]);
+        const float kp = 2.f * s0 + 0.2f, kv = 2.f * s1 + 0.2f;
+        egp[q] += -kp * da[q];
+        egv[q] += -kv * da[q];
+        d4r[2 * q] = -da[q] * ex[q] * 2.f * s0 * (1.f - s0);
+        d4r[2 * q + 1] = -da[q] * sv[q] * 2.f * s1 * (1.f - s1);
+      }
+    }
+    // back to the accumulator layout: rows 0..3 -> regs 0..3 of h = 0, rows 4..7 -> of h = 1
+    f32x16 d4 = zero16();
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float hi4 = shfl_xor32(d4r[4 + q]);
+      d4[q] = (h == 0) ? d4r[q] : hi4;
     }
     const bf16x16 d4b = to_bf16x16(d4);
     // Backward chain interleaved with the WG-shared weight-gradient stages so that each
@@ -588,12 +651,14 @@ d1b[mt] = to_bf16x16(c);
             *reinterpret_cast<bf16x4*>(drow + 8 * g + 4 * h) = v;
           }
         }
-      } else if (ok && h == 0) {
-        egod.x += c[0];   // d/d(ex) -> x
-        egod.y += c[1];   // d/d(ey) -> y
-        egod.z += c[2];   // vx
-        egod.w += c[3];   // vy
-        if (a.ego) a.ego[(long)b * N + i] = egod;
+      } else {
+        float er[8];
+        acc_rows8(c, er);                       // rows 128..128+2D-1: d/d[p - g, v]
+        if (ok && h == 0 && a.ego) {
+#pragma unroll
+          for (int q = 0; q < D; ++q) { egp[q] += er[q]; egv[q] += er[D + q]; }
+          store_rec<D>(a.ego + (long)b * N * REC<D>, (unsigned)i, egp, egv);
+        }
       }
     }
     {   // S1: dWn1f (64x160) += dY1 . P^T  (P re-read from the pooled rows: L2-hot)
@@ -601,7 +666,7 @@ d1b[mt] = to_bf16x16(c);
       bf16* imB = stg + NB_CH * 72;
 #pragma unroll
       for (int mt = 0; mt < 2; ++mt) store_tile(imA, 72, erow, 32 * mt, d1b[mt], h);
-      const bf16x8 sf = node_state_frag(ex, ey, si.z, si.w, ok, h);
+      const bf16x8 sf = node_state_frag<D>(ex, sv, ok, h);
       const bf16* prow = a.pooled + (long)b * a.p_env + (long)i * 128;
       bf16x8 zz;
 #pragma unroll
@@ -658,6 +723,7 @@ constexpr size_t EB_STAGE = (size_t)(136 + 72) * EB_CH * 2;
 
 size_t ctrl_edge_bwd_lds() { return (size_t)22 * FRAG_BYTES + EB_STAGE; }
 
+template <int D>
 __global__ __launch_bounds__(EB_WAVES * 64, 2) void ctrl_edge_bwd_kernel(CtrlEdgeBwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   bf16* wf = reinterpret_cast<bf16*>(smem);                 // ew1f (2) | ew2tn (16) | ew1ft (4)
@@ -677,26 +743,25 @@ __global__ __launch_bounds__(EB_WAVES * 64, 2) void ctrl_edge_bwd_kernel(CtrlEdg
 
   for (long chunk = blockIdx.x; chunk < nchunks; chunk += gridDim.x) {
     EdgeIdx xi1;
-    EdgeSt xs0;
+    EdgeSt<D> xs0;
     const int g0 = (int)(chunk * EB_CH) + wave * 32;
     {
       EdgeIdx xi0;
       ctrl_idx_load(a.idx, a.i_env, N, K, g0, 0, r, total, xi0);
-      ctrl_st_load(a.S, a.s_env, xi0, xs0);
+      ctrl_st_load<D>(a.S, a.s_env, xi0, xs0);
       ctrl_idx_load(a.idx, a.i_env, N, K, g0, 1, r, total, xi1);
     }
     for (int q = 0; q < 16; ++q) {
-      const EdgeSt cur = xs0;
-      ctrl_st_load(a.S, a.s_env, xi1, xs0);
+      const EdgeSt<D> cur = xs0;
+      ctrl_st_load<D>(a.S, a.s_env, xi1, xs0);
       ctrl_idx_load(a.idx, a.i_env, N, K, g0, q + 2, r, total, xi1);
       const int slot = r & 15;
       const bool ok = cur.ok;
       const int ga = g0 + 2 * q + (r >> 4);
       const int b = ok ? ga / N : 0;
       const int i = cur.i, j = cur.j;
-      const float4 rel = make_float4(cur.si.x - cur.sj.x, cur.si.y - cur.sj.y, cur.si.z - cur.sj.z, cur.si.w - cur.sj.w);
       const float eye = (j == i) ? 1.f : 0.f;
-      const bf16x8 F = ctrl_edge_frag(rel, eye, ok, h);
+      const bf16x8 F = ctrl_edge_frag<D>(cur.rp, cur.rv, eye, ok, h);
       const bf16* wt = wf + opaque_zero();
       bf16x16 H1b[2];
 #pragma unroll
@@ -748,9 +813,16 @@ __global__ __launch_bounds__(EB_WAVES * 64, 2) void ctrl_edge_bwd_kernel(CtrlEdg
           constexpr int kk = decltype(kk_)::value;
           c = mfma(frag_ld(wt, 18 + kk, lane), bacc_frag<kk & 1>(d1b[kk >> 1]), c);
         });
+        float gr[8];
+        acc_rows8(c, gr);                       // rows 0..2D-1 = dL/d(s_i - s_j)
         if (ok && h == 0 && a.dEc) {
-          const float4 g = (j != i) ? make_float4(c[0], c[1], c[2], c[3]) : make_float4(0.f, 0.f, 0.f, 0.f);
-          a.dEc[b * (int)a.de_env + i * K + slot] = g;
+          float gp[D], gv[D];
+#pragma unroll
+          for (int q2 = 0; q2 < D; ++q2) {
+            gp[q2] = (j != i) ? gr[q2] : 0.f;
+            gv[q2] = (j != i) ? gr[D + q2] : 0.f;
+          }
+          store_rec<D>(a.dEc, (unsigned)(b * (int)a.de_env + i * K + slot), gp, gv);
         }
       }
       // S1: dW2 (128x64) += dZ . H1^T ; eb2 (dZ is already in the image; bias-sum steps split
@@ -810,8 +882,13 @@ __global__ __launch_bounds__(EB_WAVES * 64, 2) void ctrl_edge_bwd_kernel(CtrlEdg
 extern "C" int mb_ctrl_node_bwd(const mb::CtrlNodeBwdArgs* a, int num_blocks, hipStream_t st) {
   using namespace mb;
   const size_t lds = ctrl_node_bwd_lds();
-  (void)hipFuncSetAttribute((const void*)ctrl_node_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL(ctrl_node_bwd_kernel, dim3(num_blocks), dim3(NB_WAVES * 64), lds, st, *a);
+  if (a->dim == 3) {
+    (void)hipFuncSetAttribute((const void*)ctrl_node_bwd_kernel<3>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(ctrl_node_bwd_kernel<3>, dim3(num_blocks), dim3(NB_WAVES * 64), lds, st, *a);
+  } else {
+    (void)hipFuncSetAttribute((const void*)ctrl_node_bwd_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(ctrl_node_bwd_kernel<2>, dim3(num_blocks), dim3(NB_WAVES * 64), lds, st, *a);
+  }
   return (int)hipGetLastError();
 }
 
@@ -819,7 +896,12 @@ extern "C" int mb_ctrl_edge_bwd(const mb::CtrlEdgeBwdArgs* a, int num_blocks, hi
   using namespace mb;
   if (a->K > 16 || a->K < 1) return -1;
   const size_t lds = ctrl_edge_bwd_lds();
-  (void)hipFuncSetAttribute((const void*)ctrl_edge_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL(ctrl_edge_bwd_kernel, dim3(num_blocks), dim3(EB_WAVES * 64), lds, st, *a);
+  if (a->dim == 3) {
+    (void)hipFuncSetAttribute((const void*)ctrl_edge_bwd_kernel<3>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(ctrl_edge_bwd_kernel<3>, dim3(num_blocks), dim3(EB_WAVES * 64), lds, st, *a);
+  } else {
+    (void)hipFuncSetAttribute((const void*)ctrl_edge_bwd_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(ctrl_edge_bwd_kernel<2>, dim3(num_blocks), dim3(EB_WAVES * 64), lds, st, *a);
+  }
   return (int)hipGetLastError();
 }

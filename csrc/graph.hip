@@ -9,6 +9,7 @@
 // (one workgroup per graph, LDS counting sort).
 #include "common.h"
 #include "args.h"
+#include "state.h"
 
 namespace mb {
 
@@ -16,23 +17,24 @@ constexpr int CSR_BLOCK = 256;
 
 __global__ __launch_bounds__(CSR_BLOCK) void rev_csr_kernel(CsrArgs a) {
   extern __shared__ __attribute__((aligned(16))) int sm[];
-  int* cnt = sm;                 // N + 1
-  int* fill = sm + a.N + 1;      // N
+  const int Nt = a.Nn > 0 ? a.Nn : a.N;   // target nodes (agents + obstacle points)
+  int* cnt = sm;                 // Nt + 1
+  int* fill = sm + Nt + 1;       // Nt
   __shared__ int wsum[CSR_BLOCK];
   const long g = blockIdx.x;
   const int N = a.N, K = a.K, NK = N * K;
   const int* idx = a.idx + g * NK;
-  for (int q = threadIdx.x; q <= N; q += CSR_BLOCK) cnt[q] = 0;
-  for (int q = threadIdx.x; q < N; q += CSR_BLOCK) fill[q] = 0;
+  for (int q = threadIdx.x; q <= Nt; q += CSR_BLOCK) cnt[q] = 0;
+  for (int q = threadIdx.x; q < Nt; q += CSR_BLOCK) fill[q] = 0;
   __syncthreads();
   for (int e = threadIdx.x; e < NK; e += CSR_BLOCK) {
     const int j = idx[e];
     if (j != e / K) atomicAdd(&cnt[j + 1], 1);
   }
   __syncthreads();
-  // exclusive scan of cnt[1..N] into cnt[0..N] (two-level: per-thread segment, then totals)
-  const int seg = (N + CSR_BLOCK - 1) / CSR_BLOCK;
-  const int lo = threadIdx.x * seg + 1, hi = min(lo + seg, N + 1);
+  // exclusive scan of cnt[1..Nt] into cnt[0..Nt] (two-level: per-thread segment, then totals)
+  const int seg = (Nt + CSR_BLOCK - 1) / CSR_BLOCK;
+  const int lo = threadIdx.x * seg + 1, hi = min(lo + seg, Nt + 1);
   int run = 0;
   for (int q = lo; q < hi; ++q) { run += cnt[q]; cnt[q] = run; }
   wsum[threadIdx.x] = run;
@@ -45,8 +47,8 @@ __global__ __launch_bounds__(CSR_BLOCK) void rev_csr_kernel(CsrArgs a) {
   const int off = wsum[threadIdx.x];
   for (int q = lo; q < hi; ++q) cnt[q] += off;
   __syncthreads();
-  int* ptr = a.ptr + g * (N + 1);
-  for (int q = threadIdx.x; q <= N; q += CSR_BLOCK) ptr[q] = cnt[q];
+  int* ptr = a.ptr + g * (Nt + 1);
+  for (int q = threadIdx.x; q <= Nt; q += CSR_BLOCK) ptr[q] = cnt[q];
   int* out = a.edges + g * NK;
   for (int e = threadIdx.x; e < NK; e += CSR_BLOCK) {
     const int j = idx[e];
@@ -58,7 +60,7 @@ __global__ __launch_bounds__(CSR_BLOCK) void rev_csr_kernel(CsrArgs a) {
   __threadfence();     // fill writes visible before other threads of the block sort them
   __syncthreads();
   // deterministic order inside each bucket: insertion sort by edge id
-  for (int j = threadIdx.x; j < N; j += CSR_BLOCK) {
+  for (int j = threadIdx.x; j < Nt; j += CSR_BLOCK) {
     const int b0 = cnt[j], b1 = cnt[j + 1];
     for (int x = b0 + 1; x < b1; ++x) {
       const int v = out[x];
@@ -69,7 +71,9 @@ __global__ __launch_bounds__(CSR_BLOCK) void rev_csr_kernel(CsrArgs a) {
   }
 }
 
-// dS[b, t', i] (+)= reduce of pass-0 edges of graph (b,t') and pass-1 edges of graph (b,t'-1)
+// dS[b, t', i] (+)= reduce of pass-0 edges of graph (b,t') and pass-1 edges of graph (b,t'-1),
+// for the N agents (obstacle nodes receive no gradient). Records of REC<D> float4.
+template <int D>
 __global__ __launch_bounds__(256) void node_reduce_kernel(NodeRedArgs a) {
   const long tid = (long)blockIdx.x * blockDim.x + threadIdx.x;
   const long total = (long)a.B * (a.T + 1) * a.N;
@@ -80,76 +84,96 @@ __global__ __launch_bounds__(256) void node_reduce_kernel(NodeRedArgs a) {
   const int tp = (int)(tb / a.B);
   const int b = (int)(tb - (long)tp * a.B);
   const int N = a.N, K = a.K;
+  const int Nt = a.Nn > 0 ? a.Nn : N;
   const long E = (long)a.B * a.T * N * K;
-  float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
+  constexpr int R = REC<D>;
+  float4 g[R];
+#pragma unroll
+  for (int q = 0; q < R; ++q) g[q] = make_float4(0.f, 0.f, 0.f, 0.f);
   for (int pass = 0; pass < a.passes; ++pass) {
     if (a.pass_mask && !((a.pass_mask >> pass) & 1)) continue;
     const int t = tp - pass;
     if (t < 0 || t >= a.T) continue;
     const long ge = (long)t * a.B + b;                          // edge block of step t
     const long gi = ge + (pass == 1 ? (long)a.shift1 * a.B : 0);  // graph (CSR) the edges live in
-    const float4* dE = a.dE + (long)pass * E + ge * N * K;
+    const float4* dE = a.dE + ((long)pass * E + ge * N * K) * R;
     for (int k = 0; k < K; ++k) {
-      const float4 v = dE[(long)i * K + k];
-      g.x += v.x; g.y += v.y; g.z += v.z; g.w += v.w;
+#pragma unroll
+      for (int q = 0; q < R; ++q) {
+        const float4 v = dE[((long)i * K + k) * R + q];
+        g[q].x += v.x; g[q].y += v.y; g[q].z += v.z; g[q].w += v.w;
+      }
     }
-    const int* ptr = a.ptr + gi * (N + 1);
+    const int* ptr = a.ptr + gi * (Nt + 1);
     const int* edges = a.edges + gi * (long)N * K;
-    for (int q = ptr[i]; q < ptr[i + 1]; ++q) {
-      const float4 v = dE[edges[q]];
-      g.x -= v.x; g.y -= v.y; g.z -= v.z; g.w -= v.w;
+    for (int q2 = ptr[i]; q2 < ptr[i + 1]; ++q2) {
+      const int e = edges[q2];
+#pragma unroll
+      for (int q = 0; q < R; ++q) {
+        const float4 v = dE[(long)e * R + q];
+        g[q].x -= v.x; g[q].y -= v.y; g[q].z -= v.z; g[q].w -= v.w;
+      }
     }
   }
-  float4* o = a.out + ((long)tp * a.B + b) * N + i;
-  if (a.accumulate) {
-    const float4 p = *o;
-    g.x += p.x; g.y += p.y; g.z += p.z; g.w += p.w;
+  float4* o = a.out + (((long)tp * a.B + b) * N + i) * R;
+#pragma unroll
+  for (int q = 0; q < R; ++q) {
+    float4 v = g[q];
+    if (a.accumulate) {
+      const float4 p = o[q];
+      v.x += p.x; v.y += p.y; v.z += p.z; v.w += p.w;
+    }
+    o[q] = v;
   }
-  *o = g;
 }
 
 // One reverse-time step of the BPTT recursion (train.py:58-103 through autograd in the
 // reference; hand-derived here):
 //   G_t = dS_direct[t] + ego_t + sum_k dEc[i,k] - sum_in dEc[e]
 //         + Euler adjoint of s_{t+1} = s_t + dt [v_t, a_t]  (if bptt)
+template <int D>
 __global__ __launch_bounds__(256) void node_combine_kernel(CombineArgs a) {
   const long tid = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (tid >= (long)a.B * a.N) return;
   const int b = (int)(tid / a.N), i = (int)(tid % a.N);
   const int N = a.N, K = a.K;
-  float4 g = a.dS[(long)b * a.ds_env + i];
+  float gp[D], gv[D], p[D], v[D];
+  load_rec<D>(a.dS + (long)b * a.ds_env * REC<D>, (unsigned)i, gp, gv);
   if (a.ego) {
-    const float4 v = a.ego[(long)b * N + i];
-    g.x += v.x; g.y += v.y; g.z += v.z; g.w += v.w;
+    load_rec<D>(a.ego + (long)b * N * REC<D>, (unsigned)i, p, v);
+#pragma unroll
+    for (int q = 0; q < D; ++q) { gp[q] += p[q]; gv[q] += v[q]; }
   }
   if (a.dEc) {
-    const float4* dE = a.dEc + (long)b * N * K;
+    const float4* dE = a.dEc + (long)b * N * K * REC<D>;
     for (int k = 0; k < K; ++k) {
-      const float4 v = dE[(long)i * K + k];
-      g.x += v.x; g.y += v.y; g.z += v.z; g.w += v.w;
+      load_rec<D>(dE, (unsigned)(i * K + k), p, v);
+#pragma unroll
+      for (int q = 0; q < D; ++q) { gp[q] += p[q]; gv[q] += v[q]; }
     }
     const int* ptr = a.ptr + (long)b * a.ptr_env;
     const int* edges = a.edges + (long)b * a.edges_env;
-    for (int q = ptr[i]; q < ptr[i + 1]; ++q) {
-      const float4 v = dE[edges[q]];
-      g.x -= v.x; g.y -= v.y; g.z -= v.z; g.w -= v.w;
+    for (int q2 = ptr[i]; q2 < ptr[i + 1]; ++q2) {
+      load_rec<D>(dE, (unsigned)edges[q2], p, v);
+#pragma unroll
+      for (int q = 0; q < D; ++q) { gp[q] -= p[q]; gv[q] -= v[q]; }
     }
   }
   if (a.Gn) {
-    const float4 n = a.Gn[(long)b * a.gn_env + i];
-    g.x += n.x;
-    g.y += n.y;
-    g.z += n.z + a.dt * n.x;
-    g.w += n.w + a.dt * n.y;
+    // Euler adjoint of s_{t+1} = s_t + dt [v_t, a_t]: dp += G_p, dv += G_v + dt G_p
+    load_rec<D>(a.Gn + (long)b * a.gn_env * REC<D>, (unsigned)i, p, v);
+#pragma unroll
+    for (int q = 0; q < D; ++q) { gp[q] += p[q]; gv[q] += v[q] + a.dt * p[q]; }
   }
-  a.Gout[(long)b * a.go_env + i] = g;
+  store_rec<D>(a.Gout + (long)b * a.go_env * REC<D>, (unsigned)i, gp, gv);
 }
 
 }  // namespace mb
 
 extern "C" int mb_rev_csr(const mb::CsrArgs* a, hipStream_t st) {
   using namespace mb;
-  const size_t lds = (size_t)(2 * a->N + 1) * 4;
+  const int Nt = a->Nn > 0 ? a->Nn : a->N;
+  const size_t lds = (size_t)(2 * Nt + 1) * 4;
   if (lds > 150 * 1024) return -1;
   (void)hipFuncSetAttribute((const void*)rev_csr_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   hipLaunchKernelGGL(rev_csr_kernel, dim3(a->G), dim3(CSR_BLOCK), lds, st, *a);
@@ -159,13 +183,15 @@ extern "C" int mb_rev_csr(const mb::CsrArgs* a, hipStream_t st) {
 extern "C" int mb_node_reduce(const mb::NodeRedArgs* a, hipStream_t st) {
   using namespace mb;
   const long total = (long)a->B * (a->T + 1) * a->N;
-  hipLaunchKernelGGL(node_reduce_kernel, dim3((total + 255) / 256), dim3(256), 0, st, *a);
+  if (a->dim == 3) hipLaunchKernelGGL(node_reduce_kernel<3>, dim3((total + 255) / 256), dim3(256), 0, st, *a);
+  else hipLaunchKernelGGL(node_reduce_kernel<2>, dim3((total + 255) / 256), dim3(256), 0, st, *a);
   return (int)hipGetLastError();
 }
 
 extern "C" int mb_node_combine(const mb::CombineArgs* a, hipStream_t st) {
   using namespace mb;
   const long total = (long)a->B * a->N;
-  hipLaunchKernelGGL(node_combine_kernel, dim3((total + 255) / 256), dim3(256), 0, st, *a);
+  if (a->dim == 3) hipLaunchKernelGGL(node_combine_kernel<3>, dim3((total + 255) / 256), dim3(256), 0, st, *a);
+  else hipLaunchKernelGGL(node_combine_kernel<2>, dim3((total + 255) / 256), dim3(256), 0, st, *a);
   return (int)hipGetLastError();
 }

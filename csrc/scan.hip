@@ -14,14 +14,19 @@
 #pragma clang fp contract(off)
 #include "common.h"
 #include "args.h"
+#include "state.h"
 
 namespace mb {
 
 
-DEV bool ttc_danger(float x, float y, float vx, float vy, float r2, float ttc) {
-  float alpha = vx * vx + vy * vy;
-  float beta = 2.0f * (x * vx + y * vy);
-  float gamma = x * x + y * y - r2;
+// D-dimensional TTC test on relative position p and velocity v (sums in coordinate order)
+template <int D>
+DEV bool ttc_danger(const float (&p)[D], const float (&v)[D], float r2, float ttc) {
+  float alpha = v[0] * v[0], pv = p[0] * v[0], pp = p[0] * p[0];
+#pragma unroll
+  for (int q = 1; q < D; ++q) { alpha = alpha + v[q] * v[q]; pv = pv + p[q] * v[q]; pp = pp + p[q] * p[q]; }
+  float beta = 2.0f * pv;
+  float gamma = pp - r2;
   float disc = beta * beta - (4.0f * alpha) * gamma;
   bool dist_d = gamma < 0.f;
   bool two_pos = (disc > 0.f) && (gamma > 0.f) && (beta < 0.f);
@@ -65,12 +70,13 @@ __global__ __launch_bounds__(SORT_BLOCK) void cell_sort_kernel(CellSortArgs a) {
   __shared__ int hist[CURVE_BINS];
   __shared__ int wsum[SORT_BLOCK / WAVE];
   const int b = blockIdx.x;
-  const float4* Sb = a.S + (long)b * a.s_env;
+  const int R = a.rec;                                  // float4s per node record
+  const float4* Sb = a.S + (long)b * a.s_env * R;
   for (int q = threadIdx.x; q < CURVE_BINS; q += SORT_BLOCK) hist[q] = 0;
   __syncthreads();
   const float inv = 32.f / a.L;
   for (int i = threadIdx.x; i < a.N; i += SORT_BLOCK) {
-    const float4 s = Sb[i];
+    const float4 s = Sb[i * R];
     const int cx = min(31, max(0, (int)(s.x * inv)));
     const int cy = min(31, max(0, (int)(s.y * inv)));
     atomicAdd(&hist[hilbert32(cx, cy)], 1);
@@ -96,7 +102,7 @@ __global__ __launch_bounds__(SORT_BLOCK) void cell_sort_kernel(CellSortArgs a) {
   __syncthreads();
   int* perm = a.perm + (long)b * a.N;
   for (int i = threadIdx.x; i < a.N; i += SORT_BLOCK) {
-    const float4 s = Sb[i];
+    const float4 s = Sb[i * R];
     const int cx = min(31, max(0, (int)(s.x * inv)));
     const int cy = min(31, max(0, (int)(s.y * inv)));
     const int p = atomicAdd(&hist[hilbert32(cx, cy)], 1);
@@ -108,9 +114,9 @@ constexpr int SCAN_BLOCK = 256;      // 4 waves x 64 agents (consecutive on the 
 constexpr int SCAN_MAXN = 4096;      // whole env staged in LDS
 constexpr int SCH = 8;               // candidates per chunk (one bounding box each)
 
-static inline size_t scan_lds_bytes(int N) {
-  const int Np = (N + SCH - 1) / SCH * SCH;
-  return (size_t)Np * 24 + (size_t)(Np / SCH) * 20;
+static inline size_t scan_lds_bytes(int Nn) {
+  const int Np = (Nn + SCH - 1) / SCH * SCH;
+  return (size_t)Np * 32 + (size_t)(Np / SCH) * 32;
 }
 
 // (d2, index) packed into one 64-bit key: d2 >= 0, so its IEEE bits order like the values and
@@ -131,78 +137,85 @@ DEV void topk_insert(uint64_t (&bk)[K], uint64_t x) {
 
 DEV float wave_min(float v) { return -wave_max(-v); }
 
-// Chunked scan with conservative culling. The env's agents are staged in curve order in LDS
-// with a bounding box (+ max speed) per chunk of 8. A wave compares the box gap to its own
-// 64-agent box: the whole chunk is skipped for kNN when the gap exceeds every lane's current
-// K-th distance (strictly, so ties are never skipped), and for the safety check when it
-// exceeds the reachable distance r + ttc*(vmax_wave + vmax_chunk) (x1.01 + 1e-4 margin). Both
-// decisions are wave-uniform branches; after the local neighbourhood has filled the lists
-// almost every far chunk costs one box test instead of 8 pair evaluations.
-template <int K>
+// Chunked scan with conservative culling. The env's graph nodes (agents, then static
+// obstacle points) are staged in curve order in LDS with a bounding box (+ max speed) per
+// chunk of 8. A wave compares the box gap to its own box (over its agent lanes): the whole
+// chunk is skipped for kNN when the gap exceeds every lane's current K-th distance (strictly,
+// so ties are never skipped), and for the safety check when it exceeds the reachable distance
+// r + ttc*(vmax_wave + vmax_chunk) (x1.01 + 1e-4 margin). Both decisions are wave-uniform
+// branches; after the local neighbourhood has filled the lists almost every far chunk costs
+// one box test instead of 8 pair evaluations. Obstacle nodes are candidates, never centres.
+template <int K, int D>
 __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanArgs a) {
   extern __shared__ float4 smem4[];
-  const int N = a.N;
-  const int Np = (N + SCH - 1) / SCH * SCH;
+  const int N = a.N, Nn = a.Nn;
+  const int Np = (Nn + SCH - 1) / SCH * SCH;
   const int nch = Np / SCH;
-  float4* tp = smem4;                                          // [Np] x, y, vx, vy
-  float2* tq = reinterpret_cast<float2*>(tp + Np);             // [Np] |v|, agent id (bits)
-  float4* cb = reinterpret_cast<float4*>(tq + Np);             // [nch] minx, miny, maxx, maxy
-  float* cv = reinterpret_cast<float*>(cb + nch);              // [nch] max |v|
+  float4* tp = smem4;                                          // [Np] x, y, z, node id (bits)
+  float4* tv = tp + Np;                                        // [Np] vx, vy, vz, |v|
+  float4* cbl = tv + Np;                                       // [nch] min x, y, z, max |v|
+  float4* cbh = cbl + nch;                                     // [nch] max x, y, z
   __shared__ float red[3][SCAN_BLOCK / WAVE];
   const int b = blockIdx.y;
-  const float4* Sb = a.S + (long)b * a.s_env;
-  const int* perm = a.perm + (long)b * N;
+  const float4* Sb = a.S + (long)b * a.s_env * REC<D>;
+  const int* perm = a.perm + (long)b * Nn;
   for (int q = threadIdx.x; q < Np; q += SCAN_BLOCK) {
-    if (q < N) {
+    if (q < Nn) {
       const int id = perm[q];
-      const float4 s = Sb[id];
-      tp[q] = s;
-      tq[q] = make_float2(sqrtf(s.z * s.z + s.w * s.w), __int_as_float(id));
+      float p[D], v[D];
+      load_rec<D>(Sb, (unsigned)id, p, v);
+      const float z = (D == 3) ? p[D - 1] : 0.f;
+      const float vz = (D == 3) ? v[D - 1] : 0.f;
+      tp[q] = make_float4(p[0], p[1], z, __int_as_float(id));
+      tv[q] = make_float4(v[0], v[1], vz, sqrtf(sqsum<D>(v)));
     } else {
-      tp[q] = make_float4(INFINITY, INFINITY, 0.f, 0.f);      // key == KEY_EMPTY: never selected
-      tq[q] = make_float2(0.f, __int_as_float(-1));
+      tp[q] = make_float4(INFINITY, INFINITY, INFINITY, __int_as_float(-1));   // key == KEY_EMPTY
+      tv[q] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
   }
   __syncthreads();
   for (int c = threadIdx.x; c < nch; c += SCAN_BLOCK) {
-    float4 bx = make_float4(INFINITY, INFINITY, -INFINITY, -INFINITY);
-    float vm = 0.f;
+    float4 lo = make_float4(INFINITY, INFINITY, INFINITY, 0.f);
+    float4 hi = make_float4(-INFINITY, -INFINITY, -INFINITY, 0.f);
 #pragma unroll
     for (int u = 0; u < SCH; ++u) {
       const int q = c * SCH + u;
-      if (q < N) {
+      if (q < Nn) {
         const float4 s = tp[q];
-        bx.x = fminf(bx.x, s.x); bx.y = fminf(bx.y, s.y);
-        bx.z = fmaxf(bx.z, s.x); bx.w = fmaxf(bx.w, s.y);
-        vm = fmaxf(vm, tq[q].x);
+        lo.x = fminf(lo.x, s.x); lo.y = fminf(lo.y, s.y); lo.z = fminf(lo.z, s.z);
+        hi.x = fmaxf(hi.x, s.x); hi.y = fmaxf(hi.y, s.y); hi.z = fmaxf(hi.z, s.z);
+        lo.w = fmaxf(lo.w, tv[q].w);
       }
     }
-    cb[c] = bx;
-    cv[c] = vm;
+    cbl[c] = lo;
+    cbh[c] = hi;
   }
   __syncthreads();
   const int wave = threadIdx.x / WAVE, lane = threadIdx.x & 63;
   const int pos = blockIdx.x * SCAN_BLOCK + threadIdx.x;      // my position on the curve
-  const bool act = pos < N;
-  float4 me = make_float4(0.f, 0.f, 0.f, 0.f);
-  float myv = 0.f;
-  int i = 0;
-  if (act) {
+  float4 me = make_float4(0.f, 0.f, 0.f, 0.f), mv = make_float4(0.f, 0.f, 0.f, 0.f);
+  int i = -1;
+  if (pos < Nn) {
     me = tp[pos];
-    const float2 mq = tq[pos];
-    myv = mq.x;
-    i = __float_as_int(mq.y);
+    mv = tv[pos];
+    i = __float_as_int(me.w);
   }
+  const bool act = pos < Nn && i >= 0 && i < N;                // agents are centres, obstacles not
   const float rc = sqrtf(a.r2_check);
   // per-pair pre-test of the safety check: dangerous => |p| < r + ttc*|v_i - v_j| <= r + ttc*(|v_i|+|v_j|)
-  const float base_i = rc + a.ttc_check * myv;
+  const float base_i = rc + a.ttc_check * mv.w;
   uint64_t bk[K];
 #pragma unroll
   for (int q = 0; q < K; ++q) bk[q] = KEY_EMPTY;
   bool danger = false;
   const float wminx = wave_min(act ? me.x : INFINITY), wmaxx = wave_max(act ? me.x : -INFINITY);
   const float wminy = wave_min(act ? me.y : INFINITY), wmaxy = wave_max(act ? me.y : -INFINITY);
-  const float wvmax = wave_max(act ? myv : 0.f);
+  float wminz = 0.f, wmaxz = 0.f;
+  if constexpr (D == 3) {
+    wminz = wave_min(act ? me.z : INFINITY);
+    wmaxz = wave_max(act ? me.z : -INFINITY);
+  }
+  const float wvmax = wave_max(act ? mv.w : 0.f);
   const bool wave_live = __any(act);
   int cc0 = (blockIdx.x * SCAN_BLOCK + wave * WAVE + 32) / SCH;
   if (cc0 >= nch) cc0 = nch - 1;
@@ -211,43 +224,53 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanArgs a) {
   if (wave_live) {
     // chunk metadata is read one step ahead of the (deterministic) walk to hide LDS latency
     int ch = cc0;
-    float4 bx = cb[ch];
-    float cvm = cv[ch];
+    float4 bl = cbl[ch], bh = cbh[ch];
     for (int m = 0; m < nch; ++m) {
       const int cur = ch;
-      const float4 cbx = bx;
-      const float ccv = cvm;
+      const float4 cl = bl, chh = bh;
       {
         const int k = (m + 2) >> 1;
         int nx = ((m + 1) & 1) ? cc0 - k : cc0 + k;
         if (nx >= nch) nx -= nch;
         if (nx < 0) nx += nch;
         ch = nx;
-        if (m + 1 < nch) { bx = cb[ch]; cvm = cv[ch]; }
+        if (m + 1 < nch) { bl = cbl[ch]; bh = cbh[ch]; }
       }
-      const float gx = fmaxf(0.f, fmaxf(cbx.x - wmaxx, wminx - cbx.z));
-      const float gy = fmaxf(0.f, fmaxf(cbx.y - wmaxy, wminy - cbx.w));
-      const float bd2 = (gx * gx + gy * gy) * 0.999f;
+      const float gx = fmaxf(0.f, fmaxf(cl.x - wmaxx, wminx - chh.x));
+      const float gy = fmaxf(0.f, fmaxf(cl.y - wmaxy, wminy - chh.y));
+      float bd2 = gx * gx + gy * gy;
+      if constexpr (D == 3) {
+        const float gz = fmaxf(0.f, fmaxf(cl.z - wmaxz, wminz - chh.z));
+        bd2 = bd2 + gz * gz;
+      }
+      bd2 = bd2 * 0.999f;
       const bool nk = a.do_knn && !(bd2 > thr);
-      const float lb = 1.01f * (rc + a.ttc_check * (wvmax + ccv)) + 1e-4f;
+      const float lb = 1.01f * (rc + a.ttc_check * (wvmax + cl.w)) + 1e-4f;
       const bool ns = a.do_safety && !all_danger && !(bd2 > lb * lb);
       if (!nk && !ns) continue;
       float4 c[SCH];
-      float2 cq[SCH];
 #pragma unroll
-      for (int u = 0; u < SCH; ++u) { c[u] = tp[cur * SCH + u]; cq[u] = tq[cur * SCH + u]; }
+      for (int u = 0; u < SCH; ++u) c[u] = tp[cur * SCH + u];
 #pragma unroll
       for (int u = 0; u < SCH; ++u) {
-        const int j = __float_as_int(cq[u].y);
-        const float dx = me.x - c[u].x;
-        const float dy = me.y - c[u].y;
-        const float d2 = dx * dx + dy * dy;
+        const int j = __float_as_int(c[u].w);
+        float dp[D];
+        dp[0] = me.x - c[u].x;
+        dp[1] = me.y - c[u].y;
+        if constexpr (D == 3) dp[2] = me.z - c[u].z;
+        const float d2 = sqsum<D>(dp);
         const uint64_t key = knn_key(d2, (unsigned)j);
         if (nk && act && key < bk[K - 1]) topk_insert<K>(bk, key);
         if (ns && act && !danger) {
-          const float lim = 1.01f * (base_i + a.ttc_check * cq[u].x) + 1e-4f;
-          if (d2 < lim * lim && j != i)
-            danger = ttc_danger(dx, dy, me.z - c[u].z, me.w - c[u].w, a.r2_check, a.ttc_check);
+          const float4 cv = tv[cur * SCH + u];
+          const float lim = 1.01f * (base_i + a.ttc_check * cv.w) + 1e-4f;
+          if (d2 < lim * lim && j != i) {
+            float dv[D];
+            dv[0] = mv.x - cv.x;
+            dv[1] = mv.y - cv.y;
+            if constexpr (D == 3) dv[2] = mv.z - cv.z;
+            danger = ttc_danger<D>(dp, dv, a.r2_check, a.ttc_check);
+          }
         }
       }
       if (nk) thr = wave_max(act ? __uint_as_float((unsigned)(bk[K - 1] >> 32)) : -INFINITY);
@@ -258,15 +281,18 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanArgs a) {
   if (act && a.do_knn) {
     int* out = a.idx + (long)b * a.i_env + (long)i * K;
     uint8_t* dout = a.dang ? a.dang + (long)b * a.i_env + (long)i * K : nullptr;
-    const float4 si = me;
+    float pi[D], vi[D];
+    load_rec<D>(Sb, (unsigned)i, pi, vi);
 #pragma unroll
     for (int q = 0; q < K; ++q) {
       const int j = (int)(unsigned)bk[q];
       out[q] = j;
-      const float4 sj = Sb[j];
+      float pj[D], vj[D], dp[D], dv[D];
+      load_rec<D>(Sb, (unsigned)j, pj, vj);
       const float eye = (j == i) ? 1.f : 0.f;
-      const bool dg = ttc_danger((si.x - sj.x) + eye, (si.y - sj.y) + eye, si.z - sj.z, si.w - sj.w,
-                                 a.r2_train, a.ttc_train);
+#pragma unroll
+      for (int d = 0; d < D; ++d) { dp[d] = (pi[d] - pj[d]) + eye; dv[d] = vi[d] - vj[d]; }
+      const bool dg = ttc_danger<D>(dp, dv, a.r2_train, a.ttc_train);
       if (dout) dout[q] = dg ? 1 : 0;
       ndang += dg ? 1.f : 0.f;
     }
@@ -289,12 +315,18 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanArgs a) {
   }
 }
 
+template <int K, int D>
+static void launch_kd(const ScanArgs& a, hipStream_t st) {
+  dim3 grid((a.Nn + SCAN_BLOCK - 1) / SCAN_BLOCK, a.B);
+  const size_t lds = scan_lds_bytes(a.Nn);
+  (void)hipFuncSetAttribute((const void*)scan_kernel<K, D>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipLaunchKernelGGL((scan_kernel<K, D>), grid, dim3(SCAN_BLOCK), lds, st, a);
+}
+
 template <int K>
 static void launch_k(const ScanArgs& a, hipStream_t st) {
-  dim3 grid((a.N + SCAN_BLOCK - 1) / SCAN_BLOCK, a.B);
-  const size_t lds = scan_lds_bytes(a.N);
-  (void)hipFuncSetAttribute((const void*)scan_kernel<K>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL(scan_kernel<K>, grid, dim3(SCAN_BLOCK), lds, st, a);
+  if (a.dim == 3) launch_kd<K, 3>(a, st);
+  else launch_kd<K, 2>(a, st);
 }
 
 }  // namespace mb
@@ -307,7 +339,7 @@ extern "C" int mb_cell_sort(const mb::CellSortArgs* a, hipStream_t st) {
 
 extern "C" int mb_scan(const mb::ScanArgs* a, hipStream_t st) {
   using namespace mb;
-  if (a->N > SCAN_MAXN || !a->perm) return -3;
+  if (a->Nn > SCAN_MAXN || a->Nn < a->N || !a->perm) return -3;
   switch (a->do_knn ? a->K : 1) {
 #define CASE(k) case k: launch_k<k>(*a, st); break;
     CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8)

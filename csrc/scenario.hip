@@ -11,21 +11,36 @@
 // tested against the host sampler. LDS: 25 B per agent (N <= 6000).
 #include "common.h"
 #include "args.h"
+#include "state.h"
 
 namespace mb {
 
 
 constexpr int SC_BLOCK = 1024;
 
+template <int D>
+DEV float d2_to(const float* c, const float* q) {
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < D; ++k) { const float d = c[k] - q[k]; s += d * d; }
+  return s;
+}
+
+// D-dimensional variant: positions in [0, L]^D, goals start + U(-spread, spread)^D, and the
+// optional static obstacle points (per env) as fixed conflict points of both phases. The
+// origin exclusion of the reference's zero rows is kept for D = 2 (core.py:45-71).
+template <int D>
 __global__ __launch_bounds__(SC_BLOCK) void scenario_kernel(ScenArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  float2* pos = reinterpret_cast<float2*>(smem);        // accepted points of this phase
-  float2* cand = pos + a.N;                               // this round's candidates
-  float2* starts = cand + a.N;                            // phase-0 result (goal anchors)
-  unsigned char* placed = reinterpret_cast<unsigned char*>(starts + a.N);
+  float* pos = reinterpret_cast<float*>(smem);           // accepted points of this phase (N x D)
+  float* cand = pos + a.N * D;                            // this round's candidates
+  float* starts = cand + a.N * D;                         // phase-0 result (goal anchors)
+  float* obs = starts + a.N * D;                          // M x D obstacle points
+  unsigned char* placed = reinterpret_cast<unsigned char*>(obs + a.M * D);
   __shared__ int n_unplaced;
   const int b = blockIdx.x;
   const float r2 = a.r * a.r;
+  for (int q = threadIdx.x; q < a.M * D; q += SC_BLOCK) obs[q] = a.obs[(long)b * a.M * D + q];
   int status = 0;
   for (int phase = 0; phase < 2; ++phase) {
     for (int i = threadIdx.x; i < a.N; i += SC_BLOCK) placed[i] = 0;
@@ -38,30 +53,23 @@ __global__ __launch_bounds__(SC_BLOCK) void scenario_kernel(ScenArgs a) {
         key = mix64(key ^ ((unsigned long long)b << 1));
         key = mix64(key ^ ((unsigned long long)phase << 7) ^ ((unsigned long long)round << 9));
         key = key ^ ((unsigned long long)i << 24);
-        const float u = u01(2 * key), v = u01(2 * key + 1);
-        float2 c;
-        if (phase == 0) {
-          c = make_float2(u * a.L, v * a.L);
-        } else {
-          const float2 s = starts[i];
-          c = make_float2(s.x + (u - 0.5f) * 2.f * a.spread, s.y + (v - 0.5f) * 2.f * a.spread);
+#pragma unroll
+        for (int k = 0; k < D; ++k) {
+          const float u = u01(D * key + k);
+          cand[i * D + k] = (phase == 0) ? u * a.L : starts[i * D + k] + (u - 0.5f) * 2.f * a.spread;
         }
-        cand[i] = c;
       }
       __syncthreads();
       for (int i = threadIdx.x; i < a.N; i += SC_BLOCK) {
         if (placed[i]) continue;
-        const float2 c = cand[i];
-        bool ok = (c.x * c.x + c.y * c.y) > r2;
+        const float* c = cand + i * D;
+        bool ok = true;
+        if (D == 2) ok = (c[0] * c[0] + c[1] * c[1]) > r2;
+        for (int q = 0; q < a.M && ok; ++q) ok = d2_to<D>(c, obs + q * D) > r2;
         for (int j = 0; j < a.N && ok; ++j) {
           const unsigned char pj = placed[j];
-          if (pj == 1) {
-            const float dx = c.x - pos[j].x, dy = c.y - pos[j].y;
-            ok = (dx * dx + dy * dy) > r2;
-          } else if (j < i) {
-            const float dx = c.x - cand[j].x, dy = c.y - cand[j].y;
-            ok = (dx * dx + dy * dy) > r2;
-          }
+          if (pj == 1) ok = d2_to<D>(c, pos + j * D) > r2;
+          else if (j < i) ok = d2_to<D>(c, cand + j * D) > r2;
         }
         if (ok) placed[i] = 2;
       }
@@ -70,8 +78,11 @@ __global__ __launch_bounds__(SC_BLOCK) void scenario_kernel(ScenArgs a) {
       __syncthreads();
       int local = 0;
       for (int i = threadIdx.x; i < a.N; i += SC_BLOCK) {
-        if (placed[i] == 2) { placed[i] = 1; pos[i] = cand[i]; }
-        else if (placed[i] == 0) ++local;
+        if (placed[i] == 2) {
+          placed[i] = 1;
+#pragma unroll
+          for (int k = 0; k < D; ++k) pos[i * D + k] = cand[i * D + k];
+        } else if (placed[i] == 0) ++local;
       }
       if (local) atomicAdd(&n_unplaced, local);
       __syncthreads();
@@ -80,17 +91,21 @@ __global__ __launch_bounds__(SC_BLOCK) void scenario_kernel(ScenArgs a) {
     if (round >= a.max_rounds) {
       status = -1;   // flagged to the host; keep the last proposals so outputs are defined
       for (int i = threadIdx.x; i < a.N; i += SC_BLOCK)
-        if (placed[i] == 0) pos[i] = cand[i];
+        if (placed[i] == 0)
+          for (int k = 0; k < D; ++k) pos[i * D + k] = cand[i * D + k];
       __syncthreads();
     }
     else if (phase == 1 && status == 0) status = round + 1;
     for (int i = threadIdx.x; i < a.N; i += SC_BLOCK) {
-      const float2 p = pos[i];
+      const float* p = pos + i * D;
       if (phase == 0) {
-        a.S[(long)b * a.N + i] = make_float4(p.x, p.y, 0.f, 0.f);
-        starts[i] = p;
+        float pp[D], vv[D];
+#pragma unroll
+        for (int k = 0; k < D; ++k) { pp[k] = p[k]; vv[k] = 0.f; starts[i * D + k] = p[k]; }
+        store_rec<D>(a.S + (long)b * a.s_env * REC<D>, (unsigned)i, pp, vv);
       } else {
-        a.G[(long)b * a.N + i] = p;
+#pragma unroll
+        for (int k = 0; k < D; ++k) a.G[((long)b * a.N + i) * D + k] = p[k];
       }
     }
     __syncthreads();
@@ -102,9 +117,15 @@ __global__ __launch_bounds__(SC_BLOCK) void scenario_kernel(ScenArgs a) {
 
 extern "C" int mb_scenario(const mb::ScenArgs* a, hipStream_t st) {
   using namespace mb;
-  const size_t lds = (size_t)a->N * 24 + (size_t)a->N;
+  const int D = a->dim;
+  const size_t lds = (size_t)(3 * a->N + a->M) * D * 4 + (size_t)a->N;
   if (lds > 160 * 1024 - 64) return -2;
-  (void)hipFuncSetAttribute((const void*)scenario_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL(scenario_kernel, dim3(a->B), dim3(SC_BLOCK), lds, st, *a);
+  if (D == 3) {
+    (void)hipFuncSetAttribute((const void*)scenario_kernel<3>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(scenario_kernel<3>, dim3(a->B), dim3(SC_BLOCK), lds, st, *a);
+  } else {
+    (void)hipFuncSetAttribute((const void*)scenario_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(scenario_kernel<2>, dim3(a->B), dim3(SC_BLOCK), lds, st, *a);
+  }
   return (int)hipGetLastError();
 }

@@ -35,31 +35,35 @@ class HipEngine:
         cfg = trainer.cfg
         self.bptt = cfg.bptt
         self.reuse = cfg.reuse_nbr_idx
-        if cfg.dim != 2 or cfg.num_obstacles:
-            raise NotImplementedError("HIP engine: 3-D / obstacle kernels not built yet")
         native.lib()
         self.dev = trainer.device
         self.B, self.N = cfg.num_envs, cfg.num_agents
-        self.K = min(self.N, cfg.top_k)
+        self.D = cfg.dim
+        self.W = native.rec_width(self.D)
+        self.M = cfg.num_obstacles * cfg.obstacle_points          # static obstacle nodes per env
+        self.Nn = self.N + self.M
+        self.K = min(self.Nn, cfg.top_k)
         if self.K > C.MAX_TOP_K:
             raise ValueError(f"top_k <= {C.MAX_TOP_K} supported by the native kernels")
         self.Tmax = cfg.inner_loops
-        self.pw = PackedWeights(trainer.fp)
+        self.pw = PackedWeights(trainer.fp, self.D)
         offs = {pn: o for (m, pn, shape, o, n) in trainer.fp.specs}
         mk = lambda a: torch.as_tensor(a, dtype=torch.long, device=self.dev)
         self.maps = {}
         for name, fn in (("cbf", L.cbf_grad_map), ("node", L.ctrl_node_grad_map), ("edge", L.ctrl_edge_grad_map)):
-            s, d = fn(offs)
+            s, d = fn(offs, self.D)
             self.maps[name] = (mk(s), mk(d))
         self._alloc()
 
     # ------------------------------------------------------------------ buffers
     def _alloc(self):
         B, N, K, T, dev = self.B, self.N, self.K, self.Tmax, self.dev
+        D, W, Nn = self.D, self.W, self.Nn
         f32, i32, u8, bf = torch.float32, torch.int32, torch.uint8, torch.bfloat16
-        self.S = torch.zeros(T + 1, B, N, 4, dtype=f32, device=dev)
-        self.G = torch.zeros(B, N, 2, dtype=f32, device=dev)
-        self.A = torch.zeros(T, B, N, 2, dtype=f32, device=dev)
+        # node records (agents, then static obstacle points), time-major
+        self.S = torch.zeros(T + 1, B, Nn, W, dtype=f32, device=dev)
+        self.G = torch.zeros(B, N, D, dtype=f32, device=dev)
+        self.A = torch.zeros(T, B, N, D, dtype=f32, device=dev)
         # one extra graph when h' uses the recomputed kNN of s_{t+1} (reuse_nbr_idx=False)
         G1 = 0 if self.reuse else 1
         self.idx = torch.zeros(T + G1, B, N, K, dtype=i32, device=dev)
@@ -70,14 +74,14 @@ class HipEngine:
         self.act = torch.zeros(T, B, dtype=f32, device=dev)
         self.pooled = torch.zeros(T, B, N, 128, dtype=bf, device=dev)
         self.argmax = torch.zeros(T, B, N, 128, dtype=u8, device=dev)
-        self.dE = torch.zeros(2 * T * B * N * K * 4, dtype=f32, device=dev)
-        self.rptr = torch.zeros((T + G1) * B, N + 1, dtype=i32, device=dev)
+        self.dE = torch.zeros(2 * T * B * N * K * W, dtype=f32, device=dev)
+        self.rptr = torch.zeros((T + G1) * B, Nn + 1, dtype=i32, device=dev)
         self.redges = torch.zeros((T + G1) * B, N * K, dtype=i32, device=dev)
-        self.dS = torch.zeros(T + 1, B, N, 4, dtype=f32, device=dev)
-        self.Gb = torch.zeros(T + 1, B, N, 4, dtype=f32, device=dev)
+        self.dS = torch.zeros(T + 1, B, N, W, dtype=f32, device=dev)
+        self.Gb = torch.zeros(T + 1, B, N, W, dtype=f32, device=dev)
         self.dP = torch.zeros(B, N, 128, dtype=bf, device=dev)
-        self.ego = torch.zeros(B, N, 4, dtype=f32, device=dev)
-        self.dEc = torch.zeros(B, N, K, 4, dtype=f32, device=dev)
+        self.ego = torch.zeros(B, N, W, dtype=f32, device=dev)
+        self.dEc = torch.zeros(B, N, K, W, dtype=f32, device=dev)
         self.counts = torch.zeros(3, dtype=f32, device=dev)
         self.nb_node, self.nb_edge = native.ctrl_bwd_grids(B * N, dev)
         self.part_node = torch.zeros(self.nb_node, native.CTRL_NODE_PARTIAL, dtype=f32, device=dev)
@@ -95,11 +99,17 @@ class HipEngine:
         self.pw.update()
 
     # ------------------------------------------------------------------ rollout
-    def rollout(self, s0, g):
+    def rollout(self, s0, g, obs=None):
         cfg = self.tr.cfg
-        B, N, K = self.B, self.N, self.K
+        B, N, K, D = self.B, self.N, self.K, self.D
         pw = self.pw
-        self.S[0].copy_(s0)
+        self.S[0, :, :N].copy_(native.to_records(s0))
+        if self.M:
+            if obs is None or tuple(obs.shape) != (B, self.M, D):
+                raise ValueError(f"expected obstacles of shape {(B, self.M, D)}")
+            # static obstacle nodes (velocity 0) in every time slice
+            ob = native.to_records(torch.cat([obs.float(), torch.zeros_like(obs, dtype=torch.float32)], -1))
+            self.S[:, :, N:].copy_(ob.unsqueeze(0).expand(self.Tmax + 1, B, self.M, self.W))
         self.G.copy_(g)
         self.cnt.zero_()
         self.safe.zero_()
@@ -109,11 +119,11 @@ class HipEngine:
         T = self.Tmax
         for t in range(self.Tmax):
             native.scan(self.S[t], self.idx[t], self.dang[t], self.cnt[t], self.safe[t], K=K,
-                        do_knn=True, do_safety=cfg.compute_safety)
+                        do_knn=True, do_safety=cfg.compute_safety, n_agents=N)
             noise = None
             if cfg.add_noise_prob > 0:
                 coin = (torch.rand(B, 1, 1, device=self.dev, generator=self.tr.torch_gen) < cfg.add_noise_prob)
-                noise = (torch.randn(B, N, 2, device=self.dev, generator=self.tr.torch_gen) * cfg.noise_scale
+                noise = (torch.randn(B, N, D, device=self.dev, generator=self.tr.torch_gen) * cfg.noise_scale
                          * coin.to(torch.float32)).contiguous()
             native.ctrl_fwd(self.S[t], self.G, self.idx[t], pw.ctrl_w, pw.ctrl_off["ew1f"], pw.ctrl_off["nw1f"],
                             pw.ctrl_v, self.A[t], self.S[t + 1], self.dist[t], self.act[t], noise=noise,
@@ -133,7 +143,7 @@ class HipEngine:
             # safety of the final state; with reuse_nbr_idx=False also the kNN graph of s_T (for h')
             native.scan(self.S[T], self.idx[T] if not self.reuse else None, None, None,
                         self.safe[T] if cfg.compute_safety else None, K=K, do_knn=not self.reuse,
-                        do_safety=cfg.compute_safety)
+                        do_safety=cfg.compute_safety, n_agents=N)
         return T
 
     def _all_done(self, t):
@@ -144,10 +154,10 @@ class HipEngine:
     def step(self, s0, g, obs=None):
         tr = self.tr
         cfg = tr.cfg
-        B, N, K = self.B, self.N, self.K
+        B, N, K, W, Nn = self.B, self.N, self.K, self.W, self.Nn
         pw = self.pw
         tm = tr.timer
-        T = self.rollout(s0, g)
+        T = self.rollout(s0, g, obs)
         tm.mark("rollout")
         # validity: step t of env b counts iff the env was not done before t
         done = (self.dist[:T] / N) < C.DIST_MIN_CHECK                 # (T, B)
@@ -169,7 +179,7 @@ class HipEngine:
         redges = self.redges[: (T + G1) * B]
         self.aux.wait_stream(torch.cuda.current_stream(self.dev))
         with torch.cuda.stream(self.aux):
-            native.rev_csr(self.idx[: T + G1].view((T + G1) * B, N, K), rptr, redges)
+            native.rev_csr(self.idx[: T + G1].view((T + G1) * B, N, K), rptr, redges, n_nodes=Nn)
             csr_done = torch.cuda.Event()
             csr_done.record(self.aux)
         # ---- CBF: h, h', hinge losses, upstream grads and the full backward in ONE kernel
@@ -178,7 +188,7 @@ class HipEngine:
         tm.mark("counts")
         nbb = native.cbf_bwd_grid(2 * E, self.dev)
         part_cbf = self._buf(self._part_cbf, nbb, native.CBF_PARTIAL)
-        dE = self.dE[: 2 * E * 4].view(2, T, B, N, K, 4)
+        dE = self.dE[: 2 * E * W].view(2, T, B, N, K, W)
         idx1 = None if self.reuse else self.idx[1: T + 1]
         native.cbf_bwd(S, idx, None, pw.cbf_w, pw.cbf_off["w1f"], pw.cbf_rm, pw.cbf_v, passes=2, dE=dE,
                        partial=part_cbf, num_blocks=nbb, fused=True, dang=self.dang[:T], valid=valid_u8,
@@ -187,7 +197,7 @@ class HipEngine:
         cur.wait_event(csr_done)
         # no-BPTT: s_t is a detached input, only h'(s_{t+1}) gradients reach a_t
         native.node_reduce(dE, rptr, redges, self.dS, T=T, B=B, N=N, K=K, passes=2,
-                           pass_mask=0 if self.bptt else 2, shift1=G1)
+                           pass_mask=0 if self.bptt else 2, shift1=G1, n_nodes=Nn)
         tm.mark("cbf")
         # ---- controller backward
         self.part_node.zero_()
@@ -197,7 +207,7 @@ class HipEngine:
         if self.bptt:
             # BPTT through the rollout: G_t = dL/ds_t, reverse time
             self.Gb[T].copy_(self.dS[T])
-            rptr3 = rptr[: T * B].view(T, B, N + 1)
+            rptr3 = rptr[: T * B].view(T, B, Nn + 1)
             redges3 = redges[: T * B].view(T, B, N * K)
             for t in range(T - 1, -1, -1):
                 native.ctrl_node_bwd(self.pooled[t], self.S[t], self.G, self.A[t], self.Gb[t + 1], valid_u8[t],
@@ -212,15 +222,16 @@ class HipEngine:
             # T*B (step, env) pairs, with dL/da_t = dt * dL/dv_{t+1} from h'(s_{t+1}) + action loss
             TB = T * B
             nb_n, nb_e, Gr, dP = self._nobptt_bufs(TB)
-            Gr[:TB].view(T, B, N, 2).copy_(self.G.unsqueeze(0).expand(T, B, N, 2))
+            D = self.D
+            Gr[:TB].view(T, B, N, D).copy_(self.G.unsqueeze(0).expand(T, B, N, D))
             pn = self._buf(self._part_cbf_nb, ("n", nb_n), native.CTRL_NODE_PARTIAL)
             pe = self._buf(self._part_cbf_nb, ("e", nb_e), native.CTRL_EDGE_PARTIAL)
             pn.zero_()
             pe.zero_()
-            native.ctrl_node_bwd(self.pooled[:T].view(TB, N, 128), self.S[:T].view(TB, N, 4), Gr[:TB],
-                                 self.A[:T].view(TB, N, 2), self.dS[1: T + 1].view(TB, N, 4), valid_u8.view(TB),
+            native.ctrl_node_bwd(self.pooled[:T].view(TB, N, 128), self.S[:T].view(TB, Nn, W), Gr[:TB],
+                                 self.A[:T].view(TB, N, D), self.dS[1: T + 1].view(TB, N, W), valid_u8.view(TB),
                                  pw.ctrl_rm, pw.node_rm_off, pw.ctrl_v, act_coef_f, dP[:TB], None, pn, nb_n)
-            native.ctrl_edge_bwd(self.S[:T].view(TB, N, 4), self.idx[:T].view(TB, N, K), self.argmax[:T].view(TB, N, 128),
+            native.ctrl_edge_bwd(self.S[:T].view(TB, Nn, W), self.idx[:T].view(TB, N, K), self.argmax[:T].view(TB, N, 128),
                                  dP[:TB], pw.ctrl_w, pw.ctrl_off["ew1f"], pw.ctrl_off["ew2tn"], None, pe, nb_e)
             self._nb_parts = (pn, pe)
         tm.mark("bptt")
@@ -267,7 +278,7 @@ class HipEngine:
             nb_n, nb_e = native.ctrl_bwd_grids(TBm * self.N, self.dev)
             self._nobptt = {
                 "grids": (nb_n, nb_e),
-                "G": torch.zeros(TBm, self.N, 2, dtype=torch.float32, device=self.dev),
+                "G": torch.zeros(TBm, self.N, self.D, dtype=torch.float32, device=self.dev),
                 "dP": torch.zeros(TBm, self.N, 128, dtype=torch.bfloat16, device=self.dev),
             }
         nb_n, nb_e = self._nobptt["grids"]

@@ -18,13 +18,14 @@ from .packing import module_pack
 
 class _CtrlFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, s, g, idx, mp, *params):
+    def forward(ctx, s, g, obs, idx, mp, *params):
         B, N, K = idx.shape
+        D = mp.dim
         dev = s.device
         w, v, rm = mp.pack(params)
-        S = s.detach().float().contiguous()
+        S = graph.node_records(s, obs)                   # (B, Nn, W)
         G = g.detach().float().contiguous()
-        A = torch.empty(B, N, 2, dtype=torch.float32, device=dev)
+        A = torch.empty(B, N, D, dtype=torch.float32, device=dev)
         pooled = torch.empty(B, N, 128, dtype=torch.bfloat16, device=dev)
         am = torch.empty(B, N, 128, dtype=torch.uint8, device=dev)
         native.ctrl_fwd(S, G, idx, w, mp.off["ew1f"], mp.off["nw1f"], v, A, None, None, None,
@@ -40,45 +41,52 @@ class _CtrlFn(torch.autograd.Function):
         mp = ctx.mp
         w, v, rm = ctx.packed
         B, N, K = idx.shape
+        Nn, W = S.shape[1], S.shape[2]
+        D = mp.dim
         dev = S.device
-        Gn = torch.zeros(B, N, 4, dtype=torch.float32, device=dev)
-        Gn[..., 2:] = gA.float() / C.TIME_STEP
+        Gn = native.to_records(torch.cat([torch.zeros(B, N, D, device=dev), gA.float() / C.TIME_STEP], -1))
         nbn, nbe = native.ctrl_bwd_grids(B * N, dev)
         # the controller kernels accumulate into their slabs (BPTT sums over steps): start at 0
         pn = torch.zeros(nbn, native.CTRL_NODE_PARTIAL, dtype=torch.float32, device=dev)
         pe = torch.zeros(nbe, native.CTRL_EDGE_PARTIAL, dtype=torch.float32, device=dev)
         dP = torch.empty(B, N, 128, dtype=torch.bfloat16, device=dev)
-        ego = torch.empty(B, N, 4, dtype=torch.float32, device=dev)
-        dEc = torch.empty(B, N, K, 4, dtype=torch.float32, device=dev)
+        ego = torch.empty(B, N, W, dtype=torch.float32, device=dev)
+        dEc = torch.empty(B, N, K, W, dtype=torch.float32, device=dev)
         native.ctrl_node_bwd(pooled, S, G, A, Gn, None, rm, mp.rm_off, v, 0.0, dP, ego, pn, nbn)
         native.ctrl_edge_bwd(S, idx, am, dP, w, mp.off["ew1f"], mp.off["ew2tn"], dEc, pe, nbe)
         gs = gg = None
         if ctx.needs_input_grad[0]:
-            rptr = torch.empty(B, N + 1, dtype=torch.int32, device=dev)
+            rptr = torch.empty(B, Nn + 1, dtype=torch.int32, device=dev)
             red_e = torch.empty(B, N * K, dtype=torch.int32, device=dev)
-            native.rev_csr(idx, rptr, red_e)
-            gs = torch.empty(B, N, 4, dtype=torch.float32, device=dev)
-            native.node_combine(torch.zeros(B, N, 4, device=dev), ego, dEc, rptr, red_e, None, gs, K=K)
+            native.rev_csr(idx, rptr, red_e, n_nodes=Nn)
+            gsr = torch.empty(B, N, W, dtype=torch.float32, device=dev)
+            native.node_combine(torch.zeros(B, N, W, device=dev), ego, dEc, rptr, red_e, None, gsr, K=K)
+            gs = native.from_records(gsr)
         rn = torch.empty(native.CTRL_NODE_PARTIAL, dtype=torch.float32, device=dev)
         re = torch.empty(native.CTRL_EDGE_PARTIAL, dtype=torch.float32, device=dev)
         native.reduce_rows(pn, rn)
         native.reduce_rows(pe, re)
         pgrads = mp.unpack_grads({"node": rn, "edge": re})
-        return (gs, gg, None, None, *pgrads)
+        return (gs, gg, None, None, None, *pgrads)
 
 
 def controller_apply(module, s: torch.Tensor, g: torch.Tensor, idx: torch.Tensor | None,
-                     top_k: int = C.TOP_K) -> torch.Tensor:
-    """s (B, N, 4), g (B, N, 2) on the HIP device -> a (B, N, 2); differentiable in s and in the
-    module's parameters (goals are treated as constants)."""
+                     top_k: int = C.TOP_K, obstacles: torch.Tensor | None = None) -> torch.Tensor:
+    """s (..., N, 2D), g (..., N, D) on the HIP device -> a (..., N, D); differentiable in s and in
+    the module's parameters (goals and obstacles are treated as constants)."""
     lead = s.shape[:-2]
-    N = s.shape[-2]
-    s3 = s.reshape(-1, N, 4)
-    g3 = g.reshape(-1, N, 2)
+    N, SD = s.shape[-2:]
+    D = SD // 2
+    s3 = s.reshape(-1, N, SD)
+    g3 = g.reshape(-1, N, D)
+    obs = None
+    if obstacles is not None:
+        obs = obstacles if obstacles.dim() == 3 else obstacles.unsqueeze(0)
+        obs = obs.expand(s3.shape[0], *obs.shape[-2:]).float()
     if idx is None:
-        idx3 = graph.knn(s3, top_k)
+        idx3 = graph.knn(s3, top_k, obs)
     else:
         idx3 = idx.reshape(-1, N, idx.shape[-1]).to(torch.int32).contiguous()
     mp = module_pack("ctrl", module, s.device)
-    a = _CtrlFn.apply(s3.float(), g3.float(), idx3, mp, *module.parameters())
-    return a.reshape(*lead, N, 2)
+    a = _CtrlFn.apply(s3.float(), g3.float(), obs, idx3, mp, *module.parameters())
+    return a.reshape(*lead, N, D)

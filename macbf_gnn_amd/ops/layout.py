@@ -109,26 +109,53 @@ def _matT(off: int, rows: int, cols: int):
     return f
 
 
-def cbf_packer(fp_offsets: Dict[str, int]) -> Packer:
+def cbf_w1_slot(k: int, dim: int = 2):
+    """Layer-1 K slot k (0..15) of the CBF edge fragment -> ('w', feature column) | ('b',) | None.
+
+    Edge features (2D + 2 columns): s_i - s_j (0..2D-1), eye (2D), |dp|_eps - r (2D+1); every
+    fp32 input is split into a bf16 hi part (lanes h = 0, K 0..7) and its residual (lanes h = 1,
+    K 8..15). D = 2: hi [rel 4, eye, dist, 1, 0] / lo [rel 4, eye(0), dist, 0, 0];
+    D = 3: hi [rel 6, dist, 1] / lo [rel 6, dist, eye] (eye is exact in bf16)."""
+    F = 2 * dim + 2
+    if dim == 2:
+        if k < F:
+            return ("w", k)
+        if k == F:
+            return ("b",)
+        if 8 <= k < 8 + F:
+            return ("w", k - 8)
+        return None
+    if k < 2 * dim:
+        return ("w", k)
+    if k == 2 * dim:
+        return ("w", F - 1)
+    if k == 2 * dim + 1:
+        return ("b",)
+    if 8 <= k < 8 + 2 * dim:
+        return ("w", k - 8)
+    if k == 8 + 2 * dim:
+        return ("w", F - 1)
+    if k == 9 + 2 * dim:
+        return ("w", 2 * dim)
+    return None
+
+
+def cbf_packer(fp_offsets: Dict[str, int], dim: int = 2) -> Packer:
     """Fragments used by csrc/cbf.hip. Offsets are flat indices of the CBF parameters."""
     W1, b1 = fp_offsets["cbf_net.0.weight"], fp_offsets["cbf_net.0.bias"]
     W2 = fp_offsets["cbf_net.2.weight"]
     W3 = fp_offsets["cbf_net.4.weight"]
+    F = 2 * dim + 2
 
-    def w1f(o, k):           # (64 x 16): [W1 | b1 | 0] hi, [W1 | 0] lo
-        if o >= 64:
+    def w1f(o, k):           # (64 x 16): hi / lo slots of the edge features + bias
+        sl = cbf_w1_slot(k, dim) if o < 64 else None
+        if sl is None:
             return ZERO
-        if k < 6:
-            return W1 + o * 6 + k
-        if k == 6:
-            return b1 + o
-        if 8 <= k < 14:
-            return W1 + o * 6 + (k - 8)
-        return ZERO
+        return b1 + o if sl[0] == "b" else W1 + o * F + sl[1]
 
-    def w1ft(f, o):          # (32 x 64): W1^T restricted to the 6 input features
-        if f < 6 and o < 64:
-            return W1 + o * 6 + f
+    def w1ft(f, o):          # (32 x 64): W1^T, rows = feature columns
+        if f < F and o < 64:
+            return W1 + o * F + f
         return ZERO
 
     p = Packer()
@@ -141,7 +168,33 @@ def cbf_packer(fp_offsets: Dict[str, int]) -> Packer:
     return p
 
 
-def ctrl_packer(fp_offsets: Dict[str, int]) -> Packer:
+def ctrl_edge_slot(k: int, dim: int = 2):
+    """Controller edge layer-1 K slot -> ('w', col) | ('b',) | None. Features (2D + 1):
+    s_i - s_j (0..2D-1), eye (2D). hi [rel, eye, 1], lo [rel]."""
+    E = 2 * dim + 1
+    if k < E:
+        return ("w", k)
+    if k == E:
+        return ("b",)
+    if 8 <= k < 8 + 2 * dim:
+        return ("w", k - 8)
+    return None
+
+
+def ctrl_node_slot(k: int, dim: int = 2):
+    """Node layer-1 K slot (0..143) -> ('w', col) | ('b',) | None. Inputs (128 + 2D): pooled
+    (0..127), [p - g, v] (128..128+2D-1); slots 128.. = state hi, 1 (bias); 136.. = state lo."""
+    n_in = 128 + 2 * dim
+    if k < n_in:
+        return ("w", k)
+    if k == n_in:
+        return ("b",)
+    if 136 <= k < 136 + 2 * dim:
+        return ("w", 128 + (k - 136))
+    return None
+
+
+def ctrl_packer(fp_offsets: Dict[str, int], dim: int = 2) -> Packer:
     """Fragments used by csrc/ctrl.hip."""
     eW1, eb1 = fp_offsets["controller_centr_net.0.weight"], fp_offsets["controller_centr_net.0.bias"]
     eW2 = fp_offsets["controller_centr_net.2.weight"]
@@ -149,21 +202,19 @@ def ctrl_packer(fp_offsets: Dict[str, int]) -> Packer:
     nW2 = fp_offsets["controller_dec_net.2.weight"]
     nW3 = fp_offsets["controller_dec_net.4.weight"]
     nW4 = fp_offsets["controller_dec_net.6.weight"]
+    E = 2 * dim + 1
+    n_in = 128 + 2 * dim
+    SD = 2 * dim
 
-    def ew1f(o, k):          # (64 x 16): [W1(5) | b1 | 0 0] hi, [W1(:4) | 0...] lo
-        if o >= 64:
+    def ew1f(o, k):          # (64 x 16): [W1 | b1] hi, [W1(rel)] lo
+        sl = ctrl_edge_slot(k, dim) if o < 64 else None
+        if sl is None:
             return ZERO
-        if k < 5:
-            return eW1 + o * 5 + k
-        if k == 5:
-            return eb1 + o
-        if 8 <= k < 12:
-            return eW1 + o * 5 + (k - 8)
-        return ZERO
+        return eb1 + o if sl[0] == "b" else eW1 + o * E + sl[1]
 
-    def ew1ft(f, o):         # (32 x 64): W1^T for the 4 relative-state features
-        if f < 4 and o < 64:
-            return eW1 + o * 5 + f
+    def ew1ft(f, o):         # (32 x 64): W1^T for the 2D relative-state features
+        if f < SD and o < 64:
+            return eW1 + o * E + f
         return ZERO
 
     def ew2tn(m, f):         # (64 x 128) = W2^T, paired with a natural-k B (dZ from LDS)
@@ -171,20 +222,15 @@ def ctrl_packer(fp_offsets: Dict[str, int]) -> Packer:
             return eW2 + f * 64 + m
         return ZERO
 
-    def nw1f(o, k):          # (64 x 144): [pooled 128 | state hi 4 | b1 | 0 0 0 | state lo 4 | 0 x4]
-        if o >= 64:
+    def nw1f(o, k):          # (64 x 144): [pooled 128 | state hi 2D | b1 | .. | state lo 2D | ..]
+        sl = ctrl_node_slot(k, dim) if o < 64 else None
+        if sl is None:
             return ZERO
-        if k < 132:
-            return nW1 + o * 132 + k
-        if k == 132:
-            return nb1 + o
-        if 136 <= k < 140:
-            return nW1 + o * 132 + 128 + (k - 136)
-        return ZERO
+        return nb1 + o if sl[0] == "b" else nW1 + o * n_in + sl[1]
 
     def nw1ft(k, o):         # (160 x 64) = nw1f^T restricted to the hi/pooled rows
-        if o < 64 and k < 132:
-            return nW1 + o * 132 + k
+        if o < 64 and k < n_in:
+            return nW1 + o * n_in + k
         return ZERO
 
     p = Packer()
@@ -195,8 +241,8 @@ def ctrl_packer(fp_offsets: Dict[str, int]) -> Packer:
     p.add("nw1f", nw1f, 2, 9, "nat")
     p.add("nw2", _mat(nW2, 128, 64), 4, 4, "acc")
     p.add("nw3", _mat(nW3, 64, 128), 2, 8, "acc")
-    p.add("nw4", _mat(nW4, 4, 64), 1, 4, "acc")
-    p.add("nw4t", _matT(nW4, 4, 64), 2, 2, "acc")
+    p.add("nw4", _mat(nW4, SD, 64), 1, 4, "acc")
+    p.add("nw4t", _matT(nW4, SD, 64), 2, 2, "acc")
     p.add("nw3t", _matT(nW3, 64, 128), 4, 4, "acc")
     p.add("nw2t", _matT(nW2, 128, 64), 2, 8, "acc")
     p.add("nw1ft", nw1ft, 5, 4, "acc")
@@ -210,11 +256,11 @@ def cbf_vec_index(fp_offsets) -> Tuple[np.ndarray, Dict[str, int]]:
     return _vec(parts)
 
 
-def ctrl_vec_index(fp_offsets) -> Tuple[np.ndarray, Dict[str, int]]:
+def ctrl_vec_index(fp_offsets, dim: int = 2) -> Tuple[np.ndarray, Dict[str, int]]:
     parts = [("eb2", fp_offsets["controller_centr_net.2.bias"], 128),
              ("nb2", fp_offsets["controller_dec_net.2.bias"], 128),
              ("nb3", fp_offsets["controller_dec_net.4.bias"], 64),
-             ("nb4", fp_offsets["controller_dec_net.6.bias"], 4, 32)]
+             ("nb4", fp_offsets["controller_dec_net.6.bias"], 2 * dim, 32)]
     return _vec(parts)
 
 
@@ -308,27 +354,25 @@ class RMPacker:
 NODE_STRIDES = {"w1": 168, "w2": 72, "w3": 136, "w4": 72}
 
 
-def ctrl_node_rm(fp_offsets) -> RMPacker:
+def ctrl_node_rm(fp_offsets, dim: int = 2) -> RMPacker:
     """Row-major node-MLP images for the controller backward kernel (csrc/ctrl.hip)."""
     nW1, nb1 = fp_offsets["controller_dec_net.0.weight"], fp_offsets["controller_dec_net.0.bias"]
     nW2 = fp_offsets["controller_dec_net.2.weight"]
     nW3 = fp_offsets["controller_dec_net.4.weight"]
     nW4 = fp_offsets["controller_dec_net.6.weight"]
+    n_in = 128 + 2 * dim
 
     def w1f(o, k):   # same virtual matrix as ctrl_packer's nw1f, 160 columns (144.. zero)
-        if k < 132:
-            return nW1 + o * 132 + k
-        if k == 132:
-            return nb1 + o
-        if 136 <= k < 140:
-            return nW1 + o * 132 + 128 + (k - 136)
-        return ZERO
+        sl = ctrl_node_slot(k, dim)
+        if sl is None:
+            return ZERO
+        return nb1 + o if sl[0] == "b" else nW1 + o * n_in + sl[1]
 
     p = RMPacker()
     p.add("w1", w1f, 64, 160, NODE_STRIDES["w1"])
     p.add("w2", _mat(nW2, 128, 64), 128, 64, NODE_STRIDES["w2"])
     p.add("w3", _mat(nW3, 64, 128), 64, 128, NODE_STRIDES["w3"])
-    p.add("w4", _mat(nW4, 4, 64), 32, 64, NODE_STRIDES["w4"])
+    p.add("w4", _mat(nW4, 2 * dim, 64), 32, 64, NODE_STRIDES["w4"])
     return p
 
 
@@ -381,65 +425,73 @@ def _pairs_rowmajor(base_slab, ncols_slab, param_off, rows, cols):
     return src, dst
 
 
-def cbf_grad_map(fp_offsets):
+def cbf_grad_map(fp_offsets, dim: int = 2):
     """(src in the reduced CBF slab, dst in the flat grad) pairs; src may repeat dst (hi/lo)."""
     W1, b1 = fp_offsets["cbf_net.0.weight"], fp_offsets["cbf_net.0.bias"]
     W2, b2 = fp_offsets["cbf_net.2.weight"], fp_offsets["cbf_net.2.bias"]
     W3, b3 = fp_offsets["cbf_net.4.weight"], fp_offsets["cbf_net.4.bias"]
     W4, b4 = fp_offsets["cbf_net.6.weight"], fp_offsets["cbf_net.6.bias"]
+    F = 2 * dim + 2
     S, D = [], []
     for s_, d_ in (_pairs_rowmajor(0, 128, W3, 64, 128), _pairs_rowmajor(8256, 64, W2, 128, 64)):
         S += s_; D += d_
     S += [8192 + m for m in range(64)]; D += [b3 + m for m in range(64)]
     S += [16448 + m for m in range(128)]; D += [b2 + m for m in range(128)]
     for o in range(64):
-        for k in range(6):
-            S += [16576 + o * 32 + k, 16576 + o * 32 + 8 + k]; D += [W1 + o * 6 + k] * 2
-        S.append(16576 + o * 32 + 6); D.append(b1 + o)
+        for k in range(16):
+            sl = cbf_w1_slot(k, dim)
+            if sl is None:
+                continue
+            S.append(16576 + o * 32 + k)
+            D.append(b1 + o if sl[0] == "b" else W1 + o * F + sl[1])
     S += [18624 + n for n in range(64)]; D += [W4 + n for n in range(64)]
     S.append(18688); D.append(b4)
     return np.asarray(S, np.int64), np.asarray(D, np.int64)
 
 
-def ctrl_node_grad_map(fp_offsets):
+def ctrl_node_grad_map(fp_offsets, dim: int = 2):
     nW1, nb1 = fp_offsets["controller_dec_net.0.weight"], fp_offsets["controller_dec_net.0.bias"]
     nW2, nb2 = fp_offsets["controller_dec_net.2.weight"], fp_offsets["controller_dec_net.2.bias"]
     nW3, nb3 = fp_offsets["controller_dec_net.4.weight"], fp_offsets["controller_dec_net.4.bias"]
     nW4, nb4 = fp_offsets["controller_dec_net.6.weight"], fp_offsets["controller_dec_net.6.bias"]
+    n_in = 128 + 2 * dim
     S, D = [], []
     for o in range(64):
-        for k in range(132):
-            S.append(o * 160 + k); D.append(nW1 + o * 132 + k)
-        S.append(o * 160 + 132); D.append(nb1 + o)
-        for k in range(4):
-            S.append(o * 160 + 136 + k); D.append(nW1 + o * 132 + 128 + k)
+        for k in range(160):
+            sl = ctrl_node_slot(k, dim)
+            if sl is None:
+                continue
+            S.append(o * 160 + k)
+            D.append(nb1 + o if sl[0] == "b" else nW1 + o * n_in + sl[1])
     for s_, d_ in (_pairs_rowmajor(10240, 64, nW2, 128, 64), _pairs_rowmajor(18560, 128, nW3, 64, 128),
-                   _pairs_rowmajor(26816, 64, nW4, 4, 64)):
+                   _pairs_rowmajor(26816, 64, nW4, 2 * dim, 64)):
         S += s_; D += d_
     S += [18432 + m for m in range(128)]; D += [nb2 + m for m in range(128)]
     S += [26752 + m for m in range(64)]; D += [nb3 + m for m in range(64)]
-    S += [28864 + m for m in range(4)]; D += [nb4 + m for m in range(4)]
+    S += [28864 + m for m in range(2 * dim)]; D += [nb4 + m for m in range(2 * dim)]
     return np.asarray(S, np.int64), np.asarray(D, np.int64)
 
 
-def ctrl_edge_grad_map(fp_offsets):
+def ctrl_edge_grad_map(fp_offsets, dim: int = 2):
     eW1, eb1 = fp_offsets["controller_centr_net.0.weight"], fp_offsets["controller_centr_net.0.bias"]
     eW2, eb2 = fp_offsets["controller_centr_net.2.weight"], fp_offsets["controller_centr_net.2.bias"]
+    E = 2 * dim + 1
     S, D = _pairs_rowmajor(0, 64, eW2, 128, 64)
     S += [8192 + m for m in range(128)]; D += [eb2 + m for m in range(128)]
     for o in range(64):
-        for k in range(5):
-            S.append(8320 + o * 32 + k); D.append(eW1 + o * 5 + k)
-        for k in range(4):
-            S.append(8320 + o * 32 + 8 + k); D.append(eW1 + o * 5 + k)
-        S.append(8320 + o * 32 + 5); D.append(eb1 + o)
+        for k in range(16):
+            sl = ctrl_edge_slot(k, dim)
+            if sl is None:
+                continue
+            S.append(8320 + o * 32 + k)
+            D.append(eb1 + o if sl[0] == "b" else eW1 + o * E + sl[1])
     return np.asarray(S, np.int64), np.asarray(D, np.int64)
 
 
 CBF_RM_STRIDES = {"w2": 72, "w3": 136}
 
 
-def cbf_rm(fp_offsets) -> RMPacker:
+def cbf_rm(fp_offsets, dim: int = 2) -> RMPacker:
     """Row-major CBF images for the backward kernel: W2 (128x64) and W3 (64x128)."""
     W2 = fp_offsets["cbf_net.2.weight"]
     W3 = fp_offsets["cbf_net.4.weight"]

@@ -80,6 +80,37 @@ def _ok(rc, what):
         raise NativeError(f"{what} launch failed: {rc} ({lib().err_str(rc) if rc > 0 else 'bad args'})")
 
 
+# ----------------------------------------------------------------------------- node records
+def rec_width(dim: int) -> int:
+    """Floats per node record: D = 2 -> (x, y, vx, vy); D = 3 -> (x, y, z, 0, vx, vy, vz, 0)."""
+    return 4 if dim == 2 else 8
+
+
+def dim_of(S) -> int:
+    w = S.shape[-1]
+    if w == 4:
+        return 2
+    if w == 8:
+        return 3
+    raise NativeError(f"node records must be 4 (2-D) or 8 (3-D) floats wide, got {w}")
+
+
+def to_records(s: torch.Tensor) -> torch.Tensor:
+    """(..., 2D) states -> (..., rec_width(D)) kernel records (identity for D = 2)."""
+    D = s.shape[-1] // 2
+    if D == 2:
+        return s.contiguous()
+    z = torch.zeros(*s.shape[:-1], 1, dtype=s.dtype, device=s.device)
+    return torch.cat([s[..., :3], z, s[..., 3:6], z], -1).contiguous()
+
+
+def from_records(r: torch.Tensor) -> torch.Tensor:
+    """Inverse of ``to_records``."""
+    if r.shape[-1] == 4:
+        return r
+    return torch.cat([r[..., 0:3], r[..., 4:7]], -1)
+
+
 # ----------------------------------------------------------------------------- kernels
 SCAN_MAX_N = 4096
 _perm_cache = {}
@@ -94,20 +125,23 @@ def _perm_buf(B, N, device):
     return t
 
 
-def scan(S, idx, dang, cnt, safe, *, K, do_knn=True, do_safety=True, perm=None):
+def scan(S, idx, dang, cnt, safe, *, K, do_knn=True, do_safety=True, perm=None, n_agents=None):
     """K1 over one timestep. S: (B, N, 4) view with env stride (may be a slice of a (B,T+1,N,4)
     buffer); idx/dang: (B, N, K) views; cnt: (B, 2) view; safe: (B,) view.
 
     Two launches: cell_sort orders each env's agents along a Hilbert curve, then the scan walks
     candidates outward along it (results are order independent; the order only keeps the
     wave-divergent top-K insertion rare)."""
-    B, N = S.shape[0], S.shape[1]
-    if N > SCAN_MAX_N:
-        raise NativeError(f"scan stages one env in LDS: N <= {SCAN_MAX_N} (got {N})")
-    if S.dtype != torch.float32 or S.stride(2) != 1 or S.stride(1) != 4:
-        raise NativeError("S must be float32 with contiguous (N,4) rows")
-    if K < 1 or K > C.MAX_TOP_K or K > N:
-        raise NativeError(f"bad K={K} for N={N}")
+    B, Nn = S.shape[0], S.shape[1]
+    D = dim_of(S)
+    W = rec_width(D)
+    N = Nn if n_agents is None else int(n_agents)     # centres = the first N nodes
+    if Nn > SCAN_MAX_N or N > Nn:
+        raise NativeError(f"scan stages one env in LDS: N <= Nn <= {SCAN_MAX_N} (got {N}, {Nn})")
+    if S.dtype != torch.float32 or S.stride(2) != 1 or S.stride(1) != W:
+        raise NativeError(f"S must be float32 with contiguous (Nn,{W}) rows")
+    if K < 1 or K > C.MAX_TOP_K or K > Nn:
+        raise NativeError(f"bad K={K} for Nn={Nn}")
     if do_knn:
         if idx.dtype != torch.int32 or tuple(idx.shape) != (B, N, K) or idx.stride(2) != 1 or idx.stride(1) != K:
             raise NativeError("idx must be int32 (B,N,K) with contiguous (N,K)")
@@ -119,28 +153,35 @@ def scan(S, idx, dang, cnt, safe, *, K, do_knn=True, do_safety=True, perm=None):
     if do_safety and safe is not None and (safe.dtype != torch.float32 or tuple(safe.shape) != (B,)):
         raise NativeError("safe must be float32 (B,)")
     if perm is None:
-        perm = _perm_buf(B, N, S.device)
-    rc = lib().cell_sort(ptr(S), S.stride(0) // 4, B, N, float(math.sqrt(max(1.0, N / C.AGENT_DENSITY))),
-                         ptr(perm), stream_handle())
+        perm = _perm_buf(B, Nn, S.device)
+    L = float(max(1.0, N / C.AGENT_DENSITY) ** (1.0 / D))
+    rc = lib().cell_sort(ptr(S), S.stride(0) // W, B, Nn, L, ptr(perm), W // 4, stream_handle())
     _ok(rc, "cell_sort")
-    rc = lib().scan(ptr(S), S.stride(0) // 4, ptr(perm), B, N, K, ptr(idx) if do_knn else 0,
+    rc = lib().scan(ptr(S), S.stride(0) // W, ptr(perm), B, N, K, ptr(idx) if do_knn else 0,
                     idx.stride(0) if do_knn else 0, ptr(dang) if do_knn else 0,
                     ptr(cnt) if do_knn else 0, cnt.stride(0) if (do_knn and cnt is not None) else 0,
                     ptr(safe) if do_safety else 0, safe.stride(0) if (do_safety and safe is not None) else 0,
                     float(C.DIST_MIN_THRES * C.DIST_MIN_THRES), float(C.TIME_TO_COLLISION),
                     float(C.DIST_MIN_CHECK * C.DIST_MIN_CHECK), float(C.TIME_TO_COLLISION_CHECK),
-                    int(do_knn), int(do_safety), stream_handle())
+                    int(do_knn), int(do_safety), Nn, D, stream_handle())
     _ok(rc, "scan")
 
 
-def scenario(S, G, *, seed, L, r=C.DIST_MIN_THRES, spread=C.GOAL_SPREAD, max_rounds=256, status=None):
-    B, N = S.shape[0], S.shape[1]
-    check(S, torch.float32, (B, N, 4), "S")
-    check(G, torch.float32, (B, N, 2), "G")
+def scenario(S, G, *, seed, L, r=C.DIST_MIN_THRES, spread=C.GOAL_SPREAD, max_rounds=256, status=None, obs=None):
+    """S (B, >=N, W) agent records out (velocity 0), G (B, N, D) goals out; obs (B, M, D) static
+    obstacle points kept > r from every start and goal."""
+    B, N, D = G.shape
+    W = rec_width(D)
+    _records(S, "S", (B, N), W)
+    check(G, torch.float32, (B, N, D), "G")
     check(status, torch.int32, (B,), "status")
-    if N * 25 > 160 * 1024 - 64:
-        raise NativeError(f"scenario sampler supports N <= 6500 per env (got {N})")
-    rc = lib().scenario(ptr(S), ptr(G), B, N, float(L), float(r), float(spread),
+    M = 0
+    if obs is not None:
+        M = obs.shape[1]
+        check(obs, torch.float32, (B, M, D), "obs")
+    if (3 * N + M) * D * 4 + N > 160 * 1024 - 64:
+        raise NativeError(f"scenario sampler: env too large for LDS (N={N}, M={M}, D={D})")
+    rc = lib().scenario(ptr(S), S.stride(0) // W, ptr(G), ptr(obs), M, D, B, N, float(L), float(r), float(spread),
                         int(seed) & 0xFFFFFFFFFFFFFFFF, int(max_rounds), ptr(status), stream_handle())
     _ok(rc, "scenario")
 
@@ -154,18 +195,29 @@ def _rows(t, last, name, lead):
         raise NativeError(f"{name}: expected {lead}x{last} with contiguous rows, got {tuple(t.shape)} {t.stride()}")
 
 
+def _records(t, name, lead, W, min_rows=None):
+    """(lead..., rows, W) float32 view with contiguous records; rows may exceed lead[-1] (nodes)."""
+    if t is None:
+        return
+    if t.dtype != torch.float32 or t.dim() != len(lead) + 1 or tuple(t.shape[:len(lead) - 1]) != tuple(lead[:-1]) \
+            or t.shape[-2] < lead[-1] or t.shape[-1] != W or t.stride(-1) != 1 or t.stride(-2) != W:
+        raise NativeError(f"{name}: expected {lead}x{W} float32 records, got {tuple(t.shape)} {t.stride()}")
+
+
 def ctrl_fwd(S, G, idx, wpack, f_edge, f_node, wvec, A, Sn, dist_sum, act_sum, noise=None, pooled=None, argmax=None):
-    """Fused controller step on per-step views: S/Sn (B,N,4), G (B,N,2), idx (B,N,K),
-    A (B,N,2), dist_sum/act_sum (B,), pooled (B,N,128) bf16, argmax (B,N,128) uint8."""
-    B, N = S.shape[0], S.shape[1]
-    K = idx.shape[2]
+    """Fused controller step on per-step views: S/Sn (B,Nn,W) node records (agents first),
+    G (B,N,D), idx (B,N,K), A (B,N,D), dist_sum/act_sum (B,), pooled (B,N,128) bf16,
+    argmax (B,N,128) uint8."""
+    B, N, K = idx.shape
+    D = dim_of(S)
+    W = rec_width(D)
     if K < 1 or K > C.MAX_TOP_K:
         raise NativeError("K out of range")
-    _rows(S, 4, "S", (B, N))
-    _rows(Sn, 4, "Sn", (B, N))
-    _rows(A, 2, "A", (B, N))
-    check(G, torch.float32, (B, N, 2), "G")
-    if idx.dtype != torch.int32 or idx.stride(2) != 1 or idx.stride(1) != K or tuple(idx.shape[:2]) != (B, N):
+    _records(S, "S", (B, N), W)
+    _records(Sn, "Sn", (B, N), W)
+    _rows(A, D, "A", (B, N))
+    check(G, torch.float32, (B, N, D), "G")
+    if idx.dtype != torch.int32 or idx.stride(2) != 1 or idx.stride(1) != K:
         raise NativeError("idx must be int32 (B,N,K)")
     check(wpack, torch.bfloat16, None, "wpack")
     check(wvec, torch.float32, None, "wvec")
@@ -174,7 +226,7 @@ def ctrl_fwd(S, G, idx, wpack, f_edge, f_node, wvec, A, Sn, dist_sum, act_sum, n
     for t, n in ((dist_sum, "dist_sum"), (act_sum, "act_sum")):
         if t is not None and (t.dtype != torch.float32 or tuple(t.shape) != (B,)):
             raise NativeError(f"{n} must be float32 (B,)")
-    _rows(noise, 2, "noise", (B, N))
+    _rows(noise, D, "noise", (B, N))
     if pooled is not None:
         _rows(pooled, 128, "pooled", (B, N))
         if pooled.dtype != torch.bfloat16:
@@ -183,17 +235,17 @@ def ctrl_fwd(S, G, idx, wpack, f_edge, f_node, wvec, A, Sn, dist_sum, act_sum, n
         _rows(argmax, 128, "argmax", (B, N))
         if argmax.dtype != torch.uint8:
             raise NativeError("argmax must be uint8")
-    rc = lib().ctrl_fwd(ptr(S), S.stride(0) // 4, ptr(G), ptr(idx), idx.stride(0), B, N, K,
+    rc = lib().ctrl_fwd(ptr(S), S.stride(0) // W, ptr(G), ptr(idx), idx.stride(0), B, N, K,
                         ptr(wpack), int(f_edge), int(f_node), ptr(wvec),
-                        ptr(A), A.stride(0) // 2 if A is not None else 0,
-                        ptr(Sn), Sn.stride(0) // 4 if Sn is not None else 0,
+                        ptr(A), A.stride(0) // D if A is not None else 0,
+                        ptr(Sn), Sn.stride(0) // W if Sn is not None else 0,
                         ptr(dist_sum), dist_sum.stride(0) if dist_sum is not None else 0,
                         ptr(act_sum), act_sum.stride(0) if act_sum is not None else 0,
-                        ptr(noise), noise.stride(0) // 2 if noise is not None else 0,
+                        ptr(noise), noise.stride(0) // D if noise is not None else 0,
                         float(C.TIME_STEP), float(C.OBS_RADIUS), float(C.SQRT3),
                         ptr(pooled), pooled.stride(0) if pooled is not None else 0,
                         ptr(argmax), argmax.stride(0) if argmax is not None else 0,
-                        num_cu(S.device), stream_handle())
+                        D, num_cu(S.device), stream_handle())
     _ok(rc, "ctrl_fwd")
 
 
@@ -212,9 +264,12 @@ def cbf_fwd_grid(E: int, device) -> int:
 
 
 def _time_major_S(S, T, B, N, need):
+    """S (>= T+need, B, Nn >= N, W) node records (agents first, then obstacle points)."""
+    W = S.shape[-1] if S.dim() == 4 else 0
     if S.dtype != torch.float32 or S.dim() != 4 or S.shape[0] < T + need or S.shape[1] != B \
-            or S.shape[2] != N or S.shape[3] != 4 or S.stride(3) != 1 or S.stride(2) != 4:
-        raise NativeError(f"S must be float32 (>=T+{need}, B, N, 4) with contiguous rows")
+            or S.shape[2] < N or W not in (4, 8) or S.stride(3) != 1 or S.stride(2) != W:
+        raise NativeError(f"S must be float32 (>=T+{need}, B, >=N, 4|8) with contiguous rows")
+    return dim_of(S), W
 
 
 def cbf_fwd(S, idx, wpack, f_fwd, wvec, *, dang=None, valid=None, two=True, h_out=None, hn_out=None,
@@ -222,7 +277,7 @@ def cbf_fwd(S, idx, wpack, f_fwd, wvec, *, dang=None, valid=None, two=True, h_ou
     """Time-major: S (>=T+two, B, N, 4); idx/dang/h (T, B, N, K); valid (T, B); dh (2, T, B, N, K)."""
     T, B, N, K = idx.shape
     check(idx, torch.int32, None, "idx")
-    _time_major_S(S, T, B, N, 1 if two else 0)
+    D, W = _time_major_S(S, T, B, N, 1 if two else 0)
     E = B * T * N * K
     check(dang, torch.uint8, (T, B, N, K), "dang")
     check(valid, torch.uint8, (T, B), "valid")
@@ -235,10 +290,11 @@ def cbf_fwd(S, idx, wpack, f_fwd, wvec, *, dang=None, valid=None, two=True, h_ou
     check(wvec, torch.float32, None, "wvec")
     nb = num_blocks or cbf_fwd_grid(E, S.device)
     check(partial, torch.float32, (nb, 10), "partial")
-    rc = lib().cbf_fwd(ptr(S), S.stride(1) // 4, S.stride(0) // 4, ptr(idx), ptr(dang), ptr(valid),
+    rc = lib().cbf_fwd(ptr(S), S.stride(1) // W, S.stride(0) // W, ptr(idx), ptr(dang), ptr(valid),
                        B, T, N, K, int(two), ptr(wpack), int(f_fwd), ptr(wvec), ptr(h_out), ptr(hn_out),
                        ptr(dh_out), ptr(counts), ptr(partial), LOSS_CONSTS,
-                       float(C.OBS_RADIUS), float(C.DIST_MIN_THRES), float(C.CBF_DIST_EPS), nb, stream_handle())
+                       float(C.OBS_RADIUS), float(C.DIST_MIN_THRES), float(C.CBF_DIST_EPS_COORD * D), D, nb,
+                       stream_handle())
     _ok(rc, "cbf_fwd")
     return nb
 
@@ -256,7 +312,7 @@ def cbf_bwd(S, idx, dh, wpack, f_bwd, wrm, wvec, *, passes=2, dE=None, partial=N
     global counts [n_dang, n_safe], and writes the 10 loss partial sums at CBF_P_LOSS."""
     T, B, N, K = idx.shape
     check(idx, torch.int32, None, "idx")
-    _time_major_S(S, T, B, N, passes - 1)
+    D, W = _time_major_S(S, T, B, N, passes - 1)
     if fused:
         if passes != 2:
             raise NativeError("fused CBF backward needs passes=2")
@@ -267,7 +323,7 @@ def cbf_bwd(S, idx, dh, wpack, f_bwd, wrm, wvec, *, passes=2, dE=None, partial=N
             raise NativeError("fused CBF backward needs dang and counts")
     else:
         check(dh, torch.float32, (passes, T, B, N, K), "dh")
-    check(dE, torch.float32, (passes, T, B, N, K, 4), "dE")
+    check(dE, torch.float32, (passes, T, B, N, K, W), "dE")
     check(wpack, torch.bfloat16, None, "wpack")
     check(wvec, torch.float32, None, "wvec")
     if wpack.numel() < (f_bwd + 70) * 512:
@@ -280,59 +336,66 @@ def cbf_bwd(S, idx, dh, wpack, f_bwd, wrm, wvec, *, passes=2, dE=None, partial=N
         raise NativeError("too many edge evaluations for 32-bit indexing")
     nb = num_blocks or cbf_bwd_grid(E * passes, S.device)
     check(partial, torch.float32, (nb, CBF_PARTIAL), "partial")
-    rc = lib().cbf_bwd(ptr(S), S.stride(1) // 4, S.stride(0) // 4, ptr(idx), B, T, N, K, int(passes),
+    rc = lib().cbf_bwd(ptr(S), S.stride(1) // W, S.stride(0) // W, ptr(idx), B, T, N, K, int(passes),
                        0 if fused else ptr(dh),
                        ptr(wpack), int(f_bwd), ptr(wrm), ptr(wvec), ptr(dE), ptr(partial), float(C.OBS_RADIUS),
-                       float(C.DIST_MIN_THRES), float(C.CBF_DIST_EPS), int(fused), ptr(dang) if fused else 0,
-                       ptr(valid) if fused else 0, ptr(counts) if fused else 0, LOSS_CONSTS, ptr(idx1), nb,
+                       float(C.DIST_MIN_THRES), float(C.CBF_DIST_EPS_COORD * D), int(fused), ptr(dang) if fused else 0,
+                       ptr(valid) if fused else 0, ptr(counts) if fused else 0, LOSS_CONSTS, ptr(idx1), D, nb,
                        stream_handle())
     _ok(rc, "cbf_bwd")
     return nb
 
 
-def rev_csr(idx, rptr, redges):
-    """idx (G, N, K) int32 contiguous -> rptr (G, N+1), redges (G, N*K)."""
+def rev_csr(idx, rptr, redges, n_nodes=None):
+    """idx (G, N, K) int32 contiguous -> rptr (G, Nn+1), redges (G, N*K); Nn = n_nodes (agents +
+    obstacle points, default N)."""
     Gn, N, K = idx.shape
+    Nn = N if n_nodes is None else int(n_nodes)
     check(idx, torch.int32, (Gn, N, K), "idx")
-    check(rptr, torch.int32, (Gn, N + 1), "rptr")
+    check(rptr, torch.int32, (Gn, Nn + 1), "rptr")
     check(redges, torch.int32, (Gn, N * K), "redges")
-    _ok(lib().rev_csr(ptr(idx), Gn, N, K, ptr(rptr), ptr(redges), stream_handle()), "rev_csr")
+    _ok(lib().rev_csr(ptr(idx), Gn, N, K, ptr(rptr), ptr(redges), Nn, stream_handle()), "rev_csr")
 
 
-def node_reduce(dE, rptr, redges, out, *, T, B, N, K, passes=2, accumulate=False, pass_mask=0, shift1=0):
-    """dE (passes, T, B, N, K, 4) -> out[t'] (+)= sum over passes p of the edge->node reduction of
-    step t' - p. pass_mask selects passes (0 = all); shift1=1: pass-1 edges live in graph t+1
-    (h' on the recomputed kNN of s_{t+1}), so the CSR arrays must hold T+1 graphs."""
-    check(dE, torch.float32, (passes, T, B, N, K, 4), "dE")
+def node_reduce(dE, rptr, redges, out, *, T, B, N, K, passes=2, accumulate=False, pass_mask=0, shift1=0,
+                n_nodes=None):
+    """dE (passes, T, B, N, K, W) -> out[t'] (+)= sum over passes p of the edge->node reduction of
+    step t' - p, for the N agents. pass_mask selects passes (0 = all); shift1=1: pass-1 edges live
+    in graph t+1 (h' on the recomputed kNN of s_{t+1}), so the CSR arrays must hold T+1 graphs."""
+    Nn = N if n_nodes is None else int(n_nodes)
+    W = dE.shape[-1]
+    D = 2 if W == 4 else 3
+    check(dE, torch.float32, (passes, T, B, N, K, W), "dE")
     check(rptr, torch.int32, None, "rptr")
     check(redges, torch.int32, None, "redges")
-    if rptr.shape[0] < (T + shift1) * B or redges.shape[0] < (T + shift1) * B:
+    if rptr.shape[0] < (T + shift1) * B or redges.shape[0] < (T + shift1) * B or rptr.shape[1] != Nn + 1:
         raise NativeError("reverse CSR too small")
     if out.dtype != torch.float32 or not out.is_contiguous() or out.shape[0] < T + 1 or \
-            tuple(out.shape[1:]) != (B, N, 4):
-        raise NativeError("out must be float32 (>=T+1, B, N, 4)")
+            tuple(out.shape[1:]) != (B, N, W):
+        raise NativeError(f"out must be float32 (>=T+1, B, N, {W})")
     _ok(lib().node_reduce(ptr(dE), ptr(rptr), ptr(redges), B, T, N, K, passes, int(accumulate), ptr(out),
-                          int(pass_mask), int(shift1), stream_handle()), "node_reduce")
+                          int(pass_mask), int(shift1), Nn, D, stream_handle()), "node_reduce")
 
 
 def node_combine(dS_t, ego, dEc, rptr_t, redges_t, Gn, Gout, *, K, dt=C.TIME_STEP):
-    """All (B,N,4) views; dEc (B,N,K,4); rptr_t (B, N+1) / redges_t (B, N*K) of graph t."""
-    B, N = dS_t.shape[:2]
-    _rows(dS_t, 4, "dS_t", (B, N))
-    _rows(Gout, 4, "Gout", (B, N))
-    _rows(Gn, 4, "Gn", (B, N))
-    check(ego, torch.float32, (B, N, 4), "ego")
-    check(dEc, torch.float32, (B, N, K, 4), "dEc")
+    """All (B,N,W) record views; dEc (B,N,K,W); rptr_t (B, Nn+1) / redges_t (B, N*K) of graph t."""
+    B, N, W = dS_t.shape
+    D = 2 if W == 4 else 3
+    _records(dS_t, "dS_t", (B, N), W)
+    _records(Gout, "Gout", (B, N), W)
+    _records(Gn, "Gn", (B, N), W)
+    check(ego, torch.float32, (B, N, W), "ego")
+    check(dEc, torch.float32, (B, N, K, W), "dEc")
     if dEc is not None:
-        if rptr_t.dtype != torch.int32 or tuple(rptr_t.shape) != (B, N + 1) or rptr_t.stride(1) != 1:
-            raise NativeError("rptr_t must be int32 (B, N+1)")
+        if rptr_t.dtype != torch.int32 or rptr_t.shape[0] != B or rptr_t.shape[1] < N + 1 or rptr_t.stride(1) != 1:
+            raise NativeError("rptr_t must be int32 (B, Nn+1)")
         if redges_t.dtype != torch.int32 or tuple(redges_t.shape) != (B, N * K) or redges_t.stride(1) != 1:
             raise NativeError("redges_t must be int32 (B, N*K)")
-    _ok(lib().node_combine(ptr(dS_t), dS_t.stride(0) // 4, ptr(ego), ptr(dEc),
+    _ok(lib().node_combine(ptr(dS_t), dS_t.stride(0) // W, ptr(ego), ptr(dEc),
                            ptr(rptr_t), rptr_t.stride(0) if dEc is not None else 0,
                            ptr(redges_t), redges_t.stride(0) if dEc is not None else 0,
-                           ptr(Gn), Gn.stride(0) // 4 if Gn is not None else 0,
-                           ptr(Gout), Gout.stride(0) // 4, B, N, K, float(dt), stream_handle()), "node_combine")
+                           ptr(Gn), Gn.stride(0) // W if Gn is not None else 0,
+                           ptr(Gout), Gout.stride(0) // W, B, N, K, float(dt), D, stream_handle()), "node_combine")
 
 
 def ctrl_bwd_grids(total_agents: int, device):
@@ -342,40 +405,43 @@ def ctrl_bwd_grids(total_agents: int, device):
 
 
 def ctrl_node_bwd(pooled, S, G, A, Gn, valid_t, wrm, offs, wvec, act_coef, dP, ego, partial, num_blocks):
-    B, N = S.shape[:2]
+    B, N = G.shape[:2]
+    D = dim_of(S)
+    W = rec_width(D)
     _rows(pooled, 128, "pooled", (B, N))
-    _rows(S, 4, "S", (B, N))
-    check(G, torch.float32, (B, N, 2), "G")
-    _rows(A, 2, "A", (B, N))
-    _rows(Gn, 4, "Gn", (B, N))
+    _records(S, "S", (B, N), W)
+    check(G, torch.float32, (B, N, D), "G")
+    _rows(A, D, "A", (B, N))
+    _records(Gn, "Gn", (B, N), W)
     if valid_t is not None and (valid_t.dtype != torch.uint8 or tuple(valid_t.shape) != (B,)):
         raise NativeError("valid_t must be uint8 (B,)")
     check(wrm, torch.bfloat16, None, "wrm")
     check(dP, torch.bfloat16, (B, N, 128), "dP")
-    check(ego, torch.float32, (B, N, 4), "ego")
+    check(ego, torch.float32, (B, N, W), "ego")
     check(partial, torch.float32, (num_blocks, CTRL_NODE_PARTIAL), "partial")
-    rc = lib().ctrl_node_bwd(ptr(pooled), pooled.stride(0), ptr(S), S.stride(0) // 4, ptr(G), ptr(A), A.stride(0) // 2,
-                             ptr(Gn), Gn.stride(0) // 4 if Gn is not None else 0,
+    rc = lib().ctrl_node_bwd(ptr(pooled), pooled.stride(0), ptr(S), S.stride(0) // W, ptr(G), ptr(A), A.stride(0) // D,
+                             ptr(Gn), Gn.stride(0) // W if Gn is not None else 0,
                              ptr(valid_t), valid_t.stride(0) if valid_t is not None else 0, B, N,
                              ptr(wrm), offs["w1"], offs["w2"], offs["w3"], offs["w4"], ptr(wvec),
                              float(act_coef), float(C.TIME_STEP), float(C.SQRT3), ptr(dP), dP.stride(0),
-                             ptr(ego), ptr(partial), int(num_blocks), stream_handle())
+                             ptr(ego), ptr(partial), D, int(num_blocks), stream_handle())
     _ok(rc, "ctrl_node_bwd")
 
 
 def ctrl_edge_bwd(S, idx, argmax, dP, wpack, f_ew1f, f_ew2tn, dEc, partial, num_blocks):
-    B, N = S.shape[:2]
-    K = idx.shape[2]
-    _rows(S, 4, "S", (B, N))
-    if idx.dtype != torch.int32 or idx.stride(2) != 1 or idx.stride(1) != K or tuple(idx.shape[:2]) != (B, N):
+    B, N, K = idx.shape
+    D = dim_of(S)
+    W = rec_width(D)
+    _records(S, "S", (B, N), W)
+    if idx.dtype != torch.int32 or idx.stride(2) != 1 or idx.stride(1) != K:
         raise NativeError("idx must be int32 (B,N,K)")
     _rows(argmax, 128, "argmax", (B, N))
     check(dP, torch.bfloat16, (B, N, 128), "dP")
-    check(dEc, torch.float32, (B, N, K, 4), "dEc")
+    check(dEc, torch.float32, (B, N, K, W), "dEc")
     check(partial, torch.float32, (num_blocks, CTRL_EDGE_PARTIAL), "partial")
-    rc = lib().ctrl_edge_bwd(ptr(S), S.stride(0) // 4, ptr(idx), idx.stride(0), ptr(argmax), argmax.stride(0),
+    rc = lib().ctrl_edge_bwd(ptr(S), S.stride(0) // W, ptr(idx), idx.stride(0), ptr(argmax), argmax.stride(0),
                              ptr(dP), dP.stride(0), B, N, K, ptr(wpack), int(f_ew1f), int(f_ew2tn), ptr(dEc),
-                             dEc.stride(0) // 4 if dEc is not None else 0, ptr(partial), int(num_blocks),
+                             dEc.stride(0) // W if dEc is not None else 0, ptr(partial), D, int(num_blocks),
                              stream_handle())
     _ok(rc, "ctrl_edge_bwd")
 

@@ -30,19 +30,21 @@ class ModulePack:
     def __init__(self, kind: str, module, device):
         self.kind = kind
         offs, self.shapes, self.n = _offsets(module)
+        dim = module.in_dim // 2
+        self.dim = dim
         mk = lambda a: torch.as_tensor(L.resolve(a, self.n), dtype=torch.long, device=device)
         mkl = lambda a: torch.as_tensor(a, dtype=torch.long, device=device)
         if kind == "cbf":
-            pk = L.cbf_packer(offs)
+            pk = L.cbf_packer(offs, dim)
             vec, _ = L.cbf_vec_index(offs)
             rm = L.cbf_rm(offs)
-            self.maps = {"cbf": tuple(mkl(x) for x in L.cbf_grad_map(offs))}
+            self.maps = {"cbf": tuple(mkl(x) for x in L.cbf_grad_map(offs, dim))}
         elif kind == "ctrl":
-            pk = L.ctrl_packer(offs)
-            vec, _ = L.ctrl_vec_index(offs)
-            rm = L.ctrl_node_rm(offs)
-            self.maps = {"node": tuple(mkl(x) for x in L.ctrl_node_grad_map(offs)),
-                         "edge": tuple(mkl(x) for x in L.ctrl_edge_grad_map(offs))}
+            pk = L.ctrl_packer(offs, dim)
+            vec, _ = L.ctrl_vec_index(offs, dim)
+            rm = L.ctrl_node_rm(offs, dim)
+            self.maps = {"node": tuple(mkl(x) for x in L.ctrl_node_grad_map(offs, dim)),
+                         "edge": tuple(mkl(x) for x in L.ctrl_edge_grad_map(offs, dim))}
         else:
             raise ValueError(kind)
         self.off = pk.offsets()
@@ -68,7 +70,7 @@ class ModulePack:
 
 
 def module_pack(kind: str, module, device) -> ModulePack:
-    key = (kind, str(device))
+    key = (kind, module.in_dim, str(device))
     mp = _CACHE.get(key)
     if mp is None:
         mp = ModulePack(kind, module, device)

@@ -5,6 +5,7 @@ checkpoint at any DP width reproduces the data stream without saving RNG state.
 """
 from __future__ import annotations
 
+import numpy as np
 import torch
 
 from .. import config as C
@@ -20,17 +21,31 @@ def _mix(*xs) -> int:
     return h
 
 
+def obstacles(B, N, *, dim, num_obstacles, points, seed, device):
+    """(B, num_obstacles*points, D) static point-set obstacles (env.generate_obstacles shapes),
+    generated on the host from the counter-based seed (a few hundred points per env)."""
+    rng = np.random.default_rng(seed & 0xFFFFFFFFFFFFFFFF)
+    L = E.side_length(N, dim)
+    o = np.stack([E.generate_obstacles(num_obstacles, L, dim, rng, points) for _ in range(B)])
+    return torch.from_numpy(o).pin_memory().to(device, non_blocking=True) if device.type == "cuda" \
+        else torch.from_numpy(o)
+
+
 def generate(B, N, *, seed=0, iteration=0, rank=0, device=None, out=None, dim=2, num_obstacles=0,
              obstacle_points=12):
-    """-> (s0 (B,N,2D), g (B,N,D), obstacles (B,M,D) or None)."""
+    """-> (s0 (B,N,2D), g (B,N,D), obstacles (B,M,D) or None): on-device parallel RSA; obstacle
+    points are fixed conflict points for starts and goals."""
     device = device or torch.device("cuda")
-    if dim != 2 or num_obstacles:
-        raise NotImplementedError("on-device sampler: 2-D without obstacles (3-D / obstacles: see generate_nd)")
-    if out is None:
-        S = torch.empty(B, N, 4, dtype=torch.float32, device=device)
-        G = torch.empty(B, N, 2, dtype=torch.float32, device=device)
+    key = _mix(seed, iteration, rank)
+    obs = None
+    if num_obstacles:
+        obs = obstacles(B, N, dim=dim, num_obstacles=num_obstacles, points=obstacle_points, seed=key ^ 0x5EED,
+                        device=device)
+    W = native.rec_width(dim)
+    if out is None or dim != 2:
+        S = torch.empty(B, N, W, dtype=torch.float32, device=device)
+        G = torch.empty(B, N, dim, dtype=torch.float32, device=device)
     else:
         S, G = out
-    native.scenario(S, G, seed=_mix(seed, iteration, rank), L=E.side_length(N), r=C.DIST_MIN_THRES,
-                    spread=C.GOAL_SPREAD)
-    return S, G, None
+    native.scenario(S, G, seed=key, L=E.side_length(N, dim), r=C.DIST_MIN_THRES, spread=C.GOAL_SPREAD, obs=obs)
+    return native.from_records(S), G, obs

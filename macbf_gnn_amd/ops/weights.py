@@ -8,23 +8,24 @@ from . import layout as L
 
 
 class PackedWeights:
-    def __init__(self, fp):
+    def __init__(self, fp, dim: int = 2):
         self.fp = fp
+        self.dim = dim
         offs = {pn: o for (m, pn, shape, o, n) in fp.specs}
         dev = fp.flat.device
         n = fp.numel
-        self.ctrl_pk = L.ctrl_packer(offs)
-        self.cbf_pk = L.cbf_packer(offs)
+        self.ctrl_pk = L.ctrl_packer(offs, dim)
+        self.cbf_pk = L.cbf_packer(offs, dim)
         self.ctrl_off = self.ctrl_pk.offsets()
         self.cbf_off = self.cbf_pk.offsets()
-        cv, self.ctrl_voff = L.ctrl_vec_index(offs)
+        cv, self.ctrl_voff = L.ctrl_vec_index(offs, dim)
         bv, self.cbf_voff = L.cbf_vec_index(offs)
         mk = lambda a: torch.as_tensor(L.resolve(a, n), dtype=torch.long, device=dev)
         self._ictrl = mk(self.ctrl_pk.index())
         self._icbf = mk(self.cbf_pk.index())
         self._vctrl = mk(cv)
         self._vcbf = mk(bv)
-        self.node_rm = L.ctrl_node_rm(offs)
+        self.node_rm = L.ctrl_node_rm(offs, dim)
         self.node_rm_off = self.node_rm.offsets()
         self._irm = mk(self.node_rm.index())
         self.cbf_rmp = L.cbf_rm(offs)
