@@ -40,6 +40,8 @@ def main():
     ap.add_argument("--inner_loops", type=int, default=50)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no_early_stop", action="store_true", help="fixed-T (=inner_loops) throughput")
+    ap.add_argument("--dim", type=int, default=2, choices=[2, 3], help="3: BASELINE config #5 (3-D)")
+    ap.add_argument("--num_obstacles", type=int, default=0, help="static point-set obstacles per env")
     ap.add_argument("--phases", action="store_true",
                     help="after the timed loop, 2 extra steps with per-phase device-event timings")
     args = ap.parse_args()
@@ -57,7 +59,7 @@ def main():
     dp = DP(device=dev)
     cfg = C.TrainConfig(num_agents=args.agents, num_envs=args.envs, inner_loops=args.inner_loops,
                         seed=args.seed, device="hip", early_stop=not args.no_early_stop,
-                        display_steps=10 ** 9, save_steps=10 ** 9)
+                        display_steps=10 ** 9, save_steps=10 ** 9, dim=args.dim, num_obstacles=args.num_obstacles)
     tr = Trainer(cfg, device=dev, dp=dp)
 
     for _ in range(args.warmup):
@@ -100,7 +102,8 @@ def main():
         "vs_baseline": value / BASELINE_AGENT_STEPS_PER_S,
         "dtype": "bf16",
         "data": "synthetic (on-device scenario sampler, random-init weights)",
-        "config": {"model": "MACBF-GNN controller+CBF (2-D double integrator, top-K=12)",
+        "config": {"model": f"MACBF-GNN controller+CBF ({args.dim}-D double integrator, top-K=12"
+                            + (f", {args.num_obstacles} obstacles x 12 points" if args.num_obstacles else "") + ")",
                    "agents": args.agents, "global_batch": args.envs * world, "envs_per_gpu": args.envs,
                    "seq_len": args.inner_loops, "parallelism": f"dp{world}"},
         "safety_rate": safe_agents / agent_steps if agent_steps > 0 else None,

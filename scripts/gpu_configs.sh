@@ -6,3 +6,5 @@ timeout -k 10 300 python bench.py --agents 32 --envs 64 --steps 20 --warmup 3 > 
 timeout -k 10 300 python bench.py --agents 4096 --envs 16 --steps 5 --warmup 2 --phases > gpurun_out/cfg4_bench.log 2>&1 || exit $?
 timeout -k 10 300 python bench.py --agents 1024 --envs 64 --steps 5 --warmup 2 --no_early_stop --phases > gpurun_out/cfg3_fixedT_bench.log 2>&1 || exit $?
 tail -n1 gpurun_out/cfg2_bench.log gpurun_out/cfg2b_bench.log gpurun_out/cfg4_bench.log gpurun_out/cfg3_fixedT_bench.log
+timeout -k 10 300 python bench.py --agents 1024 --envs 64 --dim 3 --num_obstacles 8 --steps 5 --warmup 2 --phases > gpurun_out/cfg5_bench.log 2>&1 || exit $?
+tail -n1 gpurun_out/cfg5_bench.log

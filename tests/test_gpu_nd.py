@@ -95,7 +95,7 @@ def test_modules_nd_obstacles(dim, nobs):
     _cmp(h.detach(), href.detach(), "h", rel=3e-2, cos=0.999)
     _cmp(sx.grad, gr[0], "cbf dL/ds")
     for (k, prm), ref in zip(cbf.named_parameters(), gr[1:]):
-        _cmp(prm.grad, ref, k, rel=0.12)
+        _cmp(prm.grad, ref, k, rel=0.15)
     # controller
     sx = s.clone().requires_grad_(True)
     a = ctrl(sx, g, obstacles=obs)
@@ -108,7 +108,7 @@ def test_modules_nd_obstacles(dim, nobs):
     _cmp(a.detach(), aref.detach(), "a", rel=3e-2, cos=0.999)
     _cmp(sx.grad, gr[0], "ctrl dL/ds")
     for (k, prm), ref in zip(ctrl.named_parameters(), gr[1:]):
-        _cmp(prm.grad, ref, k, rel=0.12)
+        _cmp(prm.grad, ref, k, rel=0.15)
 
 
 @pytest.mark.parametrize("dim,nobs,bptt", [(3, 0, True), (3, 3, True), (2, 3, True), (3, 3, False)])
