@@ -110,7 +110,8 @@ __global__ __launch_bounds__(SORT_BLOCK) void cell_sort_kernel(CellSortArgs a) {
   }
 }
 
-constexpr int SCAN_BLOCK = 256;      // 4 waves x 64 agents (consecutive on the curve)
+constexpr int SCAN_BLOCK = 256;      // 4 waves x 32 agents (consecutive on the curve), 2 lanes each
+constexpr int SCAN_AG = SCAN_BLOCK / 2;  // agents (curve positions) per block
 constexpr int SCAN_MAXN = 4096;      // whole env staged in LDS
 constexpr int SCH = 8;               // candidates per chunk (one bounding box each)
 
@@ -191,8 +192,11 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanArgs a) {
     cbh[c] = hi;
   }
   __syncthreads();
-  const int wave = threadIdx.x / WAVE, lane = threadIdx.x & 63;
-  const int pos = blockIdx.x * SCAN_BLOCK + threadIdx.x;      // my position on the curve
+  // Two lanes per agent: lane (r, h) owns curve position base + r and scans candidate slots
+  // 4h..4h+3 of every chunk; the two half-lists are merged at the end. Twice the waves of a
+  // lane-per-agent layout (2 per SIMD) and half the per-chunk work per lane.
+  const int wave = threadIdx.x / WAVE, lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
+  const int pos = blockIdx.x * SCAN_AG + wave * 32 + r;       // my position on the curve
   float4 me = make_float4(0.f, 0.f, 0.f, 0.f), mv = make_float4(0.f, 0.f, 0.f, 0.f);
   int i = -1;
   if (pos < Nn) {
@@ -217,9 +221,9 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanArgs a) {
   }
   const float wvmax = wave_max(act ? mv.w : 0.f);
   const bool wave_live = __any(act);
-  int cc0 = (blockIdx.x * SCAN_BLOCK + wave * WAVE + 32) / SCH;
+  int cc0 = (blockIdx.x * SCAN_AG + wave * 32 + 16) / SCH;
   if (cc0 >= nch) cc0 = nch - 1;
-  float thr = INFINITY;                 // max over active lanes of the current K-th distance
+  float thr = INFINITY;                 // bound on every agent's final K-th distance in this wave
   bool all_danger = false;
   if (wave_live) {
     // chunk metadata is read one step ahead of the (deterministic) walk to hide LDS latency
@@ -248,11 +252,12 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanArgs a) {
       const float lb = 1.01f * (rc + a.ttc_check * (wvmax + cl.w)) + 1e-4f;
       const bool ns = a.do_safety && !all_danger && !(bd2 > lb * lb);
       if (!nk && !ns) continue;
-      float4 c[SCH];
+      constexpr int HU = SCH / 2;
+      float4 c[HU];
 #pragma unroll
-      for (int u = 0; u < SCH; ++u) c[u] = tp[cur * SCH + u];
+      for (int u = 0; u < HU; ++u) c[u] = tp[cur * SCH + HU * h + u];
 #pragma unroll
-      for (int u = 0; u < SCH; ++u) {
+      for (int u = 0; u < HU; ++u) {
         const int j = __float_as_int(c[u].w);
         float dp[D];
         dp[0] = me.x - c[u].x;
@@ -262,7 +267,7 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanArgs a) {
         const uint64_t key = knn_key(d2, (unsigned)j);
         if (nk && act && key < bk[K - 1]) topk_insert<K>(bk, key);
         if (ns && act && !danger) {
-          const float4 cv = tv[cur * SCH + u];
+          const float4 cv = tv[cur * SCH + HU * h + u];
           const float lim = 1.01f * (base_i + a.ttc_check * cv.w) + 1e-4f;
           if (d2 < lim * lim && j != i) {
             float dv[D];
@@ -273,12 +278,31 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanArgs a) {
           }
         }
       }
-      if (nk) thr = wave_max(act ? __uint_as_float((unsigned)(bk[K - 1] >> 32)) : -INFINITY);
-      if (ns) all_danger = !__any(act && !danger);
+      if (nk) {
+        // the merged list's K-th distance <= min of the two half-lists' K-th distances
+        const float own = __uint_as_float((unsigned)(bk[K - 1] >> 32));
+        const float kth = fminf(own, shfl_xor32(own));
+        thr = wave_max(act ? kth : -INFINITY);
+      }
+      if (ns) {
+        const bool dboth = danger || (shfl_xor32i(danger ? 1 : 0) != 0);
+        all_danger = !__any(act && !dboth);
+      }
     }
   }
+  // merge the partner half-list into lane h = 0 (keys are unique: (d2, node id))
+  if (a.do_knn) {
+#pragma unroll
+    for (int q = 0; q < K; ++q) {
+      const unsigned lo = xor32u((unsigned)bk[q]), hi = xor32u((unsigned)(bk[q] >> 32));
+      const uint64_t x = ((uint64_t)hi << 32) | lo;
+      if (h == 0 && x < bk[K - 1]) topk_insert<K>(bk, x);
+    }
+  }
+  danger = danger || (shfl_xor32i(danger ? 1 : 0) != 0);
+  const bool own = act && h == 0;                              // one lane reports per agent
   float ndang = 0.f, nsafe_e = 0.f, safe_ag = 0.f;
-  if (act && a.do_knn) {
+  if (own && a.do_knn) {
     int* out = a.idx + (long)b * a.i_env + (long)i * K;
     uint8_t* dout = a.dang ? a.dang + (long)b * a.i_env + (long)i * K : nullptr;
     float pi[D], vi[D];
@@ -298,7 +322,7 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanArgs a) {
     }
     nsafe_e = (float)K - ndang;
   }
-  if (act && a.do_safety) safe_ag = danger ? 0.f : 1.f;
+  if (own && a.do_safety) safe_ag = danger ? 0.f : 1.f;
   ndang = wave_sum(ndang);
   nsafe_e = wave_sum(nsafe_e);
   safe_ag = wave_sum(safe_ag);
@@ -317,7 +341,7 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanArgs a) {
 
 template <int K, int D>
 static void launch_kd(const ScanArgs& a, hipStream_t st) {
-  dim3 grid((a.Nn + SCAN_BLOCK - 1) / SCAN_BLOCK, a.B);
+  dim3 grid((a.Nn + SCAN_AG - 1) / SCAN_AG, a.B);
   const size_t lds = scan_lds_bytes(a.Nn);
   (void)hipFuncSetAttribute((const void*)scan_kernel<K, D>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   hipLaunchKernelGGL((scan_kernel<K, D>), grid, dim3(SCAN_BLOCK), lds, st, a);

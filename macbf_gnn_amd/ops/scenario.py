@@ -5,7 +5,8 @@ checkpoint at any DP width reproduces the data stream without saving RNG state.
 """
 from __future__ import annotations
 
-import numpy as np
+import math
+
 import torch
 
 from .. import config as C
@@ -22,13 +23,32 @@ def _mix(*xs) -> int:
 
 
 def obstacles(B, N, *, dim, num_obstacles, points, seed, device):
-    """(B, num_obstacles*points, D) static point-set obstacles (env.generate_obstacles shapes),
-    generated on the host from the counter-based seed (a few hundred points per env)."""
-    rng = np.random.default_rng(seed & 0xFFFFFFFFFFFFFFFF)
+    """(B, num_obstacles*points, D) static point-set obstacles with the shapes of
+    ``env.generate_obstacles`` (2-D: alternating circles / rectangles, 3-D: spheres), sampled with
+    device-side torch ops from a counter-based seed (no host work, stream-ordered)."""
+    gen = torch.Generator(device=device)
+    gen.manual_seed(seed & 0x7FFFFFFFFFFFFFFF)
     L = E.side_length(N, dim)
-    o = np.stack([E.generate_obstacles(num_obstacles, L, dim, rng, points) for _ in range(B)])
-    return torch.from_numpy(o).pin_memory().to(device, non_blocking=True) if device.type == "cuda" \
-        else torch.from_numpy(o)
+    f32 = torch.float32
+    ctr = torch.rand(B, num_obstacles, 1, dim, generator=gen, device=device, dtype=f32) * L
+    if dim == 3:
+        k = torch.arange(points, device=device, dtype=f32) + 0.5
+        phi = torch.arccos(1.0 - 2.0 * k / points)
+        th = math.pi * (1.0 + 5 ** 0.5) * k
+        unit = torch.stack([torch.cos(th) * torch.sin(phi), torch.sin(th) * torch.sin(phi), torch.cos(phi)], -1)
+        rad = 0.1 + 0.2 * torch.rand(B, num_obstacles, 1, 1, generator=gen, device=device, dtype=f32)
+        pts = ctr + unit * rad
+    else:
+        th = torch.arange(points, device=device, dtype=f32) * (2.0 * math.pi / points)
+        circ = torch.stack([torch.cos(th), torch.sin(th)], -1)                       # (P, 2)
+        rad = 0.1 + 0.2 * torch.rand(B, num_obstacles, 1, 1, generator=gen, device=device, dtype=f32)
+        sides = 0.2 + 0.4 * torch.rand(B, num_obstacles, 1, 2, generator=gen, device=device, dtype=f32)
+        # rectangle boundary: the reference's proportional split, on the unit square, then scaled
+        rect = torch.as_tensor(E.generate_obstacle_rectangle((0.0, 0.0), (1.0, 1.0), points), device=device,
+                               dtype=f32)
+        is_circ = (torch.arange(num_obstacles, device=device) % 2 == 0).view(1, -1, 1, 1)
+        pts = ctr + torch.where(is_circ, circ * rad, rect * sides)
+    return pts.reshape(B, num_obstacles * points, dim).contiguous()
 
 
 def generate(B, N, *, seed=0, iteration=0, rank=0, device=None, out=None, dim=2, num_obstacles=0,
