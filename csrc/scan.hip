@@ -253,9 +253,10 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanArgs a) {
       const bool ns = a.do_safety && !all_danger && !(bd2 > lb * lb);
       if (!nk && !ns) continue;
       constexpr int HU = SCH / 2;
+      const int hoff = HU * h;
       float4 c[HU];
 #pragma unroll
-      for (int u = 0; u < HU; ++u) c[u] = tp[cur * SCH + HU * h + u];
+      for (int u = 0; u < HU; ++u) c[u] = tp[cur * SCH + hoff + u];
 #pragma unroll
       for (int u = 0; u < HU; ++u) {
         const int j = __float_as_int(c[u].w);
@@ -267,7 +268,7 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanArgs a) {
         const uint64_t key = knn_key(d2, (unsigned)j);
         if (nk && act && key < bk[K - 1]) topk_insert<K>(bk, key);
         if (ns && act && !danger) {
-          const float4 cv = tv[cur * SCH + HU * h + u];
+          const float4 cv = tv[cur * SCH + hoff + u];
           const float lim = 1.01f * (base_i + a.ttc_check * cv.w) + 1e-4f;
           if (d2 < lim * lim && j != i) {
             float dv[D];
@@ -285,7 +286,9 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanArgs a) {
         thr = wave_max(act ? kth : -INFINITY);
       }
       if (ns) {
-        const bool dboth = danger || (shfl_xor32i(danger ? 1 : 0) != 0);
+        // the lane swap must run on every lane: never inside a short-circuit '||'
+        const int pdg = shfl_xor32i(danger ? 1 : 0);
+        const bool dboth = danger || (pdg != 0);
         all_danger = !__any(act && !dboth);
       }
     }
@@ -299,7 +302,8 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanArgs a) {
       if (h == 0 && x < bk[K - 1]) topk_insert<K>(bk, x);
     }
   }
-  danger = danger || (shfl_xor32i(danger ? 1 : 0) != 0);
+  const int pd = shfl_xor32i(danger ? 1 : 0);   // unconditional lane swap (see above)
+  danger = danger || (pd != 0);
   const bool own = act && h == 0;                              // one lane reports per agent
   float ndang = 0.f, nsafe_e = 0.f, safe_ag = 0.f;
   if (own && a.do_knn) {

@@ -95,7 +95,7 @@ def test_modules_nd_obstacles(dim, nobs):
     _cmp(h.detach(), href.detach(), "h", rel=3e-2, cos=0.999)
     _cmp(sx.grad, gr[0], "cbf dL/ds")
     for (k, prm), ref in zip(cbf.named_parameters(), gr[1:]):
-        _cmp(prm.grad, ref, k, rel=0.15)
+        _cmp(prm.grad, ref, k, rel=0.2, cos=0.98)   # 128-agent graphs: bf16 activation noise
     # controller
     sx = s.clone().requires_grad_(True)
     a = ctrl(sx, g, obstacles=obs)
@@ -108,7 +108,7 @@ def test_modules_nd_obstacles(dim, nobs):
     _cmp(a.detach(), aref.detach(), "a", rel=3e-2, cos=0.999)
     _cmp(sx.grad, gr[0], "ctrl dL/ds")
     for (k, prm), ref in zip(ctrl.named_parameters(), gr[1:]):
-        _cmp(prm.grad, ref, k, rel=0.15)
+        _cmp(prm.grad, ref, k, rel=0.2, cos=0.98)   # 128-agent graphs: bf16 activation noise
 
 
 @pytest.mark.parametrize("dim,nobs,bptt", [(3, 0, True), (3, 3, True), (2, 3, True), (3, 3, False)])
