@@ -16,7 +16,7 @@ dev = torch.device("cuda")
 B, N = 64, int(sys.argv[1]) if len(sys.argv) > 1 else 1024
 cfg = C.TrainConfig(num_agents=N, num_envs=B, inner_loops=20, device="hip", early_stop=False)
 tr = Trainer(cfg, device=dev, dp=DP(device=dev))
-s0, g = tr.sample()
+s0, g, _ = tr.sample()
 tr.engine.rollout(s0, g)
 S = tr.engine.S[10].contiguous()
 K = min(N, C.TOP_K)
