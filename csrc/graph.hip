@@ -106,7 +106,27 @@ __global__ __launch_bounds__(256) void node_reduce_kernel(NodeRedArgs a) {
     }
     const int* ptr = a.ptr + gi * (Nt + 1);
     const int* edges = a.edges + gi * (long)N * K;
-    for (int q2 = ptr[i]; q2 < ptr[i + 1]; ++q2) {
+    const int q0 = ptr[i], q1 = ptr[i + 1];
+    // incoming edges in batches of 4: the 4 edge ids, then the 4 independent record loads
+    // (fixed order: the sum is the same as the one-by-one loop)
+    int q2 = q0;
+    for (; q2 + 4 <= q1; q2 += 4) {
+      int e4[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) e4[u] = edges[q2 + u];
+      float4 v4[4][R];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int q = 0; q < R; ++q) v4[u][q] = dE[(long)e4[u] * R + q];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int q = 0; q < R; ++q) {
+          g[q].x -= v4[u][q].x; g[q].y -= v4[u][q].y; g[q].z -= v4[u][q].z; g[q].w -= v4[u][q].w;
+        }
+    }
+    for (; q2 < q1; ++q2) {
       const int e = edges[q2];
 #pragma unroll
       for (int q = 0; q < R; ++q) {
@@ -153,7 +173,21 @@ __global__ __launch_bounds__(256) void node_combine_kernel(CombineArgs a) {
     }
     const int* ptr = a.ptr + (long)b * a.ptr_env;
     const int* edges = a.edges + (long)b * a.edges_env;
-    for (int q2 = ptr[i]; q2 < ptr[i + 1]; ++q2) {
+    const int q0 = ptr[i], q1 = ptr[i + 1];
+    int q2 = q0;
+    for (; q2 + 4 <= q1; q2 += 4) {     // 4 ids, then 4 independent record loads (same sum order)
+      int e4[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) e4[u] = edges[q2 + u];
+      float p4[4][D], v4[4][D];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) load_rec<D>(dE, (unsigned)e4[u], p4[u], v4[u]);
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int q = 0; q < D; ++q) { gp[q] -= p4[u][q]; gv[q] -= v4[u][q]; }
+    }
+    for (; q2 < q1; ++q2) {
       load_rec<D>(dE, (unsigned)edges[q2], p, v);
 #pragma unroll
       for (int q = 0; q < D; ++q) { gp[q] -= p[q]; gv[q] -= v[q]; }
