@@ -274,8 +274,13 @@ extern "C" int mb_cbf_fwd(const mb::CbfFwdArgs* a, int num_blocks, hipStream_t s
 // ---------------------------------------------------------------------------------------
 namespace mb {
 
-constexpr int SA128 = 136, SA64 = 72, SA32 = 40;
-constexpr int RM_W2 = 128 * 72, RM_W3 = 64 * 136;   // row-major image sizes (elements)
+// LDS row strides (bf16 elements), chosen with a bank model of the access patterns
+// (ds_read_b64 / ds_read_b64_tr_b16: 64 banks per 32-lane half; ds_write_b64: 32 banks per
+// 16-lane group): 68 = 34 dwords and 148 = 74 dwords keep 32-row weight reads, 4-row transposed
+// reads and 16-row tile stores conflict-free or 2-way at most (72 / 136 were 2-4 way).
+constexpr int SA128 = 148, SA64 = 68, SA32 = 40;
+constexpr int WS2 = 68, WS3 = 148;                  // row-major W2 [128][WS2], W3 [64][WS3] images
+constexpr int RM_W2 = 128 * WS2, RM_W3 = 64 * WS3;  // row-major image sizes (elements)
 // per-WG partial slab layout (floats)
 constexpr int P_W3 = 0, P_B3 = 8192, P_W2 = 8256, P_B2 = 16448, P_W1 = 16576, P_W4 = 18624, P_B4 = 18688;
 constexpr int P_LOSS = 18692;                 // 10 loss partial sums (fused mode)
@@ -420,7 +425,7 @@ __global__ __launch_bounds__(NW * 64, 1) void cbf_bwd_kernel(CbfBwdArgs a) {
       f32x16 t2 = bias_rows4(b2, 32 * mt, h);
       static_for<4>([&](auto kk_) {
         constexpr int kk = decltype(kk_)::value;
-        t2 = mfma(wrm_acc(W2c, SA64, 32 * mt, kk, lane), bacc_frag<kk & 1>(H1b[kk >> 1]), t2);
+        t2 = mfma(wrm_acc(W2c, WS2, 32 * mt, kk, lane), bacc_frag<kk & 1>(H1b[kk >> 1]), t2);
       });
       relu_(t2);
       H2b[mt] = to_bf16x16(t2);
@@ -430,7 +435,7 @@ __global__ __launch_bounds__(NW * 64, 1) void cbf_bwd_kernel(CbfBwdArgs a) {
       f32x16 t3 = bias_rows4(b3, 32 * mt, h);
       static_for<8>([&](auto kk_) {
         constexpr int kk = decltype(kk_)::value;
-        t3 = mfma(wrm_acc(W3c, SA128, 32 * mt, kk, lane), bacc_frag<kk & 1>(H2b[kk >> 1]), t3);
+        t3 = mfma(wrm_acc(W3c, WS3, 32 * mt, kk, lane), bacc_frag<kk & 1>(H2b[kk >> 1]), t3);
       });
       H3p[mt] = t3;
     }
@@ -529,7 +534,7 @@ __global__ __launch_bounds__(NW * 64, 1) void cbf_bwd_kernel(CbfBwdArgs a) {
       f32x16 t = zero16();
       static_for<4>([&](auto kk_) {
         constexpr int kk = decltype(kk_)::value;
-        t = mfma(wrmT_acc(W3c, SA128, 32 * mt, kk, lane), bacc_frag<kk & 1>(d3b[kk >> 1]), t);
+        t = mfma(wrmT_acc(W3c, WS3, 32 * mt, kk, lane), bacc_frag<kk & 1>(d3b[kk >> 1]), t);
       });
       d2b[mt] = to_bf16x16(t);
       mask_by_nonzero(d2b[mt], H2b[mt]);
@@ -557,7 +562,7 @@ __global__ __launch_bounds__(NW * 64, 1) void cbf_bwd_kernel(CbfBwdArgs a) {
       f32x16 t = zero16();
       static_for<8>([&](auto kk_) {
         constexpr int kk = decltype(kk_)::value;
-        t = mfma(wrmT_acc(W2c, SA64, 32 * mt, kk, lane), bacc_frag<kk & 1>(d2b[kk >> 1]), t);
+        t = mfma(wrmT_acc(W2c, WS2, 32 * mt, kk, lane), bacc_frag<kk & 1>(d2b[kk >> 1]), t);
       });
       d1b[mt] = to_bf16x16(t);
       mask_by_nonzero(d1b[mt], H1b[mt]);

@@ -334,7 +334,7 @@ class RMPacker:
         self.size = 0
 
     def add(self, name, vm, rows, cols, stride):
-        assert stride % 8 == 0 and stride >= cols
+        assert stride % 4 == 0 and stride >= cols and (rows * stride) % 8 == 0
         idx = np.full((rows, stride), ZERO, dtype=np.int64)
         for r in range(rows):
             for c in range(cols):
@@ -488,7 +488,7 @@ def ctrl_edge_grad_map(fp_offsets, dim: int = 2):
     return np.asarray(S, np.int64), np.asarray(D, np.int64)
 
 
-CBF_RM_STRIDES = {"w2": 72, "w3": 136}
+CBF_RM_STRIDES = {"w2": 68, "w3": 148}      # csrc/cbf.hip WS2 / WS3 (bank-conflict-aware)
 
 
 def cbf_rm(fp_offsets, dim: int = 2) -> RMPacker:

@@ -328,7 +328,7 @@ def cbf_bwd(S, idx, dh, wpack, f_bwd, wrm, wvec, *, passes=2, dE=None, partial=N
     check(wvec, torch.float32, None, "wvec")
     if wpack.numel() < (f_bwd + 70) * 512:
         raise NativeError("packed CBF weights too small")
-    check(wrm, torch.bfloat16, (128 * 72 + 64 * 136,), "wrm")
+    check(wrm, torch.bfloat16, (128 * 68 + 64 * 148,), "wrm")
     if idx1 is not None:
         check(idx1, torch.int32, (T, B, N, K), "idx1")
     E = B * T * N * K
