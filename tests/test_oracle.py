@@ -200,3 +200,31 @@ def test_oracle_bptt_gradient_flows_through_states():
     h = O.cbf_forward(cbf.params_dict(), traj["S"][:, :T], traj["idx"])
     h.sum().backward()
     assert ctrl.controller_dec_net[0].weight.grad.abs().sum() > 0
+
+
+def test_oracle_total_loss_gradcheck_fp64():
+    """fp64 finite-difference check of the oracle's full BPTT loss: the GPU
+    backward kernels are validated against these autograd gradients, so they must be right.
+    Hinges / max-pool / kNN are piecewise smooth; the random point is generic."""
+    torch.manual_seed(3)
+    ctrl, cbf = Controller(4).double(), CBF(4).double()
+    s0, g = E.generate_batch(1, 6, seed=7)
+    s0, g = s0.double(), g.double()
+    s0[..., 2:] = 0.3 * torch.randn_like(s0[..., 2:])
+    cp, bp = ctrl.params_dict(), cbf.params_dict()
+    # a subset of tensors keeps gradcheck fast; every layer type of both nets is represented
+    names_c = ["controller_centr_net.2.bias", "controller_dec_net.4.bias", "controller_dec_net.6.weight"]
+    names_b = ["cbf_net.0.bias", "cbf_net.4.bias", "cbf_net.6.weight"]
+    leaves = [cp[n].detach().clone().requires_grad_(True) for n in names_c]
+    leaves += [bp[n].detach().clone().requires_grad_(True) for n in names_b]
+    s_in = s0.clone().requires_grad_(True)
+
+    def total(s_init, *ps):
+        c = dict(cp)
+        c.update(zip(names_c, ps[:3]))
+        b = dict(bp)
+        b.update(zip(names_b, ps[3:]))
+        traj = O.rollout(c, s_init, g, inner_loops=3, early_stop=False)
+        return O.train_losses(c, b, traj, g)[0]["total"]
+
+    assert torch.autograd.gradcheck(total, (s_in, *leaves), eps=1e-6, atol=1e-5, rtol=1e-4)
