@@ -42,6 +42,8 @@ def main():
     ap.add_argument("--no_early_stop", action="store_true", help="fixed-T (=inner_loops) throughput")
     ap.add_argument("--dim", type=int, default=2, choices=[2, 3], help="3: BASELINE config #5 (3-D)")
     ap.add_argument("--num_obstacles", type=int, default=0, help="static point-set obstacles per env")
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp16"],
+                    help="16-bit MFMA input type (fp16: dynamic loss scaling; BASELINE config #5)")
     ap.add_argument("--phases", action="store_true",
                     help="after the timed loop, 2 extra steps with per-phase device-event timings")
     args = ap.parse_args()
@@ -59,7 +61,8 @@ def main():
     dp = DP(device=dev)
     cfg = C.TrainConfig(num_agents=args.agents, num_envs=args.envs, inner_loops=args.inner_loops,
                         seed=args.seed, device="hip", early_stop=not args.no_early_stop,
-                        display_steps=10 ** 9, save_steps=10 ** 9, dim=args.dim, num_obstacles=args.num_obstacles)
+                        display_steps=10 ** 9, save_steps=10 ** 9, dim=args.dim, num_obstacles=args.num_obstacles,
+                        dtype=args.dtype)
     tr = Trainer(cfg, device=dev, dp=dp)
 
     for _ in range(args.warmup):
@@ -100,7 +103,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": value / BASELINE_AGENT_STEPS_PER_S,
-        "dtype": "bf16",
+        "dtype": args.dtype,
         "data": "synthetic (on-device scenario sampler, random-init weights)",
         "config": {"model": f"MACBF-GNN controller+CBF ({args.dim}-D double integrator, top-K=12"
                             + (f", {args.num_obstacles} obstacles x 12 points" if args.num_obstacles else "") + ")",
@@ -109,6 +112,7 @@ def main():
         "safety_rate": safe_agents / agent_steps if agent_steps > 0 else None,
         "mean_T": t_sum / (args.steps * world),
         "early_stop": not args.no_early_stop,
+        "skipped_steps": tr.skipped_steps,
         "baseline": {"value": BASELINE_AGENT_STEPS_PER_S,
                      "source": "BASELINE.md: reference rollout-only loop @ N=1024, CPU x8 (upper bound of its "
                                "train loop, which does not run at N=1024)"},

@@ -3,7 +3,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-typedef __bf16 bf16;
+#include "prec.h"
 
 namespace mb {
 
@@ -47,7 +47,7 @@ struct CtrlArgs {
   const float* G;                     // goals (b,i,d) -> G[(b*N + i)*D + d]
   const int* idx;   long i_env;       // (b,i,k) -> idx[b*i_env + i*K + k]
   int B, N, K;
-  const bf16* wpack;                  // packed ctrl fragments
+  const h16* wpack;                  // packed ctrl fragments
   int f_edge;                         // fragment offset of ew1f (ew2 follows)
   int f_node;                         // fragment offset of nw1f (nw2, nw3, nw4 follow)
   const float* wvec;                  // eb2|nb2|nb3|nb4 (CTRL_VEC floats)
@@ -57,7 +57,7 @@ struct CtrlArgs {
   float* act_sum;   long ac_env;      // per-env sum of |‖a‖² - ‖a_ref‖²| (may be null)
   const float* noise; long n_env;     // additive action noise (b,i,d) (may be null)
   float dt, obs_r, sqrt3;
-  bf16* pooled;     long p_env;       // (b,i,128) max-pooled edge features out (bf16), or null
+  h16* pooled;     long p_env;       // (b,i,128) max-pooled edge features out (h16), or null
   uint8_t* argmax;  long am_env;      // (b,i,128) winning slot per feature (0xFF: no grad), or null
 };
 
@@ -73,7 +73,7 @@ struct CbfFwdArgs {
   const uint8_t* valid;                    // (T,B) or null (all valid)
   int B, T, N, K;
   int two;                                 // also evaluate h' on s_{t+1}
-  const bf16* wpack; int f_fwd;            // fragment offset of w1f (w2, w3 follow)
+  const h16* wpack; int f_fwd;            // fragment offset of w1f (w2, w3 follow)
   const float* wvec;
   float* h_out;                            // (E) or null
   float* hn_out;                           // (E) or null
@@ -92,8 +92,8 @@ struct CbfBwdArgs {
   int B, T, N, K;
   int passes;                              // evaluations = passes*E; pass p reads states at t+p
   const float* dh;                         // (passes, E) upstream dL/dh (radius mask folded in)
-  const bf16* wpack; int f_bwd;            // fragment offset of w1f (w2,w3,w3t,w2t,w1ft follow)
-  const bf16* wrm;                         // row-major W2 [128][72] | W3 [64][136] images
+  const h16* wpack; int f_bwd;            // fragment offset of w1f (w2,w3,w3t,w2t,w1ft follow)
+  const h16* wrm;                         // row-major W2 [128][72] | W3 [64][136] images
   const float* wvec;
   float4* dE;                              // (passes, E) records of dL/d(s_i - s_j), or null
   float* partial;                          // (gridDim.x, CBF_PARTIAL) per-workgroup dW slabs
@@ -109,7 +109,7 @@ struct CbfBwdArgs {
 };
 
 struct CtrlNodeBwdArgs {
-  const bf16* pooled;  long p_env;     // (b,i,128) pooled edge features of step t (rollout)
+  const h16* pooled;  long p_env;     // (b,i,128) pooled edge features of step t (rollout)
   const float4* S;     long s_env;     // node records s_t
   int dim;
   const float* G;                      // goals (B,N,D)
@@ -117,11 +117,11 @@ struct CtrlNodeBwdArgs {
   const float4* Gn;    long gn_env;    // G_{t+1} = dL/ds_{t+1} records (or null)
   const uint8_t* valid; long v_env;    // valid[b*v_env] for this step (or null = all valid)
   int B, N;
-  const bf16* wrm;                     // row-major node images
+  const h16* wrm;                     // row-major node images
   int o_w1, o_w2, o_w3, o_w4;          // element offsets (strides 168/72/136/72)
   const float* wvec;                   // controller side vector (eb2|nb2|nb3|nb4)
   float act_coef, dt, sqrt3;
-  bf16* dP;            long dp_env;    // (b,i,128) dL/dpooled out
+  h16* dP;            long dp_env;    // (b,i,128) dL/dpooled out
   float4* ego;                         // (B,N) records: dL/ds_t from the node path + gain law + action loss
   float* partial;                      // (gridDim.x, CTRL_NODE_PARTIAL) slabs, accumulated
 };
@@ -131,9 +131,9 @@ struct CtrlEdgeBwdArgs {
   int dim;
   const int* idx;      long i_env;
   const uint8_t* argmax; long am_env;  // (b,i,128) winning slot per pooled feature
-  const bf16* dP;      long dp_env;    // (b,i,128)
+  const h16* dP;      long dp_env;    // (b,i,128)
   int B, N, K;
-  const bf16* wpack;   int f_ew1f, f_ew2tn;   // packed fragments (ew2tn followed by ew1ft)
+  const h16* wpack;   int f_ew1f, f_ew2tn;   // packed fragments (ew2tn followed by ew1ft)
   float4* dEc;         long de_env;    // (b,i,K) records of dL/d(s_i - s_j) out
   float* partial;                      // (gridDim.x, CTRL_EDGE_PARTIAL) slabs, accumulated
 };
@@ -183,10 +183,15 @@ int mb_scan(const mb::ScanArgs* a, hipStream_t st);
 int mb_cell_sort(const mb::CellSortArgs* a, hipStream_t st);
 int mb_scenario(const mb::ScenArgs* a, hipStream_t st);
 int mb_ctrl_fwd(const mb::CtrlArgs* a, int num_cu, hipStream_t st);
+int mb_ctrl_fwd_f16(const mb::CtrlArgs* a, int num_cu, hipStream_t st);
 int mb_cbf_fwd(const mb::CbfFwdArgs* a, int num_blocks, hipStream_t st);
+int mb_cbf_fwd_f16(const mb::CbfFwdArgs* a, int num_blocks, hipStream_t st);
 int mb_cbf_bwd(const mb::CbfBwdArgs* a, int num_blocks, hipStream_t st);
+int mb_cbf_bwd_f16(const mb::CbfBwdArgs* a, int num_blocks, hipStream_t st);
 int mb_ctrl_node_bwd(const mb::CtrlNodeBwdArgs* a, int num_blocks, hipStream_t st);
+int mb_ctrl_node_bwd_f16(const mb::CtrlNodeBwdArgs* a, int num_blocks, hipStream_t st);
 int mb_ctrl_edge_bwd(const mb::CtrlEdgeBwdArgs* a, int num_blocks, hipStream_t st);
+int mb_ctrl_edge_bwd_f16(const mb::CtrlEdgeBwdArgs* a, int num_blocks, hipStream_t st);
 int mb_rev_csr(const mb::CsrArgs* a, hipStream_t st);
 int mb_node_reduce(const mb::NodeRedArgs* a, hipStream_t st);
 int mb_node_combine(const mb::CombineArgs* a, hipStream_t st);

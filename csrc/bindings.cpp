@@ -48,41 +48,41 @@ static int scenario(u64 S, long s_env, u64 G, u64 obs, int M, int dim, int B, in
 static int ctrl_fwd(u64 S, long s_env, u64 G, u64 idx, long i_env, int B, int N, int K, u64 wpack, int f_edge,
                     int f_node, u64 wvec, u64 A, long a_env, u64 Sn, long sn_env, u64 dist_sum, long d_env,
                     u64 act_sum, long ac_env, u64 noise, long n_env, float dt, float obs_r, float sqrt3,
-                    u64 pooled, long p_env, u64 argmax, long am_env, int dim, int num_cu, u64 stream) {
+                    u64 pooled, long p_env, u64 argmax, long am_env, int dim, int num_cu, int f16, u64 stream) {
   mb::CtrlArgs a{};
   a.dim = dim;
   a.S = P<const float4>(S); a.s_env = s_env; a.G = P<const float>(G); a.idx = P<const int>(idx); a.i_env = i_env;
-  a.B = B; a.N = N; a.K = K; a.wpack = P<const bf16>(wpack); a.f_edge = f_edge; a.f_node = f_node;
+  a.B = B; a.N = N; a.K = K; a.wpack = P<const h16>(wpack); a.f_edge = f_edge; a.f_node = f_node;
   a.wvec = P<const float>(wvec); a.A = P<float>(A); a.a_env = a_env; a.Snext = P<float4>(Sn); a.sn_env = sn_env;
   a.dist_sum = P<float>(dist_sum); a.d_env = d_env; a.act_sum = P<float>(act_sum); a.ac_env = ac_env;
   a.noise = P<const float>(noise); a.n_env = n_env; a.dt = dt; a.obs_r = obs_r; a.sqrt3 = sqrt3;
-  a.pooled = P<bf16>(pooled); a.p_env = p_env; a.argmax = P<uint8_t>(argmax); a.am_env = am_env;
-  return mb_ctrl_fwd(&a, num_cu, ST(stream));
+  a.pooled = P<h16>(pooled); a.p_env = p_env; a.argmax = P<uint8_t>(argmax); a.am_env = am_env;
+  return (f16 ? mb_ctrl_fwd_f16 : mb_ctrl_fwd)(&a, num_cu, ST(stream));
 }
 
 static int cbf_fwd(u64 S, long s_env, long s_step, u64 idx, u64 dang, u64 valid, int B, int T, int N, int K,
                    int two, u64 wpack, int f_fwd, u64 wvec, u64 h_out, u64 hn_out, u64 dh_out, u64 counts,
                    u64 partial, py::tuple lc, float obs_r, float dist_thr, float dist_eps, int dim, int num_blocks,
-                   u64 stream) {
+                   int f16, u64 stream) {
   mb::CbfFwdArgs a{};
   a.dim = dim;
   a.S = P<const float4>(S); a.s_env = s_env; a.s_step = s_step; a.idx = P<const int>(idx);
   a.dang = P<const uint8_t>(dang); a.valid = P<const uint8_t>(valid);
   a.B = B; a.T = T; a.N = N; a.K = K; a.two = two;
-  a.wpack = P<const bf16>(wpack); a.f_fwd = f_fwd; a.wvec = P<const float>(wvec);
+  a.wpack = P<const h16>(wpack); a.f_fwd = f_fwd; a.wvec = P<const float>(wvec);
   a.h_out = P<float>(h_out); a.hn_out = P<float>(hn_out); a.dh_out = P<float>(dh_out);
   a.counts = P<const float>(counts); a.partial = P<float>(partial);
   a.lc.eps_dang = lc[0].cast<float>(); a.lc.dt_alpha = lc[1].cast<float>(); a.lc.w_dang = lc[2].cast<float>();
   a.lc.w_safe = lc[3].cast<float>(); a.lc.w_dang_d = lc[4].cast<float>(); a.lc.w_safe_d = lc[5].cast<float>();
   a.lc.scale = lc[6].cast<float>();
   a.obs_r = obs_r; a.dist_thr = dist_thr; a.dist_eps = dist_eps;
-  return mb_cbf_fwd(&a, num_blocks, ST(stream));
+  return (f16 ? mb_cbf_fwd_f16 : mb_cbf_fwd)(&a, num_blocks, ST(stream));
 }
 
 static int cbf_bwd(u64 S, long s_env, long s_step, u64 idx, int B, int T, int N, int K, int passes, u64 dh,
                    u64 wpack, int f_bwd, u64 wrm, u64 wvec, u64 dE, u64 partial, float obs_r, float dist_thr,
                    float dist_eps, int fused, u64 dang, u64 valid, u64 counts, py::tuple lc, u64 idx1,
-                   int dim, int num_blocks, u64 stream) {
+                   int dim, int num_blocks, int f16, u64 stream) {
   mb::CbfBwdArgs a{};
   a.dim = dim;
   a.idx1 = P<const int>(idx1);
@@ -93,10 +93,10 @@ static int cbf_bwd(u64 S, long s_env, long s_step, u64 idx, int B, int T, int N,
   a.lc.scale = lc[6].cast<float>();
   a.S = P<const float4>(S); a.s_env = s_env; a.s_step = s_step; a.idx = P<const int>(idx);
   a.B = B; a.T = T; a.N = N; a.K = K; a.passes = passes; a.dh = P<const float>(dh);
-  a.wpack = P<const bf16>(wpack); a.f_bwd = f_bwd; a.wrm = P<const bf16>(wrm); a.wvec = P<const float>(wvec);
+  a.wpack = P<const h16>(wpack); a.f_bwd = f_bwd; a.wrm = P<const h16>(wrm); a.wvec = P<const float>(wvec);
   a.dE = P<float4>(dE); a.partial = P<float>(partial);
   a.obs_r = obs_r; a.dist_thr = dist_thr; a.dist_eps = dist_eps;
-  return mb_cbf_bwd(&a, num_blocks, ST(stream));
+  return (f16 ? mb_cbf_bwd_f16 : mb_cbf_bwd)(&a, num_blocks, ST(stream));
 }
 
 static int rev_csr(u64 idx, int G, int N, int K, u64 ptr, u64 edges, int Nn, u64 stream) {
@@ -142,28 +142,28 @@ static int adam(u64 param, u64 grad, u64 m, u64 v, int lo, int hi, float b1, flo
 static int ctrl_node_bwd(u64 pooled, long p_env, u64 S, long s_env, u64 G, u64 A, long a_env, u64 Gn, long gn_env,
                          u64 valid, long v_env, int B, int N, u64 wrm, int o1, int o2, int o3, int o4, u64 wvec,
                          float act_coef, float dt, float sqrt3, u64 dP, long dp_env, u64 ego, u64 partial,
-                         int dim, int num_blocks, u64 stream) {
+                         int dim, int num_blocks, int f16, u64 stream) {
   mb::CtrlNodeBwdArgs a{};
   a.dim = dim;
-  a.pooled = P<const bf16>(pooled); a.p_env = p_env; a.S = P<const float4>(S); a.s_env = s_env;
+  a.pooled = P<const h16>(pooled); a.p_env = p_env; a.S = P<const float4>(S); a.s_env = s_env;
   a.G = P<const float>(G); a.A = P<const float>(A); a.a_env = a_env; a.Gn = P<const float4>(Gn); a.gn_env = gn_env;
-  a.valid = P<const uint8_t>(valid); a.v_env = v_env; a.B = B; a.N = N; a.wrm = P<const bf16>(wrm);
+  a.valid = P<const uint8_t>(valid); a.v_env = v_env; a.B = B; a.N = N; a.wrm = P<const h16>(wrm);
   a.o_w1 = o1; a.o_w2 = o2; a.o_w3 = o3; a.o_w4 = o4; a.wvec = P<const float>(wvec);
-  a.act_coef = act_coef; a.dt = dt; a.sqrt3 = sqrt3; a.dP = P<bf16>(dP); a.dp_env = dp_env;
+  a.act_coef = act_coef; a.dt = dt; a.sqrt3 = sqrt3; a.dP = P<h16>(dP); a.dp_env = dp_env;
   a.ego = P<float4>(ego); a.partial = P<float>(partial);
-  return mb_ctrl_node_bwd(&a, num_blocks, ST(stream));
+  return (f16 ? mb_ctrl_node_bwd_f16 : mb_ctrl_node_bwd)(&a, num_blocks, ST(stream));
 }
 
 static int ctrl_edge_bwd(u64 S, long s_env, u64 idx, long i_env, u64 argmax, long am_env, u64 dP, long dp_env,
                          int B, int N, int K, u64 wpack, int f_ew1f, int f_ew2tn, u64 dEc, long de_env, u64 partial,
-                         int dim, int num_blocks, u64 stream) {
+                         int dim, int num_blocks, int f16, u64 stream) {
   mb::CtrlEdgeBwdArgs a{};
   a.dim = dim;
   a.S = P<const float4>(S); a.s_env = s_env; a.idx = P<const int>(idx); a.i_env = i_env;
-  a.argmax = P<const uint8_t>(argmax); a.am_env = am_env; a.dP = P<const bf16>(dP); a.dp_env = dp_env;
-  a.B = B; a.N = N; a.K = K; a.wpack = P<const bf16>(wpack); a.f_ew1f = f_ew1f; a.f_ew2tn = f_ew2tn;
+  a.argmax = P<const uint8_t>(argmax); a.am_env = am_env; a.dP = P<const h16>(dP); a.dp_env = dp_env;
+  a.B = B; a.N = N; a.K = K; a.wpack = P<const h16>(wpack); a.f_ew1f = f_ew1f; a.f_ew2tn = f_ew2tn;
   a.dEc = P<float4>(dEc); a.de_env = de_env; a.partial = P<float>(partial);
-  return mb_ctrl_edge_bwd(&a, num_blocks, ST(stream));
+  return (f16 ? mb_ctrl_edge_bwd_f16 : mb_ctrl_edge_bwd)(&a, num_blocks, ST(stream));
 }
 
 static int probe_mfma(u64 a, u64 b, u64 d, u64 stream) {

@@ -20,6 +20,7 @@ PKG = os.path.join(ROOT, "macbf_gnn_amd")
 BUILD = os.path.join(ROOT, "build", "csrc")
 ARCH = os.environ.get("MACBF_ARCH", "gfx950")
 KERNELS = ["scan", "scenario", "ctrl", "cbf", "graph", "optim", "probe"]
+HALF_KERNELS = {"ctrl", "cbf"}       # compiled for both 16-bit MFMA element types
 
 
 def ext_path():
@@ -53,7 +54,7 @@ def write_ninja(debug=False):
         f"bflags = {bflags}",
         f"ldflags = -shared -fPIC --offload-arch={ARCH} -Wl,-rpath,{tl} -Wl,-rpath,/opt/rocm/lib",
         "rule kcc",
-        "  command = $hipcc $kflags -c $in -o $out -MD -MF $out.d",
+        "  command = $hipcc $kflags $kdefs -c $in -o $out -MD -MF $out.d",
         "  depfile = $out.d",
         "  description = HIPCC $in",
         "rule bcc",
@@ -72,6 +73,11 @@ def write_ninja(debug=False):
         o = os.path.join(BUILD, k + ".o")
         lines.append(f"build {o}: kcc {src}")
         objs.append(o)
+        if k in HALF_KERNELS:   # second instantiation with fp16 MFMA inputs (csrc/prec.h)
+            o = os.path.join(BUILD, k + "_f16.o")
+            lines.append(f"build {o}: kcc {src}")
+            lines.append("  kdefs = -DMB_FP16=1")
+            objs.append(o)
     bo = os.path.join(BUILD, "bindings.o")
     lines.append(f"build {bo}: bcc {os.path.join(HERE, 'bindings.cpp')}")
     objs.append(bo)

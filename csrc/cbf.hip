@@ -23,6 +23,7 @@
 #endif
 
 namespace mb {
+namespace MB_PREC {
 
 constexpr int CBF_FWD_FRAGS = 34;  // w1f 2 + w2 16 + w3 16
 constexpr int CBF_VEC = 260;       // b2 128 | b3 64 | w4 64 | b4 1 (+3 pad)
@@ -30,24 +31,24 @@ constexpr int CBF_VEC = 260;       // b2 128 | b3 64 | w4 64 | b4 1 (+3 pad)
 
 
 // Layer-1 B fragment of one edge (K slots: see layout.cbf_w1_slot): fp32 features split into
-// bf16 hi (lanes h = 0) and residual lo (lanes h = 1) parts.
+// h16 hi (lanes h = 0) and residual lo (lanes h = 1) parts.
 template <int D>
-DEV bf16x8 cbf_edge_frag(const float (&rp)[D], const float (&rv)[D], float eye, float dfeat, bool ok, int h) {
-  bf16x8 f;
-  const bf16 z = (bf16)0.f;
+DEV h16x8 cbf_edge_frag(const float (&rp)[D], const float (&rv)[D], float eye, float dfeat, bool ok, int h) {
+  h16x8 f;
+  const h16 z = (h16)0.f;
 #pragma unroll
   for (int j = 0; j < 8; ++j) f[j] = z;
   if (!ok) return f;
-  bf16 hi[2 * D + 1], lo[2 * D + 1];
+  h16 hi[2 * D + 1], lo[2 * D + 1];
 #pragma unroll
   for (int q = 0; q < D; ++q) {
-    split_bf16(rp[q], hi[q], lo[q]);
-    split_bf16(rv[q], hi[D + q], lo[D + q]);
+    split_h16(rp[q], hi[q], lo[q]);
+    split_h16(rv[q], hi[D + q], lo[D + q]);
   }
-  split_bf16(dfeat, hi[2 * D], lo[2 * D]);
+  split_h16(dfeat, hi[2 * D], lo[2 * D]);
   if constexpr (D == 2) {
     if (h == 0) {
-      f[0] = hi[0]; f[1] = hi[1]; f[2] = hi[2]; f[3] = hi[3]; f[4] = (bf16)eye; f[5] = hi[4]; f[6] = (bf16)1.f;
+      f[0] = hi[0]; f[1] = hi[1]; f[2] = hi[2]; f[3] = hi[3]; f[4] = (h16)eye; f[5] = hi[4]; f[6] = (h16)1.f;
     } else {
       f[0] = lo[0]; f[1] = lo[1]; f[2] = lo[2]; f[3] = lo[3]; f[5] = lo[4];
     }
@@ -55,11 +56,11 @@ DEV bf16x8 cbf_edge_frag(const float (&rp)[D], const float (&rv)[D], float eye, 
     if (h == 0) {
 #pragma unroll
       for (int q = 0; q < 7; ++q) f[q] = hi[q];
-      f[7] = (bf16)1.f;
+      f[7] = (h16)1.f;
     } else {
 #pragma unroll
       for (int q = 0; q < 7; ++q) f[q] = lo[q];
-      f[7] = (bf16)eye;
+      f[7] = (h16)eye;
     }
   }
   return f;
@@ -68,7 +69,7 @@ DEV bf16x8 cbf_edge_frag(const float (&rp)[D], const float (&rv)[D], float eye, 
 struct CbfActs { f32x16 H1[2], H2[4], H3[2]; };
 
 // full forward for one 32-edge tile; returns the pre-mask head output for this lane's edge
-DEV float cbf_mlp(const bf16x8& F, const bf16* wl, const float* vl, int lane, CbfActs& o) {
+DEV float cbf_mlp(const h16x8& F, const h16* wl, const float* vl, int lane, CbfActs& o) {
   const int h = lane >> 5;
   const float* b2 = vl;
   const float* b3 = vl + 128;
@@ -151,7 +152,7 @@ DEV void cbf_edge(const float4* S, long s_env, long s_step, const int* idx, int 
 template <int WAVES, int D>
 __global__ __launch_bounds__(WAVES * 64) void cbf_fwd_kernel(CbfFwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  bf16* wl = reinterpret_cast<bf16*>(smem);
+  h16* wl = reinterpret_cast<h16*>(smem);
   float* vl = reinterpret_cast<float*>(smem + CBF_FWD_FRAGS * FRAG_BYTES);
   __shared__ float red[10][WAVES];
   block_copy16(wl, a.wpack + (size_t)a.f_fwd * 512, CBF_FWD_FRAGS * FRAG_BYTES);
@@ -173,7 +174,7 @@ __global__ __launch_bounds__(WAVES * 64) void cbf_fwd_kernel(CbfFwdArgs a) {
     bool mask1 = false;
 #pragma unroll 1
     for (int pass = 0; pass < 1 + a.two; ++pass) {
-      const bf16* wt = wl + opaque_zero();
+      const h16* wt = wl + opaque_zero();
       const float* vt = vl + opaque_zero();
       EdgeCtx<D> c;
       cbf_edge<D>(a.S, a.s_env, a.s_step, a.idx, a.B, a.N, a.K, e, E, pass, a.obs_r, a.dist_thr, a.dist_eps, c);
@@ -238,10 +239,12 @@ __global__ __launch_bounds__(WAVES * 64) void cbf_fwd_kernel(CbfFwdArgs a) {
 
 constexpr int CBF_FWD_WAVES = 4;
 
+}  // namespace MB_PREC
 }  // namespace mb
 
-extern "C" int mb_cbf_fwd(const mb::CbfFwdArgs* a, int num_blocks, hipStream_t st) {
+extern "C" int MB_SYM(cbf_fwd)(const mb::CbfFwdArgs* a, int num_blocks, hipStream_t st) {
   using namespace mb;
+  using namespace mb::MB_PREC;
   if (a->K > 16 || a->K < 1) return -1;
   const size_t lds = (size_t)CBF_FWD_FRAGS * FRAG_BYTES + CBF_VEC * 4;
   if (a->dim == 3) {
@@ -261,7 +264,7 @@ extern "C" int mb_cbf_fwd(const mb::CbfFwdArgs* a, int num_blocks, hipStream_t s
 //     -> dH2 = W3^T dH3 .relu' (16 MFMA) -> dH1 = W2^T dH2 .relu' (16) -> dF = W1^T dH1 (4)
 //     -> dL/d(s_i - s_j) incl. the |dp|_eps feature; written per evaluation (self edges 0)
 //   weight gradients (workgroup-shared): activations / deltas of the chunk are staged as
-//     edge-major bf16 LDS images; each wave owns a fixed subset of the 32x32 output tiles of
+//     edge-major h16 LDS images; each wave owns a fixed subset of the 32x32 output tiles of
 //     dW3 (64x128), dW2 (128x64), dW1f (64x32) and contracts over the chunk's 128 edges with
 //     ds_read_b64_tr_b16 fragments -> MFMA; bias grads are row sums of the A fragments, split
 //     over the waves that read the same row block; the 64->1 head (w4, b4) accumulates per
@@ -273,8 +276,9 @@ extern "C" int mb_cbf_fwd(const mb::CbfFwdArgs* a, int num_blocks, hipStream_t s
 //   replaces the separate forward/loss kernel and the dh round trip through HBM.
 // ---------------------------------------------------------------------------------------
 namespace mb {
+namespace MB_PREC {
 
-// LDS row strides (bf16 elements), chosen with a bank model of the access patterns
+// LDS row strides (h16 elements), chosen with a bank model of the access patterns
 // (ds_read_b64 / ds_read_b64_tr_b16: 64 banks per 32-lane half; ds_write_b64: 32 banks per
 // 16-lane group): 68 = 34 dwords and 148 = 74 dwords keep 32-row weight reads, 4-row transposed
 // reads and 16-row tile stores conflict-free or 2-way at most (72 / 136 were 2-4 way).
@@ -346,7 +350,7 @@ DEV void cbf_load(const CbfBwdArgs& a, long chunk, int wave, int r, long E, long
 //     -> dH2 = W3^T dH3 .relu' (16 MFMA) -> dH1 = W2^T dH2 .relu' (16) -> dF = W1^T dH1 (4)
 //     -> dL/d(s_i - s_j) incl. the |dp|_eps feature; written per evaluation (self edges 0)
 //   weight gradients (workgroup-shared): activations / deltas of the chunk are staged as
-//     edge-major bf16 LDS images; each wave owns a fixed subset of the 8 + 8 + 2 + 2 32x32
+//     edge-major h16 LDS images; each wave owns a fixed subset of the 8 + 8 + 2 + 2 32x32
 //     output tiles of dW3 (64x128), dW2 (128x64), dW1f (64x32), dW4pad (32x64) and contracts
 //     over the chunk's edges with ds_read_b64_tr_b16 fragments -> MFMA; bias grads are row
 //     sums of the A fragments, split over the waves that read the same row block; fixed
@@ -362,11 +366,11 @@ __global__ __launch_bounds__(NW * 64, 1) void cbf_bwd_kernel(CbfBwdArgs a) {
   constexpr int CH = Cfg::CH, KS = Cfg::KS;
   constexpr int TA = 8 / NW;                   // owned dW3 tiles (and dW2 tiles) per wave
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  bf16* W2 = reinterpret_cast<bf16*>(smem);
-  bf16* W3 = W2 + RM_W2;
-  bf16* wf = W3 + RM_W3;                       // w1f (2 frags) | w1ft (4 frags)
+  h16* W2 = reinterpret_cast<h16*>(smem);
+  h16* W3 = W2 + RM_W2;
+  h16* wf = W3 + RM_W3;                       // w1f (2 frags) | w1ft (4 frags)
   float* vl = reinterpret_cast<float*>(smem + CBF_BWD_W_BYTES);
-  bf16* stg = reinterpret_cast<bf16*>(smem + CBF_BWD_W_BYTES + CBF_VEC * 4);
+  h16* stg = reinterpret_cast<h16*>(smem + CBF_BWD_W_BYTES + CBF_VEC * 4);
   __shared__ float hx[CH];                     // fused: h / h' exchange
   __shared__ float lacc[8][FUSED ? CH / 2 : 1];  // fused: per-lane loss partial sums (pass-0 lanes)
   __shared__ float lred[NW][10];
@@ -400,25 +404,25 @@ __global__ __launch_bounds__(NW * 64, 1) void cbf_bwd_kernel(CbfBwdArgs a) {
     const CbfIn<D> cur = nx;
     if (chunk + gridDim.x < nchunks) cbf_load<FUSED, NW, D>(a, chunk + gridDim.x, wave, r, E, EV, nx);   // prefetch
     const EdgeCtx<D>& c = cur.c;
-    const bf16x8 F = cbf_edge_frag<D>(c.rp, c.rv, c.eye, c.dfeat, c.ok, h);
+    const h16x8 F = cbf_edge_frag<D>(c.rp, c.rv, c.eye, c.dfeat, c.ok, h);
     // one opaque base per LDS image per chunk: the per-lane address math is computed once and
     // shared by all fragment reads (immediate offsets), while the loads themselves cannot be
     // hoisted out of the chunk loop (~100 weight VGPRs otherwise)
-    const bf16* wt = wf + opaque_zero();
-    const bf16* W2c = W2 + opaque_zero();
-    const bf16* W3c = W3 + opaque_zero();
+    const h16* wt = wf + opaque_zero();
+    const h16* W2c = W2 + opaque_zero();
+    const h16* W3c = W3 + opaque_zero();
     const float* vlc = vl + opaque_zero();
     const float* b2 = vlc;
     const float* b3 = vlc + 128;
     const float* w4 = vlc + 192;
     // ---- forward recompute
-    bf16x16 H1b[2], H2b[4];
+    h16x16 H1b[2], H2b[4];
     f32x16 H3p[2];
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt) {
       f32x16 t1 = mfma(frag_ld(wt, mt, lane), F, zero16());
       relu_(t1);
-      H1b[mt] = to_bf16x16(t1);
+      H1b[mt] = to_h16x16(t1);
     }
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt) {
@@ -428,7 +432,7 @@ __global__ __launch_bounds__(NW * 64, 1) void cbf_bwd_kernel(CbfBwdArgs a) {
         t2 = mfma(wrm_acc(W2c, WS2, 32 * mt, kk, lane), bacc_frag<kk & 1>(H1b[kk >> 1]), t2);
       });
       relu_(t2);
-      H2b[mt] = to_bf16x16(t2);
+      H2b[mt] = to_h16x16(t2);
     }
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt) {
@@ -492,7 +496,7 @@ __global__ __launch_bounds__(NW * 64, 1) void cbf_bwd_kernel(CbfBwdArgs a) {
     }
     if (h == 0) db4 += dhv;
     // ---- head backward
-    bf16x16 d3b[2], H3b[2];
+    h16x16 d3b[2], H3b[2];
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt) {
       f32x16 d3;
@@ -508,13 +512,13 @@ __global__ __launch_bounds__(NW * 64, 1) void cbf_bwd_kernel(CbfBwdArgs a) {
           H3p[mt][reg] = fmaxf(x, 0.f);
         }
       }
-      d3b[mt] = to_bf16x16(d3);
-      H3b[mt] = to_bf16x16(H3p[mt]);
+      d3b[mt] = to_h16x16(d3);
+      H3b[mt] = to_h16x16(H3p[mt]);
     }
     // ---- stage A: dW3 (64x128) += dH3pre . H2^T ; db3   (tiles t = wave + NW u -> (t/4, t%4))
     {
-      bf16* imA = stg + par * Cfg::REGION;
-      bf16* imB = imA + CH * SA64;
+      h16* imA = stg + par * Cfg::REGION;
+      h16* imB = imA + CH * SA64;
 #pragma unroll
       for (int mt = 0; mt < 2; ++mt) store_tile(imA, SA64, erow, 32 * mt, d3b[mt], h);
 #pragma unroll
@@ -528,7 +532,7 @@ __global__ __launch_bounds__(NW * 64, 1) void cbf_bwd_kernel(CbfBwdArgs a) {
       if constexpr (Cfg::NREG == 2) par ^= 1; else __syncthreads();
     }
     // ---- dH2pre = (W3^T dH3pre) . relu'(H2)
-    bf16x16 d2b[4];
+    h16x16 d2b[4];
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt) {
       f32x16 t = zero16();
@@ -536,13 +540,13 @@ __global__ __launch_bounds__(NW * 64, 1) void cbf_bwd_kernel(CbfBwdArgs a) {
         constexpr int kk = decltype(kk_)::value;
         t = mfma(wrmT_acc(W3c, WS3, 32 * mt, kk, lane), bacc_frag<kk & 1>(d3b[kk >> 1]), t);
       });
-      d2b[mt] = to_bf16x16(t);
+      d2b[mt] = to_h16x16(t);
       mask_by_nonzero(d2b[mt], H2b[mt]);
     }
     // ---- stage B: dW2 (128x64) += dH2pre . H1^T ; db2   (tiles t = wave + NW u -> (t/2, t%2))
     {
-      bf16* imA = stg + par * Cfg::REGION;
-      bf16* imB = imA + CH * SA128;
+      h16* imA = stg + par * Cfg::REGION;
+      h16* imB = imA + CH * SA128;
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt) store_tile(imA, SA128, erow, 32 * mt, d2b[mt], h);
 #pragma unroll
@@ -556,7 +560,7 @@ __global__ __launch_bounds__(NW * 64, 1) void cbf_bwd_kernel(CbfBwdArgs a) {
       if constexpr (Cfg::NREG == 2) par ^= 1; else __syncthreads();
     }
     // ---- dH1pre = (W2^T dH2pre) . relu'(H1)
-    bf16x16 d1b[2];
+    h16x16 d1b[2];
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt) {
       f32x16 t = zero16();
@@ -564,7 +568,7 @@ __global__ __launch_bounds__(NW * 64, 1) void cbf_bwd_kernel(CbfBwdArgs a) {
         constexpr int kk = decltype(kk_)::value;
         t = mfma(wrmT_acc(W2c, WS2, 32 * mt, kk, lane), bacc_frag<kk & 1>(d2b[kk >> 1]), t);
       });
-      d1b[mt] = to_bf16x16(t);
+      d1b[mt] = to_h16x16(t);
       mask_by_nonzero(d1b[mt], H1b[mt]);
     }
     // ---- dF = W1^T dH1pre (rows: dx dy dvx dvy eye dist) -> dL/d(s_i - s_j)
@@ -595,19 +599,19 @@ __global__ __launch_bounds__(NW * 64, 1) void cbf_bwd_kernel(CbfBwdArgs a) {
     //      dW4pad (32x64) += [dh;0..] . relu(H3)^T, A = image cols 16..47 -> row 0 = dw4 (waves 2,3;
     //      rows >= 1 read padding / the next row and are discarded: MFMA rows are independent)
     {
-      bf16* imC = stg + par * Cfg::REGION;
-      bf16* imF = imC + CH * SA64;
-      bf16* imH = imF + CH * SA32;
+      h16* imC = stg + par * Cfg::REGION;
+      h16* imF = imC + CH * SA64;
+      h16* imH = imF + CH * SA32;
 #pragma unroll
       for (int mt = 0; mt < 2; ++mt) store_tile(imC, SA64, erow, 32 * mt, d1b[mt], h);
 #pragma unroll
       for (int mt = 0; mt < 2; ++mt) store_tile(imH, SA64, erow, 32 * mt, H3b[mt], h);
-      bf16x8 dv;
+      h16x8 dv;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) dv[j] = (bf16)0.f;
-      if (h == 0) dv[0] = (bf16)dhv;
-      *reinterpret_cast<bf16x8*>(imF + erow * SA32 + 8 * h) = F;
-      *reinterpret_cast<bf16x8*>(imF + erow * SA32 + 16 + 8 * h) = dv;
+      for (int j = 0; j < 8; ++j) dv[j] = (h16)0.f;
+      if (h == 0) dv[0] = (h16)dhv;
+      *reinterpret_cast<h16x8*>(imF + erow * SA32 + 8 * h) = F;
+      *reinterpret_cast<h16x8*>(imF + erow * SA32 + 16 + 8 * h) = dv;
       __syncthreads();
       if (wave < 2) stage_mma(imC, SA64, imF, SA32, wave, 0, KS, lane, accC);
       else if (wave < 4) stage_mma(imF + 16, SA32, imH, SA64, 0, wave - 2, KS, lane, accC);
@@ -682,10 +686,12 @@ static void launch_cbf_bwd(const CbfBwdArgs& a, int num_blocks, hipStream_t st) 
   hipLaunchKernelGGL((cbf_bwd_kernel<FUSED, NW, D>), dim3(num_blocks), dim3(NW * 64), lds, st, a);
 }
 
+}  // namespace MB_PREC
 }  // namespace mb
 
-extern "C" int mb_cbf_bwd(const mb::CbfBwdArgs* a, int num_blocks, hipStream_t st) {
+extern "C" int MB_SYM(cbf_bwd)(const mb::CbfBwdArgs* a, int num_blocks, hipStream_t st) {
   using namespace mb;
+  using namespace mb::MB_PREC;
   if (a->K > 16 || a->K < 1 || a->passes < 1 || a->passes > 2) return -1;
   if (a->fused && (a->passes != 2 || !a->dang || !a->counts)) return -2;
   if (a->dim == 3) {

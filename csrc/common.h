@@ -11,9 +11,9 @@
 #include <stdint.h>
 #include <type_traits>
 
-typedef __bf16 bf16;
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+#include "prec.h"
+typedef h16 h16x8 __attribute__((ext_vector_type(8)));
+typedef h16 h16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef short s16x4 __attribute__((ext_vector_type(4)));
@@ -35,8 +35,12 @@ DEV void static_for(F&& f) {
   }
 }
 
-DEV f32x16 mfma(const bf16x8& a, const bf16x8& b, const f32x16& c) {
+DEV f32x16 mfma(const h16x8& a, const h16x8& b, const f32x16& c) {
+#if MB_FP16
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+#else
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+#endif
 }
 
 DEV f32x16 zero16() {
@@ -48,12 +52,12 @@ DEV f32x16 zero16() {
 
 DEV int acc_row(int reg, int h) { return (reg & 3) + 8 * (reg >> 2) + 4 * h; }
 
-// accumulator regs 8S..8S+7 -> bf16 operand fragment
+// accumulator regs 8S..8S+7 -> h16 operand fragment
 template <int S>
-DEV bf16x8 acc_frag(const f32x16& c) {
-  bf16x8 r;
+DEV h16x8 acc_frag(const f32x16& c) {
+  h16x8 r;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) r[j] = (bf16)c[8 * S + j];
+  for (int j = 0; j < 8; ++j) r[j] = (h16)c[8 * S + j];
   return r;
 }
 
@@ -71,8 +75,8 @@ DEV f32x16 bias_rows(const float* b, int row0, int h) {
 }
 
 // 16-byte fragment load (LDS or global): fragment f, lane l
-DEV bf16x8 frag_ld(const bf16* base, int f, int lane) {
-  return *reinterpret_cast<const bf16x8*>(base + ((size_t)f * WAVE + lane) * 8);
+DEV h16x8 frag_ld(const h16* base, int f, int lane) {
+  return *reinterpret_cast<const h16x8*>(base + ((size_t)f * WAVE + lane) * 8);
 }
 
 // An opaque scalar zero: adding it to an LDS base inside a loop stops the compiler from
@@ -92,10 +96,10 @@ DEV unsigned xor32u(unsigned u) {
 DEV float shfl_xor32(float v) { return __uint_as_float(xor32u(__float_as_uint(v))); }
 DEV int shfl_xor32i(int v) { return (int)xor32u((unsigned)v); }
 
-// hi/lo bf16 split of an fp32 value: x ~= hi + lo with ~16 significant bits
-DEV void split_bf16(float x, bf16& hi, bf16& lo) {
-  hi = (bf16)x;
-  lo = (bf16)(x - (float)hi);
+// hi/lo h16 split of an fp32 value: x ~= hi + lo with ~16 significant bits
+DEV void split_h16(float x, h16& hi, h16& lo) {
+  hi = (h16)x;
+  lo = (h16)(x - (float)hi);
 }
 
 // wave-local LDS visibility: all prior LDS writes of this wave done before later LDS reads
@@ -133,32 +137,32 @@ DEV float u01(uint64_t key) { return (float)(mix64(key) >> 40) * (1.0f / 1677721
 
 namespace mb {
 
-typedef __bf16 bf16x16 __attribute__((ext_vector_type(16)));
+typedef h16 h16x16 __attribute__((ext_vector_type(16)));
 
-// f32x16 accumulator -> packed bf16 copy (8 VGPRs), element q = reg q
-DEV bf16x16 to_bf16x16(const f32x16& c) {
-  bf16x16 r;
+// f32x16 accumulator -> packed h16 copy (8 VGPRs), element q = reg q
+DEV h16x16 to_h16x16(const f32x16& c) {
+  h16x16 r;
 #pragma unroll
-  for (int q = 0; q < 16; ++q) r[q] = (bf16)c[q];
+  for (int q = 0; q < 16; ++q) r[q] = (h16)c[q];
   return r;
 }
 
 template <int S>
-DEV bf16x8 bacc_frag(const bf16x16& c) {
-  bf16x8 r;
+DEV h16x8 bacc_frag(const h16x16& c) {
+  h16x8 r;
 #pragma unroll
   for (int j = 0; j < 8; ++j) r[j] = c[8 * S + j];
   return r;
 }
 
 // store one standard-orientation tile (lane = edge row `erow` of the image, regs = features
-// col0 + acc_row(reg,h)) into an edge-major bf16 LDS image: 4 x 8-byte writes per lane
-DEV void store_tile(bf16* img, int stride, int erow, int col0, const bf16x16& v, int h) {
+// col0 + acc_row(reg,h)) into an edge-major h16 LDS image: 4 x 8-byte writes per lane
+DEV void store_tile(h16* img, int stride, int erow, int col0, const h16x16& v, int h) {
 #pragma unroll
   for (int g = 0; g < 4; ++g) {
-    bf16x4 q;
+    h16x4 q;
     q[0] = v[4 * g]; q[1] = v[4 * g + 1]; q[2] = v[4 * g + 2]; q[3] = v[4 * g + 3];
-    *reinterpret_cast<bf16x4*>(img + erow * stride + col0 + 8 * g + 4 * h) = q;
+    *reinterpret_cast<h16x4*>(img + erow * stride + col0 + 8 * g + 4 * h) = q;
   }
 }
 
@@ -166,15 +170,15 @@ DEV void store_tile(bf16* img, int stride, int erow, int col0, const bf16x16& v,
 // elements, 8-byte aligned): lane (r, h) receives img[e0 + 8h + j][m0 + r], j = 0..7, via two
 // ds_read_b64_tr_b16. Used as A (rows = m, k = e) or B (k = e, cols = m) of a contraction over
 // edges (the weight-gradient GEMMs). Requires EXEC = all 64 lanes.
-DEV bf16x8 tr_frag(const bf16* img, int stride, int e0, int m0, int lane) {
+DEV h16x8 tr_frag(const h16* img, int stride, int e0, int m0, int lane) {
   const int q = (lane & 15) >> 2, p = lane & 3, gg = (lane >> 4) & 1, h = lane >> 5;
-  const bf16* a1 = img + (e0 + 8 * h + q) * stride + m0 + 16 * gg + 4 * p;
-  const bf16* a2 = a1 + 4 * stride;
+  const h16* a1 = img + (e0 + 8 * h + q) * stride + m0 + 16 * gg + 4 * p;
+  const h16* a2 = a1 + 4 * stride;
   const s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4*)(a1));
   const s16x4 v2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4*)(a2));
-  const bf16x4 b1 = __builtin_bit_cast(bf16x4, v1);
-  const bf16x4 b2 = __builtin_bit_cast(bf16x4, v2);
-  bf16x8 r;
+  const h16x4 b1 = __builtin_bit_cast(h16x4, v1);
+  const h16x4 b2 = __builtin_bit_cast(h16x4, v2);
+  h16x8 r;
   r[0] = b1[0]; r[1] = b1[1]; r[2] = b1[2]; r[3] = b1[3];
   r[4] = b2[0]; r[5] = b2[1]; r[6] = b2[2]; r[7] = b2[3];
   return r;
@@ -184,13 +188,13 @@ DEV bf16x8 tr_frag(const bf16* img, int stride, int e0, int m0, int lane) {
 // returns the row sums of A over the edge steps [bs_lo, bs_hi) (bias gradient partial; per
 // lane: row 32mt + r over half h). Callers split the steps between the waves that read the
 // same row block, so the VALU cost of the bias sums is spread evenly.
-DEV float stage_mma(const bf16* imgA, int sA, const bf16* imgB, int sB, int mt, int nt, int esteps, int lane,
+DEV float stage_mma(const h16* imgA, int sA, const h16* imgB, int sB, int mt, int nt, int esteps, int lane,
                     f32x16& acc, int bs_lo = 0, int bs_hi = 0) {
   float s = 0.f;
 #pragma unroll 2
   for (int ks = 0; ks < esteps; ++ks) {
-    const bf16x8 a = tr_frag(imgA, sA, 16 * ks, 32 * mt, lane);
-    const bf16x8 b = tr_frag(imgB, sB, 16 * ks, 32 * nt, lane);
+    const h16x8 a = tr_frag(imgA, sA, 16 * ks, 32 * mt, lane);
+    const h16x8 b = tr_frag(imgB, sB, 16 * ks, 32 * nt, lane);
     acc = mfma(a, b, acc);
     if (ks >= bs_lo && ks < bs_hi) {
 #pragma unroll
@@ -214,7 +218,7 @@ DEV f32x16 bias_rows4(const float* b, int row0, int h) {
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 typedef unsigned int u32x8 __attribute__((ext_vector_type(8)));
 
-// d *= relu'(pre) given the bf16 post-activation H = relu(pre) (>= +0): per 16-bit element,
+// d *= relu'(pre) given the h16 post-activation H = relu(pre) (>= +0): per 16-bit element,
 // mask = 0 - min(H, 1) (0xFFFF where H != 0) with packed u16 ops, 3 ops per element pair.
 // (inline asm: the ext_vector u16x2 formulation of this was miscompiled by hipcc 7.2 into a
 // mask taken from only one register of H)
@@ -225,12 +229,12 @@ DEV unsigned nz_mask16x2(unsigned x) {
   return m;
 }
 
-DEV void mask_by_nonzero(bf16x16& d, const bf16x16& H) {
+DEV void mask_by_nonzero(h16x16& d, const h16x16& H) {
   u32x8 dv = __builtin_bit_cast(u32x8, d);
   const u32x8 hv = __builtin_bit_cast(u32x8, H);
 #pragma unroll
   for (int p = 0; p < 8; ++p) dv[p] &= nz_mask16x2(hv[p]);
-  d = __builtin_bit_cast(bf16x16, dv);
+  d = __builtin_bit_cast(h16x16, dv);
 }
 
 // write an owned dW tile (rows 32mt.., cols 32nt..) of a row-major (ncols) fp32 slab
@@ -250,22 +254,22 @@ DEV float sum32(float v) {   // sum over the 32 lanes of this lane's half
 
 namespace mb {
 
-// ---- MFMA operand readers for row-major bf16 weight images W[rows][stride] in LDS.
+// ---- MFMA operand readers for row-major h16 weight images W[rows][stride] in LDS.
 // One copy of a weight matrix serves the forward (W) and the backward (W^T) chains.
 
 // A = W, natural k:  elem j = W[m0 + r][16kk + 8h + j]        (one 16-byte read)
-DEV bf16x8 wrm_nat(const bf16* W, int stride, int m0, int kk, int lane) {
+DEV h16x8 wrm_nat(const h16* W, int stride, int m0, int kk, int lane) {
   const int r = lane & 31, h = lane >> 5;
-  return *reinterpret_cast<const bf16x8*>(W + (m0 + r) * stride + 16 * kk + 8 * h);
+  return *reinterpret_cast<const h16x8*>(W + (m0 + r) * stride + 16 * kk + 8 * h);
 }
 
 // A = W, accumulator k: elem j = W[m0 + r][32t + 16s + 8(j>>2) + 4h + (j&3)], kk = 2t + s
-DEV bf16x8 wrm_acc(const bf16* W, int stride, int m0, int kk, int lane) {
+DEV h16x8 wrm_acc(const h16* W, int stride, int m0, int kk, int lane) {
   const int r = lane & 31, h = lane >> 5;
-  const bf16* p = W + (m0 + r) * stride + 16 * kk + 4 * h;
-  const bf16x4 lo = *reinterpret_cast<const bf16x4*>(p);
-  const bf16x4 hi = *reinterpret_cast<const bf16x4*>(p + 8);
-  bf16x8 f;
+  const h16* p = W + (m0 + r) * stride + 16 * kk + 4 * h;
+  const h16x4 lo = *reinterpret_cast<const h16x4*>(p);
+  const h16x4 hi = *reinterpret_cast<const h16x4*>(p + 8);
+  h16x8 f;
   f[0] = lo[0]; f[1] = lo[1]; f[2] = lo[2]; f[3] = lo[3];
   f[4] = hi[0]; f[5] = hi[1]; f[6] = hi[2]; f[7] = hi[3];
   return f;
@@ -273,29 +277,29 @@ DEV bf16x8 wrm_acc(const bf16* W, int stride, int m0, int kk, int lane) {
 
 // two ds_read_b64_tr_b16: lane (r = 16gg + i, h) receives img[rb1 + j][c0 + r] (j<4) and
 // img[rb2 + j-4][c0 + r] (j>=4); rb1/rb2 may depend on h only (uniform per 16-lane group)
-DEV bf16x8 tr_pair(const bf16* img, int stride, int rb1, int rb2, int c0, int lane) {
+DEV h16x8 tr_pair(const h16* img, int stride, int rb1, int rb2, int c0, int lane) {
   const int q = (lane & 15) >> 2, p = lane & 3, gg = (lane >> 4) & 1;
-  const bf16* a1 = img + (rb1 + q) * stride + c0 + 16 * gg + 4 * p;
-  const bf16* a2 = img + (rb2 + q) * stride + c0 + 16 * gg + 4 * p;
+  const h16* a1 = img + (rb1 + q) * stride + c0 + 16 * gg + 4 * p;
+  const h16* a2 = img + (rb2 + q) * stride + c0 + 16 * gg + 4 * p;
   const s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4*)(a1));
   const s16x4 v2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4*)(a2));
-  const bf16x4 b1 = __builtin_bit_cast(bf16x4, v1);
-  const bf16x4 b2 = __builtin_bit_cast(bf16x4, v2);
-  bf16x8 r;
+  const h16x4 b1 = __builtin_bit_cast(h16x4, v1);
+  const h16x4 b2 = __builtin_bit_cast(h16x4, v2);
+  h16x8 r;
   r[0] = b1[0]; r[1] = b1[1]; r[2] = b1[2]; r[3] = b1[3];
   r[4] = b2[0]; r[5] = b2[1]; r[6] = b2[2]; r[7] = b2[3];
   return r;
 }
 
 // A = W^T, accumulator k: elem j = W[32t + 16s + 8(j>>2) + 4h + (j&3)][m0 + r]
-DEV bf16x8 wrmT_acc(const bf16* W, int stride, int m0, int kk, int lane) {
+DEV h16x8 wrmT_acc(const h16* W, int stride, int m0, int kk, int lane) {
   const int h = lane >> 5;
   const int rb = 16 * kk + 4 * h;
   return tr_pair(W, stride, rb, rb + 8, m0, lane);
 }
 
 // A = W^T, natural k: elem j = W[16kk + 8h + j][m0 + r]
-DEV bf16x8 wrmT_nat(const bf16* W, int stride, int m0, int kk, int lane) {
+DEV h16x8 wrmT_nat(const h16* W, int stride, int m0, int kk, int lane) {
   const int h = lane >> 5;
   const int rb = 16 * kk + 8 * h;
   return tr_pair(W, stride, rb, rb + 4, m0, lane);

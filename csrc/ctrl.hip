@@ -2,8 +2,8 @@
 //
 // A wave owns 32 agents. Edge phase: 16 tiles of 32 edges = 2 agents x 16 neighbour slots
 // (K <= 16 real, the rest masked). Per tile:
-//   F   (B operand, built in registers): [dx dy dvx dvy eye 1] hi-bf16 in lanes 0-31, the
-//       bf16 residuals (x - bf16(x)) in lanes 32-63 -> layer 1 sees ~fp32 inputs for free
+//   F   (B operand, built in registers): [dx dy dvx dvy eye 1] hi-h16 in lanes 0-31, the
+//       h16 residuals (x - h16(x)) in lanes 32-63 -> layer 1 sees ~fp32 inputs for free
 //   H1  = relu(W1f . F)               2 MFMA, standard orientation (rows = features)
 //   Z^T = H1^T . W2^T + b2           16 MFMA, H1's accumulator used directly as the A
 //                                      operand (rows = edges, lanes = features)
@@ -19,31 +19,32 @@
 #include "state.h"
 
 namespace mb {
+namespace MB_PREC {
 
-constexpr int PSTR = 136;            // pooled-image row stride (bf16): 128 + 8 pad, 272 B
+constexpr int PSTR = 136;            // pooled-image row stride (h16): 128 + 8 pad, 272 B
 constexpr int CTRL_FWD_FRAGS = 72;   // ew1f 2 + ew2 16 | nw1f 18 + nw2 16 + nw3 16 + nw4 4
 constexpr int CTRL_VEC = 352;        // eb2 128 | nb2 128 | nb3 64 | nb4 32 (padded)
 
 
 // edge layer-1 B fragment (layout.ctrl_edge_slot): hi [s_i - s_j (2D), eye, 1], lo [s_i - s_j]
 template <int D>
-DEV bf16x8 ctrl_edge_frag(const float (&rp)[D], const float (&rv)[D], float eye, bool ok, int h) {
-  bf16x8 f;
-  const bf16 z = (bf16)0.f;
+DEV h16x8 ctrl_edge_frag(const float (&rp)[D], const float (&rv)[D], float eye, bool ok, int h) {
+  h16x8 f;
+  const h16 z = (h16)0.f;
 #pragma unroll
   for (int j = 0; j < 8; ++j) f[j] = z;
   if (!ok) return f;
-  bf16 hi[2 * D], lo[2 * D];
+  h16 hi[2 * D], lo[2 * D];
 #pragma unroll
   for (int q = 0; q < D; ++q) {
-    split_bf16(rp[q], hi[q], lo[q]);
-    split_bf16(rv[q], hi[D + q], lo[D + q]);
+    split_h16(rp[q], hi[q], lo[q]);
+    split_h16(rv[q], hi[D + q], lo[D + q]);
   }
   if (h == 0) {
 #pragma unroll
     for (int q = 0; q < 2 * D; ++q) f[q] = hi[q];
-    f[2 * D] = (bf16)eye;
-    f[2 * D + 1] = (bf16)1.f;
+    f[2 * D] = (h16)eye;
+    f[2 * D + 1] = (h16)1.f;
   } else {
 #pragma unroll
     for (int q = 0; q < 2 * D; ++q) f[q] = lo[q];
@@ -53,22 +54,22 @@ DEV bf16x8 ctrl_edge_frag(const float (&rp)[D], const float (&rv)[D], float eye,
 
 // node layer-1 state fragment (layout.ctrl_node_slot): hi [p - g, v, 1], lo [p - g, v]
 template <int D>
-DEV bf16x8 node_state_frag(const float (&e)[D], const float (&v)[D], bool ok, int h) {
-  bf16x8 f;
-  const bf16 z = (bf16)0.f;
+DEV h16x8 node_state_frag(const float (&e)[D], const float (&v)[D], bool ok, int h) {
+  h16x8 f;
+  const h16 z = (h16)0.f;
 #pragma unroll
   for (int j = 0; j < 8; ++j) f[j] = z;
   if (!ok) return f;
-  bf16 hi[2 * D], lo[2 * D];
+  h16 hi[2 * D], lo[2 * D];
 #pragma unroll
   for (int q = 0; q < D; ++q) {
-    split_bf16(e[q], hi[q], lo[q]);
-    split_bf16(v[q], hi[D + q], lo[D + q]);
+    split_h16(e[q], hi[q], lo[q]);
+    split_h16(v[q], hi[D + q], lo[D + q]);
   }
   if (h == 0) {
 #pragma unroll
     for (int q = 0; q < 2 * D; ++q) f[q] = hi[q];
-    f[2 * D] = (bf16)1.f;
+    f[2 * D] = (h16)1.f;
   } else {
 #pragma unroll
     for (int q = 0; q < 2 * D; ++q) f[q] = lo[q];
@@ -84,7 +85,7 @@ DEV void acc_rows8(const f32x16& c, float (&o)[8]) {
 }
 
 // One edge tile in the transposed orientation: returns Z^T (4 column tiles) for 32 edges.
-DEV void ctrl_edge_tile(const bf16x8& F, const bf16* wl, const float* eb2, int lane, f32x16 (&Z)[4]) {
+DEV void ctrl_edge_tile(const h16x8& F, const h16* wl, const float* eb2, int lane, f32x16 (&Z)[4]) {
   const int r = lane & 31;
   f32x16 H1[2];
 #pragma unroll
@@ -109,7 +110,7 @@ DEV void ctrl_edge_tile(const bf16x8& F, const bf16* wl, const float* eb2, int l
 // node MLP forward for 32 agents; returns Y4 (rows 0..3 = the 4 gain pre-activations)
 struct NodeActs { f32x16 Y1[2], Y2[4], Y3[2], Y4; };
 
-DEV void node_forward(const bf16* pool, const bf16x8& sfrag, const bf16* wn, const float* nb2,
+DEV void node_forward(const h16* pool, const h16x8& sfrag, const h16* wn, const float* nb2,
                       const float* nb3, const float* nb4, int lane, NodeActs& o) {
   const int r = lane & 31, h = lane >> 5;
 #pragma unroll
@@ -117,7 +118,7 @@ DEV void node_forward(const bf16* pool, const bf16x8& sfrag, const bf16* wn, con
     f32x16 c = zero16();
 #pragma unroll
     for (int kk = 0; kk < 8; ++kk) {
-      const bf16x8 p = *reinterpret_cast<const bf16x8*>(pool + r * PSTR + 16 * kk + 8 * h);
+      const h16x8 p = *reinterpret_cast<const h16x8*>(pool + r * PSTR + 16 * kk + 8 * h);
       c = mfma(frag_ld(wn, mt * 9 + kk, lane), p, c);
     }
     c = mfma(frag_ld(wn, mt * 9 + 8, lane), sfrag, c);
@@ -193,10 +194,10 @@ DEV void ctrl_st_load(const float4* S, long s_env, const EdgeIdx& x, EdgeSt<D>& 
 template <int WAVES, int D>
 __global__ __launch_bounds__(WAVES * 64) void ctrl_fwd_kernel(CtrlArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  bf16* wl = reinterpret_cast<bf16*>(smem);                            // ew1f, ew2 (18 frags)
-  bf16* wn = wl + 18 * 512;                                            // nw1f..nw4 (54 frags)
+  h16* wl = reinterpret_cast<h16*>(smem);                            // ew1f, ew2 (18 frags)
+  h16* wn = wl + 18 * 512;                                            // nw1f..nw4 (54 frags)
   float* vl = reinterpret_cast<float*>(smem + CTRL_FWD_FRAGS * FRAG_BYTES);
-  bf16* pools = reinterpret_cast<bf16*>(smem + CTRL_FWD_FRAGS * FRAG_BYTES + CTRL_VEC * 4);
+  h16* pools = reinterpret_cast<h16*>(smem + CTRL_FWD_FRAGS * FRAG_BYTES + CTRL_VEC * 4);
   block_copy16(wl, a.wpack + (size_t)a.f_edge * 512, 18 * FRAG_BYTES);
   block_copy16(wn, a.wpack + (size_t)a.f_node * 512, 54 * FRAG_BYTES);
   block_copy16(vl, a.wvec, CTRL_VEC * 4);
@@ -207,7 +208,7 @@ __global__ __launch_bounds__(WAVES * 64) void ctrl_fwd_kernel(CtrlArgs a) {
   const float* nb4 = vl + 320;
 
   const int wave = threadIdx.x / WAVE, lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
-  bf16* pool = pools + wave * 32 * PSTR;
+  h16* pool = pools + wave * 32 * PSTR;
   const int N = a.N, K = a.K;
   const int total = a.B * N;
 
@@ -230,7 +231,7 @@ __global__ __launch_bounds__(WAVES * 64) void ctrl_fwd_kernel(CtrlArgs a) {
       const bool ok = cur.ok;
       const float eye = (cur.j == cur.i) ? 1.f : 0.f;
       const bool m = ok && (sqrtf(sqsum<D>(cur.rp)) < a.obs_r);   // strict, un-eps'd (controller.py:38-39)
-      const bf16x8 F = ctrl_edge_frag<D>(cur.rp, cur.rv, eye, ok, h);
+      const h16x8 F = ctrl_edge_frag<D>(cur.rp, cur.rv, eye, ok, h);
       f32x16 Z[4];
       ctrl_edge_tile(F, wl + opaque_zero(), eb2, lane, Z);
       const unsigned mask32 = (unsigned)(__ballot(m) & 0xffffffffull);
@@ -265,7 +266,7 @@ __global__ __launch_bounds__(WAVES * 64) void ctrl_fwd_kernel(CtrlArgs a) {
         if (q1 > p1 || (q1 == p1 && s1 < r1)) { p1 = q1; r1 = s1; }
         const int arow = 2 * q + h;   // h==0 writes agent 2q, h==1 agent 2q+1
         const float pv = (h == 0) ? p0 : p1;
-        pool[arow * PSTR + 32 * nt + r] = (bf16)pv;
+        pool[arow * PSTR + 32 * nt + r] = (h16)pv;
         if (a.argmax) {
           const int ga = g0 + arow;
           if (ga < total) {
@@ -283,8 +284,8 @@ __global__ __launch_bounds__(WAVES * 64) void ctrl_fwd_kernel(CtrlArgs a) {
         const int ga = g0 + ag;
         if (ga < total) {
           const int bb = ga / N, ii = ga - bb * N;
-          *reinterpret_cast<bf16x8*>(a.pooled + (long)bb * a.p_env + (long)ii * 128 + ch * 8) =
-              *reinterpret_cast<const bf16x8*>(pool + ag * PSTR + ch * 8);
+          *reinterpret_cast<h16x8*>(a.pooled + (long)bb * a.p_env + (long)ii * 128 + ch * 8) =
+              *reinterpret_cast<const h16x8*>(pool + ag * PSTR + ch * 8);
         }
       }
     }
@@ -304,7 +305,7 @@ __global__ __launch_bounds__(WAVES * 64) void ctrl_fwd_kernel(CtrlArgs a) {
     float ex[D];
 #pragma unroll
     for (int q = 0; q < D; ++q) ex[q] = sp[q] - gg[q];
-    const bf16x8 sf = node_state_frag<D>(ex, sv, ok, h);
+    const h16x8 sf = node_state_frag<D>(ex, sv, ok, h);
     NodeActs na;
     node_forward(pool, sf, wn + opaque_zero(), nb2, nb3, nb4, lane, na);
     float y4r[8];
@@ -361,10 +362,12 @@ size_t ctrl_fwd_lds() {
   return (size_t)CTRL_FWD_FRAGS * FRAG_BYTES + CTRL_VEC * 4 + (size_t)CTRL_WAVES * 32 * PSTR * 2;
 }
 
+}  // namespace MB_PREC
 }  // namespace mb
 
-extern "C" int mb_ctrl_fwd(const mb::CtrlArgs* a, int num_cu, hipStream_t st) {
+extern "C" int MB_SYM(ctrl_fwd)(const mb::CtrlArgs* a, int num_cu, hipStream_t st) {
   using namespace mb;
+  using namespace mb::MB_PREC;
   if (a->K > 16 || a->K < 1) return -1;
   const int groups = (a->B * a->N + 31) / 32;
   int blocks = (groups + CTRL_WAVES - 1) / CTRL_WAVES;
@@ -388,13 +391,14 @@ extern "C" int mb_ctrl_fwd(const mb::CtrlArgs* a, int num_cu, hipStream_t st) {
 // workgroup's LDS together with the weight-gradient staging:
 //   ctrl_node_bwd: pooled features (stored by the rollout) -> node MLP recompute -> gain law
 //     backward (dA = dt*G_{t+1}[v] + action-loss grad) -> dY4..dY1 -> dL/dpooled (to
-//     global, bf16) + dL/ds_t of the ego terms; node weight grads (WG-shared, 4 stages).
+//     global, h16) + dL/ds_t of the ego terms; node weight grads (WG-shared, 4 stages).
 //   ctrl_edge_bwd: edge MLP recompute, max-pool backward via the stored argmax slots,
 //     dH1 = W2^T dZ, dF = W1^T dH1 -> per-edge dL/d(s_i - s_j); edge weight grads.
 // Weight gradients accumulate into a fixed per-workgroup slab across all timesteps
 // (slab += partial, deterministic) and are reduced once after the recursion.
 // =======================================================================================
 namespace mb {
+namespace MB_PREC {
 
 constexpr int NB_WAVES = 4;
 constexpr int NB_CH = NB_WAVES * 32;                  // agents per chunk
@@ -417,9 +421,9 @@ DEV void add_tile(float* dst, int ncols, int mt, int nt, const f32x16& c, int la
 template <int D>
 __global__ __launch_bounds__(NB_WAVES * 64, 1) void ctrl_node_bwd_kernel(CtrlNodeBwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  bf16* wr = reinterpret_cast<bf16*>(smem);
+  h16* wr = reinterpret_cast<h16*>(smem);
   float* vl = reinterpret_cast<float*>(smem + NODE_RM_ELEMS * 2);
-  bf16* stg = reinterpret_cast<bf16*>(smem + NODE_RM_ELEMS * 2 + CTRL_VEC * 4);
+  h16* stg = reinterpret_cast<h16*>(smem + NODE_RM_ELEMS * 2 + CTRL_VEC * 4);
   block_copy16(wr, a.wrm, NODE_RM_ELEMS * 2);
   block_copy16(vl, a.wvec, CTRL_VEC * 4);
   __syncthreads();
@@ -447,8 +451,8 @@ __global__ __launch_bounds__(NB_WAVES * 64, 1) void ctrl_node_bwd_kernel(CtrlNod
 #pragma unroll
     for (int q = 0; q < D; ++q) { sp[q] = sv[q] = gg[q] = av[q] = gnp[q] = gnv[q] = 0.f; }
     bool vld = false;
-    bf16x8 Pf[9];
-    const bf16 z = (bf16)0.f;   // Pf is dead after Y1; S1 re-reads the pooled rows
+    h16x8 Pf[9];
+    const h16 z = (h16)0.f;   // Pf is dead after Y1; S1 re-reads the pooled rows
     if (ok) {
       b = ga / N; i = ga - b * N;
       load_rec<D>(a.S + (long)b * a.s_env * REC<D>, (unsigned)i, sp, sv);
@@ -459,9 +463,9 @@ __global__ __launch_bounds__(NB_WAVES * 64, 1) void ctrl_node_bwd_kernel(CtrlNod
       }
       if (a.Gn) load_rec<D>(a.Gn + (long)b * a.gn_env * REC<D>, (unsigned)i, gnp, gnv);
       vld = a.valid ? (a.valid[(long)b * a.v_env] != 0) : true;
-      const bf16* prow = a.pooled + (long)b * a.p_env + (long)i * 128;
+      const h16* prow = a.pooled + (long)b * a.p_env + (long)i * 128;
 #pragma unroll
-      for (int kk = 0; kk < 8; ++kk) Pf[kk] = *reinterpret_cast<const bf16x8*>(prow + 16 * kk + 8 * h);
+      for (int kk = 0; kk < 8; ++kk) Pf[kk] = *reinterpret_cast<const h16x8*>(prow + 16 * kk + 8 * h);
     } else {
 #pragma unroll
       for (int kk = 0; kk < 8; ++kk)
@@ -472,19 +476,19 @@ __global__ __launch_bounds__(NB_WAVES * 64, 1) void ctrl_node_bwd_kernel(CtrlNod
 #pragma unroll
     for (int q = 0; q < D; ++q) ex[q] = sp[q] - gg[q];
     Pf[8] = node_state_frag<D>(ex, sv, ok, h);
-    const bf16* W1 = wr + opaque_zero();
-    const bf16* W2 = W1 + 64 * NS1;
-    const bf16* W3 = W2 + 128 * NS2;
-    const bf16* W4 = W3 + 64 * NS3;
+    const h16* W1 = wr + opaque_zero();
+    const h16* W2 = W1 + 64 * NS1;
+    const h16* W3 = W2 + 128 * NS2;
+    const h16* W4 = W3 + 64 * NS3;
     // ---- forward recompute
-    bf16x16 Y1b[2], Y2b[4], Y3b[2];
+    h16x16 Y1b[2], Y2b[4], Y3b[2];
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt) {
       f32x16 c = zero16();
 #pragma unroll
       for (int kk = 0; kk < 9; ++kk) c = mfma(wrm_nat(W1 + opaque_zero(), NS1, 32 * mt, kk, lane), Pf[kk], c);
       relu_(c);
-      Y1b[mt] = to_bf16x16(c);
+      Y1b[mt] = to_h16x16(c);
     }
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt) {
@@ -494,7 +498,7 @@ __global__ __launch_bounds__(NB_WAVES * 64, 1) void ctrl_node_bwd_kernel(CtrlNod
         c = mfma(wrm_acc(W2 + opaque_zero(), NS2, 32 * mt, kk, lane), bacc_frag<kk & 1>(Y1b[kk >> 1]), c);
       });
       relu_(c);
-      Y2b[mt] = to_bf16x16(c);
+      Y2b[mt] = to_h16x16(c);
     }
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt) {
@@ -504,7 +508,7 @@ __global__ __launch_bounds__(NB_WAVES * 64, 1) void ctrl_node_bwd_kernel(CtrlNod
         c = mfma(wrm_acc(W3 + opaque_zero(), NS3, 32 * mt, kk, lane), bacc_frag<kk & 1>(Y2b[kk >> 1]), c);
       });
       relu_(c);
-      Y3b[mt] = to_bf16x16(c);
+      Y3b[mt] = to_h16x16(c);
     }
     f32x16 y4 = bias_rows(nb4, 0, h);
     static_for<4>([&](auto kk_) {
@@ -554,11 +558,11 @@ __global__ __launch_bounds__(NB_WAVES * 64, 1) void ctrl_node_bwd_kernel(CtrlNod
       const float hi4 = shfl_xor32(d4r[4 + q]);
       d4[q] = (h == 0) ? d4r[q] : hi4;
     }
-    const bf16x16 d4b = to_bf16x16(d4);
+    const h16x16 d4b = to_h16x16(d4);
     // Backward chain interleaved with the WG-shared weight-gradient stages so that each
     // activation dies right after its last use (register pressure).
     // ---- dY3 = W4^T dY4 (K = 32) . relu'(Y3)
-    bf16x16 d3b[2];
+    h16x16 d3b[2];
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt) {
       f32x16 c = zero16();
@@ -566,12 +570,12 @@ __global__ __launch_bounds__(NB_WAVES * 64, 1) void ctrl_node_bwd_kernel(CtrlNod
         constexpr int kk = decltype(kk_)::value;
         c = mfma(wrmT_acc(W4 + opaque_zero(), NS4, 32 * mt, kk, lane), bacc_frag<kk & 1>(d4b), c);
       });
-d3b[mt] = to_bf16x16(c);
+d3b[mt] = to_h16x16(c);
       mask_by_nonzero(d3b[mt], Y3b[mt]);
     }
     {   // S4: dWn4pad (32x64) += dY4 . Y3^T ; nb4
-      bf16* imA = stg;
-      bf16* imB = stg + NB_CH * 40;
+      h16* imA = stg;
+      h16* imB = stg + NB_CH * 40;
       store_tile(imA, 40, erow, 0, d4b, h);
 #pragma unroll
       for (int mt = 0; mt < 2; ++mt) store_tile(imB, 72, erow, 32 * mt, Y3b[mt], h);
@@ -580,7 +584,7 @@ d3b[mt] = to_bf16x16(c);
       __syncthreads();
     }
     // ---- dY2 = W3^T dY3 . relu'(Y2)
-    bf16x16 d2b[4];
+    h16x16 d2b[4];
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt) {
       f32x16 c = zero16();
@@ -588,12 +592,12 @@ d3b[mt] = to_bf16x16(c);
         constexpr int kk = decltype(kk_)::value;
         c = mfma(wrmT_acc(W3 + opaque_zero(), NS3, 32 * mt, kk, lane), bacc_frag<kk & 1>(d3b[kk >> 1]), c);
       });
-d2b[mt] = to_bf16x16(c);
+d2b[mt] = to_h16x16(c);
       mask_by_nonzero(d2b[mt], Y2b[mt]);
     }
     {   // S3: dWn3 (64x128) += dY3 . Y2^T ; nb3
-      bf16* imA = stg;
-      bf16* imB = stg + NB_CH * 72;
+      h16* imA = stg;
+      h16* imB = stg + NB_CH * 72;
 #pragma unroll
       for (int mt = 0; mt < 2; ++mt) store_tile(imA, 72, erow, 32 * mt, d3b[mt], h);
 #pragma unroll
@@ -607,7 +611,7 @@ d2b[mt] = to_bf16x16(c);
       __syncthreads();
     }
     // ---- dY1 = W2^T dY2 . relu'(Y1)
-    bf16x16 d1b[2];
+    h16x16 d1b[2];
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt) {
       f32x16 c = zero16();
@@ -615,12 +619,12 @@ d2b[mt] = to_bf16x16(c);
         constexpr int kk = decltype(kk_)::value;
         c = mfma(wrmT_acc(W2 + opaque_zero(), NS2, 32 * mt, kk, lane), bacc_frag<kk & 1>(d2b[kk >> 1]), c);
       });
-d1b[mt] = to_bf16x16(c);
+d1b[mt] = to_h16x16(c);
       mask_by_nonzero(d1b[mt], Y1b[mt]);
     }
     {   // S2: dWn2 (128x64) += dY2 . Y1^T ; nb2
-      bf16* imA = stg;
-      bf16* imB = stg + NB_CH * 136;
+      h16* imA = stg;
+      h16* imB = stg + NB_CH * 136;
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt) store_tile(imA, 136, erow, 32 * mt, d2b[mt], h);
 #pragma unroll
@@ -643,12 +647,12 @@ d1b[mt] = to_bf16x16(c);
       });
       if (mt < 4) {
         if (ok) {
-          bf16* drow = a.dP + (long)b * a.dp_env + (long)i * 128 + 32 * mt;
+          h16* drow = a.dP + (long)b * a.dp_env + (long)i * 128 + 32 * mt;
 #pragma unroll
           for (int g = 0; g < 4; ++g) {
-            bf16x4 v;
-            v[0] = (bf16)c[4 * g]; v[1] = (bf16)c[4 * g + 1]; v[2] = (bf16)c[4 * g + 2]; v[3] = (bf16)c[4 * g + 3];
-            *reinterpret_cast<bf16x4*>(drow + 8 * g + 4 * h) = v;
+            h16x4 v;
+            v[0] = (h16)c[4 * g]; v[1] = (h16)c[4 * g + 1]; v[2] = (h16)c[4 * g + 2]; v[3] = (h16)c[4 * g + 3];
+            *reinterpret_cast<h16x4*>(drow + 8 * g + 4 * h) = v;
           }
         }
       } else {
@@ -662,22 +666,22 @@ d1b[mt] = to_bf16x16(c);
       }
     }
     {   // S1: dWn1f (64x160) += dY1 . P^T  (P re-read from the pooled rows: L2-hot)
-      bf16* imA = stg;
-      bf16* imB = stg + NB_CH * 72;
+      h16* imA = stg;
+      h16* imB = stg + NB_CH * 72;
 #pragma unroll
       for (int mt = 0; mt < 2; ++mt) store_tile(imA, 72, erow, 32 * mt, d1b[mt], h);
-      const bf16x8 sf = node_state_frag<D>(ex, sv, ok, h);
-      const bf16* prow = a.pooled + (long)b * a.p_env + (long)i * 128;
-      bf16x8 zz;
+      const h16x8 sf = node_state_frag<D>(ex, sv, ok, h);
+      const h16* prow = a.pooled + (long)b * a.p_env + (long)i * 128;
+      h16x8 zz;
 #pragma unroll
       for (int j = 0; j < 8; ++j) zz[j] = z;
 #pragma unroll
       for (int kk = 0; kk < 8; ++kk) {
-        const bf16x8 pv = ok ? *reinterpret_cast<const bf16x8*>(prow + 16 * kk + 8 * h) : zz;
-        *reinterpret_cast<bf16x8*>(imB + erow * NS1 + 16 * kk + 8 * h) = pv;
+        const h16x8 pv = ok ? *reinterpret_cast<const h16x8*>(prow + 16 * kk + 8 * h) : zz;
+        *reinterpret_cast<h16x8*>(imB + erow * NS1 + 16 * kk + 8 * h) = pv;
       }
-      *reinterpret_cast<bf16x8*>(imB + erow * NS1 + 128 + 8 * h) = sf;
-      *reinterpret_cast<bf16x8*>(imB + erow * NS1 + 144 + 8 * h) = zz;
+      *reinterpret_cast<h16x8*>(imB + erow * NS1 + 128 + 8 * h) = sf;
+      *reinterpret_cast<h16x8*>(imB + erow * NS1 + 144 + 8 * h) = zz;
       __syncthreads();
 #pragma unroll
       for (int u = 0; u < 3; ++u) {
@@ -726,8 +730,8 @@ size_t ctrl_edge_bwd_lds() { return (size_t)22 * FRAG_BYTES + EB_STAGE; }
 template <int D>
 __global__ __launch_bounds__(EB_WAVES * 64, 2) void ctrl_edge_bwd_kernel(CtrlEdgeBwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  bf16* wf = reinterpret_cast<bf16*>(smem);                 // ew1f (2) | ew2tn (16) | ew1ft (4)
-  bf16* stg = reinterpret_cast<bf16*>(smem + 22 * FRAG_BYTES);
+  h16* wf = reinterpret_cast<h16*>(smem);                 // ew1f (2) | ew2tn (16) | ew1ft (4)
+  h16* stg = reinterpret_cast<h16*>(smem + 22 * FRAG_BYTES);
   block_copy16(wf, a.wpack + (size_t)a.f_ew1f * 512, 2 * FRAG_BYTES);
   block_copy16(wf + 2 * 512, a.wpack + (size_t)a.f_ew2tn * 512, 20 * FRAG_BYTES);
   __syncthreads();
@@ -739,7 +743,7 @@ __global__ __launch_bounds__(EB_WAVES * 64, 2) void ctrl_edge_bwd_kernel(CtrlEdg
   f32x16 accW2[2], accW1;
   accW2[0] = accW2[1] = accW1 = zero16();
   float bs[2] = {0.f, 0.f};
-  const bf16 z = (bf16)0.f;
+  const h16 z = (h16)0.f;
 
   for (long chunk = blockIdx.x; chunk < nchunks; chunk += gridDim.x) {
     EdgeIdx xi1;
@@ -761,20 +765,20 @@ __global__ __launch_bounds__(EB_WAVES * 64, 2) void ctrl_edge_bwd_kernel(CtrlEdg
       const int b = ok ? ga / N : 0;
       const int i = cur.i, j = cur.j;
       const float eye = (j == i) ? 1.f : 0.f;
-      const bf16x8 F = ctrl_edge_frag<D>(cur.rp, cur.rv, eye, ok, h);
-      const bf16* wt = wf + opaque_zero();
-      bf16x16 H1b[2];
+      const h16x8 F = ctrl_edge_frag<D>(cur.rp, cur.rv, eye, ok, h);
+      const h16* wt = wf + opaque_zero();
+      h16x16 H1b[2];
 #pragma unroll
       for (int mt = 0; mt < 2; ++mt) {
         f32x16 c = mfma(frag_ld(wt, mt, lane), F, zero16());
         relu_(c);
-        H1b[mt] = to_bf16x16(c);
+        H1b[mt] = to_h16x16(c);
       }
       // max-pool backward as an LDS scatter into the S1 image (rows = this wave's 32 edges =
       // agents 2q, 2q+1 x 16 slots): zero the rows, then lane (r, h) routes dP[f] of agent 2q+h,
       // f = 4r..4r+3, to row (h, argmax slot). One coalesced argmax/dP load per lane instead of
       // 16 redundant row loads + 64 compare/selects per edge lane.
-      bf16* imS = stg;                                           // S1 dZ image, stride 136
+      h16* imS = stg;                                           // S1 dZ image, stride 136
       {
         const u32x4 zero4 = {0u, 0u, 0u, 0u};
 #pragma unroll
@@ -784,7 +788,7 @@ __global__ __launch_bounds__(EB_WAVES * 64, 2) void ctrl_edge_bwd_kernel(CtrlEdg
         if (ag < total) {
           const int bb = ag / N, ii = ag - bb * N;
           const unsigned am4 = *reinterpret_cast<const unsigned*>(a.argmax + bb * (int)a.am_env + ii * 128 + 4 * r);
-          const bf16x4 dp4 = *reinterpret_cast<const bf16x4*>(a.dP + bb * (int)a.dp_env + ii * 128 + 4 * r);
+          const h16x4 dp4 = *reinterpret_cast<const h16x4*>(a.dP + bb * (int)a.dp_env + ii * 128 + 4 * r);
 #pragma unroll
           for (int jj = 0; jj < 4; ++jj) {
             const unsigned sl = (am4 >> (8 * jj)) & 0xFFu;
@@ -793,17 +797,17 @@ __global__ __launch_bounds__(EB_WAVES * 64, 2) void ctrl_edge_bwd_kernel(CtrlEdg
         }
         lds_wave_sync();
       }
-      bf16x8 dz[8];
+      h16x8 dz[8];
 #pragma unroll
-      for (int kk = 0; kk < 8; ++kk) dz[kk] = *reinterpret_cast<const bf16x8*>(imS + erow * 136 + 16 * kk + 8 * h);
+      for (int kk = 0; kk < 8; ++kk) dz[kk] = *reinterpret_cast<const h16x8*>(imS + erow * 136 + 16 * kk + 8 * h);
       // dH1 = W2^T dZ (natural k) . relu'(H1)
-      bf16x16 d1b[2];
+      h16x16 d1b[2];
 #pragma unroll
       for (int mt = 0; mt < 2; ++mt) {
         f32x16 c = zero16();
 #pragma unroll
         for (int kk = 0; kk < 8; ++kk) c = mfma(frag_ld(wt, 2 + mt * 8 + kk, lane), dz[kk], c);
-        d1b[mt] = to_bf16x16(c);
+        d1b[mt] = to_h16x16(c);
         mask_by_nonzero(d1b[mt], H1b[mt]);
       }
       // dF = W1^T dH1 -> rows dx dy dvx dvy (lanes h == 0, regs 0..3)
@@ -828,8 +832,8 @@ __global__ __launch_bounds__(EB_WAVES * 64, 2) void ctrl_edge_bwd_kernel(CtrlEdg
       // S1: dW2 (128x64) += dZ . H1^T ; eb2 (dZ is already in the image; bias-sum steps split
       //     between the two waves that read each row block)
       {
-        bf16* imA = stg;
-        bf16* imB = stg + EB_CH * 136;
+        h16* imA = stg;
+        h16* imB = stg + EB_CH * 136;
 #pragma unroll
         for (int mt = 0; mt < 2; ++mt) store_tile(imB, 72, erow, 32 * mt, H1b[mt], h);
         __syncthreads();
@@ -843,15 +847,15 @@ __global__ __launch_bounds__(EB_WAVES * 64, 2) void ctrl_edge_bwd_kernel(CtrlEdg
       }
       // S2: dW1f (64x32) += dH1 . F^T
       {
-        bf16* imA = stg;
-        bf16* imB = stg + EB_CH * 72;
+        h16* imA = stg;
+        h16* imB = stg + EB_CH * 72;
 #pragma unroll
         for (int mt = 0; mt < 2; ++mt) store_tile(imA, 72, erow, 32 * mt, d1b[mt], h);
-        bf16x8 zz;
+        h16x8 zz;
 #pragma unroll
         for (int jj = 0; jj < 8; ++jj) zz[jj] = z;
-        *reinterpret_cast<bf16x8*>(imB + erow * 40 + 8 * h) = F;
-        *reinterpret_cast<bf16x8*>(imB + erow * 40 + 16 + 8 * h) = zz;
+        *reinterpret_cast<h16x8*>(imB + erow * 40 + 8 * h) = F;
+        *reinterpret_cast<h16x8*>(imB + erow * 40 + 16 + 8 * h) = zz;
         __syncthreads();
         if (wave < 2) stage_mma(imA, 72, imB, 40, wave, 0, EB_CH / 16, lane, accW1);
         __syncthreads();
@@ -877,10 +881,12 @@ __global__ __launch_bounds__(EB_WAVES * 64, 2) void ctrl_edge_bwd_kernel(CtrlEdg
   }
 }
 
+}  // namespace MB_PREC
 }  // namespace mb
 
-extern "C" int mb_ctrl_node_bwd(const mb::CtrlNodeBwdArgs* a, int num_blocks, hipStream_t st) {
+extern "C" int MB_SYM(ctrl_node_bwd)(const mb::CtrlNodeBwdArgs* a, int num_blocks, hipStream_t st) {
   using namespace mb;
+  using namespace mb::MB_PREC;
   const size_t lds = ctrl_node_bwd_lds();
   if (a->dim == 3) {
     (void)hipFuncSetAttribute((const void*)ctrl_node_bwd_kernel<3>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -892,8 +898,9 @@ extern "C" int mb_ctrl_node_bwd(const mb::CtrlNodeBwdArgs* a, int num_blocks, hi
   return (int)hipGetLastError();
 }
 
-extern "C" int mb_ctrl_edge_bwd(const mb::CtrlEdgeBwdArgs* a, int num_blocks, hipStream_t st) {
+extern "C" int MB_SYM(ctrl_edge_bwd)(const mb::CtrlEdgeBwdArgs* a, int num_blocks, hipStream_t st) {
   using namespace mb;
+  using namespace mb::MB_PREC;
   if (a->K > 16 || a->K < 1) return -1;
   const size_t lds = ctrl_edge_bwd_lds();
   if (a->dim == 3) {

@@ -4,34 +4,34 @@
 
 namespace mb {
 
-// D = A(32x16) * B(16x32) with natural fragments loaded from global: a/b (64 lanes x 8 bf16),
+// D = A(32x16) * B(16x32) with natural fragments loaded from global: a/b (64 lanes x 8 h16),
 // d (64 lanes x 16 f32) raw accumulator registers.
-__global__ void probe_mfma_kernel(const bf16* a, const bf16* b, float* d) {
+__global__ void probe_mfma_kernel(const h16* a, const h16* b, float* d) {
   const int l = threadIdx.x;
-  const bf16x8 af = *reinterpret_cast<const bf16x8*>(a + l * 8);
-  const bf16x8 bf = *reinterpret_cast<const bf16x8*>(b + l * 8);
+  const h16x8 af = *reinterpret_cast<const h16x8*>(a + l * 8);
+  const h16x8 bf = *reinterpret_cast<const h16x8*>(b + l * 8);
   const f32x16 c = mfma(af, bf, zero16());
 #pragma unroll
   for (int q = 0; q < 16; ++q) d[l * 16 + q] = c[q];
 }
 
-__global__ void probe_tr_kernel(const bf16* img_g, int rows, int stride, int e0, int m0, bf16* out) {
-  __shared__ __attribute__((aligned(16))) bf16 img[64 * 136];
+__global__ void probe_tr_kernel(const h16* img_g, int rows, int stride, int e0, int m0, h16* out) {
+  __shared__ __attribute__((aligned(16))) h16 img[64 * 136];
   for (int i = threadIdx.x; i < rows * stride; i += blockDim.x) img[i] = img_g[i];
   __syncthreads();
-  const bf16x8 f = tr_frag(img, stride, e0, m0, threadIdx.x);
-  *reinterpret_cast<bf16x8*>(out + threadIdx.x * 8) = f;
+  const h16x8 f = tr_frag(img, stride, e0, m0, threadIdx.x);
+  *reinterpret_cast<h16x8*>(out + threadIdx.x * 8) = f;
 }
 
 }  // namespace mb
 
 extern "C" int mb_probe_mfma(const void* a, const void* b, float* d, hipStream_t st) {
-  hipLaunchKernelGGL(mb::probe_mfma_kernel, dim3(1), dim3(64), 0, st, (const bf16*)a, (const bf16*)b, d);
+  hipLaunchKernelGGL(mb::probe_mfma_kernel, dim3(1), dim3(64), 0, st, (const h16*)a, (const h16*)b, d);
   return (int)hipGetLastError();
 }
 
 extern "C" int mb_probe_tr(const void* img, int rows, int stride, int e0, int m0, void* out, hipStream_t st) {
   if (rows * stride > 64 * 136) return -1;
-  hipLaunchKernelGGL(mb::probe_tr_kernel, dim3(1), dim3(64), 0, st, (const bf16*)img, rows, stride, e0, m0, (bf16*)out);
+  hipLaunchKernelGGL(mb::probe_tr_kernel, dim3(1), dim3(64), 0, st, (const h16*)img, rows, stride, e0, m0, (h16*)out);
   return (int)hipGetLastError();
 }

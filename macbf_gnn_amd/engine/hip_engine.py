@@ -46,7 +46,8 @@ class HipEngine:
         if self.K > C.MAX_TOP_K:
             raise ValueError(f"top_k <= {C.MAX_TOP_K} supported by the native kernels")
         self.Tmax = cfg.inner_loops
-        self.pw = PackedWeights(trainer.fp, self.D)
+        self.hdt = {"bf16": torch.bfloat16, "fp16": torch.float16}.get(cfg.dtype, torch.bfloat16)
+        self.pw = PackedWeights(trainer.fp, self.D, self.hdt)
         offs = {pn: o for (m, pn, shape, o, n) in trainer.fp.specs}
         mk = lambda a: torch.as_tensor(a, dtype=torch.long, device=self.dev)
         self.maps = {}
@@ -59,7 +60,7 @@ class HipEngine:
     def _alloc(self):
         B, N, K, T, dev = self.B, self.N, self.K, self.Tmax, self.dev
         D, W, Nn = self.D, self.W, self.Nn
-        f32, i32, u8, bf = torch.float32, torch.int32, torch.uint8, torch.bfloat16
+        f32, i32, u8, bf = torch.float32, torch.int32, torch.uint8, self.hdt
         # node records (agents, then static obstacle points), time-major
         self.S = torch.zeros(T + 1, B, Nn, W, dtype=f32, device=dev)
         self.G = torch.zeros(B, N, D, dtype=f32, device=dev)
@@ -159,6 +160,9 @@ class HipEngine:
         tm = tr.timer
         T = self.rollout(s0, g, obs)
         tm.mark("rollout")
+        # loss scale of the upstream gradients (fp16: dynamic, trainer-owned; bf16: 1). Every
+        # backward quantity is linear in it; the flat gradient is unscaled after the slab reduce.
+        gs = float(tr.grad_scale)
         # validity: step t of env b counts iff the env was not done before t
         done = (self.dist[:T] / N) < C.DIST_MIN_CHECK                 # (T, B)
         di = done.to(torch.int32)
@@ -192,7 +196,7 @@ class HipEngine:
         idx1 = None if self.reuse else self.idx[1: T + 1]
         native.cbf_bwd(S, idx, None, pw.cbf_w, pw.cbf_off["w1f"], pw.cbf_rm, pw.cbf_v, passes=2, dE=dE,
                        partial=part_cbf, num_blocks=nbb, fused=True, dang=self.dang[:T], valid=valid_u8,
-                       counts=self.counts, idx1=idx1)
+                       counts=self.counts, idx1=idx1, grad_scale=gs)
         cur = torch.cuda.current_stream(self.dev)
         cur.wait_event(csr_done)
         # no-BPTT: s_t is a detached input, only h'(s_{t+1}) gradients reach a_t
@@ -203,7 +207,7 @@ class HipEngine:
         self.part_node.zero_()
         self.part_edge.zero_()
         act_coef = (C.LOSS_SCALE * C.LOSS_WEIGHTS[4]) / n_act
-        act_coef_f = float(act_coef)   # one host read per step (counts already reduced)
+        act_coef_f = float(act_coef) * gs   # one host read per step (counts already reduced)
         if self.bptt:
             # BPTT through the rollout: G_t = dL/ds_t, reverse time
             self.Gb[T].copy_(self.dS[T])
@@ -244,6 +248,8 @@ class HipEngine:
             native.reduce_rows(part, red)
             src, dst = self.maps[name]
             fg.index_add_(0, dst, red.index_select(0, src))
+        if gs != 1.0:
+            fg.mul_(1.0 / gs)
         tm.mark("grad_reduce")
         # ---- stats (device tensors; converted lazily by the logger)
         sums = self.red_cbf[native.CBF_P_LOSS: native.CBF_P_LOSS + 10].to(torch.float64)
@@ -279,7 +285,7 @@ class HipEngine:
             self._nobptt = {
                 "grids": (nb_n, nb_e),
                 "G": torch.zeros(TBm, self.N, self.D, dtype=torch.float32, device=self.dev),
-                "dP": torch.zeros(TBm, self.N, 128, dtype=torch.bfloat16, device=self.dev),
+                "dP": torch.zeros(TBm, self.N, 128, dtype=self.hdt, device=self.dev),
             }
         nb_n, nb_e = self._nobptt["grids"]
         return nb_n, nb_e, self._nobptt["G"], self._nobptt["dP"]

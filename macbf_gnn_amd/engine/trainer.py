@@ -66,6 +66,12 @@ class Trainer:
         self.logger = MetricsLogger(dp, cfg.log_path)
         self.timer = PhaseTimer(self.device, enabled=cfg.phase_timing)
         self.skipped_steps = 0
+        # fp16 mixed precision: dynamic loss scaling. The scale multiplies the
+        # in-kernel upstream gradients and is divided out of the flat gradient before the
+        # all-reduce; a non-finite step is skipped and halves it.
+        self.fp16 = cfg.dtype == "fp16" and self.device.type == "cuda"
+        self.grad_scale = float(cfg.loss_scale_init) if self.fp16 else 1.0
+        self._good_steps = 0
         self._next = None
         self._side = torch.cuda.Stream(device=self.device) if (self.device.type == "cuda" and cfg.prefetch_data) \
             else None
@@ -142,15 +148,25 @@ class Trainer:
         tm.mark("allreduce")
         # failure detection: a non-finite reduced gradient is identical on every
         # rank, so every rank skips the same step; parameters and Adam state stay untouched
-        if self.cfg.nan_guard and not bool(torch.isfinite(self.fp.grad).all()):
+        if (self.cfg.nan_guard or self.fp16) and not bool(torch.isfinite(self.fp.grad).all()):
             self.skipped_steps += 1
             stats["skipped"] = 1
+            if self.fp16:
+                self.grad_scale = max(self.grad_scale * 0.5, 1.0)
+                self._good_steps = 0
             if self.dp.rank == 0:
                 print(f"[macbf] step {self.step_count}: non-finite gradient, optimizer step skipped "
-                      f"({self.skipped_steps} so far)", flush=True)
+                      f"({self.skipped_steps} so far, grad scale {self.grad_scale:g})", flush=True)
         else:
             self.opt.step(self.groups_to_step())
             self.engine.after_update()
+            if self.fp16:
+                self._good_steps += 1
+                if self._good_steps >= self.cfg.loss_scale_growth:
+                    self.grad_scale = min(self.grad_scale * 2.0, 2.0 ** 24)
+                    self._good_steps = 0
+        if self.fp16:
+            stats["grad_scale"] = self.grad_scale
         tm.mark("optimizer")
         self.step_count += 1
         if tm.enabled:

@@ -26,7 +26,7 @@ class _CtrlFn(torch.autograd.Function):
         S = graph.node_records(s, obs)                   # (B, Nn, W)
         G = g.detach().float().contiguous()
         A = torch.empty(B, N, D, dtype=torch.float32, device=dev)
-        pooled = torch.empty(B, N, 128, dtype=torch.bfloat16, device=dev)
+        pooled = torch.empty(B, N, 128, dtype=w.dtype, device=dev)
         am = torch.empty(B, N, 128, dtype=torch.uint8, device=dev)
         native.ctrl_fwd(S, G, idx, w, mp.off["ew1f"], mp.off["nw1f"], v, A, None, None, None,
                         pooled=pooled, argmax=am)
@@ -49,7 +49,7 @@ class _CtrlFn(torch.autograd.Function):
         # the controller kernels accumulate into their slabs (BPTT sums over steps): start at 0
         pn = torch.zeros(nbn, native.CTRL_NODE_PARTIAL, dtype=torch.float32, device=dev)
         pe = torch.zeros(nbe, native.CTRL_EDGE_PARTIAL, dtype=torch.float32, device=dev)
-        dP = torch.empty(B, N, 128, dtype=torch.bfloat16, device=dev)
+        dP = torch.empty(B, N, 128, dtype=w.dtype, device=dev)
         ego = torch.empty(B, N, W, dtype=torch.float32, device=dev)
         dEc = torch.empty(B, N, K, W, dtype=torch.float32, device=dev)
         native.ctrl_node_bwd(pooled, S, G, A, Gn, None, rm, mp.rm_off, v, 0.0, dP, ego, pn, nbn)

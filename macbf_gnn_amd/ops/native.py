@@ -75,6 +75,22 @@ def check(t, dtype, shape=None, name="tensor"):
         raise NativeError(f"{name} shape {tuple(t.shape)} != {tuple(shape)}")
 
 
+HALF_DTYPES = (torch.bfloat16, torch.float16)
+
+
+def _half(t, name):
+    """16-bit MFMA element type of a packed-weight / activation tensor -> the kernel variant
+    flag (0: bf16, 1: fp16; csrc/prec.h)."""
+    if t is None or t.dtype not in HALF_DTYPES:
+        raise NativeError(f"{name} must be bf16 or fp16")
+    return int(t.dtype == torch.float16)
+
+
+def _same_half(t, ref, name):
+    if t is not None and t.dtype != ref.dtype:
+        raise NativeError(f"{name} dtype {t.dtype} != weight dtype {ref.dtype}")
+
+
 def _ok(rc, what):
     if rc != 0:
         raise NativeError(f"{what} launch failed: {rc} ({lib().err_str(rc) if rc > 0 else 'bad args'})")
@@ -219,7 +235,8 @@ def ctrl_fwd(S, G, idx, wpack, f_edge, f_node, wvec, A, Sn, dist_sum, act_sum, n
     check(G, torch.float32, (B, N, D), "G")
     if idx.dtype != torch.int32 or idx.stride(2) != 1 or idx.stride(1) != K:
         raise NativeError("idx must be int32 (B,N,K)")
-    check(wpack, torch.bfloat16, None, "wpack")
+    f16 = _half(wpack, "wpack")
+    check(wpack, wpack.dtype, None, "wpack")
     check(wvec, torch.float32, None, "wvec")
     if wvec.numel() < 352 or wpack.numel() < (f_node + 54) * 512:
         raise NativeError("packed controller weights too small")
@@ -229,8 +246,7 @@ def ctrl_fwd(S, G, idx, wpack, f_edge, f_node, wvec, A, Sn, dist_sum, act_sum, n
     _rows(noise, D, "noise", (B, N))
     if pooled is not None:
         _rows(pooled, 128, "pooled", (B, N))
-        if pooled.dtype != torch.bfloat16:
-            raise NativeError("pooled must be bf16")
+        _same_half(pooled, wpack, "pooled")
     if argmax is not None:
         _rows(argmax, 128, "argmax", (B, N))
         if argmax.dtype != torch.uint8:
@@ -245,7 +261,7 @@ def ctrl_fwd(S, G, idx, wpack, f_edge, f_node, wvec, A, Sn, dist_sum, act_sum, n
                         float(C.TIME_STEP), float(C.OBS_RADIUS), float(C.SQRT3),
                         ptr(pooled), pooled.stride(0) if pooled is not None else 0,
                         ptr(argmax), argmax.stride(0) if argmax is not None else 0,
-                        D, num_cu(S.device), stream_handle())
+                        D, num_cu(S.device), f16, stream_handle())
     _ok(rc, "ctrl_fwd")
 
 
@@ -286,7 +302,8 @@ def cbf_fwd(S, idx, wpack, f_fwd, wvec, *, dang=None, valid=None, two=True, h_ou
     check(dh_out, torch.float32, (2, T, B, N, K), "dh_out")
     if dh_out is not None:
         check(counts, torch.float32, None, "counts")
-    check(wpack, torch.bfloat16, None, "wpack")
+    f16 = _half(wpack, "wpack")
+    check(wpack, wpack.dtype, None, "wpack")
     check(wvec, torch.float32, None, "wvec")
     nb = num_blocks or cbf_fwd_grid(E, S.device)
     check(partial, torch.float32, (nb, 10), "partial")
@@ -294,7 +311,7 @@ def cbf_fwd(S, idx, wpack, f_fwd, wvec, *, dang=None, valid=None, two=True, h_ou
                        B, T, N, K, int(two), ptr(wpack), int(f_fwd), ptr(wvec), ptr(h_out), ptr(hn_out),
                        ptr(dh_out), ptr(counts), ptr(partial), LOSS_CONSTS,
                        float(C.OBS_RADIUS), float(C.DIST_MIN_THRES), float(C.CBF_DIST_EPS_COORD * D), D, nb,
-                       stream_handle())
+                       f16, stream_handle())
     _ok(rc, "cbf_fwd")
     return nb
 
@@ -304,12 +321,14 @@ def cbf_bwd_grid(EV: int, device) -> int:
 
 
 def cbf_bwd(S, idx, dh, wpack, f_bwd, wrm, wvec, *, passes=2, dE=None, partial=None, num_blocks=None,
-            fused=False, dang=None, valid=None, counts=None, idx1=None):
+            fused=False, dang=None, valid=None, counts=None, idx1=None, grad_scale=1.0):
     """dh (passes, T, B, N, K) -> dE (passes, T, B, N, K, 4), per-WG dW slabs (nb, CBF_PARTIAL).
 
     fused=True (training, passes=2): dh is not read; the kernel evaluates h and h' of every
     edge, forms the hinge-loss upstream gradients from dang (T,B,N,K), valid (T,B) and the
-    global counts [n_dang, n_safe], and writes the 10 loss partial sums at CBF_P_LOSS."""
+    global counts [n_dang, n_safe], and writes the 10 loss partial sums at CBF_P_LOSS.
+    grad_scale multiplies the in-kernel upstream gradients (fp16 loss scaling); the loss sums
+    are unscaled."""
     T, B, N, K = idx.shape
     check(idx, torch.int32, None, "idx")
     D, W = _time_major_S(S, T, B, N, passes - 1)
@@ -324,11 +343,12 @@ def cbf_bwd(S, idx, dh, wpack, f_bwd, wrm, wvec, *, passes=2, dE=None, partial=N
     else:
         check(dh, torch.float32, (passes, T, B, N, K), "dh")
     check(dE, torch.float32, (passes, T, B, N, K, W), "dE")
-    check(wpack, torch.bfloat16, None, "wpack")
+    f16 = _half(wpack, "wpack")
+    check(wpack, wpack.dtype, None, "wpack")
     check(wvec, torch.float32, None, "wvec")
     if wpack.numel() < (f_bwd + 70) * 512:
         raise NativeError("packed CBF weights too small")
-    check(wrm, torch.bfloat16, (128 * 68 + 64 * 148,), "wrm")
+    check(wrm, wpack.dtype, (128 * 68 + 64 * 148,), "wrm")
     if idx1 is not None:
         check(idx1, torch.int32, (T, B, N, K), "idx1")
     E = B * T * N * K
@@ -340,8 +360,9 @@ def cbf_bwd(S, idx, dh, wpack, f_bwd, wrm, wvec, *, passes=2, dE=None, partial=N
                        0 if fused else ptr(dh),
                        ptr(wpack), int(f_bwd), ptr(wrm), ptr(wvec), ptr(dE), ptr(partial), float(C.OBS_RADIUS),
                        float(C.DIST_MIN_THRES), float(C.CBF_DIST_EPS_COORD * D), int(fused), ptr(dang) if fused else 0,
-                       ptr(valid) if fused else 0, ptr(counts) if fused else 0, LOSS_CONSTS, ptr(idx1), D, nb,
-                       stream_handle())
+                       ptr(valid) if fused else 0, ptr(counts) if fused else 0,
+                       LOSS_CONSTS[:6] + (LOSS_CONSTS[6] * float(grad_scale),), ptr(idx1), D, nb,
+                       f16, stream_handle())
     _ok(rc, "cbf_bwd")
     return nb
 
@@ -415,8 +436,10 @@ def ctrl_node_bwd(pooled, S, G, A, Gn, valid_t, wrm, offs, wvec, act_coef, dP, e
     _records(Gn, "Gn", (B, N), W)
     if valid_t is not None and (valid_t.dtype != torch.uint8 or tuple(valid_t.shape) != (B,)):
         raise NativeError("valid_t must be uint8 (B,)")
-    check(wrm, torch.bfloat16, None, "wrm")
-    check(dP, torch.bfloat16, (B, N, 128), "dP")
+    f16 = _half(wrm, "wrm")
+    check(wrm, wrm.dtype, None, "wrm")
+    check(dP, wrm.dtype, (B, N, 128), "dP")
+    _same_half(pooled, wrm, "pooled")
     check(ego, torch.float32, (B, N, W), "ego")
     check(partial, torch.float32, (num_blocks, CTRL_NODE_PARTIAL), "partial")
     rc = lib().ctrl_node_bwd(ptr(pooled), pooled.stride(0), ptr(S), S.stride(0) // W, ptr(G), ptr(A), A.stride(0) // D,
@@ -424,7 +447,7 @@ def ctrl_node_bwd(pooled, S, G, A, Gn, valid_t, wrm, offs, wvec, act_coef, dP, e
                              ptr(valid_t), valid_t.stride(0) if valid_t is not None else 0, B, N,
                              ptr(wrm), offs["w1"], offs["w2"], offs["w3"], offs["w4"], ptr(wvec),
                              float(act_coef), float(C.TIME_STEP), float(C.SQRT3), ptr(dP), dP.stride(0),
-                             ptr(ego), ptr(partial), D, int(num_blocks), stream_handle())
+                             ptr(ego), ptr(partial), D, int(num_blocks), f16, stream_handle())
     _ok(rc, "ctrl_node_bwd")
 
 
@@ -436,13 +459,14 @@ def ctrl_edge_bwd(S, idx, argmax, dP, wpack, f_ew1f, f_ew2tn, dEc, partial, num_
     if idx.dtype != torch.int32 or idx.stride(2) != 1 or idx.stride(1) != K:
         raise NativeError("idx must be int32 (B,N,K)")
     _rows(argmax, 128, "argmax", (B, N))
-    check(dP, torch.bfloat16, (B, N, 128), "dP")
+    f16 = _half(wpack, "wpack")
+    check(dP, wpack.dtype, (B, N, 128), "dP")
     check(dEc, torch.float32, (B, N, K, W), "dEc")
     check(partial, torch.float32, (num_blocks, CTRL_EDGE_PARTIAL), "partial")
     rc = lib().ctrl_edge_bwd(ptr(S), S.stride(0) // W, ptr(idx), idx.stride(0), ptr(argmax), argmax.stride(0),
                              ptr(dP), dP.stride(0), B, N, K, ptr(wpack), int(f_ew1f), int(f_ew2tn), ptr(dEc),
                              dEc.stride(0) // W if dEc is not None else 0, ptr(partial), D, int(num_blocks),
-                             stream_handle())
+                             f16, stream_handle())
     _ok(rc, "ctrl_edge_bwd")
 
 

@@ -27,8 +27,9 @@ def _offsets(module):
 
 
 class ModulePack:
-    def __init__(self, kind: str, module, device):
+    def __init__(self, kind: str, module, device, dtype=torch.bfloat16):
         self.kind = kind
+        self.dtype = dtype      # 16-bit MFMA element type (bf16 | fp16)
         offs, self.shapes, self.n = _offsets(module)
         dim = module.in_dim // 2
         self.dim = dim
@@ -55,9 +56,9 @@ class ModulePack:
     @torch.no_grad()
     def pack(self, params):
         src = torch.cat([p.detach().float().reshape(-1) for p in params] + [self._const])
-        w = src.index_select(0, self._iw).to(torch.bfloat16)
+        w = src.index_select(0, self._iw).to(self.dtype)
         v = src.index_select(0, self._iv).contiguous()
-        rm = src.index_select(0, self._irm).to(torch.bfloat16)
+        rm = src.index_select(0, self._irm).to(self.dtype)
         return w, v, rm
 
     def unpack_grads(self, reds: Dict[str, torch.Tensor]):
@@ -69,10 +70,12 @@ class ModulePack:
         return [flat[o:o + n].view(shape) for (_, shape, o, n) in self.shapes]
 
 
-def module_pack(kind: str, module, device) -> ModulePack:
-    key = (kind, module.in_dim, str(device))
+def module_pack(kind: str, module, device, dtype=None) -> ModulePack:
+    """``dtype`` defaults to the module's ``mfma_dtype`` attribute (bf16 when unset)."""
+    dtype = dtype or getattr(module, "mfma_dtype", torch.bfloat16)
+    key = (kind, module.in_dim, str(device), dtype)
     mp = _CACHE.get(key)
     if mp is None:
-        mp = ModulePack(kind, module, device)
+        mp = ModulePack(kind, module, device, dtype)
         _CACHE[key] = mp
     return mp

@@ -8,9 +8,10 @@ from . import layout as L
 
 
 class PackedWeights:
-    def __init__(self, fp, dim: int = 2):
+    def __init__(self, fp, dim: int = 2, dtype=torch.bfloat16):
         self.fp = fp
         self.dim = dim
+        self.dtype = dtype
         offs = {pn: o for (m, pn, shape, o, n) in fp.specs}
         dev = fp.flat.device
         n = fp.numel
@@ -32,12 +33,12 @@ class PackedWeights:
         self._icrm = mk(self.cbf_rmp.index())
         self._src = torch.zeros(n + 2, dtype=torch.float32, device=dev)
         self._src[n + 1] = 1.0
-        self.ctrl_w = torch.empty(self._ictrl.numel(), dtype=torch.bfloat16, device=dev)
-        self.cbf_w = torch.empty(self._icbf.numel(), dtype=torch.bfloat16, device=dev)
+        self.ctrl_w = torch.empty(self._ictrl.numel(), dtype=dtype, device=dev)
+        self.cbf_w = torch.empty(self._icbf.numel(), dtype=dtype, device=dev)
         self.ctrl_v = torch.empty(self._vctrl.numel(), dtype=torch.float32, device=dev)
         self.cbf_v = torch.empty(self._vcbf.numel(), dtype=torch.float32, device=dev)
-        self.ctrl_rm = torch.empty(self._irm.numel(), dtype=torch.bfloat16, device=dev)
-        self.cbf_rm = torch.empty(self._icrm.numel(), dtype=torch.bfloat16, device=dev)
+        self.ctrl_rm = torch.empty(self._irm.numel(), dtype=dtype, device=dev)
+        self.cbf_rm = torch.empty(self._icrm.numel(), dtype=dtype, device=dev)
         self.update()
 
     @torch.no_grad()

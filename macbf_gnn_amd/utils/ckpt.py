@@ -34,6 +34,7 @@ def save(trainer, path: str):
         "step": int(trainer.step_count),
         "config": {k: v for k, v in cfg.items() if isinstance(v, (int, float, str, bool, type(None)))},
         "rng": {"seed": int(trainer.cfg.seed), "iteration": int(trainer.step_count)},
+        "grad_scale": float(getattr(trainer, "grad_scale", 1.0)),
     }
     tmp = path + ".tmp"
     os.makedirs(os.path.dirname(os.path.abspath(path)) or ".", exist_ok=True)
@@ -62,6 +63,8 @@ def load(trainer, path: str, strict: bool = True):
         trainer.opt.load_torch_state_dict("cbf", ck["optim_cbf"])
     if "step" in ck:
         trainer.step_count = int(ck["step"])
+    if "grad_scale" in ck and getattr(trainer, "fp16", False):
+        trainer.grad_scale = float(ck["grad_scale"])
     trainer.on_params_loaded()
     return ck
 
