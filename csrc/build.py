@@ -23,8 +23,15 @@ KERNELS = ["scan", "scenario", "ctrl", "cbf", "graph", "optim", "probe"]
 HALF_KERNELS = {"ctrl", "cbf"}       # compiled for both 16-bit MFMA element types
 
 
+HOST_SRCS = ["host/scenario_host.cpp", "host/bindings_host.cpp"]   # CPU runtime (plain C++)
+
+
 def ext_path():
     return os.path.join(PKG, "_C" + sysconfig.get_config_var("EXT_SUFFIX"))
+
+
+def host_ext_path():
+    return os.path.join(PKG, "_host" + sysconfig.get_config_var("EXT_SUFFIX"))
 
 
 def hipcc():
@@ -61,6 +68,15 @@ def write_ninja(debug=False):
         "  command = $hipcc $bflags -c $in -o $out -MD -MF $out.d",
         "  depfile = $out.d",
         "  description = CXX $in",
+        f"cxx = {shutil.which('g++') or 'g++'}",
+        f"hflags = -O3 -fPIC -std=c++17 -ffp-contract=off -Wall -I{HERE}/host -I{pybind11.get_include()} -I{py_inc}",
+        "rule hcc",
+        "  command = $cxx $hflags -c $in -o $out -MD -MF $out.d",
+        "  depfile = $out.d",
+        "  description = CXX $in",
+        "rule hlink",
+        "  command = $cxx -shared -pthread $in -o $out",
+        "  description = LINK $out",
         "rule link",
         "  command = $hipcc $ldflags $in -o $out",
         "  description = LINK $out",
@@ -82,7 +98,13 @@ def write_ninja(debug=False):
     lines.append(f"build {bo}: bcc {os.path.join(HERE, 'bindings.cpp')}")
     objs.append(bo)
     lines.append(f"build {ext_path()}: link {' '.join(objs)}")
-    lines.append(f"default {ext_path()}")
+    hobjs = []
+    for src in HOST_SRCS:
+        o = os.path.join(BUILD, "host_" + os.path.basename(src).replace(".cpp", ".o"))
+        lines.append(f"build {o}: hcc {os.path.join(HERE, src)}")
+        hobjs.append(o)
+    lines.append(f"build {host_ext_path()}: hlink {' '.join(hobjs)}")
+    lines.append(f"default {ext_path()} {host_ext_path()}")
     os.makedirs(BUILD, exist_ok=True)
     with open(os.path.join(BUILD, "build.ninja"), "w") as f:
         f.write("\n".join(lines) + "\n")

@@ -86,17 +86,14 @@ class Trainer:
 
     # ------------------------------------------------------------------ data
     def sample(self, it: Optional[int] = None):
-        """B scenarios for this rank -> (s0, g, obstacles or None). HIP: on-device parallel
-        sampler; CPU: host reference."""
+        """B scenarios for this rank -> (s0, g, obstacles or None): the parallel RSA sampler, on
+        the device (HIP kernel) or in the host runtime (C++), identical for one seed."""
         it = self.step_count if it is None else it
         cfg = self.cfg
         B, N = cfg.num_envs, cfg.num_agents
-        if self.device.type == "cuda":
-            from ..ops import scenario
-            return scenario.generate(B, N, seed=cfg.seed, iteration=it, rank=self.dp.rank, device=self.device,
-                                     dim=cfg.dim, num_obstacles=cfg.num_obstacles, obstacle_points=cfg.obstacle_points)
-        seed = (cfg.seed * 1_000_003 + it) * 4099 + self.dp.rank
-        return E.generate_scenarios(B, N, cfg.dim, cfg.num_obstacles, seed=seed)
+        from ..ops import scenario
+        return scenario.generate(B, N, seed=cfg.seed, iteration=it, rank=self.dp.rank, device=self.device,
+                                 dim=cfg.dim, num_obstacles=cfg.num_obstacles, obstacle_points=cfg.obstacle_points)
 
     def _sample_async(self, it: int):
         """Launch the (parameter-independent) scenario sampler for iteration ``it`` on a side

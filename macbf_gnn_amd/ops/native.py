@@ -195,7 +195,7 @@ def scenario(S, G, *, seed, L, r=C.DIST_MIN_THRES, spread=C.GOAL_SPREAD, max_rou
     if obs is not None:
         M = obs.shape[1]
         check(obs, torch.float32, (B, M, D), "obs")
-    if (3 * N + M) * D * 4 + N > 160 * 1024 - 64:
+    if (3 * N + M) * D * 4 + 5 * N + 16 + 4 * 2 ** D > 160 * 1024 - 64:
         raise NativeError(f"scenario sampler: env too large for LDS (N={N}, M={M}, D={D})")
     rc = lib().scenario(ptr(S), S.stride(0) // W, ptr(G), ptr(obs), M, D, B, N, float(L), float(r), float(spread),
                         int(seed) & 0xFFFFFFFFFFFFFFFF, int(max_rounds), ptr(status), stream_handle())

@@ -5,13 +5,11 @@ checkpoint at any DP width reproduces the data stream without saving RNG state.
 """
 from __future__ import annotations
 
-import math
-
 import torch
 
 from .. import config as C
 from .. import env as E
-from . import native
+from . import host, native
 
 
 def _mix(*xs) -> int:
@@ -24,43 +22,29 @@ def _mix(*xs) -> int:
 
 def obstacles(B, N, *, dim, num_obstacles, points, seed, device):
     """(B, num_obstacles*points, D) static point-set obstacles with the shapes of
-    ``env.generate_obstacles`` (2-D: alternating circles / rectangles, 3-D: spheres), sampled with
-    device-side torch ops from a counter-based seed (no host work, stream-ordered)."""
-    gen = torch.Generator(device=device)
-    gen.manual_seed(seed & 0x7FFFFFFFFFFFFFFF)
-    L = E.side_length(N, dim)
-    f32 = torch.float32
-    ctr = torch.rand(B, num_obstacles, 1, dim, generator=gen, device=device, dtype=f32) * L
-    if dim == 3:
-        k = torch.arange(points, device=device, dtype=f32) + 0.5
-        phi = torch.arccos(1.0 - 2.0 * k / points)
-        th = math.pi * (1.0 + 5 ** 0.5) * k
-        unit = torch.stack([torch.cos(th) * torch.sin(phi), torch.sin(th) * torch.sin(phi), torch.cos(phi)], -1)
-        rad = 0.1 + 0.2 * torch.rand(B, num_obstacles, 1, 1, generator=gen, device=device, dtype=f32)
-        pts = ctr + unit * rad
-    else:
-        th = torch.arange(points, device=device, dtype=f32) * (2.0 * math.pi / points)
-        circ = torch.stack([torch.cos(th), torch.sin(th)], -1)                       # (P, 2)
-        rad = 0.1 + 0.2 * torch.rand(B, num_obstacles, 1, 1, generator=gen, device=device, dtype=f32)
-        sides = 0.2 + 0.4 * torch.rand(B, num_obstacles, 1, 2, generator=gen, device=device, dtype=f32)
-        # rectangle boundary: the reference's proportional split, on the unit square, then scaled
-        rect = torch.as_tensor(E.generate_obstacle_rectangle((0.0, 0.0), (1.0, 1.0), points), device=device,
-                               dtype=f32)
-        is_circ = (torch.arange(num_obstacles, device=device) % 2 == 0).view(1, -1, 1, 1)
-        pts = ctr + torch.where(is_circ, circ * rad, rect * sides)
-    return pts.reshape(B, num_obstacles * points, dim).contiguous()
+    ``env.generate_obstacles`` (2-D: alternating circles / rectangles, 3-D: spheres), from the
+    counter-based host sampler (``ops.host``; a few hundred floats) -> identical on CPU and GPU
+    for one seed; copied to the device asynchronously from pinned memory."""
+    pin = torch.device(device).type == "cuda"
+    out = torch.empty(B, num_obstacles * points, dim, dtype=torch.float32, pin_memory=pin)
+    host.sample_obstacles(B, N, dim=dim, num_obstacles=num_obstacles, points=points, seed=seed, out=out)
+    return out.to(device, non_blocking=True) if pin else out
 
 
 def generate(B, N, *, seed=0, iteration=0, rank=0, device=None, out=None, dim=2, num_obstacles=0,
              obstacle_points=12):
-    """-> (s0 (B,N,2D), g (B,N,D), obstacles (B,M,D) or None): on-device parallel RSA; obstacle
-    points are fixed conflict points for starts and goals."""
-    device = device or torch.device("cuda")
+    """-> (s0 (B,N,2D), g (B,N,D), obstacles (B,M,D) or None). HIP device: the on-device
+    parallel RSA kernel; CPU: the same process in the host runtime (bit-identical output).
+    Obstacle points are fixed conflict points for starts and goals."""
+    device = torch.device(device or "cuda")
     key = _mix(seed, iteration, rank)
     obs = None
     if num_obstacles:
         obs = obstacles(B, N, dim=dim, num_obstacles=num_obstacles, points=obstacle_points, seed=key ^ 0x5EED,
                         device=device)
+    if device.type != "cuda":
+        s0, g, _ = host.sample_scenarios(B, N, dim=dim, seed=key, obs=obs)
+        return s0, g, obs
     W = native.rec_width(dim)
     if out is None or dim != 2:
         S = torch.empty(B, N, W, dtype=torch.float32, device=device)

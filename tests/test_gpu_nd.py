@@ -143,3 +143,14 @@ def test_train_steps_3d_obstacles():
     torch.cuda.synchronize()
     assert torch.isfinite(tr.fp.flat).all() and not torch.equal(before, tr.fp.flat)
     assert 0.0 <= float(st["safe_agents"]) <= float(st["agent_steps"])
+
+
+@pytest.mark.parametrize("dim,nobs,N", [(2, 0, 1024), (3, 4, 300), (2, 2, 500)])
+def test_device_sampler_matches_host_runtime(dim, nobs, N):
+    """The HIP sampler and the C++ host runtime run the same parallel RSA: bit-identical."""
+    kw = dict(seed=3, iteration=2, rank=1, dim=dim, num_obstacles=nobs)
+    s, g, obs = scenario.generate(4, N, device=DEV, **kw)
+    s2, g2, obs2 = scenario.generate(4, N, device="cpu", **kw)
+    assert torch.equal(s.cpu(), s2) and torch.equal(g.cpu(), g2)
+    if nobs:
+        assert torch.equal(obs.cpu(), obs2)
