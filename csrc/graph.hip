@@ -71,16 +71,48 @@ __global__ __launch_bounds__(CSR_BLOCK) void rev_csr_kernel(CsrArgs a) {
   }
 }
 
-// dS[b, t', i] (+)= reduce of pass-0 edges of graph (b,t') and pass-1 edges of graph (b,t'-1),
+// Both reductions below give each output node a 16-lane group: the K outgoing records of the
+// node are one coalesced 16*K-byte segment (lane k reads slot k), the incoming edges are
+// spread over the lanes (independent random 16-byte loads, L2-resident per step graph), and
+// a fixed xor butterfly combines the lane partials -> deterministic, no atomics.
+constexpr int RG = 16;                 // lanes per node
+
+DEV float grp_sum(float v) {
+  v += __shfl_xor(v, 8, RG);
+  v += __shfl_xor(v, 4, RG);
+  v += __shfl_xor(v, 2, RG);
+  v += __shfl_xor(v, 1, RG);
+  return v;
+}
+
+template <int R>
+DEV void grp_sum(float4 (&g)[R]) {
+#pragma unroll
+  for (int q = 0; q < R; ++q) {
+    g[q].x = grp_sum(g[q].x); g[q].y = grp_sum(g[q].y); g[q].z = grp_sum(g[q].z); g[q].w = grp_sum(g[q].w);
+  }
+}
+
+template <int R, int SIGN>
+DEV void acc_rec(float4 (&g)[R], const float4* src) {
+#pragma unroll
+  for (int q = 0; q < R; ++q) {
+    const float4 v = src[q];
+    g[q].x += SIGN * v.x; g[q].y += SIGN * v.y; g[q].z += SIGN * v.z; g[q].w += SIGN * v.w;
+  }
+}
+
+// out[t', b, i] (+)= sum over passes p of [ sum_k dE_p[t'-p, b, i, k] - sum_{e in in(i)} dE_p[e] ]
 // for the N agents (obstacle nodes receive no gradient). Records of REC<D> float4.
 template <int D>
 __global__ __launch_bounds__(256) void node_reduce_kernel(NodeRedArgs a) {
-  const long tid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long node = ((long)blockIdx.x * blockDim.x + threadIdx.x) / RG;
+  const int l = threadIdx.x % RG;
   const long total = (long)a.B * (a.T + 1) * a.N;
-  if (tid >= total) return;
+  if (node >= total) return;             // whole 16-lane groups
   // time-major: out[(t'*B + b)*N + i], graphs g = t*B + b
-  const int i = (int)(tid % a.N);
-  const long tb = tid / a.N;
+  const int i = (int)(node % a.N);
+  const long tb = node / a.N;
   const int tp = (int)(tb / a.B);
   const int b = (int)(tb - (long)tp * a.B);
   const int N = a.N, K = a.K;
@@ -97,54 +129,18 @@ __global__ __launch_bounds__(256) void node_reduce_kernel(NodeRedArgs a) {
     const long ge = (long)t * a.B + b;                          // edge block of step t
     const long gi = ge + (pass == 1 ? (long)a.shift1 * a.B : 0);  // graph (CSR) the edges live in
     const float4* dE = a.dE + ((long)pass * E + ge * N * K) * R;
-    for (int k = 0; k < K; ++k) {
-#pragma unroll
-      for (int q = 0; q < R; ++q) {
-        const float4 v = dE[((long)i * K + k) * R + q];
-        g[q].x += v.x; g[q].y += v.y; g[q].z += v.z; g[q].w += v.w;
-      }
-    }
+    for (int k = l; k < K; k += RG) acc_rec<R, 1>(g, dE + ((long)i * K + k) * R);
     const int* ptr = a.ptr + gi * (Nt + 1);
     const int* edges = a.edges + gi * (long)N * K;
     const int q0 = ptr[i], q1 = ptr[i + 1];
-    // incoming edges in batches of 4: the 4 edge ids, then the 4 independent record loads
-    // (fixed order: the sum is the same as the one-by-one loop)
-    int q2 = q0;
-    for (; q2 + 4 <= q1; q2 += 4) {
-      int e4[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) e4[u] = edges[q2 + u];
-      float4 v4[4][R];
-#pragma unroll
-      for (int u = 0; u < 4; ++u)
-#pragma unroll
-        for (int q = 0; q < R; ++q) v4[u][q] = dE[(long)e4[u] * R + q];
-#pragma unroll
-      for (int u = 0; u < 4; ++u)
-#pragma unroll
-        for (int q = 0; q < R; ++q) {
-          g[q].x -= v4[u][q].x; g[q].y -= v4[u][q].y; g[q].z -= v4[u][q].z; g[q].w -= v4[u][q].w;
-        }
-    }
-    for (; q2 < q1; ++q2) {
-      const int e = edges[q2];
-#pragma unroll
-      for (int q = 0; q < R; ++q) {
-        const float4 v = dE[(long)e * R + q];
-        g[q].x -= v.x; g[q].y -= v.y; g[q].z -= v.z; g[q].w -= v.w;
-      }
-    }
+    for (int q = q0 + l; q < q1; q += RG) acc_rec<R, -1>(g, dE + (long)edges[q] * R);
   }
+  grp_sum<R>(g);
+  if (l != 0) return;
   float4* o = a.out + (((long)tp * a.B + b) * N + i) * R;
+  if (a.accumulate) acc_rec<R, 1>(g, o);
 #pragma unroll
-  for (int q = 0; q < R; ++q) {
-    float4 v = g[q];
-    if (a.accumulate) {
-      const float4 p = o[q];
-      v.x += p.x; v.y += p.y; v.z += p.z; v.w += p.w;
-    }
-    o[q] = v;
-  }
+  for (int q = 0; q < R; ++q) o[q] = g[q];
 }
 
 // One reverse-time step of the BPTT recursion (train.py:58-103 through autograd in the
@@ -153,53 +149,47 @@ __global__ __launch_bounds__(256) void node_reduce_kernel(NodeRedArgs a) {
 //         + Euler adjoint of s_{t+1} = s_t + dt [v_t, a_t]  (if bptt)
 template <int D>
 __global__ __launch_bounds__(256) void node_combine_kernel(CombineArgs a) {
-  const long tid = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (tid >= (long)a.B * a.N) return;
-  const int b = (int)(tid / a.N), i = (int)(tid % a.N);
+  const long node = ((long)blockIdx.x * blockDim.x + threadIdx.x) / RG;
+  const int l = threadIdx.x % RG;
+  if (node >= (long)a.B * a.N) return;   // whole 16-lane groups
+  const int b = (int)(node / a.N), i = (int)(node % a.N);
   const int N = a.N, K = a.K;
+  constexpr int R = REC<D>;
+  float4 g[R];
+#pragma unroll
+  for (int q = 0; q < R; ++q) g[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (a.dEc) {
+    const float4* dE = a.dEc + (long)b * N * K * R;
+    for (int k = l; k < K; k += RG) acc_rec<R, 1>(g, dE + ((long)i * K + k) * R);
+    const int* ptr = a.ptr + (long)b * a.ptr_env;
+    const int* edges = a.edges + (long)b * a.edges_env;
+    const int q0 = ptr[i], q1 = ptr[i + 1];
+    for (int q = q0 + l; q < q1; q += RG) acc_rec<R, -1>(g, dE + (long)edges[q] * R);
+    grp_sum<R>(g);
+  }
+  if (l != 0) return;
   float gp[D], gv[D], p[D], v[D];
-  load_rec<D>(a.dS + (long)b * a.ds_env * REC<D>, (unsigned)i, gp, gv);
+  load_rec<D>(a.dS + (long)b * a.ds_env * R, (unsigned)i, gp, gv);
   if (a.ego) {
-    load_rec<D>(a.ego + (long)b * N * REC<D>, (unsigned)i, p, v);
+    load_rec<D>(a.ego + (long)b * N * R, (unsigned)i, p, v);
 #pragma unroll
     for (int q = 0; q < D; ++q) { gp[q] += p[q]; gv[q] += v[q]; }
   }
   if (a.dEc) {
-    const float4* dE = a.dEc + (long)b * N * K * REC<D>;
-    for (int k = 0; k < K; ++k) {
-      load_rec<D>(dE, (unsigned)(i * K + k), p, v);
+    // the reduced edge term, as a record
+    float ep[D], ev[D];
+    if (D == 2) { ep[0] = g[0].x; ep[1] = g[0].y; ev[0] = g[0].z; ev[1] = g[0].w; }
+    else { ep[0] = g[0].x; ep[1] = g[0].y; ep[2] = g[0].z; ev[0] = g[R - 1].x; ev[1] = g[R - 1].y; ev[2] = g[R - 1].z; }
 #pragma unroll
-      for (int q = 0; q < D; ++q) { gp[q] += p[q]; gv[q] += v[q]; }
-    }
-    const int* ptr = a.ptr + (long)b * a.ptr_env;
-    const int* edges = a.edges + (long)b * a.edges_env;
-    const int q0 = ptr[i], q1 = ptr[i + 1];
-    int q2 = q0;
-    for (; q2 + 4 <= q1; q2 += 4) {     // 4 ids, then 4 independent record loads (same sum order)
-      int e4[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) e4[u] = edges[q2 + u];
-      float p4[4][D], v4[4][D];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) load_rec<D>(dE, (unsigned)e4[u], p4[u], v4[u]);
-#pragma unroll
-      for (int u = 0; u < 4; ++u)
-#pragma unroll
-        for (int q = 0; q < D; ++q) { gp[q] -= p4[u][q]; gv[q] -= v4[u][q]; }
-    }
-    for (; q2 < q1; ++q2) {
-      load_rec<D>(dE, (unsigned)edges[q2], p, v);
-#pragma unroll
-      for (int q = 0; q < D; ++q) { gp[q] -= p[q]; gv[q] -= v[q]; }
-    }
+    for (int q = 0; q < D; ++q) { gp[q] += ep[q]; gv[q] += ev[q]; }
   }
   if (a.Gn) {
     // Euler adjoint of s_{t+1} = s_t + dt [v_t, a_t]: dp += G_p, dv += G_v + dt G_p
-    load_rec<D>(a.Gn + (long)b * a.gn_env * REC<D>, (unsigned)i, p, v);
+    load_rec<D>(a.Gn + (long)b * a.gn_env * R, (unsigned)i, p, v);
 #pragma unroll
     for (int q = 0; q < D; ++q) { gp[q] += p[q]; gv[q] += v[q] + a.dt * p[q]; }
   }
-  store_rec<D>(a.Gout + (long)b * a.go_env * REC<D>, (unsigned)i, gp, gv);
+  store_rec<D>(a.Gout + (long)b * a.go_env * R, (unsigned)i, gp, gv);
 }
 
 }  // namespace mb
@@ -216,7 +206,7 @@ extern "C" int mb_rev_csr(const mb::CsrArgs* a, hipStream_t st) {
 
 extern "C" int mb_node_reduce(const mb::NodeRedArgs* a, hipStream_t st) {
   using namespace mb;
-  const long total = (long)a->B * (a->T + 1) * a->N;
+  const long total = (long)a->B * (a->T + 1) * a->N * RG;
   if (a->dim == 3) hipLaunchKernelGGL(node_reduce_kernel<3>, dim3((total + 255) / 256), dim3(256), 0, st, *a);
   else hipLaunchKernelGGL(node_reduce_kernel<2>, dim3((total + 255) / 256), dim3(256), 0, st, *a);
   return (int)hipGetLastError();
@@ -224,7 +214,7 @@ extern "C" int mb_node_reduce(const mb::NodeRedArgs* a, hipStream_t st) {
 
 extern "C" int mb_node_combine(const mb::CombineArgs* a, hipStream_t st) {
   using namespace mb;
-  const long total = (long)a->B * a->N;
+  const long total = (long)a->B * a->N * RG;
   if (a->dim == 3) hipLaunchKernelGGL(node_combine_kernel<3>, dim3((total + 255) / 256), dim3(256), 0, st, *a);
   else hipLaunchKernelGGL(node_combine_kernel<2>, dim3((total + 255) / 256), dim3(256), 0, st, *a);
   return (int)hipGetLastError();
