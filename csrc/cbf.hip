@@ -402,7 +402,9 @@ __global__ __launch_bounds__(NW * 64, 1) void cbf_bwd_kernel(CbfBwdArgs a) {
   if ((long)blockIdx.x < nchunks) cbf_load<FUSED, NW, D>(a, blockIdx.x, wave, r, E, EV, nx);
   for (long chunk = blockIdx.x; chunk < nchunks; chunk += gridDim.x) {
     const CbfIn<D> cur = nx;
+#ifndef CBF_X_NOLOAD
     if (chunk + gridDim.x < nchunks) cbf_load<FUSED, NW, D>(a, chunk + gridDim.x, wave, r, E, EV, nx);   // prefetch
+#endif
     const EdgeCtx<D>& c = cur.c;
     const h16x8 F = cbf_edge_frag<D>(c.rp, c.rv, c.eye, c.dfeat, c.ok, h);
     // one opaque base per LDS image per chunk: the per-lane address math is computed once and
@@ -420,9 +422,8 @@ __global__ __launch_bounds__(NW * 64, 1) void cbf_bwd_kernel(CbfBwdArgs a) {
     f32x16 H3p[2];
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt) {
-      f32x16 t1 = mfma(frag_ld(wt, mt, lane), F, zero16());
-      relu_(t1);
-      H1b[mt] = to_h16x16(t1);
+      const f32x16 t1 = mfma(frag_ld(wt, mt, lane), F, zero16());
+      H1b[mt] = to_h16x16_relu(t1);
     }
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt) {
@@ -431,8 +432,7 @@ __global__ __launch_bounds__(NW * 64, 1) void cbf_bwd_kernel(CbfBwdArgs a) {
         constexpr int kk = decltype(kk_)::value;
         t2 = mfma(wrm_acc(W2c, WS2, 32 * mt, kk, lane), bacc_frag<kk & 1>(H1b[kk >> 1]), t2);
       });
-      relu_(t2);
-      H2b[mt] = to_h16x16(t2);
+      H2b[mt] = to_h16x16_relu(t2);
     }
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt) {
@@ -441,25 +441,31 @@ __global__ __launch_bounds__(NW * 64, 1) void cbf_bwd_kernel(CbfBwdArgs a) {
         constexpr int kk = decltype(kk_)::value;
         t3 = mfma(wrm_acc(W3c, WS3, 32 * mt, kk, lane), bacc_frag<kk & 1>(H2b[kk >> 1]), t3);
       });
+      relu_(t3);                                   // relu(H3) in fp32 (the head is fp32)
       H3p[mt] = t3;
     }
     float dhv = cur.dh;
     if constexpr (FUSED) {
       // ---- head, h/h' exchange, local loss + upstream gradient
-      float hs = 0.f;
+      f32x2 hs2 = {0.f, 0.f};                      // packed fp32 FMAs (v_pk_fma_f32)
 #pragma unroll
       for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           const float4 w = *reinterpret_cast<const float4*>(w4 + 32 * mt + 8 * g + 4 * h);
-          hs += w.x * fmaxf(H3p[mt][4 * g], 0.f) + w.y * fmaxf(H3p[mt][4 * g + 1], 0.f) +
-                w.z * fmaxf(H3p[mt][4 * g + 2], 0.f) + w.w * fmaxf(H3p[mt][4 * g + 3], 0.f);
+          hs2 = __builtin_elementwise_fma(f32x2{w.x, w.y}, f32x2{H3p[mt][4 * g], H3p[mt][4 * g + 1]}, hs2);
+          hs2 = __builtin_elementwise_fma(f32x2{w.z, w.w}, f32x2{H3p[mt][4 * g + 2], H3p[mt][4 * g + 3]}, hs2);
         }
+      float hs = hs2.x + hs2.y;
       hs += shfl_xor32(hs);
       const float hm = (cur.in && c.mask) ? hs + vlc[256] : 0.f;
+#ifdef CBF_X_NOEXCH
+      const float other = hm;
+#else
       if (h == 0) hx[erow] = hm;
       __syncthreads();
       const float other = hx[(wave ^ (NW / 2)) * 32 + r];
+#endif
       const float hv = pass_w == 0 ? hm : other;
       const float hnv = pass_w == 0 ? other : hm;
       float gh = 0.f, ghn = 0.f;
@@ -496,26 +502,24 @@ __global__ __launch_bounds__(NW * 64, 1) void cbf_bwd_kernel(CbfBwdArgs a) {
     }
     if (h == 0) db4 += dhv;
     // ---- head backward
+    // dH3pre = w4 * dh . relu'(H3): packed products, then the 16-bit relu' mask of relu(H3)
     h16x16 d3b[2], H3b[2];
+    const f32x2 dh2 = {dhv, dhv};
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt) {
       f32x16 d3;
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const float4 w = *reinterpret_cast<const float4*>(w4 + 32 * mt + 8 * g + 4 * h);
-        const float wv[4] = {w.x, w.y, w.z, w.w};
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int reg = 4 * g + i;
-          const float x = H3p[mt][reg];
-          d3[reg] = x > 0.f ? wv[i] * dhv : 0.f;
-          H3p[mt][reg] = fmaxf(x, 0.f);
-        }
+        const f32x2 lo = f32x2{w.x, w.y} * dh2, hi = f32x2{w.z, w.w} * dh2;
+        d3[4 * g] = lo.x; d3[4 * g + 1] = lo.y; d3[4 * g + 2] = hi.x; d3[4 * g + 3] = hi.y;
       }
-      d3b[mt] = to_h16x16(d3);
       H3b[mt] = to_h16x16(H3p[mt]);
+      d3b[mt] = to_h16x16(d3);
+      mask_by_nonzero(d3b[mt], H3b[mt]);
     }
     // ---- stage A: dW3 (64x128) += dH3pre . H2^T ; db3   (tiles t = wave + NW u -> (t/4, t%4))
+#ifndef CBF_X_NOSTAGE
     {
       h16* imA = stg + par * Cfg::REGION;
       h16* imB = imA + CH * SA64;
@@ -527,10 +531,15 @@ __global__ __launch_bounds__(NW * 64, 1) void cbf_bwd_kernel(CbfBwdArgs a) {
 #pragma unroll
       for (int u = 0; u < TA; ++u) {
         const int t = wave + NW * u;
-        bA[u] += stage_mma(imA, SA64, imB, SA128, t / 4, t % 4, KS, lane, accA[u], bsA, bsA + KS / 4);
+#ifdef CBF_X_NOBIAS
+        bA[u] += stage_mma<KS>(imA, SA64, imB, SA128, t / 4, t % 4, lane, accA[u], 0, 0);
+#else
+        bA[u] += stage_mma<KS>(imA, SA64, imB, SA128, t / 4, t % 4, lane, accA[u], bsA, bsA + KS / 4);
+#endif
       }
       if constexpr (Cfg::NREG == 2) par ^= 1; else __syncthreads();
     }
+#endif
     // ---- dH2pre = (W3^T dH3pre) . relu'(H2)
     h16x16 d2b[4];
 #pragma unroll
@@ -544,6 +553,7 @@ __global__ __launch_bounds__(NW * 64, 1) void cbf_bwd_kernel(CbfBwdArgs a) {
       mask_by_nonzero(d2b[mt], H2b[mt]);
     }
     // ---- stage B: dW2 (128x64) += dH2pre . H1^T ; db2   (tiles t = wave + NW u -> (t/2, t%2))
+#ifndef CBF_X_NOSTAGE
     {
       h16* imA = stg + par * Cfg::REGION;
       h16* imB = imA + CH * SA128;
@@ -555,10 +565,15 @@ __global__ __launch_bounds__(NW * 64, 1) void cbf_bwd_kernel(CbfBwdArgs a) {
 #pragma unroll
       for (int u = 0; u < TA; ++u) {
         const int t = wave + NW * u;
-        bB[u] += stage_mma(imA, SA128, imB, SA64, t / 2, t % 2, KS, lane, accB[u], bsB, bsB + KS / 2);
+#ifdef CBF_X_NOBIAS
+        bB[u] += stage_mma<KS>(imA, SA128, imB, SA64, t / 2, t % 2, lane, accB[u], 0, 0);
+#else
+        bB[u] += stage_mma<KS>(imA, SA128, imB, SA64, t / 2, t % 2, lane, accB[u], bsB, bsB + KS / 2);
+#endif
       }
       if constexpr (Cfg::NREG == 2) par ^= 1; else __syncthreads();
     }
+#endif
     // ---- dH1pre = (W2^T dH2pre) . relu'(H1)
     h16x16 d1b[2];
 #pragma unroll
@@ -598,6 +613,7 @@ __global__ __launch_bounds__(NW * 64, 1) void cbf_bwd_kernel(CbfBwdArgs a) {
     // ---- stage C+D: dW1f (64x32) += dH1pre . [F|dh|0]^T (waves 0,1; cols >= 16 unused);
     //      dW4pad (32x64) += [dh;0..] . relu(H3)^T, A = image cols 16..47 -> row 0 = dw4 (waves 2,3;
     //      rows >= 1 read padding / the next row and are discarded: MFMA rows are independent)
+#ifndef CBF_X_NOSTAGE
     {
       h16* imC = stg + par * Cfg::REGION;
       h16* imF = imC + CH * SA64;
@@ -613,10 +629,11 @@ __global__ __launch_bounds__(NW * 64, 1) void cbf_bwd_kernel(CbfBwdArgs a) {
       *reinterpret_cast<h16x8*>(imF + erow * SA32 + 8 * h) = F;
       *reinterpret_cast<h16x8*>(imF + erow * SA32 + 16 + 8 * h) = dv;
       __syncthreads();
-      if (wave < 2) stage_mma(imC, SA64, imF, SA32, wave, 0, KS, lane, accC);
-      else if (wave < 4) stage_mma(imF + 16, SA32, imH, SA64, 0, wave - 2, KS, lane, accC);
+      if (wave < 2) stage_mma<KS>(imC, SA64, imF, SA32, wave, 0, lane, accC);
+      else if (wave < 4) stage_mma<KS>(imF + 16, SA32, imH, SA64, 0, wave - 2, lane, accC);
       if constexpr (Cfg::NREG == 2) par ^= 1; else __syncthreads();
     }
+#endif
   }
   __syncthreads();   // all stage reads done: the stage region is reused below
   float* bred = reinterpret_cast<float*>(stg);        // [NW][192] bias partials: b3 (64) | b2 (128)

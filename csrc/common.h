@@ -16,6 +16,7 @@ typedef h16 h16x8 __attribute__((ext_vector_type(8)));
 typedef h16 h16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
@@ -61,9 +62,14 @@ DEV h16x8 acc_frag(const f32x16& c) {
   return r;
 }
 
+// relu on fp32 bit patterns: max as signed int32 (negative floats are negative ints) -- one
+// v_max_i32 per element, where fmaxf costs a canonicalising v_max plus the max in IEEE mode.
+// -0 and negative values map to +0; +NaN passes through.
+DEV float relu_f(float x) { return __int_as_float(max(__float_as_int(x), 0)); }
+
 DEV void relu_(f32x16& c) {
 #pragma unroll
-  for (int i = 0; i < 16; ++i) c[i] = c[i] > 0.f ? c[i] : 0.f;
+  for (int i = 0; i < 16; ++i) c[i] = relu_f(c[i]);
 }
 
 // accumulator init with a per-row bias b[row0 + acc_row(reg,h)] (standard orientation)
@@ -77,6 +83,12 @@ DEV f32x16 bias_rows(const float* b, int row0, int h) {
 // 16-byte fragment load (LDS or global): fragment f, lane l
 DEV h16x8 frag_ld(const h16* base, int f, int lane) {
   return *reinterpret_cast<const h16x8*>(base + ((size_t)f * WAVE + lane) * 8);
+}
+
+// LDS view of a generic pointer into LDS (its low 32 bits are the LDS offset): index math on
+// the result stays 32-bit instead of 64-bit generic-pointer arithmetic.
+DEV const LDS_AS h16* lds_ptr(const h16* p) {
+  return (const LDS_AS h16*)(uintptr_t)(unsigned)(size_t)p;
 }
 
 // An opaque scalar zero: adding it to an LDS base inside a loop stops the compiler from
@@ -147,6 +159,41 @@ DEV h16x16 to_h16x16(const f32x16& c) {
   return r;
 }
 
+// relu on packed 16-bit floats (bf16 / fp16): signed 16-bit max with 0, two elements per op.
+// Rounding commutes with relu, so to_h16x16_relu(c) == to_h16x16(relu(c)) bit for bit.
+DEV unsigned relu_pk16(unsigned x) {
+  unsigned r;
+  asm volatile("v_pk_max_i16 %0, %1, 0" : "=v"(r) : "v"(x));
+  return r;
+}
+
+typedef unsigned int u32x8 __attribute__((ext_vector_type(8)));
+
+DEV h16x16 to_h16x16_relu(const f32x16& c) {
+  u32x8 v = __builtin_bit_cast(u32x8, to_h16x16(c));
+#pragma unroll
+  for (int p = 0; p < 8; ++p) v[p] = relu_pk16(v[p]);
+  return __builtin_bit_cast(h16x16, v);
+}
+
+// sum of the 8 16-bit elements of a fragment into an fp32 accumulator: 4 v_dot2 with (1, 1)
+typedef h16 h16x2 __attribute__((ext_vector_type(2)));
+DEV float dot_sum8(const h16x8& a, float s) {
+  const h16x2 one = {(h16)1.f, (h16)1.f};
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    // element pairs by shuffle, not bit_cast: hipcc 7.2 folds a u32x4 bit_cast of the fragment
+    // into four reads of its first dword
+    const h16x2 x = {a[2 * p], a[2 * p + 1]};
+#if MB_FP16
+    s = __builtin_amdgcn_fdot2(x, one, s, false);
+#else
+    s = __builtin_amdgcn_fdot2_f32_bf16(x, one, s, false);
+#endif
+  }
+  return s;
+}
+
 template <int S>
 DEV h16x8 bacc_frag(const h16x16& c) {
   h16x8 r;
@@ -172,8 +219,9 @@ DEV void store_tile(h16* img, int stride, int erow, int col0, const h16x16& v, i
 // edges (the weight-gradient GEMMs). Requires EXEC = all 64 lanes.
 DEV h16x8 tr_frag(const h16* img, int stride, int e0, int m0, int lane) {
   const int q = (lane & 15) >> 2, p = lane & 3, gg = (lane >> 4) & 1, h = lane >> 5;
-  const h16* a1 = img + (e0 + 8 * h + q) * stride + m0 + 16 * gg + 4 * p;
-  const h16* a2 = a1 + 4 * stride;
+  const LDS_AS h16* im = lds_ptr(img);                // 32-bit LDS address arithmetic
+  const LDS_AS h16* a1 = im + (e0 + 8 * h + q) * stride + m0 + 16 * gg + 4 * p;
+  const LDS_AS h16* a2 = a1 + 4 * stride;
   const s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4*)(a1));
   const s16x4 v2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4*)(a2));
   const h16x4 b1 = __builtin_bit_cast(h16x4, v1);
@@ -184,22 +232,31 @@ DEV h16x8 tr_frag(const h16* img, int stride, int e0, int m0, int lane) {
   return r;
 }
 
-// acc += A_img[rows 32mt.., k = e] . B_img[k = e, cols 32nt..] over `esteps` x 16 edges;
+// acc += A_img[rows 32mt.., k = e] . B_img[k = e, cols 32nt..] over ES x 16 edges;
 // returns the row sums of A over the edge steps [bs_lo, bs_hi) (bias gradient partial; per
-// lane: row 32mt + r over half h). Callers split the steps between the waves that read the
-// same row block, so the VALU cost of the bias sums is spread evenly.
-DEV float stage_mma(const h16* imgA, int sA, const h16* imgB, int sB, int mt, int nt, int esteps, int lane,
-                    f32x16& acc, int bs_lo = 0, int bs_hi = 0) {
+// lane: row 32mt + r over half h; 4 v_dot2 per step). Callers split the steps between the
+// waves that read the same row block. The fragments of step ks+2 are requested before the
+// MFMA of step ks, so the ds_read_b64_tr latency hides behind two MFMAs.
+template <int ES>
+DEV float stage_mma(const h16* imgA, int sA, const h16* imgB, int sB, int mt, int nt, int lane, f32x16& acc,
+                    int bs_lo = 0, int bs_hi = 0) {
+  static_assert(ES % 2 == 0, "even edge-step count");
+  bs_lo = __builtin_amdgcn_readfirstlane(bs_lo);   // wave-uniform: scalar branches below
+  bs_hi = __builtin_amdgcn_readfirstlane(bs_hi);
   float s = 0.f;
-#pragma unroll 2
-  for (int ks = 0; ks < esteps; ++ks) {
-    const h16x8 a = tr_frag(imgA, sA, 16 * ks, 32 * mt, lane);
-    const h16x8 b = tr_frag(imgB, sB, 16 * ks, 32 * nt, lane);
-    acc = mfma(a, b, acc);
-    if (ks >= bs_lo && ks < bs_hi) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) s += (float)a[j];
-    }
+  h16x8 a0 = tr_frag(imgA, sA, 0, 32 * mt, lane), b0 = tr_frag(imgB, sB, 0, 32 * nt, lane);
+  h16x8 a1 = tr_frag(imgA, sA, 16, 32 * mt, lane), b1 = tr_frag(imgB, sB, 16, 32 * nt, lane);
+#pragma nounroll
+  for (int ks = 0; ks < ES; ks += 2) {
+    acc = mfma(a0, b0, acc);
+    if (ks >= bs_lo && ks < bs_hi) s = dot_sum8(a0, s);
+    const int k2 = ks + 2 < ES ? ks + 2 : ks;       // last pair: harmless re-read, no branch
+    a0 = tr_frag(imgA, sA, 16 * k2, 32 * mt, lane);
+    b0 = tr_frag(imgB, sB, 16 * k2, 32 * nt, lane);
+    acc = mfma(a1, b1, acc);
+    if (ks + 1 >= bs_lo && ks + 1 < bs_hi) s = dot_sum8(a1, s);
+    a1 = tr_frag(imgA, sA, 16 * (k2 + 1), 32 * mt, lane);
+    b1 = tr_frag(imgB, sB, 16 * (k2 + 1), 32 * nt, lane);
   }
   return s;
 }
@@ -216,16 +273,15 @@ DEV f32x16 bias_rows4(const float* b, int row0, int h) {
 }
 
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
-typedef unsigned int u32x8 __attribute__((ext_vector_type(8)));
 
 // d *= relu'(pre) given the h16 post-activation H = relu(pre) (>= +0): per 16-bit element,
-// mask = 0 - min(H, 1) (0xFFFF where H != 0) with packed u16 ops, 3 ops per element pair.
-// (inline asm: the ext_vector u16x2 formulation of this was miscompiled by hipcc 7.2 into a
-// mask taken from only one register of H)
-DEV unsigned nz_mask16x2(unsigned x) {
+// m = min(H, 1) (1 where H != 0, else 0) and d * m as a 16-bit integer product (d or 0):
+// two packed ops per element pair. (inline asm: an ext_vector u16x2 formulation was
+// miscompiled by hipcc 7.2 into a mask taken from only one register of H)
+DEV unsigned mask_nz16x2(unsigned d, unsigned x) {
   unsigned m;
-  const unsigned ones = 0x00010001u, zero = 0u;
-  asm volatile("v_pk_min_u16 %0, %1, %2\n\tv_pk_sub_u16 %0, %3, %0" : "=&v"(m) : "v"(x), "v"(ones), "v"(zero));
+  const unsigned ones = 0x00010001u;   // both halves (an inline constant would only fill the low half)
+  asm volatile("v_pk_min_u16 %0, %1, %3\n\tv_pk_mul_lo_u16 %0, %2, %0" : "=&v"(m) : "v"(x), "v"(d), "v"(ones));
   return m;
 }
 
@@ -233,7 +289,7 @@ DEV void mask_by_nonzero(h16x16& d, const h16x16& H) {
   u32x8 dv = __builtin_bit_cast(u32x8, d);
   const u32x8 hv = __builtin_bit_cast(u32x8, H);
 #pragma unroll
-  for (int p = 0; p < 8; ++p) dv[p] &= nz_mask16x2(hv[p]);
+  for (int p = 0; p < 8; ++p) dv[p] = mask_nz16x2(dv[p], hv[p]);
   d = __builtin_bit_cast(h16x16, dv);
 }
 
@@ -279,8 +335,9 @@ DEV h16x8 wrm_acc(const h16* W, int stride, int m0, int kk, int lane) {
 // img[rb2 + j-4][c0 + r] (j>=4); rb1/rb2 may depend on h only (uniform per 16-lane group)
 DEV h16x8 tr_pair(const h16* img, int stride, int rb1, int rb2, int c0, int lane) {
   const int q = (lane & 15) >> 2, p = lane & 3, gg = (lane >> 4) & 1;
-  const h16* a1 = img + (rb1 + q) * stride + c0 + 16 * gg + 4 * p;
-  const h16* a2 = img + (rb2 + q) * stride + c0 + 16 * gg + 4 * p;
+  const LDS_AS h16* im = lds_ptr(img);                // 32-bit LDS address arithmetic
+  const LDS_AS h16* a1 = im + (rb1 + q) * stride + c0 + 16 * gg + 4 * p;
+  const LDS_AS h16* a2 = im + (rb2 + q) * stride + c0 + 16 * gg + 4 * p;
   const s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4*)(a1));
   const s16x4 v2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4*)(a2));
   const h16x4 b1 = __builtin_bit_cast(h16x4, v1);

@@ -580,7 +580,7 @@ d3b[mt] = to_h16x16(c);
 #pragma unroll
       for (int mt = 0; mt < 2; ++mt) store_tile(imB, 72, erow, 32 * mt, Y3b[mt], h);
       __syncthreads();
-      if (wave < 2) bs4 += stage_mma(imA, 40, imB, 72, 0, wave, NB_CH / 16, lane, acc4, 0, wave == 0 ? NB_CH / 16 : 0);
+      if (wave < 2) bs4 += stage_mma<NB_CH / 16>(imA, 40, imB, 72, 0, wave, lane, acc4, 0, wave == 0 ? NB_CH / 16 : 0);
       __syncthreads();
     }
     // ---- dY2 = W3^T dY3 . relu'(Y2)
@@ -606,7 +606,7 @@ d2b[mt] = to_h16x16(c);
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         const int t = wave + 4 * u;
-        bs3[u] += stage_mma(imA, 72, imB, 136, t / 4, t % 4, NB_CH / 16, lane, acc3[u], 0, t % 4 == 0 ? NB_CH / 16 : 0);
+        bs3[u] += stage_mma<NB_CH / 16>(imA, 72, imB, 136, t / 4, t % 4, lane, acc3[u], 0, t % 4 == 0 ? NB_CH / 16 : 0);
       }
       __syncthreads();
     }
@@ -633,7 +633,7 @@ d1b[mt] = to_h16x16(c);
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         const int t = wave + 4 * u;
-        bs2[u] += stage_mma(imA, 136, imB, 72, t / 2, t % 2, NB_CH / 16, lane, acc2[u], 0, t % 2 == 0 ? NB_CH / 16 : 0);
+        bs2[u] += stage_mma<NB_CH / 16>(imA, 136, imB, 72, t / 2, t % 2, lane, acc2[u], 0, t % 2 == 0 ? NB_CH / 16 : 0);
       }
       __syncthreads();
     }
@@ -686,7 +686,7 @@ d1b[mt] = to_h16x16(c);
 #pragma unroll
       for (int u = 0; u < 3; ++u) {
         const int t = wave + 4 * u;
-        if (u < n1) stage_mma(imA, 72, imB, NS1, t / 5, t % 5, NB_CH / 16, lane, acc1[u]);
+        if (u < n1) stage_mma<NB_CH / 16>(imA, 72, imB, NS1, t / 5, t % 5, lane, acc1[u]);
       }
       __syncthreads();
     }
@@ -840,7 +840,7 @@ __global__ __launch_bounds__(EB_WAVES * 64, 2) void ctrl_edge_bwd_kernel(CtrlEdg
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
           const int t = wave + 4 * u;
-          bs[u] += stage_mma(imA, 136, imB, 72, t / 2, t % 2, EB_CH / 16, lane, accW2[u], 4 * (wave & 1),
+          bs[u] += stage_mma<EB_CH / 16>(imA, 136, imB, 72, t / 2, t % 2, lane, accW2[u], 4 * (wave & 1),
                              4 * (wave & 1) + 4);
         }
         __syncthreads();
@@ -857,7 +857,7 @@ __global__ __launch_bounds__(EB_WAVES * 64, 2) void ctrl_edge_bwd_kernel(CtrlEdg
         *reinterpret_cast<h16x8*>(imB + erow * 40 + 8 * h) = F;
         *reinterpret_cast<h16x8*>(imB + erow * 40 + 16 + 8 * h) = zz;
         __syncthreads();
-        if (wave < 2) stage_mma(imA, 72, imB, 40, wave, 0, EB_CH / 16, lane, accW1);
+        if (wave < 2) stage_mma<EB_CH / 16>(imA, 72, imB, 40, wave, 0, lane, accW1);
         __syncthreads();
       }
     }
