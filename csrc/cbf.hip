@@ -360,6 +360,20 @@ DEV void cbf_load(const CbfBwdArgs& a, long chunk, int wave, int r, long E, long
 //   wave forms its upstream dL/dh locally (barrier + derivative hinge losses with the danger
 //   bit, step validity and the global pooled counts) and the loss partial sums go to the slab.
 // ---------------------------------------------------------------------------------------
+// ablation hooks (scripts/build_cbf_variants.sh): CBF_X_NOSTSTORE / CBF_X_NOSTMMA drop the
+// stage image stores / the stage contractions (results are then wrong; timing only)
+#ifdef CBF_X_NOSTSTORE
+#define XSTORE(...) ((void)0)
+#else
+#define XSTORE store_tile
+#endif
+#ifdef CBF_X_NOSTMMA
+template <int ES> DEV float xmma_skip(...) { return 0.f; }
+#define XMMA xmma_skip
+#else
+#define XMMA stage_mma
+#endif
+
 template <bool FUSED, int NW, int D>
 __global__ __launch_bounds__(NW * 64, 1) void cbf_bwd_kernel(CbfBwdArgs a) {
   using Cfg = CbfCfg<NW>;
@@ -524,17 +538,17 @@ __global__ __launch_bounds__(NW * 64, 1) void cbf_bwd_kernel(CbfBwdArgs a) {
       h16* imA = stg + par * Cfg::REGION;
       h16* imB = imA + CH * SA64;
 #pragma unroll
-      for (int mt = 0; mt < 2; ++mt) store_tile(imA, SA64, erow, 32 * mt, d3b[mt], h);
+      for (int mt = 0; mt < 2; ++mt) XSTORE(imA, SA64, erow, 32 * mt, d3b[mt], h);
 #pragma unroll
-      for (int mt = 0; mt < 4; ++mt) store_tile(imB, SA128, erow, 32 * mt, H2b[mt], h);
+      for (int mt = 0; mt < 4; ++mt) XSTORE(imB, SA128, erow, 32 * mt, H2b[mt], h);
       __syncthreads();
 #pragma unroll
       for (int u = 0; u < TA; ++u) {
         const int t = wave + NW * u;
 #ifdef CBF_X_NOBIAS
-        bA[u] += stage_mma<KS>(imA, SA64, imB, SA128, t / 4, t % 4, lane, accA[u], 0, 0);
+        bA[u] += XMMA<KS>(imA, SA64, imB, SA128, t / 4, t % 4, lane, accA[u], 0, 0);
 #else
-        bA[u] += stage_mma<KS>(imA, SA64, imB, SA128, t / 4, t % 4, lane, accA[u], bsA, bsA + KS / 4);
+        bA[u] += XMMA<KS>(imA, SA64, imB, SA128, t / 4, t % 4, lane, accA[u], bsA, bsA + KS / 4);
 #endif
       }
       if constexpr (Cfg::NREG == 2) par ^= 1; else __syncthreads();
@@ -558,17 +572,17 @@ __global__ __launch_bounds__(NW * 64, 1) void cbf_bwd_kernel(CbfBwdArgs a) {
       h16* imA = stg + par * Cfg::REGION;
       h16* imB = imA + CH * SA128;
 #pragma unroll
-      for (int mt = 0; mt < 4; ++mt) store_tile(imA, SA128, erow, 32 * mt, d2b[mt], h);
+      for (int mt = 0; mt < 4; ++mt) XSTORE(imA, SA128, erow, 32 * mt, d2b[mt], h);
 #pragma unroll
-      for (int mt = 0; mt < 2; ++mt) store_tile(imB, SA64, erow, 32 * mt, H1b[mt], h);
+      for (int mt = 0; mt < 2; ++mt) XSTORE(imB, SA64, erow, 32 * mt, H1b[mt], h);
       __syncthreads();
 #pragma unroll
       for (int u = 0; u < TA; ++u) {
         const int t = wave + NW * u;
 #ifdef CBF_X_NOBIAS
-        bB[u] += stage_mma<KS>(imA, SA128, imB, SA64, t / 2, t % 2, lane, accB[u], 0, 0);
+        bB[u] += XMMA<KS>(imA, SA128, imB, SA64, t / 2, t % 2, lane, accB[u], 0, 0);
 #else
-        bB[u] += stage_mma<KS>(imA, SA128, imB, SA64, t / 2, t % 2, lane, accB[u], bsB, bsB + KS / 2);
+        bB[u] += XMMA<KS>(imA, SA128, imB, SA64, t / 2, t % 2, lane, accB[u], bsB, bsB + KS / 2);
 #endif
       }
       if constexpr (Cfg::NREG == 2) par ^= 1; else __syncthreads();
@@ -619,9 +633,9 @@ __global__ __launch_bounds__(NW * 64, 1) void cbf_bwd_kernel(CbfBwdArgs a) {
       h16* imF = imC + CH * SA64;
       h16* imH = imF + CH * SA32;
 #pragma unroll
-      for (int mt = 0; mt < 2; ++mt) store_tile(imC, SA64, erow, 32 * mt, d1b[mt], h);
+      for (int mt = 0; mt < 2; ++mt) XSTORE(imC, SA64, erow, 32 * mt, d1b[mt], h);
 #pragma unroll
-      for (int mt = 0; mt < 2; ++mt) store_tile(imH, SA64, erow, 32 * mt, H3b[mt], h);
+      for (int mt = 0; mt < 2; ++mt) XSTORE(imH, SA64, erow, 32 * mt, H3b[mt], h);
       h16x8 dv;
 #pragma unroll
       for (int j = 0; j < 8; ++j) dv[j] = (h16)0.f;
@@ -629,8 +643,8 @@ __global__ __launch_bounds__(NW * 64, 1) void cbf_bwd_kernel(CbfBwdArgs a) {
       *reinterpret_cast<h16x8*>(imF + erow * SA32 + 8 * h) = F;
       *reinterpret_cast<h16x8*>(imF + erow * SA32 + 16 + 8 * h) = dv;
       __syncthreads();
-      if (wave < 2) stage_mma<KS>(imC, SA64, imF, SA32, wave, 0, lane, accC);
-      else if (wave < 4) stage_mma<KS>(imF + 16, SA32, imH, SA64, 0, wave - 2, lane, accC);
+      if (wave < 2) XMMA<KS>(imC, SA64, imF, SA32, wave, 0, lane, accC);
+      else if (wave < 4) XMMA<KS>(imF + 16, SA32, imH, SA64, 0, wave - 2, lane, accC);
       if constexpr (Cfg::NREG == 2) par ^= 1; else __syncthreads();
     }
 #endif
