@@ -15,11 +15,15 @@ namespace mb {
 
 constexpr int CSR_BLOCK = 256;
 
+// LDS_SORT (N*K <= 65536): the buckets are scattered into a 16-bit LDS buffer, insertion-sorted
+// there and written out coalesced; otherwise they are scattered / sorted in global memory.
+template <bool LDS_SORT>
 __global__ __launch_bounds__(CSR_BLOCK) void rev_csr_kernel(CsrArgs a) {
   extern __shared__ __attribute__((aligned(16))) int sm[];
   const int Nt = a.Nn > 0 ? a.Nn : a.N;   // target nodes (agents + obstacle points)
   int* cnt = sm;                 // Nt + 1
   int* fill = sm + Nt + 1;       // Nt
+  unsigned short* buf = reinterpret_cast<unsigned short*>(fill + Nt);   // LDS_SORT: N*K edge ids
   __shared__ int wsum[CSR_BLOCK];
   const long g = blockIdx.x;
   const int N = a.N, K = a.K, NK = N * K;
@@ -54,20 +58,33 @@ __global__ __launch_bounds__(CSR_BLOCK) void rev_csr_kernel(CsrArgs a) {
     const int j = idx[e];
     if (j != e / K) {
       const int p = atomicAdd(&fill[j], 1);
-      out[cnt[j] + p] = e;
+      if constexpr (LDS_SORT) buf[cnt[j] + p] = (unsigned short)e;
+      else out[cnt[j] + p] = e;
     }
   }
-  __threadfence();     // fill writes visible before other threads of the block sort them
+  if constexpr (!LDS_SORT) __threadfence();     // global fill writes visible to the block
   __syncthreads();
   // deterministic order inside each bucket: insertion sort by edge id
   for (int j = threadIdx.x; j < Nt; j += CSR_BLOCK) {
     const int b0 = cnt[j], b1 = cnt[j + 1];
     for (int x = b0 + 1; x < b1; ++x) {
-      const int v = out[x];
-      int y = x - 1;
-      while (y >= b0 && out[y] > v) { out[y + 1] = out[y]; --y; }
-      out[y + 1] = v;
+      if constexpr (LDS_SORT) {
+        const unsigned short v = buf[x];
+        int y = x - 1;
+        while (y >= b0 && buf[y] > v) { buf[y + 1] = buf[y]; --y; }
+        buf[y + 1] = v;
+      } else {
+        const int v = out[x];
+        int y = x - 1;
+        while (y >= b0 && out[y] > v) { out[y + 1] = out[y]; --y; }
+        out[y + 1] = v;
+      }
     }
+  }
+  if constexpr (LDS_SORT) {
+    __syncthreads();
+    const int tot = cnt[Nt];
+    for (int q = threadIdx.x; q < tot; q += CSR_BLOCK) out[q] = buf[q];
   }
 }
 
@@ -197,10 +214,17 @@ __global__ __launch_bounds__(256) void node_combine_kernel(CombineArgs a) {
 extern "C" int mb_rev_csr(const mb::CsrArgs* a, hipStream_t st) {
   using namespace mb;
   const int Nt = a->Nn > 0 ? a->Nn : a->N;
-  const size_t lds = (size_t)(2 * Nt + 1) * 4;
-  if (lds > 150 * 1024) return -1;
-  (void)hipFuncSetAttribute((const void*)rev_csr_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL(rev_csr_kernel, dim3(a->G), dim3(CSR_BLOCK), lds, st, *a);
+  const long NK = (long)a->N * a->K;
+  const size_t base = (size_t)(2 * Nt + 1) * 4;
+  const size_t lds_sorted = base + (size_t)NK * 2;
+  if (NK <= 65536 && lds_sorted <= 150 * 1024) {
+    (void)hipFuncSetAttribute((const void*)rev_csr_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_sorted);
+    hipLaunchKernelGGL(rev_csr_kernel<true>, dim3(a->G), dim3(CSR_BLOCK), lds_sorted, st, *a);
+  } else {
+    if (base > 150 * 1024) return -1;
+    (void)hipFuncSetAttribute((const void*)rev_csr_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)base);
+    hipLaunchKernelGGL(rev_csr_kernel<false>, dim3(a->G), dim3(CSR_BLOCK), base, st, *a);
+  }
   return (int)hipGetLastError();
 }
 

@@ -268,3 +268,27 @@ def test_full_step_4096_agents_matches_oracle():
         a_, b_ = tr.fp.ranges[name]
         _cmp(g_hip[a_:b_], g_ref[a_:b_], name, rel=0.12, cos=0.99)
     assert torch.isfinite(torch.as_tensor(float(stats["loss_total"])))
+
+
+@pytest.mark.parametrize("G,N,K,Nn", [(3, 40, 12, 40), (2, 1024, 12, 1120), (1, 6000, 12, 6000)])
+def test_rev_csr_matches_sorted_reference(G, N, K, Nn):
+    """Reverse CSR (incoming non-self edges per target node, sorted by edge id): the LDS-sorted
+    path (N*K <= 65536) and the global-memory path (larger graphs) against torch."""
+    gen = torch.Generator().manual_seed(G * N)
+    idx = torch.randint(0, Nn, (G, N, K), generator=gen, dtype=torch.int32)
+    idx[:, :, 0] = torch.arange(N, dtype=torch.int32)          # self at slot 0
+    idx = idx.to(DEV)
+    rptr = torch.zeros(G, Nn + 1, dtype=torch.int32, device=DEV)
+    red = torch.zeros(G, N * K, dtype=torch.int32, device=DEV)
+    native.rev_csr(idx, rptr, red, n_nodes=Nn)
+    torch.cuda.synchronize()
+    for g in range(G):
+        flat = idx[g].reshape(-1).long().cpu()
+        e = torch.arange(N * K)
+        keep = flat != e // K
+        tgt, eid = flat[keep], e[keep]
+        order = torch.argsort(tgt * (N * K) + eid)
+        counts = torch.bincount(tgt, minlength=Nn)
+        ptr_ref = torch.cat([torch.zeros(1, dtype=torch.long), torch.cumsum(counts, 0)])
+        assert torch.equal(rptr[g].long().cpu(), ptr_ref)
+        assert torch.equal(red[g, : int(ptr_ref[-1])].long().cpu(), eid[order])
