@@ -44,6 +44,8 @@ def main():
     ap.add_argument("--num_obstacles", type=int, default=0, help="static point-set obstacles per env")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp16"],
                     help="16-bit MFMA input type (fp16: dynamic loss scaling; BASELINE config #5)")
+    ap.add_argument("--graph", action="store_true",
+                    help="replay each iteration as captured HIP graphs (launch-bound small configs)")
     ap.add_argument("--phases", action="store_true",
                     help="after the timed loop, 2 extra steps with per-phase device-event timings")
     args = ap.parse_args()
@@ -62,7 +64,7 @@ def main():
     cfg = C.TrainConfig(num_agents=args.agents, num_envs=args.envs, inner_loops=args.inner_loops,
                         seed=args.seed, device="hip", early_stop=not args.no_early_stop,
                         display_steps=10 ** 9, save_steps=10 ** 9, dim=args.dim, num_obstacles=args.num_obstacles,
-                        dtype=args.dtype)
+                        dtype=args.dtype, graph=args.graph)
     tr = Trainer(cfg, device=dev, dp=dp)
 
     for _ in range(args.warmup):
@@ -113,6 +115,7 @@ def main():
         "mean_T": t_sum / (args.steps * world),
         "early_stop": not args.no_early_stop,
         "skipped_steps": tr.skipped_steps,
+        "graph": args.graph,
         "baseline": {"value": BASELINE_AGENT_STEPS_PER_S,
                      "source": "BASELINE.md: reference rollout-only loop @ N=1024, CPU x8 (upper bound of its "
                                "train loop, which does not run at N=1024)"},

@@ -121,6 +121,7 @@ struct CtrlNodeBwdArgs {
   int o_w1, o_w2, o_w3, o_w4;          // element offsets (strides 168/72/136/72)
   const float* wvec;                   // controller side vector (eb2|nb2|nb3|nb4)
   float act_coef, dt, sqrt3;
+  const float* act_scale;              // optional device scalar: coefficient = act_coef * (*act_scale)
   h16* dP;            long dp_env;    // (b,i,128) dL/dpooled out
   float4* ego;                         // (B,N) records: dL/ds_t from the node path + gain law + action loss
   float* partial;                      // (gridDim.x, CTRL_NODE_PARTIAL) slabs, accumulated

@@ -141,7 +141,7 @@ static int adam(u64 param, u64 grad, u64 m, u64 v, int lo, int hi, float b1, flo
 
 static int ctrl_node_bwd(u64 pooled, long p_env, u64 S, long s_env, u64 G, u64 A, long a_env, u64 Gn, long gn_env,
                          u64 valid, long v_env, int B, int N, u64 wrm, int o1, int o2, int o3, int o4, u64 wvec,
-                         float act_coef, float dt, float sqrt3, u64 dP, long dp_env, u64 ego, u64 partial,
+                         float act_coef, u64 act_scale, float dt, float sqrt3, u64 dP, long dp_env, u64 ego, u64 partial,
                          int dim, int num_blocks, int f16, u64 stream) {
   mb::CtrlNodeBwdArgs a{};
   a.dim = dim;
@@ -149,7 +149,7 @@ static int ctrl_node_bwd(u64 pooled, long p_env, u64 S, long s_env, u64 G, u64 A
   a.G = P<const float>(G); a.A = P<const float>(A); a.a_env = a_env; a.Gn = P<const float4>(Gn); a.gn_env = gn_env;
   a.valid = P<const uint8_t>(valid); a.v_env = v_env; a.B = B; a.N = N; a.wrm = P<const h16>(wrm);
   a.o_w1 = o1; a.o_w2 = o2; a.o_w3 = o3; a.o_w4 = o4; a.wvec = P<const float>(wvec);
-  a.act_coef = act_coef; a.dt = dt; a.sqrt3 = sqrt3; a.dP = P<h16>(dP); a.dp_env = dp_env;
+  a.act_coef = act_coef; a.act_scale = P<const float>(act_scale); a.dt = dt; a.sqrt3 = sqrt3; a.dP = P<h16>(dP); a.dp_env = dp_env;
   a.ego = P<float4>(ego); a.partial = P<float>(partial);
   return (f16 ? mb_ctrl_node_bwd_f16 : mb_ctrl_node_bwd)(&a, num_blocks, ST(stream));
 }

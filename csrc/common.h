@@ -118,10 +118,18 @@ DEV void split_h16(float x, h16& hi, h16& lo) {
 DEV void lds_wave_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
 // cooperative copy of `bytes` (multiple of 16) from global to LDS by the whole block
+// (4 independent 16-byte loads in flight per thread before the stores: the weight staging at
+// kernel start is latency-bound, which dominates small launches)
 DEV void block_copy16(void* dst, const void* src, int bytes) {
   const u32x4* s = reinterpret_cast<const u32x4*>(src);
   u32x4* d = reinterpret_cast<u32x4*>(dst);
-  for (int i = threadIdx.x; i < bytes / 16; i += blockDim.x) d[i] = s[i];
+  const int n = bytes / 16, bd = blockDim.x;
+  int i = threadIdx.x;
+  for (; i + 3 * bd < n; i += 4 * bd) {
+    const u32x4 v0 = s[i], v1 = s[i + bd], v2 = s[i + 2 * bd], v3 = s[i + 3 * bd];
+    d[i] = v0; d[i + bd] = v1; d[i + 2 * bd] = v2; d[i + 3 * bd] = v3;
+  }
+  for (; i < n; i += bd) d[i] = s[i];
 }
 
 DEV float wave_sum(float v) {

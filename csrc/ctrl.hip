@@ -529,10 +529,11 @@ __global__ __launch_bounds__(NB_WAVES * 64, 1) void ctrl_node_bwd_kernel(CtrlNod
       float da[D], ar[D];
 #pragma unroll
       for (int q = 0; q < D; ++q) { da[q] = a.dt * gnv[q]; ar[q] = -(ex[q] + a.sqrt3 * sv[q]); }
-      if (vld && a.act_coef != 0.f) {
+      const float act_coef = a.act_scale ? a.act_coef * *a.act_scale : a.act_coef;
+      if (vld && act_coef != 0.f) {
         const float diff = sqsum<D>(av) - sqsum<D>(ar);
         const float sg = diff > 0.f ? 1.f : (diff < 0.f ? -1.f : 0.f);
-        const float c = a.act_coef * sg;
+        const float c = act_coef * sg;
 #pragma unroll
         for (int q = 0; q < D; ++q) {
           da[q] += c * 2.f * av[q];

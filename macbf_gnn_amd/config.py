@@ -90,6 +90,8 @@ class TrainConfig:
     nan_guard: bool = True            # skip the optimizer step when the reduced gradient is not finite
     phase_timing: bool = False        # per-phase device-event timings in the step stats
     prefetch_data: bool = True        # HIP: sample iteration i+1 on a side stream during iteration i
+    graph: bool = False               # HIP: replay the iteration as captured HIP graphs (Tmax steps,
+                                      # done envs masked on the device) -- for launch-bound sizes
     dim: int = 2                      # spatial dimension of the double integrator (2: reference, 3)
     num_obstacles: int = 0            # static point-set obstacles per env (12 points each)
     obstacle_points: int = 12

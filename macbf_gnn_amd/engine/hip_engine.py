@@ -55,6 +55,15 @@ class HipEngine:
             s, d = fn(offs, self.D)
             self.maps[name] = (mk(s), mk(d))
         self._alloc()
+        # whole-iteration HIP graph (cfg.graph): rollout to Tmax with device-side done masks,
+        # losses, backward; replayed per iteration (removes the per-kernel launch / Python cost
+        # that dominates small configurations). Sampling, the DP all-reduces and the optimizer
+        # stay eager around the two captured graphs.
+        self.graph_mode = bool(getattr(cfg, "graph", False))
+        if self.graph_mode and cfg.add_noise_prob > 0:
+            raise ValueError("graph mode does not support exploration noise (host-side RNG)")
+        self._graphs = None
+        self._graph_gs = None
 
     # ------------------------------------------------------------------ buffers
     def _alloc(self):
@@ -84,6 +93,7 @@ class HipEngine:
         self.ego = torch.zeros(B, N, W, dtype=f32, device=dev)
         self.dEc = torch.zeros(B, N, K, W, dtype=f32, device=dev)
         self.counts = torch.zeros(3, dtype=f32, device=dev)
+        self.act_scale = torch.zeros(1, dtype=f32, device=dev)      # action-loss coefficient
         self.nb_node, self.nb_edge = native.ctrl_bwd_grids(B * N, dev)
         self.part_node = torch.zeros(self.nb_node, native.CTRL_NODE_PARTIAL, dtype=f32, device=dev)
         self.part_edge = torch.zeros(self.nb_edge, native.CTRL_EDGE_PARTIAL, dtype=f32, device=dev)
@@ -100,10 +110,9 @@ class HipEngine:
         self.pw.update()
 
     # ------------------------------------------------------------------ rollout
-    def rollout(self, s0, g, obs=None):
-        cfg = self.tr.cfg
-        B, N, K, D = self.B, self.N, self.K, self.D
-        pw = self.pw
+    def load_inputs(self, s0, g, obs=None):
+        """Scenario -> the static input buffers (start records, goals, obstacle rows)."""
+        B, N, D = self.B, self.N, self.D
         self.S[0, :, :N].copy_(native.to_records(s0))
         if self.M:
             if obs is None or tuple(obs.shape) != (B, self.M, D):
@@ -112,6 +121,17 @@ class HipEngine:
             ob = native.to_records(torch.cat([obs.float(), torch.zeros_like(obs, dtype=torch.float32)], -1))
             self.S[:, :, N:].copy_(ob.unsqueeze(0).expand(self.Tmax + 1, B, self.M, self.W))
         self.G.copy_(g)
+
+    def rollout(self, s0, g, obs=None, early_stop=None):
+        self.load_inputs(s0, g, obs)
+        return self._rollout_steps(self.tr.cfg.early_stop if early_stop is None else early_stop)
+
+    def _rollout_steps(self, early_stop):
+        """Rollout from the loaded inputs. early_stop=False: all Tmax steps, no host round trip
+        (done envs are masked by the validity mask; used by the captured graph)."""
+        cfg = self.tr.cfg
+        B, N, K, D = self.B, self.N, self.K, self.D
+        pw = self.pw
         self.cnt.zero_()
         self.safe.zero_()
         self.dist.zero_()
@@ -129,7 +149,7 @@ class HipEngine:
             native.ctrl_fwd(self.S[t], self.G, self.idx[t], pw.ctrl_w, pw.ctrl_off["ew1f"], pw.ctrl_off["nw1f"],
                             pw.ctrl_v, self.A[t], self.S[t + 1], self.dist[t], self.act[t], noise=noise,
                             pooled=self.pooled[t], argmax=self.argmax[t])
-            if cfg.early_stop:
+            if early_stop:
                 self.host_dist[t].copy_(self.dist[t], non_blocking=True)
                 ev = torch.cuda.Event()
                 ev.record()
@@ -153,28 +173,78 @@ class HipEngine:
 
     # ------------------------------------------------------------------ step
     def step(self, s0, g, obs=None):
-        tr = self.tr
-        cfg = tr.cfg
-        B, N, K, W, Nn = self.B, self.N, self.K, self.W, self.Nn
-        pw = self.pw
-        tm = tr.timer
+        if self.graph_mode:
+            return self._step_graph(s0, g, obs)
+        tm = self.tr.timer
         T = self.rollout(s0, g, obs)
         tm.mark("rollout")
-        # loss scale of the upstream gradients (fp16: dynamic, trainer-owned; bf16: 1). Every
-        # backward quantity is linear in it; the flat gradient is unscaled after the slab reduce.
-        gs = float(tr.grad_scale)
+        valid = self._counts(T)
+        self.tr.dp.all_reduce_(self.counts)
+        tm.mark("counts")
+        return self._backward(T, valid)
+
+    # ------------------------------------------------------------------ graph mode
+    def _step_graph(self, s0, g, obs):
+        self.load_inputs(s0, g, obs)
+        gs = float(self.tr.grad_scale)
+        if self._graphs is None or self._graph_gs != gs:     # (re)capture; fp16 scale is baked in
+            self._capture()
+            self._graph_gs = gs
+        self._graphs[0].replay()
+        self.tr.dp.all_reduce_(self.counts)
+        self._graphs[1].replay()
+        return self._graph_stats
+
+    def _capture(self):
+        T = self.Tmax
+        tm = self.tr.timer
+        en, tm.enabled = tm.enabled, False
+        try:
+            cur = torch.cuda.current_stream(self.dev)
+            side = torch.cuda.Stream(device=self.dev)
+            side.wait_stream(cur)
+            with torch.cuda.stream(side):            # warm-up: lazy buffers, code objects
+                self._rollout_steps(False)
+                v = self._counts(T)
+                self._backward(T, v)
+            cur.wait_stream(side)
+            pool = torch.cuda.graph_pool_handle()
+            ga, gb = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+            with torch.cuda.graph(ga, pool=pool):
+                self._rollout_steps(False)
+                self._graph_valid = self._counts(T)
+            with torch.cuda.graph(gb, pool=pool):
+                self._graph_stats = self._backward(T, self._graph_valid)
+            self._graphs = (ga, gb)
+        finally:
+            tm.enabled = en
+
+    def _counts(self, T):
+        """Validity mask (T, B) and the pooled counts [n_dang, n_safe, n_act] of this rank."""
+        N = self.N
         # validity: step t of env b counts iff the env was not done before t
         done = (self.dist[:T] / N) < C.DIST_MIN_CHECK                 # (T, B)
         di = done.to(torch.int32)
         valid = ((torch.cumsum(di, 0) - di) == 0)
-        valid_u8 = valid.to(torch.uint8).contiguous()
         vf = valid.to(torch.float32)
-        # pooled counts (global over DP ranks)
         self.counts[0] = (self.cnt[:T, :, 0] * vf).sum()
         self.counts[1] = (self.cnt[:T, :, 1] * vf).sum()
         self.counts[2] = vf.sum() * N
-        tr.dp.all_reduce_(self.counts)
+        return valid
+
+    def _backward(self, T, valid):
+        tr = self.tr
+        B, N, K, W, Nn = self.B, self.N, self.K, self.W, self.Nn
+        pw = self.pw
+        tm = tr.timer
+        # loss scale of the upstream gradients (fp16: dynamic, trainer-owned; bf16: 1). Every
+        # backward quantity is linear in it; the flat gradient is unscaled after the slab reduce.
+        gs = float(tr.grad_scale)
+        valid_u8 = valid.to(torch.uint8).contiguous()
+        vf = valid.to(torch.float32)
         n_act = self.counts[2].clamp_min(1.0)
+        # action-loss coefficient stays on the device (read by ctrl_node_bwd): no host sync
+        torch.div(C.LOSS_SCALE * C.LOSS_WEIGHTS[4], n_act.view(1), out=self.act_scale)
         E = T * B * N * K
         # ---- reverse CSR of the step graphs (needs only idx): on the aux stream, concurrent with
         #      the CBF kernel below
@@ -189,7 +259,6 @@ class HipEngine:
         # ---- CBF: h, h', hinge losses, upstream grads and the full backward in ONE kernel
         S = self.S[: T + 1]
         idx = self.idx[:T]
-        tm.mark("counts")
         nbb = native.cbf_bwd_grid(2 * E, self.dev)
         part_cbf = self._buf(self._part_cbf, nbb, native.CBF_PARTIAL)
         dE = self.dE[: 2 * E * W].view(2, T, B, N, K, W)
@@ -206,8 +275,6 @@ class HipEngine:
         # ---- controller backward
         self.part_node.zero_()
         self.part_edge.zero_()
-        act_coef = (C.LOSS_SCALE * C.LOSS_WEIGHTS[4]) / n_act
-        act_coef_f = float(act_coef) * gs   # one host read per step (counts already reduced)
         if self.bptt:
             # BPTT through the rollout: G_t = dL/ds_t, reverse time
             self.Gb[T].copy_(self.dS[T])
@@ -215,8 +282,8 @@ class HipEngine:
             redges3 = redges[: T * B].view(T, B, N * K)
             for t in range(T - 1, -1, -1):
                 native.ctrl_node_bwd(self.pooled[t], self.S[t], self.G, self.A[t], self.Gb[t + 1], valid_u8[t],
-                                     pw.ctrl_rm, pw.node_rm_off, pw.ctrl_v, act_coef_f, self.dP, self.ego,
-                                     self.part_node, self.nb_node)
+                                     pw.ctrl_rm, pw.node_rm_off, pw.ctrl_v, gs, self.dP, self.ego,
+                                     self.part_node, self.nb_node, act_scale=self.act_scale)
                 native.ctrl_edge_bwd(self.S[t], self.idx[t], self.argmax[t], self.dP, pw.ctrl_w, pw.ctrl_off["ew1f"],
                                      pw.ctrl_off["ew2tn"], self.dEc, self.part_edge, self.nb_edge)
                 native.node_combine(self.dS[t], self.ego, self.dEc, rptr3[t], redges3[t], self.Gb[t + 1],
@@ -234,7 +301,8 @@ class HipEngine:
             pe.zero_()
             native.ctrl_node_bwd(self.pooled[:T].view(TB, N, 128), self.S[:T].view(TB, Nn, W), Gr[:TB],
                                  self.A[:T].view(TB, N, D), self.dS[1: T + 1].view(TB, N, W), valid_u8.view(TB),
-                                 pw.ctrl_rm, pw.node_rm_off, pw.ctrl_v, act_coef_f, dP[:TB], None, pn, nb_n)
+                                 pw.ctrl_rm, pw.node_rm_off, pw.ctrl_v, gs, dP[:TB], None, pn, nb_n,
+                                 act_scale=self.act_scale)
             native.ctrl_edge_bwd(self.S[:T].view(TB, Nn, W), self.idx[:T].view(TB, N, K), self.argmax[:T].view(TB, N, 128),
                                  dP[:TB], pw.ctrl_w, pw.ctrl_off["ew1f"], pw.ctrl_off["ew2tn"], None, pe, nb_e)
             self._nb_parts = (pn, pe)
@@ -266,7 +334,8 @@ class HipEngine:
             "loss_safe_deriv": lsd, "loss_action": la,
             "acc_dang_sum": sums[4], "acc_safe_sum": sums[5], "acc_dang_deriv_sum": sums[8],
             "acc_safe_deriv_sum": sums[9], "n_dang": self.counts[0], "n_safe": self.counts[1],
-            "agent_steps": vf.sum() * N, "safe_agents": (safe_next * vf).sum(), "T": T,
+            "agent_steps": vf.sum() * N, "safe_agents": (safe_next * vf).sum(),
+            "T": T if not self.graph_mode else valid.any(1).sum().to(torch.float64),
         }
 
     def _buf(self, cache, key, cols):

@@ -425,7 +425,10 @@ def ctrl_bwd_grids(total_agents: int, device):
     return max(1, min(ch, cu)), max(1, min(ch, 2 * cu))
 
 
-def ctrl_node_bwd(pooled, S, G, A, Gn, valid_t, wrm, offs, wvec, act_coef, dP, ego, partial, num_blocks):
+def ctrl_node_bwd(pooled, S, G, A, Gn, valid_t, wrm, offs, wvec, act_coef, dP, ego, partial, num_blocks,
+                  act_scale=None):
+    """act_scale: optional 1-element device tensor; the action-loss coefficient is then
+    act_coef * act_scale[0], read by the kernel (no host round trip)."""
     B, N = G.shape[:2]
     D = dim_of(S)
     W = rec_width(D)
@@ -442,11 +445,12 @@ def ctrl_node_bwd(pooled, S, G, A, Gn, valid_t, wrm, offs, wvec, act_coef, dP, e
     _same_half(pooled, wrm, "pooled")
     check(ego, torch.float32, (B, N, W), "ego")
     check(partial, torch.float32, (num_blocks, CTRL_NODE_PARTIAL), "partial")
+    check(act_scale, torch.float32, (1,), "act_scale")
     rc = lib().ctrl_node_bwd(ptr(pooled), pooled.stride(0), ptr(S), S.stride(0) // W, ptr(G), ptr(A), A.stride(0) // D,
                              ptr(Gn), Gn.stride(0) // W if Gn is not None else 0,
                              ptr(valid_t), valid_t.stride(0) if valid_t is not None else 0, B, N,
                              ptr(wrm), offs["w1"], offs["w2"], offs["w3"], offs["w4"], ptr(wvec),
-                             float(act_coef), float(C.TIME_STEP), float(C.SQRT3), ptr(dP), dP.stride(0),
+                             float(act_coef), ptr(act_scale), float(C.TIME_STEP), float(C.SQRT3), ptr(dP), dP.stride(0),
                              ptr(ego), ptr(partial), D, int(num_blocks), f16, stream_handle())
     _ok(rc, "ctrl_node_bwd")
 

@@ -38,6 +38,8 @@ def parse_args(argv=None):
     p.add_argument("--noise_prob", type=float, default=None)
     p.add_argument("--dim", type=int, default=2, choices=[2, 3], help="spatial dimension of the double integrator")
     p.add_argument("--num_obstacles", type=int, default=0, help="static point-set obstacles per env")
+    p.add_argument("--graph", action="store_true",
+                   help="HIP: replay each iteration as captured graphs (launch-bound small configs)")
     return p.parse_args(argv)
 
 
@@ -48,7 +50,7 @@ def build_config(args):
                         reuse_nbr_idx=not args.no_reuse_nbr_idx,
                         alternate_every=args.alternate_every, early_stop=not args.no_early_stop,
                         model_path=args.model_path, log_path=args.log_path, dim=args.dim,
-                        num_obstacles=args.num_obstacles)
+                        num_obstacles=args.num_obstacles, graph=args.graph)
     for name in ("train_steps", "inner_loops", "top_k", "lr", "display_steps", "save_steps"):
         v = getattr(args, name)
         if v is not None:
