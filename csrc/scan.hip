@@ -110,14 +110,17 @@ __global__ __launch_bounds__(SORT_BLOCK) void cell_sort_kernel(CellSortArgs a) {
   }
 }
 
-constexpr int SCAN_BLOCK = 256;      // 4 waves x 32 agents (consecutive on the curve), 2 lanes each
-constexpr int SCAN_AG = SCAN_BLOCK / 2;  // agents (curve positions) per block
+// Block = BS/64 waves x 32 agents (consecutive on the curve), 2 lanes each. BS = 256 for envs
+// up to 2048 nodes; 512 above (the whole env is staged per block: bigger blocks amortise it and
+// keep one 8-wave block per CU at the 128 KiB staging size of a 4096-node env).
 constexpr int SCAN_MAXN = 4096;      // whole env staged in LDS
 constexpr int SCH = 8;               // candidates per chunk (one bounding box each)
+constexpr int SSC = 8;               // chunks per superchunk (second culling level)
 
 static inline size_t scan_lds_bytes(int Nn) {
   const int Np = (Nn + SCH - 1) / SCH * SCH;
-  return (size_t)Np * 32 + (size_t)(Np / SCH) * 32;
+  const int nch = Np / SCH, nsc = (nch + SSC - 1) / SSC;
+  return (size_t)Np * 32 + (size_t)nch * 32 + (size_t)nsc * 32;
 }
 
 // (d2, index) packed into one 64-bit key: d2 >= 0, so its IEEE bits order like the values and
@@ -146,21 +149,24 @@ DEV float wave_min(float v) { return -wave_max(-v); }
 // r + ttc*(vmax_wave + vmax_chunk) (x1.01 + 1e-4 margin). Both decisions are wave-uniform
 // branches; after the local neighbourhood has filled the lists almost every far chunk costs
 // one box test instead of 8 pair evaluations. Obstacle nodes are candidates, never centres.
-template <int K, int D>
-__global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanArgs a) {
+template <int K, int D, int BS>
+__global__ __launch_bounds__(BS) void scan_kernel(ScanArgs a) {
+  constexpr int SCAN_AG = BS / 2;                              // agents (curve positions) per block
   extern __shared__ float4 smem4[];
   const int N = a.N, Nn = a.Nn;
   const int Np = (Nn + SCH - 1) / SCH * SCH;
-  const int nch = Np / SCH;
+  const int nch = Np / SCH, nsc = (nch + SSC - 1) / SSC;
   float4* tp = smem4;                                          // [Np] x, y, z, node id (bits)
   float4* tv = tp + Np;                                        // [Np] vx, vy, vz, |v|
   float4* cbl = tv + Np;                                       // [nch] min x, y, z, max |v|
   float4* cbh = cbl + nch;                                     // [nch] max x, y, z
-  __shared__ float red[3][SCAN_BLOCK / WAVE];
+  float4* sbl = cbh + nch;                                     // [nsc] superchunk boxes
+  float4* sbh = sbl + nsc;
+  __shared__ float red[3][BS / WAVE];
   const int b = blockIdx.y;
   const float4* Sb = a.S + (long)b * a.s_env * REC<D>;
   const int* perm = a.perm + (long)b * Nn;
-  for (int q = threadIdx.x; q < Np; q += SCAN_BLOCK) {
+  for (int q = threadIdx.x; q < Np; q += BS) {
     if (q < Nn) {
       const int id = perm[q];
       float p[D], v[D];
@@ -175,7 +181,7 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanArgs a) {
     }
   }
   __syncthreads();
-  for (int c = threadIdx.x; c < nch; c += SCAN_BLOCK) {
+  for (int c = threadIdx.x; c < nch; c += BS) {
     float4 lo = make_float4(INFINITY, INFINITY, INFINITY, 0.f);
     float4 hi = make_float4(-INFINITY, -INFINITY, -INFINITY, 0.f);
 #pragma unroll
@@ -190,6 +196,18 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanArgs a) {
     }
     cbl[c] = lo;
     cbh[c] = hi;
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < nsc; c += BS) {
+    float4 lo = make_float4(INFINITY, INFINITY, INFINITY, 0.f);
+    float4 hi = make_float4(-INFINITY, -INFINITY, -INFINITY, 0.f);
+    for (int u = c * SSC; u < min(c * SSC + SSC, nch); ++u) {
+      const float4 l = cbl[u], q = cbh[u];
+      lo.x = fminf(lo.x, l.x); lo.y = fminf(lo.y, l.y); lo.z = fminf(lo.z, l.z); lo.w = fmaxf(lo.w, l.w);
+      hi.x = fmaxf(hi.x, q.x); hi.y = fmaxf(hi.y, q.y); hi.z = fmaxf(hi.z, q.z);
+    }
+    sbl[c] = lo;
+    sbh[c] = hi;
   }
   __syncthreads();
   // Two lanes per agent: lane (r, h) owns curve position base + r and scans candidate slots
@@ -226,20 +244,8 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanArgs a) {
   float thr = INFINITY;                 // bound on every agent's final K-th distance in this wave
   bool all_danger = false;
   if (wave_live) {
-    // chunk metadata is read one step ahead of the (deterministic) walk to hide LDS latency
-    int ch = cc0;
-    float4 bl = cbl[ch], bh = cbh[ch];
-    for (int m = 0; m < nch; ++m) {
-      const int cur = ch;
-      const float4 cl = bl, chh = bh;
-      {
-        const int k = (m + 2) >> 1;
-        int nx = ((m + 1) & 1) ? cc0 - k : cc0 + k;
-        if (nx >= nch) nx -= nch;
-        if (nx < 0) nx += nch;
-        ch = nx;
-        if (m + 1 < nch) { bl = cbl[ch]; bh = cbh[ch]; }
-      }
+    // gap^2 (x0.999) between this wave's box and a chunk / superchunk box
+    auto gap2 = [&](const float4& cl, const float4& chh) {
       const float gx = fmaxf(0.f, fmaxf(cl.x - wmaxx, wminx - chh.x));
       const float gy = fmaxf(0.f, fmaxf(cl.y - wmaxy, wminy - chh.y));
       float bd2 = gx * gx + gy * gy;
@@ -247,49 +253,71 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanArgs a) {
         const float gz = fmaxf(0.f, fmaxf(cl.z - wmaxz, wminz - chh.z));
         bd2 = bd2 + gz * gz;
       }
-      bd2 = bd2 * 0.999f;
-      const bool nk = a.do_knn && !(bd2 > thr);
-      const float lb = 1.01f * (rc + a.ttc_check * (wvmax + cl.w)) + 1e-4f;
-      const bool ns = a.do_safety && !all_danger && !(bd2 > lb * lb);
-      if (!nk && !ns) continue;
-      constexpr int HU = SCH / 2;
-      const int hoff = HU * h;
-      float4 c[HU];
+      return bd2 * 0.999f;
+    };
+    // superchunks outward from the wave's own (sc0, sc0-1, sc0+1, ...: every one exactly once),
+    // chunks of a surviving superchunk in order; both culling levels are wave-uniform
+    const int sc0 = cc0 / SSC;
+    for (int m = 0; m < nsc; ++m) {
+      const int k = (m + 1) >> 1;
+      int sc = (m & 1) ? sc0 - k : sc0 + k;
+      if (sc >= nsc) sc -= nsc;
+      if (sc < 0) sc += nsc;
+      {
+        const float4 sl = sbl[sc], sh = sbh[sc];
+        const float sd2 = gap2(sl, sh);
+        const float slb = 1.01f * (rc + a.ttc_check * (wvmax + sl.w)) + 1e-4f;
+        const bool snk = a.do_knn && !(sd2 > thr);
+        const bool sns = a.do_safety && !all_danger && !(sd2 > slb * slb);
+        if (!snk && !sns) continue;
+      }
+      const int c_end = min(sc * SSC + SSC, nch);
+      for (int cur = sc * SSC; cur < c_end; ++cur) {
+        const float4 cl = cbl[cur], chh = cbh[cur];
+        const float bd2 = gap2(cl, chh);
+        const bool nk = a.do_knn && !(bd2 > thr);
+        const float lb = 1.01f * (rc + a.ttc_check * (wvmax + cl.w)) + 1e-4f;
+        const bool ns = a.do_safety && !all_danger && !(bd2 > lb * lb);
+        if (!nk && !ns) continue;
+        constexpr int HU = SCH / 2;
+        const int hoff = HU * h;
+        float4 c[HU];
 #pragma unroll
-      for (int u = 0; u < HU; ++u) c[u] = tp[cur * SCH + hoff + u];
+        for (int u = 0; u < HU; ++u) c[u] = tp[cur * SCH + hoff + u];
 #pragma unroll
-      for (int u = 0; u < HU; ++u) {
-        const int j = __float_as_int(c[u].w);
-        float dp[D];
-        dp[0] = me.x - c[u].x;
-        dp[1] = me.y - c[u].y;
-        if constexpr (D == 3) dp[2] = me.z - c[u].z;
-        const float d2 = sqsum<D>(dp);
-        const uint64_t key = knn_key(d2, (unsigned)j);
-        if (nk && act && key < bk[K - 1]) topk_insert<K>(bk, key);
-        if (ns && act && !danger) {
-          const float4 cv = tv[cur * SCH + hoff + u];
-          const float lim = 1.01f * (base_i + a.ttc_check * cv.w) + 1e-4f;
-          if (d2 < lim * lim && j != i) {
-            float dv[D];
-            dv[0] = mv.x - cv.x;
-            dv[1] = mv.y - cv.y;
-            if constexpr (D == 3) dv[2] = mv.z - cv.z;
-            danger = ttc_danger<D>(dp, dv, a.r2_check, a.ttc_check);
+        for (int u = 0; u < HU; ++u) {
+          const int j = __float_as_int(c[u].w);
+          float dp[D];
+          dp[0] = me.x - c[u].x;
+          dp[1] = me.y - c[u].y;
+          if constexpr (D == 3) dp[2] = me.z - c[u].z;
+          const float d2 = sqsum<D>(dp);
+          const uint64_t key = knn_key(d2, (unsigned)j);
+          if (nk && act && key < bk[K - 1]) topk_insert<K>(bk, key);
+          if (ns && act && !danger) {
+            const float4 cv = tv[cur * SCH + hoff + u];
+            const float lim = 1.01f * (base_i + a.ttc_check * cv.w) + 1e-4f;
+            if (d2 < lim * lim && j != i) {
+              float dv[D];
+              dv[0] = mv.x - cv.x;
+              dv[1] = mv.y - cv.y;
+              if constexpr (D == 3) dv[2] = mv.z - cv.z;
+              danger = ttc_danger<D>(dp, dv, a.r2_check, a.ttc_check);
+            }
           }
         }
-      }
-      if (nk) {
-        // the merged list's K-th distance <= min of the two half-lists' K-th distances
-        const float own = __uint_as_float((unsigned)(bk[K - 1] >> 32));
-        const float kth = fminf(own, shfl_xor32(own));
-        thr = wave_max(act ? kth : -INFINITY);
-      }
-      if (ns) {
-        // the lane swap must run on every lane: never inside a short-circuit '||'
-        const int pdg = shfl_xor32i(danger ? 1 : 0);
-        const bool dboth = danger || (pdg != 0);
-        all_danger = !__any(act && !dboth);
+        if (nk) {
+          // the merged list's K-th distance <= min of the two half-lists' K-th distances
+          const float own = __uint_as_float((unsigned)(bk[K - 1] >> 32));
+          const float kth = fminf(own, shfl_xor32(own));
+          thr = wave_max(act ? kth : -INFINITY);
+        }
+        if (ns) {
+          // the lane swap must run on every lane: never inside a short-circuit '||'
+          const int pdg = shfl_xor32i(danger ? 1 : 0);
+          const bool dboth = danger || (pdg != 0);
+          all_danger = !__any(act && !dboth);
+        }
       }
     }
   }
@@ -334,7 +362,7 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanArgs a) {
   __syncthreads();
   if (threadIdx.x == 0) {
     float s0 = 0.f, s1 = 0.f, s2 = 0.f;
-    for (int q = 0; q < SCAN_BLOCK / WAVE; ++q) { s0 += red[0][q]; s1 += red[1][q]; s2 += red[2][q]; }
+    for (int q = 0; q < BS / WAVE; ++q) { s0 += red[0][q]; s1 += red[1][q]; s2 += red[2][q]; }
     if (a.do_knn && a.cnt) {
       atomicAdd(a.cnt + (long)b * a.c_env + 0, s0);
       atomicAdd(a.cnt + (long)b * a.c_env + 1, s1);
@@ -343,12 +371,18 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_kernel(ScanArgs a) {
   }
 }
 
+template <int K, int D, int BS>
+static void launch_kdb(const ScanArgs& a, hipStream_t st) {
+  dim3 grid((a.Nn + BS / 2 - 1) / (BS / 2), a.B);
+  const size_t lds = scan_lds_bytes(a.Nn);
+  (void)hipFuncSetAttribute((const void*)scan_kernel<K, D, BS>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipLaunchKernelGGL((scan_kernel<K, D, BS>), grid, dim3(BS), lds, st, a);
+}
+
 template <int K, int D>
 static void launch_kd(const ScanArgs& a, hipStream_t st) {
-  dim3 grid((a.Nn + SCAN_AG - 1) / SCAN_AG, a.B);
-  const size_t lds = scan_lds_bytes(a.Nn);
-  (void)hipFuncSetAttribute((const void*)scan_kernel<K, D>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL((scan_kernel<K, D>), grid, dim3(SCAN_BLOCK), lds, st, a);
+  if (a.Nn > 2048) launch_kdb<K, D, 512>(a, st);
+  else launch_kdb<K, D, 256>(a, st);
 }
 
 template <int K>
