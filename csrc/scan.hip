@@ -111,7 +111,7 @@ __global__ __launch_bounds__(SORT_BLOCK) void cell_sort_kernel(CellSortArgs a) {
 }
 
 // Block = BS/64 waves x 32 agents (consecutive on the curve), 2 lanes each. BS = 256 for envs
-// up to 2048 nodes; 512 above (the whole env is staged per block: bigger blocks amortise it and
+// up to 512 nodes; 512 above (the whole env is staged per block: bigger blocks amortise it and
 // keep one 8-wave block per CU at the 128 KiB staging size of a 4096-node env).
 constexpr int SCAN_MAXN = 4096;      // whole env staged in LDS
 constexpr int SCH = 8;               // candidates per chunk (one bounding box each)
@@ -381,7 +381,7 @@ static void launch_kdb(const ScanArgs& a, hipStream_t st) {
 
 template <int K, int D>
 static void launch_kd(const ScanArgs& a, hipStream_t st) {
-  if (a.Nn > 2048) launch_kdb<K, D, 512>(a, st);
+  if (a.Nn > 512) launch_kdb<K, D, 512>(a, st);
   else launch_kdb<K, D, 256>(a, st);
 }
 
