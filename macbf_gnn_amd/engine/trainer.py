@@ -171,7 +171,9 @@ class Trainer:
         return stats
 
     def fit(self, steps: Optional[int] = None, progress: bool = False):
-        steps = self.cfg.train_steps if steps is None else steps
+        """Train ``steps`` iterations; by default up to ``cfg.train_steps`` in total, so a run
+        resumed from a checkpoint continues where it stopped (TRAIN_STEPS, train.py:48)."""
+        steps = max(0, self.cfg.train_steps - self.step_count) if steps is None else steps
         it = range(steps)
         if progress and self.dp.rank == 0:
             try:
@@ -188,6 +190,9 @@ class Trainer:
             if self.cfg.model_path and (self.step_count % max(self.cfg.save_steps, 1)) == 0:
                 ckpt.save(self, self.cfg.model_path)
                 self.dp.barrier()
+        if self.cfg.model_path and steps > 0 and (self.step_count % max(self.cfg.save_steps, 1)) != 0:
+            ckpt.save(self, self.cfg.model_path)      # final state of the run
+            self.dp.barrier()
         return last
 
     def save(self, path):

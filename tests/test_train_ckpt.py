@@ -128,3 +128,22 @@ def test_phase_timing_reports_phases():
     ph = st["phases_ms"]
     for k in ("sample", "rollout", "losses", "backward", "allreduce", "optimizer"):
         assert k in ph and ph[k] >= 0.0
+
+
+def test_fit_resume_runs_to_total_train_steps(tmp_path):
+    """train_steps is the total: a resumed run continues to it; the final state is saved."""
+    from macbf_gnn_amd.engine import Trainer
+    from macbf_gnn_amd.parallel import DP
+    path = str(tmp_path / "ck.pt")
+    mk = lambda steps: Trainer(C.TrainConfig(num_agents=8, num_envs=1, inner_loops=3, device="cpu", seed=1,
+                                             train_steps=steps, save_steps=100, display_steps=100,
+                                             model_path=path), device=torch.device("cpu"),
+                               dp=DP(device=torch.device("cpu")))
+    t = mk(3)
+    t.fit()
+    assert t.step_count == 3
+    t2 = mk(5)
+    assert t2.step_count == 3
+    t2.fit()
+    assert t2.step_count == 5
+    assert mk(5).step_count == 5
