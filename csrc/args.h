@@ -82,6 +82,14 @@ struct CbfFwdArgs {
   float* partial;                          // (gridDim.x, 10) or null
   LossConsts lc;
   float obs_r, dist_thr, dist_eps;
+  // deduplicated evaluation list (src != null; see dedup.hip): evaluation u < *nev, u < E is the
+  // main slot u on s_t, u >= E an extra evaluation of slot src[u] on s_{t+1} (neighbour from
+  // idx1); h_out[u] = masked h, mask_out[u] = radius mask
+  const int* src;
+  const int* nev;
+  const int* idx1;
+  uint8_t* mask_out;
+  const h16* wrm;                          // row-major W2 | W3 images (dedup forward)
 };
 
 struct CbfBwdArgs {
@@ -106,6 +114,37 @@ struct CbfBwdArgs {
   const uint8_t* valid;                    // (T,B) or null
   const float* counts;                     // [n_dang, n_safe] global
   LossConsts lc;
+  // deduplicated evaluation list (non-fused; src != null): evaluations u < *nev addressed as in
+  // CbfFwdArgs, dh / dE indexed by u
+  const int* src;
+  const int* nev;
+};
+
+// Deduplication of the h / h' evaluations (dedup.hip). h'(s_{t+1}) of slot (t,b,i,k) is the
+// same function value as h(s_{t+1}) of the slot (t+1,b,i,k') with the same neighbour, so only
+// the unmatched pairs ("extras") need their own evaluation.
+struct CbfMatchArgs {
+  const int* idx;        // (T+G1, B, N, K) neighbour slots (G1 = 1: h' on the recomputed kNN)
+  int T, B, N, K;
+  int mode;              // 0: reuse_nbr_idx (match by neighbour id), 1: recomputed kNN (slot k <-> k)
+  int phase;             // 0: count extras per row, 1: write map1 / src
+  int* cnt;              // (T*B*N) extras per (t,b,i) row (phase 0 out)
+  const int* off;        // (T*B*N) exclusive offsets (phase 1 in)
+  int* map1;             // (E) evaluation index of the h' partner of main slot e
+  int* src;              // (2E) source slot whose h' is evaluation u, or -1
+};
+
+struct CbfDhArgs {
+  const float* h;        // (U) masked h per evaluation
+  const uint8_t* hmask;  // (U) radius mask per evaluation
+  const int* map1; const int* src; const int* nev;
+  const uint8_t* dang;   // (T,B,N,K)
+  const uint8_t* valid;  // (T,B) or null
+  int B, T, N, K;
+  const float* counts;   // [n_dang, n_safe] global
+  LossConsts lc;
+  float* dh;             // (U) upstream gradient per evaluation
+  float* partial;        // (gridDim.x, 12) loss partial sums (slots 0..9 as CBF P_LOSS)
 };
 
 struct CtrlNodeBwdArgs {
@@ -156,6 +195,7 @@ struct NodeRedArgs {
   int Nn;              // CSR target nodes per graph (0 = N)
   int dim;
   int shift1;          // pass 1 edges belong to graph t + shift1 (1: h' on recomputed kNN of s_{t+1})
+  const int* map1;     // dedup: pass-1 slot e -> evaluation index (only >= E = extras are read)
 };
 
 struct CombineArgs {
@@ -187,6 +227,8 @@ int mb_ctrl_fwd(const mb::CtrlArgs* a, int num_cu, hipStream_t st);
 int mb_ctrl_fwd_f16(const mb::CtrlArgs* a, int num_cu, hipStream_t st);
 int mb_cbf_fwd(const mb::CbfFwdArgs* a, int num_blocks, hipStream_t st);
 int mb_cbf_fwd_f16(const mb::CbfFwdArgs* a, int num_blocks, hipStream_t st);
+int mb_cbf_hfwd(const mb::CbfFwdArgs* a, int num_blocks, hipStream_t st);
+int mb_cbf_hfwd_f16(const mb::CbfFwdArgs* a, int num_blocks, hipStream_t st);
 int mb_cbf_bwd(const mb::CbfBwdArgs* a, int num_blocks, hipStream_t st);
 int mb_cbf_bwd_f16(const mb::CbfBwdArgs* a, int num_blocks, hipStream_t st);
 int mb_ctrl_node_bwd(const mb::CtrlNodeBwdArgs* a, int num_blocks, hipStream_t st);
@@ -194,6 +236,8 @@ int mb_ctrl_node_bwd_f16(const mb::CtrlNodeBwdArgs* a, int num_blocks, hipStream
 int mb_ctrl_edge_bwd(const mb::CtrlEdgeBwdArgs* a, int num_blocks, hipStream_t st);
 int mb_ctrl_edge_bwd_f16(const mb::CtrlEdgeBwdArgs* a, int num_blocks, hipStream_t st);
 int mb_rev_csr(const mb::CsrArgs* a, hipStream_t st);
+int mb_cbf_match(const mb::CbfMatchArgs* a, hipStream_t st);
+int mb_cbf_dh(const mb::CbfDhArgs* a, int num_blocks, hipStream_t st);
 int mb_node_reduce(const mb::NodeRedArgs* a, hipStream_t st);
 int mb_node_combine(const mb::CombineArgs* a, hipStream_t st);
 int mb_reduce_rows(const float* partial, int rows, int cols, float* out, int accumulate, hipStream_t st);

@@ -79,12 +79,27 @@ static int cbf_fwd(u64 S, long s_env, long s_step, u64 idx, u64 dang, u64 valid,
   return (f16 ? mb_cbf_fwd_f16 : mb_cbf_fwd)(&a, num_blocks, ST(stream));
 }
 
+static int cbf_hfwd(u64 S, long s_env, long s_step, u64 idx, u64 idx1, u64 src, u64 nev, int B, int T, int N, int K,
+                    u64 wpack, int f_fwd, u64 wrm, u64 wvec, u64 h_out, u64 mask_out, float obs_r, float dist_thr,
+                    float dist_eps, int dim, int num_blocks, int f16, u64 stream) {
+  mb::CbfFwdArgs a{};
+  a.dim = dim;
+  a.S = P<const float4>(S); a.s_env = s_env; a.s_step = s_step; a.idx = P<const int>(idx);
+  a.idx1 = P<const int>(idx1); a.src = P<const int>(src); a.nev = P<const int>(nev);
+  a.B = B; a.T = T; a.N = N; a.K = K; a.two = 1;
+  a.wpack = P<const h16>(wpack); a.f_fwd = f_fwd; a.wrm = P<const h16>(wrm); a.wvec = P<const float>(wvec);
+  a.h_out = P<float>(h_out); a.mask_out = P<uint8_t>(mask_out);
+  a.obs_r = obs_r; a.dist_thr = dist_thr; a.dist_eps = dist_eps;
+  return (f16 ? mb_cbf_hfwd_f16 : mb_cbf_hfwd)(&a, num_blocks, ST(stream));
+}
+
 static int cbf_bwd(u64 S, long s_env, long s_step, u64 idx, int B, int T, int N, int K, int passes, u64 dh,
                    u64 wpack, int f_bwd, u64 wrm, u64 wvec, u64 dE, u64 partial, float obs_r, float dist_thr,
                    float dist_eps, int fused, u64 dang, u64 valid, u64 counts, py::tuple lc, u64 idx1,
-                   int dim, int num_blocks, int f16, u64 stream) {
+                   int dim, int num_blocks, int f16, u64 src, u64 nev, u64 stream) {
   mb::CbfBwdArgs a{};
   a.dim = dim;
+  a.src = P<const int>(src); a.nev = P<const int>(nev);
   a.idx1 = P<const int>(idx1);
   a.fused = fused; a.dang = P<const uint8_t>(dang); a.valid = P<const uint8_t>(valid);
   a.counts = P<const float>(counts);
@@ -107,12 +122,34 @@ static int rev_csr(u64 idx, int G, int N, int K, u64 ptr, u64 edges, int Nn, u64
 }
 
 static int node_reduce(u64 dE, u64 ptr, u64 edges, int B, int T, int N, int K, int passes, int accumulate, u64 out,
-                       int pass_mask, int shift1, int Nn, int dim, u64 stream) {
+                       int pass_mask, int shift1, int Nn, int dim, u64 map1, u64 stream) {
   mb::NodeRedArgs a{};
+  a.map1 = P<const int>(map1);
   a.pass_mask = pass_mask; a.shift1 = shift1; a.Nn = Nn; a.dim = dim;
   a.dE = P<const float4>(dE); a.ptr = P<const int>(ptr); a.edges = P<const int>(edges);
   a.B = B; a.T = T; a.N = N; a.K = K; a.passes = passes; a.accumulate = accumulate; a.out = P<float4>(out);
   return mb_node_reduce(&a, ST(stream));
+}
+
+static int cbf_match(u64 idx, int T, int B, int N, int K, int mode, int phase, u64 cnt, u64 off, u64 map1, u64 src,
+                     u64 stream) {
+  mb::CbfMatchArgs a{};
+  a.idx = P<const int>(idx); a.T = T; a.B = B; a.N = N; a.K = K; a.mode = mode; a.phase = phase;
+  a.cnt = P<int>(cnt); a.off = P<const int>(off); a.map1 = P<int>(map1); a.src = P<int>(src);
+  return mb_cbf_match(&a, ST(stream));
+}
+
+static int cbf_dh(u64 h, u64 hmask, u64 map1, u64 src, u64 nev, u64 dang, u64 valid, int B, int T, int N, int K,
+                  u64 counts, py::tuple lc, u64 dh, u64 partial, int num_blocks, u64 stream) {
+  mb::CbfDhArgs a{};
+  a.h = P<const float>(h); a.hmask = P<const uint8_t>(hmask); a.map1 = P<const int>(map1);
+  a.src = P<const int>(src); a.nev = P<const int>(nev); a.dang = P<const uint8_t>(dang);
+  a.valid = P<const uint8_t>(valid); a.B = B; a.T = T; a.N = N; a.K = K; a.counts = P<const float>(counts);
+  a.lc.eps_dang = lc[0].cast<float>(); a.lc.dt_alpha = lc[1].cast<float>(); a.lc.w_dang = lc[2].cast<float>();
+  a.lc.w_safe = lc[3].cast<float>(); a.lc.w_dang_d = lc[4].cast<float>(); a.lc.w_safe_d = lc[5].cast<float>();
+  a.lc.scale = lc[6].cast<float>();
+  a.dh = P<float>(dh); a.partial = P<float>(partial);
+  return mb_cbf_dh(&a, num_blocks, ST(stream));
 }
 
 static int node_combine(u64 dS, long ds_env, u64 ego, u64 dEc, u64 ptr, long ptr_env, u64 edges, long edges_env,
@@ -195,11 +232,14 @@ PYBIND11_MODULE(_C, m) {
   m.def("ctrl_fwd", &ctrl_fwd);
   m.def("cbf_fwd", &cbf_fwd);
   m.def("cbf_bwd", &cbf_bwd);
+  m.def("cbf_hfwd", &cbf_hfwd);
   m.def("ctrl_node_bwd", &ctrl_node_bwd);
   m.def("ctrl_edge_bwd", &ctrl_edge_bwd);
   m.def("rev_csr", &rev_csr);
   m.def("node_reduce", &node_reduce);
   m.def("node_combine", &node_combine);
+  m.def("cbf_match", &cbf_match);
+  m.def("cbf_dh", &cbf_dh);
   m.def("reduce_rows", &reduce_rows);
   m.def("adam", &adam);
   m.def("probe_mfma", &probe_mfma);

@@ -19,7 +19,7 @@ ROOT = os.path.dirname(HERE)
 PKG = os.path.join(ROOT, "macbf_gnn_amd")
 BUILD = os.path.join(ROOT, "build", "csrc")
 ARCH = os.environ.get("MACBF_ARCH", "gfx950")
-KERNELS = ["scan", "scenario", "ctrl", "cbf", "graph", "optim", "probe"]
+KERNELS = ["scan", "scenario", "ctrl", "cbf", "dedup", "graph", "optim", "probe"]
 HALF_KERNELS = {"ctrl", "cbf"}       # compiled for both 16-bit MFMA element types
 
 

@@ -327,7 +327,8 @@ DEV void cbf_load(const CbfBwdArgs& a, long chunk, int wave, int r, long E, long
     const unsigned ev = (unsigned)chunk * CH + wave * 32 + r;
     x.in = ev < (unsigned)EV;
     pass = (x.in && ev >= (unsigned)E) ? 1 : 0;
-    e = ev - (unsigned)pass * (unsigned)E;
+    if (a.src) e = pass ? (unsigned)a.src[ev] : ev;   // deduplicated list: extras name their slot
+    else e = ev - (unsigned)pass * (unsigned)E;
     x.ev = ev;
   }
   const int* idxp = (pass == 1 && a.idx1) ? a.idx1 : a.idx;
@@ -374,6 +375,93 @@ template <int ES> DEV float xmma_skip(...) { return 0.f; }
 #define XMMA stage_mma
 #endif
 
+// h over a deduplicated evaluation list (dedup.hip): evaluation u < E is main slot u on s_t,
+// u >= E the extra evaluation of slot src[u] on s_{t+1} (neighbour idx1[src[u]]). Writes the
+// masked h and the radius mask per evaluation; the losses / upstream gradients are formed by
+// cbf_dh_kernel from these values and the backward runs as cbf_bwd_kernel<false> on the same
+// list. The forward is the backward kernel's recompute chain (row-major W2/W3 images shared
+// with it, packed relu, fp32 head), without the weight-gradient stages: ~40 KB of LDS, so
+// four 8-wave workgroups share a CU; the edge gathers of the next tile are issued before the
+// MFMA chain of the current one.
+template <int NW, int D>
+__global__ __launch_bounds__(NW * 64) void cbf_hfwd_kernel(CbfFwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  h16* W2 = reinterpret_cast<h16*>(smem);
+  h16* W3 = W2 + RM_W2;
+  h16* wf = W3 + RM_W3;                       // w1f (2 frags)
+  float* vl = reinterpret_cast<float*>(smem + (size_t)(RM_W2 + RM_W3) * 2 + 2 * FRAG_BYTES);
+  block_copy16(W2, a.wrm, (RM_W2 + RM_W3) * 2);
+  block_copy16(wf, a.wpack + (size_t)a.f_fwd * 512, 2 * FRAG_BYTES);
+  block_copy16(vl, a.wvec, CBF_VEC * 4);
+  __syncthreads();
+  const int wave = threadIdx.x / WAVE, lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
+  const unsigned E = (unsigned)a.B * a.T * a.N * a.K;
+  const unsigned U = (unsigned)*a.nev;
+  const unsigned ntiles = (U + 31) / 32;
+  const unsigned stride = gridDim.x * NW;
+  auto load = [&](unsigned tile, EdgeCtx<D>& c) {
+    const unsigned u = tile * 32 + r;
+    const bool in = u < U;
+    const int pass = (in && u >= E) ? 1 : 0;
+    const unsigned e = pass ? (unsigned)a.src[u] : u;
+    cbf_edge<D>(a.S, a.s_env, a.s_step, pass ? a.idx1 : a.idx, a.B, a.N, a.K, e, in ? E : 0, pass, a.obs_r,
+                a.dist_thr, a.dist_eps, c);
+  };
+  EdgeCtx<D> nx;
+  unsigned tile = blockIdx.x * NW + wave;
+  if (tile < ntiles) load(tile, nx);
+  for (; tile < ntiles; tile += stride) {
+    const EdgeCtx<D> c = nx;
+    if (tile + stride < ntiles) load(tile + stride, nx);
+    const h16x8 F = cbf_edge_frag<D>(c.rp, c.rv, c.eye, c.dfeat, c.ok, h);
+    const h16* wt = wf + opaque_zero();
+    const h16* W2c = W2 + opaque_zero();
+    const h16* W3c = W3 + opaque_zero();
+    const float* vlc = vl + opaque_zero();
+    const float* b2 = vlc;
+    const float* b3 = vlc + 128;
+    const float* w4 = vlc + 192;
+    h16x16 H1b[2], H2b[4];
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt) H1b[mt] = to_h16x16_relu(mfma(frag_ld(wt, mt, lane), F, zero16()));
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+      f32x16 t2 = bias_rows4(b2, 32 * mt, h);
+      static_for<4>([&](auto kk_) {
+        constexpr int kk = decltype(kk_)::value;
+        t2 = mfma(wrm_acc(W2c, WS2, 32 * mt, kk, lane), bacc_frag<kk & 1>(H1b[kk >> 1]), t2);
+      });
+      H2b[mt] = to_h16x16_relu(t2);
+    }
+    f32x2 hs2 = {0.f, 0.f};
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt) {
+      f32x16 t3 = bias_rows4(b3, 32 * mt, h);
+      static_for<8>([&](auto kk_) {
+        constexpr int kk = decltype(kk_)::value;
+        t3 = mfma(wrm_acc(W3c, WS3, 32 * mt, kk, lane), bacc_frag<kk & 1>(H2b[kk >> 1]), t3);
+      });
+      relu_(t3);
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const float4 w = *reinterpret_cast<const float4*>(w4 + 32 * mt + 8 * g + 4 * h);
+        hs2 = __builtin_elementwise_fma(f32x2{w.x, w.y}, f32x2{t3[4 * g], t3[4 * g + 1]}, hs2);
+        hs2 = __builtin_elementwise_fma(f32x2{w.z, w.w}, f32x2{t3[4 * g + 2], t3[4 * g + 3]}, hs2);
+      }
+    }
+    float hs = hs2.x + hs2.y;
+    hs += shfl_xor32(hs);
+    const unsigned u = tile * 32 + r;
+    if (u < U && h == 0) {
+      a.h_out[u] = c.mask ? hs + vlc[256] : 0.f;
+      a.mask_out[u] = c.mask ? 1 : 0;
+    }
+  }
+}
+
+constexpr int HFWD_WAVES = 8;
+constexpr size_t HFWD_LDS = (size_t)(RM_W2 + RM_W3) * 2 + 2 * FRAG_BYTES + CBF_VEC * 4;
+
 template <bool FUSED, int NW, int D>
 __global__ __launch_bounds__(NW * 64, 1) void cbf_bwd_kernel(CbfBwdArgs a) {
   using Cfg = CbfCfg<NW>;
@@ -398,7 +486,7 @@ __global__ __launch_bounds__(NW * 64, 1) void cbf_bwd_kernel(CbfBwdArgs a) {
   __syncthreads();
   const int wave = threadIdx.x / WAVE, lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
   const long E = (long)a.B * a.T * a.N * a.K;
-  const long EV = E * a.passes;
+  const long EV = (!FUSED && a.nev) ? (long)*a.nev : E * a.passes;
   const long nchunks = FUSED ? (E + CH / 2 - 1) / (CH / 2) : (EV + CH - 1) / CH;
   const int erow = wave * 32 + r;
   const int pass_w = wave / (NW / 2);          // fused: this wave's pass
@@ -725,12 +813,28 @@ extern "C" int MB_SYM(cbf_bwd)(const mb::CbfBwdArgs* a, int num_blocks, hipStrea
   using namespace mb::MB_PREC;
   if (a->K > 16 || a->K < 1 || a->passes < 1 || a->passes > 2) return -1;
   if (a->fused && (a->passes != 2 || !a->dang || !a->counts)) return -2;
+  if (a->src && (a->fused || !a->nev || a->passes != 2)) return -3;
   if (a->dim == 3) {
     if (a->fused) launch_cbf_bwd<true, CBF_NW, 3>(*a, num_blocks, st);
     else launch_cbf_bwd<false, CBF_NW, 3>(*a, num_blocks, st);
   } else {
     if (a->fused) launch_cbf_bwd<true, CBF_NW, 2>(*a, num_blocks, st);
     else launch_cbf_bwd<false, CBF_NW, 2>(*a, num_blocks, st);
+  }
+  return (int)hipGetLastError();
+}
+
+extern "C" int MB_SYM(cbf_hfwd)(const mb::CbfFwdArgs* a, int num_blocks, hipStream_t st) {
+  using namespace mb;
+  using namespace mb::MB_PREC;
+  if (a->K > 16 || a->K < 1) return -1;
+  if (!a->src || !a->nev || !a->idx1 || !a->h_out || !a->mask_out || !a->wrm) return -2;
+  if (a->dim == 3) {
+    (void)hipFuncSetAttribute((const void*)cbf_hfwd_kernel<HFWD_WAVES, 3>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)HFWD_LDS);
+    hipLaunchKernelGGL((cbf_hfwd_kernel<HFWD_WAVES, 3>), dim3(num_blocks), dim3(HFWD_WAVES * 64), HFWD_LDS, st, *a);
+  } else {
+    (void)hipFuncSetAttribute((const void*)cbf_hfwd_kernel<HFWD_WAVES, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)HFWD_LDS);
+    hipLaunchKernelGGL((cbf_hfwd_kernel<HFWD_WAVES, 2>), dim3(num_blocks), dim3(HFWD_WAVES * 64), HFWD_LDS, st, *a);
   }
   return (int)hipGetLastError();
 }

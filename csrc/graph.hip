@@ -145,11 +145,25 @@ __global__ __launch_bounds__(256) void node_reduce_kernel(NodeRedArgs a) {
     if (t < 0 || t >= a.T) continue;
     const long ge = (long)t * a.B + b;                          // edge block of step t
     const long gi = ge + (pass == 1 ? (long)a.shift1 * a.B : 0);  // graph (CSR) the edges live in
-    const float4* dE = a.dE + ((long)pass * E + ge * N * K) * R;
-    for (int k = l; k < K; k += RG) acc_rec<R, 1>(g, dE + ((long)i * K + k) * R);
     const int* ptr = a.ptr + gi * (Nt + 1);
     const int* edges = a.edges + gi * (long)N * K;
     const int q0 = ptr[i], q1 = ptr[i + 1];
+    if (pass == 1 && a.map1) {
+      // deduplicated evaluations: only the extras (map1 >= E) carry a pass-1 gradient; the
+      // matched slots' h' gradient is part of the next step's main evaluation (pass 0)
+      const int* mp = a.map1 + ge * N * K;
+      for (int k = l; k < K; k += RG) {
+        const int m = mp[i * K + k];
+        if (m >= E) acc_rec<R, 1>(g, a.dE + (long)m * R);
+      }
+      for (int q = q0 + l; q < q1; q += RG) {
+        const int m = mp[edges[q]];
+        if (m >= E) acc_rec<R, -1>(g, a.dE + (long)m * R);
+      }
+      continue;
+    }
+    const float4* dE = a.dE + ((long)pass * E + ge * N * K) * R;
+    for (int k = l; k < K; k += RG) acc_rec<R, 1>(g, dE + ((long)i * K + k) * R);
     for (int q = q0 + l; q < q1; q += RG) acc_rec<R, -1>(g, dE + (long)edges[q] * R);
   }
   grp_sum<R>(g);

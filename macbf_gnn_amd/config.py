@@ -95,6 +95,8 @@ class TrainConfig:
     dim: int = 2                      # spatial dimension of the double integrator (2: reference, 3)
     num_obstacles: int = 0            # static point-set obstacles per env (12 points each)
     obstacle_points: int = 12
+    cbf_dedup: bool = True            # HIP, BPTT: evaluate h'(s_{t+1}) through the next step's h of the
+                                      # same neighbour pair (~1.08 E instead of 2 E CBF evaluations)
 
     def k_eff(self) -> int:
         return min(self.num_agents, self.top_k)

@@ -35,6 +35,8 @@ class HipEngine:
         cfg = trainer.cfg
         self.bptt = cfg.bptt
         self.reuse = cfg.reuse_nbr_idx
+        # deduplicated h/h' evaluations need both roles' state gradients on the same s_t: BPTT only
+        self.dedup = bool(getattr(cfg, "cbf_dedup", True)) and cfg.bptt
         native.lib()
         self.dev = trainer.device
         self.B, self.N = cfg.num_envs, cfg.num_agents
@@ -100,6 +102,16 @@ class HipEngine:
         self.red_cbf = torch.zeros(native.CBF_PARTIAL, dtype=f32, device=dev)
         self.red_node = torch.zeros(native.CTRL_NODE_PARTIAL, dtype=f32, device=dev)
         self.red_edge = torch.zeros(native.CTRL_EDGE_PARTIAL, dtype=f32, device=dev)
+        if self.dedup:
+            E = T * B * N * K
+            self.map1 = torch.zeros(T, B, N, K, dtype=i32, device=dev)
+            self.src = torch.zeros(2 * E, dtype=i32, device=dev)
+            self.mcnt = torch.zeros(T * B * N, dtype=i32, device=dev)
+            self.hbuf = torch.zeros(2 * E, dtype=f32, device=dev)
+            self.hmask = torch.zeros(2 * E, dtype=u8, device=dev)
+            self.dhbuf = torch.zeros(2 * E, dtype=f32, device=dev)
+            self.loss_part = torch.zeros(native.cbf_dh_grid(2 * E, dev), native.DH_PARTIAL, dtype=f32, device=dev)
+            self.loss_red = torch.zeros(native.DH_PARTIAL, dtype=f32, device=dev)
         self.host_dist = torch.zeros(T, B, dtype=f32, pin_memory=True)
         self.aux = torch.cuda.Stream(device=dev)      # reverse-CSR build overlaps the CBF kernel
         self._nobptt = {}     # lazily sized (T*B)-batched controller-backward buffers
@@ -256,21 +268,38 @@ class HipEngine:
             native.rev_csr(self.idx[: T + G1].view((T + G1) * B, N, K), rptr, redges, n_nodes=Nn)
             csr_done = torch.cuda.Event()
             csr_done.record(self.aux)
-        # ---- CBF: h, h', hinge losses, upstream grads and the full backward in ONE kernel
         S = self.S[: T + 1]
         idx = self.idx[:T]
         nbb = native.cbf_bwd_grid(2 * E, self.dev)
         part_cbf = self._buf(self._part_cbf, nbb, native.CBF_PARTIAL)
         dE = self.dE[: 2 * E * W].view(2, T, B, N, K, W)
         idx1 = None if self.reuse else self.idx[1: T + 1]
-        native.cbf_bwd(S, idx, None, pw.cbf_w, pw.cbf_off["w1f"], pw.cbf_rm, pw.cbf_v, passes=2, dE=dE,
-                       partial=part_cbf, num_blocks=nbb, fused=True, dang=self.dang[:T], valid=valid_u8,
-                       counts=self.counts, idx1=idx1, grad_scale=gs)
+        map1 = None
+        if self.dedup:
+            # ---- CBF on the deduplicated evaluation list: h'(s_{t+1}) of a slot is the next
+            #      step's h of the same pair; only unmatched pairs get an extra evaluation
+            map1 = self.map1[:T]
+            src = self.src[: 2 * E]
+            nev = native.cbf_match(self.idx[: T + G1], T, map1, src, self.mcnt, recomputed=not self.reuse)
+            hb, hm, dh = self.hbuf[: 2 * E], self.hmask[: 2 * E], self.dhbuf[: 2 * E]
+            native.cbf_hfwd(S, idx, idx if self.reuse else idx1, src, nev, pw.cbf_w, pw.cbf_off["w1f"],
+                            pw.cbf_rm, pw.cbf_v, hb, hm)
+            native.cbf_dh(hb, hm, map1, src, nev, self.dang[:T], valid_u8, self.counts, dh, self.loss_part,
+                          grad_scale=gs)
+            native.cbf_bwd(S, idx, dh.view(2, T, B, N, K), pw.cbf_w, pw.cbf_off["w1f"], pw.cbf_rm, pw.cbf_v,
+                           passes=2, dE=dE, partial=part_cbf, num_blocks=nbb, idx1=idx if self.reuse else idx1,
+                           src=src, nev=nev)
+            native.reduce_rows(self.loss_part, self.loss_red)
+        else:
+            # ---- CBF: h, h', hinge losses, upstream grads and the full backward in ONE kernel
+            native.cbf_bwd(S, idx, None, pw.cbf_w, pw.cbf_off["w1f"], pw.cbf_rm, pw.cbf_v, passes=2, dE=dE,
+                           partial=part_cbf, num_blocks=nbb, fused=True, dang=self.dang[:T], valid=valid_u8,
+                           counts=self.counts, idx1=idx1, grad_scale=gs)
         cur = torch.cuda.current_stream(self.dev)
         cur.wait_event(csr_done)
         # no-BPTT: s_t is a detached input, only h'(s_{t+1}) gradients reach a_t
         native.node_reduce(dE, rptr, redges, self.dS, T=T, B=B, N=N, K=K, passes=2,
-                           pass_mask=0 if self.bptt else 2, shift1=G1, n_nodes=Nn)
+                           pass_mask=0 if self.bptt else 2, shift1=G1, n_nodes=Nn, map1=map1)
         tm.mark("cbf")
         # ---- controller backward
         self.part_node.zero_()
@@ -320,7 +349,8 @@ class HipEngine:
             fg.mul_(1.0 / gs)
         tm.mark("grad_reduce")
         # ---- stats (device tensors; converted lazily by the logger)
-        sums = self.red_cbf[native.CBF_P_LOSS: native.CBF_P_LOSS + 10].to(torch.float64)
+        sums = (self.loss_red[:10] if self.dedup else
+                self.red_cbf[native.CBF_P_LOSS: native.CBF_P_LOSS + 10]).to(torch.float64)
         nd = 1e-5 + self.counts[0].double()
         ns = 1e-5 + self.counts[1].double()
         act_sum = (self.act[:T].double() * valid.double()).sum()

@@ -316,19 +316,124 @@ def cbf_fwd(S, idx, wpack, f_fwd, wvec, *, dang=None, valid=None, two=True, h_ou
     return nb
 
 
+# ----------------------------------------------------------------------------- deduplicated h / h'
+def cbf_match(idx, T, map1, src, cnt, *, recomputed=False):
+    """Deduplicate the h / h' evaluations of a rollout (csrc/dedup.hip).
+
+    idx (>= T + recomputed, B, N, K) int32 neighbour slots. Writes map1 (T, B, N, K): the
+    evaluation index of each slot's h' partner (< E: the next step's main slot with the same
+    neighbour; >= E: an extra evaluation) and src (2E): the slot whose h' evaluation u is, or
+    -1. cnt: (>= T*B*N) int32 scratch. Returns the device int32 tensor [U] (evaluations).
+    Stream-ordered, no host synchronisation."""
+    _, B, N, K = idx.shape
+    if idx.shape[0] < T + int(recomputed):
+        raise NativeError("idx has too few steps")
+    check(idx, torch.int32, None, "idx")
+    E = T * B * N * K
+    if 2 * E >= 2 ** 31:
+        raise NativeError("too many edge evaluations for 32-bit indexing")
+    check(map1, torch.int32, (T, B, N, K), "map1")
+    check(src, torch.int32, (2 * E,), "src")
+    rows = T * B * N
+    check(cnt, torch.int32, None, "cnt")
+    if cnt.numel() < rows:
+        raise NativeError("cnt too small")
+    c = cnt[:rows]
+    mode = 1 if recomputed else 0
+    _ok(lib().cbf_match(ptr(idx), T, B, N, K, mode, 0, ptr(c), 0, 0, 0, stream_handle()), "cbf_match/count")
+    incl = torch.cumsum(c, 0, dtype=torch.int32)
+    off = (incl - c).contiguous()
+    nev = (incl[-1:] + E).contiguous()
+    _ok(lib().cbf_match(ptr(idx), T, B, N, K, mode, 1, 0, ptr(off), ptr(map1), ptr(src), stream_handle()),
+        "cbf_match/fill")
+    return nev
+
+
+HFWD_WAVES = 8
+
+
+def cbf_hfwd_grid(EV: int, device) -> int:
+    tiles = (EV + 31) // 32
+    return max(1, min((tiles + HFWD_WAVES - 1) // HFWD_WAVES, num_cu(device) * 4))
+
+
+def cbf_hfwd(S, idx, idx1, src, nev, wpack, f_fwd, wrm, wvec, h_out, mask_out, num_blocks=None):
+    """h (masked) and the radius mask of every evaluation u < nev of the deduplicated list:
+    S (>= T+1, B, N, W); idx / idx1 (T, B, N, K) (idx1 = idx for reuse_nbr_idx); src, h_out,
+    mask_out (2E,). Weights: w1f fragments at f_fwd of wpack + the row-major W2|W3 image."""
+    T, B, N, K = idx.shape
+    check(idx, torch.int32, None, "idx")
+    check(idx1, torch.int32, (T, B, N, K), "idx1")
+    D, W = _time_major_S(S, T, B, N, 1)
+    E = B * T * N * K
+    if 2 * E >= 2 ** 31:
+        raise NativeError("too many edge evaluations for 32-bit indexing")
+    check(src, torch.int32, (2 * E,), "src")
+    check(nev, torch.int32, (1,), "nev")
+    check(h_out, torch.float32, (2 * E,), "h_out")
+    check(mask_out, torch.uint8, (2 * E,), "mask_out")
+    f16 = _half(wpack, "wpack")
+    check(wpack, wpack.dtype, None, "wpack")
+    check(wrm, wpack.dtype, (128 * 68 + 64 * 148,), "wrm")
+    check(wvec, torch.float32, None, "wvec")
+    nb = num_blocks or cbf_hfwd_grid(2 * E, S.device)
+    rc = lib().cbf_hfwd(ptr(S), S.stride(1) // W, S.stride(0) // W, ptr(idx), ptr(idx1), ptr(src), ptr(nev),
+                        B, T, N, K, ptr(wpack), int(f_fwd), ptr(wrm), ptr(wvec), ptr(h_out), ptr(mask_out),
+                        float(C.OBS_RADIUS), float(C.DIST_MIN_THRES), float(C.CBF_DIST_EPS_COORD * D), D, nb,
+                        f16, stream_handle())
+    _ok(rc, "cbf_hfwd")
+    return nb
+
+
+DH_BLOCK = 256
+DH_PARTIAL = 12
+
+
+def cbf_dh_grid(EV: int, device) -> int:
+    # >= ~8 evaluations per thread (the loop body is a chain of dependent gathers, map1 -> h),
+    # 16 blocks per CU: enough loads in flight, a small partial-sum slab
+    return max(1, min((EV + 8 * DH_BLOCK - 1) // (8 * DH_BLOCK), num_cu(device) * 16))
+
+
+def cbf_dh(h, hmask, map1, src, nev, dang, valid, counts, dh, partial, *, grad_scale=1.0):
+    """Upstream dL/dh of every deduplicated evaluation (h-role + h'-role) and the 10 loss
+    partial sums per block (slots as CBF_P_LOSS: [0, 0, 8 sums], padded) -> partial (nb, DH_PARTIAL)."""
+    T, B, N, K = map1.shape
+    E = T * B * N * K
+    check(h, torch.float32, (2 * E,), "h")
+    check(hmask, torch.uint8, (2 * E,), "hmask")
+    check(map1, torch.int32, (T, B, N, K), "map1")
+    check(src, torch.int32, (2 * E,), "src")
+    check(nev, torch.int32, (1,), "nev")
+    check(dang, torch.uint8, (T, B, N, K), "dang")
+    check(valid, torch.uint8, (T, B), "valid")
+    check(counts, torch.float32, None, "counts")
+    check(dh, torch.float32, (2 * E,), "dh")
+    if partial is None or partial.dim() != 2 or partial.shape[1] != DH_PARTIAL:
+        raise NativeError(f"partial must be (nb, {DH_PARTIAL})")
+    check(partial, torch.float32, None, "partial")
+    nb = partial.shape[0]
+    _ok(lib().cbf_dh(ptr(h), ptr(hmask), ptr(map1), ptr(src), ptr(nev), ptr(dang), ptr(valid), B, T, N, K,
+                     ptr(counts), LOSS_CONSTS[:6] + (LOSS_CONSTS[6] * float(grad_scale),), ptr(dh), ptr(partial),
+                     nb, stream_handle()), "cbf_dh")
+
+
 def cbf_bwd_grid(EV: int, device) -> int:
     return max(1, min((EV + 127) // 128, num_cu(device)))
 
 
 def cbf_bwd(S, idx, dh, wpack, f_bwd, wrm, wvec, *, passes=2, dE=None, partial=None, num_blocks=None,
-            fused=False, dang=None, valid=None, counts=None, idx1=None, grad_scale=1.0):
+            fused=False, dang=None, valid=None, counts=None, idx1=None, grad_scale=1.0, src=None, nev=None):
     """dh (passes, T, B, N, K) -> dE (passes, T, B, N, K, 4), per-WG dW slabs (nb, CBF_PARTIAL).
 
     fused=True (training, passes=2): dh is not read; the kernel evaluates h and h' of every
     edge, forms the hinge-loss upstream gradients from dang (T,B,N,K), valid (T,B) and the
     global counts [n_dang, n_safe], and writes the 10 loss partial sums at CBF_P_LOSS.
     grad_scale multiplies the in-kernel upstream gradients (fp16 loss scaling); the loss sums
-    are unscaled."""
+    are unscaled.
+
+    src/nev (deduplicated list, non-fused, passes=2): evaluation u < nev is main slot u (u < E)
+    or the extra evaluation of slot src[u] on s_{t+1}; dh / dE are indexed by u (sizes 2E)."""
     T, B, N, K = idx.shape
     check(idx, torch.int32, None, "idx")
     D, W = _time_major_S(S, T, B, N, passes - 1)
@@ -343,6 +448,11 @@ def cbf_bwd(S, idx, dh, wpack, f_bwd, wrm, wvec, *, passes=2, dE=None, partial=N
     else:
         check(dh, torch.float32, (passes, T, B, N, K), "dh")
     check(dE, torch.float32, (passes, T, B, N, K, W), "dE")
+    if src is not None:
+        if fused or passes != 2:
+            raise NativeError("deduplicated CBF backward is non-fused with passes=2")
+        check(src, torch.int32, (2 * B * T * N * K,), "src")
+        check(nev, torch.int32, (1,), "nev")
     f16 = _half(wpack, "wpack")
     check(wpack, wpack.dtype, None, "wpack")
     check(wvec, torch.float32, None, "wvec")
@@ -362,7 +472,7 @@ def cbf_bwd(S, idx, dh, wpack, f_bwd, wrm, wvec, *, passes=2, dE=None, partial=N
                        float(C.DIST_MIN_THRES), float(C.CBF_DIST_EPS_COORD * D), int(fused), ptr(dang) if fused else 0,
                        ptr(valid) if fused else 0, ptr(counts) if fused else 0,
                        LOSS_CONSTS[:6] + (LOSS_CONSTS[6] * float(grad_scale),), ptr(idx1), D, nb,
-                       f16, stream_handle())
+                       f16, ptr(src), ptr(nev) if src is not None else 0, stream_handle())
     _ok(rc, "cbf_bwd")
     return nb
 
@@ -379,10 +489,12 @@ def rev_csr(idx, rptr, redges, n_nodes=None):
 
 
 def node_reduce(dE, rptr, redges, out, *, T, B, N, K, passes=2, accumulate=False, pass_mask=0, shift1=0,
-                n_nodes=None):
+                n_nodes=None, map1=None):
     """dE (passes, T, B, N, K, W) -> out[t'] (+)= sum over passes p of the edge->node reduction of
     step t' - p, for the N agents. pass_mask selects passes (0 = all); shift1=1: pass-1 edges live
-    in graph t+1 (h' on the recomputed kNN of s_{t+1}), so the CSR arrays must hold T+1 graphs."""
+    in graph t+1 (h' on the recomputed kNN of s_{t+1}), so the CSR arrays must hold T+1 graphs.
+    map1 (T, B, N, K): deduplicated evaluations (cbf_match) -- dE is then indexed by evaluation
+    and pass 1 reads only the extras map1[e] >= E."""
     Nn = N if n_nodes is None else int(n_nodes)
     W = dE.shape[-1]
     D = 2 if W == 4 else 3
@@ -394,8 +506,12 @@ def node_reduce(dE, rptr, redges, out, *, T, B, N, K, passes=2, accumulate=False
     if out.dtype != torch.float32 or not out.is_contiguous() or out.shape[0] < T + 1 or \
             tuple(out.shape[1:]) != (B, N, W):
         raise NativeError(f"out must be float32 (>=T+1, B, N, {W})")
+    if map1 is not None:
+        check(map1, torch.int32, (T, B, N, K), "map1")
+        if passes != 2:
+            raise NativeError("map1 needs passes=2")
     _ok(lib().node_reduce(ptr(dE), ptr(rptr), ptr(redges), B, T, N, K, passes, int(accumulate), ptr(out),
-                          int(pass_mask), int(shift1), Nn, D, stream_handle()), "node_reduce")
+                          int(pass_mask), int(shift1), Nn, D, ptr(map1), stream_handle()), "node_reduce")
 
 
 def node_combine(dS_t, ego, dEc, rptr_t, redges_t, Gn, Gout, *, K, dt=C.TIME_STEP):
