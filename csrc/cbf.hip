@@ -361,7 +361,7 @@ DEV void cbf_load(const CbfBwdArgs& a, long chunk, int wave, int r, long E, long
 //   wave forms its upstream dL/dh locally (barrier + derivative hinge losses with the danger
 //   bit, step validity and the global pooled counts) and the loss partial sums go to the slab.
 // ---------------------------------------------------------------------------------------
-// ablation hooks (scripts/build_cbf_variants.sh): CBF_X_NOSTSTORE / CBF_X_NOSTMMA drop the
+// ablation hooks (scripts/build_variants.sh cbf): CBF_X_NOSTSTORE / CBF_X_NOSTMMA drop the
 // stage image stores / the stage contractions (results are then wrong; timing only)
 #ifdef CBF_X_NOSTSTORE
 #define XSTORE(...) ((void)0)

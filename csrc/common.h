@@ -314,6 +314,84 @@ DEV float sum32(float v) {   // sum over the 32 lanes of this lane's half
   return v;
 }
 
+// ---- XOR-swizzled edge-major LDS images (no row padding). Logical element (row, col) of an
+// image W elements wide lives at row*W + (((col>>3) ^ swz<W>(row)) << 3) + (col & 7): 16-byte
+// units are permuted per row, so 16-byte / 8-byte pieces stay contiguous. The permutations make
+//   * ds_read_b64_tr_b16 fragments (rows e0..e0+3, e0 % 4 == 0, a 32-column block) hit 4
+//     disjoint 16-bank ranges (padding strides could only make them 2-way at best),
+//   * 16-byte row reads of 16 different rows (W = 128) conflict-free,
+//   * 8-byte tile stores (16 rows, one column piece) at most 2-way (W = 32: conflict-free).
+template <int W> DEV int swz(int row);
+template <> DEV int swz<128>(int row) { return ((row & 3) << 2) | ((row >> 2) & 3); }
+template <> DEV int swz<64>(int row) { return (((row >> 1) & 1) << 2) | ((row >> 2) & 3); }
+template <> DEV int swz<32>(int row) { return (row >> 1) & 3; }
+
+template <int W>
+DEV int swz_off(int row, int col) { return row * W + ((((col >> 3) ^ swz<W>(row))) << 3) + (col & 7); }
+
+// store_tile into a swizzled image (4 x 8-byte writes per lane; col0 % 32 == 0)
+template <int W>
+DEV void store_tile_sw(h16* img, int erow, int col0, const h16x16& v, int h) {
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    h16x4 q;
+    q[0] = v[4 * g]; q[1] = v[4 * g + 1]; q[2] = v[4 * g + 2]; q[3] = v[4 * g + 3];
+    *reinterpret_cast<h16x4*>(img + swz_off<W>(erow, col0 + 8 * g + 4 * h)) = q;
+  }
+}
+
+// Per-lane offsets of the two ds_read_b64_tr_b16 of a fragment at edge rows e0 + 8h + q (+4),
+// column block m0: e0 % 16 == 0 keeps the row's swizzle independent of e0, so a contraction
+// adds only the uniform e0 * W to these (immediate offsets in the loop).
+struct TrOff { int o1, o2; };
+
+template <int W>
+DEV TrOff tr_off_sw(int m0, int lane) {
+  const int q = (lane & 15) >> 2, p = lane & 3, gg = (lane >> 4) & 1, h = lane >> 5;
+  const int col = m0 + 16 * gg + 4 * p;
+  return {swz_off<W>(8 * h + q, col), swz_off<W>(8 * h + q + 4, col)};
+}
+
+// tr_frag on a swizzled image: lane (r, h) receives img[e0 + 8h + j][m0 + r], j = 0..7
+template <int W>
+DEV h16x8 tr_frag_sw(const h16* img, int e0, const TrOff& o) {
+  const LDS_AS h16* im = lds_ptr(img) + e0 * W;
+  const s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4*)(im + o.o1));
+  const s16x4 v2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4*)(im + o.o2));
+  const h16x4 b1 = __builtin_bit_cast(h16x4, v1);
+  const h16x4 b2 = __builtin_bit_cast(h16x4, v2);
+  h16x8 r;
+  r[0] = b1[0]; r[1] = b1[1]; r[2] = b1[2]; r[3] = b1[3];
+  r[4] = b2[0]; r[5] = b2[1]; r[6] = b2[2]; r[7] = b2[3];
+  return r;
+}
+
+// stage_mma on swizzled images (A: WA wide, B: WB wide); same contract as stage_mma
+template <int ES, int WA, int WB>
+DEV float stage_mma_sw(const h16* imgA, const h16* imgB, int mt, int nt, int lane, f32x16& acc,
+                       int bs_lo = 0, int bs_hi = 0) {
+  static_assert(ES % 2 == 0, "even edge-step count");
+  bs_lo = __builtin_amdgcn_readfirstlane(bs_lo);
+  bs_hi = __builtin_amdgcn_readfirstlane(bs_hi);
+  const TrOff oa = tr_off_sw<WA>(32 * mt, lane), ob = tr_off_sw<WB>(32 * nt, lane);
+  float s = 0.f;
+  h16x8 a0 = tr_frag_sw<WA>(imgA, 0, oa), b0 = tr_frag_sw<WB>(imgB, 0, ob);
+  h16x8 a1 = tr_frag_sw<WA>(imgA, 16, oa), b1 = tr_frag_sw<WB>(imgB, 16, ob);
+#pragma nounroll
+  for (int ks = 0; ks < ES; ks += 2) {
+    acc = mfma(a0, b0, acc);
+    if (ks >= bs_lo && ks < bs_hi) s = dot_sum8(a0, s);
+    const int k2 = ks + 2 < ES ? ks + 2 : ks;
+    a0 = tr_frag_sw<WA>(imgA, 16 * k2, oa);
+    b0 = tr_frag_sw<WB>(imgB, 16 * k2, ob);
+    acc = mfma(a1, b1, acc);
+    if (ks + 1 >= bs_lo && ks + 1 < bs_hi) s = dot_sum8(a1, s);
+    a1 = tr_frag_sw<WA>(imgA, 16 * (k2 + 1), oa);
+    b1 = tr_frag_sw<WB>(imgB, 16 * (k2 + 1), ob);
+  }
+  return s;
+}
+
 }  // namespace mb
 
 namespace mb {

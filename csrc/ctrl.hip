@@ -14,6 +14,7 @@
 // PD law, Euler step, per-env goal-distance and action-loss sums. Weights live in LDS as
 // pre-packed 1 KiB fragments (ops/layout.py); all intermediate activations stay in VGPRs.
 #pragma clang fp contract(off)
+#include <climits>
 #include "common.h"
 #include "args.h"
 #include "state.h"
@@ -235,46 +236,42 @@ __global__ __launch_bounds__(WAVES * 64) void ctrl_fwd_kernel(CtrlArgs a) {
       f32x16 Z[4];
       ctrl_edge_tile(F, wl + opaque_zero(), eb2, lane, Z);
       const unsigned mask32 = (unsigned)(__ballot(m) & 0xffffffffull);
-      // per-register edge mask (rows acc_row(reg, h)), shared by the 4 feature tiles
-      bool mk[16];
+      // Masked max-pool of relu(Z) over each agent's 16 rows with the first-occurrence argmax,
+      // as ONE signed-int max per element: v = (bits(Z) & ~15) | c_row, c_row = 15 - slot for
+      // in-radius rows and INT_MIN for masked ones. Non-negative floats order as ints, so the
+      // max is the largest value (its low 4 mantissa bits replaced: < 16 ulp, below the h16
+      // rounding of the pooled value), ties and near-ties (< 16 ulp) go to the lowest slot,
+      // negative / masked rows never beat the initial 0 (relu), and the winning slot is read
+      // back from the low bits. (replaces compare + 3 selects per element and the tie logic)
+      int crow[16];
 #pragma unroll
-      for (int reg = 0; reg < 16; ++reg) mk[reg] = (mask32 >> acc_row(reg, h)) & 1u;
+      for (int reg = 0; reg < 16; ++reg)
+        crow[reg] = ((mask32 >> acc_row(reg, h)) & 1u) ? (15 - (acc_row(reg, h) & 15)) : INT_MIN;
+      const int arow = 2 * q + h;   // h==0 writes agent 2q, h==1 agent 2q+1
+      int bb = 0, ii = 0;
+      const int ga = g0 + arow;
+      if (a.argmax && ga < total) { bb = ga / N; ii = ga - bb * N; }
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt) {
-        // masked max-pool of relu(Z) over each agent's 16 rows + first-occurrence argmax.
-        // Pooled values start at 0 with a strict '>' so masked rows (0), negative Z (relu -> 0)
-        // and later equal values never win; rows are visited in increasing slot order.
-        float p0 = 0.f, p1 = 0.f;
-        int r0 = 255, r1 = 255;
+#ifdef CTRL_X_NOPOOL
+        { pool[arow * PSTR + 32 * nt + r] = (h16)Z[nt][0]; continue; }
+#endif
+        int p0 = 0, p1 = 0;
 #pragma unroll
         for (int reg = 0; reg < 8; ++reg) {
-          const float v = mk[reg] ? Z[nt][reg] : 0.f;
-          const bool gt = v > p0;
-          p0 = gt ? v : p0;
-          r0 = gt ? acc_row(reg, h) : r0;
+          p0 = max(p0, (__float_as_int(Z[nt][reg]) & -16) | crow[reg]);
+          p1 = max(p1, (__float_as_int(Z[nt][reg + 8]) & -16) | crow[reg + 8]);
         }
-#pragma unroll
-        for (int reg = 8; reg < 16; ++reg) {
-          const float v = mk[reg] ? Z[nt][reg] : 0.f;
-          const bool gt = v > p1;
-          p1 = gt ? v : p1;
-          r1 = gt ? acc_row(reg, h) : r1;
-        }
-        const float q0 = shfl_xor32(p0), q1 = shfl_xor32(p1);
-        const int s0 = shfl_xor32i(r0), s1 = shfl_xor32i(r1);
-        if (q0 > p0 || (q0 == p0 && s0 < r0)) { p0 = q0; r0 = s0; }
-        if (q1 > p1 || (q1 == p1 && s1 < r1)) { p1 = q1; r1 = s1; }
-        const int arow = 2 * q + h;   // h==0 writes agent 2q, h==1 agent 2q+1
-        const float pv = (h == 0) ? p0 : p1;
+        p0 = max(p0, shfl_xor32i(p0));
+        p1 = max(p1, shfl_xor32i(p1));
+        const int pw_ = (h == 0) ? p0 : p1;
+        const float pv = __int_as_float(pw_ & -16);
         pool[arow * PSTR + 32 * nt + r] = (h16)pv;
-        if (a.argmax) {
-          const int ga = g0 + arow;
-          if (ga < total) {
-            const int bb = ga / N, ii = ga - bb * N;
-            const int rr = (h == 0) ? r0 : r1 - 16;
-            a.argmax[(long)bb * a.am_env + (long)ii * 128 + 32 * nt + r] = (pv > 0.f) ? (uint8_t)rr : (uint8_t)0xFF;
-          }
-        }
+#ifndef CTRL_X_NOARGMAX
+        if (a.argmax && ga < total)
+          a.argmax[(long)bb * a.am_env + (long)ii * 128 + 32 * nt + r] =
+              (pw_ > 15) ? (uint8_t)(15 - (pw_ & 15)) : (uint8_t)0xFF;
+#endif
       }
     }
     lds_wave_sync();
@@ -289,6 +286,10 @@ __global__ __launch_bounds__(WAVES * 64) void ctrl_fwd_kernel(CtrlArgs a) {
         }
       }
     }
+#ifdef CTRL_X_NONODE
+    lds_wave_sync();
+    continue;
+#endif
     // ---------------- node phase: lane column r = agent g0 + r
     const int gi = g0 + r;
     const bool ok = gi < total;
@@ -720,16 +721,23 @@ d1b[mt] = to_h16x16(c);
 }
 
 // ---------------------------------------------------------------------------------------
-constexpr int EB_WAVES = 4;
-constexpr int EB_CH = EB_WAVES * 32;     // agents per chunk (each round: 128 edges)
+// EB_WAVES waves share a chunk of 32*EB_WAVES agents; each stage contracts the 32*EB_WAVES edges
+// of one tile round (8 waves: 256 edges per barrier pair, one dW2 tile per wave; 4 waves: 128
+// edges, two tiles per wave, two workgroups per CU)
+#ifndef CTRL_EB_WAVES
+#define CTRL_EB_WAVES 4
+#endif
+constexpr int EB_WAVES = CTRL_EB_WAVES;
+constexpr int EB_CH = EB_WAVES * 32;     // agents per chunk (each round: EB_CH edges)
+constexpr int EB_TA = 8 / EB_WAVES;      // owned dW2 tiles per wave
 constexpr int EP_W2 = 0, EP_B2 = 8192, EP_W1 = 8320;
 constexpr int CTRL_EDGE_PARTIAL = 10368;
-constexpr size_t EB_STAGE = (size_t)(136 + 72) * EB_CH * 2;
+constexpr size_t EB_STAGE = (size_t)(128 + 64) * EB_CH * 2;
 
 size_t ctrl_edge_bwd_lds() { return (size_t)22 * FRAG_BYTES + EB_STAGE; }
 
 template <int D>
-__global__ __launch_bounds__(EB_WAVES * 64, 2) void ctrl_edge_bwd_kernel(CtrlEdgeBwdArgs a) {
+__global__ __launch_bounds__(EB_WAVES * 64, EB_WAVES == 4 ? 2 : 1) void ctrl_edge_bwd_kernel(CtrlEdgeBwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   h16* wf = reinterpret_cast<h16*>(smem);                 // ew1f (2) | ew2tn (16) | ew1ft (4)
   h16* stg = reinterpret_cast<h16*>(smem + 22 * FRAG_BYTES);
@@ -741,9 +749,10 @@ __global__ __launch_bounds__(EB_WAVES * 64, 2) void ctrl_edge_bwd_kernel(CtrlEdg
   const int total = a.B * N;
   const long nchunks = (total + EB_CH - 1) / EB_CH;
   const int erow = wave * 32 + r;
-  f32x16 accW2[2], accW1;
-  accW2[0] = accW2[1] = accW1 = zero16();
-  float bs[2] = {0.f, 0.f};
+  f32x16 accW2[EB_TA], accW1 = zero16();
+  float bs[EB_TA];
+#pragma unroll
+  for (int u = 0; u < EB_TA; ++u) { accW2[u] = zero16(); bs[u] = 0.f; }
   const h16 z = (h16)0.f;
 
   for (long chunk = blockIdx.x; chunk < nchunks; chunk += gridDim.x) {
@@ -756,10 +765,27 @@ __global__ __launch_bounds__(EB_WAVES * 64, 2) void ctrl_edge_bwd_kernel(CtrlEdg
       ctrl_st_load<D>(a.S, a.s_env, xi0, xs0);
       ctrl_idx_load(a.idx, a.i_env, N, K, g0, 1, r, total, xi1);
     }
+    // argmax slots / dL/dpooled of the tile's two agents (lane (r, h): agent 2q+h, features
+    // 4r..4r+3): loaded one tile ahead, like the edge gathers
+    auto pool_load = [&](int q, unsigned& am4, h16x4& dp4) {
+      const int ag = g0 + 2 * q + h;
+      am4 = 0xFFFFFFFFu;
+      if (q < 16 && ag < total) {
+        const int bb = ag / N, ii = ag - bb * N;
+        am4 = *reinterpret_cast<const unsigned*>(a.argmax + bb * (int)a.am_env + ii * 128 + 4 * r);
+        dp4 = *reinterpret_cast<const h16x4*>(a.dP + bb * (int)a.dp_env + ii * 128 + 4 * r);
+      }
+    };
+    unsigned am_n;
+    h16x4 dp_n;
+    pool_load(0, am_n, dp_n);
     for (int q = 0; q < 16; ++q) {
       const EdgeSt<D> cur = xs0;
+      const unsigned am4 = am_n;
+      const h16x4 dp4 = dp_n;
       ctrl_st_load<D>(a.S, a.s_env, xi1, xs0);
       ctrl_idx_load(a.idx, a.i_env, N, K, g0, q + 2, r, total, xi1);
+      pool_load(q + 1, am_n, dp_n);
       const int slot = r & 15;
       const bool ok = cur.ok;
       const int ga = g0 + 2 * q + (r >> 4);
@@ -779,28 +805,23 @@ __global__ __launch_bounds__(EB_WAVES * 64, 2) void ctrl_edge_bwd_kernel(CtrlEdg
       // agents 2q, 2q+1 x 16 slots): zero the rows, then lane (r, h) routes dP[f] of agent 2q+h,
       // f = 4r..4r+3, to row (h, argmax slot). One coalesced argmax/dP load per lane instead of
       // 16 redundant row loads + 64 compare/selects per edge lane.
-      h16* imS = stg;                                           // S1 dZ image, stride 136
+      h16* imS = stg;                                           // S1 dZ image (128 wide, swizzled)
       {
         const u32x4 zero4 = {0u, 0u, 0u, 0u};
 #pragma unroll
-        for (int c8 = 0; c8 < 8; ++c8)
-          *reinterpret_cast<u32x4*>(imS + (wave * 32 + (lane >> 1)) * 136 + 64 * (lane & 1) + 8 * c8) = zero4;
-        const int ag = g0 + 2 * q + h;                          // agent of this half
-        if (ag < total) {
-          const int bb = ag / N, ii = ag - bb * N;
-          const unsigned am4 = *reinterpret_cast<const unsigned*>(a.argmax + bb * (int)a.am_env + ii * 128 + 4 * r);
-          const h16x4 dp4 = *reinterpret_cast<const h16x4*>(a.dP + bb * (int)a.dp_env + ii * 128 + 4 * r);
+        for (int c8 = 0; c8 < 8; ++c8)   // whole rows are zeroed (unit permutation irrelevant); 8
+          // consecutive lanes fill 128 contiguous bytes: conflict-free 16-byte stores
+          *reinterpret_cast<u32x4*>(imS + wave * 32 * 128 + (c8 * 64 + lane) * 8) = zero4;
 #pragma unroll
-          for (int jj = 0; jj < 4; ++jj) {
-            const unsigned sl = (am4 >> (8 * jj)) & 0xFFu;
-            if (sl < 16u) imS[(wave * 32 + 16 * h + (int)sl) * 136 + 4 * r + jj] = dp4[jj];
-          }
+        for (int jj = 0; jj < 4; ++jj) {               // (am4 = all 0xFF: agent out of range)
+          const unsigned sl = (am4 >> (8 * jj)) & 0xFFu;
+          if (sl < 16u) imS[swz_off<128>(wave * 32 + 16 * h + (int)sl, 4 * r + jj)] = dp4[jj];
         }
         lds_wave_sync();
       }
       h16x8 dz[8];
 #pragma unroll
-      for (int kk = 0; kk < 8; ++kk) dz[kk] = *reinterpret_cast<const h16x8*>(imS + erow * 136 + 16 * kk + 8 * h);
+      for (int kk = 0; kk < 8; ++kk) dz[kk] = *reinterpret_cast<const h16x8*>(imS + swz_off<128>(erow, 16 * kk + 8 * h));
       // dH1 = W2^T dZ (natural k) . relu'(H1)
       h16x16 d1b[2];
 #pragma unroll
@@ -830,55 +851,61 @@ __global__ __launch_bounds__(EB_WAVES * 64, 2) void ctrl_edge_bwd_kernel(CtrlEdg
           store_rec<D>(a.dEc, (unsigned)(b * (int)a.de_env + i * K + slot), gp, gv);
         }
       }
+#ifdef CTRL_X_EBNOSTAGE
+      lds_wave_sync();
+      continue;
+#endif
       // S1: dW2 (128x64) += dZ . H1^T ; eb2 (dZ is already in the image; bias-sum steps split
       //     between the two waves that read each row block)
       {
         h16* imA = stg;
-        h16* imB = stg + EB_CH * 136;
+        h16* imB = stg + EB_CH * 128;
 #pragma unroll
-        for (int mt = 0; mt < 2; ++mt) store_tile(imB, 72, erow, 32 * mt, H1b[mt], h);
+        for (int mt = 0; mt < 2; ++mt) store_tile_sw<64>(imB, erow, 32 * mt, H1b[mt], h);
         __syncthreads();
+        constexpr int KS = EB_CH / 16;
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          const int t = wave + 4 * u;
-          bs[u] += stage_mma<EB_CH / 16>(imA, 136, imB, 72, t / 2, t % 2, lane, accW2[u], 4 * (wave & 1),
-                             4 * (wave & 1) + 4);
+        for (int u = 0; u < EB_TA; ++u) {
+          const int t = wave + EB_WAVES * u;
+          bs[u] += stage_mma_sw<KS, 128, 64>(imA, imB, t / 2, t % 2, lane, accW2[u], (KS / 2) * (wave & 1),
+                                             (KS / 2) * (wave & 1) + KS / 2);
         }
         __syncthreads();
       }
       // S2: dW1f (64x32) += dH1 . F^T
       {
         h16* imA = stg;
-        h16* imB = stg + EB_CH * 72;
+        h16* imB = stg + EB_CH * 64;
 #pragma unroll
-        for (int mt = 0; mt < 2; ++mt) store_tile(imA, 72, erow, 32 * mt, d1b[mt], h);
+        for (int mt = 0; mt < 2; ++mt) store_tile_sw<64>(imA, erow, 32 * mt, d1b[mt], h);
         h16x8 zz;
 #pragma unroll
         for (int jj = 0; jj < 8; ++jj) zz[jj] = z;
-        *reinterpret_cast<h16x8*>(imB + erow * 40 + 8 * h) = F;
-        *reinterpret_cast<h16x8*>(imB + erow * 40 + 16 + 8 * h) = zz;
+        *reinterpret_cast<h16x8*>(imB + swz_off<32>(erow, 8 * h)) = F;
+        *reinterpret_cast<h16x8*>(imB + swz_off<32>(erow, 16 + 8 * h)) = zz;
         __syncthreads();
-        if (wave < 2) stage_mma<EB_CH / 16>(imA, 72, imB, 40, wave, 0, lane, accW1);
+        if (wave < 2) stage_mma_sw<EB_CH / 16, 64, 32>(imA, imB, wave, 0, lane, accW1);
         __syncthreads();
       }
     }
   }
   float* P = a.partial + (long)blockIdx.x * CTRL_EDGE_PARTIAL;
-  __shared__ float ebred[EB_WAVES][2][32];
+  __shared__ float ebred[EB_WAVES][EB_TA][32];
 #pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    const int t = wave + 4 * u;
+  for (int u = 0; u < EB_TA; ++u) {
+    const int t = wave + EB_WAVES * u;
     add_tile(P + EP_W2, 64, t / 2, t % 2, accW2[u], lane);
     const float s = bs[u] + shfl_xor32(bs[u]);
     if (h == 0) ebred[wave][u][r] = s;
   }
   if (wave < 2) add_tile(P + EP_W1, 32, wave, 0, accW1, lane);
   __syncthreads();
-  // eb2 row block (wave>>1) + 2u was summed half by wave w and half by w^1: add in fixed order
+  // eb2 row block mt was summed half by the owner of tile 2mt and half by the owner of tile
+  // 2mt+1 (waves w, w^1): add in fixed order
   if (threadIdx.x < 128) {
     const int mt = threadIdx.x >> 5, rr = threadIdx.x & 31;    // row block 0..3
-    const int w0 = 2 * (mt & 1), u = mt >> 1;                   // waves w0, w0+1 own it
-    P[EP_B2 + 32 * mt + rr] += ebred[w0][u][rr] + ebred[w0 + 1][u][rr];
+    const int t0 = 2 * mt, t1 = 2 * mt + 1;
+    P[EP_B2 + 32 * mt + rr] += ebred[t0 % EB_WAVES][t0 / EB_WAVES][rr] + ebred[t1 % EB_WAVES][t1 / EB_WAVES][rr];
   }
 }
 

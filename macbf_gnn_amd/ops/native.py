@@ -535,10 +535,16 @@ def node_combine(dS_t, ego, dEc, rptr_t, redges_t, Gn, Gout, *, K, dt=C.TIME_STE
                            ptr(Gout), Gout.stride(0) // W, B, N, K, float(dt), D, stream_handle()), "node_combine")
 
 
+CTRL_EDGE_WAVES = 4          # csrc/ctrl.hip EB_WAVES
+
+
 def ctrl_bwd_grids(total_agents: int, device):
+    """(node, edge) backward grids: the node kernel takes 128-agent chunks, one workgroup per CU;
+    the edge kernel 32*CTRL_EDGE_WAVES-agent chunks (8 waves: one workgroup per CU)."""
     ch = (total_agents + 127) // 128
+    che = (total_agents + 32 * CTRL_EDGE_WAVES - 1) // (32 * CTRL_EDGE_WAVES)
     cu = num_cu(device)
-    return max(1, min(ch, cu)), max(1, min(ch, 2 * cu))
+    return max(1, min(ch, cu)), max(1, min(che, (8 // CTRL_EDGE_WAVES) * cu))
 
 
 def ctrl_node_bwd(pooled, S, G, A, Gn, valid_t, wrm, offs, wvec, act_coef, dP, ego, partial, num_blocks,

@@ -1,4 +1,4 @@
-# Time the CBF training kernel for each prebuilt ablation variant (scripts/build_cbf_variants.sh).
+# Time the CBF training kernel for each prebuilt ablation variant (scripts/build_variants.sh cbf).
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 for v in "$@"; do

@@ -2,7 +2,7 @@
 
 usage: python scripts/micro_cbf.py [--so PATH] [--tag NAME]
 --so loads an alternative build of the extension (e.g. an experiment variant compiled by
-scripts/build_cbf_variants.sh) in place of macbf_gnn_amd._C before anything imports it.
+scripts/build_variants.sh cbf) in place of macbf_gnn_amd._C before anything imports it.
 """
 import argparse
 import importlib.util
