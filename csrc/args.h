@@ -118,6 +118,9 @@ struct CbfBwdArgs {
   // CbfFwdArgs, dh / dE indexed by u
   const int* src;
   const int* nev;
+  // active list (optional): only evaluations act[v], v < *nact, are processed (dh != 0)
+  const int* act;
+  const int* nact;
 };
 
 // Deduplication of the h / h' evaluations (dedup.hip). h'(s_{t+1}) of slot (t,b,i,k) is the
@@ -145,6 +148,7 @@ struct CbfDhArgs {
   LossConsts lc;
   float* dh;             // (U) upstream gradient per evaluation
   float* partial;        // (gridDim.x, 12) loss partial sums (slots 0..9 as CBF P_LOSS)
+  int* blk_active;       // (gridDim.x) evaluations with dh != 0 per block (or null)
 };
 
 struct CtrlNodeBwdArgs {
@@ -196,6 +200,8 @@ struct NodeRedArgs {
   int dim;
   int shift1;          // pass 1 edges belong to graph t + shift1 (1: h' on recomputed kNN of s_{t+1})
   const int* map1;     // dedup: pass-1 slot e -> evaluation index (only >= E = extras are read)
+  const float* gate;   // optional: dE[x] is read only where gate[x] != 0 (the skipped evaluations of
+                       // the active-list backward leave their dE records unwritten)
 };
 
 struct CombineArgs {
@@ -238,6 +244,7 @@ int mb_ctrl_edge_bwd_f16(const mb::CtrlEdgeBwdArgs* a, int num_blocks, hipStream
 int mb_rev_csr(const mb::CsrArgs* a, hipStream_t st);
 int mb_cbf_match(const mb::CbfMatchArgs* a, hipStream_t st);
 int mb_cbf_dh(const mb::CbfDhArgs* a, int num_blocks, hipStream_t st);
+int mb_cbf_compact(const float* dh, const int* nev, const int* blk_off, int* act, int num_blocks, hipStream_t st);
 int mb_node_reduce(const mb::NodeRedArgs* a, hipStream_t st);
 int mb_node_combine(const mb::CombineArgs* a, hipStream_t st);
 int mb_reduce_rows(const float* partial, int rows, int cols, float* out, int accumulate, hipStream_t st);

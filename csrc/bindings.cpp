@@ -96,10 +96,10 @@ static int cbf_hfwd(u64 S, long s_env, long s_step, u64 idx, u64 idx1, u64 src, 
 static int cbf_bwd(u64 S, long s_env, long s_step, u64 idx, int B, int T, int N, int K, int passes, u64 dh,
                    u64 wpack, int f_bwd, u64 wrm, u64 wvec, u64 dE, u64 partial, float obs_r, float dist_thr,
                    float dist_eps, int fused, u64 dang, u64 valid, u64 counts, py::tuple lc, u64 idx1,
-                   int dim, int num_blocks, int f16, u64 src, u64 nev, u64 stream) {
+                   int dim, int num_blocks, int f16, u64 src, u64 nev, u64 act, u64 nact, u64 stream) {
   mb::CbfBwdArgs a{};
   a.dim = dim;
-  a.src = P<const int>(src); a.nev = P<const int>(nev);
+  a.src = P<const int>(src); a.nev = P<const int>(nev); a.act = P<const int>(act); a.nact = P<const int>(nact);
   a.idx1 = P<const int>(idx1);
   a.fused = fused; a.dang = P<const uint8_t>(dang); a.valid = P<const uint8_t>(valid);
   a.counts = P<const float>(counts);
@@ -122,9 +122,9 @@ static int rev_csr(u64 idx, int G, int N, int K, u64 ptr, u64 edges, int Nn, u64
 }
 
 static int node_reduce(u64 dE, u64 ptr, u64 edges, int B, int T, int N, int K, int passes, int accumulate, u64 out,
-                       int pass_mask, int shift1, int Nn, int dim, u64 map1, u64 stream) {
+                       int pass_mask, int shift1, int Nn, int dim, u64 map1, u64 gate, u64 stream) {
   mb::NodeRedArgs a{};
-  a.map1 = P<const int>(map1);
+  a.map1 = P<const int>(map1); a.gate = P<const float>(gate);
   a.pass_mask = pass_mask; a.shift1 = shift1; a.Nn = Nn; a.dim = dim;
   a.dE = P<const float4>(dE); a.ptr = P<const int>(ptr); a.edges = P<const int>(edges);
   a.B = B; a.T = T; a.N = N; a.K = K; a.passes = passes; a.accumulate = accumulate; a.out = P<float4>(out);
@@ -140,8 +140,9 @@ static int cbf_match(u64 idx, int T, int B, int N, int K, int mode, int phase, u
 }
 
 static int cbf_dh(u64 h, u64 hmask, u64 map1, u64 src, u64 nev, u64 dang, u64 valid, int B, int T, int N, int K,
-                  u64 counts, py::tuple lc, u64 dh, u64 partial, int num_blocks, u64 stream) {
+                  u64 counts, py::tuple lc, u64 dh, u64 partial, u64 blk_active, int num_blocks, u64 stream) {
   mb::CbfDhArgs a{};
+  a.blk_active = P<int>(blk_active);
   a.h = P<const float>(h); a.hmask = P<const uint8_t>(hmask); a.map1 = P<const int>(map1);
   a.src = P<const int>(src); a.nev = P<const int>(nev); a.dang = P<const uint8_t>(dang);
   a.valid = P<const uint8_t>(valid); a.B = B; a.T = T; a.N = N; a.K = K; a.counts = P<const float>(counts);
@@ -150,6 +151,11 @@ static int cbf_dh(u64 h, u64 hmask, u64 map1, u64 src, u64 nev, u64 dang, u64 va
   a.lc.scale = lc[6].cast<float>();
   a.dh = P<float>(dh); a.partial = P<float>(partial);
   return mb_cbf_dh(&a, num_blocks, ST(stream));
+}
+
+static int cbf_compact(u64 dh, u64 nev, u64 blk_off, u64 act, int num_blocks, u64 stream) {
+  return mb_cbf_compact(P<const float>(dh), P<const int>(nev), P<const int>(blk_off), P<int>(act), num_blocks,
+                        ST(stream));
 }
 
 static int node_combine(u64 dS, long ds_env, u64 ego, u64 dEc, u64 ptr, long ptr_env, u64 edges, long edges_env,
@@ -240,6 +246,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("node_combine", &node_combine);
   m.def("cbf_match", &cbf_match);
   m.def("cbf_dh", &cbf_dh);
+  m.def("cbf_compact", &cbf_compact);
   m.def("reduce_rows", &reduce_rows);
   m.def("adam", &adam);
   m.def("probe_mfma", &probe_mfma);

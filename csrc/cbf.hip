@@ -324,8 +324,9 @@ DEV void cbf_load(const CbfBwdArgs& a, long chunk, int wave, int r, long E, long
     x.in = e < (unsigned)E;
     x.ev = (unsigned)pass * (unsigned)E + e;
   } else {
-    const unsigned ev = (unsigned)chunk * CH + wave * 32 + r;
-    x.in = ev < (unsigned)EV;
+    const unsigned v = (unsigned)chunk * CH + wave * 32 + r;
+    x.in = v < (unsigned)EV;
+    const unsigned ev = (a.act && x.in) ? (unsigned)a.act[v] : v;   // active list: v -> evaluation
     pass = (x.in && ev >= (unsigned)E) ? 1 : 0;
     if (a.src) e = pass ? (unsigned)a.src[ev] : ev;   // deduplicated list: extras name their slot
     else e = ev - (unsigned)pass * (unsigned)E;
@@ -486,7 +487,7 @@ __global__ __launch_bounds__(NW * 64, 1) void cbf_bwd_kernel(CbfBwdArgs a) {
   __syncthreads();
   const int wave = threadIdx.x / WAVE, lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
   const long E = (long)a.B * a.T * a.N * a.K;
-  const long EV = (!FUSED && a.nev) ? (long)*a.nev : E * a.passes;
+  const long EV = (!FUSED && a.nact) ? (long)*a.nact : (!FUSED && a.nev) ? (long)*a.nev : E * a.passes;
   const long nchunks = FUSED ? (E + CH / 2 - 1) / (CH / 2) : (EV + CH - 1) / CH;
   const int erow = wave * 32 + r;
   const int pass_w = wave / (NW / 2);          // fused: this wave's pass
@@ -814,6 +815,7 @@ extern "C" int MB_SYM(cbf_bwd)(const mb::CbfBwdArgs* a, int num_blocks, hipStrea
   if (a->K > 16 || a->K < 1 || a->passes < 1 || a->passes > 2) return -1;
   if (a->fused && (a->passes != 2 || !a->dang || !a->counts)) return -2;
   if (a->src && (a->fused || !a->nev || a->passes != 2)) return -3;
+  if (a->act && (!a->src || !a->nact)) return -4;
   if (a->dim == 3) {
     if (a->fused) launch_cbf_bwd<true, CBF_NW, 3>(*a, num_blocks, st);
     else launch_cbf_bwd<false, CBF_NW, 3>(*a, num_blocks, st);

@@ -90,6 +90,12 @@ __global__ __launch_bounds__(MATCH_BLOCK) void cbf_match_kernel(CbfMatchArgs a) 
   if (t == 0 && act) a.src[e0 + k] = -1;
 }
 
+// evaluations per dh / compact block: a multiple of DH_BLOCK, the same in both kernels
+DEV unsigned dh_span(unsigned U, unsigned nblocks) {
+  const unsigned per = (U + nblocks - 1) / nblocks;
+  return (per + DH_BLOCK - 1) / DH_BLOCK * DH_BLOCK;
+}
+
 __global__ __launch_bounds__(DH_BLOCK) void cbf_dh_kernel(CbfDhArgs a) {
   const unsigned NK = (unsigned)a.N * a.K, BNK = (unsigned)a.B * NK;
   const unsigned E = (unsigned)a.T * BNK;
@@ -99,7 +105,11 @@ __global__ __launch_bounds__(DH_BLOCK) void cbf_dh_kernel(CbfDhArgs a) {
   float acc[8];
 #pragma unroll
   for (int q = 0; q < 8; ++q) acc[q] = 0.f;
-  for (unsigned u = blockIdx.x * DH_BLOCK + threadIdx.x; u < U; u += gridDim.x * DH_BLOCK) {
+  // contiguous per-block ranges (the active-list compaction keeps this order)
+  const unsigned span = dh_span(U, gridDim.x);
+  const unsigned u_hi = min(U, (blockIdx.x + 1) * span);
+  int nact = 0;
+  for (unsigned u = blockIdx.x * span + threadIdx.x; u < u_hi; u += DH_BLOCK) {
     float g = 0.f;
     if (u < E) {                                   // h-role of main slot u
       const unsigned t = u / BNK, b = (u - t * BNK) / NK;
@@ -143,16 +153,27 @@ __global__ __launch_bounds__(DH_BLOCK) void cbf_dh_kernel(CbfDhArgs a) {
         }
       }
     }
-    a.dh[u] = a.hmask[u] ? g : 0.f;
+    const float d = a.hmask[u] ? g : 0.f;
+    a.dh[u] = d;
+    nact += (d != 0.f) ? 1 : 0;
   }
   __shared__ float red[8][DH_BLOCK / WAVE];
+  __shared__ int cred[DH_BLOCK / WAVE];
   const int wave = threadIdx.x / WAVE, lane = threadIdx.x % WAVE;
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
     const float v = wave_sum(acc[q]);
     if (lane == 0) red[q][wave] = v;
   }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) nact += __shfl_xor(nact, o);
+  if (lane == 0) cred[wave] = nact;
   __syncthreads();
+  if (a.blk_active && threadIdx.x == 0) {
+    int c = 0;
+    for (int w = 0; w < DH_BLOCK / WAVE; ++w) c += cred[w];
+    a.blk_active[blockIdx.x] = c;
+  }
   if (threadIdx.x < DH_PARTIAL) {
     float s = 0.f;
     if (threadIdx.x >= 2 && threadIdx.x < 10)
@@ -161,7 +182,45 @@ __global__ __launch_bounds__(DH_BLOCK) void cbf_dh_kernel(CbfDhArgs a) {
   }
 }
 
+// Active-evaluation list: the evaluations with a nonzero upstream gradient, in index order
+// (every other evaluation contributes exactly zero to the weight and state gradients, so the
+// backward skips it). Same block ranges as cbf_dh_kernel; blk_off = exclusive scan of its
+// per-block counts.
+__global__ __launch_bounds__(DH_BLOCK) void cbf_compact_kernel(const float* dh, const int* nev, const int* blk_off,
+                                                             int* act) {
+  const unsigned U = (unsigned)*nev;
+  const unsigned span = dh_span(U, gridDim.x);
+  const unsigned u_lo = blockIdx.x * span, u_hi = min(U, u_lo + span);
+  __shared__ int wcnt[DH_BLOCK / WAVE];
+  const int wave = threadIdx.x / WAVE, lane = threadIdx.x % WAVE;
+  int base = blk_off[blockIdx.x];
+  for (unsigned u0 = u_lo; u0 < u_hi; u0 += DH_BLOCK) {
+    const unsigned u = u0 + threadIdx.x;
+    const bool f = u < u_hi && dh[u] != 0.f;
+    const unsigned long long bal = __ballot(f);
+    const int below = __popcll(bal & ((1ull << lane) - 1ull));
+    if (lane == 0) wcnt[wave] = __popcll(bal);
+    __syncthreads();
+    int wo = 0, tot = 0;
+    for (int w = 0; w < DH_BLOCK / WAVE; ++w) {
+      const int c = wcnt[w];
+      wo += (w < wave) ? c : 0;
+      tot += c;
+    }
+    if (f) act[base + wo + below] = (int)u;
+    base += tot;
+    __syncthreads();
+  }
+}
+
 }  // namespace mb
+
+extern "C" int mb_cbf_compact(const float* dh, const int* nev, const int* blk_off, int* act, int num_blocks,
+                              hipStream_t st) {
+  using namespace mb;
+  hipLaunchKernelGGL(cbf_compact_kernel, dim3(num_blocks), dim3(DH_BLOCK), 0, st, dh, nev, blk_off, act);
+  return (int)hipGetLastError();
+}
 
 extern "C" int mb_cbf_match(const mb::CbfMatchArgs* a, hipStream_t st) {
   using namespace mb;

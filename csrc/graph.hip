@@ -119,6 +119,21 @@ DEV void acc_rec(float4 (&g)[R], const float4* src) {
   }
 }
 
+// gated record accumulation: the record and its gate are loaded together (no dependent load);
+// a zero gate selects zero (the record may hold stale data)
+template <int R, int SIGN>
+DEV void acc_rec_g(float4 (&g)[R], const float4* src, const float* gate) {
+  float4 v[R];
+#pragma unroll
+  for (int q = 0; q < R; ++q) v[q] = src[q];
+  const bool on = !gate || *gate != 0.f;
+#pragma unroll
+  for (int q = 0; q < R; ++q) {
+    if (!on) v[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+    g[q].x += SIGN * v[q].x; g[q].y += SIGN * v[q].y; g[q].z += SIGN * v[q].z; g[q].w += SIGN * v[q].w;
+  }
+}
+
 // out[t', b, i] (+)= sum over passes p of [ sum_k dE_p[t'-p, b, i, k] - sum_{e in in(i)} dE_p[e] ]
 // for the N agents (obstacle nodes receive no gradient). Records of REC<D> float4.
 template <int D>
@@ -154,17 +169,23 @@ __global__ __launch_bounds__(256) void node_reduce_kernel(NodeRedArgs a) {
       const int* mp = a.map1 + ge * N * K;
       for (int k = l; k < K; k += RG) {
         const int m = mp[i * K + k];
-        if (m >= E) acc_rec<R, 1>(g, a.dE + (long)m * R);
+        if (m >= E) acc_rec_g<R, 1>(g, a.dE + (long)m * R, a.gate ? a.gate + m : nullptr);
       }
       for (int q = q0 + l; q < q1; q += RG) {
         const int m = mp[edges[q]];
-        if (m >= E) acc_rec<R, -1>(g, a.dE + (long)m * R);
+        if (m >= E) acc_rec_g<R, -1>(g, a.dE + (long)m * R, a.gate ? a.gate + m : nullptr);
       }
       continue;
     }
-    const float4* dE = a.dE + ((long)pass * E + ge * N * K) * R;
-    for (int k = l; k < K; k += RG) acc_rec<R, 1>(g, dE + ((long)i * K + k) * R);
-    for (int q = q0 + l; q < q1; q += RG) acc_rec<R, -1>(g, dE + (long)edges[q] * R);
+    const long eb = pass * E + ge * N * K;
+    const float4* dE = a.dE + eb * R;
+    const float* gt = a.gate ? a.gate + eb : nullptr;
+    for (int k = l; k < K; k += RG)
+      acc_rec_g<R, 1>(g, dE + ((long)i * K + k) * R, gt ? gt + i * K + k : nullptr);
+    for (int q = q0 + l; q < q1; q += RG) {
+      const int e = edges[q];
+      acc_rec_g<R, -1>(g, dE + (long)e * R, gt ? gt + e : nullptr);
+    }
   }
   grp_sum<R>(g);
   if (l != 0) return;

@@ -110,7 +110,10 @@ class HipEngine:
             self.hbuf = torch.zeros(2 * E, dtype=f32, device=dev)
             self.hmask = torch.zeros(2 * E, dtype=u8, device=dev)
             self.dhbuf = torch.zeros(2 * E, dtype=f32, device=dev)
-            self.loss_part = torch.zeros(native.cbf_dh_grid(2 * E, dev), native.DH_PARTIAL, dtype=f32, device=dev)
+            ndh = native.cbf_dh_grid(2 * E, dev)
+            self.loss_part = torch.zeros(ndh, native.DH_PARTIAL, dtype=f32, device=dev)
+            self.blk_active = torch.zeros(ndh, dtype=i32, device=dev)
+            self.act_list = torch.zeros(2 * E, dtype=i32, device=dev)
             self.loss_red = torch.zeros(native.DH_PARTIAL, dtype=f32, device=dev)
         self.host_dist = torch.zeros(T, B, dtype=f32, pin_memory=True)
         self.aux = torch.cuda.Stream(device=dev)      # reverse-CSR build overlaps the CBF kernel
@@ -285,10 +288,14 @@ class HipEngine:
             native.cbf_hfwd(S, idx, idx if self.reuse else idx1, src, nev, pw.cbf_w, pw.cbf_off["w1f"],
                             pw.cbf_rm, pw.cbf_v, hb, hm)
             native.cbf_dh(hb, hm, map1, src, nev, self.dang[:T], valid_u8, self.counts, dh, self.loss_part,
-                          grad_scale=gs)
+                          grad_scale=gs, blk_active=self.blk_active)
+            # backward over the evaluations with a nonzero upstream gradient only (exact: the
+            # others contribute zeros); node_reduce reads dE where dh != 0
+            act = self.act_list[: 2 * E]
+            nact = native.cbf_active(dh, nev, self.blk_active, act)
             native.cbf_bwd(S, idx, dh.view(2, T, B, N, K), pw.cbf_w, pw.cbf_off["w1f"], pw.cbf_rm, pw.cbf_v,
                            passes=2, dE=dE, partial=part_cbf, num_blocks=nbb, idx1=idx if self.reuse else idx1,
-                           src=src, nev=nev)
+                           src=src, nev=nev, act=act, nact=nact)
             native.reduce_rows(self.loss_part, self.loss_red)
         else:
             # ---- CBF: h, h', hinge losses, upstream grads and the full backward in ONE kernel
@@ -299,7 +306,8 @@ class HipEngine:
         cur.wait_event(csr_done)
         # no-BPTT: s_t is a detached input, only h'(s_{t+1}) gradients reach a_t
         native.node_reduce(dE, rptr, redges, self.dS, T=T, B=B, N=N, K=K, passes=2,
-                           pass_mask=0 if self.bptt else 2, shift1=G1, n_nodes=Nn, map1=map1)
+                           pass_mask=0 if self.bptt else 2, shift1=G1, n_nodes=Nn, map1=map1,
+                           gate=self.dhbuf[: 2 * E] if self.dedup else None)
         tm.mark("cbf")
         # ---- controller backward
         self.part_node.zero_()

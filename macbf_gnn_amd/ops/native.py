@@ -395,7 +395,7 @@ def cbf_dh_grid(EV: int, device) -> int:
     return max(1, min((EV + 8 * DH_BLOCK - 1) // (8 * DH_BLOCK), num_cu(device) * 16))
 
 
-def cbf_dh(h, hmask, map1, src, nev, dang, valid, counts, dh, partial, *, grad_scale=1.0):
+def cbf_dh(h, hmask, map1, src, nev, dang, valid, counts, dh, partial, *, grad_scale=1.0, blk_active=None):
     """Upstream dL/dh of every deduplicated evaluation (h-role + h'-role) and the 10 loss
     partial sums per block (slots as CBF_P_LOSS: [0, 0, 8 sums], padded) -> partial (nb, DH_PARTIAL)."""
     T, B, N, K = map1.shape
@@ -413,9 +413,24 @@ def cbf_dh(h, hmask, map1, src, nev, dang, valid, counts, dh, partial, *, grad_s
         raise NativeError(f"partial must be (nb, {DH_PARTIAL})")
     check(partial, torch.float32, None, "partial")
     nb = partial.shape[0]
+    check(blk_active, torch.int32, (nb,), "blk_active")
     _ok(lib().cbf_dh(ptr(h), ptr(hmask), ptr(map1), ptr(src), ptr(nev), ptr(dang), ptr(valid), B, T, N, K,
                      ptr(counts), LOSS_CONSTS[:6] + (LOSS_CONSTS[6] * float(grad_scale),), ptr(dh), ptr(partial),
-                     nb, stream_handle()), "cbf_dh")
+                     ptr(blk_active), nb, stream_handle()), "cbf_dh")
+
+
+def cbf_active(dh, nev, blk_active, act):
+    """Stable list of the evaluations with dh != 0 (cbf_dh's per-block counts blk_active, same
+    grid): act[:nact] in index order. Returns the device int32 tensor [nact]. The backward skips
+    the rest: their upstream gradient, hence every contribution, is exactly zero."""
+    check(dh, torch.float32, None, "dh")
+    check(nev, torch.int32, (1,), "nev")
+    check(blk_active, torch.int32, None, "blk_active")
+    check(act, torch.int32, (dh.numel(),), "act")
+    incl = torch.cumsum(blk_active, 0, dtype=torch.int32)
+    off = (incl - blk_active).contiguous()
+    _ok(lib().cbf_compact(ptr(dh), ptr(nev), ptr(off), ptr(act), blk_active.numel(), stream_handle()), "cbf_compact")
+    return incl[-1:].contiguous()
 
 
 def cbf_bwd_grid(EV: int, device) -> int:
@@ -423,7 +438,8 @@ def cbf_bwd_grid(EV: int, device) -> int:
 
 
 def cbf_bwd(S, idx, dh, wpack, f_bwd, wrm, wvec, *, passes=2, dE=None, partial=None, num_blocks=None,
-            fused=False, dang=None, valid=None, counts=None, idx1=None, grad_scale=1.0, src=None, nev=None):
+            fused=False, dang=None, valid=None, counts=None, idx1=None, grad_scale=1.0, src=None, nev=None,
+            act=None, nact=None):
     """dh (passes, T, B, N, K) -> dE (passes, T, B, N, K, 4), per-WG dW slabs (nb, CBF_PARTIAL).
 
     fused=True (training, passes=2): dh is not read; the kernel evaluates h and h' of every
@@ -453,6 +469,11 @@ def cbf_bwd(S, idx, dh, wpack, f_bwd, wrm, wvec, *, passes=2, dE=None, partial=N
             raise NativeError("deduplicated CBF backward is non-fused with passes=2")
         check(src, torch.int32, (2 * B * T * N * K,), "src")
         check(nev, torch.int32, (1,), "nev")
+    if act is not None:
+        if src is None:
+            raise NativeError("the active list needs the deduplicated evaluation list")
+        check(act, torch.int32, (2 * B * T * N * K,), "act")
+        check(nact, torch.int32, (1,), "nact")
     f16 = _half(wpack, "wpack")
     check(wpack, wpack.dtype, None, "wpack")
     check(wvec, torch.float32, None, "wvec")
@@ -472,7 +493,8 @@ def cbf_bwd(S, idx, dh, wpack, f_bwd, wrm, wvec, *, passes=2, dE=None, partial=N
                        float(C.DIST_MIN_THRES), float(C.CBF_DIST_EPS_COORD * D), int(fused), ptr(dang) if fused else 0,
                        ptr(valid) if fused else 0, ptr(counts) if fused else 0,
                        LOSS_CONSTS[:6] + (LOSS_CONSTS[6] * float(grad_scale),), ptr(idx1), D, nb,
-                       f16, ptr(src), ptr(nev) if src is not None else 0, stream_handle())
+                       f16, ptr(src), ptr(nev) if src is not None else 0, ptr(act), ptr(nact) if act is not None else 0,
+                       stream_handle())
     _ok(rc, "cbf_bwd")
     return nb
 
@@ -489,7 +511,7 @@ def rev_csr(idx, rptr, redges, n_nodes=None):
 
 
 def node_reduce(dE, rptr, redges, out, *, T, B, N, K, passes=2, accumulate=False, pass_mask=0, shift1=0,
-                n_nodes=None, map1=None):
+                n_nodes=None, map1=None, gate=None):
     """dE (passes, T, B, N, K, W) -> out[t'] (+)= sum over passes p of the edge->node reduction of
     step t' - p, for the N agents. pass_mask selects passes (0 = all); shift1=1: pass-1 edges live
     in graph t+1 (h' on the recomputed kNN of s_{t+1}), so the CSR arrays must hold T+1 graphs.
@@ -510,8 +532,10 @@ def node_reduce(dE, rptr, redges, out, *, T, B, N, K, passes=2, accumulate=False
         check(map1, torch.int32, (T, B, N, K), "map1")
         if passes != 2:
             raise NativeError("map1 needs passes=2")
+    if gate is not None:
+        check(gate, torch.float32, (passes * T * B * N * K,), "gate")
     _ok(lib().node_reduce(ptr(dE), ptr(rptr), ptr(redges), B, T, N, K, passes, int(accumulate), ptr(out),
-                          int(pass_mask), int(shift1), Nn, D, ptr(map1), stream_handle()), "node_reduce")
+                          int(pass_mask), int(shift1), Nn, D, ptr(map1), ptr(gate), stream_handle()), "node_reduce")
 
 
 def node_combine(dS_t, ego, dEc, rptr_t, redges_t, Gn, Gout, *, K, dt=C.TIME_STEP):
