@@ -53,6 +53,15 @@ def k_scan():
                 do_safety=True, n_agents=N)
 
 
+def k_scan_nosafe():
+    native.scan(eng.S[t], eng.idx[t], eng.dang[t], eng.cnt[t], eng.safe[t], K=K, do_knn=True,
+                do_safety=False, n_agents=N)
+
+
+def k_scan_safeonly():
+    native.scan(eng.S[t], None, None, None, eng.safe[t], K=K, do_knn=False, do_safety=True, n_agents=N)
+
+
 def k_fwd():
     native.ctrl_fwd(eng.S[t], eng.G, eng.idx[t], pw.ctrl_w, pw.ctrl_off["ew1f"], pw.ctrl_off["nw1f"], pw.ctrl_v,
                     eng.A[t], eng.S[t + 1], eng.dist[t], eng.act[t], pooled=eng.pooled[t], argmax=eng.argmax[t])
@@ -74,7 +83,7 @@ def k_comb():
 
 
 out = {"tag": args.tag}
-for name, fn in (("scan", k_scan), ("ctrl_fwd", k_fwd), ("node_bwd", k_node), ("edge_bwd", k_edge),
+for name, fn in (("scan", k_scan), ("scan_nosafe", k_scan_nosafe), ("scan_safeonly", k_scan_safeonly), ("ctrl_fwd", k_fwd), ("node_bwd", k_node), ("edge_bwd", k_edge),
                  ("combine", k_comb)):
     for _ in range(3):
         fn()
