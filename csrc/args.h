@@ -217,10 +217,25 @@ struct CombineArgs {
   float dt;
 };
 
+struct RolloutStatsArgs {
+  const float* dist;      // (T, B) per-env sum of |p_{t+1} - g| over the N agents
+  const float* cnt;       // (T, B, 2) dangerous / safe edge counts of step t
+  const float* safe;      // (T+1, B) safe-agent counts of s_t (or null)
+  const float* act;       // (T, B) per-env action-loss sums (or null)
+  int T, B, N;
+  float thr;              // DIST_MIN_CHECK
+  uint8_t* valid;         // (T, B) out
+  float* counts;          // [n_dang, n_safe, n_act] out (this rank)
+  float* local;           // [agent-steps, safe agents of s_{t+1}, action-loss sum] out
+};
+
 struct AdamArgs {
   float* param; const float* grad; float* m; float* v;
   int lo, hi;
   float b1, b2, eps, wd, step_size, bc2_sqrt;
+  const int* ok;          // optional device guard flag (0: skip the step)
+  const int* step;        // optional device step counter (bias corrections from *step + 1, lr)
+  float lr;
 };
 
 }  // namespace mb
@@ -249,6 +264,9 @@ int mb_node_reduce(const mb::NodeRedArgs* a, hipStream_t st);
 int mb_node_combine(const mb::CombineArgs* a, hipStream_t st);
 int mb_reduce_rows(const float* partial, int rows, int cols, float* out, int accumulate, hipStream_t st);
 int mb_adam(const mb::AdamArgs* a, hipStream_t st);
+int mb_rollout_stats(const mb::RolloutStatsArgs* a, hipStream_t st);
+int mb_grad_check(const float* g, int n, int* ok, hipStream_t st);
+int mb_adam_commit(const int* ok, int* steps, int mask, int ngroups, int* skipped, hipStream_t st);
 int mb_probe_mfma(const void* a, const void* b, float* d, hipStream_t st);
 int mb_probe_tr(const void* img, int rows, int stride, int e0, int m0, void* out, hipStream_t st);
 }

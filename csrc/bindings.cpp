@@ -174,9 +174,25 @@ static int reduce_rows(u64 partial, int rows, int cols, u64 out, int accumulate,
   return mb_reduce_rows(P<const float>(partial), rows, cols, P<float>(out), accumulate, ST(stream));
 }
 
+static int grad_check(u64 g, int n, u64 ok, u64 stream) { return mb_grad_check(P<const float>(g), n, P<int>(ok), ST(stream)); }
+
+static int adam_commit(u64 ok, u64 steps, int mask, int ngroups, u64 skipped, u64 stream) {
+  return mb_adam_commit(P<const int>(ok), P<int>(steps), mask, ngroups, P<int>(skipped), ST(stream));
+}
+
+static int rollout_stats(u64 dist, u64 cnt, u64 safe, u64 act, int T, int B, int N, float thr, u64 valid,
+                         u64 counts, u64 local, u64 stream) {
+  mb::RolloutStatsArgs a{};
+  a.dist = P<const float>(dist); a.cnt = P<const float>(cnt); a.safe = P<const float>(safe);
+  a.act = P<const float>(act); a.T = T; a.B = B; a.N = N; a.thr = thr; a.valid = P<uint8_t>(valid);
+  a.counts = P<float>(counts); a.local = P<float>(local);
+  return mb_rollout_stats(&a, ST(stream));
+}
+
 static int adam(u64 param, u64 grad, u64 m, u64 v, int lo, int hi, float b1, float b2, float eps, float wd,
-                float step_size, float bc2_sqrt, u64 stream) {
+                float step_size, float bc2_sqrt, u64 ok, u64 step, float lr, u64 stream) {
   mb::AdamArgs a{};
+  a.ok = P<const int>(ok); a.step = P<const int>(step); a.lr = lr;
   a.param = P<float>(param); a.grad = P<const float>(grad); a.m = P<float>(m); a.v = P<float>(v);
   a.lo = lo; a.hi = hi; a.b1 = b1; a.b2 = b2; a.eps = eps; a.wd = wd; a.step_size = step_size; a.bc2_sqrt = bc2_sqrt;
   return mb_adam(&a, ST(stream));
@@ -249,6 +265,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("cbf_compact", &cbf_compact);
   m.def("reduce_rows", &reduce_rows);
   m.def("adam", &adam);
+  m.def("rollout_stats", &rollout_stats);
+  m.def("grad_check", &grad_check);
+  m.def("adam_commit", &adam_commit);
   m.def("probe_mfma", &probe_mfma);
   m.def("probe_tr", &probe_tr);
   m.def("device_info", &device_info);

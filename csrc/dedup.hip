@@ -31,63 +31,93 @@ constexpr int MATCH_BLOCK = 256;
 constexpr int DH_BLOCK = 256;
 constexpr int DH_PARTIAL = 12;   // loss partials per block: [0, 0, 8 sums, 0, 0] (rows padded to 4)
 
-// 16 lanes per (t,b,i) row, lane k = slot k: coalesced slot loads / stores, the neighbour
-// matching by group shuffles, extras ranked by a group ballot (slot order).
-constexpr int MG = 16;
-
+// One thread per (t,b,i) row, MATCH_BLOCK consecutive rows per block: the block's slot rows of
+// step t and step t+1 (each one contiguous segment) are staged in LDS with coalesced loads, the
+// matching runs in registers, and map1 / the next row's src go back through LDS as coalesced
+// segments (extras are written directly: a few percent of the slots).
 __global__ __launch_bounds__(MATCH_BLOCK) void cbf_match_kernel(CbfMatchArgs a) {
+  __shared__ int s0[MATCH_BLOCK * 16], s1[MATCH_BLOCK * 16];
   const long BN = (long)a.B * a.N;
   const long rows = (long)a.T * BN;
-  const long row = ((long)blockIdx.x * MATCH_BLOCK + threadIdx.x) / MG;
-  const int k = threadIdx.x % MG;
-  if (row >= rows) return;                 // whole 16-lane groups
   const int K = a.K;
-  const int t = (int)(row / BN);
-  const bool has_next = t + 1 < a.T;
-  const long e0 = row * K;
   const long NKB = BN * K;                 // slots per step
   const long E = (long)a.T * NKB;
-  const bool act = k < K;
-  const int j0 = act ? a.idx[e0 + k] : -1;
-  const int j1 = (has_next && act) ? a.idx[e0 + NKB + k] : -2;
-  // m: slot of the next row holding the same neighbour (-1: none)
-  int m = -1;
-  if (has_next) {
+  const long row0 = (long)blockIdx.x * MATCH_BLOCK;
+  const int nr = (int)min((long)MATCH_BLOCK, rows - row0);
+  const long e00 = row0 * K;
+  const int ns = nr * K;
+  // next-step rows exist for rows < (T-1)*BN
+  const int nn = (int)max(0L, min((long)nr, (long)(a.T - 1) * BN - row0));
+  for (int q = threadIdx.x; q < ns; q += MATCH_BLOCK) s0[q] = a.idx[e00 + q];
+  for (int q = threadIdx.x; q < nn * K; q += MATCH_BLOCK) s1[q] = a.idx[e00 + NKB + q];
+  __syncthreads();
+  const int lr = threadIdx.x;
+  const long row = row0 + lr;
+  const bool live = lr < nr;
+  const bool has_next = lr < nn;
+  int m[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) m[k] = -1;
+  int nmatch = 0;
+  if (live && has_next) {
     if (a.mode == 1) {
-      m = act ? k : -1;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) m[k] = (k < K) ? k : -1;
+      nmatch = K;
     } else {
-      for (int q = 0; q < K; ++q) {
-        const int jq = __shfl(j1, q, MG);
-        if (act && jq == j0) m = q;
+      int j1[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) j1[q] = (q < K) ? s1[lr * K + q] : -2;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        if (k < K) {
+          const int j0 = s0[lr * K + k];
+          int mk = -1;
+#pragma unroll
+          for (int q = 0; q < 16; ++q) mk = (j1[q] == j0) ? q : mk;
+          m[k] = mk;
+          nmatch += (mk >= 0) ? 1 : 0;
+        }
       }
     }
   }
-  const bool extra = act && m < 0;
-  const unsigned long long bal = __ballot(extra);
-  const unsigned grp = (unsigned)(bal >> ((threadIdx.x % WAVE) & ~(MG - 1))) & 0xFFFFu;
   if (a.phase == 0) {
-    if (k == 0) a.cnt[row] = __popc(grp);
+    if (live) a.cnt[row] = K - nmatch;
     return;
   }
-  if (act) {
-    if (!extra) {
-      a.map1[e0 + k] = (int)(e0 + NKB + m);
-    } else {
-      const long x = E + a.off[row] + __popc(grp & ((1u << k) - 1u));
-      a.map1[e0 + k] = (int)x;
-      a.src[x] = (int)(e0 + k);
+  __syncthreads();                         // s0 / s1 are reused as output staging
+  const long e0 = row * K;
+  if (live) {
+    const long off = E + a.off[row];
+    int x = 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      if (k >= K) continue;
+      if (m[k] >= 0) {
+        s0[lr * K + k] = (int)(e0 + NKB + m[k]);
+      } else {
+        s0[lr * K + k] = (int)(off + x);
+        a.src[off + x] = (int)(e0 + k);
+        ++x;
+      }
+    }
+    if (has_next) {
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        if (q >= K) continue;
+        int sv = -1;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) sv = (m[k] == q) ? (int)(e0 + k) : sv;
+        s1[lr * K + q] = sv;
+      }
     }
   }
-  // src of the next row's main slots (written by this row: the only possible source)
-  if (has_next) {
-    int s = -1;
-    for (int q = 0; q < K; ++q) {
-      const int mq = __shfl(m, q, MG);
-      if (mq == k) s = (int)(e0 + q);
-    }
-    if (act) a.src[e0 + NKB + k] = s;
-  }
-  if (t == 0 && act) a.src[e0 + k] = -1;
+  __syncthreads();
+  for (int q = threadIdx.x; q < ns; q += MATCH_BLOCK) a.map1[e00 + q] = s0[q];
+  for (int q = threadIdx.x; q < nn * K; q += MATCH_BLOCK) a.src[e00 + NKB + q] = s1[q];
+  // first step: its main slots have no source
+  const long first = min((long)ns, max(0L, NKB - e00));
+  for (long q = threadIdx.x; q < first; q += MATCH_BLOCK) a.src[e00 + q] = -1;
 }
 
 // evaluations per dh / compact block: a multiple of DH_BLOCK, the same in both kernels
@@ -225,8 +255,8 @@ extern "C" int mb_cbf_compact(const float* dh, const int* nev, const int* blk_of
 extern "C" int mb_cbf_match(const mb::CbfMatchArgs* a, hipStream_t st) {
   using namespace mb;
   if (a->K < 1 || a->K > 16 || a->T < 1) return -1;
-  const long lanes = (long)a->T * a->B * a->N * MG;
-  hipLaunchKernelGGL(cbf_match_kernel, dim3((unsigned)((lanes + MATCH_BLOCK - 1) / MATCH_BLOCK)), dim3(MATCH_BLOCK),
+  const long rows = (long)a->T * a->B * a->N;
+  hipLaunchKernelGGL(cbf_match_kernel, dim3((unsigned)((rows + MATCH_BLOCK - 1) / MATCH_BLOCK)), dim3(MATCH_BLOCK),
                      0, st, *a);
   return (int)hipGetLastError();
 }

@@ -46,6 +46,15 @@ __global__ __launch_bounds__(RR_COLS * RR_SLICES) void reduce_rows_kernel(const 
 __global__ __launch_bounds__(256) void adam_kernel(AdamArgs a) {
   const int i = a.lo + blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= a.hi) return;
+  // device-side failure guard: a non-finite reduced gradient skips the whole step (the flag is
+  // the same on every rank after the all-reduce), with no host round trip
+  if (a.ok && *a.ok == 0) return;
+  float step_size = a.step_size, bc2_sqrt = a.bc2_sqrt;
+  if (a.step) {   // bias corrections of step t = *step + 1 (torch.optim.Adam, in double)
+    const double t = (double)(*a.step + 1);
+    step_size = (float)((double)a.lr / (1.0 - pow((double)a.b1, t)));
+    bc2_sqrt = (float)sqrt(1.0 - pow((double)a.b2, t));
+  }
   float g = a.grad[i];
   float p = a.param[i];
   if (a.wd != 0.f) g = g + a.wd * p;
@@ -54,11 +63,93 @@ __global__ __launch_bounds__(256) void adam_kernel(AdamArgs a) {
   v = a.b2 * v + (1.f - a.b2) * g * g;
   a.m[i] = m;
   a.v[i] = v;
-  const float denom = sqrtf(v) / a.bc2_sqrt + a.eps;
-  a.param[i] = p - a.step_size * (m / denom);
+  const float denom = sqrtf(v) / bc2_sqrt + a.eps;
+  a.param[i] = p - step_size * (m / denom);
+}
+
+// ok = 0 if any gradient element is not finite (ok preset to 1 by the caller)
+__global__ __launch_bounds__(256) void grad_check_kernel(const float* g, int n, int* ok) {
+  bool bad = false;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) bad = bad || !isfinite(g[i]);
+  if (__any(bad) && (threadIdx.x % WAVE) == 0) *ok = 0;
+}
+
+// after the Adam launches of one iteration: steps[g] += 1 for the stepped groups (bit g of
+// mask) if the step was taken, else skipped += 1
+__global__ void adam_commit_kernel(const int* ok, int* steps, int mask, int ngroups, int* skipped) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  if (*ok) {
+    for (int g = 0; g < ngroups; ++g)
+      if ((mask >> g) & 1) steps[g] += 1;
+  } else {
+    *skipped += 1;
+  }
+}
+
+// Post-rollout bookkeeping in one launch (replaces ~20 small tensor ops between the rollout
+// and the backward). Env b's step t is valid iff the env was not done before t, done after
+// step t meaning dist[t, b] / N < thr (train.py:78-81 with per-env masks). Outputs the (T, B)
+// validity mask, the pooled counts [n_dang, n_safe, n_act] of this rank (all-reduced by the
+// caller) and the local stats [agent-steps, safe agents of s_{t+1}, action-loss sum]. One
+// block, fixed-order reduction: deterministic.
+constexpr int RS_BLOCK = 256;
+__global__ __launch_bounds__(RS_BLOCK) void rollout_stats_kernel(RolloutStatsArgs a) {
+  float v[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int b = threadIdx.x; b < a.B; b += RS_BLOCK) {
+    bool done = false;
+    for (int t = 0; t < a.T; ++t) {
+      const bool vl = !done;
+      a.valid[t * a.B + b] = vl ? 1 : 0;
+      if (vl) {
+        v[0] += a.cnt[(t * a.B + b) * 2];
+        v[1] += a.cnt[(t * a.B + b) * 2 + 1];
+        v[2] += (float)a.N;
+        if (a.safe) v[3] += a.safe[(t + 1) * a.B + b];
+        if (a.act) v[4] += a.act[t * a.B + b];
+      }
+      done = done || (a.dist[t * a.B + b] / (float)a.N < a.thr);
+    }
+  }
+  __shared__ float red[6][RS_BLOCK];
+#pragma unroll
+  for (int q = 0; q < 5; ++q) red[q][threadIdx.x] = v[q];
+  __syncthreads();
+  for (int o = RS_BLOCK / 2; o > 0; o >>= 1) {
+    if (threadIdx.x < o)
+#pragma unroll
+      for (int q = 0; q < 5; ++q) red[q][threadIdx.x] += red[q][threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    a.counts[0] = red[0][0];
+    a.counts[1] = red[1][0];
+    a.counts[2] = red[2][0];
+    a.local[0] = red[2][0];
+    a.local[1] = red[3][0];
+    a.local[2] = red[4][0];
+  }
 }
 
 }  // namespace mb
+
+extern "C" int mb_grad_check(const float* g, int n, int* ok, hipStream_t st) {
+  using namespace mb;
+  const int blocks = (n + 255) / 256 < 256 ? (n + 255) / 256 : 256;
+  hipLaunchKernelGGL(grad_check_kernel, dim3(blocks > 0 ? blocks : 1), dim3(256), 0, st, g, n, ok);
+  return (int)hipGetLastError();
+}
+
+extern "C" int mb_adam_commit(const int* ok, int* steps, int mask, int ngroups, int* skipped, hipStream_t st) {
+  using namespace mb;
+  hipLaunchKernelGGL(adam_commit_kernel, dim3(1), dim3(64), 0, st, ok, steps, mask, ngroups, skipped);
+  return (int)hipGetLastError();
+}
+
+extern "C" int mb_rollout_stats(const mb::RolloutStatsArgs* a, hipStream_t st) {
+  using namespace mb;
+  hipLaunchKernelGGL(rollout_stats_kernel, dim3(1), dim3(RS_BLOCK), 0, st, *a);
+  return (int)hipGetLastError();
+}
 
 extern "C" int mb_reduce_rows(const float* partial, int rows, int cols, float* out, int accumulate, hipStream_t st) {
   if (cols % 4) return -1;

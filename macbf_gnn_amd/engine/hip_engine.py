@@ -95,6 +95,8 @@ class HipEngine:
         self.ego = torch.zeros(B, N, W, dtype=f32, device=dev)
         self.dEc = torch.zeros(B, N, K, W, dtype=f32, device=dev)
         self.counts = torch.zeros(3, dtype=f32, device=dev)
+        self.local = torch.zeros(3, dtype=f32, device=dev)        # agent-steps, safe agents, action-loss sum
+        self.valid_buf = torch.zeros(T, B, dtype=u8, device=dev)
         self.act_scale = torch.zeros(1, dtype=f32, device=dev)      # action-loss coefficient
         self.nb_node, self.nb_edge = native.ctrl_bwd_grids(B * N, dev)
         self.part_node = torch.zeros(self.nb_node, native.CTRL_NODE_PARTIAL, dtype=f32, device=dev)
@@ -153,6 +155,7 @@ class HipEngine:
         self.act.zero_()
         events = []
         T = self.Tmax
+        tail_scanned = False
         for t in range(self.Tmax):
             native.scan(self.S[t], self.idx[t], self.dang[t], self.cnt[t], self.safe[t], K=K,
                         do_knn=True, do_safety=cfg.compute_safety, n_agents=N)
@@ -173,9 +176,14 @@ class HipEngine:
                 if t >= 1:
                     events[t - 1].synchronize()
                     if self._all_done(t - 1):
-                        T = t + 1   # step t was already issued; its envs are masked out
+                        # every env was done after step t-1: the trajectory is steps 0..t-1 (as
+                        # in train.py:78-81). Step t was already issued; its scan already gave
+                        # the kNN graph / safety of the final state s_t, its controller step is
+                        # simply not used.
+                        T = t
+                        tail_scanned = True
                         break
-        if cfg.compute_safety or not self.reuse:
+        if (cfg.compute_safety or not self.reuse) and not tail_scanned:
             # safety of the final state; with reuse_nbr_idx=False also the kNN graph of s_T (for h')
             native.scan(self.S[T], self.idx[T] if not self.reuse else None, None, None,
                         self.safe[T] if cfg.compute_safety else None, K=K, do_knn=not self.reuse,
@@ -235,16 +243,12 @@ class HipEngine:
             tm.enabled = en
 
     def _counts(self, T):
-        """Validity mask (T, B) and the pooled counts [n_dang, n_safe, n_act] of this rank."""
-        N = self.N
-        # validity: step t of env b counts iff the env was not done before t
-        done = (self.dist[:T] / N) < C.DIST_MIN_CHECK                 # (T, B)
-        di = done.to(torch.int32)
-        valid = ((torch.cumsum(di, 0) - di) == 0)
-        vf = valid.to(torch.float32)
-        self.counts[0] = (self.cnt[:T, :, 0] * vf).sum()
-        self.counts[1] = (self.cnt[:T, :, 1] * vf).sum()
-        self.counts[2] = vf.sum() * N
+        """Validity mask (T, B) uint8 and the pooled counts [n_dang, n_safe, n_act] of this rank
+        (+ the local stats in self.local), one kernel: step t of env b counts iff the env was
+        not done before t."""
+        valid = self.valid_buf[:T]
+        native.rollout_stats(self.dist[:T], self.cnt[:T], self.safe[: T + 1], self.act[:T], valid,
+                             self.counts, self.local, N=self.N)
         return valid
 
     def _backward(self, T, valid):
@@ -255,8 +259,7 @@ class HipEngine:
         # loss scale of the upstream gradients (fp16: dynamic, trainer-owned; bf16: 1). Every
         # backward quantity is linear in it; the flat gradient is unscaled after the slab reduce.
         gs = float(tr.grad_scale)
-        valid_u8 = valid.to(torch.uint8).contiguous()
-        vf = valid.to(torch.float32)
+        valid_u8 = valid
         n_act = self.counts[2].clamp_min(1.0)
         # action-loss coefficient stays on the device (read by ctrl_node_bwd): no host sync
         torch.div(C.LOSS_SCALE * C.LOSS_WEIGHTS[4], n_act.view(1), out=self.act_scale)
@@ -361,19 +364,18 @@ class HipEngine:
                 self.red_cbf[native.CBF_P_LOSS: native.CBF_P_LOSS + 10]).to(torch.float64)
         nd = 1e-5 + self.counts[0].double()
         ns = 1e-5 + self.counts[1].double()
-        act_sum = (self.act[:T].double() * valid.double()).sum()
+        act_sum = self.local[2].double()
         w = C.LOSS_WEIGHTS
         ld, ls, ldd, lsd = sums[2] / nd, sums[3] / ns, sums[6] / nd, sums[7] / ns
         la = act_sum / n_act.double()
         total = C.LOSS_SCALE * (w[0] * ld + w[1] * ls + w[2] * ldd + w[3] * lsd + w[4] * la)
-        safe_next = self.safe[1: T + 1]                               # safety of s_{t+1}
         return {
             "loss_total": total, "loss_dang": ld, "loss_safe": ls, "loss_dang_deriv": ldd,
             "loss_safe_deriv": lsd, "loss_action": la,
             "acc_dang_sum": sums[4], "acc_safe_sum": sums[5], "acc_dang_deriv_sum": sums[8],
             "acc_safe_deriv_sum": sums[9], "n_dang": self.counts[0], "n_safe": self.counts[1],
-            "agent_steps": vf.sum() * N, "safe_agents": (safe_next * vf).sum(),
-            "T": T if not self.graph_mode else valid.any(1).sum().to(torch.float64),
+            "agent_steps": self.local[0].double(), "safe_agents": self.local[1].double(),
+            "T": T if not self.graph_mode else (valid != 0).any(1).sum().to(torch.float64),
         }
 
     def _buf(self, cache, key, cols):

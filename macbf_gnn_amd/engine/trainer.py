@@ -65,7 +65,7 @@ class Trainer:
         self.torch_gen.manual_seed(cfg.seed * 1000003 + dp.rank)
         self.logger = MetricsLogger(dp, cfg.log_path)
         self.timer = PhaseTimer(self.device, enabled=cfg.phase_timing)
-        self.skipped_steps = 0
+        self._host_skipped = 0
         # fp16 mixed precision: dynamic loss scaling. The scale multiplies the
         # in-kernel upstream gradients and is divided out of the flat gradient before the
         # all-reduce; a non-finite step is skipped and halves it.
@@ -77,6 +77,7 @@ class Trainer:
             else None
         if self.device.type == "cuda":
             from .hip_engine import HipEngine
+            self._ok = torch.ones(1, dtype=torch.int32, device=self.device)
             self.engine = HipEngine(self)
         else:
             from .oracle_engine import OracleEngine
@@ -145,8 +146,17 @@ class Trainer:
         tm.mark("allreduce")
         # failure detection: a non-finite reduced gradient is identical on every
         # rank, so every rank skips the same step; parameters and Adam state stay untouched
-        if (self.cfg.nan_guard or self.fp16) and not bool(torch.isfinite(self.fp.grad).all()):
-            self.skipped_steps += 1
+        if self.device.type == "cuda" and self.cfg.nan_guard and not self.fp16:
+            # on the device: a flag gates the fused Adam kernel (no host round trip per step);
+            # the skipped-step count is read lazily
+            self._ok.fill_(1)
+            from ..ops import native
+            native.grad_check(self.fp.grad, self._ok)
+            self.opt.step(self.groups_to_step(), ok=self._ok)
+            self.engine.after_update()
+            stats["skipped"] = 1 - self._ok[0]
+        elif (self.cfg.nan_guard or self.fp16) and not bool(torch.isfinite(self.fp.grad).all()):
+            self._host_skipped += 1
             stats["skipped"] = 1
             if self.fp16:
                 self.grad_scale = max(self.grad_scale * 0.5, 1.0)
@@ -169,6 +179,14 @@ class Trainer:
         if tm.enabled:
             stats["phases_ms"] = tm.results()
         return stats
+
+    @property
+    def skipped_steps(self) -> int:
+        """Optimizer steps skipped by the failure guard (host path + device-side guard)."""
+        n = self._host_skipped
+        if getattr(self.opt, "on_device", False):
+            n += int(self.opt.dskipped.item())
+        return n
 
     def fit(self, steps: Optional[int] = None, progress: bool = False):
         """Train ``steps`` iterations; by default up to ``cfg.train_steps`` in total, so a run

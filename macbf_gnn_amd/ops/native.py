@@ -629,12 +629,52 @@ def reduce_rows(partial, out, accumulate=False):
     _ok(lib().reduce_rows(ptr(partial), rows, cols, ptr(out), int(accumulate), stream_handle()), "reduce_rows")
 
 
-def adam(param, grad, m, v, lo, hi, lr, b1, b2, eps, wd, step):
+def rollout_stats(dist, cnt, safe, act, valid, counts, local, *, N):
+    """dist/act (T,B), cnt (T,B,2), safe (T+1,B) or None -> valid (T,B) u8, counts[:3] =
+    [n_dang, n_safe, n_act] of this rank, local[:3] = [agent-steps, safe agents of s_{t+1},
+    action-loss sum]. One launch, deterministic."""
+    T, B = dist.shape
+    check(dist, torch.float32, (T, B), "dist")
+    check(cnt, torch.float32, (T, B, 2), "cnt")
+    check(safe, torch.float32, (T + 1, B), "safe")
+    check(act, torch.float32, (T, B), "act")
+    check(valid, torch.uint8, (T, B), "valid")
+    check(counts, torch.float32, None, "counts")
+    check(local, torch.float32, None, "local")
+    if counts.numel() < 3 or local.numel() < 3:
+        raise NativeError("counts / local need 3 slots")
+    _ok(lib().rollout_stats(ptr(dist), ptr(cnt), ptr(safe), ptr(act), T, B, int(N), float(C.DIST_MIN_CHECK),
+                            ptr(valid), ptr(counts), ptr(local), stream_handle()), "rollout_stats")
+
+
+def adam(param, grad, m, v, lo, hi, lr, b1, b2, eps, wd, step, ok=None, step_dev=None):
+    """Fused Adam over param[lo:hi]. step: host step count (bias corrections), or step_dev: a
+    1-element device int32 counter (step = *step_dev + 1, read by the kernel); ok: optional
+    device int32 guard flag (0 -> the kernel leaves everything untouched)."""
     for t, n in ((param, "param"), (grad, "grad"), (m, "m"), (v, "v")):
         check(t, torch.float32, (param.numel(),), n)
     if not (0 <= lo <= hi <= param.numel()):
         raise NativeError("bad Adam range")
-    bc1 = 1.0 - b1 ** step
-    bc2 = 1.0 - b2 ** step
+    check(ok, torch.int32, None, "ok")
+    check(step_dev, torch.int32, None, "step_dev")
+    bc1 = 1.0 - b1 ** max(step, 1)
+    bc2 = 1.0 - b2 ** max(step, 1)
     _ok(lib().adam(ptr(param), ptr(grad), ptr(m), ptr(v), int(lo), int(hi), float(b1), float(b2), float(eps),
-                   float(wd), float(lr / bc1), float(bc2 ** 0.5), stream_handle()), "adam")
+                   float(wd), float(lr / bc1), float(bc2 ** 0.5), ptr(ok), ptr(step_dev), float(lr),
+                   stream_handle()), "adam")
+
+
+def grad_check(g, ok):
+    """ok (int32, preset to 1) <- 0 if any element of g is not finite. No host sync."""
+    check(g, torch.float32, None, "g")
+    check(ok, torch.int32, None, "ok")
+    _ok(lib().grad_check(ptr(g), g.numel(), ptr(ok), stream_handle()), "grad_check")
+
+
+def adam_commit(ok, steps, mask, skipped):
+    """steps[g] += 1 for the groups in mask if *ok, else skipped += 1 (device counters)."""
+    check(ok, torch.int32, None, "ok")
+    check(steps, torch.int32, None, "steps")
+    check(skipped, torch.int32, None, "skipped")
+    _ok(lib().adam_commit(ptr(ok), ptr(steps), int(mask), steps.numel(), ptr(skipped), stream_handle()),
+        "adam_commit")

@@ -90,20 +90,53 @@ class FlatAdam:
         self.lr, self.betas, self.eps, self.wd = lr, betas, eps, weight_decay
         self.exp_avg = torch.zeros_like(fp.flat)
         self.exp_avg_sq = torch.zeros_like(fp.flat)
-        self.steps = {name: 0 for name in fp.ranges}
+        self._names = list(fp.ranges)
+        self.on_device = fp.flat.device.type != "cpu"
+        self._steps = {name: 0 for name in fp.ranges}
+        if self.on_device:
+            # step counters and the skipped-step count live on the device: the fused Adam kernel
+            # reads them (bias corrections) and a guard flag, so a step needs no host round trip
+            dev = fp.flat.device
+            self._dsteps = torch.zeros(len(self._names), dtype=torch.int32, device=dev)
+            self.dskipped = torch.zeros(1, dtype=torch.int32, device=dev)
+            self._one = torch.ones(1, dtype=torch.int32, device=dev)
 
-    def step(self, groups=None):
+    @property
+    def steps(self):
+        """Per-group step counts (host dict; synchronises with the device counters on HIP)."""
+        if self.on_device:
+            v = self._dsteps.tolist()
+            return {n: int(v[i]) for i, n in enumerate(self._names)}
+        return dict(self._steps)
+
+    def set_step(self, name, step):
+        if self.on_device:
+            self._dsteps[self._names.index(name)] = int(step)
+        else:
+            self._steps[name] = int(step)
+
+    def step(self, groups=None, ok=None):
+        """One Adam step of the named ranges. On HIP, ok (device int32 flag, optional) gates the
+        whole step on the device: 0 leaves parameters, moments and step counts untouched and
+        counts a skipped step."""
         groups = list(self.fp.ranges) if groups is None else list(groups)
+        if self.on_device:
+            from ..ops import native
+            flag = self._one if ok is None else ok
+            mask = 0
+            for name in groups:
+                a, b = self.fp.ranges[name]
+                gi = self._names.index(name)
+                native.adam(self.fp.flat, self.fp.grad, self.exp_avg, self.exp_avg_sq, a, b,
+                            self.lr, self.betas[0], self.betas[1], self.eps, self.wd, 1, ok=flag,
+                            step_dev=self._dsteps[gi:gi + 1])
+                mask |= 1 << gi
+            native.adam_commit(flag, self._dsteps, mask, self.dskipped)
+            return
         for name in groups:
             a, b = self.fp.ranges[name]
-            self.steps[name] += 1
-            t = self.steps[name]
-            if self.fp.flat.device.type != "cpu":
-                from ..ops import native
-                native.adam(self.fp.flat, self.fp.grad, self.exp_avg, self.exp_avg_sq, a, b,
-                            self.lr, self.betas[0], self.betas[1], self.eps, self.wd, t)
-            else:
-                self._step_torch(a, b, t)
+            self._steps[name] += 1
+            self._step_torch(a, b, self._steps[name])
 
     def _step_torch(self, a, b, t):
         b1, b2 = self.betas
@@ -125,11 +158,12 @@ class FlatAdam:
         a, _ = self.fp.ranges[name]
         state, ids = {}, []
         i = 0
+        nstep = self.steps[name]
         for m, pn, shape, o, n in self.fp.specs:
             if m != name:
                 continue
-            if self.steps[name] > 0:
-                state[i] = {"step": torch.tensor(float(self.steps[name])),
+            if nstep > 0:
+                state[i] = {"step": torch.tensor(float(nstep)),
                             "exp_avg": self.exp_avg[o:o + n].view(shape).detach().cpu().clone(),
                             "exp_avg_sq": self.exp_avg_sq[o:o + n].view(shape).detach().cpu().clone()}
             ids.append(i)
@@ -152,4 +186,4 @@ class FlatAdam:
                 self.exp_avg_sq[o:o + n].copy_(st["exp_avg_sq"].reshape(-1))
                 step = int(float(st["step"]))
             i += 1
-        self.steps[name] = step
+        self.set_step(name, step)

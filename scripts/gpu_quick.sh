@@ -12,7 +12,7 @@ if [ $# -gt 0 ]; then
 fi
 timeout -k 10 300 python scripts/micro_step.py --tag $TAG > gpurun_out/${TAG}_micro.log 2>&1 || { tail -5 gpurun_out/${TAG}_micro.log; exit 1; }
 tail -1 gpurun_out/${TAG}_micro.log
-timeout -k 10 300 python bench.py --steps 6 --warmup 2 --phases > gpurun_out/${TAG}_bench.log 2>&1 || { tail -5 gpurun_out/${TAG}_bench.log; exit 1; }
+timeout -k 10 300 python bench.py --steps 20 --warmup 3 --phases > gpurun_out/${TAG}_bench.log 2>&1 || { tail -5 gpurun_out/${TAG}_bench.log; exit 1; }
 tail -1 gpurun_out/${TAG}_bench.log | cut -c1-200
 if [ $PROF = 1 ]; then
   cd /tmp && export TMPDIR=/tmp

@@ -322,3 +322,51 @@ def test_graph_mode_training_runs():
     torch.cuda.synchronize()
     assert torch.isfinite(tr.fp.flat).all() and not torch.equal(before, tr.fp.flat)
     assert 1 <= float(st["T"]) <= 10
+
+
+def test_device_nan_guard_skips_step_without_host_sync():
+    """HIP bf16 path: a non-finite reduced gradient is caught on the device (flag -> fused
+    Adam), parameters / moments / step counts stay untouched, the skip is counted."""
+    tr = _trainer(DEV, N=32, B=2, T=4)
+    before = tr.fp.flat.clone()
+    m_before = tr.opt.exp_avg.clone()
+    real_step = tr.engine.step
+
+    def poisoned(s0, g0, obs=None):
+        st = real_step(s0, g0, obs)
+        tr.fp.grad[5] = float("inf")
+        return st
+
+    tr.engine.step = poisoned
+    st = tr.train_step()
+    torch.cuda.synchronize()
+    assert int(st["skipped"]) == 1 and tr.skipped_steps == 1
+    assert torch.equal(before, tr.fp.flat) and torch.equal(m_before, tr.opt.exp_avg)
+    assert tr.opt.steps == {"controller": 0, "cbf": 0}
+    tr.engine.step = real_step
+    st = tr.train_step()
+    assert int(st["skipped"]) == 0 and tr.skipped_steps == 1
+    assert not torch.equal(before, tr.fp.flat)
+    assert tr.opt.steps == {"controller": 1, "cbf": 1}
+
+
+def test_device_adam_matches_torch_adam():
+    """Fused Adam with device step counters == torch.optim.Adam (L2 weight decay)."""
+    from macbf_gnn_amd.utils.params import FlatAdam
+    ctrl, cbf, fp, _ = _nets(3)
+    ref = [p.detach().clone().requires_grad_(True) for p in fp._params()]
+    opt_ref = torch.optim.Adam(ref, lr=1e-3, weight_decay=1e-2)
+    opt = FlatAdam(fp, lr=1e-3, weight_decay=1e-2)
+    g = torch.Generator(device="cpu").manual_seed(0)
+    for _ in range(5):
+        fp.grad.copy_(torch.randn(fp.grad.shape, generator=g).to(DEV))
+        off = 0
+        for p in ref:
+            p.grad = fp.grad[off:off + p.numel()].view_as(p).clone()
+            off += p.numel()
+        opt_ref.step()
+        opt.step()
+    got = fp.flat
+    want = torch.cat([p.detach().reshape(-1) for p in ref])
+    torch.testing.assert_close(got, want, rtol=1e-5, atol=1e-6)
+    assert opt.steps == {"controller": 5, "cbf": 5}
