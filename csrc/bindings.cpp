@@ -174,6 +174,12 @@ static int reduce_rows(u64 partial, int rows, int cols, u64 out, int accumulate,
   return mb_reduce_rows(P<const float>(partial), rows, cols, P<float>(out), accumulate, ST(stream));
 }
 
+static int pack_gather(u64 src, int n, u64 idx16, int m16, u64 out16, int f16, u64 idx32, int m32, u64 out32,
+                       u64 stream) {
+  return mb_pack_gather(P<const float>(src), n, P<const int>(idx16), m16, P<unsigned short>(out16), f16,
+                        P<const int>(idx32), m32, P<float>(out32), ST(stream));
+}
+
 static int grad_check(u64 g, int n, u64 ok, u64 stream) { return mb_grad_check(P<const float>(g), n, P<int>(ok), ST(stream)); }
 
 static int adam_commit(u64 ok, u64 steps, int mask, int ngroups, u64 skipped, u64 stream) {
@@ -267,6 +273,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("adam", &adam);
   m.def("rollout_stats", &rollout_stats);
   m.def("grad_check", &grad_check);
+  m.def("pack_gather", &pack_gather);
   m.def("adam_commit", &adam_commit);
   m.def("probe_mfma", &probe_mfma);
   m.def("probe_tr", &probe_tr);

@@ -67,6 +67,32 @@ __global__ __launch_bounds__(256) void adam_kernel(AdamArgs a) {
   a.param[i] = p - step_size * (m / denom);
 }
 
+// Weight repacking after an optimizer step: every MFMA fragment / row-major image / side vector
+// of both networks is a gather of the flat fp32 master parameters (index maps from
+// ops/layout.py; index n = constant 0, n + 1 = constant 1), in ONE launch: 16-bit outputs
+// (bf16 RNE or fp16) then fp32 outputs.
+__global__ __launch_bounds__(256) void pack_gather_kernel(const float* src, int n, const int* idx16, int m16,
+                                                          unsigned short* out16, int f16, const int* idx32, int m32,
+                                                          float* out32) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < m16) {
+    const int k = idx16[i];
+    const float v = k < n ? src[k] : (k == n ? 0.f : 1.f);
+    unsigned short hbits;
+    if (f16) {
+      const _Float16 hv = (_Float16)v;
+      hbits = __builtin_bit_cast(unsigned short, hv);
+    } else {
+      const __bf16 bv = (__bf16)v;                     // round to nearest even
+      hbits = __builtin_bit_cast(unsigned short, bv);
+    }
+    out16[i] = hbits;
+  } else if (i < m16 + m32) {
+    const int k = idx32[i - m16];
+    out32[i - m16] = k < n ? src[k] : (k == n ? 0.f : 1.f);
+  }
+}
+
 // ok = 0 if any gradient element is not finite (ok preset to 1 by the caller)
 __global__ __launch_bounds__(256) void grad_check_kernel(const float* g, int n, int* ok) {
   bool bad = false;
@@ -131,6 +157,15 @@ __global__ __launch_bounds__(RS_BLOCK) void rollout_stats_kernel(RolloutStatsArg
 }
 
 }  // namespace mb
+
+extern "C" int mb_pack_gather(const float* src, int n, const int* idx16, int m16, unsigned short* out16, int f16,
+                              const int* idx32, int m32, float* out32, hipStream_t st) {
+  using namespace mb;
+  const int tot = m16 + m32;
+  hipLaunchKernelGGL(pack_gather_kernel, dim3((tot + 255) / 256), dim3(256), 0, st, src, n, idx16, m16, out16, f16,
+                     idx32, m32, out32);
+  return (int)hipGetLastError();
+}
 
 extern "C" int mb_grad_check(const float* g, int n, int* ok, hipStream_t st) {
   using namespace mb;

@@ -96,6 +96,7 @@ class HipEngine:
         self.dEc = torch.zeros(B, N, K, W, dtype=f32, device=dev)
         self.counts = torch.zeros(3, dtype=f32, device=dev)
         self.local = torch.zeros(3, dtype=f32, device=dev)        # agent-steps, safe agents, action-loss sum
+        self.raw_stats = torch.zeros(16, dtype=f32, device=dev)   # utils.metrics.StepStats layout
         self.valid_buf = torch.zeros(T, B, dtype=u8, device=dev)
         self.act_scale = torch.zeros(1, dtype=f32, device=dev)      # action-loss coefficient
         self.nb_node, self.nb_edge = native.ctrl_bwd_grids(B * N, dev)
@@ -204,7 +205,7 @@ class HipEngine:
         valid = self._counts(T)
         self.tr.dp.all_reduce_(self.counts)
         tm.mark("counts")
-        return self._backward(T, valid)
+        return self._stats(*self._backward(T, valid))
 
     # ------------------------------------------------------------------ graph mode
     def _step_graph(self, s0, g, obs):
@@ -216,7 +217,7 @@ class HipEngine:
         self._graphs[0].replay()
         self.tr.dp.all_reduce_(self.counts)
         self._graphs[1].replay()
-        return self._graph_stats
+        return self._stats(*self._graph_stats)
 
     def _capture(self):
         T = self.Tmax
@@ -359,24 +360,15 @@ class HipEngine:
         if gs != 1.0:
             fg.mul_(1.0 / gs)
         tm.mark("grad_reduce")
-        # ---- stats (device tensors; converted lazily by the logger)
-        sums = (self.loss_red[:10] if self.dedup else
-                self.red_cbf[native.CBF_P_LOSS: native.CBF_P_LOSS + 10]).to(torch.float64)
-        nd = 1e-5 + self.counts[0].double()
-        ns = 1e-5 + self.counts[1].double()
-        act_sum = self.local[2].double()
-        w = C.LOSS_WEIGHTS
-        ld, ls, ldd, lsd = sums[2] / nd, sums[3] / ns, sums[6] / nd, sums[7] / ns
-        la = act_sum / n_act.double()
-        total = C.LOSS_SCALE * (w[0] * ld + w[1] * ls + w[2] * ldd + w[3] * lsd + w[4] * la)
-        return {
-            "loss_total": total, "loss_dang": ld, "loss_safe": ls, "loss_dang_deriv": ldd,
-            "loss_safe_deriv": lsd, "loss_action": la,
-            "acc_dang_sum": sums[4], "acc_safe_sum": sums[5], "acc_dang_deriv_sum": sums[8],
-            "acc_safe_deriv_sum": sums[9], "n_dang": self.counts[0], "n_safe": self.counts[1],
-            "agent_steps": self.local[0].double(), "safe_agents": self.local[1].double(),
-            "T": T if not self.graph_mode else (valid != 0).any(1).sum().to(torch.float64),
-        }
+        # ---- stats: one raw device vector (no per-statistic kernels), derived lazily on read
+        sums = self.loss_red[:10] if self.dedup else self.red_cbf[native.CBF_P_LOSS: native.CBF_P_LOSS + 10]
+        torch.cat([sums, self.counts, self.local], out=self.raw_stats)
+        Tv = T if not self.graph_mode else (valid != 0).any(1).sum()
+        return self.raw_stats, Tv
+
+    def _stats(self, raw, T):
+        from ..utils.metrics import StepStats
+        return StepStats(raw.clone(), T.clone() if isinstance(T, torch.Tensor) else T)
 
     def _buf(self, cache, key, cols):
         b = cache.get(key)

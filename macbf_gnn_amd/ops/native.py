@@ -664,6 +664,20 @@ def adam(param, grad, m, v, lo, hi, lr, b1, b2, eps, wd, step, ok=None, step_dev
                    stream_handle()), "adam")
 
 
+def pack_gather(src, idx16, out16, idx32, out32):
+    """out16[i] = h16(src'[idx16[i]]), out32[j] = src'[idx32[j]] with src' = [src, 0, 1]: all
+    packed weight buffers of both networks in one launch."""
+    check(src, torch.float32, None, "src")
+    check(idx16, torch.int32, None, "idx16")
+    check(idx32, torch.int32, None, "idx32")
+    check(out32, torch.float32, (idx32.numel(),), "out32")
+    if out16.dtype not in HALF_DTYPES or not out16.is_contiguous() or out16.numel() != idx16.numel():
+        raise NativeError("out16 must be a contiguous bf16/fp16 buffer matching idx16")
+    n = src.numel()    # index range (<= n + 1) is validated once by ops.weights.PackedWeights
+    _ok(lib().pack_gather(ptr(src), n, ptr(idx16), idx16.numel(), ptr(out16), int(out16.dtype == torch.float16),
+                          ptr(idx32), idx32.numel(), ptr(out32), stream_handle()), "pack_gather")
+
+
 def grad_check(g, ok):
     """ok (int32, preset to 1) <- 0 if any element of g is not finite. No host sync."""
     check(g, torch.float32, None, "g")

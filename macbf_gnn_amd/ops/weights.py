@@ -21,33 +21,49 @@ class PackedWeights:
         self.cbf_off = self.cbf_pk.offsets()
         cv, self.ctrl_voff = L.ctrl_vec_index(offs, dim)
         bv, self.cbf_voff = L.cbf_vec_index(offs)
-        mk = lambda a: torch.as_tensor(L.resolve(a, n), dtype=torch.long, device=dev)
-        self._ictrl = mk(self.ctrl_pk.index())
-        self._icbf = mk(self.cbf_pk.index())
-        self._vctrl = mk(cv)
-        self._vcbf = mk(bv)
         self.node_rm = L.ctrl_node_rm(offs, dim)
         self.node_rm_off = self.node_rm.offsets()
-        self._irm = mk(self.node_rm.index())
         self.cbf_rmp = L.cbf_rm(offs)
-        self._icrm = mk(self.cbf_rmp.index())
-        self._src = torch.zeros(n + 2, dtype=torch.float32, device=dev)
-        self._src[n + 1] = 1.0
-        self.ctrl_w = torch.empty(self._ictrl.numel(), dtype=dtype, device=dev)
-        self.cbf_w = torch.empty(self._icbf.numel(), dtype=dtype, device=dev)
-        self.ctrl_v = torch.empty(self._vctrl.numel(), dtype=torch.float32, device=dev)
-        self.cbf_v = torch.empty(self._vcbf.numel(), dtype=torch.float32, device=dev)
-        self.ctrl_rm = torch.empty(self._irm.numel(), dtype=dtype, device=dev)
-        self.cbf_rm = torch.empty(self._icrm.numel(), dtype=dtype, device=dev)
+        # all 16-bit buffers are views of one allocation (segments 256-element aligned), the
+        # fp32 side vectors views of another: one gather launch repacks everything
+        seg16 = [L.resolve(self.ctrl_pk.index(), n), L.resolve(self.cbf_pk.index(), n),
+                 L.resolve(self.node_rm.index(), n), L.resolve(self.cbf_rmp.index(), n)]
+        seg32 = [L.resolve(cv, n), L.resolve(bv, n)]
+        self._idx16, v16 = self._concat(seg16, n, 256)
+        self._idx32, v32 = self._concat(seg32, n, 64)
+        for a in (self._idx16, self._idx32):        # the gather kernel trusts these bounds
+            if a.size and (a.min() < 0 or a.max() > n + 1):
+                raise ValueError("packing index out of range")
+        dev_i = lambda a: torch.as_tensor(a, dtype=torch.int32, device=dev)
+        self._idx16 = dev_i(self._idx16)
+        self._idx32 = dev_i(self._idx32)
+        self._buf16 = torch.empty(self._idx16.numel(), dtype=dtype, device=dev)
+        self._buf32 = torch.empty(self._idx32.numel(), dtype=torch.float32, device=dev)
+        self.ctrl_w, self.cbf_w, self.ctrl_rm, self.cbf_rm = [self._buf16[o:o + m] for o, m in v16]
+        self.ctrl_v, self.cbf_v = [self._buf32[o:o + m] for o, m in v32]
+        self._cpu_src = None
         self.update()
+
+    @staticmethod
+    def _concat(segs, n, align):
+        import numpy as np
+        out, views, off = [], [], 0
+        for a in segs:
+            a = np.asarray(a, dtype=np.int64).reshape(-1)
+            pad = (-len(a)) % align
+            out.append(a)
+            out.append(np.full(pad, n, dtype=np.int64))     # padding = constant 0
+            views.append((off, len(a)))
+            off += len(a) + pad
+        return np.concatenate(out), views
 
     @torch.no_grad()
     def update(self):
+        if self._buf16.is_cuda:
+            from . import native
+            native.pack_gather(self.fp.flat, self._idx16, self._buf16, self._idx32, self._buf32)
+            return
         n = self.fp.numel
-        self._src[:n].copy_(self.fp.flat)
-        self.ctrl_w.copy_(self._src.index_select(0, self._ictrl))
-        self.cbf_w.copy_(self._src.index_select(0, self._icbf))
-        torch.index_select(self._src, 0, self._vctrl, out=self.ctrl_v)
-        torch.index_select(self._src, 0, self._vcbf, out=self.cbf_v)
-        self.ctrl_rm.copy_(self._src.index_select(0, self._irm))
-        self.cbf_rm.copy_(self._src.index_select(0, self._icrm))
+        src = torch.cat([self.fp.flat, torch.tensor([0.0, 1.0], device=self.fp.flat.device)])
+        self._buf16.copy_(src.index_select(0, self._idx16.long()))
+        self._buf32.copy_(src.index_select(0, self._idx32.long()))

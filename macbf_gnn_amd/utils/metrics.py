@@ -8,6 +8,7 @@ pair under the ``core.py:212-231`` check, averaged over valid steps) and agent-s
 """
 from __future__ import annotations
 
+import collections.abc
 import json
 import sys
 import time
@@ -24,6 +25,61 @@ KEYS = ["loss_total", "loss_dang", "loss_safe", "loss_dang_deriv", "loss_safe_de
 GLOBAL_KEYS = {"n_dang", "n_safe"}
 
 
+class StepStats(collections.abc.MutableMapping):
+    """Statistics of one training iteration of the HIP engine, kept on the device as ONE raw
+    vector (cloned once per iteration) until first read: the derived values (losses,
+    accuracies, counts) are then computed on the host from a single device-to-host copy. No
+    per-statistic kernels and no host synchronisation inside the training loop.
+
+    raw = [10 loss partial sums (slots 2..9: barrier / derivative hinge sums and accuracy
+    counts), n_dang, n_safe, n_act (global pooled counts), agent-steps, safe agents, action-loss
+    sum (this rank)]."""
+
+    RAW = 16
+
+    def __init__(self, raw: torch.Tensor, T, extra=None):
+        self.raw = raw
+        self._T = T
+        self.extra = dict(extra or {})
+        self._host = None
+
+    def _compute(self):
+        if self._host is None:
+            v = [float(x) for x in self.raw.tolist()]
+            sums, (n_dang, n_safe, n_act), (ag, safe, act_sum) = v[:10], v[10:13], v[13:16]
+            nd, ns = 1e-5 + n_dang, 1e-5 + n_safe
+            w = C.LOSS_WEIGHTS
+            d = {"loss_dang": sums[2] / nd, "loss_safe": sums[3] / ns, "loss_dang_deriv": sums[6] / nd,
+                 "loss_safe_deriv": sums[7] / ns, "loss_action": act_sum / max(n_act, 1.0),
+                 "acc_dang_sum": sums[4], "acc_safe_sum": sums[5], "acc_dang_deriv_sum": sums[8],
+                 "acc_safe_deriv_sum": sums[9], "n_dang": n_dang, "n_safe": n_safe,
+                 "agent_steps": ag, "safe_agents": safe}
+            d["loss_total"] = C.LOSS_SCALE * (w[0] * d["loss_dang"] + w[1] * d["loss_safe"] + w[2] * d["loss_dang_deriv"]
+                                              + w[3] * d["loss_safe_deriv"] + w[4] * d["loss_action"])
+            d["T"] = float(self._T)
+            for k, x in self.extra.items():
+                d[k] = float(x) if isinstance(x, torch.Tensor) else x
+            self._host = d
+        return self._host
+
+    def __getitem__(self, k):
+        return self._compute()[k]
+
+    def __setitem__(self, k, v):
+        self.extra[k] = v
+        if self._host is not None:
+            self._host[k] = float(v) if isinstance(v, torch.Tensor) else v
+
+    def __delitem__(self, k):
+        raise KeyError("StepStats entries cannot be deleted")
+
+    def __iter__(self):
+        return iter(self._compute())
+
+    def __len__(self):
+        return len(self._compute())
+
+
 class MetricsLogger:
     def __init__(self, dp, path=None, stream=sys.stdout):
         self.dp = dp
@@ -33,10 +89,14 @@ class MetricsLogger:
 
     def reset(self):
         self.acc = {k: 0.0 for k in KEYS}
+        self.pending = []
         self.t0 = time.perf_counter()
 
     def update(self, stats):
         """Accumulate; device tensors stay on device (no host sync until emit)."""
+        if isinstance(stats, StepStats):       # evaluated at emit time
+            self.pending.append(stats)
+            return
         for k in KEYS:
             if k == "iters":
                 self.acc[k] += 1
@@ -47,6 +107,10 @@ class MetricsLogger:
                 self.acc[k] = self.acc[k] + v
 
     def summary(self, step):
+        for st in self.pending:
+            for k in KEYS:
+                self.acc[k] += 1 if k == "iters" else st[k]
+        self.pending = []
         vec = torch.tensor([float(self.acc[k]) for k in KEYS], dtype=torch.float64)
         if self.dp.enabled:
             dev = self.dp.device if (self.dp.device is not None and self.dp.device.type == "cuda") else "cpu"
