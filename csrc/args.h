@@ -27,6 +27,7 @@ struct ScanArgs {
   float* safe;      long sf_env;     // safe[b*sf_env] += #agents with no dangerous pair
   float r2_train, ttc_train, r2_check, ttc_check;
   int do_knn, do_safety;
+  const int* prev_idx; long pi_env;  // previous step's kNN (b,i,k) (or null): temporal K-th bound
 };
 
 struct ScenArgs {

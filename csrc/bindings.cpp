@@ -25,8 +25,9 @@ static int cell_sort(u64 S, long s_env, int B, int N, float L, u64 perm, int rec
 
 static int scan(u64 S, long s_env, u64 perm, int B, int N, int K, u64 idx, long i_env, u64 dang, u64 cnt, long c_env,
                 u64 safe, long sf_env, float r2_train, float ttc_train, float r2_check, float ttc_check,
-                int do_knn, int do_safety, int Nn, int dim, u64 stream) {
+                int do_knn, int do_safety, int Nn, int dim, u64 prev_idx, long pi_env, u64 stream) {
   mb::ScanArgs a{};
+  a.prev_idx = P<const int>(prev_idx); a.pi_env = pi_env;
   a.Nn = Nn; a.dim = dim;
   a.S = P<const float4>(S); a.s_env = s_env; a.perm = P<const int>(perm); a.B = B; a.N = N; a.K = K;
   a.idx = P<int>(idx); a.i_env = i_env; a.dang = P<uint8_t>(dang);

@@ -149,9 +149,14 @@ DEV float wave_min(float v) { return -wave_max(-v); }
 // r + ttc*(vmax_wave + vmax_chunk) (x1.01 + 1e-4 margin). Both decisions are wave-uniform
 // branches; after the local neighbourhood has filled the lists almost every far chunk costs
 // one box test instead of 8 pair evaluations. Obstacle nodes are candidates, never centres.
-template <int K, int D, int BS>
+// xor-shuffle of a lane value across the LPA lanes of one agent (o = 32: v_permlane32_swap)
+DEV float grp_xor(float v, int o) { return o == 32 ? shfl_xor32(v) : __shfl_xor(v, o); }
+DEV unsigned grp_xoru(unsigned v, int o) { return o == 32 ? xor32u(v) : (unsigned)__shfl_xor((int)v, o); }
+
+template <int K, int D, int BS, int LPA>
 __global__ __launch_bounds__(BS) void scan_kernel(ScanArgs a) {
-  constexpr int SCAN_AG = BS / 2;                              // agents (curve positions) per block
+  constexpr int APW = WAVE / LPA;                              // agents per wave
+  constexpr int SCAN_AG = BS / LPA;                            // agents (curve positions) per block
   extern __shared__ float4 smem4[];
   const int N = a.N, Nn = a.Nn;
   const int Np = (Nn + SCH - 1) / SCH * SCH;
@@ -210,11 +215,11 @@ __global__ __launch_bounds__(BS) void scan_kernel(ScanArgs a) {
     sbh[c] = hi;
   }
   __syncthreads();
-  // Two lanes per agent: lane (r, h) owns curve position base + r and scans candidate slots
-  // 4h..4h+3 of every chunk; the two half-lists are merged at the end. Twice the waves of a
-  // lane-per-agent layout (2 per SIMD) and half the per-chunk work per lane.
-  const int wave = threadIdx.x / WAVE, lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
-  const int pos = blockIdx.x * SCAN_AG + wave * 32 + r;       // my position on the curve
+  // LPA lanes per agent: lane (r, h) owns curve position base + r and scans candidate slots
+  // (SCH/LPA)h.. of every chunk; the partial lists are merged at the end (LPA x the waves of a
+  // lane-per-agent layout, 1/LPA of the per-chunk work per lane).
+  const int wave = threadIdx.x / WAVE, lane = threadIdx.x & 63, r = lane % APW, h = lane / APW;
+  const int pos = blockIdx.x * SCAN_AG + wave * APW + r;      // my position on the curve
   float4 me = make_float4(0.f, 0.f, 0.f, 0.f), mv = make_float4(0.f, 0.f, 0.f, 0.f);
   int i = -1;
   if (pos < Nn) {
@@ -237,11 +242,34 @@ __global__ __launch_bounds__(BS) void scan_kernel(ScanArgs a) {
     wminz = wave_min(act ? me.z : INFINITY);
     wmaxz = wave_max(act ? me.z : -INFINITY);
   }
+  // Temporal bound: the previous step's K neighbours are K candidates now, so the K-th distance
+  // is at most the largest of their current distances. Candidates beyond it are never inserted
+  // and the culling threshold is tight from the first chunk (the lists are still exact: every
+  // true neighbour is within the bound; ties at the bound are kept).
+  float bound = INFINITY;
+  if (a.do_knn && a.prev_idx) {
+    float mx = act ? 0.f : INFINITY;
+    if (act) {
+      const int* pr = a.prev_idx + (long)b * a.pi_env + (long)i * K;
+      for (int q = h; q < K; q += LPA) {
+        float pj[D], vj[D];
+        load_rec<D>(Sb, (unsigned)pr[q], pj, vj);
+        float dp[D];
+        dp[0] = me.x - pj[0];
+        dp[1] = me.y - pj[1];
+        if constexpr (D == 3) dp[2] = me.z - pj[2];
+        mx = fmaxf(mx, sqsum<D>(dp));
+      }
+    }
+#pragma unroll
+    for (int o = APW; o < WAVE; o <<= 1) mx = fmaxf(mx, grp_xor(mx, o));
+    bound = mx;
+  }
   const float wvmax = wave_max(act ? mv.w : 0.f);
   const bool wave_live = __any(act);
-  int cc0 = (blockIdx.x * SCAN_AG + wave * 32 + 16) / SCH;
+  int cc0 = (blockIdx.x * SCAN_AG + wave * APW + APW / 2) / SCH;
   if (cc0 >= nch) cc0 = nch - 1;
-  float thr = INFINITY;                 // bound on every agent's final K-th distance in this wave
+  float thr = wave_max(act ? bound : -INFINITY);   // bound on every agent's final K-th distance
   bool all_danger = false;
   if (wave_live) {
     // gap^2 (x0.999) between this wave's box and a chunk / superchunk box
@@ -279,7 +307,7 @@ __global__ __launch_bounds__(BS) void scan_kernel(ScanArgs a) {
         const float lb = 1.01f * (rc + a.ttc_check * (wvmax + cl.w)) + 1e-4f;
         const bool ns = a.do_safety && !all_danger && !(bd2 > lb * lb);
         if (!nk && !ns) continue;
-        constexpr int HU = SCH / 2;
+        constexpr int HU = SCH / LPA;
         const int hoff = HU * h;
         float4 c[HU];
 #pragma unroll
@@ -293,7 +321,7 @@ __global__ __launch_bounds__(BS) void scan_kernel(ScanArgs a) {
           if constexpr (D == 3) dp[2] = me.z - c[u].z;
           const float d2 = sqsum<D>(dp);
           const uint64_t key = knn_key(d2, (unsigned)j);
-          if (nk && act && key < bk[K - 1]) topk_insert<K>(bk, key);
+          if (nk && act && d2 <= bound && key < bk[K - 1]) topk_insert<K>(bk, key);
           if (ns && act && !danger) {
             const float4 cv = tv[cur * SCH + hoff + u];
             const float lim = 1.01f * (base_i + a.ttc_check * cv.w) + 1e-4f;
@@ -307,31 +335,44 @@ __global__ __launch_bounds__(BS) void scan_kernel(ScanArgs a) {
           }
         }
         if (nk) {
-          // the merged list's K-th distance <= min of the two half-lists' K-th distances
-          const float own = __uint_as_float((unsigned)(bk[K - 1] >> 32));
-          const float kth = fminf(own, shfl_xor32(own));
-          thr = wave_max(act ? kth : -INFINITY);
+          // the merged list's K-th distance <= min of the partial lists' K-th distances
+          float kth = __uint_as_float((unsigned)(bk[K - 1] >> 32));
+#pragma unroll
+          for (int o = APW; o < WAVE; o <<= 1) kth = fminf(kth, grp_xor(kth, o));
+          thr = wave_max(act ? fminf(kth, bound) : -INFINITY);
         }
         if (ns) {
-          // the lane swap must run on every lane: never inside a short-circuit '||'
-          const int pdg = shfl_xor32i(danger ? 1 : 0);
-          const bool dboth = danger || (pdg != 0);
-          all_danger = !__any(act && !dboth);
+          // the lane swaps must run on every lane: never inside a short-circuit '||'
+          unsigned dg = danger ? 1u : 0u;
+#pragma unroll
+          for (int o = APW; o < WAVE; o <<= 1) dg |= grp_xoru(dg, o);
+          all_danger = !__any(act && dg == 0u);
         }
       }
     }
   }
-  // merge the partner half-list into lane h = 0 (keys are unique: (d2, node id))
+  // merge the partial lists (butterfly: every lane ends with the full list; keys are unique:
+  // (d2, node id), and the partners' lists are disjoint)
   if (a.do_knn) {
 #pragma unroll
-    for (int q = 0; q < K; ++q) {
-      const unsigned lo = xor32u((unsigned)bk[q]), hi = xor32u((unsigned)(bk[q] >> 32));
-      const uint64_t x = ((uint64_t)hi << 32) | lo;
-      if (h == 0 && x < bk[K - 1]) topk_insert<K>(bk, x);
+    for (int o = APW; o < WAVE; o <<= 1) {
+      uint64_t px[K];
+#pragma unroll
+      for (int q = 0; q < K; ++q) {
+        const unsigned lo = grp_xoru((unsigned)bk[q], o), hi = grp_xoru((unsigned)(bk[q] >> 32), o);
+        px[q] = ((uint64_t)hi << 32) | lo;
+      }
+#pragma unroll
+      for (int q = 0; q < K; ++q)
+        if (px[q] < bk[K - 1]) topk_insert<K>(bk, px[q]);
     }
   }
-  const int pd = shfl_xor32i(danger ? 1 : 0);   // unconditional lane swap (see above)
-  danger = danger || (pd != 0);
+  {
+    unsigned dg = danger ? 1u : 0u;               // unconditional lane swaps (see above)
+#pragma unroll
+    for (int o = APW; o < WAVE; o <<= 1) dg |= grp_xoru(dg, o);
+    danger = dg != 0u;
+  }
   const bool own = act && h == 0;                              // one lane reports per agent
   float ndang = 0.f, nsafe_e = 0.f, safe_ag = 0.f;
   if (own && a.do_knn) {
@@ -371,17 +412,26 @@ __global__ __launch_bounds__(BS) void scan_kernel(ScanArgs a) {
   }
 }
 
+#ifndef SCAN_LPA
+#define SCAN_LPA 2
+#endif
+
 template <int K, int D, int BS>
 static void launch_kdb(const ScanArgs& a, hipStream_t st) {
-  dim3 grid((a.Nn + BS / 2 - 1) / (BS / 2), a.B);
+  constexpr int LPA = SCAN_LPA;
+  dim3 grid((a.Nn + BS / LPA - 1) / (BS / LPA), a.B);
   const size_t lds = scan_lds_bytes(a.Nn);
-  (void)hipFuncSetAttribute((const void*)scan_kernel<K, D, BS>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL((scan_kernel<K, D, BS>), grid, dim3(BS), lds, st, a);
+  (void)hipFuncSetAttribute((const void*)scan_kernel<K, D, BS, LPA>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipLaunchKernelGGL((scan_kernel<K, D, BS, LPA>), grid, dim3(BS), lds, st, a);
 }
+
+#ifndef SCAN_BS_BIG
+#define SCAN_BS_BIG 512
+#endif
 
 template <int K, int D>
 static void launch_kd(const ScanArgs& a, hipStream_t st) {
-  if (a.Nn > 512) launch_kdb<K, D, 512>(a, st);
+  if (a.Nn > 512) launch_kdb<K, D, SCAN_BS_BIG>(a, st);
   else launch_kdb<K, D, 256>(a, st);
 }
 

@@ -159,7 +159,8 @@ class HipEngine:
         tail_scanned = False
         for t in range(self.Tmax):
             native.scan(self.S[t], self.idx[t], self.dang[t], self.cnt[t], self.safe[t], K=K,
-                        do_knn=True, do_safety=cfg.compute_safety, n_agents=N)
+                        do_knn=True, do_safety=cfg.compute_safety, n_agents=N,
+                        prev_idx=self.idx[t - 1] if t > 0 else None)
             noise = None
             if cfg.add_noise_prob > 0:
                 coin = (torch.rand(B, 1, 1, device=self.dev, generator=self.tr.torch_gen) < cfg.add_noise_prob)
@@ -188,7 +189,8 @@ class HipEngine:
             # safety of the final state; with reuse_nbr_idx=False also the kNN graph of s_T (for h')
             native.scan(self.S[T], self.idx[T] if not self.reuse else None, None, None,
                         self.safe[T] if cfg.compute_safety else None, K=K, do_knn=not self.reuse,
-                        do_safety=cfg.compute_safety, n_agents=N)
+                        do_safety=cfg.compute_safety, n_agents=N,
+                        prev_idx=self.idx[T - 1] if (not self.reuse and T > 0) else None)
         return T
 
     def _all_done(self, t):

@@ -141,13 +141,14 @@ def _perm_buf(B, N, device):
     return t
 
 
-def scan(S, idx, dang, cnt, safe, *, K, do_knn=True, do_safety=True, perm=None, n_agents=None):
+def scan(S, idx, dang, cnt, safe, *, K, do_knn=True, do_safety=True, perm=None, n_agents=None, prev_idx=None):
     """K1 over one timestep. S: (B, N, 4) view with env stride (may be a slice of a (B,T+1,N,4)
     buffer); idx/dang: (B, N, K) views; cnt: (B, 2) view; safe: (B,) view.
 
     Two launches: cell_sort orders each env's agents along a Hilbert curve, then the scan walks
     candidates outward along it (results are order independent; the order only keeps the
-    wave-divergent top-K insertion rare)."""
+    wave-divergent top-K insertion rare). prev_idx (B, N, K): the previous step's kNN of the same
+    agents; their current distances bound the K-th distance (tighter culling, same result)."""
     B, Nn = S.shape[0], S.shape[1]
     D = dim_of(S)
     W = rec_width(D)
@@ -168,6 +169,9 @@ def scan(S, idx, dang, cnt, safe, *, K, do_knn=True, do_safety=True, perm=None, 
             raise NativeError("cnt must be float32 (B,2)")
     if do_safety and safe is not None and (safe.dtype != torch.float32 or tuple(safe.shape) != (B,)):
         raise NativeError("safe must be float32 (B,)")
+    if prev_idx is not None and (not do_knn or prev_idx.dtype != torch.int32 or tuple(prev_idx.shape) != (B, N, K)
+                                 or prev_idx.stride(2) != 1 or prev_idx.stride(1) != K):
+        raise NativeError("prev_idx must be int32 (B,N,K) with contiguous (N,K)")
     if perm is None:
         perm = _perm_buf(B, Nn, S.device)
     L = float(max(1.0, N / C.AGENT_DENSITY) ** (1.0 / D))
@@ -179,7 +183,8 @@ def scan(S, idx, dang, cnt, safe, *, K, do_knn=True, do_safety=True, perm=None, 
                     ptr(safe) if do_safety else 0, safe.stride(0) if (do_safety and safe is not None) else 0,
                     float(C.DIST_MIN_THRES * C.DIST_MIN_THRES), float(C.TIME_TO_COLLISION),
                     float(C.DIST_MIN_CHECK * C.DIST_MIN_CHECK), float(C.TIME_TO_COLLISION_CHECK),
-                    int(do_knn), int(do_safety), Nn, D, stream_handle())
+                    int(do_knn), int(do_safety), Nn, D, ptr(prev_idx),
+                    prev_idx.stride(0) if prev_idx is not None else 0, stream_handle())
     _ok(rc, "scan")
 
 

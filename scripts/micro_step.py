@@ -50,12 +50,17 @@ valid = torch.ones(B, dtype=torch.uint8, device=dev)
 
 def k_scan():
     native.scan(eng.S[t], eng.idx[t], eng.dang[t], eng.cnt[t], eng.safe[t], K=K, do_knn=True,
+                do_safety=True, n_agents=N, prev_idx=eng.idx[t - 1])
+
+
+def k_scan_noprev():
+    native.scan(eng.S[t], eng.idx[t], eng.dang[t], eng.cnt[t], eng.safe[t], K=K, do_knn=True,
                 do_safety=True, n_agents=N)
 
 
 def k_scan_nosafe():
     native.scan(eng.S[t], eng.idx[t], eng.dang[t], eng.cnt[t], eng.safe[t], K=K, do_knn=True,
-                do_safety=False, n_agents=N)
+                do_safety=False, n_agents=N, prev_idx=eng.idx[t - 1])
 
 
 def k_scan_safeonly():
@@ -83,7 +88,7 @@ def k_comb():
 
 
 out = {"tag": args.tag}
-for name, fn in (("scan", k_scan), ("scan_nosafe", k_scan_nosafe), ("scan_safeonly", k_scan_safeonly), ("ctrl_fwd", k_fwd), ("node_bwd", k_node), ("edge_bwd", k_edge),
+for name, fn in (("scan", k_scan), ("scan_noprev", k_scan_noprev), ("scan_nosafe", k_scan_nosafe), ("scan_safeonly", k_scan_safeonly), ("ctrl_fwd", k_fwd), ("node_bwd", k_node), ("edge_bwd", k_edge),
                  ("combine", k_comb)):
     for _ in range(3):
         fn()

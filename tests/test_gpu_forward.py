@@ -52,6 +52,30 @@ def test_scan_knn_ttc_safety(B, N):
     assert torch.equal(safe, O.safe_agent_count(s).float())
 
 
+@pytest.mark.parametrize("B,N,steps", [(2, 13, 3), (2, 300, 4), (1, 1100, 3), (1, 4096, 2)])
+def test_scan_temporal_bound_is_exact(B, N, steps):
+    """prev_idx (the previous step's kNN) only tightens the culling: kNN, danger bits, counts
+    and safety equal the oracle on moving states, step after step."""
+    s, _ = _states(B, N, seed=7 + N, vscale=2.0)
+    K = min(N, C.TOP_K)
+    prev = None
+    for _ in range(steps):
+        idx = torch.empty(B, N, K, dtype=torch.int32, device=DEV)
+        dang = torch.empty(B, N, K, dtype=torch.uint8, device=DEV)
+        cnt = torch.zeros(B, 2, dtype=torch.float32, device=DEV)
+        safe = torch.zeros(B, dtype=torch.float32, device=DEV)
+        native.scan(s, idx, dang, cnt, safe, K=K, prev_idx=prev)
+        torch.cuda.synchronize()
+        ref = O.knn_idx(s, K)
+        assert torch.equal(idx.long(), ref)
+        dref = O.ttc_mask_knn(s, ref)
+        assert torch.equal(dang.bool(), dref)
+        assert torch.equal(cnt[:, 0], dref.sum((1, 2)).float())
+        assert torch.equal(safe, O.safe_agent_count(s).float())
+        prev = idx
+        s = (s + torch.cat([s[..., 2:], torch.zeros_like(s[..., 2:])], -1) * 0.1).contiguous()
+
+
 @pytest.mark.parametrize("B,N", [(2, 300), (1, 4096)])
 def test_scan_ties_and_out_of_domain(B, N):
     """Morton-ordered scan: exact (d2, index) tie-breaks on a lattice with duplicates, agents
