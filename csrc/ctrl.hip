@@ -749,7 +749,8 @@ __global__ __launch_bounds__(EB_WAVES * 64, EB_WAVES == 4 ? 2 : 1) void ctrl_edg
   const int total = a.B * N;
   const long nchunks = (total + EB_CH - 1) / EB_CH;
   const int erow = wave * 32 + r;
-  f32x16 accW2[EB_TA], accW1 = zero16();
+  f32x16 accW2[EB_TA], accW1[2];
+  accW1[0] = accW1[1] = zero16();
   float bs[EB_TA];
 #pragma unroll
   for (int u = 0; u < EB_TA; ++u) { accW2[u] = zero16(); bs[u] = 0.f; }
@@ -857,6 +858,7 @@ __global__ __launch_bounds__(EB_WAVES * 64, EB_WAVES == 4 ? 2 : 1) void ctrl_edg
 #endif
       // S1: dW2 (128x64) += dZ . H1^T ; eb2 (dZ is already in the image; bias-sum steps split
       //     between the two waves that read each row block)
+#ifndef CTRL_X_EBNOS1
       {
         h16* imA = stg;
         h16* imB = stg + EB_CH * 128;
@@ -872,21 +874,30 @@ __global__ __launch_bounds__(EB_WAVES * 64, EB_WAVES == 4 ? 2 : 1) void ctrl_edg
         }
         __syncthreads();
       }
-      // S2: dW1f (64x32) += dH1 . F^T
+#else
+      __syncthreads();
+#endif
+      // S2: dW1f (64x32) += dH1 . F^T over this wave's own 32 edges -- wave-local, no barrier:
+      //     the images live in the wave's own 32 rows of the dZ image (free after S1's closing
+      //     barrier, rewritten by this wave's next scatter only), each wave accumulates both dW1
+      //     tiles; the per-wave partials are summed in fixed order at the end
+#ifndef CTRL_X_EBNOS2
       {
-        h16* imA = stg;
-        h16* imB = stg + EB_CH * 64;
+        h16* imA = stg + wave * 32 * 128;          // dH1, 32 rows x 64 (swizzled)
+        h16* imB = imA + 32 * 64;                  // [F | 0], 32 rows x 32 (swizzled)
 #pragma unroll
-        for (int mt = 0; mt < 2; ++mt) store_tile_sw<64>(imA, erow, 32 * mt, d1b[mt], h);
+        for (int mt = 0; mt < 2; ++mt) store_tile_sw<64>(imA, r, 32 * mt, d1b[mt], h);
         h16x8 zz;
 #pragma unroll
         for (int jj = 0; jj < 8; ++jj) zz[jj] = z;
-        *reinterpret_cast<h16x8*>(imB + swz_off<32>(erow, 8 * h)) = F;
-        *reinterpret_cast<h16x8*>(imB + swz_off<32>(erow, 16 + 8 * h)) = zz;
-        __syncthreads();
-        if (wave < 2) stage_mma_sw<EB_CH / 16, 64, 32>(imA, imB, wave, 0, lane, accW1);
-        __syncthreads();
+        *reinterpret_cast<h16x8*>(imB + swz_off<32>(r, 8 * h)) = F;
+        *reinterpret_cast<h16x8*>(imB + swz_off<32>(r, 16 + 8 * h)) = zz;
+        lds_wave_sync();
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt) stage_mma_sw<2, 64, 32>(imA, imB, mt, 0, lane, accW1[mt]);
+        lds_wave_sync();                           // reads done before the next scatter
       }
+#endif
     }
   }
   float* P = a.partial + (long)blockIdx.x * CTRL_EDGE_PARTIAL;
@@ -898,7 +909,21 @@ __global__ __launch_bounds__(EB_WAVES * 64, EB_WAVES == 4 ? 2 : 1) void ctrl_edg
     const float s = bs[u] + shfl_xor32(bs[u]);
     if (h == 0) ebred[wave][u][r] = s;
   }
-  if (wave < 2) add_tile(P + EP_W1, 32, wave, 0, accW1, lane);
+  // dW1: per-wave partials -> LDS (the stage region is free: every wave has left the loop) ->
+  // fixed-order sum over the waves
+  __syncthreads();
+  float* w1red = reinterpret_cast<float*>(stg);    // [EB_WAVES][2][32 rows][32 cols]
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg)
+      w1red[((wave * 2 + mt) * 32 + acc_row(reg, h)) * 32 + r] = accW1[mt][reg];
+  __syncthreads();
+  for (int q = threadIdx.x; q < 2 * 32 * 32; q += EB_WAVES * 64) {
+    float t = 0.f;
+    for (int w = 0; w < EB_WAVES; ++w) t += w1red[w * 2048 + q];
+    P[EP_W1 + q] += t;                            // rows 32mt + row, 32 cols: the slab layout
+  }
   __syncthreads();
   // eb2 row block mt was summed half by the owner of tile 2mt and half by the owner of tile
   // 2mt+1 (waves w, w^1): add in fixed order
