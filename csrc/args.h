@@ -267,6 +267,7 @@ int mb_reduce_rows(const float* partial, int rows, int cols, float* out, int acc
 int mb_adam(const mb::AdamArgs* a, hipStream_t st);
 int mb_rollout_stats(const mb::RolloutStatsArgs* a, hipStream_t st);
 int mb_grad_check(const float* g, int n, int* ok, hipStream_t st);
+int mb_grad_assemble(const float* red, const int* ptr, const int* src, int n, float scale, float* grad, hipStream_t st);
 int mb_pack_gather(const float* src, int n, const int* idx16, int m16, unsigned short* out16, int f16,
                    const int* idx32, int m32, float* out32, hipStream_t st);
 int mb_adam_commit(const int* ok, int* steps, int mask, int ngroups, int* skipped, hipStream_t st);

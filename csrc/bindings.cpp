@@ -181,6 +181,10 @@ static int pack_gather(u64 src, int n, u64 idx16, int m16, u64 out16, int f16, u
                         P<const int>(idx32), m32, P<float>(out32), ST(stream));
 }
 
+static int grad_assemble(u64 red, u64 ptr, u64 src, int n, float scale, u64 grad, u64 stream) {
+  return mb_grad_assemble(P<const float>(red), P<const int>(ptr), P<const int>(src), n, scale, P<float>(grad), ST(stream));
+}
+
 static int grad_check(u64 g, int n, u64 ok, u64 stream) { return mb_grad_check(P<const float>(g), n, P<int>(ok), ST(stream)); }
 
 static int adam_commit(u64 ok, u64 steps, int mask, int ngroups, u64 skipped, u64 stream) {
@@ -274,6 +278,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("adam", &adam);
   m.def("rollout_stats", &rollout_stats);
   m.def("grad_check", &grad_check);
+  m.def("grad_assemble", &grad_assemble);
   m.def("pack_gather", &pack_gather);
   m.def("adam_commit", &adam_commit);
   m.def("probe_mfma", &probe_mfma);

@@ -93,6 +93,17 @@ __global__ __launch_bounds__(256) void pack_gather_kernel(const float* src, int 
   }
 }
 
+// Flat gradient assembly: grad[p] = scale * sum of the reduced slab entries that map to
+// parameter p (CSR by p, fixed order: deterministic, no atomics, no zero-fill)
+__global__ __launch_bounds__(256) void grad_assemble_kernel(const float* red, const int* ptr, const int* src, int n,
+                                                            float scale, float* grad) {
+  const int p = blockIdx.x * 256 + threadIdx.x;
+  if (p >= n) return;
+  float t = 0.f;
+  for (int q = ptr[p]; q < ptr[p + 1]; ++q) t += red[src[q]];
+  grad[p] = t * scale;
+}
+
 // ok = 0 if any gradient element is not finite (ok preset to 1 by the caller)
 __global__ __launch_bounds__(256) void grad_check_kernel(const float* g, int n, int* ok) {
   bool bad = false;
@@ -164,6 +175,13 @@ extern "C" int mb_pack_gather(const float* src, int n, const int* idx16, int m16
   const int tot = m16 + m32;
   hipLaunchKernelGGL(pack_gather_kernel, dim3((tot + 255) / 256), dim3(256), 0, st, src, n, idx16, m16, out16, f16,
                      idx32, m32, out32);
+  return (int)hipGetLastError();
+}
+
+extern "C" int mb_grad_assemble(const float* red, const int* ptr, const int* src, int n, float scale, float* grad,
+                                hipStream_t st) {
+  using namespace mb;
+  hipLaunchKernelGGL(grad_assemble_kernel, dim3((n + 255) / 256), dim3(256), 0, st, red, ptr, src, n, scale, grad);
   return (int)hipGetLastError();
 }
 

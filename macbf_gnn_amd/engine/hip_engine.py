@@ -51,12 +51,27 @@ class HipEngine:
         self.hdt = {"bf16": torch.bfloat16, "fp16": torch.float16}.get(cfg.dtype, torch.bfloat16)
         self.pw = PackedWeights(trainer.fp, self.D, self.hdt)
         offs = {pn: o for (m, pn, shape, o, n) in trainer.fp.specs}
-        mk = lambda a: torch.as_tensor(a, dtype=torch.long, device=self.dev)
-        self.maps = {}
-        for name, fn in (("cbf", L.cbf_grad_map), ("node", L.ctrl_node_grad_map), ("edge", L.ctrl_edge_grad_map)):
-            s, d = fn(offs, self.D)
-            self.maps[name] = (mk(s), mk(d))
         self._alloc()
+        # flat-gradient assembly: CSR (by parameter) over the concatenated reduced slabs
+        # [cbf | node | edge]; one gather launch per iteration (deterministic)
+        import numpy as np
+        srcs, dsts, base = [], [], 0
+        for name, fn, width in (("cbf", L.cbf_grad_map, native.CBF_PARTIAL),
+                                ("node", L.ctrl_node_grad_map, native.CTRL_NODE_PARTIAL),
+                                ("edge", L.ctrl_edge_grad_map, native.CTRL_EDGE_PARTIAL)):
+            sm, dm = fn(offs, self.D)
+            sm, dm = np.asarray(sm, dtype=np.int64), np.asarray(dm, dtype=np.int64)
+            if sm.size and (sm.min() < 0 or sm.max() >= width or dm.min() < 0 or dm.max() >= trainer.fp.numel):
+                raise ValueError(f"gradient map {name} out of range")
+            srcs.append(sm + base)
+            dsts.append(dm)
+            base += width
+        srcs, dsts = np.concatenate(srcs), np.concatenate(dsts)
+        order = np.lexsort((srcs, dsts))
+        counts = np.bincount(dsts, minlength=trainer.fp.numel)
+        gptr = np.concatenate([[0], np.cumsum(counts)])
+        mk32 = lambda a: torch.as_tensor(a, dtype=torch.int32, device=self.dev)
+        self.g_ptr, self.g_src = mk32(gptr), mk32(srcs[order])
         # whole-iteration HIP graph (cfg.graph): rollout to Tmax with device-side done masks,
         # losses, backward; replayed per iteration (removes the per-kernel launch / Python cost
         # that dominates small configurations). Sampling, the DP all-reduces and the optimizer
@@ -102,9 +117,10 @@ class HipEngine:
         self.nb_node, self.nb_edge = native.ctrl_bwd_grids(B * N, dev)
         self.part_node = torch.zeros(self.nb_node, native.CTRL_NODE_PARTIAL, dtype=f32, device=dev)
         self.part_edge = torch.zeros(self.nb_edge, native.CTRL_EDGE_PARTIAL, dtype=f32, device=dev)
-        self.red_cbf = torch.zeros(native.CBF_PARTIAL, dtype=f32, device=dev)
-        self.red_node = torch.zeros(native.CTRL_NODE_PARTIAL, dtype=f32, device=dev)
-        self.red_edge = torch.zeros(native.CTRL_EDGE_PARTIAL, dtype=f32, device=dev)
+        self.red_all = torch.zeros(native.CBF_PARTIAL + native.CTRL_NODE_PARTIAL + native.CTRL_EDGE_PARTIAL,
+                                   dtype=f32, device=dev)
+        self.red_cbf, self.red_node, self.red_edge = torch.split(
+            self.red_all, [native.CBF_PARTIAL, native.CTRL_NODE_PARTIAL, native.CTRL_EDGE_PARTIAL])
         if self.dedup:
             E = T * B * N * K
             self.map1 = torch.zeros(T, B, N, K, dtype=i32, device=dev)
@@ -119,6 +135,7 @@ class HipEngine:
             self.act_list = torch.zeros(2 * E, dtype=i32, device=dev)
             self.loss_red = torch.zeros(native.DH_PARTIAL, dtype=f32, device=dev)
         self.host_dist = torch.zeros(T, B, dtype=f32, pin_memory=True)
+        self.copy_stream = torch.cuda.Stream(device=dev)
         self.aux = torch.cuda.Stream(device=dev)      # reverse-CSR build overlaps the CBF kernel
         self._nobptt = {}     # lazily sized (T*B)-batched controller-backward buffers
         self._part_cbf = {}
@@ -170,9 +187,15 @@ class HipEngine:
                             pw.ctrl_v, self.A[t], self.S[t + 1], self.dist[t], self.act[t], noise=noise,
                             pooled=self.pooled[t], argmax=self.argmax[t])
             if early_stop:
-                self.host_dist[t].copy_(self.dist[t], non_blocking=True)
-                ev = torch.cuda.Event()
-                ev.record()
+                # the per-env goal distances go to pinned host memory on a side stream (the
+                # blit stays off the compute queue's critical path)
+                done_ev = torch.cuda.Event()
+                done_ev.record()
+                self.copy_stream.wait_event(done_ev)
+                with torch.cuda.stream(self.copy_stream):
+                    self.host_dist[t].copy_(self.dist[t], non_blocking=True)
+                    ev = torch.cuda.Event()
+                    ev.record(self.copy_stream)
                 events.append(ev)
                 # 1-step-lagged host check: never stalls the queue on the step just issued
                 if t >= 1:
@@ -320,16 +343,16 @@ class HipEngine:
         self.part_edge.zero_()
         if self.bptt:
             # BPTT through the rollout: G_t = dL/ds_t, reverse time
-            self.Gb[T].copy_(self.dS[T])
             rptr3 = rptr[: T * B].view(T, B, Nn + 1)
             redges3 = redges[: T * B].view(T, B, N * K)
             for t in range(T - 1, -1, -1):
-                native.ctrl_node_bwd(self.pooled[t], self.S[t], self.G, self.A[t], self.Gb[t + 1], valid_u8[t],
+                Gn = self.dS[T] if t == T - 1 else self.Gb[t + 1]     # G_T = dL/ds_T (direct terms only)
+                native.ctrl_node_bwd(self.pooled[t], self.S[t], self.G, self.A[t], Gn, valid_u8[t],
                                      pw.ctrl_rm, pw.node_rm_off, pw.ctrl_v, gs, self.dP, self.ego,
                                      self.part_node, self.nb_node, act_scale=self.act_scale)
                 native.ctrl_edge_bwd(self.S[t], self.idx[t], self.argmax[t], self.dP, pw.ctrl_w, pw.ctrl_off["ew1f"],
                                      pw.ctrl_off["ew2tn"], self.dEc, self.part_edge, self.nb_edge)
-                native.node_combine(self.dS[t], self.ego, self.dEc, rptr3[t], redges3[t], self.Gb[t + 1],
+                native.node_combine(self.dS[t], self.ego, self.dEc, rptr3[t], redges3[t], Gn,
                                     self.Gb[t], K=K)
         else:
             # no BPTT: the steps are independent -> ONE node + ONE edge backward launch over all
@@ -351,16 +374,10 @@ class HipEngine:
             self._nb_parts = (pn, pe)
         tm.mark("bptt")
         # ---- weight-gradient slabs -> flat grad
-        fg = tr.fp.grad
-        fg.zero_()
         pnode, pedge = (self.part_node, self.part_edge) if self.bptt else self._nb_parts
-        for name, part, red in (("cbf", part_cbf, self.red_cbf), ("node", pnode, self.red_node),
-                                ("edge", pedge, self.red_edge)):
+        for part, red in ((part_cbf, self.red_cbf), (pnode, self.red_node), (pedge, self.red_edge)):
             native.reduce_rows(part, red)
-            src, dst = self.maps[name]
-            fg.index_add_(0, dst, red.index_select(0, src))
-        if gs != 1.0:
-            fg.mul_(1.0 / gs)
+        native.grad_assemble(self.red_all, self.g_ptr, self.g_src, tr.fp.grad, scale=1.0 / gs)
         tm.mark("grad_reduce")
         # ---- stats: one raw device vector (no per-statistic kernels), derived lazily on read
         sums = self.loss_red[:10] if self.dedup else self.red_cbf[native.CBF_P_LOSS: native.CBF_P_LOSS + 10]

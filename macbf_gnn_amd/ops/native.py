@@ -683,6 +683,18 @@ def pack_gather(src, idx16, out16, idx32, out32):
                           ptr(idx32), idx32.numel(), ptr(out32), stream_handle()), "pack_gather")
 
 
+def grad_assemble(red, ptr_, src, grad, scale=1.0):
+    """grad[p] = scale * sum(red[src[ptr[p]:ptr[p+1]]]) for every flat parameter p (one launch,
+    fixed order). ptr (n+1,) / src int32 from a host-built CSR (validated by the caller)."""
+    n = grad.numel()
+    check(red, torch.float32, None, "red")
+    check(ptr_, torch.int32, (n + 1,), "ptr")
+    check(src, torch.int32, None, "src")
+    check(grad, torch.float32, None, "grad")
+    _ok(lib().grad_assemble(ptr(red), ptr(ptr_), ptr(src), n, float(scale), ptr(grad), stream_handle()),
+        "grad_assemble")
+
+
 def grad_check(g, ok):
     """ok (int32, preset to 1) <- 0 if any element of g is not finite. No host sync."""
     check(g, torch.float32, None, "g")
