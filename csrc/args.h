@@ -91,6 +91,9 @@ struct CbfFwdArgs {
   const int* idx1;
   uint8_t* mask_out;
   const h16* wrm;                          // row-major W2 | W3 images (dedup forward)
+  // dedup forward range: evaluations u_begin <= u < (u_end ? u_end : *nev). Main-slot slices of
+  // one rollout step run during the rollout (T = t+1 there, so every u < E is a main slot).
+  unsigned u_begin, u_end;
 };
 
 struct CbfBwdArgs {

@@ -82,9 +82,11 @@ static int cbf_fwd(u64 S, long s_env, long s_step, u64 idx, u64 dang, u64 valid,
 
 static int cbf_hfwd(u64 S, long s_env, long s_step, u64 idx, u64 idx1, u64 src, u64 nev, int B, int T, int N, int K,
                     u64 wpack, int f_fwd, u64 wrm, u64 wvec, u64 h_out, u64 mask_out, float obs_r, float dist_thr,
-                    float dist_eps, int dim, int num_blocks, int f16, u64 stream) {
+                    float dist_eps, int dim, int num_blocks, int f16, unsigned u_begin, unsigned u_end,
+                    u64 stream) {
   mb::CbfFwdArgs a{};
   a.dim = dim;
+  a.u_begin = u_begin; a.u_end = u_end;
   a.S = P<const float4>(S); a.s_env = s_env; a.s_step = s_step; a.idx = P<const int>(idx);
   a.idx1 = P<const int>(idx1); a.src = P<const int>(src); a.nev = P<const int>(nev);
   a.B = B; a.T = T; a.N = N; a.K = K; a.two = 1;

@@ -397,11 +397,12 @@ __global__ __launch_bounds__(NW * 64) void cbf_hfwd_kernel(CbfFwdArgs a) {
   __syncthreads();
   const int wave = threadIdx.x / WAVE, lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
   const unsigned E = (unsigned)a.B * a.T * a.N * a.K;
-  const unsigned U = (unsigned)*a.nev;
-  const unsigned ntiles = (U + 31) / 32;
+  const unsigned U = a.u_end ? a.u_end : (unsigned)*a.nev;
+  const unsigned U0 = a.u_begin;
+  const unsigned ntiles = U > U0 ? (U - U0 + 31) / 32 : 0;
   const unsigned stride = gridDim.x * NW;
   auto load = [&](unsigned tile, EdgeCtx<D>& c) {
-    const unsigned u = tile * 32 + r;
+    const unsigned u = U0 + tile * 32 + r;
     const bool in = u < U;
     const int pass = (in && u >= E) ? 1 : 0;
     const unsigned e = pass ? (unsigned)a.src[u] : u;
@@ -452,7 +453,7 @@ __global__ __launch_bounds__(NW * 64) void cbf_hfwd_kernel(CbfFwdArgs a) {
     }
     float hs = hs2.x + hs2.y;
     hs += shfl_xor32(hs);
-    const unsigned u = tile * 32 + r;
+    const unsigned u = U0 + tile * 32 + r;
     if (u < U && h == 0) {
       a.h_out[u] = c.mask ? hs + vlc[256] : 0.f;
       a.mask_out[u] = c.mask ? 1 : 0;

@@ -130,6 +130,7 @@ def from_records(r: torch.Tensor) -> torch.Tensor:
 # ----------------------------------------------------------------------------- kernels
 SCAN_MAX_N = 4096
 _perm_cache = {}
+_perm_sorted = set()      # cached permutation buffers that hold a curve order
 
 
 def _perm_buf(B, N, device):
@@ -141,14 +142,17 @@ def _perm_buf(B, N, device):
     return t
 
 
-def scan(S, idx, dang, cnt, safe, *, K, do_knn=True, do_safety=True, perm=None, n_agents=None, prev_idx=None):
+def scan(S, idx, dang, cnt, safe, *, K, do_knn=True, do_safety=True, perm=None, n_agents=None, prev_idx=None,
+         sort=True):
     """K1 over one timestep. S: (B, N, 4) view with env stride (may be a slice of a (B,T+1,N,4)
     buffer); idx/dang: (B, N, K) views; cnt: (B, 2) view; safe: (B,) view.
 
     Two launches: cell_sort orders each env's agents along a Hilbert curve, then the scan walks
     candidates outward along it (results are order independent; the order only keeps the
     wave-divergent top-K insertion rare). prev_idx (B, N, K): the previous step's kNN of the same
-    agents; their current distances bound the K-th distance (tighter culling, same result)."""
+    agents; their current distances bound the K-th distance (tighter culling, same result).
+    sort=False reuses the curve order of the previous call on the same perm buffer (the agents
+    moved one step: slightly looser culling, identical results)."""
     B, Nn = S.shape[0], S.shape[1]
     D = dim_of(S)
     W = rec_width(D)
@@ -174,9 +178,15 @@ def scan(S, idx, dang, cnt, safe, *, K, do_knn=True, do_safety=True, perm=None, 
         raise NativeError("prev_idx must be int32 (B,N,K) with contiguous (N,K)")
     if perm is None:
         perm = _perm_buf(B, Nn, S.device)
-    L = float(max(1.0, N / C.AGENT_DENSITY) ** (1.0 / D))
-    rc = lib().cell_sort(ptr(S), S.stride(0) // W, B, Nn, L, ptr(perm), W // 4, stream_handle())
-    _ok(rc, "cell_sort")
+        # never scan through a never-sorted (uninitialised) cached permutation: it indexes nodes
+        key = (B, Nn, str(S.device))
+        if not sort and key not in _perm_sorted:
+            sort = True
+        _perm_sorted.add(key)
+    if sort:
+        L = float(max(1.0, N / C.AGENT_DENSITY) ** (1.0 / D))
+        rc = lib().cell_sort(ptr(S), S.stride(0) // W, B, Nn, L, ptr(perm), W // 4, stream_handle())
+        _ok(rc, "cell_sort")
     rc = lib().scan(ptr(S), S.stride(0) // W, ptr(perm), B, N, K, ptr(idx) if do_knn else 0,
                     idx.stride(0) if do_knn else 0, ptr(dang) if do_knn else 0,
                     ptr(cnt) if do_knn else 0, cnt.stride(0) if (do_knn and cnt is not None) else 0,
@@ -362,10 +372,14 @@ def cbf_hfwd_grid(EV: int, device) -> int:
     return max(1, min((tiles + HFWD_WAVES - 1) // HFWD_WAVES, num_cu(device) * 4))
 
 
-def cbf_hfwd(S, idx, idx1, src, nev, wpack, f_fwd, wrm, wvec, h_out, mask_out, num_blocks=None):
-    """h (masked) and the radius mask of every evaluation u < nev of the deduplicated list:
-    S (>= T+1, B, N, W); idx / idx1 (T, B, N, K) (idx1 = idx for reuse_nbr_idx); src, h_out,
-    mask_out (2E,). Weights: w1f fragments at f_fwd of wpack + the row-major W2|W3 image."""
+def cbf_hfwd(S, idx, idx1, src, nev, wpack, f_fwd, wrm, wvec, h_out, mask_out, num_blocks=None,
+             u_begin=0, u_end=None):
+    """h (masked) and the radius mask of every evaluation u_begin <= u < (u_end or nev) of the
+    deduplicated list: S (>= T+1, B, N, W); idx / idx1 (T, B, N, K) (idx1 = idx for
+    reuse_nbr_idx); src, h_out, mask_out (>= 2E,). Weights: w1f fragments at f_fwd of wpack + the
+    row-major W2|W3 image. A host range [u_begin, u_end) within the main slots (u_end <= E) needs
+    neither src nor nev contents: the rollout evaluates step t's main slots (idx[:t+1]) while
+    later steps are still being simulated."""
     T, B, N, K = idx.shape
     check(idx, torch.int32, None, "idx")
     check(idx1, torch.int32, (T, B, N, K), "idx1")
@@ -373,19 +387,26 @@ def cbf_hfwd(S, idx, idx1, src, nev, wpack, f_fwd, wrm, wvec, h_out, mask_out, n
     E = B * T * N * K
     if 2 * E >= 2 ** 31:
         raise NativeError("too many edge evaluations for 32-bit indexing")
-    check(src, torch.int32, (2 * E,), "src")
+    cap = src.numel() if src is not None else 0
+    if u_end is not None and not (0 <= u_begin <= u_end <= E):
+        raise NativeError(f"host range [{u_begin}, {u_end}) must lie in the main slots [0, {E})")
+    if cap < 2 * E or h_out is None or h_out.numel() < 2 * E or mask_out is None or mask_out.numel() < 2 * E:
+        raise NativeError("src / h_out / mask_out must hold >= 2E evaluations")
+    check(src, torch.int32, None, "src")
     check(nev, torch.int32, (1,), "nev")
-    check(h_out, torch.float32, (2 * E,), "h_out")
-    check(mask_out, torch.uint8, (2 * E,), "mask_out")
+    check(h_out, torch.float32, None, "h_out")
+    check(mask_out, torch.uint8, None, "mask_out")
     f16 = _half(wpack, "wpack")
     check(wpack, wpack.dtype, None, "wpack")
     check(wrm, wpack.dtype, (128 * 68 + 64 * 148,), "wrm")
     check(wvec, torch.float32, None, "wvec")
-    nb = num_blocks or cbf_hfwd_grid(2 * E, S.device)
+    if u_end is not None and u_end == u_begin:
+        return 0
+    nb = num_blocks or cbf_hfwd_grid((u_end if u_end is not None else 2 * E) - u_begin, S.device)
     rc = lib().cbf_hfwd(ptr(S), S.stride(1) // W, S.stride(0) // W, ptr(idx), ptr(idx1), ptr(src), ptr(nev),
                         B, T, N, K, ptr(wpack), int(f_fwd), ptr(wrm), ptr(wvec), ptr(h_out), ptr(mask_out),
                         float(C.OBS_RADIUS), float(C.DIST_MIN_THRES), float(C.CBF_DIST_EPS_COORD * D), D, nb,
-                        f16, stream_handle())
+                        f16, int(u_begin), int(u_end or 0), stream_handle())
     _ok(rc, "cbf_hfwd")
     return nb
 

@@ -53,6 +53,11 @@ def k_scan():
                 do_safety=True, n_agents=N, prev_idx=eng.idx[t - 1])
 
 
+def k_scan_nosort():
+    native.scan(eng.S[t], eng.idx[t], eng.dang[t], eng.cnt[t], eng.safe[t], K=K, do_knn=True,
+                do_safety=True, n_agents=N, prev_idx=eng.idx[t - 1], sort=False)
+
+
 def k_scan_noprev():
     native.scan(eng.S[t], eng.idx[t], eng.dang[t], eng.cnt[t], eng.safe[t], K=K, do_knn=True,
                 do_safety=True, n_agents=N)
@@ -88,7 +93,7 @@ def k_comb():
 
 
 out = {"tag": args.tag}
-for name, fn in (("scan", k_scan), ("scan_noprev", k_scan_noprev), ("scan_nosafe", k_scan_nosafe), ("scan_safeonly", k_scan_safeonly), ("ctrl_fwd", k_fwd), ("node_bwd", k_node), ("edge_bwd", k_edge),
+for name, fn in (("scan", k_scan), ("scan_nosort", k_scan_nosort), ("scan_noprev", k_scan_noprev), ("scan_nosafe", k_scan_nosafe), ("scan_safeonly", k_scan_safeonly), ("ctrl_fwd", k_fwd), ("node_bwd", k_node), ("edge_bwd", k_edge),
                  ("combine", k_comb)):
     for _ in range(3):
         fn()

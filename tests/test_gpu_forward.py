@@ -52,19 +52,21 @@ def test_scan_knn_ttc_safety(B, N):
     assert torch.equal(safe, O.safe_agent_count(s).float())
 
 
+@pytest.mark.parametrize("resort", [True, False])
 @pytest.mark.parametrize("B,N,steps", [(2, 13, 3), (2, 300, 4), (1, 1100, 3), (1, 4096, 2)])
-def test_scan_temporal_bound_is_exact(B, N, steps):
+def test_scan_temporal_bound_is_exact(B, N, steps, resort):
     """prev_idx (the previous step's kNN) only tightens the culling: kNN, danger bits, counts
-    and safety equal the oracle on moving states, step after step."""
+    and safety equal the oracle on moving states, step after step. resort=False keeps the
+    first step's Hilbert order (stale curve order: looser culling, identical results)."""
     s, _ = _states(B, N, seed=7 + N, vscale=2.0)
     K = min(N, C.TOP_K)
     prev = None
-    for _ in range(steps):
+    for step in range(steps):
         idx = torch.empty(B, N, K, dtype=torch.int32, device=DEV)
         dang = torch.empty(B, N, K, dtype=torch.uint8, device=DEV)
         cnt = torch.zeros(B, 2, dtype=torch.float32, device=DEV)
         safe = torch.zeros(B, dtype=torch.float32, device=DEV)
-        native.scan(s, idx, dang, cnt, safe, K=K, prev_idx=prev)
+        native.scan(s, idx, dang, cnt, safe, K=K, prev_idx=prev, sort=resort or step == 0)
         torch.cuda.synchronize()
         ref = O.knn_idx(s, K)
         assert torch.equal(idx.long(), ref)
