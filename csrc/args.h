@@ -206,6 +206,7 @@ struct NodeRedArgs {
   const int* map1;     // dedup: pass-1 slot e -> evaluation index (only >= E = extras are read)
   const float* gate;   // optional: dE[x] is read only where gate[x] != 0 (the skipped evaluations of
                        // the active-list backward leave their dE records unwritten)
+  int t_lo, t_hi;      // output steps t_lo <= t' < t_hi (t_hi = 0: all T+1)
 };
 
 struct CombineArgs {

@@ -125,8 +125,10 @@ static int rev_csr(u64 idx, int G, int N, int K, u64 ptr, u64 edges, int Nn, u64
 }
 
 static int node_reduce(u64 dE, u64 ptr, u64 edges, int B, int T, int N, int K, int passes, int accumulate, u64 out,
-                       int pass_mask, int shift1, int Nn, int dim, u64 map1, u64 gate, u64 stream) {
+                       int pass_mask, int shift1, int Nn, int dim, u64 map1, u64 gate, int t_lo, int t_hi,
+                       u64 stream) {
   mb::NodeRedArgs a{};
+  a.t_lo = t_lo; a.t_hi = t_hi;
   a.map1 = P<const int>(map1); a.gate = P<const float>(gate);
   a.pass_mask = pass_mask; a.shift1 = shift1; a.Nn = Nn; a.dim = dim;
   a.dE = P<const float4>(dE); a.ptr = P<const int>(ptr); a.edges = P<const int>(edges);

@@ -138,9 +138,10 @@ DEV void acc_rec_g(float4 (&g)[R], const float4* src, const float* gate) {
 // for the N agents (obstacle nodes receive no gradient). Records of REC<D> float4.
 template <int D>
 __global__ __launch_bounds__(256) void node_reduce_kernel(NodeRedArgs a) {
-  const long node = ((long)blockIdx.x * blockDim.x + threadIdx.x) / RG;
+  const int t_hi = a.t_hi ? a.t_hi : a.T + 1;
+  const long node = (long)a.t_lo * a.B * a.N + ((long)blockIdx.x * blockDim.x + threadIdx.x) / RG;
   const int l = threadIdx.x % RG;
-  const long total = (long)a.B * (a.T + 1) * a.N;
+  const long total = (long)a.B * t_hi * a.N;
   if (node >= total) return;             // whole 16-lane groups
   // time-major: out[(t'*B + b)*N + i], graphs g = t*B + b
   const int i = (int)(node % a.N);
@@ -265,7 +266,9 @@ extern "C" int mb_rev_csr(const mb::CsrArgs* a, hipStream_t st) {
 
 extern "C" int mb_node_reduce(const mb::NodeRedArgs* a, hipStream_t st) {
   using namespace mb;
-  const long total = (long)a->B * (a->T + 1) * a->N * RG;
+  const int t_hi = a->t_hi ? a->t_hi : a->T + 1;
+  if (a->t_lo < 0 || t_hi > a->T + 1 || a->t_lo >= t_hi) return -1;
+  const long total = (long)a->B * (t_hi - a->t_lo) * a->N * RG;
   if (a->dim == 3) hipLaunchKernelGGL(node_reduce_kernel<3>, dim3((total + 255) / 256), dim3(256), 0, st, *a);
   else hipLaunchKernelGGL(node_reduce_kernel<2>, dim3((total + 255) / 256), dim3(256), 0, st, *a);
   return (int)hipGetLastError();

@@ -31,10 +31,17 @@ class HipEngine:
     name = "hip"
     resort_every = 4          # scan: Hilbert re-sort period (rollout steps)
     overlap_hfwd = True       # CBF h of the main slots runs on a side stream during the rollout
+    reduce_late = 0           # >0: dS steps reduced before the BPTT starts, the rest on the aux stream
+                              # during it (A/B on MI355X: neutral-to-slower, 7.63 vs 7.66 ms; off)
 
     def __init__(self, trainer):
         self.tr = trainer
         cfg = trainer.cfg
+        # scheduling knobs (A/B measurements): MACBF_RESORT_EVERY, MACBF_OVERLAP_HFWD, MACBF_REDUCE_LATE
+        import os
+        self.resort_every = int(os.environ.get("MACBF_RESORT_EVERY", self.resort_every))
+        self.overlap_hfwd = bool(int(os.environ.get("MACBF_OVERLAP_HFWD", int(self.overlap_hfwd))))
+        self.reduce_late = int(os.environ.get("MACBF_REDUCE_LATE", self.reduce_late))
         self.bptt = cfg.bptt
         self.reuse = cfg.reuse_nbr_idx
         # deduplicated h/h' evaluations need both roles' state gradients on the same s_t: BPTT only
@@ -137,7 +144,8 @@ class HipEngine:
             self.act_list = torch.zeros(2 * E, dtype=i32, device=dev)
             self.loss_red = torch.zeros(native.DH_PARTIAL, dtype=f32, device=dev)
             self.nev_host = torch.zeros(1, dtype=i32, device=dev)     # unused by host-range slices
-            self.hstream = torch.cuda.Stream(device=dev)              # rollout-overlapped CBF h slices        self.host_dist = torch.zeros(T, B, dtype=f32, pin_memory=True)
+            self.hstream = torch.cuda.Stream(device=dev)              # rollout-overlapped CBF h slices
+        self.host_dist = torch.zeros(T, B, dtype=f32, pin_memory=True)
         self.copy_stream = torch.cuda.Stream(device=dev)
         self.aux = torch.cuda.Stream(device=dev)      # reverse-CSR build overlaps the CBF kernel
         self._nobptt = {}     # lazily sized (T*B)-batched controller-backward buffers
@@ -366,9 +374,22 @@ class HipEngine:
         cur = torch.cuda.current_stream(self.dev)
         cur.wait_event(csr_done)
         # no-BPTT: s_t is a detached input, only h'(s_{t+1}) gradients reach a_t
-        native.node_reduce(dE, rptr, redges, self.dS, T=T, B=B, N=N, K=K, passes=2,
-                           pass_mask=0 if self.bptt else 2, shift1=G1, n_nodes=Nn, map1=map1,
-                           gate=self.dhbuf[: 2 * E] if self.dedup else None)
+        red = dict(T=T, B=B, N=N, K=K, passes=2, pass_mask=0 if self.bptt else 2, shift1=G1, n_nodes=Nn,
+                   map1=map1, gate=self.dhbuf[: 2 * E] if self.dedup else None)
+        # BPTT consumes dS from the last step down: reduce the last reduce_late steps first, the
+        # rest on the aux stream concurrently with the first BPTT steps (no LDS: it co-resides
+        # with the latency-bound controller-backward kernels)
+        ts = T + 1 - self.reduce_late if (self.bptt and self.reduce_late and T + 1 > 2 * self.reduce_late) else 0
+        red_done = None
+        if ts:
+            native.node_reduce(dE, rptr, redges, self.dS, t_range=(ts, T + 1), **red)
+            self.aux.wait_stream(cur)
+            with torch.cuda.stream(self.aux):
+                native.node_reduce(dE, rptr, redges, self.dS, t_range=(0, ts), **red)
+                red_done = torch.cuda.Event()
+                red_done.record(self.aux)
+        else:
+            native.node_reduce(dE, rptr, redges, self.dS, **red)
         tm.mark("cbf")
         # ---- controller backward
         self.part_node.zero_()
@@ -378,6 +399,8 @@ class HipEngine:
             rptr3 = rptr[: T * B].view(T, B, Nn + 1)
             redges3 = redges[: T * B].view(T, B, N * K)
             for t in range(T - 1, -1, -1):
+                if red_done is not None and t == ts - 1:
+                    cur.wait_event(red_done)                           # dS[0..ts) from the aux stream
                 Gn = self.dS[T] if t == T - 1 else self.Gb[t + 1]     # G_T = dL/ds_T (direct terms only)
                 native.ctrl_node_bwd(self.pooled[t], self.S[t], self.G, self.A[t], Gn, valid_u8[t],
                                      pw.ctrl_rm, pw.node_rm_off, pw.ctrl_v, gs, self.dP, self.ego,

@@ -537,12 +537,14 @@ def rev_csr(idx, rptr, redges, n_nodes=None):
 
 
 def node_reduce(dE, rptr, redges, out, *, T, B, N, K, passes=2, accumulate=False, pass_mask=0, shift1=0,
-                n_nodes=None, map1=None, gate=None):
+                n_nodes=None, map1=None, gate=None, t_range=None):
     """dE (passes, T, B, N, K, W) -> out[t'] (+)= sum over passes p of the edge->node reduction of
     step t' - p, for the N agents. pass_mask selects passes (0 = all); shift1=1: pass-1 edges live
     in graph t+1 (h' on the recomputed kNN of s_{t+1}), so the CSR arrays must hold T+1 graphs.
     map1 (T, B, N, K): deduplicated evaluations (cbf_match) -- dE is then indexed by evaluation
-    and pass 1 reads only the extras map1[e] >= E."""
+    and pass 1 reads only the extras map1[e] >= E. t_range=(lo, hi): only output steps
+    lo <= t' < hi (the BPTT consumes dS from the last step down: the early steps can be reduced
+    on a side stream while it runs)."""
     Nn = N if n_nodes is None else int(n_nodes)
     W = dE.shape[-1]
     D = 2 if W == 4 else 3
@@ -560,8 +562,12 @@ def node_reduce(dE, rptr, redges, out, *, T, B, N, K, passes=2, accumulate=False
             raise NativeError("map1 needs passes=2")
     if gate is not None:
         check(gate, torch.float32, (passes * T * B * N * K,), "gate")
+    lo, hi = (0, 0) if t_range is None else (int(t_range[0]), int(t_range[1]))
+    if t_range is not None and not (0 <= lo < hi <= T + 1):
+        raise NativeError(f"t_range must satisfy 0 <= lo < hi <= T+1 (got {t_range}, T={T})")
     _ok(lib().node_reduce(ptr(dE), ptr(rptr), ptr(redges), B, T, N, K, passes, int(accumulate), ptr(out),
-                          int(pass_mask), int(shift1), Nn, D, ptr(map1), ptr(gate), stream_handle()), "node_reduce")
+                          int(pass_mask), int(shift1), Nn, D, ptr(map1), ptr(gate), int(lo), int(hi),
+                          stream_handle()), "node_reduce")
 
 
 def node_combine(dS_t, ego, dEc, rptr_t, redges_t, Gn, Gout, *, K, dt=C.TIME_STEP):

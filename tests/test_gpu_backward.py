@@ -162,12 +162,15 @@ def _trainer(device, **kw):
     return Trainer(cfg, device=device, dp=DP(device=device))
 
 
-@pytest.mark.parametrize("bptt,reuse", [(True, True), (False, True), (True, False), (False, False)])
-def test_full_step_grad_matches_oracle(bptt, reuse):
+@pytest.mark.parametrize("bptt,reuse,T", [(True, True, 5), (False, True, 5), (True, False, 5), (False, False, 5),
+                                          (True, True, 10), (True, False, 10)])
+def test_full_step_grad_matches_oracle(bptt, reuse, T):
     """One full training step: HIP engine gradient vs autograd through the oracle engine, for
-    BPTT / no-BPTT and h' on the time-t or on the recomputed time-(t+1) neighbour slots."""
+    BPTT / no-BPTT and h' on the time-t or on the recomputed time-(t+1) neighbour slots. T = 10
+    takes the split edge->node reduction (early steps on the aux stream during the BPTT)."""
     from macbf_gnn_amd.engine.oracle_engine import OracleEngine
-    tr = _trainer(DEV, bptt=bptt, reuse_nbr_idx=reuse)
+    tr = _trainer(DEV, bptt=bptt, reuse_nbr_idx=reuse, T=T)
+    tr.engine.reduce_late = 4 if T >= 8 else 0
     s0, g, _ = tr.sample()
     stats = tr.engine.step(s0, g)
     g_hip = tr.fp.grad.clone()
@@ -180,8 +183,10 @@ def test_full_step_grad_matches_oracle(bptt, reuse):
     assert abs(float(stats["loss_total"]) - stats_o["loss_total"]) <= 0.05 * abs(stats_o["loss_total"]) + 1e-4
 
 
-def test_full_step_deterministic():
-    tr = _trainer(DEV, N=64, B=3, T=4)
+@pytest.mark.parametrize("T", [4, 12])
+def test_full_step_deterministic(T):
+    tr = _trainer(DEV, N=64, B=3, T=T)
+    tr.engine.reduce_late = 4 if T >= 8 else 0
     s0, g, _ = tr.sample()
     tr.engine.step(s0, g)
     g1 = tr.fp.grad.clone()
