@@ -267,9 +267,11 @@ class HipEngine:
         T = self.rollout(s0, g, obs)
         tm.mark("rollout")
         valid = self._counts(T)
-        self.tr.dp.all_reduce_(self.counts)
+        # the count all-reduce (the only mid-step collective) overlaps the parts of the backward
+        # that do not read the global counts (reverse CSR, match, extra h evaluations)
+        work = self.tr.dp.all_reduce_async(self.counts)
         tm.mark("counts")
-        return self._stats(*self._backward(T, valid))
+        return self._stats(*self._backward(T, valid, counts_work=work))
 
     # ------------------------------------------------------------------ graph mode
     def _step_graph(self, s0, g, obs):
@@ -316,7 +318,7 @@ class HipEngine:
                              self.counts, self.local, N=self.N)
         return valid
 
-    def _backward(self, T, valid):
+    def _backward(self, T, valid, counts_work=None):
         tr = self.tr
         B, N, K, W, Nn = self.B, self.N, self.K, self.W, self.Nn
         pw = self.pw
@@ -325,9 +327,6 @@ class HipEngine:
         # backward quantity is linear in it; the flat gradient is unscaled after the slab reduce.
         gs = float(tr.grad_scale)
         valid_u8 = valid
-        n_act = self.counts[2].clamp_min(1.0)
-        # action-loss coefficient stays on the device (read by ctrl_node_bwd): no host sync
-        torch.div(C.LOSS_SCALE * C.LOSS_WEIGHTS[4], n_act.view(1), out=self.act_scale)
         E = T * B * N * K
         # ---- reverse CSR of the step graphs (needs only idx): on the aux stream, concurrent with
         #      the CBF kernel below
@@ -356,6 +355,7 @@ class HipEngine:
             # the main slots [0, E) were evaluated during the rollout (overlap_hfwd): extras only
             native.cbf_hfwd(S, idx, idx if self.reuse else idx1, src, nev, pw.cbf_w, pw.cbf_off["w1f"],
                             pw.cbf_rm, pw.cbf_v, hb, hm, u_begin=E if self.overlap_hfwd else 0)
+            self._counts_ready(counts_work)
             native.cbf_dh(hb, hm, map1, src, nev, self.dang[:T], valid_u8, self.counts, dh, self.loss_part,
                           grad_scale=gs, blk_active=self.blk_active)
             # backward over the evaluations with a nonzero upstream gradient only (exact: the
@@ -368,6 +368,7 @@ class HipEngine:
             native.reduce_rows(self.loss_part, self.loss_red)
         else:
             # ---- CBF: h, h', hinge losses, upstream grads and the full backward in ONE kernel
+            self._counts_ready(counts_work)
             native.cbf_bwd(S, idx, None, pw.cbf_w, pw.cbf_off["w1f"], pw.cbf_rm, pw.cbf_v, passes=2, dE=dE,
                            partial=part_cbf, num_blocks=nbb, fused=True, dang=self.dang[:T], valid=valid_u8,
                            counts=self.counts, idx1=idx1, grad_scale=gs)
@@ -439,6 +440,14 @@ class HipEngine:
         torch.cat([sums, self.counts, self.local], out=self.raw_stats)
         Tv = T if not self.graph_mode else (valid != 0).any(1).sum()
         return self.raw_stats, Tv
+
+    def _counts_ready(self, work):
+        """Join the (async) count all-reduce, then the device-side action-loss coefficient
+        (read by ctrl_node_bwd: no host sync)."""
+        if work is not None:
+            work.wait()
+        n_act = self.counts[2].clamp_min(1.0)
+        torch.div(C.LOSS_SCALE * C.LOSS_WEIGHTS[4], n_act.view(1), out=self.act_scale)
 
     def _stats(self, raw, T):
         from ..utils.metrics import StepStats
