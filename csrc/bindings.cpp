@@ -261,8 +261,11 @@ static py::dict device_info(int dev) {
 
 static std::string err_str(int e) { return hipGetErrorString((hipError_t)e); }
 
+void register_runtime(py::module& m);   // runtime.cpp: native rollout driver
+
 PYBIND11_MODULE(_C, m) {
   m.doc() = "macbf_gnn_amd native gfx950 kernels";
+  register_runtime(m);
   m.def("scan", &scan);
   m.def("cell_sort", &cell_sort);
   m.def("scenario", &scenario);

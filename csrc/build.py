@@ -94,9 +94,10 @@ def write_ninja(debug=False):
             lines.append(f"build {o}: kcc {src}")
             lines.append("  kdefs = -DMB_FP16=1")
             objs.append(o)
-    bo = os.path.join(BUILD, "bindings.o")
-    lines.append(f"build {bo}: bcc {os.path.join(HERE, 'bindings.cpp')}")
-    objs.append(bo)
+    for b in ("bindings", "runtime"):      # pybind11 layer + native rollout driver (host C++)
+        bo = os.path.join(BUILD, b + ".o")
+        lines.append(f"build {bo}: bcc {os.path.join(HERE, b + '.cpp')}")
+        objs.append(bo)
     lines.append(f"build {ext_path()}: link {' '.join(objs)}")
     hobjs = []
     for src in HOST_SRCS:

@@ -1,0 +1,216 @@
+// Native rollout driver: the per-step launch loop of the training rollout in C++.
+//
+// Reference: the inner loop of train.py:58-81 (controller step, Euler step, early break when
+// mean |p - g| < DIST_MIN_CHECK) with the kNN/TTC scan of every step. The Python loop paid
+// ~10 wrapper calls per step on the host while the GPU finishes a step in ~0.13 ms at
+// 1024 agents x 64 envs, so the host fell behind and the GPU idled between steps. Here the
+// argument structs of every step are pointer offsets of persistent buffers validated once on
+// the Python side (engine/hip_engine.py), and the loop issues per step:
+//   [side stream] CBF h of the previous step's main slots (overlapped with this step)
+//   cell_sort (every resort_every steps) + scan, ctrl_fwd
+//   [copy stream] per-env goal-distance sums -> pinned host memory
+// and checks the early-stop criterion one step late (never stalls the queue on the step just
+// issued). Per-env done masks are applied on the device afterwards (rollout_stats).
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <stdexcept>
+#include <vector>
+
+#include "args.h"
+
+namespace py = pybind11;
+using u64 = unsigned long long;
+
+namespace {
+
+template <typename T>
+T* P(u64 p) { return reinterpret_cast<T*>(static_cast<uintptr_t>(p)); }
+hipStream_t ST(u64 s) { return reinterpret_cast<hipStream_t>(static_cast<uintptr_t>(s)); }
+
+void chk(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+void chk(int rc, const char* what) {
+  if (rc != 0) throw std::runtime_error(std::string(what) + " launch failed: " + std::to_string(rc));
+}
+
+class RolloutDriver {
+ public:
+  explicit RolloutDriver(py::dict c) {
+    auto I = [&](const char* k) { return c[k].cast<long>(); };
+    auto F = [&](const char* k) { return c[k].cast<float>(); };
+    auto U = [&](const char* k) { return c[k].cast<u64>(); };
+    B_ = (int)I("B"); N_ = (int)I("N"); Nn_ = (int)I("Nn"); K_ = (int)I("K"); D_ = (int)I("D");
+    W_ = D_ == 2 ? 4 : 8;
+    Tmax_ = (int)I("Tmax"); num_cu_ = (int)I("num_cu"); f16_ = (int)I("f16");
+    resort_ = (int)I("resort_every"); safety_ = (int)I("compute_safety"); overlap_ = (int)I("overlap_hfwd");
+    hfwd_blocks_ = (int)I("hfwd_blocks");
+    L_ = F("L");
+    S_ = U("S"); G_ = U("G"); A_ = U("A"); idx_ = U("idx"); dang_ = U("dang"); cnt_ = U("cnt");
+    safe_ = U("safe"); dist_ = U("dist"); act_ = U("act"); pooled_ = U("pooled"); argmax_ = U("argmax");
+    perm_ = U("perm"); host_dist_ = U("host_dist");
+    ctrl_w_ = U("ctrl_w"); f_edge_ = (int)I("f_edge"); f_node_ = (int)I("f_node"); ctrl_v_ = U("ctrl_v");
+    cbf_w_ = U("cbf_w"); f_fwd_ = (int)I("f_fwd"); cbf_rm_ = U("cbf_rm"); cbf_v_ = U("cbf_v");
+    hbuf_ = U("hbuf"); hmask_ = U("hmask"); src_ = U("src"); nev_ = U("nev");
+    r2_train_ = F("r2_train"); ttc_train_ = F("ttc_train"); r2_check_ = F("r2_check"); ttc_check_ = F("ttc_check");
+    dt_ = F("dt"); obs_r_ = F("obs_r"); sqrt3_ = F("sqrt3"); dist_thr_ = F("dist_thr"); dist_eps_ = F("dist_eps");
+    done_thr_ = F("done_thr");
+    if (B_ < 1 || N_ < 1 || Nn_ < N_ || K_ < 1 || K_ > 16 || (D_ != 2 && D_ != 3) || Tmax_ < 1 || resort_ < 1)
+      throw std::invalid_argument("RolloutDriver: bad dimensions");
+    ev_copy_.resize(Tmax_);
+    for (auto& e : ev_copy_) chk(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
+    // stream -> stream dependencies on one device: a device-scope release is enough (the default
+    // system-scope fence writes back / invalidates caches for host visibility and stalls the
+    // queue behind it); the copy-completion events the host waits on keep the system fence
+    const unsigned fork_flags = hipEventDisableTiming | (c["fork_device_scope"].cast<int>() ? hipEventReleaseToDevice : 0u);
+    chk(hipEventCreateWithFlags(&ev_main_, fork_flags), "hipEventCreate");
+    chk(hipEventCreateWithFlags(&ev_side_, fork_flags), "hipEventCreate");
+  }
+  ~RolloutDriver() {
+    for (auto e : ev_copy_) (void)hipEventDestroy(e);
+    (void)hipEventDestroy(ev_main_);
+    (void)hipEventDestroy(ev_side_);
+  }
+  RolloutDriver(const RolloutDriver&) = delete;
+  RolloutDriver& operator=(const RolloutDriver&) = delete;
+
+  // Returns (T, tail_scanned): T valid steps; tail_scanned = the scan of s_T was issued (the
+  // early-stopped case, where step T's scan ran before the break).
+  std::pair<int, bool> run(u64 stream, u64 hstream, u64 copy_stream, bool early_stop) {
+    hipStream_t st = ST(stream), hs = ST(hstream), cs = ST(copy_stream);
+    const volatile float* hd = P<const volatile float>(host_dist_);
+    int T = Tmax_;
+    bool tail = false;
+    for (int t = 0; t < Tmax_; ++t) {
+      scan_step(t, st);
+      ctrl_step(t, st);
+      // ONE marker per step on the compute queue (each marker stalls the queue behind it for
+      // ~6 us: the next dispatch waits for its completion signal); both side queues wait on it
+      if (overlap_ || early_stop) chk(hipEventRecord(ev_main_, st), "hipEventRecord");
+      // CBF h of the previous step's main slots on the side stream (one step late: the slice
+      // of a step beyond the early stop is never issued)
+      if (overlap_ && t >= 1) {
+        chk(hipStreamWaitEvent(hs, ev_main_, 0), "hipStreamWaitEvent");
+        hfwd_slice(t - 1, hs);
+      }
+      if (early_stop) {
+        chk(hipStreamWaitEvent(cs, ev_main_, 0), "hipStreamWaitEvent");
+        chk(hipMemcpyAsync(P<float>(host_dist_) + (long)t * B_, P<const float>(dist_) + (long)t * B_,
+                           sizeof(float) * B_, hipMemcpyDeviceToHost, cs), "hipMemcpyAsync");
+        chk(hipEventRecord(ev_copy_[t], cs), "hipEventRecord");
+        if (t >= 1) {
+          chk(hipEventSynchronize(ev_copy_[t - 1]), "hipEventSynchronize");
+          if (all_done(hd, t - 1)) {
+            // every env was done after step t-1: the trajectory is steps 0..t-1; step t's scan
+            // already gave the kNN graph / safety of s_t, its controller step is unused
+            T = t;
+            tail = true;
+            break;
+          }
+        }
+      }
+    }
+    if (overlap_) {
+      if (!tail) {
+        // the side stream already waits on the marker after ctrl_fwd(T-1) unless T == 1
+        if (T == 1) chk(hipStreamWaitEvent(hs, ev_main_, 0), "hipStreamWaitEvent");
+        hfwd_slice(T - 1, hs);
+      }
+      chk(hipEventRecord(ev_side_, hs), "hipEventRecord");     // join the side stream
+      chk(hipStreamWaitEvent(st, ev_side_, 0), "hipStreamWaitEvent");
+    }
+    return {T, tail};     // converted to a tuple after the GIL is re-acquired
+  }
+
+ private:
+  bool all_done(const volatile float* hd, int t) const {
+    // env b is done iff its mean goal distance fell below the threshold at some step <= t
+    for (int b = 0; b < B_; ++b) {
+      bool d = false;
+      for (int q = 0; q <= t && !d; ++q) d = hd[(long)q * B_ + b] / (float)N_ < done_thr_;
+      if (!d) return false;
+    }
+    return true;
+  }
+
+  const float4* S_at(int t) const { return P<const float4>(S_) + (long)t * B_ * Nn_ * (W_ / 4); }
+
+  void scan_step(int t, hipStream_t st) {
+    if (t % resort_ == 0) {
+      mb::CellSortArgs c{};
+      c.S = S_at(t); c.s_env = Nn_; c.B = B_; c.N = Nn_; c.L = L_; c.perm = P<int>(perm_); c.rec = W_ / 4;
+      chk(mb_cell_sort(&c, st), "cell_sort");
+    }
+    mb::ScanArgs a{};
+    a.S = S_at(t); a.s_env = Nn_; a.perm = P<const int>(perm_);
+    a.B = B_; a.N = N_; a.K = K_; a.Nn = Nn_; a.dim = D_;
+    const long nk = (long)N_ * K_;
+    a.idx = P<int>(idx_) + (long)t * B_ * nk; a.i_env = nk;
+    a.dang = P<uint8_t>(dang_) + (long)t * B_ * nk;
+    a.cnt = P<float>(cnt_) + (long)t * B_ * 2; a.c_env = 2;
+    a.safe = safety_ ? P<float>(safe_) + (long)t * B_ : nullptr; a.sf_env = 1;
+    a.r2_train = r2_train_; a.ttc_train = ttc_train_; a.r2_check = r2_check_; a.ttc_check = ttc_check_;
+    a.do_knn = 1; a.do_safety = safety_;
+    a.prev_idx = t > 0 ? P<const int>(idx_) + (long)(t - 1) * B_ * nk : nullptr; a.pi_env = nk;
+    chk(mb_scan(&a, st), "scan");
+  }
+
+  void ctrl_step(int t, hipStream_t st) {
+    mb::CtrlArgs a{};
+    a.dim = D_;
+    a.S = S_at(t); a.s_env = Nn_;
+    a.G = P<const float>(G_);
+    const long nk = (long)N_ * K_;
+    a.idx = P<const int>(idx_) + (long)t * B_ * nk; a.i_env = nk;
+    a.B = B_; a.N = N_; a.K = K_;
+    a.wpack = P<const h16>(ctrl_w_); a.f_edge = f_edge_; a.f_node = f_node_; a.wvec = P<const float>(ctrl_v_);
+    a.A = P<float>(A_) + (long)t * B_ * N_ * D_; a.a_env = N_;
+    a.Snext = const_cast<float4*>(S_at(t + 1)); a.sn_env = Nn_;
+    a.dist_sum = P<float>(dist_) + (long)t * B_; a.d_env = 1;
+    a.act_sum = P<float>(act_) + (long)t * B_; a.ac_env = 1;
+    a.noise = nullptr; a.n_env = 0;
+    a.dt = dt_; a.obs_r = obs_r_; a.sqrt3 = sqrt3_;
+    a.pooled = P<h16>(pooled_) + (long)t * B_ * N_ * 128; a.p_env = (long)N_ * 128;
+    a.argmax = P<uint8_t>(argmax_) + (long)t * B_ * N_ * 128; a.am_env = (long)N_ * 128;
+    chk((f16_ ? mb_ctrl_fwd_f16 : mb_ctrl_fwd)(&a, num_cu_, st), "ctrl_fwd");
+  }
+
+  // CBF h of the main slots of step t, evaluations [t*BNK, (t+1)*BNK), on the side stream
+  void hfwd_slice(int t, hipStream_t hs) {
+    mb::CbfFwdArgs a{};
+    a.dim = D_;
+    const long bnk = (long)B_ * N_ * K_;
+    a.S = P<const float4>(S_); a.s_env = Nn_; a.s_step = (long)B_ * Nn_;
+    a.idx = P<const int>(idx_); a.idx1 = a.idx; a.src = P<const int>(src_); a.nev = P<const int>(nev_);
+    a.B = B_; a.T = t + 1; a.N = N_; a.K = K_; a.two = 1;
+    a.wpack = P<const h16>(cbf_w_); a.f_fwd = f_fwd_; a.wrm = P<const h16>(cbf_rm_);
+    a.wvec = P<const float>(cbf_v_);
+    a.h_out = P<float>(hbuf_); a.mask_out = P<uint8_t>(hmask_);
+    a.obs_r = obs_r_; a.dist_thr = dist_thr_; a.dist_eps = dist_eps_;
+    a.u_begin = (unsigned)(t * bnk); a.u_end = (unsigned)((t + 1) * bnk);
+    chk((f16_ ? mb_cbf_hfwd_f16 : mb_cbf_hfwd)(&a, hfwd_blocks_, hs), "cbf_hfwd");
+  }
+
+  int B_, N_, Nn_, K_, D_, W_, Tmax_, num_cu_, f16_, resort_, safety_, overlap_, hfwd_blocks_;
+  float L_;
+  u64 S_, G_, A_, idx_, dang_, cnt_, safe_, dist_, act_, pooled_, argmax_, perm_, host_dist_;
+  u64 ctrl_w_, ctrl_v_, cbf_w_, cbf_rm_, cbf_v_, hbuf_, hmask_, src_, nev_;
+  int f_edge_, f_node_, f_fwd_;
+  float r2_train_, ttc_train_, r2_check_, ttc_check_, dt_, obs_r_, sqrt3_, dist_thr_, dist_eps_, done_thr_;
+  std::vector<hipEvent_t> ev_copy_;
+  hipEvent_t ev_main_ = nullptr, ev_side_ = nullptr;
+};
+
+}  // namespace
+
+void register_runtime(py::module& m) {
+  py::class_<RolloutDriver>(m, "RolloutDriver")
+      .def(py::init<py::dict>())
+      .def("run", &RolloutDriver::run, py::arg("stream"), py::arg("hstream"), py::arg("copy_stream"),
+           py::arg("early_stop"),
+           // the loop blocks on hipEventSynchronize: let other Python threads run meanwhile
+           py::call_guard<py::gil_scoped_release>());
+}

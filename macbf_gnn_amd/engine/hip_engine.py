@@ -31,6 +31,7 @@ class HipEngine:
     name = "hip"
     resort_every = 4          # scan: Hilbert re-sort period (rollout steps)
     overlap_hfwd = True       # CBF h of the main slots runs on a side stream during the rollout
+    native_rollout = True     # per-step launch loop in C++ (csrc/runtime.cpp)
     reduce_late = 0           # >0: dS steps reduced before the BPTT starts, the rest on the aux stream
                               # during it (A/B on MI355X: neutral-to-slower, 7.63 vs 7.66 ms; off)
 
@@ -42,6 +43,8 @@ class HipEngine:
         self.resort_every = int(os.environ.get("MACBF_RESORT_EVERY", self.resort_every))
         self.overlap_hfwd = bool(int(os.environ.get("MACBF_OVERLAP_HFWD", int(self.overlap_hfwd))))
         self.reduce_late = int(os.environ.get("MACBF_REDUCE_LATE", self.reduce_late))
+        self.native_rollout = bool(int(os.environ.get("MACBF_NATIVE_ROLLOUT", int(self.native_rollout))))
+        self._drv = None
         self.bptt = cfg.bptt
         self.reuse = cfg.reuse_nbr_idx
         # deduplicated h/h' evaluations need both roles' state gradients on the same s_t: BPTT only
@@ -172,6 +175,53 @@ class HipEngine:
         self.load_inputs(s0, g, obs)
         return self._rollout_steps(self.tr.cfg.early_stop if early_stop is None else early_stop)
 
+    def _driver(self):
+        """The native rollout driver (csrc/runtime.cpp) over this engine's persistent buffers;
+        every pointer it offsets per step is checked here once."""
+        import os
+        if self._drv is None:
+            cfg = self.tr.cfg
+            B, N, Nn, K, D, W, T = self.B, self.N, self.Nn, self.K, self.D, self.W, self.Tmax
+            G1 = 0 if self.reuse else 1
+            exp = {"S": (self.S, torch.float32, (T + 1, B, Nn, W)), "G": (self.G, torch.float32, (B, N, D)),
+                   "A": (self.A, torch.float32, (T, B, N, D)), "idx": (self.idx, torch.int32, (T + G1, B, N, K)),
+                   "dang": (self.dang, torch.uint8, (T, B, N, K)), "cnt": (self.cnt, torch.float32, (T, B, 2)),
+                   "safe": (self.safe, torch.float32, (T + 1, B)), "dist": (self.dist, torch.float32, (T, B)),
+                   "act": (self.act, torch.float32, (T, B)), "pooled": (self.pooled, self.hdt, (T, B, N, 128)),
+                   "argmax": (self.argmax, torch.uint8, (T, B, N, 128))}
+            for name, (t, dt, shape) in exp.items():
+                native.check(t, dt, shape, name)
+            if not self.host_dist.is_pinned() or tuple(self.host_dist.shape) != (T, B):
+                raise native.NativeError("host_dist must be pinned (T, B)")
+            pw = self.pw
+            perm = native._perm_buf(B, Nn, self.dev)
+            native._perm_sorted.add((B, Nn, str(self.dev)))      # sorted at t = 0 of every run
+            overlap = bool(self.dedup and self.overlap_hfwd)
+            BNK = B * N * K
+            c = {k: native.ptr(v[0]) for k, v in exp.items()}
+            c.update(dict(
+                B=B, N=N, Nn=Nn, K=K, D=D, Tmax=T, num_cu=native.num_cu(self.dev), f16=int(self.hdt == torch.float16),
+                resort_every=int(self.resort_every), compute_safety=int(cfg.compute_safety), overlap_hfwd=int(overlap),
+                hfwd_blocks=native.cbf_hfwd_grid(BNK, self.dev), L=float(max(1.0, N / C.AGENT_DENSITY) ** (1.0 / D)),
+                perm=native.ptr(perm), host_dist=int(self.host_dist.data_ptr()),
+                ctrl_w=native.ptr(pw.ctrl_w), f_edge=int(pw.ctrl_off["ew1f"]), f_node=int(pw.ctrl_off["nw1f"]),
+                ctrl_v=native.ptr(pw.ctrl_v), cbf_w=native.ptr(pw.cbf_w), f_fwd=int(pw.cbf_off["w1f"]),
+                cbf_rm=native.ptr(pw.cbf_rm), cbf_v=native.ptr(pw.cbf_v),
+                hbuf=native.ptr(self.hbuf) if overlap else 0, hmask=native.ptr(self.hmask) if overlap else 0,
+                src=native.ptr(self.src) if overlap else 0, nev=native.ptr(self.nev_host) if overlap else 0,
+                r2_train=float(C.DIST_MIN_THRES * C.DIST_MIN_THRES), ttc_train=float(C.TIME_TO_COLLISION),
+                r2_check=float(C.DIST_MIN_CHECK * C.DIST_MIN_CHECK), ttc_check=float(C.TIME_TO_COLLISION_CHECK),
+                dt=float(C.TIME_STEP), obs_r=float(C.OBS_RADIUS), sqrt3=float(C.SQRT3),
+                dist_thr=float(C.DIST_MIN_THRES), dist_eps=float(C.CBF_DIST_EPS_COORD * D),
+                done_thr=float(C.DIST_MIN_CHECK),
+                fork_device_scope=int(os.environ.get("MACBF_FORK_DEVICE_SCOPE", "1"))))
+            if pw.ctrl_v.numel() < 352 or pw.ctrl_w.numel() < (c["f_node"] + 54) * 512:
+                raise native.NativeError("packed controller weights too small")
+            if overlap and (self.hbuf.numel() < 2 * T * BNK or self.src.numel() < 2 * T * BNK):
+                raise native.NativeError("CBF evaluation buffers too small")
+            self._drv = native.lib().RolloutDriver(c)
+        return self._drv
+
     def _rollout_steps(self, early_stop):
         """Rollout from the loaded inputs. early_stop=False: all Tmax steps, no host round trip
         (done envs are masked by the validity mask; used by the captured graph)."""
@@ -187,6 +237,11 @@ class HipEngine:
         tail_scanned = False
         cur = torch.cuda.current_stream(self.dev)
         overlap = self.dedup and self.overlap_hfwd
+        if self.native_rollout and cfg.add_noise_prob <= 0 and not torch.cuda.is_current_stream_capturing():
+            # the per-step launch loop in C++ (csrc/runtime.cpp): same launches, same order
+            T, tail_scanned = self._driver().run(cur.cuda_stream, self.hstream.cuda_stream if overlap else 0,
+                                                 self.copy_stream.cuda_stream, bool(early_stop))
+            return self._tail_scan(T, tail_scanned)
         if overlap:
             self.hstream.wait_stream(cur)
         for t in range(self.Tmax):
@@ -233,11 +288,15 @@ class HipEngine:
             if not tail_scanned:
                 self._hfwd_slice(T - 1, cur)
             cur.wait_stream(self.hstream)
+        return self._tail_scan(T, tail_scanned)
+
+    def _tail_scan(self, T, tail_scanned):
+        cfg = self.tr.cfg
         if (cfg.compute_safety or not self.reuse) and not tail_scanned:
             # safety of the final state; with reuse_nbr_idx=False also the kNN graph of s_T (for h')
             native.scan(self.S[T], self.idx[T] if not self.reuse else None, None, None,
-                        self.safe[T] if cfg.compute_safety else None, K=K, do_knn=not self.reuse,
-                        do_safety=cfg.compute_safety, n_agents=N,
+                        self.safe[T] if cfg.compute_safety else None, K=self.K, do_knn=not self.reuse,
+                        do_safety=cfg.compute_safety, n_agents=self.N,
                         prev_idx=self.idx[T - 1] if (not self.reuse and T > 0) else None)
         return T
 
