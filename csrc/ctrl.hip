@@ -403,7 +403,7 @@ namespace MB_PREC {
 
 constexpr int NB_WAVES = 4;
 constexpr int NB_CH = NB_WAVES * 32;                  // agents per chunk
-constexpr int NS1 = 168, NS2 = 72, NS3 = 136, NS4 = 72;   // row-major image strides
+constexpr int NS1 = 168, NS2 = 68, NS3 = 132, NS4 = 68;   // row-major image strides (NS2..4: 2*odd dwords, conflict-free ds_read_b64 row reads)
 constexpr int NODE_RM_ELEMS = 64 * NS1 + 128 * NS2 + 64 * NS3 + 32 * NS4;
 constexpr int NP_W1 = 0, NP_W2 = 10240, NP_B2 = 18432, NP_W3 = 18560, NP_B3 = 26752, NP_W4 = 26816, NP_B4 = 28864;
 constexpr int CTRL_NODE_PARTIAL = 28896;

@@ -351,7 +351,7 @@ class RMPacker:
         return {im.name: im.offset for im in self.images}
 
 
-NODE_STRIDES = {"w1": 168, "w2": 72, "w3": 136, "w4": 72}
+NODE_STRIDES = {"w1": 168, "w2": 68, "w3": 132, "w4": 68}
 
 
 def ctrl_node_rm(fp_offsets, dim: int = 2) -> RMPacker:
