@@ -32,6 +32,7 @@ class HipEngine:
     resort_every = 4          # scan: Hilbert re-sort period (rollout steps)
     overlap_hfwd = True       # CBF h of the main slots runs on a side stream during the rollout
     native_rollout = True     # per-step launch loop in C++ (csrc/runtime.cpp)
+    bptt_groups = 1           # independent env groups whose BPTT chains run on separate streams
     reduce_late = 0           # >0: dS steps reduced before the BPTT starts, the rest on the aux stream
                               # during it (A/B on MI355X: neutral-to-slower, 7.63 vs 7.66 ms; off)
 
@@ -44,6 +45,9 @@ class HipEngine:
         self.overlap_hfwd = bool(int(os.environ.get("MACBF_OVERLAP_HFWD", int(self.overlap_hfwd))))
         self.reduce_late = int(os.environ.get("MACBF_REDUCE_LATE", self.reduce_late))
         self.native_rollout = bool(int(os.environ.get("MACBF_NATIVE_ROLLOUT", int(self.native_rollout))))
+        self.bptt_groups = int(os.environ.get("MACBF_BPTT_GROUPS", self.bptt_groups))
+        if cfg.num_envs % self.bptt_groups:
+            self.bptt_groups = 1
         self._drv = None
         self.bptt = cfg.bptt
         self.reuse = cfg.reuse_nbr_idx
@@ -127,8 +131,16 @@ class HipEngine:
         self.valid_buf = torch.zeros(T, B, dtype=u8, device=dev)
         self.act_scale = torch.zeros(1, dtype=f32, device=dev)      # action-loss coefficient
         self.nb_node, self.nb_edge = native.ctrl_bwd_grids(B * N, dev)
-        self.part_node = torch.zeros(self.nb_node, native.CTRL_NODE_PARTIAL, dtype=f32, device=dev)
-        self.part_edge = torch.zeros(self.nb_edge, native.CTRL_EDGE_PARTIAL, dtype=f32, device=dev)
+        # BPTT env groups (independent chains on separate streams): per-group grids and slab rows
+        Gp = self.bptt_groups
+        if Gp < 1 or B % Gp:
+            raise ValueError(f"bptt_groups={Gp} must divide num_envs={B}")
+        self.grp_nb = native.ctrl_bwd_grids((B // Gp) * N, dev)
+        rows_n = max(self.nb_node, Gp * self.grp_nb[0])
+        rows_e = max(self.nb_edge, Gp * self.grp_nb[1])
+        self.part_node = torch.zeros(rows_n, native.CTRL_NODE_PARTIAL, dtype=f32, device=dev)
+        self.part_edge = torch.zeros(rows_e, native.CTRL_EDGE_PARTIAL, dtype=f32, device=dev)
+        self.gstreams = [torch.cuda.Stream(device=dev) for _ in range(Gp - 1)]
         self.red_all = torch.zeros(native.CBF_PARTIAL + native.CTRL_NODE_PARTIAL + native.CTRL_EDGE_PARTIAL,
                                    dtype=f32, device=dev)
         self.red_cbf, self.red_node, self.red_edge = torch.split(
@@ -458,17 +470,25 @@ class HipEngine:
             # BPTT through the rollout: G_t = dL/ds_t, reverse time
             rptr3 = rptr[: T * B].view(T, B, Nn + 1)
             redges3 = redges[: T * B].view(T, B, N * K)
-            for t in range(T - 1, -1, -1):
-                if red_done is not None and t == ts - 1:
-                    cur.wait_event(red_done)                           # dS[0..ts) from the aux stream
-                Gn = self.dS[T] if t == T - 1 else self.Gb[t + 1]     # G_T = dL/ds_T (direct terms only)
-                native.ctrl_node_bwd(self.pooled[t], self.S[t], self.G, self.A[t], Gn, valid_u8[t],
-                                     pw.ctrl_rm, pw.node_rm_off, pw.ctrl_v, gs, self.dP, self.ego,
-                                     self.part_node, self.nb_node, act_scale=self.act_scale)
-                native.ctrl_edge_bwd(self.S[t], self.idx[t], self.argmax[t], self.dP, pw.ctrl_w, pw.ctrl_off["ew1f"],
-                                     pw.ctrl_off["ew2tn"], self.dEc, self.part_edge, self.nb_edge)
-                native.node_combine(self.dS[t], self.ego, self.dEc, rptr3[t], redges3[t], Gn,
-                                    self.Gb[t], K=K)
+            Gp = self.bptt_groups
+            if Gp == 1:
+                self._bptt_chain(T, slice(0, B), valid_u8, gs, rptr3, redges3, self.part_node[: self.nb_node],
+                                 self.part_edge[: self.nb_edge], self.nb_node, self.nb_edge, red_done, ts, cur)
+            else:
+                # envs never interact: Gp independent reverse-time chains, one per env group and
+                # stream, interleave their latency-bound kernels on the CUs
+                Bg = B // Gp
+                nbn, nbe = self.grp_nb
+                for g in range(Gp):
+                    st = cur if g == 0 else self.gstreams[g - 1]
+                    if g:
+                        st.wait_stream(cur)
+                    with torch.cuda.stream(st):
+                        self._bptt_chain(T, slice(g * Bg, (g + 1) * Bg), valid_u8, gs, rptr3, redges3,
+                                         self.part_node[g * nbn:(g + 1) * nbn], self.part_edge[g * nbe:(g + 1) * nbe],
+                                         nbn, nbe, red_done, ts, st)
+                for st in self.gstreams:
+                    cur.wait_stream(st)
         else:
             # no BPTT: the steps are independent -> ONE node + ONE edge backward launch over all
             # T*B (step, env) pairs, with dL/da_t = dt * dL/dv_{t+1} from h'(s_{t+1}) + action loss
@@ -499,6 +519,21 @@ class HipEngine:
         torch.cat([sums, self.counts, self.local], out=self.raw_stats)
         Tv = T if not self.graph_mode else (valid != 0).any(1).sum()
         return self.raw_stats, Tv
+
+    def _bptt_chain(self, T, sl, valid_u8, gs, rptr3, redges3, part_node, part_edge, nbn, nbe, red_done, ts, st):
+        """Reverse-time BPTT over the envs `sl` on stream `st`: G_t = dL/ds_t from G_{t+1}."""
+        pw, K = self.pw, self.K
+        for t in range(T - 1, -1, -1):
+            if red_done is not None and t == ts - 1:
+                st.wait_event(red_done)                                # dS[0..ts) from the aux stream
+            Gn = self.dS[T][sl] if t == T - 1 else self.Gb[t + 1][sl]   # G_T = dL/ds_T (direct terms only)
+            native.ctrl_node_bwd(self.pooled[t][sl], self.S[t][sl], self.G[sl], self.A[t][sl], Gn, valid_u8[t][sl],
+                                 pw.ctrl_rm, pw.node_rm_off, pw.ctrl_v, gs, self.dP[sl], self.ego[sl],
+                                 part_node, nbn, act_scale=self.act_scale)
+            native.ctrl_edge_bwd(self.S[t][sl], self.idx[t][sl], self.argmax[t][sl], self.dP[sl], pw.ctrl_w,
+                                 pw.ctrl_off["ew1f"], pw.ctrl_off["ew2tn"], self.dEc[sl], part_edge, nbe)
+            native.node_combine(self.dS[t][sl], self.ego[sl], self.dEc[sl], rptr3[t][sl], redges3[t][sl], Gn,
+                                self.Gb[t][sl], K=K)
 
     def _counts_ready(self, work):
         """Join the (async) count all-reduce, then the device-side action-loss coefficient

@@ -49,3 +49,26 @@ def test_native_rollout_training_step_matches():
     tr.engine.native_rollout = True
     tr.engine.step(s0, g)
     assert torch.equal(g_py, tr.fp.grad)
+
+
+def test_bptt_env_groups_match_single_chain():
+    """Env groups on separate streams: same gradient up to the slab summation order, and
+    deterministic run to run."""
+    tr = _trainer(T=10, B=4)
+    s0, g, _ = tr.sample()
+    tr.engine.step(s0, g)
+    g1 = tr.fp.grad.clone()
+    from macbf_gnn_amd.engine.hip_engine import HipEngine
+    HipEngine.bptt_groups = 2
+    try:
+        tr2 = _trainer(T=10, B=4)
+    finally:
+        HipEngine.bptt_groups = 1
+    assert tr2.engine.bptt_groups == 2
+    tr2.fp.flat.copy_(tr.fp.flat)
+    tr2.engine.after_update()
+    tr2.engine.step(s0, g)
+    g2 = tr2.fp.grad.clone()
+    tr2.engine.step(s0, g)
+    assert torch.equal(g2, tr2.fp.grad)
+    torch.testing.assert_close(g2, g1, rtol=1e-4, atol=1e-6)
