@@ -204,9 +204,99 @@ class RolloutDriver {
   hipEvent_t ev_main_ = nullptr, ev_side_ = nullptr;
 };
 
+// Native BPTT driver: the reverse-time loop of the controller backward (hand-derived adjoints
+// of train.py:58-103's autograd through the rollout). Per step t = T-1..0:
+//   ctrl_node_bwd(t)  <- G_{t+1} (dS_T for the last step)
+//   ctrl_edge_bwd(t)
+//   node_combine(t)   -> G_t
+// over the engine's persistent time-major buffers (pointer offsets validated once in Python).
+// Three dependent launches per step: the loop is GPU-bound at 1024 x 64 agents but host-bound
+// for small scenes (BASELINE config #2: 32 agents), where Python paid ~15 us per launch.
+class BpttDriver {
+ public:
+  explicit BpttDriver(py::dict c) {
+    auto I = [&](const char* k) { return c[k].cast<long>(); };
+    auto F = [&](const char* k) { return c[k].cast<float>(); };
+    auto U = [&](const char* k) { return c[k].cast<u64>(); };
+    B_ = (int)I("B"); N_ = (int)I("N"); Nn_ = (int)I("Nn"); K_ = (int)I("K"); D_ = (int)I("D");
+    R_ = D_ == 2 ? 1 : 2;
+    Tmax_ = (int)I("Tmax"); f16_ = (int)I("f16"); nb_node_ = (int)I("nb_node"); nb_edge_ = (int)I("nb_edge");
+    pooled_ = U("pooled"); S_ = U("S"); G_ = U("G"); A_ = U("A"); dS_ = U("dS"); Gb_ = U("Gb"); valid_ = U("valid");
+    idx_ = U("idx"); argmax_ = U("argmax"); rptr_ = U("rptr"); redges_ = U("redges");
+    wrm_ = U("ctrl_rm"); o1_ = (int)I("o_w1"); o2_ = (int)I("o_w2"); o3_ = (int)I("o_w3"); o4_ = (int)I("o_w4");
+    wvec_ = U("ctrl_v"); act_scale_ = U("act_scale"); dP_ = U("dP"); ego_ = U("ego"); dEc_ = U("dEc");
+    part_node_ = U("part_node"); part_edge_ = U("part_edge");
+    wpack_ = U("ctrl_w"); f_ew1f_ = (int)I("f_ew1f"); f_ew2tn_ = (int)I("f_ew2tn");
+    dt_ = F("dt"); sqrt3_ = F("sqrt3");
+    if (B_ < 1 || N_ < 1 || Nn_ < N_ || K_ < 1 || K_ > 16 || (D_ != 2 && D_ != 3) || Tmax_ < 1 || nb_node_ < 1 ||
+        nb_edge_ < 1)
+      throw std::invalid_argument("BpttDriver: bad dimensions");
+  }
+
+  void run(int T, float act_coef, u64 stream) {
+    if (T < 1 || T > Tmax_) throw std::invalid_argument("BpttDriver: T out of range");
+    hipStream_t st = ST(stream);
+    const long BN = (long)B_ * N_;
+    const long nk = (long)N_ * K_;
+    for (int t = T - 1; t >= 0; --t) {
+      const float4* Gn = t == T - 1 ? P<const float4>(dS_) + (long)T * BN * R_ : P<const float4>(Gb_) + (long)(t + 1) * BN * R_;
+      const float4* St = P<const float4>(S_) + (long)t * B_ * Nn_ * R_;
+      {
+        mb::CtrlNodeBwdArgs a{};
+        a.dim = D_;
+        a.pooled = P<const h16>(pooled_) + (long)t * BN * 128; a.p_env = (long)N_ * 128;
+        a.S = St; a.s_env = Nn_;
+        a.G = P<const float>(G_); a.A = P<const float>(A_) + (long)t * BN * D_; a.a_env = N_;
+        a.Gn = Gn; a.gn_env = N_;
+        a.valid = P<const uint8_t>(valid_) + (long)t * B_; a.v_env = 1;
+        a.B = B_; a.N = N_;
+        a.wrm = P<const h16>(wrm_); a.o_w1 = o1_; a.o_w2 = o2_; a.o_w3 = o3_; a.o_w4 = o4_;
+        a.wvec = P<const float>(wvec_); a.act_coef = act_coef; a.act_scale = P<const float>(act_scale_);
+        a.dt = dt_; a.sqrt3 = sqrt3_;
+        a.dP = P<h16>(dP_); a.dp_env = (long)N_ * 128; a.ego = P<float4>(ego_); a.partial = P<float>(part_node_);
+        chk((f16_ ? mb_ctrl_node_bwd_f16 : mb_ctrl_node_bwd)(&a, nb_node_, st), "ctrl_node_bwd");
+      }
+      {
+        mb::CtrlEdgeBwdArgs a{};
+        a.dim = D_;
+        a.S = St; a.s_env = Nn_;
+        a.idx = P<const int>(idx_) + (long)t * B_ * nk; a.i_env = nk;
+        a.argmax = P<const uint8_t>(argmax_) + (long)t * BN * 128; a.am_env = (long)N_ * 128;
+        a.dP = P<const h16>(dP_); a.dp_env = (long)N_ * 128;
+        a.B = B_; a.N = N_; a.K = K_;
+        a.wpack = P<const h16>(wpack_); a.f_ew1f = f_ew1f_; a.f_ew2tn = f_ew2tn_;
+        a.dEc = P<float4>(dEc_); a.de_env = nk; a.partial = P<float>(part_edge_);
+        chk((f16_ ? mb_ctrl_edge_bwd_f16 : mb_ctrl_edge_bwd)(&a, nb_edge_, st), "ctrl_edge_bwd");
+      }
+      {
+        mb::CombineArgs a{};
+        a.dim = D_;
+        a.dS = P<const float4>(dS_) + (long)t * BN * R_; a.ds_env = N_;
+        a.ego = P<const float4>(ego_); a.dEc = P<const float4>(dEc_);
+        a.ptr = P<const int>(rptr_) + (long)t * B_ * (Nn_ + 1); a.ptr_env = Nn_ + 1;
+        a.edges = P<const int>(redges_) + (long)t * B_ * nk; a.edges_env = nk;
+        a.Gn = Gn; a.gn_env = N_;
+        a.Gout = P<float4>(Gb_) + (long)t * BN * R_; a.go_env = N_;
+        a.B = B_; a.N = N_; a.K = K_; a.dt = dt_;
+        chk(mb_node_combine(&a, st), "node_combine");
+      }
+    }
+  }
+
+ private:
+  int B_, N_, Nn_, K_, D_, R_, Tmax_, f16_, nb_node_, nb_edge_;
+  u64 pooled_, S_, G_, A_, dS_, Gb_, valid_, idx_, argmax_, rptr_, redges_, wrm_, wvec_, act_scale_, dP_, ego_, dEc_;
+  u64 part_node_, part_edge_, wpack_;
+  int o1_, o2_, o3_, o4_, f_ew1f_, f_ew2tn_;
+  float dt_, sqrt3_;
+};
+
 }  // namespace
 
 void register_runtime(py::module& m) {
+  py::class_<BpttDriver>(m, "BpttDriver")
+      .def(py::init<py::dict>())
+      .def("run", &BpttDriver::run, py::arg("T"), py::arg("act_coef"), py::arg("stream"));
   py::class_<RolloutDriver>(m, "RolloutDriver")
       .def(py::init<py::dict>())
       .def("run", &RolloutDriver::run, py::arg("stream"), py::arg("hstream"), py::arg("copy_stream"),

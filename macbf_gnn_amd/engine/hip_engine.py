@@ -33,6 +33,7 @@ class HipEngine:
     overlap_hfwd = True       # CBF h of the main slots runs on a side stream during the rollout
     native_rollout = True     # per-step launch loop in C++ (csrc/runtime.cpp)
     bptt_groups = 1           # independent env groups whose BPTT chains run on separate streams
+    native_bptt = True        # reverse-time BPTT launch loop in C++ (csrc/runtime.cpp)
     reduce_late = 0           # >0: dS steps reduced before the BPTT starts, the rest on the aux stream
                               # during it (A/B on MI355X: neutral-to-slower, 7.63 vs 7.66 ms; off)
 
@@ -49,6 +50,8 @@ class HipEngine:
         if cfg.num_envs % self.bptt_groups:
             self.bptt_groups = 1
         self._drv = None
+        self._bdrv = None
+        self.native_bptt = bool(int(os.environ.get("MACBF_NATIVE_BPTT", int(self.native_bptt))))
         self.bptt = cfg.bptt
         self.reuse = cfg.reuse_nbr_idx
         # deduplicated h/h' evaluations need both roles' state gradients on the same s_t: BPTT only
@@ -471,7 +474,10 @@ class HipEngine:
             rptr3 = rptr[: T * B].view(T, B, Nn + 1)
             redges3 = redges[: T * B].view(T, B, N * K)
             Gp = self.bptt_groups
-            if Gp == 1:
+            if Gp == 1 and red_done is None and self.native_bptt:
+                # the reverse-time launch loop in C++ (csrc/runtime.cpp): same launches, same order
+                self._bdriver().run(T, gs, cur.cuda_stream)
+            elif Gp == 1:
                 self._bptt_chain(T, slice(0, B), valid_u8, gs, rptr3, redges3, self.part_node[: self.nb_node],
                                  self.part_edge[: self.nb_edge], self.nb_node, self.nb_edge, red_done, ts, cur)
             else:
@@ -519,6 +525,37 @@ class HipEngine:
         torch.cat([sums, self.counts, self.local], out=self.raw_stats)
         Tv = T if not self.graph_mode else (valid != 0).any(1).sum()
         return self.raw_stats, Tv
+
+    def _bdriver(self):
+        """The native BPTT driver over this engine's persistent buffers (checked here once)."""
+        if self._bdrv is None:
+            B, N, Nn, K, D, W, T = self.B, self.N, self.Nn, self.K, self.D, self.W, self.Tmax
+            G1 = 0 if self.reuse else 1
+            exp = {"pooled": (self.pooled, self.hdt, (T, B, N, 128)), "S": (self.S, torch.float32, (T + 1, B, Nn, W)),
+                   "G": (self.G, torch.float32, (B, N, D)), "A": (self.A, torch.float32, (T, B, N, D)),
+                   "dS": (self.dS, torch.float32, (T + 1, B, N, W)), "Gb": (self.Gb, torch.float32, (T + 1, B, N, W)),
+                   "valid": (self.valid_buf, torch.uint8, (T, B)), "idx": (self.idx, torch.int32, (T + G1, B, N, K)),
+                   "argmax": (self.argmax, torch.uint8, (T, B, N, 128)),
+                   "rptr": (self.rptr, torch.int32, ((T + G1) * B, Nn + 1)),
+                   "redges": (self.redges, torch.int32, ((T + G1) * B, N * K)),
+                   "act_scale": (self.act_scale, torch.float32, (1,)), "dP": (self.dP, self.hdt, (B, N, 128)),
+                   "ego": (self.ego, torch.float32, (B, N, W)), "dEc": (self.dEc, torch.float32, (B, N, K, W))}
+            for name, (t, dt, shape) in exp.items():
+                native.check(t, dt, shape, name)
+            if self.part_node.shape[0] < self.nb_node or self.part_edge.shape[0] < self.nb_edge:
+                raise native.NativeError("controller slab buffers too small")
+            pw = self.pw
+            c = {k: native.ptr(v[0]) for k, v in exp.items()}
+            c.update(dict(
+                B=B, N=N, Nn=Nn, K=K, D=D, Tmax=T, f16=int(self.hdt == torch.float16),
+                nb_node=int(self.nb_node), nb_edge=int(self.nb_edge),
+                part_node=native.ptr(self.part_node), part_edge=native.ptr(self.part_edge),
+                ctrl_rm=native.ptr(pw.ctrl_rm), o_w1=int(pw.node_rm_off["w1"]), o_w2=int(pw.node_rm_off["w2"]),
+                o_w3=int(pw.node_rm_off["w3"]), o_w4=int(pw.node_rm_off["w4"]), ctrl_v=native.ptr(pw.ctrl_v),
+                ctrl_w=native.ptr(pw.ctrl_w), f_ew1f=int(pw.ctrl_off["ew1f"]), f_ew2tn=int(pw.ctrl_off["ew2tn"]),
+                dt=float(C.TIME_STEP), sqrt3=float(C.SQRT3)))
+            self._bdrv = native.lib().BpttDriver(c)
+        return self._bdrv
 
     def _bptt_chain(self, T, sl, valid_u8, gs, rptr3, redges3, part_node, part_edge, nbn, nbe, red_done, ts, st):
         """Reverse-time BPTT over the envs `sl` on stream `st`: G_t = dL/ds_t from G_{t+1}."""

@@ -72,3 +72,17 @@ def test_bptt_env_groups_match_single_chain():
     tr2.engine.step(s0, g)
     assert torch.equal(g2, tr2.fp.grad)
     torch.testing.assert_close(g2, g1, rtol=1e-4, atol=1e-6)
+
+
+@pytest.mark.parametrize("dim", [2, 3])
+def test_native_bptt_matches_python_loop(dim):
+    tr = _trainer(T=12, dim=dim)
+    s0, g, obs = tr.sample()
+    tr.engine.native_bptt = False
+    tr.engine.step(s0, g, obs)
+    g_py = tr.fp.grad.clone()
+    gb_py = tr.engine.Gb.clone()
+    tr.engine.native_bptt = True
+    tr.engine.step(s0, g, obs)
+    assert torch.equal(g_py, tr.fp.grad)
+    assert torch.equal(gb_py, tr.engine.Gb)
