@@ -58,7 +58,9 @@ class RolloutDriver {
     r2_train_ = F("r2_train"); ttc_train_ = F("ttc_train"); r2_check_ = F("r2_check"); ttc_check_ = F("ttc_check");
     dt_ = F("dt"); obs_r_ = F("obs_r"); sqrt3_ = F("sqrt3"); dist_thr_ = F("dist_thr"); dist_eps_ = F("dist_eps");
     done_thr_ = F("done_thr");
-    if (B_ < 1 || N_ < 1 || Nn_ < N_ || K_ < 1 || K_ > 16 || (D_ != 2 && D_ != 3) || Tmax_ < 1 || resort_ < 1)
+    check_ = (int)I("check_every");
+    if (check_ < 1) check_ = 1;
+    if (B_ < 1|| N_ < 1 || Nn_ < N_ || K_ < 1 || K_ > 16 || (D_ != 2 && D_ != 3) || Tmax_ < 1 || resort_ < 1)
       throw std::invalid_argument("RolloutDriver: bad dimensions");
     ev_copy_.resize(Tmax_);
     for (auto& e : ev_copy_) chk(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
@@ -101,16 +103,28 @@ class RolloutDriver {
         chk(hipMemcpyAsync(P<float>(host_dist_) + (long)t * B_, P<const float>(dist_) + (long)t * B_,
                            sizeof(float) * B_, hipMemcpyDeviceToHost, cs), "hipMemcpyAsync");
         chk(hipEventRecord(ev_copy_[t], cs), "hipEventRecord");
-        if (t >= 1) {
+        // host check every check_every steps (small scenes: a step's kernels take less than
+        // the host round trip, so checking every step would leave the GPU idle)
+        if (t >= 1 && (t % check_ == 0)) {
           chk(hipEventSynchronize(ev_copy_[t - 1]), "hipEventSynchronize");
-          if (all_done(hd, t - 1)) {
-            // every env was done after step t-1: the trajectory is steps 0..t-1; step t's scan
-            // already gave the kNN graph / safety of s_t, its controller step is unused
-            T = t;
+          const int Tf = first_done(hd, t - 1);
+          if (Tf > 0) {
+            // every env was done after step Tf-1: the trajectory is steps 0..Tf-1; step Tf's
+            // scan already gave the kNN graph / safety of s_Tf; later steps are unused
+            T = Tf;
             tail = true;
             break;
           }
         }
+      }
+    }
+    if (early_stop && !tail && check_ > 1 && Tmax_ >= 2) {
+      // steps after the last strided check: same horizon as a check after every step
+      chk(hipEventSynchronize(ev_copy_[Tmax_ - 2]), "hipEventSynchronize");
+      const int Tf = first_done(hd, Tmax_ - 2);
+      if (Tf > 0) {
+        T = Tf;
+        tail = true;
       }
     }
     if (overlap_) {
@@ -126,14 +140,19 @@ class RolloutDriver {
   }
 
  private:
-  bool all_done(const volatile float* hd, int t) const {
-    // env b is done iff its mean goal distance fell below the threshold at some step <= t
+  // Smallest T' (1 <= T' <= t+1) such that every env was done after step T'-1 (env b is done
+  // from the first step q_b whose mean goal distance is below the threshold: T' = max_b q_b + 1),
+  // or 0 if some env is not done by step t. Checking after every step and breaking at the first
+  // hit gives the same T'.
+  int first_done(const volatile float* hd, int t) const {
+    int last = -1;
     for (int b = 0; b < B_; ++b) {
-      bool d = false;
-      for (int q = 0; q <= t && !d; ++q) d = hd[(long)q * B_ + b] / (float)N_ < done_thr_;
-      if (!d) return false;
+      int q = 0;
+      while (q <= t && !(hd[(long)q * B_ + b] / (float)N_ < done_thr_)) ++q;
+      if (q > t) return 0;
+      if (q > last) last = q;
     }
-    return true;
+    return last + 1;
   }
 
   const float4* S_at(int t) const { return P<const float4>(S_) + (long)t * B_ * Nn_ * (W_ / 4); }
@@ -194,7 +213,7 @@ class RolloutDriver {
     chk((f16_ ? mb_cbf_hfwd_f16 : mb_cbf_hfwd)(&a, hfwd_blocks_, hs), "cbf_hfwd");
   }
 
-  int B_, N_, Nn_, K_, D_, W_, Tmax_, num_cu_, f16_, resort_, safety_, overlap_, hfwd_blocks_;
+  int B_, N_, Nn_, K_, D_, W_, Tmax_, num_cu_, f16_, resort_, safety_, overlap_, hfwd_blocks_, check_;
   float L_;
   u64 S_, G_, A_, idx_, dang_, cnt_, safe_, dist_, act_, pooled_, argmax_, perm_, host_dist_;
   u64 ctrl_w_, ctrl_v_, cbf_w_, cbf_rm_, cbf_v_, hbuf_, hmask_, src_, nev_;

@@ -34,6 +34,8 @@ class HipEngine:
     native_rollout = True     # per-step launch loop in C++ (csrc/runtime.cpp)
     bptt_groups = 1           # independent env groups whose BPTT chains run on separate streams
     native_bptt = True        # reverse-time BPTT launch loop in C++ (csrc/runtime.cpp)
+    check_every = 0           # early-stop host check period of the native driver (0: auto -- every
+                              # step at >= 16K agents per rank, up to every 4th for small scenes)
     reduce_late = 0           # >0: dS steps reduced before the BPTT starts, the rest on the aux stream
                               # during it (A/B on MI355X: neutral-to-slower, 7.63 vs 7.66 ms; off)
 
@@ -219,6 +221,7 @@ class HipEngine:
                 resort_every=int(self.resort_every), compute_safety=int(cfg.compute_safety), overlap_hfwd=int(overlap),
                 hfwd_blocks=native.cbf_hfwd_grid(BNK, self.dev), L=float(max(1.0, N / C.AGENT_DENSITY) ** (1.0 / D)),
                 perm=native.ptr(perm), host_dist=int(self.host_dist.data_ptr()),
+                check_every=int(self.check_every or max(1, min(4, 16384 // (B * N)))),
                 ctrl_w=native.ptr(pw.ctrl_w), f_edge=int(pw.ctrl_off["ew1f"]), f_node=int(pw.ctrl_off["nw1f"]),
                 ctrl_v=native.ptr(pw.ctrl_v), cbf_w=native.ptr(pw.cbf_w), f_fwd=int(pw.cbf_off["w1f"]),
                 cbf_rm=native.ptr(pw.cbf_rm), cbf_v=native.ptr(pw.cbf_v),

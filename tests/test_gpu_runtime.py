@@ -30,6 +30,7 @@ def _rollout(tr, native_rollout, s0, g, early_stop):
 @pytest.mark.parametrize("early_stop", [True, False])
 def test_native_rollout_matches_python_loop(early_stop):
     tr = _trainer()
+    tr.engine.check_every = 1
     s0, g, _ = tr.sample()
     a = _rollout(tr, False, s0, g, early_stop)
     b = _rollout(tr, True, s0, g, early_stop)
@@ -86,3 +87,21 @@ def test_native_bptt_matches_python_loop(dim):
     tr.engine.step(s0, g, obs)
     assert torch.equal(g_py, tr.fp.grad)
     assert torch.equal(gb_py, tr.engine.Gb)
+
+
+@pytest.mark.parametrize("every", [2, 3, 5])
+def test_strided_early_stop_check_same_horizon(every):
+    """Checking the early-stop criterion every few steps (small scenes) yields the horizon and
+    trajectory of a check after every step."""
+    tr = _trainer()
+    tr.engine.check_every = 1
+    s0, g, _ = tr.sample()
+    a = _rollout(tr, True, s0, g, True)
+    tr2 = _trainer()
+    tr2.fp.flat.copy_(tr.fp.flat)
+    tr2.engine.after_update()
+    tr2.engine.check_every = every
+    b = _rollout(tr2, True, s0, g, True)
+    assert a[0] == b[0] < tr.cfg.inner_loops
+    for x, y in zip(a[1:], b[1:]):
+        assert torch.equal(x, y)
