@@ -184,6 +184,7 @@ struct CtrlEdgeBwdArgs {
   const h16* wpack;   int f_ew1f, f_ew2tn;   // packed fragments (ew2tn followed by ew1ft)
   float4* dEc;         long de_env;    // (b,i,K) records of dL/d(s_i - s_j) out
   float* partial;                      // (gridDim.x, CTRL_EDGE_PARTIAL) slabs, accumulated
+  int qsplit;                          // workgroups per 128-agent chunk (tile-range split; 1, 2, 4, 8, 16)
 };
 
 struct CsrArgs {

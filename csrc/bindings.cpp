@@ -230,9 +230,10 @@ static int ctrl_node_bwd(u64 pooled, long p_env, u64 S, long s_env, u64 G, u64 A
 
 static int ctrl_edge_bwd(u64 S, long s_env, u64 idx, long i_env, u64 argmax, long am_env, u64 dP, long dp_env,
                          int B, int N, int K, u64 wpack, int f_ew1f, int f_ew2tn, u64 dEc, long de_env, u64 partial,
-                         int dim, int num_blocks, int f16, u64 stream) {
+                         int dim, int num_blocks, int f16, int qsplit, u64 stream) {
   mb::CtrlEdgeBwdArgs a{};
   a.dim = dim;
+  a.qsplit = qsplit;
   a.S = P<const float4>(S); a.s_env = s_env; a.idx = P<const int>(idx); a.i_env = i_env;
   a.argmax = P<const uint8_t>(argmax); a.am_env = am_env; a.dP = P<const h16>(dP); a.dp_env = dp_env;
   a.B = B; a.N = N; a.K = K; a.wpack = P<const h16>(wpack); a.f_ew1f = f_ew1f; a.f_ew2tn = f_ew2tn;

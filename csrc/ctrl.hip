@@ -756,15 +756,23 @@ __global__ __launch_bounds__(EB_WAVES * 64, EB_WAVES == 4 ? 2 : 1) void ctrl_edg
   for (int u = 0; u < EB_TA; ++u) { accW2[u] = zero16(); bs[u] = 0.f; }
   const h16 z = (h16)0.f;
 
-  for (long chunk = blockIdx.x; chunk < nchunks; chunk += gridDim.x) {
+  // work item = (chunk, tile range): small scenes split a chunk's 16 tile rounds over
+  // qsplit workgroups (tiles are independent; every workgroup owns its dW slab), large ones
+  // use qsplit = 1
+  const int QP = a.qsplit > 1 ? a.qsplit : 1;
+  const long nwork = nchunks * QP;
+  for (long w = blockIdx.x; w < nwork; w += gridDim.x) {
+    const long chunk = w / QP;
+    const int part = (int)(w - chunk * QP);
+    const int q0 = part * 16 / QP, q1 = (part + 1) * 16 / QP;
     EdgeIdx xi1;
     EdgeSt<D> xs0;
     const int g0 = (int)(chunk * EB_CH) + wave * 32;
     {
       EdgeIdx xi0;
-      ctrl_idx_load(a.idx, a.i_env, N, K, g0, 0, r, total, xi0);
+      ctrl_idx_load(a.idx, a.i_env, N, K, g0, q0, r, total, xi0);
       ctrl_st_load<D>(a.S, a.s_env, xi0, xs0);
-      ctrl_idx_load(a.idx, a.i_env, N, K, g0, 1, r, total, xi1);
+      ctrl_idx_load(a.idx, a.i_env, N, K, g0, q0 + 1, r, total, xi1);
     }
     // argmax slots / dL/dpooled of the tile's two agents (lane (r, h): agent 2q+h, features
     // 4r..4r+3): loaded one tile ahead, like the edge gathers
@@ -779,8 +787,8 @@ __global__ __launch_bounds__(EB_WAVES * 64, EB_WAVES == 4 ? 2 : 1) void ctrl_edg
     };
     unsigned am_n;
     h16x4 dp_n;
-    pool_load(0, am_n, dp_n);
-    for (int q = 0; q < 16; ++q) {
+    pool_load(q0, am_n, dp_n);
+    for (int q = q0; q < q1; ++q) {
       const EdgeSt<D> cur = xs0;
       const unsigned am4 = am_n;
       const h16x4 dp4 = dp_n;

@@ -240,6 +240,7 @@ class BpttDriver {
     B_ = (int)I("B"); N_ = (int)I("N"); Nn_ = (int)I("Nn"); K_ = (int)I("K"); D_ = (int)I("D");
     R_ = D_ == 2 ? 1 : 2;
     Tmax_ = (int)I("Tmax"); f16_ = (int)I("f16"); nb_node_ = (int)I("nb_node"); nb_edge_ = (int)I("nb_edge");
+    qsplit_ = (int)I("qsplit");
     pooled_ = U("pooled"); S_ = U("S"); G_ = U("G"); A_ = U("A"); dS_ = U("dS"); Gb_ = U("Gb"); valid_ = U("valid");
     idx_ = U("idx"); argmax_ = U("argmax"); rptr_ = U("rptr"); redges_ = U("redges");
     wrm_ = U("ctrl_rm"); o1_ = (int)I("o_w1"); o2_ = (int)I("o_w2"); o3_ = (int)I("o_w3"); o4_ = (int)I("o_w4");
@@ -284,7 +285,7 @@ class BpttDriver {
         a.dP = P<const h16>(dP_); a.dp_env = (long)N_ * 128;
         a.B = B_; a.N = N_; a.K = K_;
         a.wpack = P<const h16>(wpack_); a.f_ew1f = f_ew1f_; a.f_ew2tn = f_ew2tn_;
-        a.dEc = P<float4>(dEc_); a.de_env = nk; a.partial = P<float>(part_edge_);
+        a.dEc = P<float4>(dEc_); a.de_env = nk; a.partial = P<float>(part_edge_); a.qsplit = qsplit_;
         chk((f16_ ? mb_ctrl_edge_bwd_f16 : mb_ctrl_edge_bwd)(&a, nb_edge_, st), "ctrl_edge_bwd");
       }
       {
@@ -303,7 +304,7 @@ class BpttDriver {
   }
 
  private:
-  int B_, N_, Nn_, K_, D_, R_, Tmax_, f16_, nb_node_, nb_edge_;
+  int B_, N_, Nn_, K_, D_, R_, Tmax_, f16_, nb_node_, nb_edge_, qsplit_;
   u64 pooled_, S_, G_, A_, dS_, Gb_, valid_, idx_, argmax_, rptr_, redges_, wrm_, wvec_, act_scale_, dP_, ego_, dEc_;
   u64 part_node_, part_edge_, wpack_;
   int o1_, o2_, o3_, o4_, f_ew1f_, f_ew2tn_;

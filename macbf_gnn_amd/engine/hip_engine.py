@@ -552,6 +552,7 @@ class HipEngine:
             c.update(dict(
                 B=B, N=N, Nn=Nn, K=K, D=D, Tmax=T, f16=int(self.hdt == torch.float16),
                 nb_node=int(self.nb_node), nb_edge=int(self.nb_edge),
+                qsplit=int(native.ctrl_edge_qsplit(B * N, self.dev)),
                 part_node=native.ptr(self.part_node), part_edge=native.ptr(self.part_edge),
                 ctrl_rm=native.ptr(pw.ctrl_rm), o_w1=int(pw.node_rm_off["w1"]), o_w2=int(pw.node_rm_off["w2"]),
                 o_w3=int(pw.node_rm_off["w3"]), o_w4=int(pw.node_rm_off["w4"]), ctrl_v=native.ptr(pw.ctrl_v),

@@ -599,13 +599,26 @@ def node_combine(dS_t, ego, dEc, rptr_t, redges_t, Gn, Gout, *, K, dt=C.TIME_STE
 CTRL_EDGE_WAVES = 4          # csrc/ctrl.hip EB_WAVES
 
 
+def ctrl_edge_qsplit(total_agents: int, device) -> int:
+    """Workgroups per 128-agent chunk of the edge backward: small scenes split a chunk's 16 tile
+    rounds over up to 16 workgroups (the tiles are independent; a single wave would otherwise
+    run all of them back to back); 1 once the chunks alone fill the GPU."""
+    che = (total_agents + 32 * CTRL_EDGE_WAVES - 1) // (32 * CTRL_EDGE_WAVES)
+    cap = (8 // CTRL_EDGE_WAVES) * num_cu(device)
+    p = 1
+    while p < 16 and che * p * 2 <= cap:
+        p *= 2
+    return p
+
+
 def ctrl_bwd_grids(total_agents: int, device):
     """(node, edge) backward grids: the node kernel takes 128-agent chunks, one workgroup per CU;
-    the edge kernel 32*CTRL_EDGE_WAVES-agent chunks (8 waves: one workgroup per CU)."""
+    the edge kernel 32*CTRL_EDGE_WAVES-agent chunks x ctrl_edge_qsplit tile ranges (4 waves: two
+    workgroups per CU)."""
     ch = (total_agents + 127) // 128
     che = (total_agents + 32 * CTRL_EDGE_WAVES - 1) // (32 * CTRL_EDGE_WAVES)
     cu = num_cu(device)
-    return max(1, min(ch, cu)), max(1, min(che, (8 // CTRL_EDGE_WAVES) * cu))
+    return max(1, min(ch, cu)), max(1, min(che * ctrl_edge_qsplit(total_agents, device), (8 // CTRL_EDGE_WAVES) * cu))
 
 
 def ctrl_node_bwd(pooled, S, G, A, Gn, valid_t, wrm, offs, wvec, act_coef, dP, ego, partial, num_blocks,
@@ -653,7 +666,7 @@ def ctrl_edge_bwd(S, idx, argmax, dP, wpack, f_ew1f, f_ew2tn, dEc, partial, num_
     rc = lib().ctrl_edge_bwd(ptr(S), S.stride(0) // W, ptr(idx), idx.stride(0), ptr(argmax), argmax.stride(0),
                              ptr(dP), dP.stride(0), B, N, K, ptr(wpack), int(f_ew1f), int(f_ew2tn), ptr(dEc),
                              dEc.stride(0) // W if dEc is not None else 0, ptr(partial), D, int(num_blocks),
-                             f16, stream_handle())
+                             f16, ctrl_edge_qsplit(B * N, S.device), stream_handle())
     _ok(rc, "ctrl_edge_bwd")
 
 
