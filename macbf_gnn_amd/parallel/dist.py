@@ -35,7 +35,10 @@ class DP:
         self.owns_pg = False
         if self.world > 1 and not dist.is_initialized():
             if backend is None:
-                backend = "nccl" if (device is not None and device.type == "cuda") else "gloo"
+                # MACBF_DP_BACKEND=gloo rehearses multi-rank runs with several ranks sharing one
+                # GPU (RCCL places one rank per device)
+                backend = os.environ.get("MACBF_DP_BACKEND") or (
+                    "nccl" if (device is not None and device.type == "cuda") else "gloo")
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
             kw = {}
             if backend == "nccl" and device is not None:
