@@ -60,6 +60,7 @@ struct CtrlArgs {
   float dt, obs_r, sqrt3;
   h16* pooled;     long p_env;       // (b,i,128) max-pooled edge features out (h16), or null
   uint8_t* argmax;  long am_env;      // (b,i,128) winning slot per feature (0xFF: no grad), or null
+  int apw;                            // agents per wave (even, 2..32; 0 = 32): small scenes use fewer
 };
 
 struct LossConsts {

@@ -49,9 +49,11 @@ static int scenario(u64 S, long s_env, u64 G, u64 obs, int M, int dim, int B, in
 static int ctrl_fwd(u64 S, long s_env, u64 G, u64 idx, long i_env, int B, int N, int K, u64 wpack, int f_edge,
                     int f_node, u64 wvec, u64 A, long a_env, u64 Sn, long sn_env, u64 dist_sum, long d_env,
                     u64 act_sum, long ac_env, u64 noise, long n_env, float dt, float obs_r, float sqrt3,
-                    u64 pooled, long p_env, u64 argmax, long am_env, int dim, int num_cu, int f16, u64 stream) {
+                    u64 pooled, long p_env, u64 argmax, long am_env, int dim, int num_cu, int f16, int apw,
+                    u64 stream) {
   mb::CtrlArgs a{};
   a.dim = dim;
+  a.apw = apw;
   a.S = P<const float4>(S); a.s_env = s_env; a.G = P<const float>(G); a.idx = P<const int>(idx); a.i_env = i_env;
   a.B = B; a.N = N; a.K = K; a.wpack = P<const h16>(wpack); a.f_edge = f_edge; a.f_node = f_node;
   a.wvec = P<const float>(wvec); a.A = P<float>(A); a.a_env = a_env; a.Snext = P<float4>(Sn); a.sn_env = sn_env;

@@ -213,8 +213,11 @@ __global__ __launch_bounds__(WAVES * 64) void ctrl_fwd_kernel(CtrlArgs a) {
   const int N = a.N, K = a.K;
   const int total = a.B * N;
 
-  for (int grp = blockIdx.x * WAVES + wave; grp * 32 < total; grp += gridDim.x * WAVES) {
-    const int g0 = grp * 32;
+  // agents per wave: 32, or 4..16 for small scenes (more waves share the edge phase; the node
+  // phase's MFMA rows beyond APW carry ignored data)
+  const int APW = (a.apw >= 2 && a.apw <= 32) ? a.apw : 32;
+  for (int grp = blockIdx.x * WAVES + wave; grp * APW < total; grp += gridDim.x * WAVES) {
+    const int g0 = grp * APW;
     // ---------------- edge phase: 16 tiles x (2 agents x 16 slots); the gathers of tile q+1
     // (idx -> s_j, dependent global loads) are issued before tile q's MFMA chain
     EdgeIdx xi1;
@@ -225,7 +228,7 @@ __global__ __launch_bounds__(WAVES * 64) void ctrl_fwd_kernel(CtrlArgs a) {
       ctrl_st_load<D>(a.S, a.s_env, xi0, xs0);
       ctrl_idx_load(a.idx, a.i_env, N, K, g0, 1, r, total, xi1);
     }
-    for (int q = 0; q < 16; ++q) {
+    for (int q = 0; q < APW / 2; ++q) {
       const EdgeSt<D> cur = xs0;
       ctrl_st_load<D>(a.S, a.s_env, xi1, xs0);                    // states of tile q+1
       ctrl_idx_load(a.idx, a.i_env, N, K, g0, q + 2, r, total, xi1);   // idx of tile q+2
@@ -279,7 +282,7 @@ __global__ __launch_bounds__(WAVES * 64) void ctrl_fwd_kernel(CtrlArgs a) {
       for (int u = lane; u < 32 * 16; u += 64) {
         const int ag = u >> 4, ch = u & 15;
         const int ga = g0 + ag;
-        if (ga < total) {
+        if (ag < APW && ga < total) {
           const int bb = ga / N, ii = ga - bb * N;
           *reinterpret_cast<h16x8*>(a.pooled + (long)bb * a.p_env + (long)ii * 128 + ch * 8) =
               *reinterpret_cast<const h16x8*>(pool + ag * PSTR + ch * 8);
@@ -292,7 +295,7 @@ __global__ __launch_bounds__(WAVES * 64) void ctrl_fwd_kernel(CtrlArgs a) {
 #endif
     // ---------------- node phase: lane column r = agent g0 + r
     const int gi = g0 + r;
-    const bool ok = gi < total;
+    const bool ok = r < APW && gi < total;
     int b = 0, i = 0;
     float sp[D], sv[D], gg[D];
 #pragma unroll
@@ -339,7 +342,7 @@ __global__ __launch_bounds__(WAVES * 64) void ctrl_fwd_kernel(CtrlArgs a) {
       asum = fabsf(sqsum<D>(av) - sqsum<D>(ar));
     }
     // per-env sums: one atomic per wave when its 32 agents share an env
-    const int last = min(g0 + 31, total - 1);
+    const int last = min(g0 + APW - 1, total - 1);
     if (g0 / N == last / N) {
       dsum = wave_sum(dsum);
       asum = wave_sum(asum);
@@ -370,7 +373,8 @@ extern "C" int MB_SYM(ctrl_fwd)(const mb::CtrlArgs* a, int num_cu, hipStream_t s
   using namespace mb;
   using namespace mb::MB_PREC;
   if (a->K > 16 || a->K < 1) return -1;
-  const int groups = (a->B * a->N + 31) / 32;
+  const int apw = (a->apw >= 2 && a->apw <= 32) ? a->apw : 32;
+  const int groups = (a->B * a->N + apw - 1) / apw;
   int blocks = (groups + CTRL_WAVES - 1) / CTRL_WAVES;
   const int maxb = num_cu > 0 ? num_cu * 2 : blocks;
   if (blocks > maxb) blocks = maxb;

@@ -59,6 +59,7 @@ class RolloutDriver {
     dt_ = F("dt"); obs_r_ = F("obs_r"); sqrt3_ = F("sqrt3"); dist_thr_ = F("dist_thr"); dist_eps_ = F("dist_eps");
     done_thr_ = F("done_thr");
     check_ = (int)I("check_every");
+    apw_ = (int)I("apw");
     if (check_ < 1) check_ = 1;
     if (B_ < 1|| N_ < 1 || Nn_ < N_ || K_ < 1 || K_ > 16 || (D_ != 2 && D_ != 3) || Tmax_ < 1 || resort_ < 1)
       throw std::invalid_argument("RolloutDriver: bad dimensions");
@@ -194,6 +195,7 @@ class RolloutDriver {
     a.dt = dt_; a.obs_r = obs_r_; a.sqrt3 = sqrt3_;
     a.pooled = P<h16>(pooled_) + (long)t * B_ * N_ * 128; a.p_env = (long)N_ * 128;
     a.argmax = P<uint8_t>(argmax_) + (long)t * B_ * N_ * 128; a.am_env = (long)N_ * 128;
+    a.apw = apw_;
     chk((f16_ ? mb_ctrl_fwd_f16 : mb_ctrl_fwd)(&a, num_cu_, st), "ctrl_fwd");
   }
 
@@ -213,7 +215,7 @@ class RolloutDriver {
     chk((f16_ ? mb_cbf_hfwd_f16 : mb_cbf_hfwd)(&a, hfwd_blocks_, hs), "cbf_hfwd");
   }
 
-  int B_, N_, Nn_, K_, D_, W_, Tmax_, num_cu_, f16_, resort_, safety_, overlap_, hfwd_blocks_, check_;
+  int B_, N_, Nn_, K_, D_, W_, Tmax_, num_cu_, f16_, resort_, safety_, overlap_, hfwd_blocks_, check_, apw_;
   float L_;
   u64 S_, G_, A_, idx_, dang_, cnt_, safe_, dist_, act_, pooled_, argmax_, perm_, host_dist_;
   u64 ctrl_w_, ctrl_v_, cbf_w_, cbf_rm_, cbf_v_, hbuf_, hmask_, src_, nev_;
@@ -288,7 +290,7 @@ class BpttDriver {
         a.dEc = P<float4>(dEc_); a.de_env = nk; a.partial = P<float>(part_edge_); a.qsplit = qsplit_;
         chk((f16_ ? mb_ctrl_edge_bwd_f16 : mb_ctrl_edge_bwd)(&a, nb_edge_, st), "ctrl_edge_bwd");
       }
-      {
+      if (t > 0) {   // G_0 = dL/ds_0 is not needed (s_0 is sampled, not a function of the weights)
         mb::CombineArgs a{};
         a.dim = D_;
         a.dS = P<const float4>(dS_) + (long)t * BN * R_; a.ds_env = N_;

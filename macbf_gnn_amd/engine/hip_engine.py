@@ -222,6 +222,7 @@ class HipEngine:
                 hfwd_blocks=native.cbf_hfwd_grid(BNK, self.dev), L=float(max(1.0, N / C.AGENT_DENSITY) ** (1.0 / D)),
                 perm=native.ptr(perm), host_dist=int(self.host_dist.data_ptr()),
                 check_every=int(self.check_every or max(1, min(4, 16384 // (B * N)))),
+                apw=int(native.ctrl_fwd_apw(B * N, self.dev, N)),
                 ctrl_w=native.ptr(pw.ctrl_w), f_edge=int(pw.ctrl_off["ew1f"]), f_node=int(pw.ctrl_off["nw1f"]),
                 ctrl_v=native.ptr(pw.ctrl_v), cbf_w=native.ptr(pw.cbf_w), f_fwd=int(pw.cbf_off["w1f"]),
                 cbf_rm=native.ptr(pw.cbf_rm), cbf_v=native.ptr(pw.cbf_v),
@@ -573,8 +574,9 @@ class HipEngine:
                                  part_node, nbn, act_scale=self.act_scale)
             native.ctrl_edge_bwd(self.S[t][sl], self.idx[t][sl], self.argmax[t][sl], self.dP[sl], pw.ctrl_w,
                                  pw.ctrl_off["ew1f"], pw.ctrl_off["ew2tn"], self.dEc[sl], part_edge, nbe)
-            native.node_combine(self.dS[t][sl], self.ego[sl], self.dEc[sl], rptr3[t][sl], redges3[t][sl], Gn,
-                                self.Gb[t][sl], K=K)
+            if t > 0:      # G_0 = dL/ds_0 is not needed (s_0 is sampled, not a function of the weights)
+                native.node_combine(self.dS[t][sl], self.ego[sl], self.dEc[sl], rptr3[t][sl], redges3[t][sl], Gn,
+                                    self.Gb[t][sl], K=K)
 
     def _counts_ready(self, work):
         """Join the (async) count all-reduce, then the device-side action-loss coefficient

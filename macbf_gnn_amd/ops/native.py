@@ -281,8 +281,24 @@ def ctrl_fwd(S, G, idx, wpack, f_edge, f_node, wvec, A, Sn, dist_sum, act_sum, n
                         float(C.TIME_STEP), float(C.OBS_RADIUS), float(C.SQRT3),
                         ptr(pooled), pooled.stride(0) if pooled is not None else 0,
                         ptr(argmax), argmax.stride(0) if argmax is not None else 0,
-                        D, num_cu(S.device), f16, stream_handle())
+                        D, num_cu(S.device), f16, ctrl_fwd_apw(B * N, S.device, N), stream_handle())
     _ok(rc, "ctrl_fwd")
+
+
+def ctrl_fwd_apw(total_agents: int, device, n_agents: int | None = None) -> int:
+    """Agents per wave of the controller step: 32, halved (down to 4) while the scene has fewer
+    32-agent groups than two per CU, so small scenes spread the edge phase over more waves --
+    but only while every env stays covered by at most two whole waves (the per-env goal-distance
+    sums are float atomics: two addends commute, more would make the early-stop input depend
+    on the arrival order)."""
+    apw, cap = 32, 2 * num_cu(device)
+    n = total_agents if n_agents is None else int(n_agents)
+    for cand in (16, 8, 4):
+        if (total_agents + apw - 1) // apw >= cap:
+            break
+        if n % cand == 0 and n <= 2 * cand:
+            apw = cand
+    return apw
 
 
 LOSS_CONSTS = (C.LOSS_EPS_DANG, C.TIME_STEP * C.ALPHA_CBF, C.LOSS_WEIGHTS[0], C.LOSS_WEIGHTS[1],
