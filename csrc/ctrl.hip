@@ -698,6 +698,9 @@ d1b[mt] = to_h16x16(c);
     }
   }
   // ---- slab += this workgroup's partial (fixed WG -> slab map: deterministic)
+#ifdef CTRL_X_NOSLAB
+  if (a.partial) return;                        // ablation: no slab read-modify-write
+#endif
   float* P = a.partial + (long)blockIdx.x * CTRL_NODE_PARTIAL;
 #pragma unroll
   for (int u = 0; u < 3; ++u) {
@@ -912,6 +915,9 @@ __global__ __launch_bounds__(EB_WAVES * 64, EB_WAVES == 4 ? 2 : 1) void ctrl_edg
 #endif
     }
   }
+#ifdef CTRL_X_NOSLAB
+  if (a.partial) return;                        // ablation: no slab read-modify-write
+#endif
   float* P = a.partial + (long)blockIdx.x * CTRL_EDGE_PARTIAL;
   __shared__ float ebred[EB_WAVES][EB_TA][32];
 #pragma unroll
