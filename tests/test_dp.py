@@ -1,8 +1,9 @@
-"""Data parallelism without a cluster: gloo on CPU, world_size 2.
+"""Data parallelism without a cluster: gloo on CPU, world_size 2 and 4.
 
 * the DP all-reduced gradient equals the single-process gradient on the concatenated env
   batch (global pooled loss normalisation);
-* parameters stay bit-identical across ranks after k optimizer steps.
+* parameters stay bit-identical across ranks after k optimizer steps;
+* a checkpoint written by a DP run resumes in a run of a different width.
 """
 import os
 import socket
@@ -39,7 +40,14 @@ def _worker(rank, world, port, outdir, mode):
     B = 4 // world
     tr = Trainer(_cfg(B), device=torch.device("cpu"), dp=dp)
     sl = slice(rank * B, (rank + 1) * B)
-    if mode == "grad":
+    if mode == "ckpt":
+        for it in range(4):
+            if it == 2:
+                tr.save(os.path.join(outdir, "ck.pt"))
+            s, g = E.generate_batch(4, 10, seed=200 + it)
+            tr.train_step(s[sl], g[sl])
+        torch.save(tr.fp.flat.clone(), os.path.join(outdir, f"flat{rank}.pt"))
+    elif mode == "grad":
         tr.engine.step(s_all[sl], g_all[sl])
         dp.all_reduce_(tr.fp.grad)
         torch.save(tr.fp.grad.clone(), os.path.join(outdir, f"grad{rank}.pt"))
@@ -57,11 +65,12 @@ def _run(world, outdir, mode):
 
 
 @pytest.mark.timeout(600)
-def test_dp_grad_equals_single_process(tmp_path):
-    _run(2, tmp_path, "grad")
+@pytest.mark.parametrize("world", [2, 4])
+def test_dp_grad_equals_single_process(tmp_path, world):
+    _run(world, tmp_path, "grad")
     g0 = torch.load(tmp_path / "grad0.pt", weights_only=True)
-    g1 = torch.load(tmp_path / "grad1.pt", weights_only=True)
-    assert torch.equal(g0, g1)
+    for r in range(1, world):
+        assert torch.equal(g0, torch.load(tmp_path / f"grad{r}.pt", weights_only=True))
     from macbf_gnn_amd.engine import Trainer
     from macbf_gnn_amd.parallel import DP
     s_all, g_all = E.generate_batch(4, 10, seed=11)
@@ -76,3 +85,24 @@ def test_dp_params_identical_across_ranks(tmp_path):
     f0 = torch.load(tmp_path / "flat0.pt", weights_only=True)
     f1 = torch.load(tmp_path / "flat1.pt", weights_only=True)
     assert torch.equal(f0, f1)
+
+
+@pytest.mark.timeout(600)
+def test_dp_checkpoint_resumes_at_other_width(tmp_path):
+    """DP-2 run saves after 2 of 4 iterations; a 1-process run resumes from that checkpoint on
+    the full env batch and must land on the DP-2 run's final parameters."""
+    _run(2, tmp_path, "ckpt")
+    f0 = torch.load(tmp_path / "flat0.pt", weights_only=True)
+    assert torch.equal(f0, torch.load(tmp_path / "flat1.pt", weights_only=True))
+    from macbf_gnn_amd.engine import Trainer
+    from macbf_gnn_amd.parallel import DP
+    from macbf_gnn_amd.utils import ckpt
+    tr = Trainer(C.TrainConfig(num_agents=10, num_envs=4, inner_loops=6, device="cpu", seed=99,
+                               early_stop=True, train_steps=1),
+                 device=torch.device("cpu"), dp=DP(device=torch.device("cpu")))
+    ckpt.load(tr, str(tmp_path / "ck.pt"))
+    assert tr.step_count == 2
+    for it in range(2, 4):
+        s, g = E.generate_batch(4, 10, seed=200 + it)
+        tr.train_step(s, g)
+    torch.testing.assert_close(tr.fp.flat, f0, rtol=1e-4, atol=2e-6)
