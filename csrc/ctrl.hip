@@ -423,6 +423,22 @@ DEV void add_tile(float* dst, int ncols, int mt, int nt, const f32x16& c, int la
   for (int reg = 0; reg < 16; ++reg) dst[(32 * mt + acc_row(reg, h)) * ncols + 32 * nt + r] += c[reg];
 }
 
+// Split slab read-modify-write: the compiler may not move a slab load above an earlier slab
+// store (same base pointer, runtime tile offsets), so back-to-back add_tile calls serialise one
+// memory round trip per tile. Tails load every owned slab element first (load_tile), then add
+// and store (store_tile_add): one round trip in total.
+DEV void load_tile(f32x16& v, const float* src, int ncols, int mt, int nt, int lane) {
+  const int r = lane & 31, h = lane >> 5;
+#pragma unroll
+  for (int reg = 0; reg < 16; ++reg) v[reg] = src[(32 * mt + acc_row(reg, h)) * ncols + 32 * nt + r];
+}
+
+DEV void store_tile_add(float* dst, int ncols, int mt, int nt, const f32x16& old, const f32x16& c, int lane) {
+  const int r = lane & 31, h = lane >> 5;
+#pragma unroll
+  for (int reg = 0; reg < 16; ++reg) dst[(32 * mt + acc_row(reg, h)) * ncols + 32 * nt + r] = old[reg] + c[reg];
+}
+
 template <int D>
 __global__ __launch_bounds__(NB_WAVES * 64, 1) void ctrl_node_bwd_kernel(CtrlNodeBwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -702,27 +718,47 @@ d1b[mt] = to_h16x16(c);
   if (a.partial) return;                        // ablation: no slab read-modify-write
 #endif
   float* P = a.partial + (long)blockIdx.x * CTRL_NODE_PARTIAL;
+  // all slab loads first (see load_tile), then the adds and stores
+  f32x16 o1[3], o2[2], o3[2], o4;
+  float ob2[2], ob3[2], ob4 = 0.f;
 #pragma unroll
   for (int u = 0; u < 3; ++u) {
     const int t = wave + 4 * u;
-    if (u < n1) add_tile(P + NP_W1, 160, t / 5, t % 5, acc1[u], lane);
+    if (u < n1) load_tile(o1[u], P + NP_W1, 160, t / 5, t % 5, lane);
+  }
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int t = wave + 4 * u;
+    load_tile(o2[u], P + NP_W2, 64, t / 2, t % 2, lane);
+    load_tile(o3[u], P + NP_W3, 128, t / 4, t % 4, lane);
+    ob2[u] = P[NP_B2 + 32 * (t / 2) + r];
+    ob3[u] = P[NP_B3 + 32 * (t / 4) + r];
+  }
+  if (wave < 2) {
+    load_tile(o4, P + NP_W4, 64, 0, wave, lane);
+    ob4 = P[NP_B4 + r];
+  }
+#pragma unroll
+  for (int u = 0; u < 3; ++u) {
+    const int t = wave + 4 * u;
+    if (u < n1) store_tile_add(P + NP_W1, 160, t / 5, t % 5, o1[u], acc1[u], lane);
   }
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
     const int t2 = wave + 4 * u;
-    add_tile(P + NP_W2, 64, t2 / 2, t2 % 2, acc2[u], lane);
+    store_tile_add(P + NP_W2, 64, t2 / 2, t2 % 2, o2[u], acc2[u], lane);
     const float s2 = bs2[u] + shfl_xor32(bs2[u]);
-    if (t2 % 2 == 0 && h == 0) P[NP_B2 + 32 * (t2 / 2) + r] += s2;
+    if (t2 % 2 == 0 && h == 0) P[NP_B2 + 32 * (t2 / 2) + r] = ob2[u] + s2;
     const int t3 = wave + 4 * u;
-    add_tile(P + NP_W3, 128, t3 / 4, t3 % 4, acc3[u], lane);
+    store_tile_add(P + NP_W3, 128, t3 / 4, t3 % 4, o3[u], acc3[u], lane);
     const float s3 = bs3[u] + shfl_xor32(bs3[u]);
-    if (t3 % 4 == 0 && h == 0) P[NP_B3 + 32 * (t3 / 4) + r] += s3;
+    if (t3 % 4 == 0 && h == 0) P[NP_B3 + 32 * (t3 / 4) + r] = ob3[u] + s3;
   }
   if (wave < 2) {
-    add_tile(P + NP_W4, 64, 0, wave, acc4, lane);
+    store_tile_add(P + NP_W4, 64, 0, wave, o4, acc4, lane);
     if (wave == 0) {
       const float s4 = bs4 + shfl_xor32(bs4);
-      if (h == 0) P[NP_B4 + r] += s4;
+      if (h == 0) P[NP_B4 + r] = ob4 + s4;
     }
   }
 }
@@ -920,10 +956,24 @@ __global__ __launch_bounds__(EB_WAVES * 64, EB_WAVES == 4 ? 2 : 1) void ctrl_edg
 #endif
   float* P = a.partial + (long)blockIdx.x * CTRL_EDGE_PARTIAL;
   __shared__ float ebred[EB_WAVES][EB_TA][32];
+  // every slab load of the tail first (see load_tile): dW2 tiles, this thread's dW1 elements,
+  // the eb2 element
+  constexpr int NQ1 = 2 * 32 * 32 / (EB_WAVES * 64);
+  f32x16 o2[EB_TA];
+  float o1[NQ1];
+  float ob2 = 0.f;
 #pragma unroll
   for (int u = 0; u < EB_TA; ++u) {
     const int t = wave + EB_WAVES * u;
-    add_tile(P + EP_W2, 64, t / 2, t % 2, accW2[u], lane);
+    load_tile(o2[u], P + EP_W2, 64, t / 2, t % 2, lane);
+  }
+#pragma unroll
+  for (int j = 0; j < NQ1; ++j) o1[j] = P[EP_W1 + threadIdx.x + j * EB_WAVES * 64];
+  if (threadIdx.x < 128) ob2 = P[EP_B2 + threadIdx.x];
+#pragma unroll
+  for (int u = 0; u < EB_TA; ++u) {
+    const int t = wave + EB_WAVES * u;
+    store_tile_add(P + EP_W2, 64, t / 2, t % 2, o2[u], accW2[u], lane);
     const float s = bs[u] + shfl_xor32(bs[u]);
     if (h == 0) ebred[wave][u][r] = s;
   }
@@ -937,10 +987,12 @@ __global__ __launch_bounds__(EB_WAVES * 64, EB_WAVES == 4 ? 2 : 1) void ctrl_edg
     for (int reg = 0; reg < 16; ++reg)
       w1red[((wave * 2 + mt) * 32 + acc_row(reg, h)) * 32 + r] = accW1[mt][reg];
   __syncthreads();
-  for (int q = threadIdx.x; q < 2 * 32 * 32; q += EB_WAVES * 64) {
+#pragma unroll
+  for (int j = 0; j < NQ1; ++j) {
+    const int q = threadIdx.x + j * EB_WAVES * 64;
     float t = 0.f;
     for (int w = 0; w < EB_WAVES; ++w) t += w1red[w * 2048 + q];
-    P[EP_W1 + q] += t;                            // rows 32mt + row, 32 cols: the slab layout
+    P[EP_W1 + q] = o1[j] + t;                     // rows 32mt + row, 32 cols: the slab layout
   }
   __syncthreads();
   // eb2 row block mt was summed half by the owner of tile 2mt and half by the owner of tile
@@ -948,7 +1000,7 @@ __global__ __launch_bounds__(EB_WAVES * 64, EB_WAVES == 4 ? 2 : 1) void ctrl_edg
   if (threadIdx.x < 128) {
     const int mt = threadIdx.x >> 5, rr = threadIdx.x & 31;    // row block 0..3
     const int t0 = 2 * mt, t1 = 2 * mt + 1;
-    P[EP_B2 + 32 * mt + rr] += ebred[t0 % EB_WAVES][t0 / EB_WAVES][rr] + ebred[t1 % EB_WAVES][t1 / EB_WAVES][rr];
+    P[EP_B2 + 32 * mt + rr] = ob2 + (ebred[t0 % EB_WAVES][t0 / EB_WAVES][rr] + ebred[t1 % EB_WAVES][t1 / EB_WAVES][rr]);
   }
 }
 
