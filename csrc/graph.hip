@@ -211,6 +211,16 @@ __global__ __launch_bounds__(256) void node_combine_kernel(CombineArgs a) {
   float4 g[R];
 #pragma unroll
   for (int q = 0; q < R; ++q) g[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+  // the group leader's per-node records are requested before the edge gathers so that their
+  // latency overlaps the gather + group reduction instead of following it
+  float gp[D], gv[D], p[D], v[D], np_[D], nv[D];
+#pragma unroll
+  for (int q = 0; q < D; ++q) { gp[q] = gv[q] = p[q] = v[q] = np_[q] = nv[q] = 0.f; }
+  if (l == 0) {
+    load_rec<D>(a.dS + (long)b * a.ds_env * R, (unsigned)i, gp, gv);
+    if (a.ego) load_rec<D>(a.ego + (long)b * N * R, (unsigned)i, p, v);
+    if (a.Gn) load_rec<D>(a.Gn + (long)b * a.gn_env * R, (unsigned)i, np_, nv);
+  }
   if (a.dEc) {
     const float4* dE = a.dEc + (long)b * N * K * R;
     for (int k = l; k < K; k += RG) acc_rec<R, 1>(g, dE + ((long)i * K + k) * R);
@@ -221,10 +231,7 @@ __global__ __launch_bounds__(256) void node_combine_kernel(CombineArgs a) {
     grp_sum<R>(g);
   }
   if (l != 0) return;
-  float gp[D], gv[D], p[D], v[D];
-  load_rec<D>(a.dS + (long)b * a.ds_env * R, (unsigned)i, gp, gv);
   if (a.ego) {
-    load_rec<D>(a.ego + (long)b * N * R, (unsigned)i, p, v);
 #pragma unroll
     for (int q = 0; q < D; ++q) { gp[q] += p[q]; gv[q] += v[q]; }
   }
@@ -238,9 +245,8 @@ __global__ __launch_bounds__(256) void node_combine_kernel(CombineArgs a) {
   }
   if (a.Gn) {
     // Euler adjoint of s_{t+1} = s_t + dt [v_t, a_t]: dp += G_p, dv += G_v + dt G_p
-    load_rec<D>(a.Gn + (long)b * a.gn_env * R, (unsigned)i, p, v);
 #pragma unroll
-    for (int q = 0; q < D; ++q) { gp[q] += p[q]; gv[q] += v[q] + a.dt * p[q]; }
+    for (int q = 0; q < D; ++q) { gp[q] += np_[q]; gv[q] += nv[q] + a.dt * np_[q]; }
   }
   store_rec<D>(a.Gout + (long)b * a.go_env * R, (unsigned)i, gp, gv);
 }
