@@ -7,10 +7,16 @@ One timed step = a full training iteration on every rank: on-device scenario sam
 rollout (kNN scan + fused controller, until every env is done or INNER_LOOPS), CBF losses,
 hand-written backward through the CBF and BPTT through the rollout, RCCL all-reduce of the
 flat gradient, fused Adam. agent-steps = sum over envs of N x valid rollout steps.
-Weak scaling: every rank trains --envs environments of --agents agents (random-init weights,
-synthetic scenarios from the on-device sampler).
+Weak scaling (default): every rank trains --envs environments of --agents agents. Strong scaling
+(--global_envs G, BASELINE config #3 as stated: G = 64 envs over all ranks): every rank trains
+G / world of them. Random-init weights, synthetic scenarios from the on-device sampler (keyed by
+seed, iteration and rank).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+Precision (--dtype): fp32 (default) is the reference precision (/root/reference is fp32 end to
+end): the fp32-accurate 3-term split-bf16 MFMA kernels. bf16 / fp16 are the faster 16-bit-input
+modes (fp16 with dynamic loss scaling).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--dtype fp32|bf16|fp16] [--global_envs G]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
 """
 from __future__ import annotations
@@ -24,10 +30,11 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-# the reference publishes no numbers and its train loop does not run at N=1024
-# (O((T*N)^2) scene). The only N=1024 reference measurement is its rollout-only
-# loop on CPU (autograd on): 93,009 agent-steps/s -- an upper bound of its train-loop rate.
-BASELINE_AGENT_STEPS_PER_S = 93009.0
+# the reference publishes no numbers ("published": {}) and its train loop does not run
+# at N=1024 (O((T*N)^2) scene): vs_baseline is null. The only N=1024 reference
+# measurement is its rollout-only loop on CPU (autograd on, 93,009 agent-steps/s), reported as a
+# non-comparable proxy (different workload, CPU).
+CPU_ROLLOUT_PROXY = 93009.0
 
 
 def main():
@@ -37,13 +44,16 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--agents", type=int, default=1024)
     ap.add_argument("--envs", type=int, default=64, help="environments per rank (weak scaling)")
+    ap.add_argument("--global_envs", type=int, default=0,
+                    help="strong scaling: environments over all ranks (BASELINE config #3: 64), sharded per rank")
     ap.add_argument("--inner_loops", type=int, default=50)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no_early_stop", action="store_true", help="fixed-T (=inner_loops) throughput")
     ap.add_argument("--dim", type=int, default=2, choices=[2, 3], help="3: BASELINE config #5 (3-D)")
     ap.add_argument("--num_obstacles", type=int, default=0, help="static point-set obstacles per env")
-    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp16"],
-                    help="16-bit MFMA input type (fp16: dynamic loss scaling; BASELINE config #5)")
+    ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16", "fp16"],
+                    help="kernel precision: fp32 (reference precision, split-bf16 MFMA), bf16, fp16 "
+                         "(dynamic loss scaling; BASELINE config #5)")
     ap.add_argument("--graph", action="store_true",
                     help="replay each iteration as captured HIP graphs (launch-bound small configs)")
     ap.add_argument("--phases", action="store_true",
@@ -61,7 +71,11 @@ def main():
     dev = torch.device("cuda", local_rank % max(torch.cuda.device_count(), 1))
     torch.cuda.set_device(dev)
     dp = DP(device=dev)
-    cfg = C.TrainConfig(num_agents=args.agents, num_envs=args.envs, inner_loops=args.inner_loops,
+    strong = args.global_envs > 0
+    if strong and args.global_envs % world:
+        raise SystemExit(f"--global_envs {args.global_envs} must be divisible by the world size {world}")
+    envs = args.global_envs // world if strong else args.envs
+    cfg = C.TrainConfig(num_agents=args.agents, num_envs=envs, inner_loops=args.inner_loops,
                         seed=args.seed, device="hip", early_stop=not args.no_early_stop,
                         display_steps=10 ** 9, save_steps=10 ** 9, dim=args.dim, num_obstacles=args.num_obstacles,
                         dtype=args.dtype, graph=args.graph)
@@ -92,7 +106,7 @@ def main():
         phases = {k: round(v, 3) for k, v in tot.items()}
     value = agent_steps / elapsed
     out = {
-        "metric": "agent-steps/sec (train loop) + safety-rate, 1024 agents",
+        "metric": f"agent-steps/sec (train loop) + safety-rate, {args.agents} agents",
         "value": value,
         "unit": "agent-steps/s",
         "n_gpus": world,
@@ -100,22 +114,25 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": 1000.0 * elapsed / args.steps,
         "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": value / BASELINE_AGENT_STEPS_PER_S,
+        "scaling": "strong" if strong else "weak",
+        "vs_baseline": None,
         "dtype": args.dtype,
         "data": "synthetic (on-device scenario sampler, random-init weights)",
         "config": {"model": f"MACBF-GNN controller+CBF ({args.dim}-D double integrator, top-K=12"
                             + (f", {args.num_obstacles} obstacles x 12 points" if args.num_obstacles else "") + ")",
-                   "agents": args.agents, "global_batch": args.envs * world, "envs_per_gpu": args.envs,
+                   "agents": args.agents, "global_batch": envs * world, "envs_per_gpu": envs,
                    "seq_len": args.inner_loops, "parallelism": f"dp{world}"},
         "safety_rate": safe_agents / agent_steps if agent_steps > 0 else None,
         "mean_T": t_sum / (args.steps * world),
         "early_stop": not args.no_early_stop,
         "skipped_steps": tr.skipped_steps,
         "graph": args.graph,
-        "baseline": {"value": BASELINE_AGENT_STEPS_PER_S,
-                     "source": "BASELINE.md: reference rollout-only loop @ N=1024, CPU x8 (upper bound of its "
-                               "train loop, which does not run at N=1024)"},
+        "precision": {"fp32": "fp32-accurate: 3-term split-bf16 MFMA (hi*hi + hi*lo + lo*hi), fp32 accumulate",
+                      "bf16": "bf16 MFMA inputs, fp32 accumulate", "fp16": "fp16 MFMA inputs, fp32 accumulate, "
+                      "dynamic loss scaling"}[args.dtype],
+        "cpu_rollout_proxy": {"value": CPU_ROLLOUT_PROXY, "comparable": False,
+                              "source": "BASELINE.md: reference rollout-only loop (no losses / backward) @ N=1024, "
+                                        "CPU x8; the reference publishes no numbers"},
     }
     if phases is not None:
         out["phases_ms"] = phases

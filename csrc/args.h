@@ -253,16 +253,22 @@ int mb_cell_sort(const mb::CellSortArgs* a, hipStream_t st);
 int mb_scenario(const mb::ScenArgs* a, hipStream_t st);
 int mb_ctrl_fwd(const mb::CtrlArgs* a, int num_cu, hipStream_t st);
 int mb_ctrl_fwd_f16(const mb::CtrlArgs* a, int num_cu, hipStream_t st);
+int mb_ctrl_fwd_x3(const mb::CtrlArgs* a, int num_cu, hipStream_t st);
 int mb_cbf_fwd(const mb::CbfFwdArgs* a, int num_blocks, hipStream_t st);
 int mb_cbf_fwd_f16(const mb::CbfFwdArgs* a, int num_blocks, hipStream_t st);
+int mb_cbf_fwd_x3(const mb::CbfFwdArgs* a, int num_blocks, hipStream_t st);
 int mb_cbf_hfwd(const mb::CbfFwdArgs* a, int num_blocks, hipStream_t st);
 int mb_cbf_hfwd_f16(const mb::CbfFwdArgs* a, int num_blocks, hipStream_t st);
+int mb_cbf_hfwd_x3(const mb::CbfFwdArgs* a, int num_blocks, hipStream_t st);
 int mb_cbf_bwd(const mb::CbfBwdArgs* a, int num_blocks, hipStream_t st);
 int mb_cbf_bwd_f16(const mb::CbfBwdArgs* a, int num_blocks, hipStream_t st);
+int mb_cbf_bwd_x3(const mb::CbfBwdArgs* a, int num_blocks, hipStream_t st);
 int mb_ctrl_node_bwd(const mb::CtrlNodeBwdArgs* a, int num_blocks, hipStream_t st);
 int mb_ctrl_node_bwd_f16(const mb::CtrlNodeBwdArgs* a, int num_blocks, hipStream_t st);
+int mb_ctrl_node_bwd_x3(const mb::CtrlNodeBwdArgs* a, int num_blocks, hipStream_t st);
 int mb_ctrl_edge_bwd(const mb::CtrlEdgeBwdArgs* a, int num_blocks, hipStream_t st);
 int mb_ctrl_edge_bwd_f16(const mb::CtrlEdgeBwdArgs* a, int num_blocks, hipStream_t st);
+int mb_ctrl_edge_bwd_x3(const mb::CtrlEdgeBwdArgs* a, int num_blocks, hipStream_t st);
 int mb_rev_csr(const mb::CsrArgs* a, hipStream_t st);
 int mb_cbf_match(const mb::CbfMatchArgs* a, hipStream_t st);
 int mb_cbf_dh(const mb::CbfDhArgs* a, int num_blocks, hipStream_t st);

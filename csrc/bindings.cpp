@@ -49,7 +49,7 @@ static int scenario(u64 S, long s_env, u64 G, u64 obs, int M, int dim, int B, in
 static int ctrl_fwd(u64 S, long s_env, u64 G, u64 idx, long i_env, int B, int N, int K, u64 wpack, int f_edge,
                     int f_node, u64 wvec, u64 A, long a_env, u64 Sn, long sn_env, u64 dist_sum, long d_env,
                     u64 act_sum, long ac_env, u64 noise, long n_env, float dt, float obs_r, float sqrt3,
-                    u64 pooled, long p_env, u64 argmax, long am_env, int dim, int num_cu, int f16, int apw,
+                    u64 pooled, long p_env, u64 argmax, long am_env, int dim, int num_cu, int prec, int apw,
                     u64 stream) {
   mb::CtrlArgs a{};
   a.dim = dim;
@@ -60,13 +60,13 @@ static int ctrl_fwd(u64 S, long s_env, u64 G, u64 idx, long i_env, int B, int N,
   a.dist_sum = P<float>(dist_sum); a.d_env = d_env; a.act_sum = P<float>(act_sum); a.ac_env = ac_env;
   a.noise = P<const float>(noise); a.n_env = n_env; a.dt = dt; a.obs_r = obs_r; a.sqrt3 = sqrt3;
   a.pooled = P<h16>(pooled); a.p_env = p_env; a.argmax = P<uint8_t>(argmax); a.am_env = am_env;
-  return (f16 ? mb_ctrl_fwd_f16 : mb_ctrl_fwd)(&a, num_cu, ST(stream));
+  return (prec == 2 ? mb_ctrl_fwd_x3 : prec == 1 ? mb_ctrl_fwd_f16 : mb_ctrl_fwd)(&a, num_cu, ST(stream));
 }
 
 static int cbf_fwd(u64 S, long s_env, long s_step, u64 idx, u64 dang, u64 valid, int B, int T, int N, int K,
                    int two, u64 wpack, int f_fwd, u64 wvec, u64 h_out, u64 hn_out, u64 dh_out, u64 counts,
                    u64 partial, py::tuple lc, float obs_r, float dist_thr, float dist_eps, int dim, int num_blocks,
-                   int f16, u64 stream) {
+                   int prec, u64 stream) {
   mb::CbfFwdArgs a{};
   a.dim = dim;
   a.S = P<const float4>(S); a.s_env = s_env; a.s_step = s_step; a.idx = P<const int>(idx);
@@ -79,12 +79,12 @@ static int cbf_fwd(u64 S, long s_env, long s_step, u64 idx, u64 dang, u64 valid,
   a.lc.w_safe = lc[3].cast<float>(); a.lc.w_dang_d = lc[4].cast<float>(); a.lc.w_safe_d = lc[5].cast<float>();
   a.lc.scale = lc[6].cast<float>();
   a.obs_r = obs_r; a.dist_thr = dist_thr; a.dist_eps = dist_eps;
-  return (f16 ? mb_cbf_fwd_f16 : mb_cbf_fwd)(&a, num_blocks, ST(stream));
+  return (prec == 2 ? mb_cbf_fwd_x3 : prec == 1 ? mb_cbf_fwd_f16 : mb_cbf_fwd)(&a, num_blocks, ST(stream));
 }
 
 static int cbf_hfwd(u64 S, long s_env, long s_step, u64 idx, u64 idx1, u64 src, u64 nev, int B, int T, int N, int K,
                     u64 wpack, int f_fwd, u64 wrm, u64 wvec, u64 h_out, u64 mask_out, float obs_r, float dist_thr,
-                    float dist_eps, int dim, int num_blocks, int f16, unsigned u_begin, unsigned u_end,
+                    float dist_eps, int dim, int num_blocks, int prec, unsigned u_begin, unsigned u_end,
                     u64 stream) {
   mb::CbfFwdArgs a{};
   a.dim = dim;
@@ -95,13 +95,13 @@ static int cbf_hfwd(u64 S, long s_env, long s_step, u64 idx, u64 idx1, u64 src, 
   a.wpack = P<const h16>(wpack); a.f_fwd = f_fwd; a.wrm = P<const h16>(wrm); a.wvec = P<const float>(wvec);
   a.h_out = P<float>(h_out); a.mask_out = P<uint8_t>(mask_out);
   a.obs_r = obs_r; a.dist_thr = dist_thr; a.dist_eps = dist_eps;
-  return (f16 ? mb_cbf_hfwd_f16 : mb_cbf_hfwd)(&a, num_blocks, ST(stream));
+  return (prec == 2 ? mb_cbf_hfwd_x3 : prec == 1 ? mb_cbf_hfwd_f16 : mb_cbf_hfwd)(&a, num_blocks, ST(stream));
 }
 
 static int cbf_bwd(u64 S, long s_env, long s_step, u64 idx, int B, int T, int N, int K, int passes, u64 dh,
                    u64 wpack, int f_bwd, u64 wrm, u64 wvec, u64 dE, u64 partial, float obs_r, float dist_thr,
                    float dist_eps, int fused, u64 dang, u64 valid, u64 counts, py::tuple lc, u64 idx1,
-                   int dim, int num_blocks, int f16, u64 src, u64 nev, u64 act, u64 nact, u64 stream) {
+                   int dim, int num_blocks, int prec, u64 src, u64 nev, u64 act, u64 nact, u64 stream) {
   mb::CbfBwdArgs a{};
   a.dim = dim;
   a.src = P<const int>(src); a.nev = P<const int>(nev); a.act = P<const int>(act); a.nact = P<const int>(nact);
@@ -116,7 +116,7 @@ static int cbf_bwd(u64 S, long s_env, long s_step, u64 idx, int B, int T, int N,
   a.wpack = P<const h16>(wpack); a.f_bwd = f_bwd; a.wrm = P<const h16>(wrm); a.wvec = P<const float>(wvec);
   a.dE = P<float4>(dE); a.partial = P<float>(partial);
   a.obs_r = obs_r; a.dist_thr = dist_thr; a.dist_eps = dist_eps;
-  return (f16 ? mb_cbf_bwd_f16 : mb_cbf_bwd)(&a, num_blocks, ST(stream));
+  return (prec == 2 ? mb_cbf_bwd_x3 : prec == 1 ? mb_cbf_bwd_f16 : mb_cbf_bwd)(&a, num_blocks, ST(stream));
 }
 
 static int rev_csr(u64 idx, int G, int N, int K, u64 ptr, u64 edges, int Nn, u64 stream) {
@@ -218,7 +218,7 @@ static int adam(u64 param, u64 grad, u64 m, u64 v, int lo, int hi, float b1, flo
 static int ctrl_node_bwd(u64 pooled, long p_env, u64 S, long s_env, u64 G, u64 A, long a_env, u64 Gn, long gn_env,
                          u64 valid, long v_env, int B, int N, u64 wrm, int o1, int o2, int o3, int o4, u64 wvec,
                          float act_coef, u64 act_scale, float dt, float sqrt3, u64 dP, long dp_env, u64 ego, u64 partial,
-                         int dim, int num_blocks, int f16, u64 stream) {
+                         int dim, int num_blocks, int prec, u64 stream) {
   mb::CtrlNodeBwdArgs a{};
   a.dim = dim;
   a.pooled = P<const h16>(pooled); a.p_env = p_env; a.S = P<const float4>(S); a.s_env = s_env;
@@ -227,12 +227,12 @@ static int ctrl_node_bwd(u64 pooled, long p_env, u64 S, long s_env, u64 G, u64 A
   a.o_w1 = o1; a.o_w2 = o2; a.o_w3 = o3; a.o_w4 = o4; a.wvec = P<const float>(wvec);
   a.act_coef = act_coef; a.act_scale = P<const float>(act_scale); a.dt = dt; a.sqrt3 = sqrt3; a.dP = P<h16>(dP); a.dp_env = dp_env;
   a.ego = P<float4>(ego); a.partial = P<float>(partial);
-  return (f16 ? mb_ctrl_node_bwd_f16 : mb_ctrl_node_bwd)(&a, num_blocks, ST(stream));
+  return (prec == 2 ? mb_ctrl_node_bwd_x3 : prec == 1 ? mb_ctrl_node_bwd_f16 : mb_ctrl_node_bwd)(&a, num_blocks, ST(stream));
 }
 
 static int ctrl_edge_bwd(u64 S, long s_env, u64 idx, long i_env, u64 argmax, long am_env, u64 dP, long dp_env,
                          int B, int N, int K, u64 wpack, int f_ew1f, int f_ew2tn, u64 dEc, long de_env, u64 partial,
-                         int dim, int num_blocks, int f16, int qsplit, u64 stream) {
+                         int dim, int num_blocks, int prec, int qsplit, u64 stream) {
   mb::CtrlEdgeBwdArgs a{};
   a.dim = dim;
   a.qsplit = qsplit;
@@ -240,7 +240,7 @@ static int ctrl_edge_bwd(u64 S, long s_env, u64 idx, long i_env, u64 argmax, lon
   a.argmax = P<const uint8_t>(argmax); a.am_env = am_env; a.dP = P<const h16>(dP); a.dp_env = dp_env;
   a.B = B; a.N = N; a.K = K; a.wpack = P<const h16>(wpack); a.f_ew1f = f_ew1f; a.f_ew2tn = f_ew2tn;
   a.dEc = P<float4>(dEc); a.de_env = de_env; a.partial = P<float>(partial);
-  return (f16 ? mb_ctrl_edge_bwd_f16 : mb_ctrl_edge_bwd)(&a, num_blocks, ST(stream));
+  return (prec == 2 ? mb_ctrl_edge_bwd_x3 : prec == 1 ? mb_ctrl_edge_bwd_f16 : mb_ctrl_edge_bwd)(&a, num_blocks, ST(stream));
 }
 
 static int probe_mfma(u64 a, u64 b, u64 d, u64 stream) {

@@ -20,7 +20,7 @@ PKG = os.path.join(ROOT, "macbf_gnn_amd")
 BUILD = os.path.join(ROOT, "build", "csrc")
 ARCH = os.environ.get("MACBF_ARCH", "gfx950")
 KERNELS = ["scan", "scenario", "ctrl", "cbf", "dedup", "graph", "optim", "probe"]
-HALF_KERNELS = {"ctrl", "cbf"}       # compiled for both 16-bit MFMA element types
+HALF_KERNELS = {"ctrl", "cbf"}       # compiled per MFMA operand precision (csrc/prec.h)
 
 
 HOST_SRCS = ["host/scenario_host.cpp", "host/bindings_host.cpp"]   # CPU runtime (plain C++)
@@ -89,11 +89,12 @@ def write_ninja(debug=False):
         o = os.path.join(BUILD, k + ".o")
         lines.append(f"build {o}: kcc {src}")
         objs.append(o)
-        if k in HALF_KERNELS:   # second instantiation with fp16 MFMA inputs (csrc/prec.h)
-            o = os.path.join(BUILD, k + "_f16.o")
-            lines.append(f"build {o}: kcc {src}")
-            lines.append("  kdefs = -DMB_FP16=1")
-            objs.append(o)
+        if k in HALF_KERNELS:   # fp16 MFMA inputs and the fp32-accurate 3-term split (csrc/prec.h)
+            for suffix, d in (("_f16", "-DMB_FP16=1"), ("_x3", "-DMB_X3=1")):
+                o = os.path.join(BUILD, k + suffix + ".o")
+                lines.append(f"build {o}: kcc {src}")
+                lines.append(f"  kdefs = {d}")
+                objs.append(o)
     for b in ("bindings", "runtime"):      # pybind11 layer + native rollout driver (host C++)
         bo = os.path.join(BUILD, b + ".o")
         lines.append(f"build {bo}: bcc {os.path.join(HERE, b + '.cpp')}")

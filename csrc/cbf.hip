@@ -19,7 +19,11 @@
 #include "state.h"
 
 #ifndef CBF_NW
+#if MB_X3
+#define CBF_NW 4   // x3: one wave per SIMD (split activations double the register footprint)
+#else
 #define CBF_NW 8   // waves per CBF-backward workgroup (4: one per SIMD, 8: two per SIMD)
+#endif
 #endif
 
 namespace mb {
@@ -77,7 +81,7 @@ DEV float cbf_mlp(const h16x8& F, const h16* wl, const float* vl, int lane, CbfA
   const float b4 = vl[256];
 #pragma unroll
   for (int mt = 0; mt < 2; ++mt) {
-    o.H1[mt] = mfma(frag_ld(wl, mt, lane), F, zero16());
+    o.H1[mt] = mma_bx(frag_fr(wl, mt, lane), F, zero16());
     relu_(o.H1[mt]);
   }
 #pragma unroll
@@ -85,7 +89,7 @@ DEV float cbf_mlp(const h16x8& F, const h16* wl, const float* vl, int lane, CbfA
     f32x16 c = bias_rows(b2, 32 * mt, h);
     static_for<4>([&](auto kk_) {
       constexpr int kk = decltype(kk_)::value;
-      c = mfma(frag_ld(wl, 2 + mt * 4 + kk, lane), acc_frag<kk & 1>(o.H1[kk >> 1]), c);
+      c = mma(frag_fr(wl, 2 + mt * 4 + kk, lane), acc_fr<kk & 1>(o.H1[kk >> 1]), c);
     });
     relu_(c);
     o.H2[mt] = c;
@@ -95,7 +99,7 @@ DEV float cbf_mlp(const h16x8& F, const h16* wl, const float* vl, int lane, CbfA
     f32x16 c = bias_rows(b3, 32 * mt, h);
     static_for<8>([&](auto kk_) {
       constexpr int kk = decltype(kk_)::value;
-      c = mfma(frag_ld(wl, 18 + mt * 8 + kk, lane), acc_frag<kk & 1>(o.H2[kk >> 1]), c);
+      c = mma(frag_fr(wl, 18 + mt * 8 + kk, lane), acc_fr<kk & 1>(o.H2[kk >> 1]), c);
     });
     o.H3[mt] = c;   // pre-activation kept (relu' needed in backward)
   }
@@ -153,9 +157,9 @@ template <int WAVES, int D>
 __global__ __launch_bounds__(WAVES * 64) void cbf_fwd_kernel(CbfFwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   h16* wl = reinterpret_cast<h16*>(smem);
-  float* vl = reinterpret_cast<float*>(smem + CBF_FWD_FRAGS * FRAG_BYTES);
+  float* vl = reinterpret_cast<float*>(smem + CBF_FWD_FRAGS * FRAG_SZ);
   __shared__ float red[10][WAVES];
-  block_copy16(wl, a.wpack + (size_t)a.f_fwd * 512, CBF_FWD_FRAGS * FRAG_BYTES);
+  block_copy16(wl, a.wpack + (size_t)a.f_fwd * FRAG_ELEMS, CBF_FWD_FRAGS * FRAG_SZ);
   block_copy16(vl, a.wvec, CBF_VEC * 4);
   __syncthreads();
   const int wave = threadIdx.x / WAVE, lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
@@ -246,7 +250,7 @@ extern "C" int MB_SYM(cbf_fwd)(const mb::CbfFwdArgs* a, int num_blocks, hipStrea
   using namespace mb;
   using namespace mb::MB_PREC;
   if (a->K > 16 || a->K < 1) return -1;
-  const size_t lds = (size_t)CBF_FWD_FRAGS * FRAG_BYTES + CBF_VEC * 4;
+  const size_t lds = (size_t)CBF_FWD_FRAGS * FRAG_SZ + CBF_VEC * 4;
   if (a->dim == 3) {
     (void)hipFuncSetAttribute((const void*)cbf_fwd_kernel<CBF_FWD_WAVES, 3>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL((cbf_fwd_kernel<CBF_FWD_WAVES, 3>), dim3(num_blocks), dim3(CBF_FWD_WAVES * 64), lds, st, *a);
@@ -285,22 +289,32 @@ namespace MB_PREC {
 constexpr int SA128 = 148, SA64 = 68, SA32 = 40;
 constexpr int WS2 = 68, WS3 = 148;                  // row-major W2 [128][WS2], W3 [64][WS3] images
 constexpr int RM_W2 = 128 * WS2, RM_W3 = 64 * WS3;  // row-major image sizes (elements)
+constexpr int RM_LO = RM_W2 + RM_W3;                // lo plane offset of the images (x3)
+constexpr int RMP = (X3 ? 2 : 1) * RM_LO;           // elements of the W2|W3 (+ lo) images
 // per-WG partial slab layout (floats)
 constexpr int P_W3 = 0, P_B3 = 8192, P_W2 = 8256, P_B2 = 16448, P_W1 = 16576, P_W4 = 18624, P_B4 = 18688;
 constexpr int P_LOSS = 18692;                 // 10 loss partial sums (fused mode)
 constexpr int CBF_PARTIAL = 18704;
-constexpr size_t CBF_BWD_W_BYTES = (size_t)(RM_W2 + RM_W3) * 2 + 6 * FRAG_BYTES;
+constexpr size_t CBF_BWD_W_BYTES = (size_t)RMP * 2 + 6 * FRAG_SZ;
 
 // Stage regions. NW = 4 waves (one per SIMD): two regions used alternately (stage k of the
 // running sequence A,B,C,A,B,C,... writes region k&1): a region is rewritten only after every
 // wave has passed the NEXT stage's barrier, i.e. finished reading it -> one barrier per stage.
 // NW = 8 waves (two per SIMD, chunk of 256): one region (LDS), two barriers per stage.
 // Stage A/B: (128 + 64)-wide images; stage C+D: dH1 | [F, dh, 0] | relu(H3) = 64+32+64 wide.
+// x3: the images carry a lo plane, so a region holds the rows of TW = 2 waves: every stage runs
+// in NT = NW / TW turns (the waves of a turn store, everybody contracts their rows), one region,
+// two barriers per turn.
 template <int NW> struct CbfCfg {
   static constexpr int CH = NW * 32;                          // evaluations per chunk
   static constexpr int KS = CH / 16;                          // edge steps per stage contraction
-  static constexpr int NREG = NW == 4 ? 2 : 1;
-  static constexpr int REGION = (SA64 + SA128) * CH;          // elements per region
+  static constexpr int TW = X3 ? 2 : NW;                      // waves whose rows a region holds
+  static constexpr int NT = NW / TW;                          // turns per stage
+  static constexpr int RT = TW * 32;                          // region rows
+  static constexpr int KST = RT / 16;                         // edge steps per turn
+  static constexpr int NREG = (NW == 4 && NT == 1) ? 2 : 1;
+  static constexpr int PLANE = (SA64 + SA128) * RT;           // elements per region plane
+  static constexpr int REGION = (X3 ? 2 : 1) * PLANE;         // elements per region
   static constexpr size_t LDS = CBF_BWD_W_BYTES + CBF_VEC * 4 + (size_t)NREG * REGION * 2;
 };
 
@@ -367,13 +381,13 @@ DEV void cbf_load(const CbfBwdArgs& a, long chunk, int wave, int r, long E, long
 #ifdef CBF_X_NOSTSTORE
 #define XSTORE(...) ((void)0)
 #else
-#define XSTORE store_tile
+#define XSTORE store_pk
 #endif
 #ifdef CBF_X_NOSTMMA
 template <int ES> DEV float xmma_skip(...) { return 0.f; }
 #define XMMA xmma_skip
 #else
-#define XMMA stage_mma
+#define XMMA stage_mma_fr
 #endif
 
 // h over a deduplicated evaluation list (dedup.hip): evaluation u < E is main slot u on s_t,
@@ -389,10 +403,10 @@ __global__ __launch_bounds__(NW * 64) void cbf_hfwd_kernel(CbfFwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   h16* W2 = reinterpret_cast<h16*>(smem);
   h16* W3 = W2 + RM_W2;
-  h16* wf = W3 + RM_W3;                       // w1f (2 frags)
-  float* vl = reinterpret_cast<float*>(smem + (size_t)(RM_W2 + RM_W3) * 2 + 2 * FRAG_BYTES);
-  block_copy16(W2, a.wrm, (RM_W2 + RM_W3) * 2);
-  block_copy16(wf, a.wpack + (size_t)a.f_fwd * 512, 2 * FRAG_BYTES);
+  h16* wf = W2 + RMP;                         // w1f (2 frags)
+  float* vl = reinterpret_cast<float*>(smem + (size_t)RMP * 2 + 2 * FRAG_SZ);
+  block_copy16(W2, a.wrm, RMP * 2);
+  block_copy16(wf, a.wpack + (size_t)a.f_fwd * FRAG_ELEMS, 2 * FRAG_SZ);
   block_copy16(vl, a.wvec, CBF_VEC * 4);
   __syncthreads();
   const int wave = threadIdx.x / WAVE, lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
@@ -423,17 +437,17 @@ __global__ __launch_bounds__(NW * 64) void cbf_hfwd_kernel(CbfFwdArgs a) {
     const float* b2 = vlc;
     const float* b3 = vlc + 128;
     const float* w4 = vlc + 192;
-    h16x16 H1b[2], H2b[4];
+    Pk H1b[2], H2b[4];
 #pragma unroll
-    for (int mt = 0; mt < 2; ++mt) H1b[mt] = to_h16x16_relu(mfma(frag_ld(wt, mt, lane), F, zero16()));
+    for (int mt = 0; mt < 2; ++mt) H1b[mt] = to_pk_relu(mma_bx(frag_fr(wt, mt, lane), F, zero16()));
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt) {
       f32x16 t2 = bias_rows4(b2, 32 * mt, h);
       static_for<4>([&](auto kk_) {
         constexpr int kk = decltype(kk_)::value;
-        t2 = mfma(wrm_acc(W2c, WS2, 32 * mt, kk, lane), bacc_frag<kk & 1>(H1b[kk >> 1]), t2);
+        t2 = mma(wrm_acc_fr(W2c, WS2, 32 * mt, kk, lane, RM_LO), pk_fr<kk & 1>(H1b[kk >> 1]), t2);
       });
-      H2b[mt] = to_h16x16_relu(t2);
+      H2b[mt] = to_pk_relu(t2);
     }
     f32x2 hs2 = {0.f, 0.f};
 #pragma unroll
@@ -441,7 +455,7 @@ __global__ __launch_bounds__(NW * 64) void cbf_hfwd_kernel(CbfFwdArgs a) {
       f32x16 t3 = bias_rows4(b3, 32 * mt, h);
       static_for<8>([&](auto kk_) {
         constexpr int kk = decltype(kk_)::value;
-        t3 = mfma(wrm_acc(W3c, WS3, 32 * mt, kk, lane), bacc_frag<kk & 1>(H2b[kk >> 1]), t3);
+        t3 = mma(wrm_acc_fr(W3c, WS3, 32 * mt, kk, lane, RM_LO), pk_fr<kk & 1>(H2b[kk >> 1]), t3);
       });
       relu_(t3);
 #pragma unroll
@@ -462,26 +476,27 @@ __global__ __launch_bounds__(NW * 64) void cbf_hfwd_kernel(CbfFwdArgs a) {
 }
 
 constexpr int HFWD_WAVES = 8;
-constexpr size_t HFWD_LDS = (size_t)(RM_W2 + RM_W3) * 2 + 2 * FRAG_BYTES + CBF_VEC * 4;
+constexpr size_t HFWD_LDS = (size_t)RMP * 2 + 2 * FRAG_SZ + CBF_VEC * 4;
 
 template <bool FUSED, int NW, int D>
 __global__ __launch_bounds__(NW * 64, 1) void cbf_bwd_kernel(CbfBwdArgs a) {
   using Cfg = CbfCfg<NW>;
-  constexpr int CH = Cfg::CH, KS = Cfg::KS;
+  constexpr int CH = Cfg::CH, KS = Cfg::KS, KST = Cfg::KST, RT = Cfg::RT, TW = Cfg::TW, NT = Cfg::NT;
+  constexpr int PL = Cfg::PLANE;               // lo plane offset inside a region (x3)
   constexpr int TA = 8 / NW;                   // owned dW3 tiles (and dW2 tiles) per wave
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   h16* W2 = reinterpret_cast<h16*>(smem);
   h16* W3 = W2 + RM_W2;
-  h16* wf = W3 + RM_W3;                       // w1f (2 frags) | w1ft (4 frags)
+  h16* wf = W2 + RMP;                         // w1f (2 frags) | w1ft (4 frags)
   float* vl = reinterpret_cast<float*>(smem + CBF_BWD_W_BYTES);
   h16* stg = reinterpret_cast<h16*>(smem + CBF_BWD_W_BYTES + CBF_VEC * 4);
   __shared__ float hx[CH];                     // fused: h / h' exchange
   __shared__ float lacc[8][FUSED ? CH / 2 : 1];  // fused: per-lane loss partial sums (pass-0 lanes)
   __shared__ float lred[NW][10];
   __shared__ float red4[NW];
-  block_copy16(W2, a.wrm, (RM_W2 + RM_W3) * 2);
-  block_copy16(wf, a.wpack + (size_t)a.f_bwd * 512, 2 * FRAG_BYTES);
-  block_copy16(wf + 2 * 512, a.wpack + (size_t)(a.f_bwd + 66) * 512, 4 * FRAG_BYTES);
+  block_copy16(W2, a.wrm, RMP * 2);
+  block_copy16(wf, a.wpack + (size_t)a.f_bwd * FRAG_ELEMS, 2 * FRAG_SZ);
+  block_copy16(wf + 2 * FRAG_ELEMS, a.wpack + (size_t)(a.f_bwd + 66) * FRAG_ELEMS, 4 * FRAG_SZ);
   block_copy16(vl, a.wvec, CBF_VEC * 4);
   if constexpr (FUSED)
     for (int q = threadIdx.x; q < 8 * CH / 2; q += blockDim.x) (&lacc[0][0])[q] = 0.f;
@@ -491,6 +506,8 @@ __global__ __launch_bounds__(NW * 64, 1) void cbf_bwd_kernel(CbfBwdArgs a) {
   const long EV = (!FUSED && a.nact) ? (long)*a.nact : (!FUSED && a.nev) ? (long)*a.nev : E * a.passes;
   const long nchunks = FUSED ? (E + CH / 2 - 1) / (CH / 2) : (EV + CH - 1) / CH;
   const int erow = wave * 32 + r;
+  const int trow = NT == 1 ? erow : (wave % TW) * 32 + r;   // this wave's rows inside a turn's region
+  const int myturn = wave / TW;
   const int pass_w = wave / (NW / 2);          // fused: this wave's pass
   float nd = 1.f, ns = 1.f;
   if constexpr (FUSED) { nd = 1e-5f + a.counts[0]; ns = 1e-5f + a.counts[1]; }
@@ -498,7 +515,8 @@ __global__ __launch_bounds__(NW * 64, 1) void cbf_bwd_kernel(CbfBwdArgs a) {
   float bA[TA], bB[TA], db4 = 0.f;
 #pragma unroll
   for (int u = 0; u < TA; ++u) { accA[u] = accB[u] = zero16(); bA[u] = bB[u] = 0.f; }
-  // bias-sum edge steps: 4 waves read each dW3 row block, 2 waves each dW2 row block
+  // bias-sum edge steps of the whole chunk: 4 waves read each dW3 row block, 2 waves each dW2
+  // row block (split per turn by turn_range)
   const int bsA = (KS / 4) * (wave % 4), bsB = (KS / 2) * (wave % 2);
   int par = 0;                                 // stage region parity (NREG == 2)
 
@@ -522,28 +540,28 @@ __global__ __launch_bounds__(NW * 64, 1) void cbf_bwd_kernel(CbfBwdArgs a) {
     const float* b3 = vlc + 128;
     const float* w4 = vlc + 192;
     // ---- forward recompute
-    h16x16 H1b[2], H2b[4];
+    Pk H1b[2], H2b[4];
     f32x16 H3p[2];
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt) {
-      const f32x16 t1 = mfma(frag_ld(wt, mt, lane), F, zero16());
-      H1b[mt] = to_h16x16_relu(t1);
+      const f32x16 t1 = mma_bx(frag_fr(wt, mt, lane), F, zero16());
+      H1b[mt] = to_pk_relu(t1);
     }
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt) {
       f32x16 t2 = bias_rows4(b2, 32 * mt, h);
       static_for<4>([&](auto kk_) {
         constexpr int kk = decltype(kk_)::value;
-        t2 = mfma(wrm_acc(W2c, WS2, 32 * mt, kk, lane), bacc_frag<kk & 1>(H1b[kk >> 1]), t2);
+        t2 = mma(wrm_acc_fr(W2c, WS2, 32 * mt, kk, lane, RM_LO), pk_fr<kk & 1>(H1b[kk >> 1]), t2);
       });
-      H2b[mt] = to_h16x16_relu(t2);
+      H2b[mt] = to_pk_relu(t2);
     }
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt) {
       f32x16 t3 = bias_rows4(b3, 32 * mt, h);
       static_for<8>([&](auto kk_) {
         constexpr int kk = decltype(kk_)::value;
-        t3 = mfma(wrm_acc(W3c, WS3, 32 * mt, kk, lane), bacc_frag<kk & 1>(H2b[kk >> 1]), t3);
+        t3 = mma(wrm_acc_fr(W3c, WS3, 32 * mt, kk, lane, RM_LO), pk_fr<kk & 1>(H2b[kk >> 1]), t3);
       });
       relu_(t3);                                   // relu(H3) in fp32 (the head is fp32)
       H3p[mt] = t3;
@@ -607,7 +625,7 @@ __global__ __launch_bounds__(NW * 64, 1) void cbf_bwd_kernel(CbfBwdArgs a) {
     if (h == 0) db4 += dhv;
     // ---- head backward
     // dH3pre = w4 * dh . relu'(H3): packed products, then the 16-bit relu' mask of relu(H3)
-    h16x16 d3b[2], H3b[2];
+    Pk d3b[2], H3b[2];
     const f32x2 dh2 = {dhv, dhv};
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt) {
@@ -618,84 +636,96 @@ __global__ __launch_bounds__(NW * 64, 1) void cbf_bwd_kernel(CbfBwdArgs a) {
         const f32x2 lo = f32x2{w.x, w.y} * dh2, hi = f32x2{w.z, w.w} * dh2;
         d3[4 * g] = lo.x; d3[4 * g + 1] = lo.y; d3[4 * g + 2] = hi.x; d3[4 * g + 3] = hi.y;
       }
-      H3b[mt] = to_h16x16(H3p[mt]);
-      d3b[mt] = to_h16x16(d3);
-      mask_by_nonzero(d3b[mt], H3b[mt]);
+      H3b[mt] = to_pk(H3p[mt]);
+      d3b[mt] = to_pk(d3);
+      mask_pk(d3b[mt], H3b[mt]);
     }
     // ---- stage A: dW3 (64x128) += dH3pre . H2^T ; db3   (tiles t = wave + NW u -> (t/4, t%4))
 #ifndef CBF_X_NOSTAGE
-    {
+#pragma unroll
+    for (int turn = 0; turn < NT; ++turn) {
       h16* imA = stg + par * Cfg::REGION;
-      h16* imB = imA + CH * SA64;
+      h16* imB = imA + RT * SA64;
+      if (NT == 1 || myturn == turn) {
 #pragma unroll
-      for (int mt = 0; mt < 2; ++mt) XSTORE(imA, SA64, erow, 32 * mt, d3b[mt], h);
+        for (int mt = 0; mt < 2; ++mt) XSTORE(imA, SA64, trow, 32 * mt, d3b[mt], h, PL);
 #pragma unroll
-      for (int mt = 0; mt < 4; ++mt) XSTORE(imB, SA128, erow, 32 * mt, H2b[mt], h);
+        for (int mt = 0; mt < 4; ++mt) XSTORE(imB, SA128, trow, 32 * mt, H2b[mt], h, PL);
+      }
       __syncthreads();
+      int blo, bhi;
+#ifdef CBF_X_NOBIAS
+      blo = bhi = 0;
+#else
+      if constexpr (NT == 1) { blo = bsA; bhi = bsA + KS / 4; }
+      else turn_range(bsA, bsA + KS / 4, turn, KST, blo, bhi);
+#endif
 #pragma unroll
       for (int u = 0; u < TA; ++u) {
         const int t = wave + NW * u;
-#ifdef CBF_X_NOBIAS
-        bA[u] += XMMA<KS>(imA, SA64, imB, SA128, t / 4, t % 4, lane, accA[u], 0, 0);
-#else
-        bA[u] += XMMA<KS>(imA, SA64, imB, SA128, t / 4, t % 4, lane, accA[u], bsA, bsA + KS / 4);
-#endif
+        bA[u] += XMMA<KST>(imA, SA64, PL, imB, SA128, PL, t / 4, t % 4, lane, accA[u], blo, bhi);
       }
       if constexpr (Cfg::NREG == 2) par ^= 1; else __syncthreads();
     }
 #endif
     // ---- dH2pre = (W3^T dH3pre) . relu'(H2)
-    h16x16 d2b[4];
+    Pk d2b[4];
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt) {
       f32x16 t = zero16();
       static_for<4>([&](auto kk_) {
         constexpr int kk = decltype(kk_)::value;
-        t = mfma(wrmT_acc(W3c, WS3, 32 * mt, kk, lane), bacc_frag<kk & 1>(d3b[kk >> 1]), t);
+        t = mma(wrmT_acc_fr(W3c, WS3, 32 * mt, kk, lane, RM_LO), pk_fr<kk & 1>(d3b[kk >> 1]), t);
       });
-      d2b[mt] = to_h16x16(t);
-      mask_by_nonzero(d2b[mt], H2b[mt]);
+      d2b[mt] = to_pk(t);
+      mask_pk(d2b[mt], H2b[mt]);
     }
     // ---- stage B: dW2 (128x64) += dH2pre . H1^T ; db2   (tiles t = wave + NW u -> (t/2, t%2))
 #ifndef CBF_X_NOSTAGE
-    {
+#pragma unroll
+    for (int turn = 0; turn < NT; ++turn) {
       h16* imA = stg + par * Cfg::REGION;
-      h16* imB = imA + CH * SA128;
+      h16* imB = imA + RT * SA128;
+      if (NT == 1 || myturn == turn) {
 #pragma unroll
-      for (int mt = 0; mt < 4; ++mt) XSTORE(imA, SA128, erow, 32 * mt, d2b[mt], h);
+        for (int mt = 0; mt < 4; ++mt) XSTORE(imA, SA128, trow, 32 * mt, d2b[mt], h, PL);
 #pragma unroll
-      for (int mt = 0; mt < 2; ++mt) XSTORE(imB, SA64, erow, 32 * mt, H1b[mt], h);
+        for (int mt = 0; mt < 2; ++mt) XSTORE(imB, SA64, trow, 32 * mt, H1b[mt], h, PL);
+      }
       __syncthreads();
+      int blo, bhi;
+#ifdef CBF_X_NOBIAS
+      blo = bhi = 0;
+#else
+      if constexpr (NT == 1) { blo = bsB; bhi = bsB + KS / 2; }
+      else turn_range(bsB, bsB + KS / 2, turn, KST, blo, bhi);
+#endif
 #pragma unroll
       for (int u = 0; u < TA; ++u) {
         const int t = wave + NW * u;
-#ifdef CBF_X_NOBIAS
-        bB[u] += XMMA<KS>(imA, SA128, imB, SA64, t / 2, t % 2, lane, accB[u], 0, 0);
-#else
-        bB[u] += XMMA<KS>(imA, SA128, imB, SA64, t / 2, t % 2, lane, accB[u], bsB, bsB + KS / 2);
-#endif
+        bB[u] += XMMA<KST>(imA, SA128, PL, imB, SA64, PL, t / 2, t % 2, lane, accB[u], blo, bhi);
       }
       if constexpr (Cfg::NREG == 2) par ^= 1; else __syncthreads();
     }
 #endif
     // ---- dH1pre = (W2^T dH2pre) . relu'(H1)
-    h16x16 d1b[2];
+    Pk d1b[2];
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt) {
       f32x16 t = zero16();
       static_for<8>([&](auto kk_) {
         constexpr int kk = decltype(kk_)::value;
-        t = mfma(wrmT_acc(W2c, WS2, 32 * mt, kk, lane), bacc_frag<kk & 1>(d2b[kk >> 1]), t);
+        t = mma(wrmT_acc_fr(W2c, WS2, 32 * mt, kk, lane, RM_LO), pk_fr<kk & 1>(d2b[kk >> 1]), t);
       });
-      d1b[mt] = to_h16x16(t);
-      mask_by_nonzero(d1b[mt], H1b[mt]);
+      d1b[mt] = to_pk(t);
+      mask_pk(d1b[mt], H1b[mt]);
     }
     // ---- dF = W1^T dH1pre (rows: dx dy dvx dvy eye dist) -> dL/d(s_i - s_j)
     {
       f32x16 t = zero16();
       static_for<4>([&](auto kk_) {
         constexpr int kk = decltype(kk_)::value;
-        t = mfma(frag_ld(wt, 2 + kk, lane), bacc_frag<kk & 1>(d1b[kk >> 1]), t);
+        t = mma(frag_fr(wt, 2 + kk, lane), pk_fr<kk & 1>(d1b[kk >> 1]), t);
       });
       // rows = feature columns: s_i - s_j (0..2D-1), eye (2D), dist (2D+1); lane h = 0 holds rows
       // 0..3 in regs 0..3, lane h = 1 rows 4..7
@@ -716,25 +746,34 @@ __global__ __launch_bounds__(NW * 64, 1) void cbf_bwd_kernel(CbfBwdArgs a) {
     }
     // ---- stage C+D: dW1f (64x32) += dH1pre . [F|dh|0]^T (waves 0,1; cols >= 16 unused);
     //      dW4pad (32x64) += [dh;0..] . relu(H3)^T, A = image cols 16..47 -> row 0 = dw4 (waves 2,3;
-    //      rows >= 1 read padding / the next row and are discarded: MFMA rows are independent)
+    //      rows >= 1 read padding / the next row and are discarded: MFMA rows are independent).
+    //      x3: F is exact in h16 (its lo plane is zero); dh's residual goes to the lo plane.
 #ifndef CBF_X_NOSTAGE
-    {
+#pragma unroll
+    for (int turn = 0; turn < NT; ++turn) {
       h16* imC = stg + par * Cfg::REGION;
-      h16* imF = imC + CH * SA64;
-      h16* imH = imF + CH * SA32;
+      h16* imF = imC + RT * SA64;
+      h16* imH = imF + RT * SA32;
+      if (NT == 1 || myturn == turn) {
 #pragma unroll
-      for (int mt = 0; mt < 2; ++mt) XSTORE(imC, SA64, erow, 32 * mt, d1b[mt], h);
+        for (int mt = 0; mt < 2; ++mt) XSTORE(imC, SA64, trow, 32 * mt, d1b[mt], h, PL);
 #pragma unroll
-      for (int mt = 0; mt < 2; ++mt) XSTORE(imH, SA64, erow, 32 * mt, H3b[mt], h);
-      h16x8 dv;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) dv[j] = (h16)0.f;
-      if (h == 0) dv[0] = (h16)dhv;
-      *reinterpret_cast<h16x8*>(imF + erow * SA32 + 8 * h) = F;
-      *reinterpret_cast<h16x8*>(imF + erow * SA32 + 16 + 8 * h) = dv;
+        for (int mt = 0; mt < 2; ++mt) XSTORE(imH, SA64, trow, 32 * mt, H3b[mt], h, PL);
+        h16x8 dv = zero_h8();
+        const h16 dvh = (h16)dhv;
+        if (h == 0) dv[0] = dvh;
+        *reinterpret_cast<h16x8*>(imF + trow * SA32 + 8 * h) = F;
+        *reinterpret_cast<h16x8*>(imF + trow * SA32 + 16 + 8 * h) = dv;
+        if constexpr (X3) {
+          h16x8 dvl = zero_h8();
+          if (h == 0) dvl[0] = (h16)(dhv - (float)dvh);
+          *reinterpret_cast<h16x8*>(imF + PL + trow * SA32 + 8 * h) = zero_h8();
+          *reinterpret_cast<h16x8*>(imF + PL + trow * SA32 + 16 + 8 * h) = dvl;
+        }
+      }
       __syncthreads();
-      if (wave < 2) XMMA<KS>(imC, SA64, imF, SA32, wave, 0, lane, accC);
-      else if (wave < 4) XMMA<KS>(imF + 16, SA32, imH, SA64, 0, wave - 2, lane, accC);
+      if (wave < 2) XMMA<KST>(imC, SA64, PL, imF, SA32, PL, wave, 0, lane, accC);
+      else if (wave < 4) XMMA<KST>(imF + 16, SA32, PL, imH, SA64, PL, 0, wave - 2, lane, accC);
       if constexpr (Cfg::NREG == 2) par ^= 1; else __syncthreads();
     }
 #endif

@@ -449,3 +449,218 @@ DEV h16x8 wrmT_nat(const h16* W, int stride, int m0, int kk, int lane) {
 }
 
 }  // namespace mb
+
+// =======================================================================================
+// Operand-precision layer (csrc/prec.h). Kernels are written once against these types:
+//   Fr  an MFMA operand fragment (8 x h16 per lane) with its residual plane `l` (x3 only),
+//   Pk  a packed 32x32 activation tile (16 x h16 per lane, see to_h16x16) with its residual,
+//   mma a product: one MFMA (bf16 / fp16) or hi*hi + hi*lo + lo*hi (x3, small terms first).
+// In the 1-pass builds the `l` members are never written or read (the compiler drops them).
+// Weight fragments are FRAG_ELEMS apart in the packed buffers: x3 stores each 1 KiB hi fragment
+// followed by its 1 KiB lo fragment. Row-major images and LDS stage images keep their lo plane
+// at a fixed element offset (`lo` arguments) from the hi plane.
+// =======================================================================================
+namespace mb {
+
+constexpr bool X3 = MB_X3 != 0;
+constexpr int FRAG_ELEMS = X3 ? 1024 : 512;     // h16 elements per packed fragment (hi [+ lo])
+constexpr int FRAG_SZ = FRAG_ELEMS * 2;          // bytes
+constexpr int PROW = X3 ? 256 : 128;             // h16 per pooled / dL/dpooled row: [hi 128 | lo 128]
+
+struct Fr { h16x8 h, l; };
+struct Pk { h16x16 h, l; };
+
+DEV f32x16 mma(const Fr& a, const Fr& b, f32x16 c) {
+  if constexpr (X3) {
+    c = mfma(a.l, b.h, c);
+    c = mfma(a.h, b.l, c);
+  }
+  return mfma(a.h, b.h, c);
+}
+
+// b exact in h16 (the layer-1 input fragments carry their own hi/lo split along k)
+DEV f32x16 mma_bx(const Fr& a, const h16x8& b, f32x16 c) {
+  if constexpr (X3) c = mfma(a.l, b, c);
+  return mfma(a.h, b, c);
+}
+
+DEV h16x8 zero_h8() {
+  h16x8 z;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) z[j] = (h16)0.f;
+  return z;
+}
+
+// accumulator regs 8S..8S+7 -> operand fragment (acc_frag + residual)
+template <int S>
+DEV Fr acc_fr(const f32x16& c) {
+  Fr f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float x = c[8 * S + j];
+    f.h[j] = (h16)x;
+    if constexpr (X3) f.l[j] = (h16)(x - (float)f.h[j]);
+  }
+  return f;
+}
+
+DEV Pk to_pk(const f32x16& c) {
+  Pk p;
+  p.h = to_h16x16(c);
+  if constexpr (X3) {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) p.l[q] = (h16)(c[q] - (float)p.h[q]);
+  }
+  return p;
+}
+
+// relu(c) packed; x3: relu in fp32, then split (both planes are +0 where c <= 0)
+DEV Pk to_pk_relu(const f32x16& c) {
+  if constexpr (X3) {
+    f32x16 r = c;
+    relu_(r);
+    return to_pk(r);
+  } else {
+    Pk p;
+    p.h = to_h16x16_relu(c);
+    return p;
+  }
+}
+
+template <int S>
+DEV Fr pk_fr(const Pk& p) {
+  Fr f;
+  f.h = bacc_frag<S>(p.h);
+  if constexpr (X3) f.l = bacc_frag<S>(p.l);
+  return f;
+}
+
+// d *= relu'(pre), H = relu(pre) packed (>= +0): both planes of d masked by H's hi plane
+DEV void mask_pk(Pk& d, const Pk& H) {
+  mask_by_nonzero(d.h, H.h);
+  if constexpr (X3) mask_by_nonzero(d.l, H.h);
+}
+
+// ---- weight operands
+DEV Fr frag_fr(const h16* base, int f, int lane) {
+  const h16* p = base + ((size_t)f * FRAG_ELEMS + lane * 8);
+  Fr r;
+  r.h = *reinterpret_cast<const h16x8*>(p);
+  if constexpr (X3) r.l = *reinterpret_cast<const h16x8*>(p + 512);
+  return r;
+}
+
+DEV Fr wrm_nat_fr(const h16* W, int stride, int m0, int kk, int lane, int lo) {
+  Fr r;
+  r.h = wrm_nat(W, stride, m0, kk, lane);
+  if constexpr (X3) r.l = wrm_nat(W + lo, stride, m0, kk, lane);
+  return r;
+}
+
+DEV Fr wrm_acc_fr(const h16* W, int stride, int m0, int kk, int lane, int lo) {
+  Fr r;
+  r.h = wrm_acc(W, stride, m0, kk, lane);
+  if constexpr (X3) r.l = wrm_acc(W + lo, stride, m0, kk, lane);
+  return r;
+}
+
+DEV Fr wrmT_acc_fr(const h16* W, int stride, int m0, int kk, int lane, int lo) {
+  Fr r;
+  r.h = wrmT_acc(W, stride, m0, kk, lane);
+  if constexpr (X3) r.l = wrmT_acc(W + lo, stride, m0, kk, lane);
+  return r;
+}
+
+// 16-byte row read of a [row][stride] h16 image / global row, with its lo plane at +lo
+DEV Fr row_fr(const h16* p, int lo) {
+  Fr r;
+  r.h = *reinterpret_cast<const h16x8*>(p);
+  if constexpr (X3) r.l = *reinterpret_cast<const h16x8*>(p + lo);
+  return r;
+}
+
+// ---- LDS stage images (edge-major, hi plane + lo plane at +lo)
+DEV void store_pk(h16* img, int stride, int erow, int col0, const Pk& v, int h, int lo) {
+  store_tile(img, stride, erow, col0, v.h, h);
+  if constexpr (X3) store_tile(img + lo, stride, erow, col0, v.l, h);
+}
+
+template <int W>
+DEV void store_pk_sw(h16* img, int erow, int col0, const Pk& v, int h, int lo) {
+  store_tile_sw<W>(img, erow, col0, v.h, h);
+  if constexpr (X3) store_tile_sw<W>(img + lo, erow, col0, v.l, h);
+}
+
+// stage_mma with split operands: A = imgA (+loA), B = imgB (+loB); BX: B exact (no lo plane).
+// Bias row sums of A cover both planes.
+template <int ES, bool BX = false>
+DEV float stage_mma_fr(const h16* imgA, int sA, int loA, const h16* imgB, int sB, int loB, int mt, int nt, int lane,
+                       f32x16& acc, int bs_lo = 0, int bs_hi = 0) {
+  if constexpr (!X3) {
+    return stage_mma<ES>(imgA, sA, imgB, sB, mt, nt, lane, acc, bs_lo, bs_hi);
+  } else {
+    bs_lo = __builtin_amdgcn_readfirstlane(bs_lo);
+    bs_hi = __builtin_amdgcn_readfirstlane(bs_hi);
+    float s = 0.f;
+#pragma nounroll
+    for (int ks = 0; ks < ES; ++ks) {
+      Fr a, b;
+      a.h = tr_frag(imgA, sA, 16 * ks, 32 * mt, lane);
+      a.l = tr_frag(imgA + loA, sA, 16 * ks, 32 * mt, lane);
+      b.h = tr_frag(imgB, sB, 16 * ks, 32 * nt, lane);
+      if constexpr (BX) {
+        acc = mma_bx(a, b.h, acc);
+      } else {
+        b.l = tr_frag(imgB + loB, sB, 16 * ks, 32 * nt, lane);
+        acc = mma(a, b, acc);
+      }
+      if (ks >= bs_lo && ks < bs_hi) {
+        s = dot_sum8(a.l, s);
+        s = dot_sum8(a.h, s);
+      }
+    }
+    return s;
+  }
+}
+
+template <int ES, int WA, int WB, bool BX = false>
+DEV float stage_mma_sw_fr(const h16* imgA, int loA, const h16* imgB, int loB, int mt, int nt, int lane, f32x16& acc,
+                          int bs_lo = 0, int bs_hi = 0) {
+  if constexpr (!X3) {
+    return stage_mma_sw<ES, WA, WB>(imgA, imgB, mt, nt, lane, acc, bs_lo, bs_hi);
+  } else {
+    bs_lo = __builtin_amdgcn_readfirstlane(bs_lo);
+    bs_hi = __builtin_amdgcn_readfirstlane(bs_hi);
+    const TrOff oa = tr_off_sw<WA>(32 * mt, lane), ob = tr_off_sw<WB>(32 * nt, lane);
+    float s = 0.f;
+#pragma nounroll
+    for (int ks = 0; ks < ES; ++ks) {
+      Fr a, b;
+      a.h = tr_frag_sw<WA>(imgA, 16 * ks, oa);
+      a.l = tr_frag_sw<WA>(imgA + loA, 16 * ks, oa);
+      b.h = tr_frag_sw<WB>(imgB, 16 * ks, ob);
+      if constexpr (BX) {
+        acc = mma_bx(a, b.h, acc);
+      } else {
+        b.l = tr_frag_sw<WB>(imgB + loB, 16 * ks, ob);
+        acc = mma(a, b, acc);
+      }
+      if (ks >= bs_lo && ks < bs_hi) {
+        s = dot_sum8(a.l, s);
+        s = dot_sum8(a.h, s);
+      }
+    }
+    return s;
+  }
+}
+
+// per-turn share [lo, hi) of the bias-sum edge steps: a wave owns steps [w0, w1) of the whole
+// chunk (nturns x ks_turn steps); turn `turn` contracts steps [turn*ks_turn, (turn+1)*ks_turn)
+DEV void turn_range(int w0, int w1, int turn, int ks_turn, int& lo, int& hi) {
+  const int t0 = turn * ks_turn;
+  lo = max(w0, t0) - t0;
+  hi = min(w1, t0 + ks_turn) - t0;
+  if (hi < lo) hi = lo;
+}
+
+}  // namespace mb

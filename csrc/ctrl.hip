@@ -91,7 +91,7 @@ DEV void ctrl_edge_tile(const h16x8& F, const h16* wl, const float* eb2, int lan
   f32x16 H1[2];
 #pragma unroll
   for (int mt = 0; mt < 2; ++mt) {
-    H1[mt] = mfma(frag_ld(wl, mt, lane), F, zero16());
+    H1[mt] = mma_bx(frag_fr(wl, mt, lane), F, zero16());
     relu_(H1[mt]);
   }
 #pragma unroll
@@ -102,7 +102,7 @@ DEV void ctrl_edge_tile(const h16x8& F, const h16* wl, const float* eb2, int lan
     for (int q = 0; q < 16; ++q) z[q] = bv;
     static_for<4>([&](auto kk_) {
       constexpr int kk = decltype(kk_)::value;
-      z = mfma(acc_frag<kk & 1>(H1[kk >> 1]), frag_ld(wl, 2 + nt * 4 + kk, lane), z);
+      z = mma(acc_fr<kk & 1>(H1[kk >> 1]), frag_fr(wl, 2 + nt * 4 + kk, lane), z);
     });
     Z[nt] = z;
   }
@@ -111,18 +111,17 @@ DEV void ctrl_edge_tile(const h16x8& F, const h16* wl, const float* eb2, int lan
 // node MLP forward for 32 agents; returns Y4 (rows 0..3 = the 4 gain pre-activations)
 struct NodeActs { f32x16 Y1[2], Y2[4], Y3[2], Y4; };
 
-DEV void node_forward(const h16* pool, const h16x8& sfrag, const h16* wn, const float* nb2,
+// pool(kk): the pooled-feature B fragment of k-step kk (features 16kk + 8h + j of agent r)
+template <typename PoolFr>
+DEV void node_forward(PoolFr pool, const h16x8& sfrag, const h16* wn, const float* nb2,
                       const float* nb3, const float* nb4, int lane, NodeActs& o) {
-  const int r = lane & 31, h = lane >> 5;
+  const int h = lane >> 5;
 #pragma unroll
   for (int mt = 0; mt < 2; ++mt) {
     f32x16 c = zero16();
 #pragma unroll
-    for (int kk = 0; kk < 8; ++kk) {
-      const h16x8 p = *reinterpret_cast<const h16x8*>(pool + r * PSTR + 16 * kk + 8 * h);
-      c = mfma(frag_ld(wn, mt * 9 + kk, lane), p, c);
-    }
-    c = mfma(frag_ld(wn, mt * 9 + 8, lane), sfrag, c);
+    for (int kk = 0; kk < 8; ++kk) c = mma(frag_fr(wn, mt * 9 + kk, lane), pool(kk), c);
+    c = mma_bx(frag_fr(wn, mt * 9 + 8, lane), sfrag, c);
     relu_(c);
     o.Y1[mt] = c;
   }
@@ -131,7 +130,7 @@ DEV void node_forward(const h16* pool, const h16x8& sfrag, const h16* wn, const 
     f32x16 c = bias_rows(nb2, 32 * mt, h);
     static_for<4>([&](auto kk_) {
       constexpr int kk = decltype(kk_)::value;
-      c = mfma(frag_ld(wn, 18 + mt * 4 + kk, lane), acc_frag<kk & 1>(o.Y1[kk >> 1]), c);
+      c = mma(frag_fr(wn, 18 + mt * 4 + kk, lane), acc_fr<kk & 1>(o.Y1[kk >> 1]), c);
     });
     relu_(c);
     o.Y2[mt] = c;
@@ -141,7 +140,7 @@ DEV void node_forward(const h16* pool, const h16x8& sfrag, const h16* wn, const 
     f32x16 c = bias_rows(nb3, 32 * mt, h);
     static_for<8>([&](auto kk_) {
       constexpr int kk = decltype(kk_)::value;
-      c = mfma(frag_ld(wn, 34 + mt * 8 + kk, lane), acc_frag<kk & 1>(o.Y2[kk >> 1]), c);
+      c = mma(frag_fr(wn, 34 + mt * 8 + kk, lane), acc_fr<kk & 1>(o.Y2[kk >> 1]), c);
     });
     relu_(c);
     o.Y3[mt] = c;
@@ -150,7 +149,7 @@ DEV void node_forward(const h16* pool, const h16x8& sfrag, const h16* wn, const 
     f32x16 c = bias_rows(nb4, 0, h);
     static_for<4>([&](auto kk_) {
       constexpr int kk = decltype(kk_)::value;
-      c = mfma(frag_ld(wn, 50 + kk, lane), acc_frag<kk & 1>(o.Y3[kk >> 1]), c);
+      c = mma(frag_fr(wn, 50 + kk, lane), acc_fr<kk & 1>(o.Y3[kk >> 1]), c);
     });
     o.Y4 = c;
   }
@@ -192,15 +191,92 @@ DEV void ctrl_st_load(const float4* S, long s_env, const EdgeIdx& x, EdgeSt<D>& 
   }
 }
 
+// Node phase of the controller step for the 32-column group at g0 (lane column r = agent
+// g0 + r, r < APW): node MLP (pooled fragments from `pool`), gains 2*sigmoid+0.2, PD law, Euler
+// step, per-env goal-distance and action-loss sums.
+template <int D, typename PoolFr>
+DEV void node_phase(const CtrlArgs& a, int g0, int APW, int total, PoolFr pool, const h16* wn, const float* nb2,
+                    const float* nb3, const float* nb4, int lane) {
+  const int r = lane & 31, h = lane >> 5;
+  const int N = a.N;
+  const int gi = g0 + r;
+  const bool ok = r < APW && gi < total;
+  int b = 0, i = 0;
+  float sp[D], sv[D], gg[D];
+#pragma unroll
+  for (int q = 0; q < D; ++q) { sp[q] = 0.f; sv[q] = 0.f; gg[q] = 0.f; }
+  if (ok) {
+    b = gi / N; i = gi - b * N;
+    load_rec<D>(a.S + (long)b * a.s_env * REC<D>, (unsigned)i, sp, sv);
+#pragma unroll
+    for (int q = 0; q < D; ++q) gg[q] = a.G[((long)b * N + i) * D + q];
+  }
+  float ex[D];
+#pragma unroll
+  for (int q = 0; q < D; ++q) ex[q] = sp[q] - gg[q];
+  const h16x8 sf = node_state_frag<D>(ex, sv, ok, h);
+  NodeActs na;
+  node_forward(pool, sf, wn + opaque_zero(), nb2, nb3, nb4, lane, na);
+  float y4r[8];
+  acc_rows8(na.Y4, y4r);                                     // gain pre-activations 0..2D-1
+  float dsum = 0.f, asum = 0.f;
+  if (ok && h == 0) {
+    float av[D], snp[D], snv[D], ar[D];
+#pragma unroll
+    for (int q = 0; q < D; ++q) {
+      const float kp = 2.f / (1.f + __expf(-y4r[2 * q])) + 0.2f;
+      const float kv = 2.f / (1.f + __expf(-y4r[2 * q + 1])) + 0.2f;
+      av[q] = -(kp * ex[q] + kv * sv[q]);
+      if (a.noise) av[q] += a.noise[((long)b * a.n_env + i) * D + q];
+    }
+    if (a.A) {
+#pragma unroll
+      for (int q = 0; q < D; ++q) a.A[((long)b * a.a_env + i) * D + q] = av[q];
+    }
+#pragma unroll
+    for (int q = 0; q < D; ++q) {
+      snp[q] = sp[q] + sv[q] * a.dt;
+      snv[q] = sv[q] + av[q] * a.dt;
+      ar[q] = -(ex[q] + a.sqrt3 * sv[q]);
+    }
+    if (a.Snext) store_rec<D>(a.Snext + (long)b * a.sn_env * REC<D>, (unsigned)i, snp, snv);
+    float dd[D];
+#pragma unroll
+    for (int q = 0; q < D; ++q) dd[q] = snp[q] - gg[q];
+    dsum = sqrtf(sqsum<D>(dd));
+    asum = fabsf(sqsum<D>(av) - sqsum<D>(ar));
+  }
+  // per-env sums: one atomic per wave when its 32 agents share an env
+  const int last = min(g0 + APW - 1, total - 1);
+  if (g0 / N == last / N) {
+    dsum = wave_sum(dsum);
+    asum = wave_sum(asum);
+    if (lane == 0) {
+      const int be = g0 / N;
+      if (a.dist_sum) atomicAdd(a.dist_sum + (long)be * a.d_env, dsum);
+      if (a.act_sum) atomicAdd(a.act_sum + (long)be * a.ac_env, asum);
+    }
+  } else if (ok && h == 0) {
+    if (a.dist_sum) atomicAdd(a.dist_sum + (long)b * a.d_env, dsum);
+    if (a.act_sum) atomicAdd(a.act_sum + (long)b * a.ac_env, asum);
+  }
+}
+
+// Controller step. bf16 / fp16: edge and node phase in one kernel, the pooled features cross
+// from the edge lanes (features) to the node lanes (agents) through a per-wave LDS image.
+// x3: the split weights do not fit one workgroup's LDS together, so this kernel runs the edge
+// phase only and writes the pooled features ([hi | lo] rows, always stored) straight to global
+// memory; ctrl_node_fwd_kernel reads them back as node-layer B fragments.
 template <int WAVES, int D>
 __global__ __launch_bounds__(WAVES * 64) void ctrl_fwd_kernel(CtrlArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  constexpr int NFR = X3 ? 18 : CTRL_FWD_FRAGS;                     // fragments staged in LDS
   h16* wl = reinterpret_cast<h16*>(smem);                            // ew1f, ew2 (18 frags)
-  h16* wn = wl + 18 * 512;                                            // nw1f..nw4 (54 frags)
-  float* vl = reinterpret_cast<float*>(smem + CTRL_FWD_FRAGS * FRAG_BYTES);
-  h16* pools = reinterpret_cast<h16*>(smem + CTRL_FWD_FRAGS * FRAG_BYTES + CTRL_VEC * 4);
-  block_copy16(wl, a.wpack + (size_t)a.f_edge * 512, 18 * FRAG_BYTES);
-  block_copy16(wn, a.wpack + (size_t)a.f_node * 512, 54 * FRAG_BYTES);
+  h16* wn = wl + 18 * FRAG_ELEMS;                                     // nw1f..nw4 (54 frags)
+  float* vl = reinterpret_cast<float*>(smem + NFR * FRAG_SZ);
+  h16* pools = reinterpret_cast<h16*>(smem + NFR * FRAG_SZ + CTRL_VEC * 4);
+  block_copy16(wl, a.wpack + (size_t)a.f_edge * FRAG_ELEMS, 18 * FRAG_SZ);
+  if constexpr (!X3) block_copy16(wn, a.wpack + (size_t)a.f_node * FRAG_ELEMS, 54 * FRAG_SZ);
   block_copy16(vl, a.wvec, CTRL_VEC * 4);
   __syncthreads();
   const float* eb2 = vl;
@@ -253,7 +329,8 @@ __global__ __launch_bounds__(WAVES * 64) void ctrl_fwd_kernel(CtrlArgs a) {
       const int arow = 2 * q + h;   // h==0 writes agent 2q, h==1 agent 2q+1
       int bb = 0, ii = 0;
       const int ga = g0 + arow;
-      if (a.argmax && ga < total) { bb = ga / N; ii = ga - bb * N; }
+      const bool gout = (a.argmax || X3) && ga < total;
+      if (gout) { bb = ga / N; ii = ga - bb * N; }
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt) {
 #ifdef CTRL_X_NOPOOL
@@ -269,7 +346,16 @@ __global__ __launch_bounds__(WAVES * 64) void ctrl_fwd_kernel(CtrlArgs a) {
         p1 = max(p1, shfl_xor32i(p1));
         const int pw_ = (h == 0) ? p0 : p1;
         const float pv = __int_as_float(pw_ & -16);
-        pool[arow * PSTR + 32 * nt + r] = (h16)pv;
+        if constexpr (X3) {
+          if (gout) {
+            h16* prow = a.pooled + (long)bb * a.p_env + (long)ii * PROW + 32 * nt + r;
+            const h16 ph = (h16)pv;
+            prow[0] = ph;
+            prow[128] = (h16)(pv - (float)ph);
+          }
+        } else {
+          pool[arow * PSTR + 32 * nt + r] = (h16)pv;
+        }
 #ifndef CTRL_X_NOARGMAX
         if (a.argmax && ga < total)
           a.argmax[(long)bb * a.am_env + (long)ii * 128 + 32 * nt + r] =
@@ -277,6 +363,7 @@ __global__ __launch_bounds__(WAVES * 64) void ctrl_fwd_kernel(CtrlArgs a) {
 #endif
       }
     }
+    if constexpr (X3) continue;     // node phase: ctrl_node_fwd_kernel
     lds_wave_sync();
     if (a.pooled) {   // 32 agents x 256 B, 16 B per lane
       for (int u = lane; u < 32 * 16; u += 64) {
@@ -294,75 +381,39 @@ __global__ __launch_bounds__(WAVES * 64) void ctrl_fwd_kernel(CtrlArgs a) {
     continue;
 #endif
     // ---------------- node phase: lane column r = agent g0 + r
-    const int gi = g0 + r;
-    const bool ok = r < APW && gi < total;
-    int b = 0, i = 0;
-    float sp[D], sv[D], gg[D];
-#pragma unroll
-    for (int q = 0; q < D; ++q) { sp[q] = 0.f; sv[q] = 0.f; gg[q] = 0.f; }
-    if (ok) {
-      b = gi / N; i = gi - b * N;
-      load_rec<D>(a.S + (long)b * a.s_env * REC<D>, (unsigned)i, sp, sv);
-#pragma unroll
-      for (int q = 0; q < D; ++q) gg[q] = a.G[((long)b * N + i) * D + q];
-    }
-    float ex[D];
-#pragma unroll
-    for (int q = 0; q < D; ++q) ex[q] = sp[q] - gg[q];
-    const h16x8 sf = node_state_frag<D>(ex, sv, ok, h);
-    NodeActs na;
-    node_forward(pool, sf, wn + opaque_zero(), nb2, nb3, nb4, lane, na);
-    float y4r[8];
-    acc_rows8(na.Y4, y4r);                                     // gain pre-activations 0..2D-1
-    float dsum = 0.f, asum = 0.f;
-    if (ok && h == 0) {
-      float av[D], snp[D], snv[D], ar[D];
-#pragma unroll
-      for (int q = 0; q < D; ++q) {
-        const float kp = 2.f / (1.f + __expf(-y4r[2 * q])) + 0.2f;
-        const float kv = 2.f / (1.f + __expf(-y4r[2 * q + 1])) + 0.2f;
-        av[q] = -(kp * ex[q] + kv * sv[q]);
-        if (a.noise) av[q] += a.noise[((long)b * a.n_env + i) * D + q];
-      }
-      if (a.A) {
-#pragma unroll
-        for (int q = 0; q < D; ++q) a.A[((long)b * a.a_env + i) * D + q] = av[q];
-      }
-#pragma unroll
-      for (int q = 0; q < D; ++q) {
-        snp[q] = sp[q] + sv[q] * a.dt;
-        snv[q] = sv[q] + av[q] * a.dt;
-        ar[q] = -(ex[q] + a.sqrt3 * sv[q]);
-      }
-      if (a.Snext) store_rec<D>(a.Snext + (long)b * a.sn_env * REC<D>, (unsigned)i, snp, snv);
-      float dd[D];
-#pragma unroll
-      for (int q = 0; q < D; ++q) dd[q] = snp[q] - gg[q];
-      dsum = sqrtf(sqsum<D>(dd));
-      asum = fabsf(sqsum<D>(av) - sqsum<D>(ar));
-    }
-    // per-env sums: one atomic per wave when its 32 agents share an env
-    const int last = min(g0 + APW - 1, total - 1);
-    if (g0 / N == last / N) {
-      dsum = wave_sum(dsum);
-      asum = wave_sum(asum);
-      if (lane == 0) {
-        const int be = g0 / N;
-        if (a.dist_sum) atomicAdd(a.dist_sum + (long)be * a.d_env, dsum);
-        if (a.act_sum) atomicAdd(a.act_sum + (long)be * a.ac_env, asum);
-      }
-    } else if (ok && h == 0) {
-      if (a.dist_sum) atomicAdd(a.dist_sum + (long)b * a.d_env, dsum);
-      if (a.act_sum) atomicAdd(a.act_sum + (long)b * a.ac_env, asum);
-    }
+    node_phase<D>(a, g0, APW, total, [&](int kk) { return row_fr(pool + r * PSTR + 16 * kk + 8 * h, 0); },
+                  wn, nb2, nb3, nb4, lane);
     // the pool image is rewritten by the next group: finish all reads first
     lds_wave_sync();
+  }
+}
+
+// x3 node phase of the controller step over the pooled rows written by ctrl_fwd_kernel
+template <int WAVES, int D>
+__global__ __launch_bounds__(WAVES * 64) void ctrl_node_fwd_kernel(CtrlArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  h16* wn = reinterpret_cast<h16*>(smem);                             // nw1f..nw4 (54 frags)
+  float* vl = reinterpret_cast<float*>(smem + 54 * FRAG_SZ);
+  block_copy16(wn, a.wpack + (size_t)a.f_node * FRAG_ELEMS, 54 * FRAG_SZ);
+  block_copy16(vl, a.wvec, CTRL_VEC * 4);
+  __syncthreads();
+  const int wave = threadIdx.x / WAVE, lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
+  const int N = a.N;
+  const int total = a.B * N;
+  for (int grp = blockIdx.x * WAVES + wave; grp * 32 < total; grp += gridDim.x * WAVES) {
+    const int g0 = grp * 32;
+    const int gi = min(g0 + r, total - 1);
+    const int b = gi / N, i = gi - b * N;
+    const h16* prow = a.pooled + (long)b * a.p_env + (long)i * PROW + 8 * h;
+    node_phase<D>(a, g0, 32, total, [&](int kk) { return row_fr(prow + 16 * kk, 128); }, wn, vl + 128, vl + 256,
+                  vl + 320, lane);
   }
 }
 
 constexpr int CTRL_WAVES = 8;
 
 size_t ctrl_fwd_lds() {
+  if constexpr (X3) return (size_t)18 * FRAG_SZ + CTRL_VEC * 4;
   return (size_t)CTRL_FWD_FRAGS * FRAG_BYTES + CTRL_VEC * 4 + (size_t)CTRL_WAVES * 32 * PSTR * 2;
 }
 
@@ -373,18 +424,31 @@ extern "C" int MB_SYM(ctrl_fwd)(const mb::CtrlArgs* a, int num_cu, hipStream_t s
   using namespace mb;
   using namespace mb::MB_PREC;
   if (a->K > 16 || a->K < 1) return -1;
-  const int apw = (a->apw >= 2 && a->apw <= 32) ? a->apw : 32;
+  if (X3 && !a->pooled) return -2;            // the x3 node phase reads the stored pooled rows
+  const int apw = X3 ? 32 : ((a->apw >= 2 && a->apw <= 32) ? a->apw : 32);
   const int groups = (a->B * a->N + apw - 1) / apw;
   int blocks = (groups + CTRL_WAVES - 1) / CTRL_WAVES;
   const int maxb = num_cu > 0 ? num_cu * 2 : blocks;
   if (blocks > maxb) blocks = maxb;
   const size_t lds = ctrl_fwd_lds();
+  CtrlArgs b = *a;
+  b.apw = apw;
   if (a->dim == 3) {
     (void)hipFuncSetAttribute((const void*)ctrl_fwd_kernel<CTRL_WAVES, 3>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL((ctrl_fwd_kernel<CTRL_WAVES, 3>), dim3(blocks), dim3(CTRL_WAVES * 64), lds, st, *a);
+    hipLaunchKernelGGL((ctrl_fwd_kernel<CTRL_WAVES, 3>), dim3(blocks), dim3(CTRL_WAVES * 64), lds, st, b);
   } else {
     (void)hipFuncSetAttribute((const void*)ctrl_fwd_kernel<CTRL_WAVES, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL((ctrl_fwd_kernel<CTRL_WAVES, 2>), dim3(blocks), dim3(CTRL_WAVES * 64), lds, st, *a);
+    hipLaunchKernelGGL((ctrl_fwd_kernel<CTRL_WAVES, 2>), dim3(blocks), dim3(CTRL_WAVES * 64), lds, st, b);
+  }
+  if constexpr (X3) {
+    const size_t ldn = (size_t)54 * FRAG_SZ + CTRL_VEC * 4;
+    if (a->dim == 3) {
+      (void)hipFuncSetAttribute((const void*)ctrl_node_fwd_kernel<CTRL_WAVES, 3>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ldn);
+      hipLaunchKernelGGL((ctrl_node_fwd_kernel<CTRL_WAVES, 3>), dim3(blocks), dim3(CTRL_WAVES * 64), ldn, st, b);
+    } else {
+      (void)hipFuncSetAttribute((const void*)ctrl_node_fwd_kernel<CTRL_WAVES, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ldn);
+      hipLaunchKernelGGL((ctrl_node_fwd_kernel<CTRL_WAVES, 2>), dim3(blocks), dim3(CTRL_WAVES * 64), ldn, st, b);
+    }
   }
   return (int)hipGetLastError();
 }
@@ -409,11 +473,19 @@ constexpr int NB_WAVES = 4;
 constexpr int NB_CH = NB_WAVES * 32;                  // agents per chunk
 constexpr int NS1 = 168, NS2 = 68, NS3 = 132, NS4 = 68;   // row-major image strides (NS2..4: 2*odd dwords, conflict-free ds_read_b64 row reads)
 constexpr int NODE_RM_ELEMS = 64 * NS1 + 128 * NS2 + 64 * NS3 + 32 * NS4;
+constexpr int NODE_RM_LO = NODE_RM_ELEMS;             // lo plane offset of the images (x3)
 constexpr int NP_W1 = 0, NP_W2 = 10240, NP_B2 = 18432, NP_W3 = 18560, NP_B3 = 26752, NP_W4 = 26816, NP_B4 = 28864;
 constexpr int CTRL_NODE_PARTIAL = 28896;
-constexpr size_t NB_STAGE = (size_t)(72 + 168) * NB_CH * 2;
+// weight-gradient stages: a region holds the rows of NB_TW waves (all of them in the 1-pass
+// builds; one in x3, whose images carry a lo plane) -> NB_NT turns per stage
+constexpr int NB_TW = X3 ? 1 : NB_WAVES;
+constexpr int NB_NT = NB_WAVES / NB_TW;
+constexpr int NB_RT = NB_TW * 32;                     // region rows
+constexpr int NB_KST = NB_RT / 16;                    // agent steps per turn
+constexpr int NB_PL = (72 + 168) * NB_RT;             // elements per region plane
+constexpr size_t NB_STAGE = (size_t)(X3 ? 2 : 1) * NB_PL * 2;
 
-size_t ctrl_node_bwd_lds() { return (size_t)NODE_RM_ELEMS * 2 + CTRL_VEC * 4 + NB_STAGE; }
+size_t ctrl_node_bwd_lds() { return (size_t)(X3 ? 2 : 1) * NODE_RM_ELEMS * 2 + CTRL_VEC * 4 + NB_STAGE; }
 
 DEV float sigm(float x) { return 1.f / (1.f + __expf(-x)); }
 
@@ -442,10 +514,11 @@ DEV void store_tile_add(float* dst, int ncols, int mt, int nt, const f32x16& old
 template <int D>
 __global__ __launch_bounds__(NB_WAVES * 64, 1) void ctrl_node_bwd_kernel(CtrlNodeBwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  constexpr int RM = (X3 ? 2 : 1) * NODE_RM_ELEMS;
   h16* wr = reinterpret_cast<h16*>(smem);
-  float* vl = reinterpret_cast<float*>(smem + NODE_RM_ELEMS * 2);
-  h16* stg = reinterpret_cast<h16*>(smem + NODE_RM_ELEMS * 2 + CTRL_VEC * 4);
-  block_copy16(wr, a.wrm, NODE_RM_ELEMS * 2);
+  float* vl = reinterpret_cast<float*>(smem + RM * 2);
+  h16* stg = reinterpret_cast<h16*>(smem + RM * 2 + CTRL_VEC * 4);
+  block_copy16(wr, a.wrm, RM * 2);
   block_copy16(vl, a.wvec, CTRL_VEC * 4);
   __syncthreads();
   const float* nb2 = vl + 128;
@@ -456,6 +529,9 @@ __global__ __launch_bounds__(NB_WAVES * 64, 1) void ctrl_node_bwd_kernel(CtrlNod
   const int total = a.B * N;
   const long nchunks = (total + NB_CH - 1) / NB_CH;
   const int erow = wave * 32 + r;
+  const int trow = NB_NT == 1 ? erow : (wave % NB_TW) * 32 + r;   // this wave's rows inside a turn's region
+  const int myturn = wave / NB_TW;
+  constexpr int LO = NODE_RM_LO;
 
   f32x16 acc1[3], acc2[2], acc3[2], acc4;
 #pragma unroll
@@ -463,6 +539,7 @@ __global__ __launch_bounds__(NB_WAVES * 64, 1) void ctrl_node_bwd_kernel(CtrlNod
   acc2[0] = acc2[1] = acc3[0] = acc3[1] = acc4 = zero16();
   float bs2[2] = {0.f, 0.f}, bs3[2] = {0.f, 0.f}, bs4 = 0.f;
   const int n1 = (wave < 2) ? 3 : 2;
+  const h16x8 zz = zero_h8();
 
   for (long chunk = blockIdx.x; chunk < nchunks; chunk += gridDim.x) {
     const int ga = (int)(chunk * NB_CH) + erow;
@@ -472,8 +549,7 @@ __global__ __launch_bounds__(NB_WAVES * 64, 1) void ctrl_node_bwd_kernel(CtrlNod
 #pragma unroll
     for (int q = 0; q < D; ++q) { sp[q] = sv[q] = gg[q] = av[q] = gnp[q] = gnv[q] = 0.f; }
     bool vld = false;
-    h16x8 Pf[9];
-    const h16 z = (h16)0.f;   // Pf is dead after Y1; S1 re-reads the pooled rows
+    Fr Pf[8];                 // dead after Y1; S1 re-reads the pooled rows
     if (ok) {
       b = ga / N; i = ga - b * N;
       load_rec<D>(a.S + (long)b * a.s_env * REC<D>, (unsigned)i, sp, sv);
@@ -484,57 +560,56 @@ __global__ __launch_bounds__(NB_WAVES * 64, 1) void ctrl_node_bwd_kernel(CtrlNod
       }
       if (a.Gn) load_rec<D>(a.Gn + (long)b * a.gn_env * REC<D>, (unsigned)i, gnp, gnv);
       vld = a.valid ? (a.valid[(long)b * a.v_env] != 0) : true;
-      const h16* prow = a.pooled + (long)b * a.p_env + (long)i * 128;
+      const h16* prow = a.pooled + (long)b * a.p_env + (long)i * PROW;
 #pragma unroll
-      for (int kk = 0; kk < 8; ++kk) Pf[kk] = *reinterpret_cast<const h16x8*>(prow + 16 * kk + 8 * h);
+      for (int kk = 0; kk < 8; ++kk) Pf[kk] = row_fr(prow + 16 * kk + 8 * h, 128);
     } else {
 #pragma unroll
-      for (int kk = 0; kk < 8; ++kk)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) Pf[kk][j] = z;
+      for (int kk = 0; kk < 8; ++kk) Pf[kk].h = Pf[kk].l = zz;
     }
     float ex[D];
 #pragma unroll
     for (int q = 0; q < D; ++q) ex[q] = sp[q] - gg[q];
-    Pf[8] = node_state_frag<D>(ex, sv, ok, h);
+    const h16x8 sfr = node_state_frag<D>(ex, sv, ok, h);
     const h16* W1 = wr + opaque_zero();
     const h16* W2 = W1 + 64 * NS1;
     const h16* W3 = W2 + 128 * NS2;
     const h16* W4 = W3 + 64 * NS3;
     // ---- forward recompute
-    h16x16 Y1b[2], Y2b[4], Y3b[2];
+    Pk Y1b[2], Y2b[4], Y3b[2];
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt) {
       f32x16 c = zero16();
 #pragma unroll
-      for (int kk = 0; kk < 9; ++kk) c = mfma(wrm_nat(W1 + opaque_zero(), NS1, 32 * mt, kk, lane), Pf[kk], c);
+      for (int kk = 0; kk < 8; ++kk) c = mma(wrm_nat_fr(W1 + opaque_zero(), NS1, 32 * mt, kk, lane, LO), Pf[kk], c);
+      c = mma_bx(wrm_nat_fr(W1 + opaque_zero(), NS1, 32 * mt, 8, lane, LO), sfr, c);
       relu_(c);
-      Y1b[mt] = to_h16x16(c);
+      Y1b[mt] = to_pk(c);
     }
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt) {
       f32x16 c = bias_rows(nb2, 32 * mt, h);
       static_for<4>([&](auto kk_) {
         constexpr int kk = decltype(kk_)::value;
-        c = mfma(wrm_acc(W2 + opaque_zero(), NS2, 32 * mt, kk, lane), bacc_frag<kk & 1>(Y1b[kk >> 1]), c);
+        c = mma(wrm_acc_fr(W2 + opaque_zero(), NS2, 32 * mt, kk, lane, LO), pk_fr<kk & 1>(Y1b[kk >> 1]), c);
       });
       relu_(c);
-      Y2b[mt] = to_h16x16(c);
+      Y2b[mt] = to_pk(c);
     }
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt) {
       f32x16 c = bias_rows(nb3, 32 * mt, h);
       static_for<8>([&](auto kk_) {
         constexpr int kk = decltype(kk_)::value;
-        c = mfma(wrm_acc(W3 + opaque_zero(), NS3, 32 * mt, kk, lane), bacc_frag<kk & 1>(Y2b[kk >> 1]), c);
+        c = mma(wrm_acc_fr(W3 + opaque_zero(), NS3, 32 * mt, kk, lane, LO), pk_fr<kk & 1>(Y2b[kk >> 1]), c);
       });
       relu_(c);
-      Y3b[mt] = to_h16x16(c);
+      Y3b[mt] = to_pk(c);
     }
     f32x16 y4 = bias_rows(nb4, 0, h);
     static_for<4>([&](auto kk_) {
       constexpr int kk = decltype(kk_)::value;
-      y4 = mfma(wrm_acc(W4 + opaque_zero(), NS4, 0, kk, lane), bacc_frag<kk & 1>(Y3b[kk >> 1]), y4);
+      y4 = mma(wrm_acc_fr(W4 + opaque_zero(), NS4, 0, kk, lane, LO), pk_fr<kk & 1>(Y3b[kk >> 1]), y4);
     });
     // ---- gain law + action loss backward (lanes h == 0 own agent r; gain rows 0..2D-1 are
     //      regs 0..3 of lane r and (D = 3) regs 0,1 of lane r + 32)
@@ -580,82 +655,95 @@ __global__ __launch_bounds__(NB_WAVES * 64, 1) void ctrl_node_bwd_kernel(CtrlNod
       const float hi4 = shfl_xor32(d4r[4 + q]);
       d4[q] = (h == 0) ? d4r[q] : hi4;
     }
-    const h16x16 d4b = to_h16x16(d4);
+    const Pk d4b = to_pk(d4);
     // Backward chain interleaved with the WG-shared weight-gradient stages so that each
-    // activation dies right after its last use (register pressure).
+    // activation dies right after its last use (register pressure). A stage runs in NB_NT
+    // turns: the waves of a turn store their rows, every wave contracts them.
     // ---- dY3 = W4^T dY4 (K = 32) . relu'(Y3)
-    h16x16 d3b[2];
+    Pk d3b[2];
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt) {
       f32x16 c = zero16();
       static_for<2>([&](auto kk_) {
         constexpr int kk = decltype(kk_)::value;
-        c = mfma(wrmT_acc(W4 + opaque_zero(), NS4, 32 * mt, kk, lane), bacc_frag<kk & 1>(d4b), c);
+        c = mma(wrmT_acc_fr(W4 + opaque_zero(), NS4, 32 * mt, kk, lane, LO), pk_fr<kk & 1>(d4b), c);
       });
-d3b[mt] = to_h16x16(c);
-      mask_by_nonzero(d3b[mt], Y3b[mt]);
+      d3b[mt] = to_pk(c);
+      mask_pk(d3b[mt], Y3b[mt]);
     }
-    {   // S4: dWn4pad (32x64) += dY4 . Y3^T ; nb4
+#pragma unroll 1
+    for (int turn = 0; turn < NB_NT; ++turn) {   // S4: dWn4pad (32x64) += dY4 . Y3^T ; nb4
       h16* imA = stg;
-      h16* imB = stg + NB_CH * 40;
-      store_tile(imA, 40, erow, 0, d4b, h);
+      h16* imB = stg + NB_RT * 40;
+      if (NB_NT == 1 || myturn == turn) {
+        store_pk(imA, 40, trow, 0, d4b, h, NB_PL);
 #pragma unroll
-      for (int mt = 0; mt < 2; ++mt) store_tile(imB, 72, erow, 32 * mt, Y3b[mt], h);
+        for (int mt = 0; mt < 2; ++mt) store_pk(imB, 72, trow, 32 * mt, Y3b[mt], h, NB_PL);
+      }
       __syncthreads();
-      if (wave < 2) bs4 += stage_mma<NB_CH / 16>(imA, 40, imB, 72, 0, wave, lane, acc4, 0, wave == 0 ? NB_CH / 16 : 0);
+      if (wave < 2)
+        bs4 += stage_mma_fr<NB_KST>(imA, 40, NB_PL, imB, 72, NB_PL, 0, wave, lane, acc4, 0, wave == 0 ? NB_KST : 0);
       __syncthreads();
     }
     // ---- dY2 = W3^T dY3 . relu'(Y2)
-    h16x16 d2b[4];
+    Pk d2b[4];
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt) {
       f32x16 c = zero16();
       static_for<4>([&](auto kk_) {
         constexpr int kk = decltype(kk_)::value;
-        c = mfma(wrmT_acc(W3 + opaque_zero(), NS3, 32 * mt, kk, lane), bacc_frag<kk & 1>(d3b[kk >> 1]), c);
+        c = mma(wrmT_acc_fr(W3 + opaque_zero(), NS3, 32 * mt, kk, lane, LO), pk_fr<kk & 1>(d3b[kk >> 1]), c);
       });
-d2b[mt] = to_h16x16(c);
-      mask_by_nonzero(d2b[mt], Y2b[mt]);
+      d2b[mt] = to_pk(c);
+      mask_pk(d2b[mt], Y2b[mt]);
     }
-    {   // S3: dWn3 (64x128) += dY3 . Y2^T ; nb3
+#pragma unroll 1
+    for (int turn = 0; turn < NB_NT; ++turn) {   // S3: dWn3 (64x128) += dY3 . Y2^T ; nb3
       h16* imA = stg;
-      h16* imB = stg + NB_CH * 72;
+      h16* imB = stg + NB_RT * 72;
+      if (NB_NT == 1 || myturn == turn) {
 #pragma unroll
-      for (int mt = 0; mt < 2; ++mt) store_tile(imA, 72, erow, 32 * mt, d3b[mt], h);
+        for (int mt = 0; mt < 2; ++mt) store_pk(imA, 72, trow, 32 * mt, d3b[mt], h, NB_PL);
 #pragma unroll
-      for (int mt = 0; mt < 4; ++mt) store_tile(imB, 136, erow, 32 * mt, Y2b[mt], h);
+        for (int mt = 0; mt < 4; ++mt) store_pk(imB, 136, trow, 32 * mt, Y2b[mt], h, NB_PL);
+      }
       __syncthreads();
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         const int t = wave + 4 * u;
-        bs3[u] += stage_mma<NB_CH / 16>(imA, 72, imB, 136, t / 4, t % 4, lane, acc3[u], 0, t % 4 == 0 ? NB_CH / 16 : 0);
+        bs3[u] += stage_mma_fr<NB_KST>(imA, 72, NB_PL, imB, 136, NB_PL, t / 4, t % 4, lane, acc3[u], 0,
+                                       t % 4 == 0 ? NB_KST : 0);
       }
       __syncthreads();
     }
     // ---- dY1 = W2^T dY2 . relu'(Y1)
-    h16x16 d1b[2];
+    Pk d1b[2];
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt) {
       f32x16 c = zero16();
       static_for<8>([&](auto kk_) {
         constexpr int kk = decltype(kk_)::value;
-        c = mfma(wrmT_acc(W2 + opaque_zero(), NS2, 32 * mt, kk, lane), bacc_frag<kk & 1>(d2b[kk >> 1]), c);
+        c = mma(wrmT_acc_fr(W2 + opaque_zero(), NS2, 32 * mt, kk, lane, LO), pk_fr<kk & 1>(d2b[kk >> 1]), c);
       });
-d1b[mt] = to_h16x16(c);
-      mask_by_nonzero(d1b[mt], Y1b[mt]);
+      d1b[mt] = to_pk(c);
+      mask_pk(d1b[mt], Y1b[mt]);
     }
-    {   // S2: dWn2 (128x64) += dY2 . Y1^T ; nb2
+#pragma unroll 1
+    for (int turn = 0; turn < NB_NT; ++turn) {   // S2: dWn2 (128x64) += dY2 . Y1^T ; nb2
       h16* imA = stg;
-      h16* imB = stg + NB_CH * 136;
+      h16* imB = stg + NB_RT * 136;
+      if (NB_NT == 1 || myturn == turn) {
 #pragma unroll
-      for (int mt = 0; mt < 4; ++mt) store_tile(imA, 136, erow, 32 * mt, d2b[mt], h);
+        for (int mt = 0; mt < 4; ++mt) store_pk(imA, 136, trow, 32 * mt, d2b[mt], h, NB_PL);
 #pragma unroll
-      for (int mt = 0; mt < 2; ++mt) store_tile(imB, 72, erow, 32 * mt, Y1b[mt], h);
+        for (int mt = 0; mt < 2; ++mt) store_pk(imB, 72, trow, 32 * mt, Y1b[mt], h, NB_PL);
+      }
       __syncthreads();
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         const int t = wave + 4 * u;
-        bs2[u] += stage_mma<NB_CH / 16>(imA, 136, imB, 72, t / 2, t % 2, lane, acc2[u], 0, t % 2 == 0 ? NB_CH / 16 : 0);
+        bs2[u] += stage_mma_fr<NB_KST>(imA, 136, NB_PL, imB, 72, NB_PL, t / 2, t % 2, lane, acc2[u], 0,
+                                       t % 2 == 0 ? NB_KST : 0);
       }
       __syncthreads();
     }
@@ -665,16 +753,21 @@ d1b[mt] = to_h16x16(c);
       f32x16 c = zero16();
       static_for<4>([&](auto kk_) {
         constexpr int kk = decltype(kk_)::value;
-        c = mfma(wrmT_acc(W1 + opaque_zero(), NS1, 32 * mt, kk, lane), bacc_frag<kk & 1>(d1b[kk >> 1]), c);
+        c = mma(wrmT_acc_fr(W1 + opaque_zero(), NS1, 32 * mt, kk, lane, LO), pk_fr<kk & 1>(d1b[kk >> 1]), c);
       });
       if (mt < 4) {
         if (ok) {
-          h16* drow = a.dP + (long)b * a.dp_env + (long)i * 128 + 32 * mt;
+          h16* drow = a.dP + (long)b * a.dp_env + (long)i * PROW + 32 * mt;
 #pragma unroll
           for (int g = 0; g < 4; ++g) {
-            h16x4 v;
-            v[0] = (h16)c[4 * g]; v[1] = (h16)c[4 * g + 1]; v[2] = (h16)c[4 * g + 2]; v[3] = (h16)c[4 * g + 3];
+            h16x4 v, vl_;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              v[e] = (h16)c[4 * g + e];
+              if constexpr (X3) vl_[e] = (h16)(c[4 * g + e] - (float)v[e]);
+            }
             *reinterpret_cast<h16x4*>(drow + 8 * g + 4 * h) = v;
+            if constexpr (X3) *reinterpret_cast<h16x4*>(drow + 128 + 8 * g + 4 * h) = vl_;
           }
         }
       } else {
@@ -687,28 +780,35 @@ d1b[mt] = to_h16x16(c);
         }
       }
     }
-    {   // S1: dWn1f (64x160) += dY1 . P^T  (P re-read from the pooled rows: L2-hot)
+#pragma unroll 1
+    for (int turn = 0; turn < NB_NT; ++turn) {   // S1: dWn1f (64x160) += dY1 . P^T (P re-read: L2-hot)
       h16* imA = stg;
-      h16* imB = stg + NB_CH * 72;
+      h16* imB = stg + NB_RT * 72;
+      if (NB_NT == 1 || myturn == turn) {
 #pragma unroll
-      for (int mt = 0; mt < 2; ++mt) store_tile(imA, 72, erow, 32 * mt, d1b[mt], h);
-      const h16x8 sf = node_state_frag<D>(ex, sv, ok, h);
-      const h16* prow = a.pooled + (long)b * a.p_env + (long)i * 128;
-      h16x8 zz;
+        for (int mt = 0; mt < 2; ++mt) store_pk(imA, 72, trow, 32 * mt, d1b[mt], h, NB_PL);
+        const h16* prow = a.pooled + (long)b * a.p_env + (long)i * PROW;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) zz[j] = z;
-#pragma unroll
-      for (int kk = 0; kk < 8; ++kk) {
-        const h16x8 pv = ok ? *reinterpret_cast<const h16x8*>(prow + 16 * kk + 8 * h) : zz;
-        *reinterpret_cast<h16x8*>(imB + erow * NS1 + 16 * kk + 8 * h) = pv;
+        for (int kk = 0; kk < 8; ++kk) {
+          const h16x8 pv = ok ? *reinterpret_cast<const h16x8*>(prow + 16 * kk + 8 * h) : zz;
+          *reinterpret_cast<h16x8*>(imB + trow * NS1 + 16 * kk + 8 * h) = pv;
+          if constexpr (X3) {
+            const h16x8 pl = ok ? *reinterpret_cast<const h16x8*>(prow + 128 + 16 * kk + 8 * h) : zz;
+            *reinterpret_cast<h16x8*>(imB + NB_PL + trow * NS1 + 16 * kk + 8 * h) = pl;
+          }
+        }
+        *reinterpret_cast<h16x8*>(imB + trow * NS1 + 128 + 8 * h) = sfr;
+        *reinterpret_cast<h16x8*>(imB + trow * NS1 + 144 + 8 * h) = zz;
+        if constexpr (X3) {      // the state fragment is exact: zero lo plane
+          *reinterpret_cast<h16x8*>(imB + NB_PL + trow * NS1 + 128 + 8 * h) = zz;
+          *reinterpret_cast<h16x8*>(imB + NB_PL + trow * NS1 + 144 + 8 * h) = zz;
+        }
       }
-      *reinterpret_cast<h16x8*>(imB + erow * NS1 + 128 + 8 * h) = sf;
-      *reinterpret_cast<h16x8*>(imB + erow * NS1 + 144 + 8 * h) = zz;
       __syncthreads();
 #pragma unroll
       for (int u = 0; u < 3; ++u) {
         const int t = wave + 4 * u;
-        if (u < n1) stage_mma<NB_CH / 16>(imA, 72, imB, NS1, t / 5, t % 5, lane, acc1[u]);
+        if (u < n1) stage_mma_fr<NB_KST>(imA, 72, NB_PL, imB, NS1, NB_PL, t / 5, t % 5, lane, acc1[u]);
       }
       __syncthreads();
     }
@@ -775,17 +875,18 @@ constexpr int EB_CH = EB_WAVES * 32;     // agents per chunk (each round: EB_CH 
 constexpr int EB_TA = 8 / EB_WAVES;      // owned dW2 tiles per wave
 constexpr int EP_W2 = 0, EP_B2 = 8192, EP_W1 = 8320;
 constexpr int CTRL_EDGE_PARTIAL = 10368;
-constexpr size_t EB_STAGE = (size_t)(128 + 64) * EB_CH * 2;
+constexpr int EB_PL = (128 + 64) * EB_CH;             // elements per stage plane (x3: lo plane at +EB_PL)
+constexpr size_t EB_STAGE = (size_t)(X3 ? 2 : 1) * EB_PL * 2;
 
-size_t ctrl_edge_bwd_lds() { return (size_t)22 * FRAG_BYTES + EB_STAGE; }
+size_t ctrl_edge_bwd_lds() { return (size_t)22 * FRAG_SZ + EB_STAGE; }
 
 template <int D>
-__global__ __launch_bounds__(EB_WAVES * 64, EB_WAVES == 4 ? 2 : 1) void ctrl_edge_bwd_kernel(CtrlEdgeBwdArgs a) {
+__global__ __launch_bounds__(EB_WAVES * 64, (EB_WAVES == 4 && !X3) ? 2 : 1) void ctrl_edge_bwd_kernel(CtrlEdgeBwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   h16* wf = reinterpret_cast<h16*>(smem);                 // ew1f (2) | ew2tn (16) | ew1ft (4)
-  h16* stg = reinterpret_cast<h16*>(smem + 22 * FRAG_BYTES);
-  block_copy16(wf, a.wpack + (size_t)a.f_ew1f * 512, 2 * FRAG_BYTES);
-  block_copy16(wf + 2 * 512, a.wpack + (size_t)a.f_ew2tn * 512, 20 * FRAG_BYTES);
+  h16* stg = reinterpret_cast<h16*>(smem + 22 * FRAG_SZ);
+  block_copy16(wf, a.wpack + (size_t)a.f_ew1f * FRAG_ELEMS, 2 * FRAG_SZ);
+  block_copy16(wf + 2 * FRAG_ELEMS, a.wpack + (size_t)a.f_ew2tn * FRAG_ELEMS, 20 * FRAG_SZ);
   __syncthreads();
   const int wave = threadIdx.x / WAVE, lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
   const int N = a.N, K = a.K;
@@ -819,25 +920,27 @@ __global__ __launch_bounds__(EB_WAVES * 64, EB_WAVES == 4 ? 2 : 1) void ctrl_edg
     }
     // argmax slots / dL/dpooled of the tile's two agents (lane (r, h): agent 2q+h, features
     // 4r..4r+3): loaded one tile ahead, like the edge gathers
-    auto pool_load = [&](int q, unsigned& am4, h16x4& dp4) {
+    auto pool_load = [&](int q, unsigned& am4, h16x4& dp4, h16x4& dl4) {
       const int ag = g0 + 2 * q + h;
       am4 = 0xFFFFFFFFu;
       if (q < 16 && ag < total) {
         const int bb = ag / N, ii = ag - bb * N;
         am4 = *reinterpret_cast<const unsigned*>(a.argmax + bb * (int)a.am_env + ii * 128 + 4 * r);
-        dp4 = *reinterpret_cast<const h16x4*>(a.dP + bb * (int)a.dp_env + ii * 128 + 4 * r);
+        const h16* dpr = a.dP + bb * (int)a.dp_env + ii * PROW + 4 * r;
+        dp4 = *reinterpret_cast<const h16x4*>(dpr);
+        if constexpr (X3) dl4 = *reinterpret_cast<const h16x4*>(dpr + 128);
       }
     };
     unsigned am_n;
-    h16x4 dp_n;
-    pool_load(q0, am_n, dp_n);
+    h16x4 dp_n, dl_n;
+    pool_load(q0, am_n, dp_n, dl_n);
     for (int q = q0; q < q1; ++q) {
       const EdgeSt<D> cur = xs0;
       const unsigned am4 = am_n;
-      const h16x4 dp4 = dp_n;
+      const h16x4 dp4 = dp_n, dl4 = dl_n;
       ctrl_st_load<D>(a.S, a.s_env, xi1, xs0);
       ctrl_idx_load(a.idx, a.i_env, N, K, g0, q + 2, r, total, xi1);
-      pool_load(q + 1, am_n, dp_n);
+      pool_load(q + 1, am_n, dp_n, dl_n);
       const int slot = r & 15;
       const bool ok = cur.ok;
       const int ga = g0 + 2 * q + (r >> 4);
@@ -846,12 +949,12 @@ __global__ __launch_bounds__(EB_WAVES * 64, EB_WAVES == 4 ? 2 : 1) void ctrl_edg
       const float eye = (j == i) ? 1.f : 0.f;
       const h16x8 F = ctrl_edge_frag<D>(cur.rp, cur.rv, eye, ok, h);
       const h16* wt = wf + opaque_zero();
-      h16x16 H1b[2];
+      Pk H1b[2];
 #pragma unroll
       for (int mt = 0; mt < 2; ++mt) {
-        f32x16 c = mfma(frag_ld(wt, mt, lane), F, zero16());
+        f32x16 c = mma_bx(frag_fr(wt, mt, lane), F, zero16());
         relu_(c);
-        H1b[mt] = to_h16x16(c);
+        H1b[mt] = to_pk(c);
       }
       // max-pool backward as an LDS scatter into the S1 image (rows = this wave's 32 edges =
       // agents 2q, 2q+1 x 16 slots): zero the rows, then lane (r, h) routes dP[f] of agent 2q+h,
@@ -861,35 +964,41 @@ __global__ __launch_bounds__(EB_WAVES * 64, EB_WAVES == 4 ? 2 : 1) void ctrl_edg
       {
         const u32x4 zero4 = {0u, 0u, 0u, 0u};
 #pragma unroll
-        for (int c8 = 0; c8 < 8; ++c8)   // whole rows are zeroed (unit permutation irrelevant); 8
+        for (int c8 = 0; c8 < 8; ++c8) {   // whole rows are zeroed (unit permutation irrelevant); 8
           // consecutive lanes fill 128 contiguous bytes: conflict-free 16-byte stores
           *reinterpret_cast<u32x4*>(imS + wave * 32 * 128 + (c8 * 64 + lane) * 8) = zero4;
+          if constexpr (X3) *reinterpret_cast<u32x4*>(imS + EB_PL + wave * 32 * 128 + (c8 * 64 + lane) * 8) = zero4;
+        }
 #pragma unroll
         for (int jj = 0; jj < 4; ++jj) {               // (am4 = all 0xFF: agent out of range)
           const unsigned sl = (am4 >> (8 * jj)) & 0xFFu;
-          if (sl < 16u) imS[swz_off<128>(wave * 32 + 16 * h + (int)sl, 4 * r + jj)] = dp4[jj];
+          if (sl < 16u) {
+            const int o = swz_off<128>(wave * 32 + 16 * h + (int)sl, 4 * r + jj);
+            imS[o] = dp4[jj];
+            if constexpr (X3) imS[EB_PL + o] = dl4[jj];
+          }
         }
         lds_wave_sync();
       }
-      h16x8 dz[8];
+      Fr dz[8];
 #pragma unroll
-      for (int kk = 0; kk < 8; ++kk) dz[kk] = *reinterpret_cast<const h16x8*>(imS + swz_off<128>(erow, 16 * kk + 8 * h));
+      for (int kk = 0; kk < 8; ++kk) dz[kk] = row_fr(imS + swz_off<128>(erow, 16 * kk + 8 * h), EB_PL);
       // dH1 = W2^T dZ (natural k) . relu'(H1)
-      h16x16 d1b[2];
+      Pk d1b[2];
 #pragma unroll
       for (int mt = 0; mt < 2; ++mt) {
         f32x16 c = zero16();
 #pragma unroll
-        for (int kk = 0; kk < 8; ++kk) c = mfma(frag_ld(wt, 2 + mt * 8 + kk, lane), dz[kk], c);
-        d1b[mt] = to_h16x16(c);
-        mask_by_nonzero(d1b[mt], H1b[mt]);
+        for (int kk = 0; kk < 8; ++kk) c = mma(frag_fr(wt, 2 + mt * 8 + kk, lane), dz[kk], c);
+        d1b[mt] = to_pk(c);
+        mask_pk(d1b[mt], H1b[mt]);
       }
       // dF = W1^T dH1 -> rows dx dy dvx dvy (lanes h == 0, regs 0..3)
       {
         f32x16 c = zero16();
         static_for<4>([&](auto kk_) {
           constexpr int kk = decltype(kk_)::value;
-          c = mfma(frag_ld(wt, 18 + kk, lane), bacc_frag<kk & 1>(d1b[kk >> 1]), c);
+          c = mma(frag_fr(wt, 18 + kk, lane), pk_fr<kk & 1>(d1b[kk >> 1]), c);
         });
         float gr[8];
         acc_rows8(c, gr);                       // rows 0..2D-1 = dL/d(s_i - s_j)
@@ -914,14 +1023,14 @@ __global__ __launch_bounds__(EB_WAVES * 64, EB_WAVES == 4 ? 2 : 1) void ctrl_edg
         h16* imA = stg;
         h16* imB = stg + EB_CH * 128;
 #pragma unroll
-        for (int mt = 0; mt < 2; ++mt) store_tile_sw<64>(imB, erow, 32 * mt, H1b[mt], h);
+        for (int mt = 0; mt < 2; ++mt) store_pk_sw<64>(imB, erow, 32 * mt, H1b[mt], h, EB_PL);
         __syncthreads();
         constexpr int KS = EB_CH / 16;
 #pragma unroll
         for (int u = 0; u < EB_TA; ++u) {
           const int t = wave + EB_WAVES * u;
-          bs[u] += stage_mma_sw<KS, 128, 64>(imA, imB, t / 2, t % 2, lane, accW2[u], (KS / 2) * (wave & 1),
-                                             (KS / 2) * (wave & 1) + KS / 2);
+          bs[u] += stage_mma_sw_fr<KS, 128, 64>(imA, EB_PL, imB, EB_PL, t / 2, t % 2, lane, accW2[u],
+                                                (KS / 2) * (wave & 1), (KS / 2) * (wave & 1) + KS / 2);
         }
         __syncthreads();
       }
@@ -937,7 +1046,7 @@ __global__ __launch_bounds__(EB_WAVES * 64, EB_WAVES == 4 ? 2 : 1) void ctrl_edg
         h16* imA = stg + wave * 32 * 128;          // dH1, 32 rows x 64 (swizzled)
         h16* imB = imA + 32 * 64;                  // [F | 0], 32 rows x 32 (swizzled)
 #pragma unroll
-        for (int mt = 0; mt < 2; ++mt) store_tile_sw<64>(imA, r, 32 * mt, d1b[mt], h);
+        for (int mt = 0; mt < 2; ++mt) store_pk_sw<64>(imA, r, 32 * mt, d1b[mt], h, EB_PL);
         h16x8 zz;
 #pragma unroll
         for (int jj = 0; jj < 8; ++jj) zz[jj] = z;
@@ -945,7 +1054,7 @@ __global__ __launch_bounds__(EB_WAVES * 64, EB_WAVES == 4 ? 2 : 1) void ctrl_edg
         *reinterpret_cast<h16x8*>(imB + swz_off<32>(r, 16 + 8 * h)) = zz;
         lds_wave_sync();
 #pragma unroll
-        for (int mt = 0; mt < 2; ++mt) stage_mma_sw<2, 64, 32>(imA, imB, mt, 0, lane, accW1[mt]);
+        for (int mt = 0; mt < 2; ++mt) stage_mma_sw_fr<2, 64, 32, true>(imA, EB_PL, imB, 0, mt, 0, lane, accW1[mt]);
         lds_wave_sync();                           // reads done before the next scatter
       }
 #endif

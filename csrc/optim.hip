@@ -76,14 +76,17 @@ __global__ __launch_bounds__(256) void pack_gather_kernel(const float* src, int 
                                                           float* out32) {
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i < m16) {
-    const int k = idx16[i];
+    // bit 30 of an index selects the bf16 residual v - bf16(v) (the lo plane of the x3 split)
+    const int k0 = idx16[i];
+    const int k = k0 & 0x3FFFFFFF;
     const float v = k < n ? src[k] : (k == n ? 0.f : 1.f);
     unsigned short hbits;
     if (f16) {
       const _Float16 hv = (_Float16)v;
       hbits = __builtin_bit_cast(unsigned short, hv);
     } else {
-      const __bf16 bv = (__bf16)v;                     // round to nearest even
+      const __bf16 hi = (__bf16)v;                     // round to nearest even
+      const __bf16 bv = (k0 & 0x40000000) ? (__bf16)(v - (float)hi) : hi;
       hbits = __builtin_bit_cast(unsigned short, bv);
     }
     out16[i] = hbits;

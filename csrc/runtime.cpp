@@ -45,7 +45,7 @@ class RolloutDriver {
     auto U = [&](const char* k) { return c[k].cast<u64>(); };
     B_ = (int)I("B"); N_ = (int)I("N"); Nn_ = (int)I("Nn"); K_ = (int)I("K"); D_ = (int)I("D");
     W_ = D_ == 2 ? 4 : 8;
-    Tmax_ = (int)I("Tmax"); num_cu_ = (int)I("num_cu"); f16_ = (int)I("f16");
+    Tmax_ = (int)I("Tmax"); num_cu_ = (int)I("num_cu"); prec_ = (int)I("prec"); prow_ = prec_ == 2 ? 256 : 128;
     resort_ = (int)I("resort_every"); safety_ = (int)I("compute_safety"); overlap_ = (int)I("overlap_hfwd");
     hfwd_blocks_ = (int)I("hfwd_blocks");
     L_ = F("L");
@@ -193,10 +193,10 @@ class RolloutDriver {
     a.act_sum = P<float>(act_) + (long)t * B_; a.ac_env = 1;
     a.noise = nullptr; a.n_env = 0;
     a.dt = dt_; a.obs_r = obs_r_; a.sqrt3 = sqrt3_;
-    a.pooled = P<h16>(pooled_) + (long)t * B_ * N_ * 128; a.p_env = (long)N_ * 128;
+    a.pooled = P<h16>(pooled_) + (long)t * B_ * N_ * prow_; a.p_env = (long)N_ * prow_;
     a.argmax = P<uint8_t>(argmax_) + (long)t * B_ * N_ * 128; a.am_env = (long)N_ * 128;
     a.apw = apw_;
-    chk((f16_ ? mb_ctrl_fwd_f16 : mb_ctrl_fwd)(&a, num_cu_, st), "ctrl_fwd");
+    chk((prec_ == 2 ? mb_ctrl_fwd_x3 : prec_ == 1 ? mb_ctrl_fwd_f16 : mb_ctrl_fwd)(&a, num_cu_, st), "ctrl_fwd");
   }
 
   // CBF h of the main slots of step t, evaluations [t*BNK, (t+1)*BNK), on the side stream
@@ -212,10 +212,10 @@ class RolloutDriver {
     a.h_out = P<float>(hbuf_); a.mask_out = P<uint8_t>(hmask_);
     a.obs_r = obs_r_; a.dist_thr = dist_thr_; a.dist_eps = dist_eps_;
     a.u_begin = (unsigned)(t * bnk); a.u_end = (unsigned)((t + 1) * bnk);
-    chk((f16_ ? mb_cbf_hfwd_f16 : mb_cbf_hfwd)(&a, hfwd_blocks_, hs), "cbf_hfwd");
+    chk((prec_ == 2 ? mb_cbf_hfwd_x3 : prec_ == 1 ? mb_cbf_hfwd_f16 : mb_cbf_hfwd)(&a, hfwd_blocks_, hs), "cbf_hfwd");
   }
 
-  int B_, N_, Nn_, K_, D_, W_, Tmax_, num_cu_, f16_, resort_, safety_, overlap_, hfwd_blocks_, check_, apw_;
+  int B_, N_, Nn_, K_, D_, W_, Tmax_, num_cu_, prec_, prow_, resort_, safety_, overlap_, hfwd_blocks_, check_, apw_;
   float L_;
   u64 S_, G_, A_, idx_, dang_, cnt_, safe_, dist_, act_, pooled_, argmax_, perm_, host_dist_;
   u64 ctrl_w_, ctrl_v_, cbf_w_, cbf_rm_, cbf_v_, hbuf_, hmask_, src_, nev_;
@@ -241,7 +241,7 @@ class BpttDriver {
     auto U = [&](const char* k) { return c[k].cast<u64>(); };
     B_ = (int)I("B"); N_ = (int)I("N"); Nn_ = (int)I("Nn"); K_ = (int)I("K"); D_ = (int)I("D");
     R_ = D_ == 2 ? 1 : 2;
-    Tmax_ = (int)I("Tmax"); f16_ = (int)I("f16"); nb_node_ = (int)I("nb_node"); nb_edge_ = (int)I("nb_edge");
+    Tmax_ = (int)I("Tmax"); prec_ = (int)I("prec"); prow_ = prec_ == 2 ? 256 : 128; nb_node_ = (int)I("nb_node"); nb_edge_ = (int)I("nb_edge");
     qsplit_ = (int)I("qsplit");
     pooled_ = U("pooled"); S_ = U("S"); G_ = U("G"); A_ = U("A"); dS_ = U("dS"); Gb_ = U("Gb"); valid_ = U("valid");
     idx_ = U("idx"); argmax_ = U("argmax"); rptr_ = U("rptr"); redges_ = U("redges");
@@ -266,7 +266,7 @@ class BpttDriver {
       {
         mb::CtrlNodeBwdArgs a{};
         a.dim = D_;
-        a.pooled = P<const h16>(pooled_) + (long)t * BN * 128; a.p_env = (long)N_ * 128;
+        a.pooled = P<const h16>(pooled_) + (long)t * BN * prow_; a.p_env = (long)N_ * prow_;
         a.S = St; a.s_env = Nn_;
         a.G = P<const float>(G_); a.A = P<const float>(A_) + (long)t * BN * D_; a.a_env = N_;
         a.Gn = Gn; a.gn_env = N_;
@@ -275,8 +275,8 @@ class BpttDriver {
         a.wrm = P<const h16>(wrm_); a.o_w1 = o1_; a.o_w2 = o2_; a.o_w3 = o3_; a.o_w4 = o4_;
         a.wvec = P<const float>(wvec_); a.act_coef = act_coef; a.act_scale = P<const float>(act_scale_);
         a.dt = dt_; a.sqrt3 = sqrt3_;
-        a.dP = P<h16>(dP_); a.dp_env = (long)N_ * 128; a.ego = P<float4>(ego_); a.partial = P<float>(part_node_);
-        chk((f16_ ? mb_ctrl_node_bwd_f16 : mb_ctrl_node_bwd)(&a, nb_node_, st), "ctrl_node_bwd");
+        a.dP = P<h16>(dP_); a.dp_env = (long)N_ * prow_; a.ego = P<float4>(ego_); a.partial = P<float>(part_node_);
+        chk((prec_ == 2 ? mb_ctrl_node_bwd_x3 : prec_ == 1 ? mb_ctrl_node_bwd_f16 : mb_ctrl_node_bwd)(&a, nb_node_, st), "ctrl_node_bwd");
       }
       {
         mb::CtrlEdgeBwdArgs a{};
@@ -284,11 +284,11 @@ class BpttDriver {
         a.S = St; a.s_env = Nn_;
         a.idx = P<const int>(idx_) + (long)t * B_ * nk; a.i_env = nk;
         a.argmax = P<const uint8_t>(argmax_) + (long)t * BN * 128; a.am_env = (long)N_ * 128;
-        a.dP = P<const h16>(dP_); a.dp_env = (long)N_ * 128;
+        a.dP = P<const h16>(dP_); a.dp_env = (long)N_ * prow_;
         a.B = B_; a.N = N_; a.K = K_;
         a.wpack = P<const h16>(wpack_); a.f_ew1f = f_ew1f_; a.f_ew2tn = f_ew2tn_;
         a.dEc = P<float4>(dEc_); a.de_env = nk; a.partial = P<float>(part_edge_); a.qsplit = qsplit_;
-        chk((f16_ ? mb_ctrl_edge_bwd_f16 : mb_ctrl_edge_bwd)(&a, nb_edge_, st), "ctrl_edge_bwd");
+        chk((prec_ == 2 ? mb_ctrl_edge_bwd_x3 : prec_ == 1 ? mb_ctrl_edge_bwd_f16 : mb_ctrl_edge_bwd)(&a, nb_edge_, st), "ctrl_edge_bwd");
       }
       if (t > 0) {   // G_0 = dL/ds_0 is not needed (s_0 is sampled, not a function of the weights)
         mb::CombineArgs a{};
@@ -306,7 +306,7 @@ class BpttDriver {
   }
 
  private:
-  int B_, N_, Nn_, K_, D_, R_, Tmax_, f16_, nb_node_, nb_edge_, qsplit_;
+  int B_, N_, Nn_, K_, D_, R_, Tmax_, prec_, prow_, nb_node_, nb_edge_, qsplit_;
   u64 pooled_, S_, G_, A_, dS_, Gb_, valid_, idx_, argmax_, rptr_, redges_, wrm_, wvec_, act_scale_, dP_, ego_, dEc_;
   u64 part_node_, part_edge_, wpack_;
   int o1_, o2_, o3_, o4_, f_ew1f_, f_ew2tn_;

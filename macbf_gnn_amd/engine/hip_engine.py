@@ -69,8 +69,15 @@ class HipEngine:
         if self.K > C.MAX_TOP_K:
             raise ValueError(f"top_k <= {C.MAX_TOP_K} supported by the native kernels")
         self.Tmax = cfg.inner_loops
-        self.hdt = {"bf16": torch.bfloat16, "fp16": torch.float16}.get(cfg.dtype, torch.bfloat16)
-        self.pw = PackedWeights(trainer.fp, self.D, self.hdt)
+        # kernel precision (csrc/prec.h): bf16 / fp16 MFMA inputs, or "fp32" -- the reference
+        # precision, fp32-accurate 3-term split-bf16 kernels (x3)
+        mdt = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": torch.float32}.get(cfg.dtype)
+        if mdt is None:
+            raise ValueError(f"dtype must be bf16, fp16 or fp32 on the HIP path, got {cfg.dtype!r}")
+        self.pw = PackedWeights(trainer.fp, self.D, mdt)
+        self.prec = self.pw.prec
+        self.hdt = self.pw.dtype                 # packed / pooled element type (bf16 | fp16)
+        self.prow = L.pooled_row(self.prec)      # pooled / dL/dpooled row: [hi | lo] for fp32
         offs = {pn: o for (m, pn, shape, o, n) in trainer.fp.specs}
         self._alloc()
         # flat-gradient assembly: CSR (by parameter) over the concatenated reduced slabs
@@ -120,14 +127,14 @@ class HipEngine:
         self.safe = torch.zeros(T + 1, B, dtype=f32, device=dev)
         self.dist = torch.zeros(T, B, dtype=f32, device=dev)
         self.act = torch.zeros(T, B, dtype=f32, device=dev)
-        self.pooled = torch.zeros(T, B, N, 128, dtype=bf, device=dev)
+        self.pooled = torch.zeros(T, B, N, self.prow, dtype=bf, device=dev)
         self.argmax = torch.zeros(T, B, N, 128, dtype=u8, device=dev)
         self.dE = torch.zeros(2 * T * B * N * K * W, dtype=f32, device=dev)
         self.rptr = torch.zeros((T + G1) * B, Nn + 1, dtype=i32, device=dev)
         self.redges = torch.zeros((T + G1) * B, N * K, dtype=i32, device=dev)
         self.dS = torch.zeros(T + 1, B, N, W, dtype=f32, device=dev)
         self.Gb = torch.zeros(T + 1, B, N, W, dtype=f32, device=dev)
-        self.dP = torch.zeros(B, N, 128, dtype=bf, device=dev)
+        self.dP = torch.zeros(B, N, self.prow, dtype=bf, device=dev)
         self.ego = torch.zeros(B, N, W, dtype=f32, device=dev)
         self.dEc = torch.zeros(B, N, K, W, dtype=f32, device=dev)
         self.counts = torch.zeros(3, dtype=f32, device=dev)
@@ -204,7 +211,7 @@ class HipEngine:
                    "A": (self.A, torch.float32, (T, B, N, D)), "idx": (self.idx, torch.int32, (T + G1, B, N, K)),
                    "dang": (self.dang, torch.uint8, (T, B, N, K)), "cnt": (self.cnt, torch.float32, (T, B, 2)),
                    "safe": (self.safe, torch.float32, (T + 1, B)), "dist": (self.dist, torch.float32, (T, B)),
-                   "act": (self.act, torch.float32, (T, B)), "pooled": (self.pooled, self.hdt, (T, B, N, 128)),
+                   "act": (self.act, torch.float32, (T, B)), "pooled": (self.pooled, self.hdt, (T, B, N, self.prow)),
                    "argmax": (self.argmax, torch.uint8, (T, B, N, 128))}
             for name, (t, dt, shape) in exp.items():
                 native.check(t, dt, shape, name)
@@ -217,7 +224,7 @@ class HipEngine:
             BNK = B * N * K
             c = {k: native.ptr(v[0]) for k, v in exp.items()}
             c.update(dict(
-                B=B, N=N, Nn=Nn, K=K, D=D, Tmax=T, num_cu=native.num_cu(self.dev), f16=int(self.hdt == torch.float16),
+                B=B, N=N, Nn=Nn, K=K, D=D, Tmax=T, num_cu=native.num_cu(self.dev), prec=L.PREC_CODE[self.prec],
                 resort_every=int(self.resort_every), compute_safety=int(cfg.compute_safety), overlap_hfwd=int(overlap),
                 hfwd_blocks=native.cbf_hfwd_grid(BNK, self.dev), L=float(max(1.0, N / C.AGENT_DENSITY) ** (1.0 / D)),
                 perm=native.ptr(perm), host_dist=int(self.host_dist.data_ptr()),
@@ -234,7 +241,7 @@ class HipEngine:
                 dist_thr=float(C.DIST_MIN_THRES), dist_eps=float(C.CBF_DIST_EPS_COORD * D),
                 done_thr=float(C.DIST_MIN_CHECK),
                 fork_device_scope=int(os.environ.get("MACBF_FORK_DEVICE_SCOPE", "1"))))
-            if pw.ctrl_v.numel() < 352 or pw.ctrl_w.numel() < (c["f_node"] + 54) * 512:
+            if pw.ctrl_v.numel() < 352 or pw.ctrl_w.numel() < (c["f_node"] + 54) * 512 * (2 if pw.x3 else 1):
                 raise native.NativeError("packed controller weights too small")
             if overlap and (self.hbuf.numel() < 2 * T * BNK or self.src.numel() < 2 * T * BNK):
                 raise native.NativeError("CBF evaluation buffers too small")
@@ -280,7 +287,7 @@ class HipEngine:
                          * coin.to(torch.float32)).contiguous()
             native.ctrl_fwd(self.S[t], self.G, self.idx[t], pw.ctrl_w, pw.ctrl_off["ew1f"], pw.ctrl_off["nw1f"],
                             pw.ctrl_v, self.A[t], self.S[t + 1], self.dist[t], self.act[t], noise=noise,
-                            pooled=self.pooled[t], argmax=self.argmax[t])
+                            pooled=self.pooled[t], argmax=self.argmax[t], prec=self.prec)
             if early_stop:
                 # the per-env goal distances go to pinned host memory on a side stream (the
                 # blit stays off the compute queue's critical path)
@@ -330,7 +337,7 @@ class HipEngine:
         idx = self.idx[: t + 1]
         with torch.cuda.stream(self.hstream):
             native.cbf_hfwd(self.S, idx, idx, self.src, self.nev_host, pw.cbf_w, pw.cbf_off["w1f"], pw.cbf_rm,
-                            pw.cbf_v, self.hbuf, self.hmask, u_begin=t * BNK, u_end=(t + 1) * BNK)
+                            pw.cbf_v, self.hbuf, self.hmask, u_begin=t * BNK, u_end=(t + 1) * BNK, prec=self.prec)
 
     def _all_done(self, t):
         d = self.host_dist[: t + 1] / self.N < C.DIST_MIN_CHECK      # (t+1, B)
@@ -432,7 +439,7 @@ class HipEngine:
             hb, hm, dh = self.hbuf[: 2 * E], self.hmask[: 2 * E], self.dhbuf[: 2 * E]
             # the main slots [0, E) were evaluated during the rollout (overlap_hfwd): extras only
             native.cbf_hfwd(S, idx, idx if self.reuse else idx1, src, nev, pw.cbf_w, pw.cbf_off["w1f"],
-                            pw.cbf_rm, pw.cbf_v, hb, hm, u_begin=E if self.overlap_hfwd else 0)
+                            pw.cbf_rm, pw.cbf_v, hb, hm, u_begin=E if self.overlap_hfwd else 0, prec=self.prec)
             self._counts_ready(counts_work)
             native.cbf_dh(hb, hm, map1, src, nev, self.dang[:T], valid_u8, self.counts, dh, self.loss_part,
                           grad_scale=gs, blk_active=self.blk_active)
@@ -442,14 +449,14 @@ class HipEngine:
             nact = native.cbf_active(dh, nev, self.blk_active, act)
             native.cbf_bwd(S, idx, dh.view(2, T, B, N, K), pw.cbf_w, pw.cbf_off["w1f"], pw.cbf_rm, pw.cbf_v,
                            passes=2, dE=dE, partial=part_cbf, num_blocks=nbb, idx1=idx if self.reuse else idx1,
-                           src=src, nev=nev, act=act, nact=nact)
+                           src=src, nev=nev, act=act, nact=nact, prec=self.prec)
             native.reduce_rows(self.loss_part, self.loss_red)
         else:
             # ---- CBF: h, h', hinge losses, upstream grads and the full backward in ONE kernel
             self._counts_ready(counts_work)
             native.cbf_bwd(S, idx, None, pw.cbf_w, pw.cbf_off["w1f"], pw.cbf_rm, pw.cbf_v, passes=2, dE=dE,
                            partial=part_cbf, num_blocks=nbb, fused=True, dang=self.dang[:T], valid=valid_u8,
-                           counts=self.counts, idx1=idx1, grad_scale=gs)
+                           counts=self.counts, idx1=idx1, grad_scale=gs, prec=self.prec)
         cur = torch.cuda.current_stream(self.dev)
         cur.wait_event(csr_done)
         # no-BPTT: s_t is a detached input, only h'(s_{t+1}) gradients reach a_t
@@ -510,12 +517,12 @@ class HipEngine:
             pe = self._buf(self._part_cbf_nb, ("e", nb_e), native.CTRL_EDGE_PARTIAL)
             pn.zero_()
             pe.zero_()
-            native.ctrl_node_bwd(self.pooled[:T].view(TB, N, 128), self.S[:T].view(TB, Nn, W), Gr[:TB],
+            native.ctrl_node_bwd(self.pooled[:T].view(TB, N, self.prow), self.S[:T].view(TB, Nn, W), Gr[:TB],
                                  self.A[:T].view(TB, N, D), self.dS[1: T + 1].view(TB, N, W), valid_u8.view(TB),
                                  pw.ctrl_rm, pw.node_rm_off, pw.ctrl_v, gs, dP[:TB], None, pn, nb_n,
-                                 act_scale=self.act_scale)
+                                 act_scale=self.act_scale, prec=self.prec)
             native.ctrl_edge_bwd(self.S[:T].view(TB, Nn, W), self.idx[:T].view(TB, N, K), self.argmax[:T].view(TB, N, 128),
-                                 dP[:TB], pw.ctrl_w, pw.ctrl_off["ew1f"], pw.ctrl_off["ew2tn"], None, pe, nb_e)
+                                 dP[:TB], pw.ctrl_w, pw.ctrl_off["ew1f"], pw.ctrl_off["ew2tn"], None, pe, nb_e, prec=self.prec)
             self._nb_parts = (pn, pe)
         tm.mark("bptt")
         # ---- weight-gradient slabs -> flat grad
@@ -535,14 +542,14 @@ class HipEngine:
         if self._bdrv is None:
             B, N, Nn, K, D, W, T = self.B, self.N, self.Nn, self.K, self.D, self.W, self.Tmax
             G1 = 0 if self.reuse else 1
-            exp = {"pooled": (self.pooled, self.hdt, (T, B, N, 128)), "S": (self.S, torch.float32, (T + 1, B, Nn, W)),
+            exp = {"pooled": (self.pooled, self.hdt, (T, B, N, self.prow)), "S": (self.S, torch.float32, (T + 1, B, Nn, W)),
                    "G": (self.G, torch.float32, (B, N, D)), "A": (self.A, torch.float32, (T, B, N, D)),
                    "dS": (self.dS, torch.float32, (T + 1, B, N, W)), "Gb": (self.Gb, torch.float32, (T + 1, B, N, W)),
                    "valid": (self.valid_buf, torch.uint8, (T, B)), "idx": (self.idx, torch.int32, (T + G1, B, N, K)),
                    "argmax": (self.argmax, torch.uint8, (T, B, N, 128)),
                    "rptr": (self.rptr, torch.int32, ((T + G1) * B, Nn + 1)),
                    "redges": (self.redges, torch.int32, ((T + G1) * B, N * K)),
-                   "act_scale": (self.act_scale, torch.float32, (1,)), "dP": (self.dP, self.hdt, (B, N, 128)),
+                   "act_scale": (self.act_scale, torch.float32, (1,)), "dP": (self.dP, self.hdt, (B, N, self.prow)),
                    "ego": (self.ego, torch.float32, (B, N, W)), "dEc": (self.dEc, torch.float32, (B, N, K, W))}
             for name, (t, dt, shape) in exp.items():
                 native.check(t, dt, shape, name)
@@ -551,7 +558,7 @@ class HipEngine:
             pw = self.pw
             c = {k: native.ptr(v[0]) for k, v in exp.items()}
             c.update(dict(
-                B=B, N=N, Nn=Nn, K=K, D=D, Tmax=T, f16=int(self.hdt == torch.float16),
+                B=B, N=N, Nn=Nn, K=K, D=D, Tmax=T, prec=L.PREC_CODE[self.prec],
                 nb_node=int(self.nb_node), nb_edge=int(self.nb_edge),
                 qsplit=int(native.ctrl_edge_qsplit(B * N, self.dev)),
                 part_node=native.ptr(self.part_node), part_edge=native.ptr(self.part_edge),
@@ -571,9 +578,9 @@ class HipEngine:
             Gn = self.dS[T][sl] if t == T - 1 else self.Gb[t + 1][sl]   # G_T = dL/ds_T (direct terms only)
             native.ctrl_node_bwd(self.pooled[t][sl], self.S[t][sl], self.G[sl], self.A[t][sl], Gn, valid_u8[t][sl],
                                  pw.ctrl_rm, pw.node_rm_off, pw.ctrl_v, gs, self.dP[sl], self.ego[sl],
-                                 part_node, nbn, act_scale=self.act_scale)
+                                 part_node, nbn, act_scale=self.act_scale, prec=self.prec)
             native.ctrl_edge_bwd(self.S[t][sl], self.idx[t][sl], self.argmax[t][sl], self.dP[sl], pw.ctrl_w,
-                                 pw.ctrl_off["ew1f"], pw.ctrl_off["ew2tn"], self.dEc[sl], part_edge, nbe)
+                                 pw.ctrl_off["ew1f"], pw.ctrl_off["ew2tn"], self.dEc[sl], part_edge, nbe, prec=self.prec)
             if t > 0:      # G_0 = dL/ds_0 is not needed (s_0 is sampled, not a function of the weights)
                 native.node_combine(self.dS[t][sl], self.ego[sl], self.dEc[sl], rptr3[t][sl], redges3[t][sl], Gn,
                                     self.Gb[t][sl], K=K)
@@ -606,7 +613,7 @@ class HipEngine:
             self._nobptt = {
                 "grids": (nb_n, nb_e),
                 "G": torch.zeros(TBm, self.N, self.D, dtype=torch.float32, device=self.dev),
-                "dP": torch.zeros(TBm, self.N, 128, dtype=self.hdt, device=self.dev),
+                "dP": torch.zeros(TBm, self.N, self.prow, dtype=self.hdt, device=self.dev),
             }
         nb_n, nb_e = self._nobptt["grids"]
         return nb_n, nb_e, self._nobptt["G"], self._nobptt["dP"]

@@ -36,7 +36,7 @@ class _CBFFn(torch.autograd.Function):
         S = Sr.view(1, *Sr.shape)
         idx1 = idx.view(1, B, N, K)
         h = torch.empty(1, B, N, K, dtype=torch.float32, device=s.device)
-        native.cbf_fwd(S, idx1, w, mp.off["w1f"], v, two=False, h_out=h)
+        native.cbf_fwd(S, idx1, w, mp.off["w1f"], v, two=False, h_out=h, prec=mp.prec)
         ctx.mp = mp
         ctx.packed = (w, v, rm)
         ctx.save_for_backward(S, idx1)
@@ -55,7 +55,8 @@ class _CBFFn(torch.autograd.Function):
         dE = torch.empty(1, 1, B, N, K, W, dtype=torch.float32, device=dev)
         nb = native.cbf_bwd_grid(B * N * K, dev)
         part = torch.empty(nb, native.CBF_PARTIAL, dtype=torch.float32, device=dev)
-        native.cbf_bwd(S, idx1, dh, w, mp.off["w1f"], rm, v, passes=1, dE=dE, partial=part, num_blocks=nb)
+        native.cbf_bwd(S, idx1, dh, w, mp.off["w1f"], rm, v, passes=1, dE=dE, partial=part, num_blocks=nb,
+                       prec=mp.prec)
         gs = None
         if ctx.needs_input_grad[0]:
             rptr = torch.empty(B, Nn + 1, dtype=torch.int32, device=dev)

@@ -6,6 +6,10 @@ law), no Euler step. Backward: ``ctrl_node_bwd`` (node MLP + gain law; the upstr
 fed as the velocity adjoint of s_{t+1} = s_t + dt [v, a], i.e. G = (0, 0, dL/da / dt)),
 ``ctrl_edge_bwd`` (max-pool routing via argmax, edge MLP), ``node_combine`` (edge -> node,
 reverse CSR, no Euler term) and the slab reductions for the parameter gradients.
+
+Goals enter only through p - g (node-MLP input and the PD law), so dL/dg is minus the position
+part of the node-path adjoint ``ego`` (reference: autograd through ``controller.py:47,54-61``).
+Precision: the module's ``mfma_dtype`` (default torch.float32 = the fp32-accurate x3 kernels).
 """
 from __future__ import annotations
 
@@ -13,6 +17,7 @@ import torch
 
 from .. import config as C
 from . import graph, native
+from . import layout as L
 from .packing import module_pack
 
 
@@ -26,10 +31,10 @@ class _CtrlFn(torch.autograd.Function):
         S = graph.node_records(s, obs)                   # (B, Nn, W)
         G = g.detach().float().contiguous()
         A = torch.empty(B, N, D, dtype=torch.float32, device=dev)
-        pooled = torch.empty(B, N, 128, dtype=w.dtype, device=dev)
+        pooled = torch.empty(B, N, L.pooled_row(mp.prec), dtype=w.dtype, device=dev)
         am = torch.empty(B, N, 128, dtype=torch.uint8, device=dev)
         native.ctrl_fwd(S, G, idx, w, mp.off["ew1f"], mp.off["nw1f"], v, A, None, None, None,
-                        pooled=pooled, argmax=am)
+                        pooled=pooled, argmax=am, prec=mp.prec)
         ctx.mp = mp
         ctx.packed = (w, v, rm)
         ctx.save_for_backward(S, G, idx, A, pooled, am)
@@ -49,12 +54,15 @@ class _CtrlFn(torch.autograd.Function):
         # the controller kernels accumulate into their slabs (BPTT sums over steps): start at 0
         pn = torch.zeros(nbn, native.CTRL_NODE_PARTIAL, dtype=torch.float32, device=dev)
         pe = torch.zeros(nbe, native.CTRL_EDGE_PARTIAL, dtype=torch.float32, device=dev)
-        dP = torch.empty(B, N, 128, dtype=w.dtype, device=dev)
+        dP = torch.empty(B, N, L.pooled_row(mp.prec), dtype=w.dtype, device=dev)
         ego = torch.empty(B, N, W, dtype=torch.float32, device=dev)
         dEc = torch.empty(B, N, K, W, dtype=torch.float32, device=dev)
-        native.ctrl_node_bwd(pooled, S, G, A, Gn, None, rm, mp.rm_off, v, 0.0, dP, ego, pn, nbn)
-        native.ctrl_edge_bwd(S, idx, am, dP, w, mp.off["ew1f"], mp.off["ew2tn"], dEc, pe, nbe)
+        native.ctrl_node_bwd(pooled, S, G, A, Gn, None, rm, mp.rm_off, v, 0.0, dP, ego, pn, nbn, prec=mp.prec)
+        native.ctrl_edge_bwd(S, idx, am, dP, w, mp.off["ew1f"], mp.off["ew2tn"], dEc, pe, nbe, prec=mp.prec)
         gs = gg = None
+        if ctx.needs_input_grad[1]:
+            # goals only enter through p - g: dL/dg = -dL/d(p - g) of the node path
+            gg = -native.from_records(ego)[..., :D]
         if ctx.needs_input_grad[0]:
             rptr = torch.empty(B, Nn + 1, dtype=torch.int32, device=dev)
             red_e = torch.empty(B, N * K, dtype=torch.int32, device=dev)
@@ -72,8 +80,8 @@ class _CtrlFn(torch.autograd.Function):
 
 def controller_apply(module, s: torch.Tensor, g: torch.Tensor, idx: torch.Tensor | None,
                      top_k: int = C.TOP_K, obstacles: torch.Tensor | None = None) -> torch.Tensor:
-    """s (..., N, 2D), g (..., N, D) on the HIP device -> a (..., N, D); differentiable in s and in
-    the module's parameters (goals and obstacles are treated as constants)."""
+    """s (..., N, 2D), g (..., N, D) on the HIP device -> a (..., N, D); differentiable in s, g and
+    the module's parameters (obstacles are constants)."""
     lead = s.shape[:-2]
     N, SD = s.shape[-2:]
     D = SD // 2

@@ -499,3 +499,35 @@ def cbf_rm(fp_offsets, dim: int = 2) -> RMPacker:
     p.add("w2", _mat(W2, 128, 64), 128, 64, CBF_RM_STRIDES["w2"])
     p.add("w3", _mat(W3, 64, 128), 64, 128, CBF_RM_STRIDES["w3"])
     return p
+
+
+# ------------------------------------------------------------------ operand precision (csrc/prec.h)
+# "bf16" / "fp16": one 16-bit MFMA per product. "fp32": the fp32-accurate 3-term split (x3 kernels):
+# every packed weight carries a bf16 residual plane; the pack gathers flag residual entries with
+# LO_FLAG (pack_gather computes bf16(v - bf16(v)) for them).
+PRECISIONS = ("bf16", "fp16", "fp32")
+PREC_CODE = {"bf16": 0, "fp16": 1, "fp32": 2}
+LO_FLAG = 1 << 30
+
+
+def check_prec(prec: str) -> str:
+    if prec not in PREC_CODE:
+        raise ValueError(f"precision must be one of {PRECISIONS}, got {prec!r}")
+    return prec
+
+
+def pooled_row(prec: str) -> int:
+    """h16 elements per pooled / dL/dpooled row: [hi 128 | lo 128] for the x3 kernels."""
+    return 256 if prec == "fp32" else 128
+
+
+def x3_frags(index: np.ndarray) -> np.ndarray:
+    """Resolved fragment index (nfrag * 512,) -> per fragment [hi 512 | lo 512] (x3 packing)."""
+    a = np.asarray(index, dtype=np.int64).reshape(-1, LANES * FRAG)
+    return np.stack([a, a | LO_FLAG], 1).reshape(-1)
+
+
+def x3_planes(index: np.ndarray) -> np.ndarray:
+    """Resolved row-major image index -> [hi plane | lo plane] (x3 packing)."""
+    a = np.asarray(index, dtype=np.int64).reshape(-1)
+    return np.concatenate([a, a | LO_FLAG])

@@ -15,6 +15,7 @@ import os
 import torch
 
 from .. import config as C
+from . import layout as L
 
 _LIB = None
 
@@ -83,12 +84,27 @@ def check(t, dtype, shape=None, name="tensor"):
 HALF_DTYPES = (torch.bfloat16, torch.float16)
 
 
-def _half(t, name):
-    """16-bit MFMA element type of a packed-weight / activation tensor -> the kernel variant
-    flag (0: bf16, 1: fp16; csrc/prec.h)."""
+def _half(t, name, prec=None):
+    """Kernel precision variant of a packed-weight tensor (csrc/prec.h): 0 bf16, 1 fp16, 2 the
+    fp32-accurate 3-term split ("fp32", bf16 hi/lo planes). prec=None: from the dtype."""
     if t is None or t.dtype not in HALF_DTYPES:
         raise NativeError(f"{name} must be bf16 or fp16")
-    return int(t.dtype == torch.float16)
+    if prec is None:
+        return int(t.dtype == torch.float16)
+    if prec not in L.PREC_CODE:
+        raise NativeError(f"unknown precision {prec!r}")
+    code = L.PREC_CODE[prec]
+    if (code == 1) != (t.dtype == torch.float16):
+        raise NativeError(f"{name}: dtype {t.dtype} does not match precision {prec}")
+    return code
+
+
+def _planes(code):
+    return 2 if code == 2 else 1
+
+
+def _prow(code):
+    return 256 if code == 2 else 128
 
 
 def _same_half(t, ref, name):
@@ -240,10 +256,11 @@ def _records(t, name, lead, W, min_rows=None):
         raise NativeError(f"{name}: expected {lead}x{W} float32 records, got {tuple(t.shape)} {t.stride()}")
 
 
-def ctrl_fwd(S, G, idx, wpack, f_edge, f_node, wvec, A, Sn, dist_sum, act_sum, noise=None, pooled=None, argmax=None):
+def ctrl_fwd(S, G, idx, wpack, f_edge, f_node, wvec, A, Sn, dist_sum, act_sum, noise=None, pooled=None, argmax=None,
+             prec=None):
     """Fused controller step on per-step views: S/Sn (B,Nn,W) node records (agents first),
-    G (B,N,D), idx (B,N,K), A (B,N,D), dist_sum/act_sum (B,), pooled (B,N,128) bf16,
-    argmax (B,N,128) uint8."""
+    G (B,N,D), idx (B,N,K), A (B,N,D), dist_sum/act_sum (B,), pooled (B,N,128) bf16
+    ((B,N,256) [hi | lo] rows for prec="fp32", required there), argmax (B,N,128) uint8."""
     B, N, K = idx.shape
     D = dim_of(S)
     W = rec_width(D)
@@ -255,17 +272,19 @@ def ctrl_fwd(S, G, idx, wpack, f_edge, f_node, wvec, A, Sn, dist_sum, act_sum, n
     check(G, torch.float32, (B, N, D), "G")
     if idx.dtype != torch.int32 or idx.stride(2) != 1 or idx.stride(1) != K:
         raise NativeError("idx must be int32 (B,N,K)")
-    f16 = _half(wpack, "wpack")
+    f16 = _half(wpack, "wpack", prec)
     check(wpack, wpack.dtype, None, "wpack")
     check(wvec, torch.float32, None, "wvec")
-    if wvec.numel() < 352 or wpack.numel() < (f_node + 54) * 512:
+    if wvec.numel() < 352 or wpack.numel() < (f_node + 54) * 512 * _planes(f16):
         raise NativeError("packed controller weights too small")
+    if f16 == 2 and pooled is None:
+        raise NativeError("the fp32 (x3) controller step needs the pooled buffer")
     for t, n in ((dist_sum, "dist_sum"), (act_sum, "act_sum")):
         if t is not None and (t.dtype != torch.float32 or tuple(t.shape) != (B,)):
             raise NativeError(f"{n} must be float32 (B,)")
     _rows(noise, D, "noise", (B, N))
     if pooled is not None:
-        _rows(pooled, 128, "pooled", (B, N))
+        _rows(pooled, _prow(f16), "pooled", (B, N))
         _same_half(pooled, wpack, "pooled")
     if argmax is not None:
         _rows(argmax, 128, "argmax", (B, N))
@@ -308,6 +327,7 @@ CBF_PARTIAL = 18704
 CBF_P_LOSS = 18692          # 10 loss partial sums in the CBF slab (fused mode)
 CTRL_NODE_PARTIAL = 28896
 CTRL_EDGE_PARTIAL = 10368
+NODE_RM_ELEMS = 64 * 168 + 128 * 68 + 64 * 132 + 32 * 68     # csrc/ctrl.hip row-major node images
 
 
 def cbf_fwd_grid(E: int, device) -> int:
@@ -325,7 +345,7 @@ def _time_major_S(S, T, B, N, need):
 
 
 def cbf_fwd(S, idx, wpack, f_fwd, wvec, *, dang=None, valid=None, two=True, h_out=None, hn_out=None,
-            dh_out=None, counts=None, partial=None, num_blocks=None):
+            dh_out=None, counts=None, partial=None, num_blocks=None, prec=None):
     """Time-major: S (>=T+two, B, N, 4); idx/dang/h (T, B, N, K); valid (T, B); dh (2, T, B, N, K)."""
     T, B, N, K = idx.shape
     check(idx, torch.int32, None, "idx")
@@ -338,9 +358,11 @@ def cbf_fwd(S, idx, wpack, f_fwd, wvec, *, dang=None, valid=None, two=True, h_ou
     check(dh_out, torch.float32, (2, T, B, N, K), "dh_out")
     if dh_out is not None:
         check(counts, torch.float32, None, "counts")
-    f16 = _half(wpack, "wpack")
+    f16 = _half(wpack, "wpack", prec)
     check(wpack, wpack.dtype, None, "wpack")
     check(wvec, torch.float32, None, "wvec")
+    if wpack.numel() < (f_fwd + 34) * 512 * _planes(f16):
+        raise NativeError("packed CBF weights too small")
     nb = num_blocks or cbf_fwd_grid(E, S.device)
     check(partial, torch.float32, (nb, 10), "partial")
     rc = lib().cbf_fwd(ptr(S), S.stride(1) // W, S.stride(0) // W, ptr(idx), ptr(dang), ptr(valid),
@@ -394,7 +416,7 @@ def cbf_hfwd_grid(EV: int, device) -> int:
 
 
 def cbf_hfwd(S, idx, idx1, src, nev, wpack, f_fwd, wrm, wvec, h_out, mask_out, num_blocks=None,
-             u_begin=0, u_end=None):
+             u_begin=0, u_end=None, prec=None):
     """h (masked) and the radius mask of every evaluation u_begin <= u < (u_end or nev) of the
     deduplicated list: S (>= T+1, B, N, W); idx / idx1 (T, B, N, K) (idx1 = idx for
     reuse_nbr_idx); src, h_out, mask_out (>= 2E,). Weights: w1f fragments at f_fwd of wpack + the
@@ -417,10 +439,12 @@ def cbf_hfwd(S, idx, idx1, src, nev, wpack, f_fwd, wrm, wvec, h_out, mask_out, n
     check(nev, torch.int32, (1,), "nev")
     check(h_out, torch.float32, None, "h_out")
     check(mask_out, torch.uint8, None, "mask_out")
-    f16 = _half(wpack, "wpack")
+    f16 = _half(wpack, "wpack", prec)
     check(wpack, wpack.dtype, None, "wpack")
-    check(wrm, wpack.dtype, (128 * 68 + 64 * 148,), "wrm")
+    check(wrm, wpack.dtype, (_planes(f16) * (128 * 68 + 64 * 148),), "wrm")
     check(wvec, torch.float32, None, "wvec")
+    if wpack.numel() < (f_fwd + 2) * 512 * _planes(f16):
+        raise NativeError("packed CBF weights too small")
     if u_end is not None and u_end == u_begin:
         return 0
     nb = num_blocks or cbf_hfwd_grid((u_end if u_end is not None else 2 * E) - u_begin, S.device)
@@ -486,7 +510,7 @@ def cbf_bwd_grid(EV: int, device) -> int:
 
 def cbf_bwd(S, idx, dh, wpack, f_bwd, wrm, wvec, *, passes=2, dE=None, partial=None, num_blocks=None,
             fused=False, dang=None, valid=None, counts=None, idx1=None, grad_scale=1.0, src=None, nev=None,
-            act=None, nact=None):
+            act=None, nact=None, prec=None):
     """dh (passes, T, B, N, K) -> dE (passes, T, B, N, K, 4), per-WG dW slabs (nb, CBF_PARTIAL).
 
     fused=True (training, passes=2): dh is not read; the kernel evaluates h and h' of every
@@ -521,12 +545,12 @@ def cbf_bwd(S, idx, dh, wpack, f_bwd, wrm, wvec, *, passes=2, dE=None, partial=N
             raise NativeError("the active list needs the deduplicated evaluation list")
         check(act, torch.int32, (2 * B * T * N * K,), "act")
         check(nact, torch.int32, (1,), "nact")
-    f16 = _half(wpack, "wpack")
+    f16 = _half(wpack, "wpack", prec)
     check(wpack, wpack.dtype, None, "wpack")
     check(wvec, torch.float32, None, "wvec")
-    if wpack.numel() < (f_bwd + 70) * 512:
+    if wpack.numel() < (f_bwd + 70) * 512 * _planes(f16):
         raise NativeError("packed CBF weights too small")
-    check(wrm, wpack.dtype, (128 * 68 + 64 * 148,), "wrm")
+    check(wrm, wpack.dtype, (_planes(f16) * (128 * 68 + 64 * 148),), "wrm")
     if idx1 is not None:
         check(idx1, torch.int32, (T, B, N, K), "idx1")
     E = B * T * N * K
@@ -638,22 +662,24 @@ def ctrl_bwd_grids(total_agents: int, device):
 
 
 def ctrl_node_bwd(pooled, S, G, A, Gn, valid_t, wrm, offs, wvec, act_coef, dP, ego, partial, num_blocks,
-                  act_scale=None):
+                  act_scale=None, prec=None):
     """act_scale: optional 1-element device tensor; the action-loss coefficient is then
     act_coef * act_scale[0], read by the kernel (no host round trip)."""
     B, N = G.shape[:2]
     D = dim_of(S)
     W = rec_width(D)
-    _rows(pooled, 128, "pooled", (B, N))
+    f16 = _half(wrm, "wrm", prec)
+    _rows(pooled, _prow(f16), "pooled", (B, N))
     _records(S, "S", (B, N), W)
     check(G, torch.float32, (B, N, D), "G")
     _rows(A, D, "A", (B, N))
     _records(Gn, "Gn", (B, N), W)
     if valid_t is not None and (valid_t.dtype != torch.uint8 or tuple(valid_t.shape) != (B,)):
         raise NativeError("valid_t must be uint8 (B,)")
-    f16 = _half(wrm, "wrm")
     check(wrm, wrm.dtype, None, "wrm")
-    check(dP, wrm.dtype, (B, N, 128), "dP")
+    if wrm.numel() < _planes(f16) * NODE_RM_ELEMS:
+        raise NativeError("node weight images too small")
+    check(dP, wrm.dtype, (B, N, _prow(f16)), "dP")
     _same_half(pooled, wrm, "pooled")
     check(ego, torch.float32, (B, N, W), "ego")
     check(partial, torch.float32, (num_blocks, CTRL_NODE_PARTIAL), "partial")
@@ -667,7 +693,7 @@ def ctrl_node_bwd(pooled, S, G, A, Gn, valid_t, wrm, offs, wvec, act_coef, dP, e
     _ok(rc, "ctrl_node_bwd")
 
 
-def ctrl_edge_bwd(S, idx, argmax, dP, wpack, f_ew1f, f_ew2tn, dEc, partial, num_blocks):
+def ctrl_edge_bwd(S, idx, argmax, dP, wpack, f_ew1f, f_ew2tn, dEc, partial, num_blocks, prec=None):
     B, N, K = idx.shape
     D = dim_of(S)
     W = rec_width(D)
@@ -675,8 +701,10 @@ def ctrl_edge_bwd(S, idx, argmax, dP, wpack, f_ew1f, f_ew2tn, dEc, partial, num_
     if idx.dtype != torch.int32 or idx.stride(2) != 1 or idx.stride(1) != K:
         raise NativeError("idx must be int32 (B,N,K)")
     _rows(argmax, 128, "argmax", (B, N))
-    f16 = _half(wpack, "wpack")
-    check(dP, wpack.dtype, (B, N, 128), "dP")
+    f16 = _half(wpack, "wpack", prec)
+    check(dP, wpack.dtype, (B, N, _prow(f16)), "dP")
+    if wpack.numel() < (f_ew2tn + 20) * 512 * _planes(f16) or wpack.numel() < (f_ew1f + 2) * 512 * _planes(f16):
+        raise NativeError("packed controller weights too small")
     check(dEc, torch.float32, (B, N, K, W), "dEc")
     check(partial, torch.float32, (num_blocks, CTRL_EDGE_PARTIAL), "partial")
     rc = lib().ctrl_edge_bwd(ptr(S), S.stride(0) // W, ptr(idx), idx.stride(0), ptr(argmax), argmax.stride(0),

@@ -26,10 +26,26 @@ def _offsets(module):
     return offs, shapes, o
 
 
+DTYPE_PREC = {torch.bfloat16: "bf16", torch.float16: "fp16", torch.float32: "fp32"}
+
+
+def gather16(src: torch.Tensor, idx: torch.Tensor, dtype, x3: bool) -> torch.Tensor:
+    """out[i] = h16(src[idx[i]]); x3: entries flagged with layout.LO_FLAG get the bf16 residual
+    src - bf16(src) (the lo plane). Host / module-API twin of the pack_gather kernel."""
+    if not x3:
+        return src.index_select(0, idx).to(dtype)
+    v = src.index_select(0, idx & (L.LO_FLAG - 1))
+    hi = v.to(torch.bfloat16)
+    lo = (v - hi.float()).to(torch.bfloat16)
+    return torch.where((idx & L.LO_FLAG) != 0, lo, hi)
+
+
 class ModulePack:
-    def __init__(self, kind: str, module, device, dtype=torch.bfloat16):
+    def __init__(self, kind: str, module, device, dtype=torch.float32):
         self.kind = kind
-        self.dtype = dtype      # 16-bit MFMA element type (bf16 | fp16)
+        self.prec = DTYPE_PREC[dtype]     # bf16 | fp16 | fp32 (x3 split kernels)
+        self.x3 = self.prec == "fp32"
+        self.dtype = torch.float16 if self.prec == "fp16" else torch.bfloat16   # packed element type
         offs, self.shapes, self.n = _offsets(module)
         dim = module.in_dim // 2
         self.dim = dim
@@ -50,15 +66,18 @@ class ModulePack:
             raise ValueError(kind)
         self.off = pk.offsets()
         self.rm_off = rm.offsets()
-        self._iw, self._iv, self._irm = mk(pk.index()), mk(vec), mk(rm.index())
+        iw, irm = L.resolve(pk.index(), self.n), L.resolve(rm.index(), self.n)
+        if self.x3:
+            iw, irm = L.x3_frags(iw), L.x3_planes(irm)
+        self._iw, self._iv, self._irm = mkl(iw), mk(vec), mkl(irm)
         self._const = torch.tensor([0.0, 1.0], dtype=torch.float32, device=device)
 
     @torch.no_grad()
     def pack(self, params):
         src = torch.cat([p.detach().float().reshape(-1) for p in params] + [self._const])
-        w = src.index_select(0, self._iw).to(self.dtype)
+        w = gather16(src, self._iw, self.dtype, self.x3)
         v = src.index_select(0, self._iv).contiguous()
-        rm = src.index_select(0, self._irm).to(self.dtype)
+        rm = gather16(src, self._irm, self.dtype, self.x3)
         return w, v, rm
 
     def unpack_grads(self, reds: Dict[str, torch.Tensor]):
@@ -71,8 +90,10 @@ class ModulePack:
 
 
 def module_pack(kind: str, module, device, dtype=None) -> ModulePack:
-    """``dtype`` defaults to the module's ``mfma_dtype`` attribute (bf16 when unset)."""
-    dtype = dtype or getattr(module, "mfma_dtype", torch.bfloat16)
+    """``dtype`` defaults to the module's ``mfma_dtype`` attribute: torch.float32 (unset: the
+    reference precision, fp32-accurate x3 kernels), torch.bfloat16 or torch.float16 (one 16-bit
+    MFMA per product)."""
+    dtype = dtype or getattr(module, "mfma_dtype", torch.float32)
     key = (kind, module.in_dim, str(device), dtype)
     mp = _CACHE.get(key)
     if mp is None:

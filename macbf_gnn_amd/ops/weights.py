@@ -1,17 +1,24 @@
 """Per-step repacking of the flat fp32 master parameters into the kernels' bf16 MFMA
-fragment buffers (+ fp32 side vectors). One gather per network per optimizer step."""
+fragment buffers (+ fp32 side vectors). One gather per network per optimizer step.
+
+dtype selects the kernel precision (csrc/prec.h): torch.bfloat16 / torch.float16 (one 16-bit
+MFMA per product) or torch.float32 -- the fp32-accurate 3-term split kernels, whose packed
+buffers (bf16) carry a residual plane next to every fragment / image (layout.x3_*)."""
 from __future__ import annotations
 
 import torch
 
 from . import layout as L
+from .packing import DTYPE_PREC, gather16
 
 
 class PackedWeights:
     def __init__(self, fp, dim: int = 2, dtype=torch.bfloat16):
         self.fp = fp
         self.dim = dim
-        self.dtype = dtype
+        self.prec = DTYPE_PREC[dtype]                      # bf16 | fp16 | fp32 (x3)
+        self.x3 = self.prec == "fp32"
+        self.dtype = torch.float16 if self.prec == "fp16" else torch.bfloat16   # packed element type
         offs = {pn: o for (m, pn, shape, o, n) in fp.specs}
         dev = fp.flat.device
         n = fp.numel
@@ -28,16 +35,18 @@ class PackedWeights:
         # fp32 side vectors views of another: one gather launch repacks everything
         seg16 = [L.resolve(self.ctrl_pk.index(), n), L.resolve(self.cbf_pk.index(), n),
                  L.resolve(self.node_rm.index(), n), L.resolve(self.cbf_rmp.index(), n)]
+        if self.x3:
+            seg16 = [L.x3_frags(seg16[0]), L.x3_frags(seg16[1]), L.x3_planes(seg16[2]), L.x3_planes(seg16[3])]
         seg32 = [L.resolve(cv, n), L.resolve(bv, n)]
         self._idx16, v16 = self._concat(seg16, n, 256)
         self._idx32, v32 = self._concat(seg32, n, 64)
-        for a in (self._idx16, self._idx32):        # the gather kernel trusts these bounds
+        for a in (self._idx16 & (L.LO_FLAG - 1), self._idx32):   # the gather kernel trusts these bounds
             if a.size and (a.min() < 0 or a.max() > n + 1):
                 raise ValueError("packing index out of range")
         dev_i = lambda a: torch.as_tensor(a, dtype=torch.int32, device=dev)
         self._idx16 = dev_i(self._idx16)
         self._idx32 = dev_i(self._idx32)
-        self._buf16 = torch.empty(self._idx16.numel(), dtype=dtype, device=dev)
+        self._buf16 = torch.empty(self._idx16.numel(), dtype=self.dtype, device=dev)
         self._buf32 = torch.empty(self._idx32.numel(), dtype=torch.float32, device=dev)
         self.ctrl_w, self.cbf_w, self.ctrl_rm, self.cbf_rm = [self._buf16[o:o + m] for o, m in v16]
         self.ctrl_v, self.cbf_v = [self._buf32[o:o + m] for o, m in v32]
@@ -65,5 +74,5 @@ class PackedWeights:
             return
         n = self.fp.numel
         src = torch.cat([self.fp.flat, torch.tensor([0.0, 1.0], device=self.fp.flat.device)])
-        self._buf16.copy_(src.index_select(0, self._idx16.long()))
+        self._buf16.copy_(gather16(src, self._idx16.long(), self.dtype, self.x3))
         self._buf32.copy_(src.index_select(0, self._idx32.long()))
