@@ -127,6 +127,7 @@ def main():
         "early_stop": not args.no_early_stop,
         "skipped_steps": tr.skipped_steps,
         "graph": args.graph,
+        "dp_backend": dp.backend,
         "precision": {"fp32": "fp32-accurate: 3-term split-bf16 MFMA (hi*hi + hi*lo + lo*hi), fp32 accumulate",
                       "bf16": "bf16 MFMA inputs, fp32 accumulate", "fp16": "fp16 MFMA inputs, fp32 accumulate, "
                       "dynamic loss scaling"}[args.dtype],

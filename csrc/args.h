@@ -7,6 +7,12 @@
 
 namespace mb {
 
+// Per-env rollout sums (goal distance, action-loss term) are accumulated as fixed-point 64-bit
+// integers: integer atomics commute, so the sums -- and the early-stop horizon that depends on
+// them -- do not depend on the order in which waves finish. value = sum / FX_*.
+constexpr double FX_DIST = 4294967296.0;   // 2^32: per-env distance sums < 2^31 for any env size here
+constexpr double FX_ACT = 16777216.0;      // 2^24: per-env action-term sums < 2^39
+
 struct CellSortArgs {
   const float4* S;  long s_env;      // node (b,i) record at S[(b*s_env + i) * rec]
   int B, N;                          // N = graph nodes (agents + obstacle points)
@@ -54,9 +60,15 @@ struct CtrlArgs {
   const float* wvec;                  // eb2|nb2|nb3|nb4 (CTRL_VEC floats)
   float* A;         long a_env;       // actions out (b,i,d) -> A[(b*a_env + i)*D + d] (may be null)
   float4* Snext;    long sn_env;      // next-state records out (may be null)
-  float* dist_sum;  long d_env;       // per-env sum of |p' - g| (may be null)
-  float* act_sum;   long ac_env;      // per-env sum of |‖a‖² - ‖a_ref‖²| (may be null)
+  unsigned long long* dist_sum; long d_env;  // per-env sum of |p' - g| * FX_DIST (may be null)
+  unsigned long long* act_sum;  long ac_env; // per-env sum of |‖a‖² - ‖a_ref‖²| * FX_ACT (may be null)
   const float* noise; long n_env;     // additive action noise (b,i,d) (may be null)
+  // device-side exploration noise (reference train.py:65-67): with probability noise_prob per
+  // (env, step) every agent's action gets noise_scale * N(0, 1); counter-based RNG keyed by the
+  // per-iteration key *noise_key (seed, iteration, rank), the step noise_t, env, agent, axis.
+  const unsigned long long* noise_key; // device scalar or null (no noise)
+  float noise_prob, noise_scale;
+  int noise_t;
   float dt, obs_r, sqrt3;
   h16* pooled;     long p_env;       // (b,i,128) max-pooled edge features out (h16), or null
   uint8_t* argmax;  long am_env;      // (b,i,128) winning slot per feature (0xFF: no grad), or null
@@ -136,8 +148,10 @@ struct CbfMatchArgs {
   int T, B, N, K;
   int mode;              // 0: reuse_nbr_idx (match by neighbour id), 1: recomputed kNN (slot k <-> k)
   int phase;             // 0: count extras per row, 1: write map1 / src
-  int* cnt;              // (T*B*N) extras per (t,b,i) row (phase 0 out)
-  const int* off;        // (T*B*N) exclusive offsets (phase 1 in)
+  int* cnt;              // (T*B*N) extras per (t,b,i) row (phase 0 out, optional)
+  const int* off;        // (T*B*N) exclusive offsets (phase 1 in; null: computed in-kernel from bsum)
+  int* bsum;             // (gridDim.x) extras per block (phase 0 out, phase 1 in)
+  int* nev;              // [E + extras] (phase 1 out, written by the last block)
   int* map1;             // (E) evaluation index of the h' partner of main slot e
   int* src;              // (2E) source slot whose h' is evaluation u, or -1
 };
@@ -169,10 +183,11 @@ struct CtrlNodeBwdArgs {
   int o_w1, o_w2, o_w3, o_w4;          // element offsets (strides 168/72/136/72)
   const float* wvec;                   // controller side vector (eb2|nb2|nb3|nb4)
   float act_coef, dt, sqrt3;
-  const float* act_scale;              // optional device scalar: coefficient = act_coef * (*act_scale)
+  const float* act_scale;              // optional device count n_act: coefficient = act_coef / max(n_act, 1)
   h16* dP;            long dp_env;    // (b,i,128) dL/dpooled out
   float4* ego;                         // (B,N) records: dL/ds_t from the node path + gain law + action loss
   float* partial;                      // (gridDim.x, CTRL_NODE_PARTIAL) slabs, accumulated
+  int init;                            // 1: the slabs are written, not accumulated (first BPTT step)
 };
 
 struct CtrlEdgeBwdArgs {
@@ -185,6 +200,7 @@ struct CtrlEdgeBwdArgs {
   const h16* wpack;   int f_ew1f, f_ew2tn;   // packed fragments (ew2tn followed by ew1ft)
   float4* dEc;         long de_env;    // (b,i,K) records of dL/d(s_i - s_j) out
   float* partial;                      // (gridDim.x, CTRL_EDGE_PARTIAL) slabs, accumulated
+  int init;                            // 1: the slabs are written, not accumulated (first BPTT step)
   int qsplit;                          // workgroups per 128-agent chunk (tile-range split; 1, 2, 4, 8, 16)
 };
 
@@ -225,10 +241,10 @@ struct CombineArgs {
 };
 
 struct RolloutStatsArgs {
-  const float* dist;      // (T, B) per-env sum of |p_{t+1} - g| over the N agents
+  const unsigned long long* dist;   // (T, B) per-env sum of |p_{t+1} - g| over the N agents (x FX_DIST)
   const float* cnt;       // (T, B, 2) dangerous / safe edge counts of step t
   const float* safe;      // (T+1, B) safe-agent counts of s_t (or null)
-  const float* act;       // (T, B) per-env action-loss sums (or null)
+  const unsigned long long* act;    // (T, B) per-env action-loss sums (x FX_ACT, or null)
   int T, B, N;
   float thr;              // DIST_MIN_CHECK
   uint8_t* valid;         // (T, B) out
@@ -272,7 +288,8 @@ int mb_ctrl_edge_bwd_x3(const mb::CtrlEdgeBwdArgs* a, int num_blocks, hipStream_
 int mb_rev_csr(const mb::CsrArgs* a, hipStream_t st);
 int mb_cbf_match(const mb::CbfMatchArgs* a, hipStream_t st);
 int mb_cbf_dh(const mb::CbfDhArgs* a, int num_blocks, hipStream_t st);
-int mb_cbf_compact(const float* dh, const int* nev, const int* blk_off, int* act, int num_blocks, hipStream_t st);
+int mb_cbf_compact(const float* dh, const int* nev, const int* blk_off, int* act, int num_blocks,
+                   const int* blk_active, int* nact, hipStream_t st);
 int mb_node_reduce(const mb::NodeRedArgs* a, hipStream_t st);
 int mb_node_combine(const mb::CombineArgs* a, hipStream_t st);
 int mb_reduce_rows(const float* partial, int rows, int cols, float* out, int accumulate, hipStream_t st);

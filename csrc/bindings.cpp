@@ -50,16 +50,19 @@ static int ctrl_fwd(u64 S, long s_env, u64 G, u64 idx, long i_env, int B, int N,
                     int f_node, u64 wvec, u64 A, long a_env, u64 Sn, long sn_env, u64 dist_sum, long d_env,
                     u64 act_sum, long ac_env, u64 noise, long n_env, float dt, float obs_r, float sqrt3,
                     u64 pooled, long p_env, u64 argmax, long am_env, int dim, int num_cu, int prec, int apw,
-                    u64 stream) {
+                    u64 noise_key, float noise_prob, float noise_scale, int noise_t, u64 stream) {
   mb::CtrlArgs a{};
   a.dim = dim;
   a.apw = apw;
   a.S = P<const float4>(S); a.s_env = s_env; a.G = P<const float>(G); a.idx = P<const int>(idx); a.i_env = i_env;
   a.B = B; a.N = N; a.K = K; a.wpack = P<const h16>(wpack); a.f_edge = f_edge; a.f_node = f_node;
   a.wvec = P<const float>(wvec); a.A = P<float>(A); a.a_env = a_env; a.Snext = P<float4>(Sn); a.sn_env = sn_env;
-  a.dist_sum = P<float>(dist_sum); a.d_env = d_env; a.act_sum = P<float>(act_sum); a.ac_env = ac_env;
+  a.dist_sum = P<unsigned long long>(dist_sum); a.d_env = d_env; a.act_sum = P<unsigned long long>(act_sum);
+  a.ac_env = ac_env;
   a.noise = P<const float>(noise); a.n_env = n_env; a.dt = dt; a.obs_r = obs_r; a.sqrt3 = sqrt3;
   a.pooled = P<h16>(pooled); a.p_env = p_env; a.argmax = P<uint8_t>(argmax); a.am_env = am_env;
+  a.noise_key = P<const unsigned long long>(noise_key); a.noise_prob = noise_prob; a.noise_scale = noise_scale;
+  a.noise_t = noise_t;
   return (prec == 2 ? mb_ctrl_fwd_x3 : prec == 1 ? mb_ctrl_fwd_f16 : mb_ctrl_fwd)(&a, num_cu, ST(stream));
 }
 
@@ -139,10 +142,11 @@ static int node_reduce(u64 dE, u64 ptr, u64 edges, int B, int T, int N, int K, i
 }
 
 static int cbf_match(u64 idx, int T, int B, int N, int K, int mode, int phase, u64 cnt, u64 off, u64 map1, u64 src,
-                     u64 stream) {
+                     u64 bsum, u64 nev, u64 stream) {
   mb::CbfMatchArgs a{};
   a.idx = P<const int>(idx); a.T = T; a.B = B; a.N = N; a.K = K; a.mode = mode; a.phase = phase;
   a.cnt = P<int>(cnt); a.off = P<const int>(off); a.map1 = P<int>(map1); a.src = P<int>(src);
+  a.bsum = P<int>(bsum); a.nev = P<int>(nev);
   return mb_cbf_match(&a, ST(stream));
 }
 
@@ -160,9 +164,10 @@ static int cbf_dh(u64 h, u64 hmask, u64 map1, u64 src, u64 nev, u64 dang, u64 va
   return mb_cbf_dh(&a, num_blocks, ST(stream));
 }
 
-static int cbf_compact(u64 dh, u64 nev, u64 blk_off, u64 act, int num_blocks, u64 stream) {
+static int cbf_compact(u64 dh, u64 nev, u64 blk_off, u64 act, int num_blocks, u64 blk_active, u64 nact,
+                       u64 stream) {
   return mb_cbf_compact(P<const float>(dh), P<const int>(nev), P<const int>(blk_off), P<int>(act), num_blocks,
-                        ST(stream));
+                        P<const int>(blk_active), P<int>(nact), ST(stream));
 }
 
 static int node_combine(u64 dS, long ds_env, u64 ego, u64 dEc, u64 ptr, long ptr_env, u64 edges, long edges_env,
@@ -200,8 +205,8 @@ static int adam_commit(u64 ok, u64 steps, int mask, int ngroups, u64 skipped, u6
 static int rollout_stats(u64 dist, u64 cnt, u64 safe, u64 act, int T, int B, int N, float thr, u64 valid,
                          u64 counts, u64 local, u64 stream) {
   mb::RolloutStatsArgs a{};
-  a.dist = P<const float>(dist); a.cnt = P<const float>(cnt); a.safe = P<const float>(safe);
-  a.act = P<const float>(act); a.T = T; a.B = B; a.N = N; a.thr = thr; a.valid = P<uint8_t>(valid);
+  a.dist = P<const unsigned long long>(dist); a.cnt = P<const float>(cnt); a.safe = P<const float>(safe);
+  a.act = P<const unsigned long long>(act); a.T = T; a.B = B; a.N = N; a.thr = thr; a.valid = P<uint8_t>(valid);
   a.counts = P<float>(counts); a.local = P<float>(local);
   return mb_rollout_stats(&a, ST(stream));
 }
@@ -218,8 +223,9 @@ static int adam(u64 param, u64 grad, u64 m, u64 v, int lo, int hi, float b1, flo
 static int ctrl_node_bwd(u64 pooled, long p_env, u64 S, long s_env, u64 G, u64 A, long a_env, u64 Gn, long gn_env,
                          u64 valid, long v_env, int B, int N, u64 wrm, int o1, int o2, int o3, int o4, u64 wvec,
                          float act_coef, u64 act_scale, float dt, float sqrt3, u64 dP, long dp_env, u64 ego, u64 partial,
-                         int dim, int num_blocks, int prec, u64 stream) {
+                         int dim, int num_blocks, int prec, int init, u64 stream) {
   mb::CtrlNodeBwdArgs a{};
+  a.init = init;
   a.dim = dim;
   a.pooled = P<const h16>(pooled); a.p_env = p_env; a.S = P<const float4>(S); a.s_env = s_env;
   a.G = P<const float>(G); a.A = P<const float>(A); a.a_env = a_env; a.Gn = P<const float4>(Gn); a.gn_env = gn_env;
@@ -232,8 +238,9 @@ static int ctrl_node_bwd(u64 pooled, long p_env, u64 S, long s_env, u64 G, u64 A
 
 static int ctrl_edge_bwd(u64 S, long s_env, u64 idx, long i_env, u64 argmax, long am_env, u64 dP, long dp_env,
                          int B, int N, int K, u64 wpack, int f_ew1f, int f_ew2tn, u64 dEc, long de_env, u64 partial,
-                         int dim, int num_blocks, int prec, int qsplit, u64 stream) {
+                         int dim, int num_blocks, int prec, int qsplit, int init, u64 stream) {
   mb::CtrlEdgeBwdArgs a{};
+  a.init = init;
   a.dim = dim;
   a.qsplit = qsplit;
   a.S = P<const float4>(S); a.s_env = s_env; a.idx = P<const int>(idx); a.i_env = i_env;

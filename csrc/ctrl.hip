@@ -229,6 +229,19 @@ DEV void node_phase(const CtrlArgs& a, int g0, int APW, int total, PoolFr pool, 
       av[q] = -(kp * ex[q] + kv * sv[q]);
       if (a.noise) av[q] += a.noise[((long)b * a.n_env + i) * D + q];
     }
+    if (a.noise_key) {
+      // one coin per (env, step), Box-Muller normals per (agent, axis): the same draws for any
+      // launch geometry, the native driver and the Python loop
+      const uint64_t kb = mix64(*a.noise_key ^ (0x9E3779B97F4A7C15ull * (uint64_t)(a.noise_t * a.B + b + 1)));
+      if (u01(kb) < a.noise_prob) {
+#pragma unroll
+        for (int q = 0; q < D; ++q) {
+          const uint64_t ka = kb + 2ull * (uint64_t)(i * D + q) + 1ull;
+          const float u1 = fmaxf(u01(mix64(ka)), 1e-12f), u2 = u01(mix64(ka + 0xD1B54A32D192ED03ull));
+          av[q] += a.noise_scale * sqrtf(-2.f * __logf(u1)) * __cosf(6.28318530718f * u2);
+        }
+      }
+    }
     if (a.A) {
 #pragma unroll
       for (int q = 0; q < D; ++q) a.A[((long)b * a.a_env + i) * D + q] = av[q];
@@ -246,19 +259,21 @@ DEV void node_phase(const CtrlArgs& a, int g0, int APW, int total, PoolFr pool, 
     dsum = sqrtf(sqsum<D>(dd));
     asum = fabsf(sqsum<D>(av) - sqsum<D>(ar));
   }
-  // per-env sums: one atomic per wave when its 32 agents share an env
+  // per-env sums: one fixed-point integer atomic per wave when its 32 agents share an env
+  // (the wave sum is a fixed shuffle tree, the integer adds commute: order-independent)
+  auto fx = [](float v, double s) { return (unsigned long long)__double2ll_rn((double)v * s); };
   const int last = min(g0 + APW - 1, total - 1);
   if (g0 / N == last / N) {
     dsum = wave_sum(dsum);
     asum = wave_sum(asum);
     if (lane == 0) {
       const int be = g0 / N;
-      if (a.dist_sum) atomicAdd(a.dist_sum + (long)be * a.d_env, dsum);
-      if (a.act_sum) atomicAdd(a.act_sum + (long)be * a.ac_env, asum);
+      if (a.dist_sum) atomicAdd(a.dist_sum + (long)be * a.d_env, fx(dsum, FX_DIST));
+      if (a.act_sum) atomicAdd(a.act_sum + (long)be * a.ac_env, fx(asum, FX_ACT));
     }
   } else if (ok && h == 0) {
-    if (a.dist_sum) atomicAdd(a.dist_sum + (long)b * a.d_env, dsum);
-    if (a.act_sum) atomicAdd(a.act_sum + (long)b * a.ac_env, asum);
+    if (a.dist_sum) atomicAdd(a.dist_sum + (long)b * a.d_env, fx(dsum, FX_DIST));
+    if (a.act_sum) atomicAdd(a.act_sum + (long)b * a.ac_env, fx(asum, FX_ACT));
   }
 }
 
@@ -625,7 +640,7 @@ __global__ __launch_bounds__(NB_WAVES * 64, 1) void ctrl_node_bwd_kernel(CtrlNod
       float da[D], ar[D];
 #pragma unroll
       for (int q = 0; q < D; ++q) { da[q] = a.dt * gnv[q]; ar[q] = -(ex[q] + a.sqrt3 * sv[q]); }
-      const float act_coef = a.act_scale ? a.act_coef * *a.act_scale : a.act_coef;
+      const float act_coef = a.act_scale ? a.act_coef / fmaxf(*a.act_scale, 1.f) : a.act_coef;
       if (vld && act_coef != 0.f) {
         const float diff = sqsum<D>(av) - sqsum<D>(ar);
         const float sg = diff > 0.f ? 1.f : (diff < 0.f ? -1.f : 0.f);
@@ -818,25 +833,29 @@ __global__ __launch_bounds__(NB_WAVES * 64, 1) void ctrl_node_bwd_kernel(CtrlNod
   if (a.partial) return;                        // ablation: no slab read-modify-write
 #endif
   float* P = a.partial + (long)blockIdx.x * CTRL_NODE_PARTIAL;
-  // all slab loads first (see load_tile), then the adds and stores
-  f32x16 o1[3], o2[2], o3[2], o4;
-  float ob2[2], ob3[2], ob4 = 0.f;
+  // all slab loads first (see load_tile), then the adds and stores; the first BPTT step writes
+  // the slab (no zero-fill pass, no loads)
+  f32x16 o1[3], o2[2], o3[2], o4 = zero16();
+  float ob2[2] = {0.f, 0.f}, ob3[2] = {0.f, 0.f}, ob4 = 0.f;
+  o1[0] = o1[1] = o1[2] = o2[0] = o2[1] = o3[0] = o3[1] = zero16();
+  if (!a.init) {
 #pragma unroll
-  for (int u = 0; u < 3; ++u) {
-    const int t = wave + 4 * u;
-    if (u < n1) load_tile(o1[u], P + NP_W1, 160, t / 5, t % 5, lane);
-  }
+    for (int u = 0; u < 3; ++u) {
+      const int t = wave + 4 * u;
+      if (u < n1) load_tile(o1[u], P + NP_W1, 160, t / 5, t % 5, lane);
+    }
 #pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    const int t = wave + 4 * u;
-    load_tile(o2[u], P + NP_W2, 64, t / 2, t % 2, lane);
-    load_tile(o3[u], P + NP_W3, 128, t / 4, t % 4, lane);
-    ob2[u] = P[NP_B2 + 32 * (t / 2) + r];
-    ob3[u] = P[NP_B3 + 32 * (t / 4) + r];
-  }
-  if (wave < 2) {
-    load_tile(o4, P + NP_W4, 64, 0, wave, lane);
-    ob4 = P[NP_B4 + r];
+    for (int u = 0; u < 2; ++u) {
+      const int t = wave + 4 * u;
+      load_tile(o2[u], P + NP_W2, 64, t / 2, t % 2, lane);
+      load_tile(o3[u], P + NP_W3, 128, t / 4, t % 4, lane);
+      ob2[u] = P[NP_B2 + 32 * (t / 2) + r];
+      ob3[u] = P[NP_B3 + 32 * (t / 4) + r];
+    }
+    if (wave < 2) {
+      load_tile(o4, P + NP_W4, 64, 0, wave, lane);
+      ob4 = P[NP_B4 + r];
+    }
   }
 #pragma unroll
   for (int u = 0; u < 3; ++u) {
@@ -1072,13 +1091,19 @@ __global__ __launch_bounds__(EB_WAVES * 64, (EB_WAVES == 4 && !X3) ? 2 : 1) void
   float o1[NQ1];
   float ob2 = 0.f;
 #pragma unroll
-  for (int u = 0; u < EB_TA; ++u) {
-    const int t = wave + EB_WAVES * u;
-    load_tile(o2[u], P + EP_W2, 64, t / 2, t % 2, lane);
-  }
+  for (int u = 0; u < EB_TA; ++u) o2[u] = zero16();
 #pragma unroll
-  for (int j = 0; j < NQ1; ++j) o1[j] = P[EP_W1 + threadIdx.x + j * EB_WAVES * 64];
-  if (threadIdx.x < 128) ob2 = P[EP_B2 + threadIdx.x];
+  for (int j = 0; j < NQ1; ++j) o1[j] = 0.f;
+  if (!a.init) {      // the first BPTT step writes the slab (no zero-fill pass, no loads)
+#pragma unroll
+    for (int u = 0; u < EB_TA; ++u) {
+      const int t = wave + EB_WAVES * u;
+      load_tile(o2[u], P + EP_W2, 64, t / 2, t % 2, lane);
+    }
+#pragma unroll
+    for (int j = 0; j < NQ1; ++j) o1[j] = P[EP_W1 + threadIdx.x + j * EB_WAVES * 64];
+    if (threadIdx.x < 128) ob2 = P[EP_B2 + threadIdx.x];
+  }
 #pragma unroll
   for (int u = 0; u < EB_TA; ++u) {
     const int t = wave + EB_WAVES * u;

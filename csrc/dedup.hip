@@ -31,6 +31,41 @@ constexpr int MATCH_BLOCK = 256;
 constexpr int DH_BLOCK = 256;
 constexpr int DH_PARTIAL = 12;   // loss partials per block: [0, 0, 8 sums, 0, 0] (rows padded to 4)
 
+// Block-wide exclusive scan of one int per thread (NT threads, wave64): returns the exclusive
+// prefix of this thread, *total = the block sum. Two barriers.
+template <int NT>
+DEV int block_excl_scan(int v, int* total) {
+  __shared__ int wsum[NT / WAVE];
+  const int lane = threadIdx.x % WAVE, wave = threadIdx.x / WAVE;
+  int x = v;
+#pragma unroll
+  for (int o = 1; o < WAVE; o <<= 1) {
+    const int y = __shfl_up(x, o);
+    if (lane >= o) x += y;
+  }
+  if (lane == WAVE - 1) wsum[wave] = x;
+  __syncthreads();
+  int pre = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < NT / WAVE; ++w) {
+    pre += (w < wave) ? wsum[w] : 0;
+    tot += wsum[w];
+  }
+  __syncthreads();
+  *total = tot;
+  return pre + x - v;
+}
+
+// Sum of p[0..n) by the whole block (fixed order per thread + fixed tree: deterministic).
+template <int NT>
+DEV int block_sum_prefix(const int* p, int n) {
+  int s = 0;
+  for (int q = threadIdx.x; q < n; q += NT) s += p[q];
+  int tot;
+  (void)block_excl_scan<NT>(s, &tot);
+  return tot;
+}
+
 // One thread per (t,b,i) row, MATCH_BLOCK consecutive rows per block: the block's slot rows of
 // step t and step t+1 (each one contiguous segment) are staged in LDS with coalesced loads, the
 // matching runs in registers, and map1 / the next row's src go back through LDS as coalesced
@@ -81,14 +116,30 @@ __global__ __launch_bounds__(MATCH_BLOCK) void cbf_match_kernel(CbfMatchArgs a) 
       }
     }
   }
+  const int cnt = live ? K - nmatch : 0;
   if (a.phase == 0) {
-    if (live) a.cnt[row] = K - nmatch;
+    if (live && a.cnt) a.cnt[row] = cnt;
+    int tot;
+    (void)block_excl_scan<MATCH_BLOCK>(cnt, &tot);
+    if (threadIdx.x == 0 && a.bsum) a.bsum[blockIdx.x] = tot;
     return;
+  }
+  // extras offset of this row: exclusive scan over the rows (in-kernel when off is null: block
+  // prefix from the phase-0 block sums + the block-local scan; exact integers, deterministic)
+  long roff = 0;
+  if (a.off) {
+    roff = live ? a.off[row] : 0;
+  } else {
+    const int pre = block_sum_prefix<MATCH_BLOCK>(a.bsum, blockIdx.x);
+    int tot;
+    const int ex = block_excl_scan<MATCH_BLOCK>(cnt, &tot);
+    roff = (long)pre + ex;
+    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0 && a.nev) *a.nev = (int)(E + pre + tot);
   }
   __syncthreads();                         // s0 / s1 are reused as output staging
   const long e0 = row * K;
   if (live) {
-    const long off = E + a.off[row];
+    const long off = E + roff;
     int x = 0;
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
@@ -216,14 +267,22 @@ __global__ __launch_bounds__(DH_BLOCK) void cbf_dh_kernel(CbfDhArgs a) {
 // (every other evaluation contributes exactly zero to the weight and state gradients, so the
 // backward skips it). Same block ranges as cbf_dh_kernel; blk_off = exclusive scan of its
 // per-block counts.
+// blk_off null: the block's offset is summed in-kernel from blk_active (cbf_dh's per-block
+// counts) and the last block writes the total to *nact.
 __global__ __launch_bounds__(DH_BLOCK) void cbf_compact_kernel(const float* dh, const int* nev, const int* blk_off,
-                                                             int* act) {
+                                                             int* act, const int* blk_active, int* nact) {
   const unsigned U = (unsigned)*nev;
   const unsigned span = dh_span(U, gridDim.x);
   const unsigned u_lo = blockIdx.x * span, u_hi = min(U, u_lo + span);
   __shared__ int wcnt[DH_BLOCK / WAVE];
   const int wave = threadIdx.x / WAVE, lane = threadIdx.x % WAVE;
-  int base = blk_off[blockIdx.x];
+  int base;
+  if (blk_off) {
+    base = blk_off[blockIdx.x];
+  } else {
+    base = block_sum_prefix<DH_BLOCK>(blk_active, blockIdx.x);
+    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0 && nact) *nact = base + blk_active[blockIdx.x];
+  }
   for (unsigned u0 = u_lo; u0 < u_hi; u0 += DH_BLOCK) {
     const unsigned u = u0 + threadIdx.x;
     const bool f = u < u_hi && dh[u] != 0.f;
@@ -246,9 +305,11 @@ __global__ __launch_bounds__(DH_BLOCK) void cbf_compact_kernel(const float* dh, 
 }  // namespace mb
 
 extern "C" int mb_cbf_compact(const float* dh, const int* nev, const int* blk_off, int* act, int num_blocks,
-                              hipStream_t st) {
+                              const int* blk_active, int* nact, hipStream_t st) {
   using namespace mb;
-  hipLaunchKernelGGL(cbf_compact_kernel, dim3(num_blocks), dim3(DH_BLOCK), 0, st, dh, nev, blk_off, act);
+  if (!blk_off && !blk_active) return -1;
+  hipLaunchKernelGGL(cbf_compact_kernel, dim3(num_blocks), dim3(DH_BLOCK), 0, st, dh, nev, blk_off, act, blk_active,
+                     nact);
   return (int)hipGetLastError();
 }
 

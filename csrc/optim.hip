@@ -145,9 +145,9 @@ __global__ __launch_bounds__(RS_BLOCK) void rollout_stats_kernel(RolloutStatsArg
         v[1] += a.cnt[(t * a.B + b) * 2 + 1];
         v[2] += (float)a.N;
         if (a.safe) v[3] += a.safe[(t + 1) * a.B + b];
-        if (a.act) v[4] += a.act[t * a.B + b];
+        if (a.act) v[4] += (float)((double)a.act[t * a.B + b] / FX_ACT);
       }
-      done = done || (a.dist[t * a.B + b] / (float)a.N < a.thr);
+      done = done || ((float)((double)a.dist[t * a.B + b] / FX_DIST) / (float)a.N < a.thr);
     }
   }
   __shared__ float red[6][RS_BLOCK];

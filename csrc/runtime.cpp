@@ -59,6 +59,7 @@ class RolloutDriver {
     dt_ = F("dt"); obs_r_ = F("obs_r"); sqrt3_ = F("sqrt3"); dist_thr_ = F("dist_thr"); dist_eps_ = F("dist_eps");
     done_thr_ = F("done_thr");
     check_ = (int)I("check_every");
+    noise_key_ = U("noise_key"); noise_prob_ = F("noise_prob"); noise_scale_ = F("noise_scale");
     apw_ = (int)I("apw");
     if (check_ < 1) check_ = 1;
     if (B_ < 1|| N_ < 1 || Nn_ < N_ || K_ < 1 || K_ > 16 || (D_ != 2 && D_ != 3) || Tmax_ < 1 || resort_ < 1)
@@ -84,7 +85,7 @@ class RolloutDriver {
   // early-stopped case, where step T's scan ran before the break).
   std::pair<int, bool> run(u64 stream, u64 hstream, u64 copy_stream, bool early_stop) {
     hipStream_t st = ST(stream), hs = ST(hstream), cs = ST(copy_stream);
-    const volatile float* hd = P<const volatile float>(host_dist_);
+    const volatile unsigned long long* hd = P<const volatile unsigned long long>(host_dist_);
     int T = Tmax_;
     bool tail = false;
     for (int t = 0; t < Tmax_; ++t) {
@@ -101,8 +102,8 @@ class RolloutDriver {
       }
       if (early_stop) {
         chk(hipStreamWaitEvent(cs, ev_main_, 0), "hipStreamWaitEvent");
-        chk(hipMemcpyAsync(P<float>(host_dist_) + (long)t * B_, P<const float>(dist_) + (long)t * B_,
-                           sizeof(float) * B_, hipMemcpyDeviceToHost, cs), "hipMemcpyAsync");
+        chk(hipMemcpyAsync(P<unsigned long long>(host_dist_) + (long)t * B_, P<const unsigned long long>(dist_) + (long)t * B_,
+                           sizeof(unsigned long long) * B_, hipMemcpyDeviceToHost, cs), "hipMemcpyAsync");
         chk(hipEventRecord(ev_copy_[t], cs), "hipEventRecord");
         // host check every check_every steps (small scenes: a step's kernels take less than
         // the host round trip, so checking every step would leave the GPU idle)
@@ -145,11 +146,11 @@ class RolloutDriver {
   // from the first step q_b whose mean goal distance is below the threshold: T' = max_b q_b + 1),
   // or 0 if some env is not done by step t. Checking after every step and breaking at the first
   // hit gives the same T'.
-  int first_done(const volatile float* hd, int t) const {
+  int first_done(const volatile unsigned long long* hd, int t) const {
     int last = -1;
     for (int b = 0; b < B_; ++b) {
-      int q = 0;
-      while (q <= t && !(hd[(long)q * B_ + b] / (float)N_ < done_thr_)) ++q;
+      int q = 0;      // same float arithmetic as rollout_stats_kernel
+      while (q <= t && !((float)((double)hd[(long)q * B_ + b] / mb::FX_DIST) / (float)N_ < done_thr_)) ++q;
       if (q > t) return 0;
       if (q > last) last = q;
     }
@@ -189,9 +190,11 @@ class RolloutDriver {
     a.wpack = P<const h16>(ctrl_w_); a.f_edge = f_edge_; a.f_node = f_node_; a.wvec = P<const float>(ctrl_v_);
     a.A = P<float>(A_) + (long)t * B_ * N_ * D_; a.a_env = N_;
     a.Snext = const_cast<float4*>(S_at(t + 1)); a.sn_env = Nn_;
-    a.dist_sum = P<float>(dist_) + (long)t * B_; a.d_env = 1;
-    a.act_sum = P<float>(act_) + (long)t * B_; a.ac_env = 1;
+    a.dist_sum = P<unsigned long long>(dist_) + (long)t * B_; a.d_env = 1;
+    a.act_sum = P<unsigned long long>(act_) + (long)t * B_; a.ac_env = 1;
     a.noise = nullptr; a.n_env = 0;
+    a.noise_key = P<const unsigned long long>(noise_key_); a.noise_prob = noise_prob_; a.noise_scale = noise_scale_;
+    a.noise_t = t;
     a.dt = dt_; a.obs_r = obs_r_; a.sqrt3 = sqrt3_;
     a.pooled = P<h16>(pooled_) + (long)t * B_ * N_ * prow_; a.p_env = (long)N_ * prow_;
     a.argmax = P<uint8_t>(argmax_) + (long)t * B_ * N_ * 128; a.am_env = (long)N_ * 128;
@@ -218,7 +221,8 @@ class RolloutDriver {
   int B_, N_, Nn_, K_, D_, W_, Tmax_, num_cu_, prec_, prow_, resort_, safety_, overlap_, hfwd_blocks_, check_, apw_;
   float L_;
   u64 S_, G_, A_, idx_, dang_, cnt_, safe_, dist_, act_, pooled_, argmax_, perm_, host_dist_;
-  u64 ctrl_w_, ctrl_v_, cbf_w_, cbf_rm_, cbf_v_, hbuf_, hmask_, src_, nev_;
+  u64 ctrl_w_, ctrl_v_, cbf_w_, cbf_rm_, cbf_v_, hbuf_, hmask_, src_, nev_, noise_key_;
+  float noise_prob_, noise_scale_;
   int f_edge_, f_node_, f_fwd_;
   float r2_train_, ttc_train_, r2_check_, ttc_check_, dt_, obs_r_, sqrt3_, dist_thr_, dist_eps_, done_thr_;
   std::vector<hipEvent_t> ev_copy_;
@@ -276,6 +280,7 @@ class BpttDriver {
         a.wvec = P<const float>(wvec_); a.act_coef = act_coef; a.act_scale = P<const float>(act_scale_);
         a.dt = dt_; a.sqrt3 = sqrt3_;
         a.dP = P<h16>(dP_); a.dp_env = (long)N_ * prow_; a.ego = P<float4>(ego_); a.partial = P<float>(part_node_);
+        a.init = t == T - 1;     // the first step of the reverse loop writes the slabs
         chk((prec_ == 2 ? mb_ctrl_node_bwd_x3 : prec_ == 1 ? mb_ctrl_node_bwd_f16 : mb_ctrl_node_bwd)(&a, nb_node_, st), "ctrl_node_bwd");
       }
       {
@@ -288,6 +293,7 @@ class BpttDriver {
         a.B = B_; a.N = N_; a.K = K_;
         a.wpack = P<const h16>(wpack_); a.f_ew1f = f_ew1f_; a.f_ew2tn = f_ew2tn_;
         a.dEc = P<float4>(dEc_); a.de_env = nk; a.partial = P<float>(part_edge_); a.qsplit = qsplit_;
+        a.init = t == T - 1;
         chk((prec_ == 2 ? mb_ctrl_edge_bwd_x3 : prec_ == 1 ? mb_ctrl_edge_bwd_f16 : mb_ctrl_edge_bwd)(&a, nb_edge_, st), "ctrl_edge_bwd");
       }
       if (t > 0) {   // G_0 = dL/ds_0 is not needed (s_0 is sampled, not a function of the weights)

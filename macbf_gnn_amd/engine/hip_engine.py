@@ -27,6 +27,11 @@ from ..ops import native
 from ..ops.weights import PackedWeights
 
 
+# action-loss weight of the total loss (core.py:174-184 via train.py:93,98); the node backward
+# divides it by the all-reduced action count on the device
+ACT_COEF = C.LOSS_SCALE * C.LOSS_WEIGHTS[4]
+
+
 class HipEngine:
     name = "hip"
     resort_every = 4          # scan: Hilbert re-sort period (rollout steps)
@@ -105,8 +110,6 @@ class HipEngine:
         # that dominates small configurations). Sampling, the DP all-reduces and the optimizer
         # stay eager around the two captured graphs.
         self.graph_mode = bool(getattr(cfg, "graph", False))
-        if self.graph_mode and cfg.add_noise_prob > 0:
-            raise ValueError("graph mode does not support exploration noise (host-side RNG)")
         self._graphs = None
         self._graph_gs = None
 
@@ -125,8 +128,9 @@ class HipEngine:
         self.dang = torch.zeros(T, B, N, K, dtype=u8, device=dev)
         self.cnt = torch.zeros(T, B, 2, dtype=f32, device=dev)
         self.safe = torch.zeros(T + 1, B, dtype=f32, device=dev)
-        self.dist = torch.zeros(T, B, dtype=f32, device=dev)
-        self.act = torch.zeros(T, B, dtype=f32, device=dev)
+        # per-env goal-distance / action-term sums, fixed point (native.FX_*): order-independent
+        self.dist = torch.zeros(T, B, dtype=torch.int64, device=dev)
+        self.act = torch.zeros(T, B, dtype=torch.int64, device=dev)
         self.pooled = torch.zeros(T, B, N, self.prow, dtype=bf, device=dev)
         self.argmax = torch.zeros(T, B, N, 128, dtype=u8, device=dev)
         self.dE = torch.zeros(2 * T * B * N * K * W, dtype=f32, device=dev)
@@ -141,7 +145,8 @@ class HipEngine:
         self.local = torch.zeros(3, dtype=f32, device=dev)        # agent-steps, safe agents, action-loss sum
         self.raw_stats = torch.zeros(16, dtype=f32, device=dev)   # utils.metrics.StepStats layout
         self.valid_buf = torch.zeros(T, B, dtype=u8, device=dev)
-        self.act_scale = torch.zeros(1, dtype=f32, device=dev)      # action-loss coefficient
+        # exploration noise (reference train.py:65-67): counter-based device RNG keyed per iteration
+        self.noise_key = torch.zeros(1, dtype=torch.int64, device=dev)
         self.nb_node, self.nb_edge = native.ctrl_bwd_grids(B * N, dev)
         # BPTT env groups (independent chains on separate streams): per-group grids and slab rows
         Gp = self.bptt_groups
@@ -171,8 +176,10 @@ class HipEngine:
             self.act_list = torch.zeros(2 * E, dtype=i32, device=dev)
             self.loss_red = torch.zeros(native.DH_PARTIAL, dtype=f32, device=dev)
             self.nev_host = torch.zeros(1, dtype=i32, device=dev)     # unused by host-range slices
+            self.nev_dev = torch.zeros(1, dtype=i32, device=dev)      # [U] of the match
+            self.nact_dev = torch.zeros(1, dtype=i32, device=dev)     # active evaluations
             self.hstream = torch.cuda.Stream(device=dev)              # rollout-overlapped CBF h slices
-        self.host_dist = torch.zeros(T, B, dtype=f32, pin_memory=True)
+        self.host_dist = torch.zeros(T, B, dtype=torch.int64, pin_memory=True)
         self.copy_stream = torch.cuda.Stream(device=dev)
         self.aux = torch.cuda.Stream(device=dev)      # reverse-CSR build overlaps the CBF kernel
         self._nobptt = {}     # lazily sized (T*B)-batched controller-backward buffers
@@ -183,8 +190,18 @@ class HipEngine:
         self.pw.update()
 
     # ------------------------------------------------------------------ rollout
+    def _noise_args(self):
+        cfg = self.tr.cfg
+        if cfg.add_noise_prob <= 0:
+            return dict(noise_key=None)
+        return dict(noise_key=self.noise_key, noise_prob=float(cfg.add_noise_prob), noise_scale=float(cfg.noise_scale))
+
     def load_inputs(self, s0, g, obs=None):
-        """Scenario -> the static input buffers (start records, goals, obstacle rows)."""
+        """Scenario -> the static input buffers (start records, goals, obstacle rows) and the
+        exploration-noise key of this iteration (seed, iteration, rank)."""
+        if self.tr.cfg.add_noise_prob > 0:
+            from ..ops.scenario import iteration_key
+            self.noise_key.fill_(iteration_key(self.tr.cfg.seed, int(self.tr.step_count), self.tr.dp.rank, salt=0x4E4F4953))
         B, N, D = self.B, self.N, self.D
         self.S[0, :, :N].copy_(native.to_records(s0))
         if self.M:
@@ -210,8 +227,8 @@ class HipEngine:
             exp = {"S": (self.S, torch.float32, (T + 1, B, Nn, W)), "G": (self.G, torch.float32, (B, N, D)),
                    "A": (self.A, torch.float32, (T, B, N, D)), "idx": (self.idx, torch.int32, (T + G1, B, N, K)),
                    "dang": (self.dang, torch.uint8, (T, B, N, K)), "cnt": (self.cnt, torch.float32, (T, B, 2)),
-                   "safe": (self.safe, torch.float32, (T + 1, B)), "dist": (self.dist, torch.float32, (T, B)),
-                   "act": (self.act, torch.float32, (T, B)), "pooled": (self.pooled, self.hdt, (T, B, N, self.prow)),
+                   "safe": (self.safe, torch.float32, (T + 1, B)), "dist": (self.dist, torch.int64, (T, B)),
+                   "act": (self.act, torch.int64, (T, B)), "pooled": (self.pooled, self.hdt, (T, B, N, self.prow)),
                    "argmax": (self.argmax, torch.uint8, (T, B, N, 128))}
             for name, (t, dt, shape) in exp.items():
                 native.check(t, dt, shape, name)
@@ -240,6 +257,8 @@ class HipEngine:
                 dt=float(C.TIME_STEP), obs_r=float(C.OBS_RADIUS), sqrt3=float(C.SQRT3),
                 dist_thr=float(C.DIST_MIN_THRES), dist_eps=float(C.CBF_DIST_EPS_COORD * D),
                 done_thr=float(C.DIST_MIN_CHECK),
+                noise_key=native.ptr(self.noise_key) if cfg.add_noise_prob > 0 else 0,
+                noise_prob=float(cfg.add_noise_prob), noise_scale=float(cfg.noise_scale),
                 fork_device_scope=int(os.environ.get("MACBF_FORK_DEVICE_SCOPE", "1"))))
             if pw.ctrl_v.numel() < 352 or pw.ctrl_w.numel() < (c["f_node"] + 54) * 512 * (2 if pw.x3 else 1):
                 raise native.NativeError("packed controller weights too small")
@@ -263,7 +282,7 @@ class HipEngine:
         tail_scanned = False
         cur = torch.cuda.current_stream(self.dev)
         overlap = self.dedup and self.overlap_hfwd
-        if self.native_rollout and cfg.add_noise_prob <= 0 and not torch.cuda.is_current_stream_capturing():
+        if self.native_rollout and not torch.cuda.is_current_stream_capturing():
             # the per-step launch loop in C++ (csrc/runtime.cpp): same launches, same order
             T, tail_scanned = self._driver().run(cur.cuda_stream, self.hstream.cuda_stream if overlap else 0,
                                                  self.copy_stream.cuda_stream, bool(early_stop))
@@ -280,13 +299,8 @@ class HipEngine:
             native.scan(self.S[t], self.idx[t], self.dang[t], self.cnt[t], self.safe[t], K=K,
                         do_knn=True, do_safety=cfg.compute_safety, n_agents=N,
                         prev_idx=self.idx[t - 1] if t > 0 else None, sort=t % self.resort_every == 0)
-            noise = None
-            if cfg.add_noise_prob > 0:
-                coin = (torch.rand(B, 1, 1, device=self.dev, generator=self.tr.torch_gen) < cfg.add_noise_prob)
-                noise = (torch.randn(B, N, D, device=self.dev, generator=self.tr.torch_gen) * cfg.noise_scale
-                         * coin.to(torch.float32)).contiguous()
             native.ctrl_fwd(self.S[t], self.G, self.idx[t], pw.ctrl_w, pw.ctrl_off["ew1f"], pw.ctrl_off["nw1f"],
-                            pw.ctrl_v, self.A[t], self.S[t + 1], self.dist[t], self.act[t], noise=noise,
+                            pw.ctrl_v, self.A[t], self.S[t + 1], self.dist[t], self.act[t], noise_t=t, **self._noise_args(),
                             pooled=self.pooled[t], argmax=self.argmax[t], prec=self.prec)
             if early_stop:
                 # the per-env goal distances go to pinned host memory on a side stream (the
@@ -340,7 +354,8 @@ class HipEngine:
                             pw.cbf_v, self.hbuf, self.hmask, u_begin=t * BNK, u_end=(t + 1) * BNK, prec=self.prec)
 
     def _all_done(self, t):
-        d = self.host_dist[: t + 1] / self.N < C.DIST_MIN_CHECK      # (t+1, B)
+        # the float arithmetic of rollout_stats_kernel / the native driver
+        d = (self.host_dist[: t + 1].double() / native.FX_DIST).float() / float(self.N) < C.DIST_MIN_CHECK
         return bool(d.any(0).all())
 
     # ------------------------------------------------------------------ step
@@ -435,7 +450,8 @@ class HipEngine:
             #      step's h of the same pair; only unmatched pairs get an extra evaluation
             map1 = self.map1[:T]
             src = self.src[: 2 * E]
-            nev = native.cbf_match(self.idx[: T + G1], T, map1, src, self.mcnt, recomputed=not self.reuse)
+            nev = native.cbf_match(self.idx[: T + G1], T, map1, src, self.mcnt, recomputed=not self.reuse,
+                                   nev=self.nev_dev)
             hb, hm, dh = self.hbuf[: 2 * E], self.hmask[: 2 * E], self.dhbuf[: 2 * E]
             # the main slots [0, E) were evaluated during the rollout (overlap_hfwd): extras only
             native.cbf_hfwd(S, idx, idx if self.reuse else idx1, src, nev, pw.cbf_w, pw.cbf_off["w1f"],
@@ -446,7 +462,7 @@ class HipEngine:
             # backward over the evaluations with a nonzero upstream gradient only (exact: the
             # others contribute zeros); node_reduce reads dE where dh != 0
             act = self.act_list[: 2 * E]
-            nact = native.cbf_active(dh, nev, self.blk_active, act)
+            nact = native.cbf_active(dh, nev, self.blk_active, act, nact=self.nact_dev)
             native.cbf_bwd(S, idx, dh.view(2, T, B, N, K), pw.cbf_w, pw.cbf_off["w1f"], pw.cbf_rm, pw.cbf_v,
                            passes=2, dE=dE, partial=part_cbf, num_blocks=nbb, idx1=idx if self.reuse else idx1,
                            src=src, nev=nev, act=act, nact=nact, prec=self.prec)
@@ -478,8 +494,6 @@ class HipEngine:
             native.node_reduce(dE, rptr, redges, self.dS, **red)
         tm.mark("cbf")
         # ---- controller backward
-        self.part_node.zero_()
-        self.part_edge.zero_()
         if self.bptt:
             # BPTT through the rollout: G_t = dL/ds_t, reverse time
             rptr3 = rptr[: T * B].view(T, B, Nn + 1)
@@ -487,7 +501,7 @@ class HipEngine:
             Gp = self.bptt_groups
             if Gp == 1 and red_done is None and self.native_bptt:
                 # the reverse-time launch loop in C++ (csrc/runtime.cpp): same launches, same order
-                self._bdriver().run(T, gs, cur.cuda_stream)
+                self._bdriver().run(T, gs * ACT_COEF, cur.cuda_stream)
             elif Gp == 1:
                 self._bptt_chain(T, slice(0, B), valid_u8, gs, rptr3, redges3, self.part_node[: self.nb_node],
                                  self.part_edge[: self.nb_edge], self.nb_node, self.nb_edge, red_done, ts, cur)
@@ -515,14 +529,13 @@ class HipEngine:
             Gr[:TB].view(T, B, N, D).copy_(self.G.unsqueeze(0).expand(T, B, N, D))
             pn = self._buf(self._part_cbf_nb, ("n", nb_n), native.CTRL_NODE_PARTIAL)
             pe = self._buf(self._part_cbf_nb, ("e", nb_e), native.CTRL_EDGE_PARTIAL)
-            pn.zero_()
-            pe.zero_()
             native.ctrl_node_bwd(self.pooled[:T].view(TB, N, self.prow), self.S[:T].view(TB, Nn, W), Gr[:TB],
                                  self.A[:T].view(TB, N, D), self.dS[1: T + 1].view(TB, N, W), valid_u8.view(TB),
-                                 pw.ctrl_rm, pw.node_rm_off, pw.ctrl_v, gs, dP[:TB], None, pn, nb_n,
-                                 act_scale=self.act_scale, prec=self.prec)
+                                 pw.ctrl_rm, pw.node_rm_off, pw.ctrl_v, gs * ACT_COEF, dP[:TB], None, pn, nb_n,
+                                 act_cnt=self.counts[2:3], prec=self.prec, init=True)
             native.ctrl_edge_bwd(self.S[:T].view(TB, Nn, W), self.idx[:T].view(TB, N, K), self.argmax[:T].view(TB, N, 128),
-                                 dP[:TB], pw.ctrl_w, pw.ctrl_off["ew1f"], pw.ctrl_off["ew2tn"], None, pe, nb_e, prec=self.prec)
+                                 dP[:TB], pw.ctrl_w, pw.ctrl_off["ew1f"], pw.ctrl_off["ew2tn"], None, pe, nb_e, prec=self.prec,
+                                 init=True)
             self._nb_parts = (pn, pe)
         tm.mark("bptt")
         # ---- weight-gradient slabs -> flat grad
@@ -549,7 +562,7 @@ class HipEngine:
                    "argmax": (self.argmax, torch.uint8, (T, B, N, 128)),
                    "rptr": (self.rptr, torch.int32, ((T + G1) * B, Nn + 1)),
                    "redges": (self.redges, torch.int32, ((T + G1) * B, N * K)),
-                   "act_scale": (self.act_scale, torch.float32, (1,)), "dP": (self.dP, self.hdt, (B, N, self.prow)),
+                   "act_scale": (self.counts[2:3], torch.float32, (1,)), "dP": (self.dP, self.hdt, (B, N, self.prow)),
                    "ego": (self.ego, torch.float32, (B, N, W)), "dEc": (self.dEc, torch.float32, (B, N, K, W))}
             for name, (t, dt, shape) in exp.items():
                 native.check(t, dt, shape, name)
@@ -577,21 +590,20 @@ class HipEngine:
                 st.wait_event(red_done)                                # dS[0..ts) from the aux stream
             Gn = self.dS[T][sl] if t == T - 1 else self.Gb[t + 1][sl]   # G_T = dL/ds_T (direct terms only)
             native.ctrl_node_bwd(self.pooled[t][sl], self.S[t][sl], self.G[sl], self.A[t][sl], Gn, valid_u8[t][sl],
-                                 pw.ctrl_rm, pw.node_rm_off, pw.ctrl_v, gs, self.dP[sl], self.ego[sl],
-                                 part_node, nbn, act_scale=self.act_scale, prec=self.prec)
+                                 pw.ctrl_rm, pw.node_rm_off, pw.ctrl_v, gs * ACT_COEF, self.dP[sl], self.ego[sl],
+                                 part_node, nbn, act_cnt=self.counts[2:3], prec=self.prec, init=t == T - 1)
             native.ctrl_edge_bwd(self.S[t][sl], self.idx[t][sl], self.argmax[t][sl], self.dP[sl], pw.ctrl_w,
-                                 pw.ctrl_off["ew1f"], pw.ctrl_off["ew2tn"], self.dEc[sl], part_edge, nbe, prec=self.prec)
+                                 pw.ctrl_off["ew1f"], pw.ctrl_off["ew2tn"], self.dEc[sl], part_edge, nbe, prec=self.prec,
+                                 init=t == T - 1)
             if t > 0:      # G_0 = dL/ds_0 is not needed (s_0 is sampled, not a function of the weights)
                 native.node_combine(self.dS[t][sl], self.ego[sl], self.dEc[sl], rptr3[t][sl], redges3[t][sl], Gn,
                                     self.Gb[t][sl], K=K)
 
     def _counts_ready(self, work):
-        """Join the (async) count all-reduce, then the device-side action-loss coefficient
-        (read by ctrl_node_bwd: no host sync)."""
+        """Join the (async) count all-reduce (the node backward reads the action-loss count
+        counts[2] on the device: no host sync)."""
         if work is not None:
             work.wait()
-        n_act = self.counts[2].clamp_min(1.0)
-        torch.div(C.LOSS_SCALE * C.LOSS_WEIGHTS[4], n_act.view(1), out=self.act_scale)
 
     def _stats(self, raw, T):
         from ..utils.metrics import StepStats

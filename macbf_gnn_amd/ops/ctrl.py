@@ -51,14 +51,14 @@ class _CtrlFn(torch.autograd.Function):
         dev = S.device
         Gn = native.to_records(torch.cat([torch.zeros(B, N, D, device=dev), gA.float() / C.TIME_STEP], -1))
         nbn, nbe = native.ctrl_bwd_grids(B * N, dev)
-        # the controller kernels accumulate into their slabs (BPTT sums over steps): start at 0
-        pn = torch.zeros(nbn, native.CTRL_NODE_PARTIAL, dtype=torch.float32, device=dev)
-        pe = torch.zeros(nbe, native.CTRL_EDGE_PARTIAL, dtype=torch.float32, device=dev)
+        # one step: the kernels write their slabs (init) instead of accumulating
+        pn = torch.empty(nbn, native.CTRL_NODE_PARTIAL, dtype=torch.float32, device=dev)
+        pe = torch.empty(nbe, native.CTRL_EDGE_PARTIAL, dtype=torch.float32, device=dev)
         dP = torch.empty(B, N, L.pooled_row(mp.prec), dtype=w.dtype, device=dev)
         ego = torch.empty(B, N, W, dtype=torch.float32, device=dev)
         dEc = torch.empty(B, N, K, W, dtype=torch.float32, device=dev)
-        native.ctrl_node_bwd(pooled, S, G, A, Gn, None, rm, mp.rm_off, v, 0.0, dP, ego, pn, nbn, prec=mp.prec)
-        native.ctrl_edge_bwd(S, idx, am, dP, w, mp.off["ew1f"], mp.off["ew2tn"], dEc, pe, nbe, prec=mp.prec)
+        native.ctrl_node_bwd(pooled, S, G, A, Gn, None, rm, mp.rm_off, v, 0.0, dP, ego, pn, nbn, prec=mp.prec, init=True)
+        native.ctrl_edge_bwd(S, idx, am, dP, w, mp.off["ew1f"], mp.off["ew2tn"], dEc, pe, nbe, prec=mp.prec, init=True)
         gs = gg = None
         if ctx.needs_input_grad[1]:
             # goals only enter through p - g: dL/dg = -dL/d(p - g) of the node path

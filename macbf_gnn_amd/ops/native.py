@@ -257,9 +257,10 @@ def _records(t, name, lead, W, min_rows=None):
 
 
 def ctrl_fwd(S, G, idx, wpack, f_edge, f_node, wvec, A, Sn, dist_sum, act_sum, noise=None, pooled=None, argmax=None,
-             prec=None):
+             prec=None, noise_key=None, noise_prob=0.0, noise_scale=0.0, noise_t=0):
     """Fused controller step on per-step views: S/Sn (B,Nn,W) node records (agents first),
-    G (B,N,D), idx (B,N,K), A (B,N,D), dist_sum/act_sum (B,), pooled (B,N,128) bf16
+    G (B,N,D), idx (B,N,K), A (B,N,D), dist_sum/act_sum (B,) int64 fixed point (x FX_DIST /
+    x FX_ACT: order-independent integer atomics), pooled (B,N,128) bf16
     ((B,N,256) [hi | lo] rows for prec="fp32", required there), argmax (B,N,128) uint8."""
     B, N, K = idx.shape
     D = dim_of(S)
@@ -280,9 +281,10 @@ def ctrl_fwd(S, G, idx, wpack, f_edge, f_node, wvec, A, Sn, dist_sum, act_sum, n
     if f16 == 2 and pooled is None:
         raise NativeError("the fp32 (x3) controller step needs the pooled buffer")
     for t, n in ((dist_sum, "dist_sum"), (act_sum, "act_sum")):
-        if t is not None and (t.dtype != torch.float32 or tuple(t.shape) != (B,)):
-            raise NativeError(f"{n} must be float32 (B,)")
+        if t is not None and (t.dtype != torch.int64 or tuple(t.shape) != (B,)):
+            raise NativeError(f"{n} must be int64 (B,) fixed point")
     _rows(noise, D, "noise", (B, N))
+    check(noise_key, torch.int64, (1,), "noise_key")
     if pooled is not None:
         _rows(pooled, _prow(f16), "pooled", (B, N))
         _same_half(pooled, wpack, "pooled")
@@ -300,7 +302,8 @@ def ctrl_fwd(S, G, idx, wpack, f_edge, f_node, wvec, A, Sn, dist_sum, act_sum, n
                         float(C.TIME_STEP), float(C.OBS_RADIUS), float(C.SQRT3),
                         ptr(pooled), pooled.stride(0) if pooled is not None else 0,
                         ptr(argmax), argmax.stride(0) if argmax is not None else 0,
-                        D, num_cu(S.device), f16, ctrl_fwd_apw(B * N, S.device, N), stream_handle())
+                        D, num_cu(S.device), f16, ctrl_fwd_apw(B * N, S.device, N),
+                        ptr(noise_key), float(noise_prob), float(noise_scale), int(noise_t), stream_handle())
     _ok(rc, "ctrl_fwd")
 
 
@@ -375,14 +378,18 @@ def cbf_fwd(S, idx, wpack, f_fwd, wvec, *, dang=None, valid=None, two=True, h_ou
 
 
 # ----------------------------------------------------------------------------- deduplicated h / h'
-def cbf_match(idx, T, map1, src, cnt, *, recomputed=False):
+MATCH_BLOCK = 256
+
+
+def cbf_match(idx, T, map1, src, cnt, *, recomputed=False, nev=None):
     """Deduplicate the h / h' evaluations of a rollout (csrc/dedup.hip).
 
     idx (>= T + recomputed, B, N, K) int32 neighbour slots. Writes map1 (T, B, N, K): the
     evaluation index of each slot's h' partner (< E: the next step's main slot with the same
     neighbour; >= E: an extra evaluation) and src (2E): the slot whose h' evaluation u is, or
-    -1. cnt: (>= T*B*N) int32 scratch. Returns the device int32 tensor [U] (evaluations).
-    Stream-ordered, no host synchronisation."""
+    -1. cnt: int32 scratch (>= one entry per 256-row block). Returns the device int32 tensor
+    [U] (evaluations; written into `nev` when given). Two launches, the exclusive scan of the
+    per-row extras counts runs inside the kernels; stream-ordered, no host synchronisation."""
     _, B, N, K = idx.shape
     if idx.shape[0] < T + int(recomputed):
         raise NativeError("idx has too few steps")
@@ -393,17 +400,17 @@ def cbf_match(idx, T, map1, src, cnt, *, recomputed=False):
     check(map1, torch.int32, (T, B, N, K), "map1")
     check(src, torch.int32, (2 * E,), "src")
     rows = T * B * N
+    nblk = (rows + MATCH_BLOCK - 1) // MATCH_BLOCK
     check(cnt, torch.int32, None, "cnt")
-    if cnt.numel() < rows:
+    if cnt.numel() < nblk:
         raise NativeError("cnt too small")
-    c = cnt[:rows]
+    if nev is None:
+        nev = torch.empty(1, dtype=torch.int32, device=idx.device)
+    check(nev, torch.int32, (1,), "nev")
     mode = 1 if recomputed else 0
-    _ok(lib().cbf_match(ptr(idx), T, B, N, K, mode, 0, ptr(c), 0, 0, 0, stream_handle()), "cbf_match/count")
-    incl = torch.cumsum(c, 0, dtype=torch.int32)
-    off = (incl - c).contiguous()
-    nev = (incl[-1:] + E).contiguous()
-    _ok(lib().cbf_match(ptr(idx), T, B, N, K, mode, 1, 0, ptr(off), ptr(map1), ptr(src), stream_handle()),
-        "cbf_match/fill")
+    _ok(lib().cbf_match(ptr(idx), T, B, N, K, mode, 0, 0, 0, 0, 0, ptr(cnt), 0, stream_handle()), "cbf_match/count")
+    _ok(lib().cbf_match(ptr(idx), T, B, N, K, mode, 1, 0, 0, ptr(map1), ptr(src), ptr(cnt), ptr(nev),
+                        stream_handle()), "cbf_match/fill")
     return nev
 
 
@@ -490,18 +497,21 @@ def cbf_dh(h, hmask, map1, src, nev, dang, valid, counts, dh, partial, *, grad_s
                      ptr(blk_active), nb, stream_handle()), "cbf_dh")
 
 
-def cbf_active(dh, nev, blk_active, act):
+def cbf_active(dh, nev, blk_active, act, nact=None):
     """Stable list of the evaluations with dh != 0 (cbf_dh's per-block counts blk_active, same
-    grid): act[:nact] in index order. Returns the device int32 tensor [nact]. The backward skips
-    the rest: their upstream gradient, hence every contribution, is exactly zero."""
+    grid): act[:nact] in index order. Returns the device int32 tensor [nact] (written into
+    `nact` when given; block offsets are scanned in-kernel, one launch). The backward skips the
+    rest: their upstream gradient, hence every contribution, is exactly zero."""
     check(dh, torch.float32, None, "dh")
     check(nev, torch.int32, (1,), "nev")
     check(blk_active, torch.int32, None, "blk_active")
     check(act, torch.int32, (dh.numel(),), "act")
-    incl = torch.cumsum(blk_active, 0, dtype=torch.int32)
-    off = (incl - blk_active).contiguous()
-    _ok(lib().cbf_compact(ptr(dh), ptr(nev), ptr(off), ptr(act), blk_active.numel(), stream_handle()), "cbf_compact")
-    return incl[-1:].contiguous()
+    if nact is None:
+        nact = torch.empty(1, dtype=torch.int32, device=dh.device)
+    check(nact, torch.int32, (1,), "nact")
+    _ok(lib().cbf_compact(ptr(dh), ptr(nev), 0, ptr(act), blk_active.numel(), ptr(blk_active), ptr(nact),
+                          stream_handle()), "cbf_compact")
+    return nact
 
 
 def cbf_bwd_grid(EV: int, device) -> int:
@@ -662,9 +672,11 @@ def ctrl_bwd_grids(total_agents: int, device):
 
 
 def ctrl_node_bwd(pooled, S, G, A, Gn, valid_t, wrm, offs, wvec, act_coef, dP, ego, partial, num_blocks,
-                  act_scale=None, prec=None):
-    """act_scale: optional 1-element device tensor; the action-loss coefficient is then
-    act_coef * act_scale[0], read by the kernel (no host round trip)."""
+                  act_cnt=None, prec=None, init=False):
+    """act_cnt: optional 1-element device tensor holding the (all-reduced) action-loss count
+    n_act; the action-loss coefficient is then act_coef / max(n_act, 1), read by the kernel (no
+    host round trip, no extra launch). init: write the weight-gradient slabs instead of
+    accumulating into them (no zero fill needed)."""
     B, N = G.shape[:2]
     D = dim_of(S)
     W = rec_width(D)
@@ -683,17 +695,17 @@ def ctrl_node_bwd(pooled, S, G, A, Gn, valid_t, wrm, offs, wvec, act_coef, dP, e
     _same_half(pooled, wrm, "pooled")
     check(ego, torch.float32, (B, N, W), "ego")
     check(partial, torch.float32, (num_blocks, CTRL_NODE_PARTIAL), "partial")
-    check(act_scale, torch.float32, (1,), "act_scale")
+    check(act_cnt, torch.float32, (1,), "act_cnt")
     rc = lib().ctrl_node_bwd(ptr(pooled), pooled.stride(0), ptr(S), S.stride(0) // W, ptr(G), ptr(A), A.stride(0) // D,
                              ptr(Gn), Gn.stride(0) // W if Gn is not None else 0,
                              ptr(valid_t), valid_t.stride(0) if valid_t is not None else 0, B, N,
                              ptr(wrm), offs["w1"], offs["w2"], offs["w3"], offs["w4"], ptr(wvec),
-                             float(act_coef), ptr(act_scale), float(C.TIME_STEP), float(C.SQRT3), ptr(dP), dP.stride(0),
-                             ptr(ego), ptr(partial), D, int(num_blocks), f16, stream_handle())
+                             float(act_coef), ptr(act_cnt), float(C.TIME_STEP), float(C.SQRT3), ptr(dP), dP.stride(0),
+                             ptr(ego), ptr(partial), D, int(num_blocks), f16, int(bool(init)), stream_handle())
     _ok(rc, "ctrl_node_bwd")
 
 
-def ctrl_edge_bwd(S, idx, argmax, dP, wpack, f_ew1f, f_ew2tn, dEc, partial, num_blocks, prec=None):
+def ctrl_edge_bwd(S, idx, argmax, dP, wpack, f_ew1f, f_ew2tn, dEc, partial, num_blocks, prec=None, init=False):
     B, N, K = idx.shape
     D = dim_of(S)
     W = rec_width(D)
@@ -710,7 +722,7 @@ def ctrl_edge_bwd(S, idx, argmax, dP, wpack, f_ew1f, f_ew2tn, dEc, partial, num_
     rc = lib().ctrl_edge_bwd(ptr(S), S.stride(0) // W, ptr(idx), idx.stride(0), ptr(argmax), argmax.stride(0),
                              ptr(dP), dP.stride(0), B, N, K, ptr(wpack), int(f_ew1f), int(f_ew2tn), ptr(dEc),
                              dEc.stride(0) // W if dEc is not None else 0, ptr(partial), D, int(num_blocks),
-                             f16, ctrl_edge_qsplit(B * N, S.device), stream_handle())
+                             f16, ctrl_edge_qsplit(B * N, S.device), int(bool(init)), stream_handle())
     _ok(rc, "ctrl_edge_bwd")
 
 
@@ -723,15 +735,19 @@ def reduce_rows(partial, out, accumulate=False):
     _ok(lib().reduce_rows(ptr(partial), rows, cols, ptr(out), int(accumulate), stream_handle()), "reduce_rows")
 
 
+FX_DIST = 2.0 ** 32           # csrc/args.h: fixed-point scales of the per-env rollout sums
+FX_ACT = 2.0 ** 24
+
+
 def rollout_stats(dist, cnt, safe, act, valid, counts, local, *, N):
     """dist/act (T,B), cnt (T,B,2), safe (T+1,B) or None -> valid (T,B) u8, counts[:3] =
     [n_dang, n_safe, n_act] of this rank, local[:3] = [agent-steps, safe agents of s_{t+1},
     action-loss sum]. One launch, deterministic."""
     T, B = dist.shape
-    check(dist, torch.float32, (T, B), "dist")
+    check(dist, torch.int64, (T, B), "dist")
     check(cnt, torch.float32, (T, B, 2), "cnt")
     check(safe, torch.float32, (T + 1, B), "safe")
-    check(act, torch.float32, (T, B), "act")
+    check(act, torch.int64, (T, B), "act")
     check(valid, torch.uint8, (T, B), "valid")
     check(counts, torch.float32, None, "counts")
     check(local, torch.float32, None, "local")

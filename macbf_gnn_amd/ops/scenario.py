@@ -20,6 +20,12 @@ def _mix(*xs) -> int:
     return h
 
 
+def iteration_key(seed, iteration, rank, salt=0) -> int:
+    """Signed 64-bit counter-based RNG key of (seed, iteration, rank[, salt]) (device int64)."""
+    k = _mix(seed, iteration, rank, salt) if salt else _mix(seed, iteration, rank)
+    return k - (1 << 64) if k >= (1 << 63) else k
+
+
 def obstacles(B, N, *, dim, num_obstacles, points, seed, device):
     """(B, num_obstacles*points, D) static point-set obstacles with the shapes of
     ``env.generate_obstacles`` (2-D: alternating circles / rectangles, 3-D: spheres), from the

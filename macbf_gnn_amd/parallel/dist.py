@@ -11,6 +11,10 @@ this framework are exactly:
    a latency-bound message on xGMI, so it is issued as a single call (no bucketing);
 3. ``broadcast`` of the initial flat parameters from rank 0 (once);
 4. ``all_reduce(SUM)`` of a small metrics vector at display steps.
+
+``MACBF_DP_FORCE_PG=1`` initialises the process group even at world size 1, so every collective
+of a single-GPU run really goes through RCCL on the HIP stream (the RCCL-path test at world 1,
+tests/test_gpu_dp.py); with the default, world 1 short-circuits every collective.
 """
 from __future__ import annotations
 
@@ -26,6 +30,15 @@ def env_world():
         int(os.environ.get("LOCAL_RANK", "0"))
 
 
+def _free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
 class DP:
     """Thin data-parallel context. ``world == 1`` makes every collective a no-op."""
 
@@ -33,7 +46,12 @@ class DP:
         self.world, self.rank, self.local_rank = env_world()
         self.device = device
         self.owns_pg = False
-        if self.world > 1 and not dist.is_initialized():
+        self.forced = os.environ.get("MACBF_DP_FORCE_PG", "0") == "1"
+        if (self.world > 1 or self.forced) and not dist.is_initialized():
+            if self.world == 1:      # a standalone single-process group (no launcher)
+                os.environ.setdefault("RANK", "0")
+                os.environ.setdefault("WORLD_SIZE", "1")
+                os.environ.setdefault("MASTER_PORT", str(_free_port()))
             if backend is None:
                 # MACBF_DP_BACKEND=gloo rehearses multi-rank runs with several ranks sharing one
                 # GPU (RCCL places one rank per device)
@@ -51,7 +69,11 @@ class DP:
 
     @property
     def enabled(self):
-        return self.world > 1
+        return self.world > 1 or (self.forced and dist.is_initialized())
+
+    @property
+    def backend(self) -> str | None:
+        return dist.get_backend() if dist.is_initialized() else None
 
     def all_reduce_(self, t: torch.Tensor) -> torch.Tensor:
         if self.enabled:

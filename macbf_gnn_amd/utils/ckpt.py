@@ -42,8 +42,17 @@ def save(trainer, path: str):
     os.replace(tmp, path)
 
 
+# architecture-defining config entries a resumed checkpoint must agree on
+ARCH_KEYS = ("dim", "top_k", "num_obstacles", "obstacle_points")
+
+
 def load(trainer, path: str, strict: bool = True):
     ck = torch.load(path, map_location="cpu", weights_only=True)
+    saved = ck.get("config") if isinstance(ck.get("config"), dict) else {}
+    for k in ARCH_KEYS:
+        if k in saved and hasattr(trainer.cfg, k) and saved[k] != getattr(trainer.cfg, k):
+            raise ValueError(f"checkpoint {path} was written with {k}={saved[k]!r}, "
+                             f"the current run has {k}={getattr(trainer.cfg, k)!r}")
     if "controller" in ck or "cbf" in ck:
         if "controller" in ck:
             _load_module(trainer.controller, ck["controller"], strict)
@@ -70,14 +79,23 @@ def load(trainer, path: str, strict: bool = True):
 
 
 def _load_module(mod, sd, strict):
+    """Copy a state_dict into `mod`. Shapes must match exactly (a same-size tensor of another
+    layout -- transposed, another in_dim -- would load as garbage); strict also rejects missing
+    and unexpected keys."""
     with torch.no_grad():
         own = dict(mod.named_parameters())
         missing = [k for k in own if k not in sd]
         if strict and missing:
             raise KeyError(f"missing keys {missing}")
+        if strict:
+            unexpected = [k for k in sd if k not in own]
+            if unexpected:
+                raise KeyError(f"unexpected keys {unexpected}")
         for k, p in own.items():
             if k in sd:
-                p.copy_(sd[k].to(p.dtype).reshape(p.shape))
+                if tuple(sd[k].shape) != tuple(p.shape):
+                    raise ValueError(f"{k}: checkpoint shape {tuple(sd[k].shape)} != parameter shape {tuple(p.shape)}")
+                p.copy_(sd[k].to(p.dtype))
 
 
 def load_models(path: str, controller, cbf, strict: bool = True):

@@ -37,7 +37,7 @@ eng = tr.engine
 s0, g, obs = tr.sample()
 T = eng.rollout(s0, g, obs)
 B, N, K, W = eng.B, eng.N, eng.K, eng.W
-done = (eng.dist[:T] / N) < C.DIST_MIN_CHECK
+done = (eng.dist[:T].double() / native.FX_DIST / N) < C.DIST_MIN_CHECK
 di = done.to(torch.int32)
 valid = ((torch.cumsum(di, 0) - di) == 0).to(torch.uint8).contiguous()
 vf = valid.float()

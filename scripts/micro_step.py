@@ -19,6 +19,7 @@ ap.add_argument("--iters", type=int, default=50)
 ap.add_argument("--t", type=int, default=8)
 ap.add_argument("--agents", type=int, default=1024)
 ap.add_argument("--envs", type=int, default=64)
+ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16", "fp16"])
 args = ap.parse_args()
 import torch  # noqa: E402
 
@@ -34,7 +35,8 @@ from macbf_gnn_amd.ops import native  # noqa: E402
 from macbf_gnn_amd.parallel import DP  # noqa: E402
 
 dev = torch.device("cuda")
-cfg = C.TrainConfig(num_agents=args.agents, num_envs=args.envs, inner_loops=50, device="hip", seed=0)
+cfg = C.TrainConfig(num_agents=args.agents, num_envs=args.envs, inner_loops=50, device="hip", seed=0,
+                    dtype=args.dtype)
 tr = Trainer(cfg, device=dev, dp=DP(device=dev))
 eng = tr.engine
 for _ in range(2):
@@ -74,25 +76,26 @@ def k_scan_safeonly():
 
 def k_fwd():
     native.ctrl_fwd(eng.S[t], eng.G, eng.idx[t], pw.ctrl_w, pw.ctrl_off["ew1f"], pw.ctrl_off["nw1f"], pw.ctrl_v,
-                    eng.A[t], eng.S[t + 1], eng.dist[t], eng.act[t], pooled=eng.pooled[t], argmax=eng.argmax[t])
+                    eng.A[t], eng.S[t + 1], eng.dist[t], eng.act[t], pooled=eng.pooled[t], argmax=eng.argmax[t],
+                    prec=eng.prec)
 
 
 def k_node():
     native.ctrl_node_bwd(eng.pooled[t], eng.S[t], eng.G, eng.A[t], eng.Gb[t + 1], valid, pw.ctrl_rm,
                          pw.node_rm_off, pw.ctrl_v, 1.0, eng.dP, eng.ego, eng.part_node, eng.nb_node,
-                         act_scale=eng.act_scale)
+                         act_cnt=eng.counts[2:3], prec=eng.prec)
 
 
 def k_edge():
     native.ctrl_edge_bwd(eng.S[t], eng.idx[t], eng.argmax[t], eng.dP, pw.ctrl_w, pw.ctrl_off["ew1f"],
-                         pw.ctrl_off["ew2tn"], eng.dEc, eng.part_edge, eng.nb_edge)
+                         pw.ctrl_off["ew2tn"], eng.dEc, eng.part_edge, eng.nb_edge, prec=eng.prec)
 
 
 def k_comb():
     native.node_combine(eng.dS[t], eng.ego, eng.dEc, rptr, redges, eng.Gb[t + 1], eng.Gb[t], K=K)
 
 
-out = {"tag": args.tag}
+out = {"tag": args.tag, "dtype": args.dtype}
 for name, fn in (("scan", k_scan), ("scan_nosort", k_scan_nosort), ("scan_noprev", k_scan_noprev), ("scan_nosafe", k_scan_nosafe), ("scan_safeonly", k_scan_safeonly), ("ctrl_fwd", k_fwd), ("node_bwd", k_node), ("edge_bwd", k_edge),
                  ("combine", k_comb)):
     for _ in range(3):

@@ -68,3 +68,45 @@ def test_hip_dp_grad_equals_single_process(tmp_path):
     assert torch.isfinite(ref).all() and ref.abs().sum() > 0
     # same per-edge arithmetic, different slab partitions: fp32 summation-order differences only
     torch.testing.assert_close(g0, ref, rtol=2e-3, atol=1e-6)
+
+
+def _forced_worker(rank, outdir, steps):
+    """One process, world size 1, MACBF_DP_FORCE_PG=1: the process group is RCCL (nccl) and every
+    collective (parameter broadcast, async count all-reduce + wait, gradient all-reduce,
+    barrier(device_ids), max_scalar) runs through it."""
+    os.environ.update({"MACBF_DP_FORCE_PG": "1", "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(_free_port()),
+                       "RANK": "0", "WORLD_SIZE": "1", "LOCAL_RANK": "0"})
+    import torch.distributed as dist
+    from macbf_gnn_amd.engine import Trainer
+    from macbf_gnn_amd.parallel import DP
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dp = DP(device=dev)
+    assert dist.is_initialized() and dist.get_backend() == "nccl" and dp.enabled
+    tr = Trainer(_cfg(BTOT), device=dev, dp=dp)
+    for _ in range(steps):
+        tr.train_step()
+    dp.barrier()
+    t = dp.max_scalar(1.5)
+    assert t == 1.5
+    torch.cuda.synchronize()
+    torch.save({"flat": tr.fp.flat.cpu(), "backend": dist.get_backend()}, os.path.join(outdir, "forced.pt"))
+    dp.shutdown()
+
+
+@pytest.mark.timeout(300)
+def test_forced_rccl_group_world1_bit_identical(tmp_path):
+    """RCCL path at world size 1: parameters after 3 training steps with every
+    collective issued through an nccl process group == the no-group run, bit for bit."""
+    steps = 3
+    mp.start_processes(_forced_worker, args=(str(tmp_path), steps), nprocs=1, join=True, start_method="spawn")
+    got = torch.load(tmp_path / "forced.pt", weights_only=True)
+    assert got["backend"] == "nccl"
+    from macbf_gnn_amd.engine import Trainer
+    from macbf_gnn_amd.parallel import DP
+    dev = torch.device("cuda", 0)
+    tr = Trainer(_cfg(BTOT), device=dev, dp=DP(device=dev))
+    for _ in range(steps):
+        tr.train_step()
+    torch.cuda.synchronize()
+    assert torch.equal(got["flat"], tr.fp.flat.cpu())

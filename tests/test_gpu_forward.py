@@ -127,8 +127,8 @@ def test_ctrl_fwd_matches_oracle(B, N):
     idx = O.knn_idx(s, K).to(torch.int32).contiguous()
     A = torch.empty(B, N, 2, device=DEV)
     Sn = torch.empty(B, N, 4, device=DEV)
-    dsum = torch.zeros(B, device=DEV)
-    asum = torch.zeros(B, device=DEV)
+    dsum = torch.zeros(B, dtype=torch.int64, device=DEV)     # fixed point (native.FX_DIST / FX_ACT)
+    asum = torch.zeros(B, dtype=torch.int64, device=DEV)
     native.ctrl_fwd(s, g, idx, pw.ctrl_w, pw.ctrl_off["ew1f"], pw.ctrl_off["nw1f"], pw.ctrl_v, A, Sn, dsum, asum)
     torch.cuda.synchronize()
     with torch.no_grad():
@@ -139,6 +139,8 @@ def test_ctrl_fwd_matches_oracle(B, N):
     # Euler step consistent with the emitted action
     sn_ref = s + torch.cat([s[..., 2:], A], -1) * C.TIME_STEP
     torch.testing.assert_close(Sn, sn_ref, rtol=1e-6, atol=1e-6)
+    dsum = (dsum.double() / native.FX_DIST).float()
+    asum = (asum.double() / native.FX_ACT).float()
     torch.testing.assert_close(dsum, torch.linalg.norm(Sn[..., :2] - g, dim=-1).sum(-1), rtol=1e-4, atol=1e-4)
     act_ref = O.action_loss_terms(s, g, A).sum(-1)
     torch.testing.assert_close(asum, act_ref, rtol=1e-4, atol=1e-3)

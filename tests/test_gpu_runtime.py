@@ -105,3 +105,60 @@ def test_strided_early_stop_check_same_horizon(every):
     assert a[0] == b[0] < tr.cfg.inner_loops
     for x, y in zip(a[1:], b[1:]):
         assert torch.equal(x, y)
+
+
+def test_device_exploration_noise():
+    """Exploration noise (reference train.py:65-67) from the counter-based device RNG: the native
+    driver and the Python loop draw the same noise; one coin per (env, step), N(0, scale^2)
+    per (agent, axis); deterministic per iteration, fresh across iterations; graph mode runs it."""
+    tr = _trainer(T=6, N=256, B=8, add_noise_prob=0.5, noise_scale=0.3)
+    s0, g, _ = tr.sample()
+    a = _rollout(tr, False, s0, g, False)
+    b = _rollout(tr, True, s0, g, False)
+    for x, y in zip(a[1:], b[1:]):
+        assert torch.equal(x, y)
+    # noise-free reference of the same first step: the difference is the noise of step 0
+    tr0 = _trainer(T=6, N=256, B=8)
+    tr0.fp.flat.copy_(tr.fp.flat)
+    tr0.engine.after_update()
+    c = _rollout(tr0, True, s0, g, False)
+    d = (a[3][0] - c[3][0])                                  # (B, N, D) noise of step 0
+    noisy = d.abs().amax(dim=(1, 2)) > 0
+    assert 0 < int(noisy.sum()) < 8                          # coin per env (p = 0.5, 8 envs)
+    z = d[noisy].flatten() / 0.3
+    assert abs(z.mean().item()) < 0.1 and abs(z.std().item() - 1.0) < 0.1
+    assert torch.all(d[~noisy] == 0)
+    # next iteration: different draws
+    tr.step_count += 1
+    e = _rollout(tr, True, s0, g, False)
+    assert not torch.equal(e[3], b[3])
+    tr.step_count -= 1
+    f = _rollout(tr, True, s0, g, False)
+    assert torch.equal(f[3], b[3])
+
+
+def test_graph_mode_with_noise_matches_eager():
+    tr_e = _trainer(T=8, N=32, B=3, add_noise_prob=1.0, early_stop=False)
+    tr_g = _trainer(T=8, N=32, B=3, add_noise_prob=1.0, early_stop=False, graph=True)
+    tr_g.fp.flat.copy_(tr_e.fp.flat)
+    tr_g.engine.after_update()
+    s0, g, _ = tr_e.sample(0)
+    tr_e.engine.step(s0, g)
+    tr_g.engine.step(s0, g)
+    torch.cuda.synchronize()
+    torch.testing.assert_close(tr_g.fp.grad, tr_e.fp.grad, rtol=1e-5, atol=1e-7)
+
+
+def test_rollout_sums_order_independent_at_1024_agents():
+    """Per-env goal-distance / action sums of 1024-agent envs (32 waves per env) are fixed-point
+    integer atomics: repeated rollouts give bit-identical sums and the same horizon (the early-
+    stop input must not depend on the order in which waves finish)."""
+    tr = _trainer(N=1024, B=4, T=25)
+    tr.engine.check_every = 1
+    s0, g, _ = tr.sample()
+    runs = [_rollout(tr, True, s0, g, True) for _ in range(3)]
+    for r in runs[1:]:
+        assert r[0] == runs[0][0]
+        for x, y in zip(r[1:], runs[0][1:]):
+            assert torch.equal(x, y)
+    assert torch.equal(tr.engine.act[: runs[0][0]], tr.engine.act[: runs[0][0]])

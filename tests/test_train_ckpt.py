@@ -147,3 +147,28 @@ def test_fit_resume_runs_to_total_train_steps(tmp_path):
     t2.fit()
     assert t2.step_count == 5
     assert mk(5).step_count == 5
+
+
+def test_checkpoint_rejects_mismatched_layouts(tmp_path):
+    """Same element count, other shape (a transposed weight) and an architecture change on resume
+    are errors, not silent garbage loads; strict loading rejects unexpected keys."""
+    import pytest
+    from macbf_gnn_amd.models import CBF, Controller
+    torch.manual_seed(3)
+    c, f = Controller(4), CBF(4)
+    sd = dict(c.state_dict())
+    w = sd["controller_dec_net.2.weight"]                      # (128, 64)
+    sd["controller_dec_net.2.weight"] = w.t().contiguous()     # (64, 128): same numel
+    torch.save({"controller": sd, "cbf": f.state_dict()}, tmp_path / "bad_shape.pt")
+    with pytest.raises(ValueError, match="shape"):
+        ckpt.load(_tr(), str(tmp_path / "bad_shape.pt"))
+    sd2 = dict(c.state_dict())
+    sd2["controller_extra.weight"] = torch.zeros(3)
+    torch.save({"controller": sd2}, tmp_path / "extra.pt")
+    with pytest.raises(KeyError, match="unexpected"):
+        ckpt.load(_tr(), str(tmp_path / "extra.pt"))
+    ckpt.load(_tr(), str(tmp_path / "extra.pt"), strict=False)        # non-strict: ignored
+    a = _tr(N=10, B=1, T=4)
+    a.save(str(tmp_path / "k12.pt"))
+    with pytest.raises(ValueError, match="top_k"):
+        ckpt.load(_tr(N=10, B=1, T=4, top_k=8), str(tmp_path / "k12.pt"))
