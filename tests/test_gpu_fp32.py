@@ -343,3 +343,29 @@ def test_module_api_fp32_default():
     _cmp(h.detach(), href.detach(), "h", 1e-4)
     _cmp_nodes(sx.grad, gr[0], "dL/ds", 1e-3)
     _cmp_nodes(g.grad, gr[1], "dL/dg", 1e-3)
+
+
+def test_training_parity_fp32_vs_oracle():
+    """60 training iterations of the fp32 HIP engine and of autograd through the fp32 oracle from
+    the same initial weights on the same scenarios (each applies its own gradients): the loss
+    curves agree to 1e-3 and the parameters stay within 1e-3 relative distance
+    (scripts/parity_run.py: 200 iterations, profiles/r2_parity/)."""
+    from macbf_gnn_amd.engine import Trainer
+    from macbf_gnn_amd.engine.oracle_engine import OracleEngine
+    from macbf_gnn_amd.parallel import DP
+
+    def make(oracle):
+        cfg = C.TrainConfig(num_agents=32, num_envs=8, inner_loops=C.INNER_LOOPS, device="hip", seed=0,
+                            dtype="fp32", prefetch_data=False)
+        tr = Trainer(cfg, device=DEV, dp=DP(device=DEV))
+        if oracle:
+            tr.engine = OracleEngine(tr)
+        return tr
+
+    hip, orc = make(False), make(True)
+    for it in range(60):
+        a = float(hip.train_step()["loss_total"])
+        b = float(orc.train_step()["loss_total"])
+        assert abs(a - b) <= 1e-3 * abs(b), (it, a, b)
+    d = float((hip.fp.flat.double() - orc.fp.flat.double()).norm() / orc.fp.flat.double().norm())
+    assert d <= 1e-3, d
