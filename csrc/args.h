@@ -34,6 +34,7 @@ struct ScanArgs {
   float r2_train, ttc_train, r2_check, ttc_check;
   int do_knn, do_safety;
   const int* prev_idx; long pi_env;  // previous step's kNN (b,i,k) (or null): temporal K-th bound
+  float4* ws; long ws_env;           // Nn > 4096: per-env global staging (float4s per env), else null
 };
 
 struct ScenArgs {
@@ -46,6 +47,7 @@ struct ScenArgs {
   unsigned long long seed;
   int max_rounds;
   int* status;    // per env: rounds used for goals (or -1 if max_rounds hit)
+  unsigned char* ws; long ws_env;   // envs too large for LDS: per-env global workspace (bytes), else null
 };
 
 struct CtrlArgs {

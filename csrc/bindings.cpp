@@ -25,8 +25,10 @@ static int cell_sort(u64 S, long s_env, int B, int N, float L, u64 perm, int rec
 
 static int scan(u64 S, long s_env, u64 perm, int B, int N, int K, u64 idx, long i_env, u64 dang, u64 cnt, long c_env,
                 u64 safe, long sf_env, float r2_train, float ttc_train, float r2_check, float ttc_check,
-                int do_knn, int do_safety, int Nn, int dim, u64 prev_idx, long pi_env, u64 stream) {
+                int do_knn, int do_safety, int Nn, int dim, u64 prev_idx, long pi_env, u64 ws, long ws_env,
+                u64 stream) {
   mb::ScanArgs a{};
+  a.ws = P<float4>(ws); a.ws_env = ws_env;
   a.prev_idx = P<const int>(prev_idx); a.pi_env = pi_env;
   a.Nn = Nn; a.dim = dim;
   a.S = P<const float4>(S); a.s_env = s_env; a.perm = P<const int>(perm); a.B = B; a.N = N; a.K = K;
@@ -38,8 +40,9 @@ static int scan(u64 S, long s_env, u64 perm, int B, int N, int K, u64 idx, long 
 }
 
 static int scenario(u64 S, long s_env, u64 G, u64 obs, int M, int dim, int B, int N, float L, float r, float spread,
-                    u64 seed, int max_rounds, u64 status, u64 stream) {
+                    u64 seed, int max_rounds, u64 status, u64 ws, long ws_env, u64 stream) {
   mb::ScenArgs a{};
+  a.ws = P<unsigned char>(ws); a.ws_env = ws_env;
   a.S = P<float4>(S); a.s_env = s_env; a.G = P<float>(G); a.obs = P<const float>(obs); a.M = M; a.dim = dim;
   a.B = B; a.N = N; a.L = L; a.r = r; a.spread = spread;
   a.seed = seed; a.max_rounds = max_rounds; a.status = P<int>(status);

@@ -592,33 +592,38 @@ DEV void store_pk_sw(h16* img, int erow, int col0, const Pk& v, int h, int lo) {
 }
 
 // stage_mma with split operands: A = imgA (+loA), B = imgB (+loB); BX: B exact (no lo plane).
-// Bias row sums of A cover both planes.
+// Bias row sums of A cover both planes. x3: fully unrolled (ES <= 8 here) so every fragment read
+// has an immediate LDS offset, double-buffered fragments (no register copies), the fragments of
+// step ks+2 requested right after the three MFMAs of step ks have read their operands.
 template <int ES, bool BX = false>
 DEV float stage_mma_fr(const h16* imgA, int sA, int loA, const h16* imgB, int sB, int loB, int mt, int nt, int lane,
                        f32x16& acc, int bs_lo = 0, int bs_hi = 0) {
   if constexpr (!X3) {
     return stage_mma<ES>(imgA, sA, imgB, sB, mt, nt, lane, acc, bs_lo, bs_hi);
   } else {
+    static_assert(ES % 2 == 0 && ES <= 16, "even edge-step count");
     bs_lo = __builtin_amdgcn_readfirstlane(bs_lo);
     bs_hi = __builtin_amdgcn_readfirstlane(bs_hi);
     float s = 0.f;
-#pragma nounroll
-    for (int ks = 0; ks < ES; ++ks) {
-      Fr a, b;
-      a.h = tr_frag(imgA, sA, 16 * ks, 32 * mt, lane);
-      a.l = tr_frag(imgA + loA, sA, 16 * ks, 32 * mt, lane);
-      b.h = tr_frag(imgB, sB, 16 * ks, 32 * nt, lane);
-      if constexpr (BX) {
-        acc = mma_bx(a, b.h, acc);
-      } else {
-        b.l = tr_frag(imgB + loB, sB, 16 * ks, 32 * nt, lane);
-        acc = mma(a, b, acc);
-      }
+    Fr a[2], b[2];
+    auto ld = [&](int ks, Fr& x, Fr& y) {
+      x.h = tr_frag(imgA, sA, 16 * ks, 32 * mt, lane);
+      x.l = tr_frag(imgA + loA, sA, 16 * ks, 32 * mt, lane);
+      y.h = tr_frag(imgB, sB, 16 * ks, 32 * nt, lane);
+      if constexpr (!BX) y.l = tr_frag(imgB + loB, sB, 16 * ks, 32 * nt, lane);
+    };
+    ld(0, a[0], b[0]);
+    ld(1, a[1], b[1]);
+    static_for<ES>([&](auto ks_) {
+      constexpr int ks = decltype(ks_)::value, sl = ks & 1;
+      if constexpr (BX) acc = mma_bx(a[sl], b[sl].h, acc);
+      else acc = mma(a[sl], b[sl], acc);
       if (ks >= bs_lo && ks < bs_hi) {
-        s = dot_sum8(a.l, s);
-        s = dot_sum8(a.h, s);
+        s = dot_sum8(a[sl].l, s);
+        s = dot_sum8(a[sl].h, s);
       }
-    }
+      if constexpr (ks + 2 < ES) ld(ks + 2, a[sl], b[sl]);
+    });
     return s;
   }
 }
@@ -629,27 +634,30 @@ DEV float stage_mma_sw_fr(const h16* imgA, int loA, const h16* imgB, int loB, in
   if constexpr (!X3) {
     return stage_mma_sw<ES, WA, WB>(imgA, imgB, mt, nt, lane, acc, bs_lo, bs_hi);
   } else {
+    static_assert(ES % 2 == 0 && ES <= 16, "even edge-step count");
     bs_lo = __builtin_amdgcn_readfirstlane(bs_lo);
     bs_hi = __builtin_amdgcn_readfirstlane(bs_hi);
     const TrOff oa = tr_off_sw<WA>(32 * mt, lane), ob = tr_off_sw<WB>(32 * nt, lane);
     float s = 0.f;
-#pragma nounroll
-    for (int ks = 0; ks < ES; ++ks) {
-      Fr a, b;
-      a.h = tr_frag_sw<WA>(imgA, 16 * ks, oa);
-      a.l = tr_frag_sw<WA>(imgA + loA, 16 * ks, oa);
-      b.h = tr_frag_sw<WB>(imgB, 16 * ks, ob);
-      if constexpr (BX) {
-        acc = mma_bx(a, b.h, acc);
-      } else {
-        b.l = tr_frag_sw<WB>(imgB + loB, 16 * ks, ob);
-        acc = mma(a, b, acc);
-      }
+    Fr a[2], b[2];
+    auto ld = [&](int ks, Fr& x, Fr& y) {
+      x.h = tr_frag_sw<WA>(imgA, 16 * ks, oa);
+      x.l = tr_frag_sw<WA>(imgA + loA, 16 * ks, oa);
+      y.h = tr_frag_sw<WB>(imgB, 16 * ks, ob);
+      if constexpr (!BX) y.l = tr_frag_sw<WB>(imgB + loB, 16 * ks, ob);
+    };
+    ld(0, a[0], b[0]);
+    ld(1, a[1], b[1]);
+    static_for<ES>([&](auto ks_) {
+      constexpr int ks = decltype(ks_)::value, sl = ks & 1;
+      if constexpr (BX) acc = mma_bx(a[sl], b[sl].h, acc);
+      else acc = mma(a[sl], b[sl], acc);
       if (ks >= bs_lo && ks < bs_hi) {
-        s = dot_sum8(a.l, s);
-        s = dot_sum8(a.h, s);
+        s = dot_sum8(a[sl].l, s);
+        s = dot_sum8(a[sl].h, s);
       }
-    }
+      if constexpr (ks + 2 < ES) ld(ks + 2, a[sl], b[sl]);
+    });
     return s;
   }
 }

@@ -999,18 +999,33 @@ __global__ __launch_bounds__(EB_WAVES * 64, (EB_WAVES == 4 && !X3) ? 2 : 1) void
         }
         lds_wave_sync();
       }
-      Fr dz[8];
-#pragma unroll
-      for (int kk = 0; kk < 8; ++kk) dz[kk] = row_fr(imS + swz_off<128>(erow, 16 * kk + 8 * h), EB_PL);
       // dH1 = W2^T dZ (natural k) . relu'(H1)
       Pk d1b[2];
+      if constexpr (X3) {      // k-outer: one split dZ fragment (8 VGPRs) live at a time
+        f32x16 c[2] = {zero16(), zero16()};
 #pragma unroll
-      for (int mt = 0; mt < 2; ++mt) {
-        f32x16 c = zero16();
+        for (int kk = 0; kk < 8; ++kk) {
+          const Fr dzk = row_fr(imS + swz_off<128>(erow, 16 * kk + 8 * h), EB_PL);
 #pragma unroll
-        for (int kk = 0; kk < 8; ++kk) c = mma(frag_fr(wt, 2 + mt * 8 + kk, lane), dz[kk], c);
-        d1b[mt] = to_pk(c);
-        mask_pk(d1b[mt], H1b[mt]);
+          for (int mt = 0; mt < 2; ++mt) c[mt] = mma(frag_fr(wt, 2 + mt * 8 + kk, lane), dzk, c[mt]);
+        }
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt) {
+          d1b[mt] = to_pk(c[mt]);
+          mask_pk(d1b[mt], H1b[mt]);
+        }
+      } else {
+        Fr dz[8];
+#pragma unroll
+        for (int kk = 0; kk < 8; ++kk) dz[kk] = row_fr(imS + swz_off<128>(erow, 16 * kk + 8 * h), EB_PL);
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt) {
+          f32x16 c = zero16();
+#pragma unroll
+          for (int kk = 0; kk < 8; ++kk) c = mma(frag_fr(wt, 2 + mt * 8 + kk, lane), dz[kk], c);
+          d1b[mt] = to_pk(c);
+          mask_pk(d1b[mt], H1b[mt]);
+        }
       }
       // dF = W1^T dH1 -> rows dx dy dvx dvy (lanes h == 0, regs 0..3)
       {

@@ -60,6 +60,7 @@ class RolloutDriver {
     done_thr_ = F("done_thr");
     check_ = (int)I("check_every");
     noise_key_ = U("noise_key"); noise_prob_ = F("noise_prob"); noise_scale_ = F("noise_scale");
+    scan_ws_ = U("scan_ws"); scan_ws_env_ = I("scan_ws_env");
     apw_ = (int)I("apw");
     if (check_ < 1) check_ = 1;
     if (B_ < 1|| N_ < 1 || Nn_ < N_ || K_ < 1 || K_ > 16 || (D_ != 2 && D_ != 3) || Tmax_ < 1 || resort_ < 1)
@@ -176,6 +177,7 @@ class RolloutDriver {
     a.r2_train = r2_train_; a.ttc_train = ttc_train_; a.r2_check = r2_check_; a.ttc_check = ttc_check_;
     a.do_knn = 1; a.do_safety = safety_;
     a.prev_idx = t > 0 ? P<const int>(idx_) + (long)(t - 1) * B_ * nk : nullptr; a.pi_env = nk;
+    a.ws = P<float4>(scan_ws_); a.ws_env = scan_ws_env_;
     chk(mb_scan(&a, st), "scan");
   }
 
@@ -223,6 +225,8 @@ class RolloutDriver {
   u64 S_, G_, A_, idx_, dang_, cnt_, safe_, dist_, act_, pooled_, argmax_, perm_, host_dist_;
   u64 ctrl_w_, ctrl_v_, cbf_w_, cbf_rm_, cbf_v_, hbuf_, hmask_, src_, nev_, noise_key_;
   float noise_prob_, noise_scale_;
+  u64 scan_ws_;
+  long scan_ws_env_;
   int f_edge_, f_node_, f_fwd_;
   float r2_train_, ttc_train_, r2_check_, ttc_check_, dt_, obs_r_, sqrt3_, dist_thr_, dist_eps_, done_thr_;
   std::vector<hipEvent_t> ev_copy_;

@@ -153,7 +153,70 @@ DEV float wave_min(float v) { return -wave_max(-v); }
 DEV float grp_xor(float v, int o) { return o == 32 ? shfl_xor32(v) : __shfl_xor(v, o); }
 DEV unsigned grp_xoru(unsigned v, int o) { return o == 32 ? xor32u(v) : (unsigned)__shfl_xor((int)v, o); }
 
-template <int K, int D, int BS, int LPA>
+// Large envs (Nn > SCAN_MAXN, the whole env no longer fits LDS): scan_stage_kernel writes the
+// curve-ordered node arrays and the chunk / superchunk boxes of every env ONCE per step to a
+// global workspace [tp Np | tv Np | cbl nch | cbh nch | sbl nsc | sbh nsc]; scan_kernel<GLB>
+// copies only the boxes to LDS (the culling runs from LDS) and reads the candidate nodes of the
+// surviving chunks from global memory (L2-resident; wave-uniform addresses). Same results.
+constexpr int STAGE_BLOCK = 256;                 // chunks per stage block (a multiple of SSC)
+
+template <int D>
+__global__ __launch_bounds__(STAGE_BLOCK) void scan_stage_kernel(ScanArgs a) {
+  __shared__ float4 lbl[STAGE_BLOCK], lbh[STAGE_BLOCK];
+  const int Nn = a.Nn;
+  const int Np = (Nn + SCH - 1) / SCH * SCH;
+  const int nch = Np / SCH, nsc = (nch + SSC - 1) / SSC;
+  const int b = blockIdx.y;
+  float4* w = a.ws + (long)b * a.ws_env;
+  float4 *tp = w, *tv = w + Np, *cbl = tv + Np, *cbh = cbl + nch, *sbl = cbh + nch, *sbh = sbl + nsc;
+  const float4* Sb = a.S + (long)b * a.s_env * REC<D>;
+  const int* perm = a.perm + (long)b * Nn;
+  const int c = blockIdx.x * STAGE_BLOCK + threadIdx.x;
+  float4 lo = make_float4(INFINITY, INFINITY, INFINITY, 0.f);
+  float4 hi = make_float4(-INFINITY, -INFINITY, -INFINITY, 0.f);
+  if (c < nch) {
+#pragma unroll
+    for (int u = 0; u < SCH; ++u) {
+      const int q = c * SCH + u;
+      if (q < Nn) {
+        const int id = perm[q];
+        float p[D], v[D];
+        load_rec<D>(Sb, (unsigned)id, p, v);
+        const float z = (D == 3) ? p[D - 1] : 0.f;
+        const float vz = (D == 3) ? v[D - 1] : 0.f;
+        const float4 s = make_float4(p[0], p[1], z, __int_as_float(id));
+        const float vm = sqrtf(sqsum<D>(v));
+        tp[q] = s;
+        tv[q] = make_float4(v[0], v[1], vz, vm);
+        lo.x = fminf(lo.x, s.x); lo.y = fminf(lo.y, s.y); lo.z = fminf(lo.z, s.z);
+        hi.x = fmaxf(hi.x, s.x); hi.y = fmaxf(hi.y, s.y); hi.z = fmaxf(hi.z, s.z);
+        lo.w = fmaxf(lo.w, vm);
+      } else {
+        tp[q] = make_float4(INFINITY, INFINITY, INFINITY, __int_as_float(-1));
+        tv[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    }
+    cbl[c] = lo;
+    cbh[c] = hi;
+  }
+  lbl[threadIdx.x] = lo;
+  lbh[threadIdx.x] = hi;
+  __syncthreads();
+  const int sc = blockIdx.x * (STAGE_BLOCK / SSC) + threadIdx.x;
+  if (threadIdx.x < STAGE_BLOCK / SSC && sc < nsc) {
+    float4 sl = make_float4(INFINITY, INFINITY, INFINITY, 0.f);
+    float4 sh = make_float4(-INFINITY, -INFINITY, -INFINITY, 0.f);
+    for (int u = threadIdx.x * SSC; u < threadIdx.x * SSC + SSC && blockIdx.x * STAGE_BLOCK + u < nch; ++u) {
+      const float4 l = lbl[u], q = lbh[u];
+      sl.x = fminf(sl.x, l.x); sl.y = fminf(sl.y, l.y); sl.z = fminf(sl.z, l.z); sl.w = fmaxf(sl.w, l.w);
+      sh.x = fmaxf(sh.x, q.x); sh.y = fmaxf(sh.y, q.y); sh.z = fmaxf(sh.z, q.z);
+    }
+    sbl[sc] = sl;
+    sbh[sc] = sh;
+  }
+}
+
+template <int K, int D, int BS, int LPA, bool GLB>
 __global__ __launch_bounds__(BS) void scan_kernel(ScanArgs a) {
   constexpr int APW = WAVE / LPA;                              // agents per wave
   constexpr int SCAN_AG = BS / LPA;                            // agents (curve positions) per block
@@ -161,16 +224,30 @@ __global__ __launch_bounds__(BS) void scan_kernel(ScanArgs a) {
   const int N = a.N, Nn = a.Nn;
   const int Np = (Nn + SCH - 1) / SCH * SCH;
   const int nch = Np / SCH, nsc = (nch + SSC - 1) / SSC;
-  float4* tp = smem4;                                          // [Np] x, y, z, node id (bits)
-  float4* tv = tp + Np;                                        // [Np] vx, vy, vz, |v|
-  float4* cbl = tv + Np;                                       // [nch] min x, y, z, max |v|
-  float4* cbh = cbl + nch;                                     // [nch] max x, y, z
-  float4* sbl = cbh + nch;                                     // [nsc] superchunk boxes
-  float4* sbh = sbl + nsc;
   __shared__ float red[3][BS / WAVE];
   const int b = blockIdx.y;
+  float4 *tp, *tv, *cbl, *cbh, *sbl, *sbh;
+  if constexpr (GLB) {
+    tp = a.ws + (long)b * a.ws_env;                            // [Np] x, y, z, node id (global)
+    tv = tp + Np;                                              // [Np] vx, vy, vz, |v| (global)
+    cbl = smem4;                                               // boxes: LDS copies
+    cbh = cbl + nch;
+    sbl = cbh + nch;
+    sbh = sbl + nsc;
+  } else {
+    tp = smem4;                                                // [Np] x, y, z, node id (bits)
+    tv = tp + Np;                                              // [Np] vx, vy, vz, |v|
+    cbl = tv + Np;                                             // [nch] min x, y, z, max |v|
+    cbh = cbl + nch;                                           // [nch] max x, y, z
+    sbl = cbh + nch;                                           // [nsc] superchunk boxes
+    sbh = sbl + nsc;
+  }
   const float4* Sb = a.S + (long)b * a.s_env * REC<D>;
   const int* perm = a.perm + (long)b * Nn;
+  if constexpr (GLB) {
+    const float4* gb = tv + Np;
+    for (int q = threadIdx.x; q < 2 * (nch + nsc); q += BS) cbl[q] = gb[q];
+  } else
   for (int q = threadIdx.x; q < Np; q += BS) {
     if (q < Nn) {
       const int id = perm[q];
@@ -186,6 +263,7 @@ __global__ __launch_bounds__(BS) void scan_kernel(ScanArgs a) {
     }
   }
   __syncthreads();
+  if constexpr (!GLB) {
   for (int c = threadIdx.x; c < nch; c += BS) {
     float4 lo = make_float4(INFINITY, INFINITY, INFINITY, 0.f);
     float4 hi = make_float4(-INFINITY, -INFINITY, -INFINITY, 0.f);
@@ -215,6 +293,7 @@ __global__ __launch_bounds__(BS) void scan_kernel(ScanArgs a) {
     sbh[c] = hi;
   }
   __syncthreads();
+  }
   // LPA lanes per agent: lane (r, h) owns curve position base + r and scans candidate slots
   // (SCH/LPA)h.. of every chunk; the partial lists are merged at the end (LPA x the waves of a
   // lane-per-agent layout, 1/LPA of the per-chunk work per lane).
@@ -420,9 +499,18 @@ template <int K, int D, int BS>
 static void launch_kdb(const ScanArgs& a, hipStream_t st) {
   constexpr int LPA = SCAN_LPA;
   dim3 grid((a.Nn + BS / LPA - 1) / (BS / LPA), a.B);
+  if (a.Nn > SCAN_MAXN) {
+    const int Np = (a.Nn + SCH - 1) / SCH * SCH, nch = Np / SCH, nsc = (nch + SSC - 1) / SSC;
+    hipLaunchKernelGGL(scan_stage_kernel<D>, dim3((nch + STAGE_BLOCK - 1) / STAGE_BLOCK, a.B), dim3(STAGE_BLOCK), 0,
+                       st, a);
+    const size_t lds = (size_t)2 * (nch + nsc) * 16;
+    (void)hipFuncSetAttribute((const void*)scan_kernel<K, D, BS, LPA, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL((scan_kernel<K, D, BS, LPA, true>), grid, dim3(BS), lds, st, a);
+    return;
+  }
   const size_t lds = scan_lds_bytes(a.Nn);
-  (void)hipFuncSetAttribute((const void*)scan_kernel<K, D, BS, LPA>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL((scan_kernel<K, D, BS, LPA>), grid, dim3(BS), lds, st, a);
+  (void)hipFuncSetAttribute((const void*)scan_kernel<K, D, BS, LPA, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipLaunchKernelGGL((scan_kernel<K, D, BS, LPA, false>), grid, dim3(BS), lds, st, a);
 }
 
 #ifndef SCAN_BS_BIG
@@ -451,7 +539,12 @@ extern "C" int mb_cell_sort(const mb::CellSortArgs* a, hipStream_t st) {
 
 extern "C" int mb_scan(const mb::ScanArgs* a, hipStream_t st) {
   using namespace mb;
-  if (a->Nn > SCAN_MAXN || a->Nn < a->N || !a->perm) return -3;
+  if (a->Nn < a->N || !a->perm) return -3;
+  if (a->Nn > SCAN_MAXN) {       // global staging: the workspace must hold scan_ws_f4(Nn) per env
+    const int Np = (a->Nn + SCH - 1) / SCH * SCH, nch = Np / SCH, nsc = (nch + SSC - 1) / SSC;
+    if (!a->ws || a->ws_env < 2L * Np + 2L * (nch + nsc)) return -4;
+    if ((size_t)2 * (nch + nsc) * 16 > 160 * 1024 - 1024) return -5;   // boxes must fit LDS
+  }
   switch (a->do_knn ? a->K : 1) {
 #define CASE(k) case k: launch_k<k>(*a, st); break;
     CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8)

@@ -8,7 +8,10 @@
 // zero rows also exclude the origin). Starts are uniform in [0, L]^2, L = sqrt(max(1,N/8));
 // goals are start + U(-0.5,0.5)^2 with the same separation rule among goals.
 // Invariants (min pair distance > r, goal offsets in +-0.5, v = 0, density 8/unit^2) are
-// tested against the host sampler. LDS: 25 B per agent (N <= 6000).
+// tested against the host sampler. LDS: 25 B per agent (N <= ~6000); larger envs keep the same
+// arrays in a per-env global workspace (a.ws; one workgroup's waves share one CU and its L1, and
+// __syncthreads orders their global accesses) with a full-resolution cell grid: identical
+// results (acceptance is order independent).
 #include "common.h"
 #include "args.h"
 #include "state.h"
@@ -73,7 +76,8 @@ DEV bool grid_all(const CellGrid& g, const int* head, const int* next, const flo
 template <int D>
 __global__ __launch_bounds__(SC_BLOCK) void scenario_kernel(ScenArgs a, CellGrid grid) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  float* pos = reinterpret_cast<float*>(smem);           // accepted points of this phase (N x D)
+  unsigned char* base = a.ws ? a.ws + (long)blockIdx.x * a.ws_env : smem;
+  float* pos = reinterpret_cast<float*>(base);           // accepted points of this phase (N x D)
   float* cand = pos + a.N * D;                            // this round's candidates
   float* starts = cand + a.N * D;                         // phase-0 result (goal anchors)
   float* obs = starts + a.N * D;                          // M x D obstacle points
@@ -173,16 +177,23 @@ extern "C" int mb_scenario(const mb::ScenArgs* a, hipStream_t st) {
   if (D != 2 && D != 3) return -1;
   // fixed arrays, then as many grid cells (cell size >= r) as the remaining LDS holds
   const size_t base = (size_t)(3 * a->N + a->M) * D * 4 + (size_t)a->N * 4 + (size_t)a->N + 16;
-  if (base + 4 * (size_t)sc_cells(1, D) > SC_LDS_MAX) return -2;
   CellGrid g;
   g.lo = -a->spread - a->r;
   const float span = a->L + 2.f * (a->spread + a->r);
   int G = max(1, (int)floorf(span / a->r));
-  const size_t room = (SC_LDS_MAX - base) / 4;
-  while (G > 1 && (size_t)sc_cells(G, D) > room) --G;
+  size_t lds;
+  if (a->ws) {
+    // global workspace: full-resolution grid; a->ws_env must hold scenario_ws_bytes(N, M, D)
+    if ((size_t)a->ws_env < base + 4 * (size_t)sc_cells(G, D)) return -3;
+    lds = 0;
+  } else {
+    if (base + 4 * (size_t)sc_cells(1, D) > SC_LDS_MAX) return -2;
+    const size_t room = (SC_LDS_MAX - base) / 4;
+    while (G > 1 && (size_t)sc_cells(G, D) > room) --G;
+    lds = base + 4 * (size_t)sc_cells(G, D);
+  }
   g.G = G;
   g.inv = (float)G / span;
-  const size_t lds = base + 4 * (size_t)sc_cells(G, D);
   if (D == 3) {
     (void)hipFuncSetAttribute((const void*)scenario_kernel<3>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL(scenario_kernel<3>, dim3(a->B), dim3(SC_BLOCK), lds, st, *a, g);

@@ -236,6 +236,10 @@ class HipEngine:
                 raise native.NativeError("host_dist must be pinned (T, B)")
             pw = self.pw
             perm = native._perm_buf(B, Nn, self.dev)
+            scan_f4 = native.scan_ws_f4(Nn)                          # large envs: global staging
+            # owned by the engine (the driver keeps the pointer for its lifetime)
+            self._scan_ws = torch.empty(max(B * scan_f4 * 16, 16), dtype=torch.uint8, device=self.dev)
+            scan_ws = self._scan_ws if scan_f4 else None
             native._perm_sorted.add((B, Nn, str(self.dev)))      # sorted at t = 0 of every run
             overlap = bool(self.dedup and self.overlap_hfwd)
             BNK = B * N * K
@@ -258,6 +262,7 @@ class HipEngine:
                 dist_thr=float(C.DIST_MIN_THRES), dist_eps=float(C.CBF_DIST_EPS_COORD * D),
                 done_thr=float(C.DIST_MIN_CHECK),
                 noise_key=native.ptr(self.noise_key) if cfg.add_noise_prob > 0 else 0,
+                scan_ws=native.ptr(scan_ws), scan_ws_env=int(scan_f4),
                 noise_prob=float(cfg.add_noise_prob), noise_scale=float(cfg.noise_scale),
                 fork_device_scope=int(os.environ.get("MACBF_FORK_DEVICE_SCOPE", "1"))))
             if pw.ctrl_v.numel() < 352 or pw.ctrl_w.numel() < (c["f_node"] + 54) * 512 * (2 if pw.x3 else 1):

@@ -149,7 +149,26 @@ def from_records(r: torch.Tensor) -> torch.Tensor:
 
 
 # ----------------------------------------------------------------------------- kernels
-SCAN_MAX_N = 4096
+SCAN_MAX_N = 4096           # envs up to this many graph nodes are staged whole in LDS
+SCAN_MAX_NODES = 36864      # beyond: global staging (csrc/scan.hip scan_stage_kernel), boxes in LDS
+
+
+def scan_ws_f4(Nn: int) -> int:
+    """float4s of global scan staging per env (0 when the env fits LDS)."""
+    if Nn <= SCAN_MAX_N:
+        return 0
+    Np = (Nn + 7) // 8 * 8
+    nch = Np // 8
+    nsc = (nch + 7) // 8
+    return 2 * Np + 2 * (nch + nsc)
+
+
+def scan_ws(B: int, Nn: int, device):
+    """(workspace tensor or None, float4s per env) for scans of B envs of Nn graph nodes."""
+    f4 = scan_ws_f4(Nn)
+    if not f4:
+        return None, 0
+    return _workspace("scan", B * f4 * 16, device), f4
 _perm_cache = {}
 _perm_sorted = set()      # cached permutation buffers that hold a curve order
 
@@ -178,8 +197,8 @@ def scan(S, idx, dang, cnt, safe, *, K, do_knn=True, do_safety=True, perm=None, 
     D = dim_of(S)
     W = rec_width(D)
     N = Nn if n_agents is None else int(n_agents)     # centres = the first N nodes
-    if Nn > SCAN_MAX_N or N > Nn:
-        raise NativeError(f"scan stages one env in LDS: N <= Nn <= {SCAN_MAX_N} (got {N}, {Nn})")
+    if Nn > SCAN_MAX_NODES or N > Nn:
+        raise NativeError(f"scan: N <= Nn <= {SCAN_MAX_NODES} graph nodes per env (got {N}, {Nn})")
     if S.dtype != torch.float32 or S.stride(2) != 1 or S.stride(1) != W:
         raise NativeError(f"S must be float32 with contiguous (Nn,{W}) rows")
     if K < 1 or K > C.MAX_TOP_K or K > Nn:
@@ -204,6 +223,7 @@ def scan(S, idx, dang, cnt, safe, *, K, do_knn=True, do_safety=True, perm=None, 
         if not sort and key not in _perm_sorted:
             sort = True
         _perm_sorted.add(key)
+    ws, ws_f4 = scan_ws(B, Nn, S.device)
     if sort:
         L = float(max(1.0, N / C.AGENT_DENSITY) ** (1.0 / D))
         rc = lib().cell_sort(ptr(S), S.stride(0) // W, B, Nn, L, ptr(perm), W // 4, stream_handle())
@@ -215,7 +235,7 @@ def scan(S, idx, dang, cnt, safe, *, K, do_knn=True, do_safety=True, perm=None, 
                     float(C.DIST_MIN_THRES * C.DIST_MIN_THRES), float(C.TIME_TO_COLLISION),
                     float(C.DIST_MIN_CHECK * C.DIST_MIN_CHECK), float(C.TIME_TO_COLLISION_CHECK),
                     int(do_knn), int(do_safety), Nn, D, ptr(prev_idx),
-                    prev_idx.stride(0) if prev_idx is not None else 0, stream_handle())
+                    prev_idx.stride(0) if prev_idx is not None else 0, ptr(ws), int(ws_f4), stream_handle())
     _ok(rc, "scan")
 
 
@@ -231,11 +251,33 @@ def scenario(S, G, *, seed, L, r=C.DIST_MIN_THRES, spread=C.GOAL_SPREAD, max_rou
     if obs is not None:
         M = obs.shape[1]
         check(obs, torch.float32, (B, M, D), "obs")
-    if (3 * N + M) * D * 4 + 5 * N + 16 + 4 * 2 ** D > 160 * 1024 - 64:
-        raise NativeError(f"scenario sampler: env too large for LDS (N={N}, M={M}, D={D})")
+    base = (3 * N + M) * D * 4 + 5 * N + 16
+    ws, ws_env = None, 0
+    if base + 4 * 2 ** D > 160 * 1024 - 64:
+        # env too large for LDS: the sampler's arrays live in a per-env global workspace with a
+        # full-resolution cell grid (same results: acceptance does not depend on the grid)
+        span = float(L) + 2.0 * (float(spread) + float(r))
+        import numpy as _np
+        G1 = max(1, int(_np.floor(_np.float32(span) / _np.float32(r))))
+        ws_env = (base + 4 * (G1 + 2) ** D + 255) // 256 * 256      # (+2: float rounding slack)
+        ws = _workspace("scenario", B * ws_env, S.device)
     rc = lib().scenario(ptr(S), S.stride(0) // W, ptr(G), ptr(obs), M, D, B, N, float(L), float(r), float(spread),
-                        int(seed) & 0xFFFFFFFFFFFFFFFF, int(max_rounds), ptr(status), stream_handle())
+                        int(seed) & 0xFFFFFFFFFFFFFFFF, int(max_rounds), ptr(status), ptr(ws), int(ws_env),
+                        stream_handle())
     _ok(rc, "scenario")
+
+
+_WS = {}
+
+
+def _workspace(name, nbytes, device):
+    """Cached uint8 device scratch (grown on demand; stream-ordered reuse)."""
+    key = (name, str(device))
+    t = _WS.get(key)
+    if t is None or t.numel() < nbytes:
+        t = torch.empty(max(int(nbytes), 1), dtype=torch.uint8, device=device)
+        _WS[key] = t
+    return t
 
 
 def _rows(t, last, name, lead):
