@@ -75,6 +75,22 @@ struct CtrlArgs {
   h16* pooled;     long p_env;       // (b,i,128) max-pooled edge features out (h16), or null
   uint8_t* argmax;  long am_env;      // (b,i,128) winning slot per feature (0xFF: no grad), or null
   int apw;                            // agents per wave (even, 2..32; 0 = 32): small scenes use fewer
+  int b0, nb_total;                   // env offset / total envs of a per-env view (noise keys; 0, 0 = this view)
+};
+
+// Persistent small-scene rollout (ctrl.hip rollout_small_kernel): one workgroup per env runs
+// every step of the rollout in one launch.
+struct RolloutSmallArgs {
+  CtrlArgs c;           // time-major bases: S (T+1,B,Nn), A (T,B,N), dist/act sums (T,B), pooled,
+                        // argmax (T,B,N,.); weights, noise and constants as for one step
+  int* idx;             // (>=T, B, N, K) kNN out (row Tmax only with knn_tail)
+  uint8_t* dang;        // (T, B, N, K)
+  float* cnt;           // (T, B, 2)
+  float* safe;          // (T+1, B) or null (no safety statistic)
+  int Nn, Tmax, knn_tail;
+  float r2_train, ttc_train, r2_check, ttc_check;
+  float done_thr;       // early stop: mean goal distance < done_thr (-inf: run all Tmax steps)
+  int* ctl;             // [envs done, max first-done step]: zeroed before the launch
 };
 
 struct LossConsts {
@@ -272,6 +288,9 @@ int mb_scenario(const mb::ScenArgs* a, hipStream_t st);
 int mb_ctrl_fwd(const mb::CtrlArgs* a, int num_cu, hipStream_t st);
 int mb_ctrl_fwd_f16(const mb::CtrlArgs* a, int num_cu, hipStream_t st);
 int mb_ctrl_fwd_x3(const mb::CtrlArgs* a, int num_cu, hipStream_t st);
+int mb_rollout_small(const mb::RolloutSmallArgs* a, hipStream_t st);
+int mb_rollout_small_f16(const mb::RolloutSmallArgs* a, hipStream_t st);
+int mb_rollout_small_x3(const mb::RolloutSmallArgs* a, hipStream_t st);
 int mb_cbf_fwd(const mb::CbfFwdArgs* a, int num_blocks, hipStream_t st);
 int mb_cbf_fwd_f16(const mb::CbfFwdArgs* a, int num_blocks, hipStream_t st);
 int mb_cbf_fwd_x3(const mb::CbfFwdArgs* a, int num_blocks, hipStream_t st);

@@ -118,13 +118,21 @@ DEV void split_h16(float x, h16& hi, h16& lo) {
 DEV void lds_wave_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
 // cooperative copy of `bytes` (multiple of 16) from global to LDS by the whole block
-// (4 independent 16-byte loads in flight per thread before the stores: the weight staging at
-// kernel start is latency-bound, which dominates small launches)
+// (8 independent 16-byte loads in flight per thread before the stores: the weight staging at
+// kernel start is latency-bound, which dominates small launches -- a 120 KB x3 image is 30
+// loads per thread of a 256-thread block)
 DEV void block_copy16(void* dst, const void* src, int bytes) {
   const u32x4* s = reinterpret_cast<const u32x4*>(src);
   u32x4* d = reinterpret_cast<u32x4*>(dst);
   const int n = bytes / 16, bd = blockDim.x;
   int i = threadIdx.x;
+  for (; i + 7 * bd < n; i += 8 * bd) {
+    u32x4 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = s[i + u * bd];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) d[i + u * bd] = v[u];
+  }
   for (; i + 3 * bd < n; i += 4 * bd) {
     const u32x4 v0 = s[i], v1 = s[i + bd], v2 = s[i + 2 * bd], v3 = s[i + 3 * bd];
     d[i] = v0; d[i + bd] = v1; d[i + 2 * bd] = v2; d[i + 3 * bd] = v3;
@@ -135,6 +143,16 @@ DEV void block_copy16(void* dst, const void* src, int bytes) {
 DEV float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+// integer wave sum (exact, so independent of how the addends are grouped over waves)
+DEV unsigned long long wave_sum_u64(unsigned long long v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const unsigned lo = (unsigned)__shfl_xor((int)(unsigned)v, o), hi = (unsigned)__shfl_xor((int)(unsigned)(v >> 32), o);
+    v += ((unsigned long long)hi << 32) | lo;
+  }
   return v;
 }
 

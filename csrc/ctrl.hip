@@ -18,6 +18,7 @@
 #include "common.h"
 #include "args.h"
 #include "state.h"
+#include "ttc.h"
 
 namespace mb {
 namespace MB_PREC {
@@ -232,7 +233,8 @@ DEV void node_phase(const CtrlArgs& a, int g0, int APW, int total, PoolFr pool, 
     if (a.noise_key) {
       // one coin per (env, step), Box-Muller normals per (agent, axis): the same draws for any
       // launch geometry, the native driver and the Python loop
-      const uint64_t kb = mix64(*a.noise_key ^ (0x9E3779B97F4A7C15ull * (uint64_t)(a.noise_t * a.B + b + 1)));
+      const int nbt = a.nb_total ? a.nb_total : a.B;     // per-env sub-arguments: global env b0 + b
+      const uint64_t kb = mix64(*a.noise_key ^ (0x9E3779B97F4A7C15ull * (uint64_t)(a.noise_t * nbt + a.b0 + b + 1)));
       if (u01(kb) < a.noise_prob) {
 #pragma unroll
         for (int q = 0; q < D; ++q) {
@@ -259,21 +261,24 @@ DEV void node_phase(const CtrlArgs& a, int g0, int APW, int total, PoolFr pool, 
     dsum = sqrtf(sqsum<D>(dd));
     asum = fabsf(sqsum<D>(av) - sqsum<D>(ar));
   }
-  // per-env sums: one fixed-point integer atomic per wave when its 32 agents share an env
-  // (the wave sum is a fixed shuffle tree, the integer adds commute: order-independent)
+  // per-env sums in fixed point: every agent's term is rounded to an integer first, so the
+  // integer wave sums and atomics give the same value for any grouping of agents over waves and
+  // any arrival order (the early-stop input is launch-geometry independent)
   auto fx = [](float v, double s) { return (unsigned long long)__double2ll_rn((double)v * s); };
+  unsigned long long dq = 0, aq = 0;
+  if (ok && h == 0) { dq = fx(dsum, FX_DIST); aq = fx(asum, FX_ACT); }
   const int last = min(g0 + APW - 1, total - 1);
-  if (g0 / N == last / N) {
-    dsum = wave_sum(dsum);
-    asum = wave_sum(asum);
+  if (g0 / N == last / N) {      // the wave's agents share an env: one atomic per wave
+    dq = wave_sum_u64(dq);
+    aq = wave_sum_u64(aq);
     if (lane == 0) {
       const int be = g0 / N;
-      if (a.dist_sum) atomicAdd(a.dist_sum + (long)be * a.d_env, fx(dsum, FX_DIST));
-      if (a.act_sum) atomicAdd(a.act_sum + (long)be * a.ac_env, fx(asum, FX_ACT));
+      if (a.dist_sum) atomicAdd(a.dist_sum + (long)be * a.d_env, dq);
+      if (a.act_sum) atomicAdd(a.act_sum + (long)be * a.ac_env, aq);
     }
   } else if (ok && h == 0) {
-    if (a.dist_sum) atomicAdd(a.dist_sum + (long)b * a.d_env, fx(dsum, FX_DIST));
-    if (a.act_sum) atomicAdd(a.act_sum + (long)b * a.ac_env, fx(asum, FX_ACT));
+    if (a.dist_sum) atomicAdd(a.dist_sum + (long)b * a.d_env, dq);
+    if (a.act_sum) atomicAdd(a.act_sum + (long)b * a.ac_env, aq);
   }
 }
 
@@ -282,18 +287,14 @@ DEV void node_phase(const CtrlArgs& a, int g0, int APW, int total, PoolFr pool, 
 // x3: the split weights do not fit one workgroup's LDS together, so this kernel runs the edge
 // phase only and writes the pooled features ([hi | lo] rows, always stored) straight to global
 // memory; ctrl_node_fwd_kernel reads them back as node-layer B fragments.
-template <int WAVES, int D>
-__global__ __launch_bounds__(WAVES * 64) void ctrl_fwd_kernel(CtrlArgs a) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  constexpr int NFR = X3 ? 18 : CTRL_FWD_FRAGS;                     // fragments staged in LDS
-  h16* wl = reinterpret_cast<h16*>(smem);                            // ew1f, ew2 (18 frags)
-  h16* wn = wl + 18 * FRAG_ELEMS;                                     // nw1f..nw4 (54 frags)
-  float* vl = reinterpret_cast<float*>(smem + NFR * FRAG_SZ);
-  h16* pools = reinterpret_cast<h16*>(smem + NFR * FRAG_SZ + CTRL_VEC * 4);
-  block_copy16(wl, a.wpack + (size_t)a.f_edge * FRAG_ELEMS, 18 * FRAG_SZ);
-  if constexpr (!X3) block_copy16(wn, a.wpack + (size_t)a.f_node * FRAG_ELEMS, 54 * FRAG_SZ);
-  block_copy16(vl, a.wvec, CTRL_VEC * 4);
-  __syncthreads();
+// Body of the controller step over the agent groups grp0, grp0 + gstride, ... of `a` (weights
+// already in LDS: wl = ew1f|ew2, wn = nw1f..nw4, vl = CTRL_VEC floats, pools = one 32-row pool
+// image per wave). SPLIT (always for x3): edge phase only, the pooled rows go to global memory
+// and ctrl_node_groups runs the node phase.
+template <int D, bool SPLIT>
+DEV void ctrl_fwd_groups(const CtrlArgs& a, const h16* wl, const h16* wn, const float* vl, h16* pools, int grp0,
+                         int gstride) {
+  constexpr bool GPOOL = X3 || SPLIT;
   const float* eb2 = vl;
   const float* nb2 = vl + 128;
   const float* nb3 = vl + 256;
@@ -307,7 +308,7 @@ __global__ __launch_bounds__(WAVES * 64) void ctrl_fwd_kernel(CtrlArgs a) {
   // agents per wave: 32, or 4..16 for small scenes (more waves share the edge phase; the node
   // phase's MFMA rows beyond APW carry ignored data)
   const int APW = (a.apw >= 2 && a.apw <= 32) ? a.apw : 32;
-  for (int grp = blockIdx.x * WAVES + wave; grp * APW < total; grp += gridDim.x * WAVES) {
+  for (int grp = grp0; grp * APW < total; grp += gstride) {
     const int g0 = grp * APW;
     // ---------------- edge phase: 16 tiles x (2 agents x 16 slots); the gathers of tile q+1
     // (idx -> s_j, dependent global loads) are issued before tile q's MFMA chain
@@ -344,7 +345,7 @@ __global__ __launch_bounds__(WAVES * 64) void ctrl_fwd_kernel(CtrlArgs a) {
       const int arow = 2 * q + h;   // h==0 writes agent 2q, h==1 agent 2q+1
       int bb = 0, ii = 0;
       const int ga = g0 + arow;
-      const bool gout = (a.argmax || X3) && ga < total;
+      const bool gout = (a.argmax || GPOOL) && ga < total;
       if (gout) { bb = ga / N; ii = ga - bb * N; }
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt) {
@@ -361,12 +362,12 @@ __global__ __launch_bounds__(WAVES * 64) void ctrl_fwd_kernel(CtrlArgs a) {
         p1 = max(p1, shfl_xor32i(p1));
         const int pw_ = (h == 0) ? p0 : p1;
         const float pv = __int_as_float(pw_ & -16);
-        if constexpr (X3) {
+        if constexpr (GPOOL) {
           if (gout) {
             h16* prow = a.pooled + (long)bb * a.p_env + (long)ii * PROW + 32 * nt + r;
             const h16 ph = (h16)pv;
             prow[0] = ph;
-            prow[128] = (h16)(pv - (float)ph);
+            if constexpr (X3) prow[128] = (h16)(pv - (float)ph);
           }
         } else {
           pool[arow * PSTR + 32 * nt + r] = (h16)pv;
@@ -378,7 +379,7 @@ __global__ __launch_bounds__(WAVES * 64) void ctrl_fwd_kernel(CtrlArgs a) {
 #endif
       }
     }
-    if constexpr (X3) continue;     // node phase: ctrl_node_fwd_kernel
+    if constexpr (GPOOL) continue;     // node phase: ctrl_node_groups
     lds_wave_sync();
     if (a.pooled) {   // 32 agents x 256 B, 16 B per lane
       for (int u = lane; u < 32 * 16; u += 64) {
@@ -403,6 +404,38 @@ __global__ __launch_bounds__(WAVES * 64) void ctrl_fwd_kernel(CtrlArgs a) {
   }
 }
 
+template <int WAVES, int D>
+__global__ __launch_bounds__(WAVES * 64) void ctrl_fwd_kernel(CtrlArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  constexpr int NFR = X3 ? 18 : CTRL_FWD_FRAGS;                     // fragments staged in LDS
+  h16* wl = reinterpret_cast<h16*>(smem);                            // ew1f, ew2 (18 frags)
+  h16* wn = wl + 18 * FRAG_ELEMS;                                     // nw1f..nw4 (54 frags)
+  float* vl = reinterpret_cast<float*>(smem + NFR * FRAG_SZ);
+  h16* pools = reinterpret_cast<h16*>(smem + NFR * FRAG_SZ + CTRL_VEC * 4);
+  block_copy16(wl, a.wpack + (size_t)a.f_edge * FRAG_ELEMS, 18 * FRAG_SZ);
+  if constexpr (!X3) block_copy16(wn, a.wpack + (size_t)a.f_node * FRAG_ELEMS, 54 * FRAG_SZ);
+  block_copy16(vl, a.wvec, CTRL_VEC * 4);
+  __syncthreads();
+  ctrl_fwd_groups<D, false>(a, wl, wn, vl, pools, blockIdx.x * WAVES + threadIdx.x / WAVE, gridDim.x * WAVES);
+}
+
+// Node phase of the controller step over the pooled rows in global memory, 32-agent groups
+// grp0, grp0 + gstride, ... (x3 steps, and the persistent small-scene rollout)
+template <int D>
+DEV void ctrl_node_groups(const CtrlArgs& a, const h16* wn, const float* vl, int grp0, int gstride) {
+  const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
+  const int N = a.N;
+  const int total = a.B * N;
+  for (int grp = grp0; grp * 32 < total; grp += gstride) {
+    const int g0 = grp * 32;
+    const int gi = min(g0 + r, total - 1);
+    const int b = gi / N, i = gi - b * N;
+    const h16* prow = a.pooled + (long)b * a.p_env + (long)i * PROW + 8 * h;
+    node_phase<D>(a, g0, 32, total, [&](int kk) { return row_fr(prow + 16 * kk, 128); }, wn, vl + 128, vl + 256,
+                  vl + 320, lane);
+  }
+}
+
 // x3 node phase of the controller step over the pooled rows written by ctrl_fwd_kernel
 template <int WAVES, int D>
 __global__ __launch_bounds__(WAVES * 64) void ctrl_node_fwd_kernel(CtrlArgs a) {
@@ -412,17 +445,7 @@ __global__ __launch_bounds__(WAVES * 64) void ctrl_node_fwd_kernel(CtrlArgs a) {
   block_copy16(wn, a.wpack + (size_t)a.f_node * FRAG_ELEMS, 54 * FRAG_SZ);
   block_copy16(vl, a.wvec, CTRL_VEC * 4);
   __syncthreads();
-  const int wave = threadIdx.x / WAVE, lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
-  const int N = a.N;
-  const int total = a.B * N;
-  for (int grp = blockIdx.x * WAVES + wave; grp * 32 < total; grp += gridDim.x * WAVES) {
-    const int g0 = grp * 32;
-    const int gi = min(g0 + r, total - 1);
-    const int b = gi / N, i = gi - b * N;
-    const h16* prow = a.pooled + (long)b * a.p_env + (long)i * PROW + 8 * h;
-    node_phase<D>(a, g0, 32, total, [&](int kk) { return row_fr(prow + 16 * kk, 128); }, wn, vl + 128, vl + 256,
-                  vl + 320, lane);
-  }
+  ctrl_node_groups<D>(a, wn, vl, blockIdx.x * WAVES + threadIdx.x / WAVE, gridDim.x * WAVES);
 }
 
 constexpr int CTRL_WAVES = 8;
@@ -559,6 +582,9 @@ __global__ __launch_bounds__(NB_WAVES * 64, 1) void ctrl_node_bwd_kernel(CtrlNod
   for (long chunk = blockIdx.x; chunk < nchunks; chunk += gridDim.x) {
     const int ga = (int)(chunk * NB_CH) + erow;
     const bool ok = ga < total;
+    // stage turns holding at least one valid agent (a partial last chunk -- all but the first
+    // for small scenes -- skips the turns of its empty waves: zero rows contribute nothing)
+    const int nturn = min(NB_NT, (int)((total - chunk * NB_CH + NB_RT - 1) / NB_RT));
     int b = 0, i = 0;
     float sp[D], sv[D], gg[D], av[D], gnp[D], gnv[D];
 #pragma unroll
@@ -687,7 +713,7 @@ __global__ __launch_bounds__(NB_WAVES * 64, 1) void ctrl_node_bwd_kernel(CtrlNod
       mask_pk(d3b[mt], Y3b[mt]);
     }
 #pragma unroll 1
-    for (int turn = 0; turn < NB_NT; ++turn) {   // S4: dWn4pad (32x64) += dY4 . Y3^T ; nb4
+    for (int turn = 0; turn < nturn; ++turn) {   // S4: dWn4pad (32x64) += dY4 . Y3^T ; nb4
       h16* imA = stg;
       h16* imB = stg + NB_RT * 40;
       if (NB_NT == 1 || myturn == turn) {
@@ -713,7 +739,7 @@ __global__ __launch_bounds__(NB_WAVES * 64, 1) void ctrl_node_bwd_kernel(CtrlNod
       mask_pk(d2b[mt], Y2b[mt]);
     }
 #pragma unroll 1
-    for (int turn = 0; turn < NB_NT; ++turn) {   // S3: dWn3 (64x128) += dY3 . Y2^T ; nb3
+    for (int turn = 0; turn < nturn; ++turn) {   // S3: dWn3 (64x128) += dY3 . Y2^T ; nb3
       h16* imA = stg;
       h16* imB = stg + NB_RT * 72;
       if (NB_NT == 1 || myturn == turn) {
@@ -744,7 +770,7 @@ __global__ __launch_bounds__(NB_WAVES * 64, 1) void ctrl_node_bwd_kernel(CtrlNod
       mask_pk(d1b[mt], Y1b[mt]);
     }
 #pragma unroll 1
-    for (int turn = 0; turn < NB_NT; ++turn) {   // S2: dWn2 (128x64) += dY2 . Y1^T ; nb2
+    for (int turn = 0; turn < nturn; ++turn) {   // S2: dWn2 (128x64) += dY2 . Y1^T ; nb2
       h16* imA = stg;
       h16* imB = stg + NB_RT * 136;
       if (NB_NT == 1 || myturn == turn) {
@@ -796,7 +822,7 @@ __global__ __launch_bounds__(NB_WAVES * 64, 1) void ctrl_node_bwd_kernel(CtrlNod
       }
     }
 #pragma unroll 1
-    for (int turn = 0; turn < NB_NT; ++turn) {   // S1: dWn1f (64x160) += dY1 . P^T (P re-read: L2-hot)
+    for (int turn = 0; turn < nturn; ++turn) {   // S1: dWn1f (64x160) += dY1 . P^T (P re-read: L2-hot)
       h16* imA = stg;
       h16* imB = stg + NB_RT * 72;
       if (NB_NT == 1 || myturn == turn) {
@@ -1153,6 +1179,195 @@ __global__ __launch_bounds__(EB_WAVES * 64, (EB_WAVES == 4 && !X3) ? 2 : 1) void
   }
 }
 
+// =======================================================================================
+// Persistent small-scene rollout (envs of <= SMALL_MAXN graph nodes; reference train.py:58-81).
+// The per-step kernels of a 32-agent env are single-workgroup launches whose latency, not work,
+// sets the step time (~60 us per step as scan + controller launches). Here ONE launch runs the
+// whole rollout: one workgroup per env loops over the steps,
+//   small_scan: brute-force kNN by rank selection, TTC danger bits and counts, all-pairs safety;
+//   controller edge phase over all waves (groups of apw agents), node phase (32-agent groups),
+//   Euler step, per-env goal-distance sums -> the env's early-stop state.
+// Early stop without a grid barrier: an env that becomes done publishes its step (max into
+// ctl[1], then ctl[0] += 1). A workgroup keeps simulating its env (done envs are masked later,
+// as on the launch-per-step path) until every env has published and it has scanned s_T,
+// T = max published step + 1, or until it has scanned s_Tmax. No workgroup ever waits for
+// another, so the launch terminates for any residency / order; steps a fast workgroup computes
+// beyond T are never read. Outputs are those of the per-step path, bit for bit.
+// =======================================================================================
+constexpr int SR_WAVES = 8;
+constexpr int SMALL_MAXN = 64;
+constexpr int SR_JG = 8;                       // kNN candidates per work item
+
+struct SmallScanLds {
+  float4 tp[SMALL_MAXN], tv[SMALL_MAXN];       // positions / velocities of s_t (z = 0 in 2-D)
+  int nbr[SMALL_MAXN * 16];                    // the env's kNN slots
+  int unsafe[SMALL_MAXN];
+  float red[2][SR_WAVES];
+  int dec;
+};
+
+template <int D>
+DEV void rel_d2(const float4& a, const float4& c, float (&dp)[D]) {
+  dp[0] = a.x - c.x;
+  dp[1] = a.y - c.y;
+  if constexpr (D == 3) dp[2] = a.z - c.z;
+}
+
+// kNN / danger / counts / safety of one env's s_t (Sb: the env's records) by the whole workgroup.
+// Same keys, arithmetic and tie order as scan_kernel: (d2 bits, node id) ranks, so the lists are
+// those of the all-pairs oracle; the safety test runs on every pair (no culling pre-test).
+template <int D>
+DEV void small_scan(const RolloutSmallArgs& ra, const float4* Sb, int N, int Nn, int K, bool knn, bool dng,
+                    int* idx_out, uint8_t* dang_out, float* cnt_out, float* safe_out, SmallScanLds& L) {
+  const int tid = threadIdx.x, wave = tid / WAVE, lane = tid & 63;
+  constexpr int NTH = SR_WAVES * WAVE;
+  for (int q = tid; q < Nn; q += NTH) {
+    float p[D], v[D];
+    load_rec<D>(Sb, (unsigned)q, p, v);
+    L.tp[q] = make_float4(p[0], p[1], D == 3 ? p[D - 1] : 0.f, 0.f);
+    L.tv[q] = make_float4(v[0], v[1], D == 3 ? v[D - 1] : 0.f, 0.f);
+    L.unsafe[q] = 0;
+  }
+  __syncthreads();
+  if (knn) {
+    // slot of candidate j in agent i's list = #{j' : key(i, j') < key(i, j)}; keys are unique
+    const int ng = (Nn + SR_JG - 1) / SR_JG;
+    for (int w = tid; w < N * ng; w += NTH) {
+      const int i = w / ng, j0 = (w - i * ng) * SR_JG;
+      const float4 me = L.tp[i];
+      uint64_t key[SR_JG];
+      int rank[SR_JG];
+#pragma unroll
+      for (int u = 0; u < SR_JG; ++u) {
+        float dp[D];
+        rel_d2<D>(me, L.tp[min(j0 + u, Nn - 1)], dp);
+        key[u] = j0 + u < Nn ? knn_key(sqsum<D>(dp), (unsigned)(j0 + u)) : ~0ull;
+        rank[u] = 0;
+      }
+      for (int jp = 0; jp < Nn; ++jp) {
+        float dp[D];
+        rel_d2<D>(me, L.tp[jp], dp);
+        const uint64_t kp = knn_key(sqsum<D>(dp), (unsigned)jp);
+#pragma unroll
+        for (int u = 0; u < SR_JG; ++u) rank[u] += kp < key[u] ? 1 : 0;
+      }
+#pragma unroll
+      for (int u = 0; u < SR_JG; ++u)
+        if (j0 + u < Nn && rank[u] < K) {
+          L.nbr[i * K + rank[u]] = j0 + u;
+          idx_out[i * K + rank[u]] = j0 + u;
+        }
+    }
+    __syncthreads();
+  }
+  float nd = 0.f, ns = 0.f;
+  if (dng) {
+    for (int w = tid; w < N * K; w += NTH) {
+      const int i = w / K, j = L.nbr[w];
+      const float eye = (j == i) ? 1.f : 0.f;
+      const float pi[3] = {L.tp[i].x, L.tp[i].y, L.tp[i].z}, pj[3] = {L.tp[j].x, L.tp[j].y, L.tp[j].z};
+      const float vi[3] = {L.tv[i].x, L.tv[i].y, L.tv[i].z}, vj[3] = {L.tv[j].x, L.tv[j].y, L.tv[j].z};
+      float dp[D], dv[D];
+#pragma unroll
+      for (int d = 0; d < D; ++d) { dp[d] = (pi[d] - pj[d]) + eye; dv[d] = vi[d] - vj[d]; }
+      const bool dg = ttc_danger<D>(dp, dv, ra.r2_train, ra.ttc_train);
+      dang_out[w] = dg ? 1 : 0;
+      nd += dg ? 1.f : 0.f;
+    }
+  }
+  if (safe_out) {
+    for (int w = tid; w < N * Nn; w += NTH) {
+      const int i = w / Nn, j = w - i * Nn;
+      if (j == i || L.unsafe[i]) continue;     // (a racy skip: the flag only ever goes 0 -> 1)
+      float dp[D], dv[D];
+      rel_d2<D>(L.tp[i], L.tp[j], dp);
+      rel_d2<D>(L.tv[i], L.tv[j], dv);
+      if (ttc_danger<D>(dp, dv, ra.r2_check, ra.ttc_check)) atomicOr(&L.unsafe[i], 1);
+    }
+    __syncthreads();
+    for (int q = tid; q < N; q += NTH) ns += L.unsafe[q] ? 0.f : 1.f;
+  }
+  nd = wave_sum(nd);
+  ns = wave_sum(ns);
+  if (lane == 0) { L.red[0][wave] = nd; L.red[1][wave] = ns; }
+  __syncthreads();
+  if (tid == 0) {
+    float s0 = 0.f, s1 = 0.f;
+    for (int q = 0; q < SR_WAVES; ++q) { s0 += L.red[0][q]; s1 += L.red[1][q]; }
+    if (dng) { cnt_out[0] = s0; cnt_out[1] = (float)(N * K) - s0; }
+    if (safe_out) safe_out[0] = s1;
+  }
+}
+
+template <int D>
+__global__ __launch_bounds__(SR_WAVES * 64) void rollout_small_kernel(RolloutSmallArgs ra) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  __shared__ SmallScanLds L;
+  h16* wl = reinterpret_cast<h16*>(smem);                            // ew1f, ew2 (18 frags)
+  h16* wn = wl + 18 * FRAG_ELEMS;                                     // nw1f..nw4 (54 frags)
+  float* vl = reinterpret_cast<float*>(smem + (size_t)CTRL_FWD_FRAGS * FRAG_SZ);
+  const CtrlArgs& c = ra.c;
+  block_copy16(wl, c.wpack + (size_t)c.f_edge * FRAG_ELEMS, 18 * FRAG_SZ);
+  block_copy16(wn, c.wpack + (size_t)c.f_node * FRAG_ELEMS, 54 * FRAG_SZ);
+  block_copy16(vl, c.wvec, CTRL_VEC * 4);
+  __syncthreads();
+  const int b = blockIdx.x, B = c.B, N = c.N, K = c.K, Nn = ra.Nn, Tmax = ra.Tmax;
+  const long nk = (long)N * K;
+  const int wave = threadIdx.x / WAVE;
+  int T = -1;                  // horizon, once every env has published its first done step
+  bool done = false;           // (thread 0) this env has published
+  for (int t = 0; t <= Tmax; ++t) {
+    // the control words are only ever touched by device-scope atomics (performed past the XCD
+    // L2s), so relaxed atomic loads see them without acquire fences (which would invalidate the
+    // L2 every step); ctl[1] is complete before ctl[0] counts its env (publisher below)
+    if (threadIdx.x == 0) {
+      if (T < 0 && __hip_atomic_load(ra.ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == B)
+        T = min(Tmax, __hip_atomic_load(ra.ctl + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1);
+      L.dec = T;
+    }
+    __syncthreads();
+    T = L.dec;
+    if (T >= 0 && t > T) break;
+    const bool tail = t == Tmax || t == T;       // s_T: scan only
+    const long tb = (long)t * B + b;
+    const float4* St = c.S + tb * Nn * REC<D>;
+    small_scan<D>(ra, St, N, Nn, K, t < Tmax || ra.knn_tail, t < Tmax, ra.idx + tb * nk, ra.dang + tb * nk,
+                  ra.cnt + tb * 2, ra.safe ? ra.safe + tb : nullptr, L);
+    if (tail) break;
+    // env b's view of step t: the per-step controller bodies over this env's agents only
+    CtrlArgs e = c;
+    e.S = St; e.s_env = Nn;
+    e.G = c.G + (long)b * N * D;
+    e.idx = ra.idx + tb * nk; e.i_env = nk;
+    e.B = 1; e.b0 = b; e.nb_total = B;
+    e.A = c.A ? c.A + tb * N * D : nullptr; e.a_env = N;
+    e.Snext = const_cast<float4*>(c.S) + (tb + B) * Nn * REC<D>; e.sn_env = Nn;
+    e.dist_sum = c.dist_sum + tb; e.d_env = 1;
+    e.act_sum = c.act_sum ? c.act_sum + tb : nullptr; e.ac_env = 1;
+    e.pooled = c.pooled + tb * N * PROW; e.p_env = (long)N * PROW;
+    e.argmax = c.argmax + tb * N * 128; e.am_env = (long)N * 128;
+    e.noise_t = t;
+    ctrl_fwd_groups<D, true>(e, wl, wn, vl, nullptr, wave, SR_WAVES);
+    __syncthreads();                                // the env's pooled rows -> node phase
+    ctrl_node_groups<D>(e, wn, vl, wave, SR_WAVES);
+    // s_{t+1} (read by this workgroup only) and the env's sum atomics (device scope) complete
+    // before the barrier; the workgroup-scope barrier is enough for both
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0 && !done) {
+      const unsigned long long d = __hip_atomic_load(e.dist_sum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if ((float)((double)d / FX_DIST) / (float)N < ra.done_thr) {   // the host check's arithmetic
+        done = true;
+        __hip_atomic_fetch_max(ra.ctl + 1, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");           // the max lands before the count
+        __hip_atomic_fetch_add(ra.ctl, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  }
+}
+
+size_t rollout_small_lds() { return (size_t)CTRL_FWD_FRAGS * FRAG_SZ + CTRL_VEC * 4; }
+
 }  // namespace MB_PREC
 }  // namespace mb
 
@@ -1181,6 +1396,24 @@ extern "C" int MB_SYM(ctrl_edge_bwd)(const mb::CtrlEdgeBwdArgs* a, int num_block
   } else {
     (void)hipFuncSetAttribute((const void*)ctrl_edge_bwd_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL(ctrl_edge_bwd_kernel<2>, dim3(num_blocks), dim3(EB_WAVES * 64), lds, st, *a);
+  }
+  return (int)hipGetLastError();
+}
+
+extern "C" int MB_SYM(rollout_small)(const mb::RolloutSmallArgs* a, hipStream_t st) {
+  using namespace mb;
+  using namespace mb::MB_PREC;
+  const CtrlArgs& c = a->c;
+  if (c.K > 16 || c.K < 1 || c.N < 1 || a->Nn < c.N || a->Nn > SMALL_MAXN || c.K > a->Nn || a->Tmax < 1) return -1;
+  if (!a->ctl || !a->idx || !a->dang || !a->cnt || !c.pooled || !c.argmax || !c.dist_sum || !c.S) return -2;
+  if (c.apw < 2 || c.apw > 32 || (c.apw & 1)) return -3;
+  const size_t lds = rollout_small_lds();
+  if (c.dim == 3) {
+    (void)hipFuncSetAttribute((const void*)rollout_small_kernel<3>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(rollout_small_kernel<3>, dim3(c.B), dim3(SR_WAVES * 64), lds, st, *a);
+  } else {
+    (void)hipFuncSetAttribute((const void*)rollout_small_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(rollout_small_kernel<2>, dim3(c.B), dim3(SR_WAVES * 64), lds, st, *a);
   }
   return (int)hipGetLastError();
 }

@@ -15,6 +15,7 @@
 #include <pybind11/stl.h>
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <stdexcept>
 #include <vector>
@@ -62,6 +63,8 @@ class RolloutDriver {
     noise_key_ = U("noise_key"); noise_prob_ = F("noise_prob"); noise_scale_ = F("noise_scale");
     scan_ws_ = U("scan_ws"); scan_ws_env_ = I("scan_ws_env");
     apw_ = (int)I("apw");
+    small_ctl_ = U("small_ctl"); small_apw_ = (int)I("small_apw"); knn_tail_ = (int)I("knn_tail");
+    if (small_ctl_) chk(hipHostMalloc((void**)&host_ctl_, 2 * sizeof(int), hipHostMallocDefault), "hipHostMalloc");
     if (check_ < 1) check_ = 1;
     if (B_ < 1|| N_ < 1 || Nn_ < N_ || K_ < 1 || K_ > 16 || (D_ != 2 && D_ != 3) || Tmax_ < 1 || resort_ < 1)
       throw std::invalid_argument("RolloutDriver: bad dimensions");
@@ -78,6 +81,7 @@ class RolloutDriver {
     for (auto e : ev_copy_) (void)hipEventDestroy(e);
     (void)hipEventDestroy(ev_main_);
     (void)hipEventDestroy(ev_side_);
+    if (host_ctl_) (void)hipHostFree(host_ctl_);
   }
   RolloutDriver(const RolloutDriver&) = delete;
   RolloutDriver& operator=(const RolloutDriver&) = delete;
@@ -140,6 +144,39 @@ class RolloutDriver {
       chk(hipStreamWaitEvent(st, ev_side_, 0), "hipStreamWaitEvent");
     }
     return {T, tail};     // converted to a tuple after the GIL is re-acquired
+  }
+
+  // Persistent small-scene rollout (ctrl.hip rollout_small_kernel): the whole rollout in one
+  // launch, early stop decided on the device; returns (T, true) -- the kernel also scanned s_T.
+  std::pair<int, bool> run_small(u64 stream, bool early_stop) {
+    if (!small_ctl_) throw std::runtime_error("RolloutDriver: no small-scene control buffer");
+    hipStream_t st = ST(stream);
+    int* ctl = P<int>(small_ctl_);
+    chk(hipMemsetAsync(ctl, 0, 2 * sizeof(int), st), "hipMemsetAsync");
+    mb::RolloutSmallArgs a{};
+    mb::CtrlArgs& c = a.c;
+    c.dim = D_;
+    c.S = S_at(0); c.s_env = Nn_;
+    c.G = P<const float>(G_);
+    c.B = B_; c.N = N_; c.K = K_;
+    c.wpack = P<const h16>(ctrl_w_); c.f_edge = f_edge_; c.f_node = f_node_; c.wvec = P<const float>(ctrl_v_);
+    c.A = P<float>(A_);
+    c.dist_sum = P<unsigned long long>(dist_); c.act_sum = P<unsigned long long>(act_);
+    c.noise_key = P<const unsigned long long>(noise_key_); c.noise_prob = noise_prob_; c.noise_scale = noise_scale_;
+    c.dt = dt_; c.obs_r = obs_r_; c.sqrt3 = sqrt3_;
+    c.pooled = P<h16>(pooled_); c.argmax = P<uint8_t>(argmax_);
+    c.apw = small_apw_;
+    a.idx = P<int>(idx_); a.dang = P<uint8_t>(dang_); a.cnt = P<float>(cnt_);
+    a.safe = safety_ ? P<float>(safe_) : nullptr;
+    a.Nn = Nn_; a.Tmax = Tmax_; a.knn_tail = knn_tail_;
+    a.r2_train = r2_train_; a.ttc_train = ttc_train_; a.r2_check = r2_check_; a.ttc_check = ttc_check_;
+    a.done_thr = early_stop ? done_thr_ : -INFINITY;
+    a.ctl = ctl;
+    chk((prec_ == 2 ? mb_rollout_small_x3 : prec_ == 1 ? mb_rollout_small_f16 : mb_rollout_small)(&a, st), "rollout_small");
+    chk(hipMemcpyAsync(host_ctl_, ctl, 2 * sizeof(int), hipMemcpyDeviceToHost, st), "hipMemcpyAsync");
+    chk(hipStreamSynchronize(st), "hipStreamSynchronize");
+    const int T = host_ctl_[0] == B_ ? std::min(Tmax_, host_ctl_[1] + 1) : Tmax_;
+    return {T, true};
   }
 
  private:
@@ -227,6 +264,9 @@ class RolloutDriver {
   float noise_prob_, noise_scale_;
   u64 scan_ws_;
   long scan_ws_env_;
+  u64 small_ctl_ = 0;
+  int small_apw_ = 0, knn_tail_ = 0;
+  int* host_ctl_ = nullptr;
   int f_edge_, f_node_, f_fwd_;
   float r2_train_, ttc_train_, r2_check_, ttc_check_, dt_, obs_r_, sqrt3_, dist_thr_, dist_eps_, done_thr_;
   std::vector<hipEvent_t> ev_copy_;
@@ -331,6 +371,8 @@ void register_runtime(py::module& m) {
       .def("run", &BpttDriver::run, py::arg("T"), py::arg("act_coef"), py::arg("stream"));
   py::class_<RolloutDriver>(m, "RolloutDriver")
       .def(py::init<py::dict>())
+      .def("run_small", &RolloutDriver::run_small, py::arg("stream"), py::arg("early_stop"),
+           py::call_guard<py::gil_scoped_release>())
       .def("run", &RolloutDriver::run, py::arg("stream"), py::arg("hstream"), py::arg("copy_stream"),
            py::arg("early_stop"),
            // the loop blocks on hipEventSynchronize: let other Python threads run meanwhile

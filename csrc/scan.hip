@@ -15,26 +15,10 @@
 #include "common.h"
 #include "args.h"
 #include "state.h"
+#include "ttc.h"
 
 namespace mb {
 
-
-// D-dimensional TTC test on relative position p and velocity v (sums in coordinate order)
-template <int D>
-DEV bool ttc_danger(const float (&p)[D], const float (&v)[D], float r2, float ttc) {
-  float alpha = v[0] * v[0], pv = p[0] * v[0], pp = p[0] * p[0];
-#pragma unroll
-  for (int q = 1; q < D; ++q) { alpha = alpha + v[q] * v[q]; pv = pv + p[q] * v[q]; pp = pp + p[q] * p[q]; }
-  float beta = 2.0f * pv;
-  float gamma = pp - r2;
-  float disc = beta * beta - (4.0f * alpha) * gamma;
-  bool dist_d = gamma < 0.f;
-  bool two_pos = (disc > 0.f) && (gamma > 0.f) && (beta < 0.f);
-  float t2 = (2.0f * alpha) * ttc;
-  float bt = beta + t2;
-  bool lt = ((-beta) - t2 < 0.f) || (bt * bt < disc);
-  return dist_d || (two_pos && lt);
-}
 
 // ---------------------------------------------------------------------------------------
 // Spatial ordering. The top-K insertion is wave-divergent: a wave pays for the 12-step
@@ -123,9 +107,6 @@ static inline size_t scan_lds_bytes(int Nn) {
   return (size_t)Np * 32 + (size_t)nch * 32 + (size_t)nsc * 32;
 }
 
-// (d2, index) packed into one 64-bit key: d2 >= 0, so its IEEE bits order like the values and
-// a single unsigned compare is the lexicographic (distance, lower index) order.
-DEV uint64_t knn_key(float d2, unsigned j) { return ((uint64_t)__float_as_uint(d2) << 32) | j; }
 constexpr uint64_t KEY_EMPTY = (0x7f800000ull << 32) | 0xffffffffull;   // (+inf, max index)
 
 template <int K>

@@ -43,6 +43,8 @@ class HipEngine:
                               # step at >= 16K agents per rank, up to every 4th for small scenes)
     reduce_late = 0           # >0: dS steps reduced before the BPTT starts, the rest on the aux stream
                               # during it (A/B on MI355X: neutral-to-slower, 7.63 vs 7.66 ms; off)
+    small_rollout = True      # envs of <= native.SMALL_MAXN graph nodes: the whole rollout is ONE
+                              # persistent launch (one workgroup per env, device-side early stop)
 
     def __init__(self, trainer):
         self.tr = trainer
@@ -53,6 +55,7 @@ class HipEngine:
         self.overlap_hfwd = bool(int(os.environ.get("MACBF_OVERLAP_HFWD", int(self.overlap_hfwd))))
         self.reduce_late = int(os.environ.get("MACBF_REDUCE_LATE", self.reduce_late))
         self.native_rollout = bool(int(os.environ.get("MACBF_NATIVE_ROLLOUT", int(self.native_rollout))))
+        self.small_rollout = bool(int(os.environ.get("MACBF_SMALL_ROLLOUT", int(self.small_rollout))))
         self.bptt_groups = int(os.environ.get("MACBF_BPTT_GROUPS", self.bptt_groups))
         if cfg.num_envs % self.bptt_groups:
             self.bptt_groups = 1
@@ -74,6 +77,9 @@ class HipEngine:
         if self.K > C.MAX_TOP_K:
             raise ValueError(f"top_k <= {C.MAX_TOP_K} supported by the native kernels")
         self.Tmax = cfg.inner_loops
+        self.small_rollout = self.small_rollout and self.native_rollout and self.Nn <= native.SMALL_MAXN
+        if self.small_rollout:
+            self.overlap_hfwd = False     # the CBF h of all main slots runs after the one-launch rollout
         # kernel precision (csrc/prec.h): bf16 / fp16 MFMA inputs, or "fp32" -- the reference
         # precision, fp32-accurate 3-term split-bf16 kernels (x3)
         mdt = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": torch.float32}.get(cfg.dtype)
@@ -147,6 +153,7 @@ class HipEngine:
         self.valid_buf = torch.zeros(T, B, dtype=u8, device=dev)
         # exploration noise (reference train.py:65-67): counter-based device RNG keyed per iteration
         self.noise_key = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.small_ctl = torch.zeros(2, dtype=i32, device=dev)     # persistent rollout: [envs done, max step]
         self.nb_node, self.nb_edge = native.ctrl_bwd_grids(B * N, dev)
         # BPTT env groups (independent chains on separate streams): per-group grids and slab rows
         Gp = self.bptt_groups
@@ -263,6 +270,8 @@ class HipEngine:
                 done_thr=float(C.DIST_MIN_CHECK),
                 noise_key=native.ptr(self.noise_key) if cfg.add_noise_prob > 0 else 0,
                 scan_ws=native.ptr(scan_ws), scan_ws_env=int(scan_f4),
+                small_ctl=native.ptr(self.small_ctl) if self.small_rollout else 0,
+                small_apw=int(native.small_apw(N)), knn_tail=int(not self.reuse),
                 noise_prob=float(cfg.add_noise_prob), noise_scale=float(cfg.noise_scale),
                 fork_device_scope=int(os.environ.get("MACBF_FORK_DEVICE_SCOPE", "1"))))
             if pw.ctrl_v.numel() < 352 or pw.ctrl_w.numel() < (c["f_node"] + 54) * 512 * (2 if pw.x3 else 1):
@@ -288,6 +297,10 @@ class HipEngine:
         cur = torch.cuda.current_stream(self.dev)
         overlap = self.dedup and self.overlap_hfwd
         if self.native_rollout and not torch.cuda.is_current_stream_capturing():
+            if self.small_rollout:
+                # one persistent launch for the whole rollout (csrc/ctrl.hip rollout_small_kernel)
+                T, tail_scanned = self._driver().run_small(cur.cuda_stream, bool(early_stop))
+                return self._tail_scan(T, tail_scanned)
             # the per-step launch loop in C++ (csrc/runtime.cpp): same launches, same order
             T, tail_scanned = self._driver().run(cur.cuda_stream, self.hstream.cuda_stream if overlap else 0,
                                                  self.copy_stream.cuda_stream, bool(early_stop))

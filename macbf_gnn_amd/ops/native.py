@@ -27,6 +27,14 @@ class NativeError(RuntimeError):
 def lib():
     global _LIB
     if _LIB is None:
+        alt = os.environ.get("MACBF_EXT")
+        if alt:   # experiment builds (scripts/build_variants.sh) loaded in place of the in-tree .so
+            import importlib.util
+            import sys
+            spec = importlib.util.spec_from_file_location("macbf_gnn_amd._C", alt)
+            mod = importlib.util.module_from_spec(spec)
+            sys.modules["macbf_gnn_amd._C"] = mod
+            spec.loader.exec_module(mod)
         try:
             from .. import _C  # noqa: F401  (in-tree .so)
         except ImportError as e:  # pragma: no cover - exercised on GPU boxes only
@@ -149,6 +157,16 @@ def from_records(r: torch.Tensor) -> torch.Tensor:
 
 
 # ----------------------------------------------------------------------------- kernels
+SMALL_MAXN = 64             # envs up to this many graph nodes: persistent one-launch rollout (ctrl.hip)
+SMALL_WAVES = 8
+
+
+def small_apw(N: int) -> int:
+    """Agents per wave of the persistent rollout's edge phase: the env's agents over its 8 waves."""
+    a = -(-N // SMALL_WAVES)
+    return max(2, min(32, a + (a & 1)))
+
+
 SCAN_MAX_N = 4096           # envs up to this many graph nodes are staged whole in LDS
 SCAN_MAX_NODES = 36864      # beyond: global staging (csrc/scan.hip scan_stage_kernel), boxes in LDS
 

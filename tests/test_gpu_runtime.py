@@ -10,11 +10,18 @@ DEV = torch.device("cuda")
 
 
 def _trainer(**kw):
+    """Launch-per-step paths (the persistent small-scene rollout is tested in test_gpu_small.py)."""
     from macbf_gnn_amd.engine import Trainer
+    from macbf_gnn_amd.engine.hip_engine import HipEngine
     from macbf_gnn_amd.parallel import DP
     cfg = C.TrainConfig(num_agents=kw.pop("N", 64), num_envs=kw.pop("B", 4), inner_loops=kw.pop("T", 30),
                         seed=1, device="hip", **kw)
-    return Trainer(cfg, device=DEV, dp=DP(device=DEV))
+    old = HipEngine.small_rollout
+    HipEngine.small_rollout = False
+    try:
+        return Trainer(cfg, device=DEV, dp=DP(device=DEV))
+    finally:
+        HipEngine.small_rollout = old
 
 
 def _rollout(tr, native_rollout, s0, g, early_stop):

@@ -1,0 +1,97 @@
+"""Persistent small-scene rollout (csrc/ctrl.hip rollout_small_kernel): one launch for the whole
+rollout, one workgroup per env, device-side early stop. It must reproduce the launch-per-step
+native driver bit for bit: horizon, trajectories, kNN graphs, danger bits, counts, safety, actions,
+per-env sums, pooled features / argmax slots, and the training gradient."""
+import pytest
+import torch
+
+from macbf_gnn_amd import config as C
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda")
+
+
+def _trainer(small, **kw):
+    from macbf_gnn_amd.engine import Trainer
+    from macbf_gnn_amd.engine.hip_engine import HipEngine
+    from macbf_gnn_amd.parallel import DP
+    cfg = C.TrainConfig(num_agents=kw.pop("N", 32), num_envs=kw.pop("B", 4), inner_loops=kw.pop("T", 40),
+                        seed=kw.pop("seed", 3), device="hip", **kw)
+    old = HipEngine.small_rollout
+    HipEngine.small_rollout = small
+    try:
+        tr = Trainer(cfg, device=DEV, dp=DP(device=DEV))
+    finally:
+        HipEngine.small_rollout = old
+    assert tr.engine.small_rollout == (small and tr.engine.Nn <= 64)
+    return tr
+
+
+def _outputs(tr, s0, g, obs, early_stop):
+    eng = tr.engine
+    T = eng.rollout(s0, g, obs, early_stop=early_stop)
+    torch.cuda.synchronize()
+    out = dict(S=eng.S[: T + 1], idx=eng.idx[:T], dang=eng.dang[:T], cnt=eng.cnt[:T], A=eng.A[:T],
+               dist=eng.dist[:T], act=eng.act[:T], pooled=eng.pooled[:T], argmax=eng.argmax[:T])
+    if tr.cfg.compute_safety:
+        out["safe"] = eng.safe[: T + 1]
+    return T, {k: v.clone() for k, v in out.items()}
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+@pytest.mark.parametrize("early_stop", [True, False])
+def test_small_rollout_matches_per_step_driver(dtype, early_stop):
+    a, b = _trainer(False, dtype=dtype), _trainer(True, dtype=dtype)
+    b.fp.flat.copy_(a.fp.flat)
+    b.engine.after_update()
+    s0, g, obs = a.sample()
+    Ta, oa = _outputs(a, s0, g, obs, early_stop)
+    Tb, ob = _outputs(b, s0, g, obs, early_stop)
+    assert Ta == Tb
+    if early_stop:
+        assert Ta < a.cfg.inner_loops
+    for k in oa:
+        assert torch.equal(oa[k], ob[k]), k
+
+
+@pytest.mark.parametrize("kw", [dict(dim=3, num_obstacles=2, N=24), dict(N=64, B=2), dict(N=10, B=5),
+                                dict(N=32, B=3, add_noise_prob=0.5, noise_scale=0.3)])
+def test_small_rollout_variants(kw):
+    """3-D with obstacle nodes (Nn = 24 + 24), a full 64-node env, an odd agent count, and the
+    device exploration noise (keyed by the global env index)."""
+    a, b = _trainer(False, T=25, **kw), _trainer(True, T=25, **kw)
+    b.fp.flat.copy_(a.fp.flat)
+    b.engine.after_update()
+    s0, g, obs = a.sample()
+    Ta, oa = _outputs(a, s0, g, obs, True)
+    Tb, ob = _outputs(b, s0, g, obs, True)
+    assert Ta == Tb
+    for k in oa:
+        assert torch.equal(oa[k], ob[k]), k
+
+
+def test_small_rollout_training_step_matches():
+    a, b = _trainer(False, T=20), _trainer(True, T=20)
+    b.fp.flat.copy_(a.fp.flat)
+    b.engine.after_update()
+    s0, g, obs = a.sample()
+    sa = a.engine.step(s0, g, obs)
+    sb = b.engine.step(s0, g, obs)
+    assert float(sa["T"]) == float(sb["T"])
+    assert torch.equal(a.fp.grad, b.fp.grad)
+
+
+def test_small_rollout_repeatable_and_trains():
+    tr = _trainer(True, T=30, B=6)
+    s0, g, obs = tr.sample()
+    T1, o1 = _outputs(tr, s0, g, obs, True)
+    T2, o2 = _outputs(tr, s0, g, obs, True)
+    assert T1 == T2
+    for k in o1:
+        assert torch.equal(o1[k], o2[k]), k
+    before = tr.fp.flat.clone()
+    for _ in range(3):
+        st = tr.train_step()
+    torch.cuda.synchronize()
+    assert torch.isfinite(tr.fp.flat).all() and not torch.equal(before, tr.fp.flat)
+    assert float(st["agent_steps"]) > 0
