@@ -19,6 +19,7 @@
 #include "args.h"
 #include "state.h"
 #include "ttc.h"
+#include "combine.h"
 
 namespace mb {
 namespace MB_PREC {
@@ -463,7 +464,7 @@ extern "C" int MB_SYM(ctrl_fwd)(const mb::CtrlArgs* a, int num_cu, hipStream_t s
   using namespace mb::MB_PREC;
   if (a->K > 16 || a->K < 1) return -1;
   if (X3 && !a->pooled) return -2;            // the x3 node phase reads the stored pooled rows
-  const int apw = X3 ? 32 : ((a->apw >= 2 && a->apw <= 32) ? a->apw : 32);
+  const int apw = (a->apw >= 2 && a->apw <= 32 && !(a->apw & 1)) ? a->apw : 32;
   const int groups = (a->B * a->N + apw - 1) / apw;
   int blocks = (groups + CTRL_WAVES - 1) / CTRL_WAVES;
   const int maxb = num_cu > 0 ? num_cu * 2 : blocks;
@@ -480,12 +481,14 @@ extern "C" int MB_SYM(ctrl_fwd)(const mb::CtrlArgs* a, int num_cu, hipStream_t s
   }
   if constexpr (X3) {
     const size_t ldn = (size_t)54 * FRAG_SZ + CTRL_VEC * 4;
+    int nblocks = (a->B * a->N + 32 * CTRL_WAVES - 1) / (32 * CTRL_WAVES);     // 32-agent node groups
+    if (nblocks > maxb) nblocks = maxb;
     if (a->dim == 3) {
       (void)hipFuncSetAttribute((const void*)ctrl_node_fwd_kernel<CTRL_WAVES, 3>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ldn);
-      hipLaunchKernelGGL((ctrl_node_fwd_kernel<CTRL_WAVES, 3>), dim3(blocks), dim3(CTRL_WAVES * 64), ldn, st, b);
+      hipLaunchKernelGGL((ctrl_node_fwd_kernel<CTRL_WAVES, 3>), dim3(nblocks), dim3(CTRL_WAVES * 64), ldn, st, b);
     } else {
       (void)hipFuncSetAttribute((const void*)ctrl_node_fwd_kernel<CTRL_WAVES, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ldn);
-      hipLaunchKernelGGL((ctrl_node_fwd_kernel<CTRL_WAVES, 2>), dim3(blocks), dim3(CTRL_WAVES * 64), ldn, st, b);
+      hipLaunchKernelGGL((ctrl_node_fwd_kernel<CTRL_WAVES, 2>), dim3(nblocks), dim3(CTRL_WAVES * 64), ldn, st, b);
     }
   }
   return (int)hipGetLastError();
@@ -549,9 +552,10 @@ DEV void store_tile_add(float* dst, int ncols, int mt, int nt, const f32x16& old
   for (int reg = 0; reg < 16; ++reg) dst[(32 * mt + acc_row(reg, h)) * ncols + 32 * nt + r] = old[reg] + c[reg];
 }
 
+// Node backward over the chunks c0, c0 + cstride, ... of `a` (smem: the kernel's dynamic LDS;
+// P: this workgroup's slab row)
 template <int D>
-__global__ __launch_bounds__(NB_WAVES * 64, 1) void ctrl_node_bwd_kernel(CtrlNodeBwdArgs a) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+DEV void node_bwd_body(const CtrlNodeBwdArgs& a, unsigned char* smem, long c0, long cstride, float* P) {
   constexpr int RM = (X3 ? 2 : 1) * NODE_RM_ELEMS;
   h16* wr = reinterpret_cast<h16*>(smem);
   float* vl = reinterpret_cast<float*>(smem + RM * 2);
@@ -579,7 +583,7 @@ __global__ __launch_bounds__(NB_WAVES * 64, 1) void ctrl_node_bwd_kernel(CtrlNod
   const int n1 = (wave < 2) ? 3 : 2;
   const h16x8 zz = zero_h8();
 
-  for (long chunk = blockIdx.x; chunk < nchunks; chunk += gridDim.x) {
+  for (long chunk = c0; chunk < nchunks; chunk += cstride) {
     const int ga = (int)(chunk * NB_CH) + erow;
     const bool ok = ga < total;
     // stage turns holding at least one valid agent (a partial last chunk -- all but the first
@@ -858,7 +862,6 @@ __global__ __launch_bounds__(NB_WAVES * 64, 1) void ctrl_node_bwd_kernel(CtrlNod
 #ifdef CTRL_X_NOSLAB
   if (a.partial) return;                        // ablation: no slab read-modify-write
 #endif
-  float* P = a.partial + (long)blockIdx.x * CTRL_NODE_PARTIAL;
   // all slab loads first (see load_tile), then the adds and stores; the first BPTT step writes
   // the slab (no zero-fill pass, no loads)
   f32x16 o1[3], o2[2], o3[2], o4 = zero16();
@@ -908,6 +911,12 @@ __global__ __launch_bounds__(NB_WAVES * 64, 1) void ctrl_node_bwd_kernel(CtrlNod
   }
 }
 
+template <int D>
+__global__ __launch_bounds__(NB_WAVES * 64, 1) void ctrl_node_bwd_kernel(CtrlNodeBwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  node_bwd_body<D>(a, smem, blockIdx.x, gridDim.x, a.partial + (long)blockIdx.x * CTRL_NODE_PARTIAL);
+}
+
 // ---------------------------------------------------------------------------------------
 // EB_WAVES waves share a chunk of 32*EB_WAVES agents; each stage contracts the 32*EB_WAVES edges
 // of one tile round (8 waves: 256 edges per barrier pair, one dW2 tile per wave; 4 waves: 128
@@ -925,9 +934,10 @@ constexpr size_t EB_STAGE = (size_t)(X3 ? 2 : 1) * EB_PL * 2;
 
 size_t ctrl_edge_bwd_lds() { return (size_t)22 * FRAG_SZ + EB_STAGE; }
 
+// Edge backward over the work items w0, w0 + wstride, ... of `a` (smem: the kernel's dynamic
+// LDS; P: this workgroup's slab row)
 template <int D>
-__global__ __launch_bounds__(EB_WAVES * 64, (EB_WAVES == 4 && !X3) ? 2 : 1) void ctrl_edge_bwd_kernel(CtrlEdgeBwdArgs a) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+DEV void edge_bwd_body(const CtrlEdgeBwdArgs& a, unsigned char* smem, long w0, long wstride, float* P) {
   h16* wf = reinterpret_cast<h16*>(smem);                 // ew1f (2) | ew2tn (16) | ew1ft (4)
   h16* stg = reinterpret_cast<h16*>(smem + 22 * FRAG_SZ);
   block_copy16(wf, a.wpack + (size_t)a.f_ew1f * FRAG_ELEMS, 2 * FRAG_SZ);
@@ -950,7 +960,7 @@ __global__ __launch_bounds__(EB_WAVES * 64, (EB_WAVES == 4 && !X3) ? 2 : 1) void
   // use qsplit = 1
   const int QP = a.qsplit > 1 ? a.qsplit : 1;
   const long nwork = nchunks * QP;
-  for (long w = blockIdx.x; w < nwork; w += gridDim.x) {
+  for (long w = w0; w < nwork; w += wstride) {
     const long chunk = w / QP;
     const int part = (int)(w - chunk * QP);
     const int q0 = part * 16 / QP, q1 = (part + 1) * 16 / QP;
@@ -1123,7 +1133,6 @@ __global__ __launch_bounds__(EB_WAVES * 64, (EB_WAVES == 4 && !X3) ? 2 : 1) void
 #ifdef CTRL_X_NOSLAB
   if (a.partial) return;                        // ablation: no slab read-modify-write
 #endif
-  float* P = a.partial + (long)blockIdx.x * CTRL_EDGE_PARTIAL;
   __shared__ float ebred[EB_WAVES][EB_TA][32];
   // every slab load of the tail first (see load_tile): dW2 tiles, this thread's dW1 elements,
   // the eb2 element
@@ -1177,6 +1186,12 @@ __global__ __launch_bounds__(EB_WAVES * 64, (EB_WAVES == 4 && !X3) ? 2 : 1) void
     const int t0 = 2 * mt, t1 = 2 * mt + 1;
     P[EP_B2 + 32 * mt + rr] = ob2 + (ebred[t0 % EB_WAVES][t0 / EB_WAVES][rr] + ebred[t1 % EB_WAVES][t1 / EB_WAVES][rr]);
   }
+}
+
+template <int D>
+__global__ __launch_bounds__(EB_WAVES * 64, (EB_WAVES == 4 && !X3) ? 2 : 1) void ctrl_edge_bwd_kernel(CtrlEdgeBwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  edge_bwd_body<D>(a, smem, blockIdx.x, gridDim.x, a.partial + (long)blockIdx.x * CTRL_EDGE_PARTIAL);
 }
 
 // =======================================================================================
@@ -1368,6 +1383,92 @@ __global__ __launch_bounds__(SR_WAVES * 64) void rollout_small_kernel(RolloutSma
 
 size_t rollout_small_lds() { return (size_t)CTRL_FWD_FRAGS * FRAG_SZ + CTRL_VEC * 4; }
 
+// ---------------------------------------------------------------------------------------
+// Persistent small-scene BPTT (envs of <= NB_CH agents; the reverse-time loop of
+// train.py:58-103's autograd, BpttDriver's launches): one workgroup per env runs, for
+// t = T-1..0, the node backward, the edge backward and the BPTT combine of its env -- the same
+// device bodies as the per-step kernels over a B = 1 view of the env, so the results are those
+// of the launch-per-step path bit for bit. Envs never interact, so the only synchronisation is
+// the workgroup barrier between phases (the phases reuse the dynamic LDS). Weight gradients
+// accumulate in the env's slab row (first step writes).
+// ---------------------------------------------------------------------------------------
+// The phases are separate (non-inlined) functions here: inlined into the time loop the node
+// body's register allocation degrades (scratch spills); each call is one per step.
+template <int D>
+__device__ __noinline__ void node_bwd_call(const CtrlNodeBwdArgs& a, unsigned char* smem, float* P) {
+  node_bwd_body<D>(a, smem, 0, 1, P);
+}
+template <int D>
+__device__ __noinline__ void edge_bwd_call(const CtrlEdgeBwdArgs& a, unsigned char* smem, float* P) {
+  edge_bwd_body<D>(a, smem, 0, 1, P);
+}
+
+template <int D>
+__global__ __launch_bounds__(NB_WAVES * 64, 1) void bptt_small_kernel(BpttSmallArgs ba) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  constexpr int R = REC<D>;
+  const int b = blockIdx.x, T = ba.T, Nn = ba.Nn;
+  const int B = ba.nb.B, N = ba.nb.N, K = ba.eb.K;
+  const long nk = (long)N * K;
+  float* Pn = ba.nb.partial + (long)b * CTRL_NODE_PARTIAL;
+  float* Pe = ba.eb.partial + (long)b * CTRL_EDGE_PARTIAL;
+  h16* dPb = ba.nb.dP + (long)b * N * PROW;
+  float4* egb = ba.nb.ego + (long)b * N * R;
+  float4* dEcb = ba.eb.dEc + (long)b * nk * R;
+  for (int t = T - 1; t >= 0; --t) {
+    const long tb = (long)t * B + b;
+    // G_{t+1} = dL/ds_{t+1}: the direct terms dS_T for the last step, else the combined Gb
+    const float4* Gn = (t == T - 1 ? ba.cb.dS : ba.cb.Gout) + (tb + B) * N * R;
+    const float4* St = ba.nb.S + tb * Nn * R;
+    {
+      CtrlNodeBwdArgs a = ba.nb;
+      a.pooled = ba.nb.pooled + tb * N * PROW; a.p_env = (long)N * PROW;
+      a.S = St; a.s_env = Nn;
+      a.G = ba.nb.G + (long)b * N * D;
+      a.A = ba.nb.A + tb * N * D; a.a_env = N;
+      a.Gn = Gn; a.gn_env = N;
+      a.valid = ba.nb.valid ? ba.nb.valid + tb : nullptr; a.v_env = 1;
+      a.B = 1;
+      a.dP = dPb; a.dp_env = (long)N * PROW;
+      a.ego = egb;
+      a.init = t == T - 1;
+      node_bwd_call<D>(a, smem, Pn);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // dP / ego stores complete
+    __syncthreads();
+    {
+      CtrlEdgeBwdArgs a = ba.eb;
+      a.S = St; a.s_env = Nn;
+      a.idx = ba.eb.idx + tb * nk; a.i_env = nk;
+      a.argmax = ba.eb.argmax + tb * N * 128; a.am_env = (long)N * 128;
+      a.dP = dPb; a.dp_env = (long)N * PROW;
+      a.B = 1;
+      a.dEc = dEcb; a.de_env = nk;
+      a.qsplit = 1;
+      a.init = t == T - 1;
+      edge_bwd_call<D>(a, smem, Pe);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (t > 0) {        // G_0 is not needed (s_0 is sampled)
+      CombineArgs a = ba.cb;
+      a.dS = ba.cb.dS + tb * N * R; a.ds_env = N;
+      a.ego = egb;
+      a.dEc = dEcb;
+      a.ptr = ba.cb.ptr + tb * (Nn + 1); a.ptr_env = Nn + 1;
+      a.edges = ba.cb.edges + tb * nk; a.edges_env = nk;
+      a.Gn = Gn; a.gn_env = N;
+      a.Gout = ba.cb.Gout + tb * N * R; a.go_env = N;
+      a.B = 1;
+      for (int node = threadIdx.x / RG; node < N; node += NB_WAVES * WAVE / RG) combine_node<D>(a, node, threadIdx.x % RG);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+  }
+}
+
+size_t bptt_small_lds() { return ctrl_node_bwd_lds() > ctrl_edge_bwd_lds() ? ctrl_node_bwd_lds() : ctrl_edge_bwd_lds(); }
+
 }  // namespace MB_PREC
 }  // namespace mb
 
@@ -1414,6 +1515,27 @@ extern "C" int MB_SYM(rollout_small)(const mb::RolloutSmallArgs* a, hipStream_t 
   } else {
     (void)hipFuncSetAttribute((const void*)rollout_small_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL(rollout_small_kernel<2>, dim3(c.B), dim3(SR_WAVES * 64), lds, st, *a);
+  }
+  return (int)hipGetLastError();
+}
+
+extern "C" int MB_SYM(bptt_small)(const mb::BpttSmallArgs* a, hipStream_t st) {
+  using namespace mb;
+  using namespace mb::MB_PREC;
+  const int B = a->nb.B, N = a->nb.N, K = a->eb.K;
+  if (K > 16 || K < 1 || N < 1 || N > NB_CH || a->eb.N != N || a->eb.B != B || a->cb.N != N || a->cb.K != K ||
+      a->Nn < N || a->T < 1 || B < 1)
+    return -1;
+  if (!a->nb.partial || !a->eb.partial || !a->nb.dP || !a->nb.ego || !a->eb.dEc || !a->cb.dS || !a->cb.Gout ||
+      !a->cb.ptr || !a->cb.edges)
+    return -2;
+  const size_t lds = bptt_small_lds();
+  if (a->nb.dim == 3) {
+    (void)hipFuncSetAttribute((const void*)bptt_small_kernel<3>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(bptt_small_kernel<3>, dim3(B), dim3(NB_WAVES * 64), lds, st, *a);
+  } else {
+    (void)hipFuncSetAttribute((const void*)bptt_small_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(bptt_small_kernel<2>, dim3(B), dim3(NB_WAVES * 64), lds, st, *a);
   }
   return (int)hipGetLastError();
 }

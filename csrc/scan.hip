@@ -94,9 +94,9 @@ __global__ __launch_bounds__(SORT_BLOCK) void cell_sort_kernel(CellSortArgs a) {
   }
 }
 
-// Block = BS/64 waves x 32 agents (consecutive on the curve), 2 lanes each. BS = 256 for envs
-// up to 512 nodes; 512 above (the whole env is staged per block: bigger blocks amortise it and
-// keep one 8-wave block per CU at the 128 KiB staging size of a 4096-node env).
+// Block = BS/64 waves x 64/LPA agents (consecutive on the curve), LPA lanes each. BS = 256 for
+// envs up to 512 nodes; SCAN_BS_BIG above (the whole env is staged per block: bigger blocks
+// amortise it; a 4096-node env stages 128 KiB, one 16-wave block per CU).
 constexpr int SCAN_MAXN = 4096;      // whole env staged in LDS
 constexpr int SCH = 8;               // candidates per chunk (one bounding box each)
 constexpr int SSC = 8;               // chunks per superchunk (second culling level)
@@ -473,7 +473,7 @@ __global__ __launch_bounds__(BS) void scan_kernel(ScanArgs a) {
 }
 
 #ifndef SCAN_LPA
-#define SCAN_LPA 2
+#define SCAN_LPA 4      // lanes per agent (A/B at 1024 x 64: 2 -> 4 lanes 65.4 -> 61.5 us per step)
 #endif
 
 template <int K, int D, int BS>
@@ -495,7 +495,7 @@ static void launch_kdb(const ScanArgs& a, hipStream_t st) {
 }
 
 #ifndef SCAN_BS_BIG
-#define SCAN_BS_BIG 512
+#define SCAN_BS_BIG 1024  // block size above 512 nodes per env (4 lanes/agent: 512 -> 1024, 61.5 -> 60.5 us)
 #endif
 
 template <int K, int D>

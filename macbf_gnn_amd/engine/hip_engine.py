@@ -45,6 +45,11 @@ class HipEngine:
                               # during it (A/B on MI355X: neutral-to-slower, 7.63 vs 7.66 ms; off)
     small_rollout = True      # envs of <= native.SMALL_MAXN graph nodes: the whole rollout is ONE
                               # persistent launch (one workgroup per env, device-side early stop)
+    small_bptt = False        # envs of <= native.SMALL_MAXN agents: the BPTT recursion as ONE
+                              # persistent launch (one workgroup per env). Off: measured 3x slower
+                              # at 32 x 1 (2.17 vs 0.69 ms) -- the per-step launches spread a small
+                              # env's 16 edge tile rounds over 16 workgroups (qsplit), one
+                              # workgroup per env runs them in sequence
 
     def __init__(self, trainer):
         self.tr = trainer
@@ -56,6 +61,7 @@ class HipEngine:
         self.reduce_late = int(os.environ.get("MACBF_REDUCE_LATE", self.reduce_late))
         self.native_rollout = bool(int(os.environ.get("MACBF_NATIVE_ROLLOUT", int(self.native_rollout))))
         self.small_rollout = bool(int(os.environ.get("MACBF_SMALL_ROLLOUT", int(self.small_rollout))))
+        self.small_bptt = bool(int(os.environ.get("MACBF_SMALL_BPTT", int(self.small_bptt))))
         self.bptt_groups = int(os.environ.get("MACBF_BPTT_GROUPS", self.bptt_groups))
         if cfg.num_envs % self.bptt_groups:
             self.bptt_groups = 1
@@ -78,6 +84,7 @@ class HipEngine:
             raise ValueError(f"top_k <= {C.MAX_TOP_K} supported by the native kernels")
         self.Tmax = cfg.inner_loops
         self.small_rollout = self.small_rollout and self.native_rollout and self.Nn <= native.SMALL_MAXN
+        self.small_bptt = self.small_bptt and self.native_bptt and self.N <= native.SMALL_MAXN
         if self.small_rollout:
             self.overlap_hfwd = False     # the CBF h of all main slots runs after the one-launch rollout
         # kernel precision (csrc/prec.h): bf16 / fp16 MFMA inputs, or "fp32" -- the reference
@@ -162,8 +169,10 @@ class HipEngine:
         self.grp_nb = native.ctrl_bwd_grids((B // Gp) * N, dev)
         rows_n = max(self.nb_node, Gp * self.grp_nb[0])
         rows_e = max(self.nb_edge, Gp * self.grp_nb[1])
-        self.part_node = torch.zeros(rows_n, native.CTRL_NODE_PARTIAL, dtype=f32, device=dev)
-        self.part_edge = torch.zeros(rows_e, native.CTRL_EDGE_PARTIAL, dtype=f32, device=dev)
+        # slab rows written by the launch-per-step BPTT / by the persistent one (one row per env)
+        self.slab_rows = (rows_n, rows_e)
+        self.part_node = torch.zeros(max(rows_n, B), native.CTRL_NODE_PARTIAL, dtype=f32, device=dev)
+        self.part_edge = torch.zeros(max(rows_e, B), native.CTRL_EDGE_PARTIAL, dtype=f32, device=dev)
         self.gstreams = [torch.cuda.Stream(device=dev) for _ in range(Gp - 1)]
         self.red_all = torch.zeros(native.CBF_PARTIAL + native.CTRL_NODE_PARTIAL + native.CTRL_EDGE_PARTIAL,
                                    dtype=f32, device=dev)
@@ -517,7 +526,12 @@ class HipEngine:
             rptr3 = rptr[: T * B].view(T, B, Nn + 1)
             redges3 = redges[: T * B].view(T, B, N * K)
             Gp = self.bptt_groups
-            if Gp == 1 and red_done is None and self.native_bptt:
+            slab_rows = self.slab_rows
+            if Gp == 1 and red_done is None and self.native_bptt and self.small_bptt:
+                # one persistent launch for the whole recursion (csrc/ctrl.hip bptt_small_kernel)
+                self._bdriver().run_small(T, gs * ACT_COEF, cur.cuda_stream)
+                slab_rows = (B, B)
+            elif Gp == 1 and red_done is None and self.native_bptt:
                 # the reverse-time launch loop in C++ (csrc/runtime.cpp): same launches, same order
                 self._bdriver().run(T, gs * ACT_COEF, cur.cuda_stream)
             elif Gp == 1:
@@ -557,7 +571,7 @@ class HipEngine:
             self._nb_parts = (pn, pe)
         tm.mark("bptt")
         # ---- weight-gradient slabs -> flat grad
-        pnode, pedge = (self.part_node, self.part_edge) if self.bptt else self._nb_parts
+        pnode, pedge = (self.part_node[: slab_rows[0]], self.part_edge[: slab_rows[1]]) if self.bptt else self._nb_parts
         for part, red in ((part_cbf, self.red_cbf), (pnode, self.red_node), (pedge, self.red_edge)):
             native.reduce_rows(part, red)
         native.grad_assemble(self.red_all, self.g_ptr, self.g_src, tr.fp.grad, scale=1.0 / gs)
@@ -596,7 +610,7 @@ class HipEngine:
                 ctrl_rm=native.ptr(pw.ctrl_rm), o_w1=int(pw.node_rm_off["w1"]), o_w2=int(pw.node_rm_off["w2"]),
                 o_w3=int(pw.node_rm_off["w3"]), o_w4=int(pw.node_rm_off["w4"]), ctrl_v=native.ptr(pw.ctrl_v),
                 ctrl_w=native.ptr(pw.ctrl_w), f_ew1f=int(pw.ctrl_off["ew1f"]), f_ew2tn=int(pw.ctrl_off["ew2tn"]),
-                dt=float(C.TIME_STEP), sqrt3=float(C.SQRT3)))
+                dt=float(C.TIME_STEP), sqrt3=float(C.SQRT3), small=int(self.small_bptt)))
             self._bdrv = native.lib().BpttDriver(c)
         return self._bdrv
 

@@ -368,18 +368,18 @@ def ctrl_fwd(S, G, idx, wpack, f_edge, f_node, wvec, A, Sn, dist_sum, act_sum, n
 
 
 def ctrl_fwd_apw(total_agents: int, device, n_agents: int | None = None) -> int:
-    """Agents per wave of the controller step: 32, halved (down to 4) while the scene has fewer
-    32-agent groups than two per CU, so small scenes spread the edge phase over more waves --
-    but only while every env stays covered by at most two whole waves (the per-env goal-distance
-    sums are float atomics: two addends commute, more would make the early-stop input depend
-    on the arrival order)."""
+    """Agents per wave of the controller step's edge phase: 32, halved (down to 4) while the
+    scene has fewer groups than two per CU, so small scenes spread the edge phase over more
+    waves. Any grouping gives the same results (the per-env sums are per-agent fixed-point
+    integers). MACBF_CTRL_APW overrides (A/B measurements)."""
+    env = os.environ.get("MACBF_CTRL_APW")
+    if env:
+        return int(env)
     apw, cap = 32, 2 * num_cu(device)
-    n = total_agents if n_agents is None else int(n_agents)
     for cand in (16, 8, 4):
         if (total_agents + apw - 1) // apw >= cap:
             break
-        if n % cand == 0 and n <= 2 * cand:
-            apw = cand
+        apw = cand
     return apw
 
 

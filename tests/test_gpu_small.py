@@ -11,18 +11,19 @@ pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda")
 
 
-def _trainer(small, **kw):
+def _trainer(small, small_bptt=None, **kw):
     from macbf_gnn_amd.engine import Trainer
     from macbf_gnn_amd.engine.hip_engine import HipEngine
     from macbf_gnn_amd.parallel import DP
     cfg = C.TrainConfig(num_agents=kw.pop("N", 32), num_envs=kw.pop("B", 4), inner_loops=kw.pop("T", 40),
                         seed=kw.pop("seed", 3), device="hip", **kw)
-    old = HipEngine.small_rollout
+    old = HipEngine.small_rollout, HipEngine.small_bptt
     HipEngine.small_rollout = small
+    HipEngine.small_bptt = small if small_bptt is None else small_bptt
     try:
         tr = Trainer(cfg, device=DEV, dp=DP(device=DEV))
     finally:
-        HipEngine.small_rollout = old
+        HipEngine.small_rollout, HipEngine.small_bptt = old
     assert tr.engine.small_rollout == (small and tr.engine.Nn <= 64)
     return tr
 
@@ -71,7 +72,7 @@ def test_small_rollout_variants(kw):
 
 
 def test_small_rollout_training_step_matches():
-    a, b = _trainer(False, T=20), _trainer(True, T=20)
+    a, b = _trainer(False, small_bptt=False, T=20), _trainer(True, small_bptt=False, T=20)
     b.fp.flat.copy_(a.fp.flat)
     b.engine.after_update()
     s0, g, obs = a.sample()
@@ -95,3 +96,27 @@ def test_small_rollout_repeatable_and_trains():
     torch.cuda.synchronize()
     assert torch.isfinite(tr.fp.flat).all() and not torch.equal(before, tr.fp.flat)
     assert float(st["agent_steps"]) > 0
+
+
+@pytest.mark.parametrize("kw", [dict(dtype="fp32"), dict(dtype="bf16"), dict(dtype="fp32", dim=3, num_obstacles=2, N=24),
+                                dict(dtype="fp32", N=64, B=2), dict(dtype="bf16", N=10, B=5)])
+def test_small_bptt_matches_per_step_launches(kw):
+    """Persistent BPTT (one workgroup per env, csrc/ctrl.hip bptt_small_kernel): the same device
+    bodies as the per-step kernels -> the same dL/ds_t recursion and weight gradients bit for bit
+    (slab rows differ: one per env, so the final slab sums may differ in rounding order)."""
+    a = _trainer(True, small_bptt=False, T=20, **kw)
+    b = _trainer(True, small_bptt=True, T=20, **kw)
+    assert b.engine.small_bptt and not a.engine.small_bptt
+    b.fp.flat.copy_(a.fp.flat)
+    b.engine.after_update()
+    s0, g, obs = a.sample()
+    a.engine.step(s0, g, obs)
+    b.engine.step(s0, g, obs)
+    torch.cuda.synchronize()
+    assert torch.equal(a.engine.Gb, b.engine.Gb)
+    assert torch.equal(a.engine.dP, b.engine.dP) and torch.equal(a.engine.ego, b.engine.ego)
+    torch.testing.assert_close(b.fp.grad, a.fp.grad, rtol=2e-5, atol=1e-8)
+    b.engine.step(s0, g, obs)           # deterministic run to run
+    g1 = b.fp.grad.clone()
+    b.engine.step(s0, g, obs)
+    assert torch.equal(g1, b.fp.grad)
