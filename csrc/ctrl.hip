@@ -292,7 +292,7 @@ DEV void node_phase(const CtrlArgs& a, int g0, int APW, int total, PoolFr pool, 
 // already in LDS: wl = ew1f|ew2, wn = nw1f..nw4, vl = CTRL_VEC floats, pools = one 32-row pool
 // image per wave). SPLIT (always for x3): edge phase only, the pooled rows go to global memory
 // and ctrl_node_groups runs the node phase.
-template <int D, bool SPLIT>
+template <int D, bool SPLIT, bool GNODE = false>
 DEV void ctrl_fwd_groups(const CtrlArgs& a, const h16* wl, const h16* wn, const float* vl, h16* pools, int grp0,
                          int gstride) {
   constexpr bool GPOOL = X3 || SPLIT;
@@ -380,6 +380,17 @@ DEV void ctrl_fwd_groups(const CtrlArgs& a, const h16* wl, const h16* wn, const 
 #endif
       }
     }
+    if constexpr (GPOOL && GNODE) {
+      // x3 fused step: the group's node phase right here, over the pooled rows this wave just
+      // wrote to global memory (the stores are complete after the wait; the rows were not read
+      // before, so no stale L1 line can hide them)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const int gi = min(g0 + min(r, APW - 1), total - 1);
+      const int bb = gi / N, ii = gi - bb * N;
+      const h16* prow = a.pooled + (long)bb * a.p_env + (long)ii * PROW + 8 * h;
+      node_phase<D>(a, g0, APW, total, [&](int kk) { return row_fr(prow + 16 * kk, 128); }, wn, nb2, nb3, nb4, lane);
+      continue;
+    }
     if constexpr (GPOOL) continue;     // node phase: ctrl_node_groups
     lds_wave_sync();
     if (a.pooled) {   // 32 agents x 256 B, 16 B per lane
@@ -405,19 +416,21 @@ DEV void ctrl_fwd_groups(const CtrlArgs& a, const h16* wl, const h16* wn, const 
   }
 }
 
-template <int WAVES, int D>
+// FUSE (x3): all 72 fragments in LDS (145 KB) and the node phase of each group in the same
+// wave right after its edge phase (pooled rows through global memory): one launch per step.
+template <int WAVES, int D, bool FUSE = false>
 __global__ __launch_bounds__(WAVES * 64) void ctrl_fwd_kernel(CtrlArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  constexpr int NFR = X3 ? 18 : CTRL_FWD_FRAGS;                     // fragments staged in LDS
+  constexpr int NFR = (X3 && !FUSE) ? 18 : CTRL_FWD_FRAGS;          // fragments staged in LDS
   h16* wl = reinterpret_cast<h16*>(smem);                            // ew1f, ew2 (18 frags)
   h16* wn = wl + 18 * FRAG_ELEMS;                                     // nw1f..nw4 (54 frags)
   float* vl = reinterpret_cast<float*>(smem + NFR * FRAG_SZ);
   h16* pools = reinterpret_cast<h16*>(smem + NFR * FRAG_SZ + CTRL_VEC * 4);
   block_copy16(wl, a.wpack + (size_t)a.f_edge * FRAG_ELEMS, 18 * FRAG_SZ);
-  if constexpr (!X3) block_copy16(wn, a.wpack + (size_t)a.f_node * FRAG_ELEMS, 54 * FRAG_SZ);
+  if constexpr (!X3 || FUSE) block_copy16(wn, a.wpack + (size_t)a.f_node * FRAG_ELEMS, 54 * FRAG_SZ);
   block_copy16(vl, a.wvec, CTRL_VEC * 4);
   __syncthreads();
-  ctrl_fwd_groups<D, false>(a, wl, wn, vl, pools, blockIdx.x * WAVES + threadIdx.x / WAVE, gridDim.x * WAVES);
+  ctrl_fwd_groups<D, false, FUSE>(a, wl, wn, vl, pools, blockIdx.x * WAVES + threadIdx.x / WAVE, gridDim.x * WAVES);
 }
 
 // Node phase of the controller step over the pooled rows in global memory, 32-agent groups
@@ -469,9 +482,22 @@ extern "C" int MB_SYM(ctrl_fwd)(const mb::CtrlArgs* a, int num_cu, hipStream_t s
   int blocks = (groups + CTRL_WAVES - 1) / CTRL_WAVES;
   const int maxb = num_cu > 0 ? num_cu * 2 : blocks;
   if (blocks > maxb) blocks = maxb;
-  const size_t lds = ctrl_fwd_lds();
   CtrlArgs b = *a;
   b.apw = apw;
+  // x3: one fused launch (edge + node phase per group, 145 KB of weights) unless MACBF_X3_SPLIT
+  static const bool split = [] { const char* e = getenv("MACBF_X3_SPLIT"); return e && e[0] == '1'; }();
+  if (X3 && !split) {
+    const size_t ldf = (size_t)CTRL_FWD_FRAGS * FRAG_SZ + CTRL_VEC * 4;
+    if (a->dim == 3) {
+      (void)hipFuncSetAttribute((const void*)ctrl_fwd_kernel<CTRL_WAVES, 3, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ldf);
+      hipLaunchKernelGGL((ctrl_fwd_kernel<CTRL_WAVES, 3, true>), dim3(blocks), dim3(CTRL_WAVES * 64), ldf, st, b);
+    } else {
+      (void)hipFuncSetAttribute((const void*)ctrl_fwd_kernel<CTRL_WAVES, 2, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ldf);
+      hipLaunchKernelGGL((ctrl_fwd_kernel<CTRL_WAVES, 2, true>), dim3(blocks), dim3(CTRL_WAVES * 64), ldf, st, b);
+    }
+    return (int)hipGetLastError();
+  }
+  const size_t lds = ctrl_fwd_lds();
   if (a->dim == 3) {
     (void)hipFuncSetAttribute((const void*)ctrl_fwd_kernel<CTRL_WAVES, 3>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL((ctrl_fwd_kernel<CTRL_WAVES, 3>), dim3(blocks), dim3(CTRL_WAVES * 64), lds, st, b);

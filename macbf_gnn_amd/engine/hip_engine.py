@@ -35,7 +35,10 @@ ACT_COEF = C.LOSS_SCALE * C.LOSS_WEIGHTS[4]
 class HipEngine:
     name = "hip"
     resort_every = 4          # scan: Hilbert re-sort period (rollout steps)
-    overlap_hfwd = True       # CBF h of the main slots runs on a side stream during the rollout
+    overlap_hfwd = None       # CBF h of the main slots on a side stream during the rollout (None: by
+                              # precision -- on for bf16/fp16 (A/B 7.83 -> 7.63 ms); off for fp32, whose
+                              # fused one-launch controller step holds 145 KB of LDS per workgroup,
+                              # so the slices only delay it (A/B: 15.04 with vs 14.60 ms without)
     native_rollout = True     # per-step launch loop in C++ (csrc/runtime.cpp)
     bptt_groups = 1           # independent env groups whose BPTT chains run on separate streams
     native_bptt = True        # reverse-time BPTT launch loop in C++ (csrc/runtime.cpp)
@@ -57,7 +60,8 @@ class HipEngine:
         # scheduling knobs (A/B measurements): MACBF_RESORT_EVERY, MACBF_OVERLAP_HFWD, MACBF_REDUCE_LATE
         import os
         self.resort_every = int(os.environ.get("MACBF_RESORT_EVERY", self.resort_every))
-        self.overlap_hfwd = bool(int(os.environ.get("MACBF_OVERLAP_HFWD", int(self.overlap_hfwd))))
+        ov = os.environ.get("MACBF_OVERLAP_HFWD")
+        self.overlap_hfwd = bool(int(ov)) if ov is not None else self.overlap_hfwd
         self.reduce_late = int(os.environ.get("MACBF_REDUCE_LATE", self.reduce_late))
         self.native_rollout = bool(int(os.environ.get("MACBF_NATIVE_ROLLOUT", int(self.native_rollout))))
         self.small_rollout = bool(int(os.environ.get("MACBF_SMALL_ROLLOUT", int(self.small_rollout))))
@@ -94,6 +98,8 @@ class HipEngine:
             raise ValueError(f"dtype must be bf16, fp16 or fp32 on the HIP path, got {cfg.dtype!r}")
         self.pw = PackedWeights(trainer.fp, self.D, mdt)
         self.prec = self.pw.prec
+        if self.overlap_hfwd is None:
+            self.overlap_hfwd = self.prec != "fp32"
         self.hdt = self.pw.dtype                 # packed / pooled element type (bf16 | fp16)
         self.prow = L.pooled_row(self.prec)      # pooled / dL/dpooled row: [hi | lo] for fp32
         offs = {pn: o for (m, pn, shape, o, n) in trainer.fp.specs}

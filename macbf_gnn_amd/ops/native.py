@@ -477,9 +477,12 @@ def cbf_match(idx, T, map1, src, cnt, *, recomputed=False, nev=None):
 HFWD_WAVES = 8
 
 
-def cbf_hfwd_grid(EV: int, device) -> int:
+def cbf_hfwd_grid(EV: int, device, per_cu: int | None = None) -> int:
+    """Workgroups of an h evaluation launch: up to per_cu per CU (MACBF_HFWD_PER_CU; default 4)."""
     tiles = (EV + 31) // 32
-    return max(1, min((tiles + HFWD_WAVES - 1) // HFWD_WAVES, num_cu(device) * 4))
+    if per_cu is None:
+        per_cu = int(os.environ.get("MACBF_HFWD_PER_CU", "4"))
+    return max(1, min((tiles + HFWD_WAVES - 1) // HFWD_WAVES, num_cu(device) * per_cu))
 
 
 def cbf_hfwd(S, idx, idx1, src, nev, wpack, f_fwd, wrm, wvec, h_out, mask_out, num_blocks=None,
