@@ -549,7 +549,19 @@ constexpr int NB_TW = X3 ? 1 : NB_WAVES;
 constexpr int NB_NT = NB_WAVES / NB_TW;
 constexpr int NB_RT = NB_TW * 32;                     // region rows
 constexpr int NB_KST = NB_RT / 16;                    // agent steps per turn
-constexpr int NB_PL = (72 + 168) * NB_RT;             // elements per region plane
+// stage image row strides (h16 elements) for 32 / 64 / 128-wide images and the 160-wide
+// pooled|state image of S1
+#ifndef NBS64
+#define NBS64 72
+#endif
+#ifndef NBS128
+#define NBS128 136
+#endif
+#ifndef NBSP
+#define NBSP 168
+#endif
+constexpr int NBS_32 = 40, NBS_64 = NBS64, NBS_128 = NBS128, NBS_P = NBSP;
+constexpr int NB_PL = ((NBS_P > NBS_128 ? NBS_P : NBS_128) + NBS_64) * NB_RT;   // elements per region plane
 constexpr size_t NB_STAGE = (size_t)(X3 ? 2 : 1) * NB_PL * 2;
 
 size_t ctrl_node_bwd_lds() { return (size_t)(X3 ? 2 : 1) * NODE_RM_ELEMS * 2 + CTRL_VEC * 4 + NB_STAGE; }
@@ -614,7 +626,11 @@ DEV void node_bwd_body(const CtrlNodeBwdArgs& a, unsigned char* smem, long c0, l
     const bool ok = ga < total;
     // stage turns holding at least one valid agent (a partial last chunk -- all but the first
     // for small scenes -- skips the turns of its empty waves: zero rows contribute nothing)
+#ifdef CTRL_X_NBNOSTAGE
+    const int nturn = 0;       // ablation (timing only): no weight-gradient stages
+#else
     const int nturn = min(NB_NT, (int)((total - chunk * NB_CH + NB_RT - 1) / NB_RT));
+#endif
     int b = 0, i = 0;
     float sp[D], sv[D], gg[D], av[D], gnp[D], gnv[D];
 #pragma unroll
@@ -745,15 +761,15 @@ DEV void node_bwd_body(const CtrlNodeBwdArgs& a, unsigned char* smem, long c0, l
 #pragma unroll 1
     for (int turn = 0; turn < nturn; ++turn) {   // S4: dWn4pad (32x64) += dY4 . Y3^T ; nb4
       h16* imA = stg;
-      h16* imB = stg + NB_RT * 40;
+      h16* imB = stg + NB_RT * NBS_32;
       if (NB_NT == 1 || myturn == turn) {
-        store_pk(imA, 40, trow, 0, d4b, h, NB_PL);
+        store_pk(imA, NBS_32, trow, 0, d4b, h, NB_PL);
 #pragma unroll
-        for (int mt = 0; mt < 2; ++mt) store_pk(imB, 72, trow, 32 * mt, Y3b[mt], h, NB_PL);
+        for (int mt = 0; mt < 2; ++mt) store_pk(imB, NBS_64, trow, 32 * mt, Y3b[mt], h, NB_PL);
       }
       __syncthreads();
       if (wave < 2)
-        bs4 += stage_mma_fr<NB_KST>(imA, 40, NB_PL, imB, 72, NB_PL, 0, wave, lane, acc4, 0, wave == 0 ? NB_KST : 0);
+        bs4 += stage_mma_fr<NB_KST>(imA, NBS_32, NB_PL, imB, NBS_64, NB_PL, 0, wave, lane, acc4, 0, wave == 0 ? NB_KST : 0);
       __syncthreads();
     }
     // ---- dY2 = W3^T dY3 . relu'(Y2)
@@ -771,18 +787,18 @@ DEV void node_bwd_body(const CtrlNodeBwdArgs& a, unsigned char* smem, long c0, l
 #pragma unroll 1
     for (int turn = 0; turn < nturn; ++turn) {   // S3: dWn3 (64x128) += dY3 . Y2^T ; nb3
       h16* imA = stg;
-      h16* imB = stg + NB_RT * 72;
+      h16* imB = stg + NB_RT * NBS_64;
       if (NB_NT == 1 || myturn == turn) {
 #pragma unroll
-        for (int mt = 0; mt < 2; ++mt) store_pk(imA, 72, trow, 32 * mt, d3b[mt], h, NB_PL);
+        for (int mt = 0; mt < 2; ++mt) store_pk(imA, NBS_64, trow, 32 * mt, d3b[mt], h, NB_PL);
 #pragma unroll
-        for (int mt = 0; mt < 4; ++mt) store_pk(imB, 136, trow, 32 * mt, Y2b[mt], h, NB_PL);
+        for (int mt = 0; mt < 4; ++mt) store_pk(imB, NBS_128, trow, 32 * mt, Y2b[mt], h, NB_PL);
       }
       __syncthreads();
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         const int t = wave + 4 * u;
-        bs3[u] += stage_mma_fr<NB_KST>(imA, 72, NB_PL, imB, 136, NB_PL, t / 4, t % 4, lane, acc3[u], 0,
+        bs3[u] += stage_mma_fr<NB_KST>(imA, NBS_64, NB_PL, imB, NBS_128, NB_PL, t / 4, t % 4, lane, acc3[u], 0,
                                        t % 4 == 0 ? NB_KST : 0);
       }
       __syncthreads();
@@ -802,18 +818,18 @@ DEV void node_bwd_body(const CtrlNodeBwdArgs& a, unsigned char* smem, long c0, l
 #pragma unroll 1
     for (int turn = 0; turn < nturn; ++turn) {   // S2: dWn2 (128x64) += dY2 . Y1^T ; nb2
       h16* imA = stg;
-      h16* imB = stg + NB_RT * 136;
+      h16* imB = stg + NB_RT * NBS_128;
       if (NB_NT == 1 || myturn == turn) {
 #pragma unroll
-        for (int mt = 0; mt < 4; ++mt) store_pk(imA, 136, trow, 32 * mt, d2b[mt], h, NB_PL);
+        for (int mt = 0; mt < 4; ++mt) store_pk(imA, NBS_128, trow, 32 * mt, d2b[mt], h, NB_PL);
 #pragma unroll
-        for (int mt = 0; mt < 2; ++mt) store_pk(imB, 72, trow, 32 * mt, Y1b[mt], h, NB_PL);
+        for (int mt = 0; mt < 2; ++mt) store_pk(imB, NBS_64, trow, 32 * mt, Y1b[mt], h, NB_PL);
       }
       __syncthreads();
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         const int t = wave + 4 * u;
-        bs2[u] += stage_mma_fr<NB_KST>(imA, 136, NB_PL, imB, 72, NB_PL, t / 2, t % 2, lane, acc2[u], 0,
+        bs2[u] += stage_mma_fr<NB_KST>(imA, NBS_128, NB_PL, imB, NBS_64, NB_PL, t / 2, t % 2, lane, acc2[u], 0,
                                        t % 2 == 0 ? NB_KST : 0);
       }
       __syncthreads();
@@ -854,32 +870,32 @@ DEV void node_bwd_body(const CtrlNodeBwdArgs& a, unsigned char* smem, long c0, l
 #pragma unroll 1
     for (int turn = 0; turn < nturn; ++turn) {   // S1: dWn1f (64x160) += dY1 . P^T (P re-read: L2-hot)
       h16* imA = stg;
-      h16* imB = stg + NB_RT * 72;
+      h16* imB = stg + NB_RT * NBS_64;
       if (NB_NT == 1 || myturn == turn) {
 #pragma unroll
-        for (int mt = 0; mt < 2; ++mt) store_pk(imA, 72, trow, 32 * mt, d1b[mt], h, NB_PL);
+        for (int mt = 0; mt < 2; ++mt) store_pk(imA, NBS_64, trow, 32 * mt, d1b[mt], h, NB_PL);
         const h16* prow = a.pooled + (long)b * a.p_env + (long)i * PROW;
 #pragma unroll
         for (int kk = 0; kk < 8; ++kk) {
           const h16x8 pv = ok ? *reinterpret_cast<const h16x8*>(prow + 16 * kk + 8 * h) : zz;
-          *reinterpret_cast<h16x8*>(imB + trow * NS1 + 16 * kk + 8 * h) = pv;
+          *reinterpret_cast<h16x8*>(imB + trow * NBS_P + 16 * kk + 8 * h) = pv;
           if constexpr (X3) {
             const h16x8 pl = ok ? *reinterpret_cast<const h16x8*>(prow + 128 + 16 * kk + 8 * h) : zz;
-            *reinterpret_cast<h16x8*>(imB + NB_PL + trow * NS1 + 16 * kk + 8 * h) = pl;
+            *reinterpret_cast<h16x8*>(imB + NB_PL + trow * NBS_P + 16 * kk + 8 * h) = pl;
           }
         }
-        *reinterpret_cast<h16x8*>(imB + trow * NS1 + 128 + 8 * h) = sfr;
-        *reinterpret_cast<h16x8*>(imB + trow * NS1 + 144 + 8 * h) = zz;
+        *reinterpret_cast<h16x8*>(imB + trow * NBS_P + 128 + 8 * h) = sfr;
+        *reinterpret_cast<h16x8*>(imB + trow * NBS_P + 144 + 8 * h) = zz;
         if constexpr (X3) {      // the state fragment is exact: zero lo plane
-          *reinterpret_cast<h16x8*>(imB + NB_PL + trow * NS1 + 128 + 8 * h) = zz;
-          *reinterpret_cast<h16x8*>(imB + NB_PL + trow * NS1 + 144 + 8 * h) = zz;
+          *reinterpret_cast<h16x8*>(imB + NB_PL + trow * NBS_P + 128 + 8 * h) = zz;
+          *reinterpret_cast<h16x8*>(imB + NB_PL + trow * NBS_P + 144 + 8 * h) = zz;
         }
       }
       __syncthreads();
 #pragma unroll
       for (int u = 0; u < 3; ++u) {
         const int t = wave + 4 * u;
-        if (u < n1) stage_mma_fr<NB_KST>(imA, 72, NB_PL, imB, NS1, NB_PL, t / 5, t % 5, lane, acc1[u]);
+        if (u < n1) stage_mma_fr<NB_KST>(imA, NBS_64, NB_PL, imB, NBS_P, NB_PL, t / 5, t % 5, lane, acc1[u]);
       }
       __syncthreads();
     }
