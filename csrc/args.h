@@ -206,6 +206,8 @@ struct CtrlNodeBwdArgs {
   float4* ego;                         // (B,N) records: dL/ds_t from the node path + gain law + action loss
   float* partial;                      // (gridDim.x, CTRL_NODE_PARTIAL) slabs, accumulated
   int init;                            // 1: the slabs are written, not accumulated (first BPTT step)
+  int chunk;                           // agents per workgroup chunk: 32, 64 or 128 (0 = 128); small
+                                       // scenes use smaller chunks to spread over more CUs
 };
 
 struct CtrlEdgeBwdArgs {

@@ -226,9 +226,10 @@ static int adam(u64 param, u64 grad, u64 m, u64 v, int lo, int hi, float b1, flo
 static int ctrl_node_bwd(u64 pooled, long p_env, u64 S, long s_env, u64 G, u64 A, long a_env, u64 Gn, long gn_env,
                          u64 valid, long v_env, int B, int N, u64 wrm, int o1, int o2, int o3, int o4, u64 wvec,
                          float act_coef, u64 act_scale, float dt, float sqrt3, u64 dP, long dp_env, u64 ego, u64 partial,
-                         int dim, int num_blocks, int prec, int init, u64 stream) {
+                         int dim, int num_blocks, int prec, int init, int chunk, u64 stream) {
   mb::CtrlNodeBwdArgs a{};
   a.init = init;
+  a.chunk = chunk;
   a.dim = dim;
   a.pooled = P<const h16>(pooled); a.p_env = p_env; a.S = P<const float4>(S); a.s_env = s_env;
   a.G = P<const float>(G); a.A = P<const float>(A); a.a_env = a_env; a.Gn = P<const float4>(Gn); a.gn_env = gn_env;

@@ -607,7 +607,8 @@ DEV void node_bwd_body(const CtrlNodeBwdArgs& a, unsigned char* smem, long c0, l
   const int wave = threadIdx.x / WAVE, lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
   const int N = a.N;
   const int total = a.B * N;
-  const long nchunks = (total + NB_CH - 1) / NB_CH;
+  const int CA = (a.chunk == 32 || a.chunk == 64) ? a.chunk : NB_CH;   // agents per chunk
+  const long nchunks = (total + CA - 1) / CA;
   const int erow = wave * 32 + r;
   const int trow = NB_NT == 1 ? erow : (wave % NB_TW) * 32 + r;   // this wave's rows inside a turn's region
   const int myturn = wave / NB_TW;
@@ -622,14 +623,14 @@ DEV void node_bwd_body(const CtrlNodeBwdArgs& a, unsigned char* smem, long c0, l
   const h16x8 zz = zero_h8();
 
   for (long chunk = c0; chunk < nchunks; chunk += cstride) {
-    const int ga = (int)(chunk * NB_CH) + erow;
-    const bool ok = ga < total;
+    const int ga = (int)(chunk * CA) + erow;
+    const bool ok = erow < CA && ga < total;
     // stage turns holding at least one valid agent (a partial last chunk -- all but the first
     // for small scenes -- skips the turns of its empty waves: zero rows contribute nothing)
 #ifdef CTRL_X_NBNOSTAGE
     const int nturn = 0;       // ablation (timing only): no weight-gradient stages
 #else
-    const int nturn = min(NB_NT, (int)((total - chunk * NB_CH + NB_RT - 1) / NB_RT));
+    const int nturn = min(NB_NT, (int)((min((long)CA, total - chunk * CA) + NB_RT - 1) / NB_RT));
 #endif
     int b = 0, i = 0;
     float sp[D], sv[D], gg[D], av[D], gnp[D], gnv[D];

@@ -299,6 +299,7 @@ class BpttDriver {
     wpack_ = U("ctrl_w"); f_ew1f_ = (int)I("f_ew1f"); f_ew2tn_ = (int)I("f_ew2tn");
     dt_ = F("dt"); sqrt3_ = F("sqrt3");
     small_ = (int)I("small");
+    node_chunk_ = (int)I("node_chunk");
     if (B_ < 1 || N_ < 1 || Nn_ < N_ || K_ < 1 || K_ > 16 || (D_ != 2 && D_ != 3) || Tmax_ < 1 || nb_node_ < 1 ||
         nb_edge_ < 1)
       throw std::invalid_argument("BpttDriver: bad dimensions");
@@ -349,6 +350,7 @@ class BpttDriver {
         a.dt = dt_; a.sqrt3 = sqrt3_;
         a.dP = P<h16>(dP_); a.dp_env = (long)N_ * prow_; a.ego = P<float4>(ego_); a.partial = P<float>(part_node_);
         a.init = t == T - 1;     // the first step of the reverse loop writes the slabs
+        a.chunk = node_chunk_;
         chk((prec_ == 2 ? mb_ctrl_node_bwd_x3 : prec_ == 1 ? mb_ctrl_node_bwd_f16 : mb_ctrl_node_bwd)(&a, nb_node_, st), "ctrl_node_bwd");
       }
       {
@@ -380,7 +382,7 @@ class BpttDriver {
   }
 
  private:
-  int B_, N_, Nn_, K_, D_, R_, Tmax_, prec_, prow_, nb_node_, nb_edge_, qsplit_, small_ = 0;
+  int B_, N_, Nn_, K_, D_, R_, Tmax_, prec_, prow_, nb_node_, nb_edge_, qsplit_, small_ = 0, node_chunk_ = 0;
   u64 pooled_, S_, G_, A_, dS_, Gb_, valid_, idx_, argmax_, rptr_, redges_, wrm_, wvec_, act_scale_, dP_, ego_, dEc_;
   u64 part_node_, part_edge_, wpack_;
   int o1_, o2_, o3_, o4_, f_ew1f_, f_ew2tn_;

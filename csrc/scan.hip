@@ -12,6 +12,7 @@
 // fp contraction is OFF in this file so distances / TTC decisions are bit-identical to the
 // PyTorch oracle (separately rounded products, same association order).
 #pragma clang fp contract(off)
+#include <cstdlib>
 #include "common.h"
 #include "args.h"
 #include "state.h"
@@ -498,9 +499,24 @@ static void launch_kdb(const ScanArgs& a, hipStream_t st) {
 #define SCAN_BS_BIG 1024  // block size above 512 nodes per env (4 lanes/agent: 512 -> 1024, 61.5 -> 60.5 us)
 #endif
 
+// Small scans (a strong-scaling slice: few envs) would fill only some CUs with big blocks: use
+// 256-thread blocks whenever the big-block grid has fewer blocks than CUs (MACBF_SCAN_SMALL=0/1
+// forces the choice for A/B runs).
+static bool scan_small_grid(const ScanArgs& a) {
+  static const int force = [] { const char* e = getenv("MACBF_SCAN_SMALL"); return e ? atoi(e) : -1; }();
+  if (force >= 0) return force != 0;
+  static const int cus = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) v = 256;
+    return v;
+  }();
+  constexpr int AG = SCAN_BS_BIG / SCAN_LPA;      // agents per big block
+  return (long)a.B * ((a.Nn + AG - 1) / AG) < cus;
+}
+
 template <int K, int D>
 static void launch_kd(const ScanArgs& a, hipStream_t st) {
-  if (a.Nn > 512) launch_kdb<K, D, SCAN_BS_BIG>(a, st);
+  if (a.Nn > 512 && !scan_small_grid(a)) launch_kdb<K, D, SCAN_BS_BIG>(a, st);
   else launch_kdb<K, D, 256>(a, st);
 }
 

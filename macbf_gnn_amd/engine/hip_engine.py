@@ -616,7 +616,8 @@ class HipEngine:
                 ctrl_rm=native.ptr(pw.ctrl_rm), o_w1=int(pw.node_rm_off["w1"]), o_w2=int(pw.node_rm_off["w2"]),
                 o_w3=int(pw.node_rm_off["w3"]), o_w4=int(pw.node_rm_off["w4"]), ctrl_v=native.ptr(pw.ctrl_v),
                 ctrl_w=native.ptr(pw.ctrl_w), f_ew1f=int(pw.ctrl_off["ew1f"]), f_ew2tn=int(pw.ctrl_off["ew2tn"]),
-                dt=float(C.TIME_STEP), sqrt3=float(C.SQRT3), small=int(self.small_bptt)))
+                dt=float(C.TIME_STEP), sqrt3=float(C.SQRT3), small=int(self.small_bptt),
+                node_chunk=int(native.node_bwd_chunk(B * N, self.dev))))
             self._bdrv = native.lib().BpttDriver(c)
         return self._bdrv
 

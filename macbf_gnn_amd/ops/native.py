@@ -369,13 +369,14 @@ def ctrl_fwd(S, G, idx, wpack, f_edge, f_node, wvec, A, Sn, dist_sum, act_sum, n
 
 def ctrl_fwd_apw(total_agents: int, device, n_agents: int | None = None) -> int:
     """Agents per wave of the controller step's edge phase: 32, halved (down to 4) while the
-    scene has fewer groups than two per CU, so small scenes spread the edge phase over more
-    waves. Any grouping gives the same results (the per-env sums are per-agent fixed-point
-    integers). MACBF_CTRL_APW overrides (A/B measurements)."""
+    scene has fewer groups than four per CU, so small scenes spread the edge phase over more
+    waves (8-env strong-scaling slice, fp32: 16 / 8 / 4 agents per wave -> 4.36 / 3.82 / 3.95 ms
+    per iteration with the other small-grid choices). Any grouping gives the same results (the
+    per-env sums are per-agent fixed-point integers). MACBF_CTRL_APW overrides (A/B runs)."""
     env = os.environ.get("MACBF_CTRL_APW")
     if env:
         return int(env)
-    apw, cap = 32, 2 * num_cu(device)
+    apw, cap = 32, 4 * num_cu(device)
     for cand in (16, 8, 4):
         if (total_agents + apw - 1) // apw >= cap:
             break
@@ -724,18 +725,33 @@ def ctrl_edge_qsplit(total_agents: int, device) -> int:
     return p
 
 
+def node_bwd_chunk(total_agents: int, device) -> int:
+    """Agents per node-backward workgroup chunk: 128 while the chunks fill the CUs, else 64 / 32
+    (small scenes and strong-scaling slices: more, shorter workgroups; a chunk's empty stage
+    turns are skipped). MACBF_NODE_CHUNK overrides."""
+    env = os.environ.get("MACBF_NODE_CHUNK")
+    if env:
+        return int(env)
+    cu = num_cu(device)
+    for ca in (128, 64):
+        if (total_agents + ca - 1) // ca >= cu:
+            return ca
+    return 32
+
+
 def ctrl_bwd_grids(total_agents: int, device):
-    """(node, edge) backward grids: the node kernel takes 128-agent chunks, one workgroup per CU;
-    the edge kernel 32*CTRL_EDGE_WAVES-agent chunks x ctrl_edge_qsplit tile ranges (4 waves: two
-    workgroups per CU)."""
-    ch = (total_agents + 127) // 128
+    """(node, edge) backward grids: the node kernel takes node_bwd_chunk-agent chunks, one
+    workgroup per CU; the edge kernel 32*CTRL_EDGE_WAVES-agent chunks x ctrl_edge_qsplit tile
+    ranges (4 waves: two workgroups per CU)."""
+    ca = node_bwd_chunk(total_agents, device)
+    ch = (total_agents + ca - 1) // ca
     che = (total_agents + 32 * CTRL_EDGE_WAVES - 1) // (32 * CTRL_EDGE_WAVES)
     cu = num_cu(device)
     return max(1, min(ch, cu)), max(1, min(che * ctrl_edge_qsplit(total_agents, device), (8 // CTRL_EDGE_WAVES) * cu))
 
 
 def ctrl_node_bwd(pooled, S, G, A, Gn, valid_t, wrm, offs, wvec, act_coef, dP, ego, partial, num_blocks,
-                  act_cnt=None, prec=None, init=False):
+                  act_cnt=None, prec=None, init=False, chunk=None):
     """act_cnt: optional 1-element device tensor holding the (all-reduced) action-loss count
     n_act; the action-loss coefficient is then act_coef / max(n_act, 1), read by the kernel (no
     host round trip, no extra launch). init: write the weight-gradient slabs instead of
@@ -764,7 +780,8 @@ def ctrl_node_bwd(pooled, S, G, A, Gn, valid_t, wrm, offs, wvec, act_coef, dP, e
                              ptr(valid_t), valid_t.stride(0) if valid_t is not None else 0, B, N,
                              ptr(wrm), offs["w1"], offs["w2"], offs["w3"], offs["w4"], ptr(wvec),
                              float(act_coef), ptr(act_cnt), float(C.TIME_STEP), float(C.SQRT3), ptr(dP), dP.stride(0),
-                             ptr(ego), ptr(partial), D, int(num_blocks), f16, int(bool(init)), stream_handle())
+                             ptr(ego), ptr(partial), D, int(num_blocks), f16, int(bool(init)),
+                             int(chunk or node_bwd_chunk(B * N, S.device)), stream_handle())
     _ok(rc, "ctrl_node_bwd")
 
 
