@@ -9,9 +9,8 @@
 // goals are start + U(-0.5,0.5)^2 with the same separation rule among goals.
 // Invariants (min pair distance > r, goal offsets in +-0.5, v = 0, density 8/unit^2) are
 // tested against the host sampler. LDS: 25 B per agent (N <= ~6000); larger envs keep the same
-// arrays in a per-env global workspace (a.ws; one workgroup's waves share one CU and its L1, and
-// __syncthreads orders their global accesses) with a full-resolution cell grid: identical
-// results (acceptance is order independent).
+// arrays in a per-env global workspace (a.ws) with a full-resolution cell grid: identical results
+// (acceptance is order independent); its round barriers carry agent-scope fences (round_sync).
 #include "common.h"
 #include "args.h"
 #include "state.h"
@@ -73,6 +72,17 @@ DEV bool grid_all(const CellGrid& g, const int* head, const int* next, const flo
 // Each round rebuilds an LDS cell list of every agent's current point (placed position or
 // this round's candidate; lists built with LDS atomics, whose order does not matter because
 // acceptance needs *all* tests to pass), so a round is O(N) instead of O(N^2).
+// Barrier of the round loop. With the arrays in a global workspace the cell heads are written
+// by atomics (performed in L2) and read by plain loads, and every array is rewritten each round:
+// a plain load may hit an L1 line left from an earlier round, and a stale head links into the
+// previous round's list -- a cycle the cell walk never leaves. Agent-scope fences around the
+// barrier publish this round's stores / atomics to L2 and drop the workgroup's L1 lines.
+DEV void round_sync(bool global_ws) {
+  if (global_ws) __threadfence();
+  __syncthreads();
+  if (global_ws) __threadfence();
+}
+
 template <int D>
 __global__ __launch_bounds__(SC_BLOCK) void scenario_kernel(ScenArgs a, CellGrid grid) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -88,11 +98,12 @@ __global__ __launch_bounds__(SC_BLOCK) void scenario_kernel(ScenArgs a, CellGrid
   const int b = blockIdx.x;
   const float r2 = a.r * a.r;
   const int ncell = sc_cells(grid.G, D);
+  const bool gws = a.ws != nullptr;
   for (int q = threadIdx.x; q < a.M * D; q += SC_BLOCK) obs[q] = a.obs[(long)b * a.M * D + q];
   int status = 0;
   for (int phase = 0; phase < 2; ++phase) {
     for (int i = threadIdx.x; i < a.N; i += SC_BLOCK) placed[i] = 0;
-    __syncthreads();
+    round_sync(gws);
     int round = 0;
     for (; round < a.max_rounds; ++round) {
       for (int c = threadIdx.x; c < ncell; c += SC_BLOCK) head[c] = -1;
@@ -108,12 +119,12 @@ __global__ __launch_bounds__(SC_BLOCK) void scenario_kernel(ScenArgs a, CellGrid
           cand[i * D + k] = (phase == 0) ? u * a.L : starts[i * D + k] + (u - 0.5f) * 2.f * a.spread;
         }
       }
-      __syncthreads();
+      round_sync(gws);
       for (int i = threadIdx.x; i < a.N; i += SC_BLOCK) {
         const int c = cell_of<D>(grid, (placed[i] ? pos : cand) + i * D);
         next[i] = atomicExch(&head[c], i);
       }
-      __syncthreads();
+      round_sync(gws);
       for (int i = threadIdx.x; i < a.N; i += SC_BLOCK) {
         if (placed[i]) continue;
         const float* c = cand + i * D;
@@ -129,9 +140,9 @@ __global__ __launch_bounds__(SC_BLOCK) void scenario_kernel(ScenArgs a, CellGrid
           });
         if (ok) placed[i] = 2;
       }
-      __syncthreads();
+      round_sync(gws);
       if (threadIdx.x == 0) n_unplaced = 0;
-      __syncthreads();
+      round_sync(gws);
       int local = 0;
       for (int i = threadIdx.x; i < a.N; i += SC_BLOCK) {
         if (placed[i] == 2) {
@@ -141,7 +152,7 @@ __global__ __launch_bounds__(SC_BLOCK) void scenario_kernel(ScenArgs a, CellGrid
         } else if (placed[i] == 0) ++local;
       }
       if (local) atomicAdd(&n_unplaced, local);
-      __syncthreads();
+      round_sync(gws);
       if (n_unplaced == 0) break;
     }
     if (round >= a.max_rounds) {
@@ -149,7 +160,7 @@ __global__ __launch_bounds__(SC_BLOCK) void scenario_kernel(ScenArgs a, CellGrid
       for (int i = threadIdx.x; i < a.N; i += SC_BLOCK)
         if (placed[i] == 0)
           for (int k = 0; k < D; ++k) pos[i * D + k] = cand[i * D + k];
-      __syncthreads();
+      round_sync(gws);
     }
     else if (phase == 1 && status == 0) status = round + 1;
     for (int i = threadIdx.x; i < a.N; i += SC_BLOCK) {
@@ -164,7 +175,7 @@ __global__ __launch_bounds__(SC_BLOCK) void scenario_kernel(ScenArgs a, CellGrid
         for (int k = 0; k < D; ++k) a.G[((long)b * a.N + i) * D + k] = p[k];
       }
     }
-    __syncthreads();
+    round_sync(gws);
   }
   if (threadIdx.x == 0 && a.status) a.status[b] = status;
 }

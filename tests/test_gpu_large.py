@@ -117,3 +117,16 @@ def test_training_runs_16384_agents():
     torch.cuda.synchronize()
     assert torch.isfinite(tr.fp.flat).all() and not torch.equal(before, tr.fp.flat)
     assert float(st["agent_steps"]) > 0
+
+
+def test_sampler_global_workspace_many_rounds():
+    """Repeated large-env sampling (the global-workspace path re-links its cell lists every
+    round): every call terminates and equals the host runtime. Regression test for stale L1
+    lines of the cell heads, which could link a round's list into the previous one's (a cycle
+    the cell walk never left)."""
+    for it in range(12):
+        kw = dict(seed=100 + it, iteration=it, rank=0)
+        s, g, _ = scenario.generate(2, 8192, device=DEV, **kw)
+        torch.cuda.synchronize()
+        s2, g2, _ = scenario.generate(2, 8192, device="cpu", **kw)
+        assert torch.equal(s.cpu(), s2) and torch.equal(g.cpu(), g2)
