@@ -289,8 +289,11 @@ _WS = {}
 
 
 def _workspace(name, nbytes, device):
-    """Cached uint8 device scratch (grown on demand; stream-ordered reuse)."""
-    key = (name, str(device))
+    """Cached uint8 device scratch, one per (name, device, current stream): grown on demand,
+    reused in stream order. Per stream, because launches on different streams may run
+    concurrently (the trainer samples the next iteration's scenarios on a side stream while
+    the current one is still being sampled / simulated) and must not share scratch."""
+    key = (name, str(device), stream_handle(device))
     t = _WS.get(key)
     if t is None or t.numel() < nbytes:
         t = torch.empty(max(int(nbytes), 1), dtype=torch.uint8, device=device)

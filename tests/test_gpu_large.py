@@ -130,3 +130,20 @@ def test_sampler_global_workspace_many_rounds():
         torch.cuda.synchronize()
         s2, g2, _ = scenario.generate(2, 8192, device="cpu", **kw)
         assert torch.equal(s.cpu(), s2) and torch.equal(g.cpu(), g2)
+
+
+def test_sampler_concurrent_streams():
+    """The trainer samples iteration k+1 on a side stream while iteration k's sampling may still
+    run on the main stream: the large-env samplers must not share scratch (regression test: a
+    shared global workspace corrupted both cell lists and could hang the walk)."""
+    side = torch.cuda.Stream(device=DEV)
+    for it in range(4):
+        ka = dict(seed=7, iteration=2 * it, rank=0)
+        kb = dict(seed=7, iteration=2 * it + 1, rank=0)
+        sa, ga, _ = scenario.generate(2, 8192, device=DEV, **ka)
+        with torch.cuda.stream(side):
+            sb, gb, _ = scenario.generate(2, 8192, device=DEV, **kb)
+        torch.cuda.synchronize()
+        for (s, g), kw in (((sa, ga), ka), ((sb, gb), kb)):
+            s2, g2, _ = scenario.generate(2, 8192, device="cpu", **kw)
+            assert torch.equal(s.cpu(), s2) and torch.equal(g.cpu(), g2)
