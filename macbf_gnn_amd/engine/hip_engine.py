@@ -35,10 +35,11 @@ ACT_COEF = C.LOSS_SCALE * C.LOSS_WEIGHTS[4]
 class HipEngine:
     name = "hip"
     resort_every = 4          # scan: Hilbert re-sort period (rollout steps)
-    overlap_hfwd = None       # CBF h of the main slots on a side stream during the rollout (None: by
-                              # precision -- on for bf16/fp16 (A/B 7.83 -> 7.63 ms); off for fp32, whose
-                              # fused one-launch controller step holds 145 KB of LDS per workgroup,
-                              # so the slices only delay it (A/B: 15.04 with vs 14.60 ms without)
+    overlap_hfwd = False      # CBF h of the main slots on a side stream during the rollout. Off: the
+                              # one-launch controller steps hold a CU's LDS (145 KB) and the 1024-thread
+                              # scan blocks leave no room either, so the slices only delay the rollout's
+                              # critical chain (A/B fp32 15.04 vs 14.60 ms, bf16 8.06 vs 7.92 ms; round 1,
+                              # with smaller scan blocks, measured the overlap 7.83 -> 7.63 ms for bf16)
     native_rollout = True     # per-step launch loop in C++ (csrc/runtime.cpp)
     bptt_groups = 1           # independent env groups whose BPTT chains run on separate streams
     native_bptt = True        # reverse-time BPTT launch loop in C++ (csrc/runtime.cpp)
@@ -98,8 +99,6 @@ class HipEngine:
             raise ValueError(f"dtype must be bf16, fp16 or fp32 on the HIP path, got {cfg.dtype!r}")
         self.pw = PackedWeights(trainer.fp, self.D, mdt)
         self.prec = self.pw.prec
-        if self.overlap_hfwd is None:
-            self.overlap_hfwd = self.prec != "fp32"
         self.hdt = self.pw.dtype                 # packed / pooled element type (bf16 | fp16)
         self.prow = L.pooled_row(self.prec)      # pooled / dL/dpooled row: [hi | lo] for fp32
         offs = {pn: o for (m, pn, shape, o, n) in trainer.fp.specs}
