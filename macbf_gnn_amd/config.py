@@ -76,7 +76,8 @@ class TrainConfig:
     display_steps: int = DISPLAY_STEPS
     save_steps: int = SAVE_STEPS
     seed: int = 0
-    dtype: str = "bf16"               # HIP kernel precision: bf16 | fp16 | fp32 (fp32-accurate split kernels); CPU: fp32 oracle
+    dtype: str = "fp32"               # HIP kernel precision: fp32 (fp32-accurate split kernels, the reference's
+                                      # precision) | bf16 | fp16 (faster, reduced precision); CPU: fp32 oracle
     loss_scale_init: float = 4096.0   # fp16: initial dynamic loss scale of the upstream gradients
     loss_scale_growth: int = 1000     # fp16: double the scale after this many finite steps
     bptt: bool = True                 # keep the rollout graph (reference behaviour, train.py:58-81)

@@ -26,8 +26,9 @@ def parse_args(argv=None):
     p.add_argument("--lr", type=float, default=None)
     p.add_argument("--seed", type=int, default=0)
     p.add_argument("--device", type=str, default="auto", choices=["auto", "cpu", "hip"])
-    p.add_argument("--dtype", type=str, default="bf16", choices=["bf16", "fp16", "fp32"],
-                   help="HIP MFMA input type (fp16: dynamic loss scaling); the CPU path is fp32")
+    p.add_argument("--dtype", type=str, default="fp32", choices=["fp32", "bf16", "fp16"],
+                   help="HIP kernel precision: fp32 (default; fp32-accurate split-bf16 MFMA, the reference's "
+                        "precision), bf16 or fp16 (faster; fp16 with dynamic loss scaling); the CPU path is fp32")
     p.add_argument("--no_bptt", action="store_true", help="detach states between rollout steps")
     p.add_argument("--no_reuse_nbr_idx", action="store_true", help="recompute kNN for h(s')")
     p.add_argument("--alternate_every", type=int, default=0)
