@@ -475,7 +475,10 @@ __global__ __launch_bounds__(NW * 64) void cbf_hfwd_kernel(CbfFwdArgs a) {
   }
 }
 
-constexpr int HFWD_WAVES = 8;
+#ifndef CBF_HFWD_WAVES
+#define CBF_HFWD_WAVES 8
+#endif
+constexpr int HFWD_WAVES = CBF_HFWD_WAVES;
 constexpr size_t HFWD_LDS = (size_t)RMP * 2 + 2 * FRAG_SZ + CBF_VEC * 4;
 
 template <bool FUSED, int NW, int D>

@@ -560,8 +560,14 @@ constexpr int NB_KST = NB_RT / 16;                    // agent steps per turn
 #ifndef NBSP
 #define NBSP 168
 #endif
+// NB_MERGE43: stages S4 and S3 share one set of turns (their four images fit one region)
+#ifndef NB_MERGE43
+#define NB_MERGE43 1
+#endif
 constexpr int NBS_32 = 40, NBS_64 = NBS64, NBS_128 = NBS128, NBS_P = NBSP;
-constexpr int NB_PL = ((NBS_P > NBS_128 ? NBS_P : NBS_128) + NBS_64) * NB_RT;   // elements per region plane
+constexpr int nb_max(int a, int b) { return a > b ? a : b; }
+constexpr int NB_PL = nb_max(nb_max(NBS_P + NBS_64, NBS_128 + NBS_64),
+                             NB_MERGE43 ? NBS_32 + 2 * NBS_64 + NBS_128 : 0) * NB_RT;   // elements per region plane
 constexpr size_t NB_STAGE = (size_t)(X3 ? 2 : 1) * NB_PL * 2;
 
 size_t ctrl_node_bwd_lds() { return (size_t)(X3 ? 2 : 1) * NODE_RM_ELEMS * 2 + CTRL_VEC * 4 + NB_STAGE; }
@@ -759,6 +765,47 @@ DEV void node_bwd_body(const CtrlNodeBwdArgs& a, unsigned char* smem, long c0, l
       d3b[mt] = to_pk(c);
       mask_pk(d3b[mt], Y3b[mt]);
     }
+#if NB_MERGE43
+#pragma unroll 1
+    for (int turn = 0; turn < nturn; ++turn) {   // S4 + S3: dWn4pad += dY4 . Y3^T ; nb4 | dWn3 += dY3 . Y2^T ; nb3
+      h16* im4A = stg;
+      h16* im4B = im4A + NB_RT * NBS_32;
+      h16* im3A = im4B + NB_RT * NBS_64;
+      h16* im3B = im3A + NB_RT * NBS_64;
+      if (NB_NT == 1 || myturn == turn) {
+        store_pk(im4A, NBS_32, trow, 0, d4b, h, NB_PL);
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt) {
+          store_pk(im4B, NBS_64, trow, 32 * mt, Y3b[mt], h, NB_PL);
+          store_pk(im3A, NBS_64, trow, 32 * mt, d3b[mt], h, NB_PL);
+        }
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) store_pk(im3B, NBS_128, trow, 32 * mt, Y2b[mt], h, NB_PL);
+      }
+      __syncthreads();
+      if (wave < 2)
+        bs4 += stage_mma_fr<NB_KST>(im4A, NBS_32, NB_PL, im4B, NBS_64, NB_PL, 0, wave, lane, acc4, 0, wave == 0 ? NB_KST : 0);
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int t = wave + 4 * u;
+        bs3[u] += stage_mma_fr<NB_KST>(im3A, NBS_64, NB_PL, im3B, NBS_128, NB_PL, t / 4, t % 4, lane, acc3[u], 0,
+                                       t % 4 == 0 ? NB_KST : 0);
+      }
+      __syncthreads();
+    }
+    // ---- dY2 = W3^T dY3 . relu'(Y2)
+    Pk d2b[4];
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+      f32x16 c = zero16();
+      static_for<4>([&](auto kk_) {
+        constexpr int kk = decltype(kk_)::value;
+        c = mma(wrmT_acc_fr(W3 + opaque_zero(), NS3, 32 * mt, kk, lane, LO), pk_fr<kk & 1>(d3b[kk >> 1]), c);
+      });
+      d2b[mt] = to_pk(c);
+      mask_pk(d2b[mt], Y2b[mt]);
+    }
+#else
 #pragma unroll 1
     for (int turn = 0; turn < nturn; ++turn) {   // S4: dWn4pad (32x64) += dY4 . Y3^T ; nb4
       h16* imA = stg;
@@ -804,6 +851,7 @@ DEV void node_bwd_body(const CtrlNodeBwdArgs& a, unsigned char* smem, long c0, l
       }
       __syncthreads();
     }
+#endif
     // ---- dY1 = W2^T dY2 . relu'(Y1)
     Pk d1b[2];
 #pragma unroll
