@@ -1621,6 +1621,11 @@ extern "C" int MB_SYM(bptt_small)(const mb::BpttSmallArgs* a, hipStream_t st) {
       !a->cb.ptr || !a->cb.edges)
     return -2;
   const size_t lds = bptt_small_lds();
+  {   // static + dynamic LDS must fit one workgroup: refuse before launching
+    hipFuncAttributes fa{};
+    const void* k = a->nb.dim == 3 ? (const void*)bptt_small_kernel<3> : (const void*)bptt_small_kernel<2>;
+    if (hipFuncGetAttributes(&fa, k) != hipSuccess || fa.sharedSizeBytes + lds > 160u * 1024u) return -4;
+  }
   if (a->nb.dim == 3) {
     (void)hipFuncSetAttribute((const void*)bptt_small_kernel<3>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL(bptt_small_kernel<3>, dim3(B), dim3(NB_WAVES * 64), lds, st, *a);
