@@ -390,6 +390,15 @@ class HipEngine:
         d = (self.host_dist[: t + 1].double() / native.FX_DIST).float() / float(self.N) < C.DIST_MIN_CHECK
         return bool(d.any(0).all())
 
+    def trajectory(self, T: int) -> dict:
+        """The last rollout of T steps in the oracle's layout (``oracle.rollout(forced=...)``):
+        agent states (B, T+1, N, 2D), neighbour graphs (B, T, N, K) and the controller's
+        max-pool argmax slots (B, T, N, 128) -- tests replay it through the oracle."""
+        N = self.N
+        S = native.from_records(self.S[: T + 1, :, :N]).transpose(0, 1).contiguous()
+        return {"S": S, "idx": self.idx[:T].transpose(0, 1).long().contiguous(),
+                "slots": self.argmax[:T].transpose(0, 1).contiguous()}
+
     # ------------------------------------------------------------------ step
     def step(self, s0, g, obs=None):
         if self.graph_mode:

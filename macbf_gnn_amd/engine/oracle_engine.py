@@ -21,7 +21,8 @@ class OracleEngine:
     def after_update(self):
         pass
 
-    def step(self, s0, g, obs=None):
+    def step(self, s0, g, obs=None, forced=None):
+        """``forced``: replay a trajectory (``oracle.rollout``), e.g. ``HipEngine.trajectory()``."""
         tr = self.tr
         cfg = tr.cfg
         cp = tr.controller.params_dict()
@@ -29,7 +30,8 @@ class OracleEngine:
         traj = oracle.rollout(cp, s0, g, top_k=cfg.top_k, inner_loops=cfg.inner_loops,
                               bptt=cfg.bptt, early_stop=cfg.early_stop,
                               noise_prob=cfg.add_noise_prob, noise_scale=cfg.noise_scale,
-                              generator=tr.torch_gen, compute_safety=cfg.compute_safety, obs=obs)
+                              generator=tr.torch_gen, compute_safety=cfg.compute_safety, obs=obs,
+                              forced=forced)
         tr.timer.mark("rollout")
         T = traj["A"].shape[1]
         valid = traj["valid"]

@@ -138,38 +138,142 @@ def safe_agent_count(s: torch.Tensor, nodes: Optional[torch.Tensor] = None) -> t
 
 
 # ----------------------------------------------------------------------------- networks
-def _lin(x, w, b):
+# bf16 kernel emulation (tests only): the bf16 MFMA build rounds at fixed points -- the
+# hidden activations entering MFMA layers (not the CBF's fp32 64 -> 1 head), the pooled
+# features, and every pre-activation
+# gradient dZ (the MFMA input of both dX = W^T dZ and dW = dZ X^T; not the CBF's scalar head)
+# plus dL/dpooled. Layer-1
+# inputs are exact (hi/lo split along k, csrc/common.h mma_bx) and accumulation is fp32.
+# With the weights rounded to bf16 as well, the oracle then evaluates the kernels' function up
+# to accumulation order and rounding-boundary ties.
+_EMULATE = {"bf16": False}
+
+
+class emulate_bf16:
+    """Context manager: oracle networks round like the bf16 kernels (see above)."""
+
+    def __init__(self, on: bool = True):
+        self.on = on
+
+    def __enter__(self):
+        self.prev = _EMULATE["bf16"]
+        _EMULATE["bf16"] = self.on
+        return self
+
+    def __exit__(self, *exc):
+        _EMULATE["bf16"] = self.prev
+
+
+def _round16(x):
+    return x.to(torch.bfloat16).to(x.dtype)
+
+
+class _RoundFwd(torch.autograd.Function):        # activation rounding, straight-through grad
+    @staticmethod
+    def forward(ctx, x):
+        return _round16(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g
+
+
+class _RoundGrad(torch.autograd.Function):       # identity forward, rounded gradient
+    @staticmethod
+    def forward(ctx, x):
+        return x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        return _round16(g)
+
+
+class _HeadBf16(torch.autograd.Function):
+    """The CBF's 64 -> 1 head in the bf16 build: fp32 forward and dX = dh w4, but dW4 from
+    bf16 dh and bf16 relu(H3) (an MFMA stage, csrc/cbf.hip stage C+D) and db4 = sum of fp32 dh."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        ctx.save_for_backward(x, w)
+        return F.linear(x, w, b)
+
+    @staticmethod
+    def backward(ctx, g):
+        x, w = ctx.saved_tensors
+        g2 = g.reshape(-1, g.shape[-1])
+        dw = _round16(g2).t() @ _round16(x.reshape(-1, x.shape[-1]))
+        return g @ w, dw, g2.sum(0)
+
+
+def _qa(x):
+    return _RoundFwd.apply(x) if _EMULATE["bf16"] else x
+
+
+def _qg(x):
+    return _RoundGrad.apply(x) if _EMULATE["bf16"] else x
+
+
+def _lin(x, w, b, first=False, head=False):
     if w.dim() == 3:          # Conv1d(k=1) weight (out, in, 1)
         w = w[..., 0]
-    return F.linear(x, w, b)
+    if head:
+        return _HeadBf16.apply(x, w, b) if _EMULATE["bf16"] else F.linear(x, w, b)
+    return _qg(F.linear(x if first else _qa(x), w, b))
 
 
-def controller_forward(p: Dict[str, torch.Tensor], s, g, idx, return_aux=False, nodes=None):
+def controller_forward(p: Dict[str, torch.Tensor], s, g, idx, return_aux=False, nodes=None, pool_slots=None,
+                       pool_values=None):
     """Gain-scheduled GNN controller (controller.py:31-63), intended semantics.
 
     ``p`` is the controller ``state_dict`` (or named parameters) keyed like the reference.
     D-dimensional: edge input [s_i - s_j, eye] (2D+1), node input [pooled, p - g, v] (128+2D),
     2D gains, a_d = -(k_{2d} (p_d - g_d) + k_{2d+1} v_d) (D = 2: the reference law).
+    ``pool_slots`` (..., N, 128; 255 = no positive row) replaces the max-pool's argmax by given
+    neighbour slots (the kernels' saved argmax): the max-pool subgradient at near-ties is a
+    choice, and tests pin it to the kernels' choice (see ``pool_slot_gap``). ``pool_values``
+    (tests) replaces the pooled values (straight-through: the gradient is unchanged), e.g. by
+    the kernels' stored 16-bit pooled rows, so a rounding-boundary tie of one pooled element
+    cannot flip the node MLP's path.
     """
     D = sdim(s)
     rel, eye = edge_rel(s, idx, nodes)
     x = torch.cat([rel, eye.unsqueeze(-1)], dim=-1)                     # (...,N,K,2D+1)
     dist = torch.sqrt(sq_dist(rel, D))
     mask = (dist < C.OBS_RADIUS).to(s.dtype)                            # strict, no eps
-    h = F.relu(_lin(x, p["controller_centr_net.0.weight"], p["controller_centr_net.0.bias"]))
+    h = F.relu(_lin(x, p["controller_centr_net.0.weight"], p["controller_centr_net.0.bias"], first=True))
     h = F.relu(_lin(h, p["controller_centr_net.2.weight"], p["controller_centr_net.2.bias"]))
-    pooled = (h * mask.unsqueeze(-1)).max(dim=-2).values                # (...,N,128)
-    z = torch.cat([pooled, s[..., :D] - g, s[..., D:2 * D]], dim=-1)
+    hm = h * mask.unsqueeze(-1)
+    if pool_slots is None:
+        pooled = hm.max(dim=-2).values                                   # (...,N,128)
+    else:
+        sl = pool_slots.long()
+        has = (sl < hm.shape[-2]).to(hm.dtype)
+        pooled = hm.gather(-2, sl.clamp(max=hm.shape[-2] - 1).unsqueeze(-2)).squeeze(-2) * has
+    if pool_values is not None:
+        pooled = pool_values.to(pooled.dtype) + (pooled - pooled.detach())
+    z = torch.cat([_qg(_qa(pooled)), s[..., :D] - g, s[..., D:2 * D]], dim=-1)
     for i, act in ((0, True), (2, True), (4, True), (6, False)):
-        z = _lin(z, p[f"controller_dec_net.{i}.weight"], p[f"controller_dec_net.{i}.bias"])
+        z = _lin(z, p[f"controller_dec_net.{i}.weight"], p[f"controller_dec_net.{i}.bias"], first=i == 0)
         if act:
             z = F.relu(z)
     k = 2.0 * torch.sigmoid(z) + 0.2
     a = torch.stack([-(k[..., 2 * q] * (s[..., q] - g[..., q]) + k[..., 2 * q + 1] * s[..., D + q])
                      for q in range(D)], dim=-1)
     if return_aux:
-        return a, {"gains": k, "pooled": pooled, "mask": mask}
+        return a, {"gains": k, "pooled": pooled, "mask": mask, "hm": hm}
     return a
+
+
+def pool_slot_gap(hm: torch.Tensor, pool_slots: torch.Tensor) -> torch.Tensor:
+    """How far given max-pool slots are from the true max: max over (agent, feature) of
+    (max_k hm - hm[slot]) / max(max_k hm, tiny) (0 when the slots are argmaxes; 255 = no slot
+    must mean no positive row)."""
+    top = hm.max(dim=-2).values
+    sl = pool_slots.long()
+    has = sl < hm.shape[-2]
+    val = hm.gather(-2, sl.clamp(max=hm.shape[-2] - 1).unsqueeze(-2)).squeeze(-2)
+    gap = torch.where(has, (top - val) / top.clamp_min(1e-30), (top > 0).to(top.dtype))
+    return gap.max()
 
 
 def cbf_features(s, idx, nodes=None):
@@ -187,7 +291,9 @@ def cbf_forward(p: Dict[str, torch.Tensor], s, idx, nodes=None):
     x, mask = cbf_features(s, idx, nodes)
     z = x
     for i, act in ((0, True), (2, True), (4, True), (6, False)):
-        z = _lin(z, p[f"cbf_net.{i}.weight"], p[f"cbf_net.{i}.bias"])
+        # (the 64 -> 1 head is an fp32 dot product on the fp32 relu(H3), csrc/cbf.hip; db4 sums
+        # the fp32 dh; dH3 = w4 dh is rounded at layer 3's pre-activation)
+        z = _lin(z, p[f"cbf_net.{i}.weight"], p[f"cbf_net.{i}.bias"], first=i == 0, head=i == 6)
         if act:
             z = F.relu(z)
     return z[..., 0] * mask
@@ -256,26 +362,42 @@ def finalize_losses(sums, n_act_sum, n_act):
 # ----------------------------------------------------------------------------- rollout
 def rollout(ctrl_params, s0, g, *, top_k=C.TOP_K, inner_loops=C.INNER_LOOPS, bptt=True,
             early_stop=True, noise_prob=0.0, noise_scale=C.NOISE_SCALE, generator=None,
-            compute_safety=False, obs=None):
+            compute_safety=False, obs=None, forced=None):
     """Batched rollout with per-env done masks (train.py:58-81).
 
     Returns dict with S (B,T+1,N,4), A (B,T,N,2), idx (B,T,N,K), valid (B,T) bool,
     dist (B,T) mean goal distance after each step, safe (B,T) safe-agent counts of s_{t+1}.
+
+    ``forced`` (tests): replay another engine's trajectory -- dict S (B,T+1,N,2D), idx
+    (B,T,N,K), optional slots (B,T,N,128) max-pool argmax. The states take the given values
+    while their gradients follow this rollout's own expressions (straight-through:
+    s_{t+1} = S_{t+1} + (e - e.detach()), e = s_t + dt [v, a]), so the gradient is the oracle's
+    gradient along exactly that trajectory, graph and pooling choice.
     """
     B = s0.shape[0]
     s = s0
     active = torch.ones(B, dtype=torch.bool, device=s0.device)
     S, A, I, V, D, SF = [s0], [], [], [], [], []
     dim = sdim(s0)
-    for _ in range(inner_loops):
+    if forced is not None:
+        inner_loops = forced["idx"].shape[1]
+        s = forced["S"][:, 0] + (s0 - s0.detach())
+    for t in range(inner_loops):
         nodes = with_obstacles(s, obs)
-        idx = knn_idx(s.detach(), top_k, nodes.detach())
-        a = controller_forward(ctrl_params, s, g, idx, nodes=nodes)
+        if forced is None:
+            idx = knn_idx(s.detach(), top_k, nodes.detach())
+            a = controller_forward(ctrl_params, s, g, idx, nodes=nodes)
+        else:
+            idx = forced["idx"][:, t].long()
+            sl = forced.get("slots")
+            a = controller_forward(ctrl_params, s, g, idx, nodes=nodes, pool_slots=None if sl is None else sl[:, t])
         if noise_prob > 0:
             coin = torch.rand(B, generator=generator, device=s.device) < noise_prob
             nz = torch.randn(a.shape, generator=generator, device=s.device) * noise_scale
             a = a + nz * coin[:, None, None].to(a.dtype)
         s_next = s + torch.cat([s[..., dim:], a], -1) * C.TIME_STEP
+        if forced is not None:
+            s_next = forced["S"][:, t + 1] + (s_next - s_next.detach())
         dist = torch.linalg.norm(s_next[..., :dim] - g, dim=-1).mean(-1)
         V.append(active.clone())
         A.append(a)

@@ -1,6 +1,9 @@
-"""GPU numerics of the hand-written backward kernels against PyTorch autograd on the fp32
-oracle (MI355X only). bf16 MFMA inputs -> compared per parameter tensor by relative norm
-error and cosine similarity."""
+"""GPU numerics of the hand-written backward kernels against PyTorch autograd on the oracle
+(MI355X only). The bf16 kernels are compared with the oracle in bf16-emulation mode
+(``oracle.emulate_bf16``: weights, hidden activations, pooled features and pre-activation
+gradients rounded where the kernels round), per parameter tensor by relative norm error; the
+fp32 (x3) kernels with the plain fp32 oracle (tests/test_gpu_fp32.py holds the per-kernel
+fp32 cases)."""
 import math
 
 import pytest
@@ -13,6 +16,7 @@ from macbf_gnn_amd.ops import layout as L
 from macbf_gnn_amd.ops import native
 from macbf_gnn_amd.ops.weights import PackedWeights
 from macbf_gnn_amd.utils.params import FlatParams
+from numerics import rel_cmp
 
 pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda")
@@ -37,16 +41,8 @@ def _states(lead, N, seed=0, vscale=0.6, dens=1.0):
     return torch.cat([p, v], -1).to(DEV)
 
 
-def _cmp(got, ref, name, rel=6e-2, cos=0.995):
-    got = got.double().flatten()
-    ref = ref.double().flatten()
-    rn = ref.norm().item()
-    if rn < 1e-12:
-        assert got.norm().item() < 1e-6, name
-        return
-    err = (got - ref).norm().item() / rn
-    c = torch.nn.functional.cosine_similarity(got, ref, dim=0).item()
-    assert err < rel and c > cos, f"{name}: rel err {err:.3e}, cos {c:.5f}"
+def _cmp(got, ref, name, rel, cos=None):
+    rel_cmp(got, ref, name, rel, cos)
 
 
 def _unpack(fp, maps, reds):
@@ -76,10 +72,11 @@ def test_cbf_bwd_matches_autograd(T, B, N):
     dh_raw = torch.randn(2, T, B, N, K, generator=g).to(DEV)
     p = {k: v.detach().clone().requires_grad_(True) for k, v in cbf.params_dict().items()}
     Sx = S.clone().requires_grad_(True)
-    h0 = O.cbf_forward(p, Sx[:T], idx.long())
-    h1 = O.cbf_forward(p, Sx[1:], idx.long())
-    Lsum = (dh_raw[0] * h0).sum() + (dh_raw[1] * h1).sum()
-    gr = torch.autograd.grad(Lsum, [Sx] + list(p.values()))
+    with O.emulate_bf16():
+        h0 = O.cbf_forward(p, Sx[:T], idx.long())
+        h1 = O.cbf_forward(p, Sx[1:], idx.long())
+        Lsum = (dh_raw[0] * h0).sum() + (dh_raw[1] * h1).sum()
+        gr = torch.autograd.grad(Lsum, [Sx] + list(p.values()))
     m0 = O.cbf_features(S[:T], idx.long())[1]
     m1 = O.cbf_features(S[1:], idx.long())[1]
     dh = torch.stack([dh_raw[0] * m0, dh_raw[1] * m1]).contiguous()
@@ -95,11 +92,11 @@ def test_cbf_bwd_matches_autograd(T, B, N):
     red = torch.zeros(native.CBF_PARTIAL, device=DEV)
     native.reduce_rows(part, red)
     torch.cuda.synchronize()
-    _cmp(dS, gr[0], "dL/dS", rel=0.1, cos=0.99)
+    _cmp(dS, gr[0], "dL/dS", rel=TOL_KERNEL)
     flat = _unpack(fp, {"cbf": L.cbf_grad_map}, {"cbf": red})
     mine = _param_grads(fp, flat, "cbf")
     for (k, _), ref in zip(p.items(), gr[1:]):
-        _cmp(mine[k], ref, k, rel=0.1, cos=0.99)   # bf16 activations/deltas (AMP-level noise)
+        _cmp(mine[k], ref, k, rel=TOL_KERNEL)
 
 
 @pytest.mark.parametrize("B,N", [(1, 32), (2, 64), (1, 200)])
@@ -142,16 +139,36 @@ def test_ctrl_step_bwd_matches_autograd(B, N):
     # ---- oracle
     p = {k: v.detach().clone().requires_grad_(True) for k, v in ctrl.params_dict().items()}
     sx = s.clone().requires_grad_(True)
-    a = O.controller_forward(p, sx, gg, idx.long())
-    torch.testing.assert_close(A, a.detach(), rtol=3e-2, atol=3e-2 * a.abs().max().item())
-    s_next = sx + torch.cat([sx[..., 2:], a], -1) * C.TIME_STEP
-    Lsum = (Gn * s_next).sum() + act_coef * O.action_loss_terms(sx, gg, a).sum()
-    gr = torch.autograd.grad(Lsum, [sx] + list(p.values()))
-    _cmp(Gout, gr[0], "dL/ds_t", rel=0.1, cos=0.99)
+    with O.emulate_bf16():
+        a = O.controller_forward(p, sx, gg, idx.long())
+        s_next = sx + torch.cat([sx[..., 2:], a], -1) * C.TIME_STEP
+        Lsum = (Gn * s_next).sum() + act_coef * O.action_loss_terms(sx, gg, a).sum()
+        gr = torch.autograd.grad(Lsum, [sx] + list(p.values()))
+    _cmp(A, a.detach(), "a", rel=TOL_FWD)
+    _cmp(Gout, gr[0], "dL/ds_t", rel=TOL_KERNEL)
     flat = _unpack(fp, {"node": L.ctrl_node_grad_map, "edge": L.ctrl_edge_grad_map}, {"node": rn, "edge": re})
     mine = _param_grads(fp, flat, "controller")
     for (k, _), ref in zip(p.items(), gr[1:]):
-        _cmp(mine[k], ref, k, rel=8e-2, cos=0.99)
+        _cmp(mine[k], ref, k, rel=TOL_KERNEL)
+
+
+# bf16 kernels vs the bf16-emulating oracle (relative norm error per tensor). Calibrated on
+# MI355X (profiles/r2_numerics/): measured errors are 3-10x below these bounds.
+TOL_FWD = 1e-2
+TOL_KERNEL = 2e-2
+TOL_STEP = 2e-2
+
+
+def _round_params(tr):
+    """bf16-representable weights: the oracle then evaluates the kernels' function."""
+    with torch.no_grad():
+        tr.fp.flat.copy_(tr.fp.flat.bfloat16().float())
+    tr.engine.after_update()
+
+
+def _cmp_tensors(tr, g_hip, g_ref, rel):
+    for m, pn, shape, o, n in tr.fp.specs:
+        _cmp(g_hip[o:o + n], g_ref[o:o + n], f"{m}.{pn}", rel=rel)
 
 
 def _trainer(device, **kw):
@@ -162,25 +179,29 @@ def _trainer(device, **kw):
     return Trainer(cfg, device=device, dp=DP(device=device))
 
 
+@pytest.mark.parametrize("prec", ["bf16", "fp32"])
 @pytest.mark.parametrize("bptt,reuse,T", [(True, True, 5), (False, True, 5), (True, False, 5), (False, False, 5),
                                           (True, True, 10), (True, False, 10)])
-def test_full_step_grad_matches_oracle(bptt, reuse, T):
-    """One full training step: HIP engine gradient vs autograd through the oracle engine, for
-    BPTT / no-BPTT and h' on the time-t or on the recomputed time-(t+1) neighbour slots. T = 10
-    takes the split edge->node reduction (early steps on the aux stream during the BPTT)."""
+def test_full_step_grad_matches_oracle(bptt, reuse, T, prec):
+    """One training step: HIP engine gradient vs autograd through the oracle engine replaying
+    the HIP trajectory, per parameter tensor, for BPTT / no-BPTT and h' on the time-t or on the
+    recomputed time-(t+1) neighbour slots. bf16: bf16-rounded weights, oracle in bf16-emulation
+    mode; fp32: the x3 kernels vs the fp32 oracle. T = 10 takes the split edge->node reduction
+    (early steps on the aux stream during the BPTT)."""
     from macbf_gnn_amd.engine.oracle_engine import OracleEngine
-    tr = _trainer(DEV, bptt=bptt, reuse_nbr_idx=reuse, T=T)
+    tr = _trainer(DEV, bptt=bptt, reuse_nbr_idx=reuse, T=T, dtype=prec)
+    if prec == "bf16":
+        _round_params(tr)
     tr.engine.reduce_late = 4 if T >= 8 else 0
     s0, g, _ = tr.sample()
     stats = tr.engine.step(s0, g)
     g_hip = tr.fp.grad.clone()
-    orc = OracleEngine(tr)
-    stats_o = orc.step(s0, g)
+    with O.emulate_bf16(prec == "bf16"):     # replay the HIP trajectory, graphs and pooling choices
+        stats_o = OracleEngine(tr).step(s0, g, forced=tr.engine.trajectory(int(float(stats["T"]))))
     g_ref = tr.fp.grad.clone()
-    for name in ("controller", "cbf"):
-        a_, b_ = tr.fp.ranges[name]
-        _cmp(g_hip[a_:b_], g_ref[a_:b_], name, rel=0.12, cos=0.99)
-    assert abs(float(stats["loss_total"]) - stats_o["loss_total"]) <= 0.05 * abs(stats_o["loss_total"]) + 1e-4
+    _cmp_tensors(tr, g_hip, g_ref, TOL_STEP if prec == "bf16" else 1e-3)
+    tf = TOL_FWD if prec == "bf16" else 1e-4
+    assert abs(float(stats["loss_total"]) - stats_o["loss_total"]) <= tf * abs(stats_o["loss_total"]) + 1e-6
 
 
 @pytest.mark.parametrize("T", [4, 12])
@@ -261,17 +282,16 @@ def test_prefetched_sampling_is_identical():
 
 
 def test_full_step_4096_agents_matches_oracle():
-    """BASELINE config #4 scale (4096 agents / env, LDS neighbour-tile stress) on a short horizon."""
+    """BASELINE config #4 scale (4096 agents / env, LDS neighbour-tile stress) on a short horizon,
+    fp32 (x3) kernels vs the fp32 oracle, per parameter tensor."""
     from macbf_gnn_amd.engine.oracle_engine import OracleEngine
-    tr = _trainer(DEV, N=4096, B=2, T=3)
+    tr = _trainer(DEV, N=4096, B=2, T=3, dtype="fp32")
     s0, g, _ = tr.sample()
     stats = tr.engine.step(s0, g)
     g_hip = tr.fp.grad.clone()
-    OracleEngine(tr).step(s0, g)
+    OracleEngine(tr).step(s0, g, forced=tr.engine.trajectory(int(float(stats["T"]))))
     g_ref = tr.fp.grad.clone()
-    for name in ("controller", "cbf"):
-        a_, b_ = tr.fp.ranges[name]
-        _cmp(g_hip[a_:b_], g_ref[a_:b_], name, rel=0.12, cos=0.99)
+    _cmp_tensors(tr, g_hip, g_ref, 1e-3)
     assert torch.isfinite(torch.as_tensor(float(stats["loss_total"])))
 
 

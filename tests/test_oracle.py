@@ -228,3 +228,73 @@ def test_oracle_total_loss_gradcheck_fp64():
         return O.train_losses(c, b, traj, g)[0]["total"]
 
     assert torch.autograd.gradcheck(total, (s_in, *leaves), eps=1e-6, atol=1e-5, rtol=1e-4)
+
+
+def test_bf16_emulation_mode():
+    """oracle.emulate_bf16: rounds hidden activations / pre-activation gradients like the bf16
+    kernels (small, non-zero change vs the fp32 oracle), restores the fp32 oracle on exit."""
+    import torch
+    from macbf_gnn_amd import oracle as O
+    from macbf_gnn_amd.models import CBF, Controller
+    torch.manual_seed(0)
+    ctrl, cbf = Controller(4), CBF(4)
+    s = torch.cat([torch.rand(2, 24, 2) * 3, torch.rand(2, 24, 2) - 0.5], -1)
+    g = s[..., :2] + 0.3
+    idx = O.knn_idx(s, 12)
+    pc = {k: v.detach().clone().requires_grad_(True) for k, v in ctrl.params_dict().items()}
+    pb = {k: v.detach().clone().requires_grad_(True) for k, v in cbf.params_dict().items()}
+
+    def run():
+        a = O.controller_forward(pc, s, g, idx)
+        h = O.cbf_forward(pb, s, idx)
+        gr = torch.autograd.grad(a.square().sum() + h.square().sum(), list(pc.values()) + list(pb.values()))
+        return a.detach(), h.detach(), gr
+
+    a0, h0, g0 = run()
+    with O.emulate_bf16():
+        a1, h1, g1 = run()
+    a2, h2, g2 = run()
+    assert torch.equal(a0, a2) and torch.equal(h0, h2)
+    for x, y in ((a1, a0), (h1, h0)):
+        e = ((x - y).norm() / y.norm()).item()
+        assert 0 < e < 2e-2
+    for x, y in zip(g1, g0):
+        assert ((x - y).norm() / y.norm()).item() < 5e-2
+
+
+def test_forced_rollout_replays_own_trajectory():
+    """oracle.rollout(forced=own trajectory): same states, same gradient (straight-through
+    replay); pool_slots = the true argmax: same action and gradient as the max-pool."""
+    import torch
+    from macbf_gnn_amd import oracle as O
+    from macbf_gnn_amd.models import CBF, Controller
+    torch.manual_seed(1)
+    ctrl, cbf = Controller(4), CBF(4)
+    s0 = torch.cat([torch.rand(2, 20, 2) * 3, torch.zeros(2, 20, 2)], -1)
+    g = s0[..., :2] + 0.4
+    pc = {k: v.detach().clone().requires_grad_(True) for k, v in ctrl.params_dict().items()}
+    pb = {k: v.detach().clone().requires_grad_(True) for k, v in cbf.params_dict().items()}
+
+    def grads(forced=None):
+        tr = O.rollout(pc, s0, g, inner_loops=6, early_stop=False, forced=forced)
+        losses, _, _ = O.train_losses(pc, pb, tr, g)
+        return tr, torch.autograd.grad(losses["total"], list(pc.values()) + list(pb.values()))
+
+    t0, g0 = grads()
+    forced = {"S": t0["S"].detach(), "idx": t0["idx"]}
+    t1, g1 = grads(forced)
+    assert torch.equal(t1["S"], t0["S"].detach())
+    for x, y in zip(g1, g0):
+        torch.testing.assert_close(x, y, rtol=1e-4, atol=1e-7)
+    # pool slots
+    idx = O.knn_idx(s0, 12)
+    a, aux = O.controller_forward(pc, s0, g, idx, return_aux=True)
+    slots = aux["hm"].argmax(dim=-2)
+    slots = torch.where(aux["hm"].max(dim=-2).values > 0, slots, torch.full_like(slots, 255))
+    assert float(O.pool_slot_gap(aux["hm"], slots)) == 0.0
+    a2 = O.controller_forward(pc, s0, g, idx, pool_slots=slots)
+    torch.testing.assert_close(a2, a)
+    ga = torch.autograd.grad(a.sum(), list(pc.values()))
+    gb = torch.autograd.grad(a2.sum(), list(pc.values()))
+    for x, y in zip(ga, gb):
+        torch.testing.assert_close(x, y)
