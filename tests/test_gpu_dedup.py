@@ -35,12 +35,15 @@ def test_cbf_match_equals_reference(recomputed):
         assert n_ref > E            # the states move: some neighbour sets change
 
 
+@pytest.mark.parametrize("prec", ["fp32", "bf16"])
 @pytest.mark.parametrize("reuse", [True, False])
-def test_dedup_step_matches_fused_kernel(reuse):
+def test_dedup_step_matches_fused_kernel(reuse, prec):
     """One training step: deduplicated evaluation list vs the fused h/h' kernel (same
-    semantics, different evaluation order and bf16 rounding of the summed upstream grads)."""
-    a = _trainer(DEV, N=96, B=3, T=6, reuse_nbr_idx=reuse, cbf_dedup=True)
-    b = _trainer(DEV, N=96, B=3, T=6, reuse_nbr_idx=reuse, cbf_dedup=False)
+    semantics, different evaluation order; bf16: the summed upstream grads dh + dh' of a
+    shared evaluation are rounded once instead of twice -> a looser bound)."""
+    a = _trainer(DEV, N=96, B=3, T=6, reuse_nbr_idx=reuse, cbf_dedup=True, dtype=prec)
+    b = _trainer(DEV, N=96, B=3, T=6, reuse_nbr_idx=reuse, cbf_dedup=False, dtype=prec)
+    rel = 1e-4 if prec == "fp32" else 2e-2
     assert a.engine.dedup and not b.engine.dedup
     s0, g, _ = a.sample()
     sa = a.engine.step(s0, g)
@@ -49,13 +52,13 @@ def test_dedup_step_matches_fused_kernel(reuse):
     gb = b.fp.grad.clone()
     for name in ("controller", "cbf"):
         lo, hi = a.fp.ranges[name]
-        _cmp(ga[lo:hi], gb[lo:hi], name, rel=3e-2, cos=0.999)
+        _cmp(ga[lo:hi], gb[lo:hi], name, rel=rel)
     for k in ("loss_dang", "loss_safe", "loss_dang_deriv", "loss_safe_deriv", "loss_action",
               "acc_dang_sum", "acc_safe_sum", "acc_dang_deriv_sum", "acc_safe_deriv_sum"):
         x, y = float(sa[k]), float(sb[k])
         assert abs(x - y) <= 2e-3 * abs(y) + 1e-5, (k, x, y)
     # the per-step state gradients (CBF -> dS) agree too
-    _cmp(a.engine.dS, b.engine.dS, "dS", rel=3e-2, cos=0.999)
+    _cmp(a.engine.dS, b.engine.dS, "dS", rel=rel)
 
 
 def test_dedup_deterministic():
