@@ -398,8 +398,18 @@ template <int ES> DEV float xmma_skip(...) { return 0.f; }
 // with it, packed relu, fp32 head), without the weight-gradient stages: ~40 KB of LDS, so
 // four 8-wave workgroups share a CU; the edge gathers of the next tile are issued before the
 // MFMA chain of the current one.
+// x3: without the next-tile prefetch the kernel fits 122 VGPRs -> two 8-wave workgroups
+// (4 waves/SIMD, LDS 2 x 70 KB) per CU instead of one: 1.31 -> 1.22 ms per iteration's h
+// (profiles/r2_hfwd/); the 16-bit builds keep the prefetch (40 KB LDS, more resident waves)
+#ifndef CBF_HFWD_MINW
+#if MB_X3
+#define CBF_HFWD_MINW 4
+#else
+#define CBF_HFWD_MINW 1
+#endif
+#endif
 template <int NW, int D>
-__global__ __launch_bounds__(NW * 64) void cbf_hfwd_kernel(CbfFwdArgs a) {
+__global__ __launch_bounds__(NW * 64, CBF_HFWD_MINW) void cbf_hfwd_kernel(CbfFwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   h16* W2 = reinterpret_cast<h16*>(smem);
   h16* W3 = W2 + RM_W2;
@@ -423,12 +433,24 @@ __global__ __launch_bounds__(NW * 64) void cbf_hfwd_kernel(CbfFwdArgs a) {
     cbf_edge<D>(a.S, a.s_env, a.s_step, pass ? a.idx1 : a.idx, a.B, a.N, a.K, e, in ? E : 0, pass, a.obs_r,
                 a.dist_thr, a.dist_eps, c);
   };
+#ifndef CBF_HFWD_PREFETCH
+#if MB_X3
+#define CBF_HFWD_PREFETCH 0
+#else
+#define CBF_HFWD_PREFETCH 1
+#endif
+#endif
   EdgeCtx<D> nx;
   unsigned tile = blockIdx.x * NW + wave;
-  if (tile < ntiles) load(tile, nx);
+  if (CBF_HFWD_PREFETCH && tile < ntiles) load(tile, nx);
   for (; tile < ntiles; tile += stride) {
+#if CBF_HFWD_PREFETCH
     const EdgeCtx<D> c = nx;
     if (tile + stride < ntiles) load(tile + stride, nx);
+#else
+    EdgeCtx<D> c;
+    load(tile, c);
+#endif
     const h16x8 F = cbf_edge_frag<D>(c.rp, c.rv, c.eye, c.dfeat, c.ok, h);
     const h16* wt = wf + opaque_zero();
     const h16* W2c = W2 + opaque_zero();
