@@ -176,6 +176,25 @@ DEV void ctrl_idx_load(const int* idx, long i_env, int N, int K, int g0, int q, 
   }
 }
 
+// dense edge rows (edge backward): a wave's 32 agents x K slots are 32K consecutive rows =
+// K tiles; row e = 32q + r -> agent e / K, slot e % K (invK = ceil(2^16 / K): exact for e < 512)
+DEV int dense_agent(int e, unsigned invK) { return (int)(((unsigned)e * invK) >> 16); }
+
+DEV void ctrl_idx_load_dense(const int* idx, long i_env, int N, int K, unsigned invK, int g0, int q, int r,
+                             int total, EdgeIdx& o) {
+  const int e = 32 * q + r;
+  const int al = dense_agent(e, invK);
+  const int slot = e - al * K;
+  const int gi = g0 + al;
+  o.ok = (q < K) && (gi < total);
+  o.b = 0; o.i = 0; o.j = 0;
+  if (o.ok) {
+    o.b = gi / N;
+    o.i = gi - o.b * N;
+    o.j = idx[o.b * (int)i_env + o.i * K + slot];
+  }
+}
+
 template <int D>
 DEV void ctrl_st_load(const float4* S, long s_env, const EdgeIdx& x, EdgeSt<D>& o) {
   o.ok = x.ok;
@@ -1018,6 +1037,12 @@ __global__ __launch_bounds__(NB_WAVES * 64, 1) void ctrl_node_bwd_kernel(CtrlNod
 constexpr int EB_WAVES = CTRL_EB_WAVES;
 constexpr int EB_CH = EB_WAVES * 32;     // agents per chunk (each round: EB_CH edges)
 constexpr int EB_TA = 8 / EB_WAVES;      // owned dW2 tiles per wave
+// dense edge rows: K tiles per 32-agent wave (12 at K = 12) instead of 16 tiles of 2 agents x 16
+// slots (a quarter of them padding rows at K = 12)
+#ifndef CTRL_EB_DENSE
+#define CTRL_EB_DENSE 1
+#endif
+constexpr bool EB_DENSE = CTRL_EB_DENSE;
 constexpr int EP_W2 = 0, EP_B2 = 8192, EP_W1 = 8320;
 constexpr int CTRL_EDGE_PARTIAL = 10368;
 constexpr int EB_PL = (128 + 64) * EB_CH;             // elements per stage plane (x3: lo plane at +EB_PL)
@@ -1051,25 +1076,33 @@ DEV void edge_bwd_body(const CtrlEdgeBwdArgs& a, unsigned char* smem, long w0, l
   // use qsplit = 1
   const int QP = a.qsplit > 1 ? a.qsplit : 1;
   const long nwork = nchunks * QP;
+  const int NT = EB_DENSE ? K : 16;                         // tiles per 32-agent wave
+  const unsigned invK = (65536u + (unsigned)K - 1u) / (unsigned)K;
+  auto idx_load = [&](int g0_, int q, EdgeIdx& o) {
+    if constexpr (EB_DENSE) ctrl_idx_load_dense(a.idx, a.i_env, N, K, invK, g0_, q, r, total, o);
+    else ctrl_idx_load(a.idx, a.i_env, N, K, g0_, q, r, total, o);
+  };
   for (long w = w0; w < nwork; w += wstride) {
     const long chunk = w / QP;
     const int part = (int)(w - chunk * QP);
-    const int q0 = part * 16 / QP, q1 = (part + 1) * 16 / QP;
+    const int q0 = part * NT / QP, q1 = (part + 1) * NT / QP;
     EdgeIdx xi1;
     EdgeSt<D> xs0;
     const int g0 = (int)(chunk * EB_CH) + wave * 32;
     {
       EdgeIdx xi0;
-      ctrl_idx_load(a.idx, a.i_env, N, K, g0, q0, r, total, xi0);
+      idx_load(g0, q0, xi0);
       ctrl_st_load<D>(a.S, a.s_env, xi0, xs0);
-      ctrl_idx_load(a.idx, a.i_env, N, K, g0, q0 + 1, r, total, xi1);
+      idx_load(g0, q0 + 1, xi1);
     }
     // argmax slots / dL/dpooled of the tile's two agents (lane (r, h): agent 2q+h, features
     // 4r..4r+3): loaded one tile ahead, like the edge gathers
-    auto pool_load = [&](int q, unsigned& am4, h16x4& dp4, h16x4& dl4) {
-      const int ag = g0 + 2 * q + h;
+    // dense rows: tile q holds agents af(q) .. (32q + 31) / K; pass p of a tile = agents
+    // af + 2p + h (lane half h), two passes prefetched (all of a tile's agents for K >= 11)
+    auto pool_load_ag = [&](int al, unsigned& am4, h16x4& dp4, h16x4& dl4) {
+      const int ag = g0 + al;
       am4 = 0xFFFFFFFFu;
-      if (q < 16 && ag < total) {
+      if (al < 32 && ag < total) {
         const int bb = ag / N, ii = ag - bb * N;
         am4 = *reinterpret_cast<const unsigned*>(a.argmax + bb * (int)a.am_env + ii * 128 + 4 * r);
         const h16* dpr = a.dP + bb * (int)a.dp_env + ii * PROW + 4 * r;
@@ -1077,19 +1110,43 @@ DEV void edge_bwd_body(const CtrlEdgeBwdArgs& a, unsigned char* smem, long w0, l
         if constexpr (X3) dl4 = *reinterpret_cast<const h16x4*>(dpr + 128);
       }
     };
-    unsigned am_n;
-    h16x4 dp_n, dl_n;
+    constexpr int NPF = EB_DENSE ? 2 : 1;                 // prefetched agent passes per tile
+    auto pass_agent = [&](int q, int p) {
+      if constexpr (EB_DENSE) {
+        const int af = dense_agent(32 * q, invK);
+        const int al = af + 2 * p + h;
+        return (q < NT && al * K < 32 * q + 32) ? al : 32;      // 32: no agent
+      } else {
+        return q < NT ? 2 * q + h : 32;
+      }
+    };
+    auto pool_load = [&](int q, unsigned (&am4)[NPF], h16x4 (&dp4)[NPF], h16x4 (&dl4)[NPF]) {
+#pragma unroll
+      for (int p = 0; p < NPF; ++p) pool_load_ag(pass_agent(q, p), am4[p], dp4[p], dl4[p]);
+    };
+    unsigned am_n[NPF];
+    h16x4 dp_n[NPF], dl_n[NPF];
     pool_load(q0, am_n, dp_n, dl_n);
     for (int q = q0; q < q1; ++q) {
       const EdgeSt<D> cur = xs0;
-      const unsigned am4 = am_n;
-      const h16x4 dp4 = dp_n, dl4 = dl_n;
+      unsigned am4[NPF];
+      h16x4 dp4[NPF], dl4[NPF];
+#pragma unroll
+      for (int p = 0; p < NPF; ++p) { am4[p] = am_n[p]; dp4[p] = dp_n[p]; dl4[p] = dl_n[p]; }
       ctrl_st_load<D>(a.S, a.s_env, xi1, xs0);
-      ctrl_idx_load(a.idx, a.i_env, N, K, g0, q + 2, r, total, xi1);
+      idx_load(g0, q + 2, xi1);
       pool_load(q + 1, am_n, dp_n, dl_n);
-      const int slot = r & 15;
+      int slot, ga;
+      if constexpr (EB_DENSE) {
+        const int e = 32 * q + r;
+        const int al = dense_agent(e, invK);
+        slot = e - al * K;
+        ga = g0 + al;
+      } else {
+        slot = r & 15;
+        ga = g0 + 2 * q + (r >> 4);
+      }
       const bool ok = cur.ok;
-      const int ga = g0 + 2 * q + (r >> 4);
       const int b = ok ? ga / N : 0;
       const int i = cur.i, j = cur.j;
       const float eye = (j == i) ? 1.f : 0.f;
@@ -1115,13 +1172,32 @@ DEV void edge_bwd_body(const CtrlEdgeBwdArgs& a, unsigned char* smem, long w0, l
           *reinterpret_cast<u32x4*>(imS + wave * 32 * 128 + (c8 * 64 + lane) * 8) = zero4;
           if constexpr (X3) *reinterpret_cast<u32x4*>(imS + EB_PL + wave * 32 * 128 + (c8 * 64 + lane) * 8) = zero4;
         }
+        // (am4 = all 0xFF: agent out of range)
+        auto scatter = [&](int al, unsigned am, const h16x4& dp, const h16x4& dl) {
 #pragma unroll
-        for (int jj = 0; jj < 4; ++jj) {               // (am4 = all 0xFF: agent out of range)
-          const unsigned sl = (am4 >> (8 * jj)) & 0xFFu;
-          if (sl < 16u) {
-            const int o = swz_off<128>(wave * 32 + 16 * h + (int)sl, 4 * r + jj);
-            imS[o] = dp4[jj];
-            if constexpr (X3) imS[EB_PL + o] = dl4[jj];
+          for (int jj = 0; jj < 4; ++jj) {
+            const unsigned sl = (am >> (8 * jj)) & 0xFFu;
+            if (sl < 16u) {
+              const int row = EB_DENSE ? al * K + (int)sl - 32 * q : 16 * h + (int)sl;
+              if (!EB_DENSE || (unsigned)row < 32u) {
+                const int o = swz_off<128>(wave * 32 + row, 4 * r + jj);
+                imS[o] = dp[jj];
+                if constexpr (X3) imS[EB_PL + o] = dl[jj];
+              }
+            }
+          }
+        };
+#pragma unroll
+        for (int p = 0; p < NPF; ++p) scatter(pass_agent(q, p), am4[p], dp4[p], dl4[p]);
+        if constexpr (EB_DENSE) {      // K <= 10: a tile spans more than 4 agents (not prefetched)
+          for (int p = NPF; p < 16; ++p) {
+            const int a0 = dense_agent(32 * q, invK) + 2 * p;      // the pass's first agent (uniform)
+            if (a0 > 31 || a0 * K >= 32 * q + 32) break;
+            const int al = pass_agent(q, p);
+            unsigned am;
+            h16x4 dp, dl;
+            pool_load_ag(al, am, dp, dl);
+            scatter(al, am, dp, dl);
           }
         }
         lds_wave_sync();
