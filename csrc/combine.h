@@ -11,13 +11,14 @@ namespace mb {
 // node are one coalesced 16*K-byte segment (lane k reads slot k), the incoming edges are
 // spread over the lanes (independent random 16-byte loads, L2-resident per step graph), and
 // a fixed xor butterfly combines the lane partials -> deterministic, no atomics.
-constexpr int RG = 16;                 // lanes per node
+#ifndef CMB_RG
+#define CMB_RG 16
+#endif
+constexpr int RG = CMB_RG;             // lanes per node
 
 DEV float grp_sum(float v) {
-  v += __shfl_xor(v, 8, RG);
-  v += __shfl_xor(v, 4, RG);
-  v += __shfl_xor(v, 2, RG);
-  v += __shfl_xor(v, 1, RG);
+#pragma unroll
+  for (int o = RG / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, RG);
   return v;
 }
 
