@@ -163,15 +163,41 @@ DEV void node_forward(PoolFr pool, const h16x8& sfrag, const h16* wn, const floa
 struct EdgeIdx { int j, b, i; bool ok; };
 template <int D> struct EdgeSt { float rp[D], rv[D]; int j, i; bool ok; };
 
-DEV void ctrl_idx_load(const int* idx, long i_env, int N, int K, int g0, int q, int r, int total, EdgeIdx& o) {
+// (env, index) of the agents g0 + al, 0 <= al < 32, of a 32-agent group: one division per group;
+// with N >= 32 the group wraps into the next env at most once (a per-tile 32-bit division by the
+// runtime N is a dozen VALU instructions, two of them quarter rate)
+#ifndef CTRL_GROUP_BASE
+#define CTRL_GROUP_BASE 1
+#endif
+struct AgentBase { int g0, b0, i0; };
+DEV AgentBase agent_base(int g0, int N) {
+  AgentBase o;
+  o.g0 = g0;
+  o.b0 = g0 / N;
+  o.i0 = g0 - o.b0 * N;
+  return o;
+}
+DEV void agent_bi(const AgentBase& ab, int al, int N, int& b, int& i) {
+  if (CTRL_GROUP_BASE && N >= 32) {
+    i = ab.i0 + al;
+    b = ab.b0;
+    if (i >= N) { i -= N; ++b; }
+  } else {
+    const int g = ab.g0 + al;
+    b = g / N;
+    i = g - b * N;
+  }
+}
+
+DEV void ctrl_idx_load(const int* idx, long i_env, int N, int K, const AgentBase& ab, int q, int r, int total,
+                       EdgeIdx& o) {
   const int al = 2 * q + (r >> 4);
   const int slot = r & 15;
-  const int gi = g0 + al;
+  const int gi = ab.g0 + al;
   o.ok = (q < 16) && (gi < total) && (slot < K);
   o.b = 0; o.i = 0; o.j = 0;
   if (o.ok) {
-    o.b = gi / N;
-    o.i = gi - o.b * N;
+    agent_bi(ab, al, N, o.b, o.i);
     o.j = idx[o.b * (int)i_env + o.i * K + slot];
   }
 }
@@ -180,17 +206,16 @@ DEV void ctrl_idx_load(const int* idx, long i_env, int N, int K, int g0, int q, 
 // K tiles; row e = 32q + r -> agent e / K, slot e % K (invK = ceil(2^16 / K): exact for e < 512)
 DEV int dense_agent(int e, unsigned invK) { return (int)(((unsigned)e * invK) >> 16); }
 
-DEV void ctrl_idx_load_dense(const int* idx, long i_env, int N, int K, unsigned invK, int g0, int q, int r,
-                             int total, EdgeIdx& o) {
+DEV void ctrl_idx_load_dense(const int* idx, long i_env, int N, int K, unsigned invK, const AgentBase& ab, int q,
+                             int r, int total, EdgeIdx& o) {
   const int e = 32 * q + r;
   const int al = dense_agent(e, invK);
   const int slot = e - al * K;
-  const int gi = g0 + al;
+  const int gi = ab.g0 + al;
   o.ok = (q < K) && (gi < total);
   o.b = 0; o.i = 0; o.j = 0;
   if (o.ok) {
-    o.b = gi / N;
-    o.i = gi - o.b * N;
+    agent_bi(ab, al, N, o.b, o.i);
     o.j = idx[o.b * (int)i_env + o.i * K + slot];
   }
 }
@@ -330,20 +355,21 @@ DEV void ctrl_fwd_groups(const CtrlArgs& a, const h16* wl, const h16* wn, const 
   const int APW = (a.apw >= 2 && a.apw <= 32) ? a.apw : 32;
   for (int grp = grp0; grp * APW < total; grp += gstride) {
     const int g0 = grp * APW;
+    const AgentBase ab = agent_base(g0, N);
     // ---------------- edge phase: 16 tiles x (2 agents x 16 slots); the gathers of tile q+1
     // (idx -> s_j, dependent global loads) are issued before tile q's MFMA chain
     EdgeIdx xi1;
     EdgeSt<D> xs0;
     {
       EdgeIdx xi0;
-      ctrl_idx_load(a.idx, a.i_env, N, K, g0, 0, r, total, xi0);
+      ctrl_idx_load(a.idx, a.i_env, N, K, ab, 0, r, total, xi0);
       ctrl_st_load<D>(a.S, a.s_env, xi0, xs0);
-      ctrl_idx_load(a.idx, a.i_env, N, K, g0, 1, r, total, xi1);
+      ctrl_idx_load(a.idx, a.i_env, N, K, ab, 1, r, total, xi1);
     }
     for (int q = 0; q < APW / 2; ++q) {
       const EdgeSt<D> cur = xs0;
       ctrl_st_load<D>(a.S, a.s_env, xi1, xs0);                    // states of tile q+1
-      ctrl_idx_load(a.idx, a.i_env, N, K, g0, q + 2, r, total, xi1);   // idx of tile q+2
+      ctrl_idx_load(a.idx, a.i_env, N, K, ab, q + 2, r, total, xi1);   // idx of tile q+2
       const bool ok = cur.ok;
       const float eye = (cur.j == cur.i) ? 1.f : 0.f;
       const bool m = ok && (sqrtf(sqsum<D>(cur.rp)) < a.obs_r);   // strict, un-eps'd (controller.py:38-39)
@@ -366,7 +392,7 @@ DEV void ctrl_fwd_groups(const CtrlArgs& a, const h16* wl, const h16* wn, const 
       int bb = 0, ii = 0;
       const int ga = g0 + arow;
       const bool gout = (a.argmax || GPOOL) && ga < total;
-      if (gout) { bb = ga / N; ii = ga - bb * N; }
+      if (gout) agent_bi(ab, arow, N, bb, ii);
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt) {
 #ifdef CTRL_X_NOPOOL
@@ -405,7 +431,8 @@ DEV void ctrl_fwd_groups(const CtrlArgs& a, const h16* wl, const h16* wn, const 
       // before, so no stale L1 line can hide them)
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       const int gi = min(g0 + min(r, APW - 1), total - 1);
-      const int bb = gi / N, ii = gi - bb * N;
+      int bb, ii;
+      agent_bi(ab, gi - g0, N, bb, ii);
       const h16* prow = a.pooled + (long)bb * a.p_env + (long)ii * PROW + 8 * h;
       node_phase<D>(a, g0, APW, total, [&](int kk) { return row_fr(prow + 16 * kk, 128); }, wn, nb2, nb3, nb4, lane);
       continue;
@@ -1078,9 +1105,9 @@ DEV void edge_bwd_body(const CtrlEdgeBwdArgs& a, unsigned char* smem, long w0, l
   const long nwork = nchunks * QP;
   const int NT = EB_DENSE ? K : 16;                         // tiles per 32-agent wave
   const unsigned invK = (65536u + (unsigned)K - 1u) / (unsigned)K;
-  auto idx_load = [&](int g0_, int q, EdgeIdx& o) {
-    if constexpr (EB_DENSE) ctrl_idx_load_dense(a.idx, a.i_env, N, K, invK, g0_, q, r, total, o);
-    else ctrl_idx_load(a.idx, a.i_env, N, K, g0_, q, r, total, o);
+  auto idx_load = [&](const AgentBase& ab_, int q, EdgeIdx& o) {
+    if constexpr (EB_DENSE) ctrl_idx_load_dense(a.idx, a.i_env, N, K, invK, ab_, q, r, total, o);
+    else ctrl_idx_load(a.idx, a.i_env, N, K, ab_, q, r, total, o);
   };
   for (long w = w0; w < nwork; w += wstride) {
     const long chunk = w / QP;
@@ -1089,11 +1116,12 @@ DEV void edge_bwd_body(const CtrlEdgeBwdArgs& a, unsigned char* smem, long w0, l
     EdgeIdx xi1;
     EdgeSt<D> xs0;
     const int g0 = (int)(chunk * EB_CH) + wave * 32;
+    const AgentBase ab = agent_base(g0, N);
     {
       EdgeIdx xi0;
-      idx_load(g0, q0, xi0);
+      idx_load(ab, q0, xi0);
       ctrl_st_load<D>(a.S, a.s_env, xi0, xs0);
-      idx_load(g0, q0 + 1, xi1);
+      idx_load(ab, q0 + 1, xi1);
     }
     // argmax slots / dL/dpooled of the tile's two agents (lane (r, h): agent 2q+h, features
     // 4r..4r+3): loaded one tile ahead, like the edge gathers
@@ -1103,7 +1131,8 @@ DEV void edge_bwd_body(const CtrlEdgeBwdArgs& a, unsigned char* smem, long w0, l
       const int ag = g0 + al;
       am4 = 0xFFFFFFFFu;
       if (al < 32 && ag < total) {
-        const int bb = ag / N, ii = ag - bb * N;
+        int bb, ii;
+        agent_bi(ab, al, N, bb, ii);
         am4 = *reinterpret_cast<const unsigned*>(a.argmax + bb * (int)a.am_env + ii * 128 + 4 * r);
         const h16* dpr = a.dP + bb * (int)a.dp_env + ii * PROW + 4 * r;
         dp4 = *reinterpret_cast<const h16x4*>(dpr);
@@ -1134,20 +1163,20 @@ DEV void edge_bwd_body(const CtrlEdgeBwdArgs& a, unsigned char* smem, long w0, l
 #pragma unroll
       for (int p = 0; p < NPF; ++p) { am4[p] = am_n[p]; dp4[p] = dp_n[p]; dl4[p] = dl_n[p]; }
       ctrl_st_load<D>(a.S, a.s_env, xi1, xs0);
-      idx_load(g0, q + 2, xi1);
+      idx_load(ab, q + 2, xi1);
       pool_load(q + 1, am_n, dp_n, dl_n);
-      int slot, ga;
+      int slot, al;
       if constexpr (EB_DENSE) {
         const int e = 32 * q + r;
-        const int al = dense_agent(e, invK);
+        al = dense_agent(e, invK);
         slot = e - al * K;
-        ga = g0 + al;
       } else {
         slot = r & 15;
-        ga = g0 + 2 * q + (r >> 4);
+        al = 2 * q + (r >> 4);
       }
       const bool ok = cur.ok;
-      const int b = ok ? ga / N : 0;
+      int b = 0, ib_;
+      if (ok) agent_bi(ab, al, N, b, ib_);
       const int i = cur.i, j = cur.j;
       const float eye = (j == i) ? 1.f : 0.f;
       const h16x8 F = ctrl_edge_frag<D>(cur.rp, cur.rv, eye, ok, h);
