@@ -29,7 +29,10 @@ namespace mb {
 
 constexpr int MATCH_BLOCK = 256;
 constexpr int DH_BLOCK = 256;
-constexpr int DH_PARTIAL = 12;   // loss partials per block: [0, 0, 8 sums, 0, 0] (rows padded to 4)
+constexpr int DH_PARTIAL = 12;
+#ifndef DH_UNROLL
+#define DH_UNROLL 4
+#endif   // loss partials per block: [0, 0, 8 sums, 0, 0] (rows padded to 4)
 
 // Block-wide exclusive scan of one int per thread (NT threads, wave64): returns the exclusive
 // prefix of this thread, *total = the block sum. Two barriers.
@@ -190,14 +193,59 @@ __global__ __launch_bounds__(DH_BLOCK) void cbf_dh_kernel(CbfDhArgs a) {
   const unsigned span = dh_span(U, gridDim.x);
   const unsigned u_hi = min(U, (blockIdx.x + 1) * span);
   int nact = 0;
-  for (unsigned u = blockIdx.x * span + threadIdx.x; u < u_hi; u += DH_BLOCK) {
-    float g = 0.f;
-    if (u < E) {                                   // h-role of main slot u
-      const unsigned t = u / BNK, b = (u - t * BNK) / NK;
-      if (!a.valid || a.valid[t * a.B + b]) {
-        const float hv = a.h[u], hnv = a.h[a.map1[u]];
+  // DH_UNROLL evaluations per thread per round: every round issues the independent loads of all
+  // of them first, then the dependent ones (partner h, source slot), then computes -- the same
+  // per-thread order of u as a plain loop (u, u + DH_BLOCK, ...), so the partial sums are unchanged
+  constexpr int UR = DH_UNROLL;
+  for (unsigned u0 = blockIdx.x * span + threadIdx.x; u0 < u_hi; u0 += UR * DH_BLOCK) {
+    bool in[UR], mv[UR], sv[UR];
+    float hv0[UR], hn0[UR], hv1[UR], hn1[UR];
+    unsigned m1[UR];
+    int src[UR];
+    uint8_t dg0[UR], dg1[UR], hm[UR];
+#pragma unroll
+    for (int j = 0; j < UR; ++j) {
+      const unsigned u = u0 + j * DH_BLOCK;
+      in[j] = u < u_hi;
+      mv[j] = sv[j] = false;
+      src[j] = -1;
+      if (in[j]) {
+        hm[j] = a.hmask[u];
+        src[j] = a.src[u];
+        hn1[j] = a.h[u];
+        if (u < E) {
+          const unsigned t = u / BNK, b = (u - t * BNK) / NK;
+          mv[j] = !a.valid || a.valid[t * a.B + b];
+          m1[j] = (unsigned)a.map1[u];
+          dg0[j] = a.dang[u];
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < UR; ++j) {
+      const unsigned u = u0 + j * DH_BLOCK;
+      if (mv[j]) {
+        hv0[j] = hn1[j];            // h of main slot u
+        hn0[j] = a.h[m1[j]];
+      }
+      if (in[j] && src[j] >= 0) {
+        const unsigned su = (unsigned)src[j];
+        const unsigned t = su / BNK, b = (su - t * BNK) / NK;
+        sv[j] = !a.valid || a.valid[t * a.B + b];
+        hv1[j] = a.h[su];
+        dg1[j] = a.dang[su];
+      }
+      (void)u;
+    }
+#pragma unroll
+    for (int j = 0; j < UR; ++j) {
+      if (!in[j]) continue;
+      const unsigned u = u0 + j * DH_BLOCK;
+      float g = 0.f;
+      if (mv[j]) {                                   // h-role of main slot u
+        const float hv = hv0[j], hnv = hn0[j];
         const float deriv = hnv - hv + lc.dt_alpha * hv;
-        if (a.dang[u]) {
+        if (dg0[j]) {
           const float cc = lc.scale / nd;
           const float ind_b = (hv + lc.eps_dang > 0.f) ? 1.f : 0.f;
           const float ind_d = (-deriv + lc.eps_dang > 0.f) ? 1.f : 0.f;
@@ -217,15 +265,10 @@ __global__ __launch_bounds__(DH_BLOCK) void cbf_dh_kernel(CbfDhArgs a) {
           acc[7] += (deriv > 0.f) ? 1.f : 0.f;
         }
       }
-    }
-    const int s = a.src[u];
-    if (s >= 0) {                                  // h'-role: derivative term of source slot s
-      const unsigned su = (unsigned)s;
-      const unsigned t = su / BNK, b = (su - t * BNK) / NK;
-      if (!a.valid || a.valid[t * a.B + b]) {
-        const float hv = a.h[su], hnv = a.h[u];
+      if (sv[j]) {                                   // h'-role: derivative term of source slot s
+        const float hv = hv1[j], hnv = hn1[j];
         const float deriv = hnv - hv + lc.dt_alpha * hv;
-        if (a.dang[su]) {
+        if (dg1[j]) {
           const float ind_d = (-deriv + lc.eps_dang > 0.f) ? 1.f : 0.f;
           g += -(lc.scale / nd) * lc.w_dang_d * ind_d;
         } else {
@@ -233,10 +276,10 @@ __global__ __launch_bounds__(DH_BLOCK) void cbf_dh_kernel(CbfDhArgs a) {
           g += -(lc.scale / ns) * lc.w_safe_d * ind_d;
         }
       }
+      const float d = hm[j] ? g : 0.f;
+      a.dh[u] = d;
+      nact += (d != 0.f) ? 1 : 0;
     }
-    const float d = a.hmask[u] ? g : 0.f;
-    a.dh[u] = d;
-    nact += (d != 0.f) ? 1 : 0;
   }
   __shared__ float red[8][DH_BLOCK / WAVE];
   __shared__ int cred[DH_BLOCK / WAVE];
