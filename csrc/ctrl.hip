@@ -88,7 +88,10 @@ DEV void acc_rows8(const f32x16& c, float (&o)[8]) {
 }
 
 // One edge tile in the transposed orientation: returns Z^T (4 column tiles) for 32 edges.
-DEV void ctrl_edge_tile(const h16x8& F, const h16* wl, const float* eb2, int lane, f32x16 (&Z)[4]) {
+// ZB (optional): loop-invariant bias accumulators (4 x 16 registers, one bias per lane column),
+// the C operand of each column tile's first MFMA -> no per-tile bias broadcast (64 VALU moves)
+DEV void ctrl_edge_tile(const h16x8& F, const h16* wl, const float* eb2, int lane, f32x16 (&Z)[4],
+                        const f32x16* ZB = nullptr) {
   const int r = lane & 31;
   f32x16 H1[2];
 #pragma unroll
@@ -98,10 +101,14 @@ DEV void ctrl_edge_tile(const h16x8& F, const h16* wl, const float* eb2, int lan
   }
 #pragma unroll
   for (int nt = 0; nt < 4; ++nt) {
-    const float bv = eb2[32 * nt + r];
     f32x16 z;
+    if (ZB) {
+      z = ZB[nt];
+    } else {
+      const float bv = eb2[32 * nt + r];
 #pragma unroll
-    for (int q = 0; q < 16; ++q) z[q] = bv;
+      for (int q = 0; q < 16; ++q) z[q] = bv;
+    }
     static_for<4>([&](auto kk_) {
       constexpr int kk = decltype(kk_)::value;
       z = mma(acc_fr<kk & 1>(H1[kk >> 1]), frag_fr(wl, 2 + nt * 4 + kk, lane), z);
@@ -336,6 +343,9 @@ DEV void node_phase(const CtrlArgs& a, int g0, int APW, int total, PoolFr pool, 
 // already in LDS: wl = ew1f|ew2, wn = nw1f..nw4, vl = CTRL_VEC floats, pools = one 32-row pool
 // image per wave). SPLIT (always for x3): edge phase only, the pooled rows go to global memory
 // and ctrl_node_groups runs the node phase.
+#ifndef CTRL_HOIST_EB
+#define CTRL_HOIST_EB 1
+#endif
 template <int D, bool SPLIT, bool GNODE = false>
 DEV void ctrl_fwd_groups(const CtrlArgs& a, const h16* wl, const h16* wn, const float* vl, h16* pools, int grp0,
                          int gstride) {
@@ -353,6 +363,18 @@ DEV void ctrl_fwd_groups(const CtrlArgs& a, const h16* wl, const h16* wn, const 
   // agents per wave: 32, or 4..16 for small scenes (more waves share the edge phase; the node
   // phase's MFMA rows beyond APW carry ignored data)
   const int APW = (a.apw >= 2 && a.apw <= 32) ? a.apw : 32;
+  // x3 fused step: 2 waves/SIMD whatever the register count (145 KB LDS per 8-wave workgroup),
+  // so the 64 bias registers are free
+  constexpr bool HOIST_EB = CTRL_HOIST_EB && X3 && GNODE;
+  f32x16 zb[4];
+  if constexpr (HOIST_EB) {
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      const float bv = eb2[32 * nt + r];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) zb[nt][q] = bv;
+    }
+  }
   for (int grp = grp0; grp * APW < total; grp += gstride) {
     const int g0 = grp * APW;
     const AgentBase ab = agent_base(g0, N);
@@ -375,7 +397,7 @@ DEV void ctrl_fwd_groups(const CtrlArgs& a, const h16* wl, const h16* wn, const 
       const bool m = ok && (sqrtf(sqsum<D>(cur.rp)) < a.obs_r);   // strict, un-eps'd (controller.py:38-39)
       const h16x8 F = ctrl_edge_frag<D>(cur.rp, cur.rv, eye, ok, h);
       f32x16 Z[4];
-      ctrl_edge_tile(F, wl + opaque_zero(), eb2, lane, Z);
+      ctrl_edge_tile(F, wl + opaque_zero(), eb2, lane, Z, HOIST_EB ? zb : nullptr);
       const unsigned mask32 = (unsigned)(__ballot(m) & 0xffffffffull);
       // Masked max-pool of relu(Z) over each agent's 16 rows with the first-occurrence argmax,
       // as ONE signed-int max per element: v = (bits(Z) & ~15) | c_row, c_row = 15 - slot for
