@@ -388,7 +388,11 @@ DEV void ctrl_fwd_groups(const CtrlArgs& a, const h16* wl, const h16* wn, const 
       ctrl_st_load<D>(a.S, a.s_env, xi0, xs0);
       ctrl_idx_load(a.idx, a.i_env, N, K, ab, 1, r, total, xi1);
     }
+#ifdef CTRL_X_TILES
+    for (int q = 0; q < min(APW / 2, CTRL_X_TILES); ++q) {     // ablation: fewer edge tiles (timing only)
+#else
     for (int q = 0; q < APW / 2; ++q) {
+#endif
       const EdgeSt<D> cur = xs0;
       ctrl_st_load<D>(a.S, a.s_env, xi1, xs0);                    // states of tile q+1
       ctrl_idx_load(a.idx, a.i_env, N, K, ab, q + 2, r, total, xi1);   // idx of tile q+2
