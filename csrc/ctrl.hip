@@ -214,12 +214,12 @@ DEV void ctrl_idx_load(const int* idx, long i_env, int N, int K, const AgentBase
 DEV int dense_agent(int e, unsigned invK) { return (int)(((unsigned)e * invK) >> 16); }
 
 DEV void ctrl_idx_load_dense(const int* idx, long i_env, int N, int K, unsigned invK, const AgentBase& ab, int q,
-                             int r, int total, EdgeIdx& o) {
+                             int r, int total, EdgeIdx& o, int nag = 32) {
   const int e = 32 * q + r;
   const int al = dense_agent(e, invK);
   const int slot = e - al * K;
   const int gi = ab.g0 + al;
-  o.ok = (q < K) && (gi < total);
+  o.ok = (al < nag) && (gi < total);
   o.b = 0; o.i = 0; o.j = 0;
   if (o.ok) {
     agent_bi(ab, al, N, o.b, o.i);
@@ -334,6 +334,101 @@ DEV void node_phase(const CtrlArgs& a, int g0, int APW, int total, PoolFr pool, 
   }
 }
 
+// DENSE12 emission target of one lane for one tile: the row pointers of a group agent (pooled
+// row [+ lo plane], argmax row; LDS pool row for the non-GPOOL path), computed once per tile
+struct PoolDst { h16* prow; uint8_t* arow; bool ok; };
+
+DEV PoolDst pool_dst(const CtrlArgs& a, const AgentBase& ab, int g0, int APW, int total, int al, h16* pool, bool gpool,
+                     int r) {
+  PoolDst d;
+  d.ok = al < APW && g0 + al < total;
+  d.prow = nullptr;
+  d.arow = nullptr;
+  if (d.ok) {
+    int bb, ii;
+    agent_bi(ab, al, a.N, bb, ii);
+    d.prow = gpool ? a.pooled + (long)bb * a.p_env + (long)ii * PROW + r : pool + al * PSTR + r;
+    if (a.argmax) d.arow = a.argmax + (long)bb * a.am_env + (long)ii * 128 + r;
+  }
+  return d;
+}
+
+template <bool IS_X3, bool GPOOL>
+DEV void pool_store(const PoolDst& d, int nt, int pw_) {
+  if (!d.ok) return;
+  const float pv = __int_as_float(pw_ & -16);
+  const h16 ph = (h16)pv;
+  d.prow[32 * nt] = ph;
+  if constexpr (IS_X3 && GPOOL) d.prow[32 * nt + 128] = (h16)(pv - (float)ph);
+#ifndef CTRL_X_NOARGMAX
+  if (d.arow) d.arow[32 * nt] = (pw_ > 15) ? (uint8_t)(15 - (pw_ & 15)) : (uint8_t)0xFF;
+#endif
+}
+
+// DENSE12 pool of edge tile q (see ctrl_fwd_groups): Z = relu-free pre-activations of the tile's
+// 32 edges (rows) x 128 features (4 column tiles), mask32 = in-radius rows
+template <bool IS_X3, bool GPOOL>
+DEV void pool_dense12(const CtrlArgs& a, const AgentBase& ab, int g0, int APW, int total, int q, unsigned mask32,
+                      const f32x16 (&Z)[4], int (&carry)[4], h16* pool, int lane) {
+  const int r = lane & 31, h = lane >> 5;
+  const int ph = (2 * q) % 3;                  // tile phase (uniform)
+  const int af = (8 * q) / 3;                  // first agent (group-relative) with rows in the tile
+  const bool three = ph != 0;                  // agents completed in this tile: 2 (ph 0) or 3
+  // this lane's emissions: half 0 the tile's 1st and 3rd completed agent, half 1 the 2nd
+  const PoolDst d1 = pool_dst(a, ab, g0, APW, total, af + h, pool, GPOOL, r);
+  const PoolDst d2 = pool_dst(a, ab, g0, APW, total, (h == 0 && three) ? af + 2 : APW, pool, GPOOL, r);
+  // slot code of every accumulator row: quad j = 2m + h holds slots 4 ((ph + j) mod 3) + i
+  int crow[16];
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    const int sq = 4 * ((ph + 2 * m + h) % 3);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int reg = 4 * m + i;
+      crow[reg] = ((mask32 >> acc_row(reg, h)) & 1u) ? (15 - (sq + i)) : INT_MIN;
+    }
+  }
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt) {
+    int g[4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      int v[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] = (__float_as_int(Z[nt][4 * m + i]) & -16) | crow[4 * m + i];
+      g[m] = max(max(max(0, v[0]), max(v[1], v[2])), v[3]);
+    }
+    int Q[8];                                  // quad maxima of the whole tile, in row order
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const int o = shfl_xor32i(g[m]);
+      Q[2 * m] = h ? o : g[m];
+      Q[2 * m + 1] = h ? g[m] : o;
+    }
+    // agents of the tile: ph 0: [0-2] [3-5] [6,7 -> carry]; ph 2: [carry, 0] [1-3] [4-6] [7 -> carry];
+    // ph 1: [carry, 0, 1] [2-4] [5-7]
+    int e0, e1, e2;
+    if (ph == 0) {
+      e0 = max(max(Q[0], Q[1]), Q[2]);
+      e1 = max(max(Q[3], Q[4]), Q[5]);
+      e2 = 0;
+      carry[nt] = max(Q[6], Q[7]);
+    } else if (ph == 2) {
+      e0 = max(carry[nt], Q[0]);
+      e1 = max(max(Q[1], Q[2]), Q[3]);
+      e2 = max(max(Q[4], Q[5]), Q[6]);
+      carry[nt] = Q[7];
+    } else {
+      e0 = max(max(carry[nt], Q[0]), Q[1]);
+      e1 = max(max(Q[2], Q[3]), Q[4]);
+      e2 = max(max(Q[5], Q[6]), Q[7]);
+      carry[nt] = 0;
+    }
+    pool_store<IS_X3, GPOOL>(d1, nt, h ? e1 : e0);
+    pool_store<IS_X3, GPOOL>(d2, nt, e2);
+  }
+}
+
 // Controller step. bf16 / fp16: edge and node phase in one kernel, the pooled features cross
 // from the edge lanes (features) to the node lanes (agents) through a per-wave LDS image.
 // x3: the split weights do not fit one workgroup's LDS together, so this kernel runs the edge
@@ -346,7 +441,18 @@ DEV void node_phase(const CtrlArgs& a, int g0, int APW, int total, PoolFr pool, 
 #ifndef CTRL_HOIST_EB
 #define CTRL_HOIST_EB 1
 #endif
-template <int D, bool SPLIT, bool GNODE = false>
+#ifndef CTRL_FWD_DENSE
+#define CTRL_FWD_DENSE 1
+#endif
+// DENSE12 (K = 12, agents per wave a multiple of 8): dense edge rows -- a group's APW agents x 12
+// slots are APW * 12 / 32 tiles of 32 consecutive edges (no padding slots). Rows come in quads of
+// 4 that never straddle an agent (12 = 3 quads); tile q covers quads j = 0..7 of agents
+// floor((8q + j) / 3), a pattern with period 3 tiles (8 agents): phase ph = 2q mod 3. The pool
+// takes the max per quad, exchanges quads across the lane halves, then per agent the max of its
+// quads (an agent that straddles two tiles carries its partial max in a register). Pooled values
+// and argmax slots are bit-identical to the 2-agent x 16-slot path (same per-edge MFMA values,
+// same slot codes and tie rule).
+template <int D, bool SPLIT, bool GNODE = false, bool DENSE12 = false>
 DEV void ctrl_fwd_groups(const CtrlArgs& a, const h16* wl, const h16* wn, const float* vl, h16* pools, int grp0,
                          int gstride) {
   constexpr bool GPOOL = X3 || SPLIT;
@@ -380,22 +486,29 @@ DEV void ctrl_fwd_groups(const CtrlArgs& a, const h16* wl, const h16* wn, const 
     const AgentBase ab = agent_base(g0, N);
     // ---------------- edge phase: 16 tiles x (2 agents x 16 slots); the gathers of tile q+1
     // (idx -> s_j, dependent global loads) are issued before tile q's MFMA chain
+    constexpr unsigned INV12 = (65536u + 11u) / 12u;
+    auto idx_load = [&](int q, EdgeIdx& o) {
+      if constexpr (DENSE12) ctrl_idx_load_dense(a.idx, a.i_env, N, 12, INV12, ab, q, r, total, o, APW);
+      else ctrl_idx_load(a.idx, a.i_env, N, K, ab, q, r, total, o);
+    };
+    const int NTL = DENSE12 ? APW * 12 / 32 : APW / 2;          // edge tiles of the group
+    int carry[4] = {0, 0, 0, 0};                                // DENSE12: straddling agent's partial pool
     EdgeIdx xi1;
     EdgeSt<D> xs0;
     {
       EdgeIdx xi0;
-      ctrl_idx_load(a.idx, a.i_env, N, K, ab, 0, r, total, xi0);
+      idx_load(0, xi0);
       ctrl_st_load<D>(a.S, a.s_env, xi0, xs0);
-      ctrl_idx_load(a.idx, a.i_env, N, K, ab, 1, r, total, xi1);
+      idx_load(1, xi1);
     }
 #ifdef CTRL_X_TILES
-    for (int q = 0; q < min(APW / 2, CTRL_X_TILES); ++q) {     // ablation: fewer edge tiles (timing only)
+    for (int q = 0; q < min(NTL, CTRL_X_TILES); ++q) {     // ablation: fewer edge tiles (timing only)
 #else
-    for (int q = 0; q < APW / 2; ++q) {
+    for (int q = 0; q < NTL; ++q) {
 #endif
       const EdgeSt<D> cur = xs0;
       ctrl_st_load<D>(a.S, a.s_env, xi1, xs0);                    // states of tile q+1
-      ctrl_idx_load(a.idx, a.i_env, N, K, ab, q + 2, r, total, xi1);   // idx of tile q+2
+      idx_load(q + 2, xi1);                                        // idx of tile q+2
       const bool ok = cur.ok;
       const float eye = (cur.j == cur.i) ? 1.f : 0.f;
       const bool m = ok && (sqrtf(sqsum<D>(cur.rp)) < a.obs_r);   // strict, un-eps'd (controller.py:38-39)
@@ -403,6 +516,10 @@ DEV void ctrl_fwd_groups(const CtrlArgs& a, const h16* wl, const h16* wn, const 
       f32x16 Z[4];
       ctrl_edge_tile(F, wl + opaque_zero(), eb2, lane, Z, HOIST_EB ? zb : nullptr);
       const unsigned mask32 = (unsigned)(__ballot(m) & 0xffffffffull);
+      if constexpr (DENSE12) {
+        pool_dense12<X3, GPOOL>(a, ab, g0, APW, total, q, mask32, Z, carry, pool, lane);
+        continue;
+      }
       // Masked max-pool of relu(Z) over each agent's 16 rows with the first-occurrence argmax,
       // as ONE signed-int max per element: v = (bits(Z) & ~15) | c_row, c_row = 15 - slot for
       // in-radius rows and INT_MIN for masked ones. Non-negative floats order as ints, so the
@@ -502,7 +619,11 @@ __global__ __launch_bounds__(WAVES * 64) void ctrl_fwd_kernel(CtrlArgs a) {
   if constexpr (!X3 || FUSE) block_copy16(wn, a.wpack + (size_t)a.f_node * FRAG_ELEMS, 54 * FRAG_SZ);
   block_copy16(vl, a.wvec, CTRL_VEC * 4);
   __syncthreads();
-  ctrl_fwd_groups<D, false, FUSE>(a, wl, wn, vl, pools, blockIdx.x * WAVES + threadIdx.x / WAVE, gridDim.x * WAVES);
+  const int apw = (a.apw >= 2 && a.apw <= 32) ? a.apw : 32;
+  if (CTRL_FWD_DENSE && a.K == 12 && apw % 8 == 0)
+    ctrl_fwd_groups<D, false, FUSE, true>(a, wl, wn, vl, pools, blockIdx.x * WAVES + threadIdx.x / WAVE, gridDim.x * WAVES);
+  else
+    ctrl_fwd_groups<D, false, FUSE>(a, wl, wn, vl, pools, blockIdx.x * WAVES + threadIdx.x / WAVE, gridDim.x * WAVES);
 }
 
 // Node phase of the controller step over the pooled rows in global memory, 32-agent groups

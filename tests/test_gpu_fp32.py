@@ -369,3 +369,36 @@ def test_training_parity_fp32_vs_oracle():
         assert abs(a - b) <= 1e-3 * abs(b), (it, a, b)
     d = float((hip.fp.flat.double() - orc.fp.flat.double()).norm() / orc.fp.flat.double().norm())
     assert d <= 1e-3, d
+
+
+@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+@pytest.mark.parametrize("B,N", [(3, 200), (2, 1024), (1, 40)])
+def test_ctrl_fwd_dense_rows_bitwise(B, N, prec, monkeypatch):
+    """K = 12: the dense-row edge phase (32 agents x 12 slots = 12 tiles, agents straddling tiles,
+    used when the agents per wave are a multiple of 8) gives bit-identical actions, next states,
+    pooled rows, argmax slots and per-env sums to the 2-agent x 16-slot path (apw = 4)."""
+    import os
+    ctrl, cbf, fp, _ = _nets(5)
+    pw = PackedWeights(fp, dtype=torch.float32 if prec == "fp32" else torch.bfloat16)
+    s = _states((B,), N, seed=2, dens=0.8)
+    g = (s[..., :2] + (torch.rand(B, N, 2, device=DEV) - 0.5)).contiguous()
+    idx = O.knn_idx(s, C.TOP_K).to(torch.int32).contiguous()
+    prow = 256 if prec == "fp32" else 128
+    out = {}
+    for apw in ("32", "8", "4"):
+        monkeypatch.setenv("MACBF_CTRL_APW", apw)
+        A = torch.full((B, N, 2), 7.0, device=DEV)
+        Sn = torch.full((B, N, 4), 7.0, device=DEV)
+        pooled = torch.zeros(B, N, prow, dtype=torch.bfloat16, device=DEV)
+        am = torch.full((B, N, 128), 77, dtype=torch.uint8, device=DEV)
+        ds = torch.zeros(B, dtype=torch.int64, device=DEV)
+        acs = torch.zeros(B, dtype=torch.int64, device=DEV)
+        native.ctrl_fwd(s, g, idx, pw.ctrl_w, pw.ctrl_off["ew1f"], pw.ctrl_off["nw1f"], pw.ctrl_v, A, Sn, ds, acs,
+                        pooled=pooled, argmax=am, prec=prec)
+        torch.cuda.synchronize()
+        out[apw] = (A, Sn, pooled, am, ds, acs)
+    assert os.environ["MACBF_CTRL_APW"] == "4"
+    for apw in ("32", "8"):
+        for x, y, name in zip(out[apw], out["4"], ("A", "Sn", "pooled", "argmax", "dist", "act")):
+            assert torch.equal(x, y), (apw, name)
+    assert int((out["4"][3] != 255).sum()) > 0
