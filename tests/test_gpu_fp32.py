@@ -402,3 +402,33 @@ def test_ctrl_fwd_dense_rows_bitwise(B, N, prec, monkeypatch):
         for x, y, name in zip(out[apw], out["4"], ("A", "Sn", "pooled", "argmax", "dist", "act")):
             assert torch.equal(x, y), (apw, name)
     assert int((out["4"][3] != 255).sum()) > 0
+
+
+@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+def test_ctrl_fwd_dense_rows_bitwise_3d_obstacles(prec, monkeypatch):
+    """The dense-row controller step with 3-D states and obstacle nodes (config #5 layout)."""
+    from macbf_gnn_amd import env as E
+    from macbf_gnn_amd.ops import graph
+    ctrl, cbf, fp, _ = _nets(6, dim=3)
+    pw = PackedWeights(fp, 3, torch.float32 if prec == "fp32" else torch.bfloat16)
+    B, N = 2, 256
+    s, g, obs = E.generate_scenarios(B, N, dim=3, num_obstacles=3, seed=4)
+    gen = torch.Generator().manual_seed(4)
+    s[..., 3:] = (torch.rand(B, N, 3, generator=gen) - 0.5) * 1.2
+    s, g, obs = s.to(DEV), g.to(DEV).contiguous(), obs.to(DEV)
+    S = graph.node_records(s, obs)
+    idx = O.knn_idx(s, C.TOP_K, O.with_obstacles(s, obs)).to(torch.int32).contiguous()
+    prow = 256 if prec == "fp32" else 128
+    out = {}
+    for apw in ("32", "4"):
+        monkeypatch.setenv("MACBF_CTRL_APW", apw)
+        A = torch.full((B, N, 3), 7.0, device=DEV)
+        Sn = S.clone()
+        pooled = torch.zeros(B, N, prow, dtype=torch.bfloat16, device=DEV)
+        am = torch.full((B, N, 128), 77, dtype=torch.uint8, device=DEV)
+        native.ctrl_fwd(S, g, idx, pw.ctrl_w, pw.ctrl_off["ew1f"], pw.ctrl_off["nw1f"], pw.ctrl_v, A, Sn, None, None,
+                        pooled=pooled, argmax=am, prec=prec)
+        torch.cuda.synchronize()
+        out[apw] = (A, Sn, pooled, am)
+    for x, y, name in zip(out["32"], out["4"], ("A", "Sn", "pooled", "argmax")):
+        assert torch.equal(x, y), name
