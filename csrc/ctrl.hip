@@ -484,7 +484,8 @@ DEV void ctrl_fwd_groups(const CtrlArgs& a, const h16* wl, const h16* wn, const 
   for (int grp = grp0; grp * APW < total; grp += gstride) {
     const int g0 = grp * APW;
     const AgentBase ab = agent_base(g0, N);
-    // ---------------- edge phase: 16 tiles x (2 agents x 16 slots); the gathers of tile q+1
+    // ---------------- edge phase: APW/2 tiles x (2 agents x 16 slots), or APW*12/32 dense tiles
+    // (DENSE12); the gathers of tile q+1
     // (idx -> s_j, dependent global loads) are issued before tile q's MFMA chain
     constexpr unsigned INV12 = (65536u + 11u) / 12u;
     auto idx_load = [&](int q, EdgeIdx& o) {
@@ -1245,7 +1246,7 @@ DEV void edge_bwd_body(const CtrlEdgeBwdArgs& a, unsigned char* smem, long w0, l
   for (int u = 0; u < EB_TA; ++u) { accW2[u] = zero16(); bs[u] = 0.f; }
   const h16 z = (h16)0.f;
 
-  // work item = (chunk, tile range): small scenes split a chunk's 16 tile rounds over
+  // work item = (chunk, tile range): small scenes split a chunk's NT tile rounds over
   // qsplit workgroups (tiles are independent; every workgroup owns its dW slab), large ones
   // use qsplit = 1
   const int QP = a.qsplit > 1 ? a.qsplit : 1;
@@ -1270,9 +1271,9 @@ DEV void edge_bwd_body(const CtrlEdgeBwdArgs& a, unsigned char* smem, long w0, l
       ctrl_st_load<D>(a.S, a.s_env, xi0, xs0);
       idx_load(ab, q0 + 1, xi1);
     }
-    // argmax slots / dL/dpooled of the tile's two agents (lane (r, h): agent 2q+h, features
-    // 4r..4r+3): loaded one tile ahead, like the edge gathers
-    // dense rows: tile q holds agents af(q) .. (32q + 31) / K; pass p of a tile = agents
+    // argmax slots / dL/dpooled of a tile's agents (lane (r, h): features 4r..4r+3 of one
+    // agent per pass), loaded one tile ahead like the edge gathers. 16-slot rows: tile q = agents
+    // 2q + h, one pass; dense rows: tile q holds agents af(q) .. (32q + 31) / K, pass p = agents
     // af + 2p + h (lane half h), two passes prefetched (all of a tile's agents for K >= 11)
     auto pool_load_ag = [&](int al, unsigned& am4, h16x4& dp4, h16x4& dl4) {
       const int ag = g0 + al;
@@ -1335,10 +1336,10 @@ DEV void edge_bwd_body(const CtrlEdgeBwdArgs& a, unsigned char* smem, long w0, l
         relu_(c);
         H1b[mt] = to_pk(c);
       }
-      // max-pool backward as an LDS scatter into the S1 image (rows = this wave's 32 edges =
-      // agents 2q, 2q+1 x 16 slots): zero the rows, then lane (r, h) routes dP[f] of agent 2q+h,
-      // f = 4r..4r+3, to row (h, argmax slot). One coalesced argmax/dP load per lane instead of
-      // 16 redundant row loads + 64 compare/selects per edge lane.
+      // max-pool backward as an LDS scatter into the S1 image (rows = this wave's 32 edges of the
+      // tile): zero the rows, then lane (r, h) routes dP[f] of its pass agent, f = 4r..4r+3, to
+      // the row of (agent, argmax slot) when that row lies in the tile. One coalesced argmax/dP
+      // load per lane and pass instead of redundant row loads + compare/selects per edge lane.
       h16* imS = stg;                                           // S1 dZ image (128 wide, swizzled)
       {
         const u32x4 zero4 = {0u, 0u, 0u, 0u};
