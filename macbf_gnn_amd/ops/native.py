@@ -717,9 +717,10 @@ CTRL_EDGE_WAVES = 4          # csrc/ctrl.hip EB_WAVES
 
 
 def ctrl_edge_qsplit(total_agents: int, device) -> int:
-    """Workgroups per 128-agent chunk of the edge backward: small scenes split a chunk's 16 tile
-    rounds over up to 16 workgroups (the tiles are independent; a single wave would otherwise
-    run all of them back to back); 1 once the chunks alone fill the GPU."""
+    """Workgroups per 128-agent chunk of the edge backward: small scenes split a chunk's tile
+    rounds (K of them with the dense edge rows, csrc/ctrl.hip) over up to 16 workgroups (the tiles
+    are independent; a single wave would otherwise run all of them back to back; a part with no
+    tile writes a zero slab row); 1 once the chunks alone fill the GPU."""
     che = (total_agents + 32 * CTRL_EDGE_WAVES - 1) // (32 * CTRL_EDGE_WAVES)
     cap = (8 // CTRL_EDGE_WAVES) * num_cu(device)
     p = 1
