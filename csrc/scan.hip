@@ -436,25 +436,34 @@ __global__ __launch_bounds__(BS) void scan_kernel(ScanArgs a) {
   }
   const bool own = act && h == 0;                              // one lane reports per agent
   float ndang = 0.f, nsafe_e = 0.f, safe_ag = 0.f;
-  if (own && a.do_knn) {
+  if (act && a.do_knn) {
+    // every lane of the agent holds the merged list: lane h writes slots h, h + LPA, ... and
+    // their train-threshold danger bits (the per-env counts are sums of 0/1: order-free)
     int* out = a.idx + (long)b * a.i_env + (long)i * K;
     uint8_t* dout = a.dang ? a.dang + (long)b * a.i_env + (long)i * K : nullptr;
     float pi[D], vi[D];
     load_rec<D>(Sb, (unsigned)i, pi, vi);
 #pragma unroll
-    for (int q = 0; q < K; ++q) {
-      const int j = (int)(unsigned)bk[q];
-      out[q] = j;
-      float pj[D], vj[D], dp[D], dv[D];
-      load_rec<D>(Sb, (unsigned)j, pj, vj);
-      const float eye = (j == i) ? 1.f : 0.f;
+    for (int q0 = 0; q0 < K; q0 += LPA) {
+      const int q = q0 + h;
+      if (q < K) {
+        uint64_t key = bk[q0];                   // bk[q] (register array: selects on h)
 #pragma unroll
-      for (int d = 0; d < D; ++d) { dp[d] = (pi[d] - pj[d]) + eye; dv[d] = vi[d] - vj[d]; }
-      const bool dg = ttc_danger<D>(dp, dv, a.r2_train, a.ttc_train);
-      if (dout) dout[q] = dg ? 1 : 0;
-      ndang += dg ? 1.f : 0.f;
+        for (int u = 1; u < LPA; ++u)
+          if (q0 + u < K) key = (h == u) ? bk[q0 + u] : key;
+        const int j = (int)(unsigned)key;
+        out[q] = j;
+        float pj[D], vj[D], dp[D], dv[D];
+        load_rec<D>(Sb, (unsigned)j, pj, vj);
+        const float eye = (j == i) ? 1.f : 0.f;
+#pragma unroll
+        for (int d = 0; d < D; ++d) { dp[d] = (pi[d] - pj[d]) + eye; dv[d] = vi[d] - vj[d]; }
+        const bool dg = ttc_danger<D>(dp, dv, a.r2_train, a.ttc_train);
+        if (dout) dout[q] = dg ? 1 : 0;
+        ndang += dg ? 1.f : 0.f;
+        nsafe_e += dg ? 0.f : 1.f;
+      }
     }
-    nsafe_e = (float)K - ndang;
   }
   if (own && a.do_safety) safe_ag = danger ? 0.f : 1.f;
   ndang = wave_sum(ndang);
