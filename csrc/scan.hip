@@ -486,9 +486,8 @@ __global__ __launch_bounds__(BS) void scan_kernel(ScanArgs a) {
 #define SCAN_LPA 4      // lanes per agent (A/B at 1024 x 64: 2 -> 4 lanes 65.4 -> 61.5 us per step)
 #endif
 
-template <int K, int D, int BS>
+template <int K, int D, int BS, int LPA = SCAN_LPA>
 static void launch_kdb(const ScanArgs& a, hipStream_t st) {
-  constexpr int LPA = SCAN_LPA;
   dim3 grid((a.Nn + BS / LPA - 1) / (BS / LPA), a.B);
   if (a.Nn > SCAN_MAXN) {
     const int Np = (a.Nn + SCH - 1) / SCH * SCH, nch = Np / SCH, nsc = (nch + SSC - 1) / SSC;
@@ -508,24 +507,40 @@ static void launch_kdb(const ScanArgs& a, hipStream_t st) {
 #define SCAN_BS_BIG 1024  // block size above 512 nodes per env (4 lanes/agent: 512 -> 1024, 61.5 -> 60.5 us)
 #endif
 
+static int scan_num_cu() {
+  static const int cus = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) v = 256;
+    return v;
+  }();
+  return cus;
+}
+
 // Small scans (a strong-scaling slice: few envs) would fill only some CUs with big blocks: use
 // 256-thread blocks whenever the big-block grid has fewer blocks than CUs (MACBF_SCAN_SMALL=0/1
 // forces the choice for A/B runs).
 static bool scan_small_grid(const ScanArgs& a) {
   static const int force = [] { const char* e = getenv("MACBF_SCAN_SMALL"); return e ? atoi(e) : -1; }();
   if (force >= 0) return force != 0;
-  static const int cus = [] {
-    int dev = 0, v = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) v = 256;
-    return v;
-  }();
   constexpr int AG = SCAN_BS_BIG / SCAN_LPA;      // agents per big block
-  return (long)a.B * ((a.Nn + AG - 1) / AG) < cus;
+  return (long)a.B * ((a.Nn + AG - 1) / AG) < scan_num_cu();
+}
+
+// Still fewer 256-thread blocks than CUs (e.g. 8 envs x 1024 nodes: 128 blocks): 8 lanes per
+// agent (one candidate of every chunk per lane) halve the agents per block and the per-lane
+// chunk work -> twice the blocks (MACBF_SCAN_LPA8=0/1 forces the choice for A/B runs).
+// Same keys and tie order: the merged lists are identical for any LPA.
+static bool scan_lpa8(const ScanArgs& a) {
+  static const int force = [] { const char* e = getenv("MACBF_SCAN_LPA8"); return e ? atoi(e) : -1; }();
+  if (force >= 0) return force != 0;
+  constexpr int AG = 256 / SCAN_LPA;
+  return SCAN_LPA < 8 && (long)a.B * ((a.Nn + AG - 1) / AG) < scan_num_cu();
 }
 
 template <int K, int D>
 static void launch_kd(const ScanArgs& a, hipStream_t st) {
   if (a.Nn > 512 && !scan_small_grid(a)) launch_kdb<K, D, SCAN_BS_BIG>(a, st);
+  else if (scan_lpa8(a)) launch_kdb<K, D, 256, 8>(a, st);
   else launch_kdb<K, D, 256>(a, st);
 }
 

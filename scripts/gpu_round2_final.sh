@@ -2,7 +2,7 @@
 #   full GPU suite -> smoke() -> headline bench (default flags, fp32) -> bf16 bench ->
 #   rocprofv3 kernel stats -> 2-rank gloo rehearsal of the torchrun bench -> 1-rank RCCL torchrun bench
 cd $GRAFT_REPO_ROOT
-O=gpurun_out/r2_final_b
+O=${O:-gpurun_out/r2_final_b}
 mkdir -p $O
 timeout -k 10 900 python -u -m pytest tests -x -q -m gpu -p no:cacheprovider --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1
 rc=$?; tail -2 $O/gpu_tests.log; [ $rc -eq 0 ] || exit $rc
