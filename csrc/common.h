@@ -121,11 +121,32 @@ DEV void lds_wave_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 // (8 independent 16-byte loads in flight per thread before the stores: the weight staging at
 // kernel start is latency-bound, which dominates small launches -- a 120 KB x3 image is 30
 // loads per thread of a 256-thread block)
+// MB_GLDS_COPY (default): LDS-DMA instead -- every wave issues all of its 16-byte
+// global_load_lds_dwordx4 copies back to back (no VGPR staging, one latency round trip for the
+// whole image instead of one per 8 loads), then waits for them before the caller's barrier.
+// The destination of one wave instruction is its wave-uniform base + lane x 16: a lane-linear
+// image, which a plain copy is. Callers pass LDS destinations and global sources.
+#ifndef MB_GLDS_COPY
+#define MB_GLDS_COPY 1
+#endif
 DEV void block_copy16(void* dst, const void* src, int bytes) {
   const u32x4* s = reinterpret_cast<const u32x4*>(src);
   u32x4* d = reinterpret_cast<u32x4*>(dst);
   const int n = bytes / 16, bd = blockDim.x;
   int i = threadIdx.x;
+#if MB_GLDS_COPY
+  {
+    const int lane = threadIdx.x & 63;
+    for (; i - lane < n; i += bd) {       // wave-uniform trip count (the wave's first index)
+      if (i < n)
+        __builtin_amdgcn_global_load_lds(
+            (const __attribute__((address_space(1))) void*)(s + i),
+            (__attribute__((address_space(3))) void*)(d + (i - lane)), 16, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    return;
+  }
+#endif
   for (; i + 7 * bd < n; i += 8 * bd) {
     u32x4 v[8];
 #pragma unroll
