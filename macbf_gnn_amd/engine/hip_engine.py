@@ -166,12 +166,12 @@ class HipEngine:
         # exploration noise (reference train.py:65-67): counter-based device RNG keyed per iteration
         self.noise_key = torch.zeros(1, dtype=torch.int64, device=dev)
         self.small_ctl = torch.zeros(2, dtype=i32, device=dev)     # persistent rollout: [envs done, max step]
-        self.nb_node, self.nb_edge = native.ctrl_bwd_grids(B * N, dev)
+        self.nb_node, self.nb_edge = native.ctrl_bwd_grids(B * N, dev, self.prec)
         # BPTT env groups (independent chains on separate streams): per-group grids and slab rows
         Gp = self.bptt_groups
         if Gp < 1 or B % Gp:
             raise ValueError(f"bptt_groups={Gp} must divide num_envs={B}")
-        self.grp_nb = native.ctrl_bwd_grids((B // Gp) * N, dev)
+        self.grp_nb = native.ctrl_bwd_grids((B // Gp) * N, dev, self.prec)
         rows_n = max(self.nb_node, Gp * self.grp_nb[0])
         rows_e = max(self.nb_edge, Gp * self.grp_nb[1])
         # slab rows written by the launch-per-step BPTT / by the persistent one (one row per env)
@@ -668,7 +668,7 @@ class HipEngine:
         """(T*B)-batched buffers for the no-BPTT controller backward (sized for Tmax)."""
         if "dP" not in self._nobptt:
             TBm = self.Tmax * self.B
-            nb_n, nb_e = native.ctrl_bwd_grids(TBm * self.N, self.dev)
+            nb_n, nb_e = native.ctrl_bwd_grids(TBm * self.N, self.dev, self.prec)
             self._nobptt = {
                 "grids": (nb_n, nb_e),
                 "G": torch.zeros(TBm, self.N, self.D, dtype=torch.float32, device=self.dev),

@@ -50,7 +50,7 @@ class _CtrlFn(torch.autograd.Function):
         D = mp.dim
         dev = S.device
         Gn = native.to_records(torch.cat([torch.zeros(B, N, D, device=dev), gA.float() / C.TIME_STEP], -1))
-        nbn, nbe = native.ctrl_bwd_grids(B * N, dev)
+        nbn, nbe = native.ctrl_bwd_grids(B * N, dev, mp.prec)
         # one step: the kernels write their slabs (init) instead of accumulating
         pn = torch.empty(nbn, native.CTRL_NODE_PARTIAL, dtype=torch.float32, device=dev)
         pe = torch.empty(nbe, native.CTRL_EDGE_PARTIAL, dtype=torch.float32, device=dev)

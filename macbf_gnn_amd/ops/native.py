@@ -743,15 +743,20 @@ def node_bwd_chunk(total_agents: int, device) -> int:
     return 32
 
 
-def ctrl_bwd_grids(total_agents: int, device):
+def ctrl_bwd_grids(total_agents: int, device, prec=None):
     """(node, edge) backward grids: the node kernel takes node_bwd_chunk-agent chunks, one
     workgroup per CU; the edge kernel 32*CTRL_EDGE_WAVES-agent chunks x ctrl_edge_qsplit tile
-    ranges (4 waves: two workgroups per CU)."""
+    ranges, at most as many workgroups as fit the CUs at once (4 waves: two per CU in the 16-bit
+    builds; one in the fp32 (x3) build -- 322 registers, 118 KB of LDS: a grid of one per CU
+    loops over two chunks instead of running a second round of workgroups, 142 -> 137 us per
+    call at 1024 x 64, profiles/r2_egrid/). MACBF_EDGE_WG_PER_CU overrides the cap."""
     ca = node_bwd_chunk(total_agents, device)
     ch = (total_agents + ca - 1) // ca
     che = (total_agents + 32 * CTRL_EDGE_WAVES - 1) // (32 * CTRL_EDGE_WAVES)
     cu = num_cu(device)
-    return max(1, min(ch, cu)), max(1, min(che * ctrl_edge_qsplit(total_agents, device), (8 // CTRL_EDGE_WAVES) * cu))
+    per_cu = 1 if prec == "fp32" else 8 // CTRL_EDGE_WAVES
+    per_cu = int(os.environ.get("MACBF_EDGE_WG_PER_CU", per_cu))
+    return max(1, min(ch, cu)), max(1, min(che * ctrl_edge_qsplit(total_agents, device), per_cu * cu))
 
 
 def ctrl_node_bwd(pooled, S, G, A, Gn, valid_t, wrm, offs, wvec, act_coef, dP, ego, partial, num_blocks,
