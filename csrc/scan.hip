@@ -531,6 +531,7 @@ static bool scan_small_grid(const ScanArgs& a) {
 // chunk work -> twice the blocks (MACBF_SCAN_LPA8=0/1 forces the choice for A/B runs).
 // Same keys and tie order: the merged lists are identical for any LPA.
 static bool scan_lpa8(const ScanArgs& a) {
+  if (a.lanes == 4 || a.lanes == 8) return a.lanes == 8;
   static const int force = [] { const char* e = getenv("MACBF_SCAN_LPA8"); return e ? atoi(e) : -1; }();
   if (force >= 0) return force != 0;
   constexpr int AG = 256 / SCAN_LPA;
@@ -539,8 +540,8 @@ static bool scan_lpa8(const ScanArgs& a) {
 
 template <int K, int D>
 static void launch_kd(const ScanArgs& a, hipStream_t st) {
-  if (a.Nn > 512 && !scan_small_grid(a)) launch_kdb<K, D, SCAN_BS_BIG>(a, st);
-  else if (scan_lpa8(a)) launch_kdb<K, D, 256, 8>(a, st);
+  if (scan_lpa8(a)) launch_kdb<K, D, 256, 8>(a, st);
+  else if (a.Nn > 512 && !scan_small_grid(a)) launch_kdb<K, D, SCAN_BS_BIG>(a, st);
   else launch_kdb<K, D, 256>(a, st);
 }
 

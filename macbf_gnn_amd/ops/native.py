@@ -201,7 +201,7 @@ def _perm_buf(B, N, device):
 
 
 def scan(S, idx, dang, cnt, safe, *, K, do_knn=True, do_safety=True, perm=None, n_agents=None, prev_idx=None,
-         sort=True):
+         sort=True, lanes=0):
     """K1 over one timestep. S: (B, N, 4) view with env stride (may be a slice of a (B,T+1,N,4)
     buffer); idx/dang: (B, N, K) views; cnt: (B, 2) view; safe: (B,) view.
 
@@ -210,7 +210,11 @@ def scan(S, idx, dang, cnt, safe, *, K, do_knn=True, do_safety=True, perm=None, 
     wave-divergent top-K insertion rare). prev_idx (B, N, K): the previous step's kNN of the same
     agents; their current distances bound the K-th distance (tighter culling, same result).
     sort=False reuses the curve order of the previous call on the same perm buffer (the agents
-    moved one step: slightly looser culling, identical results)."""
+    moved one step: slightly looser culling, identical results). lanes: lanes per agent (0: by
+    grid size -- 8 when 4-lane 256-thread blocks leave CUs idle; 4 or 8 forces the layout; the
+    lists, bits and counts are identical for either)."""
+    if lanes not in (0, 4, 8):
+        raise NativeError("lanes must be 0 (auto), 4 or 8")
     B, Nn = S.shape[0], S.shape[1]
     D = dim_of(S)
     W = rec_width(D)
@@ -253,7 +257,8 @@ def scan(S, idx, dang, cnt, safe, *, K, do_knn=True, do_safety=True, perm=None, 
                     float(C.DIST_MIN_THRES * C.DIST_MIN_THRES), float(C.TIME_TO_COLLISION),
                     float(C.DIST_MIN_CHECK * C.DIST_MIN_CHECK), float(C.TIME_TO_COLLISION_CHECK),
                     int(do_knn), int(do_safety), Nn, D, ptr(prev_idx),
-                    prev_idx.stride(0) if prev_idx is not None else 0, ptr(ws), int(ws_f4), stream_handle())
+                    prev_idx.stride(0) if prev_idx is not None else 0, ptr(ws), int(ws_f4), int(lanes),
+                    stream_handle())
     _ok(rc, "scan")
 
 

@@ -33,15 +33,27 @@ def _nets(seed=0):
     return ctrl, cbf, fp, PackedWeights(fp)
 
 
+@pytest.mark.parametrize("lanes", [4, 8])
 @pytest.mark.parametrize("B,N", [(2, 8), (3, 13), (2, 64), (1, 1100)])
-def test_scan_knn_ttc_safety(B, N):
+def test_scan_knn_ttc_safety(B, N, lanes):
+    _scan_vs_oracle(B, N, lanes)
+
+
+@pytest.mark.parametrize("lanes", [0, 8])
+def test_scan_headline_grid(lanes):
+    """64 envs x 1024 agents: the 1,024-thread-block scan (lanes=0 picks it at this size) and
+    the 8-lane 256-thread layout give the oracle's lists, bits, counts and safety."""
+    _scan_vs_oracle(64, 1024, lanes)
+
+
+def _scan_vs_oracle(B, N, lanes):
     s, _ = _states(B, N, seed=N)
     K = min(N, C.TOP_K)
     idx = torch.empty(B, N, K, dtype=torch.int32, device=DEV)
     dang = torch.empty(B, N, K, dtype=torch.uint8, device=DEV)
     cnt = torch.zeros(B, 2, dtype=torch.float32, device=DEV)
     safe = torch.zeros(B, dtype=torch.float32, device=DEV)
-    native.scan(s, idx, dang, cnt, safe, K=K)
+    native.scan(s, idx, dang, cnt, safe, K=K, lanes=lanes)
     torch.cuda.synchronize()
     ref = O.knn_idx(s, K)
     assert torch.equal(idx.long(), ref)
@@ -52,9 +64,10 @@ def test_scan_knn_ttc_safety(B, N):
     assert torch.equal(safe, O.safe_agent_count(s).float())
 
 
+@pytest.mark.parametrize("lanes", [4, 8])
 @pytest.mark.parametrize("resort", [True, False])
 @pytest.mark.parametrize("B,N,steps", [(2, 13, 3), (2, 300, 4), (1, 1100, 3), (1, 4096, 2)])
-def test_scan_temporal_bound_is_exact(B, N, steps, resort):
+def test_scan_temporal_bound_is_exact(B, N, steps, resort, lanes):
     """prev_idx (the previous step's kNN) only tightens the culling: kNN, danger bits, counts
     and safety equal the oracle on moving states, step after step. resort=False keeps the
     first step's Hilbert order (stale curve order: looser culling, identical results)."""
@@ -66,7 +79,7 @@ def test_scan_temporal_bound_is_exact(B, N, steps, resort):
         dang = torch.empty(B, N, K, dtype=torch.uint8, device=DEV)
         cnt = torch.zeros(B, 2, dtype=torch.float32, device=DEV)
         safe = torch.zeros(B, dtype=torch.float32, device=DEV)
-        native.scan(s, idx, dang, cnt, safe, K=K, prev_idx=prev, sort=resort or step == 0)
+        native.scan(s, idx, dang, cnt, safe, K=K, prev_idx=prev, sort=resort or step == 0, lanes=lanes)
         torch.cuda.synchronize()
         ref = O.knn_idx(s, K)
         assert torch.equal(idx.long(), ref)
