@@ -77,6 +77,12 @@ struct CtrlArgs {
   uint8_t* argmax;  long am_env;      // (b,i,128) winning slot per feature (0xFF: no grad), or null
   int apw;                            // agents per wave (even, 2..32; 0 = 32): small scenes use fewer
   int b0, nb_total;                   // env offset / total envs of a per-env view (noise keys; 0, 0 = this view)
+  // early-stop publication (native rollout driver; null = off): the step's last workgroup copies
+  // the B per-env dist_sum values to host-coherent pub_dist and then stores pub_gen to *pub_flag
+  unsigned* pub_ctr;                  // this step's workgroup counter (zeroed before the rollout)
+  unsigned long long* pub_dist;       // host-coherent (B) slots of this step
+  unsigned* pub_flag;                 // host-coherent flag of this step
+  unsigned pub_gen;                   // the rollout's generation number
 };
 
 // Persistent small-scene rollout (ctrl.hip rollout_small_kernel): one workgroup per env runs

@@ -16,7 +16,9 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
+#include <cstring>
 #include <stdexcept>
 #include <vector>
 
@@ -65,6 +67,16 @@ class RolloutDriver {
     apw_ = (int)I("apw");
     small_ctl_ = U("small_ctl"); small_apw_ = (int)I("small_apw"); knn_tail_ = (int)I("knn_tail");
     if (small_ctl_) chk(hipHostMalloc((void**)&host_ctl_, 2 * sizeof(int), hipHostMallocDefault), "hipHostMalloc");
+    // early-stop publication (ctrl.hip publish_step): per-step workgroup counters on the device,
+    // the per-env sums and a flag per step in host-coherent memory
+    publish_ = c.contains("publish") ? (int)I("publish") : 0;
+    if (publish_) {
+      const size_t nd = (size_t)Tmax_ * B_, bytes = nd * sizeof(unsigned long long) + (size_t)Tmax_ * sizeof(unsigned);
+      chk(hipHostMalloc((void**)&pub_host_, bytes, hipHostMallocMapped | hipHostMallocCoherent), "hipHostMalloc");
+      std::memset(pub_host_, 0, bytes);
+      chk(hipHostGetDevicePointer((void**)&pub_dev_, pub_host_, 0), "hipHostGetDevicePointer");
+      chk(hipMalloc((void**)&pub_ctr_, (size_t)Tmax_ * sizeof(unsigned)), "hipMalloc");
+    }
     if (check_ < 1) check_ = 1;
     if (B_ < 1|| N_ < 1 || Nn_ < N_ || K_ < 1 || K_ > 16 || (D_ != 2 && D_ != 3) || Tmax_ < 1 || resort_ < 1)
       throw std::invalid_argument("RolloutDriver: bad dimensions");
@@ -82,6 +94,8 @@ class RolloutDriver {
     (void)hipEventDestroy(ev_main_);
     (void)hipEventDestroy(ev_side_);
     if (host_ctl_) (void)hipHostFree(host_ctl_);
+    if (pub_host_) (void)hipHostFree(pub_host_);
+    if (pub_ctr_) (void)hipFree(pub_ctr_);
   }
   RolloutDriver(const RolloutDriver&) = delete;
   RolloutDriver& operator=(const RolloutDriver&) = delete;
@@ -93,12 +107,19 @@ class RolloutDriver {
     const volatile unsigned long long* hd = P<const volatile unsigned long long>(host_dist_);
     int T = Tmax_;
     bool tail = false;
+    // published early stop: the controller kernels hand the per-env sums to the host (no marker)
+    const bool pub = publish_ && early_stop;
+    if (pub) {
+      ++gen_;
+      chk(hipMemsetAsync(pub_ctr_, 0, (size_t)Tmax_ * sizeof(unsigned), st), "hipMemsetAsync");
+      hd = pub_host_;
+    }
     for (int t = 0; t < Tmax_; ++t) {
       scan_step(t, st);
-      ctrl_step(t, st);
+      ctrl_step(t, st, pub);
       // ONE marker per step on the compute queue (each marker stalls the queue behind it for
       // ~6 us: the next dispatch waits for its completion signal); both side queues wait on it
-      if (overlap_ || early_stop) chk(hipEventRecord(ev_main_, st), "hipEventRecord");
+      if (overlap_ || (early_stop && !pub)) chk(hipEventRecord(ev_main_, st), "hipEventRecord");
       // CBF h of the previous step's main slots on the side stream (one step late: the slice
       // of a step beyond the early stop is never issued)
       if (overlap_ && t >= 1) {
@@ -106,14 +127,17 @@ class RolloutDriver {
         hfwd_slice(t - 1, hs);
       }
       if (early_stop) {
-        chk(hipStreamWaitEvent(cs, ev_main_, 0), "hipStreamWaitEvent");
-        chk(hipMemcpyAsync(P<unsigned long long>(host_dist_) + (long)t * B_, P<const unsigned long long>(dist_) + (long)t * B_,
-                           sizeof(unsigned long long) * B_, hipMemcpyDeviceToHost, cs), "hipMemcpyAsync");
-        chk(hipEventRecord(ev_copy_[t], cs), "hipEventRecord");
+        if (!pub) {
+          chk(hipStreamWaitEvent(cs, ev_main_, 0), "hipStreamWaitEvent");
+          chk(hipMemcpyAsync(P<unsigned long long>(host_dist_) + (long)t * B_, P<const unsigned long long>(dist_) + (long)t * B_,
+                             sizeof(unsigned long long) * B_, hipMemcpyDeviceToHost, cs), "hipMemcpyAsync");
+          chk(hipEventRecord(ev_copy_[t], cs), "hipEventRecord");
+        }
         // host check every check_every steps (small scenes: a step's kernels take less than
         // the host round trip, so checking every step would leave the GPU idle)
         if (t >= 1 && (t % check_ == 0)) {
-          chk(hipEventSynchronize(ev_copy_[t - 1]), "hipEventSynchronize");
+          if (pub) wait_published(t - 1, st);
+          else chk(hipEventSynchronize(ev_copy_[t - 1]), "hipEventSynchronize");
           const int Tf = first_done(hd, t - 1);
           if (Tf > 0) {
             // every env was done after step Tf-1: the trajectory is steps 0..Tf-1; step Tf's
@@ -127,7 +151,8 @@ class RolloutDriver {
     }
     if (early_stop && !tail && check_ > 1 && Tmax_ >= 2) {
       // steps after the last strided check: same horizon as a check after every step
-      chk(hipEventSynchronize(ev_copy_[Tmax_ - 2]), "hipEventSynchronize");
+      if (pub) wait_published(Tmax_ - 2, st);
+      else chk(hipEventSynchronize(ev_copy_[Tmax_ - 2]), "hipEventSynchronize");
       const int Tf = first_done(hd, Tmax_ - 2);
       if (Tf > 0) {
         T = Tf;
@@ -197,6 +222,25 @@ class RolloutDriver {
 
   const float4* S_at(int t) const { return P<const float4>(S_) + (long)t * B_ * Nn_ * (W_ / 4); }
 
+  // Waits until the controller kernel of step t has published its per-env sums (flag == this
+  // rollout's generation). Polls host-coherent memory; a stream error or a minute without the
+  // flag raises instead of spinning forever.
+  void wait_published(int t, hipStream_t st) const {
+    const unsigned* flag = reinterpret_cast<const unsigned*>(pub_host_ + (size_t)Tmax_ * B_) + t;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (unsigned long n = 0; __atomic_load_n(flag, __ATOMIC_ACQUIRE) != gen_; ++n) {
+      if ((n & 4095) == 4095) {
+        const hipError_t e = hipStreamQuery(st);
+        if (e != hipSuccess && e != hipErrorNotReady) chk(e, "rollout stream");
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(60))
+          throw std::runtime_error("RolloutDriver: early-stop flag of step " + std::to_string(t) + " not published");
+      }
+#if defined(__x86_64__)
+      __builtin_ia32_pause();
+#endif
+    }
+  }
+
   void scan_step(int t, hipStream_t st) {
     if (t % resort_ == 0) {
       mb::CellSortArgs c{};
@@ -218,8 +262,14 @@ class RolloutDriver {
     chk(mb_scan(&a, st), "scan");
   }
 
-  void ctrl_step(int t, hipStream_t st) {
+  void ctrl_step(int t, hipStream_t st, bool pub = false) {
     mb::CtrlArgs a{};
+    if (pub) {
+      a.pub_ctr = pub_ctr_ + t;
+      a.pub_dist = pub_dev_ + (long)t * B_;
+      a.pub_flag = reinterpret_cast<unsigned*>(pub_dev_ + (size_t)Tmax_ * B_) + t;
+      a.pub_gen = gen_;
+    }
     a.dim = D_;
     a.S = S_at(t); a.s_env = Nn_;
     a.G = P<const float>(G_);
@@ -258,6 +308,11 @@ class RolloutDriver {
   }
 
   int B_, N_, Nn_, K_, D_, W_, Tmax_, num_cu_, prec_, prow_, resort_, safety_, overlap_, hfwd_blocks_, check_, apw_;
+  int publish_ = 0;
+  unsigned gen_ = 0;
+  unsigned long long* pub_host_ = nullptr;   // host view: [Tmax][B] sums, then [Tmax] flags
+  unsigned long long* pub_dev_ = nullptr;    // the same memory, device view
+  unsigned* pub_ctr_ = nullptr;              // [Tmax] per-step workgroup counters (device)
   float L_;
   u64 S_, G_, A_, idx_, dang_, cnt_, safe_, dist_, act_, pooled_, argmax_, perm_, host_dist_;
   u64 ctrl_w_, ctrl_v_, cbf_w_, cbf_rm_, cbf_v_, hbuf_, hmask_, src_, nev_, noise_key_;

@@ -287,7 +287,9 @@ class HipEngine:
                 small_ctl=native.ptr(self.small_ctl) if self.small_rollout else 0,
                 small_apw=int(native.small_apw(N)), knn_tail=int(not self.reuse),
                 noise_prob=float(cfg.add_noise_prob), noise_scale=float(cfg.noise_scale),
-                fork_device_scope=int(os.environ.get("MACBF_FORK_DEVICE_SCOPE", "1"))))
+                fork_device_scope=int(os.environ.get("MACBF_FORK_DEVICE_SCOPE", "1")),
+                # early stop published by the controller kernels (no per-step queue marker / copy)
+                publish=int(os.environ.get("MACBF_PUBLISH", "1"))))
             if pw.ctrl_v.numel() < 352 or pw.ctrl_w.numel() < (c["f_node"] + 54) * 512 * (2 if pw.x3 else 1):
                 raise native.NativeError("packed controller weights too small")
             if overlap and (self.hbuf.numel() < 2 * T * BNK or self.src.numel() < 2 * T * BNK):

@@ -169,3 +169,30 @@ def test_rollout_sums_order_independent_at_1024_agents():
         for x, y in zip(r[1:], runs[0][1:]):
             assert torch.equal(x, y)
     assert torch.equal(tr.engine.act[: runs[0][0]], tr.engine.act[: runs[0][0]])
+
+
+def test_published_early_stop_matches_copy_path(monkeypatch):
+    """The controller kernels publish the per-env goal-distance sums to host-coherent memory
+    (csrc/ctrl.hip publish_step, no per-step queue marker / side-stream copy): over consecutive
+    rollouts -- each a new generation, the previous one's late steps still in flight when the
+    host breaks -- horizons and trajectories equal the marker + copy path's."""
+    monkeypatch.setenv("MACBF_PUBLISH", "0")
+    tr_c = _trainer()
+    tr_c.engine._driver()                  # the driver reads MACBF_PUBLISH when it is built
+    monkeypatch.setenv("MACBF_PUBLISH", "1")
+    tr_p = _trainer()
+    tr_p.engine._driver()
+    tr_p.fp.flat.copy_(tr_c.fp.flat)
+    tr_p.engine.after_update()
+    for tr in (tr_c, tr_p):
+        tr.engine.check_every = 1
+    stopped = 0
+    for rep in range(5):
+        s0, g, _ = tr_c.sample()
+        a = _rollout(tr_c, True, s0, g, True)
+        b = _rollout(tr_p, True, s0, g, True)
+        assert a[0] == b[0]
+        stopped += a[0] < tr_c.cfg.inner_loops
+        for x, y in zip(a[1:], b[1:]):
+            assert torch.equal(x, y)
+    assert stopped >= 1
