@@ -14,6 +14,8 @@ oracle engine on CPU.
 """
 from __future__ import annotations
 
+import os
+
 import time
 from typing import Optional
 
@@ -73,8 +75,8 @@ class Trainer:
         self.grad_scale = float(cfg.loss_scale_init) if self.fp16 else 1.0
         self._good_steps = 0
         self._next = None
-        self._side = torch.cuda.Stream(device=self.device) if (self.device.type == "cuda" and cfg.prefetch_data) \
-            else None
+        prefetch = cfg.prefetch_data if os.environ.get("MACBF_PREFETCH") is None else os.environ["MACBF_PREFETCH"] == "1"
+        self._side = torch.cuda.Stream(device=self.device) if (self.device.type == "cuda" and prefetch) else None
         if self.device.type == "cuda":
             from .hip_engine import HipEngine
             self._ok = torch.ones(1, dtype=torch.int32, device=self.device)
