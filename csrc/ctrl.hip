@@ -1257,7 +1257,9 @@ size_t ctrl_edge_bwd_lds() { return (size_t)22 * FRAG_SZ + EB_STAGE; }
 
 // Edge backward over the work items w0, w0 + wstride, ... of `a` (smem: the kernel's dynamic
 // LDS; P: this workgroup's slab row)
-template <int D>
+// KC: compile-time neighbour count (12 = TOP_K: the slot / agent / row index arithmetic of the
+// dense rows folds to constants), 0 = runtime a.K
+template <int D, int KC = 0>
 DEV void edge_bwd_body(const CtrlEdgeBwdArgs& a, unsigned char* smem, long w0, long wstride, float* P) {
   h16* wf = reinterpret_cast<h16*>(smem);                 // ew1f (2) | ew2tn (16) | ew1ft (4)
   h16* stg = reinterpret_cast<h16*>(smem + 22 * FRAG_SZ);
@@ -1265,7 +1267,7 @@ DEV void edge_bwd_body(const CtrlEdgeBwdArgs& a, unsigned char* smem, long w0, l
   block_copy16(wf + 2 * FRAG_ELEMS, a.wpack + (size_t)a.f_ew2tn * FRAG_ELEMS, 20 * FRAG_SZ);
   __syncthreads();
   const int wave = threadIdx.x / WAVE, lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
-  const int N = a.N, K = a.K;
+  const int N = a.N, K = KC ? KC : a.K;
   const int total = a.B * N;
   const long nchunks = (total + EB_CH - 1) / EB_CH;
   const int erow = wave * 32 + r;
@@ -1562,10 +1564,10 @@ DEV void edge_bwd_body(const CtrlEdgeBwdArgs& a, unsigned char* smem, long w0, l
   }
 }
 
-template <int D>
+template <int D, int KC = 0>
 __global__ __launch_bounds__(EB_WAVES * 64, (EB_WAVES == 4 && !X3) ? 2 : 1) void ctrl_edge_bwd_kernel(CtrlEdgeBwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  edge_bwd_body<D>(a, smem, blockIdx.x, gridDim.x, a.partial + (long)blockIdx.x * CTRL_EDGE_PARTIAL);
+  edge_bwd_body<D, KC>(a, smem, blockIdx.x, gridDim.x, a.partial + (long)blockIdx.x * CTRL_EDGE_PARTIAL);
 }
 
 // =======================================================================================
@@ -1865,12 +1867,19 @@ extern "C" int MB_SYM(ctrl_edge_bwd)(const mb::CtrlEdgeBwdArgs* a, int num_block
   using namespace mb::MB_PREC;
   if (a->K > 16 || a->K < 1) return -1;
   const size_t lds = ctrl_edge_bwd_lds();
+  // K = 12 (TOP_K): constant-K instantiation (MACBF_EB_K12=0 forces the runtime-K one, A/B)
+  static const bool k12_off = [] { const char* e = getenv("MACBF_EB_K12"); return e && e[0] == '0'; }();
+  auto go = [&](auto kern) {
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(kern, dim3(num_blocks), dim3(EB_WAVES * 64), lds, st, *a);
+  };
+  const bool k12 = a->K == 12 && !k12_off;
   if (a->dim == 3) {
-    (void)hipFuncSetAttribute((const void*)ctrl_edge_bwd_kernel<3>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL(ctrl_edge_bwd_kernel<3>, dim3(num_blocks), dim3(EB_WAVES * 64), lds, st, *a);
+    if (k12) go(ctrl_edge_bwd_kernel<3, 12>);
+    else go(ctrl_edge_bwd_kernel<3>);
   } else {
-    (void)hipFuncSetAttribute((const void*)ctrl_edge_bwd_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL(ctrl_edge_bwd_kernel<2>, dim3(num_blocks), dim3(EB_WAVES * 64), lds, st, *a);
+    if (k12) go(ctrl_edge_bwd_kernel<2, 12>);
+    else go(ctrl_edge_bwd_kernel<2>);
   }
   return (int)hipGetLastError();
 }
