@@ -852,6 +852,26 @@ DEV void node_bwd_body(const CtrlNodeBwdArgs& a, unsigned char* smem, long c0, l
   const int n1 = (wave < 2) ? 3 : 2;
   const h16x8 zz = zero_h8();
 
+  // NB_PREFETCH: the next chunk's pooled rows are requested right after this chunk's layer 1 (the
+  // last use of its own): their latency overlaps the rest of the chunk instead of stalling the
+  // next chunk's layer 1 (one wave per SIMD has nothing else to run meanwhile)
+#ifndef NB_PREFETCH
+#define NB_PREFETCH 1
+#endif
+  Fr Pn[8];
+  auto pooled_rows = [&](long ch, Fr (&dst)[8]) {
+    const int gq = (int)(ch * CA) + erow;
+    if (ch < nchunks && erow < CA && gq < total) {
+      const int bq = gq / N, iq = gq - bq * N;
+      const h16* prow = a.pooled + (long)bq * a.p_env + (long)iq * PROW;
+#pragma unroll
+      for (int kk = 0; kk < 8; ++kk) dst[kk] = row_fr(prow + 16 * kk + 8 * h, 128);
+    } else {
+#pragma unroll
+      for (int kk = 0; kk < 8; ++kk) dst[kk].h = dst[kk].l = zz;
+    }
+  };
+  if (NB_PREFETCH) pooled_rows(c0, Pn);
   for (long chunk = c0; chunk < nchunks; chunk += cstride) {
     const int ga = (int)(chunk * CA) + erow;
     const bool ok = erow < CA && ga < total;
@@ -878,12 +898,18 @@ DEV void node_bwd_body(const CtrlNodeBwdArgs& a, unsigned char* smem, long c0, l
       }
       if (a.Gn) load_rec<D>(a.Gn + (long)b * a.gn_env * REC<D>, (unsigned)i, gnp, gnv);
       vld = a.valid ? (a.valid[(long)b * a.v_env] != 0) : true;
-      const h16* prow = a.pooled + (long)b * a.p_env + (long)i * PROW;
+      if (!NB_PREFETCH) {
+        const h16* prow = a.pooled + (long)b * a.p_env + (long)i * PROW;
 #pragma unroll
-      for (int kk = 0; kk < 8; ++kk) Pf[kk] = row_fr(prow + 16 * kk + 8 * h, 128);
-    } else {
+        for (int kk = 0; kk < 8; ++kk) Pf[kk] = row_fr(prow + 16 * kk + 8 * h, 128);
+      }
+    } else if (!NB_PREFETCH) {
 #pragma unroll
       for (int kk = 0; kk < 8; ++kk) Pf[kk].h = Pf[kk].l = zz;
+    }
+    if (NB_PREFETCH) {
+#pragma unroll
+      for (int kk = 0; kk < 8; ++kk) Pf[kk] = Pn[kk];
     }
     float ex[D];
 #pragma unroll
@@ -904,6 +930,7 @@ DEV void node_bwd_body(const CtrlNodeBwdArgs& a, unsigned char* smem, long c0, l
       relu_(c);
       Y1b[mt] = to_pk(c);
     }
+    if (NB_PREFETCH) pooled_rows(chunk + cstride, Pn);
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt) {
       f32x16 c = bias_rows(nb2, 32 * mt, h);
