@@ -102,7 +102,10 @@ struct RolloutSmallArgs {
 
 struct LossConsts {
   float eps_dang, dt_alpha, w_dang, w_safe, w_dang_d, w_safe_d, scale;
+  const float* gscale;        // optional device loss scale (fp16 dynamic scaling): multiplies `scale`
 };
+// upstream-gradient multiplier of the hinge terms (the device loss scale folded in)
+__host__ __device__ inline float lc_scale(const LossConsts& lc) { return lc.gscale ? lc.scale * *lc.gscale : lc.scale; }
 
 struct CbfFwdArgs {
   const float4* S;  long s_env, s_step;   // node record of (b,t,i): S[(b*s_env + t*s_step + i) * REC]
@@ -209,6 +212,7 @@ struct CtrlNodeBwdArgs {
   const float* wvec;                   // controller side vector (eb2|nb2|nb3|nb4)
   float act_coef, dt, sqrt3;
   const float* act_scale;              // optional device count n_act: coefficient = act_coef / max(n_act, 1)
+  const float* gscale;                 // optional device loss scale (fp16): multiplies the coefficient
   h16* dP;            long dp_env;    // (b,i,128) dL/dpooled out
   float4* ego;                         // (B,N) records: dL/ds_t from the node path + gain law + action loss
   float* partial;                      // (gridDim.x, CTRL_NODE_PARTIAL) slabs, accumulated
@@ -278,15 +282,26 @@ struct BpttSmallArgs {
 };
 
 struct RolloutStatsArgs {
-  const unsigned long long* dist;   // (T, B) per-env sum of |p_{t+1} - g| over the N agents (x FX_DIST)
-  const float* cnt;       // (T, B, 2) dangerous / safe edge counts of step t
-  const float* safe;      // (T+1, B) safe-agent counts of s_t (or null)
-  const unsigned long long* act;    // (T, B) per-env action-loss sums (x FX_ACT, or null)
+  unsigned long long* dist;   // (T, B) per-env sum of |p_{t+1} - g| over the N agents (x FX_DIST)
+  float* cnt;             // (T, B, 2) dangerous / safe edge counts of step t
+  float* safe;            // (T+1, B) safe-agent counts of s_t (or null)
+  unsigned long long* act;    // (T, B) per-env action-loss sums (x FX_ACT, or null)
   int T, B, N;
+  int reset_T;            // > 0: after reading, zero the Tmax = reset_T rows of dist / cnt / act and the
+                          // Tmax + 1 rows of safe (the next rollout's atomics start from zero: no fills)
   float thr;              // DIST_MIN_CHECK
   uint8_t* valid;         // (T, B) out
   float* counts;          // [n_dang, n_safe, n_act] out (this rank)
   float* local;           // [agent-steps, safe agents of s_{t+1}, action-loss sum] out
+};
+
+// End of an optimizer step (one thread): step counters or the skipped count, the fp16 dynamic
+// loss scale (halved on a non-finite step, doubled after `growth` finite ones), this step's
+// statistics row [16] = skipped, [17] = loss scale, and the guard flag reset to 1 for the next step.
+struct StepCommitArgs {
+  int* ok; int* steps; int mask, ngroups; int* skipped;
+  float* gscale; int* good; int growth; float max_scale;   // gscale null: no loss scaling
+  float* stats_row;                                        // null: no statistics row
 };
 
 struct AdamArgs {
@@ -339,10 +354,12 @@ int mb_reduce_rows(const float* partial, int rows, int cols, float* out, int acc
 int mb_adam(const mb::AdamArgs* a, hipStream_t st);
 int mb_rollout_stats(const mb::RolloutStatsArgs* a, hipStream_t st);
 int mb_grad_check(const float* g, int n, int* ok, hipStream_t st);
-int mb_grad_assemble(const float* red, const int* ptr, const int* src, int n, float scale, float* grad, hipStream_t st);
+int mb_grad_assemble(const float* red, const int* ptr, const int* src, int n, float scale, const float* gscale, float* grad,
+                     hipStream_t st);
 int mb_pack_gather(const float* src, int n, const int* idx16, int m16, unsigned short* out16, int f16,
                    const int* idx32, int m32, float* out32, hipStream_t st);
-int mb_adam_commit(const int* ok, int* steps, int mask, int ngroups, int* skipped, hipStream_t st);
+int mb_step_commit(const mb::StepCommitArgs* a, hipStream_t st);
+int mb_stats_pack(const float* sums, const float* counts, const float* local, float* row, hipStream_t st);
 int mb_probe_mfma(const void* a, const void* b, float* d, hipStream_t st);
 int mb_probe_tr(const void* img, int rows, int stride, int e0, int m0, void* out, hipStream_t st);
 }

@@ -16,6 +16,16 @@ template <typename T>
 static T* P(u64 p) { return reinterpret_cast<T*>(static_cast<uintptr_t>(p)); }
 static hipStream_t ST(u64 s) { return reinterpret_cast<hipStream_t>(static_cast<uintptr_t>(s)); }
 
+// loss constants: 7 floats (+ optional device loss-scale pointer)
+static mb::LossConsts LC(const py::tuple& lc) {
+  mb::LossConsts c{};
+  c.eps_dang = lc[0].cast<float>(); c.dt_alpha = lc[1].cast<float>(); c.w_dang = lc[2].cast<float>();
+  c.w_safe = lc[3].cast<float>(); c.w_dang_d = lc[4].cast<float>(); c.w_safe_d = lc[5].cast<float>();
+  c.scale = lc[6].cast<float>();
+  c.gscale = lc.size() > 7 ? P<const float>(lc[7].cast<u64>()) : nullptr;
+  return c;
+}
+
 static int cell_sort(u64 S, long s_env, int B, int N, float L, u64 perm, int rec, u64 stream) {
   mb::CellSortArgs a{};
   a.rec = rec;
@@ -82,9 +92,7 @@ static int cbf_fwd(u64 S, long s_env, long s_step, u64 idx, u64 dang, u64 valid,
   a.wpack = P<const h16>(wpack); a.f_fwd = f_fwd; a.wvec = P<const float>(wvec);
   a.h_out = P<float>(h_out); a.hn_out = P<float>(hn_out); a.dh_out = P<float>(dh_out);
   a.counts = P<const float>(counts); a.partial = P<float>(partial);
-  a.lc.eps_dang = lc[0].cast<float>(); a.lc.dt_alpha = lc[1].cast<float>(); a.lc.w_dang = lc[2].cast<float>();
-  a.lc.w_safe = lc[3].cast<float>(); a.lc.w_dang_d = lc[4].cast<float>(); a.lc.w_safe_d = lc[5].cast<float>();
-  a.lc.scale = lc[6].cast<float>();
+  a.lc = LC(lc);
   a.obs_r = obs_r; a.dist_thr = dist_thr; a.dist_eps = dist_eps;
   return (prec == 2 ? mb_cbf_fwd_x3 : prec == 1 ? mb_cbf_fwd_f16 : mb_cbf_fwd)(&a, num_blocks, ST(stream));
 }
@@ -115,9 +123,7 @@ static int cbf_bwd(u64 S, long s_env, long s_step, u64 idx, int B, int T, int N,
   a.idx1 = P<const int>(idx1);
   a.fused = fused; a.dang = P<const uint8_t>(dang); a.valid = P<const uint8_t>(valid);
   a.counts = P<const float>(counts);
-  a.lc.eps_dang = lc[0].cast<float>(); a.lc.dt_alpha = lc[1].cast<float>(); a.lc.w_dang = lc[2].cast<float>();
-  a.lc.w_safe = lc[3].cast<float>(); a.lc.w_dang_d = lc[4].cast<float>(); a.lc.w_safe_d = lc[5].cast<float>();
-  a.lc.scale = lc[6].cast<float>();
+  a.lc = LC(lc);
   a.S = P<const float4>(S); a.s_env = s_env; a.s_step = s_step; a.idx = P<const int>(idx);
   a.B = B; a.T = T; a.N = N; a.K = K; a.passes = passes; a.dh = P<const float>(dh);
   a.wpack = P<const h16>(wpack); a.f_bwd = f_bwd; a.wrm = P<const h16>(wrm); a.wvec = P<const float>(wvec);
@@ -161,9 +167,7 @@ static int cbf_dh(u64 h, u64 hmask, u64 map1, u64 src, u64 nev, u64 dang, u64 va
   a.h = P<const float>(h); a.hmask = P<const uint8_t>(hmask); a.map1 = P<const int>(map1);
   a.src = P<const int>(src); a.nev = P<const int>(nev); a.dang = P<const uint8_t>(dang);
   a.valid = P<const uint8_t>(valid); a.B = B; a.T = T; a.N = N; a.K = K; a.counts = P<const float>(counts);
-  a.lc.eps_dang = lc[0].cast<float>(); a.lc.dt_alpha = lc[1].cast<float>(); a.lc.w_dang = lc[2].cast<float>();
-  a.lc.w_safe = lc[3].cast<float>(); a.lc.w_dang_d = lc[4].cast<float>(); a.lc.w_safe_d = lc[5].cast<float>();
-  a.lc.scale = lc[6].cast<float>();
+  a.lc = LC(lc);
   a.dh = P<float>(dh); a.partial = P<float>(partial);
   return mb_cbf_dh(&a, num_blocks, ST(stream));
 }
@@ -196,21 +200,32 @@ static int pack_gather(u64 src, int n, u64 idx16, int m16, u64 out16, int f16, u
                         P<const int>(idx32), m32, P<float>(out32), ST(stream));
 }
 
-static int grad_assemble(u64 red, u64 ptr, u64 src, int n, float scale, u64 grad, u64 stream) {
-  return mb_grad_assemble(P<const float>(red), P<const int>(ptr), P<const int>(src), n, scale, P<float>(grad), ST(stream));
+static int grad_assemble(u64 red, u64 ptr, u64 src, int n, float scale, u64 gscale, u64 grad, u64 stream) {
+  return mb_grad_assemble(P<const float>(red), P<const int>(ptr), P<const int>(src), n, scale, P<const float>(gscale),
+                          P<float>(grad), ST(stream));
 }
 
 static int grad_check(u64 g, int n, u64 ok, u64 stream) { return mb_grad_check(P<const float>(g), n, P<int>(ok), ST(stream)); }
 
-static int adam_commit(u64 ok, u64 steps, int mask, int ngroups, u64 skipped, u64 stream) {
-  return mb_adam_commit(P<const int>(ok), P<int>(steps), mask, ngroups, P<int>(skipped), ST(stream));
+static int step_commit(u64 ok, u64 steps, int mask, int ngroups, u64 skipped, u64 gscale, u64 good, int growth,
+                       float max_scale, u64 stats_row, u64 stream) {
+  mb::StepCommitArgs a{};
+  a.ok = P<int>(ok); a.steps = P<int>(steps); a.mask = mask; a.ngroups = ngroups; a.skipped = P<int>(skipped);
+  a.gscale = P<float>(gscale); a.good = P<int>(good); a.growth = growth; a.max_scale = max_scale;
+  a.stats_row = P<float>(stats_row);
+  return mb_step_commit(&a, ST(stream));
+}
+
+static int stats_pack(u64 sums, u64 counts, u64 local, u64 row, u64 stream) {
+  return mb_stats_pack(P<const float>(sums), P<const float>(counts), P<const float>(local), P<float>(row), ST(stream));
 }
 
 static int rollout_stats(u64 dist, u64 cnt, u64 safe, u64 act, int T, int B, int N, float thr, u64 valid,
-                         u64 counts, u64 local, u64 stream) {
+                         u64 counts, u64 local, int reset_T, u64 stream) {
   mb::RolloutStatsArgs a{};
-  a.dist = P<const unsigned long long>(dist); a.cnt = P<const float>(cnt); a.safe = P<const float>(safe);
-  a.act = P<const unsigned long long>(act); a.T = T; a.B = B; a.N = N; a.thr = thr; a.valid = P<uint8_t>(valid);
+  a.reset_T = reset_T;
+  a.dist = P<unsigned long long>(dist); a.cnt = P<float>(cnt); a.safe = P<float>(safe);
+  a.act = P<unsigned long long>(act); a.T = T; a.B = B; a.N = N; a.thr = thr; a.valid = P<uint8_t>(valid);
   a.counts = P<float>(counts); a.local = P<float>(local);
   return mb_rollout_stats(&a, ST(stream));
 }
@@ -227,8 +242,9 @@ static int adam(u64 param, u64 grad, u64 m, u64 v, int lo, int hi, float b1, flo
 static int ctrl_node_bwd(u64 pooled, long p_env, u64 S, long s_env, u64 G, u64 A, long a_env, u64 Gn, long gn_env,
                          u64 valid, long v_env, int B, int N, u64 wrm, int o1, int o2, int o3, int o4, u64 wvec,
                          float act_coef, u64 act_scale, float dt, float sqrt3, u64 dP, long dp_env, u64 ego, u64 partial,
-                         int dim, int num_blocks, int prec, int init, int chunk, u64 stream) {
+                         int dim, int num_blocks, int prec, int init, int chunk, u64 gscale, u64 stream) {
   mb::CtrlNodeBwdArgs a{};
+  a.gscale = P<const float>(gscale);
   a.init = init;
   a.chunk = chunk;
   a.dim = dim;
@@ -302,7 +318,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("grad_check", &grad_check);
   m.def("grad_assemble", &grad_assemble);
   m.def("pack_gather", &pack_gather);
-  m.def("adam_commit", &adam_commit);
+  m.def("step_commit", &step_commit);
+  m.def("stats_pack", &stats_pack);
   m.def("probe_mfma", &probe_mfma);
   m.def("probe_tr", &probe_tr);
   m.def("device_info", &device_info);

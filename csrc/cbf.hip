@@ -165,8 +165,8 @@ __global__ __launch_bounds__(WAVES * 64) void cbf_fwd_kernel(CbfFwdArgs a) {
   const int wave = threadIdx.x / WAVE, lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
   const long E = (long)a.B * a.T * a.N * a.K;
   const long ntiles = (E + 31) / 32;
-  float nd = 0.f, ns = 0.f;
-  if (a.dh_out) { nd = 1e-5f + a.counts[0]; ns = 1e-5f + a.counts[1]; }
+  float nd = 0.f, ns = 0.f, lsc = a.lc.scale;
+  if (a.dh_out) { nd = 1e-5f + a.counts[0]; ns = 1e-5f + a.counts[1]; lsc = lc_scale(a.lc); }
   float acc[10];
 #pragma unroll
   for (int q = 0; q < 10; ++q) acc[q] = 0.f;
@@ -201,7 +201,7 @@ __global__ __launch_bounds__(WAVES * 64) void cbf_fwd_kernel(CbfFwdArgs a) {
         acc[6] += fmaxf(-deriv + a.lc.eps_dang, 0.f);
         acc[8] += (deriv >= 0.f) ? 1.f : 0.f;
         if (a.dh_out) {
-          const float c = a.lc.scale / nd;
+          const float c = lsc / nd;
           const float ind_b = (hv + a.lc.eps_dang > 0.f) ? 1.f : 0.f;
           const float ind_d = (-deriv + a.lc.eps_dang > 0.f) ? 1.f : 0.f;
           gh = c * (a.lc.w_dang * ind_b + a.lc.w_dang_d * ind_d * (1.f - a.lc.dt_alpha));
@@ -214,7 +214,7 @@ __global__ __launch_bounds__(WAVES * 64) void cbf_fwd_kernel(CbfFwdArgs a) {
         acc[7] += fmaxf(-deriv, 0.f);
         acc[9] += (deriv > 0.f) ? 1.f : 0.f;
         if (a.dh_out) {
-          const float c = a.lc.scale / ns;
+          const float c = lsc / ns;
           const float ind_b = (-hv > 0.f) ? 1.f : 0.f;
           const float ind_d = (-deriv > 0.f) ? 1.f : 0.f;
           gh = c * (-a.lc.w_safe * ind_b + a.lc.w_safe_d * ind_d * (1.f - a.lc.dt_alpha));
@@ -376,19 +376,6 @@ DEV void cbf_load(const CbfBwdArgs& a, long chunk, int wave, int r, long E, long
 //   wave forms its upstream dL/dh locally (barrier + derivative hinge losses with the danger
 //   bit, step validity and the global pooled counts) and the loss partial sums go to the slab.
 // ---------------------------------------------------------------------------------------
-// ablation hooks (scripts/build_variants.sh cbf): CBF_X_NOSTSTORE / CBF_X_NOSTMMA drop the
-// stage image stores / the stage contractions (results are then wrong; timing only)
-#ifdef CBF_X_NOSTSTORE
-#define XSTORE(...) ((void)0)
-#else
-#define XSTORE store_pk
-#endif
-#ifdef CBF_X_NOSTMMA
-template <int ES> DEV float xmma_skip(...) { return 0.f; }
-#define XMMA xmma_skip
-#else
-#define XMMA stage_mma_fr
-#endif
 
 // h over a deduplicated evaluation list (dedup.hip): evaluation u < E is main slot u on s_t,
 // u >= E the extra evaluation of slot src[u] on s_{t+1} (neighbour idx1[src[u]]). Writes the
@@ -534,8 +521,8 @@ __global__ __launch_bounds__(NW * 64, 1) void cbf_bwd_kernel(CbfBwdArgs a) {
   const int trow = NT == 1 ? erow : (wave % TW) * 32 + r;   // this wave's rows inside a turn's region
   const int myturn = wave / TW;
   const int pass_w = wave / (NW / 2);          // fused: this wave's pass
-  float nd = 1.f, ns = 1.f;
-  if constexpr (FUSED) { nd = 1e-5f + a.counts[0]; ns = 1e-5f + a.counts[1]; }
+  float nd = 1.f, ns = 1.f, lsc = a.lc.scale;
+  if constexpr (FUSED) { nd = 1e-5f + a.counts[0]; ns = 1e-5f + a.counts[1]; lsc = lc_scale(a.lc); }
   f32x16 accA[TA], accB[TA], accC = zero16();
   float bA[TA], bB[TA], db4 = 0.f;
 #pragma unroll
@@ -549,9 +536,7 @@ __global__ __launch_bounds__(NW * 64, 1) void cbf_bwd_kernel(CbfBwdArgs a) {
   if ((long)blockIdx.x < nchunks) cbf_load<FUSED, NW, D>(a, blockIdx.x, wave, r, E, EV, nx);
   for (long chunk = blockIdx.x; chunk < nchunks; chunk += gridDim.x) {
     const CbfIn<D> cur = nx;
-#ifndef CBF_X_NOLOAD
     if (chunk + gridDim.x < nchunks) cbf_load<FUSED, NW, D>(a, chunk + gridDim.x, wave, r, E, EV, nx);   // prefetch
-#endif
     const EdgeCtx<D>& c = cur.c;
     const h16x8 F = cbf_edge_frag<D>(c.rp, c.rv, c.eye, c.dfeat, c.ok, h);
     // one opaque base per LDS image per chunk: the per-lane address math is computed once and
@@ -606,13 +591,9 @@ __global__ __launch_bounds__(NW * 64, 1) void cbf_bwd_kernel(CbfBwdArgs a) {
       float hs = hs2.x + hs2.y;
       hs += shfl_xor32(hs);
       const float hm = (cur.in && c.mask) ? hs + vlc[256] : 0.f;
-#ifdef CBF_X_NOEXCH
-      const float other = hm;
-#else
       if (h == 0) hx[erow] = hm;
       __syncthreads();
       const float other = hx[(wave ^ (NW / 2)) * 32 + r];
-#endif
       const float hv = pass_w == 0 ? hm : other;
       const float hnv = pass_w == 0 ? other : hm;
       float gh = 0.f, ghn = 0.f;
@@ -620,7 +601,7 @@ __global__ __launch_bounds__(NW * 64, 1) void cbf_bwd_kernel(CbfBwdArgs a) {
         const float deriv = hnv - hv + a.lc.dt_alpha * hv;
         const bool acc_here = (pass_w == 0) && (h == 0);
         if (cur.dg) {
-          const float cc = a.lc.scale / nd;
+          const float cc = lsc / nd;
           const float ind_b = (hv + a.lc.eps_dang > 0.f) ? 1.f : 0.f;
           const float ind_d = (-deriv + a.lc.eps_dang > 0.f) ? 1.f : 0.f;
           gh = cc * (a.lc.w_dang * ind_b + a.lc.w_dang_d * ind_d * (1.f - a.lc.dt_alpha));
@@ -632,7 +613,7 @@ __global__ __launch_bounds__(NW * 64, 1) void cbf_bwd_kernel(CbfBwdArgs a) {
             lacc[6][erow] += (deriv >= 0.f) ? 1.f : 0.f;
           }
         } else {
-          const float cc = a.lc.scale / ns;
+          const float cc = lsc / ns;
           const float ind_b = (-hv > 0.f) ? 1.f : 0.f;
           const float ind_d = (-deriv > 0.f) ? 1.f : 0.f;
           gh = cc * (-a.lc.w_safe * ind_b + a.lc.w_safe_d * ind_d * (1.f - a.lc.dt_alpha));
@@ -666,33 +647,27 @@ __global__ __launch_bounds__(NW * 64, 1) void cbf_bwd_kernel(CbfBwdArgs a) {
       mask_pk(d3b[mt], H3b[mt]);
     }
     // ---- stage A: dW3 (64x128) += dH3pre . H2^T ; db3   (tiles t = wave + NW u -> (t/4, t%4))
-#ifndef CBF_X_NOSTAGE
 #pragma unroll
     for (int turn = 0; turn < NT; ++turn) {
       h16* imA = stg + par * Cfg::REGION;
       h16* imB = imA + RT * SA64;
       if (NT == 1 || myturn == turn) {
 #pragma unroll
-        for (int mt = 0; mt < 2; ++mt) XSTORE(imA, SA64, trow, 32 * mt, d3b[mt], h, PL);
+        for (int mt = 0; mt < 2; ++mt) store_pk(imA, SA64, trow, 32 * mt, d3b[mt], h, PL);
 #pragma unroll
-        for (int mt = 0; mt < 4; ++mt) XSTORE(imB, SA128, trow, 32 * mt, H2b[mt], h, PL);
+        for (int mt = 0; mt < 4; ++mt) store_pk(imB, SA128, trow, 32 * mt, H2b[mt], h, PL);
       }
       __syncthreads();
       int blo, bhi;
-#ifdef CBF_X_NOBIAS
-      blo = bhi = 0;
-#else
       if constexpr (NT == 1) { blo = bsA; bhi = bsA + KS / 4; }
       else turn_range(bsA, bsA + KS / 4, turn, KST, blo, bhi);
-#endif
 #pragma unroll
       for (int u = 0; u < TA; ++u) {
         const int t = wave + NW * u;
-        bA[u] += XMMA<KST>(imA, SA64, PL, imB, SA128, PL, t / 4, t % 4, lane, accA[u], blo, bhi);
+        bA[u] += stage_mma_fr<KST>(imA, SA64, PL, imB, SA128, PL, t / 4, t % 4, lane, accA[u], blo, bhi);
       }
       if constexpr (Cfg::NREG == 2) par ^= 1; else __syncthreads();
     }
-#endif
     // ---- dH2pre = (W3^T dH3pre) . relu'(H2)
     Pk d2b[4];
 #pragma unroll
@@ -706,33 +681,27 @@ __global__ __launch_bounds__(NW * 64, 1) void cbf_bwd_kernel(CbfBwdArgs a) {
       mask_pk(d2b[mt], H2b[mt]);
     }
     // ---- stage B: dW2 (128x64) += dH2pre . H1^T ; db2   (tiles t = wave + NW u -> (t/2, t%2))
-#ifndef CBF_X_NOSTAGE
 #pragma unroll
     for (int turn = 0; turn < NT; ++turn) {
       h16* imA = stg + par * Cfg::REGION;
       h16* imB = imA + RT * SA128;
       if (NT == 1 || myturn == turn) {
 #pragma unroll
-        for (int mt = 0; mt < 4; ++mt) XSTORE(imA, SA128, trow, 32 * mt, d2b[mt], h, PL);
+        for (int mt = 0; mt < 4; ++mt) store_pk(imA, SA128, trow, 32 * mt, d2b[mt], h, PL);
 #pragma unroll
-        for (int mt = 0; mt < 2; ++mt) XSTORE(imB, SA64, trow, 32 * mt, H1b[mt], h, PL);
+        for (int mt = 0; mt < 2; ++mt) store_pk(imB, SA64, trow, 32 * mt, H1b[mt], h, PL);
       }
       __syncthreads();
       int blo, bhi;
-#ifdef CBF_X_NOBIAS
-      blo = bhi = 0;
-#else
       if constexpr (NT == 1) { blo = bsB; bhi = bsB + KS / 2; }
       else turn_range(bsB, bsB + KS / 2, turn, KST, blo, bhi);
-#endif
 #pragma unroll
       for (int u = 0; u < TA; ++u) {
         const int t = wave + NW * u;
-        bB[u] += XMMA<KST>(imA, SA128, PL, imB, SA64, PL, t / 2, t % 2, lane, accB[u], blo, bhi);
+        bB[u] += stage_mma_fr<KST>(imA, SA128, PL, imB, SA64, PL, t / 2, t % 2, lane, accB[u], blo, bhi);
       }
       if constexpr (Cfg::NREG == 2) par ^= 1; else __syncthreads();
     }
-#endif
     // ---- dH1pre = (W2^T dH2pre) . relu'(H1)
     Pk d1b[2];
 #pragma unroll
@@ -773,7 +742,6 @@ __global__ __launch_bounds__(NW * 64, 1) void cbf_bwd_kernel(CbfBwdArgs a) {
     //      dW4pad (32x64) += [dh;0..] . relu(H3)^T, A = image cols 16..47 -> row 0 = dw4 (waves 2,3;
     //      rows >= 1 read padding / the next row and are discarded: MFMA rows are independent).
     //      x3: F is exact in h16 (its lo plane is zero); dh's residual goes to the lo plane.
-#ifndef CBF_X_NOSTAGE
 #pragma unroll
     for (int turn = 0; turn < NT; ++turn) {
       h16* imC = stg + par * Cfg::REGION;
@@ -781,9 +749,9 @@ __global__ __launch_bounds__(NW * 64, 1) void cbf_bwd_kernel(CbfBwdArgs a) {
       h16* imH = imF + RT * SA32;
       if (NT == 1 || myturn == turn) {
 #pragma unroll
-        for (int mt = 0; mt < 2; ++mt) XSTORE(imC, SA64, trow, 32 * mt, d1b[mt], h, PL);
+        for (int mt = 0; mt < 2; ++mt) store_pk(imC, SA64, trow, 32 * mt, d1b[mt], h, PL);
 #pragma unroll
-        for (int mt = 0; mt < 2; ++mt) XSTORE(imH, SA64, trow, 32 * mt, H3b[mt], h, PL);
+        for (int mt = 0; mt < 2; ++mt) store_pk(imH, SA64, trow, 32 * mt, H3b[mt], h, PL);
         h16x8 dv = zero_h8();
         const h16 dvh = (h16)dhv;
         if (h == 0) dv[0] = dvh;
@@ -797,11 +765,10 @@ __global__ __launch_bounds__(NW * 64, 1) void cbf_bwd_kernel(CbfBwdArgs a) {
         }
       }
       __syncthreads();
-      if (wave < 2) XMMA<KST>(imC, SA64, PL, imF, SA32, PL, wave, 0, lane, accC);
-      else if (wave < 4) XMMA<KST>(imF + 16, SA32, PL, imH, SA64, PL, 0, wave - 2, lane, accC);
+      if (wave < 2) stage_mma_fr<KST>(imC, SA64, PL, imF, SA32, PL, wave, 0, lane, accC);
+      else if (wave < 4) stage_mma_fr<KST>(imF + 16, SA32, PL, imH, SA64, PL, 0, wave - 2, lane, accC);
       if constexpr (Cfg::NREG == 2) par ^= 1; else __syncthreads();
     }
-#endif
   }
   __syncthreads();   // all stage reads done: the stage region is reused below
   float* bred = reinterpret_cast<float*>(stg);        // [NW][192] bias partials: b3 (64) | b2 (128)

@@ -173,9 +173,7 @@ template <int D> struct EdgeSt { float rp[D], rv[D]; int j, i; bool ok; };
 // (env, index) of the agents g0 + al, 0 <= al < 32, of a 32-agent group: one division per group;
 // with N >= 32 the group wraps into the next env at most once (a per-tile 32-bit division by the
 // runtime N is a dozen VALU instructions, two of them quarter rate)
-#ifndef CTRL_GROUP_BASE
-#define CTRL_GROUP_BASE 1
-#endif
+constexpr int CTRL_GROUP_BASE = 1;
 struct AgentBase { int g0, b0, i0; };
 DEV AgentBase agent_base(int g0, int N) {
   AgentBase o;
@@ -360,9 +358,7 @@ DEV void pool_store(const PoolDst& d, int nt, int pw_) {
   const h16 ph = (h16)pv;
   d.prow[32 * nt] = ph;
   if constexpr (IS_X3 && GPOOL) d.prow[32 * nt + 128] = (h16)(pv - (float)ph);
-#ifndef CTRL_X_NOARGMAX
   if (d.arow) d.arow[32 * nt] = (pw_ > 15) ? (uint8_t)(15 - (pw_ & 15)) : (uint8_t)0xFF;
-#endif
 }
 
 // DENSE12 pool of edge tile q (see ctrl_fwd_groups): Z = relu-free pre-activations of the tile's
@@ -438,12 +434,8 @@ DEV void pool_dense12(const CtrlArgs& a, const AgentBase& ab, int g0, int APW, i
 // already in LDS: wl = ew1f|ew2, wn = nw1f..nw4, vl = CTRL_VEC floats, pools = one 32-row pool
 // image per wave). SPLIT (always for x3): edge phase only, the pooled rows go to global memory
 // and ctrl_node_groups runs the node phase.
-#ifndef CTRL_HOIST_EB
-#define CTRL_HOIST_EB 1
-#endif
-#ifndef CTRL_FWD_DENSE
-#define CTRL_FWD_DENSE 1
-#endif
+constexpr int CTRL_HOIST_EB = 1;
+constexpr int CTRL_FWD_DENSE = 1;
 // DENSE12 (K = 12, agents per wave a multiple of 8): dense edge rows -- a group's APW agents x 12
 // slots are APW * 12 / 32 tiles of 32 consecutive edges (no padding slots). Rows come in quads of
 // 4 that never straddle an agent (12 = 3 quads); tile q covers quads j = 0..7 of agents
@@ -502,11 +494,7 @@ DEV void ctrl_fwd_groups(const CtrlArgs& a, const h16* wl, const h16* wn, const 
       ctrl_st_load<D>(a.S, a.s_env, xi0, xs0);
       idx_load(1, xi1);
     }
-#ifdef CTRL_X_TILES
-    for (int q = 0; q < min(NTL, CTRL_X_TILES); ++q) {     // ablation: fewer edge tiles (timing only)
-#else
     for (int q = 0; q < NTL; ++q) {
-#endif
       const EdgeSt<D> cur = xs0;
       ctrl_st_load<D>(a.S, a.s_env, xi1, xs0);                    // states of tile q+1
       idx_load(q + 2, xi1);                                        // idx of tile q+2
@@ -539,9 +527,6 @@ DEV void ctrl_fwd_groups(const CtrlArgs& a, const h16* wl, const h16* wn, const 
       if (gout) agent_bi(ab, arow, N, bb, ii);
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt) {
-#ifdef CTRL_X_NOPOOL
-        { pool[arow * PSTR + 32 * nt + r] = (h16)Z[nt][0]; continue; }
-#endif
         int p0 = 0, p1 = 0;
 #pragma unroll
         for (int reg = 0; reg < 8; ++reg) {
@@ -562,11 +547,9 @@ DEV void ctrl_fwd_groups(const CtrlArgs& a, const h16* wl, const h16* wn, const 
         } else {
           pool[arow * PSTR + 32 * nt + r] = (h16)pv;
         }
-#ifndef CTRL_X_NOARGMAX
         if (a.argmax && ga < total)
           a.argmax[(long)bb * a.am_env + (long)ii * 128 + 32 * nt + r] =
               (pw_ > 15) ? (uint8_t)(15 - (pw_ & 15)) : (uint8_t)0xFF;
-#endif
       }
     }
     if constexpr (GPOOL && GNODE) {
@@ -594,10 +577,6 @@ DEV void ctrl_fwd_groups(const CtrlArgs& a, const h16* wl, const h16* wn, const 
         }
       }
     }
-#ifdef CTRL_X_NONODE
-    lds_wave_sync();
-    continue;
-#endif
     // ---------------- node phase: lane column r = agent g0 + r
     node_phase<D>(a, g0, APW, total, [&](int kk) { return row_fr(pool + r * PSTR + 16 * kk + 8 * h, 0); },
                   wn, nb2, nb3, nb4, lane);
@@ -775,23 +754,14 @@ constexpr int NB_RT = NB_TW * 32;                     // region rows
 constexpr int NB_KST = NB_RT / 16;                    // agent steps per turn
 // stage image row strides (h16 elements) for 32 / 64 / 128-wide images and the 160-wide
 // pooled|state image of S1
-#ifndef NBS64
-#define NBS64 72
-#endif
-#ifndef NBS128
-#define NBS128 136
-#endif
-#ifndef NBSP
-#define NBSP 168
-#endif
-// NB_MERGE43: stages S4 and S3 share one set of turns (their four images fit one region)
-#ifndef NB_MERGE43
-#define NB_MERGE43 1
-#endif
+constexpr int NBS64 = 72;
+constexpr int NBS128 = 136;
+constexpr int NBSP = 168;
+// stages S4 and S3 share one set of turns (their four images fit one region)
 constexpr int NBS_32 = 40, NBS_64 = NBS64, NBS_128 = NBS128, NBS_P = NBSP;
 constexpr int nb_max(int a, int b) { return a > b ? a : b; }
 constexpr int NB_PL = nb_max(nb_max(NBS_P + NBS_64, NBS_128 + NBS_64),
-                             NB_MERGE43 ? NBS_32 + 2 * NBS_64 + NBS_128 : 0) * NB_RT;   // elements per region plane
+                             NBS_32 + 2 * NBS_64 + NBS_128) * NB_RT;   // elements per region plane
 constexpr size_t NB_STAGE = (size_t)(X3 ? 2 : 1) * NB_PL * 2;
 
 size_t ctrl_node_bwd_lds() { return (size_t)(X3 ? 2 : 1) * NODE_RM_ELEMS * 2 + CTRL_VEC * 4 + NB_STAGE; }
@@ -855,9 +825,7 @@ DEV void node_bwd_body(const CtrlNodeBwdArgs& a, unsigned char* smem, long c0, l
   // NB_PREFETCH: the next chunk's pooled rows are requested right after this chunk's layer 1 (the
   // last use of its own): their latency overlaps the rest of the chunk instead of stalling the
   // next chunk's layer 1 (one wave per SIMD has nothing else to run meanwhile)
-#ifndef NB_PREFETCH
-#define NB_PREFETCH 1
-#endif
+constexpr int NB_PREFETCH = 1;
   Fr Pn[8];
   auto pooled_rows = [&](long ch, Fr (&dst)[8]) {
     const int gq = (int)(ch * CA) + erow;
@@ -877,11 +845,7 @@ DEV void node_bwd_body(const CtrlNodeBwdArgs& a, unsigned char* smem, long c0, l
     const bool ok = erow < CA && ga < total;
     // stage turns holding at least one valid agent (a partial last chunk -- all but the first
     // for small scenes -- skips the turns of its empty waves: zero rows contribute nothing)
-#ifdef CTRL_X_NBNOSTAGE
-    const int nturn = 0;       // ablation (timing only): no weight-gradient stages
-#else
     const int nturn = min(NB_NT, (int)((min((long)CA, total - chunk * CA) + NB_RT - 1) / NB_RT));
-#endif
     int b = 0, i = 0;
     float sp[D], sv[D], gg[D], av[D], gnp[D], gnv[D];
 #pragma unroll
@@ -970,7 +934,8 @@ DEV void node_bwd_body(const CtrlNodeBwdArgs& a, unsigned char* smem, long c0, l
       float da[D], ar[D];
 #pragma unroll
       for (int q = 0; q < D; ++q) { da[q] = a.dt * gnv[q]; ar[q] = -(ex[q] + a.sqrt3 * sv[q]); }
-      const float act_coef = a.act_scale ? a.act_coef / fmaxf(*a.act_scale, 1.f) : a.act_coef;
+      float act_coef = a.act_scale ? a.act_coef / fmaxf(*a.act_scale, 1.f) : a.act_coef;
+      if (a.gscale) act_coef *= *a.gscale;        // fp16: device loss scale
       if (vld && act_coef != 0.f) {
         const float diff = sqsum<D>(av) - sqsum<D>(ar);
         const float sg = diff > 0.f ? 1.f : (diff < 0.f ? -1.f : 0.f);
@@ -1016,7 +981,6 @@ DEV void node_bwd_body(const CtrlNodeBwdArgs& a, unsigned char* smem, long c0, l
       d3b[mt] = to_pk(c);
       mask_pk(d3b[mt], Y3b[mt]);
     }
-#if NB_MERGE43
 #pragma unroll 1
     for (int turn = 0; turn < nturn; ++turn) {   // S4 + S3: dWn4pad += dY4 . Y3^T ; nb4 | dWn3 += dY3 . Y2^T ; nb3
       h16* im4A = stg;
@@ -1056,53 +1020,6 @@ DEV void node_bwd_body(const CtrlNodeBwdArgs& a, unsigned char* smem, long c0, l
       d2b[mt] = to_pk(c);
       mask_pk(d2b[mt], Y2b[mt]);
     }
-#else
-#pragma unroll 1
-    for (int turn = 0; turn < nturn; ++turn) {   // S4: dWn4pad (32x64) += dY4 . Y3^T ; nb4
-      h16* imA = stg;
-      h16* imB = stg + NB_RT * NBS_32;
-      if (NB_NT == 1 || myturn == turn) {
-        store_pk(imA, NBS_32, trow, 0, d4b, h, NB_PL);
-#pragma unroll
-        for (int mt = 0; mt < 2; ++mt) store_pk(imB, NBS_64, trow, 32 * mt, Y3b[mt], h, NB_PL);
-      }
-      __syncthreads();
-      if (wave < 2)
-        bs4 += stage_mma_fr<NB_KST>(imA, NBS_32, NB_PL, imB, NBS_64, NB_PL, 0, wave, lane, acc4, 0, wave == 0 ? NB_KST : 0);
-      __syncthreads();
-    }
-    // ---- dY2 = W3^T dY3 . relu'(Y2)
-    Pk d2b[4];
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt) {
-      f32x16 c = zero16();
-      static_for<4>([&](auto kk_) {
-        constexpr int kk = decltype(kk_)::value;
-        c = mma(wrmT_acc_fr(W3 + opaque_zero(), NS3, 32 * mt, kk, lane, LO), pk_fr<kk & 1>(d3b[kk >> 1]), c);
-      });
-      d2b[mt] = to_pk(c);
-      mask_pk(d2b[mt], Y2b[mt]);
-    }
-#pragma unroll 1
-    for (int turn = 0; turn < nturn; ++turn) {   // S3: dWn3 (64x128) += dY3 . Y2^T ; nb3
-      h16* imA = stg;
-      h16* imB = stg + NB_RT * NBS_64;
-      if (NB_NT == 1 || myturn == turn) {
-#pragma unroll
-        for (int mt = 0; mt < 2; ++mt) store_pk(imA, NBS_64, trow, 32 * mt, d3b[mt], h, NB_PL);
-#pragma unroll
-        for (int mt = 0; mt < 4; ++mt) store_pk(imB, NBS_128, trow, 32 * mt, Y2b[mt], h, NB_PL);
-      }
-      __syncthreads();
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const int t = wave + 4 * u;
-        bs3[u] += stage_mma_fr<NB_KST>(imA, NBS_64, NB_PL, imB, NBS_128, NB_PL, t / 4, t % 4, lane, acc3[u], 0,
-                                       t % 4 == 0 ? NB_KST : 0);
-      }
-      __syncthreads();
-    }
-#endif
     // ---- dY1 = W2^T dY2 . relu'(Y1)
     Pk d1b[2];
 #pragma unroll
@@ -1201,9 +1118,6 @@ DEV void node_bwd_body(const CtrlNodeBwdArgs& a, unsigned char* smem, long c0, l
     }
   }
   // ---- slab += this workgroup's partial (fixed WG -> slab map: deterministic)
-#ifdef CTRL_X_NOSLAB
-  if (a.partial) return;                        // ablation: no slab read-modify-write
-#endif
   // all slab loads first (see load_tile), then the adds and stores; the first BPTT step writes
   // the slab (no zero-fill pass, no loads)
   f32x16 o1[3], o2[2], o3[2], o4 = zero16();
@@ -1263,17 +1177,13 @@ __global__ __launch_bounds__(NB_WAVES * 64, 1) void ctrl_node_bwd_kernel(CtrlNod
 // EB_WAVES waves share a chunk of 32*EB_WAVES agents; each stage contracts the 32*EB_WAVES edges
 // of one tile round (8 waves: 256 edges per barrier pair, one dW2 tile per wave; 4 waves: 128
 // edges, two tiles per wave, two workgroups per CU)
-#ifndef CTRL_EB_WAVES
-#define CTRL_EB_WAVES 4
-#endif
+constexpr int CTRL_EB_WAVES = 4;
 constexpr int EB_WAVES = CTRL_EB_WAVES;
 constexpr int EB_CH = EB_WAVES * 32;     // agents per chunk (each round: EB_CH edges)
 constexpr int EB_TA = 8 / EB_WAVES;      // owned dW2 tiles per wave
 // dense edge rows: K tiles per 32-agent wave (12 at K = 12) instead of 16 tiles of 2 agents x 16
 // slots (a quarter of them padding rows at K = 12)
-#ifndef CTRL_EB_DENSE
-#define CTRL_EB_DENSE 1
-#endif
+constexpr int CTRL_EB_DENSE = 1;
 constexpr bool EB_DENSE = CTRL_EB_DENSE;
 constexpr int EP_W2 = 0, EP_B2 = 8192, EP_W1 = 8320;
 constexpr int CTRL_EDGE_PARTIAL = 10368;
@@ -1485,13 +1395,8 @@ DEV void edge_bwd_body(const CtrlEdgeBwdArgs& a, unsigned char* smem, long w0, l
           store_rec<D>(a.dEc, (unsigned)(b * (int)a.de_env + i * K + slot), gp, gv);
         }
       }
-#ifdef CTRL_X_EBNOSTAGE
-      lds_wave_sync();
-      continue;
-#endif
       // S1: dW2 (128x64) += dZ . H1^T ; eb2 (dZ is already in the image; bias-sum steps split
       //     between the two waves that read each row block)
-#ifndef CTRL_X_EBNOS1
       {
         h16* imA = stg;
         h16* imB = stg + EB_CH * 128;
@@ -1507,14 +1412,10 @@ DEV void edge_bwd_body(const CtrlEdgeBwdArgs& a, unsigned char* smem, long w0, l
         }
         __syncthreads();
       }
-#else
-      __syncthreads();
-#endif
       // S2: dW1f (64x32) += dH1 . F^T over this wave's own 32 edges -- wave-local, no barrier:
       //     the images live in the wave's own 32 rows of the dZ image (free after S1's closing
       //     barrier, rewritten by this wave's next scatter only), each wave accumulates both dW1
       //     tiles; the per-wave partials are summed in fixed order at the end
-#ifndef CTRL_X_EBNOS2
       {
         h16* imA = stg + wave * 32 * 128;          // dH1, 32 rows x 64 (swizzled)
         h16* imB = imA + 32 * 64;                  // [F | 0], 32 rows x 32 (swizzled)
@@ -1530,12 +1431,8 @@ DEV void edge_bwd_body(const CtrlEdgeBwdArgs& a, unsigned char* smem, long w0, l
         for (int mt = 0; mt < 2; ++mt) stage_mma_sw_fr<2, 64, 32, true>(imA, EB_PL, imB, 0, mt, 0, lane, accW1[mt]);
         lds_wave_sync();                           // reads done before the next scatter
       }
-#endif
     }
   }
-#ifdef CTRL_X_NOSLAB
-  if (a.partial) return;                        // ablation: no slab read-modify-write
-#endif
   __shared__ float ebred[EB_WAVES][EB_TA][32];
   // every slab load of the tail first (see load_tile): dW2 tiles, this thread's dW1 elements,
   // the eb2 element

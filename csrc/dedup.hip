@@ -185,6 +185,7 @@ __global__ __launch_bounds__(DH_BLOCK) void cbf_dh_kernel(CbfDhArgs a) {
   const unsigned E = (unsigned)a.T * BNK;
   const unsigned U = (unsigned)*a.nev;
   const float nd = 1e-5f + a.counts[0], ns = 1e-5f + a.counts[1];
+  const float lsc = lc_scale(a.lc);
   const LossConsts lc = a.lc;
   float acc[8];
 #pragma unroll
@@ -246,7 +247,7 @@ __global__ __launch_bounds__(DH_BLOCK) void cbf_dh_kernel(CbfDhArgs a) {
         const float hv = hv0[j], hnv = hn0[j];
         const float deriv = hnv - hv + lc.dt_alpha * hv;
         if (dg0[j]) {
-          const float cc = lc.scale / nd;
+          const float cc = lsc / nd;
           const float ind_b = (hv + lc.eps_dang > 0.f) ? 1.f : 0.f;
           const float ind_d = (-deriv + lc.eps_dang > 0.f) ? 1.f : 0.f;
           g += cc * (lc.w_dang * ind_b + lc.w_dang_d * ind_d * (1.f - lc.dt_alpha));
@@ -255,7 +256,7 @@ __global__ __launch_bounds__(DH_BLOCK) void cbf_dh_kernel(CbfDhArgs a) {
           acc[4] += fmaxf(-deriv + lc.eps_dang, 0.f);
           acc[6] += (deriv >= 0.f) ? 1.f : 0.f;
         } else {
-          const float cc = lc.scale / ns;
+          const float cc = lsc / ns;
           const float ind_b = (-hv > 0.f) ? 1.f : 0.f;
           const float ind_d = (-deriv > 0.f) ? 1.f : 0.f;
           g += cc * (-lc.w_safe * ind_b + lc.w_safe_d * ind_d * (1.f - lc.dt_alpha));
@@ -270,10 +271,10 @@ __global__ __launch_bounds__(DH_BLOCK) void cbf_dh_kernel(CbfDhArgs a) {
         const float deriv = hnv - hv + lc.dt_alpha * hv;
         if (dg1[j]) {
           const float ind_d = (-deriv + lc.eps_dang > 0.f) ? 1.f : 0.f;
-          g += -(lc.scale / nd) * lc.w_dang_d * ind_d;
+          g += -(lsc / nd) * lc.w_dang_d * ind_d;
         } else {
           const float ind_d = (-deriv > 0.f) ? 1.f : 0.f;
-          g += -(lc.scale / ns) * lc.w_safe_d * ind_d;
+          g += -(lsc / ns) * lc.w_safe_d * ind_d;
         }
       }
       const float d = hm[j] ? g : 0.f;

@@ -99,31 +99,64 @@ __global__ __launch_bounds__(256) void pack_gather_kernel(const float* src, int 
 // Flat gradient assembly: grad[p] = scale * sum of the reduced slab entries that map to
 // parameter p (CSR by p, fixed order: deterministic, no atomics, no zero-fill)
 __global__ __launch_bounds__(256) void grad_assemble_kernel(const float* red, const int* ptr, const int* src, int n,
-                                                            float scale, float* grad) {
+                                                            float scale, const float* gscale, float* grad) {
   const int p = blockIdx.x * 256 + threadIdx.x;
   if (p >= n) return;
+  if (gscale) scale /= *gscale;     // fp16: unscale by the device loss scale
   float t = 0.f;
   for (int q = ptr[p]; q < ptr[p + 1]; ++q) t += red[src[q]];
   grad[p] = t * scale;
 }
 
-// ok = 0 if any gradient element is not finite (ok preset to 1 by the caller)
+// ok = 0 if any gradient element is not finite (ok is 1 between steps: step_commit resets it)
 __global__ __launch_bounds__(256) void grad_check_kernel(const float* g, int n, int* ok) {
   bool bad = false;
   for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) bad = bad || !isfinite(g[i]);
   if (__any(bad) && (threadIdx.x % WAVE) == 0) *ok = 0;
 }
 
-// after the Adam launches of one iteration: steps[g] += 1 for the stepped groups (bit g of
-// mask) if the step was taken, else skipped += 1
-__global__ void adam_commit_kernel(const int* ok, int* steps, int mask, int ngroups, int* skipped) {
+// after the Adam launches of one iteration (see StepCommitArgs): no host round trip, no
+// torch glue kernels between the optimizer and the next iteration
+__global__ void step_commit_kernel(StepCommitArgs a) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  if (*ok) {
-    for (int g = 0; g < ngroups; ++g)
-      if ((mask >> g) & 1) steps[g] += 1;
+  const int ok = *a.ok;
+  if (ok) {
+    for (int g = 0; g < a.ngroups; ++g)
+      if ((a.mask >> g) & 1) a.steps[g] += 1;
   } else {
-    *skipped += 1;
+    *a.skipped += 1;
   }
+  if (a.gscale) {
+    float s = *a.gscale;
+    if (!ok) {
+      s = fmaxf(0.5f * s, 1.f);
+      *a.good = 0;
+    } else {
+      const int g = *a.good + 1;
+      if (g >= a.growth) {
+        s = fminf(2.f * s, a.max_scale);
+        *a.good = 0;
+      } else {
+        *a.good = g;
+      }
+    }
+    *a.gscale = s;
+  }
+  if (a.stats_row) {
+    a.stats_row[16] = ok ? 0.f : 1.f;
+    a.stats_row[17] = a.gscale ? *a.gscale : 1.f;
+  }
+  *a.ok = 1;
+}
+
+// One iteration's statistics row (utils.metrics.StepStats): [10 loss sums | counts 3 | local 3 |
+// skipped | loss scale] -- written into a ring of rows instead of torch.cat + clone
+__global__ void stats_pack_kernel(const float* sums, const float* counts, const float* local, float* row) {
+  const int t = threadIdx.x;
+  if (t < 10) row[t] = sums[t];
+  else if (t < 13) row[t] = counts[t - 10];
+  else if (t < 16) row[t] = local[t - 13];
+  else if (t < 18) row[t] = t == 16 ? 0.f : 1.f;
 }
 
 // Post-rollout bookkeeping in one launch (replaces ~20 small tensor ops between the rollout
@@ -168,6 +201,17 @@ __global__ __launch_bounds__(RS_BLOCK) void rollout_stats_kernel(RolloutStatsArg
     a.local[1] = red[3][0];
     a.local[2] = red[4][0];
   }
+  if (a.reset_T > 0) {     // every read above precedes the reduction's barriers
+    const int n = a.reset_T * a.B;
+    for (int q = threadIdx.x; q < n; q += RS_BLOCK) {
+      a.dist[q] = 0ull;
+      a.cnt[2 * q] = 0.f;
+      a.cnt[2 * q + 1] = 0.f;
+      if (a.act) a.act[q] = 0ull;
+    }
+    if (a.safe)
+      for (int q = threadIdx.x; q < n + a.B; q += RS_BLOCK) a.safe[q] = 0.f;
+  }
 }
 
 }  // namespace mb
@@ -181,10 +225,11 @@ extern "C" int mb_pack_gather(const float* src, int n, const int* idx16, int m16
   return (int)hipGetLastError();
 }
 
-extern "C" int mb_grad_assemble(const float* red, const int* ptr, const int* src, int n, float scale, float* grad,
-                                hipStream_t st) {
+extern "C" int mb_grad_assemble(const float* red, const int* ptr, const int* src, int n, float scale,
+                                const float* gscale, float* grad, hipStream_t st) {
   using namespace mb;
-  hipLaunchKernelGGL(grad_assemble_kernel, dim3((n + 255) / 256), dim3(256), 0, st, red, ptr, src, n, scale, grad);
+  hipLaunchKernelGGL(grad_assemble_kernel, dim3((n + 255) / 256), dim3(256), 0, st, red, ptr, src, n, scale, gscale,
+                     grad);
   return (int)hipGetLastError();
 }
 
@@ -195,9 +240,15 @@ extern "C" int mb_grad_check(const float* g, int n, int* ok, hipStream_t st) {
   return (int)hipGetLastError();
 }
 
-extern "C" int mb_adam_commit(const int* ok, int* steps, int mask, int ngroups, int* skipped, hipStream_t st) {
+extern "C" int mb_step_commit(const mb::StepCommitArgs* a, hipStream_t st) {
   using namespace mb;
-  hipLaunchKernelGGL(adam_commit_kernel, dim3(1), dim3(64), 0, st, ok, steps, mask, ngroups, skipped);
+  hipLaunchKernelGGL(step_commit_kernel, dim3(1), dim3(64), 0, st, *a);
+  return (int)hipGetLastError();
+}
+
+extern "C" int mb_stats_pack(const float* sums, const float* counts, const float* local, float* row, hipStream_t st) {
+  using namespace mb;
+  hipLaunchKernelGGL(stats_pack_kernel, dim3(1), dim3(64), 0, st, sums, counts, local, row);
   return (int)hipGetLastError();
 }
 

@@ -355,6 +355,7 @@ class BpttDriver {
     dt_ = F("dt"); sqrt3_ = F("sqrt3");
     small_ = (int)I("small");
     node_chunk_ = (int)I("node_chunk");
+    gscale_ = c.contains("gscale") ? U("gscale") : 0;   // fp16: device loss scale (or 0)
     if (B_ < 1 || N_ < 1 || Nn_ < N_ || K_ < 1 || K_ > 16 || (D_ != 2 && D_ != 3) || Tmax_ < 1 || nb_node_ < 1 ||
         nb_edge_ < 1)
       throw std::invalid_argument("BpttDriver: bad dimensions");
@@ -372,6 +373,7 @@ class BpttDriver {
     n.A = P<const float>(A_); n.valid = P<const uint8_t>(valid_); n.B = B_; n.N = N_;
     n.wrm = P<const h16>(wrm_); n.o_w1 = o1_; n.o_w2 = o2_; n.o_w3 = o3_; n.o_w4 = o4_;
     n.wvec = P<const float>(wvec_); n.act_coef = act_coef; n.act_scale = P<const float>(act_scale_);
+    n.gscale = P<const float>(gscale_);
     n.dt = dt_; n.sqrt3 = sqrt3_; n.dP = P<h16>(dP_); n.ego = P<float4>(ego_); n.partial = P<float>(part_node_);
     mb::CtrlEdgeBwdArgs& e = a.eb;
     e.dim = D_; e.S = n.S; e.idx = P<const int>(idx_); e.argmax = P<const uint8_t>(argmax_); e.dP = n.dP;
@@ -402,6 +404,7 @@ class BpttDriver {
         a.B = B_; a.N = N_;
         a.wrm = P<const h16>(wrm_); a.o_w1 = o1_; a.o_w2 = o2_; a.o_w3 = o3_; a.o_w4 = o4_;
         a.wvec = P<const float>(wvec_); a.act_coef = act_coef; a.act_scale = P<const float>(act_scale_);
+        a.gscale = P<const float>(gscale_);
         a.dt = dt_; a.sqrt3 = sqrt3_;
         a.dP = P<h16>(dP_); a.dp_env = (long)N_ * prow_; a.ego = P<float4>(ego_); a.partial = P<float>(part_node_);
         a.init = t == T - 1;     // the first step of the reverse loop writes the slabs
@@ -439,7 +442,7 @@ class BpttDriver {
  private:
   int B_, N_, Nn_, K_, D_, R_, Tmax_, prec_, prow_, nb_node_, nb_edge_, qsplit_, small_ = 0, node_chunk_ = 0;
   u64 pooled_, S_, G_, A_, dS_, Gb_, valid_, idx_, argmax_, rptr_, redges_, wrm_, wvec_, act_scale_, dP_, ego_, dEc_;
-  u64 part_node_, part_edge_, wpack_;
+  u64 part_node_, part_edge_, wpack_, gscale_ = 0;
   int o1_, o2_, o3_, o4_, f_ew1f_, f_ew2tn_;
   float dt_, sqrt3_;
 };

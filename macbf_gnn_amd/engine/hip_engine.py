@@ -30,6 +30,8 @@ from ..ops.weights import PackedWeights
 # action-loss weight of the total loss (core.py:174-184 via train.py:93,98); the node backward
 # divides it by the all-reduced action count on the device
 ACT_COEF = C.LOSS_SCALE * C.LOSS_WEIGHTS[4]
+STATS_COLS = 18       # StepStats row: 10 loss sums | 3 counts | 3 local | skipped | loss scale
+STATS_RING = 256
 
 
 class HipEngine:
@@ -161,7 +163,15 @@ class HipEngine:
         self.dEc = torch.zeros(B, N, K, W, dtype=f32, device=dev)
         self.counts = torch.zeros(3, dtype=f32, device=dev)
         self.local = torch.zeros(3, dtype=f32, device=dev)        # agent-steps, safe agents, action-loss sum
-        self.raw_stats = torch.zeros(16, dtype=f32, device=dev)   # utils.metrics.StepStats layout
+        self.raw_stats = torch.zeros(STATS_COLS, dtype=f32, device=dev)   # graph mode (fixed address)
+        # per-iteration statistics rows (utils.metrics.StepStats layout), written by one kernel per
+        # iteration into a ring; a full ring is replaced by a fresh one (torch.empty: no kernel), so
+        # a StepStats keeps its row for as long as it is referenced
+        self._ring = torch.empty(STATS_RING, STATS_COLS, dtype=f32, device=dev)
+        self._ring_pos = 0
+        # cnt / safe / dist / act are accumulated by atomics: rollout_stats zeroes them after reading
+        # (no fill kernels in the training step); a rollout not followed by _counts zeroes them first
+        self._sums_dirty = False
         self.valid_buf = torch.zeros(T, B, dtype=u8, device=dev)
         # exploration noise (reference train.py:65-67): counter-based device RNG keyed per iteration
         self.noise_key = torch.zeros(1, dtype=torch.int64, device=dev)
@@ -303,10 +313,12 @@ class HipEngine:
         cfg = self.tr.cfg
         B, N, K, D = self.B, self.N, self.K, self.D
         pw = self.pw
-        self.cnt.zero_()
-        self.safe.zero_()
-        self.dist.zero_()
-        self.act.zero_()
+        if self._sums_dirty or self.graph_mode or torch.cuda.is_current_stream_capturing():
+            self.cnt.zero_()
+            self.safe.zero_()
+            self.dist.zero_()
+            self.act.zero_()
+        self._sums_dirty = True
         events = []
         T = self.Tmax
         tail_scanned = False
@@ -419,8 +431,8 @@ class HipEngine:
     # ------------------------------------------------------------------ graph mode
     def _step_graph(self, s0, g, obs):
         self.load_inputs(s0, g, obs)
-        gs = float(self.tr.grad_scale)
-        if self._graphs is None or self._graph_gs != gs:     # (re)capture; fp16 scale is baked in
+        gs = self._gscale()[0]
+        if self._graphs is None or self._graph_gs != gs:     # (re)capture when a host scale changes
             self._capture()
             self._graph_gs = gs
         self._graphs[0].replay()
@@ -457,8 +469,11 @@ class HipEngine:
         (+ the local stats in self.local), one kernel: step t of env b counts iff the env was
         not done before t."""
         valid = self.valid_buf[:T]
+        reset = None if self.graph_mode else (self.dist, self.cnt, self.safe, self.act)
         native.rollout_stats(self.dist[:T], self.cnt[:T], self.safe[: T + 1], self.act[:T], valid,
-                             self.counts, self.local, N=self.N)
+                             self.counts, self.local, N=self.N, reset=reset)
+        if reset is not None:
+            self._sums_dirty = False
         return valid
 
     def _backward(self, T, valid, counts_work=None):
@@ -468,7 +483,7 @@ class HipEngine:
         tm = tr.timer
         # loss scale of the upstream gradients (fp16: dynamic, trainer-owned; bf16: 1). Every
         # backward quantity is linear in it; the flat gradient is unscaled after the slab reduce.
-        gs = float(tr.grad_scale)
+        gs, gsd = self._gscale()
         valid_u8 = valid
         E = T * B * N * K
         # ---- reverse CSR of the step graphs (needs only idx): on the aux stream, concurrent with
@@ -501,7 +516,7 @@ class HipEngine:
                             pw.cbf_rm, pw.cbf_v, hb, hm, u_begin=E if self.overlap_hfwd else 0, prec=self.prec)
             self._counts_ready(counts_work)
             native.cbf_dh(hb, hm, map1, src, nev, self.dang[:T], valid_u8, self.counts, dh, self.loss_part,
-                          grad_scale=gs, blk_active=self.blk_active)
+                          grad_scale=gs, blk_active=self.blk_active, gscale=gsd)
             # backward over the evaluations with a nonzero upstream gradient only (exact: the
             # others contribute zeros); node_reduce reads dE where dh != 0
             act = self.act_list[: 2 * E]
@@ -515,7 +530,7 @@ class HipEngine:
             self._counts_ready(counts_work)
             native.cbf_bwd(S, idx, None, pw.cbf_w, pw.cbf_off["w1f"], pw.cbf_rm, pw.cbf_v, passes=2, dE=dE,
                            partial=part_cbf, num_blocks=nbb, fused=True, dang=self.dang[:T], valid=valid_u8,
-                           counts=self.counts, idx1=idx1, grad_scale=gs, prec=self.prec)
+                           counts=self.counts, idx1=idx1, grad_scale=gs, prec=self.prec, gscale=gsd)
         cur = torch.cuda.current_stream(self.dev)
         cur.wait_event(csr_done)
         # no-BPTT: s_t is a detached input, only h'(s_{t+1}) gradients reach a_t
@@ -580,7 +595,7 @@ class HipEngine:
             native.ctrl_node_bwd(self.pooled[:T].view(TB, N, self.prow), self.S[:T].view(TB, Nn, W), Gr[:TB],
                                  self.A[:T].view(TB, N, D), self.dS[1: T + 1].view(TB, N, W), valid_u8.view(TB),
                                  pw.ctrl_rm, pw.node_rm_off, pw.ctrl_v, gs * ACT_COEF, dP[:TB], None, pn, nb_n,
-                                 act_cnt=self.counts[2:3], prec=self.prec, init=True)
+                                 act_cnt=self.counts[2:3], prec=self.prec, init=True, gscale=gsd)
             native.ctrl_edge_bwd(self.S[:T].view(TB, Nn, W), self.idx[:T].view(TB, N, K), self.argmax[:T].view(TB, N, 128),
                                  dP[:TB], pw.ctrl_w, pw.ctrl_off["ew1f"], pw.ctrl_off["ew2tn"], None, pe, nb_e, prec=self.prec,
                                  init=True)
@@ -590,13 +605,30 @@ class HipEngine:
         pnode, pedge = (self.part_node[: slab_rows[0]], self.part_edge[: slab_rows[1]]) if self.bptt else self._nb_parts
         for part, red in ((part_cbf, self.red_cbf), (pnode, self.red_node), (pedge, self.red_edge)):
             native.reduce_rows(part, red)
-        native.grad_assemble(self.red_all, self.g_ptr, self.g_src, tr.fp.grad, scale=1.0 / gs)
+        native.grad_assemble(self.red_all, self.g_ptr, self.g_src, tr.fp.grad, scale=1.0 / gs, gscale=gsd)
         tm.mark("grad_reduce")
-        # ---- stats: one raw device vector (no per-statistic kernels), derived lazily on read
+        # ---- stats: one raw device row per iteration (no per-statistic kernels), derived lazily on read
         sums = self.loss_red[:10] if self.dedup else self.red_cbf[native.CBF_P_LOSS: native.CBF_P_LOSS + 10]
-        torch.cat([sums, self.counts, self.local], out=self.raw_stats)
+        row = self.raw_stats if self.graph_mode else self._next_row()
+        native.stats_pack(sums, self.counts, self.local, row)
         Tv = T if not self.graph_mode else (valid != 0).any(1).sum()
-        return self.raw_stats, Tv
+        return row, Tv
+
+    def _next_row(self):
+        if self._ring_pos == self._ring.shape[0]:
+            self._ring = torch.empty_like(self._ring)
+            self._ring_pos = 0
+        row = self._ring[self._ring_pos]
+        self._ring_pos += 1
+        return row
+
+    def _gscale(self):
+        """(host upstream-gradient scale, device loss scale or None): fp16 training keeps its
+        dynamic loss scale on the device (no host round trip per step)."""
+        d = getattr(self.tr, "gscale_dev", None)
+        if d is not None:
+            return 1.0, d
+        return float(self.tr.grad_scale), None
 
     def _bdriver(self):
         """The native BPTT driver over this engine's persistent buffers (checked here once)."""
@@ -627,7 +659,8 @@ class HipEngine:
                 o_w3=int(pw.node_rm_off["w3"]), o_w4=int(pw.node_rm_off["w4"]), ctrl_v=native.ptr(pw.ctrl_v),
                 ctrl_w=native.ptr(pw.ctrl_w), f_ew1f=int(pw.ctrl_off["ew1f"]), f_ew2tn=int(pw.ctrl_off["ew2tn"]),
                 dt=float(C.TIME_STEP), sqrt3=float(C.SQRT3), small=int(self.small_bptt),
-                node_chunk=int(native.node_bwd_chunk(B * N, self.dev))))
+                node_chunk=int(native.node_bwd_chunk(B * N, self.dev)),
+                gscale=native.ptr(getattr(self.tr, "gscale_dev", None))))
             self._bdrv = native.lib().BpttDriver(c)
         return self._bdrv
 
@@ -640,7 +673,8 @@ class HipEngine:
             Gn = self.dS[T][sl] if t == T - 1 else self.Gb[t + 1][sl]   # G_T = dL/ds_T (direct terms only)
             native.ctrl_node_bwd(self.pooled[t][sl], self.S[t][sl], self.G[sl], self.A[t][sl], Gn, valid_u8[t][sl],
                                  pw.ctrl_rm, pw.node_rm_off, pw.ctrl_v, gs * ACT_COEF, self.dP[sl], self.ego[sl],
-                                 part_node, nbn, act_cnt=self.counts[2:3], prec=self.prec, init=t == T - 1)
+                                 part_node, nbn, act_cnt=self.counts[2:3], prec=self.prec, init=t == T - 1,
+                                 gscale=getattr(self.tr, "gscale_dev", None))
             native.ctrl_edge_bwd(self.S[t][sl], self.idx[t][sl], self.argmax[t][sl], self.dP[sl], pw.ctrl_w,
                                  pw.ctrl_off["ew1f"], pw.ctrl_off["ew2tn"], self.dEc[sl], part_edge, nbe, prec=self.prec,
                                  init=t == T - 1)
@@ -656,7 +690,9 @@ class HipEngine:
 
     def _stats(self, raw, T):
         from ..utils.metrics import StepStats
-        return StepStats(raw.clone(), T.clone() if isinstance(T, torch.Tensor) else T)
+        if self.graph_mode:      # the captured graph writes fixed buffers
+            return StepStats(raw.clone(), T.clone() if isinstance(T, torch.Tensor) else T)
+        return StepStats(raw, T)
 
     def _buf(self, cache, key, cols):
         b = cache.get(key)

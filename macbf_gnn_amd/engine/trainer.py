@@ -72,8 +72,13 @@ class Trainer:
         # in-kernel upstream gradients and is divided out of the flat gradient before the
         # all-reduce; a non-finite step is skipped and halves it.
         self.fp16 = cfg.dtype == "fp16" and self.device.type == "cuda"
-        self.grad_scale = float(cfg.loss_scale_init) if self.fp16 else 1.0
-        self._good_steps = 0
+        # on the device (fp16): the scale and the finite-step count live in device memory and are
+        # updated by the optimizer's commit kernel -- no host round trip per step
+        self.gscale_dev = None
+        self._grad_scale = float(cfg.loss_scale_init) if self.fp16 else 1.0
+        if self.fp16:
+            self.gscale_dev = torch.full((1,), float(cfg.loss_scale_init), dtype=torch.float32, device=self.device)
+            self._good_dev = torch.zeros(1, dtype=torch.int32, device=self.device)
         self._next = None
         prefetch = cfg.prefetch_data if os.environ.get("MACBF_PREFETCH") is None else os.environ["MACBF_PREFETCH"] == "1"
         self._side = torch.cuda.Stream(device=self.device) if (self.device.type == "cuda" and prefetch) else None
@@ -123,6 +128,21 @@ class Trainer:
         self._next = self._sample_async(self.step_count + 1)
         return data
 
+    @property
+    def grad_scale(self) -> float:
+        """Current loss scale of the upstream gradients (fp16: read from the device)."""
+        if self.gscale_dev is not None:
+            return float(self.gscale_dev.item())
+        return self._grad_scale
+
+    @grad_scale.setter
+    def grad_scale(self, v):
+        if self.gscale_dev is not None:
+            self.gscale_dev.fill_(float(v))
+            self._good_dev.zero_()
+        else:
+            self._grad_scale = float(v)
+
     def on_params_loaded(self):
         self.fp.rebind()
         self.engine.after_update()
@@ -148,34 +168,33 @@ class Trainer:
         tm.mark("allreduce")
         # failure detection: a non-finite reduced gradient is identical on every
         # rank, so every rank skips the same step; parameters and Adam state stay untouched
-        if self.device.type == "cuda" and self.cfg.nan_guard and not self.fp16:
-            # on the device: a flag gates the fused Adam kernel (no host round trip per step);
-            # the skipped-step count is read lazily
-            self._ok.fill_(1)
+        if self.device.type == "cuda":
+            # on the device: grad_check clears a flag that gates the fused Adam kernels; the commit
+            # kernel counts the step (or the skip), updates the fp16 loss scale, writes both into
+            # this step's statistics row and re-arms the flag -- no host round trip, no torch glue
             from ..ops import native
-            native.grad_check(self.fp.grad, self._ok)
-            self.opt.step(self.groups_to_step(), ok=self._ok)
+            guard = self.cfg.nan_guard or self.fp16
+            if guard:
+                native.grad_check(self.fp.grad, self._ok)
+            row = getattr(stats, "raw", None)
+            row = row if (row is not None and row.numel() >= 18) else None
+            self.opt.step(self.groups_to_step(), ok=self._ok if guard else None, gscale=self.gscale_dev,
+                          good=self._good_dev if self.fp16 else None, growth=self.cfg.loss_scale_growth,
+                          stats_row=row)
             self.engine.after_update()
-            stats["skipped"] = 1 - self._ok[0]
-        elif (self.cfg.nan_guard or self.fp16) and not bool(torch.isfinite(self.fp.grad).all()):
+            if row is None:
+                stats["skipped"] = 1 - self._ok[0]
+            elif self.fp16:
+                stats.scaled = True
+        elif self.cfg.nan_guard and not bool(torch.isfinite(self.fp.grad).all()):
             self._host_skipped += 1
             stats["skipped"] = 1
-            if self.fp16:
-                self.grad_scale = max(self.grad_scale * 0.5, 1.0)
-                self._good_steps = 0
             if self.dp.rank == 0:
                 print(f"[macbf] step {self.step_count}: non-finite gradient, optimizer step skipped "
-                      f"({self.skipped_steps} so far, grad scale {self.grad_scale:g})", flush=True)
+                      f"({self.skipped_steps} so far)", flush=True)
         else:
             self.opt.step(self.groups_to_step())
             self.engine.after_update()
-            if self.fp16:
-                self._good_steps += 1
-                if self._good_steps >= self.cfg.loss_scale_growth:
-                    self.grad_scale = min(self.grad_scale * 2.0, 2.0 ** 24)
-                    self._good_steps = 0
-        if self.fp16:
-            stats["grad_scale"] = self.grad_scale
         tm.mark("optimizer")
         self.step_count += 1
         if tm.enabled:

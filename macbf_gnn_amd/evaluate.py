@@ -39,6 +39,7 @@ class EvalConfig:
     top_k: int = C.TOP_K
     seed: int = 0
     early_stop: bool = True
+    diagnose: bool = False      # dense all-pairs check: are the flagged pairs top-K neighbours?
 
 
 def _knn(s, k):
@@ -55,27 +56,45 @@ def _safe_count(s):
     return oracle.safe_agent_count(s).float()
 
 
-def refine_actions(cbf, s, a, idx, loops: int = C.REFINE_LOOPS, lr: float = C.REFINE_LEARNING_RATE):
+def refine_actions(cbf, s, a, idx, loops: int = C.REFINE_LOOPS, lr: float = C.REFINE_LEARNING_RATE,
+                   check_every: int = 10):
     """Gradient refinement of the actions on the discrete CBF condition. Returns
-    (refined actions, iterations used, remaining violation sum)."""
+    (refined actions, iterations used, remaining violation sum).
+
+    The violation is a hinge: once it is exactly zero its gradient is exactly zero, so further
+    iterations leave the actions unchanged. The loop therefore only looks at the violation on
+    the host every ``check_every`` iterations (one sync instead of one per iteration); the
+    iteration count (iterations that still had a violation) is kept on the device."""
     with torch.no_grad():
         h = cbf(s, idx=idx)
     delta = torch.zeros_like(a, requires_grad=True)
     viol = torch.zeros((), device=s.device)
-    it = 0
+    used = torch.zeros((), dtype=torch.int64, device=s.device)
     for it in range(1, loops + 1):
         ar = a + delta
         s_next = s + torch.cat([s[..., 2:], ar], -1) * C.TIME_STEP
         hn = cbf(s_next, idx=idx)
         deriv = hn - h + C.TIME_STEP * C.ALPHA_CBF * h
         viol = torch.relu(-deriv).sum()
-        if float(viol.detach()) <= 0.0:
-            it -= 1
+        pending = viol.detach() > 0
+        used += pending.long()
+        if it % check_every == 0 and not bool(pending):
             break
         g, = torch.autograd.grad(viol, delta)
         with torch.no_grad():
             delta -= lr * g
-    return (a + delta).detach(), it, float(viol.detach())
+    return (a + delta).detach(), int(used), float(viol.detach())
+
+
+def _unsafe_diag(s_next, idx):
+    """(unsafe agents, unsafe agents whose every flagged pair is one of their top-K neighbours at
+    the step's graph) -- do the controller / CBF see the pairs that the safety check flags?"""
+    dang = oracle.ttc_mask_all_pairs(s_next)                  # (B, N, N) check mask
+    unsafe = dang.any(-1)
+    in_k = torch.zeros_like(dang)
+    in_k.scatter_(-1, idx.long(), True)
+    seen = unsafe & ~(dang & ~in_k).any(-1)
+    return unsafe.sum(), seen.sum()
 
 
 def rollout_eval(controller, cbf, s0, g, cfg: EvalConfig) -> Dict[str, float]:
@@ -85,6 +104,8 @@ def rollout_eval(controller, cbf, s0, g, cfg: EvalConfig) -> Dict[str, float]:
     safe_sum = 0.0
     steps = 0
     refine_iters = 0
+    unsafe_n = torch.zeros((), device=s.device)
+    seen_n = torch.zeros((), device=s.device)
     active = torch.ones(B, dtype=torch.bool, device=s.device)
     for t in range(cfg.max_steps):
         idx = _knn(s, k)
@@ -97,6 +118,10 @@ def rollout_eval(controller, cbf, s0, g, cfg: EvalConfig) -> Dict[str, float]:
             s = s + torch.cat([s[..., 2:], a], -1) * C.TIME_STEP
             safe = _safe_count(s)
             safe_sum += float((safe * active.float()).sum())
+            if cfg.diagnose:
+                u, sn = _unsafe_diag(s[active], idx[active])
+                unsafe_n += u
+                seen_n += sn
             steps += int(active.sum()) * N
             dist = torch.linalg.vector_norm(s[..., :2] - g, dim=-1).mean(-1)
             active = active & (dist >= C.DIST_MIN_CHECK)
@@ -106,8 +131,12 @@ def rollout_eval(controller, cbf, s0, g, cfg: EvalConfig) -> Dict[str, float]:
         d = torch.linalg.vector_norm(s[..., :2] - g, dim=-1)
         reach = float((d < C.DIST_MIN_CHECK).float().mean())
         mean_dist = float(d.mean())
-    return {"safety_rate": safe_sum / max(steps, 1), "reaching_rate": reach, "mean_goal_dist": mean_dist,
-            "steps": t + 1, "agent_steps": steps, "refine_iters": refine_iters}
+    out = {"safety_rate": safe_sum / max(steps, 1), "reaching_rate": reach, "mean_goal_dist": mean_dist,
+           "steps": t + 1, "agent_steps": steps, "refine_iters": refine_iters}
+    if cfg.diagnose:
+        out["unsafe_agent_steps"] = float(unsafe_n)
+        out["unsafe_pairs_in_topk_share"] = float(seen_n) / max(float(unsafe_n), 1.0)
+    return out
 
 
 def evaluate(controller, cbf, cfg: EvalConfig, device: Optional[torch.device] = None) -> Dict[str, float]:

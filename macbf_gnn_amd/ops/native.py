@@ -394,6 +394,13 @@ def ctrl_fwd_apw(total_agents: int, device, n_agents: int | None = None) -> int:
 
 LOSS_CONSTS = (C.LOSS_EPS_DANG, C.TIME_STEP * C.ALPHA_CBF, C.LOSS_WEIGHTS[0], C.LOSS_WEIGHTS[1],
                C.LOSS_WEIGHTS[2], C.LOSS_WEIGHTS[3], C.LOSS_SCALE)
+
+
+def _loss_consts(grad_scale=1.0, gscale=None):
+    """LOSS_CONSTS with the upstream-gradient scale: a host factor and/or a device loss scale
+    (fp16 dynamic scaling: 1-element float32 tensor read by the kernel, no host round trip)."""
+    check(gscale, torch.float32, (1,), "gscale")
+    return LOSS_CONSTS[:6] + (LOSS_CONSTS[6] * float(grad_scale), ptr(gscale))
 CBF_FWD_WAVES = 4
 CBF_PARTIAL = 18704
 CBF_P_LOSS = 18692          # 10 loss partial sums in the CBF slab (fused mode)
@@ -545,7 +552,8 @@ def cbf_dh_grid(EV: int, device) -> int:
     return max(1, min((EV + 8 * DH_BLOCK - 1) // (8 * DH_BLOCK), num_cu(device) * 16))
 
 
-def cbf_dh(h, hmask, map1, src, nev, dang, valid, counts, dh, partial, *, grad_scale=1.0, blk_active=None):
+def cbf_dh(h, hmask, map1, src, nev, dang, valid, counts, dh, partial, *, grad_scale=1.0, blk_active=None,
+           gscale=None):
     """Upstream dL/dh of every deduplicated evaluation (h-role + h'-role) and the 10 loss
     partial sums per block (slots as CBF_P_LOSS: [0, 0, 8 sums], padded) -> partial (nb, DH_PARTIAL)."""
     T, B, N, K = map1.shape
@@ -565,7 +573,7 @@ def cbf_dh(h, hmask, map1, src, nev, dang, valid, counts, dh, partial, *, grad_s
     nb = partial.shape[0]
     check(blk_active, torch.int32, (nb,), "blk_active")
     _ok(lib().cbf_dh(ptr(h), ptr(hmask), ptr(map1), ptr(src), ptr(nev), ptr(dang), ptr(valid), B, T, N, K,
-                     ptr(counts), LOSS_CONSTS[:6] + (LOSS_CONSTS[6] * float(grad_scale),), ptr(dh), ptr(partial),
+                     ptr(counts), _loss_consts(grad_scale, gscale), ptr(dh), ptr(partial),
                      ptr(blk_active), nb, stream_handle()), "cbf_dh")
 
 
@@ -592,7 +600,7 @@ def cbf_bwd_grid(EV: int, device) -> int:
 
 def cbf_bwd(S, idx, dh, wpack, f_bwd, wrm, wvec, *, passes=2, dE=None, partial=None, num_blocks=None,
             fused=False, dang=None, valid=None, counts=None, idx1=None, grad_scale=1.0, src=None, nev=None,
-            act=None, nact=None, prec=None):
+            act=None, nact=None, prec=None, gscale=None):
     """dh (passes, T, B, N, K) -> dE (passes, T, B, N, K, 4), per-WG dW slabs (nb, CBF_PARTIAL).
 
     fused=True (training, passes=2): dh is not read; the kernel evaluates h and h' of every
@@ -645,7 +653,7 @@ def cbf_bwd(S, idx, dh, wpack, f_bwd, wrm, wvec, *, passes=2, dE=None, partial=N
                        ptr(wpack), int(f_bwd), ptr(wrm), ptr(wvec), ptr(dE), ptr(partial), float(C.OBS_RADIUS),
                        float(C.DIST_MIN_THRES), float(C.CBF_DIST_EPS_COORD * D), int(fused), ptr(dang) if fused else 0,
                        ptr(valid) if fused else 0, ptr(counts) if fused else 0,
-                       LOSS_CONSTS[:6] + (LOSS_CONSTS[6] * float(grad_scale),), ptr(idx1), D, nb,
+                       _loss_consts(grad_scale, gscale), ptr(idx1), D, nb,
                        f16, ptr(src), ptr(nev) if src is not None else 0, ptr(act), ptr(nact) if act is not None else 0,
                        stream_handle())
     _ok(rc, "cbf_bwd")
@@ -765,7 +773,7 @@ def ctrl_bwd_grids(total_agents: int, device, prec=None):
 
 
 def ctrl_node_bwd(pooled, S, G, A, Gn, valid_t, wrm, offs, wvec, act_coef, dP, ego, partial, num_blocks,
-                  act_cnt=None, prec=None, init=False, chunk=None):
+                  act_cnt=None, prec=None, init=False, chunk=None, gscale=None):
     """act_cnt: optional 1-element device tensor holding the (all-reduced) action-loss count
     n_act; the action-loss coefficient is then act_coef / max(n_act, 1), read by the kernel (no
     host round trip, no extra launch). init: write the weight-gradient slabs instead of
@@ -789,13 +797,14 @@ def ctrl_node_bwd(pooled, S, G, A, Gn, valid_t, wrm, offs, wvec, act_coef, dP, e
     check(ego, torch.float32, (B, N, W), "ego")
     check(partial, torch.float32, (num_blocks, CTRL_NODE_PARTIAL), "partial")
     check(act_cnt, torch.float32, (1,), "act_cnt")
+    check(gscale, torch.float32, (1,), "gscale")
     rc = lib().ctrl_node_bwd(ptr(pooled), pooled.stride(0), ptr(S), S.stride(0) // W, ptr(G), ptr(A), A.stride(0) // D,
                              ptr(Gn), Gn.stride(0) // W if Gn is not None else 0,
                              ptr(valid_t), valid_t.stride(0) if valid_t is not None else 0, B, N,
                              ptr(wrm), offs["w1"], offs["w2"], offs["w3"], offs["w4"], ptr(wvec),
                              float(act_coef), ptr(act_cnt), float(C.TIME_STEP), float(C.SQRT3), ptr(dP), dP.stride(0),
                              ptr(ego), ptr(partial), D, int(num_blocks), f16, int(bool(init)),
-                             int(chunk or node_bwd_chunk(B * N, S.device)), stream_handle())
+                             int(chunk or node_bwd_chunk(B * N, S.device)), ptr(gscale), stream_handle())
     _ok(rc, "ctrl_node_bwd")
 
 
@@ -833,11 +842,23 @@ FX_DIST = 2.0 ** 32           # csrc/args.h: fixed-point scales of the per-env r
 FX_ACT = 2.0 ** 24
 
 
-def rollout_stats(dist, cnt, safe, act, valid, counts, local, *, N):
+def rollout_stats(dist, cnt, safe, act, valid, counts, local, *, N, reset=None):
     """dist/act (T,B), cnt (T,B,2), safe (T+1,B) or None -> valid (T,B) u8, counts[:3] =
     [n_dang, n_safe, n_act] of this rank, local[:3] = [agent-steps, safe agents of s_{t+1},
-    action-loss sum]. One launch, deterministic."""
+    action-loss sum]. One launch, deterministic. reset = (dist, cnt, safe, act) full (Tmax, ...)
+    buffers whose leading views are the inputs: zeroed after they are read, so the next
+    rollout's atomics start from zero without fill kernels."""
     T, B = dist.shape
+    reset_T = 0
+    if reset is not None:
+        zd, zc, zs, za = reset
+        reset_T = zd.shape[0]
+        check(zd, torch.int64, (reset_T, B), "reset dist")
+        check(zc, torch.float32, (reset_T, B, 2), "reset cnt")
+        check(zs, torch.float32, (reset_T + 1, B), "reset safe")
+        check(za, torch.int64, (reset_T, B), "reset act")
+        if (ptr(zd), ptr(zc), ptr(zs), ptr(za)) != (ptr(dist), ptr(cnt), ptr(safe), ptr(act)) or T > reset_T:
+            raise NativeError("reset buffers must start at the inputs")
     check(dist, torch.int64, (T, B), "dist")
     check(cnt, torch.float32, (T, B, 2), "cnt")
     check(safe, torch.float32, (T + 1, B), "safe")
@@ -848,7 +869,7 @@ def rollout_stats(dist, cnt, safe, act, valid, counts, local, *, N):
     if counts.numel() < 3 or local.numel() < 3:
         raise NativeError("counts / local need 3 slots")
     _ok(lib().rollout_stats(ptr(dist), ptr(cnt), ptr(safe), ptr(act), T, B, int(N), float(C.DIST_MIN_CHECK),
-                            ptr(valid), ptr(counts), ptr(local), stream_handle()), "rollout_stats")
+                            ptr(valid), ptr(counts), ptr(local), int(reset_T), stream_handle()), "rollout_stats")
 
 
 def adam(param, grad, m, v, lo, hi, lr, b1, b2, eps, wd, step, ok=None, step_dev=None):
@@ -882,29 +903,54 @@ def pack_gather(src, idx16, out16, idx32, out32):
                           ptr(idx32), idx32.numel(), ptr(out32), stream_handle()), "pack_gather")
 
 
-def grad_assemble(red, ptr_, src, grad, scale=1.0):
-    """grad[p] = scale * sum(red[src[ptr[p]:ptr[p+1]]]) for every flat parameter p (one launch,
-    fixed order). ptr (n+1,) / src int32 from a host-built CSR (validated by the caller)."""
+def grad_assemble(red, ptr_, src, grad, scale=1.0, gscale=None):
+    """grad[p] = scale * sum(red[src[ptr[p]:ptr[p+1]]]) (/ *gscale: the device loss scale) for
+    every flat parameter p (one launch, fixed order). ptr (n+1,) / src int32 from a host-built CSR
+    (validated by the caller)."""
     n = grad.numel()
     check(red, torch.float32, None, "red")
     check(ptr_, torch.int32, (n + 1,), "ptr")
     check(src, torch.int32, None, "src")
     check(grad, torch.float32, None, "grad")
-    _ok(lib().grad_assemble(ptr(red), ptr(ptr_), ptr(src), n, float(scale), ptr(grad), stream_handle()),
+    check(gscale, torch.float32, (1,), "gscale")
+    _ok(lib().grad_assemble(ptr(red), ptr(ptr_), ptr(src), n, float(scale), ptr(gscale), ptr(grad), stream_handle()),
         "grad_assemble")
 
 
 def grad_check(g, ok):
-    """ok (int32, preset to 1) <- 0 if any element of g is not finite. No host sync."""
+    """ok (int32, 1 between steps: step_commit resets it) <- 0 if any element of g is not finite.
+    No host sync."""
     check(g, torch.float32, None, "g")
     check(ok, torch.int32, None, "ok")
     _ok(lib().grad_check(ptr(g), g.numel(), ptr(ok), stream_handle()), "grad_check")
 
 
-def adam_commit(ok, steps, mask, skipped):
-    """steps[g] += 1 for the groups in mask if *ok, else skipped += 1 (device counters)."""
-    check(ok, torch.int32, None, "ok")
+def step_commit(ok, steps, mask, skipped, *, gscale=None, good=None, growth=1000, max_scale=2.0 ** 24,
+                stats_row=None):
+    """End of an optimizer step on the device: steps[g] += 1 for the groups in mask if *ok, else
+    skipped += 1; fp16 (gscale, good): the dynamic loss scale halves on a skipped step and doubles
+    after `growth` finite ones; stats_row[16:18] = [skipped, loss scale]; *ok reset to 1."""
+    check(ok, torch.int32, (1,), "ok")
     check(steps, torch.int32, None, "steps")
-    check(skipped, torch.int32, None, "skipped")
-    _ok(lib().adam_commit(ptr(ok), ptr(steps), int(mask), steps.numel(), ptr(skipped), stream_handle()),
-        "adam_commit")
+    check(skipped, torch.int32, (1,), "skipped")
+    check(gscale, torch.float32, (1,), "gscale")
+    check(good, torch.int32, (1,), "good")
+    if (gscale is None) != (good is None):
+        raise NativeError("gscale and good go together")
+    if stats_row is not None and (stats_row.dtype != torch.float32 or stats_row.numel() < 18
+                                  or not stats_row.is_contiguous()):
+        raise NativeError("stats_row must be a contiguous float32 row of >= 18")
+    _ok(lib().step_commit(ptr(ok), ptr(steps), int(mask), steps.numel(), ptr(skipped), ptr(gscale), ptr(good),
+                          int(growth), float(max_scale), ptr(stats_row), stream_handle()), "step_commit")
+
+
+def stats_pack(sums, counts, local, row):
+    """row[:18] = [sums (10) | counts (3) | local (3) | 0 | 1] (one launch; utils.metrics.StepStats)."""
+    check(sums, torch.float32, None, "sums")
+    check(counts, torch.float32, None, "counts")
+    check(local, torch.float32, None, "local")
+    if sums.numel() < 10 or counts.numel() < 3 or local.numel() < 3:
+        raise NativeError("stats_pack needs 10 sums, 3 counts, 3 local values")
+    if row.dtype != torch.float32 or row.numel() < 18 or not row.is_contiguous():
+        raise NativeError("row must be a contiguous float32 row of >= 18")
+    _ok(lib().stats_pack(ptr(sums), ptr(counts), ptr(local), ptr(row), stream_handle()), "stats_pack")

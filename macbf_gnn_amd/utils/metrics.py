@@ -33,12 +33,13 @@ class StepStats(collections.abc.MutableMapping):
 
     raw = [10 loss partial sums (slots 2..9: barrier / derivative hinge sums and accuracy
     counts), n_dang, n_safe, n_act (global pooled counts), agent-steps, safe agents, action-loss
-    sum (this rank)]."""
+    sum (this rank) (, skipped step, loss scale: written by the optimizer's commit kernel)]."""
 
     RAW = 16
 
     def __init__(self, raw: torch.Tensor, T, extra=None):
         self.raw = raw
+        self.scaled = False          # fp16: report the loss scale (raw[17])
         self._T = T
         self.extra = dict(extra or {})
         self._host = None
@@ -57,6 +58,10 @@ class StepStats(collections.abc.MutableMapping):
             d["loss_total"] = C.LOSS_SCALE * (w[0] * d["loss_dang"] + w[1] * d["loss_safe"] + w[2] * d["loss_dang_deriv"]
                                               + w[3] * d["loss_safe_deriv"] + w[4] * d["loss_action"])
             d["T"] = float(self._T)
+            if len(v) >= 18:
+                d["skipped"] = v[16]
+                if self.scaled:
+                    d["grad_scale"] = v[17]
             for k, x in self.extra.items():
                 d[k] = float(x) if isinstance(x, torch.Tensor) else x
             self._host = d

@@ -115,10 +115,12 @@ class FlatAdam:
         else:
             self._steps[name] = int(step)
 
-    def step(self, groups=None, ok=None):
+    def step(self, groups=None, ok=None, gscale=None, good=None, growth=1000, stats_row=None):
         """One Adam step of the named ranges. On HIP, ok (device int32 flag, optional) gates the
         whole step on the device: 0 leaves parameters, moments and step counts untouched and
-        counts a skipped step."""
+        counts a skipped step; the commit kernel then re-arms the flag. gscale / good (fp16): the
+        device loss scale and finite-step count, updated by the commit kernel (``native.step_commit``);
+        stats_row: the iteration's statistics row (skipped flag and loss scale written into it)."""
         groups = list(self.fp.ranges) if groups is None else list(groups)
         if self.on_device:
             from ..ops import native
@@ -131,7 +133,8 @@ class FlatAdam:
                             self.lr, self.betas[0], self.betas[1], self.eps, self.wd, 1, ok=flag,
                             step_dev=self._dsteps[gi:gi + 1])
                 mask |= 1 << gi
-            native.adam_commit(flag, self._dsteps, mask, self.dskipped)
+            native.step_commit(flag, self._dsteps, mask, self.dskipped, gscale=gscale, good=good, growth=growth,
+                               stats_row=stats_row)
             return
         for name in groups:
             a, b = self.fp.ranges[name]
