@@ -12,6 +12,10 @@ namespace mb {
 // them -- do not depend on the order in which waves finish. value = sum / FX_*.
 constexpr double FX_DIST = 4294967296.0;   // 2^32: per-env distance sums < 2^31 for any env size here
 constexpr double FX_ACT = 16777216.0;      // 2^24: per-env action-term sums < 2^39
+// per-agent saturation of the fixed-point terms: a non-finite (diverged) or absurdly large term
+// becomes 2^46 (a goal distance of 2^14), so its env never looks done (mean >= 2^14 / N > 0.07 for
+// any N here) and an action sum >= FX_SAT is reported as NaN; 2^17 saturated agents fit an int64
+constexpr double FX_SAT = 70368744177664.0;   // 2^46
 
 struct CellSortArgs {
   const float4* S;  long s_env;      // node (b,i) record at S[(b*s_env + i) * rec]
@@ -361,5 +365,6 @@ int mb_pack_gather(const float* src, int n, const int* idx16, int m16, unsigned 
 int mb_step_commit(const mb::StepCommitArgs* a, hipStream_t st);
 int mb_stats_pack(const float* sums, const float* counts, const float* local, float* row, hipStream_t st);
 int mb_probe_mfma(const void* a, const void* b, float* d, hipStream_t st);
+int mb_probe_smfmac(const void* a, const void* b, const int* idx, float* d, hipStream_t st);
 int mb_probe_tr(const void* img, int rows, int stride, int e0, int m0, void* out, hipStream_t st);
 }

@@ -178,7 +178,10 @@ __global__ __launch_bounds__(RS_BLOCK) void rollout_stats_kernel(RolloutStatsArg
         v[1] += a.cnt[(t * a.B + b) * 2 + 1];
         v[2] += (float)a.N;
         if (a.safe) v[3] += a.safe[(t + 1) * a.B + b];
-        if (a.act) v[4] += (float)((double)a.act[t * a.B + b] / FX_ACT);
+        if (a.act) {   // a saturated (diverged) agent term: the action loss is not a number
+          const unsigned long long q = a.act[t * a.B + b];
+          v[4] += (double)q >= FX_SAT ? __builtin_nanf("") : (float)((double)q / FX_ACT);
+        }
       }
       done = done || ((float)((double)a.dist[t * a.B + b] / FX_DIST) / (float)a.N < a.thr);
     }

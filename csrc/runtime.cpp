@@ -76,6 +76,7 @@ class RolloutDriver {
       std::memset(pub_host_, 0, bytes);
       chk(hipHostGetDevicePointer((void**)&pub_dev_, pub_host_, 0), "hipHostGetDevicePointer");
       chk(hipMalloc((void**)&pub_ctr_, (size_t)Tmax_ * sizeof(unsigned)), "hipMalloc");
+      chk(hipMemset(pub_ctr_, 0, (size_t)Tmax_ * sizeof(unsigned)), "hipMemset");   // once: kernels re-arm them
     }
     if (check_ < 1) check_ = 1;
     if (B_ < 1|| N_ < 1 || Nn_ < N_ || K_ < 1 || K_ > 16 || (D_ != 2 && D_ != 3) || Tmax_ < 1 || resort_ < 1)
@@ -110,8 +111,7 @@ class RolloutDriver {
     // published early stop: the controller kernels hand the per-env sums to the host (no marker)
     const bool pub = publish_ && early_stop;
     if (pub) {
-      ++gen_;
-      chk(hipMemsetAsync(pub_ctr_, 0, (size_t)Tmax_ * sizeof(unsigned), st), "hipMemsetAsync");
+      ++gen_;      // the per-step counters are zero: set at allocation, re-armed by the last workgroup
       hd = pub_host_;
     }
     for (int t = 0; t < Tmax_; ++t) {

@@ -51,6 +51,10 @@ DEV int hilbert32(int x, int y) {
   return d;
 }
 
+// cell coordinate 0..31 of a scaled position; NaN (a diverged state) and out-of-range values clamp
+// (a float -> int conversion of NaN / out-of-range values is undefined)
+DEV int grid_cell(float x) { return x >= 1.f ? (x < 31.f ? (int)x : 31) : 0; }
+
 __global__ __launch_bounds__(SORT_BLOCK) void cell_sort_kernel(CellSortArgs a) {
   __shared__ int hist[CURVE_BINS];
   __shared__ int wsum[SORT_BLOCK / WAVE];
@@ -62,8 +66,8 @@ __global__ __launch_bounds__(SORT_BLOCK) void cell_sort_kernel(CellSortArgs a) {
   const float inv = 32.f / a.L;
   for (int i = threadIdx.x; i < a.N; i += SORT_BLOCK) {
     const float4 s = Sb[i * R];
-    const int cx = min(31, max(0, (int)(s.x * inv)));
-    const int cy = min(31, max(0, (int)(s.y * inv)));
+    const int cx = grid_cell(s.x * inv);
+    const int cy = grid_cell(s.y * inv);
     atomicAdd(&hist[hilbert32(cx, cy)], 1);
   }
   __syncthreads();
@@ -88,8 +92,8 @@ __global__ __launch_bounds__(SORT_BLOCK) void cell_sort_kernel(CellSortArgs a) {
   int* perm = a.perm + (long)b * a.N;
   for (int i = threadIdx.x; i < a.N; i += SORT_BLOCK) {
     const float4 s = Sb[i * R];
-    const int cx = min(31, max(0, (int)(s.x * inv)));
-    const int cy = min(31, max(0, (int)(s.y * inv)));
+    const int cx = grid_cell(s.x * inv);
+    const int cy = grid_cell(s.y * inv);
     const int p = atomicAdd(&hist[hilbert32(cx, cy)], 1);
     perm[p] = i;
   }

@@ -182,10 +182,10 @@ class HipEngine:
         if Gp < 1 or B % Gp:
             raise ValueError(f"bptt_groups={Gp} must divide num_envs={B}")
         self.grp_nb = native.ctrl_bwd_grids((B // Gp) * N, dev, self.prec)
-        rows_n = max(self.nb_node, Gp * self.grp_nb[0])
-        rows_e = max(self.nb_edge, Gp * self.grp_nb[1])
-        # slab rows written by the launch-per-step BPTT / by the persistent one (one row per env)
-        self.slab_rows = (rows_n, rows_e)
+        # slab rows each BPTT path writes (and the slab reduction reads): exactly those, so rows no
+        # path writes are never summed (the persistent small-scene BPTT: one row per env)
+        self.slab_rows = (self.nb_node, self.nb_edge) if Gp == 1 else (Gp * self.grp_nb[0], Gp * self.grp_nb[1])
+        rows_n, rows_e = self.slab_rows
         self.part_node = torch.zeros(max(rows_n, B), native.CTRL_NODE_PARTIAL, dtype=f32, device=dev)
         self.part_edge = torch.zeros(max(rows_e, B), native.CTRL_EDGE_PARTIAL, dtype=f32, device=dev)
         self.gstreams = [torch.cuda.Stream(device=dev) for _ in range(Gp - 1)]

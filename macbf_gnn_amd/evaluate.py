@@ -40,6 +40,9 @@ class EvalConfig:
     seed: int = 0
     early_stop: bool = True
     diagnose: bool = False      # dense all-pairs check: are the flagged pairs top-K neighbours?
+    refine_space: str = "actions"   # "actions" (upstream MACBF) or "gains": refine only the PD gains
+                                    # of the reference controller law (controller.py:53-61) -- what
+                                    # the trained policy class itself can express
 
 
 def _knn(s, k):
@@ -86,6 +89,42 @@ def refine_actions(cbf, s, a, idx, loops: int = C.REFINE_LOOPS, lr: float = C.RE
     return (a + delta).detach(), int(used), float(viol.detach())
 
 
+def _pd_action(s, g, y):
+    """The reference PD law a_d = -(k_2d (p_d - g_d) + k_2d+1 v_d), k = 2 sigmoid(y) + 0.2."""
+    D = s.shape[-1] // 2
+    k = 2.0 * torch.sigmoid(y) + 0.2
+    return torch.stack([-(k[..., 2 * q] * (s[..., q] - g[..., q]) + k[..., 2 * q + 1] * s[..., D + q])
+                        for q in range(D)], dim=-1)
+
+
+def refine_gains(cbf, s, g, k0, idx, loops: int = C.REFINE_LOOPS, lr: float = C.REFINE_LEARNING_RATE,
+                 check_every: int = 10):
+    """refine_actions restricted to the controller's action space: gradient steps on the gain
+    pre-activations y (k = 2 sigmoid(y) + 0.2, started at the network's gains k0) instead of free
+    actions."""
+    with torch.no_grad():
+        h = cbf(s, idx=idx)
+        u = ((k0 - 0.2) / 2.0).clamp(1e-6, 1 - 1e-6)
+        y = torch.log(u / (1 - u))
+    y = y.clone().requires_grad_(True)
+    viol = torch.zeros((), device=s.device)
+    used = torch.zeros((), dtype=torch.int64, device=s.device)
+    for it in range(1, loops + 1):
+        a = _pd_action(s, g, y)
+        s_next = s + torch.cat([s[..., 2:], a], -1) * C.TIME_STEP
+        hn = cbf(s_next, idx=idx)
+        viol = torch.relu(-(hn - h + C.TIME_STEP * C.ALPHA_CBF * h)).sum()
+        pending = viol.detach() > 0
+        used += pending.long()
+        if it % check_every == 0 and not bool(pending):
+            break
+        gy, = torch.autograd.grad(viol, y)
+        with torch.no_grad():
+            y -= lr * gy
+    with torch.no_grad():
+        return _pd_action(s, g, y), int(used), float(viol.detach())
+
+
 def _unsafe_diag(s_next, idx):
     """(unsafe agents, unsafe agents whose every flagged pair is one of their top-K neighbours at
     the step's graph) -- do the controller / CBF see the pairs that the safety check flags?"""
@@ -111,7 +150,12 @@ def rollout_eval(controller, cbf, s0, g, cfg: EvalConfig) -> Dict[str, float]:
         idx = _knn(s, k)
         with torch.no_grad():
             a = controller(s, g, idx=idx)
-        if cfg.refine:
+        if cfg.refine and cfg.refine_space == "gains":
+            with torch.no_grad():
+                _, aux = oracle.controller_forward(controller.params_dict(), s, g, idx, return_aux=True)
+            a, it, _ = refine_gains(cbf, s, g, aux["gains"], idx, cfg.refine_loops, cfg.refine_lr)
+            refine_iters += it
+        elif cfg.refine:
             a, it, _ = refine_actions(cbf, s, a, idx, cfg.refine_loops, cfg.refine_lr)
             refine_iters += it
         with torch.no_grad():

@@ -67,13 +67,14 @@ def cmd_eval(args):
     dev = resolve_device("auto")
     rows = []
     for m in args.models.split(","):
-        for refine in (False, True):
+        for refine in ((False, "actions"), (True, "actions"), (True, "gains")):
+            refine, space = refine
             ctrl, cbf = _load(m, dev)
             cfg = EvalConfig(num_agents=args.agents, num_envs=1, episodes=args.episodes, refine=refine,
-                             seed=args.seed, diagnose=True)
+                             seed=args.seed, diagnose=True, refine_space=space)
             t0 = time.time()
             r = evaluate(ctrl, cbf, cfg, device=dev)
-            r.update(model=os.path.basename(m), refine=refine, agents=args.agents, episodes=args.episodes,
+            r.update(model=os.path.basename(m), refine=refine and space, agents=args.agents, episodes=args.episodes,
                      seconds=round(time.time() - t0, 1))
             rows.append(r)
             print(json.dumps(r), flush=True)
