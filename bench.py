@@ -13,8 +13,10 @@ G / world of them. Random-init weights, synthetic scenarios from the on-device s
 seed, iteration and rank).
 
 Precision (--dtype): fp32 (default) is the reference precision (/root/reference is fp32 end to
-end): the fp32-accurate 3-term split-bf16 MFMA kernels. bf16 / fp16 are the faster 16-bit-input
-modes (fp16 with dynamic loss scaling).
+end): the near-fp32 3-term split-bf16 MFMA kernels (each operand hi + lo, ~16 significant bits;
+hi*hi + hi*lo + lo*hi, fp32 accumulation: ~2^-16 relative per product, tighter than the TF32 path
+cuDNN uses for the reference's Conv1d layers). bf16 / fp16 are the faster 16-bit-input modes (fp16
+with dynamic loss scaling). Default window: 20 timed steps after 5 warm-up steps.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--dtype fp32|bf16|fp16] [--global_envs G]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
@@ -40,8 +42,8 @@ CPU_ROLLOUT_PROXY = 93009.0
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--agents", type=int, default=1024)
     ap.add_argument("--envs", type=int, default=64, help="environments per rank (weak scaling)")
     ap.add_argument("--global_envs", type=int, default=0,
@@ -128,7 +130,8 @@ def main():
         "skipped_steps": tr.skipped_steps,
         "graph": args.graph,
         "dp_backend": dp.backend,
-        "precision": {"fp32": "fp32-accurate: 3-term split-bf16 MFMA (hi*hi + hi*lo + lo*hi), fp32 accumulate",
+        "precision": {"fp32": "near-fp32: 3-term split-bf16 MFMA (hi*hi + hi*lo + lo*hi, ~2^-16 relative per "
+                              "product), fp32 accumulate; fp32 distances, TTC, losses, Adam",
                       "bf16": "bf16 MFMA inputs, fp32 accumulate", "fp16": "fp16 MFMA inputs, fp32 accumulate, "
                       "dynamic loss scaling"}[args.dtype],
         "cpu_rollout_proxy": {"value": CPU_ROLLOUT_PROXY, "comparable": False,

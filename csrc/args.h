@@ -223,6 +223,17 @@ struct CtrlNodeBwdArgs {
   int init;                            // 1: the slabs are written, not accumulated (first BPTT step)
   int chunk;                           // agents per workgroup chunk: 32, 64 or 128 (0 = 128); small
                                        // scenes use smaller chunks to spread over more CUs
+  // Fused BPTT combine (ctrl.hip fused_combine; cdS != null): G_{t+1} = dS_{t+1} + ego_{t+1} +
+  // the edge terms of dEc_{t+1} + the Euler adjoint of G_{t+2} is formed per agent in the prologue
+  // (replacing a node_combine launch between reverse steps), used as Gn and written to cGout
+  const float4* cdS;   long cds_env;   // dS_{t+1} (B,N) view
+  const float4* cego;                  // ego_{t+1} (B,N) contiguous (this kernel then overwrites ego)
+  const float4* cdEc;                  // dEc_{t+1} (B,N,K) contiguous
+  const int* cptr;     long cptr_env;  // reverse CSR of graph t+1 (per env strides)
+  const int* cedges;   long cedges_env;
+  const float4* cGn;   long cgn_env;   // G_{t+2} (or null)
+  float4* cGout;       long cgo_env;   // G_{t+1} out
+  int K;
 };
 
 struct CtrlEdgeBwdArgs {

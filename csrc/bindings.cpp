@@ -242,9 +242,20 @@ static int adam(u64 param, u64 grad, u64 m, u64 v, int lo, int hi, float b1, flo
 static int ctrl_node_bwd(u64 pooled, long p_env, u64 S, long s_env, u64 G, u64 A, long a_env, u64 Gn, long gn_env,
                          u64 valid, long v_env, int B, int N, u64 wrm, int o1, int o2, int o3, int o4, u64 wvec,
                          float act_coef, u64 act_scale, float dt, float sqrt3, u64 dP, long dp_env, u64 ego, u64 partial,
-                         int dim, int num_blocks, int prec, int init, int chunk, u64 gscale, u64 stream) {
+                         int dim, int num_blocks, int prec, int init, int chunk, u64 gscale, py::tuple cmb,
+                         u64 stream) {
   mb::CtrlNodeBwdArgs a{};
   a.gscale = P<const float>(gscale);
+  if (cmb.size() == 13) {     // fused BPTT combine: (dS, ds_env, ego, dEc, ptr, ptr_env, edges, edges_env, Gn, gn_env,
+                              //                     Gout, go_env, K)
+    a.cdS = P<const float4>(cmb[0].cast<u64>()); a.cds_env = cmb[1].cast<long>();
+    a.cego = P<const float4>(cmb[2].cast<u64>()); a.cdEc = P<const float4>(cmb[3].cast<u64>());
+    a.cptr = P<const int>(cmb[4].cast<u64>()); a.cptr_env = cmb[5].cast<long>();
+    a.cedges = P<const int>(cmb[6].cast<u64>()); a.cedges_env = cmb[7].cast<long>();
+    a.cGn = P<const float4>(cmb[8].cast<u64>()); a.cgn_env = cmb[9].cast<long>();
+    a.cGout = P<float4>(cmb[10].cast<u64>()); a.cgo_env = cmb[11].cast<long>();
+    a.K = cmb[12].cast<int>();
+  }
   a.init = init;
   a.chunk = chunk;
   a.dim = dim;

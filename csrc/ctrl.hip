@@ -813,6 +813,55 @@ DEV void store_tile_add(float* dst, int ncols, int mt, int nt, const f32x16& old
   for (int reg = 0; reg < 16; ++reg) dst[(32 * mt + acc_row(reg, h)) * ncols + 32 * nt + r] = old[reg] + c[reg];
 }
 
+// Fused BPTT combine (replaces the node_combine launch between two reverse steps): G_{t+1} of
+// agent i = dS_{t+1} + ego_{t+1} + sum_k dEc[i,k] - sum_in dEc[e] + the Euler adjoint of G_{t+2},
+// the terms and addition order of combine.h combine_node. The agent's two lane halves (h) split
+// its out- and in-edges, one lane swap adds the halves: fixed order, deterministic. All lanes
+// call it (lane swaps); lanes without an agent get zeros. Both halves return G_{t+1}; half 0
+// stores it (the next reverse step's Euler term).
+template <int D>
+DEV void fused_combine(const CtrlNodeBwdArgs& a, bool ok, int b, int i, int h, float (&gp)[D], float (&gv)[D]) {
+  constexpr int R = REC<D>;
+  const int N = a.N, K = a.K;
+  float4 g[R];
+#pragma unroll
+  for (int q = 0; q < R; ++q) g[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+  float dp[D], dv[D], ep[D], ev[D], np_[D], nv[D];
+#pragma unroll
+  for (int q = 0; q < D; ++q) { dp[q] = dv[q] = ep[q] = ev[q] = np_[q] = nv[q] = 0.f; }
+  if (ok) {
+    load_rec<D>(a.cdS + (long)b * a.cds_env * R, (unsigned)i, dp, dv);
+    load_rec<D>(a.cego + (long)b * N * R, (unsigned)i, ep, ev);
+    if (a.cGn) load_rec<D>(a.cGn + (long)b * a.cgn_env * R, (unsigned)i, np_, nv);
+    const float4* dE = a.cdEc + (long)b * N * K * R;
+    for (int k = h; k < K; k += 2) acc_rec<R, 1>(g, dE + ((long)i * K + k) * R);
+    const int* ptr = a.cptr + (long)b * a.cptr_env;
+    const int* edges = a.cedges + (long)b * a.cedges_env;
+    const int q0 = ptr[i], q1 = ptr[i + 1];
+    for (int q = q0 + h; q < q1; q += 2) acc_rec<R, -1>(g, dE + (long)edges[q] * R);
+  }
+#pragma unroll
+  for (int q = 0; q < R; ++q) {
+    g[q].x += shfl_xor32(g[q].x); g[q].y += shfl_xor32(g[q].y);
+    g[q].z += shfl_xor32(g[q].z); g[q].w += shfl_xor32(g[q].w);
+  }
+  float eg_p[D], eg_v[D];
+  if (D == 2) { eg_p[0] = g[0].x; eg_p[1] = g[0].y; eg_v[0] = g[0].z; eg_v[1] = g[0].w; }
+  else { eg_p[0] = g[0].x; eg_p[1] = g[0].y; eg_p[2] = g[0].z; eg_v[0] = g[R - 1].x; eg_v[1] = g[R - 1].y; eg_v[2] = g[R - 1].z; }
+#pragma unroll
+  for (int q = 0; q < D; ++q) {
+    gp[q] = dp[q] + ep[q];
+    gv[q] = dv[q] + ev[q];
+    gp[q] += eg_p[q];
+    gv[q] += eg_v[q];
+    if (a.cGn) {
+      gp[q] += np_[q];
+      gv[q] += nv[q] + a.dt * np_[q];
+    }
+  }
+  if (ok && h == 0 && a.cGout) store_rec<D>(a.cGout + (long)b * a.cgo_env * R, (unsigned)i, gp, gv);
+}
+
 // Node backward over the chunks c0, c0 + cstride, ... of `a` (smem: the kernel's dynamic LDS;
 // P: this workgroup's slab row)
 template <int D>
@@ -883,7 +932,7 @@ constexpr int NB_PREFETCH = 1;
         gg[q] = a.G[((long)b * N + i) * D + q];
         av[q] = a.A[((long)b * a.a_env + i) * D + q];
       }
-      if (a.Gn) load_rec<D>(a.Gn + (long)b * a.gn_env * REC<D>, (unsigned)i, gnp, gnv);
+      if (a.Gn && !a.cdS) load_rec<D>(a.Gn + (long)b * a.gn_env * REC<D>, (unsigned)i, gnp, gnv);
       vld = a.valid ? (a.valid[(long)b * a.v_env] != 0) : true;
       if (!NB_PREFETCH) {
         const h16* prow = a.pooled + (long)b * a.p_env + (long)i * PROW;
@@ -898,6 +947,7 @@ constexpr int NB_PREFETCH = 1;
 #pragma unroll
       for (int kk = 0; kk < 8; ++kk) Pf[kk] = Pn[kk];
     }
+    if (a.cdS) fused_combine<D>(a, ok, b, i, h, gnp, gnv);      // G_{t+1} (all lanes: lane swaps)
     float ex[D];
 #pragma unroll
     for (int q = 0; q < D; ++q) ex[q] = sp[q] - gg[q];
@@ -1741,11 +1791,22 @@ __global__ __launch_bounds__(NB_WAVES * 64, 1) void bptt_small_kernel(BpttSmallA
   float4* dEcb = ba.eb.dEc + (long)b * nk * R;
   for (int t = T - 1; t >= 0; --t) {
     const long tb = (long)t * B + b;
-    // G_{t+1} = dL/ds_{t+1}: the direct terms dS_T for the last step, else the combined Gb
-    const float4* Gn = (t == T - 1 ? ba.cb.dS : ba.cb.Gout) + (tb + B) * N * R;
+    // G_{t+1} = dL/ds_{t+1}: the direct terms dS_T for the last step, else combined in the node
+    // phase's prologue from step t+1's records (fused_combine) and written to Gb[t+1]
+    const float4* Gn = ba.cb.dS + (tb + B) * N * R;
     const float4* St = ba.nb.S + tb * Nn * R;
     {
       CtrlNodeBwdArgs a = ba.nb;
+      a.cdS = nullptr;
+      a.K = K;
+      if (t < T - 1) {
+        a.cdS = ba.cb.dS + (tb + B) * N * R; a.cds_env = N;
+        a.cego = egb; a.cdEc = dEcb;
+        a.cptr = ba.cb.ptr + (tb + B) * (Nn + 1); a.cptr_env = Nn + 1;
+        a.cedges = ba.cb.edges + (tb + B) * nk; a.cedges_env = nk;
+        a.cGn = (t + 1 == T - 1 ? ba.cb.dS : ba.cb.Gout) + (tb + 2 * B) * N * R; a.cgn_env = N;
+        a.cGout = ba.cb.Gout + (tb + B) * N * R; a.cgo_env = N;
+      }
       a.pooled = ba.nb.pooled + tb * N * PROW; a.p_env = (long)N * PROW;
       a.S = St; a.s_env = Nn;
       a.G = ba.nb.G + (long)b * N * D;
@@ -1772,22 +1833,8 @@ __global__ __launch_bounds__(NB_WAVES * 64, 1) void bptt_small_kernel(BpttSmallA
       a.init = t == T - 1;
       edge_bwd_call<D>(a, smem, Pe);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // dEc stores complete (read by the next node phase)
     __syncthreads();
-    if (t > 0) {        // G_0 is not needed (s_0 is sampled)
-      CombineArgs a = ba.cb;
-      a.dS = ba.cb.dS + tb * N * R; a.ds_env = N;
-      a.ego = egb;
-      a.dEc = dEcb;
-      a.ptr = ba.cb.ptr + tb * (Nn + 1); a.ptr_env = Nn + 1;
-      a.edges = ba.cb.edges + tb * nk; a.edges_env = nk;
-      a.Gn = Gn; a.gn_env = N;
-      a.Gout = ba.cb.Gout + tb * N * R; a.go_env = N;
-      a.B = 1;
-      for (int node = threadIdx.x / RG; node < N; node += NB_WAVES * WAVE / RG) combine_node<D>(a, node, threadIdx.x % RG);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-    }
   }
 }
 

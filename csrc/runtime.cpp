@@ -391,7 +391,7 @@ class BpttDriver {
     const long BN = (long)B_ * N_;
     const long nk = (long)N_ * K_;
     for (int t = T - 1; t >= 0; --t) {
-      const float4* Gn = t == T - 1 ? P<const float4>(dS_) + (long)T * BN * R_ : P<const float4>(Gb_) + (long)(t + 1) * BN * R_;
+      const float4* Gn = P<const float4>(dS_) + (long)T * BN * R_;       // t = T-1: the direct terms dS_T
       const float4* St = P<const float4>(S_) + (long)t * B_ * Nn_ * R_;
       {
         mb::CtrlNodeBwdArgs a{};
@@ -409,6 +409,18 @@ class BpttDriver {
         a.dP = P<h16>(dP_); a.dp_env = (long)N_ * prow_; a.ego = P<float4>(ego_); a.partial = P<float>(part_node_);
         a.init = t == T - 1;     // the first step of the reverse loop writes the slabs
         a.chunk = node_chunk_;
+        a.K = K_;
+        if (t < T - 1) {
+          // fused BPTT combine: G_{t+1} from step t+1's records (dS, ego, dEc, graph t+1, G_{t+2})
+          const long t1 = t + 1;
+          a.cdS = P<const float4>(dS_) + t1 * BN * R_; a.cds_env = N_;
+          a.cego = P<const float4>(ego_); a.cdEc = P<const float4>(dEc_);
+          a.cptr = P<const int>(rptr_) + t1 * B_ * (Nn_ + 1); a.cptr_env = Nn_ + 1;
+          a.cedges = P<const int>(redges_) + t1 * B_ * nk; a.cedges_env = nk;
+          a.cGn = (t1 == T - 1 ? P<const float4>(dS_) + (long)T * BN * R_ : P<const float4>(Gb_) + (t1 + 1) * BN * R_);
+          a.cgn_env = N_;
+          a.cGout = P<float4>(Gb_) + t1 * BN * R_; a.cgo_env = N_;
+        }
         chk((prec_ == 2 ? mb_ctrl_node_bwd_x3 : prec_ == 1 ? mb_ctrl_node_bwd_f16 : mb_ctrl_node_bwd)(&a, nb_node_, st), "ctrl_node_bwd");
       }
       {
@@ -424,18 +436,8 @@ class BpttDriver {
         a.init = t == T - 1;
         chk((prec_ == 2 ? mb_ctrl_edge_bwd_x3 : prec_ == 1 ? mb_ctrl_edge_bwd_f16 : mb_ctrl_edge_bwd)(&a, nb_edge_, st), "ctrl_edge_bwd");
       }
-      if (t > 0) {   // G_0 = dL/ds_0 is not needed (s_0 is sampled, not a function of the weights)
-        mb::CombineArgs a{};
-        a.dim = D_;
-        a.dS = P<const float4>(dS_) + (long)t * BN * R_; a.ds_env = N_;
-        a.ego = P<const float4>(ego_); a.dEc = P<const float4>(dEc_);
-        a.ptr = P<const int>(rptr_) + (long)t * B_ * (Nn_ + 1); a.ptr_env = Nn_ + 1;
-        a.edges = P<const int>(redges_) + (long)t * B_ * nk; a.edges_env = nk;
-        a.Gn = Gn; a.gn_env = N_;
-        a.Gout = P<float4>(Gb_) + (long)t * BN * R_; a.go_env = N_;
-        a.B = B_; a.N = N_; a.K = K_; a.dt = dt_;
-        chk(mb_node_combine(&a, st), "node_combine");
-      }
+      // (no combine launch: the next step's node backward forms G_t in its prologue; G_0 = dL/ds_0
+      // is not needed -- s_0 is sampled, not a function of the weights)
     }
   }
 

@@ -455,7 +455,9 @@ __global__ __launch_bounds__(BS) void scan_kernel(ScanArgs a) {
 #pragma unroll
         for (int u = 1; u < LPA; ++u)
           if (q0 + u < K) key = (h == u) ? bk[q0 + u] : key;
-        const int j = (int)(unsigned)key;
+        // an agent whose distances are all NaN (a diverged state) finds no candidate: its unfilled
+        // slots name the agent itself, so every gather downstream stays in range
+        const int j = key == KEY_EMPTY ? i : (int)(unsigned)key;
         out[q] = j;
         float pj[D], vj[D], dp[D], dv[D];
         load_rec<D>(Sb, (unsigned)j, pj, vj);

@@ -13,7 +13,8 @@ backward
     cbf_bwd (fused) -> h(s_t), h'(s_{t+1}) on the same slots, loss sums, dL/dh, dL/dh' formed
                       in-kernel, dL/d(s_i - s_j) per edge (h and h' paths) + CBF dW slabs
     rev_csr + node_reduce -> direct dL/ds_t (edge -> node, deterministic, no atomics)
-    for t = T-1..0 (BPTT):  ctrl_node_bwd -> ctrl_edge_bwd -> node_combine
+    for t = T-1..0 (BPTT):  ctrl_node_bwd (its prologue forms G_{t+1} from step t+1's records:
+                      the fused BPTT combine) -> ctrl_edge_bwd
                       (dA_t = dt*G_{t+1}[v] + action-loss grad; G_t = dL/ds_t)
     slab reductions -> the flat gradient buffer (then RCCL all-reduce + fused Adam).
 """
@@ -670,17 +671,20 @@ class HipEngine:
         for t in range(T - 1, -1, -1):
             if red_done is not None and t == ts - 1:
                 st.wait_event(red_done)                                # dS[0..ts) from the aux stream
-            Gn = self.dS[T][sl] if t == T - 1 else self.Gb[t + 1][sl]   # G_T = dL/ds_T (direct terms only)
-            native.ctrl_node_bwd(self.pooled[t][sl], self.S[t][sl], self.G[sl], self.A[t][sl], Gn, valid_u8[t][sl],
-                                 pw.ctrl_rm, pw.node_rm_off, pw.ctrl_v, gs * ACT_COEF, self.dP[sl], self.ego[sl],
-                                 part_node, nbn, act_cnt=self.counts[2:3], prec=self.prec, init=t == T - 1,
-                                 gscale=getattr(self.tr, "gscale_dev", None))
+            # G_{t+1}: the direct terms dS_T for t = T-1; else formed in the node kernel's prologue
+            # from step t+1's records (fused BPTT combine, written to Gb[t+1])
+            cmb = None
+            if t < T - 1:
+                cmb = dict(dS=self.dS[t + 1][sl], ego=self.ego[sl], dEc=self.dEc[sl], rptr=rptr3[t + 1][sl],
+                           redges=redges3[t + 1][sl], Gn=self.dS[T][sl] if t + 1 == T - 1 else self.Gb[t + 2][sl],
+                           Gout=self.Gb[t + 1][sl], K=K)
+            native.ctrl_node_bwd(self.pooled[t][sl], self.S[t][sl], self.G[sl], self.A[t][sl], self.dS[T][sl],
+                                 valid_u8[t][sl], pw.ctrl_rm, pw.node_rm_off, pw.ctrl_v, gs * ACT_COEF, self.dP[sl],
+                                 self.ego[sl], part_node, nbn, act_cnt=self.counts[2:3], prec=self.prec, init=t == T - 1,
+                                 gscale=getattr(self.tr, "gscale_dev", None), combine=cmb)
             native.ctrl_edge_bwd(self.S[t][sl], self.idx[t][sl], self.argmax[t][sl], self.dP[sl], pw.ctrl_w,
                                  pw.ctrl_off["ew1f"], pw.ctrl_off["ew2tn"], self.dEc[sl], part_edge, nbe, prec=self.prec,
                                  init=t == T - 1)
-            if t > 0:      # G_0 = dL/ds_0 is not needed (s_0 is sampled, not a function of the weights)
-                native.node_combine(self.dS[t][sl], self.ego[sl], self.dEc[sl], rptr3[t][sl], redges3[t][sl], Gn,
-                                    self.Gb[t][sl], K=K)
 
     def _counts_ready(self, work):
         """Join the (async) count all-reduce (the node backward reads the action-loss count

@@ -773,7 +773,7 @@ def ctrl_bwd_grids(total_agents: int, device, prec=None):
 
 
 def ctrl_node_bwd(pooled, S, G, A, Gn, valid_t, wrm, offs, wvec, act_coef, dP, ego, partial, num_blocks,
-                  act_cnt=None, prec=None, init=False, chunk=None, gscale=None):
+                  act_cnt=None, prec=None, init=False, chunk=None, gscale=None, combine=None):
     """act_cnt: optional 1-element device tensor holding the (all-reduced) action-loss count
     n_act; the action-loss coefficient is then act_coef / max(n_act, 1), read by the kernel (no
     host round trip, no extra launch). init: write the weight-gradient slabs instead of
@@ -798,13 +798,31 @@ def ctrl_node_bwd(pooled, S, G, A, Gn, valid_t, wrm, offs, wvec, act_coef, dP, e
     check(partial, torch.float32, (num_blocks, CTRL_NODE_PARTIAL), "partial")
     check(act_cnt, torch.float32, (1,), "act_cnt")
     check(gscale, torch.float32, (1,), "gscale")
+    cmb = ()
+    if combine is not None:
+        # fused BPTT combine: Gn is formed in the kernel from step t+1's records (node_combine's terms)
+        c = combine
+        K = int(c["K"])
+        _records(c["dS"], "combine dS", (B, N), W)
+        check(c["ego"], torch.float32, (B, N, W), "combine ego")
+        check(c["dEc"], torch.float32, (B, N, K, W), "combine dEc")
+        _rows(c["rptr"], c["rptr"].shape[1], "combine rptr", (B,))
+        _rows(c["redges"], N * K, "combine redges", (B,))
+        _records(c["Gn"], "combine Gn", (B, N), W)
+        _records(c["Gout"], "combine Gout", (B, N), W)
+        if c["rptr"].dtype != torch.int32 or c["redges"].dtype != torch.int32 or c["rptr"].shape[1] < N + 1:
+            raise NativeError("combine rptr / redges must be int32 CSR rows")
+        Gn_c = c["Gn"]
+        cmb = (ptr(c["dS"]), c["dS"].stride(0) // W, ptr(c["ego"]), ptr(c["dEc"]), ptr(c["rptr"]), c["rptr"].stride(0),
+               ptr(c["redges"]), c["redges"].stride(0), ptr(Gn_c), Gn_c.stride(0) // W if Gn_c is not None else 0,
+               ptr(c["Gout"]), c["Gout"].stride(0) // W, K)
     rc = lib().ctrl_node_bwd(ptr(pooled), pooled.stride(0), ptr(S), S.stride(0) // W, ptr(G), ptr(A), A.stride(0) // D,
                              ptr(Gn), Gn.stride(0) // W if Gn is not None else 0,
                              ptr(valid_t), valid_t.stride(0) if valid_t is not None else 0, B, N,
                              ptr(wrm), offs["w1"], offs["w2"], offs["w3"], offs["w4"], ptr(wvec),
                              float(act_coef), ptr(act_cnt), float(C.TIME_STEP), float(C.SQRT3), ptr(dP), dP.stride(0),
                              ptr(ego), ptr(partial), D, int(num_blocks), f16, int(bool(init)),
-                             int(chunk or node_bwd_chunk(B * N, S.device)), ptr(gscale), stream_handle())
+                             int(chunk or node_bwd_chunk(B * N, S.device)), ptr(gscale), cmb, stream_handle())
     _ok(rc, "ctrl_node_bwd")
 
 
