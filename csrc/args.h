@@ -1,5 +1,6 @@
 // Kernel argument structs shared by the HIP sources and the pybind11 layer.
 #pragma once
+#include <cstdlib>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -234,7 +235,14 @@ struct CtrlNodeBwdArgs {
   const float4* cGn;   long cgn_env;   // G_{t+2} (or null)
   float4* cGout;       long cgo_env;   // G_{t+1} out
   int K;
+  int coop;                            // set by the launchers: 32-agent chunks run node_bwd_coop
 };
+
+// MACBF_NODE_COOP=0 disables the cooperative 32-agent node backward (A/B runs)
+inline bool node_bwd_coop_enabled() {
+  static const bool on = [] { const char* e = getenv("MACBF_NODE_COOP"); return !(e && e[0] == '0'); }();
+  return on;
+}
 
 struct CtrlEdgeBwdArgs {
   const float4* S;     long s_env;     // node records (strides in records)

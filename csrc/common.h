@@ -603,6 +603,25 @@ DEV Fr wrm_acc_fr(const h16* W, int stride, int m0, int kk, int lane, int lo) {
   return r;
 }
 
+DEV Fr wrmT_nat_fr(const h16* W, int stride, int m0, int kk, int lane, int lo) {
+  Fr r;
+  r.h = wrmT_nat(W, stride, m0, kk, lane);
+  if constexpr (X3) r.l = wrmT_nat(W + lo, stride, m0, kk, lane);
+  return r;
+}
+
+// hi plane of a standard-orientation tile stored by store_tile (row = this lane's agent/edge,
+// regs = features col0 + acc_row(reg, h)): the inverse of store_tile, 4 x 8-byte reads
+DEV h16x16 load_tile_h(const h16* img, int stride, int erow, int col0, int h) {
+  h16x16 v;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const h16x4 q = *reinterpret_cast<const h16x4*>(img + erow * stride + col0 + 8 * g + 4 * h);
+    v[4 * g] = q[0]; v[4 * g + 1] = q[1]; v[4 * g + 2] = q[2]; v[4 * g + 3] = q[3];
+  }
+  return v;
+}
+
 DEV Fr wrmT_acc_fr(const h16* W, int stride, int m0, int kk, int lane, int lo) {
   Fr r;
   r.h = wrmT_acc(W, stride, m0, kk, lane);

@@ -1240,10 +1240,344 @@ constexpr int NB_PREFETCH = 1;
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// Cooperative node backward for 32-agent chunks (strong-scaling slices and small scenes, where
+// a workgroup holds one 32-agent chunk): in node_bwd_body one wave would run the whole
+// forward-recompute / backward MFMA chain of its 32 agents while three idle. Here the four waves
+// split every layer's 32-row output tiles and meet in LDS between layers: a layer's tiles are
+// stored agent-major into the stage region (natural feature order), read back by every wave as
+// natural-k B fragments (the weights as natural-k A fragments, wrm_nat / wrmT_nat), and the same
+// images are the operands of the weight-gradient contractions (one turn: 32 rows). Critical path
+// per chunk: about a quarter of the MFMA chain plus ~10 workgroup barriers. Same slab layout and
+// outputs (dP, ego, fused combine) as node_bwd_body; only the summation order of the weight
+// gradients differs (per tile owner instead of per turn).
+//   layer tiles -> waves: L1 {0,1} | L2 {0..3} | L3 {2,3} | L4 {0} (+ gain law, combine, ego) |
+//   dY3 {1,2} | dY2 {0..3} | dY1 {0,1} | dP {0..3} + the state tile on wave 0
+//   region columns (NC_SW per row, 32 rows, lo plane at NB_PL):
+//     [Y1 0..63]  -> [Y2 0..127] -> + [Y3 128..191] + [d4 192..223] + [d3 224..287]  (S4, S3)
+//     -> [d2 0..127 | Y1 128..191] (S2) -> [d1 0..63 | P, s 64..223] (S1)
+constexpr int NC_SW = 296;                           // 148 dwords: row reads spread over the banks
+static_assert(NC_SW * 32 <= NB_PL, "cooperative region must fit the stage plane");
+
+template <int D>
+DEV void node_bwd_coop(const CtrlNodeBwdArgs& a, unsigned char* smem, long c0, long cstride, float* P) {
+  constexpr int RM = (X3 ? 2 : 1) * NODE_RM_ELEMS;
+  constexpr int SW = NC_SW, PLN = NB_PL;
+  h16* wr = reinterpret_cast<h16*>(smem);
+  float* vl = reinterpret_cast<float*>(smem + RM * 2);
+  h16* stg = reinterpret_cast<h16*>(smem + RM * 2 + CTRL_VEC * 4);
+  block_copy16(wr, a.wrm, RM * 2);
+  block_copy16(vl, a.wvec, CTRL_VEC * 4);
+  __syncthreads();
+  const float* nb2 = vl + 128;
+  const float* nb3 = vl + 256;
+  const float* nb4 = vl + 320;
+  const int wave = threadIdx.x / WAVE, lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
+  const int N = a.N;
+  const int total = a.B * N;
+  const long nchunks = (total + 31) / 32;
+  constexpr int LO = NODE_RM_LO;
+  const h16x8 zz = zero_h8();
+  // owned weight-gradient tiles: S4 (dW4pad 1x2) wave < 2 nt = wave; S3 (2x4) t = wave + 4u;
+  // S2 (4x2) t = wave + 4u; S1 (2x5) t = wave + 4u (u < 3, t < 10)
+  f32x16 acc4 = zero16(), acc3[2], acc2[2], acc1[3];
+  float bs4 = 0.f, bs3[2] = {0.f, 0.f}, bs2[2] = {0.f, 0.f};
+#pragma unroll
+  for (int u = 0; u < 2; ++u) { acc3[u] = zero16(); acc2[u] = zero16(); }
+#pragma unroll
+  for (int u = 0; u < 3; ++u) acc1[u] = zero16();
+  const int n1 = (wave < 2) ? 3 : 2;
+  // B fragment (natural k) of image columns c0 + 16kk.. for this lane's agent row
+  auto img_fr = [&](int col0, int kk) { return row_fr(stg + r * SW + col0 + 16 * kk + 8 * h, PLN); };
+
+  for (long chunk = c0; chunk < nchunks; chunk += cstride) {
+    const int ga = (int)(chunk * 32) + r;
+    const bool ok = ga < total;
+    int b = 0, i = 0;
+    float sp[D], sv[D], gg[D], av[D], gnp[D], gnv[D];
+#pragma unroll
+    for (int q = 0; q < D; ++q) { sp[q] = sv[q] = gg[q] = av[q] = gnp[q] = gnv[q] = 0.f; }
+    bool vld = false;
+    if (ok) {
+      b = ga / N; i = ga - b * N;
+      load_rec<D>(a.S + (long)b * a.s_env * REC<D>, (unsigned)i, sp, sv);
+#pragma unroll
+      for (int q = 0; q < D; ++q) gg[q] = a.G[((long)b * N + i) * D + q];
+      if (wave == 0) {
+#pragma unroll
+        for (int q = 0; q < D; ++q) av[q] = a.A[((long)b * a.a_env + i) * D + q];
+        if (a.Gn && !a.cdS) load_rec<D>(a.Gn + (long)b * a.gn_env * REC<D>, (unsigned)i, gnp, gnv);
+        vld = a.valid ? (a.valid[(long)b * a.v_env] != 0) : true;
+      }
+    }
+    if (wave == 0 && a.cdS) fused_combine<D>(a, ok, b, i, h, gnp, gnv);    // G_{t+1} (wave 0 only)
+    float ex[D];
+#pragma unroll
+    for (int q = 0; q < D; ++q) ex[q] = sp[q] - gg[q];
+    const h16x8 sfr = node_state_frag<D>(ex, sv, ok, h);
+    const h16* prow = a.pooled + (long)b * a.p_env + (long)i * PROW;
+    const h16* W1 = wr + opaque_zero();
+    const h16* W2 = W1 + 64 * NS1;
+    const h16* W3 = W2 + 128 * NS2;
+    const h16* W4 = W3 + 64 * NS3;
+    // ---- L1 (waves 0, 1): Y1 tile `wave` = relu(W1f [P; s])
+    Pk Y1b, Y2b, Y3b;
+    if (wave < 2) {
+      f32x16 c = zero16();
+#pragma unroll
+      for (int kk = 0; kk < 8; ++kk) {
+        Fr pf;
+        if (ok) pf = row_fr(prow + 16 * kk + 8 * h, 128);
+        else pf.h = pf.l = zz;
+        c = mma(wrm_nat_fr(W1, NS1, 32 * wave, kk, lane, LO), pf, c);
+      }
+      c = mma_bx(wrm_nat_fr(W1, NS1, 32 * wave, 8, lane, LO), sfr, c);
+      relu_(c);
+      Y1b = to_pk(c);
+      store_pk(stg, SW, r, 32 * wave, Y1b, h, PLN);
+    }
+    __syncthreads();
+    // ---- L2 (all waves): Y2 tile `wave`
+    {
+      f32x16 c = bias_rows(nb2, 32 * wave, h);
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) c = mma(wrm_nat_fr(W2, NS2, 32 * wave, kk, lane, LO), img_fr(0, kk), c);
+      relu_(c);
+      Y2b = to_pk(c);
+    }
+    __syncthreads();                                   // Y1 image read by every wave
+    store_pk(stg, SW, r, 32 * wave, Y2b, h, PLN);
+    __syncthreads();
+    // ---- L3 (waves 2, 3): Y3 tile wave - 2
+    if (wave >= 2) {
+      const int mt = wave - 2;
+      f32x16 c = bias_rows(nb3, 32 * mt, h);
+#pragma unroll
+      for (int kk = 0; kk < 8; ++kk) c = mma(wrm_nat_fr(W3, NS3, 32 * mt, kk, lane, LO), img_fr(0, kk), c);
+      relu_(c);
+      Y3b = to_pk(c);
+      store_pk(stg, SW, r, 128 + 32 * mt, Y3b, h, PLN);
+    }
+    __syncthreads();
+    // ---- L4 + gain law + action-loss backward (wave 0) -> d4, ego terms
+    float egp[D], egv[D];
+#pragma unroll
+    for (int q = 0; q < D; ++q) { egp[q] = 0.f; egv[q] = 0.f; }
+    if (wave == 0) {
+      f32x16 y4 = bias_rows(nb4, 0, h);
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) y4 = mma(wrm_nat_fr(W4, NS4, 0, kk, lane, LO), img_fr(128, kk), y4);
+      float y4r[8];
+      acc_rows8(y4, y4r);
+      float d4r[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) d4r[q] = 0.f;
+      if (ok && h == 0) {
+        float da[D], ar[D];
+#pragma unroll
+        for (int q = 0; q < D; ++q) { da[q] = a.dt * gnv[q]; ar[q] = -(ex[q] + a.sqrt3 * sv[q]); }
+        float act_coef = a.act_scale ? a.act_coef / fmaxf(*a.act_scale, 1.f) : a.act_coef;
+        if (a.gscale) act_coef *= *a.gscale;
+        if (vld && act_coef != 0.f) {
+          const float diff = sqsum<D>(av) - sqsum<D>(ar);
+          const float sg = diff > 0.f ? 1.f : (diff < 0.f ? -1.f : 0.f);
+          const float cf = act_coef * sg;
+#pragma unroll
+          for (int q = 0; q < D; ++q) {
+            da[q] += cf * 2.f * av[q];
+            egp[q] += cf * 2.f * ar[q];
+            egv[q] += cf * 2.f * a.sqrt3 * ar[q];
+          }
+        }
+#pragma unroll
+        for (int q = 0; q < D; ++q) {
+          const float s0 = sigm(y4r[2 * q]), s1 = sigm(y4r[2 * q + 1]);
+          const float kp = 2.f * s0 + 0.2f, kv = 2.f * s1 + 0.2f;
+          egp[q] += -kp * da[q];
+          egv[q] += -kv * da[q];
+          d4r[2 * q] = -da[q] * ex[q] * 2.f * s0 * (1.f - s0);
+          d4r[2 * q + 1] = -da[q] * sv[q] * 2.f * s1 * (1.f - s1);
+        }
+      }
+      f32x16 d4 = zero16();
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float hi4 = shfl_xor32(d4r[4 + q]);
+        d4[q] = (h == 0) ? d4r[q] : hi4;
+      }
+      store_pk(stg, SW, r, 192, to_pk(d4), h, PLN);
+    }
+    __syncthreads();
+    // ---- dY3 (waves 1, 2): tile wave - 1 = (W4^T d4) . relu'(Y3)
+    if (wave == 1 || wave == 2) {
+      const int mt = wave - 1;
+      f32x16 c = zero16();
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) c = mma(wrmT_nat_fr(W4, NS4, 32 * mt, kk, lane, LO), img_fr(192, kk), c);
+      Pk d3b = to_pk(c);
+      Pk y3;
+      y3.h = load_tile_h(stg, SW, r, 128 + 32 * mt, h);
+      mask_pk(d3b, y3);
+      store_pk(stg, SW, r, 224 + 32 * mt, d3b, h, PLN);
+    }
+    __syncthreads();
+    // ---- S4: dW4pad (32x64) += d4 . Y3^T ; nb4  (waves 0, 1)   S3: dW3 (64x128) += d3 . Y2^T ; nb3
+    if (wave < 2)
+      bs4 += stage_mma_fr<2>(stg + 192, SW, PLN, stg + 128, SW, PLN, 0, wave, lane, acc4, 0, wave == 0 ? 2 : 0);
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int t = wave + 4 * u;
+      bs3[u] += stage_mma_fr<2>(stg + 224, SW, PLN, stg, SW, PLN, t / 4, t % 4, lane, acc3[u], 0, t % 4 == 0 ? 2 : 0);
+    }
+    // ---- dY2 (all waves): tile `wave` = (W3^T d3) . relu'(Y2)
+    Pk d2b;
+    {
+      f32x16 c = zero16();
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) c = mma(wrmT_nat_fr(W3, NS3, 32 * wave, kk, lane, LO), img_fr(224, kk), c);
+      d2b = to_pk(c);
+      mask_pk(d2b, Y2b);
+    }
+    __syncthreads();                                   // S4 / S3 images and d3 read by every wave
+    store_pk(stg, SW, r, 32 * wave, d2b, h, PLN);
+    if (wave < 2) store_pk(stg, SW, r, 128 + 32 * wave, Y1b, h, PLN);
+    __syncthreads();
+    // ---- S2: dW2 (128x64) += d2 . Y1^T ; nb2
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int t = wave + 4 * u;
+      bs2[u] += stage_mma_fr<2>(stg, SW, PLN, stg + 128, SW, PLN, t / 2, t % 2, lane, acc2[u], 0, t % 2 == 0 ? 2 : 0);
+    }
+    // ---- dY1 (waves 0, 1): tile `wave` = (W2^T d2) . relu'(Y1)
+    Pk d1b;
+    if (wave < 2) {
+      f32x16 c = zero16();
+#pragma unroll
+      for (int kk = 0; kk < 8; ++kk) c = mma(wrmT_nat_fr(W2, NS2, 32 * wave, kk, lane, LO), img_fr(0, kk), c);
+      d1b = to_pk(c);
+      mask_pk(d1b, Y1b);
+    }
+    __syncthreads();                                   // S2 images and d2 read by every wave
+    // ---- S1 images: d1 (cols 0..63), [P | s | 0] (cols 64..223: pooled 128, state fragment 16, zeros 16)
+    if (wave < 2) store_pk(stg, SW, r, 32 * wave, d1b, h, PLN);
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int kk = 2 * wave + u;
+      const h16x8 pv = ok ? *reinterpret_cast<const h16x8*>(prow + 16 * kk + 8 * h) : zz;
+      *reinterpret_cast<h16x8*>(stg + r * SW + 64 + 16 * kk + 8 * h) = pv;
+      if constexpr (X3) {
+        const h16x8 pl = ok ? *reinterpret_cast<const h16x8*>(prow + 128 + 16 * kk + 8 * h) : zz;
+        *reinterpret_cast<h16x8*>(stg + PLN + r * SW + 64 + 16 * kk + 8 * h) = pl;
+      }
+    }
+    if (wave == 3) {
+      *reinterpret_cast<h16x8*>(stg + r * SW + 64 + 128 + 8 * h) = sfr;
+      *reinterpret_cast<h16x8*>(stg + r * SW + 64 + 144 + 8 * h) = zz;
+      if constexpr (X3) {      // the state fragment is exact: zero lo plane
+        *reinterpret_cast<h16x8*>(stg + PLN + r * SW + 64 + 128 + 8 * h) = zz;
+        *reinterpret_cast<h16x8*>(stg + PLN + r * SW + 64 + 144 + 8 * h) = zz;
+      }
+    }
+    __syncthreads();
+    // ---- S1: dW1f (64x160) += d1 . [P | s]^T
+#pragma unroll
+    for (int u = 0; u < 3; ++u) {
+      const int t = wave + 4 * u;
+      if (u < n1) stage_mma_fr<2>(stg, SW, PLN, stg + 64, SW, PLN, t / 5, t % 5, lane, acc1[u]);
+    }
+    // ---- dP = W1f^T d1: tiles 0..3 (one per wave) -> dL/dpooled rows; tile 4 (wave 0) -> ego
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int mt = u == 0 ? wave : 4;
+      if (u == 1 && wave != 0) break;
+      f32x16 c = zero16();
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) c = mma(wrmT_nat_fr(W1, NS1, 32 * mt, kk, lane, LO), img_fr(0, kk), c);
+      if (mt < 4) {
+        if (ok) {
+          h16* drow = a.dP + (long)b * a.dp_env + (long)i * PROW + 32 * mt;
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            h16x4 v, vl_;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              v[e] = (h16)c[4 * g + e];
+              if constexpr (X3) vl_[e] = (h16)(c[4 * g + e] - (float)v[e]);
+            }
+            *reinterpret_cast<h16x4*>(drow + 8 * g + 4 * h) = v;
+            if constexpr (X3) *reinterpret_cast<h16x4*>(drow + 128 + 8 * g + 4 * h) = vl_;
+          }
+        }
+      } else {
+        float er[8];
+        acc_rows8(c, er);                       // rows 128..128+2D-1: d/d[p - g, v]
+        if (ok && h == 0 && a.ego) {
+#pragma unroll
+          for (int q = 0; q < D; ++q) { egp[q] += er[q]; egv[q] += er[D + q]; }
+          store_rec<D>(a.ego + (long)b * N * REC<D>, (unsigned)i, egp, egv);
+        }
+      }
+    }
+    __syncthreads();                                   // region reused by the next chunk
+  }
+  // ---- slab += this workgroup's partial (fixed tile owners: deterministic); loads first
+  f32x16 o1[3], o2[2], o3[2], o4 = zero16();
+  float ob2[2] = {0.f, 0.f}, ob3[2] = {0.f, 0.f}, ob4 = 0.f;
+  o1[0] = o1[1] = o1[2] = o2[0] = o2[1] = o3[0] = o3[1] = zero16();
+  if (!a.init) {
+#pragma unroll
+    for (int u = 0; u < 3; ++u) {
+      const int t = wave + 4 * u;
+      if (u < n1) load_tile(o1[u], P + NP_W1, 160, t / 5, t % 5, lane);
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int t = wave + 4 * u;
+      load_tile(o2[u], P + NP_W2, 64, t / 2, t % 2, lane);
+      load_tile(o3[u], P + NP_W3, 128, t / 4, t % 4, lane);
+      ob2[u] = P[NP_B2 + 32 * (t / 2) + r];
+      ob3[u] = P[NP_B3 + 32 * (t / 4) + r];
+    }
+    if (wave < 2) {
+      load_tile(o4, P + NP_W4, 64, 0, wave, lane);
+      ob4 = P[NP_B4 + r];
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < 3; ++u) {
+    const int t = wave + 4 * u;
+    if (u < n1) store_tile_add(P + NP_W1, 160, t / 5, t % 5, o1[u], acc1[u], lane);
+  }
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int t = wave + 4 * u;
+    store_tile_add(P + NP_W2, 64, t / 2, t % 2, o2[u], acc2[u], lane);
+    const float s2 = bs2[u] + shfl_xor32(bs2[u]);
+    if (t % 2 == 0 && h == 0) P[NP_B2 + 32 * (t / 2) + r] = ob2[u] + s2;
+    store_tile_add(P + NP_W3, 128, t / 4, t % 4, o3[u], acc3[u], lane);
+    const float s3 = bs3[u] + shfl_xor32(bs3[u]);
+    if (t % 4 == 0 && h == 0) P[NP_B3 + 32 * (t / 4) + r] = ob3[u] + s3;
+  }
+  if (wave < 2) {
+    store_tile_add(P + NP_W4, 64, 0, wave, o4, acc4, lane);
+    if (wave == 0) {
+      const float s4 = bs4 + shfl_xor32(bs4);
+      if (h == 0) P[NP_B4 + r] = ob4 + s4;
+    }
+  }
+}
+
 template <int D>
 __global__ __launch_bounds__(NB_WAVES * 64, 1) void ctrl_node_bwd_kernel(CtrlNodeBwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   node_bwd_body<D>(a, smem, blockIdx.x, gridDim.x, a.partial + (long)blockIdx.x * CTRL_NODE_PARTIAL);
+}
+
+// separate kernel: one shared body would size both paths' registers for the larger (spills)
+template <int D>
+__global__ __launch_bounds__(NB_WAVES * 64, 1) void ctrl_node_bwd_coop_kernel(CtrlNodeBwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  node_bwd_coop<D>(a, smem, blockIdx.x, gridDim.x, a.partial + (long)blockIdx.x * CTRL_NODE_PARTIAL);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1773,6 +2107,10 @@ __device__ __noinline__ void node_bwd_call(const CtrlNodeBwdArgs& a, unsigned ch
   node_bwd_body<D>(a, smem, 0, 1, P);
 }
 template <int D>
+__device__ __noinline__ void node_coop_call(const CtrlNodeBwdArgs& a, unsigned char* smem, float* P) {
+  node_bwd_coop<D>(a, smem, 0, 1, P);
+}
+template <int D>
 __device__ __noinline__ void edge_bwd_call(const CtrlEdgeBwdArgs& a, unsigned char* smem, float* P) {
   edge_bwd_body<D>(a, smem, 0, 1, P);
 }
@@ -1817,7 +2155,8 @@ __global__ __launch_bounds__(NB_WAVES * 64, 1) void bptt_small_kernel(BpttSmallA
       a.dP = dPb; a.dp_env = (long)N * PROW;
       a.ego = egb;
       a.init = t == T - 1;
-      node_bwd_call<D>(a, smem, Pn);
+      if (a.coop) node_coop_call<D>(a, smem, Pn);
+      else node_bwd_call<D>(a, smem, Pn);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // dP / ego stores complete
     __syncthreads();
@@ -1847,13 +2186,13 @@ extern "C" int MB_SYM(ctrl_node_bwd)(const mb::CtrlNodeBwdArgs* a, int num_block
   using namespace mb;
   using namespace mb::MB_PREC;
   const size_t lds = ctrl_node_bwd_lds();
-  if (a->dim == 3) {
-    (void)hipFuncSetAttribute((const void*)ctrl_node_bwd_kernel<3>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL(ctrl_node_bwd_kernel<3>, dim3(num_blocks), dim3(NB_WAVES * 64), lds, st, *a);
-  } else {
-    (void)hipFuncSetAttribute((const void*)ctrl_node_bwd_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL(ctrl_node_bwd_kernel<2>, dim3(num_blocks), dim3(NB_WAVES * 64), lds, st, *a);
-  }
+  CtrlNodeBwdArgs b = *a;
+  b.coop = node_bwd_coop_enabled() && a->chunk == 32;     // 32-agent chunks: the four waves cooperate
+  const void* fn = a->dim == 3 ? (b.coop ? (const void*)ctrl_node_bwd_coop_kernel<3> : (const void*)ctrl_node_bwd_kernel<3>)
+                               : (b.coop ? (const void*)ctrl_node_bwd_coop_kernel<2> : (const void*)ctrl_node_bwd_kernel<2>);
+  (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  void* kargs[] = {&b};
+  hipLaunchKernel(fn, dim3(num_blocks), dim3(NB_WAVES * 64), kargs, lds, st);
   return (int)hipGetLastError();
 }
 

@@ -375,6 +375,7 @@ class BpttDriver {
     n.wvec = P<const float>(wvec_); n.act_coef = act_coef; n.act_scale = P<const float>(act_scale_);
     n.gscale = P<const float>(gscale_);
     n.dt = dt_; n.sqrt3 = sqrt3_; n.dP = P<h16>(dP_); n.ego = P<float4>(ego_); n.partial = P<float>(part_node_);
+    n.coop = mb::node_bwd_coop_enabled() && N_ <= 64;   // 32-agent chunks over the four waves
     mb::CtrlEdgeBwdArgs& e = a.eb;
     e.dim = D_; e.S = n.S; e.idx = P<const int>(idx_); e.argmax = P<const uint8_t>(argmax_); e.dP = n.dP;
     e.B = B_; e.N = N_; e.K = K_; e.wpack = P<const h16>(wpack_); e.f_ew1f = f_ew1f_; e.f_ew2tn = f_ew2tn_;

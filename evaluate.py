@@ -1,10 +1,13 @@
 """Evaluate a trained controller + CBF with test-time action refinement.
 
     python evaluate.py --num_agents 32 [--model_path ckpt.pt] [--num_envs 4] [--episodes 10]
-                       [--max_steps 50] [--no_refine] [--device auto|cpu|hip] [--gpu 0]
+                       [--max_steps 50] [--no_refine] [--refine_space actions|gains] [--diagnose]
+                       [--device auto|cpu|hip] [--gpu 0]
 
 Prints one JSON line: safety rate, reaching rate, mean final goal distance, refinement
 iterations. Without --model_path the networks are random-initialised (plumbing check).
+--refine_space gains refines only the PD gains of the controller law (what the trained policy
+class can express); --diagnose adds the share of unsafe pairs that are top-K neighbours.
 """
 from __future__ import annotations
 
@@ -24,6 +27,8 @@ def main(argv=None):
     ap.add_argument("--no_refine", action="store_true")
     ap.add_argument("--refine_loops", type=int, default=None)
     ap.add_argument("--refine_lr", type=float, default=None)
+    ap.add_argument("--refine_space", choices=["actions", "gains"], default="actions")
+    ap.add_argument("--diagnose", action="store_true")
     ap.add_argument("--device", type=str, default="auto")
     ap.add_argument("--seed", type=int, default=0)
     args = ap.parse_args(argv)
@@ -41,7 +46,8 @@ def main(argv=None):
     ctrl, cbf = Controller(4).to(dev), CBF(4).to(dev)
     if args.model_path:
         ckpt.load_models(args.model_path, ctrl, cbf)
-    cfg = EvalConfig(num_agents=args.num_agents, num_envs=args.num_envs, seed=args.seed, refine=not args.no_refine)
+    cfg = EvalConfig(num_agents=args.num_agents, num_envs=args.num_envs, seed=args.seed, refine=not args.no_refine,
+                     refine_space=args.refine_space, diagnose=args.diagnose)
     if args.episodes is not None:
         cfg.episodes = args.episodes
     if args.max_steps is not None:
