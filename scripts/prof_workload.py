@@ -3,7 +3,7 @@ tests/test_gpu_profiler.py): the fp32 (x3) HIP engine at 512 agents x 8 envs, fi
 early stop: every run issues the same launches), seed 0, ``--iters`` full training iterations
 after one warm-up iteration. Run it under ``rocprofv3`` with this program right after ``--``.
 
-    python scripts/prof_workload.py [--iters 2] [--dtype fp32]
+    python scripts/prof_workload.py [--iters 2] [--dtype fp32] [--agents 512 --envs 8]
 
 With ``--summarize PMC_CSV [PMC_CSV ...] --out JSON`` it instead folds rocprofv3 ``--pmc`` CSV
 outputs into per-kernel per-dispatch averages (the baseline format of the test).
@@ -41,22 +41,29 @@ def summarize(paths):
             for k, row in agg.items()}
 
 
-def run(iters, dtype):
+def run(iters, dtype, agents=None, envs=None):
     import torch
     from macbf_gnn_amd import config as C
     from macbf_gnn_amd.engine import Trainer
-    cfg = C.TrainConfig(device="hip", dtype=dtype, display_steps=10 ** 9, save_steps=10 ** 9, **CONFIG)
+    conf = dict(CONFIG)
+    if agents:
+        conf["num_agents"] = agents
+    if envs:
+        conf["num_envs"] = envs
+    cfg = C.TrainConfig(device="hip", dtype=dtype, display_steps=10 ** 9, save_steps=10 ** 9, **conf)
     tr = Trainer(cfg)
     for _ in range(iters + 1):
         tr.train_step()
     torch.cuda.synchronize()
-    print(json.dumps({"iters": iters, "dtype": dtype, **CONFIG}), flush=True)
+    print(json.dumps({"iters": iters, "dtype": dtype, **conf}), flush=True)
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=2)
     ap.add_argument("--dtype", default="fp32")
+    ap.add_argument("--agents", type=int, default=None)
+    ap.add_argument("--envs", type=int, default=None)
     ap.add_argument("--summarize", nargs="*", default=None)
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
@@ -66,7 +73,7 @@ def main():
             json.dump(s, open(a.out, "w"), indent=1, sort_keys=True)
         print(json.dumps(s, indent=1, sort_keys=True))
         return
-    run(a.iters, a.dtype)
+    run(a.iters, a.dtype, a.agents, a.envs)
 
 
 if __name__ == "__main__":
