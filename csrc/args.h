@@ -384,6 +384,7 @@ int mb_pack_gather(const float* src, int n, const int* idx16, int m16, unsigned 
 int mb_step_commit(const mb::StepCommitArgs* a, hipStream_t st);
 int mb_stats_pack(const float* sums, const float* counts, const float* local, float* row, hipStream_t st);
 int mb_probe_mfma(const void* a, const void* b, float* d, hipStream_t st);
+int mb_probe_lane_xor(const unsigned* in, unsigned* out, hipStream_t st);
 int mb_probe_smfmac(const void* a, const void* b, const int* idx, float* d, hipStream_t st);
 int mb_probe_tr(const void* img, int rows, int stride, int e0, int m0, void* out, hipStream_t st);
 }

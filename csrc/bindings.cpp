@@ -288,6 +288,9 @@ static int probe_mfma(u64 a, u64 b, u64 d, u64 stream) {
 static int probe_smfmac(u64 a, u64 b, u64 idx, u64 d, u64 stream) {
   return mb_probe_smfmac(P<const void>(a), P<const void>(b), P<const int>(idx), P<float>(d), ST(stream));
 }
+static int probe_lane_xor(u64 in, u64 out, u64 stream) {
+  return mb_probe_lane_xor(P<const unsigned>(in), P<unsigned>(out), ST(stream));
+}
 static int probe_tr(u64 img, int rows, int stride, int e0, int m0, u64 out, u64 stream) {
   return mb_probe_tr(P<const void>(img), rows, stride, e0, m0, P<void>(out), ST(stream));
 }
@@ -337,6 +340,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("probe_mfma", &probe_mfma);
   m.def("probe_tr", &probe_tr);
   m.def("probe_smfmac", &probe_smfmac);
+  m.def("probe_lane_xor", &probe_lane_xor);
   m.def("device_info", &device_info);
   m.def("err_str", &err_str);
   m.attr("ARCH") = "gfx950";

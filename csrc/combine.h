@@ -17,8 +17,11 @@ namespace mb {
 constexpr int RG = CMB_RG;             // lanes per node
 
 DEV float grp_sum(float v) {
-#pragma unroll
-  for (int o = RG / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, RG);
+  static_assert(RG == 16, "16-lane groups");
+  v += lane_xorf<8>(v);
+  v += lane_xorf<4>(v);
+  v += lane_xorf<2>(v);
+  v += lane_xorf<1>(v);
   return v;
 }
 

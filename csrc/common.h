@@ -161,25 +161,82 @@ DEV void block_copy16(void* dst, const void* src, int bytes) {
   for (; i < n; i += bd) d[i] = s[i];
 }
 
+// ---- lane exchanges without the LDS crossbar. __shfl_xor is a ds_bpermute_b32: an LDS-unit
+// round trip (~50+ cycles of latency plus the lgkmcnt wait) per step, six of them per wave
+// reduction -- in a latency-bound loop (the kNN scan's per-chunk threshold update) that was most of
+// the wave's time. lane_xor<O> returns the value of lane (lane ^ O) exactly, on the VALU:
+//   O = 1, 2   DPP quad_perm          O = 4   DPP row_shl:4 / row_shr:4 + select
+//   O = 8      DPP row_ror:8 (a rotation by 8 inside a 16-lane row is the xor)
+//   O = 16     v_permlane16_swap      O = 32  v_permlane32_swap (CDNA4)
+// Same partners as the xor butterfly, so every reduction below adds / compares in the same order
+// as before (bit-identical results).
+template <int O>
+DEV unsigned lane_xor(unsigned v) {
+  static_assert(O == 1 || O == 2 || O == 4 || O == 8 || O == 16 || O == 32, "xor distance");
+  if constexpr (O == 32) {
+    return xor32u(v);
+  } else if constexpr (O == 16) {
+    const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+    return (threadIdx.x & 16) ? r[0] : r[1];
+  } else if constexpr (O == 8) {
+    return (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x128, 0xF, 0xF, false);        // row_ror:8
+  } else if constexpr (O == 4) {
+    const int up = __builtin_amdgcn_update_dpp(0, (int)v, 0x104, 0xF, 0xF, false);          // row_shl:4: lane + 4
+    const int dn = __builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false);          // row_shr:4: lane - 4
+    return (unsigned)((threadIdx.x & 4) ? dn : up);
+  } else if constexpr (O == 2) {
+    return (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);         // quad_perm [2,3,0,1]
+  } else {
+    return (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);         // quad_perm [1,0,3,2]
+  }
+}
+template <int O>
+DEV float lane_xorf(float v) { return __uint_as_float(lane_xor<O>(__float_as_uint(v))); }
+// runtime distance (folds to one branch when o is a constant after unrolling)
+DEV unsigned lane_xor_rt(unsigned v, int o) {
+  switch (o) {
+    case 1: return lane_xor<1>(v);
+    case 2: return lane_xor<2>(v);
+    case 4: return lane_xor<4>(v);
+    case 8: return lane_xor<8>(v);
+    case 16: return lane_xor<16>(v);
+    default: return lane_xor<32>(v);
+  }
+}
+
 DEV float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  v += lane_xorf<32>(v);
+  v += lane_xorf<16>(v);
+  v += lane_xorf<8>(v);
+  v += lane_xorf<4>(v);
+  v += lane_xorf<2>(v);
+  v += lane_xorf<1>(v);
   return v;
 }
 
 // integer wave sum (exact, so independent of how the addends are grouped over waves)
 DEV unsigned long long wave_sum_u64(unsigned long long v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const unsigned lo = (unsigned)__shfl_xor((int)(unsigned)v, o), hi = (unsigned)__shfl_xor((int)(unsigned)(v >> 32), o);
-    v += ((unsigned long long)hi << 32) | lo;
-  }
+  auto step = [](unsigned long long x, auto o_) {
+    constexpr int O = decltype(o_)::value;
+    const unsigned lo = lane_xor<O>((unsigned)x), hi = lane_xor<O>((unsigned)(x >> 32));
+    return x + (((unsigned long long)hi << 32) | lo);
+  };
+  v = step(v, std::integral_constant<int, 32>{});
+  v = step(v, std::integral_constant<int, 16>{});
+  v = step(v, std::integral_constant<int, 8>{});
+  v = step(v, std::integral_constant<int, 4>{});
+  v = step(v, std::integral_constant<int, 2>{});
+  v = step(v, std::integral_constant<int, 1>{});
   return v;
 }
 
 DEV float wave_max(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+  v = fmaxf(v, lane_xorf<32>(v));
+  v = fmaxf(v, lane_xorf<16>(v));
+  v = fmaxf(v, lane_xorf<8>(v));
+  v = fmaxf(v, lane_xorf<4>(v));
+  v = fmaxf(v, lane_xorf<2>(v));
+  v = fmaxf(v, lane_xorf<1>(v));
   return v;
 }
 
@@ -348,8 +405,11 @@ DEV void write_tile(float* dst, int ncols, int mt, int nt, const f32x16& c, int 
 }
 
 DEV float sum32(float v) {   // sum over the 32 lanes of this lane's half
-#pragma unroll
-  for (int o = 16; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  v += lane_xorf<16>(v);
+  v += lane_xorf<8>(v);
+  v += lane_xorf<4>(v);
+  v += lane_xorf<2>(v);
+  v += lane_xorf<1>(v);
   return v;
 }
 

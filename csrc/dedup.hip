@@ -290,8 +290,7 @@ __global__ __launch_bounds__(DH_BLOCK) void cbf_dh_kernel(CbfDhArgs a) {
     const float v = wave_sum(acc[q]);
     if (lane == 0) red[q][wave] = v;
   }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) nact += __shfl_xor(nact, o);
+  nact = (int)wave_sum_u64((unsigned long long)(unsigned)nact);
   if (lane == 0) cred[wave] = nact;
   __syncthreads();
   if (a.blk_active && threadIdx.x == 0) {

@@ -37,7 +37,29 @@ __global__ void probe_smfmac_kernel(const __bf16* a, const __bf16* b, const int*
   for (int q = 0; q < 16; ++q) d[l * 16 + q] = c[q];
 }
 
+// lane exchanges: out[s * 64 + lane] = lane_xor<1 << s>(in[lane]), s = 0..5; out[384 + lane] =
+// wave_sum, out[448 + lane] = wave_max, out[512 + lane] = grp_sum (16-lane groups) of in (as float)
+__global__ void probe_lane_xor_kernel(const unsigned* in, unsigned* out) {
+  const int lane = threadIdx.x;
+  const unsigned v = in[lane];
+  out[0 * 64 + lane] = lane_xor<1>(v);
+  out[1 * 64 + lane] = lane_xor<2>(v);
+  out[2 * 64 + lane] = lane_xor<4>(v);
+  out[3 * 64 + lane] = lane_xor<8>(v);
+  out[4 * 64 + lane] = lane_xor<16>(v);
+  out[5 * 64 + lane] = lane_xor<32>(v);
+  const float f = __uint_as_float(v);
+  out[6 * 64 + lane] = __float_as_uint(wave_sum(f));
+  out[7 * 64 + lane] = __float_as_uint(wave_max(f));
+  out[8 * 64 + lane] = __float_as_uint(sum32(f));
+}
+
 }  // namespace mb
+
+extern "C" int mb_probe_lane_xor(const unsigned* in, unsigned* out, hipStream_t st) {
+  hipLaunchKernelGGL(mb::probe_lane_xor_kernel, dim3(1), dim3(64), 0, st, in, out);
+  return (int)hipGetLastError();
+}
 
 extern "C" int mb_probe_smfmac(const void* a, const void* b, const int* idx, float* d, hipStream_t st) {
   hipLaunchKernelGGL(mb::probe_smfmac_kernel, dim3(1), dim3(64), 0, st, (const __bf16*)a, (const __bf16*)b, idx, d);

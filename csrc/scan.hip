@@ -136,8 +136,8 @@ DEV float wave_min(float v) { return -wave_max(-v); }
 // branches; after the local neighbourhood has filled the lists almost every far chunk costs
 // one box test instead of 8 pair evaluations. Obstacle nodes are candidates, never centres.
 // xor-shuffle of a lane value across the LPA lanes of one agent (o = 32: v_permlane32_swap)
-DEV float grp_xor(float v, int o) { return o == 32 ? shfl_xor32(v) : __shfl_xor(v, o); }
-DEV unsigned grp_xoru(unsigned v, int o) { return o == 32 ? xor32u(v) : (unsigned)__shfl_xor((int)v, o); }
+DEV float grp_xor(float v, int o) { return __uint_as_float(lane_xor_rt(__float_as_uint(v), o)); }
+DEV unsigned grp_xoru(unsigned v, int o) { return lane_xor_rt(v, o); }
 
 // Large envs (Nn > SCAN_MAXN, the whole env no longer fits LDS): scan_stage_kernel writes the
 // curve-ordered node arrays and the chunk / superchunk boxes of every env ONCE per step to a

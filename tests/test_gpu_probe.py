@@ -90,3 +90,31 @@ def test_smfmac_layout_exact():
         for reg in range(16):
             D[L.acc_row(reg, h), r] = d[l, reg]
     np.testing.assert_array_equal(D, A @ B)
+
+
+def test_lane_xor_exchanges_and_reductions():
+    """lane_xor<O> (DPP / permlane, common.h) returns lane (l ^ O)'s value for every O, and the wave
+    reductions built on it equal the xor-butterfly reference bit for bit (same pairing order)."""
+    rng = np.random.default_rng(3)
+    vals = rng.standard_normal(64).astype(np.float32)
+    vin = torch.tensor(vals.view(np.uint32).astype(np.int64), dtype=torch.int64).to(torch.int32).to(DEV)
+    out = torch.zeros(9 * 64, dtype=torch.int32, device=DEV)
+    assert native.lib().probe_lane_xor(vin.data_ptr(), out.data_ptr(), native.stream_handle()) == 0
+    torch.cuda.synchronize()
+    got = out.cpu().numpy().astype(np.int64).astype(np.uint32).reshape(9, 64)
+    bits = vals.view(np.uint32)
+    lanes = np.arange(64)
+    for s in range(6):
+        np.testing.assert_array_equal(got[s], bits[lanes ^ (1 << s)], err_msg=f"xor {1 << s}")
+
+    def butterfly(x, dists, op):
+        x = x.copy()
+        for o in dists:
+            x = op(x, x[lanes ^ o]).astype(np.float32)
+        return x
+    ws = butterfly(vals, [32, 16, 8, 4, 2, 1], lambda a, b: a + b)
+    wm = butterfly(vals, [32, 16, 8, 4, 2, 1], np.maximum)
+    s32 = butterfly(vals, [16, 8, 4, 2, 1], lambda a, b: a + b)
+    np.testing.assert_array_equal(got[6], ws.view(np.uint32))
+    np.testing.assert_array_equal(got[7], wm.view(np.uint32))
+    np.testing.assert_array_equal(got[8], s32.view(np.uint32))
