@@ -1603,7 +1603,12 @@ size_t ctrl_edge_bwd_lds() { return (size_t)22 * FRAG_SZ + EB_STAGE; }
 // LDS; P: this workgroup's slab row)
 // KC: compile-time neighbour count (12 = TOP_K: the slot / agent / row index arithmetic of the
 // dense rows folds to constants), 0 = runtime a.K
-template <int D, int KC = 0>
+// SPLIT (the persistent small-scene BPTT): a work item is ONE 32-agent group whose K edge tiles
+// are spread over the waves (wave w: tiles w, w + EB_WAVES, ...; a round's shared dW2 stage
+// contracts the EB_WAVES tiles of the round) instead of one 32-agent group per wave -- a
+// 32-agent env keeps all four waves busy. Waves without a tile in the last round (K not a
+// multiple of EB_WAVES) contribute zero rows.
+template <int D, int KC = 0, bool SPLIT = false>
 DEV void edge_bwd_body(const CtrlEdgeBwdArgs& a, unsigned char* smem, long w0, long wstride, float* P) {
   h16* wf = reinterpret_cast<h16*>(smem);                 // ew1f (2) | ew2tn (16) | ew1ft (4)
   h16* stg = reinterpret_cast<h16*>(smem + 22 * FRAG_SZ);
@@ -1613,7 +1618,7 @@ DEV void edge_bwd_body(const CtrlEdgeBwdArgs& a, unsigned char* smem, long w0, l
   const int wave = threadIdx.x / WAVE, lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
   const int N = a.N, K = KC ? KC : a.K;
   const int total = a.B * N;
-  const long nchunks = (total + EB_CH - 1) / EB_CH;
+  const long nchunks = SPLIT ? (total + 31) / 32 : (total + EB_CH - 1) / EB_CH;
   const int erow = wave * 32 + r;
   f32x16 accW2[EB_TA], accW1[2];
   accW1[0] = accW1[1] = zero16();
@@ -1625,7 +1630,7 @@ DEV void edge_bwd_body(const CtrlEdgeBwdArgs& a, unsigned char* smem, long w0, l
   // work item = (chunk, tile range): small scenes split a chunk's NT tile rounds over
   // qsplit workgroups (tiles are independent; every workgroup owns its dW slab), large ones
   // use qsplit = 1
-  const int QP = a.qsplit > 1 ? a.qsplit : 1;
+  const int QP = (!SPLIT && a.qsplit > 1) ? a.qsplit : 1;
   const long nwork = nchunks * QP;
   const int NT = EB_DENSE ? K : 16;                         // tiles per 32-agent wave
   const unsigned invK = (65536u + (unsigned)K - 1u) / (unsigned)K;
@@ -1636,16 +1641,19 @@ DEV void edge_bwd_body(const CtrlEdgeBwdArgs& a, unsigned char* smem, long w0, l
   for (long w = w0; w < nwork; w += wstride) {
     const long chunk = w / QP;
     const int part = (int)(w - chunk * QP);
-    const int q0 = part * NT / QP, q1 = (part + 1) * NT / QP;
+    // tiles of this wave: q0, q0 + QS, ... (< q1); every wave runs NR rounds (stage barriers)
+    const int QS = SPLIT ? EB_WAVES : 1;
+    const int q0 = SPLIT ? wave : part * NT / QP, q1 = SPLIT ? NT : (part + 1) * NT / QP;
+    const int NR = SPLIT ? (NT + EB_WAVES - 1) / EB_WAVES : q1 - q0;
     EdgeIdx xi1;
     EdgeSt<D> xs0;
-    const int g0 = (int)(chunk * EB_CH) + wave * 32;
+    const int g0 = SPLIT ? (int)(chunk * 32) : (int)(chunk * EB_CH) + wave * 32;
     const AgentBase ab = agent_base(g0, N);
     {
       EdgeIdx xi0;
       idx_load(ab, q0, xi0);
       ctrl_st_load<D>(a.S, a.s_env, xi0, xs0);
-      idx_load(ab, q0 + 1, xi1);
+      idx_load(ab, q0 + QS, xi1);
     }
     // argmax slots / dL/dpooled of a tile's agents (lane (r, h): features 4r..4r+3 of one
     // agent per pass), loaded one tile ahead like the edge gathers. 16-slot rows: tile q = agents
@@ -1680,15 +1688,16 @@ DEV void edge_bwd_body(const CtrlEdgeBwdArgs& a, unsigned char* smem, long w0, l
     unsigned am_n[NPF];
     h16x4 dp_n[NPF], dl_n[NPF];
     pool_load(q0, am_n, dp_n, dl_n);
-    for (int q = q0; q < q1; ++q) {
+    for (int rd = 0; rd < NR; ++rd) {
+      const int q = q0 + rd * QS;               // SPLIT: q >= NT in a wave's empty last round
       const EdgeSt<D> cur = xs0;
       unsigned am4[NPF];
       h16x4 dp4[NPF], dl4[NPF];
 #pragma unroll
       for (int p = 0; p < NPF; ++p) { am4[p] = am_n[p]; dp4[p] = dp_n[p]; dl4[p] = dl_n[p]; }
       ctrl_st_load<D>(a.S, a.s_env, xi1, xs0);
-      idx_load(ab, q + 2, xi1);
-      pool_load(q + 1, am_n, dp_n, dl_n);
+      idx_load(ab, q + 2 * QS, xi1);
+      pool_load(q + QS, am_n, dp_n, dl_n);
       int slot, al;
       if constexpr (EB_DENSE) {
         const int e = 32 * q + r;
@@ -2112,7 +2121,7 @@ __device__ __noinline__ void node_coop_call(const CtrlNodeBwdArgs& a, unsigned c
 }
 template <int D>
 __device__ __noinline__ void edge_bwd_call(const CtrlEdgeBwdArgs& a, unsigned char* smem, float* P) {
-  edge_bwd_body<D>(a, smem, 0, 1, P);
+  edge_bwd_body<D, 0, true>(a, smem, 0, 1, P);    // one 32-agent group at a time over all waves
 }
 
 template <int D>

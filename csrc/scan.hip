@@ -109,7 +109,7 @@ constexpr int SSC = 8;               // chunks per superchunk (second culling le
 static inline size_t scan_lds_bytes(int Nn) {
   const int Np = (Nn + SCH - 1) / SCH * SCH;
   const int nch = Np / SCH, nsc = (nch + SSC - 1) / SSC;
-  return (size_t)Np * 32 + (size_t)nch * 32 + (size_t)nsc * 32;
+  return (size_t)Np * 32 + (size_t)nch * 32 + (size_t)nsc * 32 + (size_t)Np * 2;   // + pinv (u16)
 }
 
 constexpr uint64_t KEY_EMPTY = (0x7f800000ull << 32) | 0xffffffffull;   // (+inf, max index)
@@ -228,6 +228,10 @@ __global__ __launch_bounds__(BS) void scan_kernel(ScanArgs a) {
     sbl = cbh + nch;                                           // [nsc] superchunk boxes
     sbh = sbl + nsc;
   }
+  // LDS path: curve position of every node id, so the neighbour records the kernel needs after
+  // the staging (the temporal bound's previous neighbours, the output slots' TTC test) come from
+  // the staged LDS arrays instead of dependent global gathers
+  unsigned short* pinv = reinterpret_cast<unsigned short*>(sbh + nsc);
   const float4* Sb = a.S + (long)b * a.s_env * REC<D>;
   const int* perm = a.perm + (long)b * Nn;
   if constexpr (GLB) {
@@ -243,6 +247,7 @@ __global__ __launch_bounds__(BS) void scan_kernel(ScanArgs a) {
       const float vz = (D == 3) ? v[D - 1] : 0.f;
       tp[q] = make_float4(p[0], p[1], z, __int_as_float(id));
       tv[q] = make_float4(v[0], v[1], vz, sqrtf(sqsum<D>(v)));
+      pinv[id] = (unsigned short)q;
     } else {
       tp[q] = make_float4(INFINITY, INFINITY, INFINITY, __int_as_float(-1));   // key == KEY_EMPTY
       tv[q] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -317,8 +322,15 @@ __global__ __launch_bounds__(BS) void scan_kernel(ScanArgs a) {
     if (act) {
       const int* pr = a.prev_idx + (long)b * a.pi_env + (long)i * K;
       for (int q = h; q < K; q += LPA) {
-        float pj[D], vj[D];
-        load_rec<D>(Sb, (unsigned)pr[q], pj, vj);
+        float pj[D];
+        if constexpr (GLB) {
+          float vj[D];
+          load_rec<D>(Sb, (unsigned)pr[q], pj, vj);
+        } else {
+          const float4 c = tp[pinv[pr[q]]];
+          pj[0] = c.x; pj[1] = c.y;
+          if constexpr (D == 3) pj[2] = c.z;
+        }
         float dp[D];
         dp[0] = me.x - pj[0];
         dp[1] = me.y - pj[1];
@@ -446,7 +458,12 @@ __global__ __launch_bounds__(BS) void scan_kernel(ScanArgs a) {
     int* out = a.idx + (long)b * a.i_env + (long)i * K;
     uint8_t* dout = a.dang ? a.dang + (long)b * a.i_env + (long)i * K : nullptr;
     float pi[D], vi[D];
-    load_rec<D>(Sb, (unsigned)i, pi, vi);
+    if constexpr (GLB) {
+      load_rec<D>(Sb, (unsigned)i, pi, vi);
+    } else {                                  // this lane's own staged record
+      pi[0] = me.x; pi[1] = me.y; vi[0] = mv.x; vi[1] = mv.y;
+      if constexpr (D == 3) { pi[2] = me.z; vi[2] = mv.z; }
+    }
 #pragma unroll
     for (int q0 = 0; q0 < K; q0 += LPA) {
       const int q = q0 + h;
@@ -460,7 +477,14 @@ __global__ __launch_bounds__(BS) void scan_kernel(ScanArgs a) {
         const int j = key == KEY_EMPTY ? i : (int)(unsigned)key;
         out[q] = j;
         float pj[D], vj[D], dp[D], dv[D];
-        load_rec<D>(Sb, (unsigned)j, pj, vj);
+        if constexpr (GLB) {
+          load_rec<D>(Sb, (unsigned)j, pj, vj);
+        } else {
+          const int qj = pinv[j];
+          const float4 cp = tp[qj], cv = tv[qj];
+          pj[0] = cp.x; pj[1] = cp.y; vj[0] = cv.x; vj[1] = cv.y;
+          if constexpr (D == 3) { pj[2] = cp.z; vj[2] = cv.z; }
+        }
         const float eye = (j == i) ? 1.f : 0.f;
 #pragma unroll
         for (int d = 0; d < D; ++d) { dp[d] = (pi[d] - pj[d]) + eye; dv[d] = vi[d] - vj[d]; }
