@@ -236,6 +236,8 @@ struct CtrlNodeBwdArgs {
   float4* cGout;       long cgo_env;   // G_{t+1} out
   int K;
   int coop;                            // set by the launchers: 32-agent chunks run node_bwd_coop
+  unsigned long long* stamps;          // diagnostics (null in production): node_bwd_coop phase clocks,
+                                       // [workgroup][wave][16] shader-clock values (scripts/stamps_node.py)
 };
 
 // MACBF_NODE_COOP=0 disables the cooperative 32-agent node backward (A/B runs)
@@ -360,6 +362,9 @@ int mb_cbf_bwd_x3(const mb::CbfBwdArgs* a, int num_blocks, hipStream_t st);
 int mb_ctrl_node_bwd(const mb::CtrlNodeBwdArgs* a, int num_blocks, hipStream_t st);
 int mb_ctrl_node_bwd_f16(const mb::CtrlNodeBwdArgs* a, int num_blocks, hipStream_t st);
 int mb_ctrl_node_bwd_x3(const mb::CtrlNodeBwdArgs* a, int num_blocks, hipStream_t st);
+int mb_ctrl_bwd_step(const mb::CtrlNodeBwdArgs* na, const mb::CtrlEdgeBwdArgs* ea, int num_blocks, hipStream_t st);
+int mb_ctrl_bwd_step_f16(const mb::CtrlNodeBwdArgs* na, const mb::CtrlEdgeBwdArgs* ea, int num_blocks, hipStream_t st);
+int mb_ctrl_bwd_step_x3(const mb::CtrlNodeBwdArgs* na, const mb::CtrlEdgeBwdArgs* ea, int num_blocks, hipStream_t st);
 int mb_ctrl_edge_bwd(const mb::CtrlEdgeBwdArgs* a, int num_blocks, hipStream_t st);
 int mb_ctrl_edge_bwd_f16(const mb::CtrlEdgeBwdArgs* a, int num_blocks, hipStream_t st);
 int mb_ctrl_edge_bwd_x3(const mb::CtrlEdgeBwdArgs* a, int num_blocks, hipStream_t st);

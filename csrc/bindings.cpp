@@ -239,13 +239,20 @@ static int adam(u64 param, u64 grad, u64 m, u64 v, int lo, int hi, float b1, flo
   return mb_adam(&a, ST(stream));
 }
 
-static int ctrl_node_bwd(u64 pooled, long p_env, u64 S, long s_env, u64 G, u64 A, long a_env, u64 Gn, long gn_env,
-                         u64 valid, long v_env, int B, int N, u64 wrm, int o1, int o2, int o3, int o4, u64 wvec,
-                         float act_coef, u64 act_scale, float dt, float sqrt3, u64 dP, long dp_env, u64 ego, u64 partial,
-                         int dim, int num_blocks, int prec, int init, int chunk, u64 gscale, py::tuple cmb,
-                         u64 stream) {
+#define NODE_BWD_PARAMS                                                                                     \
+  u64 pooled, long p_env, u64 S, long s_env, u64 G, u64 A, long a_env, u64 Gn, long gn_env, u64 valid, long v_env, \
+      int B, int N, u64 wrm, int o1, int o2, int o3, int o4, u64 wvec, float act_coef, u64 act_scale, float dt,    \
+      float sqrt3, u64 dP, long dp_env, u64 ego, u64 partial, int dim, int num_blocks, int prec, int init,          \
+      int chunk, u64 gscale, py::tuple cmb, u64 stamps
+#define NODE_BWD_ARGS                                                                                         \
+  pooled, p_env, S, s_env, G, A, a_env, Gn, gn_env, valid, v_env, B, N, wrm, o1, o2, o3, o4, wvec, act_coef,    \
+      act_scale, dt, sqrt3, dP, dp_env, ego, partial, dim, num_blocks, prec, init, chunk, gscale, cmb, stamps
+
+static mb::CtrlNodeBwdArgs node_bwd_args(NODE_BWD_PARAMS) {
+  (void)num_blocks; (void)prec;
   mb::CtrlNodeBwdArgs a{};
   a.gscale = P<const float>(gscale);
+  a.stamps = P<unsigned long long>(stamps);
   if (cmb.size() == 13) {     // fused BPTT combine: (dS, ds_env, ego, dEc, ptr, ptr_env, edges, edges_env, Gn, gn_env,
                               //                     Gout, go_env, K)
     a.cdS = P<const float4>(cmb[0].cast<u64>()); a.cds_env = cmb[1].cast<long>();
@@ -265,12 +272,23 @@ static int ctrl_node_bwd(u64 pooled, long p_env, u64 S, long s_env, u64 G, u64 A
   a.o_w1 = o1; a.o_w2 = o2; a.o_w3 = o3; a.o_w4 = o4; a.wvec = P<const float>(wvec);
   a.act_coef = act_coef; a.act_scale = P<const float>(act_scale); a.dt = dt; a.sqrt3 = sqrt3; a.dP = P<h16>(dP); a.dp_env = dp_env;
   a.ego = P<float4>(ego); a.partial = P<float>(partial);
+  return a;
+}
+
+static int ctrl_node_bwd(NODE_BWD_PARAMS, u64 stream) {
+  const mb::CtrlNodeBwdArgs a = node_bwd_args(NODE_BWD_ARGS);
   return (prec == 2 ? mb_ctrl_node_bwd_x3 : prec == 1 ? mb_ctrl_node_bwd_f16 : mb_ctrl_node_bwd)(&a, num_blocks, ST(stream));
 }
 
-static int ctrl_edge_bwd(u64 S, long s_env, u64 idx, long i_env, u64 argmax, long am_env, u64 dP, long dp_env,
-                         int B, int N, int K, u64 wpack, int f_ew1f, int f_ew2tn, u64 dEc, long de_env, u64 partial,
-                         int dim, int num_blocks, int prec, int qsplit, int init, u64 stream) {
+#define EDGE_BWD_PARAMS                                                                                     \
+  u64 S, long s_env, u64 idx, long i_env, u64 argmax, long am_env, u64 dP, long dp_env, int B, int N, int K,  \
+      u64 wpack, int f_ew1f, int f_ew2tn, u64 dEc, long de_env, u64 partial, int dim, int num_blocks, int prec, \
+      int qsplit, int init
+#define EDGE_BWD_ARGS \
+  S, s_env, idx, i_env, argmax, am_env, dP, dp_env, B, N, K, wpack, f_ew1f, f_ew2tn, dEc, de_env, partial, dim, num_blocks, prec, qsplit, init
+
+static mb::CtrlEdgeBwdArgs edge_bwd_args(EDGE_BWD_PARAMS) {
+  (void)num_blocks; (void)prec;
   mb::CtrlEdgeBwdArgs a{};
   a.init = init;
   a.dim = dim;
@@ -279,7 +297,35 @@ static int ctrl_edge_bwd(u64 S, long s_env, u64 idx, long i_env, u64 argmax, lon
   a.argmax = P<const uint8_t>(argmax); a.am_env = am_env; a.dP = P<const h16>(dP); a.dp_env = dp_env;
   a.B = B; a.N = N; a.K = K; a.wpack = P<const h16>(wpack); a.f_ew1f = f_ew1f; a.f_ew2tn = f_ew2tn;
   a.dEc = P<float4>(dEc); a.de_env = de_env; a.partial = P<float>(partial);
+  return a;
+}
+
+static int ctrl_edge_bwd(EDGE_BWD_PARAMS, u64 stream) {
+  const mb::CtrlEdgeBwdArgs a = edge_bwd_args(EDGE_BWD_ARGS);
   return (prec == 2 ? mb_ctrl_edge_bwd_x3 : prec == 1 ? mb_ctrl_edge_bwd_f16 : mb_ctrl_edge_bwd)(&a, num_blocks, ST(stream));
+}
+
+// One fused BPTT step (ctrl.hip ctrl_bwd_step_kernel): `node` and `edge` are the argument tuples
+// of ctrl_node_bwd / ctrl_edge_bwd without the stream; one launch of num_blocks workgroups.
+static int ctrl_bwd_step(py::tuple node, py::tuple edge, int num_blocks, int prec, u64 stream) {
+  if (node.size() != 35 || edge.size() != 22) throw std::invalid_argument("ctrl_bwd_step: bad argument tuples");
+  auto n = [&](int i) { return node[i]; };
+  const mb::CtrlNodeBwdArgs na = node_bwd_args(
+      n(0).cast<u64>(), n(1).cast<long>(), n(2).cast<u64>(), n(3).cast<long>(), n(4).cast<u64>(), n(5).cast<u64>(),
+      n(6).cast<long>(), n(7).cast<u64>(), n(8).cast<long>(), n(9).cast<u64>(), n(10).cast<long>(), n(11).cast<int>(),
+      n(12).cast<int>(), n(13).cast<u64>(), n(14).cast<int>(), n(15).cast<int>(), n(16).cast<int>(), n(17).cast<int>(),
+      n(18).cast<u64>(), n(19).cast<float>(), n(20).cast<u64>(), n(21).cast<float>(), n(22).cast<float>(),
+      n(23).cast<u64>(), n(24).cast<long>(), n(25).cast<u64>(), n(26).cast<u64>(), n(27).cast<int>(), n(28).cast<int>(),
+      n(29).cast<int>(), n(30).cast<int>(), n(31).cast<int>(), n(32).cast<u64>(), n(33).cast<py::tuple>(),
+      n(34).cast<u64>());
+  auto e = [&](int i) { return edge[i]; };
+  const mb::CtrlEdgeBwdArgs ea = edge_bwd_args(
+      e(0).cast<u64>(), e(1).cast<long>(), e(2).cast<u64>(), e(3).cast<long>(), e(4).cast<u64>(), e(5).cast<long>(),
+      e(6).cast<u64>(), e(7).cast<long>(), e(8).cast<int>(), e(9).cast<int>(), e(10).cast<int>(), e(11).cast<u64>(),
+      e(12).cast<int>(), e(13).cast<int>(), e(14).cast<u64>(), e(15).cast<long>(), e(16).cast<u64>(), e(17).cast<int>(),
+      e(18).cast<int>(), e(19).cast<int>(), e(20).cast<int>(), e(21).cast<int>());
+  return (prec == 2 ? mb_ctrl_bwd_step_x3 : prec == 1 ? mb_ctrl_bwd_step_f16 : mb_ctrl_bwd_step)(&na, &ea, num_blocks,
+                                                                                                 ST(stream));
 }
 
 static int probe_mfma(u64 a, u64 b, u64 d, u64 stream) {
@@ -341,6 +387,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("probe_tr", &probe_tr);
   m.def("probe_smfmac", &probe_smfmac);
   m.def("probe_lane_xor", &probe_lane_xor);
+  m.def("ctrl_bwd_step", &ctrl_bwd_step);
   m.def("device_info", &device_info);
   m.def("err_str", &err_str);
   m.attr("ARCH") = "gfx950";

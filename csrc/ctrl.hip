@@ -1267,6 +1267,8 @@ DEV void node_bwd_coop(const CtrlNodeBwdArgs& a, unsigned char* smem, long c0, l
   float* vl = reinterpret_cast<float*>(smem + RM * 2);
   h16* stg = reinterpret_cast<h16*>(smem + RM * 2 + CTRL_VEC * 4);
   block_copy16(wr, a.wrm, RM * 2);
+  if (a.stamps && (threadIdx.x & 63) == 0)
+    a.stamps[((long)blockIdx.x * NB_WAVES + threadIdx.x / WAVE) * 16] = __builtin_amdgcn_s_memtime();
   block_copy16(vl, a.wvec, CTRL_VEC * 4);
   __syncthreads();
   const float* nb2 = vl + 128;
@@ -1278,6 +1280,15 @@ DEV void node_bwd_coop(const CtrlNodeBwdArgs& a, unsigned char* smem, long c0, l
   const long nchunks = (total + 31) / 32;
   constexpr int LO = NODE_RM_LO;
   const h16x8 zz = zero_h8();
+  // diagnostics: shader clock at the phase boundaries (a.stamps, normally null; a workgroup with
+  // several chunks keeps its last chunk's clocks, slot 15 = that chunk's start)
+  auto stamp = [&](int k) {
+    if (a.stamps) {
+      const unsigned long long t = __builtin_amdgcn_s_memtime();
+      if (lane == 0) a.stamps[((long)blockIdx.x * NB_WAVES + wave) * 16 + k] = t;
+    }
+  };
+  stamp(1);                                            // weights staged
   // owned weight-gradient tiles: S4 (dW4pad 1x2) wave < 2 nt = wave; S3 (2x4) t = wave + 4u;
   // S2 (4x2) t = wave + 4u; S1 (2x5) t = wave + 4u (u < 3, t < 10)
   f32x16 acc4 = zero16(), acc3[2], acc2[2], acc1[3];
@@ -1291,6 +1302,7 @@ DEV void node_bwd_coop(const CtrlNodeBwdArgs& a, unsigned char* smem, long c0, l
   auto img_fr = [&](int col0, int kk) { return row_fr(stg + r * SW + col0 + 16 * kk + 8 * h, PLN); };
 
   for (long chunk = c0; chunk < nchunks; chunk += cstride) {
+    stamp(15);
     const int ga = (int)(chunk * 32) + r;
     const bool ok = ga < total;
     int b = 0, i = 0;
@@ -1314,6 +1326,7 @@ DEV void node_bwd_coop(const CtrlNodeBwdArgs& a, unsigned char* smem, long c0, l
     float ex[D];
 #pragma unroll
     for (int q = 0; q < D; ++q) ex[q] = sp[q] - gg[q];
+    stamp(2);
     const h16x8 sfr = node_state_frag<D>(ex, sv, ok, h);
     const h16* prow = a.pooled + (long)b * a.p_env + (long)i * PROW;
     const h16* W1 = wr + opaque_zero();
@@ -1337,6 +1350,7 @@ DEV void node_bwd_coop(const CtrlNodeBwdArgs& a, unsigned char* smem, long c0, l
       store_pk(stg, SW, r, 32 * wave, Y1b, h, PLN);
     }
     __syncthreads();
+    stamp(3);
     // ---- L2 (all waves): Y2 tile `wave`
     {
       f32x16 c = bias_rows(nb2, 32 * wave, h);
@@ -1348,6 +1362,7 @@ DEV void node_bwd_coop(const CtrlNodeBwdArgs& a, unsigned char* smem, long c0, l
     __syncthreads();                                   // Y1 image read by every wave
     store_pk(stg, SW, r, 32 * wave, Y2b, h, PLN);
     __syncthreads();
+    stamp(4);
     // ---- L3 (waves 2, 3): Y3 tile wave - 2
     if (wave >= 2) {
       const int mt = wave - 2;
@@ -1359,6 +1374,7 @@ DEV void node_bwd_coop(const CtrlNodeBwdArgs& a, unsigned char* smem, long c0, l
       store_pk(stg, SW, r, 128 + 32 * mt, Y3b, h, PLN);
     }
     __syncthreads();
+    stamp(5);
     // ---- L4 + gain law + action-loss backward (wave 0) -> d4, ego terms
     float egp[D], egv[D];
 #pragma unroll
@@ -1408,6 +1424,7 @@ DEV void node_bwd_coop(const CtrlNodeBwdArgs& a, unsigned char* smem, long c0, l
       store_pk(stg, SW, r, 192, to_pk(d4), h, PLN);
     }
     __syncthreads();
+    stamp(6);
     // ---- dY3 (waves 1, 2): tile wave - 1 = (W4^T d4) . relu'(Y3)
     if (wave == 1 || wave == 2) {
       const int mt = wave - 1;
@@ -1421,6 +1438,7 @@ DEV void node_bwd_coop(const CtrlNodeBwdArgs& a, unsigned char* smem, long c0, l
       store_pk(stg, SW, r, 224 + 32 * mt, d3b, h, PLN);
     }
     __syncthreads();
+    stamp(7);
     // ---- S4: dW4pad (32x64) += d4 . Y3^T ; nb4  (waves 0, 1)   S3: dW3 (64x128) += d3 . Y2^T ; nb3
     if (wave < 2)
       bs4 += stage_mma_fr<2>(stg + 192, SW, PLN, stg + 128, SW, PLN, 0, wave, lane, acc4, 0, wave == 0 ? 2 : 0);
@@ -1442,6 +1460,7 @@ DEV void node_bwd_coop(const CtrlNodeBwdArgs& a, unsigned char* smem, long c0, l
     store_pk(stg, SW, r, 32 * wave, d2b, h, PLN);
     if (wave < 2) store_pk(stg, SW, r, 128 + 32 * wave, Y1b, h, PLN);
     __syncthreads();
+    stamp(8);
     // ---- S2: dW2 (128x64) += d2 . Y1^T ; nb2
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
@@ -1458,6 +1477,7 @@ DEV void node_bwd_coop(const CtrlNodeBwdArgs& a, unsigned char* smem, long c0, l
       mask_pk(d1b, Y1b);
     }
     __syncthreads();                                   // S2 images and d2 read by every wave
+    stamp(9);
     // ---- S1 images: d1 (cols 0..63), [P | s | 0] (cols 64..223: pooled 128, state fragment 16, zeros 16)
     if (wave < 2) store_pk(stg, SW, r, 32 * wave, d1b, h, PLN);
 #pragma unroll
@@ -1479,12 +1499,14 @@ DEV void node_bwd_coop(const CtrlNodeBwdArgs& a, unsigned char* smem, long c0, l
       }
     }
     __syncthreads();
+    stamp(10);
     // ---- S1: dW1f (64x160) += d1 . [P | s]^T
 #pragma unroll
     for (int u = 0; u < 3; ++u) {
       const int t = wave + 4 * u;
       if (u < n1) stage_mma_fr<2>(stg, SW, PLN, stg + 64, SW, PLN, t / 5, t % 5, lane, acc1[u]);
     }
+    stamp(11);
     // ---- dP = W1f^T d1: tiles 0..3 (one per wave) -> dL/dpooled rows; tile 4 (wave 0) -> ego
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
@@ -1519,7 +1541,9 @@ DEV void node_bwd_coop(const CtrlNodeBwdArgs& a, unsigned char* smem, long c0, l
       }
     }
     __syncthreads();                                   // region reused by the next chunk
+    stamp(12);
   }
+  stamp(13);
   // ---- slab += this workgroup's partial (fixed tile owners: deterministic); loads first
   f32x16 o1[3], o2[2], o3[2], o4 = zero16();
   float ob2[2] = {0.f, 0.f}, ob3[2] = {0.f, 0.f}, ob4 = 0.f;
@@ -1565,6 +1589,8 @@ DEV void node_bwd_coop(const CtrlNodeBwdArgs& a, unsigned char* smem, long c0, l
       if (h == 0) P[NP_B4 + r] = ob4 + s4;
     }
   }
+  if (a.stamps) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  stamp(14);                                           // slab stores complete
 }
 
 template <int D>
@@ -1910,6 +1936,16 @@ __global__ __launch_bounds__(EB_WAVES * 64, (EB_WAVES == 4 && !X3) ? 2 : 1) void
   edge_bwd_body<D, KC>(a, smem, blockIdx.x, gridDim.x, a.partial + (long)blockIdx.x * CTRL_EDGE_PARTIAL);
 }
 
+static_assert(EB_WAVES == NB_WAVES, "the fused BPTT step runs both phases with one block shape");
+template <int D, int KC>
+__global__ __launch_bounds__(NB_WAVES * 64, 1) void ctrl_bwd_step_kernel(CtrlNodeBwdArgs na, CtrlEdgeBwdArgs ea) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  node_bwd_coop<D>(na, smem, blockIdx.x, gridDim.x, na.partial + (long)blockIdx.x * CTRL_NODE_PARTIAL);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this workgroup's dP / ego stores complete
+  __syncthreads();                                      // (and the node phase's LDS reads done)
+  edge_bwd_body<D, KC, true>(ea, smem, blockIdx.x, gridDim.x, ea.partial + (long)blockIdx.x * CTRL_EDGE_PARTIAL);
+}
+
 // =======================================================================================
 // Persistent small-scene rollout (envs of <= SMALL_MAXN graph nodes; reference train.py:58-81).
 // The per-step kernels of a 32-agent env are single-workgroup launches whose latency, not work,
@@ -2223,6 +2259,38 @@ extern "C" int MB_SYM(ctrl_edge_bwd)(const mb::CtrlEdgeBwdArgs* a, int num_block
   } else {
     if (k12) go(ctrl_edge_bwd_kernel<2, 12>);
     else go(ctrl_edge_bwd_kernel<2>);
+  }
+  return (int)hipGetLastError();
+}
+
+// One BPTT step in one launch for the cooperative regime (32-agent chunks: strong-scaling slices):
+// the node backward of a workgroup's chunks, then the edge backward of the SAME agents (SPLIT: a
+// chunk's K edge tiles over the four waves). The edge phase needs only its own agents' dL/dpooled
+// rows, written by this workgroup's node phase (stores drained + barrier, same CU), so no grid-wide
+// synchronisation; the next step's node phase (fused combine: other agents' in-edges) is the next
+// launch. Saves one launch and its drain per reverse step. Slab rows: one node and one edge row
+// per workgroup.
+extern "C" int MB_SYM(ctrl_bwd_step)(const mb::CtrlNodeBwdArgs* na, const mb::CtrlEdgeBwdArgs* ea, int num_blocks,
+                                     hipStream_t st) {
+  using namespace mb;
+  using namespace mb::MB_PREC;
+  if (ea->K > 16 || ea->K < 1 || na->chunk != 32 || na->dim != ea->dim || na->B != ea->B || na->N != ea->N) return -1;
+  const size_t lds = ctrl_node_bwd_lds() > ctrl_edge_bwd_lds() ? ctrl_node_bwd_lds() : ctrl_edge_bwd_lds();
+  CtrlNodeBwdArgs n = *na;
+  n.coop = 1;
+  CtrlEdgeBwdArgs e = *ea;
+  e.qsplit = 1;
+  auto go = [&](auto kern) {
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(kern, dim3(num_blocks), dim3(NB_WAVES * 64), lds, st, n, e);
+  };
+  const bool k12 = ea->K == 12;
+  if (ea->dim == 3) {
+    if (k12) go(ctrl_bwd_step_kernel<3, 12>);
+    else go(ctrl_bwd_step_kernel<3, 0>);
+  } else {
+    if (k12) go(ctrl_bwd_step_kernel<2, 12>);
+    else go(ctrl_bwd_step_kernel<2, 0>);
   }
   return (int)hipGetLastError();
 }

@@ -355,6 +355,9 @@ class BpttDriver {
     dt_ = F("dt"); sqrt3_ = F("sqrt3");
     small_ = (int)I("small");
     node_chunk_ = (int)I("node_chunk");
+    fused_ = c.contains("fused_step") ? (int)I("fused_step") : 0;
+    if (fused_ && (node_chunk_ != 32 || nb_node_ != nb_edge_))
+      throw std::invalid_argument("BpttDriver: the fused step needs 32-agent chunks and one grid");
     gscale_ = c.contains("gscale") ? U("gscale") : 0;   // fp16: device loss scale (or 0)
     if (B_ < 1 || N_ < 1 || Nn_ < N_ || K_ < 1 || K_ > 16 || (D_ != 2 && D_ != 3) || Tmax_ < 1 || nb_node_ < 1 ||
         nb_edge_ < 1)
@@ -394,8 +397,10 @@ class BpttDriver {
     for (int t = T - 1; t >= 0; --t) {
       const float4* Gn = P<const float4>(dS_) + (long)T * BN * R_;       // t = T-1: the direct terms dS_T
       const float4* St = P<const float4>(S_) + (long)t * B_ * Nn_ * R_;
+      mb::CtrlNodeBwdArgs na{};
+      mb::CtrlEdgeBwdArgs ea{};
       {
-        mb::CtrlNodeBwdArgs a{};
+        mb::CtrlNodeBwdArgs& a = na;
         a.dim = D_;
         a.pooled = P<const h16>(pooled_) + (long)t * BN * prow_; a.p_env = (long)N_ * prow_;
         a.S = St; a.s_env = Nn_;
@@ -422,10 +427,9 @@ class BpttDriver {
           a.cgn_env = N_;
           a.cGout = P<float4>(Gb_) + t1 * BN * R_; a.cgo_env = N_;
         }
-        chk((prec_ == 2 ? mb_ctrl_node_bwd_x3 : prec_ == 1 ? mb_ctrl_node_bwd_f16 : mb_ctrl_node_bwd)(&a, nb_node_, st), "ctrl_node_bwd");
       }
       {
-        mb::CtrlEdgeBwdArgs a{};
+        mb::CtrlEdgeBwdArgs& a = ea;
         a.dim = D_;
         a.S = St; a.s_env = Nn_;
         a.idx = P<const int>(idx_) + (long)t * B_ * nk; a.i_env = nk;
@@ -435,7 +439,15 @@ class BpttDriver {
         a.wpack = P<const h16>(wpack_); a.f_ew1f = f_ew1f_; a.f_ew2tn = f_ew2tn_;
         a.dEc = P<float4>(dEc_); a.de_env = nk; a.partial = P<float>(part_edge_); a.qsplit = qsplit_;
         a.init = t == T - 1;
-        chk((prec_ == 2 ? mb_ctrl_edge_bwd_x3 : prec_ == 1 ? mb_ctrl_edge_bwd_f16 : mb_ctrl_edge_bwd)(&a, nb_edge_, st), "ctrl_edge_bwd");
+      }
+      if (fused_) {      // node + edge backward of the same 32-agent chunks in one launch
+        chk((prec_ == 2 ? mb_ctrl_bwd_step_x3 : prec_ == 1 ? mb_ctrl_bwd_step_f16 : mb_ctrl_bwd_step)(&na, &ea, nb_node_, st),
+            "ctrl_bwd_step");
+      } else {
+        chk((prec_ == 2 ? mb_ctrl_node_bwd_x3 : prec_ == 1 ? mb_ctrl_node_bwd_f16 : mb_ctrl_node_bwd)(&na, nb_node_, st),
+            "ctrl_node_bwd");
+        chk((prec_ == 2 ? mb_ctrl_edge_bwd_x3 : prec_ == 1 ? mb_ctrl_edge_bwd_f16 : mb_ctrl_edge_bwd)(&ea, nb_edge_, st),
+            "ctrl_edge_bwd");
       }
       // (no combine launch: the next step's node backward forms G_t in its prologue; G_0 = dL/ds_0
       // is not needed -- s_0 is sampled, not a function of the weights)
@@ -443,7 +455,7 @@ class BpttDriver {
   }
 
  private:
-  int B_, N_, Nn_, K_, D_, R_, Tmax_, prec_, prow_, nb_node_, nb_edge_, qsplit_, small_ = 0, node_chunk_ = 0;
+  int B_, N_, Nn_, K_, D_, R_, Tmax_, prec_, prow_, nb_node_, nb_edge_, qsplit_, small_ = 0, node_chunk_ = 0, fused_ = 0;
   u64 pooled_, S_, G_, A_, dS_, Gb_, valid_, idx_, argmax_, rptr_, redges_, wrm_, wvec_, act_scale_, dP_, ego_, dEc_;
   u64 part_node_, part_edge_, wpack_, gscale_ = 0;
   int o1_, o2_, o3_, o4_, f_ew1f_, f_ew2tn_;

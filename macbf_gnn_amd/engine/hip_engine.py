@@ -661,6 +661,7 @@ class HipEngine:
                 ctrl_w=native.ptr(pw.ctrl_w), f_ew1f=int(pw.ctrl_off["ew1f"]), f_ew2tn=int(pw.ctrl_off["ew2tn"]),
                 dt=float(C.TIME_STEP), sqrt3=float(C.SQRT3), small=int(self.small_bptt),
                 node_chunk=int(native.node_bwd_chunk(B * N, self.dev)),
+                fused_step=int(native.bwd_step_fused(B * N, self.dev)),
                 gscale=native.ptr(getattr(self.tr, "gscale_dev", None))))
             self._bdrv = native.lib().BpttDriver(c)
         return self._bdrv
@@ -678,13 +679,19 @@ class HipEngine:
                 cmb = dict(dS=self.dS[t + 1][sl], ego=self.ego[sl], dEc=self.dEc[sl], rptr=rptr3[t + 1][sl],
                            redges=redges3[t + 1][sl], Gn=self.dS[T][sl] if t + 1 == T - 1 else self.Gb[t + 2][sl],
                            Gout=self.Gb[t + 1][sl], K=K)
-            native.ctrl_node_bwd(self.pooled[t][sl], self.S[t][sl], self.G[sl], self.A[t][sl], self.dS[T][sl],
-                                 valid_u8[t][sl], pw.ctrl_rm, pw.node_rm_off, pw.ctrl_v, gs * ACT_COEF, self.dP[sl],
-                                 self.ego[sl], part_node, nbn, act_cnt=self.counts[2:3], prec=self.prec, init=t == T - 1,
-                                 gscale=getattr(self.tr, "gscale_dev", None), combine=cmb)
-            native.ctrl_edge_bwd(self.S[t][sl], self.idx[t][sl], self.argmax[t][sl], self.dP[sl], pw.ctrl_w,
-                                 pw.ctrl_off["ew1f"], pw.ctrl_off["ew2tn"], self.dEc[sl], part_edge, nbe, prec=self.prec,
-                                 init=t == T - 1)
+            node = dict(pooled=self.pooled[t][sl], S=self.S[t][sl], G=self.G[sl], A=self.A[t][sl], Gn=self.dS[T][sl],
+                        valid_t=valid_u8[t][sl], wrm=pw.ctrl_rm, offs=pw.node_rm_off, wvec=pw.ctrl_v,
+                        act_coef=gs * ACT_COEF, dP=self.dP[sl], ego=self.ego[sl], partial=part_node,
+                        act_cnt=self.counts[2:3], prec=self.prec, init=t == T - 1,
+                        gscale=getattr(self.tr, "gscale_dev", None), combine=cmb)
+            edge = dict(S=self.S[t][sl], idx=self.idx[t][sl], argmax=self.argmax[t][sl], dP=self.dP[sl], wpack=pw.ctrl_w,
+                        f_ew1f=pw.ctrl_off["ew1f"], f_ew2tn=pw.ctrl_off["ew2tn"], dEc=self.dEc[sl], partial=part_edge,
+                        prec=self.prec, init=t == T - 1)
+            if nbn == nbe and native.bwd_step_fused(self.G[sl].shape[0] * self.N, self.dev):
+                native.ctrl_bwd_step(node, edge, nbn)            # node + edge backward: one launch
+            else:
+                native.ctrl_node_bwd(**node, num_blocks=nbn)
+                native.ctrl_edge_bwd(**edge, num_blocks=nbe)
 
     def _counts_ready(self, work):
         """Join the (async) count all-reduce (the node backward reads the action-loss count

@@ -767,17 +767,21 @@ def ctrl_bwd_grids(total_agents: int, device, prec=None):
     ch = (total_agents + ca - 1) // ca
     che = (total_agents + 32 * CTRL_EDGE_WAVES - 1) // (32 * CTRL_EDGE_WAVES)
     cu = num_cu(device)
+    if bwd_step_fused(total_agents, device):      # one fused launch per step: one grid for both
+        n = max(1, min(ch, cu))
+        return n, n
     per_cu = 1 if prec == "fp32" else 8 // CTRL_EDGE_WAVES
     per_cu = int(os.environ.get("MACBF_EDGE_WG_PER_CU", per_cu))
     return max(1, min(ch, cu)), max(1, min(che * ctrl_edge_qsplit(total_agents, device), per_cu * cu))
 
 
 def ctrl_node_bwd(pooled, S, G, A, Gn, valid_t, wrm, offs, wvec, act_coef, dP, ego, partial, num_blocks,
-                  act_cnt=None, prec=None, init=False, chunk=None, gscale=None, combine=None):
+                  act_cnt=None, prec=None, init=False, chunk=None, gscale=None, combine=None, stamps=None, _defer=False):
     """act_cnt: optional 1-element device tensor holding the (all-reduced) action-loss count
     n_act; the action-loss coefficient is then act_coef / max(n_act, 1), read by the kernel (no
     host round trip, no extra launch). init: write the weight-gradient slabs instead of
-    accumulating into them (no zero fill needed)."""
+    accumulating into them (no zero fill needed). stamps: diagnostics only, int64
+    (num_blocks, 4, 16) phase clocks of the cooperative 32-agent path (scripts/stamps_node.py)."""
     B, N = G.shape[:2]
     D = dim_of(S)
     W = rec_width(D)
@@ -798,6 +802,7 @@ def ctrl_node_bwd(pooled, S, G, A, Gn, valid_t, wrm, offs, wvec, act_coef, dP, e
     check(partial, torch.float32, (num_blocks, CTRL_NODE_PARTIAL), "partial")
     check(act_cnt, torch.float32, (1,), "act_cnt")
     check(gscale, torch.float32, (1,), "gscale")
+    check(stamps, torch.int64, (num_blocks, 4, 16), "stamps")
     cmb = ()
     if combine is not None:
         # fused BPTT combine: Gn is formed in the kernel from step t+1's records (node_combine's terms)
@@ -816,17 +821,20 @@ def ctrl_node_bwd(pooled, S, G, A, Gn, valid_t, wrm, offs, wvec, act_coef, dP, e
         cmb = (ptr(c["dS"]), c["dS"].stride(0) // W, ptr(c["ego"]), ptr(c["dEc"]), ptr(c["rptr"]), c["rptr"].stride(0),
                ptr(c["redges"]), c["redges"].stride(0), ptr(Gn_c), Gn_c.stride(0) // W if Gn_c is not None else 0,
                ptr(c["Gout"]), c["Gout"].stride(0) // W, K)
-    rc = lib().ctrl_node_bwd(ptr(pooled), pooled.stride(0), ptr(S), S.stride(0) // W, ptr(G), ptr(A), A.stride(0) // D,
-                             ptr(Gn), Gn.stride(0) // W if Gn is not None else 0,
-                             ptr(valid_t), valid_t.stride(0) if valid_t is not None else 0, B, N,
-                             ptr(wrm), offs["w1"], offs["w2"], offs["w3"], offs["w4"], ptr(wvec),
-                             float(act_coef), ptr(act_cnt), float(C.TIME_STEP), float(C.SQRT3), ptr(dP), dP.stride(0),
-                             ptr(ego), ptr(partial), D, int(num_blocks), f16, int(bool(init)),
-                             int(chunk or node_bwd_chunk(B * N, S.device)), ptr(gscale), cmb, stream_handle())
-    _ok(rc, "ctrl_node_bwd")
+    args = (ptr(pooled), pooled.stride(0), ptr(S), S.stride(0) // W, ptr(G), ptr(A), A.stride(0) // D,
+            ptr(Gn), Gn.stride(0) // W if Gn is not None else 0,
+            ptr(valid_t), valid_t.stride(0) if valid_t is not None else 0, B, N,
+            ptr(wrm), offs["w1"], offs["w2"], offs["w3"], offs["w4"], ptr(wvec),
+            float(act_coef), ptr(act_cnt), float(C.TIME_STEP), float(C.SQRT3), ptr(dP), dP.stride(0),
+            ptr(ego), ptr(partial), D, int(num_blocks), f16, int(bool(init)),
+            int(chunk or node_bwd_chunk(B * N, S.device)), ptr(gscale), cmb, ptr(stamps))
+    if _defer:
+        return args
+    _ok(lib().ctrl_node_bwd(*args, stream_handle()), "ctrl_node_bwd")
 
 
-def ctrl_edge_bwd(S, idx, argmax, dP, wpack, f_ew1f, f_ew2tn, dEc, partial, num_blocks, prec=None, init=False):
+def ctrl_edge_bwd(S, idx, argmax, dP, wpack, f_ew1f, f_ew2tn, dEc, partial, num_blocks, prec=None, init=False,
+                  _defer=False):
     B, N, K = idx.shape
     D = dim_of(S)
     W = rec_width(D)
@@ -840,11 +848,37 @@ def ctrl_edge_bwd(S, idx, argmax, dP, wpack, f_ew1f, f_ew2tn, dEc, partial, num_
         raise NativeError("packed controller weights too small")
     check(dEc, torch.float32, (B, N, K, W), "dEc")
     check(partial, torch.float32, (num_blocks, CTRL_EDGE_PARTIAL), "partial")
-    rc = lib().ctrl_edge_bwd(ptr(S), S.stride(0) // W, ptr(idx), idx.stride(0), ptr(argmax), argmax.stride(0),
-                             ptr(dP), dP.stride(0), B, N, K, ptr(wpack), int(f_ew1f), int(f_ew2tn), ptr(dEc),
-                             dEc.stride(0) // W if dEc is not None else 0, ptr(partial), D, int(num_blocks),
-                             f16, ctrl_edge_qsplit(B * N, S.device), int(bool(init)), stream_handle())
-    _ok(rc, "ctrl_edge_bwd")
+    args = (ptr(S), S.stride(0) // W, ptr(idx), idx.stride(0), ptr(argmax), argmax.stride(0),
+            ptr(dP), dP.stride(0), B, N, K, ptr(wpack), int(f_ew1f), int(f_ew2tn), ptr(dEc),
+            dEc.stride(0) // W if dEc is not None else 0, ptr(partial), D, int(num_blocks),
+            f16, ctrl_edge_qsplit(B * N, S.device), int(bool(init)))
+    if _defer:
+        return args
+    _ok(lib().ctrl_edge_bwd(*args, stream_handle()), "ctrl_edge_bwd")
+
+
+def ctrl_bwd_step(node: dict, edge: dict, num_blocks: int):
+    """One fused BPTT step (csrc/ctrl.hip ctrl_bwd_step_kernel): the node backward of each
+    workgroup's 32-agent chunks, then the edge backward of the same agents, in one launch.
+    `node` / `edge` are the keyword arguments of ctrl_node_bwd / ctrl_edge_bwd (validated the same
+    way); both run on num_blocks workgroups (their slabs need num_blocks rows each)."""
+    na = ctrl_node_bwd(**node, num_blocks=num_blocks, chunk=32, _defer=True)
+    ea = ctrl_edge_bwd(**edge, num_blocks=num_blocks, _defer=True)
+    _ok(lib().ctrl_bwd_step(na, ea, int(num_blocks), na[29], stream_handle()), "ctrl_bwd_step")
+
+
+BWD_FUSED_DEFAULT = False
+
+
+def bwd_step_fused(total_agents: int, device) -> bool:
+    """Whether the BPTT runs as fused node+edge launches (ctrl_bwd_step): in the cooperative regime
+    (32-agent node chunks) with at least half a chunk per CU -- strong-scaling slices. Small scenes
+    keep the separate launches: their edge backward splits a chunk over up to 16 workgroups
+    (qsplit), which one fused workgroup cannot. MACBF_BWD_FUSED=0/1 forces the choice."""
+    env = os.environ.get("MACBF_BWD_FUSED")
+    if env is not None:
+        return env == "1" and node_bwd_chunk(total_agents, device) == 32
+    return BWD_FUSED_DEFAULT and node_bwd_chunk(total_agents, device) == 32 and (total_agents + 31) // 32 >= num_cu(device) // 2
 
 
 def reduce_rows(partial, out, accumulate=False):

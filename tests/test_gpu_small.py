@@ -120,3 +120,30 @@ def test_small_bptt_matches_per_step_launches(kw):
     g1 = b.fp.grad.clone()
     b.engine.step(s0, g, obs)
     assert torch.equal(g1, b.fp.grad)
+
+
+@pytest.mark.parametrize("native_bptt", [True, False])
+def test_fused_bptt_step_matches_separate_launches(native_bptt, monkeypatch):
+    """Fused node + edge backward per reverse step (csrc/ctrl.hip ctrl_bwd_step_kernel, the
+    strong-scaling slice path) against the separate node / edge launches: the recursion (G, dP,
+    ego) bit for bit; the weight gradients up to the slab summation order (the edge slab rows
+    differ)."""
+    from macbf_gnn_amd.engine.hip_engine import HipEngine
+    monkeypatch.setattr(HipEngine, "native_bptt", native_bptt)
+    trs = []
+    for fused in ("0", "1"):
+        monkeypatch.setenv("MACBF_BWD_FUSED", fused)
+        trs.append(_trainer(False, small_bptt=False, N=256, B=8, T=12))
+    a, b = trs
+    assert b.engine.nb_node == b.engine.nb_edge
+    b.fp.flat.copy_(a.fp.flat)
+    b.engine.after_update()
+    s0, g, obs = a.sample()
+    monkeypatch.setenv("MACBF_BWD_FUSED", "0")
+    a.engine.step(s0, g, obs)
+    monkeypatch.setenv("MACBF_BWD_FUSED", "1")
+    b.engine.step(s0, g, obs)
+    torch.cuda.synchronize()
+    assert torch.equal(a.engine.Gb, b.engine.Gb)
+    assert torch.equal(a.engine.dP, b.engine.dP) and torch.equal(a.engine.ego, b.engine.ego)
+    torch.testing.assert_close(b.fp.grad, a.fp.grad, rtol=2e-5, atol=1e-8)
