@@ -266,6 +266,7 @@ struct CsrArgs {
   int Nn;              // target nodes (agents + obstacle points); 0 = N
   int* ptr;            // (G, Nn+1) incoming-edge offsets
   int* edges;          // (G, N*K) incoming edge ids (i*K + k), self edges excluded
+  int* ws;             // (G, Nn) fill counters of the global path (envs whose counters exceed LDS)
 };
 
 struct NodeRedArgs {

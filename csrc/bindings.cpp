@@ -132,9 +132,10 @@ static int cbf_bwd(u64 S, long s_env, long s_step, u64 idx, int B, int T, int N,
   return (prec == 2 ? mb_cbf_bwd_x3 : prec == 1 ? mb_cbf_bwd_f16 : mb_cbf_bwd)(&a, num_blocks, ST(stream));
 }
 
-static int rev_csr(u64 idx, int G, int N, int K, u64 ptr, u64 edges, int Nn, u64 stream) {
+static int rev_csr(u64 idx, int G, int N, int K, u64 ptr, u64 edges, int Nn, u64 ws, u64 stream) {
   mb::CsrArgs a{};
   a.Nn = Nn;
+  a.ws = P<int>(ws);
   a.idx = P<const int>(idx); a.G = G; a.N = N; a.K = K; a.ptr = P<int>(ptr); a.edges = P<int>(edges);
   return mb_rev_csr(&a, ST(stream));
 }

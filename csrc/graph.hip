@@ -89,6 +89,85 @@ __global__ __launch_bounds__(CSR_BLOCK) void rev_csr_kernel(CsrArgs a) {
   }
 }
 
+// Global path (envs whose 2 Nn + 1 counters exceed LDS, > ~19 K nodes): counters in global
+// memory -- the counts in the ptr output itself, scanned in LDS tiles of CSR_TILE entries with a
+// running carry, the bucket fill counters in a.ws; the buckets are scattered and insertion-sorted
+// in global memory. Values another thread wrote are read with agent-scope atomic loads after a
+// fence + barrier (they come from L2: this CU's L1 may hold a stale line of them).
+constexpr int CSR_TILE = 4096;
+DEV int ld_l2(const int* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+
+__global__ __launch_bounds__(CSR_BLOCK) void rev_csr_glb_kernel(CsrArgs a) {
+  __shared__ int tile[CSR_TILE];
+  __shared__ int wsum[CSR_BLOCK];
+  const int Nt = a.Nn > 0 ? a.Nn : a.N;
+  const long g = blockIdx.x;
+  const int N = a.N, K = a.K, NK = N * K;
+  const int* idx = a.idx + g * NK;
+  int* cnt = a.ptr + g * (Nt + 1);
+  int* fill = a.ws + g * Nt;
+  int* out = a.edges + g * NK;
+  for (int q = threadIdx.x; q <= Nt; q += CSR_BLOCK) cnt[q] = 0;
+  for (int q = threadIdx.x; q < Nt; q += CSR_BLOCK) fill[q] = 0;
+  __threadfence();
+  __syncthreads();
+  for (int e = threadIdx.x; e < NK; e += CSR_BLOCK) {
+    const int j = idx[e];
+    if (j != e / K) atomicAdd(&cnt[j + 1], 1);
+  }
+  __threadfence();
+  __syncthreads();
+  // exclusive scan of cnt[1..Nt] (cnt[0] stays 0), tile by tile with a running carry
+  __shared__ int total;
+  int carry = 0;
+  constexpr int PER = CSR_TILE / CSR_BLOCK;
+  for (int base = 1; base <= Nt; base += CSR_TILE) {
+    const int n = min(CSR_TILE, Nt + 1 - base);
+    for (int q = threadIdx.x; q < n; q += CSR_BLOCK) tile[q] = ld_l2(&cnt[base + q]);
+    __syncthreads();
+    int run = 0;
+    const int lo = threadIdx.x * PER, hi = min(lo + PER, n);
+    for (int q = lo; q < hi; ++q) { run += tile[q]; tile[q] = run; }
+    wsum[threadIdx.x] = run;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int acc = carry;
+      for (int w = 0; w < CSR_BLOCK; ++w) { const int v = wsum[w]; wsum[w] = acc; acc += v; }
+      total = acc;
+    }
+    __syncthreads();
+    const int off = wsum[threadIdx.x];
+    for (int q = lo; q < hi; ++q) cnt[base + q] = tile[q] + off;
+    carry = total;
+    __syncthreads();                               // tile / wsum are reused by the next tile
+  }
+  __threadfence();
+  __syncthreads();
+  for (int e = threadIdx.x; e < NK; e += CSR_BLOCK) {
+    const int j = idx[e];
+    if (j != e / K) {
+      const int p = atomicAdd(&fill[j], 1);
+      out[ld_l2(&cnt[j]) + p] = e;
+    }
+  }
+  __threadfence();
+  __syncthreads();
+  for (int j = threadIdx.x; j < Nt; j += CSR_BLOCK) {
+    const int b0 = ld_l2(&cnt[j]), b1 = ld_l2(&cnt[j + 1]);
+    if (b1 - b0 < 2) continue;
+    // the bucket's entries were written by other threads: read them from L2 once, then sort in
+    // place with this thread's own stores
+    for (int x = b0 + 1; x < b1; ++x) {
+      const int v = ld_l2(&out[x]);
+      int y = x - 1;
+      int w;
+      while (y >= b0 && (w = ld_l2(&out[y])) > v) { out[y + 1] = w; __threadfence(); --y; }
+      out[y + 1] = v;
+      __threadfence();
+    }
+  }
+}
+
 // gated record accumulation: a zero gate selects zero (the record may hold stale data). The
 // gate is read first and inactive evaluations skip the record load (CMB_GATE_FIRST: one more
 // dependent round trip, but most evaluations are inactive: node_reduce 330 -> 297 us per
@@ -195,10 +274,12 @@ extern "C" int mb_rev_csr(const mb::CsrArgs* a, hipStream_t st) {
   if (NK <= 65536 && lds_sorted <= 150 * 1024) {
     (void)hipFuncSetAttribute((const void*)rev_csr_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_sorted);
     hipLaunchKernelGGL(rev_csr_kernel<true>, dim3(a->G), dim3(CSR_BLOCK), lds_sorted, st, *a);
-  } else {
-    if (base > 150 * 1024) return -1;
+  } else if (base <= 150 * 1024) {
     (void)hipFuncSetAttribute((const void*)rev_csr_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)base);
     hipLaunchKernelGGL(rev_csr_kernel<false>, dim3(a->G), dim3(CSR_BLOCK), base, st, *a);
+  } else {
+    if (!a->ws) return -2;                       // global path: the caller provides (G, Nn) ints
+    hipLaunchKernelGGL(rev_csr_glb_kernel, dim3(a->G), dim3(CSR_BLOCK), 0, st, *a);
   }
   return (int)hipGetLastError();
 }

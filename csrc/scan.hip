@@ -202,7 +202,9 @@ __global__ __launch_bounds__(STAGE_BLOCK) void scan_stage_kernel(ScanArgs a) {
   }
 }
 
-template <int K, int D, int BS, int LPA, bool GLB>
+// GLB: 0 = env staged in LDS; 1 = nodes in the global workspace, culling boxes copied to LDS;
+// 2 = boxes read from the workspace too (envs whose boxes exceed LDS: > ~36 K nodes)
+template <int K, int D, int BS, int LPA, int GLB>
 __global__ __launch_bounds__(BS) void scan_kernel(ScanArgs a) {
   constexpr int APW = WAVE / LPA;                              // agents per wave
   constexpr int SCAN_AG = BS / LPA;                            // agents (curve positions) per block
@@ -216,7 +218,7 @@ __global__ __launch_bounds__(BS) void scan_kernel(ScanArgs a) {
   if constexpr (GLB) {
     tp = a.ws + (long)b * a.ws_env;                            // [Np] x, y, z, node id (global)
     tv = tp + Np;                                              // [Np] vx, vy, vz, |v| (global)
-    cbl = smem4;                                               // boxes: LDS copies
+    cbl = GLB == 2 ? tv + Np : smem4;                          // boxes: LDS copies (GLB 1)
     cbh = cbl + nch;
     sbl = cbh + nch;
     sbh = sbl + nsc;
@@ -234,7 +236,8 @@ __global__ __launch_bounds__(BS) void scan_kernel(ScanArgs a) {
   unsigned short* pinv = reinterpret_cast<unsigned short*>(sbh + nsc);
   const float4* Sb = a.S + (long)b * a.s_env * REC<D>;
   const int* perm = a.perm + (long)b * Nn;
-  if constexpr (GLB) {
+  if constexpr (GLB == 2) {
+  } else if constexpr (GLB == 1) {
     const float4* gb = tv + Np;
     for (int q = threadIdx.x; q < 2 * (nch + nsc); q += BS) cbl[q] = gb[q];
   } else
@@ -516,6 +519,11 @@ __global__ __launch_bounds__(BS) void scan_kernel(ScanArgs a) {
 #define SCAN_LPA 4      // lanes per agent (A/B at 1024 x 64: 2 -> 4 lanes 65.4 -> 61.5 us per step)
 #endif
 
+#ifndef SCAN_BS_BIG
+#define SCAN_BS_BIG 1024  // block size above 512 nodes per env (4 lanes/agent: 512 -> 1024, 61.5 -> 60.5 us)
+#endif
+constexpr size_t SCAN_BOX_LDS = 160 * 1024 - 1024;   // LDS budget of the culling boxes (GLB 1)
+
 template <int K, int D, int BS, int LPA = SCAN_LPA>
 static void launch_kdb(const ScanArgs& a, hipStream_t st) {
   dim3 grid((a.Nn + BS / LPA - 1) / (BS / LPA), a.B);
@@ -524,18 +532,20 @@ static void launch_kdb(const ScanArgs& a, hipStream_t st) {
     hipLaunchKernelGGL(scan_stage_kernel<D>, dim3((nch + STAGE_BLOCK - 1) / STAGE_BLOCK, a.B), dim3(STAGE_BLOCK), 0,
                        st, a);
     const size_t lds = (size_t)2 * (nch + nsc) * 16;
-    (void)hipFuncSetAttribute((const void*)scan_kernel<K, D, BS, LPA, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL((scan_kernel<K, D, BS, LPA, true>), grid, dim3(BS), lds, st, a);
+    if (lds > SCAN_BOX_LDS) {                // huge envs: the boxes stay in the global workspace
+      if constexpr (BS == SCAN_BS_BIG && LPA == SCAN_LPA)
+        hipLaunchKernelGGL((scan_kernel<K, D, BS, LPA, 2>), grid, dim3(BS), 0, st, a);
+      return;
+    }
+    (void)hipFuncSetAttribute((const void*)scan_kernel<K, D, BS, LPA, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL((scan_kernel<K, D, BS, LPA, 1>), grid, dim3(BS), lds, st, a);
     return;
   }
   const size_t lds = scan_lds_bytes(a.Nn);
-  (void)hipFuncSetAttribute((const void*)scan_kernel<K, D, BS, LPA, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL((scan_kernel<K, D, BS, LPA, false>), grid, dim3(BS), lds, st, a);
+  (void)hipFuncSetAttribute((const void*)scan_kernel<K, D, BS, LPA, 0>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipLaunchKernelGGL((scan_kernel<K, D, BS, LPA, 0>), grid, dim3(BS), lds, st, a);
 }
 
-#ifndef SCAN_BS_BIG
-#define SCAN_BS_BIG 1024  // block size above 512 nodes per env (4 lanes/agent: 512 -> 1024, 61.5 -> 60.5 us)
-#endif
 
 static int scan_num_cu() {
   static const int cus = [] {
@@ -568,9 +578,18 @@ static bool scan_lpa8(const ScanArgs& a) {
   return SCAN_LPA < 8 && (long)a.B * ((a.Nn + AG - 1) / AG) < scan_num_cu();
 }
 
+// envs whose culling boxes exceed LDS (> ~36 K nodes): the boxes are read from the workspace,
+// a layout instantiated for the 1024-thread blocks only (such envs fill the CUs by themselves)
+static bool scan_boxes_global(const ScanArgs& a) {
+  if (a.Nn <= SCAN_MAXN) return false;
+  const int Np = (a.Nn + SCH - 1) / SCH * SCH, nch = Np / SCH, nsc = (nch + SSC - 1) / SSC;
+  return (size_t)2 * (nch + nsc) * 16 > SCAN_BOX_LDS;
+}
+
 template <int K, int D>
 static void launch_kd(const ScanArgs& a, hipStream_t st) {
-  if (scan_lpa8(a)) launch_kdb<K, D, 256, 8>(a, st);
+  if (scan_boxes_global(a)) launch_kdb<K, D, SCAN_BS_BIG>(a, st);
+  else if (scan_lpa8(a)) launch_kdb<K, D, 256, 8>(a, st);
   else if (a.Nn > 512 && !scan_small_grid(a)) launch_kdb<K, D, SCAN_BS_BIG>(a, st);
   else launch_kdb<K, D, 256>(a, st);
 }
@@ -595,7 +614,6 @@ extern "C" int mb_scan(const mb::ScanArgs* a, hipStream_t st) {
   if (a->Nn > SCAN_MAXN) {       // global staging: the workspace must hold scan_ws_f4(Nn) per env
     const int Np = (a->Nn + SCH - 1) / SCH * SCH, nch = Np / SCH, nsc = (nch + SSC - 1) / SSC;
     if (!a->ws || a->ws_env < 2L * Np + 2L * (nch + nsc)) return -4;
-    if ((size_t)2 * (nch + nsc) * 16 > 160 * 1024 - 1024) return -5;   // boxes must fit LDS
   }
   switch (a->do_knn ? a->K : 1) {
 #define CASE(k) case k: launch_k<k>(*a, st); break;

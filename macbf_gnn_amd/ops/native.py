@@ -168,7 +168,8 @@ def small_apw(N: int) -> int:
 
 
 SCAN_MAX_N = 4096           # envs up to this many graph nodes are staged whole in LDS
-SCAN_MAX_NODES = 36864      # beyond: global staging (csrc/scan.hip scan_stage_kernel), boxes in LDS
+SCAN_MAX_NODES = 262144     # beyond SCAN_MAX_N: global staging (csrc/scan.hip scan_stage_kernel); the
+                            # culling boxes in LDS up to ~36 K nodes, read from the workspace above
 
 
 def scan_ws_f4(Nn: int) -> int:
@@ -668,7 +669,10 @@ def rev_csr(idx, rptr, redges, n_nodes=None):
     check(idx, torch.int32, (Gn, N, K), "idx")
     check(rptr, torch.int32, (Gn, Nn + 1), "rptr")
     check(redges, torch.int32, (Gn, N * K), "redges")
-    _ok(lib().rev_csr(ptr(idx), Gn, N, K, ptr(rptr), ptr(redges), Nn, stream_handle()), "rev_csr")
+    ws = None
+    if (2 * Nn + 1) * 4 > 150 * 1024:         # counters beyond LDS: csrc/graph.hip global path
+        ws = _workspace("csr", Gn * Nn * 4, idx.device)
+    _ok(lib().rev_csr(ptr(idx), Gn, N, K, ptr(rptr), ptr(redges), Nn, ptr(ws), stream_handle()), "rev_csr")
 
 
 def node_reduce(dE, rptr, redges, out, *, T, B, N, K, passes=2, accumulate=False, pass_mask=0, shift1=0,
@@ -867,7 +871,7 @@ def ctrl_bwd_step(node: dict, edge: dict, num_blocks: int):
     _ok(lib().ctrl_bwd_step(na, ea, int(num_blocks), na[29], stream_handle()), "ctrl_bwd_step")
 
 
-BWD_FUSED_DEFAULT = False
+BWD_FUSED_DEFAULT = True
 
 
 def bwd_step_fused(total_agents: int, device) -> bool:
