@@ -125,6 +125,38 @@ DEV void topk_insert(uint64_t (&bk)[K], uint64_t x) {
   bk[0] = c[0] ? x : bk[0];
 }
 
+// Merge of two ascending key lists of length K into the K smallest keys of both, ascending, by
+// a bitonic network (lists padded to P = 2^ceil(log2 K) with KEY_EMPTY): c[i] = min(a[i],
+// b[P-1-i]) holds the P smallest keys of the union as a bitonic sequence, log2 P half-cleaner
+// stages sort it. Branch-free and fixed cost (P mins + P/2 log2 P compare-exchanges), where the
+// insertion merge ran up to K wave-divergent K-step insertions per butterfly level. Keys are
+// unique, so the result equals the insertion merge's.
+template <int K>
+DEV void topk_merge(uint64_t (&bk)[K], const uint64_t (&px)[K]) {
+  constexpr int P = K <= 1 ? 1 : K <= 2 ? 2 : K <= 4 ? 4 : K <= 8 ? 8 : 16;
+  uint64_t c[P];
+#pragma unroll
+  for (int i = 0; i < P; ++i) {
+    const uint64_t x = i < K ? bk[i] : KEY_EMPTY;
+    const uint64_t y = (P - 1 - i) < K ? px[P - 1 - i] : KEY_EMPTY;
+    c[i] = x < y ? x : y;
+  }
+#pragma unroll
+  for (int st = P / 2; st >= 1; st >>= 1) {
+#pragma unroll
+    for (int i = 0; i < P; ++i) {
+      if ((i & st) == 0) {
+        const uint64_t x = c[i], y = c[i + st];
+        const bool sw = y < x;
+        c[i] = sw ? y : x;
+        c[i + st] = sw ? x : y;
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < K; ++i) bk[i] = c[i];
+}
+
 DEV float wave_min(float v) { return -wave_max(-v); }
 
 // Chunked scan with conservative culling. The env's graph nodes (agents, then static
@@ -442,9 +474,7 @@ __global__ __launch_bounds__(BS) void scan_kernel(ScanArgs a) {
         const unsigned lo = grp_xoru((unsigned)bk[q], o), hi = grp_xoru((unsigned)(bk[q] >> 32), o);
         px[q] = ((uint64_t)hi << 32) | lo;
       }
-#pragma unroll
-      for (int q = 0; q < K; ++q)
-        if (px[q] < bk[K - 1]) topk_insert<K>(bk, px[q]);
+      topk_merge<K>(bk, px);
     }
   }
   {
