@@ -171,6 +171,14 @@ struct CbfBwdArgs {
   // active list (optional): only evaluations act[v], v < *nact, are processed (dh != 0)
   const int* act;
   const int* nact;
+  // 16x16x32 x3 backward (csrc/cbf16.h; rec != null selects it): cbf_compact's 16-byte records
+  // of the active evaluations, the column-permuted W2 | W3 images and the layer-1 fragments
+  const int4* rec;
+  const h16* wrm16;
+  const h16* w16;
+  unsigned long long* stamps;   // diagnostics (null in production): per-wave shader-clock cycles
+                                // summed per phase over the wave's chunks, [workgroup][wave][8]
+                                // (scripts/stamps_cbf.py)
 };
 
 // Deduplication of the h / h' evaluations (dedup.hip). h'(s_{t+1}) of slot (t,b,i,k) is the
@@ -376,7 +384,8 @@ int mb_rev_csr(const mb::CsrArgs* a, hipStream_t st);
 int mb_cbf_match(const mb::CbfMatchArgs* a, hipStream_t st);
 int mb_cbf_dh(const mb::CbfDhArgs* a, int num_blocks, hipStream_t st);
 int mb_cbf_compact(const float* dh, const int* nev, const int* blk_off, int* act, int num_blocks,
-                   const int* blk_active, int* nact, hipStream_t st);
+                   const int* blk_active, int* nact, const int* src, const int* idx, const int* idx1, unsigned E,
+                   void* rec, hipStream_t st);
 int mb_node_reduce(const mb::NodeRedArgs* a, hipStream_t st);
 int mb_node_combine(const mb::CombineArgs* a, hipStream_t st);
 int mb_reduce_rows(const float* partial, int rows, int cols, float* out, int accumulate, hipStream_t st);
@@ -389,6 +398,7 @@ int mb_pack_gather(const float* src, int n, const int* idx16, int m16, unsigned 
                    const int* idx32, int m32, float* out32, hipStream_t st);
 int mb_step_commit(const mb::StepCommitArgs* a, hipStream_t st);
 int mb_stats_pack(const float* sums, const float* counts, const float* local, float* row, hipStream_t st);
+int mb_probe_mfma16(const void* a, const void* b, float* d, hipStream_t st);
 int mb_probe_mfma(const void* a, const void* b, float* d, hipStream_t st);
 int mb_probe_lane_xor(const unsigned* in, unsigned* out, hipStream_t st);
 int mb_probe_smfmac(const void* a, const void* b, const int* idx, float* d, hipStream_t st);

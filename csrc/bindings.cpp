@@ -116,8 +116,11 @@ static int cbf_hfwd(u64 S, long s_env, long s_step, u64 idx, u64 idx1, u64 src, 
 static int cbf_bwd(u64 S, long s_env, long s_step, u64 idx, int B, int T, int N, int K, int passes, u64 dh,
                    u64 wpack, int f_bwd, u64 wrm, u64 wvec, u64 dE, u64 partial, float obs_r, float dist_thr,
                    float dist_eps, int fused, u64 dang, u64 valid, u64 counts, py::tuple lc, u64 idx1,
-                   int dim, int num_blocks, int prec, u64 src, u64 nev, u64 act, u64 nact, u64 stream) {
+                   int dim, int num_blocks, int prec, u64 src, u64 nev, u64 act, u64 nact, u64 rec, u64 wrm16, u64 w16,
+                   u64 stamps, u64 stream) {
   mb::CbfBwdArgs a{};
+  a.stamps = P<unsigned long long>(stamps);
+  a.rec = P<const int4>(rec); a.wrm16 = P<const h16>(wrm16); a.w16 = P<const h16>(w16);
   a.dim = dim;
   a.src = P<const int>(src); a.nev = P<const int>(nev); a.act = P<const int>(act); a.nact = P<const int>(nact);
   a.idx1 = P<const int>(idx1);
@@ -174,9 +177,10 @@ static int cbf_dh(u64 h, u64 hmask, u64 map1, u64 src, u64 nev, u64 dang, u64 va
 }
 
 static int cbf_compact(u64 dh, u64 nev, u64 blk_off, u64 act, int num_blocks, u64 blk_active, u64 nact,
-                       u64 stream) {
+                       u64 src, u64 idx, u64 idx1, unsigned E, u64 rec, u64 stream) {
   return mb_cbf_compact(P<const float>(dh), P<const int>(nev), P<const int>(blk_off), P<int>(act), num_blocks,
-                        P<const int>(blk_active), P<int>(nact), ST(stream));
+                        P<const int>(blk_active), P<int>(nact), P<const int>(src), P<const int>(idx),
+                        P<const int>(idx1), E, P<void>(rec), ST(stream));
 }
 
 static int node_combine(u64 dS, long ds_env, u64 ego, u64 dEc, u64 ptr, long ptr_env, u64 edges, long edges_env,
@@ -332,6 +336,9 @@ static int ctrl_bwd_step(py::tuple node, py::tuple edge, int num_blocks, int pre
 static int probe_mfma(u64 a, u64 b, u64 d, u64 stream) {
   return mb_probe_mfma(P<const void>(a), P<const void>(b), P<float>(d), ST(stream));
 }
+static int probe_mfma16(u64 a, u64 b, u64 d, u64 stream) {
+  return mb_probe_mfma16(P<const void>(a), P<const void>(b), P<float>(d), ST(stream));
+}
 static int probe_smfmac(u64 a, u64 b, u64 idx, u64 d, u64 stream) {
   return mb_probe_smfmac(P<const void>(a), P<const void>(b), P<const int>(idx), P<float>(d), ST(stream));
 }
@@ -385,6 +392,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("step_commit", &step_commit);
   m.def("stats_pack", &stats_pack);
   m.def("probe_mfma", &probe_mfma);
+  m.def("probe_mfma16", &probe_mfma16);
   m.def("probe_tr", &probe_tr);
   m.def("probe_smfmac", &probe_smfmac);
   m.def("probe_lane_xor", &probe_lane_xor);

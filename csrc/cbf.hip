@@ -532,9 +532,19 @@ __global__ __launch_bounds__(NW * 64, 1) void cbf_bwd_kernel(CbfBwdArgs a) {
   const int bsA = (KS / 4) * (wave % 4), bsB = (KS / 2) * (wave % 2);
   int par = 0;                                 // stage region parity (NREG == 2)
 
+  // diagnostics (a.stamps, normally null): shader-clock cycles per phase summed over the chunks
+  unsigned long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tck = 0;
+  auto stamp = [&](int k) {
+    if (a.stamps) {
+      const unsigned long long t = __builtin_amdgcn_s_memtime();
+      ph[k] += t - tck;
+      tck = t;
+    }
+  };
   CbfIn<D> nx;
   if ((long)blockIdx.x < nchunks) cbf_load<FUSED, NW, D>(a, blockIdx.x, wave, r, E, EV, nx);
   for (long chunk = blockIdx.x; chunk < nchunks; chunk += gridDim.x) {
+    if (a.stamps) { tck = __builtin_amdgcn_s_memtime(); ph[7] += 1; }
     const CbfIn<D> cur = nx;
     if (chunk + gridDim.x < nchunks) cbf_load<FUSED, NW, D>(a, chunk + gridDim.x, wave, r, E, EV, nx);   // prefetch
     const EdgeCtx<D>& c = cur.c;
@@ -576,6 +586,7 @@ __global__ __launch_bounds__(NW * 64, 1) void cbf_bwd_kernel(CbfBwdArgs a) {
       relu_(t3);                                   // relu(H3) in fp32 (the head is fp32)
       H3p[mt] = t3;
     }
+    stamp(0);                                      // loads + forward recompute
     float dhv = cur.dh;
     if constexpr (FUSED) {
       // ---- head, h/h' exchange, local loss + upstream gradient
@@ -668,6 +679,7 @@ __global__ __launch_bounds__(NW * 64, 1) void cbf_bwd_kernel(CbfBwdArgs a) {
       }
       if constexpr (Cfg::NREG == 2) par ^= 1; else __syncthreads();
     }
+    stamp(1);                                      // head backward + stage A
     // ---- dH2pre = (W3^T dH3pre) . relu'(H2)
     Pk d2b[4];
 #pragma unroll
@@ -680,6 +692,7 @@ __global__ __launch_bounds__(NW * 64, 1) void cbf_bwd_kernel(CbfBwdArgs a) {
       d2b[mt] = to_pk(t);
       mask_pk(d2b[mt], H2b[mt]);
     }
+    stamp(2);                                      // dH2
     // ---- stage B: dW2 (128x64) += dH2pre . H1^T ; db2   (tiles t = wave + NW u -> (t/2, t%2))
 #pragma unroll
     for (int turn = 0; turn < NT; ++turn) {
@@ -702,6 +715,7 @@ __global__ __launch_bounds__(NW * 64, 1) void cbf_bwd_kernel(CbfBwdArgs a) {
       }
       if constexpr (Cfg::NREG == 2) par ^= 1; else __syncthreads();
     }
+    stamp(3);                                      // stage B
     // ---- dH1pre = (W2^T dH2pre) . relu'(H1)
     Pk d1b[2];
 #pragma unroll
@@ -738,6 +752,7 @@ __global__ __launch_bounds__(NW * 64, 1) void cbf_bwd_kernel(CbfBwdArgs a) {
         store_rec<D>(a.dE, cur.ev, dp, dv);
       }
     }
+    stamp(4);                                      // dH1, dF, dE store
     // ---- stage C+D: dW1f (64x32) += dH1pre . [F|dh|0]^T (waves 0,1; cols >= 16 unused);
     //      dW4pad (32x64) += [dh;0..] . relu(H3)^T, A = image cols 16..47 -> row 0 = dw4 (waves 2,3;
     //      rows >= 1 read padding / the next row and are discarded: MFMA rows are independent).
@@ -769,7 +784,11 @@ __global__ __launch_bounds__(NW * 64, 1) void cbf_bwd_kernel(CbfBwdArgs a) {
       else if (wave < 4) stage_mma_fr<KST>(imF + 16, SA32, PL, imH, SA64, PL, 0, wave - 2, lane, accC);
       if constexpr (Cfg::NREG == 2) par ^= 1; else __syncthreads();
     }
+    stamp(5);                                      // stage C+D
   }
+  if (a.stamps && lane == 0)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) a.stamps[((long)blockIdx.x * NW + wave) * 8 + k] = ph[k];
   __syncthreads();   // all stage reads done: the stage region is reused below
   float* bred = reinterpret_cast<float*>(stg);        // [NW][192] bias partials: b3 (64) | b2 (128)
   for (int q = threadIdx.x; q < NW * 192; q += blockDim.x) bred[q] = 0.f;
@@ -841,10 +860,24 @@ static void launch_cbf_bwd(const CbfBwdArgs& a, int num_blocks, hipStream_t st) 
 }  // namespace MB_PREC
 }  // namespace mb
 
+#if MB_X3
+#include "cbf16.h"
+#endif
+
 extern "C" int MB_SYM(cbf_bwd)(const mb::CbfBwdArgs* a, int num_blocks, hipStream_t st) {
   using namespace mb;
   using namespace mb::MB_PREC;
   if (a->K > 16 || a->K < 1 || a->passes < 1 || a->passes > 2) return -1;
+  if (a->rec) {   // 16x16x32 backward over cbf_compact's records (x3 build only)
+#if MB_X3
+    if (a->fused || !a->nact || !a->wrm16 || !a->w16) return -5;
+    if (a->dim == 3) launch_cbf_bwd16<3>(*a, num_blocks, st);
+    else launch_cbf_bwd16<2>(*a, num_blocks, st);
+    return (int)hipGetLastError();
+#else
+    return -6;
+#endif
+  }
   if (a->fused && (a->passes != 2 || !a->dang || !a->counts)) return -2;
   if (a->src && (a->fused || !a->nev || a->passes != 2)) return -3;
   if (a->act && (!a->src || !a->nact)) return -4;

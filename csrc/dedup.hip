@@ -312,8 +312,13 @@ __global__ __launch_bounds__(DH_BLOCK) void cbf_dh_kernel(CbfDhArgs a) {
 // per-block counts.
 // blk_off null: the block's offset is summed in-kernel from blk_active (cbf_dh's per-block
 // counts) and the last block writes the total to *nact.
+// rec (optional, the 16x16x32 x3 backward's input): instead of act, one 16-byte record per
+// active evaluation {u, e | pass << 31, neighbour j, dh bits} -- the backward then needs no
+// dependent index chain (act -> src -> idx -> states) inside its loop.
 __global__ __launch_bounds__(DH_BLOCK) void cbf_compact_kernel(const float* dh, const int* nev, const int* blk_off,
-                                                             int* act, const int* blk_active, int* nact) {
+                                                             int* act, const int* blk_active, int* nact,
+                                                             const int* src, const int* idx, const int* idx1,
+                                                             unsigned E, int4* rec) {
   const unsigned U = (unsigned)*nev;
   const unsigned span = dh_span(U, gridDim.x);
   const unsigned u_lo = blockIdx.x * span, u_hi = min(U, u_lo + span);
@@ -328,7 +333,8 @@ __global__ __launch_bounds__(DH_BLOCK) void cbf_compact_kernel(const float* dh, 
   }
   for (unsigned u0 = u_lo; u0 < u_hi; u0 += DH_BLOCK) {
     const unsigned u = u0 + threadIdx.x;
-    const bool f = u < u_hi && dh[u] != 0.f;
+    const float dv = u < u_hi ? dh[u] : 0.f;
+    const bool f = dv != 0.f;
     const unsigned long long bal = __ballot(f);
     const int below = __popcll(bal & ((1ull << lane) - 1ull));
     if (lane == 0) wcnt[wave] = __popcll(bal);
@@ -339,7 +345,16 @@ __global__ __launch_bounds__(DH_BLOCK) void cbf_compact_kernel(const float* dh, 
       wo += (w < wave) ? c : 0;
       tot += c;
     }
-    if (f) act[base + wo + below] = (int)u;
+    if (f) {
+      if (rec) {
+        const unsigned pass = u >= E ? 1u : 0u;
+        const unsigned e = pass ? (unsigned)src[u] : u;
+        const int j = ((pass && idx1) ? idx1 : idx)[e];
+        rec[base + wo + below] = int4{(int)u, (int)(e | (pass << 31)), j, __float_as_int(dv)};
+      } else {
+        act[base + wo + below] = (int)u;
+      }
+    }
     base += tot;
     __syncthreads();
   }
@@ -348,11 +363,14 @@ __global__ __launch_bounds__(DH_BLOCK) void cbf_compact_kernel(const float* dh, 
 }  // namespace mb
 
 extern "C" int mb_cbf_compact(const float* dh, const int* nev, const int* blk_off, int* act, int num_blocks,
-                              const int* blk_active, int* nact, hipStream_t st) {
+                              const int* blk_active, int* nact, const int* src, const int* idx, const int* idx1,
+                              unsigned E, void* rec, hipStream_t st) {
   using namespace mb;
   if (!blk_off && !blk_active) return -1;
+  if (rec && (!src || !idx)) return -2;
+  if (!rec && !act) return -3;
   hipLaunchKernelGGL(cbf_compact_kernel, dim3(num_blocks), dim3(DH_BLOCK), 0, st, dh, nev, blk_off, act, blk_active,
-                     nact);
+                     nact, src, idx, idx1, E, (int4*)rec);
   return (int)hipGetLastError();
 }
 

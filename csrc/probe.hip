@@ -15,6 +15,20 @@ __global__ void probe_mfma_kernel(const h16* a, const h16* b, float* d) {
   for (int q = 0; q < 16; ++q) d[l * 16 + q] = c[q];
 }
 
+// D = A(16x32) * B(32x16), v_mfma_f32_16x16x32 with natural fragments: a/b (64 x 8 h16), d (64 x 4)
+__global__ void probe_mfma16_kernel(const h16* a, const h16* b, float* d) {
+  const int l = threadIdx.x;
+  const h16x8 af = *reinterpret_cast<const h16x8*>(a + l * 8);
+  const h16x8 bf = *reinterpret_cast<const h16x8*>(b + l * 8);
+#if MB_FP16
+  const f32x4 c = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, bf, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+#else
+  const f32x4 c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bf, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+#endif
+#pragma unroll
+  for (int q = 0; q < 4; ++q) d[l * 4 + q] = c[q];
+}
+
 __global__ void probe_tr_kernel(const h16* img_g, int rows, int stride, int e0, int m0, h16* out) {
   __shared__ __attribute__((aligned(16))) h16 img[64 * 136];
   for (int i = threadIdx.x; i < rows * stride; i += blockDim.x) img[i] = img_g[i];
@@ -63,6 +77,11 @@ extern "C" int mb_probe_lane_xor(const unsigned* in, unsigned* out, hipStream_t 
 
 extern "C" int mb_probe_smfmac(const void* a, const void* b, const int* idx, float* d, hipStream_t st) {
   hipLaunchKernelGGL(mb::probe_smfmac_kernel, dim3(1), dim3(64), 0, st, (const __bf16*)a, (const __bf16*)b, idx, d);
+  return (int)hipGetLastError();
+}
+
+extern "C" int mb_probe_mfma16(const void* a, const void* b, float* d, hipStream_t st) {
+  hipLaunchKernelGGL(mb::probe_mfma16_kernel, dim3(1), dim3(64), 0, st, (const h16*)a, (const h16*)b, d);
   return (int)hipGetLastError();
 }
 

@@ -20,6 +20,8 @@ backward
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from .. import config as C
@@ -205,7 +207,12 @@ class HipEngine:
             ndh = native.cbf_dh_grid(2 * E, dev)
             self.loss_part = torch.zeros(ndh, native.DH_PARTIAL, dtype=f32, device=dev)
             self.blk_active = torch.zeros(ndh, dtype=i32, device=dev)
-            self.act_list = torch.zeros(2 * E, dtype=i32, device=dev)
+            # x3: the 16x16x32 backward (csrc/cbf16.h, two waves per SIMD) reads cbf_compact's
+            # 16-byte records of the active evaluations instead of the index list
+            # (MACBF_CBF16=0: the 32x32x16 kernel on the index list, for A/B runs)
+            self.cbf16 = self.prec == "fp32" and os.environ.get("MACBF_CBF16", "0") != "0"
+            self.act_list = torch.zeros(2 * E, dtype=i32, device=dev) if not self.cbf16 else None
+            self.rec_list = torch.zeros(2 * E, 4, dtype=i32, device=dev) if self.cbf16 else None
             self.loss_red = torch.zeros(native.DH_PARTIAL, dtype=f32, device=dev)
             self.nev_host = torch.zeros(1, dtype=i32, device=dev)     # unused by host-range slices
             self.nev_dev = torch.zeros(1, dtype=i32, device=dev)      # [U] of the match
@@ -520,11 +527,20 @@ class HipEngine:
                           grad_scale=gs, blk_active=self.blk_active, gscale=gsd)
             # backward over the evaluations with a nonzero upstream gradient only (exact: the
             # others contribute zeros); node_reduce reads dE where dh != 0
-            act = self.act_list[: 2 * E]
-            nact = native.cbf_active(dh, nev, self.blk_active, act, nact=self.nact_dev)
-            native.cbf_bwd(S, idx, dh.view(2, T, B, N, K), pw.cbf_w, pw.cbf_off["w1f"], pw.cbf_rm, pw.cbf_v,
-                           passes=2, dE=dE, partial=part_cbf, num_blocks=nbb, idx1=idx if self.reuse else idx1,
-                           src=src, nev=nev, act=act, nact=nact, prec=self.prec)
+            if self.cbf16:
+                rec = self.rec_list[: 2 * E]
+                nact = native.cbf_active(dh, nev, self.blk_active, None, nact=self.nact_dev, rec=rec, src=src,
+                                         idx=idx, idx1=idx if self.reuse else idx1)
+                native.cbf_bwd(S, idx, dh.view(2, T, B, N, K), pw.cbf_w, pw.cbf_off["w1f"], pw.cbf_rm, pw.cbf_v,
+                               passes=2, dE=dE, partial=part_cbf, num_blocks=nbb, idx1=idx if self.reuse else idx1,
+                               src=src, nev=nev, nact=nact, prec=self.prec, rec=rec, wrm16=pw.cbf_rm16,
+                               w16=pw.cbf_w16)
+            else:
+                act = self.act_list[: 2 * E]
+                nact = native.cbf_active(dh, nev, self.blk_active, act, nact=self.nact_dev)
+                native.cbf_bwd(S, idx, dh.view(2, T, B, N, K), pw.cbf_w, pw.cbf_off["w1f"], pw.cbf_rm, pw.cbf_v,
+                               passes=2, dE=dE, partial=part_cbf, num_blocks=nbb, idx1=idx if self.reuse else idx1,
+                               src=src, nev=nev, act=act, nact=nact, prec=self.prec)
             native.reduce_rows(self.loss_part, self.loss_red)
         else:
             # ---- CBF: h, h', hinge losses, upstream grads and the full backward in ONE kernel

@@ -501,6 +501,93 @@ def cbf_rm(fp_offsets, dim: int = 2) -> RMPacker:
     return p
 
 
+# ------------------------------------------------------------------ 16x16x32 layouts (x3 CBF backward)
+# v_mfma_f32_16x16x32_bf16, lane l: n = l & 15, g = l >> 4.
+#   A fragment (16x32): element j = A[n][8g + j]     B fragment (32x16): element j = B[8g + j][n]
+#   C/D (16x16), 4 regs: reg i = D[4g + i][n]
+# The B operand of K-step s built from the packed accumulator tiles 2s, 2s+1 has
+# k(8g + j) = 32s + kacc16(g, j): the weight operands use the same permutation.
+CBF16_STRIDES = {"w2": 80, "w3": 144}     # csrc/cbf16.h S16_W2 / S16_W3 (conflict-free b128 / tr reads)
+
+
+def kacc16(g: int, j: int) -> int:
+    return 16 * (j >> 2) + 4 * g + (j & 3)
+
+
+def acc_row16(i: int, g: int) -> int:
+    return 4 * g + i
+
+
+def perm32_logical(c: int) -> int:
+    """Column c of a 16x16x32 row-major image -> logical weight column: within every 32-column
+    block, physical 8g + j holds logical kacc16(g, j), so an A fragment is one 16-byte read."""
+    b, q = divmod(c, 32)
+    return 32 * b + kacc16(q >> 3, q & 7)
+
+
+def cbf_rm16(fp_offsets, dim: int = 2) -> RMPacker:
+    """Column-permuted row-major images of W2 (128x64) and W3 (64x128) for the 16x16x32 x3 CBF
+    backward (csrc/cbf16.h): rows = output units; read as A = W (one ds_read_b128 per lane) and
+    A = W^T (two ds_read_b64_tr_b16 per lane)."""
+    W2 = fp_offsets["cbf_net.2.weight"]
+    W3 = fp_offsets["cbf_net.4.weight"]
+    m2, m3 = _mat(W2, 128, 64), _mat(W3, 64, 128)
+    p = RMPacker()
+    p.add("w2", lambda r, c: m2(r, perm32_logical(c)), 128, 64, CBF16_STRIDES["w2"])
+    p.add("w3", lambda r, c: m3(r, perm32_logical(c)), 64, 128, CBF16_STRIDES["w3"])
+    return p
+
+
+def pack_frags16(vm: Callable[[int, int], int], mtiles: int, ksteps: int, kind: str) -> np.ndarray:
+    """16x32 A fragments: element j of lane (n, g) at K-step s is vm(16mt + n, k) with
+    k = 32s + 8g + j ("nat") or 32s + kacc16(g, j) ("acc"). 64 lanes x 8 per fragment."""
+    out = np.empty((mtiles, ksteps, LANES, FRAG), dtype=np.int64)
+    for mt in range(mtiles):
+        for s in range(ksteps):
+            for l in range(LANES):
+                n, g = l & 15, l >> 4
+                for j in range(FRAG):
+                    k = 32 * s + (8 * g + j if kind == "nat" else kacc16(g, j))
+                    out[mt, s, l, j] = vm(16 * mt + n, k)
+    return out.reshape(-1)
+
+
+def cbf_packer16(fp_offsets: Dict[str, int], dim: int = 2) -> Packer:
+    """Layer-1 fragments of the 16x16x32 x3 CBF backward: w1f16 (64 x 32: the 16 edge-feature
+    slots of cbf_w1_slot, slots 16..31 zero; 4 M-tiles) and w1ft16 (16 x 64: W1^T, rows = feature
+    columns, accumulator-ordered k; 2 K-steps)."""
+    W1, b1 = fp_offsets["cbf_net.0.weight"], fp_offsets["cbf_net.0.bias"]
+    F = 2 * dim + 2
+
+    def w1f(o, k):
+        sl = cbf_w1_slot(k, dim) if (o < 64 and k < 16) else None
+        if sl is None:
+            return ZERO
+        return b1 + o if sl[0] == "b" else W1 + o * F + sl[1]
+
+    def w1ft(f, o):
+        if f < F and o < 64:
+            return W1 + o * F + f
+        return ZERO
+
+    p = Packer()
+    p.blocks.append(Block("w1f16", pack_frags16(w1f, 4, 1, "nat"), 0))
+    p.blocks.append(Block("w1ft16", pack_frags16(w1ft, 1, 2, "acc"), 4))
+    p.nfrag = 6
+    return p
+
+
+def emu_mfma16(a: np.ndarray, b: np.ndarray) -> np.ndarray:
+    """v_mfma_f32_16x16x32 on per-lane fragments a, b (64, 8) -> D (16, 16)."""
+    A = np.zeros((16, 32))
+    B = np.zeros((32, 16))
+    for l in range(64):
+        n, g = l & 15, l >> 4
+        A[n, 8 * g:8 * g + 8] = a[l]
+        B[8 * g:8 * g + 8, n] = b[l]
+    return A @ B
+
+
 # ------------------------------------------------------------------ operand precision (csrc/prec.h)
 # "bf16" / "fp16": one 16-bit MFMA per product. "fp32": the fp32-accurate 3-term split (x3 kernels):
 # every packed weight carries a bf16 residual plane; the pack gathers flag residual entries with

@@ -578,19 +578,33 @@ def cbf_dh(h, hmask, map1, src, nev, dang, valid, counts, dh, partial, *, grad_s
                      ptr(blk_active), nb, stream_handle()), "cbf_dh")
 
 
-def cbf_active(dh, nev, blk_active, act, nact=None):
+def cbf_active(dh, nev, blk_active, act, nact=None, *, rec=None, src=None, idx=None, idx1=None):
     """Stable list of the evaluations with dh != 0 (cbf_dh's per-block counts blk_active, same
     grid): act[:nact] in index order. Returns the device int32 tensor [nact] (written into
     `nact` when given; block offsets are scanned in-kernel, one launch). The backward skips the
-    rest: their upstream gradient, hence every contribution, is exactly zero."""
+    rest: their upstream gradient, hence every contribution, is exactly zero.
+
+    rec (int32 (2E, 4), the 16x16x32 x3 backward's input) replaces act: one record per active
+    evaluation {u, e | pass << 31, neighbour j, dh bits}, resolved through src (deduplicated
+    list) and idx (T,B,N,K) / idx1 (pass-1 neighbours, None = idx)."""
     check(dh, torch.float32, None, "dh")
     check(nev, torch.int32, (1,), "nev")
     check(blk_active, torch.int32, None, "blk_active")
-    check(act, torch.int32, (dh.numel(),), "act")
+    if rec is None:
+        check(act, torch.int32, (dh.numel(),), "act")
+    else:
+        check(rec, torch.int32, (dh.numel(), 4), "rec")
+        check(src, torch.int32, (dh.numel(),), "src")
+        check(idx, torch.int32, None, "idx")
+        check(idx1, torch.int32, tuple(idx.shape), "idx1")
+        if 2 * idx.numel() != dh.numel():
+            raise NativeError("rec: dh must cover the two passes of idx")
     if nact is None:
         nact = torch.empty(1, dtype=torch.int32, device=dh.device)
     check(nact, torch.int32, (1,), "nact")
-    _ok(lib().cbf_compact(ptr(dh), ptr(nev), 0, ptr(act), blk_active.numel(), ptr(blk_active), ptr(nact),
+    E = idx.numel() if idx is not None else 0
+    _ok(lib().cbf_compact(ptr(dh), ptr(nev), 0, ptr(act) if rec is None else 0, blk_active.numel(),
+                          ptr(blk_active), ptr(nact), ptr(src), ptr(idx), ptr(idx1), int(E), ptr(rec),
                           stream_handle()), "cbf_compact")
     return nact
 
@@ -599,9 +613,12 @@ def cbf_bwd_grid(EV: int, device) -> int:
     return max(1, min((EV + 127) // 128, num_cu(device)))
 
 
+CBF_RM16 = 128 * 80 + 64 * 144     # elements per plane of the 16x16x32 W2 | W3 images (layout.cbf_rm16)
+
+
 def cbf_bwd(S, idx, dh, wpack, f_bwd, wrm, wvec, *, passes=2, dE=None, partial=None, num_blocks=None,
             fused=False, dang=None, valid=None, counts=None, idx1=None, grad_scale=1.0, src=None, nev=None,
-            act=None, nact=None, prec=None, gscale=None):
+            act=None, nact=None, prec=None, gscale=None, stamps=None, rec=None, wrm16=None, w16=None):
     """dh (passes, T, B, N, K) -> dE (passes, T, B, N, K, 4), per-WG dW slabs (nb, CBF_PARTIAL).
 
     fused=True (training, passes=2): dh is not read; the kernel evaluates h and h' of every
@@ -637,6 +654,14 @@ def cbf_bwd(S, idx, dh, wpack, f_bwd, wrm, wvec, *, passes=2, dE=None, partial=N
         check(act, torch.int32, (2 * B * T * N * K,), "act")
         check(nact, torch.int32, (1,), "nact")
     f16 = _half(wpack, "wpack", prec)
+    if rec is not None:
+        # 16x16x32 x3 backward over cbf_compact's records (csrc/cbf16.h)
+        if f16 != 2 or fused or src is None:
+            raise NativeError("record backward: fp32 (x3) precision, deduplicated non-fused path only")
+        check(rec, torch.int32, (2 * B * T * N * K, 4), "rec")
+        check(nact, torch.int32, (1,), "nact")
+        check(wrm16, wpack.dtype, (2 * CBF_RM16,), "wrm16")
+        check(w16, wpack.dtype, (6 * 1024,), "w16")
     check(wpack, wpack.dtype, None, "wpack")
     check(wvec, torch.float32, None, "wvec")
     if wpack.numel() < (f_bwd + 70) * 512 * _planes(f16):
@@ -649,14 +674,15 @@ def cbf_bwd(S, idx, dh, wpack, f_bwd, wrm, wvec, *, passes=2, dE=None, partial=N
         raise NativeError("too many edge evaluations for 32-bit indexing")
     nb = num_blocks or cbf_bwd_grid(E * passes, S.device)
     check(partial, torch.float32, (nb, CBF_PARTIAL), "partial")
+    check(stamps, torch.int64, (nb, 8 if (rec is not None or f16 != 2) else 4, 8), "stamps")   # phase cycles
     rc = lib().cbf_bwd(ptr(S), S.stride(1) // W, S.stride(0) // W, ptr(idx), B, T, N, K, int(passes),
                        0 if fused else ptr(dh),
                        ptr(wpack), int(f_bwd), ptr(wrm), ptr(wvec), ptr(dE), ptr(partial), float(C.OBS_RADIUS),
                        float(C.DIST_MIN_THRES), float(C.CBF_DIST_EPS_COORD * D), int(fused), ptr(dang) if fused else 0,
                        ptr(valid) if fused else 0, ptr(counts) if fused else 0,
                        _loss_consts(grad_scale, gscale), ptr(idx1), D, nb,
-                       f16, ptr(src), ptr(nev) if src is not None else 0, ptr(act), ptr(nact) if act is not None else 0,
-                       stream_handle())
+                       f16, ptr(src), ptr(nev) if src is not None else 0, ptr(act), ptr(nact) if (act is not None or rec is not None) else 0,
+                       ptr(rec), ptr(wrm16), ptr(w16), ptr(stamps), stream_handle())
     _ok(rc, "cbf_bwd")
     return nb
 

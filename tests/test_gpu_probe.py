@@ -118,3 +118,23 @@ def test_lane_xor_exchanges_and_reductions():
     np.testing.assert_array_equal(got[6], ws.view(np.uint32))
     np.testing.assert_array_equal(got[7], wm.view(np.uint32))
     np.testing.assert_array_equal(got[8], s32.view(np.uint32))
+
+
+def test_mfma16_layout_exact():
+    """v_mfma_f32_16x16x32_bf16 (the x3 CBF backward, csrc/cbf16.h): lane (n = l & 15, g = l >> 4)
+    holds A[n][8g + j], B[8g + j][n] and D[4g + i][n] (layout.emu_mfma16)."""
+    rng = np.random.default_rng(5)
+    a = rng.integers(-4, 5, size=(64, 8)).astype(np.float32)
+    b = rng.integers(-4, 5, size=(64, 8)).astype(np.float32)
+    ta = torch.tensor(a, dtype=torch.bfloat16, device=DEV).contiguous()
+    tb = torch.tensor(b, dtype=torch.bfloat16, device=DEV).contiguous()
+    d = torch.zeros(64, 4, dtype=torch.float32, device=DEV)
+    assert native.lib().probe_mfma16(ta.data_ptr(), tb.data_ptr(), d.data_ptr(), native.stream_handle()) == 0
+    torch.cuda.synchronize()
+    d = d.cpu().numpy()
+    D = np.zeros((16, 16), np.float32)
+    for l in range(64):
+        n, g = l & 15, l >> 4
+        for i in range(4):
+            D[L.acc_row16(i, g), n] = d[l, i]
+    np.testing.assert_array_equal(D, L.emu_mfma16(a, b))

@@ -231,3 +231,43 @@ def test_emulated_rowmajor_node_forward_backward():
             b = np.stack([Bn[16 * kk + 8 * (l >> 5): 16 * kk + 8 * (l >> 5) + 8, l & 31] for l in range(64)])
             c = L.emu_mfma(L.emu_wrmT_nat(im["w2"], 32 * mt, kk), b, c)
         np.testing.assert_allclose(acc_to_mat(c), (W[1].T @ Bn)[32 * mt:32 * mt + 32], rtol=1e-6, atol=1e-6)
+
+
+def test_cbf16_permuted_image_chain():
+    """16x16x32 data path (csrc/cbf16.h) emulated lane by lane: A = W from the column-permuted
+    image (one 16-byte read at col 32s + 8g), A = W^T through the transposed-read addressing, and
+    B from packed accumulator tiles (pk4_fr) reproduce W @ X and W^T @ Y."""
+    rng = np.random.default_rng(0)
+    W = rng.standard_normal((128, 64))
+    X = rng.standard_normal((64, 16))
+    Y = rng.standard_normal((128, 16))
+    img = np.array([[W[r, L.perm32_logical(c)] for c in range(64)] for r in range(128)])
+
+    def tiles(M):     # C-layout tiles: tile t, lane (n, g), reg i = M[16t + 4g + i][n]
+        return [[[M[16 * t + 4 * (l >> 4) + i, l & 15] for i in range(4)] for l in range(64)]
+                for t in range(M.shape[0] // 16)]
+
+    def bfrag(T, s):  # pk4_fr(T[2s], T[2s + 1])
+        return np.array([T[2 * s][l] + T[2 * s + 1][l] for l in range(64)])
+
+    TX, TY = tiles(X), tiles(Y)
+    for mt in range(8):
+        D = np.zeros((16, 16))
+        for s in range(2):
+            a = np.array([img[16 * mt + (l & 15), 32 * s + 8 * (l >> 4): 32 * s + 8 * (l >> 4) + 8] for l in range(64)])
+            D += L.emu_mfma16(a, bfrag(TX, s))
+        np.testing.assert_allclose(D, (W @ X)[16 * mt:16 * mt + 16], rtol=1e-12, atol=1e-12)
+    for mt in range(4):                     # W^T: rows = logical columns 16mt.., K over W's rows
+        m0 = 16 * mt
+        D = np.zeros((16, 16))
+        for s in range(4):
+            a = np.zeros((64, 8))
+            for l in range(64):
+                n, g = l & 15, l >> 4
+                p, t = n >> 2, n & 3
+                col = 32 * (m0 >> 5) + 4 * ((m0 >> 4) & 1) + 8 * p + t
+                assert L.perm32_logical(col) == m0 + n
+                for j in range(8):
+                    a[l, j] = img[32 * s + 4 * g + (j & 3) + 16 * (j >> 2), col]
+            D += L.emu_mfma16(a, bfrag(TY, s))
+        np.testing.assert_allclose(D, (W.T @ Y)[m0:m0 + 16], rtol=1e-12, atol=1e-12)
