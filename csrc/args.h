@@ -176,6 +176,7 @@ struct CbfBwdArgs {
   const int4* rec;
   const h16* wrm16;
   const h16* w16;
+  float* dbg;                   // diagnostics (null in production): per-record forward sums (cbf16)
   unsigned long long* stamps;   // diagnostics (null in production): per-wave shader-clock cycles
                                 // summed per phase over the wave's chunks, [workgroup][wave][8]
                                 // (scripts/stamps_cbf.py)

@@ -117,10 +117,11 @@ static int cbf_bwd(u64 S, long s_env, long s_step, u64 idx, int B, int T, int N,
                    u64 wpack, int f_bwd, u64 wrm, u64 wvec, u64 dE, u64 partial, float obs_r, float dist_thr,
                    float dist_eps, int fused, u64 dang, u64 valid, u64 counts, py::tuple lc, u64 idx1,
                    int dim, int num_blocks, int prec, u64 src, u64 nev, u64 act, u64 nact, u64 rec, u64 wrm16, u64 w16,
-                   u64 stamps, u64 stream) {
+                   u64 dbg, u64 stamps, u64 stream) {
   mb::CbfBwdArgs a{};
   a.stamps = P<unsigned long long>(stamps);
   a.rec = P<const int4>(rec); a.wrm16 = P<const h16>(wrm16); a.w16 = P<const h16>(w16);
+  a.dbg = P<float>(dbg);
   a.dim = dim;
   a.src = P<const int>(src); a.nev = P<const int>(nev); a.act = P<const int>(act); a.nact = P<const int>(nact);
   a.idx1 = P<const int>(idx1);

@@ -47,6 +47,13 @@ static_assert(C16_LDS <= 160 * 1024 - 512, "LDS budget");
 
 struct Pk4 { h16x4 h, l; };
 
+#ifndef CBF16_DBG
+#define CBF16_DBG 0    // 1: per-record forward sums to a.dbg (scripts/check_cbf16.py)
+#endif
+#ifndef CBF16_REC2
+#define CBF16_REC2 1   // records two chunks ahead, states one chunk ahead (0: record + states at the loop end)
+#endif
+
 DEV f32x4 mfma16(const h16x8& a, const h16x8& b, const f32x4& c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
@@ -187,10 +194,11 @@ struct Ev16 {
   float4 si[D == 2 ? 1 : 2], sj[D == 2 ? 1 : 2];   // raw state records of i and j
 };
 
+// branch-free: r is always a real record (the index is clamped), so the loads need no guard and
+// no merge -- a conditional load would make the compiler wait for it right at the merge
 template <int D>
-DEV void ev16_issue(const CbfBwdArgs& a, const int4& r, bool in, Ev16<D>& x) {
+DEV void ev16_issue(const CbfBwdArgs& a, const int4& r, Ev16<D>& x) {
   x.r = r;
-  if (!in) return;
   const unsigned e = (unsigned)r.y & 0x7fffffffu, pass = (unsigned)r.y >> 31;
   const unsigned ik = e / (unsigned)a.K;
   const unsigned tb = ik / (unsigned)a.N;
@@ -258,22 +266,30 @@ __global__ __launch_bounds__(C16_NW * 64) void cbf_bwd16_kernel(CbfBwdArgs a) {
 
   // load pipeline: records two chunks ahead, state records one chunk ahead
   const long stride = gridDim.x;
+  // (indices past the list are clamped to its last record: unconditional loads, no merges)
   auto rec_at = [&](long chunk) -> int4 {
     const long v = chunk * C16_CH + wave * 16 + n;
-    return (chunk < nchunks && v < EV) ? rec[v] : int4{0, 0, 0, 0};
+    return rec[v < EV ? v : EV - 1];
   };
-  auto in_at = [&](long chunk) { return chunk < nchunks && chunk * C16_CH + wave * 16 + n < EV; };
+  auto in_at = [&](long chunk) { return chunk * C16_CH + wave * 16 + n < EV; };
+  const long c0 = blockIdx.x;
+  if (c0 < nchunks) {   // else no chunk for this workgroup (EV may be 0): zero slab
   Ev16<D> nx;
-  long c0 = blockIdx.x;
-  ev16_issue<D>(a, rec_at(c0), in_at(c0), nx);
+  ev16_issue<D>(a, rec_at(c0), nx);
+#if CBF16_REC2
   int4 r2 = rec_at(c0 + stride);
+#endif
 
   for (long chunk = c0; chunk < nchunks; chunk += stride) {
     if (a.stamps) { tck = __builtin_amdgcn_s_memtime(); ph[7] += 1; }
     const Ev16<D> cur = nx;
     const bool in = in_at(chunk);
-    ev16_issue<D>(a, r2, in_at(chunk + stride), nx);          // state records of the next chunk
+#if CBF16_REC2
+    ev16_issue<D>(a, r2, nx);                                 // state records of the next chunk
     r2 = rec_at(chunk + 2 * stride);                          // records two chunks ahead
+#else
+    const int4 rn = rec_at(chunk + stride);                   // next chunk's record (states: loop end)
+#endif
     // ---- edge features of this lane's evaluation (all four g-lanes of column n hold it)
     float rp[D], rv[D];
     {
@@ -305,7 +321,10 @@ __global__ __launch_bounds__(C16_NW * 64) void cbf_bwd16_kernel(CbfBwdArgs a) {
     Pk4 H1[4], H2[8];
     f32x4 H3[4];
 #pragma unroll
-    for (int mt = 0; mt < 4; ++mt) H1[mt] = to_pk4(relu4(mma16_bx(frag_fr(a.w16, mt, lane), F, zero4())));
+    for (int mt = 0; mt < 4; ++mt) {
+      const f32x4 t = mma16_bx(frag_fr(a.w16, mt, lane), F, zero4());
+      H1[mt] = to_pk4(relu4(t));
+    }
 #pragma unroll
     for (int mt = 0; mt < 8; ++mt) {
       f32x4 t = bias4(b2, 16 * mt, g);
@@ -320,6 +339,34 @@ __global__ __launch_bounds__(C16_NW * 64) void cbf_bwd16_kernel(CbfBwdArgs a) {
       for (int s = 0; s < 4; ++s) t = mma16(w16_fr(W3c, S16_W3, 16 * mt, s, lane), pk4_fr(H2[2 * s], H2[2 * s + 1]), t);
       H3[mt] = relu4(t);
     }
+#if CBF16_DBG
+    if (a.dbg) {   // diagnostics: sum H1, sum H2, sum w4 . H3 per record
+      float s1 = 0.f, s2 = 0.f, s3 = 0.f;
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          s1 += (float)H1[mt].h[i] + (float)H1[mt].l[i];
+          s3 += vl[192 + 16 * mt + 4 * g + i] * H3[mt][i];
+        }
+#pragma unroll
+      for (int mt = 0; mt < 8; ++mt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) s2 += (float)H2[mt].h[i] + (float)H2[mt].l[i];
+      s1 += lane_xorf<16>(s1); s1 += lane_xorf<32>(s1);
+      s2 += lane_xorf<16>(s2); s2 += lane_xorf<32>(s2);
+      s3 += lane_xorf<16>(s3); s3 += lane_xorf<32>(s3);
+      const long v = chunk * C16_CH + wave * 16 + n;
+      if (in && g == 0) { a.dbg[3 * v] = s1; a.dbg[3 * v + 1] = s2; a.dbg[3 * v + 2] = s3; }
+    }
+#endif
+    // Scheduling boundary between the forward recompute and the head backward. Measured
+    // (scripts/check_cbf16.py, profiles/r3_cbf16/variants.log): when hipcc 7.2 interleaves the
+    // two, a deterministic ~20 % of the evaluations get a wrong forward (h, dE, dW off by 2-80 %);
+    // with this barrier (or at -O1, or with other code at this point) every section matches the
+    // 32x32x16 kernel to ~1e-7 and dE matches an fp64 reference. The GPU tests
+    // (test_gpu_dedup / test_gpu_fp32 / test_gpu_cbf16) pin it.
+    __builtin_amdgcn_sched_barrier(0);
     stamp(0);
     // ---- head backward: dW4 / db4 exact fp32 per lane, dH3pre = w4 * dh . relu'(H3)
     if (g == 0) db4 += dhv;
@@ -445,6 +492,10 @@ __global__ __launch_bounds__(C16_NW * 64) void cbf_bwd16_kernel(CbfBwdArgs a) {
       __syncthreads();
     }
     stamp(3);
+#if !CBF16_REC2
+    ev16_issue<D>(a, rn, nx);
+#endif
+  }
   }
   if (a.stamps && lane == 0)
 #pragma unroll

@@ -210,7 +210,7 @@ class HipEngine:
             # x3: the 16x16x32 backward (csrc/cbf16.h, two waves per SIMD) reads cbf_compact's
             # 16-byte records of the active evaluations instead of the index list
             # (MACBF_CBF16=0: the 32x32x16 kernel on the index list, for A/B runs)
-            self.cbf16 = self.prec == "fp32" and os.environ.get("MACBF_CBF16", "0") != "0"
+            self.cbf16 = self.prec == "fp32" and os.environ.get("MACBF_CBF16", "1") != "0"
             self.act_list = torch.zeros(2 * E, dtype=i32, device=dev) if not self.cbf16 else None
             self.rec_list = torch.zeros(2 * E, 4, dtype=i32, device=dev) if self.cbf16 else None
             self.loss_red = torch.zeros(native.DH_PARTIAL, dtype=f32, device=dev)

@@ -618,7 +618,7 @@ CBF_RM16 = 128 * 80 + 64 * 144     # elements per plane of the 16x16x32 W2 | W3 
 
 def cbf_bwd(S, idx, dh, wpack, f_bwd, wrm, wvec, *, passes=2, dE=None, partial=None, num_blocks=None,
             fused=False, dang=None, valid=None, counts=None, idx1=None, grad_scale=1.0, src=None, nev=None,
-            act=None, nact=None, prec=None, gscale=None, stamps=None, rec=None, wrm16=None, w16=None):
+            act=None, nact=None, prec=None, gscale=None, stamps=None, rec=None, wrm16=None, w16=None, dbg=None):
     """dh (passes, T, B, N, K) -> dE (passes, T, B, N, K, 4), per-WG dW slabs (nb, CBF_PARTIAL).
 
     fused=True (training, passes=2): dh is not read; the kernel evaluates h and h' of every
@@ -682,7 +682,7 @@ def cbf_bwd(S, idx, dh, wpack, f_bwd, wrm, wvec, *, passes=2, dE=None, partial=N
                        ptr(valid) if fused else 0, ptr(counts) if fused else 0,
                        _loss_consts(grad_scale, gscale), ptr(idx1), D, nb,
                        f16, ptr(src), ptr(nev) if src is not None else 0, ptr(act), ptr(nact) if (act is not None or rec is not None) else 0,
-                       ptr(rec), ptr(wrm16), ptr(w16), ptr(stamps), stream_handle())
+                       ptr(rec), ptr(wrm16), ptr(w16), ptr(dbg), ptr(stamps), stream_handle())
     _ok(rc, "cbf_bwd")
     return nb
 

@@ -20,8 +20,15 @@ def main():
     ap.add_argument("--agents", type=int, default=96)
     ap.add_argument("--envs", type=int, default=3)
     ap.add_argument("--T", type=int, default=6)
+    ap.add_argument("--so", default=None)
     a = ap.parse_args()
     import torch
+    if a.so:
+        import importlib.util
+        spec = importlib.util.spec_from_file_location("macbf_gnn_amd._C", a.so)
+        mod = importlib.util.module_from_spec(spec)
+        sys.modules["macbf_gnn_amd._C"] = mod
+        spec.loader.exec_module(mod)
     from macbf_gnn_amd import config as C
     from macbf_gnn_amd.engine import Trainer
     from macbf_gnn_amd.ops import native
@@ -56,6 +63,10 @@ def main():
             act[:nact] = rec[:nact, 0]
             kk.pop("rec"); kk.pop("wrm16"); kk.pop("w16")
             kk["act"] = act
+        dbg = torch.zeros(3 * nact + 3, dtype=torch.float32, device=dev)
+        if mode == "new" and os.environ.get("CHK_DBG", "0") == "1":
+            dbg = torch.zeros(3 * nact + 3, dtype=torch.float32, device=dev)
+            kk["dbg"] = dbg
         orig(*x, **kk)
         torch.cuda.synchronize()
         outs[mode] = (dE.clone(), part.double().sum(0))
@@ -77,10 +88,10 @@ def main():
     T, B, N, K = idx.shape
     E = idx.numel()
     prm = {pn: tr.fp.flat[o:o + n].view(shape).double().cpu() for (m, pn, shape, o, n) in tr.fp.specs}
-    W1, b1 = prm["cbf_net.0.weight"], prm["cbf_net.0.bias"]
-    W2, b2 = prm["cbf_net.2.weight"], prm["cbf_net.2.bias"]
-    W3, b3 = prm["cbf_net.4.weight"], prm["cbf_net.4.bias"]
-    W4 = prm["cbf_net.6.weight"]
+    W1, b1 = prm["cbf_net.0.weight"].reshape(64, -1), prm["cbf_net.0.bias"]
+    W2, b2 = prm["cbf_net.2.weight"].reshape(128, -1), prm["cbf_net.2.bias"]
+    W3, b3 = prm["cbf_net.4.weight"].reshape(64, -1), prm["cbf_net.4.bias"]
+    W4 = prm["cbf_net.6.weight"].reshape(1, -1)
     rows = torch.cat([bad[:24].cpu(), torch.arange(0, min(nact, 8))])
     errs = []
     for v in rows.tolist():
@@ -101,12 +112,14 @@ def main():
         h3 = torch.relu(W3 @ h2 + b3)
         h = (W4 @ h3).sum()
         (gr,) = torch.autograd.grad(h * dhv, r)
+        dv3 = dbg[3 * v: 3 * v + 3].double().cpu().tolist()
+        sums = {"h1": [dv3[0], float(h1.sum())], "h2": [dv3[1], float(h2.sum())], "h": [dv3[2], float(h)]}
         ref = gr if i != j else torch.zeros(4, dtype=torch.float64)
         dn_ = outs["new"][0].view(-1, dE.shape[-1])[u_].double().cpu()
         do_ = outs["old"][0].view(-1, dE.shape[-1])[u_].double().cpu()
         errs.append({"v": v, "pass": pas, "self": i == j, "n": v % 16, "wave": (v // 16) % 8,
                      "e_new": float((dn_ - ref).norm() / ref.norm().clamp(min=1e-30)),
-                     "e_old": float((do_ - ref).norm() / ref.norm().clamp(min=1e-30))})
+                     "e_old": float((do_ - ref).norm() / ref.norm().clamp(min=1e-30)), **sums})
     for q in errs:
         print(json.dumps(q))
     print(json.dumps(res))
