@@ -2241,10 +2241,24 @@ extern "C" int MB_SYM(ctrl_node_bwd)(const mb::CtrlNodeBwdArgs* a, int num_block
   return (int)hipGetLastError();
 }
 
+#if MB_X3
+#include "ctrl16.h"
+#endif
+
 extern "C" int MB_SYM(ctrl_edge_bwd)(const mb::CtrlEdgeBwdArgs* a, int num_blocks, hipStream_t st) {
   using namespace mb;
   using namespace mb::MB_PREC;
   if (a->K > 16 || a->K < 1) return -1;
+  if (a->w16) {   // 16x16x32 kernel, two waves per SIMD (x3 build, K = 12)
+#if MB_X3
+    if (a->K != 12) return -7;
+    if (a->dim == 3) launch_ctrl_edge_bwd16<3>(*a, num_blocks, st);
+    else launch_ctrl_edge_bwd16<2>(*a, num_blocks, st);
+    return (int)hipGetLastError();
+#else
+    return -8;
+#endif
+  }
   const size_t lds = ctrl_edge_bwd_lds();
   // K = 12 (TOP_K): constant-K instantiation (MACBF_EB_K12=0 forces the runtime-K one, A/B)
   static const bool k12_off = [] { const char* e = getenv("MACBF_EB_K12"); return e && e[0] == '0'; }();

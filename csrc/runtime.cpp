@@ -359,6 +359,7 @@ class BpttDriver {
     if (fused_ && (node_chunk_ != 32 || nb_node_ != nb_edge_))
       throw std::invalid_argument("BpttDriver: the fused step needs 32-agent chunks and one grid");
     gscale_ = c.contains("gscale") ? U("gscale") : 0;   // fp16: device loss scale (or 0)
+    ew16_ = c.contains("ctrl_w16") ? U("ctrl_w16") : 0;   // x3, K = 12: 16x16x32 edge backward fragments
     if (B_ < 1 || N_ < 1 || Nn_ < N_ || K_ < 1 || K_ > 16 || (D_ != 2 && D_ != 3) || Tmax_ < 1 || nb_node_ < 1 ||
         nb_edge_ < 1)
       throw std::invalid_argument("BpttDriver: bad dimensions");
@@ -439,6 +440,7 @@ class BpttDriver {
         a.wpack = P<const h16>(wpack_); a.f_ew1f = f_ew1f_; a.f_ew2tn = f_ew2tn_;
         a.dEc = P<float4>(dEc_); a.de_env = nk; a.partial = P<float>(part_edge_); a.qsplit = qsplit_;
         a.init = t == T - 1;
+        a.w16 = fused_ ? nullptr : P<const h16>(ew16_);   // (the fused step keeps its own edge phase)
       }
       if (fused_) {      // node + edge backward of the same 32-agent chunks in one launch
         chk((prec_ == 2 ? mb_ctrl_bwd_step_x3 : prec_ == 1 ? mb_ctrl_bwd_step_f16 : mb_ctrl_bwd_step)(&na, &ea, nb_node_, st),
@@ -457,7 +459,7 @@ class BpttDriver {
  private:
   int B_, N_, Nn_, K_, D_, R_, Tmax_, prec_, prow_, nb_node_, nb_edge_, qsplit_, small_ = 0, node_chunk_ = 0, fused_ = 0;
   u64 pooled_, S_, G_, A_, dS_, Gb_, valid_, idx_, argmax_, rptr_, redges_, wrm_, wvec_, act_scale_, dP_, ego_, dEc_;
-  u64 part_node_, part_edge_, wpack_, gscale_ = 0;
+  u64 part_node_, part_edge_, wpack_, gscale_ = 0, ew16_ = 0;
   int o1_, o2_, o3_, o4_, f_ew1f_, f_ew2tn_;
   float dt_, sqrt3_;
 };

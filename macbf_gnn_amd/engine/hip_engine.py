@@ -218,6 +218,10 @@ class HipEngine:
             self.nev_dev = torch.zeros(1, dtype=i32, device=dev)      # [U] of the match
             self.nact_dev = torch.zeros(1, dtype=i32, device=dev)     # active evaluations
             self.hstream = torch.cuda.Stream(device=dev)              # rollout-overlapped CBF h slices
+        # x3, K = 12: the 16x16x32 controller edge backward (csrc/ctrl16.h, two waves per SIMD);
+        # MACBF_EB16=0: the 32x32x16 kernel (A/B runs)
+        self.eb16_w = (self.pw.ctrl_w16 if (self.prec == "fp32" and K == 12
+                                            and os.environ.get("MACBF_EB16", "0") != "0") else None)
         self.host_dist = torch.zeros(T, B, dtype=torch.int64, pin_memory=True)
         self.copy_stream = torch.cuda.Stream(device=dev)
         self.aux = torch.cuda.Stream(device=dev)      # reverse-CSR build overlaps the CBF kernel
@@ -678,6 +682,7 @@ class HipEngine:
                 dt=float(C.TIME_STEP), sqrt3=float(C.SQRT3), small=int(self.small_bptt),
                 node_chunk=int(native.node_bwd_chunk(B * N, self.dev)),
                 fused_step=int(native.bwd_step_fused(B * N, self.dev)),
+                ctrl_w16=native.ptr(self.eb16_w) if self.eb16_w is not None else 0,
                 gscale=native.ptr(getattr(self.tr, "gscale_dev", None))))
             self._bdrv = native.lib().BpttDriver(c)
         return self._bdrv
@@ -707,7 +712,7 @@ class HipEngine:
                 native.ctrl_bwd_step(node, edge, nbn)            # node + edge backward: one launch
             else:
                 native.ctrl_node_bwd(**node, num_blocks=nbn)
-                native.ctrl_edge_bwd(**edge, num_blocks=nbe)
+                native.ctrl_edge_bwd(**edge, num_blocks=nbe, w16=self.eb16_w)
 
     def _counts_ready(self, work):
         """Join the (async) count all-reduce (the node backward reads the action-loss count

@@ -577,6 +577,39 @@ def cbf_packer16(fp_offsets: Dict[str, int], dim: int = 2) -> Packer:
     return p
 
 
+def ctrl_edge_packer16(fp_offsets: Dict[str, int], dim: int = 2) -> Packer:
+    """Fragments of the 16x16x32 x3 controller edge backward (csrc/ctrl16.h): ew1f16 (64 x 32:
+    the 16 edge-feature slots of ctrl_edge_slot, 4 M-tiles), ew2tn16 (64 x 128 = W2^T with a
+    natural-k B read from the dZ image rows: 4 M-tiles x 4 K-steps), ew1ft16 (16 x 64 = W1^T for the
+    2D relative-state features, accumulator-ordered k: 2 K-steps)."""
+    eW1, eb1 = fp_offsets["controller_centr_net.0.weight"], fp_offsets["controller_centr_net.0.bias"]
+    eW2 = fp_offsets["controller_centr_net.2.weight"]
+    E = 2 * dim + 1
+
+    def ew1f(o, k):
+        sl = ctrl_edge_slot(k, dim) if (o < 64 and k < 16) else None
+        if sl is None:
+            return ZERO
+        return eb1 + o if sl[0] == "b" else eW1 + o * E + sl[1]
+
+    def ew2tn(m, f):
+        if m < 64 and f < 128:
+            return eW2 + f * 64 + m
+        return ZERO
+
+    def ew1ft(f, o):
+        if f < 2 * dim and o < 64:
+            return eW1 + o * E + f
+        return ZERO
+
+    p = Packer()
+    p.blocks.append(Block("ew1f16", pack_frags16(ew1f, 4, 1, "nat"), 0))
+    p.blocks.append(Block("ew2tn16", pack_frags16(ew2tn, 4, 4, "nat"), 4))
+    p.blocks.append(Block("ew1ft16", pack_frags16(ew1ft, 1, 2, "acc"), 20))
+    p.nfrag = 22
+    return p
+
+
 def emu_mfma16(a: np.ndarray, b: np.ndarray) -> np.ndarray:
     """v_mfma_f32_16x16x32 on per-lane fragments a, b (64, 8) -> D (16, 16)."""
     A = np.zeros((16, 32))

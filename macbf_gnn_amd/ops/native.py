@@ -864,7 +864,9 @@ def ctrl_node_bwd(pooled, S, G, A, Gn, valid_t, wrm, offs, wvec, act_coef, dP, e
 
 
 def ctrl_edge_bwd(S, idx, argmax, dP, wpack, f_ew1f, f_ew2tn, dEc, partial, num_blocks, prec=None, init=False,
-                  _defer=False):
+                  _defer=False, w16=None):
+    """w16 (x3, K = 12): the 16x16x32 fragments (layout.ctrl_edge_packer16) -> the two-waves-per-SIMD
+    kernel (csrc/ctrl16.h); same slabs, same dEc records."""
     B, N, K = idx.shape
     D = dim_of(S)
     W = rec_width(D)
@@ -884,7 +886,11 @@ def ctrl_edge_bwd(S, idx, argmax, dP, wpack, f_ew1f, f_ew2tn, dEc, partial, num_
             f16, ctrl_edge_qsplit(B * N, S.device), int(bool(init)))
     if _defer:
         return args
-    _ok(lib().ctrl_edge_bwd(*args, stream_handle()), "ctrl_edge_bwd")
+    if w16 is not None:
+        if f16 != 2 or K != 12:
+            raise NativeError("16x16x32 edge backward: fp32 (x3) precision and K = 12 only")
+        check(w16, wpack.dtype, (22 * 1024,), "w16")
+    _ok(lib().ctrl_edge_bwd(*args, ptr(w16), stream_handle()), "ctrl_edge_bwd")
 
 
 def ctrl_bwd_step(node: dict, edge: dict, num_blocks: int):
