@@ -221,7 +221,7 @@ class HipEngine:
         # x3, K = 12: the 16x16x32 controller edge backward (csrc/ctrl16.h, two waves per SIMD);
         # MACBF_EB16=0: the 32x32x16 kernel (A/B runs)
         self.eb16_w = (self.pw.ctrl_w16 if (self.prec == "fp32" and K == 12
-                                            and os.environ.get("MACBF_EB16", "0") != "0") else None)
+                                            and os.environ.get("MACBF_EB16", "1") != "0") else None)
         self.host_dist = torch.zeros(T, B, dtype=torch.int64, pin_memory=True)
         self.copy_stream = torch.cuda.Stream(device=dev)
         self.aux = torch.cuda.Stream(device=dev)      # reverse-CSR build overlaps the CBF kernel

@@ -100,10 +100,13 @@ def test_small_rollout_repeatable_and_trains():
 
 @pytest.mark.parametrize("kw", [dict(dtype="fp32"), dict(dtype="bf16"), dict(dtype="fp32", dim=3, num_obstacles=2, N=24),
                                 dict(dtype="fp32", N=64, B=2), dict(dtype="bf16", N=10, B=5)])
-def test_small_bptt_matches_per_step_launches(kw):
+def test_small_bptt_matches_per_step_launches(kw, monkeypatch):
     """Persistent BPTT (one workgroup per env, csrc/ctrl.hip bptt_small_kernel): the same device
     bodies as the per-step kernels -> the same dL/ds_t recursion and weight gradients bit for bit
-    (slab rows differ: one per env, so the final slab sums may differ in rounding order)."""
+    (slab rows differ: one per env, so the final slab sums may differ in rounding order). The
+    per-step side uses the 32x32x16 edge backward (MACBF_EB16=0), whose body the persistent kernel
+    shares; the 16x16x32 one is checked against it in test_gpu_eb16.py."""
+    monkeypatch.setenv("MACBF_EB16", "0")
     a = _trainer(True, small_bptt=False, T=20, **kw)
     b = _trainer(True, small_bptt=True, T=20, **kw)
     assert b.engine.small_bptt and not a.engine.small_bptt
@@ -127,9 +130,11 @@ def test_fused_bptt_step_matches_separate_launches(native_bptt, monkeypatch):
     """Fused node + edge backward per reverse step (csrc/ctrl.hip ctrl_bwd_step_kernel, the
     strong-scaling slice path) against the separate node / edge launches: the recursion (G, dP,
     ego) bit for bit; the weight gradients up to the slab summation order (the edge slab rows
-    differ)."""
+    differ). The separate launches use the 32x32x16 edge backward (MACBF_EB16=0), whose body the
+    fused step shares."""
     from macbf_gnn_amd.engine.hip_engine import HipEngine
     monkeypatch.setattr(HipEngine, "native_bptt", native_bptt)
+    monkeypatch.setenv("MACBF_EB16", "0")
     trs = []
     for fused in ("0", "1"):
         monkeypatch.setenv("MACBF_BWD_FUSED", fused)
