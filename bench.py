@@ -20,6 +20,11 @@ with dynamic loss scaling). Default window: 20 timed steps after 5 warm-up steps
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--dtype fp32|bf16|fp16] [--global_envs G]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+
+`python bench.py --gpus N` without a launcher starts the N ranks itself (parallel/launch.py): one
+process per GPU, rank r on device r, over RCCL; it fails before any work if fewer than N devices
+are visible (MACBF_DP_BACKEND=gloo rehearses N ranks on one device) or if a launcher's
+WORLD_SIZE disagrees with --gpus.
 """
 from __future__ import annotations
 
@@ -41,7 +46,9 @@ CPU_ROLLOUT_PROXY = 93009.0
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one per GPU, RCCL). Standalone (WORLD_SIZE unset) N > 1 starts N rank "
+                         "processes through torch.distributed.run; under a launcher it must equal WORLD_SIZE")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--agents", type=int, default=1024)
@@ -60,40 +67,62 @@ def main():
                     help="replay each iteration as captured HIP graphs (launch-bound small configs)")
     ap.add_argument("--phases", action="store_true",
                     help="after the timed loop, 2 extra steps with per-phase device-event timings")
+    ap.add_argument("--device", default="hip", choices=["hip", "cpu"],
+                    help="cpu: the pure-torch oracle engine over gloo (launch-path rehearsal and CPU tests; "
+                         "not a benchmark)")
     args = ap.parse_args()
 
     import torch
+    from macbf_gnn_amd.parallel import launch
+
+    # the parent decides before any GPU call: device_count() does not initialise the device
+    ndev = torch.cuda.device_count() if args.device == "hip" else 0
+    plan = launch.plan(args.gpus, device_count=ndev, device=args.device)
+    if plan.action == "spawn":
+        sys.exit(launch.spawn(os.path.abspath(__file__), sys.argv[1:], plan.ranks))
+
     from macbf_gnn_amd import config as C
     from macbf_gnn_amd.engine import Trainer
-    from macbf_gnn_amd.parallel import DP, env_world
+    from macbf_gnn_amd.parallel import DP
 
-    world, rank, local_rank = env_world()
-    if not torch.cuda.is_available():
-        raise SystemExit("bench.py needs a HIP device")
-    dev = torch.device("cuda", local_rank % max(torch.cuda.device_count(), 1))
-    torch.cuda.set_device(dev)
+    cpu = args.device == "cpu"
+    if cpu:
+        dev = torch.device("cpu")
+    else:
+        if not torch.cuda.is_available():
+            raise SystemExit("bench.py needs a HIP device (--device cpu rehearses the launch path)")
+        dev = torch.device("cuda", launch.device_index(plan, ndev))
+        torch.cuda.set_device(dev)
     dp = DP(device=dev)
+    world, rank = dp.world, dp.rank
+    if world != plan.ranks:
+        raise SystemExit(f"launch error: process group has {world} ranks, expected {plan.ranks}")
+    # every rank reports its device; an RCCL run must hold one distinct device per rank
+    dev_ids = dp.gather_ints([-1 if cpu else dev.index, _device_uid(torch, dev)])
+    if not cpu and not plan.share_devices and len({u for _, u in dev_ids}) != world:
+        raise SystemExit(f"launch error: ranks share devices {dev_ids}; RCCL needs one device per rank")
+    sync = (lambda: None) if cpu else torch.cuda.synchronize
     strong = args.global_envs > 0
     if strong and args.global_envs % world:
         raise SystemExit(f"--global_envs {args.global_envs} must be divisible by the world size {world}")
     envs = args.global_envs // world if strong else args.envs
     cfg = C.TrainConfig(num_agents=args.agents, num_envs=envs, inner_loops=args.inner_loops,
-                        seed=args.seed, device="hip", early_stop=not args.no_early_stop,
+                        seed=args.seed, device="cpu" if cpu else "hip", early_stop=not args.no_early_stop,
                         display_steps=10 ** 9, save_steps=10 ** 9, dim=args.dim, num_obstacles=args.num_obstacles,
-                        dtype=args.dtype, graph=args.graph)
+                        dtype=args.dtype if not cpu else "fp32", graph=args.graph and not cpu)
     tr = Trainer(cfg, device=dev, dp=dp)
 
     for _ in range(args.warmup):
         tr.train_step()
     dp.barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     stats = [tr.train_step() for _ in range(args.steps)]   # device-resident until read
     dp.barrier()
-    torch.cuda.synchronize()
+    sync()
     elapsed = time.perf_counter() - t0
     elapsed = dp.max_scalar(elapsed)
-    acc = torch.tensor([[st["agent_steps"], st["safe_agents"], st["T"]] for st in stats],
+    acc = torch.tensor([[float(st["agent_steps"]), float(st["safe_agents"]), float(st["T"])] for st in stats],
                        dtype=torch.float64, device=dev).sum(0)    # agent_steps, safe_agents, T
     dp.all_reduce_(acc)
     agent_steps, safe_agents, t_sum = acc.tolist()
@@ -107,6 +136,7 @@ def main():
         tr.timer.enabled = False
         phases = {k: round(v, 3) for k, v in tot.items()}
     value = agent_steps / elapsed
+    backend = dp.backend
     out = {
         "metric": f"agent-steps/sec (train loop) + safety-rate, {args.agents} agents",
         "value": value,
@@ -118,7 +148,7 @@ def main():
         "higher_is_better": True,
         "scaling": "strong" if strong else "weak",
         "vs_baseline": None,
-        "dtype": args.dtype,
+        "dtype": cfg.dtype,
         "data": "synthetic (on-device scenario sampler, random-init weights)",
         "config": {"model": f"MACBF-GNN controller+CBF ({args.dim}-D double integrator, top-K=12"
                             + (f", {args.num_obstacles} obstacles x 12 points" if args.num_obstacles else "") + ")",
@@ -128,21 +158,37 @@ def main():
         "mean_T": t_sum / (args.steps * world),
         "early_stop": not args.no_early_stop,
         "skipped_steps": tr.skipped_steps,
-        "graph": args.graph,
-        "dp_backend": dp.backend,
+        "graph": cfg.graph,
+        "world": world,
+        "dp_backend": backend,
+        "rccl_ranks": world if backend == "nccl" else 0,
+        "device_ids": [d for d, _ in dev_ids],
+        "shared_devices": plan.share_devices,
         "precision": {"fp32": "near-fp32: 3-term split-bf16 MFMA (hi*hi + hi*lo + lo*hi, ~2^-16 relative per "
                               "product), fp32 accumulate; fp32 distances, TTC, losses, Adam",
                       "bf16": "bf16 MFMA inputs, fp32 accumulate", "fp16": "fp16 MFMA inputs, fp32 accumulate, "
-                      "dynamic loss scaling"}[args.dtype],
+                      "dynamic loss scaling"}[cfg.dtype] if not cpu else "fp32 (CPU oracle engine)",
         "cpu_rollout_proxy": {"value": CPU_ROLLOUT_PROXY, "comparable": False,
                               "source": "BASELINE.md: reference rollout-only loop (no losses / backward) @ N=1024, "
                                         "CPU x8; the reference publishes no numbers"},
     }
+    if cpu:
+        out["device"] = "cpu"
     if phases is not None:
         out["phases_ms"] = phases
     if rank == 0:
         print(json.dumps(out), flush=True)
     dp.shutdown()
+
+
+def _device_uid(torch, dev) -> int:
+    """A 62-bit id of the physical device (its UUID, else bus id) for the distinct-device check."""
+    if dev.type != "cuda":
+        return -1
+    import hashlib
+    p = torch.cuda.get_device_properties(dev)
+    key = str(getattr(p, "uuid", "") or "") or f"{getattr(p, 'pci_domain_id', 0)}:{getattr(p, 'pci_bus_id', dev.index)}"
+    return int.from_bytes(hashlib.sha1(key.encode()).digest()[:8], "little") >> 2
 
 
 if __name__ == "__main__":

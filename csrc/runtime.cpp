@@ -421,7 +421,9 @@ class BpttDriver {
           // fused BPTT combine: G_{t+1} from step t+1's records (dS, ego, dEc, graph t+1, G_{t+2})
           const long t1 = t + 1;
           a.cdS = P<const float4>(dS_) + t1 * BN * R_; a.cds_env = N_;
-          a.cego = P<const float4>(ego_); a.cdEc = P<const float4>(dEc_);
+          // dEc is double-buffered by step parity: step t+1's edge records sit in buffer (t+1)&1
+          // while step t's edge phase writes buffer t&1 (the fused launch overlaps the two)
+          a.cego = P<const float4>(ego_); a.cdEc = P<const float4>(dEc_) + (t1 & 1) * BN * K_ * R_;
           a.cptr = P<const int>(rptr_) + t1 * B_ * (Nn_ + 1); a.cptr_env = Nn_ + 1;
           a.cedges = P<const int>(redges_) + t1 * B_ * nk; a.cedges_env = nk;
           a.cGn = (t1 == T - 1 ? P<const float4>(dS_) + (long)T * BN * R_ : P<const float4>(Gb_) + (t1 + 1) * BN * R_);
@@ -438,7 +440,8 @@ class BpttDriver {
         a.dP = P<const h16>(dP_); a.dp_env = (long)N_ * prow_;
         a.B = B_; a.N = N_; a.K = K_;
         a.wpack = P<const h16>(wpack_); a.f_ew1f = f_ew1f_; a.f_ew2tn = f_ew2tn_;
-        a.dEc = P<float4>(dEc_); a.de_env = nk; a.partial = P<float>(part_edge_); a.qsplit = qsplit_;
+        a.dEc = P<float4>(dEc_) + (long)(t & 1) * BN * K_ * R_; a.de_env = nk; a.partial = P<float>(part_edge_);
+        a.qsplit = qsplit_;
         a.init = t == T - 1;
         a.w16 = fused_ ? nullptr : P<const h16>(ew16_);   // (the fused step keeps its own edge phase)
       }

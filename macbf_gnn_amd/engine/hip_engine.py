@@ -163,7 +163,11 @@ class HipEngine:
         self.Gb = torch.zeros(T + 1, B, N, W, dtype=f32, device=dev)
         self.dP = torch.zeros(B, N, self.prow, dtype=bf, device=dev)
         self.ego = torch.zeros(B, N, W, dtype=f32, device=dev)
-        self.dEc = torch.zeros(B, N, K, W, dtype=f32, device=dev)
+        # per-edge controller records of the BPTT, double-buffered by step parity: step t's edge
+        # backward writes dEc[t & 1] while the node backward of step t forms G_{t+1} from
+        # dEc[(t+1) & 1] (in-edges of agents of other workgroups: in the fused node+edge launch the
+        # two phases of different workgroups overlap)
+        self.dEc = torch.zeros(2, B, N, K, W, dtype=f32, device=dev)
         self.counts = torch.zeros(3, dtype=f32, device=dev)
         self.local = torch.zeros(3, dtype=f32, device=dev)        # agent-steps, safe agents, action-loss sum
         self.raw_stats = torch.zeros(STATS_COLS, dtype=f32, device=dev)   # graph mode (fixed address)
@@ -482,6 +486,10 @@ class HipEngine:
         not done before t."""
         valid = self.valid_buf[:T]
         reset = None if self.graph_mode else (self.dist, self.cnt, self.safe, self.act)
+        if reset is not None and not torch.cuda.is_current_stream_capturing():
+            # the early-stop copies of dist[t] into pinned host memory run on copy_stream: the reset
+            # below must not overwrite a row such a copy is still reading (ADVICE r3)
+            torch.cuda.current_stream(self.dev).wait_stream(self.copy_stream)
         native.rollout_stats(self.dist[:T], self.cnt[:T], self.safe[: T + 1], self.act[:T], valid,
                              self.counts, self.local, N=self.N, reset=reset)
         if reset is not None:
@@ -664,7 +672,7 @@ class HipEngine:
                    "rptr": (self.rptr, torch.int32, ((T + G1) * B, Nn + 1)),
                    "redges": (self.redges, torch.int32, ((T + G1) * B, N * K)),
                    "act_scale": (self.counts[2:3], torch.float32, (1,)), "dP": (self.dP, self.hdt, (B, N, self.prow)),
-                   "ego": (self.ego, torch.float32, (B, N, W)), "dEc": (self.dEc, torch.float32, (B, N, K, W))}
+                   "ego": (self.ego, torch.float32, (B, N, W)), "dEc": (self.dEc, torch.float32, (2, B, N, K, W))}
             for name, (t, dt, shape) in exp.items():
                 native.check(t, dt, shape, name)
             if self.part_node.shape[0] < self.nb_node or self.part_edge.shape[0] < self.nb_edge:
@@ -697,7 +705,7 @@ class HipEngine:
             # from step t+1's records (fused BPTT combine, written to Gb[t+1])
             cmb = None
             if t < T - 1:
-                cmb = dict(dS=self.dS[t + 1][sl], ego=self.ego[sl], dEc=self.dEc[sl], rptr=rptr3[t + 1][sl],
+                cmb = dict(dS=self.dS[t + 1][sl], ego=self.ego[sl], dEc=self.dEc[(t + 1) & 1][sl], rptr=rptr3[t + 1][sl],
                            redges=redges3[t + 1][sl], Gn=self.dS[T][sl] if t + 1 == T - 1 else self.Gb[t + 2][sl],
                            Gout=self.Gb[t + 1][sl], K=K)
             node = dict(pooled=self.pooled[t][sl], S=self.S[t][sl], G=self.G[sl], A=self.A[t][sl], Gn=self.dS[T][sl],
@@ -706,7 +714,7 @@ class HipEngine:
                         act_cnt=self.counts[2:3], prec=self.prec, init=t == T - 1,
                         gscale=getattr(self.tr, "gscale_dev", None), combine=cmb)
             edge = dict(S=self.S[t][sl], idx=self.idx[t][sl], argmax=self.argmax[t][sl], dP=self.dP[sl], wpack=pw.ctrl_w,
-                        f_ew1f=pw.ctrl_off["ew1f"], f_ew2tn=pw.ctrl_off["ew2tn"], dEc=self.dEc[sl], partial=part_edge,
+                        f_ew1f=pw.ctrl_off["ew1f"], f_ew2tn=pw.ctrl_off["ew2tn"], dEc=self.dEc[t & 1][sl], partial=part_edge,
                         prec=self.prec, init=t == T - 1)
             if nbn == nbe and native.bwd_step_fused(self.G[sl].shape[0] * self.N, self.dev):
                 native.ctrl_bwd_step(node, edge, nbn)            # node + edge backward: one launch

@@ -178,12 +178,14 @@ class Trainer:
                 native.grad_check(self.fp.grad, self._ok)
             row = getattr(stats, "raw", None)
             row = row if (row is not None and row.numel() >= 18) else None
+            # without a stats row the skip flag is read before the commit kernel re-arms it
+            ok_snap = self._ok.clone() if (row is None and guard) else None
             self.opt.step(self.groups_to_step(), ok=self._ok if guard else None, gscale=self.gscale_dev,
                           good=self._good_dev if self.fp16 else None, growth=self.cfg.loss_scale_growth,
                           stats_row=row)
             self.engine.after_update()
             if row is None:
-                stats["skipped"] = 1 - self._ok[0]
+                stats["skipped"] = 1 - ok_snap[0] if ok_snap is not None else 0
             elif self.fp16:
                 stats.scaled = True
         elif self.cfg.nan_guard and not bool(torch.isfinite(self.fp.grad).all()):

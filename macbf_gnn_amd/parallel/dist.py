@@ -105,6 +105,17 @@ class DP:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
+    def gather_ints(self, vals: list[int]) -> list[tuple]:
+        """Every rank's `vals` (same length on all ranks), ordered by rank: one SUM all-reduce of a
+        (world, len) int64 table in which each rank fills its own row (no object pickling)."""
+        if not self.enabled:
+            return [tuple(int(v) for v in vals)]
+        dev = self.device if (dist.get_backend() == "nccl" and self.device is not None) else "cpu"
+        t = torch.zeros(self.world, len(vals), dtype=torch.int64, device=dev)
+        t[self.rank] = torch.tensor([int(v) for v in vals], dtype=torch.int64)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        return [tuple(r) for r in t.cpu().tolist()]
+
     def shutdown(self):
         if self.owns_pg and dist.is_initialized():
             dist.destroy_process_group()

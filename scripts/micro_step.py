@@ -88,11 +88,11 @@ def k_node():
 
 def k_edge():
     native.ctrl_edge_bwd(eng.S[t], eng.idx[t], eng.argmax[t], eng.dP, pw.ctrl_w, pw.ctrl_off["ew1f"],
-                         pw.ctrl_off["ew2tn"], eng.dEc, eng.part_edge, eng.nb_edge, prec=eng.prec)
+                         pw.ctrl_off["ew2tn"], eng.dEc[0], eng.part_edge, eng.nb_edge, prec=eng.prec)
 
 
 def k_comb():
-    native.node_combine(eng.dS[t], eng.ego, eng.dEc, rptr, redges, eng.Gb[t + 1], eng.Gb[t], K=K)
+    native.node_combine(eng.dS[t], eng.ego, eng.dEc[0], rptr, redges, eng.Gb[t + 1], eng.Gb[t], K=K)
 
 
 out = {"tag": args.tag, "dtype": args.dtype}

@@ -6,6 +6,7 @@ import pytest
 import torch
 
 from macbf_gnn_amd import config as C
+from macbf_gnn_amd.ops import native
 
 pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda")
@@ -125,22 +126,25 @@ def test_small_bptt_matches_per_step_launches(kw, monkeypatch):
     assert torch.equal(g1, b.fp.grad)
 
 
-@pytest.mark.parametrize("native_bptt", [True, False])
-def test_fused_bptt_step_matches_separate_launches(native_bptt, monkeypatch):
+@pytest.mark.parametrize("native_bptt,N,B", [(True, 256, 8), (False, 256, 8), (True, 1024, 12), (False, 1024, 12)])
+def test_fused_bptt_step_matches_separate_launches(native_bptt, N, B, monkeypatch):
     """Fused node + edge backward per reverse step (csrc/ctrl.hip ctrl_bwd_step_kernel, the
     strong-scaling slice path) against the separate node / edge launches: the recursion (G, dP,
     ego) bit for bit; the weight gradients up to the slab summation order (the edge slab rows
     differ). The separate launches use the 32x32x16 edge backward (MACBF_EB16=0), whose body the
-    fused step shares."""
+    fused step shares. 1024 x 12 agents: 384 32-agent chunks on a grid of one workgroup per CU, so
+    workgroups run a second node chunk while others already write step t's edge records (the
+    double-buffered dEc keeps step t+1's records intact)."""
     from macbf_gnn_amd.engine.hip_engine import HipEngine
     monkeypatch.setattr(HipEngine, "native_bptt", native_bptt)
     monkeypatch.setenv("MACBF_EB16", "0")
     trs = []
     for fused in ("0", "1"):
         monkeypatch.setenv("MACBF_BWD_FUSED", fused)
-        trs.append(_trainer(False, small_bptt=False, N=256, B=8, T=12))
+        trs.append(_trainer(False, small_bptt=False, N=N, B=B, T=12))
     a, b = trs
     assert b.engine.nb_node == b.engine.nb_edge
+    assert native.bwd_step_fused(B * N, b.engine.dev) and native.node_bwd_chunk(B * N, b.engine.dev) == 32
     b.fp.flat.copy_(a.fp.flat)
     b.engine.after_update()
     s0, g, obs = a.sample()
