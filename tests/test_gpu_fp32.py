@@ -305,16 +305,24 @@ def _trainer(**kw):
     return Trainer(cfg, device=DEV, dp=DP(device=DEV))
 
 
-@pytest.mark.parametrize("bptt,reuse,N", [(True, True, 32), (False, True, 32), (True, False, 32), (True, True, 256)])
-def test_full_step_grad_fp32(bptt, reuse, N):
-    """One full training step (rollout, losses, BPTT backward) of the fp32 HIP engine against
-    autograd through the fp32 oracle engine: every parameter tensor <= 1e-3 relative norm."""
+@pytest.mark.parametrize("bptt,reuse,N,extra", [
+    (True, True, 32, {}), (False, True, 32, {}), (True, False, 32, {}), (True, True, 256, {}),
+    # SURVEY 4.3 shape list: N <= K (the reference's N <= TOP_K branch, core.py:234-237, D3) and
+    # the tile-straddling sizes of the 16-agent edge waves / 16-evaluation CBF records
+    (True, True, 1, {}), (True, True, 12, {}), (True, True, 13, {}), (True, True, 17, {}),
+    (True, False, 13, {}),
+    (True, True, 40, dict(dim=3, num_obstacles=2)), (True, True, 9, dict(dim=3, num_obstacles=1)),
+])
+def test_full_step_grad_fp32(bptt, reuse, N, extra):
+    """One full training step (rollout, losses, BPTT backward) of the fp32 HIP engine (its default
+    kernels: 16x16x32 CBF / edge backward where they apply) against autograd through the fp32
+    oracle engine: every parameter tensor <= 1e-3 relative norm."""
     from macbf_gnn_amd.engine.oracle_engine import OracleEngine
-    tr = _trainer(bptt=bptt, reuse_nbr_idx=reuse, N=N)
-    s0, g, _ = tr.sample()
-    stats = tr.engine.step(s0, g)
+    tr = _trainer(bptt=bptt, reuse_nbr_idx=reuse, N=N, B=3 if N < 32 else 2, **extra)
+    s0, g, obs = tr.sample()
+    stats = tr.engine.step(s0, g, obs)
     g_hip = tr.fp.grad.clone()
-    stats_o = OracleEngine(tr).step(s0, g)
+    stats_o = OracleEngine(tr).step(s0, g, obs)
     g_ref = tr.fp.grad.clone()
     worst = []
     for m, pn, shape, o, n in tr.fp.specs:
