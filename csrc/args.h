@@ -222,6 +222,7 @@ struct CtrlNodeBwdArgs {
   const uint8_t* valid; long v_env;    // valid[b*v_env] for this step (or null = all valid)
   int B, N;
   const h16* wrm;                     // row-major node images
+  const h16* wrm16;                   // x3: the 16x16x32 kernel's images (layout.node_rm16) -> csrc/node16.h
   int o_w1, o_w2, o_w3, o_w4;          // element offsets (strides 168/72/136/72)
   const float* wvec;                   // controller side vector (eb2|nb2|nb3|nb4)
   float act_coef, dt, sqrt3;

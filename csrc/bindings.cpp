@@ -281,8 +281,9 @@ static mb::CtrlNodeBwdArgs node_bwd_args(NODE_BWD_PARAMS) {
   return a;
 }
 
-static int ctrl_node_bwd(NODE_BWD_PARAMS, u64 stream) {
-  const mb::CtrlNodeBwdArgs a = node_bwd_args(NODE_BWD_ARGS);
+static int ctrl_node_bwd(NODE_BWD_PARAMS, u64 wrm16, u64 stream) {
+  mb::CtrlNodeBwdArgs a = node_bwd_args(NODE_BWD_ARGS);
+  a.wrm16 = P<const h16>(wrm16);      // x3, 128-agent chunks: the 16x16x32 kernel (csrc/node16.h)
   return (prec == 2 ? mb_ctrl_node_bwd_x3 : prec == 1 ? mb_ctrl_node_bwd_f16 : mb_ctrl_node_bwd)(&a, num_blocks, ST(stream));
 }
 

@@ -255,7 +255,9 @@ __global__ __launch_bounds__(C16_NW * 64) void cbf_bwd16_kernel(CbfBwdArgs a) {
     // with this barrier (or at -O1, or with other code at this point) every section matches the
     // 32x32x16 kernel to ~1e-7 and dE matches an fp64 reference. The GPU tests
     // (test_gpu_dedup / test_gpu_fp32 / test_gpu_cbf16) pin it.
+#ifndef CBF16_NO_SCHED_BARRIER
     __builtin_amdgcn_sched_barrier(0);
+#endif
     stamp(0);
     // ---- head backward: dW4 / db4 exact fp32 per lane, dH3pre = w4 * dh . relu'(H3)
     if (g == 0) db4 += dhv;

@@ -819,7 +819,9 @@ DEV void store_tile_add(float* dst, int ncols, int mt, int nt, const f32x16& old
 // its out- and in-edges, one lane swap adds the halves: fixed order, deterministic. All lanes
 // call it (lane swaps); lanes without an agent get zeros. Both halves return G_{t+1}; half 0
 // stores it (the next reverse step's Euler term).
-template <int D>
+// XO: lane distance between the two halves of an agent (32: lane halves h; 16: the g = 0 / 1
+// lanes of the 16x16x32 node kernel)
+template <int D, int XO = 32>
 DEV void fused_combine(const CtrlNodeBwdArgs& a, bool ok, int b, int i, int h, float (&gp)[D], float (&gv)[D]) {
   constexpr int R = REC<D>;
   const int N = a.N, K = a.K;
@@ -842,8 +844,8 @@ DEV void fused_combine(const CtrlNodeBwdArgs& a, bool ok, int b, int i, int h, f
   }
 #pragma unroll
   for (int q = 0; q < R; ++q) {
-    g[q].x += shfl_xor32(g[q].x); g[q].y += shfl_xor32(g[q].y);
-    g[q].z += shfl_xor32(g[q].z); g[q].w += shfl_xor32(g[q].w);
+    g[q].x += lane_xorf<XO>(g[q].x); g[q].y += lane_xorf<XO>(g[q].y);
+    g[q].z += lane_xorf<XO>(g[q].z); g[q].w += lane_xorf<XO>(g[q].w);
   }
   float eg_p[D], eg_v[D];
   if (D == 2) { eg_p[0] = g[0].x; eg_p[1] = g[0].y; eg_v[0] = g[0].z; eg_v[1] = g[0].w; }
@@ -2227,9 +2229,23 @@ size_t bptt_small_lds() { return ctrl_node_bwd_lds() > ctrl_edge_bwd_lds() ? ctr
 }  // namespace MB_PREC
 }  // namespace mb
 
+#if MB_X3
+#include "ctrl16.h"
+#include "node16.h"
+#endif
+
 extern "C" int MB_SYM(ctrl_node_bwd)(const mb::CtrlNodeBwdArgs* a, int num_blocks, hipStream_t st) {
   using namespace mb;
   using namespace mb::MB_PREC;
+  if (a->wrm16) {   // 16x16x32 kernel, two waves per SIMD (x3 build, 128-agent chunks)
+#if MB_X3
+    if (a->dim == 3) launch_ctrl_node_bwd16<3>(*a, num_blocks, st);
+    else launch_ctrl_node_bwd16<2>(*a, num_blocks, st);
+    return (int)hipGetLastError();
+#else
+    return -8;
+#endif
+  }
   const size_t lds = ctrl_node_bwd_lds();
   CtrlNodeBwdArgs b = *a;
   b.coop = node_bwd_coop_enabled() && a->chunk == 32;     // 32-agent chunks: the four waves cooperate
@@ -2241,9 +2257,7 @@ extern "C" int MB_SYM(ctrl_node_bwd)(const mb::CtrlNodeBwdArgs* a, int num_block
   return (int)hipGetLastError();
 }
 
-#if MB_X3
-#include "ctrl16.h"
-#endif
+
 
 extern "C" int MB_SYM(ctrl_edge_bwd)(const mb::CtrlEdgeBwdArgs* a, int num_blocks, hipStream_t st) {
   using namespace mb;

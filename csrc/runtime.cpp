@@ -360,6 +360,9 @@ class BpttDriver {
       throw std::invalid_argument("BpttDriver: the fused step needs 32-agent chunks and one grid");
     gscale_ = c.contains("gscale") ? U("gscale") : 0;   // fp16: device loss scale (or 0)
     ew16_ = c.contains("ctrl_w16") ? U("ctrl_w16") : 0;   // x3, K = 12: 16x16x32 edge backward fragments
+    nw16_ = c.contains("node_rm16") ? U("node_rm16") : 0;  // x3, 128-agent chunks: 16x16x32 node backward images
+    if (nw16_ && (node_chunk_ != 128 || prec_ != 2 || fused_))
+      throw std::invalid_argument("BpttDriver: the 16x16x32 node backward needs x3 and 128-agent chunks");
     if (B_ < 1 || N_ < 1 || Nn_ < N_ || K_ < 1 || K_ > 16 || (D_ != 2 && D_ != 3) || Tmax_ < 1 || nb_node_ < 1 ||
         nb_edge_ < 1)
       throw std::invalid_argument("BpttDriver: bad dimensions");
@@ -416,6 +419,7 @@ class BpttDriver {
         a.dP = P<h16>(dP_); a.dp_env = (long)N_ * prow_; a.ego = P<float4>(ego_); a.partial = P<float>(part_node_);
         a.init = t == T - 1;     // the first step of the reverse loop writes the slabs
         a.chunk = node_chunk_;
+        a.wrm16 = P<const h16>(nw16_);
         a.K = K_;
         if (t < T - 1) {
           // fused BPTT combine: G_{t+1} from step t+1's records (dS, ego, dEc, graph t+1, G_{t+2})
@@ -462,7 +466,7 @@ class BpttDriver {
  private:
   int B_, N_, Nn_, K_, D_, R_, Tmax_, prec_, prow_, nb_node_, nb_edge_, qsplit_, small_ = 0, node_chunk_ = 0, fused_ = 0;
   u64 pooled_, S_, G_, A_, dS_, Gb_, valid_, idx_, argmax_, rptr_, redges_, wrm_, wvec_, act_scale_, dP_, ego_, dEc_;
-  u64 part_node_, part_edge_, wpack_, gscale_ = 0, ew16_ = 0;
+  u64 part_node_, part_edge_, wpack_, gscale_ = 0, ew16_ = 0, nw16_ = 0;
   int o1_, o2_, o3_, o4_, f_ew1f_, f_ew2tn_;
   float dt_, sqrt3_;
 };

@@ -226,6 +226,10 @@ class HipEngine:
         # MACBF_EB16=0: the 32x32x16 kernel (A/B runs)
         self.eb16_w = (self.pw.ctrl_w16 if (self.prec == "fp32" and K == 12
                                             and os.environ.get("MACBF_EB16", "1") != "0") else None)
+        # x3, 128-agent node chunks: the 16x16x32 node backward (csrc/node16.h, two waves per SIMD);
+        # MACBF_NODE16=0: the 32x32x16 kernel (A/B runs)
+        self.node16_w = (self.pw.node_rm16 if (self.prec == "fp32" and os.environ.get("MACBF_NODE16", "1") != "0")
+                         else None)
         self.host_dist = torch.zeros(T, B, dtype=torch.int64, pin_memory=True)
         self.copy_stream = torch.cuda.Stream(device=dev)
         self.aux = torch.cuda.Stream(device=dev)      # reverse-CSR build overlaps the CBF kernel
@@ -624,7 +628,8 @@ class HipEngine:
             native.ctrl_node_bwd(self.pooled[:T].view(TB, N, self.prow), self.S[:T].view(TB, Nn, W), Gr[:TB],
                                  self.A[:T].view(TB, N, D), self.dS[1: T + 1].view(TB, N, W), valid_u8.view(TB),
                                  pw.ctrl_rm, pw.node_rm_off, pw.ctrl_v, gs * ACT_COEF, dP[:TB], None, pn, nb_n,
-                                 act_cnt=self.counts[2:3], prec=self.prec, init=True, gscale=gsd)
+                                 act_cnt=self.counts[2:3], prec=self.prec, init=True, gscale=gsd,
+                                 wrm16=self._node16(TB * N))
             native.ctrl_edge_bwd(self.S[:T].view(TB, Nn, W), self.idx[:T].view(TB, N, K), self.argmax[:T].view(TB, N, 128),
                                  dP[:TB], pw.ctrl_w, pw.ctrl_off["ew1f"], pw.ctrl_off["ew2tn"], None, pe, nb_e, prec=self.prec,
                                  init=True)
@@ -691,6 +696,7 @@ class HipEngine:
                 node_chunk=int(native.node_bwd_chunk(B * N, self.dev)),
                 fused_step=int(native.bwd_step_fused(B * N, self.dev)),
                 ctrl_w16=native.ptr(self.eb16_w) if self.eb16_w is not None else 0,
+                node_rm16=native.ptr(self._node16(B * N)),
                 gscale=native.ptr(getattr(self.tr, "gscale_dev", None))))
             self._bdrv = native.lib().BpttDriver(c)
         return self._bdrv
@@ -719,8 +725,15 @@ class HipEngine:
             if nbn == nbe and native.bwd_step_fused(self.G[sl].shape[0] * self.N, self.dev):
                 native.ctrl_bwd_step(node, edge, nbn)            # node + edge backward: one launch
             else:
-                native.ctrl_node_bwd(**node, num_blocks=nbn)
+                native.ctrl_node_bwd(**node, num_blocks=nbn, wrm16=self._node16(self.G[sl].shape[0] * self.N))
                 native.ctrl_edge_bwd(**edge, num_blocks=nbe, w16=self.eb16_w)
+
+    def _node16(self, total_agents):
+        """The 16x16x32 node-backward images when a launch over `total_agents` agents takes the
+        128-agent chunks that kernel runs (else None: the 32x32x16 / cooperative kernels)."""
+        if self.node16_w is None or native.node_bwd_chunk(total_agents, self.dev) != 128:
+            return None
+        return self.node16_w
 
     def _counts_ready(self, work):
         """Join the (async) count all-reduce (the node backward reads the action-loss count

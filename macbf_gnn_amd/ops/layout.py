@@ -538,6 +538,36 @@ def cbf_rm16(fp_offsets, dim: int = 2) -> RMPacker:
     return p
 
 
+NODE16_STRIDES = {"w1": 176, "w2": 80, "w3": 144, "w4": 80}    # csrc/node16.h N16_S1..S4 (bank model)
+
+
+def node_rm16(fp_offsets, dim: int = 2) -> RMPacker:
+    """Row-major node-MLP images for the 16x16x32 x3 node backward (csrc/node16.h): W1f (64 x 160,
+    the layer-1 slots of ctrl_node_slot in natural order: its forward B operand is the pooled row),
+    W2 (128x64), W3 (64x128) and W4 (16 x 64: rows >= 2D zero), the last three column-permuted
+    (perm32_logical: their forward B operands are packed C-tile pairs). A = W is one 16-byte read
+    per lane, A = W^T two ds_read_b64_tr_b16."""
+    nW1, nb1 = fp_offsets["controller_dec_net.0.weight"], fp_offsets["controller_dec_net.0.bias"]
+    nW2 = fp_offsets["controller_dec_net.2.weight"]
+    nW3 = fp_offsets["controller_dec_net.4.weight"]
+    nW4 = fp_offsets["controller_dec_net.6.weight"]
+    n_in = 128 + 2 * dim
+
+    def w1f(o, k):
+        sl = ctrl_node_slot(k, dim)
+        if sl is None:
+            return ZERO
+        return nb1 + o if sl[0] == "b" else nW1 + o * n_in + sl[1]
+
+    m2, m3, m4 = _mat(nW2, 128, 64), _mat(nW3, 64, 128), _mat(nW4, 2 * dim, 64)
+    p = RMPacker()
+    p.add("w1", w1f, 64, 160, NODE16_STRIDES["w1"])
+    p.add("w2", lambda r, c: m2(r, perm32_logical(c)), 128, 64, NODE16_STRIDES["w2"])
+    p.add("w3", lambda r, c: m3(r, perm32_logical(c)), 64, 128, NODE16_STRIDES["w3"])
+    p.add("w4", lambda r, c: m4(r, perm32_logical(c)) if r < 2 * dim else ZERO, 16, 64, NODE16_STRIDES["w4"])
+    return p
+
+
 def pack_frags16(vm: Callable[[int, int], int], mtiles: int, ksteps: int, kind: str) -> np.ndarray:
     """16x32 A fragments: element j of lane (n, g) at K-step s is vm(16mt + n, k) with
     k = 32s + 8g + j ("nat") or 32s + kacc16(g, j) ("acc"). 64 lanes x 8 per fragment."""

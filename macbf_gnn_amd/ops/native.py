@@ -805,8 +805,12 @@ def ctrl_bwd_grids(total_agents: int, device, prec=None):
     return max(1, min(ch, cu)), max(1, min(che * ctrl_edge_qsplit(total_agents, device), per_cu * cu))
 
 
+NODE16_RM = 2 * (64 * 176 + 128 * 80 + 64 * 144 + 16 * 80)    # csrc/node16.h: both planes (layout.node_rm16)
+
+
 def ctrl_node_bwd(pooled, S, G, A, Gn, valid_t, wrm, offs, wvec, act_coef, dP, ego, partial, num_blocks,
-                  act_cnt=None, prec=None, init=False, chunk=None, gscale=None, combine=None, stamps=None, _defer=False):
+                  act_cnt=None, prec=None, init=False, chunk=None, gscale=None, combine=None, stamps=None, _defer=False,
+                  wrm16=None):
     """act_cnt: optional 1-element device tensor holding the (all-reduced) action-loss count
     n_act; the action-loss coefficient is then act_coef / max(n_act, 1), read by the kernel (no
     host round trip, no extra launch). init: write the weight-gradient slabs instead of
@@ -860,7 +864,12 @@ def ctrl_node_bwd(pooled, S, G, A, Gn, valid_t, wrm, offs, wvec, act_coef, dP, e
             int(chunk or node_bwd_chunk(B * N, S.device)), ptr(gscale), cmb, ptr(stamps))
     if _defer:
         return args
-    _ok(lib().ctrl_node_bwd(*args, stream_handle()), "ctrl_node_bwd")
+    if wrm16 is not None:
+        # 16x16x32 kernel (csrc/node16.h): x3, 128-agent chunks (eight 16-agent waves)
+        if f16 != 2 or args[-4] != 128:
+            raise NativeError("16x16x32 node backward: fp32 (x3) precision and 128-agent chunks only")
+        check(wrm16, wrm.dtype, (NODE16_RM,), "wrm16")
+    _ok(lib().ctrl_node_bwd(*args, ptr(wrm16), stream_handle()), "ctrl_node_bwd")
 
 
 def ctrl_edge_bwd(S, idx, argmax, dP, wpack, f_ew1f, f_ew2tn, dEc, partial, num_blocks, prec=None, init=False,
