@@ -95,9 +95,19 @@ __global__ __launch_bounds__(N16_NW * 64) void ctrl_node_bwd16_kernel(CtrlNodeBw
   h16* W1 = reinterpret_cast<h16*>(smem);
   float* vl = reinterpret_cast<float*>(smem + (size_t)2 * N16_RM * 2);
   h16* stg = reinterpret_cast<h16*>(smem + (size_t)2 * N16_RM * 2 + N16_VEC * 4);
+  // diagnostics: shader clock at the phase boundaries (a.stamps, normally null; [workgroup][wave][16],
+  // a workgroup with several chunks keeps its last chunk's clocks; scripts/stamps_node.py --node16)
+  auto stamp = [&](int k) {
+    if (a.stamps) {
+      const unsigned long long t = __builtin_amdgcn_s_memtime();
+      if ((threadIdx.x & 63) == 0) a.stamps[((long)blockIdx.x * N16_NW + threadIdx.x / WAVE) * 16 + k] = t;
+    }
+  };
+  stamp(0);
   block_copy16(W1, a.wrm16, 2 * N16_RM * 2);
   block_copy16(vl, a.wvec + 128, N16_VEC * 4);
   __syncthreads();
+  stamp(1);
   const float* nb2 = vl;
   const float* nb3 = vl + 128;
   const float* nb4 = vl + 192;
@@ -131,6 +141,7 @@ __global__ __launch_bounds__(N16_NW * 64) void ctrl_node_bwd16_kernel(CtrlNodeBw
   const int myturn = wave >> 1;
 
   for (long chunk = blockIdx.x; chunk < nchunks; chunk += gridDim.x) {
+    stamp(15);
     const int ga = (int)(chunk * N16_CH) + wave * 16 + n;
     const bool ok = ga < total;
     // stage turns holding at least one valid agent (a partial chunk skips its empty turns)
@@ -162,6 +173,7 @@ __global__ __launch_bounds__(N16_NW * 64) void ctrl_node_bwd16_kernel(CtrlNodeBw
     // as the 2-lane combine of the other node kernels (same terms, same order: bit-identical);
     // lanes g >= 2 join the lane exchange with zeros
     if (a.cdS) fused_combine<D, 16>(a, ok && g < 2, b, i, g & 1, gnp, gnv);
+    stamp(2);
     float ex[D];
 #pragma unroll
     for (int q = 0; q < D; ++q) ex[q] = sp[q] - gg[q];
@@ -194,6 +206,7 @@ __global__ __launch_bounds__(N16_NW * 64) void ctrl_node_bwd16_kernel(CtrlNodeBw
     f32x4 y4 = bias4n(nb4, 0, g);
 #pragma unroll
     for (int s = 0; s < 2; ++s) y4 = mma16(n16_w(W4, N16_S4, 0, s, lane), pk4_fr(Y3[2 * s], Y3[2 * s + 1]), y4);
+    stamp(3);
     // ---- gain law + action-loss backward on the g = 0 lane of each agent (rows 0..3 of y4 are its
     //      regs, rows 4..7 the regs of lane g = 1)
     float y4r[8];
@@ -250,6 +263,7 @@ __global__ __launch_bounds__(N16_NW * 64) void ctrl_node_bwd16_kernel(CtrlNodeBw
       dY3[mt] = to_pk4(c);
       mask_pk4(dY3[mt], Y3[mt]);
     }
+    stamp(4);
     // ---- stage 1: dW3 += dY3 . Y2^T, db3; dW4 += d4 . Y3^T, db4
 #pragma unroll 1
     for (int turn = 0; turn < nturn; ++turn) {
@@ -278,6 +292,7 @@ __global__ __launch_bounds__(N16_NW * 64) void ctrl_node_bwd16_kernel(CtrlNodeBw
       }
       __syncthreads();
     }
+    stamp(5);
     // ---- dY2 = W3^T dY3 . relu'(Y2); dY1 = W2^T dY2 . relu'(Y1)
     Pk4 dY2[8], dY1[4];
 #pragma unroll
@@ -296,6 +311,7 @@ __global__ __launch_bounds__(N16_NW * 64) void ctrl_node_bwd16_kernel(CtrlNodeBw
       dY1[mt] = to_pk4(c);
       mask_pk4(dY1[mt], Y1[mt]);
     }
+    stamp(6);
     // ---- stage 2: dW2 += dY2 . Y1^T, db2
 #pragma unroll 1
     for (int turn = 0; turn < nturn; ++turn) {
@@ -314,6 +330,7 @@ __global__ __launch_bounds__(N16_NW * 64) void ctrl_node_bwd16_kernel(CtrlNodeBw
       }
       __syncthreads();
     }
+    stamp(7);
     // ---- [dL/dpooled; d/ds] = W1^T dY1: tiles 0..7 -> dP rows (hi | lo), tile 8 -> ego terms
 #pragma unroll
     for (int mt = 0; mt < 9; ++mt) {
@@ -340,6 +357,7 @@ __global__ __launch_bounds__(N16_NW * 64) void ctrl_node_bwd16_kernel(CtrlNodeBw
         }
       }
     }
+    stamp(8);
     // ---- stage 3: dW1f += dY1 . [P | s]^T (P re-read: L2-hot)
 #pragma unroll 1
     for (int turn = 0; turn < nturn; ++turn) {
@@ -371,7 +389,9 @@ __global__ __launch_bounds__(N16_NW * 64) void ctrl_node_bwd16_kernel(CtrlNodeBw
       }
       __syncthreads();
     }
+    stamp(9);
   }
+  stamp(13);
   // ---- slab (same layout as node_bwd_body: NP_W1 64x160, NP_W2 128x64, NP_B2, NP_W3 64x128,
   //      NP_B3, NP_W4 32x64, NP_B4); every owned element is read first, then added and stored
   float* P = a.partial + (long)blockIdx.x * CTRL_NODE_PARTIAL;
@@ -430,6 +450,8 @@ __global__ __launch_bounds__(N16_NW * 64) void ctrl_node_bwd16_kernel(CtrlNodeBw
     for (int q = threadIdx.x; q < 16 * 64; q += blockDim.x) P[NP_W4 + 16 * 64 + q] = 0.f;
     if (threadIdx.x < 16) P[NP_B4 + 16 + threadIdx.x] = 0.f;
   }
+  if (a.stamps) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  stamp(14);                                           // slab stores complete
 }
 
 template <int D>

@@ -836,7 +836,7 @@ def ctrl_node_bwd(pooled, S, G, A, Gn, valid_t, wrm, offs, wvec, act_coef, dP, e
     check(partial, torch.float32, (num_blocks, CTRL_NODE_PARTIAL), "partial")
     check(act_cnt, torch.float32, (1,), "act_cnt")
     check(gscale, torch.float32, (1,), "gscale")
-    check(stamps, torch.int64, (num_blocks, 4, 16), "stamps")
+    check(stamps, torch.int64, (num_blocks, 8 if wrm16 is not None else 4, 16), "stamps")
     cmb = ()
     if combine is not None:
         # fused BPTT combine: Gn is formed in the kernel from step t+1's records (node_combine's terms)
