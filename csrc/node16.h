@@ -37,6 +37,10 @@ constexpr int N16_PL = N16_RT * N16_SW;                   // lo-plane offset of 
 //                 3: [dY1 0..63 | P 64..191 | s 192..207 | 0 208..223]
 constexpr int N16_C_D4 = 64, N16_C_Y3 = 80, N16_C_Y2 = 144, N16_C_Y1 = 128, N16_C_P = 64, N16_C_S = 192;
 constexpr size_t N16_LDS = (size_t)2 * N16_RM * 2 + N16_VEC * 4 + (size_t)2 * N16_PL * 2;
+// tile-major slab (floats): 32 dW2 tiles | 32 dW3 tiles | 8 x 5 dW1f tile slots | 4 dW4 tiles | b2 | b3 | b4
+constexpr int N16_SL_W2 = 0, N16_SL_W3 = 32 * 256, N16_SL_W1 = 64 * 256, N16_SL_W4 = 104 * 256;
+constexpr int N16_SL_B2 = 108 * 256, N16_SL_B3 = N16_SL_B2 + 128, N16_SL_B4 = N16_SL_B3 + 64;
+static_assert(N16_SL_B4 + 16 <= CTRL_NODE_PARTIAL, "slab row");
 static_assert(N16_LDS <= 160 * 1024, "LDS budget");
 static_assert(N16_C_S + 32 <= N16_SW && N16_C_Y2 + 128 <= N16_SW, "stage columns");
 
@@ -312,6 +316,14 @@ __global__ __launch_bounds__(N16_NW * 64) void ctrl_node_bwd16_kernel(CtrlNodeBw
       mask_pk4(dY1[mt], Y1[mt]);
     }
     stamp(6);
+    // the pooled rows for stage 3, requested now: their latency hides behind stage 2 (issued after
+    // every store of this chunk so far, they wait for nothing else)
+    h16x8 Ph[4], Pl[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      Ph[s] = ok ? *reinterpret_cast<const h16x8*>(prow + 32 * s + 8 * g) : zero_h8();
+      Pl[s] = ok ? *reinterpret_cast<const h16x8*>(prow + 128 + 32 * s + 8 * g) : zero_h8();
+    }
     // ---- stage 2: dW2 += dY2 . Y1^T, db2
 #pragma unroll 1
     for (int turn = 0; turn < nturn; ++turn) {
@@ -331,6 +343,36 @@ __global__ __launch_bounds__(N16_NW * 64) void ctrl_node_bwd16_kernel(CtrlNodeBw
       __syncthreads();
     }
     stamp(7);
+    // ---- stage 3: dW1f += dY1 . [P | s]^T (P: the rows requested before stage 2)
+#pragma unroll 1
+    for (int turn = 0; turn < nturn; ++turn) {
+      if (myturn == turn) {
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) store4(stg, N16_SW, N16_PL, trow, mt, g, dY1[mt]);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          *reinterpret_cast<h16x8*>(stg + trow * N16_SW + N16_C_P + 32 * s + 8 * g) = Ph[s];
+          *reinterpret_cast<h16x8*>(stg + N16_PL + trow * N16_SW + N16_C_P + 32 * s + 8 * g) = Pl[s];
+        }
+        if (g < 2) {      // the state fragment is exact: zero lo plane
+          *reinterpret_cast<h16x8*>(stg + trow * N16_SW + N16_C_S + 8 * g) = sfr;
+          *reinterpret_cast<h16x8*>(stg + N16_PL + trow * N16_SW + N16_C_S + 8 * g) = zero_h8();
+        }
+      }
+      __syncthreads();
+      {
+        const Fr A = tr16_fr(stg, N16_SW, N16_PL, 0, 16 * m1, lane);
+#pragma unroll
+        for (int v = 0; v < 5; ++v) {
+          if (v < nv1) {
+            const int nt = n1 + 2 * v;
+            acc1[v] = mma16(A, tr16_fr(stg + N16_C_P, N16_SW, N16_PL, 0, 16 * nt, lane), acc1[v]);
+          }
+        }
+      }
+      __syncthreads();
+    }
+    stamp(8);
     // ---- [dL/dpooled; d/ds] = W1^T dY1: tiles 0..7 -> dP rows (hi | lo), tile 8 -> ego terms
 #pragma unroll
     for (int mt = 0; mt < 9; ++mt) {
@@ -357,98 +399,53 @@ __global__ __launch_bounds__(N16_NW * 64) void ctrl_node_bwd16_kernel(CtrlNodeBw
         }
       }
     }
-    stamp(8);
-    // ---- stage 3: dW1f += dY1 . [P | s]^T (P re-read: L2-hot)
-#pragma unroll 1
-    for (int turn = 0; turn < nturn; ++turn) {
-      if (myturn == turn) {
-#pragma unroll
-        for (int mt = 0; mt < 4; ++mt) store4(stg, N16_SW, N16_PL, trow, mt, g, dY1[mt]);
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-          const h16x8 ph = ok ? *reinterpret_cast<const h16x8*>(prow + 32 * s + 8 * g) : zero_h8();
-          const h16x8 pl = ok ? *reinterpret_cast<const h16x8*>(prow + 128 + 32 * s + 8 * g) : zero_h8();
-          *reinterpret_cast<h16x8*>(stg + trow * N16_SW + N16_C_P + 32 * s + 8 * g) = ph;
-          *reinterpret_cast<h16x8*>(stg + N16_PL + trow * N16_SW + N16_C_P + 32 * s + 8 * g) = pl;
-        }
-        if (g < 2) {      // the state fragment is exact: zero lo plane
-          *reinterpret_cast<h16x8*>(stg + trow * N16_SW + N16_C_S + 8 * g) = sfr;
-          *reinterpret_cast<h16x8*>(stg + N16_PL + trow * N16_SW + N16_C_S + 8 * g) = zero_h8();
-        }
-      }
-      __syncthreads();
-      {
-        const Fr A = tr16_fr(stg, N16_SW, N16_PL, 0, 16 * m1, lane);
-#pragma unroll
-        for (int v = 0; v < 5; ++v) {
-          if (v < nv1) {
-            const int nt = n1 + 2 * v;
-            acc1[v] = mma16(A, tr16_fr(stg + N16_C_P, N16_SW, N16_PL, 0, 16 * nt, lane), acc1[v]);
-          }
-        }
-      }
-      __syncthreads();
-    }
     stamp(9);
   }
   stamp(13);
-  // ---- slab (same layout as node_bwd_body: NP_W1 64x160, NP_W2 128x64, NP_B2, NP_W3 64x128,
-  //      NP_B3, NP_W4 32x64, NP_B4); every owned element is read first, then added and stored
+  // ---- slab: TILE-MAJOR (layout.ctrl_node16_grad_map): every owned 16x16 tile is 64 lanes x 4
+  //      floats, one 16-byte load + store per lane (the row-major layout of the other node kernels
+  //      costs 4 scattered 64-byte segments per wave instruction: 22 k cycles of a 170 k call).
+  //      Owned elements are read first, then added and stored; the first BPTT step writes.
+  //      [dW2: wave x 4 tiles | dW3: wave x 4 | dW1f: wave x 5 slots | dW4: waves 0..3 | biases]
+  float4* P4 = reinterpret_cast<float4*>(a.partial + (long)blockIdx.x * CTRL_NODE_PARTIAL);
   float* P = a.partial + (long)blockIdx.x * CTRL_NODE_PARTIAL;
   const bool accum = !a.init;
-  float o2[4][4], o3[4][4], o1[5][4], o4[4];
+  const int t2 = N16_SL_W2 / 256 + wave * 4, t3 = N16_SL_W3 / 256 + wave * 4, t1 = N16_SL_W1 / 256 + wave * 5;
+  float4 o2[4], o3[4], o1[5], o4 = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-  for (int u = 0; u < 4; ++u)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      o2[u][q] = accum ? P[NP_W2 + (16 * wave + 4 * g + q) * 64 + 16 * u + n] : 0.f;
-      o3[u][q] = accum ? P[NP_W3 + (16 * m3 + 4 * g + q) * 128 + 16 * (n3 + u) + n] : 0.f;
-    }
-#pragma unroll
-  for (int v = 0; v < 5; ++v)
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-      o1[v][q] = (accum && v < nv1) ? P[NP_W1 + (16 * m1 + 4 * g + q) * 160 + 16 * (n1 + 2 * v) + n] : 0.f;
-#pragma unroll
-  for (int q = 0; q < 4; ++q) o4[q] = (accum && wave < 4) ? P[NP_W4 + (4 * g + q) * 64 + 16 * wave + n] : 0.f;
-#pragma unroll
-  for (int u = 0; u < 4; ++u)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      P[NP_W2 + (16 * wave + 4 * g + q) * 64 + 16 * u + n] = o2[u][q] + acc2[u][q];
-      P[NP_W3 + (16 * m3 + 4 * g + q) * 128 + 16 * (n3 + u) + n] = o3[u][q] + acc3[u][q];
-    }
-#pragma unroll
-  for (int v = 0; v < 5; ++v)
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-      if (v < nv1) P[NP_W1 + (16 * m1 + 4 * g + q) * 160 + 16 * (n1 + 2 * v) + n] = o1[v][q] + acc1[v][q];
-  if (wave < 4) {
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      // dW4pad rows 0..15 of the 32-row slab tile (rows 16..31 stay as written by init: zero)
-      P[NP_W4 + (4 * g + q) * 64 + 16 * wave + n] = o4[q] + acc4[q];
-    }
+  for (int u = 0; u < 4; ++u) {
+    o2[u] = accum ? P4[(t2 + u) * 64 + lane] : make_float4(0.f, 0.f, 0.f, 0.f);
+    o3[u] = accum ? P4[(t3 + u) * 64 + lane] : make_float4(0.f, 0.f, 0.f, 0.f);
   }
+#pragma unroll
+  for (int v = 0; v < 5; ++v) o1[v] = (accum && v < nv1) ? P4[(t1 + v) * 64 + lane] : make_float4(0.f, 0.f, 0.f, 0.f);
+  if (accum && wave < 4) o4 = P4[(N16_SL_W4 / 256 + wave) * 64 + lane];
+  float ob[3] = {0.f, 0.f, 0.f};          // bias rows (n == 0 lanes): b2 | b3 | b4, 4 per lane
+  auto add4 = [](const float4& o, const f32x4& c) { return make_float4(o.x + c[0], o.y + c[1], o.z + c[2], o.w + c[3]); };
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    P4[(t2 + u) * 64 + lane] = add4(o2[u], acc2[u]);
+    P4[(t3 + u) * 64 + lane] = add4(o3[u], acc3[u]);
+  }
+#pragma unroll
+  for (int v = 0; v < 5; ++v)
+    if (v < nv1) P4[(t1 + v) * 64 + lane] = add4(o1[v], acc1[v]);
+  if (wave < 4) P4[(N16_SL_W4 / 256 + wave) * 64 + lane] = add4(o4, acc4);
+  (void)ob;
   if (n == 0) {     // bias rows: column 0 of the ones products (every column holds the row sum)
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int r2 = 16 * wave + 4 * g + q;
-      P[NP_B2 + r2] = (accum ? P[NP_B2 + r2] : 0.f) + bias2[q];
+      P[N16_SL_B2 + r2] = (accum ? P[N16_SL_B2 + r2] : 0.f) + bias2[q];
       if (wave < 4) {
         const int r3 = 16 * m3 + 4 * g + q;
-        P[NP_B3 + r3] = (accum ? P[NP_B3 + r3] : 0.f) + bias3[q];
+        P[N16_SL_B3 + r3] = (accum ? P[N16_SL_B3 + r3] : 0.f) + bias3[q];
       }
       if (wave == 0) {
         const int r4 = 4 * g + q;
-        P[NP_B4 + r4] = (accum ? P[NP_B4 + r4] : 0.f) + bias4_[q];
+        P[N16_SL_B4 + r4] = (accum ? P[N16_SL_B4 + r4] : 0.f) + bias4_[q];
       }
     }
-  }
-  if (!accum) {   // first BPTT step: the slab parts no tile of this kernel owns are written as zeros
-    for (int q = threadIdx.x; q < 64 * 16; q += blockDim.x) P[NP_W1 + (q >> 4) * 160 + 144 + (q & 15)] = 0.f;
-    for (int q = threadIdx.x; q < 16 * 64; q += blockDim.x) P[NP_W4 + 16 * 64 + q] = 0.f;
-    if (threadIdx.x < 16) P[NP_B4 + 16 + threadIdx.x] = 0.f;
   }
   if (a.stamps) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   stamp(14);                                           // slab stores complete

@@ -108,12 +108,13 @@ class HipEngine:
         self.prow = L.pooled_row(self.prec)      # pooled / dL/dpooled row: [hi | lo] for fp32
         offs = {pn: o for (m, pn, shape, o, n) in trainer.fp.specs}
         self._alloc()
+        node_map = L.ctrl_node16_grad_map if self.node16_w is not None else L.ctrl_node_grad_map
         # flat-gradient assembly: CSR (by parameter) over the concatenated reduced slabs
         # [cbf | node | edge]; one gather launch per iteration (deterministic)
         import numpy as np
         srcs, dsts, base = [], [], 0
         for name, fn, width in (("cbf", L.cbf_grad_map, native.CBF_PARTIAL),
-                                ("node", L.ctrl_node_grad_map, native.CTRL_NODE_PARTIAL),
+                                ("node", node_map, native.CTRL_NODE_PARTIAL),
                                 ("edge", L.ctrl_edge_grad_map, native.CTRL_EDGE_PARTIAL)):
             sm, dm = fn(offs, self.D)
             sm, dm = np.asarray(sm, dtype=np.int64), np.asarray(dm, dtype=np.int64)
@@ -227,9 +228,13 @@ class HipEngine:
         self.eb16_w = (self.pw.ctrl_w16 if (self.prec == "fp32" and K == 12
                                             and os.environ.get("MACBF_EB16", "1") != "0") else None)
         # x3, 128-agent node chunks: the 16x16x32 node backward (csrc/node16.h, two waves per SIMD);
-        # MACBF_NODE16=0: the 32x32x16 kernel (A/B runs)
-        self.node16_w = (self.pw.node_rm16 if (self.prec == "fp32" and os.environ.get("MACBF_NODE16", "1") != "0")
-                         else None)
+        # MACBF_NODE16=0: the 32x32x16 kernel (A/B runs). Decided once per engine (its slab layout
+        # differs, layout.ctrl_node16_grad_map): the BPTT launches cover (B / groups) x N agents,
+        # the no-BPTT launch T x B x N >= that, so every node launch of this engine takes the same kernel
+        Gp = self.bptt_groups
+        self.node16_w = (self.pw.node_rm16 if (self.prec == "fp32" and os.environ.get("MACBF_NODE16", "1") != "0"
+                                               and native.node_bwd_chunk((B // Gp) * N, dev) == 128
+                                               and not self.small_bptt) else None)
         self.host_dist = torch.zeros(T, B, dtype=torch.int64, pin_memory=True)
         self.copy_stream = torch.cuda.Stream(device=dev)
         self.aux = torch.cuda.Stream(device=dev)      # reverse-CSR build overlaps the CBF kernel
@@ -729,10 +734,10 @@ class HipEngine:
                 native.ctrl_edge_bwd(**edge, num_blocks=nbe, w16=self.eb16_w)
 
     def _node16(self, total_agents):
-        """The 16x16x32 node-backward images when a launch over `total_agents` agents takes the
-        128-agent chunks that kernel runs (else None: the 32x32x16 / cooperative kernels)."""
-        if self.node16_w is None or native.node_bwd_chunk(total_agents, self.dev) != 128:
-            return None
+        """The 16x16x32 node-backward images if this engine runs that kernel (a launch over
+        total_agents >= (B / groups) x N agents then takes 128-agent chunks too)."""
+        if self.node16_w is not None and native.node_bwd_chunk(total_agents, self.dev) != 128:
+            raise native.NativeError("16x16x32 node backward: a launch without 128-agent chunks")
         return self.node16_w
 
     def _counts_ready(self, work):

@@ -472,6 +472,50 @@ def ctrl_node_grad_map(fp_offsets, dim: int = 2):
     return np.asarray(S, np.int64), np.asarray(D, np.int64)
 
 
+def ctrl_node16_grad_map(fp_offsets, dim: int = 2):
+    """Slab -> flat grad pairs of the 16x16x32 node backward (csrc/node16.h, tile-major slab):
+    a 16x16 tile (M, N) is 64 lanes x 4 floats, lane l = (n = l & 15, g = l >> 4), float q ->
+    row 16M + 4g + q, column 16N + n. Wave w owns dW2 tiles (w, u < 4), dW3 tiles (w & 3, 4(w >> 2) + u),
+    dW1f slots v < 5 -> tile (w & 3, (w >> 2) + 2v) for tile columns < 9, dW4 tile (0, w) for w < 4;
+    then the bias rows b2 (128), b3 (64), b4 (16)."""
+    nW1, nb1 = fp_offsets["controller_dec_net.0.weight"], fp_offsets["controller_dec_net.0.bias"]
+    nW2, nb2 = fp_offsets["controller_dec_net.2.weight"], fp_offsets["controller_dec_net.2.bias"]
+    nW3, nb3 = fp_offsets["controller_dec_net.4.weight"], fp_offsets["controller_dec_net.4.bias"]
+    nW4, nb4 = fp_offsets["controller_dec_net.6.weight"], fp_offsets["controller_dec_net.6.bias"]
+    n_in = 128 + 2 * dim
+    S, D = [], []
+
+    def tile(base, M, Nt, dst):
+        for lane in range(64):
+            n, g = lane & 15, lane >> 4
+            for q in range(4):
+                d = dst(16 * M + 4 * g + q, 16 * Nt + n)
+                if d is not None:
+                    S.append(base + lane * 4 + q)
+                    D.append(d)
+
+    for w in range(8):
+        for u in range(4):
+            tile((w * 4 + u) * 256, w, u, lambda r, c: nW2 + r * 64 + c)
+            tile((32 + w * 4 + u) * 256, w & 3, 4 * (w >> 2) + u, lambda r, c: nW3 + r * 128 + c)
+        for v in range(5):
+            nt = (w >> 2) + 2 * v
+            if nt < 9:
+                def w1(r, c):
+                    sl = ctrl_node_slot(c, dim)
+                    if sl is None:
+                        return None
+                    return nb1 + r if sl[0] == "b" else nW1 + r * n_in + sl[1]
+                tile((64 + w * 5 + v) * 256, w & 3, nt, w1)
+        if w < 4:
+            tile((104 + w) * 256, 0, w, lambda r, c: nW4 + r * 64 + c if r < 2 * dim else None)
+    b2 = 108 * 256
+    S += [b2 + m for m in range(128)]; D += [nb2 + m for m in range(128)]
+    S += [b2 + 128 + m for m in range(64)]; D += [nb3 + m for m in range(64)]
+    S += [b2 + 192 + m for m in range(2 * dim)]; D += [nb4 + m for m in range(2 * dim)]
+    return np.asarray(S, np.int64), np.asarray(D, np.int64)
+
+
 def ctrl_edge_grad_map(fp_offsets, dim: int = 2):
     eW1, eb1 = fp_offsets["controller_centr_net.0.weight"], fp_offsets["controller_centr_net.0.bias"]
     eW2, eb2 = fp_offsets["controller_centr_net.2.weight"], fp_offsets["controller_centr_net.2.bias"]

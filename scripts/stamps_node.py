@@ -14,8 +14,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 PHASES = ["start", "weights", "loads", "L1", "L2", "L3", "L4+gain", "dY3", "S4/S3+dY2", "S2+dY1",
           "S1 stage", "S1", "dP", "chunk end", "slab"]
-PHASES16 = ["start", "weights", "loads+combine", "forward", "gain+dY3", "stage1", "dY2+dY1", "stage2", "dP",
-            "stage3", "-", "-", "-", "chunk end", "slab"]
+PHASES16 = ["start", "weights", "loads+combine", "forward", "gain+dY3", "stage1", "dY2+dY1", "stage2", "stage3",
+            "dP", "-", "-", "-", "chunk end", "slab"]
 
 
 def main():

@@ -111,8 +111,11 @@ def _capture_cbf(monkeypatch, **cfg):
         return orig(*a, **k)
 
     monkeypatch.setattr(native, "cbf_bwd", spy)
+    flat0 = tr.fp.flat.clone()
     tr.train_step()
     torch.cuda.synchronize()
+    tr.fp.flat.copy_(flat0)          # the weights of the captured call
+    tr.engine.after_update()
     return tr, orig, cap["a"], cap["k"]
 
 
@@ -202,9 +205,14 @@ def _capture_edge(monkeypatch, **cfg):
         return orig(*a, **k)
 
     monkeypatch.setattr(native, "ctrl_edge_bwd", spy)
+    flat0 = tr.fp.flat.clone()
     tr.train_step()
     torch.cuda.synchronize()
     assert cap, "no 16x16x32 edge backward call"
+    # back to the weights the rollout ran with: the saved argmax slots are the max-pool of THAT
+    # forward (the backward routes dL/dpooled through them assuming a positive pre-activation)
+    tr.fp.flat.copy_(flat0)
+    tr.engine.after_update()
     return tr, orig, cap[len(cap) // 2]
 
 
