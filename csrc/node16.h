@@ -138,9 +138,6 @@ __global__ __launch_bounds__(N16_NW * 64) void ctrl_node_bwd16_kernel(CtrlNodeBw
 #pragma unroll
   for (int u = 0; u < 5; ++u) acc1[u] = zero4();
 
-  const h16* W2 = W1 + N16_O2;
-  const h16* W3 = W1 + N16_O3;
-  const h16* W4 = W1 + N16_O4;
   const int trow = (wave & 1) * 16 + n;        // this wave's rows inside its turn
   const int myturn = wave >> 1;
 
@@ -182,7 +179,12 @@ __global__ __launch_bounds__(N16_NW * 64) void ctrl_node_bwd16_kernel(CtrlNodeBw
 #pragma unroll
     for (int q = 0; q < D; ++q) ex[q] = sp[q] - gg[q];
     const h16x8 sfr = g < 2 ? node_state_frag<D>(ex, sv, ok, g) : zero_h8();
+    // opaque bases: every weight fragment is re-read from LDS per chunk (loop-invariant loads
+    // hoisted out of the chunk loop would pin registers and spill)
     const h16* W1c = W1 + opaque_zero();
+    const h16* W2 = W1c + N16_O2;
+    const h16* W3 = W1c + N16_O3;
+    const h16* W4 = W1c + N16_O4;
     // ---- forward recompute
     Pk4 Y1[4], Y2[8], Y3[4];
 #pragma unroll
