@@ -404,6 +404,5 @@ int mb_stats_pack(const float* sums, const float* counts, const float* local, fl
 int mb_probe_mfma16(const void* a, const void* b, float* d, hipStream_t st);
 int mb_probe_mfma(const void* a, const void* b, float* d, hipStream_t st);
 int mb_probe_lane_xor(const unsigned* in, unsigned* out, hipStream_t st);
-int mb_probe_smfmac(const void* a, const void* b, const int* idx, float* d, hipStream_t st);
 int mb_probe_tr(const void* img, int rows, int stride, int e0, int m0, void* out, hipStream_t st);
 }

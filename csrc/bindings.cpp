@@ -342,9 +342,6 @@ static int probe_mfma(u64 a, u64 b, u64 d, u64 stream) {
 static int probe_mfma16(u64 a, u64 b, u64 d, u64 stream) {
   return mb_probe_mfma16(P<const void>(a), P<const void>(b), P<float>(d), ST(stream));
 }
-static int probe_smfmac(u64 a, u64 b, u64 idx, u64 d, u64 stream) {
-  return mb_probe_smfmac(P<const void>(a), P<const void>(b), P<const int>(idx), P<float>(d), ST(stream));
-}
 static int probe_lane_xor(u64 in, u64 out, u64 stream) {
   return mb_probe_lane_xor(P<const unsigned>(in), P<unsigned>(out), ST(stream));
 }
@@ -397,7 +394,6 @@ PYBIND11_MODULE(_C, m) {
   m.def("probe_mfma", &probe_mfma);
   m.def("probe_mfma16", &probe_mfma16);
   m.def("probe_tr", &probe_tr);
-  m.def("probe_smfmac", &probe_smfmac);
   m.def("probe_lane_xor", &probe_lane_xor);
   m.def("ctrl_bwd_step", &ctrl_bwd_step);
   m.def("device_info", &device_info);

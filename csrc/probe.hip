@@ -37,22 +37,6 @@ __global__ void probe_tr_kernel(const h16* img_g, int rows, int stride, int e0, 
   *reinterpret_cast<h16x8*>(out + threadIdx.x * 8) = f;
 }
 
-// Sparse (2:4 along K) MFMA v_smfmac_f32_32x32x32_bf16: a = the compressed A operand (64 lanes x
-// 8 bf16), b = the dense B operand (64 lanes x 16 bf16), idx = the per-lane index register,
-// d = raw accumulator registers (64 x 16 f32). Layout tests: tests/test_gpu_probe.py.
-typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
-typedef __bf16 bf16x16_t __attribute__((ext_vector_type(16)));
-__global__ void probe_smfmac_kernel(const __bf16* a, const __bf16* b, const int* idx, float* d) {
-  const int l = threadIdx.x;
-  const bf16x8_t af = *reinterpret_cast<const bf16x8_t*>(a + l * 8);
-  const bf16x16_t bf = *reinterpret_cast<const bf16x16_t*>(b + l * 16);
-  const f32x16 c = __builtin_amdgcn_smfmac_f32_32x32x32_bf16(af, bf, zero16(), idx[l], 0, 0);
-#pragma unroll
-  for (int q = 0; q < 16; ++q) d[l * 16 + q] = c[q];
-}
-
-// lane exchanges: out[s * 64 + lane] = lane_xor<1 << s>(in[lane]), s = 0..5; out[384 + lane] =
-// wave_sum, out[448 + lane] = wave_max, out[512 + lane] = grp_sum (16-lane groups) of in (as float)
 __global__ void probe_lane_xor_kernel(const unsigned* in, unsigned* out) {
   const int lane = threadIdx.x;
   const unsigned v = in[lane];
@@ -72,11 +56,6 @@ __global__ void probe_lane_xor_kernel(const unsigned* in, unsigned* out) {
 
 extern "C" int mb_probe_lane_xor(const unsigned* in, unsigned* out, hipStream_t st) {
   hipLaunchKernelGGL(mb::probe_lane_xor_kernel, dim3(1), dim3(64), 0, st, in, out);
-  return (int)hipGetLastError();
-}
-
-extern "C" int mb_probe_smfmac(const void* a, const void* b, const int* idx, float* d, hipStream_t st) {
-  hipLaunchKernelGGL(mb::probe_smfmac_kernel, dim3(1), dim3(64), 0, st, (const __bf16*)a, (const __bf16*)b, idx, d);
   return (int)hipGetLastError();
 }
 

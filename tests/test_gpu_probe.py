@@ -52,46 +52,6 @@ def test_tr16_transposed_fragment(stride, e0, m0):
     np.testing.assert_array_equal(got, exp)
 
 
-def test_smfmac_layout_exact():
-    """v_smfmac_f32_32x32x32_bf16 (2:4-sparse A along K), the map measured on MI355X
-    (scripts/probe_smfmac.py + scripts/infer_smfmac.py): lane (r, h) holds row r of A in four groups
-    of four K columns starting at 16h + 4g, two stored values per group at the positions of index
-    nibble g (bits 4g..4g+3 of the low 16 bits: i0 = bits 0-1, i1 = bits 2-3); B elements j < 8 are
-    K = 8h + j, j >= 8 are K = 16 + 8h + (j - 8), column r (two standard K = 16 fragments)."""
-    rng = np.random.default_rng(3)
-    pairs = [(0, 1), (0, 2), (0, 3), (1, 2), (1, 3), (2, 3)]
-    a = rng.integers(-4, 5, size=(64, 8)).astype(np.float32)
-    b = rng.integers(-4, 5, size=(64, 16)).astype(np.float32)
-    idx = np.zeros(64, np.int64)
-    A = np.zeros((32, 32), np.float64)
-    B = np.zeros((32, 32), np.float64)
-    for l in range(64):
-        r, h = l & 31, l >> 5
-        v = 0
-        for g in range(4):
-            i0, i1 = pairs[rng.integers(0, 6)]
-            v |= (i0 | (i1 << 2)) << (4 * g)
-            A[r, 16 * h + 4 * g + i0] += a[l, 2 * g]
-            A[r, 16 * h + 4 * g + i1] += a[l, 2 * g + 1]
-        idx[l] = v
-        for j in range(16):
-            B[8 * h + j if j < 8 else 16 + 8 * h + j - 8, r] = b[l, j]
-    ta = torch.tensor(a, dtype=torch.bfloat16, device=DEV).contiguous()
-    tb = torch.tensor(b, dtype=torch.bfloat16, device=DEV).contiguous()
-    ti = torch.tensor(idx.astype(np.int32), device=DEV).contiguous()
-    d = torch.zeros(64, 16, dtype=torch.float32, device=DEV)
-    assert native.lib().probe_smfmac(ta.data_ptr(), tb.data_ptr(), ti.data_ptr(), d.data_ptr(),
-                                     native.stream_handle()) == 0
-    torch.cuda.synchronize()
-    d = d.cpu().numpy()
-    D = np.zeros((32, 32), np.float64)
-    for l in range(64):
-        r, h = l & 31, l >> 5
-        for reg in range(16):
-            D[L.acc_row(reg, h), r] = d[l, reg]
-    np.testing.assert_array_equal(D, A @ B)
-
-
 def test_lane_xor_exchanges_and_reductions():
     """lane_xor<O> (DPP / permlane, common.h) returns lane (l ^ O)'s value for every O, and the wave
     reductions built on it equal the xor-butterfly reference bit for bit (same pairing order)."""
