@@ -136,6 +136,13 @@ class HipEngine:
         self.graph_mode = bool(getattr(cfg, "graph", False))
         self._graphs = None
         self._graph_gs = None
+        # x3: the 16x16x32 backward kernels against their float64 oracles once, before training
+        # (ops/selfcheck.py: a miscompiled schedule stops here instead of corrupting gradients)
+        self.selfcheck = None
+        if self.prec == "fp32":
+            from ..ops import selfcheck
+            if selfcheck.enabled():
+                self.selfcheck = selfcheck.check(self)
 
     # ------------------------------------------------------------------ buffers
     def _alloc(self):

@@ -20,7 +20,6 @@ differentiated by /root/reference/train.py:103.
 """
 import pytest
 import torch
-import torch.nn.functional as F
 
 from macbf_gnn_amd import config as C
 from macbf_gnn_amd.engine import Trainer
@@ -29,9 +28,8 @@ from macbf_gnn_amd.ops import native
 
 pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda", 0)
-TAU = 3e-5
-ROW_TOL = 1e-3
-ABS_TOL = 1e-4
+from macbf_gnn_amd.ops.selfcheck import (ABS_TOL, ROW_TOL, TAU, bad_rows, cbf_record_oracle,  # noqa: E402,F401
+                                         edge_oracle)
 
 
 def _params(tr, module):
@@ -47,40 +45,9 @@ def _unpack(tr, fn, red):
     return g
 
 
-def _lin(x, w, b):
-    return x @ w.reshape(w.shape[0], -1).t() + b
-
-
-def _tie(pre, x, w, b):
-    """Per row: some unit's |pre-activation| within TAU of the sum of its |terms|."""
-    scale = x.abs() @ w.reshape(w.shape[0], -1).abs().t() + b.abs()
-    return (pre.abs() <= TAU * scale).any(-1)
-
-
 def _check_rows(got, ref, tie, what, scale):
-    """Per row: |kernel - float64| <= ROW_TOL |ref| + ABS_TOL |scale|, scale = the row's sum of
-    |terms| (|W1^T| |dZ1|: the features' gradient is a sum over 64 hidden units that can cancel)."""
-    err = (got - ref).norm(dim=1)
-    tol = ROW_TOL * ref.norm(dim=1) + ABS_TOL * scale.norm(dim=1) + 1e-30
-    bad = (err > tol) & ~tie
-    n_bad = int(bad.sum())
-    assert n_bad == 0, (what, n_bad, int(tie.sum()), got.shape[0], float((err / tol.clamp(min=1e-30)).max()))
-
-
-def _abs_scales(pr, ins, dzs, prefix, layers, head=None):
-    """Per parameter: the sum over records of |per-record gradient| (float64), the scale the kernels'
-    fp32 accumulation of split-bf16 products is accurate against (a weight-gradient sum over
-    10^5-10^6 records cancels: its relative error against its own norm is not bounded)."""
-    out = {}
-    for li, x, dz in zip(layers, ins, dzs):
-        dz = dz.detach().abs()
-        out[f"{prefix}.{li}.weight"] = (dz.t() @ x.abs()).reshape(pr[f"{prefix}.{li}.weight"].shape)
-        out[f"{prefix}.{li}.bias"] = dz.sum(0)
-    if head is not None:
-        x, dh = head
-        out[f"{prefix}.6.weight"] = (dh.abs().unsqueeze(-1) * x.abs()).sum(0).reshape(pr[f"{prefix}.6.weight"].shape)
-        out[f"{prefix}.6.bias"] = dh.abs().sum().reshape(1)
-    return out
+    bad, worst = bad_rows(got, ref, tie, scale)
+    assert int(bad.sum()) == 0, (what, int(bad.sum()), int(tie.sum()), got.shape[0], worst)
 
 
 def _check_grads(tr, got, ref_dw, scale, what, tol=1e-4):
@@ -117,48 +84,6 @@ def _capture_cbf(monkeypatch, **cfg):
     tr.fp.flat.copy_(flat0)          # the weights of the captured call
     tr.engine.after_update()
     return tr, orig, cap["a"], cap["k"]
-
-
-def cbf_record_oracle(p, S, rec, T, B, N, K, D):
-    """float64 autograd over the records: (dE rows (n, 2D), tie flags (n,), flat dW dict)."""
-    Sf = native.from_records(S).double()                        # (T+1, B, Nn, 2D)
-    u = rec[:, 1]
-    ps = (u < 0).long()
-    e = (u & 0x7FFFFFFF).long()
-    k = e % K
-    i = (e // K) % N
-    b = (e // (K * N)) % B
-    t = e // (K * N * B)
-    j = rec[:, 2].long()
-    dh = rec[:, 3].contiguous().view(torch.float32).double()
-    ts = t + ps
-    si, sj = Sf[ts, b, i], Sf[ts, b, j]
-    rel = (si - sj).requires_grad_(True)
-    eye = (i == j).double().unsqueeze(-1)
-    pr = {n_: v.clone().requires_grad_(True) for n_, v in p.items()}
-    d = torch.sqrt((rel[:, :D] ** 2).sum(-1) + C.CBF_DIST_EPS_COORD * D)
-    x = torch.cat([rel, eye, (d - C.DIST_MIN_THRES).unsqueeze(-1)], -1)
-    mask = (d <= C.OBS_RADIUS).double()
-    tie = (d - C.OBS_RADIUS).abs() <= 1e-6
-    z = x
-    pres, ins = [], []
-    for li in (0, 2, 4):
-        w, bb = pr[f"cbf_net.{li}.weight"], pr[f"cbf_net.{li}.bias"]
-        pre = _lin(z, w, bb)
-        tie |= _tie(pre.detach(), z.detach(), w.detach(), bb.detach())
-        pres.append(pre)
-        ins.append(z.detach())
-        z = F.relu(pre)
-    h = _lin(z, pr["cbf_net.6.weight"], pr["cbf_net.6.bias"])[:, 0] * mask
-    grads = torch.autograd.grad((dh * h).sum(), [rel] + list(pr.values()) + pres)
-    notself = (i != j).double().unsqueeze(-1)
-    drel = grads[0] * notself                          # self pairs: +i - i cancels, the kernel writes 0
-    dws = dict(zip(pr.keys(), grads[1:1 + len(pr)]))
-    w1 = pr["cbf_net.0.weight"].detach().reshape(64, -1).abs()
-    dz1 = grads[1 + len(pr)].detach().abs()
-    rscale = (dz1 @ w1[:, :2 * D] + (dz1 @ w1[:, 2 * D + 1:2 * D + 2])) * notself
-    return drel, tie & (mask > 0), dws, _abs_scales(pr, ins, grads[1 + len(pr):], "cbf_net", (0, 2, 4),
-                                                    head=(z.detach(), dh * mask)), rscale
 
 
 @pytest.mark.parametrize("cfg", [
@@ -216,47 +141,6 @@ def _capture_edge(monkeypatch, **cfg):
     return tr, orig, cap[len(cap) // 2]
 
 
-def edge_oracle(p, S, idx, argmax, dP, N, D):
-    """float64: dL/d(s_i - s_j) (B, N, K, 2D), tie flags (B, N, K), dW dict, for
-    L = sum dP * maxpool_{argmax}(mask * relu(W2 relu(W1 [rel, eye] + b1) + b2))."""
-    Sf = native.from_records(S).double()                         # (B, Nn, 2D)
-    B, _, K = idx.shape
-    il = idx.long()
-    sj = torch.gather(Sf, 1, il.reshape(B, -1, 1).expand(-1, -1, 2 * D)).reshape(B, N, K, 2 * D)
-    rel = (Sf[:, :N].unsqueeze(2) - sj).requires_grad_(True)
-    ar = torch.arange(N, device=DEV).view(1, N, 1)
-    eye = (il == ar).double().unsqueeze(-1)
-    pr = {n_: v.clone().requires_grad_(True) for n_, v in p.items()
-          if n_.startswith("controller_centr_net")}
-    x = torch.cat([rel, eye], -1)
-    d = torch.sqrt((rel[..., :D] ** 2).sum(-1))
-    mask = (d < C.OBS_RADIUS).double()
-    tie = ((d - C.OBS_RADIUS).abs() <= 1e-6).reshape(-1)
-    w1, b1 = pr["controller_centr_net.0.weight"], pr["controller_centr_net.0.bias"]
-    w2, b2 = pr["controller_centr_net.2.weight"], pr["controller_centr_net.2.bias"]
-    x = x.reshape(-1, x.shape[-1])
-    z1 = _lin(x, w1, b1)
-    tie |= _tie(z1.detach(), x.detach(), w1.detach(), b1.detach())
-    h1 = F.relu(z1)
-    z2 = _lin(h1, w2, b2)
-    tie |= _tie(z2.detach(), h1.detach(), w2.detach(), b2.detach())
-    hm = (F.relu(z2) * mask.reshape(-1, 1)).reshape(B, N, K, -1)
-    sl = argmax.long()
-    has = (sl < K).double()
-    pooled = hm.gather(-2, sl.clamp(max=K - 1).unsqueeze(-2)).squeeze(-2) * has
-    dPf = dP[..., :128].double() + dP[..., 128:256].double()          # x3 rows: [hi | lo]
-    grads = torch.autograd.grad((dPf * pooled).sum(), [rel] + list(pr.values()) + [z1, z2])
-    notself = (il != ar).double().unsqueeze(-1)
-    drel = grads[0] * notself                             # self pairs: +i - i cancels, the kernel writes 0
-    dws = dict(zip(pr.keys(), grads[1:1 + len(pr)]))
-    scale = _abs_scales(pr, [x.detach(), h1.detach()], grads[1 + len(pr):], "controller_centr_net", (0, 2))
-    # row scale: |W1^T| (|W2^T| |dZ2| . relu'(Z1)) over the relative-state features
-    dz2 = grads[-1].detach().abs()
-    s1 = (dz2 @ w2.detach().reshape(128, 64).abs()) * (z1.detach() > 0).double()
-    rscale = (s1 @ w1.detach().reshape(64, -1)[:, :2 * D].abs()).reshape(B, N, K, 2 * D) * notself
-    return drel, tie.reshape(B, N, K), dws, scale, rscale
-
-
 @pytest.mark.parametrize("cfg", [
     dict(num_agents=1024, num_envs=4, inner_loops=6),
     dict(num_agents=96, num_envs=3, inner_loops=6),
@@ -284,3 +168,26 @@ def test_eb16_matches_fp64_oracle(monkeypatch, cfg):
     assert torch.isfinite(part).all()
     mine = _unpack(tr, L.ctrl_edge_grad_map, part.sum(0))
     _check_grads(tr, mine, ref_dw, scale, "edge dW")
+
+
+@pytest.mark.parametrize("dim", [2, 3])
+def test_startup_selfcheck_passes_and_catches_corruption(dim):
+    """ops.selfcheck.check runs at x3 engine construction; it passes on the shipped kernels and
+    raises when the 16x16x32 weight images are corrupted (a stand-in for a miscompiled schedule)."""
+    from macbf_gnn_amd.ops import selfcheck
+    tr = Trainer(C.TrainConfig(device="hip", seed=0, dtype="fp32", num_agents=64, num_envs=2, inner_loops=4,
+                               dim=dim), device=DEV)
+    rep = tr.engine.selfcheck
+    assert rep and rep["cbf16"]["rows"] > 0 and rep["cbf16"]["bad"] == 0 and rep["eb16"]["bad"] == 0
+    pw = tr.engine.pw
+    keep = pw.cbf_rm16.clone()
+    pw.cbf_rm16.view(-1)[:4096] = pw.cbf_rm16.view(-1)[:4096] * 1.5
+    with pytest.raises(native.NativeError):
+        selfcheck.check(tr.engine)
+    pw.cbf_rm16.copy_(keep)
+    keep = tr.engine.eb16_w.clone()
+    tr.engine.eb16_w.view(-1)[4096:8192] = 0
+    with pytest.raises(native.NativeError):
+        selfcheck.check(tr.engine)
+    tr.engine.eb16_w.copy_(keep)
+    assert selfcheck.check(tr.engine)["eb16"]["bad"] == 0
