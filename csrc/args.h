@@ -250,11 +250,8 @@ struct CtrlNodeBwdArgs {
                                        // [workgroup][wave][16] shader-clock values (scripts/stamps_node.py)
 };
 
-// MACBF_NODE_COOP=0 disables the cooperative 32-agent node backward (A/B runs)
-inline bool node_bwd_coop_enabled() {
-  static const bool on = [] { const char* e = getenv("MACBF_NODE_COOP"); return !(e && e[0] == '0'); }();
-  return on;
-}
+// the cooperative 32-agent node backward (node_bwd_coop) runs every 32-agent chunk
+inline bool node_bwd_coop_enabled() { return true; }
 
 struct CtrlEdgeBwdArgs {
   const float4* S;     long s_env;     // node records (strides in records)

@@ -710,9 +710,8 @@ extern "C" int MB_SYM(ctrl_fwd)(const mb::CtrlArgs* a, int num_cu, hipStream_t s
   if (blocks > maxb) blocks = maxb;
   CtrlArgs b = *a;
   b.apw = apw;
-  // x3: one fused launch (edge + node phase per group, 145 KB of weights) unless MACBF_X3_SPLIT
-  static const bool split = [] { const char* e = getenv("MACBF_X3_SPLIT"); return e && e[0] == '1'; }();
-  if (X3 && !split) {
+  // x3: one fused launch (edge + node phase per group, 145 KB of weights)
+  if (X3) {
     const size_t ldf = (size_t)CTRL_FWD_FRAGS * FRAG_SZ + CTRL_VEC * 4;
     if (a->dim == 3) {
       (void)hipFuncSetAttribute((const void*)ctrl_fwd_kernel<CTRL_WAVES, 3, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ldf);
@@ -2274,8 +2273,8 @@ extern "C" int MB_SYM(ctrl_edge_bwd)(const mb::CtrlEdgeBwdArgs* a, int num_block
 #endif
   }
   const size_t lds = ctrl_edge_bwd_lds();
-  // K = 12 (TOP_K): constant-K instantiation (MACBF_EB_K12=0 forces the runtime-K one, A/B)
-  static const bool k12_off = [] { const char* e = getenv("MACBF_EB_K12"); return e && e[0] == '0'; }();
+  // K = 12 (TOP_K): constant-K instantiation (A/B vs runtime K: 136.7 vs 137.1-139.6 us, PERF.md)
+  constexpr bool k12_off = false;
   auto go = [&](auto kern) {
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL(kern, dim3(num_blocks), dim3(EB_WAVES * 64), lds, st, *a);

@@ -587,23 +587,18 @@ static int scan_num_cu() {
 }
 
 // Small scans (a strong-scaling slice: few envs) would fill only some CUs with big blocks: use
-// 256-thread blocks whenever the big-block grid has fewer blocks than CUs (MACBF_SCAN_SMALL=0/1
-// forces the choice for A/B runs).
+// 256-thread blocks whenever the big-block grid has fewer blocks than CUs.
 static bool scan_small_grid(const ScanArgs& a) {
-  static const int force = [] { const char* e = getenv("MACBF_SCAN_SMALL"); return e ? atoi(e) : -1; }();
-  if (force >= 0) return force != 0;
   constexpr int AG = SCAN_BS_BIG / SCAN_LPA;      // agents per big block
   return (long)a.B * ((a.Nn + AG - 1) / AG) < scan_num_cu();
 }
 
 // Still fewer 256-thread blocks than CUs (e.g. 8 envs x 1024 nodes: 128 blocks): 8 lanes per
 // agent (one candidate of every chunk per lane) halve the agents per block and the per-lane
-// chunk work -> twice the blocks (MACBF_SCAN_LPA8=0/1 forces the choice for A/B runs).
-// Same keys and tie order: the merged lists are identical for any LPA.
+// chunk work -> twice the blocks. Same keys and tie order: the merged lists are identical for
+// any LPA (tests/test_gpu_forward.py forces lanes = 4 / 8 through ScanArgs.lanes).
 static bool scan_lpa8(const ScanArgs& a) {
   if (a.lanes == 4 || a.lanes == 8) return a.lanes == 8;
-  static const int force = [] { const char* e = getenv("MACBF_SCAN_LPA8"); return e ? atoi(e) : -1; }();
-  if (force >= 0) return force != 0;
   constexpr int AG = 256 / SCAN_LPA;
   return SCAN_LPA < 8 && (long)a.B * ((a.Nn + AG - 1) / AG) < scan_num_cu();
 }

@@ -25,6 +25,7 @@ import os
 import torch
 
 from .. import config as C
+from .. import knobs
 from ..ops import layout as L
 from ..ops import native
 from ..ops.weights import PackedWeights
@@ -63,21 +64,14 @@ class HipEngine:
     def __init__(self, trainer):
         self.tr = trainer
         cfg = trainer.cfg
-        # scheduling knobs (A/B measurements): MACBF_RESORT_EVERY, MACBF_OVERLAP_HFWD, MACBF_REDUCE_LATE
-        import os
-        self.resort_every = int(os.environ.get("MACBF_RESORT_EVERY", self.resort_every))
-        ov = os.environ.get("MACBF_OVERLAP_HFWD")
-        self.overlap_hfwd = bool(int(ov)) if ov is not None else self.overlap_hfwd
-        self.reduce_late = int(os.environ.get("MACBF_REDUCE_LATE", self.reduce_late))
-        self.native_rollout = bool(int(os.environ.get("MACBF_NATIVE_ROLLOUT", int(self.native_rollout))))
-        self.small_rollout = bool(int(os.environ.get("MACBF_SMALL_ROLLOUT", int(self.small_rollout))))
-        self.small_bptt = bool(int(os.environ.get("MACBF_SMALL_BPTT", int(self.small_bptt))))
-        self.bptt_groups = int(os.environ.get("MACBF_BPTT_GROUPS", self.bptt_groups))
+        # scheduling choices are class attributes (tests / A/B scripts set them); the environment
+        # knobs that remain are listed in macbf_gnn_amd/knobs.py
+        self.small_bptt = bool(knobs.get_int("MACBF_SMALL_BPTT", int(self.small_bptt)))
         if cfg.num_envs % self.bptt_groups:
             self.bptt_groups = 1
         self._drv = None
         self._bdrv = None
-        self.native_bptt = bool(int(os.environ.get("MACBF_NATIVE_BPTT", int(self.native_bptt))))
+        self.native_bptt = bool(knobs.get_int("MACBF_NATIVE_BPTT", int(self.native_bptt)))
         self.bptt = cfg.bptt
         self.reuse = cfg.reuse_nbr_idx
         # deduplicated h/h' evaluations need both roles' state gradients on the same s_t: BPTT only
@@ -220,9 +214,9 @@ class HipEngine:
             self.loss_part = torch.zeros(ndh, native.DH_PARTIAL, dtype=f32, device=dev)
             self.blk_active = torch.zeros(ndh, dtype=i32, device=dev)
             # x3: the 16x16x32 backward (csrc/cbf16.h, two waves per SIMD) reads cbf_compact's
-            # 16-byte records of the active evaluations instead of the index list
-            # (MACBF_CBF16=0: the 32x32x16 kernel on the index list, for A/B runs)
-            self.cbf16 = self.prec == "fp32" and os.environ.get("MACBF_CBF16", "1") != "0"
+            # 16-byte records of the active evaluations; bf16 / fp16: the 32x32x16 kernel on the
+            # index list
+            self.cbf16 = self.prec == "fp32"
             self.act_list = torch.zeros(2 * E, dtype=i32, device=dev) if not self.cbf16 else None
             self.rec_list = torch.zeros(2 * E, 4, dtype=i32, device=dev) if self.cbf16 else None
             self.loss_red = torch.zeros(native.DH_PARTIAL, dtype=f32, device=dev)
@@ -233,13 +227,13 @@ class HipEngine:
         # x3, K = 12: the 16x16x32 controller edge backward (csrc/ctrl16.h, two waves per SIMD);
         # MACBF_EB16=0: the 32x32x16 kernel (A/B runs)
         self.eb16_w = (self.pw.ctrl_w16 if (self.prec == "fp32" and K == 12
-                                            and os.environ.get("MACBF_EB16", "1") != "0") else None)
+                                            and knobs.get_int("MACBF_EB16", 1)) else None)
         # x3, 128-agent node chunks: the 16x16x32 node backward (csrc/node16.h, two waves per SIMD);
         # MACBF_NODE16=0: the 32x32x16 kernel (A/B runs). Decided once per engine (its slab layout
         # differs, layout.ctrl_node16_grad_map): the BPTT launches cover (B / groups) x N agents,
         # the no-BPTT launch T x B x N >= that, so every node launch of this engine takes the same kernel
         Gp = self.bptt_groups
-        self.node16_w = (self.pw.node_rm16 if (self.prec == "fp32" and os.environ.get("MACBF_NODE16", "1") != "0"
+        self.node16_w = (self.pw.node_rm16 if (self.prec == "fp32" and knobs.get_int("MACBF_NODE16", 1)
                                                and native.node_bwd_chunk((B // Gp) * N, dev) == 128
                                                and not self.small_bptt) else None)
         self.host_dist = torch.zeros(T, B, dtype=torch.int64, pin_memory=True)
@@ -329,9 +323,9 @@ class HipEngine:
                 small_ctl=native.ptr(self.small_ctl) if self.small_rollout else 0,
                 small_apw=int(native.small_apw(N)), knn_tail=int(not self.reuse),
                 noise_prob=float(cfg.add_noise_prob), noise_scale=float(cfg.noise_scale),
-                fork_device_scope=int(os.environ.get("MACBF_FORK_DEVICE_SCOPE", "1")),
+                fork_device_scope=1,
                 # early stop published by the controller kernels (no per-step queue marker / copy)
-                publish=int(os.environ.get("MACBF_PUBLISH", "1"))))
+                publish=knobs.get_int("MACBF_PUBLISH", 1)))
             if pw.ctrl_v.numel() < 352 or pw.ctrl_w.numel() < (c["f_node"] + 54) * 512 * (2 if pw.x3 else 1):
                 raise native.NativeError("packed controller weights too small")
             if overlap and (self.hbuf.numel() < 2 * T * BNK or self.src.numel() < 2 * T * BNK):

@@ -80,7 +80,7 @@ class Trainer:
             self.gscale_dev = torch.full((1,), float(cfg.loss_scale_init), dtype=torch.float32, device=self.device)
             self._good_dev = torch.zeros(1, dtype=torch.int32, device=self.device)
         self._next = None
-        prefetch = cfg.prefetch_data if os.environ.get("MACBF_PREFETCH") is None else os.environ["MACBF_PREFETCH"] == "1"
+        prefetch = cfg.prefetch_data
         self._side = torch.cuda.Stream(device=self.device) if (self.device.type == "cuda" and prefetch) else None
         if self.device.type == "cuda":
             from .hip_engine import HipEngine

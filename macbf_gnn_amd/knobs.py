@@ -1,0 +1,31 @@
+"""Every environment knob the framework reads (one list, each with its user).
+
+Production runs set none of them. The remaining knobs exist for tests (they force a code path a
+test compares against) or for A/B measurement scripts; knobs whose A/B question was settled were
+removed (their decision is the code's default, the measurement is in docs/PERF.md).
+
+| knob | default | read by | used by |
+|---|---|---|---|
+| MACBF_DP_BACKEND | nccl on GPU, gloo on CPU | parallel/dist.py, parallel/launch.py | rehearsal of N ranks on one GPU (gloo) |
+| MACBF_DP_FORCE_PG | 0 | parallel/dist.py | RCCL process group at world 1 (tests/test_gpu_dp.py) |
+| MACBF_EXT | -- | ops/native.py | load an alternative extension build (scripts/build_variant.sh A/B, no-barrier builds) |
+| MACBF_NATIVE_BPTT | 1 | engine/hip_engine.py | Python BPTT launch loop, so tests can spy on the calls |
+| MACBF_SMALL_BPTT | 0 | engine/hip_engine.py | persistent small-scene BPTT (scripts/gpu_ab_cfg2.sh) |
+| MACBF_EB16 | 1 | engine/hip_engine.py | 32x32x16 x3 edge backward (tests/test_gpu_small.py compares the persistent kernels with it) |
+| MACBF_NODE16 | 1 | engine/hip_engine.py | 32x32x16 x3 node backward (tests/test_gpu_node16.py) |
+| MACBF_NODE_CHUNK | by size | ops/native.py | agents per node-backward chunk (tests force 128 at small sizes) |
+| MACBF_BWD_FUSED | by size | ops/native.py | fused node + edge BPTT step on / off (tests) |
+| MACBF_CTRL_APW | by size | ops/native.py | agents per wave of the controller step (tests/test_gpu_fp32.py dense-row equality) |
+| MACBF_EDGE_WG_PER_CU | 1 (x3) | ops/native.py | edge-backward workgroups per CU (tests) |
+| MACBF_PUBLISH | 1 | engine/hip_engine.py | early stop through a queue marker instead of kernel publication (tests) |
+| MACBF_SELFCHECK | 1 | ops/selfcheck.py | skip the start-up self-check of the 16x16x32 kernels |
+| MACBF_ARCH | gfx950 | csrc/build.py | build target |
+"""
+from __future__ import annotations
+
+import os
+
+
+def get_int(name: str, default: int) -> int:
+    v = os.environ.get(name)
+    return default if v is None or v == "" else int(v)

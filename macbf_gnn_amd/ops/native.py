@@ -495,10 +495,10 @@ HFWD_WAVES = 8
 
 
 def cbf_hfwd_grid(EV: int, device, per_cu: int | None = None) -> int:
-    """Workgroups of an h evaluation launch: up to per_cu per CU (MACBF_HFWD_PER_CU; default 4)."""
+    """Workgroups of an h evaluation launch: up to per_cu per CU (default 4)."""
     tiles = (EV + 31) // 32
     if per_cu is None:
-        per_cu = int(os.environ.get("MACBF_HFWD_PER_CU", "4"))
+        per_cu = 4
     return max(1, min((tiles + HFWD_WAVES - 1) // HFWD_WAVES, num_cu(device) * per_cu))
 
 

@@ -106,7 +106,7 @@ def test_small_bptt_matches_per_step_launches(kw, monkeypatch):
     bodies as the per-step kernels -> the same dL/ds_t recursion and weight gradients bit for bit
     (slab rows differ: one per env, so the final slab sums may differ in rounding order). The
     per-step side uses the 32x32x16 edge backward (MACBF_EB16=0), whose body the persistent kernel
-    shares; the 16x16x32 one is checked against it in test_gpu_eb16.py."""
+    shares; the 16x16x32 one is pinned to a float64 oracle in test_gpu_oracle16.py."""
     monkeypatch.setenv("MACBF_EB16", "0")
     a = _trainer(True, small_bptt=False, T=20, **kw)
     b = _trainer(True, small_bptt=True, T=20, **kw)
