@@ -377,6 +377,10 @@ int mb_ctrl_bwd_step_x3(const mb::CtrlNodeBwdArgs* na, const mb::CtrlEdgeBwdArgs
 int mb_ctrl_edge_bwd(const mb::CtrlEdgeBwdArgs* a, int num_blocks, hipStream_t st);
 int mb_ctrl_edge_bwd_f16(const mb::CtrlEdgeBwdArgs* a, int num_blocks, hipStream_t st);
 int mb_ctrl_edge_bwd_x3(const mb::CtrlEdgeBwdArgs* a, int num_blocks, hipStream_t st);
+// 16x16x32 backward workgroups per CU of each build (the launch grid; csrc/cbf16.h, csrc/ctrl16.h)
+int mb_k16_wg_per_cu(int kernel);
+int mb_k16_wg_per_cu_f16(int kernel);
+int mb_k16_wg_per_cu_x3(int kernel);
 int mb_bptt_small(const mb::BpttSmallArgs* a, hipStream_t st);
 int mb_bptt_small_f16(const mb::BpttSmallArgs* a, hipStream_t st);
 int mb_bptt_small_x3(const mb::BpttSmallArgs* a, hipStream_t st);

@@ -342,6 +342,10 @@ static int probe_mfma(u64 a, u64 b, u64 d, u64 stream) {
 static int probe_mfma16(u64 a, u64 b, u64 d, u64 stream) {
   return mb_probe_mfma16(P<const void>(a), P<const void>(b), P<float>(d), ST(stream));
 }
+extern "C" int mb_probe_mfma_exec(const void* a, float* out, int uniform, hipStream_t st);
+static int probe_mfma_exec(u64 a, u64 out, int uniform, u64 stream) {
+  return mb_probe_mfma_exec(P<const void>(a), P<float>(out), uniform, ST(stream));
+}
 static int probe_lane_xor(u64 in, u64 out, u64 stream) {
   return mb_probe_lane_xor(P<const unsigned>(in), P<unsigned>(out), ST(stream));
 }
@@ -362,6 +366,11 @@ static py::dict device_info(int dev) {
 }
 
 static std::string err_str(int e) { return hipGetErrorString((hipError_t)e); }
+
+// workgroups per CU of the 16x16x32 backward kernels of build `prec` (kernel 0 CBF, 1 edge, 2 node)
+static int k16_wg_per_cu(int prec, int kernel) {
+  return (prec == 2 ? mb_k16_wg_per_cu_x3 : prec == 1 ? mb_k16_wg_per_cu_f16 : mb_k16_wg_per_cu)(kernel);
+}
 
 void register_runtime(py::module& m);   // runtime.cpp: native rollout driver
 
@@ -395,8 +404,10 @@ PYBIND11_MODULE(_C, m) {
   m.def("probe_mfma16", &probe_mfma16);
   m.def("probe_tr", &probe_tr);
   m.def("probe_lane_xor", &probe_lane_xor);
+  m.def("probe_mfma_exec", &probe_mfma_exec);
   m.def("ctrl_bwd_step", &ctrl_bwd_step);
   m.def("device_info", &device_info);
   m.def("err_str", &err_str);
+  m.def("k16_wg_per_cu", &k16_wg_per_cu);
   m.attr("ARCH") = "gfx950";
 }

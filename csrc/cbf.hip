@@ -162,7 +162,7 @@ __global__ __launch_bounds__(WAVES * 64) void cbf_fwd_kernel(CbfFwdArgs a) {
   block_copy16(wl, a.wpack + (size_t)a.f_fwd * FRAG_ELEMS, CBF_FWD_FRAGS * FRAG_SZ);
   block_copy16(vl, a.wvec, CBF_VEC * 4);
   __syncthreads();
-  const int wave = threadIdx.x / WAVE, lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
+  const int wave = wave_id(), lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
   const long E = (long)a.B * a.T * a.N * a.K;
   const long ntiles = (E + 31) / 32;
   float nd = 0.f, ns = 0.f, lsc = a.lc.scale;
@@ -406,7 +406,7 @@ __global__ __launch_bounds__(NW * 64, CBF_HFWD_MINW) void cbf_hfwd_kernel(CbfFwd
   block_copy16(wf, a.wpack + (size_t)a.f_fwd * FRAG_ELEMS, 2 * FRAG_SZ);
   block_copy16(vl, a.wvec, CBF_VEC * 4);
   __syncthreads();
-  const int wave = threadIdx.x / WAVE, lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
+  const int wave = wave_id(), lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
   const unsigned E = (unsigned)a.B * a.T * a.N * a.K;
   const unsigned U = a.u_end ? a.u_end : (unsigned)*a.nev;
   const unsigned U0 = a.u_begin;
@@ -513,7 +513,7 @@ __global__ __launch_bounds__(NW * 64, 1) void cbf_bwd_kernel(CbfBwdArgs a) {
   if constexpr (FUSED)
     for (int q = threadIdx.x; q < 8 * CH / 2; q += blockDim.x) (&lacc[0][0])[q] = 0.f;
   __syncthreads();
-  const int wave = threadIdx.x / WAVE, lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
+  const int wave = wave_id(), lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
   const long E = (long)a.B * a.T * a.N * a.K;
   const long EV = (!FUSED && a.nact) ? (long)*a.nact : (!FUSED && a.nev) ? (long)*a.nev : E * a.passes;
   const long nchunks = FUSED ? (E + CH / 2 - 1) / (CH / 2) : (EV + CH - 1) / CH;
@@ -860,23 +860,17 @@ static void launch_cbf_bwd(const CbfBwdArgs& a, int num_blocks, hipStream_t st) 
 }  // namespace MB_PREC
 }  // namespace mb
 
-#if MB_X3
 #include "cbf16.h"
-#endif
 
 extern "C" int MB_SYM(cbf_bwd)(const mb::CbfBwdArgs* a, int num_blocks, hipStream_t st) {
   using namespace mb;
   using namespace mb::MB_PREC;
   if (a->K > 16 || a->K < 1 || a->passes < 1 || a->passes > 2) return -1;
-  if (a->rec) {   // 16x16x32 backward over cbf_compact's records (x3 build only)
-#if MB_X3
+  if (a->rec) {   // 16x16x32 backward over cbf_compact's records (csrc/cbf16.h)
     if (a->fused || !a->nact || !a->wrm16 || !a->w16) return -5;
     if (a->dim == 3) launch_cbf_bwd16<3>(*a, num_blocks, st);
     else launch_cbf_bwd16<2>(*a, num_blocks, st);
     return (int)hipGetLastError();
-#else
-    return -6;
-#endif
   }
   if (a->fused && (a->passes != 2 || !a->dang || !a->counts)) return -2;
   if (a->src && (a->fused || !a->nev || a->passes != 2)) return -3;

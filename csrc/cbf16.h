@@ -1,5 +1,6 @@
-// 16x16x32 x3 CBF backward: the fp32-accurate (3-term split-bf16) backward of the CBF edge MLP
-// over the active evaluation list, at TWO waves per SIMD.
+// 16x16x32 CBF backward over the active evaluation list: the fp32-accurate (3-term split-bf16) x3
+// backward of the CBF edge MLP at TWO waves per SIMD, and the same kernel in the 1-pass bf16 /
+// fp16 builds (no lo planes: half the weight-image and stage LDS, one MFMA per product).
 //
 // Why a second kernel: the 32x32x16 x3 backward (cbf_bwd_kernel) keeps 32 evaluations per wave
 // and needs 464 registers, so it runs one wave per SIMD; its phase clocks (scripts/stamps_cbf.py,
@@ -32,19 +33,23 @@ namespace MB_PREC {
 
 constexpr int S16_W2 = 80, S16_W3 = 144;                   // layout.CBF16_STRIDES
 constexpr int RM16_W2 = 128 * S16_W2, RM16_W3 = 64 * S16_W3;
-constexpr int RM16 = RM16_W2 + RM16_W3;                    // lo-plane offset of the images
+constexpr int RM16 = RM16_W2 + RM16_W3;                    // lo-plane offset of the images (x3)
+constexpr int C16_PLANES = X3 ? 2 : 1;
 constexpr int C16_NW = 8, C16_CH = 16 * C16_NW, C16_RT = 64;   // waves, evaluations per chunk, rows per turn
 constexpr int S16_64 = 68, S16_128 = 148, S16_F = 24;      // stage image strides (scripts: bank model)
 // stage A region: D3 [64 x S16_64] | H2 [64 x S16_128], lo plane at +PLA
 constexpr int C16_PLA = C16_RT * (S16_64 + S16_128);
 // stage BC region: D2 [64 x S16_128] | H1 [64 x S16_64] | D1 [64 x S16_64], lo plane at +PLB, then F
 constexpr int C16_PLB = C16_RT * (S16_128 + 2 * S16_64);
-constexpr int C16_REGION = 2 * C16_PLB + C16_RT * S16_F;   // elements (>= 2 * C16_PLA)
-constexpr size_t C16_LDS_W = (size_t)2 * RM16 * 2;        // W2 | W3 images, hi + lo
-constexpr size_t C16_LDS_F = 2 * FRAG_SZ;                 // w1ft16 (2 fragments, hi + lo)
+constexpr int C16_REGION = C16_PLANES * C16_PLB + C16_RT * S16_F;   // elements (>= planes * C16_PLA)
+constexpr size_t C16_LDS_W = (size_t)C16_PLANES * RM16 * 2;        // W2 | W3 images, hi [+ lo]
+constexpr size_t C16_LDS_F = 2 * FRAG_SZ;                          // w1ft16 (2 fragments, hi [+ lo])
 constexpr size_t C16_LDS = C16_LDS_W + C16_LDS_F + CBF_VEC * 4 + (size_t)C16_REGION * 2;
-static_assert(C16_REGION >= 2 * C16_PLA, "stage A fits the region");
-static_assert(C16_LDS <= 160 * 1024 - 512, "LDS budget");
+// x3: one 8-wave workgroup per CU (2 waves / SIMD); 1-pass: two (<= 80 KiB each, 4 waves / SIMD at
+// <= 128 registers; the second __launch_bounds__ argument is HIP's minimum waves per SIMD).
+constexpr int C16_WG_PER_CU = CBF16_WGPC;
+static_assert(C16_REGION >= C16_PLANES * C16_PLA, "stage A fits the region");
+static_assert(C16_LDS <= 160 * 1024 / C16_WG_PER_CU - 64, "LDS budget");
 
 #ifndef CBF16_DBG
 #define CBF16_DBG 0    // 1: per-record forward sums to a.dbg (scripts/check_cbf16.py)
@@ -63,7 +68,7 @@ DEV Fr w16_fr(const h16* W, int stride, int m0, int s, int lane) {
   const h16* p = W + (m0 + n) * stride + 32 * s + 8 * g;
   Fr r;
   r.h = *reinterpret_cast<const h16x8*>(p);
-  r.l = *reinterpret_cast<const h16x8*>(p + RM16);
+  if constexpr (X3) r.l = *reinterpret_cast<const h16x8*>(p + RM16);
   return r;
 }
 // A = W^T: rows = logical columns m0..m0+15 of the permuted image, K-step s over W's rows in
@@ -73,7 +78,7 @@ DEV Fr w16T_fr(const h16* W, int stride, int m0, int s, int lane) {
   const int colp = 32 * (m0 >> 5) + 4 * ((m0 >> 4) & 1) + 8 * p;
   Fr r;
   r.h = tr_pair16(W, stride, 32 * s + 4 * g, 16, colp, lane);
-  r.l = tr_pair16(W + RM16, stride, 32 * s + 4 * g, 16, colp, lane);
+  if constexpr (X3) r.l = tr_pair16(W + RM16, stride, 32 * s + 4 * g, 16, colp, lane);
   return r;
 }
 // record of one active evaluation (cbf_compact): {u, e | pass << 31, neighbour j, dh bits}
@@ -105,11 +110,11 @@ DEV void ev16_issue(const CbfBwdArgs& a, const int4& r, Ev16<D>& x) {
 }
 
 template <int D>
-__global__ __launch_bounds__(C16_NW * 64) void cbf_bwd16_kernel(CbfBwdArgs a) {
+__global__ __launch_bounds__(C16_NW * 64, 2 * C16_WG_PER_CU) void cbf_bwd16_kernel(CbfBwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   h16* W2 = reinterpret_cast<h16*>(smem);
   h16* W3 = W2 + RM16_W2;
-  h16* wft = W2 + 2 * RM16;                                   // w1ft16: 2 fragments [hi | lo]
+  h16* wft = W2 + C16_PLANES * RM16;                          // w1ft16: 2 fragments [hi | lo]
   float* vl = reinterpret_cast<float*>(smem + C16_LDS_W + C16_LDS_F);
   h16* stg = reinterpret_cast<h16*>(smem + C16_LDS_W + C16_LDS_F + CBF_VEC * 4);
   __shared__ float red4[C16_NW];
@@ -117,7 +122,7 @@ __global__ __launch_bounds__(C16_NW * 64) void cbf_bwd16_kernel(CbfBwdArgs a) {
   block_copy16(wft, a.w16 + 4 * FRAG_ELEMS, (int)C16_LDS_F);
   block_copy16(vl, a.wvec, CBF_VEC * 4);
   __syncthreads();
-  const int wave = threadIdx.x / WAVE, lane = threadIdx.x & 63, n = lane & 15, g = lane >> 4;
+  const int wave = wave_id(), lane = threadIdx.x & 63, n = lane & 15, g = lane >> 4;
   const long EV = (long)*a.nact;
   const long nchunks = (EV + C16_CH - 1) / C16_CH;
   const float* b2 = vl;
@@ -351,7 +356,7 @@ __global__ __launch_bounds__(C16_NW * 64) void cbf_bwd16_kernel(CbfBwdArgs a) {
       h16* imD2 = stg;
       h16* imH1 = imD2 + C16_RT * S16_128;
       h16* imD1 = imH1 + C16_RT * S16_64;
-      h16* imF = stg + 2 * C16_PLB;
+      h16* imF = stg + C16_PLANES * C16_PLB;
       if ((wave >> 2) == turn) {
         const int row = (wave & 3) * 16 + n;
 #pragma unroll

@@ -100,6 +100,17 @@ DEV int opaque_zero() {
   return z;
 }
 
+// The wave's index in its workgroup as a wave-uniform (SGPR) value. Every branch on it is then a
+// scalar branch (s_cbranch_scc) rather than an EXEC-masked region. This matters for MFMAs: the
+// compiler drops the s_cbranch_execz skip of a short EXEC-masked block and lets it run with EXEC
+// = 0 -- harmless for VALU, but a v_mfma there still updates its accumulator, and with operand
+// registers the masked block was meant to set (measured: the 1-pass 16x16x32 edge backward's
+// `if (ub == u) biasB = mfma(A, ones)` with threadIdx.x / 64 put the bias MFMA of the other wave
+// parity in a masked block without the skip; every wave then added A x {ones, stale registers}
+// and db2 came out 90 % wrong, docs/ARCHITECTURE.md "MFMA and EXEC"). Rule in these kernels: no
+// MFMA under a lane-divergent condition, wave-dependent conditions on wave_id().
+DEV int wave_id() { return __builtin_amdgcn_readfirstlane((int)(threadIdx.x / WAVE)); }
+
 // lane l <- lane l^32 with v_permlane32_swap (CDNA4, VALU) instead of ds_bpermute (LDS path)
 DEV unsigned xor32u(unsigned u) {
   const auto r = __builtin_amdgcn_permlane32_swap(u, u, false, false);

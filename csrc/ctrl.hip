@@ -457,7 +457,7 @@ DEV void ctrl_fwd_groups(const CtrlArgs& a, const h16* wl, const h16* wn, const 
   const float* nb3 = vl + 256;
   const float* nb4 = vl + 320;
 
-  const int wave = threadIdx.x / WAVE, lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
+  const int wave = wave_id(), lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
   h16* pool = pools + wave * 32 * PSTR;
   const int N = a.N, K = a.K;
   const int total = a.B * N;
@@ -652,9 +652,9 @@ __global__ __launch_bounds__(WAVES * 64) void ctrl_fwd_kernel(CtrlArgs a) {
   __syncthreads();
   const int apw = (a.apw >= 2 && a.apw <= 32) ? a.apw : 32;
   if (CTRL_FWD_DENSE && a.K == 12 && apw % 8 == 0)
-    ctrl_fwd_groups<D, false, FUSE, true>(a, wl, wn, vl, pools, blockIdx.x * WAVES + threadIdx.x / WAVE, gridDim.x * WAVES);
+    ctrl_fwd_groups<D, false, FUSE, true>(a, wl, wn, vl, pools, blockIdx.x * WAVES + wave_id(), gridDim.x * WAVES);
   else
-    ctrl_fwd_groups<D, false, FUSE>(a, wl, wn, vl, pools, blockIdx.x * WAVES + threadIdx.x / WAVE, gridDim.x * WAVES);
+    ctrl_fwd_groups<D, false, FUSE>(a, wl, wn, vl, pools, blockIdx.x * WAVES + wave_id(), gridDim.x * WAVES);
   if constexpr (!X3 || FUSE) publish_step(a);   // the x3 split path publishes from its node kernel
 }
 
@@ -684,7 +684,7 @@ __global__ __launch_bounds__(WAVES * 64) void ctrl_node_fwd_kernel(CtrlArgs a) {
   block_copy16(wn, a.wpack + (size_t)a.f_node * FRAG_ELEMS, 54 * FRAG_SZ);
   block_copy16(vl, a.wvec, CTRL_VEC * 4);
   __syncthreads();
-  ctrl_node_groups<D>(a, wn, vl, blockIdx.x * WAVES + threadIdx.x / WAVE, gridDim.x * WAVES);
+  ctrl_node_groups<D>(a, wn, vl, blockIdx.x * WAVES + wave_id(), gridDim.x * WAVES);
   publish_step(a);
 }
 
@@ -877,7 +877,7 @@ DEV void node_bwd_body(const CtrlNodeBwdArgs& a, unsigned char* smem, long c0, l
   const float* nb2 = vl + 128;
   const float* nb3 = vl + 256;
   const float* nb4 = vl + 320;
-  const int wave = threadIdx.x / WAVE, lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
+  const int wave = wave_id(), lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
   const int N = a.N;
   const int total = a.B * N;
   const int CA = (a.chunk == 32 || a.chunk == 64) ? a.chunk : NB_CH;   // agents per chunk
@@ -1275,7 +1275,7 @@ DEV void node_bwd_coop(const CtrlNodeBwdArgs& a, unsigned char* smem, long c0, l
   const float* nb2 = vl + 128;
   const float* nb3 = vl + 256;
   const float* nb4 = vl + 320;
-  const int wave = threadIdx.x / WAVE, lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
+  const int wave = wave_id(), lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
   const int N = a.N;
   const int total = a.B * N;
   const long nchunks = (total + 31) / 32;
@@ -1642,7 +1642,7 @@ DEV void edge_bwd_body(const CtrlEdgeBwdArgs& a, unsigned char* smem, long w0, l
   block_copy16(wf, a.wpack + (size_t)a.f_ew1f * FRAG_ELEMS, 2 * FRAG_SZ);
   block_copy16(wf + 2 * FRAG_ELEMS, a.wpack + (size_t)a.f_ew2tn * FRAG_ELEMS, 20 * FRAG_SZ);
   __syncthreads();
-  const int wave = threadIdx.x / WAVE, lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
+  const int wave = wave_id(), lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
   const int N = a.N, K = KC ? KC : a.K;
   const int total = a.B * N;
   const long nchunks = SPLIT ? (total + 31) / 32 : (total + EB_CH - 1) / EB_CH;
@@ -2081,7 +2081,7 @@ __global__ __launch_bounds__(SR_WAVES * 64) void rollout_small_kernel(RolloutSma
   __syncthreads();
   const int b = blockIdx.x, B = c.B, N = c.N, K = c.K, Nn = ra.Nn, Tmax = ra.Tmax;
   const long nk = (long)N * K;
-  const int wave = threadIdx.x / WAVE;
+  const int wave = wave_id();
   int T = -1;                  // horizon, once every env has published its first done step
   bool done = false;           // (thread 0) this env has published
   for (int t = 0; t <= Tmax; ++t) {
@@ -2228,22 +2228,21 @@ size_t bptt_small_lds() { return ctrl_node_bwd_lds() > ctrl_edge_bwd_lds() ? ctr
 }  // namespace MB_PREC
 }  // namespace mb
 
-#if MB_X3
 #include "ctrl16.h"
 #include "node16.h"
-#endif
+
+// kernel 0: CBF backward (cbf16.h), 1: edge backward (ctrl16.h), 2: node backward (node16.h)
+extern "C" int MB_SYM(k16_wg_per_cu)(int kernel) {
+  return kernel == 0 ? CBF16_WGPC : kernel == 1 ? mb::MB_PREC::E16_WG_PER_CU : 1;
+}
 
 extern "C" int MB_SYM(ctrl_node_bwd)(const mb::CtrlNodeBwdArgs* a, int num_blocks, hipStream_t st) {
   using namespace mb;
   using namespace mb::MB_PREC;
-  if (a->wrm16) {   // 16x16x32 kernel, two waves per SIMD (x3 build, 128-agent chunks)
-#if MB_X3
+  if (a->wrm16) {   // 16x16x32 kernel (csrc/node16.h; 128-agent chunks)
     if (a->dim == 3) launch_ctrl_node_bwd16<3>(*a, num_blocks, st);
     else launch_ctrl_node_bwd16<2>(*a, num_blocks, st);
     return (int)hipGetLastError();
-#else
-    return -8;
-#endif
   }
   const size_t lds = ctrl_node_bwd_lds();
   CtrlNodeBwdArgs b = *a;
@@ -2262,15 +2261,11 @@ extern "C" int MB_SYM(ctrl_edge_bwd)(const mb::CtrlEdgeBwdArgs* a, int num_block
   using namespace mb;
   using namespace mb::MB_PREC;
   if (a->K > 16 || a->K < 1) return -1;
-  if (a->w16) {   // 16x16x32 kernel, two waves per SIMD (x3 build, K = 12)
-#if MB_X3
+  if (a->w16) {   // 16x16x32 kernel (csrc/ctrl16.h; K = 12)
     if (a->K != 12) return -7;
     if (a->dim == 3) launch_ctrl_edge_bwd16<3>(*a, num_blocks, st);
     else launch_ctrl_edge_bwd16<2>(*a, num_blocks, st);
     return (int)hipGetLastError();
-#else
-    return -8;
-#endif
   }
   const size_t lds = ctrl_edge_bwd_lds();
   // K = 12 (TOP_K): constant-K instantiation (A/B vs runtime K: 136.7 vs 137.1-139.6 us, PERF.md)

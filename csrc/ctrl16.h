@@ -1,4 +1,5 @@
-// 16x16x32 x3 controller edge backward (the fp32-accurate BPTT edge step at TWO waves per SIMD).
+// 16x16x32 controller edge backward: the fp32-accurate x3 BPTT edge step at TWO waves per SIMD, and
+// the same kernel in the 1-pass bf16 / fp16 builds (no lo planes: two workgroups per CU).
 //
 // Same math as edge_bwd_body (ctrl.hip): per edge of the 1024-agent step, layer-1 recompute
 // H1 = relu(W1 [s_i - s_j, eye, 1]), the max-pool backward (dP of each pooled feature routed to
@@ -20,14 +21,15 @@ constexpr int E16_NW = 8, E16_AG = 16, E16_CH = E16_NW * E16_AG;   // waves, age
 constexpr int E16_SZ = 144, E16_SH = 68;                           // dZ / H1 image strides (bank model)
 constexpr int E16_PL = E16_CH * (E16_SZ + E16_SH);                 // lo-plane offset (elements)
 constexpr int E16_FRAGS = 22;                                      // ew1f16 4 | ew2tn16 16 | ew1ft16 2
-constexpr size_t E16_LDS = (size_t)E16_FRAGS * FRAG_SZ + (size_t)2 * E16_PL * 2;
-static_assert(E16_LDS <= 160 * 1024 - 1024, "LDS budget");
+constexpr size_t E16_LDS = (size_t)E16_FRAGS * FRAG_SZ + (size_t)(X3 ? 2 : 1) * E16_PL * 2;
+constexpr int E16_WG_PER_CU = E16_WGPC;
+static_assert(E16_LDS <= 160 * 1024 / E16_WG_PER_CU - 1024, "LDS budget");
 
 template <int D>
 struct E16Idx { int j, b, i, slot; bool ok; };
 
 template <int D>
-__global__ __launch_bounds__(E16_NW * 64) void ctrl_edge_bwd16_kernel(CtrlEdgeBwdArgs a) {
+__global__ __launch_bounds__(E16_NW * 64, 2 * E16_WG_PER_CU) void ctrl_edge_bwd16_kernel(CtrlEdgeBwdArgs a) {
   constexpr int K = 12;                           // TOP_K (the host falls back to the 32x32 kernel)
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   h16* wf = reinterpret_cast<h16*>(smem);
@@ -35,7 +37,7 @@ __global__ __launch_bounds__(E16_NW * 64) void ctrl_edge_bwd16_kernel(CtrlEdgeBw
   h16* imH = imZ + E16_CH * E16_SZ;                                        // H1 [128][E16_SH]
   block_copy16(wf, a.w16, E16_FRAGS * FRAG_SZ);
   __syncthreads();
-  const int wave = threadIdx.x / WAVE, lane = threadIdx.x & 63, n = lane & 15, g = lane >> 4;
+  const int wave = wave_id(), lane = threadIdx.x & 63, n = lane & 15, g = lane >> 4;
   const int r = lane & 31, h = lane >> 5;         // max-pool lanes: features 4r..4r+3, agent half h
   const int N = a.N, total = a.B * N;
   const long nchunks = (total + E16_CH - 1) / E16_CH;
@@ -94,7 +96,7 @@ __global__ __launch_bounds__(E16_NW * 64) void ctrl_edge_bwd16_kernel(CtrlEdgeBw
           am[p] = *reinterpret_cast<const unsigned*>(a.argmax + bb * (int)a.am_env + ii * 128 + 4 * r);
           const h16* dpr = a.dP + bb * (int)a.dp_env + ii * PROW + 4 * r;
           dp[p] = *reinterpret_cast<const h16x4*>(dpr);
-          dl[p] = *reinterpret_cast<const h16x4*>(dpr + 128);
+          if constexpr (X3) dl[p] = *reinterpret_cast<const h16x4*>(dpr + 128);
         }
       }
     };
@@ -139,7 +141,7 @@ __global__ __launch_bounds__(E16_NW * 64) void ctrl_edge_bwd16_kernel(CtrlEdgeBw
         for (int c = 0; c < 4; ++c) {
           const int rr = row0 + 4 * c + (lane >> 4);
           *reinterpret_cast<u32x4*>(imZ + rr * E16_SZ + 8 * (lane & 15)) = z4;
-          *reinterpret_cast<u32x4*>(imZ + E16_PL + rr * E16_SZ + 8 * (lane & 15)) = z4;
+          if constexpr (X3) *reinterpret_cast<u32x4*>(imZ + E16_PL + rr * E16_SZ + 8 * (lane & 15)) = z4;
         }
         lds_wave_sync();
 #pragma unroll
@@ -152,7 +154,7 @@ __global__ __launch_bounds__(E16_NW * 64) void ctrl_edge_bwd16_kernel(CtrlEdgeBw
             if (sl < 16u && (unsigned)row < (unsigned)E16_AG) {
               const int o = (row0 + row) * E16_SZ + 4 * r + jj;
               imZ[o] = dp[p][jj];
-              imZ[E16_PL + o] = dl[p][jj];
+              if constexpr (X3) imZ[E16_PL + o] = dl[p][jj];
             }
           }
         }
@@ -167,7 +169,7 @@ __global__ __launch_bounds__(E16_NW * 64) void ctrl_edge_bwd16_kernel(CtrlEdgeBw
         for (int s = 0; s < 4; ++s) {
           Fr bz;
           bz.h = *reinterpret_cast<const h16x8*>(zr + 32 * s);
-          bz.l = *reinterpret_cast<const h16x8*>(zr + E16_PL + 32 * s);
+          if constexpr (X3) bz.l = *reinterpret_cast<const h16x8*>(zr + E16_PL + 32 * s);
 #pragma unroll
           for (int mt = 0; mt < 4; ++mt) c[mt] = mma16(frag_fr(wf, 4 + 4 * mt + s, lane), bz, c[mt]);
         }
@@ -228,7 +230,7 @@ __global__ __launch_bounds__(E16_NW * 64) void ctrl_edge_bwd16_kernel(CtrlEdgeBw
         for (int mt = 0; mt < 4; ++mt) {
           Fr A;
           A.h = tr_pair16(imZ, E16_SZ, rb, 4, 16 * mt + 4 * (lane & 3), lane);
-          A.l = tr_pair16(imZ, E16_SZ, rb, 4, 64 + 16 * mt + 4 * (lane & 3), lane);
+          if constexpr (X3) A.l = tr_pair16(imZ, E16_SZ, rb, 4, 64 + 16 * mt + 4 * (lane & 3), lane);
           accC[mt] = mma16_bx(A, bf, accC[mt]);
         }
         lds_wave_sync();                      // reads done before the next tile's zero fill

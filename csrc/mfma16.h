@@ -1,9 +1,24 @@
-// 16x16x32 x3 building blocks shared by csrc/cbf16.h and csrc/ctrl16.h (fp32-accurate split-bf16
-// operands, v_mfma_f32_16x16x32_bf16; lane l: n = l & 15, g = l >> 4).
+// 16x16x32 building blocks shared by csrc/cbf16.h, csrc/ctrl16.h and csrc/node16.h
+// (v_mfma_f32_16x16x32_bf16 / _f16; lane l: n = l & 15, g = l >> 4). x3 build: fp32-accurate
+// split operands (hi + lo planes, three MFMAs per product); the 1-pass builds (bf16 / fp16, prec.h)
+// carry only the hi plane -- the `l` members are never written or read and the lo-plane reads
+// and stores compile away.
 //   A (16x32): elem j = A[n][8g + j]   B (32x16): elem j = B[8g + j][n]   C: reg i = C[4g + i][n]
 // A packed C tile (Pk4) is the B operand of the next layer with k(8g + j) = 32s + 16(j >> 2) + 4g +
 // (j & 3) for the tile pair (2s, 2s + 1) (layout.kacc16); weights are packed to match.
 #pragma once
+
+// Workgroups per CU of the 8-wave CBF (cbf16.h) and edge (ctrl16.h) backward kernels: one (two
+// waves per SIMD at <= 256 registers). The 1-pass builds fit two in LDS (<= 80 KiB each) but only
+// at <= 128 registers: the CBF kernel then spills 96 registers, the edge kernel 6, and both run
+// slower (bf16 headline 6.48 vs 6.25 ms, profiles/r4_k16/) -- -DCBF16_WGPC=2 / -DE16_WGPC=2 build
+// that variant (scripts/build_variant.sh). The launch grids follow (mb_k16_wg_per_cu).
+#ifndef CBF16_WGPC
+#define CBF16_WGPC 1
+#endif
+#ifndef E16_WGPC
+#define E16_WGPC 1
+#endif
 
 namespace mb {
 namespace MB_PREC {
@@ -11,16 +26,22 @@ namespace MB_PREC {
 struct Pk4 { h16x4 h, l; };
 
 DEV f32x4 mfma16(const h16x8& a, const h16x8& b, const f32x4& c) {
+#if MB_FP16
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+#else
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+#endif
 }
-// x3 product, small terms first (same order as mma())
+// x3 product, small terms first (same order as mma()); one MFMA in the 1-pass builds
 DEV f32x4 mma16(const Fr& a, const Fr& b, f32x4 c) {
-  c = mfma16(a.l, b.h, c);
-  c = mfma16(a.h, b.l, c);
+  if constexpr (X3) {
+    c = mfma16(a.l, b.h, c);
+    c = mfma16(a.h, b.l, c);
+  }
   return mfma16(a.h, b.h, c);
 }
 DEV f32x4 mma16_bx(const Fr& a, const h16x8& b, f32x4 c) {
-  c = mfma16(a.l, b, c);
+  if constexpr (X3) c = mfma16(a.l, b, c);
   return mfma16(a.h, b, c);
 }
 DEV f32x4 zero4() { return f32x4{0.f, 0.f, 0.f, 0.f}; }
@@ -34,7 +55,7 @@ DEV Pk4 to_pk4(const f32x4& c) {
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     p.h[i] = (h16)c[i];
-    p.l[i] = (h16)(c[i] - (float)p.h[i]);
+    if constexpr (X3) p.l[i] = (h16)(c[i] - (float)p.h[i]);
   }
   return p;
 }
@@ -44,7 +65,7 @@ DEV Fr pk4_fr(const Pk4& t0, const Pk4& t1) {
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     f.h[i] = t0.h[i]; f.h[4 + i] = t1.h[i];
-    f.l[i] = t0.l[i]; f.l[4 + i] = t1.l[i];
+    if constexpr (X3) { f.l[i] = t0.l[i]; f.l[4 + i] = t1.l[i]; }
   }
   return f;
 }
@@ -52,11 +73,14 @@ typedef unsigned u32x2v __attribute__((ext_vector_type(2)));
 // d *= relu'(pre) with H = relu(pre) packed (both planes of d masked by H's hi plane)
 DEV void mask_pk4(Pk4& d, const Pk4& H) {
   const u32x2v m = __builtin_bit_cast(u32x2v, H.h);
-  u32x2v dh = __builtin_bit_cast(u32x2v, d.h), dl = __builtin_bit_cast(u32x2v, d.l);
+  u32x2v dh = __builtin_bit_cast(u32x2v, d.h);
   dh[0] = mask_nz16x2(dh[0], m[0]); dh[1] = mask_nz16x2(dh[1], m[1]);
-  dl[0] = mask_nz16x2(dl[0], m[0]); dl[1] = mask_nz16x2(dl[1], m[1]);
   d.h = __builtin_bit_cast(h16x4, dh);
-  d.l = __builtin_bit_cast(h16x4, dl);
+  if constexpr (X3) {
+    u32x2v dl = __builtin_bit_cast(u32x2v, d.l);
+    dl[0] = mask_nz16x2(dl[0], m[0]); dl[1] = mask_nz16x2(dl[1], m[1]);
+    d.l = __builtin_bit_cast(h16x4, dl);
+  }
 }
 // two ds_read_b64_tr_b16: lane (n, g) receives img[r1 + j][col(n)] (j < 4), img[r1 + d2 + j - 4]
 // (j >= 4), where lane (q, p) of each 16-lane group addresses row r1 + q at column c + 4p
@@ -80,14 +104,14 @@ DEV h16x8 tr16(const h16* img, int stride, int e0, int c0, int lane) {
 DEV Fr tr16_fr(const h16* img, int stride, int lo, int e0, int c0, int lane) {
   Fr r;
   r.h = tr16(img, stride, e0, c0, lane);
-  r.l = tr16(img + lo, stride, e0, c0, lane);
+  if constexpr (X3) r.l = tr16(img + lo, stride, e0, c0, lane);
   return r;
 }
 // store a packed C tile (rows 16mt + 4g + i of evaluation row `erow`) into an edge-major image
 DEV void store4(h16* img, int stride, int lo, int erow, int mt, int g, const Pk4& v) {
   h16* p = img + erow * stride + 16 * mt + 4 * g;
   *reinterpret_cast<h16x4*>(p) = v.h;
-  *reinterpret_cast<h16x4*>(p + lo) = v.l;
+  if constexpr (X3) *reinterpret_cast<h16x4*>(p + lo) = v.l;
 }
 // row-major slab tile write: rows 16mt + 4g + i, column 16nt + n
 DEV void write_tile16(float* P, int ncols, int mt, int nt, const f32x4& c, int lane) {

@@ -1,4 +1,5 @@
-// 16x16x32 x3 controller NODE backward: the fp32-accurate BPTT node step at TWO waves per SIMD.
+// 16x16x32 controller NODE backward: the fp32-accurate x3 BPTT node step at TWO waves per SIMD, and
+// the same kernel in the 1-pass bf16 / fp16 builds (hi planes only, one MFMA per product).
 //
 // Same math as node_bwd_body (ctrl.hip) -- per agent of the step: node MLP recompute
 // Y1 = relu(W1 [P; s]), Y2 = relu(W2 Y1 + b2), Y3 = relu(W3 Y2 + b3), y4 = W4 Y3 + b4; gain law
@@ -36,7 +37,9 @@ constexpr int N16_PL = N16_RT * N16_SW;                   // lo-plane offset of 
 // stage columns. 1: [dY3 0..63 | d4 64..79 | Y3 80..143 | Y2 144..271]  2: [dY2 0..127 | Y1 128..191]
 //                 3: [dY1 0..63 | P 64..191 | s 192..207 | 0 208..223]
 constexpr int N16_C_D4 = 64, N16_C_Y3 = 80, N16_C_Y2 = 144, N16_C_Y1 = 128, N16_C_P = 64, N16_C_S = 192;
-constexpr size_t N16_LDS = (size_t)2 * N16_RM * 2 + N16_VEC * 4 + (size_t)2 * N16_PL * 2;
+constexpr int N16_PLANES = X3 ? 2 : 1;
+constexpr size_t N16_LDS_W = (size_t)N16_PLANES * N16_RM * 2;   // weight images, hi [+ lo]
+constexpr size_t N16_LDS = N16_LDS_W + N16_VEC * 4 + (size_t)N16_PLANES * N16_PL * 2;
 // tile-major slab (floats): 32 dW2 tiles | 32 dW3 tiles | 8 x 5 dW1f tile slots | 4 dW4 tiles | b2 | b3 | b4
 constexpr int N16_SL_W2 = 0, N16_SL_W3 = 32 * 256, N16_SL_W1 = 64 * 256, N16_SL_W4 = 104 * 256;
 constexpr int N16_SL_B2 = 108 * 256, N16_SL_B3 = N16_SL_B2 + 128, N16_SL_B4 = N16_SL_B3 + 64;
@@ -49,7 +52,7 @@ DEV Fr n16_w(const h16* W, int stride, int m0, int s, int lane) {
   const h16* p = W + (m0 + (lane & 15)) * stride + 32 * s + 8 * (lane >> 4);
   Fr r;
   r.h = *reinterpret_cast<const h16x8*>(p);
-  r.l = *reinterpret_cast<const h16x8*>(p + N16_RM);
+  if constexpr (X3) r.l = *reinterpret_cast<const h16x8*>(p + N16_RM);
   return r;
 }
 // A = W^T of a column-permuted image (W2 / W3 / W4): rows = logical columns m0.., K-step s over
@@ -59,7 +62,7 @@ DEV Fr n16_wT_perm(const h16* W, int stride, int m0, int s, int lane) {
   const int colp = 32 * (m0 >> 5) + 4 * ((m0 >> 4) & 1) + 8 * p;
   Fr r;
   r.h = tr_pair16(W, stride, 32 * s + 4 * g, 16, colp, lane);
-  r.l = tr_pair16(W + N16_RM, stride, 32 * s + 4 * g, 16, colp, lane);
+  if constexpr (X3) r.l = tr_pair16(W + N16_RM, stride, 32 * s + 4 * g, 16, colp, lane);
   return r;
 }
 // A = W4^T (16 real rows: K-step elements j >= 4 would be rows 16..31, past the image): one
@@ -69,7 +72,7 @@ DEV Fr n16_w4T(const h16* W, int m0, int lane) {
   const int colp = 32 * (m0 >> 5) + 4 * ((m0 >> 4) & 1) + 8 * p;
   Fr r;
 #pragma unroll
-  for (int pl = 0; pl < 2; ++pl) {
+  for (int pl = 0; pl < N16_PLANES; ++pl) {
     const LDS_AS h16* a1 = lds_ptr(W + pl * N16_RM) + (4 * g + q) * N16_S4 + colp;
     const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4*)(a1));
     const h16x4 b4 = __builtin_bit_cast(h16x4, v);
@@ -89,7 +92,7 @@ DEV Fr n16_w1T(const h16* W, int m0, int s, int lane) {
   const int g = lane >> 4, p = lane & 3;
   Fr r;
   r.h = tr_pair16(W, N16_S1, 32 * s + 4 * g, 16, m0 + 4 * p, lane);
-  r.l = tr_pair16(W + N16_RM, N16_S1, 32 * s + 4 * g, 16, m0 + 4 * p, lane);
+  if constexpr (X3) r.l = tr_pair16(W + N16_RM, N16_S1, 32 * s + 4 * g, 16, m0 + 4 * p, lane);
   return r;
 }
 
@@ -97,8 +100,8 @@ template <int D>
 __global__ __launch_bounds__(N16_NW * 64) void ctrl_node_bwd16_kernel(CtrlNodeBwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   h16* W1 = reinterpret_cast<h16*>(smem);
-  float* vl = reinterpret_cast<float*>(smem + (size_t)2 * N16_RM * 2);
-  h16* stg = reinterpret_cast<h16*>(smem + (size_t)2 * N16_RM * 2 + N16_VEC * 4);
+  float* vl = reinterpret_cast<float*>(smem + N16_LDS_W);
+  h16* stg = reinterpret_cast<h16*>(smem + N16_LDS_W + N16_VEC * 4);
   // diagnostics: shader clock at the phase boundaries (a.stamps, normally null; [workgroup][wave][16],
   // a workgroup with several chunks keeps its last chunk's clocks; scripts/stamps_node.py --node16)
   auto stamp = [&](int k) {
@@ -108,14 +111,14 @@ __global__ __launch_bounds__(N16_NW * 64) void ctrl_node_bwd16_kernel(CtrlNodeBw
     }
   };
   stamp(0);
-  block_copy16(W1, a.wrm16, 2 * N16_RM * 2);
+  block_copy16(W1, a.wrm16, (int)N16_LDS_W);
   block_copy16(vl, a.wvec + 128, N16_VEC * 4);
   __syncthreads();
   stamp(1);
   const float* nb2 = vl;
   const float* nb3 = vl + 128;
   const float* nb4 = vl + 192;
-  const int wave = threadIdx.x / WAVE, lane = threadIdx.x & 63, n = lane & 15, g = lane >> 4;
+  const int wave = wave_id(), lane = threadIdx.x & 63, n = lane & 15, g = lane >> 4;
   const int N = a.N;
   const int total = a.B * N;
   const long nchunks = (total + N16_CH - 1) / N16_CH;
@@ -324,7 +327,7 @@ __global__ __launch_bounds__(N16_NW * 64) void ctrl_node_bwd16_kernel(CtrlNodeBw
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       Ph[s] = ok ? *reinterpret_cast<const h16x8*>(prow + 32 * s + 8 * g) : zero_h8();
-      Pl[s] = ok ? *reinterpret_cast<const h16x8*>(prow + 128 + 32 * s + 8 * g) : zero_h8();
+      if constexpr (X3) Pl[s] = ok ? *reinterpret_cast<const h16x8*>(prow + 128 + 32 * s + 8 * g) : zero_h8();
     }
     // ---- stage 2: dW2 += dY2 . Y1^T, db2
 #pragma unroll 1
@@ -354,11 +357,11 @@ __global__ __launch_bounds__(N16_NW * 64) void ctrl_node_bwd16_kernel(CtrlNodeBw
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
           *reinterpret_cast<h16x8*>(stg + trow * N16_SW + N16_C_P + 32 * s + 8 * g) = Ph[s];
-          *reinterpret_cast<h16x8*>(stg + N16_PL + trow * N16_SW + N16_C_P + 32 * s + 8 * g) = Pl[s];
+          if constexpr (X3) *reinterpret_cast<h16x8*>(stg + N16_PL + trow * N16_SW + N16_C_P + 32 * s + 8 * g) = Pl[s];
         }
         if (g < 2) {      // the state fragment is exact: zero lo plane
           *reinterpret_cast<h16x8*>(stg + trow * N16_SW + N16_C_S + 8 * g) = sfr;
-          *reinterpret_cast<h16x8*>(stg + N16_PL + trow * N16_SW + N16_C_S + 8 * g) = zero_h8();
+          if constexpr (X3) *reinterpret_cast<h16x8*>(stg + N16_PL + trow * N16_SW + N16_C_S + 8 * g) = zero_h8();
         }
       }
       __syncthreads();
@@ -386,7 +389,7 @@ __global__ __launch_bounds__(N16_NW * 64) void ctrl_node_bwd16_kernel(CtrlNodeBw
           h16* drow = a.dP + (long)b * a.dp_env + (long)i * PROW + 16 * mt + 4 * g;
           const Pk4 v = to_pk4(c);
           *reinterpret_cast<h16x4*>(drow) = v.h;
-          *reinterpret_cast<h16x4*>(drow + 128) = v.l;
+          if constexpr (X3) *reinterpret_cast<h16x4*>(drow + 128) = v.l;
         }
       } else {
         // rows 128 + 4g + q: the state slots [p - g, v] (hi: slots 0..2D-1; lane g = 0 holds rows

@@ -52,7 +52,45 @@ __global__ void probe_lane_xor_kernel(const unsigned* in, unsigned* out) {
   out[8 * 64 + lane] = __float_as_uint(sum32(f));
 }
 
+// MFMA under a wave-parity condition (the round-4 1-pass bias bug, csrc/common.h wave_id()): 8 waves;
+// per wave acc = sum_{it,u} X X^T and bias = sum_it X_{it, wave & 1} x ones, X the 16x32 fragment
+// a[it][u] (64 lanes x 8). UNIFORM: the condition on wave_id() (scalar branch); else on the wave
+// index in a VGPR (an EXEC-masked block the compiler may leave without its execz skip).
+// out: (512 threads x 4) acc + bias.
+template <bool UNIFORM>
+__global__ __launch_bounds__(512) void probe_mfma_exec_kernel(const h16* a, float* out) {
+  const int wave = UNIFORM ? wave_id() : (int)(threadIdx.x / WAVE);
+  const int lane = threadIdx.x & 63;
+  h16x8 ones;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) ones[j] = (h16)1.f;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f}, bias = {0.f, 0.f, 0.f, 0.f};
+  for (int it = 0; it < 4; ++it) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const h16x8 x = *reinterpret_cast<const h16x8*>(a + ((it * 2 + u) * 64 + lane) * 8);
+#if MB_FP16
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(x, x, acc, 0, 0, 0);
+      if ((wave & 1) == u) bias = __builtin_amdgcn_mfma_f32_16x16x32_f16(x, ones, bias, 0, 0, 0);
+#else
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x, x, acc, 0, 0, 0);
+      if ((wave & 1) == u) bias = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x, ones, bias, 0, 0, 0);
+#endif
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) out[threadIdx.x * 4 + i] = acc[i] + bias[i];
+}
+
 }  // namespace mb
+
+extern "C" int mb_probe_mfma_exec(const void* a, float* out, int uniform, hipStream_t st) {
+  if (uniform)
+    hipLaunchKernelGGL(mb::probe_mfma_exec_kernel<true>, dim3(1), dim3(512), 0, st, (const h16*)a, out);
+  else
+    hipLaunchKernelGGL(mb::probe_mfma_exec_kernel<false>, dim3(1), dim3(512), 0, st, (const h16*)a, out);
+  return (int)hipGetLastError();
+}
 
 extern "C" int mb_probe_lane_xor(const unsigned* in, unsigned* out, hipStream_t st) {
   hipLaunchKernelGGL(mb::probe_lane_xor_kernel, dim3(1), dim3(64), 0, st, in, out);

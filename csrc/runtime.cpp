@@ -359,10 +359,10 @@ class BpttDriver {
     if (fused_ && (node_chunk_ != 32 || nb_node_ != nb_edge_))
       throw std::invalid_argument("BpttDriver: the fused step needs 32-agent chunks and one grid");
     gscale_ = c.contains("gscale") ? U("gscale") : 0;   // fp16: device loss scale (or 0)
-    ew16_ = c.contains("ctrl_w16") ? U("ctrl_w16") : 0;   // x3, K = 12: 16x16x32 edge backward fragments
-    nw16_ = c.contains("node_rm16") ? U("node_rm16") : 0;  // x3, 128-agent chunks: 16x16x32 node backward images
-    if (nw16_ && (node_chunk_ != 128 || prec_ != 2 || fused_))
-      throw std::invalid_argument("BpttDriver: the 16x16x32 node backward needs x3 and 128-agent chunks");
+    ew16_ = c.contains("ctrl_w16") ? U("ctrl_w16") : 0;   // K = 12: 16x16x32 edge backward fragments
+    nw16_ = c.contains("node_rm16") ? U("node_rm16") : 0;  // 128-agent chunks: 16x16x32 node backward images
+    if (nw16_ && (node_chunk_ != 128 || fused_))
+      throw std::invalid_argument("BpttDriver: the 16x16x32 node backward needs 128-agent chunks");
     if (B_ < 1 || N_ < 1 || Nn_ < N_ || K_ < 1 || K_ > 16 || (D_ != 2 && D_ != 3) || Tmax_ < 1 || nb_node_ < 1 ||
         nb_edge_ < 1)
       throw std::invalid_argument("BpttDriver: bad dimensions");

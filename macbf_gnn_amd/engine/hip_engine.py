@@ -67,8 +67,8 @@ class HipEngine:
         # scheduling choices are class attributes (tests / A/B scripts set them); the environment
         # knobs that remain are listed in macbf_gnn_amd/knobs.py
         self.small_bptt = bool(knobs.get_int("MACBF_SMALL_BPTT", int(self.small_bptt)))
-        if cfg.num_envs % self.bptt_groups:
-            self.bptt_groups = 1
+        # instance snapshots of the class-level choices (a test may reset the class attribute)
+        self.bptt_groups = int(self.bptt_groups) if cfg.num_envs % self.bptt_groups == 0 else 1
         self._drv = None
         self._bdrv = None
         self.native_bptt = bool(knobs.get_int("MACBF_NATIVE_BPTT", int(self.native_bptt)))
@@ -185,12 +185,16 @@ class HipEngine:
         # exploration noise (reference train.py:65-67): counter-based device RNG keyed per iteration
         self.noise_key = torch.zeros(1, dtype=torch.int64, device=dev)
         self.small_ctl = torch.zeros(2, dtype=i32, device=dev)     # persistent rollout: [envs done, max step]
-        self.nb_node, self.nb_edge = native.ctrl_bwd_grids(B * N, dev, self.prec)
+        # K = 12: the 16x16x32 controller edge backward (csrc/ctrl16.h, 8-wave workgroups);
+        # MACBF_EB16=0: the 32x32x16 kernel (A/B runs). Decided before the grids (per-CU residency)
+        self.eb16_w = (self.pw.ctrl_w16 if (K == 12 and knobs.get_int("MACBF_EB16", 1)) else None)
+        eb16 = self.eb16_w is not None
+        self.nb_node, self.nb_edge = native.ctrl_bwd_grids(B * N, dev, self.prec, eb16=eb16)
         # BPTT env groups (independent chains on separate streams): per-group grids and slab rows
         Gp = self.bptt_groups
         if Gp < 1 or B % Gp:
             raise ValueError(f"bptt_groups={Gp} must divide num_envs={B}")
-        self.grp_nb = native.ctrl_bwd_grids((B // Gp) * N, dev, self.prec)
+        self.grp_nb = native.ctrl_bwd_grids((B // Gp) * N, dev, self.prec, eb16=eb16)
         # slab rows each BPTT path writes (and the slab reduction reads): exactly those, so rows no
         # path writes are never summed (the persistent small-scene BPTT: one row per env)
         self.slab_rows = (self.nb_node, self.nb_edge) if Gp == 1 else (Gp * self.grp_nb[0], Gp * self.grp_nb[1])
@@ -213,10 +217,10 @@ class HipEngine:
             ndh = native.cbf_dh_grid(2 * E, dev)
             self.loss_part = torch.zeros(ndh, native.DH_PARTIAL, dtype=f32, device=dev)
             self.blk_active = torch.zeros(ndh, dtype=i32, device=dev)
-            # x3: the 16x16x32 backward (csrc/cbf16.h, two waves per SIMD) reads cbf_compact's
-            # 16-byte records of the active evaluations; bf16 / fp16: the 32x32x16 kernel on the
-            # index list
-            self.cbf16 = self.prec == "fp32"
+            # the 16x16x32 backward (csrc/cbf16.h; x3: two waves per SIMD, 1-pass builds: four)
+            # reads cbf_compact's 16-byte records of the active evaluations; MACBF_CBF16=0: the
+            # 32x32x16 kernel on the index list (A/B runs)
+            self.cbf16 = bool(knobs.get_int("MACBF_CBF16", 1))
             self.act_list = torch.zeros(2 * E, dtype=i32, device=dev) if not self.cbf16 else None
             self.rec_list = torch.zeros(2 * E, 4, dtype=i32, device=dev) if self.cbf16 else None
             self.loss_red = torch.zeros(native.DH_PARTIAL, dtype=f32, device=dev)
@@ -224,16 +228,12 @@ class HipEngine:
             self.nev_dev = torch.zeros(1, dtype=i32, device=dev)      # [U] of the match
             self.nact_dev = torch.zeros(1, dtype=i32, device=dev)     # active evaluations
             self.hstream = torch.cuda.Stream(device=dev)              # rollout-overlapped CBF h slices
-        # x3, K = 12: the 16x16x32 controller edge backward (csrc/ctrl16.h, two waves per SIMD);
-        # MACBF_EB16=0: the 32x32x16 kernel (A/B runs)
-        self.eb16_w = (self.pw.ctrl_w16 if (self.prec == "fp32" and K == 12
-                                            and knobs.get_int("MACBF_EB16", 1)) else None)
-        # x3, 128-agent node chunks: the 16x16x32 node backward (csrc/node16.h, two waves per SIMD);
+        # 128-agent node chunks: the 16x16x32 node backward (csrc/node16.h, 8-wave workgroups);
         # MACBF_NODE16=0: the 32x32x16 kernel (A/B runs). Decided once per engine (its slab layout
         # differs, layout.ctrl_node16_grad_map): the BPTT launches cover (B / groups) x N agents,
         # the no-BPTT launch T x B x N >= that, so every node launch of this engine takes the same kernel
         Gp = self.bptt_groups
-        self.node16_w = (self.pw.node_rm16 if (self.prec == "fp32" and knobs.get_int("MACBF_NODE16", 1)
+        self.node16_w = (self.pw.node_rm16 if (knobs.get_int("MACBF_NODE16", 1)
                                                and native.node_bwd_chunk((B // Gp) * N, dev) == 128
                                                and not self.small_bptt) else None)
         self.host_dist = torch.zeros(T, B, dtype=torch.int64, pin_memory=True)
@@ -528,7 +528,7 @@ class HipEngine:
             csr_done.record(self.aux)
         S = self.S[: T + 1]
         idx = self.idx[:T]
-        nbb = native.cbf_bwd_grid(2 * E, self.dev)
+        nbb = native.cbf_bwd_grid(2 * E, self.dev, self.prec if (self.dedup and self.cbf16) else None)
         part_cbf = self._buf(self._part_cbf, nbb, native.CBF_PARTIAL)
         dE = self.dE[: 2 * E * W].view(2, T, B, N, K, W)
         idx1 = None if self.reuse else self.idx[1: T + 1]
@@ -765,7 +765,7 @@ class HipEngine:
         """(T*B)-batched buffers for the no-BPTT controller backward (sized for Tmax)."""
         if "dP" not in self._nobptt:
             TBm = self.Tmax * self.B
-            nb_n, nb_e = native.ctrl_bwd_grids(TBm * self.N, self.dev, self.prec)
+            nb_n, nb_e = native.ctrl_bwd_grids(TBm * self.N, self.dev, self.prec, eb16=self.eb16_w is not None)
             self._nobptt = {
                 "grids": (nb_n, nb_e),
                 "G": torch.zeros(TBm, self.N, self.D, dtype=torch.float32, device=self.dev),

@@ -609,8 +609,17 @@ def cbf_active(dh, nev, blk_active, act, nact=None, *, rec=None, src=None, idx=N
     return nact
 
 
-def cbf_bwd_grid(EV: int, device) -> int:
-    return max(1, min((EV + 127) // 128, num_cu(device)))
+def k16_wg_per_cu(prec, kernel: int) -> int:
+    """Workgroups per CU of the 16x16x32 backward kernel `kernel` (0 CBF, 1 edge, 2 node) of the
+    build of `prec` (csrc/mfma16.h: x3 one, the 1-pass builds two)."""
+    return int(lib().k16_wg_per_cu(L.PREC_CODE[prec], kernel))
+
+
+def cbf_bwd_grid(EV: int, device, prec=None) -> int:
+    """Workgroups of the CBF backward over EV evaluations (128 per chunk): one per CU, or as many
+    as the 16x16x32 kernel of `prec` keeps resident per CU when prec is given."""
+    per_cu = k16_wg_per_cu(prec, 0) if prec is not None else 1
+    return max(1, min((EV + 127) // 128, per_cu * num_cu(device)))
 
 
 CBF_RM16 = 128 * 80 + 64 * 144     # elements per plane of the 16x16x32 W2 | W3 images (layout.cbf_rm16)
@@ -655,13 +664,13 @@ def cbf_bwd(S, idx, dh, wpack, f_bwd, wrm, wvec, *, passes=2, dE=None, partial=N
         check(nact, torch.int32, (1,), "nact")
     f16 = _half(wpack, "wpack", prec)
     if rec is not None:
-        # 16x16x32 x3 backward over cbf_compact's records (csrc/cbf16.h)
-        if f16 != 2 or fused or src is None:
-            raise NativeError("record backward: fp32 (x3) precision, deduplicated non-fused path only")
+        # 16x16x32 backward over cbf_compact's records (csrc/cbf16.h)
+        if fused or src is None:
+            raise NativeError("record backward: deduplicated non-fused path only")
         check(rec, torch.int32, (2 * B * T * N * K, 4), "rec")
         check(nact, torch.int32, (1,), "nact")
-        check(wrm16, wpack.dtype, (2 * CBF_RM16,), "wrm16")
-        check(w16, wpack.dtype, (6 * 1024,), "w16")
+        check(wrm16, wpack.dtype, (_planes(f16) * CBF_RM16,), "wrm16")
+        check(w16, wpack.dtype, (6 * 512 * _planes(f16),), "w16")
     check(wpack, wpack.dtype, None, "wpack")
     check(wvec, torch.float32, None, "wvec")
     if wpack.numel() < (f_bwd + 70) * 512 * _planes(f16):
@@ -786,13 +795,14 @@ def node_bwd_chunk(total_agents: int, device) -> int:
     return 32
 
 
-def ctrl_bwd_grids(total_agents: int, device, prec=None):
+def ctrl_bwd_grids(total_agents: int, device, prec=None, eb16=False):
     """(node, edge) backward grids: the node kernel takes node_bwd_chunk-agent chunks, one
     workgroup per CU; the edge kernel 32*CTRL_EDGE_WAVES-agent chunks x ctrl_edge_qsplit tile
     ranges, at most as many workgroups as fit the CUs at once (4 waves: two per CU in the 16-bit
     builds; one in the fp32 (x3) build -- 322 registers, 118 KB of LDS: a grid of one per CU
     loops over two chunks instead of running a second round of workgroups, 142 -> 137 us per
-    call at 1024 x 64, profiles/r2_egrid/). MACBF_EDGE_WG_PER_CU overrides the cap."""
+    call at 1024 x 64, profiles/r2_egrid/); eb16: the 8-wave 16x16x32 kernel (same 128-agent
+    chunks, k16_wg_per_cu per CU). MACBF_EDGE_WG_PER_CU overrides the cap."""
     ca = node_bwd_chunk(total_agents, device)
     ch = (total_agents + ca - 1) // ca
     che = (total_agents + 32 * CTRL_EDGE_WAVES - 1) // (32 * CTRL_EDGE_WAVES)
@@ -800,12 +810,15 @@ def ctrl_bwd_grids(total_agents: int, device, prec=None):
     if bwd_step_fused(total_agents, device):      # one fused launch per step: one grid for both
         n = max(1, min(ch, cu))
         return n, n
-    per_cu = 1 if prec == "fp32" else 8 // CTRL_EDGE_WAVES
+    if eb16:
+        per_cu = k16_wg_per_cu(prec or "bf16", 1)
+    else:
+        per_cu = 1 if prec == "fp32" else 8 // CTRL_EDGE_WAVES
     per_cu = int(os.environ.get("MACBF_EDGE_WG_PER_CU", per_cu))
     return max(1, min(ch, cu)), max(1, min(che * ctrl_edge_qsplit(total_agents, device), per_cu * cu))
 
 
-NODE16_RM = 2 * (64 * 176 + 128 * 80 + 64 * 144 + 16 * 80)    # csrc/node16.h: both planes (layout.node_rm16)
+NODE16_RM = 64 * 176 + 128 * 80 + 64 * 144 + 16 * 80    # csrc/node16.h: elements per plane (layout.node_rm16)
 
 
 def ctrl_node_bwd(pooled, S, G, A, Gn, valid_t, wrm, offs, wvec, act_coef, dP, ego, partial, num_blocks,
@@ -865,17 +878,17 @@ def ctrl_node_bwd(pooled, S, G, A, Gn, valid_t, wrm, offs, wvec, act_coef, dP, e
     if _defer:
         return args
     if wrm16 is not None:
-        # 16x16x32 kernel (csrc/node16.h): x3, 128-agent chunks (eight 16-agent waves)
-        if f16 != 2 or args[-4] != 128:
-            raise NativeError("16x16x32 node backward: fp32 (x3) precision and 128-agent chunks only")
-        check(wrm16, wrm.dtype, (NODE16_RM,), "wrm16")
+        # 16x16x32 kernel (csrc/node16.h): 128-agent chunks (eight 16-agent waves)
+        if args[-4] != 128:
+            raise NativeError("16x16x32 node backward: 128-agent chunks only")
+        check(wrm16, wrm.dtype, (_planes(f16) * NODE16_RM,), "wrm16")
     _ok(lib().ctrl_node_bwd(*args, ptr(wrm16), stream_handle()), "ctrl_node_bwd")
 
 
 def ctrl_edge_bwd(S, idx, argmax, dP, wpack, f_ew1f, f_ew2tn, dEc, partial, num_blocks, prec=None, init=False,
                   _defer=False, w16=None):
-    """w16 (x3, K = 12): the 16x16x32 fragments (layout.ctrl_edge_packer16) -> the two-waves-per-SIMD
-    kernel (csrc/ctrl16.h); same slabs, same dEc records."""
+    """w16 (K = 12): the 16x16x32 fragments (layout.ctrl_edge_packer16) -> the 8-wave 16x16x32 kernel
+    (csrc/ctrl16.h); same slabs, same dEc records."""
     B, N, K = idx.shape
     D = dim_of(S)
     W = rec_width(D)
@@ -896,9 +909,9 @@ def ctrl_edge_bwd(S, idx, argmax, dP, wpack, f_ew1f, f_ew2tn, dEc, partial, num_
     if _defer:
         return args
     if w16 is not None:
-        if f16 != 2 or K != 12:
-            raise NativeError("16x16x32 edge backward: fp32 (x3) precision and K = 12 only")
-        check(w16, wpack.dtype, (22 * 1024,), "w16")
+        if K != 12:
+            raise NativeError("16x16x32 edge backward: K = 12 only")
+        check(w16, wpack.dtype, (22 * 512 * _planes(f16),), "w16")
     _ok(lib().ctrl_edge_bwd(*args, ptr(w16), stream_handle()), "ctrl_edge_bwd")
 
 

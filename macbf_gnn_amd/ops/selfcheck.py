@@ -50,17 +50,24 @@ def bad_rows(got, ref, tie, scale):
     return bad, float((err / tol).max()) if err.numel() else 0.0
 
 
-def abs_scales(pr, ins, dzs, prefix, layers, head=None):
-    """Per parameter: the sum over records of |per-record gradient| (float64)."""
+def abs_scales(pr, ins, dzs, prefix, layers, head=None, tie=None):
+    """Per parameter: the sum over records of |per-record gradient| (float64). With a tie mask
+    (rows), also "<name>@tie": the same sum over the tie rows only -- a relu / radius flip inside
+    the x3 error band may move a weight gradient by up to its tie rows' whole contribution."""
     out = {}
-    for li, x, dz in zip(layers, ins, dzs):
-        dz = dz.detach().abs()
-        out[f"{prefix}.{li}.weight"] = (dz.t() @ x.abs()).reshape(pr[f"{prefix}.{li}.weight"].shape)
-        out[f"{prefix}.{li}.bias"] = dz.sum(0)
-    if head is not None:
-        x, dh = head
-        out[f"{prefix}.6.weight"] = (dh.abs().unsqueeze(-1) * x.abs()).sum(0).reshape(pr[f"{prefix}.6.weight"].shape)
-        out[f"{prefix}.6.bias"] = dh.abs().sum().reshape(1)
+    masks = [("", None)] + ([("@tie", tie.reshape(-1, 1).double())] if tie is not None else [])
+    for sfx, m in masks:
+        for li, x, dz in zip(layers, ins, dzs):
+            dz = dz.detach().abs()
+            if m is not None:
+                dz = dz * m
+            out[f"{prefix}.{li}.weight{sfx}"] = (dz.t() @ x.abs()).reshape(pr[f"{prefix}.{li}.weight"].shape)
+            out[f"{prefix}.{li}.bias{sfx}"] = dz.sum(0)
+        if head is not None:
+            x, dh = head
+            dh = dh.abs() if m is None else dh.abs() * m[:, 0]
+            out[f"{prefix}.6.weight{sfx}"] = (dh.unsqueeze(-1) * x.abs()).sum(0).reshape(pr[f"{prefix}.6.weight"].shape)
+            out[f"{prefix}.6.bias{sfx}"] = dh.sum().reshape(1)
     return out
 
 
@@ -101,8 +108,9 @@ def cbf_record_oracle(p, S, rec, T, B, N, K, D):
     w1 = pr["cbf_net.0.weight"].detach().reshape(64, -1).abs()
     dz1 = grads[1 + len(pr)].detach().abs()
     rscale = (dz1 @ w1[:, :2 * D] + (dz1 @ w1[:, 2 * D + 1:2 * D + 2])) * notself
-    scales = abs_scales(pr, ins, grads[1 + len(pr):], "cbf_net", (0, 2, 4), head=(z.detach(), dh * mask))
-    return drel, tie & (mask > 0), dws, scales, rscale
+    tie = tie & (mask > 0)
+    scales = abs_scales(pr, ins, grads[1 + len(pr):], "cbf_net", (0, 2, 4), head=(z.detach(), dh * mask), tie=tie)
+    return drel, tie, dws, scales, rscale
 
 
 def edge_forward(p, S, idx, N, D):
@@ -145,7 +153,8 @@ def edge_oracle(p, S, idx, argmax, dP, N, D):
     notself = (il != ar).double().unsqueeze(-1)
     drel = grads[0] * notself                             # self pairs: +i - i cancels, the kernel writes 0
     dws = dict(zip(pr.keys(), grads[1:1 + len(pr)]))
-    scales = abs_scales(pr, [x.detach(), h1.detach()], grads[1 + len(pr):], "controller_centr_net", (0, 2))
+    scales = abs_scales(pr, [x.detach(), h1.detach()], grads[1 + len(pr):], "controller_centr_net", (0, 2),
+                        tie=tie)
     dz2 = grads[-1].detach().abs()
     s1 = (dz2 @ w2.detach().reshape(128, 64).abs()) * (z1.detach() > 0).double()
     rscale = (s1 @ w1.detach().reshape(64, -1)[:, :2 * D].abs()).reshape(B, N, K, 2 * D) * notself
@@ -196,6 +205,16 @@ def check(engine) -> dict:
     rec[E:, 1] = (e - (1 << 31)).to(torch.int32)              # e | pass << 31 as int32 (pass 1: s_{t+1})
     rec[:E, 2] = j.to(torch.int32)
     rec[E:, 2] = j.to(torch.int32)
+    # the kernel's contract (cbf_dh / cbf_compact): records carry dh = 0 outside the radius mask (h is
+    # masked there, its gradient zero) -- the kernel itself does not re-apply the mask
+    Sf = native.from_records(S).double()
+    ps = torch.cat([torch.zeros(E, dtype=torch.int64, device=dev), torch.ones(E, dtype=torch.int64, device=dev)])
+    ee = torch.cat([e, e])
+    ii, bb_, tt = (ee // K) % N, (ee // (K * N)) % B, ee // (K * N * B)
+    jj = torch.cat([j, j])
+    rel = Sf[tt + ps, bb_, ii, :D] - Sf[tt + ps, bb_, jj, :D]
+    dist = torch.sqrt((rel ** 2).sum(-1) + C.CBF_DIST_EPS_COORD * D)
+    dh = torch.where(dist <= C.OBS_RADIUS, dh.double(), torch.zeros_like(dist)).float()
     rec[:, 3] = dh.view(torch.int32)
     W = S.shape[-1]
     dE = torch.zeros(2, T, B, N, K, W, dtype=torch.float32, device=dev)

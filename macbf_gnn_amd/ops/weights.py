@@ -35,17 +35,19 @@ class PackedWeights:
         # fp32 side vectors views of another: one gather launch repacks everything
         seg16 = [L.resolve(self.ctrl_pk.index(), n), L.resolve(self.cbf_pk.index(), n),
                  L.resolve(self.node_rm.index(), n), L.resolve(self.cbf_rmp.index(), n)]
-        if self.x3:
-            seg16 = [L.x3_frags(seg16[0]), L.x3_frags(seg16[1]), L.x3_planes(seg16[2]), L.x3_planes(seg16[3])]
-            # 16x16x32 x3 CBF backward (csrc/cbf16.h): permuted W2/W3 images + layer-1 fragments
-            self.cbf_rmp16 = L.cbf_rm16(offs)
-            self.cbf_pk16 = L.cbf_packer16(offs, dim)
-            self.ctrl_pk16 = L.ctrl_edge_packer16(offs, dim)     # 16x16x32 x3 edge backward (csrc/ctrl16.h)
-            self.node_rmp16 = L.node_rm16(offs, dim)               # 16x16x32 x3 node backward (csrc/node16.h)
-            seg16 += [L.x3_planes(L.resolve(self.cbf_rmp16.index(), n)),
-                      L.x3_frags(L.resolve(self.cbf_pk16.index(), n)),
-                      L.x3_frags(L.resolve(self.ctrl_pk16.index(), n)),
-                      L.x3_planes(L.resolve(self.node_rmp16.index(), n))]
+        frags = L.x3_frags if self.x3 else (lambda a: a)       # x3: [hi | lo] per fragment
+        planes = L.x3_planes if self.x3 else (lambda a: a)     # x3: [hi plane | lo plane] per image
+        seg16 = [frags(seg16[0]), frags(seg16[1]), planes(seg16[2]), planes(seg16[3])]
+        # the 16x16x32 backward kernels (every precision): CBF (csrc/cbf16.h: permuted W2/W3 images +
+        # layer-1 fragments), controller edge (csrc/ctrl16.h) and node (csrc/node16.h)
+        self.cbf_rmp16 = L.cbf_rm16(offs)
+        self.cbf_pk16 = L.cbf_packer16(offs, dim)
+        self.ctrl_pk16 = L.ctrl_edge_packer16(offs, dim)
+        self.node_rmp16 = L.node_rm16(offs, dim)
+        seg16 += [planes(L.resolve(self.cbf_rmp16.index(), n)),
+                  frags(L.resolve(self.cbf_pk16.index(), n)),
+                  frags(L.resolve(self.ctrl_pk16.index(), n)),
+                  planes(L.resolve(self.node_rmp16.index(), n))]
         seg32 = [L.resolve(cv, n), L.resolve(bv, n)]
         self._idx16, v16 = self._concat(seg16, n, 256)
         self._idx32, v32 = self._concat(seg32, n, 64)
@@ -58,8 +60,7 @@ class PackedWeights:
         self._buf16 = torch.empty(self._idx16.numel(), dtype=self.dtype, device=dev)
         self._buf32 = torch.empty(self._idx32.numel(), dtype=torch.float32, device=dev)
         self.ctrl_w, self.cbf_w, self.ctrl_rm, self.cbf_rm = [self._buf16[o:o + m] for o, m in v16[:4]]
-        self.cbf_rm16, self.cbf_w16, self.ctrl_w16, self.node_rm16 = (
-            [self._buf16[o:o + m] for o, m in v16[4:8]] if self.x3 else (None, None, None, None))
+        self.cbf_rm16, self.cbf_w16, self.ctrl_w16, self.node_rm16 = [self._buf16[o:o + m] for o, m in v16[4:8]]
         self.ctrl_v, self.cbf_v = [self._buf32[o:o + m] for o, m in v32]
         self._cpu_src = None
         self.update()

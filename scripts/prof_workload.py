@@ -42,6 +42,8 @@ def summarize(paths):
 
 
 def run(iters, dtype, agents=None, envs=None):
+    # no start-up self-check: its kernel launches would enter the per-dispatch counter averages
+    os.environ.setdefault("MACBF_SELFCHECK", "0")
     import torch
     from macbf_gnn_amd import config as C
     from macbf_gnn_amd.engine import Trainer

@@ -98,3 +98,35 @@ def test_mfma16_layout_exact():
         for i in range(4):
             D[L.acc_row16(i, g), n] = d[l, i]
     np.testing.assert_array_equal(D, L.emu_mfma16(a, b))
+
+
+def test_mfma_under_wave_condition():
+    """The round-4 hazard (csrc/common.h wave_id()): a wave-parity-conditional MFMA. With the
+    condition on wave_id() (scalar branch) the result equals the reference for every wave; the
+    VGPR-condition build is run too and its deviation recorded (printed), documenting what the
+    hardware does with an MFMA in a block the compiler left without its execz skip."""
+    rng = np.random.default_rng(3)
+    a = rng.integers(-3, 4, size=(4, 2, 64, 8)).astype(np.float32)
+    ta = torch.tensor(a, dtype=torch.bfloat16, device=DEV).contiguous()
+    outs = {}
+    for uniform in (1, 0):
+        o = torch.full((512, 4), float("nan"), dtype=torch.float32, device=DEV)
+        assert native.lib().probe_mfma_exec(ta.data_ptr(), o.data_ptr(), uniform, native.stream_handle()) == 0
+        torch.cuda.synchronize()
+        outs[uniform] = o.cpu().numpy()
+    # reference: X (16 x 32), X[n][8g + j] = a[lane (n, g)][j]; acc = sum X X^T, bias = row sums
+    X = np.zeros((4, 2, 16, 32), np.float32)
+    for l in range(64):
+        n, g = l & 15, l >> 4
+        X[:, :, n, 8 * g:8 * g + 8] = a[:, :, l]
+    acc = sum(X[i, u] @ X[i, u].T for i in range(4) for u in range(2))
+    ref = np.zeros((512, 4), np.float32)
+    for w in range(8):
+        bias = sum(X[i, w & 1].sum(1) for i in range(4))          # (16,) per output row
+        C = acc + bias[:, None]
+        for l in range(64):
+            n, g = l & 15, l >> 4
+            ref[w * 64 + l] = C[4 * g:4 * g + 4, n]
+    np.testing.assert_array_equal(outs[1], ref)
+    dev = float(np.nanmax(np.abs(outs[0] - ref)))
+    print(f"VGPR-condition build: max |deviation| = {dev} (0: the hardware skipped the masked MFMA)")

@@ -5,12 +5,14 @@ fresh child process with the program itself right after ``--``.
 * kernel trace: a training iteration launches only ``mb::`` kernels (no ``at::native`` glue, no
   fills) and at most two copies (the sampled start states and goals);
 * PMC counters: per kernel and dispatch, the MFMA instruction count stays within 10 % of the
-  recorded baseline (``tests/data/pmc_baseline.json``; a changed count means a changed kernel
+  recorded baseline (``tests/data/pmc_baseline*.json``; a changed count means a changed kernel
   structure, which must come with a re-recorded baseline) and the LDS bank-conflict share
-  (``SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE``) does not regress by more than 5 points.
+  (``SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE``) does not regress by more than 5 points. Two
+  workloads: 512 x 8 (the fused node + edge BPTT step) and 1024 x 32 (32 K agents per step: the
+  16x16x32 node and edge backward kernels of the headline, csrc/node16.h and csrc/ctrl16.h).
 
-Re-record the baseline on an MI355X with ``MACBF_PMC_RECORD=1`` (written to
-``gpurun_out/pmc_baseline.json``; copy it to tests/data/).
+Re-record a baseline on an MI355X with ``MACBF_PMC_RECORD=1`` (written to
+``gpurun_out/pmc_baseline*.json``; copy it to tests/data/).
 """
 import csv
 import glob
@@ -24,18 +26,19 @@ import pytest
 
 pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-BASELINE = os.path.join(ROOT, "tests", "data", "pmc_baseline.json")
+WORKLOADS = {"512x8": ((), "pmc_baseline.json"),
+             "1024x32": (("--agents", "1024", "--envs", "32"), "pmc_baseline_1024x32.json")}
 COUNTERS = ["SQ_INSTS_MFMA", "SQ_INSTS_VALU", "SQ_LDS_BANK_CONFLICT", "SQ_LDS_IDX_ACTIVE", "SQ_WAVES"]
 sys.path.insert(0, os.path.join(ROOT, "scripts"))
 
 
-def _rocprof(out, args):
+def _rocprof(out, args, wl=()):
     exe = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
     if not os.path.exists(exe):
         pytest.skip("rocprofv3 not available")
     env = dict(os.environ, TMPDIR="/tmp")
     cmd = ["timeout", "-s", "KILL", "200", exe, *args, "-d", str(out), "-o", "run", "--output-format", "csv", "--",
-           sys.executable, os.path.join(ROOT, "scripts", "prof_workload.py"), "--iters", "2"]
+           sys.executable, os.path.join(ROOT, "scripts", "prof_workload.py"), "--iters", "2", *wl]
     r = subprocess.run(cmd, cwd="/tmp", env=env, capture_output=True, text=True, timeout=260)
     assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
     return out
@@ -59,18 +62,24 @@ def test_iteration_launches_only_native_kernels(tmp_path):
     assert not glue, f"non-native kernels in the training iteration: {glue}"
 
 
-def test_pmc_mfma_counts_and_lds_conflicts(tmp_path):
+@pytest.mark.parametrize("workload", sorted(WORKLOADS))
+def test_pmc_mfma_counts_and_lds_conflicts(tmp_path, workload):
     from prof_workload import summarize
-    _rocprof(tmp_path / "pmc", ["--pmc", *COUNTERS])
+    wl, fname = WORKLOADS[workload]
+    _rocprof(tmp_path / "pmc", ["--pmc", *COUNTERS], wl)
     got = summarize([_find(tmp_path / "pmc", "counter_collection.csv")])
     got = {k: v for k, v in got.items() if k.startswith("mb::")}
     if os.environ.get("MACBF_PMC_RECORD") == "1":
         os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
-        with open(os.path.join(ROOT, "gpurun_out", "pmc_baseline.json"), "w") as f:
+        with open(os.path.join(ROOT, "gpurun_out", fname), "w") as f:
             json.dump(got, f, indent=1, sort_keys=True)
-    if not os.path.exists(BASELINE):
+    baseline = os.path.join(ROOT, "tests", "data", fname)
+    if not os.path.exists(baseline):
         pytest.skip("no recorded PMC baseline")
-    base = json.load(open(BASELINE))
+    base = json.load(open(baseline))
+    if workload == "1024x32":      # the workload exists to pin these kernels
+        for k in ("mb::x3::ctrl_node_bwd16_kernel<2>", "mb::x3::ctrl_edge_bwd16_kernel<2>", "mb::x3::cbf_bwd16_kernel<2>"):
+            assert k in base, f"baseline lacks {k}"
     bad = []
     for k, b in base.items():
         if b.get("SQ_INSTS_MFMA", 0) <= 0:
