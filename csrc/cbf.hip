@@ -535,7 +535,7 @@ __global__ __launch_bounds__(NW * 64, 1) void cbf_bwd_kernel(CbfBwdArgs a) {
   // diagnostics (a.stamps, normally null): shader-clock cycles per phase summed over the chunks
   unsigned long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tck = 0;
   auto stamp = [&](int k) {
-    if (a.stamps) {
+    if (MB_STAMPS && a.stamps) {
       const unsigned long long t = __builtin_amdgcn_s_memtime();
       ph[k] += t - tck;
       tck = t;
@@ -544,7 +544,7 @@ __global__ __launch_bounds__(NW * 64, 1) void cbf_bwd_kernel(CbfBwdArgs a) {
   CbfIn<D> nx;
   if ((long)blockIdx.x < nchunks) cbf_load<FUSED, NW, D>(a, blockIdx.x, wave, r, E, EV, nx);
   for (long chunk = blockIdx.x; chunk < nchunks; chunk += gridDim.x) {
-    if (a.stamps) { tck = __builtin_amdgcn_s_memtime(); ph[7] += 1; }
+    if (MB_STAMPS && a.stamps) { tck = __builtin_amdgcn_s_memtime(); ph[7] += 1; }
     const CbfIn<D> cur = nx;
     if (chunk + gridDim.x < nchunks) cbf_load<FUSED, NW, D>(a, chunk + gridDim.x, wave, r, E, EV, nx);   // prefetch
     const EdgeCtx<D>& c = cur.c;
@@ -786,7 +786,7 @@ __global__ __launch_bounds__(NW * 64, 1) void cbf_bwd_kernel(CbfBwdArgs a) {
     }
     stamp(5);                                      // stage C+D
   }
-  if (a.stamps && lane == 0)
+  if (MB_STAMPS && a.stamps && lane == 0)
 #pragma unroll
     for (int k = 0; k < 8; ++k) a.stamps[((long)blockIdx.x * NW + wave) * 8 + k] = ph[k];
   __syncthreads();   // all stage reads done: the stage region is reused below

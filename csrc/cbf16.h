@@ -109,7 +109,11 @@ DEV void ev16_issue(const CbfBwdArgs& a, const int4& r, Ev16<D>& x) {
   }
 }
 
-template <int D>
+// ST: phase clocks (a.stamps, diagnostics) -- a separate instantiation, so the production kernel
+// has no runtime stamp branches: a branch taken right after the forward's last MFMA left its
+// VALU consumers without the MFMA result wait states on that path (the round-3 "miscompile",
+// docs/ARCHITECTURE.md "MFMA result hazard across a branch")
+template <int D, bool ST>
 __global__ __launch_bounds__(C16_NW * 64, 2 * C16_WG_PER_CU) void cbf_bwd16_kernel(CbfBwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   h16* W2 = reinterpret_cast<h16*>(smem);
@@ -151,7 +155,7 @@ __global__ __launch_bounds__(C16_NW * 64, 2 * C16_WG_PER_CU) void cbf_bwd16_kern
 
   unsigned long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tck = 0;
   auto stamp = [&](int k) {
-    if (a.stamps) {
+    if constexpr (ST) {
       const unsigned long long t = __builtin_amdgcn_s_memtime();
       ph[k] += t - tck;
       tck = t;
@@ -175,7 +179,7 @@ __global__ __launch_bounds__(C16_NW * 64, 2 * C16_WG_PER_CU) void cbf_bwd16_kern
 #endif
 
   for (long chunk = c0; chunk < nchunks; chunk += stride) {
-    if (a.stamps) { tck = __builtin_amdgcn_s_memtime(); ph[7] += 1; }
+    if constexpr (ST) { tck = __builtin_amdgcn_s_memtime(); ph[7] += 1; }
     const Ev16<D> cur = nx;
     const bool in = in_at(chunk);
 #if CBF16_REC2
@@ -393,7 +397,7 @@ __global__ __launch_bounds__(C16_NW * 64, 2 * C16_WG_PER_CU) void cbf_bwd16_kern
 #endif
   }
   }
-  if (a.stamps && lane == 0)
+  if (ST && lane == 0)
 #pragma unroll
     for (int k = 0; k < 8; ++k) a.stamps[((long)blockIdx.x * C16_NW + wave) * 8 + k] = ph[k];
 
@@ -453,8 +457,12 @@ __global__ __launch_bounds__(C16_NW * 64, 2 * C16_WG_PER_CU) void cbf_bwd16_kern
 
 template <int D>
 static void launch_cbf_bwd16(const CbfBwdArgs& a, int num_blocks, hipStream_t st) {
-  (void)hipFuncSetAttribute((const void*)cbf_bwd16_kernel<D>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)C16_LDS);
-  hipLaunchKernelGGL((cbf_bwd16_kernel<D>), dim3(num_blocks), dim3(C16_NW * 64), C16_LDS, st, a);
+  auto go = [&](auto kern) {
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)C16_LDS);
+    hipLaunchKernelGGL(kern, dim3(num_blocks), dim3(C16_NW * 64), C16_LDS, st, a);
+  };
+  if (a.stamps) go(cbf_bwd16_kernel<D, true>);
+  else go(cbf_bwd16_kernel<D, false>);
 }
 
 }  // namespace MB_PREC

@@ -100,6 +100,15 @@ DEV int opaque_zero() {
   return z;
 }
 
+// Phase clocks (a.stamps) of the 32x32x16 backward kernels: compiled only into diagnostics builds
+// (scripts/build_variant.sh stamps cbf,ctrl "-DMB_STAMPS=1"). A runtime `if (a.stamps)` block right
+// after an MFMA chain is a branch whose taken path reaches the MFMA's VALU consumers with too few
+// wait states (scripts/check_mfma_exec.py; the round-3 "miscompile" of the 16x16x32 CBF kernel, whose
+// stamps are now a template instantiation)
+#ifndef MB_STAMPS
+#define MB_STAMPS 0
+#endif
+
 // The wave's index in its workgroup as a wave-uniform (SGPR) value. Every branch on it is then a
 // scalar branch (s_cbranch_scc) rather than an EXEC-masked region. This matters for MFMAs: the
 // compiler drops the s_cbranch_execz skip of a short EXEC-masked block and lets it run with EXEC

@@ -1268,7 +1268,7 @@ DEV void node_bwd_coop(const CtrlNodeBwdArgs& a, unsigned char* smem, long c0, l
   float* vl = reinterpret_cast<float*>(smem + RM * 2);
   h16* stg = reinterpret_cast<h16*>(smem + RM * 2 + CTRL_VEC * 4);
   block_copy16(wr, a.wrm, RM * 2);
-  if (a.stamps && (threadIdx.x & 63) == 0)
+  if (MB_STAMPS && a.stamps && (threadIdx.x & 63) == 0)
     a.stamps[((long)blockIdx.x * NB_WAVES + threadIdx.x / WAVE) * 16] = __builtin_amdgcn_s_memtime();
   block_copy16(vl, a.wvec, CTRL_VEC * 4);
   __syncthreads();
@@ -1284,7 +1284,7 @@ DEV void node_bwd_coop(const CtrlNodeBwdArgs& a, unsigned char* smem, long c0, l
   // diagnostics: shader clock at the phase boundaries (a.stamps, normally null; a workgroup with
   // several chunks keeps its last chunk's clocks, slot 15 = that chunk's start)
   auto stamp = [&](int k) {
-    if (a.stamps) {
+    if (MB_STAMPS && a.stamps) {
       const unsigned long long t = __builtin_amdgcn_s_memtime();
       if (lane == 0) a.stamps[((long)blockIdx.x * NB_WAVES + wave) * 16 + k] = t;
     }
@@ -1590,7 +1590,7 @@ DEV void node_bwd_coop(const CtrlNodeBwdArgs& a, unsigned char* smem, long c0, l
       if (h == 0) P[NP_B4 + r] = ob4 + s4;
     }
   }
-  if (a.stamps) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (MB_STAMPS && a.stamps) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   stamp(14);                                           // slab stores complete
 }
 

@@ -1,12 +1,12 @@
 // 16x16x32 controller edge backward: the fp32-accurate x3 BPTT edge step at TWO waves per SIMD, and
-// the same kernel in the 1-pass bf16 / fp16 builds (no lo planes: two workgroups per CU).
+// the same kernel in the 1-pass bf16 / fp16 builds (no lo planes).
 //
 // Same math as edge_bwd_body (ctrl.hip): per edge of the 1024-agent step, layer-1 recompute
 // H1 = relu(W1 [s_i - s_j, eye, 1]), the max-pool backward (dP of each pooled feature routed to
 // the edge of its argmax slot: dZ), dH1 = W2^T dZ . relu'(H1), dL/d(s_i - s_j) = W1^T dH1, and
-// the weight gradients dW2 += dZ . H1^T, db2 += sum dZ, dW1f += dH1 . F^T. The 32x32x16 kernel
-// holds 32 edges per wave in 322 registers (one wave per SIMD, ~3x its MFMA issue time); here a
-// wave owns 16 agents (K = 12 tiles of 16 dense edge rows) and 16x16 tiles (csrc/mfma16.h), so an
+// the weight gradients dW2 += dZ . H1^T, db2 += sum dZ (fp32 sums of the routed values),
+// dW1f += dH1 . F^T. The 32x32x16 kernel holds 32 edges per wave in 322 registers (one wave per
+// SIMD, ~3x its MFMA issue time); here a wave owns 16 agents (K = 12 tiles of 16 dense edge rows) and 16x16 tiles (csrc/mfma16.h), so an
 // 8-wave workgroup (128 agents, 128 edges per tile round) runs two waves per SIMD and the shared
 // dW2 stage contracts the whole round in one barrier pair (the dZ and H1 images of 128 rows fit
 // next to the 44 KB of weight fragments). Reference op: /root/reference/controller.py:43-50
@@ -45,15 +45,15 @@ __global__ __launch_bounds__(E16_NW * 64, 2 * E16_WG_PER_CU) void ctrl_edge_bwd1
   const long nwork = nchunks * QP;
   const unsigned invK = (65536u + K - 1u) / K;
   const int row0 = wave * E16_AG;                 // this wave's rows in the round images
-  const int mb0 = 2 * (wave >> 1), nb0 = 2 * (wave & 1), ub = wave & 1;
-  f32x4 accB[2][2], biasB = zero4(), accC[4];
+  const int mb0 = 2 * (wave >> 1), nb0 = 2 * (wave & 1);
+  f32x4 accB[2][2], accC[4];
+  // db2 = sum over edges of dZ = the routed dL/dpooled values: summed in fp32 as they are routed
+  // (lane (r, h): features 4r..4r+3 of its agents; x3: hi + lo) -- no ones-operand MFMAs
+  float db2r[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int u = 0; u < 2; ++u) accB[u][0] = accB[u][1] = zero4();
 #pragma unroll
   for (int mt = 0; mt < 4; ++mt) accC[mt] = zero4();
-  h16x8 ones;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) ones[j] = (h16)1.f;
 
   for (long w = blockIdx.x; w < nwork; w += gridDim.x) {
     const long chunk = w / QP;
@@ -154,7 +154,11 @@ __global__ __launch_bounds__(E16_NW * 64, 2 * E16_WG_PER_CU) void ctrl_edge_bwd1
             if (sl < 16u && (unsigned)row < (unsigned)E16_AG) {
               const int o = (row0 + row) * E16_SZ + 4 * r + jj;
               imZ[o] = dp[p][jj];
-              if constexpr (X3) imZ[E16_PL + o] = dl[p][jj];
+              db2r[jj] += (float)dp[p][jj];
+              if constexpr (X3) {
+                imZ[E16_PL + o] = dl[p][jj];
+                db2r[jj] += (float)dl[p][jj];
+              }
             }
           }
         }
@@ -210,7 +214,6 @@ __global__ __launch_bounds__(E16_NW * 64, 2 * E16_WG_PER_CU) void ctrl_edge_bwd1
           const Fr A = tr16_fr(imZ, E16_SZ, E16_PL, 32 * ks, 16 * (mb0 + u), lane);
           accB[u][0] = mma16(A, B0, accB[u][0]);
           accB[u][1] = mma16(A, B1, accB[u][1]);
-          if (ub == u) biasB = mma16_bx(A, ones, biasB);
         }
       }
       __syncthreads();
@@ -252,11 +255,10 @@ __global__ __launch_bounds__(E16_NW * 64, 2 * E16_WG_PER_CU) void ctrl_edge_bwd1
   __syncthreads();                            // every wave is out of the loop: the region is free
   float* red = reinterpret_cast<float*>(imZ); // [wave][128] db2 rows | [wave][4 tiles][16][16] dW1f
   float* w1r = red + E16_NW * 128;
-  for (int q = threadIdx.x; q < E16_NW * 128; q += blockDim.x) red[q] = 0.f;
-  __syncthreads();
-  if (n == 0) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) red[wave * 128 + 16 * (mb0 + ub) + 4 * g + i] = biasB[i];
+  for (int jj = 0; jj < 4; ++jj) {             // the two agent halves h, then one row per feature
+    const float v = db2r[jj] + lane_xorf<32>(db2r[jj]);
+    if (h == 0) red[wave * 128 + 4 * r + jj] = v;
   }
 #pragma unroll
   for (int mt = 0; mt < 4; ++mt)

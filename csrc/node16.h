@@ -96,7 +96,9 @@ DEV Fr n16_w1T(const h16* W, int m0, int s, int lane) {
   return r;
 }
 
-template <int D>
+// ST: phase clocks (diagnostics) in a separate instantiation (no runtime stamp branches in the
+// production kernel: see cbf16.h)
+template <int D, bool ST>
 __global__ __launch_bounds__(N16_NW * 64) void ctrl_node_bwd16_kernel(CtrlNodeBwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   h16* W1 = reinterpret_cast<h16*>(smem);
@@ -105,7 +107,7 @@ __global__ __launch_bounds__(N16_NW * 64) void ctrl_node_bwd16_kernel(CtrlNodeBw
   // diagnostics: shader clock at the phase boundaries (a.stamps, normally null; [workgroup][wave][16],
   // a workgroup with several chunks keeps its last chunk's clocks; scripts/stamps_node.py --node16)
   auto stamp = [&](int k) {
-    if (a.stamps) {
+    if constexpr (ST) {
       const unsigned long long t = __builtin_amdgcn_s_memtime();
       if ((threadIdx.x & 63) == 0) a.stamps[((long)blockIdx.x * N16_NW + threadIdx.x / WAVE) * 16 + k] = t;
     }
@@ -452,15 +454,18 @@ __global__ __launch_bounds__(N16_NW * 64) void ctrl_node_bwd16_kernel(CtrlNodeBw
       }
     }
   }
-  if (a.stamps) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if constexpr (ST) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   stamp(14);                                           // slab stores complete
 }
 
 template <int D>
 static void launch_ctrl_node_bwd16(const CtrlNodeBwdArgs& a, int num_blocks, hipStream_t st) {
-  (void)hipFuncSetAttribute((const void*)ctrl_node_bwd16_kernel<D>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)N16_LDS);
-  hipLaunchKernelGGL((ctrl_node_bwd16_kernel<D>), dim3(num_blocks), dim3(N16_NW * 64), N16_LDS, st, a);
+  auto go = [&](auto kern) {
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)N16_LDS);
+    hipLaunchKernelGGL(kern, dim3(num_blocks), dim3(N16_NW * 64), N16_LDS, st, a);
+  };
+  if (a.stamps) go(ctrl_node_bwd16_kernel<D, true>);
+  else go(ctrl_node_bwd16_kernel<D, false>);
 }
 
 }  // namespace MB_PREC

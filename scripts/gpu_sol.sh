@@ -9,6 +9,7 @@ mkdir -p $O
 P1="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_MFMA"
 P2="SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_INSTS_SALU SQ_INSTS_SMEM SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_VALU SQ_INSTS_VMEM_RD"
 cd /tmp && export TMPDIR=/tmp
+export MACBF_SELFCHECK=0      # its small start-up dispatches would enter the per-dispatch averages
 n=0
 for P in "$P1" "$P2"; do
   n=$((n+1))

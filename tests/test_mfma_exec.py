@@ -32,6 +32,38 @@ def test_shipped_kernels_have_no_exec_masked_mfma():
     assert c.main(objs) == 0
 
 
+def test_hazard_scan_follows_the_taken_branch():
+    """The round-3 CBF pattern in objdump form: the forward's last MFMA, a runtime stamp branch to a
+    label right after the stamp block, and the relu read of the MFMA result at that label. The
+    fall-through path has 8 states, the taken path 1: the scan reports the 1."""
+    c = _tools()
+    text = """
+0000000000001000 <k>:
+  v_mfma_f32_16x16x32_bf16 v[132:135], v[136:139], v[88:91], v[132:135] // 000000001000: D3B50084 0612B188
+  s_cbranch_vccnz 8 // 000000001008: BF870008 <k+0x2c>
+  s_memtime s[26:27] // 00000000100C: C0900680 00000000
+  s_waitcnt lgkmcnt(0) // 000000001014: BF8CC07F
+  s_sub_u32 s1, s26, s94 // 000000001018: 80815E1A
+  s_subb_u32 s28, s27, s95 // 00000000101C: 829C5F1B
+  s_add_u32 s80, s1, s80 // 000000001020: 80505001
+  s_addc_u32 s81, s28, s81 // 000000001024: 8251511C
+  s_mov_b64 s[94:95], s[26:27] // 000000001028: BEDE011A
+  v_max_i32_e32 v148, 0, v132 // 00000000102C: 1B290880
+  s_endpgm // 000000001030: BF810000
+"""
+    hz = c.hazards_in(text)
+    assert [h[1] for h in hz] == [1], hz
+    # with the stamp branch compiled out (straight line + the compiler's nops): nothing to report
+    text2 = """
+0000000000001000 <k>:
+  v_mfma_f32_16x16x32_bf16 v[132:135], v[136:139], v[88:91], v[132:135] // 000000001000: D3B50084 0612B188
+  s_nop 7 // 000000001008: BF800007
+  v_max_i32_e32 v148, 0, v132 // 00000000100C: 1B290880
+  s_endpgm // 000000001010: BF810000
+"""
+    assert c.hazards_in(text2) == []
+
+
 def test_scan_flags_a_masked_bias_mfma(tmp_path):
     """A wave-parity-conditional MFMA with the wave index in a VGPR (the round-4 bug) is flagged;
     the same kernel with wave_id() is not."""
