@@ -258,12 +258,14 @@ __global__ __launch_bounds__(C16_NW * 64, 2 * C16_WG_PER_CU) void cbf_bwd16_kern
       if (in && g == 0) { a.dbg[3 * v] = s1; a.dbg[3 * v + 1] = s2; a.dbg[3 * v + 2] = s3; }
     }
 #endif
-    // Scheduling boundary between the forward recompute and the head backward. Measured
-    // (scripts/check_cbf16.py, profiles/r3_cbf16/variants.log): when hipcc 7.2 interleaves the
-    // two, a deterministic ~20 % of the evaluations get a wrong forward (h, dE, dW off by 2-80 %);
-    // with this barrier (or at -O1, or with other code at this point) every section matches the
-    // 32x32x16 kernel to ~1e-7 and dE matches an fp64 reference. The GPU tests
-    // (test_gpu_dedup / test_gpu_fp32 / test_gpu_cbf16) pin it.
+    // Scheduling boundary between the forward recompute and the head backward. Round 3 needed it
+    // against a deterministic ~20 % of wrong forwards; round 4 found the cause (docs/ARCHITECTURE.md
+    // "MFMA result hazard"): the runtime stamp branch that followed here was taken with the
+    // forward's last MFMA result read 1 wait state later on the taken path (8 needed; the barrier
+    // kept a second instruction in between, which happened to suffice). The stamps are now a
+    // template instantiation and the no-barrier build passes the float64-oracle tests
+    // (profiles/r4_k16/); scripts/check_mfma_exec.py checks every MFMA -> read path of the build.
+    // The barrier stays until an A/B shows the schedule without it is not slower.
 #ifndef CBF16_NO_SCHED_BARRIER
     __builtin_amdgcn_sched_barrier(0);
 #endif
