@@ -258,17 +258,11 @@ __global__ __launch_bounds__(C16_NW * 64, 2 * C16_WG_PER_CU) void cbf_bwd16_kern
       if (in && g == 0) { a.dbg[3 * v] = s1; a.dbg[3 * v + 1] = s2; a.dbg[3 * v + 2] = s3; }
     }
 #endif
-    // Scheduling boundary between the forward recompute and the head backward. Round 3 needed it
-    // against a deterministic ~20 % of wrong forwards; round 4 found the cause (docs/ARCHITECTURE.md
-    // "MFMA result hazard"): the runtime stamp branch that followed here was taken with the
-    // forward's last MFMA result read 1 wait state later on the taken path (8 needed; the barrier
-    // kept a second instruction in between, which happened to suffice). The stamps are now a
-    // template instantiation and the no-barrier build passes the float64-oracle tests
-    // (profiles/r4_k16/); scripts/check_mfma_exec.py checks every MFMA -> read path of the build.
-    // The barrier stays until an A/B shows the schedule without it is not slower.
-#ifndef CBF16_NO_SCHED_BARRIER
-    __builtin_amdgcn_sched_barrier(0);
-#endif
+    // (Round 3 kept a __builtin_amdgcn_sched_barrier(0) here against a deterministic ~20 % of wrong
+    // forwards. Round 4 found the cause -- a runtime stamp branch taken with the forward's last MFMA
+    // result read 1 wait state later, 8 needed; docs/ARCHITECTURE.md "MFMA result hazard" -- made
+    // the stamps a template instantiation, and dropped the barrier: the no-barrier build passes the
+    // float64-oracle tests and runs as fast (11.13 vs 11.13 ms, profiles/r4_validate/).)
     stamp(0);
     // ---- head backward: dW4 / db4 exact fp32 per lane, dH3pre = w4 * dh . relu'(H3)
     if (g == 0) db4 += dhv;

@@ -130,9 +130,6 @@ __global__ __launch_bounds__(E16_NW * 64, 2 * E16_WG_PER_CU) void ctrl_edge_bwd1
       Pk4 H1[4];
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt) H1[mt] = to_pk4(relu4(mma16_bx(frag_fr(wf, mt, lane), F, zero4())));
-#ifndef CTRL16_NO_SCHED_BARRIER
-      __builtin_amdgcn_sched_barrier(0);      // see cbf16.h: keep the recompute apart from what follows
-#endif
       // ---- max-pool backward: zero this wave's 16 dZ rows, route dP[f] of each tile agent to the
       //      row of (agent, argmax slot f) when that row is in the tile
       {

@@ -185,9 +185,11 @@ class HipEngine:
         # exploration noise (reference train.py:65-67): counter-based device RNG keyed per iteration
         self.noise_key = torch.zeros(1, dtype=torch.int64, device=dev)
         self.small_ctl = torch.zeros(2, dtype=i32, device=dev)     # persistent rollout: [envs done, max step]
-        # K = 12: the 16x16x32 controller edge backward (csrc/ctrl16.h, 8-wave workgroups);
-        # MACBF_EB16=0: the 32x32x16 kernel (A/B runs). Decided before the grids (per-CU residency)
-        self.eb16_w = (self.pw.ctrl_w16 if (K == 12 and knobs.get_int("MACBF_EB16", 1)) else None)
+        # K = 12, x3: the 16x16x32 controller edge backward (csrc/ctrl16.h, 8-wave workgroups); the
+        # 1-pass builds keep the 32x32x16 kernel (70 vs 78 us per call in bf16, 74 vs 89 us fp16 3-D,
+        # profiles/r4_validate/). MACBF_EB16=0/1 forces either. Decided before the grids (per-CU residency)
+        self.eb16_w = (self.pw.ctrl_w16 if (K == 12 and knobs.get_int("MACBF_EB16", int(self.prec == "fp32")))
+                       else None)
         eb16 = self.eb16_w is not None
         self.nb_node, self.nb_edge = native.ctrl_bwd_grids(B * N, dev, self.prec, eb16=eb16)
         # BPTT env groups (independent chains on separate streams): per-group grids and slab rows
@@ -217,10 +219,11 @@ class HipEngine:
             ndh = native.cbf_dh_grid(2 * E, dev)
             self.loss_part = torch.zeros(ndh, native.DH_PARTIAL, dtype=f32, device=dev)
             self.blk_active = torch.zeros(ndh, dtype=i32, device=dev)
-            # the 16x16x32 backward (csrc/cbf16.h; x3: two waves per SIMD, 1-pass builds: four)
-            # reads cbf_compact's 16-byte records of the active evaluations; MACBF_CBF16=0: the
-            # 32x32x16 kernel on the index list (A/B runs)
-            self.cbf16 = bool(knobs.get_int("MACBF_CBF16", 1))
+            # x3: the 16x16x32 backward (csrc/cbf16.h, two waves per SIMD) reads cbf_compact's
+            # 16-byte records of the active evaluations; bf16 / fp16: the 32x32x16 kernel on the
+            # index list (already two waves per SIMD there; 1635 vs 1791 us per call in bf16,
+            # profiles/r4_validate/). MACBF_CBF16=0/1 forces either (A/B runs)
+            self.cbf16 = bool(knobs.get_int("MACBF_CBF16", int(self.prec == "fp32")))
             self.act_list = torch.zeros(2 * E, dtype=i32, device=dev) if not self.cbf16 else None
             self.rec_list = torch.zeros(2 * E, 4, dtype=i32, device=dev) if self.cbf16 else None
             self.loss_red = torch.zeros(native.DH_PARTIAL, dtype=f32, device=dev)
@@ -228,7 +231,8 @@ class HipEngine:
             self.nev_dev = torch.zeros(1, dtype=i32, device=dev)      # [U] of the match
             self.nact_dev = torch.zeros(1, dtype=i32, device=dev)     # active evaluations
             self.hstream = torch.cuda.Stream(device=dev)              # rollout-overlapped CBF h slices
-        # 128-agent node chunks: the 16x16x32 node backward (csrc/node16.h, 8-wave workgroups);
+        # 128-agent node chunks: the 16x16x32 node backward (csrc/node16.h, 8-wave workgroups; every
+        # precision: 55 vs 59 us per call in bf16, 62 vs 66 us fp16 3-D, profiles/r4_validate/);
         # MACBF_NODE16=0: the 32x32x16 kernel (A/B runs). Decided once per engine (its slab layout
         # differs, layout.ctrl_node16_grad_map): the BPTT launches cover (B / groups) x N agents,
         # the no-BPTT launch T x B x N >= that, so every node launch of this engine takes the same kernel

@@ -23,10 +23,6 @@ for f in sorted(glob.glob(sys.argv[1] + "/diag_*.json")):
 PY
 timeout -k 10 600 python -u -m pytest tests -q -m gpu -p no:cacheprovider --timeout 240 --timeout-method thread > $O/gpu_tests.log 2>&1
 rc=$?; tail -15 $O/gpu_tests.log; ok $rc tests
-for v in cbf_nobar ctrl_nobar; do
-  MACBF_EXT=alt_so/$v/_C.so MACBF_SELFCHECK=0 timeout -k 10 200 python -u -m pytest tests/test_gpu_oracle16.py -q -m gpu -p no:cacheprovider --timeout 120 --timeout-method thread -k "not selfcheck" > $O/$v.log 2>&1
-  rc=$?; echo "$v rc=$rc"; tail -3 $O/$v.log; ok $rc $v
-done
 b() { local name=$1; shift; env "$@" > $O/$name.log 2>&1; local rc=$?; ok $rc $name; grep '^{' $O/$name.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('$name', round(d['ms_per_step'],3), 'ms', d['dtype'])"; }
 b bench_bf16 timeout -k 10 300 python bench.py --dtype bf16
 b bench_bf16_wg2 MACBF_EXT=alt_so/k16wg2/_C.so timeout -k 10 300 python bench.py --dtype bf16

@@ -8,10 +8,6 @@ mkdir -p $O
 ok() { local rc=$1; if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "STOP rc=$rc ($2)"; exit $rc; fi; }
 timeout -k 10 600 python -u -m pytest tests -q -m gpu -p no:cacheprovider --timeout 240 --timeout-method thread > $O/gpu_tests.log 2>&1
 rc=$?; tail -8 $O/gpu_tests.log; ok $rc tests
-for v in cbf_nobar ctrl_nobar; do
-  MACBF_EXT=alt_so/$v/_C.so MACBF_SELFCHECK=0 timeout -k 10 200 python -u -m pytest tests/test_gpu_oracle16.py -q -m gpu -p no:cacheprovider --timeout 120 --timeout-method thread -k "not selfcheck" > $O/$v.log 2>&1
-  rc=$?; echo "$v rc=$rc: $(tail -1 $O/$v.log)"; ok $rc $v
-done
 : > $O/ab.jsonl
 b() { local name=$1; shift; env "$@" > $O/$name.log 2>&1; local rc=$?; ok $rc $name
   local line=$(grep '^{' $O/$name.log | tail -1)

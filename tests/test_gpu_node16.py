@@ -73,3 +73,32 @@ def test_node16_matches_node32(N, B, extra, monkeypatch):
     for m, pn, shape, o, n in new[4]:
         if m == "controller":
             assert _rel(new[3][o:o + n], old[3][o:o + n]) <= 1e-4, pn
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "fp16"])
+def test_node16_matches_node32_1pass(dtype, monkeypatch):
+    """The 1-pass builds (round 4: the 16x16x32 node backward is their default at 128-agent chunks):
+    same step against the 32x32x16 kernel. Both round the activations to 16 bits at the same points;
+    accumulation orders differ, so a rounding can flip: bounds of the bf16 full-step tests (2e-2)."""
+    monkeypatch.setenv("MACBF_NODE_CHUNK", "128")
+    monkeypatch.setenv("MACBF_BWD_FUSED", "0")
+    out = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("MACBF_NODE16", mode)
+        from macbf_gnn_amd.engine import Trainer
+        from macbf_gnn_amd.parallel import DP
+        cfg = C.TrainConfig(num_agents=256, num_envs=2, inner_loops=8, early_stop=False, seed=0, device="hip",
+                            dtype=dtype)
+        tr = Trainer(cfg, device=DEV, dp=DP(device=DEV))
+        assert (tr.engine._node16(2 * 256) is not None) == (mode == "1")
+        s0, g, obs = tr.sample()
+        tr.engine.step(s0, g, obs)
+        torch.cuda.synchronize()
+        out[mode] = (tr.engine.Gb.clone(), tr.engine.dP.float().clone(), tr.fp.grad.clone(), tr.fp.specs)
+    new, old = out["1"], out["0"]
+    assert torch.isfinite(new[0]).all() and torch.isfinite(new[2]).all()
+    assert _rel(new[0], old[0]) <= 2e-2, _rel(new[0], old[0])
+    assert _rel(new[1], old[1]) <= 2e-2, _rel(new[1], old[1])
+    for m, pn, shape, o, n in new[3]:
+        if m == "controller":
+            assert _rel(new[2][o:o + n], old[2][o:o + n]) <= 2e-2, pn
