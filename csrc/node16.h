@@ -381,11 +381,28 @@ __global__ __launch_bounds__(N16_NW * 64) void ctrl_node_bwd16_kernel(CtrlNodeBw
     }
     stamp(8);
     // ---- [dL/dpooled; d/ds] = W1^T dY1: tiles 0..7 -> dP rows (hi | lo), tile 8 -> ego terms
+    f32x4 dpair = zero4();
+    // tiles in pairs: two independent MFMA chains per step, the next pair's W1^T reads issued
+    // while the current pair's chains run (one tile at a time left the LDS latency and the
+    // dependent 6-MFMA chain exposed nine times: 13.7 k cycles per chunk, profiles/r4_validate/)
 #pragma unroll
     for (int mt = 0; mt < 9; ++mt) {
       f32x4 c = zero4();
+      if (mt % 2 == 0 && mt + 1 < 9) {
+        f32x4 c1 = zero4();
 #pragma unroll
-      for (int s = 0; s < 2; ++s) c = mma16(n16_w1T(W1c, 16 * mt, s, lane), pk4_fr(dY1[2 * s], dY1[2 * s + 1]), c);
+        for (int s = 0; s < 2; ++s) {
+          const Fr B = pk4_fr(dY1[2 * s], dY1[2 * s + 1]);
+          c = mma16(n16_w1T(W1c, 16 * mt, s, lane), B, c);
+          c1 = mma16(n16_w1T(W1c, 16 * (mt + 1), s, lane), B, c1);
+        }
+        dpair = c1;
+      } else if (mt % 2 == 1) {
+        c = dpair;
+      } else {
+#pragma unroll
+        for (int s = 0; s < 2; ++s) c = mma16(n16_w1T(W1c, 16 * mt, s, lane), pk4_fr(dY1[2 * s], dY1[2 * s + 1]), c);
+      }
       if (mt < 8) {
         if (ok) {
           h16* drow = a.dP + (long)b * a.dp_env + (long)i * PROW + 16 * mt + 4 * g;
