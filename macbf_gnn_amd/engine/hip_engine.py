@@ -55,6 +55,8 @@ class HipEngine:
                               # during it (A/B on MI355X: neutral-to-slower, 7.63 vs 7.66 ms; off)
     small_rollout = True      # envs of <= native.SMALL_MAXN graph nodes: the whole rollout is ONE
                               # persistent launch (one workgroup per env, device-side early stop)
+    bptt_graph = False        # replay the native BPTT launch loop from HIP graphs captured per
+                              # (T, grad scale) (MACBF_BPTT_GRAPH; A/B in docs/PERF.md)
     small_bptt = False        # envs of <= native.SMALL_MAXN agents: the BPTT recursion as ONE
                               # persistent launch (one workgroup per env). Off: measured 3x slower
                               # at 32 x 1 (2.17 vs 0.69 ms) -- the per-step launches spread a small
@@ -72,6 +74,8 @@ class HipEngine:
         self._drv = None
         self._bdrv = None
         self.native_bptt = bool(knobs.get_int("MACBF_NATIVE_BPTT", int(self.native_bptt)))
+        self.bptt_graph = bool(knobs.get_int("MACBF_BPTT_GRAPH", int(self.bptt_graph)))
+        self._bptt_graphs = {}
         self.bptt = cfg.bptt
         self.reuse = cfg.reuse_nbr_idx
         # deduplicated h/h' evaluations need both roles' state gradients on the same s_t: BPTT only
@@ -264,13 +268,20 @@ class HipEngine:
             from ..ops.scenario import iteration_key
             self.noise_key.fill_(iteration_key(self.tr.cfg.seed, int(self.tr.step_count), self.tr.dp.rank, salt=0x4E4F4953))
         B, N, D = self.B, self.N, self.D
-        self.S[0, :, :N].copy_(native.to_records(s0))
+        if D == 2:
+            self.S[0, :, :N].copy_(s0)
+        else:
+            # 3-D records (x, y, z, 0 | vx, vy, vz, 0): two strided copies into the record halves
+            # (the pad lanes of S are zero from the allocation and never written)
+            r = self.S[0, :, :N].view(B, N, 2, 4)
+            r[..., 0, :3].copy_(s0[..., :3])
+            r[..., 1, :3].copy_(s0[..., 3:6])
         if self.M:
             if obs is None or tuple(obs.shape) != (B, self.M, D):
                 raise ValueError(f"expected obstacles of shape {(B, self.M, D)}")
-            # static obstacle nodes (velocity 0) in every time slice
-            ob = native.to_records(torch.cat([obs.float(), torch.zeros_like(obs, dtype=torch.float32)], -1))
-            self.S[:, :, N:].copy_(ob.unsqueeze(0).expand(self.Tmax + 1, B, self.M, self.W))
+            # static obstacle nodes in every time slice: one strided copy of the positions (their
+            # velocity and pad lanes stay zero: no kernel writes them)
+            self.S[:, :, N:, :D].copy_(obs.unsqueeze(0).expand(self.Tmax + 1, B, self.M, D))
         self.G.copy_(g)
 
     def rollout(self, s0, g, obs=None, early_stop=None):
@@ -607,7 +618,10 @@ class HipEngine:
                 slab_rows = (B, B)
             elif Gp == 1 and red_done is None and self.native_bptt:
                 # the reverse-time launch loop in C++ (csrc/runtime.cpp): same launches, same order
-                self._bdriver().run(T, gs * ACT_COEF, cur.cuda_stream)
+                if self.bptt_graph and not self.graph_mode and not torch.cuda.is_current_stream_capturing():
+                    self._bptt_graph_replay(T, gs, cur)
+                else:
+                    self._bdriver().run(T, gs * ACT_COEF, cur.cuda_stream)
             elif Gp == 1:
                 self._bptt_chain(T, slice(0, B), valid_u8, gs, rptr3, redges3, self.part_node[: self.nb_node],
                                  self.part_edge[: self.nb_edge], self.nb_node, self.nb_edge, red_done, ts, cur)
@@ -673,6 +687,23 @@ class HipEngine:
         if d is not None:
             return 1.0, d
         return float(self.tr.grad_scale), None
+
+    def _bptt_graph_replay(self, T, gs, cur):
+        """The native BPTT launch loop of horizon T as a HIP graph, captured once per (T, grad
+        scale) and replayed: the kernels, their order and their arguments are those of
+        BpttDriver.run (every buffer is allocated once per engine); the graph only removes the
+        per-launch host and dispatch cost of the 2T launches."""
+        key = (int(T), float(gs))
+        g = self._bptt_graphs.get(key)
+        if g is None:
+            g = torch.cuda.CUDAGraph()
+            side = torch.cuda.Stream(device=self.dev)
+            side.wait_stream(cur)
+            with torch.cuda.graph(g, stream=side):
+                self._bdriver().run(T, gs * ACT_COEF, side.cuda_stream)
+            cur.wait_stream(side)
+            self._bptt_graphs[key] = g
+        g.replay()
 
     def _bdriver(self):
         """The native BPTT driver over this engine's persistent buffers (checked here once)."""

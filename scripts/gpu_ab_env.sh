@@ -1,13 +1,17 @@
 #!/bin/bash
-# Interleaved A/B of an environment knob on one box: VAR=NAME VALS="0 1" ARGS="bench args"
-# ROUNDS=2 -> gpurun_out/${TAG:-ab_env}/NAME_<val>_<round>.log and one summary line per run.
+# Interleaved A/B of an environment setting on one box: bench.py $ARGS with $ENV_A vs $ENV_B, $REPS
+# repetitions; optional GPU test subset first (TESTS=...). Output: gpurun_out/${TAG:-abenv}/
 cd $GRAFT_REPO_ROOT
-O=gpurun_out/${TAG:-ab_env}
+O=gpurun_out/${TAG:-abenv}
 mkdir -p $O
-for r in $(seq ${ROUNDS:-2}); do
-  for v in ${VALS:-0 1}; do
-    f=$O/${VAR}_${v}_$r.log
-    env $VAR=$v timeout -k 10 200 python bench.py $ARGS --phases > $f 2>&1 || { tail -5 $f; exit 1; }
-    python -c "import json; d=json.loads(open('$f').read().strip().split(chr(10))[-1]); print('$VAR=$v', round(d['ms_per_step'],3), d.get('phases_ms'))"
+if [ -n "$TESTS" ]; then
+  timeout -k 10 400 python -u -m pytest $TESTS -q -m gpu -p no:cacheprovider --timeout 240 --timeout-method thread > $O/tests.log 2>&1
+  rc=$?; tail -3 $O/tests.log; if [ $rc -ne 0 ]; then echo "STOP tests rc=$rc"; exit $rc; fi
+fi
+for rep in $(seq 1 ${REPS:-3}); do
+  for v in A B; do
+    if [ $v = A ]; then E=${ENV_A:-X=1}; else E=${ENV_B:-X=1}; fi
+    env $E timeout -k 10 300 python bench.py $ARGS > $O/${v}_${rep}.log 2>&1 || { echo "STOP $v"; tail -3 $O/${v}_${rep}.log; exit 1; }
+    echo "$v ($E) $rep: $(grep '^{' $O/${v}_${rep}.log | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(round(d["ms_per_step"],3), "ms T", d["mean_T"])')"
   done
 done
