@@ -39,22 +39,26 @@ def short(name: str) -> str:
 
 
 def load(paths):
-    per = defaultdict(lambda: defaultdict(float))   # (kernel, dispatch) -> counters
+    # keyed by (pass, kernel, dispatch): the passes are separate runs of one deterministic program,
+    # so their dispatch ids coincide -- a (kernel, dispatch) key would merge the passes' dispatches
+    # and halve the dispatch count the per-dispatch averages divide by (the round-4 first table
+    # reported every MFMA / VALU column 2x too high this way)
+    per = defaultdict(lambda: defaultdict(float))   # (pass, kernel, dispatch) -> counters
     times = {}
-    for p in paths:
+    for i, p in enumerate(paths):
         for r in csv.DictReader(open(p)):
-            k = (r["Kernel_Name"], r.get("Dispatch_Id") or r.get("Correlation_Id"))
-            per[k][r["Counter_Name"]] += float(r["Counter_Value"])
+            did = r.get("Dispatch_Id") or r.get("Correlation_Id")
+            per[(i, r["Kernel_Name"], did)][r["Counter_Name"]] += float(r["Counter_Value"])
             if r.get("Start_Timestamp") and r.get("End_Timestamp"):
-                times.setdefault(k, []).append(float(r["End_Timestamp"]) - float(r["Start_Timestamp"]))
+                times.setdefault((r["Kernel_Name"], did), {})[i] = float(r["End_Timestamp"]) - float(r["Start_Timestamp"])
     agg = defaultdict(lambda: defaultdict(float))
-    for (kname, _), c in per.items():
+    for (_, kname, _), c in per.items():
         a = agg[kname]
         a["dispatches"] += 1
         for cn, v in c.items():
             a[cn] += v
     for (kname, did), ts in times.items():
-        agg[kname]["ns_sum"] += sum(ts) / len(ts)       # one duration per dispatch (passes averaged)
+        agg[kname]["ns_sum"] += sum(ts.values()) / len(ts)      # one duration per dispatch (passes averaged)
         agg[kname]["ns_n"] += 1
     return agg
 

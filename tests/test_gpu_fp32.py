@@ -132,23 +132,34 @@ def test_cbf_fwd_fp32(B, T, N):
 
 
 def test_cbf_hfwd_fp32():
-    """Deduplicated forward (row-major W2/W3 images with lo planes) == oracle h at 1e-4."""
+    """Deduplicated forward (row-major W2/W3 images with lo planes) == oracle h at 1e-4: main
+    slots on s_t, extras (every 5th slot) on s_{t+1} with their own neighbour slots; radius masks
+    exact."""
     ctrl, cbf, fp, pw = _nets(2)
     T, B, N = 3, 2, 96
     K = C.TOP_K
     S = _states((T + 1, B), N, seed=4, dens=0.6).contiguous()
     idx = torch.stack([O.knn_idx(S[t], K) for t in range(T)]).to(torch.int32).contiguous()
+    idx1 = torch.stack([O.knn_idx(S[t + 1], K) for t in range(T)]).to(torch.int32).contiguous()
     E = T * B * N * K
+    ex = torch.arange(0, E, 5, dtype=torch.int32, device=DEV)
     src = torch.full((2 * E,), -1, dtype=torch.int32, device=DEV)
-    nev = torch.tensor([E], dtype=torch.int32, device=DEV)
+    src[E:E + ex.numel()] = ex
+    nev = torch.tensor([E + ex.numel()], dtype=torch.int32, device=DEV)
     h = torch.zeros(2 * E, device=DEV)
     m = torch.zeros(2 * E, dtype=torch.uint8, device=DEV)
-    native.cbf_hfwd(S, idx, idx, src, nev, pw.cbf_w, pw.cbf_off["w1f"], pw.cbf_rm, pw.cbf_v, h, m,
-                    u_begin=0, u_end=E, prec=P32)
+    native.cbf_hfwd(S, idx, idx1, src, nev, pw.cbf_w, pw.cbf_off["w1f"], pw.cbf_rm, pw.cbf_v, h, m, prec=P32)
     torch.cuda.synchronize()
     with torch.no_grad():
         href = O.cbf_forward(cbf.params_dict(), S[:T], idx.long()).reshape(-1)
+        h1ref = O.cbf_forward(cbf.params_dict(), S[1:], idx1.long()).reshape(-1)[ex.long()]
+        _, mref = O.cbf_features(S[:T], idx.long())
+        _, m1ref = O.cbf_features(S[1:], idx1.long())
     _cmp(h[:E], href, "h", 1e-4)
+    _cmp(h[E:E + ex.numel()], h1ref, "h' extras", 1e-4)
+    assert torch.equal(m[:E].bool(), mref.reshape(-1).bool())
+    assert torch.equal(m[E:E + ex.numel()].bool(), m1ref.reshape(-1)[ex.long()].bool())
+    assert m[:E].bool().any()
 
 
 @pytest.mark.parametrize("B,N", [(1, 8), (2, 32), (3, 100), (64, 1024)])
