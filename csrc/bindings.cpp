@@ -307,9 +307,10 @@ static mb::CtrlEdgeBwdArgs edge_bwd_args(EDGE_BWD_PARAMS) {
   return a;
 }
 
-static int ctrl_edge_bwd(EDGE_BWD_PARAMS, u64 w16, u64 stream) {
+static int ctrl_edge_bwd(EDGE_BWD_PARAMS, u64 w16, u64 stamps, u64 stream) {
   mb::CtrlEdgeBwdArgs a = edge_bwd_args(EDGE_BWD_ARGS);
   a.w16 = P<const h16>(w16);
+  a.stamps = P<unsigned long long>(stamps);
   return (prec == 2 ? mb_ctrl_edge_bwd_x3 : prec == 1 ? mb_ctrl_edge_bwd_f16 : mb_ctrl_edge_bwd)(&a, num_blocks, ST(stream));
 }
 

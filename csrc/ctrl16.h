@@ -28,7 +28,9 @@ static_assert(E16_LDS <= 160 * 1024 / E16_WG_PER_CU - 1024, "LDS budget");
 template <int D>
 struct E16Idx { int j, b, i, slot; bool ok; };
 
-template <int D>
+// ST: phase clocks (a.stamps, diagnostics) -- a separate instantiation, no runtime stamp branches
+// in the production kernel (docs/ARCHITECTURE.md "MFMA result hazard across a branch")
+template <int D, bool ST>
 __global__ __launch_bounds__(E16_NW * 64, 2 * E16_WG_PER_CU) void ctrl_edge_bwd16_kernel(CtrlEdgeBwdArgs a) {
   constexpr int K = 12;                           // TOP_K (the host falls back to the 32x32 kernel)
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -54,6 +56,16 @@ __global__ __launch_bounds__(E16_NW * 64, 2 * E16_WG_PER_CU) void ctrl_edge_bwd1
   for (int u = 0; u < 2; ++u) accB[u][0] = accB[u][1] = zero4();
 #pragma unroll
   for (int mt = 0; mt < 4; ++mt) accC[mt] = zero4();
+  // phases: 0 loads + F + layer 1, 1 max-pool routing, 2 dH1 + dF + dEc, 3 H1 stage store,
+  // 4 first barrier, 5 S1 + second barrier, 6 S2; slot 7 counts tiles
+  unsigned long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tck = 0;
+  auto stamp = [&](int k) {
+    if constexpr (ST) {
+      const unsigned long long t = __builtin_amdgcn_s_memtime();
+      ph[k] += t - tck;
+      tck = t;
+    }
+  };
 
   for (long w = blockIdx.x; w < nwork; w += gridDim.x) {
     const long chunk = w / QP;
@@ -113,6 +125,7 @@ __global__ __launch_bounds__(E16_NW * 64, 2 * E16_WG_PER_CU) void ctrl_edge_bwd1
     h16x4 dp_n[2], dl_n[2];
     pool_load(q0, am_n, dp_n, dl_n);
     for (int q = q0; q < q1; ++q) {
+      if constexpr (ST) { tck = __builtin_amdgcn_s_memtime(); ph[7] += 1; }
       const EdgeSt<D> cur = xs;
       const E16Idx<D> ci = xc;
       unsigned am[2];
@@ -130,6 +143,7 @@ __global__ __launch_bounds__(E16_NW * 64, 2 * E16_WG_PER_CU) void ctrl_edge_bwd1
       Pk4 H1[4];
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt) H1[mt] = to_pk4(relu4(mma16_bx(frag_fr(wf, mt, lane), F, zero4())));
+      stamp(0);
       // ---- max-pool backward: zero this wave's 16 dZ rows, route dP[f] of each tile agent to the
       //      row of (agent, argmax slot f) when that row is in the tile
       {
@@ -161,6 +175,7 @@ __global__ __launch_bounds__(E16_NW * 64, 2 * E16_WG_PER_CU) void ctrl_edge_bwd1
         }
         lds_wave_sync();
       }
+      stamp(1);
       // ---- dH1 = W2^T dZ . relu'(H1): B = this edge's dZ row (natural k, one 16-byte read per plane)
       Pk4 D1[4];
       {
@@ -198,10 +213,13 @@ __global__ __launch_bounds__(E16_NW * 64, 2 * E16_WG_PER_CU) void ctrl_edge_bwd1
           store_rec<D>(a.dEc, (unsigned)(ci.b * (int)a.de_env + ci.i * K + ci.slot), gp, gv);
         }
       }
+      stamp(2);
       // ---- S1: dW2 (128 x 64) += dZ . H1^T, db2 over the round's 128 edges (one barrier pair)
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt) store4(imH, E16_SH, E16_PL, row0 + n, mt, g, H1[mt]);
+      stamp(3);
       __syncthreads();
+      stamp(4);
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
         const Fr B0 = tr16_fr(imH, E16_SH, E16_PL, 32 * ks, 16 * nb0, lane);
@@ -214,6 +232,7 @@ __global__ __launch_bounds__(E16_NW * 64, 2 * E16_WG_PER_CU) void ctrl_edge_bwd1
         }
       }
       __syncthreads();
+      stamp(5);
       // ---- S2 (wave-local, no barrier): dW1f (64 x 16) += dH1 . F^T over this wave's 16 edges;
       //      images in the wave's own dZ rows (free after S1): dH1 hi cols 0..63, lo 64..127, F
       //      128..143; K = 32 rows per MFMA: lanes g >= 2 (rows 16..31) re-read rows 0..15 and
@@ -235,8 +254,12 @@ __global__ __launch_bounds__(E16_NW * 64, 2 * E16_WG_PER_CU) void ctrl_edge_bwd1
         }
         lds_wave_sync();                      // reads done before the next tile's zero fill
       }
+      stamp(6);
     }
   }
+  if (ST && lane == 0)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) a.stamps[((long)blockIdx.x * E16_NW + wave) * 8 + k] = ph[k];
   // ---- slab: dW2 tiles (one owner each), db2 rows and dW1f summed over the waves in fixed order
   float* P = a.partial + (long)blockIdx.x * CTRL_EDGE_PARTIAL;
   const bool acc = !a.init;
@@ -280,9 +303,12 @@ __global__ __launch_bounds__(E16_NW * 64, 2 * E16_WG_PER_CU) void ctrl_edge_bwd1
 
 template <int D>
 static void launch_ctrl_edge_bwd16(const CtrlEdgeBwdArgs& a, int num_blocks, hipStream_t st) {
-  (void)hipFuncSetAttribute((const void*)ctrl_edge_bwd16_kernel<D>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)E16_LDS);
-  hipLaunchKernelGGL((ctrl_edge_bwd16_kernel<D>), dim3(num_blocks), dim3(E16_NW * 64), E16_LDS, st, a);
+  auto go = [&](auto kern) {
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)E16_LDS);
+    hipLaunchKernelGGL(kern, dim3(num_blocks), dim3(E16_NW * 64), E16_LDS, st, a);
+  };
+  if (a.stamps) go(ctrl_edge_bwd16_kernel<D, true>);
+  else go(ctrl_edge_bwd16_kernel<D, false>);
 }
 
 }  // namespace MB_PREC

@@ -78,7 +78,7 @@ def test_pmc_mfma_counts_and_lds_conflicts(tmp_path, workload):
         pytest.skip("no recorded PMC baseline")
     base = json.load(open(baseline))
     if workload == "1024x32":      # the workload exists to pin these kernels
-        for k in ("mb::x3::ctrl_node_bwd16_kernel<2, false>", "mb::x3::ctrl_edge_bwd16_kernel<2>",
+        for k in ("mb::x3::ctrl_node_bwd16_kernel<2, false>", "mb::x3::ctrl_edge_bwd16_kernel<2, false>",
                   "mb::x3::cbf_bwd16_kernel<2, false>"):
             assert k in base, f"baseline lacks {k}"
     bad = []
