@@ -266,7 +266,7 @@ struct CtrlEdgeBwdArgs {
   int init;                            // 1: the slabs are written, not accumulated (first BPTT step)
   int qsplit;                          // workgroups per 128-agent chunk (tile-range split; 1, 2, 4, 8, 16)
   const h16* w16;                      // x3, K = 12: 16x16x32 fragments (csrc/ctrl16.h) -> the two-waves-per-SIMD kernel
-  unsigned long long* stamps;          // diagnostics or null: [workgroup][wave][8] phase cycles (16x16x32 kernel)
+  unsigned long long* stamps;          // diagnostics or null: [workgroup][wave][16] phase cycles (16x16x32 kernel)
 };
 
 struct CsrArgs {

@@ -427,6 +427,88 @@ __global__ __launch_bounds__(NW * 64, CBF_HFWD_MINW) void cbf_hfwd_kernel(CbfFwd
 #define CBF_HFWD_PREFETCH 1
 #endif
 #endif
+// 1-pass builds: the three-stage gather pipeline below (bf16 headline 6.86-6.88 vs 6.89-6.91 ms,
+// profiles/r4_loads/); x3: no prefetch at all -- the pipeline's registers spill at the 128 of four
+// waves per SIMD (10.91-10.94 vs 10.93 ms, 3 waves per SIMD 10.96-10.98 ms)
+#ifndef CBF_HFWD_PIPE
+#if MB_X3
+#define CBF_HFWD_PIPE 0
+#else
+#define CBF_HFWD_PIPE 1
+#endif
+#endif
+#if CBF_HFWD_PIPE
+  // Gather pipeline over a wave's tiles k, k + stride, ...: the chain src[u] (extras) -> idx[e] ->
+  // S[i], S[j] is three dependent loads, so each runs one tile apart -- src three tiles ahead, idx
+  // two ahead, the two node records one ahead -- every load unconditional (clamped indices) and
+  // consumed an iteration after its issue: no memory latency inside the MFMA loop.
+  struct P0 { unsigned srcv; };
+  struct P1 { int j; unsigned e; int pass; bool in; };
+  struct P2 { float4 si[REC<D>], sj[REC<D>]; int i, j; bool in; };
+  auto tile_u = [&](unsigned tl) { return U0 + tl * 32 + r; };
+  auto s0 = [&](unsigned tl, P0& o) {
+    const unsigned u = tile_u(tl);
+    const bool pass = u < U && u >= E;
+    o.srcv = (unsigned)a.src[pass ? u : 0u];
+  };
+  auto s1 = [&](unsigned tl, const P0& x, P1& o) {
+    const unsigned u = tile_u(tl);
+    o.in = u < U;
+    o.pass = (o.in && u >= E) ? 1 : 0;
+    o.e = o.in ? (o.pass ? x.srcv : u) : 0u;
+    o.j = (o.pass ? a.idx1 : a.idx)[o.e];
+  };
+  auto s2 = [&](const P1& x, P2& o) {
+    const unsigned ik = x.e / (unsigned)a.K;
+    const unsigned tb = ik / (unsigned)a.N;
+    const unsigned i = ik - tb * (unsigned)a.N;
+    const unsigned t = tb / (unsigned)a.B;
+    const unsigned b = tb - t * (unsigned)a.B;
+    const float4* Sb = a.S + ((unsigned)b * (unsigned)a.s_env + (t + (unsigned)x.pass) * (unsigned)a.s_step) * REC<D>;
+#pragma unroll
+    for (int k = 0; k < REC<D>; ++k) { o.si[k] = Sb[REC<D> * i + k]; o.sj[k] = Sb[REC<D> * (unsigned)x.j + k]; }
+    o.i = (int)i;
+    o.j = x.j;
+    o.in = x.in;
+  };
+  const unsigned t0 = blockIdx.x * NW + wave;
+  P0 p0{};
+  P1 p1{};
+  P2 p2{};
+  {
+    // prologue: tiles t0 (-> P2), t0 + stride (-> P1), t0 + 2 stride (-> P0); tiles past the end
+    // load clamped records (never used)
+    P0 q0;
+    s0(t0, q0);
+    P1 q1;
+    s1(t0, q0, q1);
+    s2(q1, p2);
+    s0(t0 + stride, q0);
+    s1(t0 + stride, q0, p1);
+    s0(t0 + 2 * stride, p0);
+  }
+  for (unsigned tile = t0; tile < ntiles; tile += stride) {
+    const P2 cur = p2;
+    s2(p1, p2);                                   // node j of tile + stride
+    s1(tile + 2 * stride, p0, p1);                // idx + node i of tile + 2 stride
+    s0(tile + 3 * stride, p0);                    // src of tile + 3 stride
+    EdgeCtx<D> c;
+    {
+      float pi[D], vi[D], pj[D], vj[D];
+      load_rec_regs<D>(cur.si, pi, vi);
+      load_rec_regs<D>(cur.sj, pj, vj);
+      c.ok = cur.in;
+#pragma unroll
+      for (int q = 0; q < D; ++q) {
+        c.rp[q] = cur.in ? pi[q] - pj[q] : 0.f;
+        c.rv[q] = cur.in ? vi[q] - vj[q] : 0.f;
+      }
+      c.eye = (cur.in && cur.j == cur.i) ? 1.f : 0.f;
+      c.d = sqrtf(sqsum<D>(c.rp) + a.dist_eps);
+      c.dfeat = cur.in ? c.d - a.dist_thr : 0.f;
+      c.mask = cur.in && c.d <= a.obs_r;
+    }
+#else
   EdgeCtx<D> nx;
   unsigned tile = blockIdx.x * NW + wave;
   if (CBF_HFWD_PREFETCH && tile < ntiles) load(tile, nx);
@@ -437,6 +519,7 @@ __global__ __launch_bounds__(NW * 64, CBF_HFWD_MINW) void cbf_hfwd_kernel(CbfFwd
 #else
     EdgeCtx<D> c;
     load(tile, c);
+#endif
 #endif
     const h16x8 F = cbf_edge_frag<D>(c.rp, c.rv, c.eye, c.dfeat, c.ok, h);
     const h16* wt = wf + opaque_zero();

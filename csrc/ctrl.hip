@@ -168,7 +168,7 @@ DEV void node_forward(PoolFr pool, const h16x8& sfrag, const h16* wn, const floa
 // loads): at tile q the kernel issues the idx load of tile q+2 and the state loads of tile
 // q+1, then computes tile q, so every load has a full tile of MFMA work to land under.
 struct EdgeIdx { int j, b, i; bool ok; };
-template <int D> struct EdgeSt { float rp[D], rv[D]; int j, i; bool ok; };
+template <int D> struct EdgeSt { float4 si[D == 2 ? 1 : 2], sj[D == 2 ? 1 : 2]; int j, i; bool ok; };   // ctrl_st_load
 
 // (env, index) of the agents g0 + al, 0 <= al < 32, of a 32-agent group: one division per group;
 // with N >= 32 the group wraps into the next env at most once (a per-tile 32-bit division by the
@@ -200,11 +200,11 @@ DEV void ctrl_idx_load(const int* idx, long i_env, int N, int K, const AgentBase
   const int slot = r & 15;
   const int gi = ab.g0 + al;
   o.ok = (q < 16) && (gi < total) && (slot < K);
-  o.b = 0; o.i = 0; o.j = 0;
-  if (o.ok) {
-    agent_bi(ab, al, N, o.b, o.i);
-    o.j = idx[o.b * (int)i_env + o.i * K + slot];
-  }
+  int bb, ii;
+  agent_bi(ab, al, N, bb, ii);
+  o.b = o.ok ? bb : 0;
+  o.i = o.ok ? ii : 0;
+  o.j = idx[o.b * (int)i_env + o.i * K + (o.ok ? slot : 0)];   // unconditional (see ctrl_st_load)
 }
 
 // dense edge rows (edge backward): a wave's 32 agents x K slots are 32K consecutive rows =
@@ -218,27 +218,49 @@ DEV void ctrl_idx_load_dense(const int* idx, long i_env, int N, int K, unsigned 
   const int slot = e - al * K;
   const int gi = ab.g0 + al;
   o.ok = (al < nag) && (gi < total);
-  o.b = 0; o.i = 0; o.j = 0;
-  if (o.ok) {
-    agent_bi(ab, al, N, o.b, o.i);
-    o.j = idx[o.b * (int)i_env + o.i * K + slot];
-  }
+  int bb, ii;
+  agent_bi(ab, al, N, bb, ii);
+  o.b = o.ok ? bb : 0;
+  o.i = o.ok ? ii : 0;
+  o.j = idx[o.b * (int)i_env + o.i * K + (o.ok ? slot : 0)];
 }
 
+// The endpoint records of an edge, loaded one tile ahead of their use. Every load is
+// unconditional (a lane without an edge reads env 0's node 0 / slot 0: ctrl_idx_load*) and the
+// relative state is formed only when the tile is processed (edge_rel): a load inside an `if`, or
+// arithmetic on its value right after it, makes the compiler wait for the load there -- one full
+// memory latency per tile (the 16x16x32 edge backward's phase clocks: 1.4 k cycles per tile).
 template <int D>
 DEV void ctrl_st_load(const float4* S, long s_env, const EdgeIdx& x, EdgeSt<D>& o) {
   o.ok = x.ok;
   o.j = x.j;
   o.i = x.i;
+  const float4* Sb = S + (x.b * (int)s_env) * REC<D>;
+  if constexpr (D == 2) {
+    o.si[0] = Sb[x.i];
+    o.sj[0] = Sb[x.j];
+  } else {
+    o.si[0] = Sb[2 * x.i]; o.si[1] = Sb[2 * x.i + 1];
+    o.sj[0] = Sb[2 * x.j]; o.sj[1] = Sb[2 * x.j + 1];
+  }
+}
+// s_i - s_j of a loaded edge (zero without an edge)
+template <int D>
+DEV void edge_rel(const EdgeSt<D>& c, float (&rp)[D], float (&rv)[D]) {
+  float pi[D], vi[D], pj[D], vj[D];
+  if constexpr (D == 2) {
+    pi[0] = c.si[0].x; pi[1] = c.si[0].y; vi[0] = c.si[0].z; vi[1] = c.si[0].w;
+    pj[0] = c.sj[0].x; pj[1] = c.sj[0].y; vj[0] = c.sj[0].z; vj[1] = c.sj[0].w;
+  } else {
+    pi[0] = c.si[0].x; pi[1] = c.si[0].y; pi[2] = c.si[0].z;
+    vi[0] = c.si[1].x; vi[1] = c.si[1].y; vi[2] = c.si[1].z;
+    pj[0] = c.sj[0].x; pj[1] = c.sj[0].y; pj[2] = c.sj[0].z;
+    vj[0] = c.sj[1].x; vj[1] = c.sj[1].y; vj[2] = c.sj[1].z;
+  }
 #pragma unroll
-  for (int q = 0; q < D; ++q) { o.rp[q] = 0.f; o.rv[q] = 0.f; }
-  if (x.ok) {
-    const float4* Sb = S + (x.b * (int)s_env) * REC<D>;
-    float pi[D], vi[D], pj[D], vj[D];
-    load_rec<D>(Sb, (unsigned)x.i, pi, vi);
-    load_rec<D>(Sb, (unsigned)x.j, pj, vj);
-#pragma unroll
-    for (int q = 0; q < D; ++q) { o.rp[q] = pi[q] - pj[q]; o.rv[q] = vi[q] - vj[q]; }
+  for (int q = 0; q < D; ++q) {
+    rp[q] = c.ok ? pi[q] - pj[q] : 0.f;
+    rv[q] = c.ok ? vi[q] - vj[q] : 0.f;
   }
 }
 
@@ -504,8 +526,10 @@ DEV void ctrl_fwd_groups(const CtrlArgs& a, const h16* wl, const h16* wn, const 
       idx_load(q + 2, xi1);                                        // idx of tile q+2
       const bool ok = cur.ok;
       const float eye = (cur.j == cur.i) ? 1.f : 0.f;
-      const bool m = ok && (sqrtf(sqsum<D>(cur.rp)) < a.obs_r);   // strict, un-eps'd (controller.py:38-39)
-      const h16x8 F = ctrl_edge_frag<D>(cur.rp, cur.rv, eye, ok, h);
+      float rp[D], rv[D];
+      edge_rel<D>(cur, rp, rv);
+      const bool m = ok && (sqrtf(sqsum<D>(rp)) < a.obs_r);   // strict, un-eps'd (controller.py:38-39)
+      const h16x8 F = ctrl_edge_frag<D>(rp, rv, eye, ok, h);
       f32x16 Z[4];
       ctrl_edge_tile(F, wl + opaque_zero(), eb2, lane, Z, HOIST_EB ? zb : nullptr);
       const unsigned mask32 = (unsigned)(__ballot(m) & 0xffffffffull);
@@ -1739,7 +1763,9 @@ DEV void edge_bwd_body(const CtrlEdgeBwdArgs& a, unsigned char* smem, long w0, l
       if (ok) agent_bi(ab, al, N, b, ib_);
       const int i = cur.i, j = cur.j;
       const float eye = (j == i) ? 1.f : 0.f;
-      const h16x8 F = ctrl_edge_frag<D>(cur.rp, cur.rv, eye, ok, h);
+      float rp[D], rv[D];
+      edge_rel<D>(cur, rp, rv);
+      const h16x8 F = ctrl_edge_frag<D>(rp, rv, eye, ok, h);
       const h16* wt = wf + opaque_zero();
       Pk H1b[2];
 #pragma unroll

@@ -56,9 +56,10 @@ __global__ __launch_bounds__(E16_NW * 64, 2 * E16_WG_PER_CU) void ctrl_edge_bwd1
   for (int u = 0; u < 2; ++u) accB[u][0] = accB[u][1] = zero4();
 #pragma unroll
   for (int mt = 0; mt < 4; ++mt) accC[mt] = zero4();
-  // phases: 0 loads + F + layer 1, 1 max-pool routing, 2 dH1 + dF + dEc, 3 H1 stage store,
-  // 4 first barrier, 5 S1 + second barrier, 6 S2; slot 7 counts tiles
-  unsigned long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tck = 0;
+  // phases (scripts/stamps_edge16.py): 0 load issue, 1 F, 2 layer 1, 3 dZ zero fill, 4 routing,
+  // 5 dH1, 6 dF + dEc, 7 H1 stage store, 8 first barrier, 9 S1, 10 second barrier, 11 S2 stores,
+  // 12 S2 contraction; slot 15 counts tiles
+  unsigned long long ph[16] = {}, tck = 0;
   auto stamp = [&](int k) {
     if constexpr (ST) {
       const unsigned long long t = __builtin_amdgcn_s_memtime();
@@ -74,17 +75,18 @@ __global__ __launch_bounds__(E16_NW * 64, 2 * E16_WG_PER_CU) void ctrl_edge_bwd1
     const int g0 = (int)(chunk * E16_CH) + row0;
     const AgentBase ab = agent_base(g0, N);
     // edge e = 16q + n of this wave's 16 x K dense rows -> (agent, slot); loads pipelined: idx two
-    // tiles ahead, states one tile ahead (as edge_bwd_body)
+    // tiles ahead, states one tile ahead (as edge_bwd_body); every load unconditional (ctrl.hip
+    // ctrl_st_load: a conditional load costs one memory latency per tile)
     auto idx_load = [&](int q, E16Idx<D>& o) {
       const int e = E16_AG * q + n;
       const int al = dense_agent(e, invK);
-      o.slot = e - al * K;
       o.ok = (q < q1) && (al < E16_AG) && (ab.g0 + al < total);
-      o.b = 0; o.i = 0; o.j = 0;
-      if (o.ok) {
-        agent_bi(ab, al, N, o.b, o.i);
-        o.j = a.idx[o.b * (int)a.i_env + o.i * K + o.slot];
-      }
+      int bb, ii;
+      agent_bi(ab, al, N, bb, ii);
+      o.b = o.ok ? bb : 0;
+      o.i = o.ok ? ii : 0;
+      o.slot = o.ok ? e - al * K : 0;
+      o.j = a.idx[o.b * (int)a.i_env + o.i * K + o.slot];
     };
     auto st_load = [&](const E16Idx<D>& x, EdgeSt<D>& o) {
       EdgeIdx xi;
@@ -92,6 +94,7 @@ __global__ __launch_bounds__(E16_NW * 64, 2 * E16_WG_PER_CU) void ctrl_edge_bwd1
       ctrl_st_load<D>(a.S, a.s_env, xi, o);
     };
     // the argmax slots / dL/dpooled of the (<= 3) agents of a tile: pass p = agents af + 2p + h
+    // (E16_AG: none; agents past `total` are dropped by the routing)
     auto pass_agent = [&](int q, int p) {
       const int af = dense_agent(E16_AG * q, invK);
       const int al = af + 2 * p + h;
@@ -101,15 +104,15 @@ __global__ __launch_bounds__(E16_NW * 64, 2 * E16_WG_PER_CU) void ctrl_edge_bwd1
 #pragma unroll
       for (int p = 0; p < 2; ++p) {
         const int al = pass_agent(q, p);
-        am[p] = 0xFFFFFFFFu;
-        if (al < E16_AG && ab.g0 + al < total) {
-          int bb, ii;
-          agent_bi(ab, al, N, bb, ii);
-          am[p] = *reinterpret_cast<const unsigned*>(a.argmax + bb * (int)a.am_env + ii * 128 + 4 * r);
-          const h16* dpr = a.dP + bb * (int)a.dp_env + ii * PROW + 4 * r;
-          dp[p] = *reinterpret_cast<const h16x4*>(dpr);
-          if constexpr (X3) dl[p] = *reinterpret_cast<const h16x4*>(dpr + 128);
-        }
+        const bool v = al < E16_AG && ab.g0 + al < total;
+        int bb, ii;
+        agent_bi(ab, al, N, bb, ii);
+        bb = v ? bb : 0;
+        ii = v ? ii : 0;
+        am[p] = *reinterpret_cast<const unsigned*>(a.argmax + bb * (int)a.am_env + ii * 128 + 4 * r);
+        const h16* dpr = a.dP + bb * (int)a.dp_env + ii * PROW + 4 * r;
+        dp[p] = *reinterpret_cast<const h16x4*>(dpr);
+        if constexpr (X3) dl[p] = *reinterpret_cast<const h16x4*>(dpr + 128);
       }
     };
     E16Idx<D> xc, xn;
@@ -125,7 +128,7 @@ __global__ __launch_bounds__(E16_NW * 64, 2 * E16_WG_PER_CU) void ctrl_edge_bwd1
     h16x4 dp_n[2], dl_n[2];
     pool_load(q0, am_n, dp_n, dl_n);
     for (int q = q0; q < q1; ++q) {
-      if constexpr (ST) { tck = __builtin_amdgcn_s_memtime(); ph[7] += 1; }
+      if constexpr (ST) { tck = __builtin_amdgcn_s_memtime(); ph[15] += 1; }
       const EdgeSt<D> cur = xs;
       const E16Idx<D> ci = xc;
       unsigned am[2];
@@ -136,14 +139,18 @@ __global__ __launch_bounds__(E16_NW * 64, 2 * E16_WG_PER_CU) void ctrl_edge_bwd1
       xc = xn;
       idx_load(q + 2, xn);
       pool_load(q + 1, am_n, dp_n, dl_n);
+      stamp(0);
       const bool ok = cur.ok;
       const bool self = cur.j == cur.i;
-      const h16x8 F = ctrl_edge_frag<D>(cur.rp, cur.rv, self ? 1.f : 0.f, ok && g < 2, g & 1);
+      float rp[D], rv[D];
+      edge_rel<D>(cur, rp, rv);
+      const h16x8 F = ctrl_edge_frag<D>(rp, rv, self ? 1.f : 0.f, ok && g < 2, g & 1);
+      stamp(1);
       // ---- layer-1 recompute
       Pk4 H1[4];
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt) H1[mt] = to_pk4(relu4(mma16_bx(frag_fr(wf, mt, lane), F, zero4())));
-      stamp(0);
+      stamp(2);
       // ---- max-pool backward: zero this wave's 16 dZ rows, route dP[f] of each tile agent to the
       //      row of (agent, argmax slot f) when that row is in the tile
       {
@@ -154,7 +161,8 @@ __global__ __launch_bounds__(E16_NW * 64, 2 * E16_WG_PER_CU) void ctrl_edge_bwd1
           *reinterpret_cast<u32x4*>(imZ + rr * E16_SZ + 8 * (lane & 15)) = z4;
           if constexpr (X3) *reinterpret_cast<u32x4*>(imZ + E16_PL + rr * E16_SZ + 8 * (lane & 15)) = z4;
         }
-        lds_wave_sync();
+        lds_wave_order();
+        stamp(3);
 #pragma unroll
         for (int p = 0; p < 2; ++p) {
           const int al = pass_agent(q, p);
@@ -162,7 +170,7 @@ __global__ __launch_bounds__(E16_NW * 64, 2 * E16_WG_PER_CU) void ctrl_edge_bwd1
           for (int jj = 0; jj < 4; ++jj) {
             const unsigned sl = (am[p] >> (8 * jj)) & 0xFFu;
             const int row = al * K + (int)sl - E16_AG * q;
-            if (sl < 16u && (unsigned)row < (unsigned)E16_AG) {
+            if (sl < 16u && (unsigned)row < (unsigned)E16_AG && ab.g0 + al < total) {
               const int o = (row0 + row) * E16_SZ + 4 * r + jj;
               imZ[o] = dp[p][jj];
               db2r[jj] += (float)dp[p][jj];
@@ -173,9 +181,9 @@ __global__ __launch_bounds__(E16_NW * 64, 2 * E16_WG_PER_CU) void ctrl_edge_bwd1
             }
           }
         }
-        lds_wave_sync();
+        lds_wave_order();
       }
-      stamp(1);
+      stamp(4);
       // ---- dH1 = W2^T dZ . relu'(H1): B = this edge's dZ row (natural k, one 16-byte read per plane)
       Pk4 D1[4];
       {
@@ -195,6 +203,7 @@ __global__ __launch_bounds__(E16_NW * 64, 2 * E16_WG_PER_CU) void ctrl_edge_bwd1
           mask_pk4(D1[mt], H1[mt]);
         }
       }
+      stamp(5);
       // ---- dF = W1^T dH1 (rows 4g + i: relative-state features) -> dL/d(s_i - s_j)
       {
         f32x4 t = zero4();
@@ -213,13 +222,13 @@ __global__ __launch_bounds__(E16_NW * 64, 2 * E16_WG_PER_CU) void ctrl_edge_bwd1
           store_rec<D>(a.dEc, (unsigned)(ci.b * (int)a.de_env + ci.i * K + ci.slot), gp, gv);
         }
       }
-      stamp(2);
+      stamp(6);
       // ---- S1: dW2 (128 x 64) += dZ . H1^T, db2 over the round's 128 edges (one barrier pair)
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt) store4(imH, E16_SH, E16_PL, row0 + n, mt, g, H1[mt]);
-      stamp(3);
+      stamp(7);
       __syncthreads();
-      stamp(4);
+      stamp(8);
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
         const Fr B0 = tr16_fr(imH, E16_SH, E16_PL, 32 * ks, 16 * nb0, lane);
@@ -231,8 +240,9 @@ __global__ __launch_bounds__(E16_NW * 64, 2 * E16_WG_PER_CU) void ctrl_edge_bwd1
           accB[u][1] = mma16(A, B1, accB[u][1]);
         }
       }
+      stamp(9);
       __syncthreads();
-      stamp(5);
+      stamp(10);
       // ---- S2 (wave-local, no barrier): dW1f (64 x 16) += dH1 . F^T over this wave's 16 edges;
       //      images in the wave's own dZ rows (free after S1): dH1 hi cols 0..63, lo 64..127, F
       //      128..143; K = 32 rows per MFMA: lanes g >= 2 (rows 16..31) re-read rows 0..15 and
@@ -241,7 +251,8 @@ __global__ __launch_bounds__(E16_NW * 64, 2 * E16_WG_PER_CU) void ctrl_edge_bwd1
 #pragma unroll
         for (int mt = 0; mt < 4; ++mt) store4(imZ, E16_SZ, 64, row0 + n, mt, g, D1[mt]);
         if (g < 2) *reinterpret_cast<h16x8*>(imZ + (row0 + n) * E16_SZ + 128 + 8 * g) = F;
-        lds_wave_sync();
+        lds_wave_order();
+        stamp(11);
         const int rb = row0 + 8 * (g & 1);
         h16x8 bf = tr_pair16(imZ, E16_SZ, rb, 4, 128 + 4 * (lane & 3), lane);
         if (g >= 2) bf = zero_h8();
@@ -252,14 +263,14 @@ __global__ __launch_bounds__(E16_NW * 64, 2 * E16_WG_PER_CU) void ctrl_edge_bwd1
           if constexpr (X3) A.l = tr_pair16(imZ, E16_SZ, rb, 4, 64 + 16 * mt + 4 * (lane & 3), lane);
           accC[mt] = mma16_bx(A, bf, accC[mt]);
         }
-        lds_wave_sync();                      // reads done before the next tile's zero fill
+        lds_wave_order();                      // reads done before the next tile's zero fill
       }
-      stamp(6);
+      stamp(12);
     }
   }
   if (ST && lane == 0)
 #pragma unroll
-    for (int k = 0; k < 8; ++k) a.stamps[((long)blockIdx.x * E16_NW + wave) * 8 + k] = ph[k];
+    for (int k = 0; k < 16; ++k) a.stamps[((long)blockIdx.x * E16_NW + wave) * 16 + k] = ph[k];
   // ---- slab: dW2 tiles (one owner each), db2 rows and dW1f summed over the waves in fixed order
   float* P = a.partial + (long)blockIdx.x * CTRL_EDGE_PARTIAL;
   const bool acc = !a.init;

@@ -20,6 +20,17 @@ DEV void load_rec(const float4* base, unsigned i, float (&p)[D], float (&v)[D]) 
   }
 }
 
+// the same unpacking from records already in registers
+template <int D>
+DEV void load_rec_regs(const float4 (&r)[REC<D>], float (&p)[D], float (&v)[D]) {
+  if constexpr (D == 2) {
+    p[0] = r[0].x; p[1] = r[0].y; v[0] = r[0].z; v[1] = r[0].w;
+  } else {
+    p[0] = r[0].x; p[1] = r[0].y; p[2] = r[0].z;
+    v[0] = r[1].x; v[1] = r[1].y; v[2] = r[1].z;
+  }
+}
+
 template <int D>
 DEV void store_rec(float4* base, unsigned i, const float (&p)[D], const float (&v)[D]) {
   if constexpr (D == 2) {

@@ -888,9 +888,9 @@ def ctrl_node_bwd(pooled, S, G, A, Gn, valid_t, wrm, offs, wvec, act_coef, dP, e
 def ctrl_edge_bwd(S, idx, argmax, dP, wpack, f_ew1f, f_ew2tn, dEc, partial, num_blocks, prec=None, init=False,
                   _defer=False, w16=None, stamps=None):
     """w16 (K = 12): the 16x16x32 fragments (layout.ctrl_edge_packer16) -> the 8-wave 16x16x32 kernel
-    (csrc/ctrl16.h); same slabs, same dEc records. stamps (num_blocks, 8, 8) int64 (diagnostics,
+    (csrc/ctrl16.h); same slabs, same dEc records. stamps (num_blocks, 8, 16) int64 (diagnostics,
     16x16x32 kernel): per wave the shader-clock cycles of each loop phase summed over its tiles
-    (slot 7: tiles), scripts/stamps_edge16.py."""
+    (slot 15: tiles), scripts/stamps_edge16.py."""
     B, N, K = idx.shape
     D = dim_of(S)
     W = rec_width(D)
@@ -917,7 +917,7 @@ def ctrl_edge_bwd(S, idx, argmax, dP, wpack, f_ew1f, f_ew2tn, dEc, partial, num_
     if stamps is not None:
         if w16 is None:
             raise NativeError("edge backward stamps: 16x16x32 kernel only")
-        check(stamps, torch.int64, (num_blocks, 8, 8), "stamps")
+        check(stamps, torch.int64, (num_blocks, 8, 16), "stamps")
     _ok(lib().ctrl_edge_bwd(*args, ptr(w16), ptr(stamps), stream_handle()), "ctrl_edge_bwd")
 
 
