@@ -120,6 +120,28 @@ DEV int opaque_zero() {
 // MFMA under a lane-divergent condition, wave-dependent conditions on wave_id().
 DEV int wave_id() { return __builtin_amdgcn_readfirstlane((int)(threadIdx.x / WAVE)); }
 
+// XCD-aware block order: the dispatcher hands consecutive workgroups to the 8 XCDs in turn (each
+// with its own L2), so a kernel whose neighbouring blocks gather from the same data (one graph's
+// edge records) re-fetches it in every XCD. xcd_block maps the blocks sharing an XCD (bid % 8,
+// a label, not the XCD id) to one contiguous range of logical blocks -- bijective for any count
+// (cdna_hip_programming.md T1). A pure speed choice: any mapping is correct.
+constexpr int NXCD = 8;
+DEV int xcd_block(int bid, int nwg) {
+  const int q = nwg / NXCD, r = nwg % NXCD, x = bid % NXCD;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / NXCD;
+}
+// BPTT_XCD: the 128-agent chunks of one env (graph) on one XCD in the BPTT chain's edge and node
+// backward kernels, so a graph's records stay in one L2 from kernel to kernel (fp32 headline
+// 10.85 -> 10.69 ms, bf16 6.85 -> 6.74, profiles/r4_xcd/). ROLL_XCD: the same for the rollout's
+// forward step and kNN scan (blocks of one env on one XCD: 10.68-10.69 -> 10.67-10.68 ms, bf16
+// 6.73 -> 6.72). node_reduce (graph.hip NODE_RED_XCD): neutral, kept for the same locality.
+#ifndef BPTT_XCD
+#define BPTT_XCD 1
+#endif
+#ifndef ROLL_XCD
+#define ROLL_XCD 1
+#endif
+
 // lane l <- lane l^32 with v_permlane32_swap (CDNA4, VALU) instead of ds_bpermute (LDS path)
 DEV unsigned xor32u(unsigned u) {
   const auto r = __builtin_amdgcn_permlane32_swap(u, u, false, false);

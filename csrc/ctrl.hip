@@ -675,10 +675,11 @@ __global__ __launch_bounds__(WAVES * 64) void ctrl_fwd_kernel(CtrlArgs a) {
   block_copy16(vl, a.wvec, CTRL_VEC * 4);
   __syncthreads();
   const int apw = (a.apw >= 2 && a.apw <= 32) ? a.apw : 32;
+  const int lb = ROLL_XCD ? xcd_block((int)blockIdx.x, (int)gridDim.x) : (int)blockIdx.x;
   if (CTRL_FWD_DENSE && a.K == 12 && apw % 8 == 0)
-    ctrl_fwd_groups<D, false, FUSE, true>(a, wl, wn, vl, pools, blockIdx.x * WAVES + wave_id(), gridDim.x * WAVES);
+    ctrl_fwd_groups<D, false, FUSE, true>(a, wl, wn, vl, pools, lb * WAVES + wave_id(), gridDim.x * WAVES);
   else
-    ctrl_fwd_groups<D, false, FUSE>(a, wl, wn, vl, pools, blockIdx.x * WAVES + wave_id(), gridDim.x * WAVES);
+    ctrl_fwd_groups<D, false, FUSE>(a, wl, wn, vl, pools, lb * WAVES + wave_id(), gridDim.x * WAVES);
   if constexpr (!X3 || FUSE) publish_step(a);   // the x3 split path publishes from its node kernel
 }
 

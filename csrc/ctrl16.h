@@ -68,7 +68,7 @@ __global__ __launch_bounds__(E16_NW * 64, 2 * E16_WG_PER_CU) void ctrl_edge_bwd1
     }
   };
 
-  for (long w = blockIdx.x; w < nwork; w += gridDim.x) {
+  for (long w = BPTT_XCD ? xcd_block((int)blockIdx.x, (int)gridDim.x) : (int)blockIdx.x; w < nwork; w += gridDim.x) {
     const long chunk = w / QP;
     const int part = (int)(w - chunk * QP);
     const int q0 = part * K / QP, q1 = (part + 1) * K / QP;

@@ -194,12 +194,18 @@ DEV void acc_rec_g(float4 (&g)[R], const float4* src, const float* gate) {
   }
 }
 
+#ifndef NODE_RED_XCD
+#define NODE_RED_XCD 1
+#endif
 // out[t', b, i] (+)= sum over passes p of [ sum_k dE_p[t'-p, b, i, k] - sum_{e in in(i)} dE_p[e] ]
 // for the N agents (obstacle nodes receive no gradient). Records of REC<D> float4.
 template <int D>
 __global__ __launch_bounds__(256) void node_reduce_kernel(NodeRedArgs a) {
   const int t_hi = a.t_hi ? a.t_hi : a.T + 1;
-  const long node = (long)a.t_lo * a.B * a.N + ((long)blockIdx.x * blockDim.x + threadIdx.x) / RG;
+  // one graph's nodes on one XCD: the in-edge gathers read the records the graph's out-edge reads
+  // just brought into that XCD's L2
+  const int lb = NODE_RED_XCD ? xcd_block((int)blockIdx.x, (int)gridDim.x) : (int)blockIdx.x;
+  const long node = (long)a.t_lo * a.B * a.N + ((long)lb * blockDim.x + threadIdx.x) / RG;
   const int l = threadIdx.x % RG;
   const long total = (long)a.B * t_hi * a.N;
   if (node >= total) return;             // whole 16-lane groups

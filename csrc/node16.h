@@ -146,7 +146,7 @@ __global__ __launch_bounds__(N16_NW * 64) void ctrl_node_bwd16_kernel(CtrlNodeBw
   const int trow = (wave & 1) * 16 + n;        // this wave's rows inside its turn
   const int myturn = wave >> 1;
 
-  for (long chunk = blockIdx.x; chunk < nchunks; chunk += gridDim.x) {
+  for (long chunk = BPTT_XCD ? xcd_block((int)blockIdx.x, (int)gridDim.x) : (int)blockIdx.x; chunk < nchunks; chunk += gridDim.x) {
     stamp(15);
     const int ga = (int)(chunk * N16_CH) + wave * 16 + n;
     const bool ok = ga < total;

@@ -245,7 +245,11 @@ __global__ __launch_bounds__(BS) void scan_kernel(ScanArgs a) {
   const int Np = (Nn + SCH - 1) / SCH * SCH;
   const int nch = Np / SCH, nsc = (nch + SSC - 1) / SSC;
   __shared__ float red[3][BS / WAVE];
-  const int b = blockIdx.y;
+  // ROLL_XCD: the blocks of one env (consecutive in x) on one XCD (they stage the same env)
+  const int lin0 = (int)(blockIdx.y * gridDim.x + blockIdx.x);
+  const int lin = ROLL_XCD ? xcd_block(lin0, (int)(gridDim.x * gridDim.y)) : lin0;
+  const int bx = lin % (int)gridDim.x;
+  const int b = lin / (int)gridDim.x;
   float4 *tp, *tv, *cbl, *cbh, *sbl, *sbh;
   if constexpr (GLB) {
     tp = a.ws + (long)b * a.ws_env;                            // [Np] x, y, z, node id (global)
@@ -324,7 +328,7 @@ __global__ __launch_bounds__(BS) void scan_kernel(ScanArgs a) {
   // (SCH/LPA)h.. of every chunk; the partial lists are merged at the end (LPA x the waves of a
   // lane-per-agent layout, 1/LPA of the per-chunk work per lane).
   const int wave = threadIdx.x / WAVE, lane = threadIdx.x & 63, r = lane % APW, h = lane / APW;
-  const int pos = blockIdx.x * SCAN_AG + wave * APW + r;      // my position on the curve
+  const int pos = bx * SCAN_AG + wave * APW + r;              // my position on the curve
   float4 me = make_float4(0.f, 0.f, 0.f, 0.f), mv = make_float4(0.f, 0.f, 0.f, 0.f);
   int i = -1;
   if (pos < Nn) {
@@ -379,7 +383,7 @@ __global__ __launch_bounds__(BS) void scan_kernel(ScanArgs a) {
   }
   const float wvmax = wave_max(act ? mv.w : 0.f);
   const bool wave_live = __any(act);
-  int cc0 = (blockIdx.x * SCAN_AG + wave * APW + APW / 2) / SCH;
+  int cc0 = (bx * SCAN_AG + wave * APW + APW / 2) / SCH;
   if (cc0 >= nch) cc0 = nch - 1;
   float thr = wave_max(act ? bound : -INFINITY);   // bound on every agent's final K-th distance
   bool all_danger = false;
