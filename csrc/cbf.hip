@@ -471,7 +471,7 @@ __global__ __launch_bounds__(NW * 64, CBF_HFWD_MINW) void cbf_hfwd_kernel(CbfFwd
     o.j = x.j;
     o.in = x.in;
   };
-  const unsigned t0 = blockIdx.x * NW + wave;
+  const unsigned t0 = (CBF_XCD ? xcd_block((int)blockIdx.x, (int)gridDim.x) : (int)blockIdx.x) * NW + wave;
   P0 p0{};
   P1 p1{};
   P2 p2{};
@@ -510,7 +510,7 @@ __global__ __launch_bounds__(NW * 64, CBF_HFWD_MINW) void cbf_hfwd_kernel(CbfFwd
     }
 #else
   EdgeCtx<D> nx;
-  unsigned tile = blockIdx.x * NW + wave;
+  unsigned tile = (CBF_XCD ? xcd_block((int)blockIdx.x, (int)gridDim.x) : (int)blockIdx.x) * NW + wave;
   if (CBF_HFWD_PREFETCH && tile < ntiles) load(tile, nx);
   for (; tile < ntiles; tile += stride) {
 #if CBF_HFWD_PREFETCH

@@ -170,7 +170,7 @@ __global__ __launch_bounds__(C16_NW * 64, 2 * C16_WG_PER_CU) void cbf_bwd16_kern
     return rec[v < EV ? v : EV - 1];
   };
   auto in_at = [&](long chunk) { return chunk * C16_CH + wave * 16 + n < EV; };
-  const long c0 = blockIdx.x;
+  const long c0 = CBF_XCD ? xcd_block((int)blockIdx.x, (int)gridDim.x) : (int)blockIdx.x;
   if (c0 < nchunks) {   // else no chunk for this workgroup (EV may be 0): zero slab
   Ev16<D> nx;
   ev16_issue<D>(a, rec_at(c0), nx);
