@@ -675,7 +675,11 @@ __global__ __launch_bounds__(WAVES * 64) void ctrl_fwd_kernel(CtrlArgs a) {
   block_copy16(vl, a.wvec, CTRL_VEC * 4);
   __syncthreads();
   const int apw = (a.apw >= 2 && a.apw <= 32) ? a.apw : 32;
-  const int lb = ROLL_XCD ? xcd_block((int)blockIdx.x, (int)gridDim.x) : (int)blockIdx.x;
+  // remap over the blocks that have a group (a small scene leaves most of the grid idle: the
+  // remap must not gather the busy ones onto one XCD)
+  const int ngrp = (a.B * a.N + apw - 1) / apw;
+  const int nact = min((int)gridDim.x, (ngrp + WAVES - 1) / WAVES);
+  const int lb = (ROLL_XCD && (int)blockIdx.x < nact) ? xcd_block((int)blockIdx.x, nact) : (int)blockIdx.x;
   if (CTRL_FWD_DENSE && a.K == 12 && apw % 8 == 0)
     ctrl_fwd_groups<D, false, FUSE, true>(a, wl, wn, vl, pools, lb * WAVES + wave_id(), gridDim.x * WAVES);
   else
