@@ -5,7 +5,7 @@ re-runs it with a stamps buffer and prints the shader-clock cycles per chunk of 
 (median over waves; the slowest wave's sum over its chunks in the last column), for the captured
 active list and for all deduplicated evaluations.
 
-    python scripts/stamps_cbf.py [--so PATH]
+    python scripts/stamps_cbf.py [--so PATH] [--envs 64]
 """
 import argparse
 import importlib.util
@@ -22,6 +22,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--so", default=None)
     ap.add_argument("--warm", type=int, default=2)
+    ap.add_argument("--envs", type=int, default=64)
     a = ap.parse_args()
     import torch
     if a.so:
@@ -34,7 +35,7 @@ def main():
     from macbf_gnn_amd.ops import native
 
     dev = torch.device("cuda", 0)
-    tr = Trainer(C.TrainConfig(num_agents=1024, num_envs=64, inner_loops=50, device="hip", seed=0), device=dev)
+    tr = Trainer(C.TrainConfig(num_agents=1024, num_envs=a.envs, inner_loops=50, device="hip", seed=0), device=dev)
     cap = {}
     orig = native.cbf_bwd
 
