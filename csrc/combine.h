@@ -41,6 +41,14 @@ DEV void acc_rec(float4 (&g)[R], const float4* src) {
     g[q].x += SIGN * v.x; g[q].y += SIGN * v.y; g[q].z += SIGN * v.z; g[q].w += SIGN * v.w;
   }
 }
+// the same from records already in registers
+template <int R, int SIGN>
+DEV void acc_rec_v(float4 (&g)[R], const float4 (&v)[R]) {
+#pragma unroll
+  for (int q = 0; q < R; ++q) {
+    g[q].x += SIGN * v[q].x; g[q].y += SIGN * v[q].y; g[q].z += SIGN * v[q].z; g[q].w += SIGN * v[q].w;
+  }
+}
 
 // One reverse-time step of the BPTT recursion (train.py:58-103 through autograd in the
 // reference; hand-derived here):

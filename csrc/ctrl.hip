@@ -849,6 +849,9 @@ DEV void store_tile_add(float* dst, int ncols, int mt, int nt, const f32x16& old
 // stores it (the next reverse step's Euler term).
 // XO: lane distance between the two halves of an agent (32: lane halves h; 16: the g = 0 / 1
 // lanes of the 16x16x32 node kernel)
+#ifndef CMB_BT
+#define CMB_BT 4
+#endif
 template <int D, int XO = 32>
 DEV void fused_combine(const CtrlNodeBwdArgs& a, bool ok, int b, int i, int h, float (&gp)[D], float (&gv)[D]) {
   constexpr int R = REC<D>;
@@ -864,11 +867,39 @@ DEV void fused_combine(const CtrlNodeBwdArgs& a, bool ok, int b, int i, int h, f
     load_rec<D>(a.cego + (long)b * N * R, (unsigned)i, ep, ev);
     if (a.cGn) load_rec<D>(a.cGn + (long)b * a.cgn_env * R, (unsigned)i, np_, nv);
     const float4* dE = a.cdEc + (long)b * N * K * R;
-    for (int k = h; k < K; k += 2) acc_rec<R, 1>(g, dE + ((long)i * K + k) * R);
+    // batches of CMB_BT records in flight (clamped indices, unconditional loads, predicated adds in
+    // the original order): a loop of dependent load -> add iterations waits one memory latency per
+    // edge (ptr -> edges -> record for the in-edges), ~12 latencies per agent
+#pragma unroll 1
+    for (int k0 = h; k0 < K; k0 += 2 * CMB_BT) {
+      float4 v[CMB_BT][R];
+#pragma unroll
+      for (int u = 0; u < CMB_BT; ++u) {
+        const int k = min(k0 + 2 * u, K - 1);
+#pragma unroll
+        for (int q = 0; q < R; ++q) v[u][q] = dE[((long)i * K + k) * R + q];
+      }
+#pragma unroll
+      for (int u = 0; u < CMB_BT; ++u)
+        if (k0 + 2 * u < K) acc_rec_v<R, 1>(g, v[u]);
+    }
     const int* ptr = a.cptr + (long)b * a.cptr_env;
     const int* edges = a.cedges + (long)b * a.cedges_env;
     const int q0 = ptr[i], q1 = ptr[i + 1];
-    for (int q = q0 + h; q < q1; q += 2) acc_rec<R, -1>(g, dE + (long)edges[q] * R);
+#pragma unroll 1
+    for (int qb = q0 + h; qb < q1; qb += 2 * CMB_BT) {
+      int e[CMB_BT];
+#pragma unroll
+      for (int u = 0; u < CMB_BT; ++u) e[u] = edges[min(qb + 2 * u, q1 - 1)];
+      float4 v[CMB_BT][R];
+#pragma unroll
+      for (int u = 0; u < CMB_BT; ++u)
+#pragma unroll
+        for (int q = 0; q < R; ++q) v[u][q] = dE[(long)e[u] * R + q];
+#pragma unroll
+      for (int u = 0; u < CMB_BT; ++u)
+        if (qb + 2 * u < q1) acc_rec_v<R, -1>(g, v[u]);
+    }
   }
 #pragma unroll
   for (int q = 0; q < R; ++q) {
