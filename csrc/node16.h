@@ -152,28 +152,33 @@ __global__ __launch_bounds__(N16_NW * 64) void ctrl_node_bwd16_kernel(CtrlNodeBw
     const bool ok = ga < total;
     // stage turns holding at least one valid agent (a partial chunk skips its empty turns)
     const int nturn = min(4, (int)((min((long)N16_CH, total - chunk * N16_CH) + N16_RT - 1) / N16_RT));
-    int b = 0, i = 0;
+    // every load unconditional (a lane past the end reads agent 0) and issued before any use: a
+    // load inside `if (ok)` waits at the branch merge, serialising this block, the pooled rows
+    // and the combine's gathers (ctrl.hip ctrl_st_load)
+    const int gac = ok ? ga : 0;
+    const int b = gac / N, i = gac - b * N;
     float sp[D], sv[D], gg[D], av[D], gnp[D], gnv[D];
+    load_rec<D>(a.S + (long)b * a.s_env * REC<D>, (unsigned)i, sp, sv);
 #pragma unroll
-    for (int q = 0; q < D; ++q) { sp[q] = sv[q] = gg[q] = av[q] = gnp[q] = gnv[q] = 0.f; }
-    bool vld = false;
-    if (ok) {
-      b = ga / N; i = ga - b * N;
-      load_rec<D>(a.S + (long)b * a.s_env * REC<D>, (unsigned)i, sp, sv);
-#pragma unroll
-      for (int q = 0; q < D; ++q) {
-        gg[q] = a.G[((long)b * N + i) * D + q];
-        av[q] = a.A[((long)b * a.a_env + i) * D + q];
-      }
-      if (a.Gn && !a.cdS) load_rec<D>(a.Gn + (long)b * a.gn_env * REC<D>, (unsigned)i, gnp, gnv);
-      vld = a.valid ? (a.valid[(long)b * a.v_env] != 0) : true;
+    for (int q = 0; q < D; ++q) {
+      gg[q] = a.G[((long)b * N + i) * D + q];
+      av[q] = a.A[((long)b * a.a_env + i) * D + q];
+      gnp[q] = gnv[q] = 0.f;
     }
+    if (a.Gn && !a.cdS) load_rec<D>(a.Gn + (long)b * a.gn_env * REC<D>, (unsigned)i, gnp, gnv);
+    const bool vld = ok && (a.valid ? (a.valid[(long)b * a.v_env] != 0) : true);
     const h16* prow = a.pooled + (long)b * a.p_env + (long)i * PROW;
     Fr Pf[4];
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      if (ok) Pf[s] = row_fr(prow + 32 * s + 8 * g, 128);
-      else Pf[s].h = Pf[s].l = zero_h8();
+    for (int s = 0; s < 4; ++s) Pf[s] = row_fr(prow + 32 * s + 8 * g, 128);
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+      if (!ok) Pf[s].h = Pf[s].l = zero_h8();
+#pragma unroll
+    for (int q = 0; q < D; ++q) {
+      sp[q] = ok ? sp[q] : 0.f; sv[q] = ok ? sv[q] : 0.f;
+      gg[q] = ok ? gg[q] : 0.f; av[q] = ok ? av[q] : 0.f;
+      gnp[q] = ok ? gnp[q] : 0.f; gnv[q] = ok ? gnv[q] : 0.f;
     }
     // G_{t+1} (fused BPTT combine): lanes g = 0 / 1 split the agent's out- and in-edges exactly
     // as the 2-lane combine of the other node kernels (same terms, same order: bit-identical);

@@ -236,6 +236,9 @@ __global__ __launch_bounds__(STAGE_BLOCK) void scan_stage_kernel(ScanArgs a) {
 
 // GLB: 0 = env staged in LDS; 1 = nodes in the global workspace, culling boxes copied to LDS;
 // 2 = boxes read from the workspace too (envs whose boxes exceed LDS: > ~36 K nodes)
+#ifndef SCAN_STAGE_BT
+#define SCAN_STAGE_BT 4
+#endif
 template <int K, int D, int BS, int LPA, int GLB>
 __global__ __launch_bounds__(BS) void scan_kernel(ScanArgs a) {
   constexpr int APW = WAVE / LPA;                              // agents per wave
@@ -277,19 +280,29 @@ __global__ __launch_bounds__(BS) void scan_kernel(ScanArgs a) {
     const float4* gb = tv + Np;
     for (int q = threadIdx.x; q < 2 * (nch + nsc); q += BS) cbl[q] = gb[q];
   } else
-  for (int q = threadIdx.x; q < Np; q += BS) {
-    if (q < Nn) {
-      const int id = perm[q];
-      float p[D], v[D];
-      load_rec<D>(Sb, (unsigned)id, p, v);
-      const float z = (D == 3) ? p[D - 1] : 0.f;
-      const float vz = (D == 3) ? v[D - 1] : 0.f;
-      tp[q] = make_float4(p[0], p[1], z, __int_as_float(id));
-      tv[q] = make_float4(v[0], v[1], vz, sqrtf(sqsum<D>(v)));
-      pinv[id] = (unsigned short)q;
-    } else {
-      tp[q] = make_float4(INFINITY, INFINITY, INFINITY, __int_as_float(-1));   // key == KEY_EMPTY
-      tv[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+  // batches of SCAN_STAGE_BT positions per thread: the perm -> record chains of a batch are in
+  // flight together (clamped indices, unconditional loads), not one dependent pair per iteration
+  for (int q0 = threadIdx.x; q0 < Np; q0 += SCAN_STAGE_BT * BS) {
+    int ids[SCAN_STAGE_BT];
+#pragma unroll
+    for (int u = 0; u < SCAN_STAGE_BT; ++u) ids[u] = perm[min(q0 + u * BS, Nn - 1)];
+    float p[SCAN_STAGE_BT][D], v[SCAN_STAGE_BT][D];
+#pragma unroll
+    for (int u = 0; u < SCAN_STAGE_BT; ++u) load_rec<D>(Sb, (unsigned)ids[u], p[u], v[u]);
+#pragma unroll
+    for (int u = 0; u < SCAN_STAGE_BT; ++u) {
+      const int q = q0 + u * BS;
+      if (q >= Np) break;
+      if (q < Nn) {
+        const float z = (D == 3) ? p[u][D - 1] : 0.f;
+        const float vz = (D == 3) ? v[u][D - 1] : 0.f;
+        tp[q] = make_float4(p[u][0], p[u][1], z, __int_as_float(ids[u]));
+        tv[q] = make_float4(v[u][0], v[u][1], vz, sqrtf(sqsum<D>(v[u])));
+        pinv[ids[u]] = (unsigned short)q;
+      } else {
+        tp[q] = make_float4(INFINITY, INFINITY, INFINITY, __int_as_float(-1));   // key == KEY_EMPTY
+        tv[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+      }
     }
   }
   __syncthreads();
