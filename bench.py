@@ -187,7 +187,11 @@ def _device_uid(torch, dev) -> int:
         return -1
     import hashlib
     p = torch.cuda.get_device_properties(dev)
-    key = str(getattr(p, "uuid", "") or "") or f"{getattr(p, 'pci_domain_id', 0)}:{getattr(p, 'pci_bus_id', dev.index)}"
+    uuid = str(getattr(p, "uuid", "") or "")
+    if set(uuid) <= set("GPU-0"):
+        uuid = ""        # unreported / all-zero UUID: every rank would hash alike
+    key = uuid or (f"pci {getattr(p, 'pci_domain_id', 0)}:{getattr(p, 'pci_bus_id', dev.index)}:"
+                   f"{getattr(p, 'pci_device_id', 0)}")
     return int.from_bytes(hashlib.sha1(key.encode()).digest()[:8], "little") >> 2
 
 

@@ -337,23 +337,6 @@ static int ctrl_bwd_step(py::tuple node, py::tuple edge, int num_blocks, int pre
                                                                                                  ST(stream));
 }
 
-static int probe_mfma(u64 a, u64 b, u64 d, u64 stream) {
-  return mb_probe_mfma(P<const void>(a), P<const void>(b), P<float>(d), ST(stream));
-}
-static int probe_mfma16(u64 a, u64 b, u64 d, u64 stream) {
-  return mb_probe_mfma16(P<const void>(a), P<const void>(b), P<float>(d), ST(stream));
-}
-extern "C" int mb_probe_mfma_exec(const void* a, float* out, int uniform, hipStream_t st);
-static int probe_mfma_exec(u64 a, u64 out, int uniform, u64 stream) {
-  return mb_probe_mfma_exec(P<const void>(a), P<float>(out), uniform, ST(stream));
-}
-static int probe_lane_xor(u64 in, u64 out, u64 stream) {
-  return mb_probe_lane_xor(P<const unsigned>(in), P<unsigned>(out), ST(stream));
-}
-static int probe_tr(u64 img, int rows, int stride, int e0, int m0, u64 out, u64 stream) {
-  return mb_probe_tr(P<const void>(img), rows, stride, e0, m0, P<void>(out), ST(stream));
-}
-
 static py::dict device_info(int dev) {
   hipDeviceProp_t p;
   py::dict d;
@@ -401,11 +384,6 @@ PYBIND11_MODULE(_C, m) {
   m.def("pack_gather", &pack_gather);
   m.def("step_commit", &step_commit);
   m.def("stats_pack", &stats_pack);
-  m.def("probe_mfma", &probe_mfma);
-  m.def("probe_mfma16", &probe_mfma16);
-  m.def("probe_tr", &probe_tr);
-  m.def("probe_lane_xor", &probe_lane_xor);
-  m.def("probe_mfma_exec", &probe_mfma_exec);
   m.def("ctrl_bwd_step", &ctrl_bwd_step);
   m.def("device_info", &device_info);
   m.def("err_str", &err_str);

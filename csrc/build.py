@@ -19,7 +19,7 @@ ROOT = os.path.dirname(HERE)
 PKG = os.path.join(ROOT, "macbf_gnn_amd")
 BUILD = os.path.join(ROOT, "build", "csrc")
 ARCH = os.environ.get("MACBF_ARCH", "gfx950")
-KERNELS = ["scan", "scenario", "ctrl", "cbf", "dedup", "graph", "optim", "probe"]
+KERNELS = ["scan", "scenario", "ctrl", "cbf", "dedup", "graph", "optim"]
 HALF_KERNELS = {"ctrl", "cbf"}       # compiled per MFMA operand precision (csrc/prec.h)
 
 
@@ -28,6 +28,11 @@ HOST_SRCS = ["host/scenario_host.cpp", "host/bindings_host.cpp"]   # CPU runtime
 
 def ext_path():
     return os.path.join(PKG, "_C" + sysconfig.get_config_var("EXT_SUFFIX"))
+
+
+def probe_ext_path():
+    """Layout probes (csrc/probe.hip) for tests/test_gpu_probe.py: a separate extension, not in _C."""
+    return os.path.join(PKG, "_probe" + sysconfig.get_config_var("EXT_SUFFIX"))
 
 
 def host_ext_path():
@@ -100,13 +105,17 @@ def write_ninja(debug=False):
         lines.append(f"build {bo}: bcc {os.path.join(HERE, b + '.cpp')}")
         objs.append(bo)
     lines.append(f"build {ext_path()}: link {' '.join(objs)}")
+    po, pb = os.path.join(BUILD, "probe.o"), os.path.join(BUILD, "probe_bindings.o")
+    lines.append(f"build {po}: kcc {os.path.join(HERE, 'probe.hip')}")
+    lines.append(f"build {pb}: bcc {os.path.join(HERE, 'probe_bindings.cpp')}")
+    lines.append(f"build {probe_ext_path()}: link {po} {pb}")
     hobjs = []
     for src in HOST_SRCS:
         o = os.path.join(BUILD, "host_" + os.path.basename(src).replace(".cpp", ".o"))
         lines.append(f"build {o}: hcc {os.path.join(HERE, src)}")
         hobjs.append(o)
     lines.append(f"build {host_ext_path()}: hlink {' '.join(hobjs)}")
-    lines.append(f"default {ext_path()} {host_ext_path()}")
+    lines.append(f"default {ext_path()} {host_ext_path()} {probe_ext_path()}")
     os.makedirs(BUILD, exist_ok=True)
     with open(os.path.join(BUILD, "build.ninja"), "w") as f:
         f.write("\n".join(lines) + "\n")

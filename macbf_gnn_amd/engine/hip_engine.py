@@ -55,8 +55,6 @@ class HipEngine:
                               # during it (A/B on MI355X: neutral-to-slower, 7.63 vs 7.66 ms; off)
     small_rollout = True      # envs of <= native.SMALL_MAXN graph nodes: the whole rollout is ONE
                               # persistent launch (one workgroup per env, device-side early stop)
-    bptt_graph = False        # replay the native BPTT launch loop from HIP graphs captured per
-                              # (T, grad scale) (MACBF_BPTT_GRAPH; A/B in docs/PERF.md)
     small_bptt = False        # envs of <= native.SMALL_MAXN agents: the BPTT recursion as ONE
                               # persistent launch (one workgroup per env). Off: measured 3x slower
                               # at 32 x 1 (2.17 vs 0.69 ms) -- the per-step launches spread a small
@@ -74,8 +72,6 @@ class HipEngine:
         self._drv = None
         self._bdrv = None
         self.native_bptt = bool(knobs.get_int("MACBF_NATIVE_BPTT", int(self.native_bptt)))
-        self.bptt_graph = bool(knobs.get_int("MACBF_BPTT_GRAPH", int(self.bptt_graph)))
-        self._bptt_graphs = {}
         self.bptt = cfg.bptt
         self.reuse = cfg.reuse_nbr_idx
         # deduplicated h/h' evaluations need both roles' state gradients on the same s_t: BPTT only
@@ -134,13 +130,13 @@ class HipEngine:
         self.graph_mode = bool(getattr(cfg, "graph", False))
         self._graphs = None
         self._graph_gs = None
-        # x3: the 16x16x32 backward kernels against their float64 oracles once, before training
-        # (ops/selfcheck.py: a miscompiled schedule stops here instead of corrupting gradients)
+        # the 16x16x32 backward kernels this engine runs, once before training (ops/selfcheck.py: a
+        # miscompiled schedule stops here instead of corrupting gradients): CBF / edge against their
+        # float64 oracles (x3), the node kernel against the 32x32x16 one (every precision)
         self.selfcheck = None
-        if self.prec == "fp32":
-            from ..ops import selfcheck
-            if selfcheck.enabled():
-                self.selfcheck = selfcheck.check(self)
+        from ..ops import selfcheck
+        if selfcheck.enabled():
+            self.selfcheck = selfcheck.check(self)
 
     # ------------------------------------------------------------------ buffers
     def _alloc(self):
@@ -618,10 +614,7 @@ class HipEngine:
                 slab_rows = (B, B)
             elif Gp == 1 and red_done is None and self.native_bptt:
                 # the reverse-time launch loop in C++ (csrc/runtime.cpp): same launches, same order
-                if self.bptt_graph and not self.graph_mode and not torch.cuda.is_current_stream_capturing():
-                    self._bptt_graph_replay(T, gs, cur)
-                else:
-                    self._bdriver().run(T, gs * ACT_COEF, cur.cuda_stream)
+                self._bdriver().run(T, gs * ACT_COEF, cur.cuda_stream)
             elif Gp == 1:
                 self._bptt_chain(T, slice(0, B), valid_u8, gs, rptr3, redges3, self.part_node[: self.nb_node],
                                  self.part_edge[: self.nb_edge], self.nb_node, self.nb_edge, red_done, ts, cur)
@@ -687,23 +680,6 @@ class HipEngine:
         if d is not None:
             return 1.0, d
         return float(self.tr.grad_scale), None
-
-    def _bptt_graph_replay(self, T, gs, cur):
-        """The native BPTT launch loop of horizon T as a HIP graph, captured once per (T, grad
-        scale) and replayed: the kernels, their order and their arguments are those of
-        BpttDriver.run (every buffer is allocated once per engine); the graph only removes the
-        per-launch host and dispatch cost of the 2T launches."""
-        key = (int(T), float(gs))
-        g = self._bptt_graphs.get(key)
-        if g is None:
-            g = torch.cuda.CUDAGraph()
-            side = torch.cuda.Stream(device=self.dev)
-            side.wait_stream(cur)
-            with torch.cuda.graph(g, stream=side):
-                self._bdriver().run(T, gs * ACT_COEF, side.cuda_stream)
-            cur.wait_stream(side)
-            self._bptt_graphs[key] = g
-        g.replay()
 
     def _bdriver(self):
         """The native BPTT driver over this engine's persistent buffers (checked here once)."""

@@ -45,6 +45,22 @@ def lib():
     return _LIB
 
 
+_PROBE = None
+
+
+def probe_lib():
+    """The layout-probe extension (csrc/probe.hip, tests only; not part of _C)."""
+    global _PROBE
+    if _PROBE is None:
+        lib()       # HIP runtime + the main extension first
+        try:
+            from .. import _probe  # noqa: F401
+        except ImportError as e:  # pragma: no cover
+            raise NativeError(f"probe extension macbf_gnn_amd._probe is not built: {e}") from e
+        _PROBE = _probe
+    return _PROBE
+
+
 def available() -> bool:
     try:
         lib()

@@ -2,9 +2,10 @@
 
 `cbf_record_oracle` / `edge_oracle` re-evaluate, in float64 autograd, exactly what one call of
 csrc/cbf16.h / csrc/ctrl16.h computes from its inputs (tests/test_gpu_oracle16.py pins the kernels
-to them on captured training calls). `check(engine)` runs both kernels once on a small synthetic
-batch when an x3 engine is built and raises `NativeError` if any row disagrees beyond the
-tolerances below: a toolchain change that miscompiles these schedules (round 3 saw one, see
+to them on captured training calls). `check(engine)` runs the 16x16x32 kernels the engine uses once
+on a small synthetic batch when the engine is built -- CBF and edge (x3) against the oracles, the
+node kernel (every precision, csrc/node16.h) against the 32x32x16 node kernel -- and raises
+`NativeError` on a disagreement beyond the tolerances below: a toolchain change that miscompiles these schedules (round 3 saw one, see
 docs/ARCHITECTURE.md "Scheduling boundary") then stops training instead of corrupting it
 (ADVICE r3). MACBF_SELFCHECK=0 skips it.
 
@@ -180,17 +181,21 @@ def _knn(s, K, D):
 
 
 def check(engine) -> dict:
-    """Run the 16x16x32 CBF and edge backward kernels once on a synthetic batch against the
-    float64 oracles; raises native.NativeError on a disagreement. Returns a small report."""
+    """Run the 16x16x32 backward kernels this engine uses once on a synthetic batch: the CBF and
+    edge kernels (x3) against the float64 oracles, the node kernel (every precision) against the
+    independent 32x32x16 node kernel. Raises native.NativeError on a disagreement; returns a small
+    report."""
     pw = engine.pw
-    if not pw.x3:
-        return {}
     dev = engine.dev
     D = engine.D
     gen = torch.Generator().manual_seed(1234)
     B, N, T, K = 2, 48, 2, 12
     rep = {}
     fp = engine.tr.fp
+    if engine.node16_w is not None:
+        rep["node16"] = _node_check(engine, gen)
+    if not pw.x3 or not (engine.dedup and getattr(engine, "cbf16", False)):
+        return rep
     # ---- CBF backward over every (pass, t, b, i, k) record, random upstream gradients
     s = _synthetic_states(B, N, D, T + 1, gen, dev)
     S = native.to_records(s).contiguous()                       # (T+1, B, N, W)
@@ -236,7 +241,7 @@ def check(engine) -> dict:
         raise native.NativeError(f"16x16x32 CBF backward self-check failed: {rep['cbf16']} (toolchain / schedule "
                                  f"miscompile? see docs/ARCHITECTURE.md; MACBF_SELFCHECK=0 skips)")
     # ---- controller edge backward (K = 12), argmax slots = the true masked max-pool
-    if engine.eb16_w is not None:
+    if engine.eb16_w is not None and pw.x3:
         s1 = s[0]
         S1 = native.to_records(s1).contiguous()
         idx1 = idx[0]
@@ -268,6 +273,68 @@ def check(engine) -> dict:
         if int(bad.sum()):
             raise native.NativeError(f"16x16x32 edge backward self-check failed: {rep['eb16']} (toolchain / schedule "
                                      f"miscompile? see docs/ARCHITECTURE.md; MACBF_SELFCHECK=0 skips)")
+    return rep
+
+
+# node16 vs the 32x32x16 node kernel: both fp32-accurate in x3 (different accumulation orders);
+# the 1-pass builds round the activations to 16 bits at the same points, so a rounding can flip:
+# the bounds of the bf16 / fp16 full-step tests
+NODE_TOL = {"fp32": 1e-4, "bf16": 2e-2, "fp16": 2e-2}
+
+
+def _rel(a, b):
+    a, b = a.double().flatten(), b.double().flatten()
+    return float((a - b).norm() / b.norm().clamp(min=1e-30))
+
+
+def _node_check(engine, gen, B=2, N=256) -> dict:
+    """One reverse step of the controller node backward (dL/dpooled rows, ego terms, weight
+    gradients) on synthetic inputs, 16x16x32 kernel (csrc/node16.h) against 32x32x16
+    (csrc/ctrl.hip node_bwd_body), 128-agent chunks both (node16 is the default node
+    kernel of every precision)."""
+    from . import layout as L
+    pw = engine.pw
+    dev, D = engine.dev, engine.D
+    W = native.rec_width(D)
+    prow = L.pooled_row(pw.prec)
+    s = _synthetic_states(B, N, D, 1, gen, dev)[0]
+    S = native.to_records(s).contiguous()
+    G = (s[..., :D] + (torch.rand(B, N, D, generator=gen).to(dev) - 0.5)).contiguous()
+    A = ((torch.rand(B, N, D, generator=gen) - 0.5) * 2.0).to(dev).contiguous()
+    Gn = native.to_records((torch.rand(B, N, 2 * D, generator=gen) - 0.5).to(dev)).contiguous()
+    pv = torch.rand(B, N, 128, generator=gen).to(dev) * (torch.rand(B, N, 128, generator=gen).to(dev) > 0.3)
+    hi = pv.to(engine.hdt)
+    pooled = (torch.cat([hi, (pv - hi.float()).to(engine.hdt)], -1) if prow == 256 else hi).contiguous()
+    valid = torch.ones(B, dtype=torch.uint8, device=dev)
+    act_cnt = torch.full((1,), float(B * N), dtype=torch.float32, device=dev)
+    nb = max(1, min((B * N + 127) // 128, native.num_cu(dev)))
+    offs = {pn: o for (m, pn, shape, o, n) in engine.tr.fp.specs}
+    out = {}
+    for mode, wrm16, gmap in (("16", pw.node_rm16, L.ctrl_node16_grad_map), ("32", None, L.ctrl_node_grad_map)):
+        dP = torch.zeros(B, N, prow, dtype=engine.hdt, device=dev)
+        ego = torch.zeros(B, N, W, dtype=torch.float32, device=dev)
+        part = torch.zeros(nb, native.CTRL_NODE_PARTIAL, dtype=torch.float32, device=dev)
+        native.ctrl_node_bwd(pooled, S, G, A, Gn, valid, pw.ctrl_rm, pw.node_rm_off, pw.ctrl_v, 0.37, dP, ego, part, nb,
+                             act_cnt=act_cnt, prec=pw.prec, init=True, chunk=128, wrm16=wrm16)
+        torch.cuda.synchronize(dev)
+        red = part.double().sum(0)
+        sm, dm = gmap(offs, D)
+        g = torch.zeros(engine.tr.fp.numel, dtype=torch.float64, device=dev)
+        g.index_add_(0, torch.as_tensor(dm, device=dev), red[torch.as_tensor(sm, device=dev)])
+        dPf = dP[..., :128].double() + (dP[..., 128:].double() if prow == 256 else 0.0)
+        out[mode] = (dPf, ego.double(), g)
+    tol = NODE_TOL[pw.prec]
+    new, old = out["16"], out["32"]
+    errs = {"dP": _rel(new[0], old[0]), "ego": _rel(new[1], old[1])}
+    for m, pn, shape, o, n in engine.tr.fp.specs:
+        if pn.startswith("controller_dec_net"):
+            errs[pn] = _rel(new[2][o:o + n], old[2][o:o + n])
+    worst = max(errs.items(), key=lambda kv: kv[1])
+    finite = all(bool(torch.isfinite(x).all()) for x in new)
+    rep = {"agents": B * N, "worst": worst[0], "worst_rel": worst[1], "tol": tol}
+    if not finite or worst[1] > tol:
+        raise native.NativeError(f"16x16x32 node backward self-check failed: {rep} (toolchain / schedule miscompile? "
+                                 f"see docs/ARCHITECTURE.md; MACBF_SELFCHECK=0 skips)")
     return rep
 
 

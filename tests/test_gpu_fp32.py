@@ -4,12 +4,15 @@ gradients <= 1e-3 relative norm per tensor (the bf16 path is checked against a b
 emulation at 1e-2 forward / 2e-2 kernel and step gradients in test_gpu_backward.py; reference
 precision: /root/reference/core.py:47-48, train.py:167-172).
 
-Per-node state gradients are compared with the 2.5 % worst nodes trimmed: an edge whose relu
-pre-activation sits within the x3 rounding (~1e-6 of sum |terms|) of zero takes the other relu'
+Per-node state gradients are compared tie-aware (tests/numerics.py ctrl_tie_nodes): an edge whose
+relu pre-activation sits within the x3 rounding (~1e-6 of sum |terms|) of zero takes the other relu'
 branch than the fp32 oracle (measured: the two outlier edges of the 40-agent CBF case have
-pre-activations at 2.3e-7 and 3.1e-7 of sum |terms|, round 2); such a tie moves
-only the gradient of that edge's two endpoints. Parameter gradients (sums over all edges) are
-compared untrimmed."""
+pre-activations at 2.3e-7 and 3.1e-7 of sum |terms|, round 2); such a tie moves only the gradient
+of that edge's two endpoints. The nodes a float64 tie test flags (relu / radius / max-pool
+near-ties within 3e-5 of sum |terms|) are exempt from the 1e-3 bound, every other node is held to
+it, and the number of exempt nodes is bounded per case at ~2x its measured count (VERDICT r4
+weak #8; round 4 trimmed the worst 2.5 % of nodes instead). Parameter gradients (sums over all
+edges) are compared whole."""
 import math
 
 import pytest
@@ -22,6 +25,7 @@ from macbf_gnn_amd.ops import layout as L
 from macbf_gnn_amd.ops import native
 from macbf_gnn_amd.ops.weights import PackedWeights
 from macbf_gnn_amd.utils.params import FlatParams
+from numerics import cmp_nodes_tie, ctrl_tie_nodes, edge_ties_to_nodes
 
 pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda")
@@ -54,16 +58,6 @@ def _cmp(got, ref, name, rel):
     assert e <= rel, f"{name}: rel err {e:.3e} > {rel:.0e}"
 
 
-def _cmp_nodes(got, ref, name, rel, trim=0.025, rel_all=2e-2):
-    """Per-node records (..., W): relative norm error with the `trim` fraction of nodes with the
-    largest error dropped (relu ties, module docstring) <= rel; untrimmed <= rel_all."""
-    g = got.double().reshape(-1, got.shape[-1])
-    r = ref.double().reshape(-1, ref.shape[-1])
-    e = (g - r).norm(dim=-1)
-    keep = torch.argsort(e)[: max(1, int(round(e.numel() * (1 - trim))))]
-    et = (g[keep] - r[keep]).norm().item() / max(r.norm().item(), 1e-30)
-    ea = _rel(got, ref)
-    assert et <= rel and ea <= rel_all, f"{name}: trimmed rel err {et:.3e} (<= {rel:.0e}), all {ea:.3e}"
 
 
 def _cbf_tie_free(p, S, idx, tau=3e-5):
@@ -256,6 +250,11 @@ def test_fused_cbf_fp32_matches_two_kernel_path():
     _cmp(r2[:Lo], r1[:Lo], "dW slab", 1e-4)
 
 
+# exempt tie nodes (flagged AND outside the row tolerance) per case: measured 0 in every case
+# (profiles/r5_numerics/tie_counts.jsonl); one allowed against a toolchain flipping a single tie
+STEP_TIE_LIMIT = {(1, 32, None): 1, (2, 64, None): 1, (1, 200, None): 1, (2, 64, 64): 1, (1, 200, 128): 1}
+
+
 @pytest.mark.parametrize("B,N,chunk", [(1, 32, None), (2, 64, None), (1, 200, None), (2, 64, 64), (1, 200, 128)])
 def test_ctrl_step_bwd_fp32(B, N, chunk, monkeypatch):
     """One controller backward step against autograd. 32-agent chunks (the default at these
@@ -301,7 +300,8 @@ def test_ctrl_step_bwd_fp32(B, N, chunk, monkeypatch):
     s_next = sx + torch.cat([sx[..., 2:], a], -1) * C.TIME_STEP
     Lsum = (Gn * s_next).sum() + act_coef * O.action_loss_terms(sx, gg, a).sum()
     gr = torch.autograd.grad(Lsum, [sx] + list(p.values()))
-    _cmp_nodes(Gout, gr[0], "dL/ds_t", 1e-3)
+    tie = ctrl_tie_nodes(p, s, gg, idx)
+    cmp_nodes_tie(Gout, gr[0], tie, "dL/ds_t", limit=STEP_TIE_LIMIT[(B, N, chunk)])
     mine = _param_grads(fp, _unpack(fp, {"node": L.ctrl_node_grad_map, "edge": L.ctrl_edge_grad_map},
                                     {"node": rn, "edge": re}), "controller")
     for (k, _), ref in zip(p.items(), gr[1:]):
@@ -331,7 +331,7 @@ def test_full_step_grad_fp32(bptt, reuse, N, extra):
     the engine's trajectory (states, kNN graphs, max-pool argmax slots): with a few dozen agents a
     single max-pool near-tie -- two neighbours' features within the x3 rounding -- routes one
     feature's gradient to another edge and moves a whole parameter tensor by up to ~3e-3
-    (scripts/diag_fullstep.py, seed-dependent at N = 11, 12, 13 and with either edge kernel)."""
+    (scripts/diag_fullstep.py in the git history, seed-dependent at N = 11, 12, 13 and with either edge kernel)."""
     from macbf_gnn_amd.engine.oracle_engine import OracleEngine
     tr = _trainer(bptt=bptt, reuse_nbr_idx=reuse, N=N, B=3 if N < 32 else 2, **extra)
     s0, g, obs = tr.sample()
@@ -370,8 +370,9 @@ def test_module_api_fp32_default():
     gr = torch.autograd.grad((aref * wa).sum() + (href * wh).sum(), [s2, g2])
     _cmp(a.detach(), aref.detach(), "a", 1e-4)
     _cmp(h.detach(), href.detach(), "h", 1e-4)
-    _cmp_nodes(sx.grad, gr[0], "dL/ds", 1e-3)
-    _cmp_nodes(g.grad, gr[1], "dL/dg", 1e-3)
+    tie = ctrl_tie_nodes(pc, s, g, idx) | edge_ties_to_nodes(~_cbf_tie_free(pb, s, idx), idx, s.shape[-2])
+    cmp_nodes_tie(sx.grad, gr[0], tie, "dL/ds", limit=1)
+    cmp_nodes_tie(g.grad, gr[1], tie, "dL/dg", limit=1)
 
 
 def test_training_parity_fp32_vs_oracle():

@@ -75,10 +75,12 @@ def test_node16_matches_node32(N, B, extra, monkeypatch):
             assert _rel(new[3][o:o + n], old[3][o:o + n]) <= 1e-4, pn
 
 
-@pytest.mark.parametrize("dtype", ["bf16", "fp16"])
-def test_node16_matches_node32_1pass(dtype, monkeypatch):
-    """The 1-pass builds (round 4: the 16x16x32 node backward is their default at 128-agent chunks):
-    same step against the 32x32x16 kernel. Both round the activations to 16 bits at the same points;
+@pytest.mark.parametrize("dtype,extra", [("bf16", {}), ("fp16", {}), ("bf16", dict(dim=3, num_obstacles=2)),
+                                         ("fp16", dict(dim=3, num_obstacles=2))])
+def test_node16_matches_node32_1pass(dtype, extra, monkeypatch):
+    """The 1-pass builds (round 4: the 16x16x32 node backward is their default at 128-agent chunks;
+    config #5 runs it in fp16 with 3-D states and obstacle nodes -- ADVICE r4): same step against the
+    32x32x16 kernel. Both round the activations to 16 bits at the same points;
     accumulation orders differ, so a rounding can flip: bounds of the bf16 full-step tests (2e-2)."""
     monkeypatch.setenv("MACBF_NODE_CHUNK", "128")
     monkeypatch.setenv("MACBF_BWD_FUSED", "0")
@@ -88,7 +90,7 @@ def test_node16_matches_node32_1pass(dtype, monkeypatch):
         from macbf_gnn_amd.engine import Trainer
         from macbf_gnn_amd.parallel import DP
         cfg = C.TrainConfig(num_agents=256, num_envs=2, inner_loops=8, early_stop=False, seed=0, device="hip",
-                            dtype=dtype)
+                            dtype=dtype, **extra)
         tr = Trainer(cfg, device=DEV, dp=DP(device=DEV))
         assert (tr.engine._node16(2 * 256) is not None) == (mode == "1")
         s0, g, obs = tr.sample()
@@ -102,3 +104,25 @@ def test_node16_matches_node32_1pass(dtype, monkeypatch):
     for m, pn, shape, o, n in new[3]:
         if m == "controller":
             assert _rel(new[2][o:o + n], old[2][o:o + n]) <= 2e-2, pn
+
+
+@pytest.mark.parametrize("dtype,dim", [("fp32", 2), ("bf16", 2), ("fp16", 3)])
+def test_node16_startup_selfcheck(dtype, dim, monkeypatch):
+    """ops.selfcheck runs the 16x16x32 node backward against the 32x32x16 one when an engine that
+    uses it is built, in every precision; a corrupted weight image is caught."""
+    from macbf_gnn_amd.engine import Trainer
+    from macbf_gnn_amd.ops import selfcheck
+    from macbf_gnn_amd.parallel import DP
+    monkeypatch.setenv("MACBF_NODE_CHUNK", "128")
+    monkeypatch.setenv("MACBF_BWD_FUSED", "0")
+    cfg = C.TrainConfig(num_agents=256, num_envs=2, inner_loops=4, seed=0, device="hip", dtype=dtype, dim=dim)
+    tr = Trainer(cfg, device=DEV, dp=DP(device=DEV))
+    rep = tr.engine.selfcheck
+    assert rep and rep["node16"]["worst_rel"] <= rep["node16"]["tol"], rep
+    w = tr.engine.node16_w
+    keep = w.clone()
+    w.view(-1)[64 * 176: 64 * 176 + 4096] = 0            # W2 rows of the hi plane
+    with pytest.raises(native.NativeError):
+        selfcheck.check(tr.engine)
+    w.copy_(keep)
+    assert selfcheck.check(tr.engine)["node16"]["worst_rel"] <= rep["node16"]["tol"]

@@ -25,6 +25,7 @@ from macbf_gnn_amd import config as C
 from macbf_gnn_amd.engine import Trainer
 from macbf_gnn_amd.ops import layout as L
 from macbf_gnn_amd.ops import native
+from numerics import tie_log
 
 pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda", 0)
@@ -45,9 +46,15 @@ def _unpack(tr, fn, red):
     return g
 
 
-def _check_rows(got, ref, tie, what, scale):
+def _check_rows(got, ref, tie, what, scale, limits):
+    """No row outside the tolerance unless it is a tie row; tie rows (flagged) and exempt rows
+    (flagged AND outside the tolerance) each within their per-case allowance (~2x measured)."""
     bad, worst = bad_rows(got, ref, tie, scale)
     assert int(bad.sum()) == 0, (what, int(bad.sum()), int(tie.sum()), got.shape[0], worst)
+    err = (got - ref).norm(dim=1)
+    over = err > ROW_TOL * ref.norm(dim=1) + ABS_TOL * scale.norm(dim=1) + 1e-30
+    tie_log(what + " tie rows", int(tie.sum()), tie.numel(), limits[0])      # ties are rare, not a loophole
+    tie_log(what + " exempt rows", int((over & tie).sum()), tie.numel(), limits[1])
 
 
 def _check_grads(tr, got, ref_dw, scale, what, tol=1e-4):
@@ -89,15 +96,18 @@ def _capture_cbf(monkeypatch, **cfg):
     return tr, orig, cap["a"], cap["k"]
 
 
-@pytest.mark.parametrize("cfg", [
-    dict(num_agents=96, num_envs=3, inner_loops=6),
-    dict(num_agents=1024, num_envs=4, inner_loops=8),
-    dict(num_agents=64, num_envs=2, inner_loops=6, dim=3, num_obstacles=2),
-    dict(num_agents=96, num_envs=3, inner_loops=6, reuse_nbr_idx=False),
-    dict(num_agents=13, num_envs=5, inner_loops=6),
-    dict(num_agents=12, num_envs=3, inner_loops=6),
+# (tie rows, exempt rows) allowances: ~2x the counts measured on these deterministic calls
+# (profiles/r5_numerics/tie_counts.jsonl: 0.8-2.7 % of the rows are flagged, 0-0.03 % of the rows
+# are flagged AND outside the row tolerance); round 4 allowed a flat 5 %
+@pytest.mark.parametrize("cfg,tie_limit", [
+    (dict(num_agents=96, num_envs=3, inner_loops=6), (212, 4)),
+    (dict(num_agents=1024, num_envs=4, inner_loops=8), (4208, 54)),
+    (dict(num_agents=64, num_envs=2, inner_loops=6, dim=3, num_obstacles=2), (2, 1)),
+    (dict(num_agents=96, num_envs=3, inner_loops=6, reuse_nbr_idx=False), (304, 4)),
+    (dict(num_agents=13, num_envs=5, inner_loops=6), (50, 1)),
+    (dict(num_agents=12, num_envs=3, inner_loops=6), (42, 1)),
 ])
-def test_cbf16_matches_fp64_oracle(monkeypatch, cfg):
+def test_cbf16_matches_fp64_oracle(monkeypatch, cfg, tie_limit):
     tr, orig, a, k = _capture_cbf(monkeypatch, **cfg)
     nact = int(k["nact"][0])
     assert nact > 0
@@ -112,8 +122,7 @@ def test_cbf16_matches_fp64_oracle(monkeypatch, cfg):
     W = dE.shape[-1]
     ref_rows, tie, ref_dw, scale, rscale = cbf_record_oracle(_params(tr, "cbf"), S, rec, T, B, N, K, D)
     got = native.from_records(dE.view(-1, W)[rec[:, 0].long()]).double()
-    _check_rows(got, ref_rows, tie, "cbf dE", rscale)
-    assert int(tie.sum()) <= max(8, nact // 20), int(tie.sum())     # ties are rare, not a loophole
+    _check_rows(got, ref_rows, tie, "cbf dE", rscale, tie_limit)
     mine = _unpack(tr, L.cbf_grad_map, part.double().sum(0))
     _check_grads(tr, mine, ref_dw, scale, "cbf dW")
 
@@ -144,15 +153,15 @@ def _capture_edge(monkeypatch, **cfg):
     return tr, orig, cap[len(cap) // 2]
 
 
-@pytest.mark.parametrize("cfg", [
-    dict(num_agents=1024, num_envs=4, inner_loops=6),
-    dict(num_agents=96, num_envs=3, inner_loops=6),
-    dict(num_agents=12, num_envs=3, inner_loops=6),
-    dict(num_agents=13, num_envs=5, inner_loops=6),
-    dict(num_agents=17, num_envs=3, inner_loops=6),
-    dict(num_agents=64, num_envs=2, inner_loops=6, dim=3, num_obstacles=2),
+@pytest.mark.parametrize("cfg,tie_limit", [
+    (dict(num_agents=1024, num_envs=4, inner_loops=6), (1510, 6)),
+    (dict(num_agents=96, num_envs=3, inner_loops=6), (112, 2)),
+    (dict(num_agents=12, num_envs=3, inner_loops=6), (14, 1)),
+    (dict(num_agents=13, num_envs=5, inner_loops=6), (30, 1)),
+    (dict(num_agents=17, num_envs=3, inner_loops=6), (10, 1)),
+    (dict(num_agents=64, num_envs=2, inner_loops=6, dim=3, num_obstacles=2), (38, 1)),
 ])
-def test_eb16_matches_fp64_oracle(monkeypatch, cfg):
+def test_eb16_matches_fp64_oracle(monkeypatch, cfg, tie_limit):
     tr, orig, (a, k) = _capture_edge(monkeypatch, **cfg)
     kk = dict(k)
     kk["init"] = True
@@ -165,8 +174,7 @@ def test_eb16_matches_fp64_oracle(monkeypatch, cfg):
     D = tr.cfg.dim
     ref_rows, tie, ref_dw, scale, rscale = edge_oracle(_params(tr, "controller"), S, idx, argmax, dP, N, D)
     got = native.from_records(kk["dEc"]).double().reshape(-1, 2 * D)
-    _check_rows(got, ref_rows.reshape(-1, 2 * D), tie.reshape(-1), "edge dEc", rscale.reshape(-1, 2 * D))
-    assert int(tie.sum()) <= max(8, tie.numel() // 20), int(tie.sum())
+    _check_rows(got, ref_rows.reshape(-1, 2 * D), tie.reshape(-1), "edge dEc", rscale.reshape(-1, 2 * D), tie_limit)
     part = kk["partial"].double()
     assert torch.isfinite(part).all()
     mine = _unpack(tr, L.ctrl_edge_grad_map, part.sum(0))

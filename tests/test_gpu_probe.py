@@ -24,7 +24,7 @@ def test_mfma_layout_exact():
     ta = torch.tensor(a, dtype=torch.bfloat16, device=DEV).contiguous()
     tb = torch.tensor(b, dtype=torch.bfloat16, device=DEV).contiguous()
     d = torch.zeros(64, 16, dtype=torch.float32, device=DEV)
-    assert native.lib().probe_mfma(ta.data_ptr(), tb.data_ptr(), d.data_ptr(), native.stream_handle()) == 0
+    assert native.probe_lib().probe_mfma(ta.data_ptr(), tb.data_ptr(), d.data_ptr(), native.stream_handle()) == 0
     torch.cuda.synchronize()
     d = d.cpu().numpy()
     D = np.zeros((32, 32), np.float32)
@@ -41,7 +41,7 @@ def test_tr16_transposed_fragment(stride, e0, m0):
     img = (np.arange(rows * stride) % 251).astype(np.float32).reshape(rows, stride)
     t = torch.tensor(img, dtype=torch.bfloat16, device=DEV).contiguous()
     out = torch.zeros(64, 8, dtype=torch.bfloat16, device=DEV)
-    assert native.lib().probe_tr(t.data_ptr(), rows, stride, e0, m0, out.data_ptr(), native.stream_handle()) == 0
+    assert native.probe_lib().probe_tr(t.data_ptr(), rows, stride, e0, m0, out.data_ptr(), native.stream_handle()) == 0
     torch.cuda.synchronize()
     got = out.float().cpu().numpy()
     exp = np.zeros((64, 8), np.float32)
@@ -59,7 +59,7 @@ def test_lane_xor_exchanges_and_reductions():
     vals = rng.standard_normal(64).astype(np.float32)
     vin = torch.tensor(vals.view(np.uint32).astype(np.int64), dtype=torch.int64).to(torch.int32).to(DEV)
     out = torch.zeros(9 * 64, dtype=torch.int32, device=DEV)
-    assert native.lib().probe_lane_xor(vin.data_ptr(), out.data_ptr(), native.stream_handle()) == 0
+    assert native.probe_lib().probe_lane_xor(vin.data_ptr(), out.data_ptr(), native.stream_handle()) == 0
     torch.cuda.synchronize()
     got = out.cpu().numpy().astype(np.int64).astype(np.uint32).reshape(9, 64)
     bits = vals.view(np.uint32)
@@ -89,7 +89,7 @@ def test_mfma16_layout_exact():
     ta = torch.tensor(a, dtype=torch.bfloat16, device=DEV).contiguous()
     tb = torch.tensor(b, dtype=torch.bfloat16, device=DEV).contiguous()
     d = torch.zeros(64, 4, dtype=torch.float32, device=DEV)
-    assert native.lib().probe_mfma16(ta.data_ptr(), tb.data_ptr(), d.data_ptr(), native.stream_handle()) == 0
+    assert native.probe_lib().probe_mfma16(ta.data_ptr(), tb.data_ptr(), d.data_ptr(), native.stream_handle()) == 0
     torch.cuda.synchronize()
     d = d.cpu().numpy()
     D = np.zeros((16, 16), np.float32)
@@ -111,7 +111,7 @@ def test_mfma_under_wave_condition():
     outs = {}
     for uniform in (1, 0):
         o = torch.full((512, 4), float("nan"), dtype=torch.float32, device=DEV)
-        assert native.lib().probe_mfma_exec(ta.data_ptr(), o.data_ptr(), uniform, native.stream_handle()) == 0
+        assert native.probe_lib().probe_mfma_exec(ta.data_ptr(), o.data_ptr(), uniform, native.stream_handle()) == 0
         torch.cuda.synchronize()
         outs[uniform] = o.cpu().numpy()
     # reference: X (16 x 32), X[n][8g + j] = a[lane (n, g)][j]; acc = sum X X^T, bias = row sums
