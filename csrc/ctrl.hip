@@ -654,6 +654,9 @@ DEV void publish_step(const CtrlArgs& a) {
     // release (system scope) by one lane of one workgroup, then the flag; the explicit wait keeps
     // the write-back ahead of the flag (MI355X_MICROARCH: compiler hazard after buffer_wbl2).
     // The host polls the flag with an acquire load (csrc/runtime.cpp wait_published).
+    // (Without the release -- the host reads only pub_dist and the flag, both written to
+    // fine-grained host memory by system-scope stores -- the headline ran the same: 10.686-10.712
+    // vs 10.703-10.706 ms, profiles/r5_b1/; kept.)
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __hip_atomic_store(a.pub_flag, a.pub_gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);

@@ -123,6 +123,18 @@ class HipEngine:
         gptr = np.concatenate([[0], np.cumsum(counts)])
         mk32 = lambda a: torch.as_tensor(a, dtype=torch.int32, device=self.dev)
         self.g_ptr, self.g_src = mk32(gptr), mk32(srcs[order])
+        # DP: the CBF range of the flat gradient is final once the CBF slabs are reduced, before the
+        # BPTT starts; its all-reduce is issued then (async) and joined before Adam, so at world > 1
+        # it is in flight during the BPTT. The controller range is
+        # all-reduced after the BPTT. Both ranges are contiguous in the flat buffer.
+        rng = {}
+        for m, pn, shape, o, n in trainer.fp.specs:
+            lo, hi = rng.get(m, (o, o))
+            rng[m] = (min(lo, o), max(hi, o + n))
+        if sum(hi - lo for lo, hi in rng.values()) != trainer.fp.numel or set(rng) != {"controller", "cbf"}:
+            raise ValueError("flat parameters must be the contiguous controller and CBF ranges")
+        self.grad_ranges = rng
+        self._grad_work = None
         # whole-iteration HIP graph (cfg.graph): rollout to Tmax with device-side done masks,
         # losses, backward; replayed per iteration (removes the per-kernel launch / Python cost
         # that dominates small configurations). Sampling, the DP all-reduces and the optimizer
@@ -601,6 +613,15 @@ class HipEngine:
         else:
             native.node_reduce(dE, rptr, redges, self.dS, **red)
         tm.mark("cbf")
+        # (not inside a captured graph: the collectives stay eager around the graphs)
+        split = self.tr.dp.enabled and self.bptt and not self.graph_mode and not torch.cuda.is_current_stream_capturing()
+        if split:
+            # the CBF range now: reduced slab -> flat gradient -> async all-reduce during the BPTT
+            native.reduce_rows(part_cbf, self.red_cbf)
+            lo, hi = self.grad_ranges["cbf"]
+            native.grad_assemble(self.red_all, self.g_ptr[lo: hi + 1], self.g_src, tr.fp.grad[lo:hi], scale=1.0 / gs,
+                                 gscale=gsd)
+            self._grad_work = self.tr.dp.all_reduce_async(tr.fp.grad[lo:hi])
         # ---- controller backward
         if self.bptt:
             # BPTT through the rollout: G_t = dL/ds_t, reverse time
@@ -654,9 +675,14 @@ class HipEngine:
         tm.mark("bptt")
         # ---- weight-gradient slabs -> flat grad
         pnode, pedge = (self.part_node[: slab_rows[0]], self.part_edge[: slab_rows[1]]) if self.bptt else self._nb_parts
-        for part, red in ((part_cbf, self.red_cbf), (pnode, self.red_node), (pedge, self.red_edge)):
+        for part, red in (((part_cbf, self.red_cbf),) if not split else ()) + ((pnode, self.red_node), (pedge, self.red_edge)):
             native.reduce_rows(part, red)
-        native.grad_assemble(self.red_all, self.g_ptr, self.g_src, tr.fp.grad, scale=1.0 / gs, gscale=gsd)
+        if split:
+            lo, hi = self.grad_ranges["controller"]
+            native.grad_assemble(self.red_all, self.g_ptr[lo: hi + 1], self.g_src, tr.fp.grad[lo:hi], scale=1.0 / gs,
+                                 gscale=gsd)
+        else:
+            native.grad_assemble(self.red_all, self.g_ptr, self.g_src, tr.fp.grad, scale=1.0 / gs, gscale=gsd)
         tm.mark("grad_reduce")
         # ---- stats: one raw device row per iteration (no per-statistic kernels), derived lazily on read
         sums = self.loss_red[:10] if self.dedup else self.red_cbf[native.CBF_P_LOSS: native.CBF_P_LOSS + 10]
@@ -680,6 +706,19 @@ class HipEngine:
         if d is not None:
             return 1.0, d
         return float(self.tr.grad_scale), None
+
+    def reduce_grad(self):
+        """DP all-reduce of this step's flat gradient (Trainer.reduce_grad): the CBF range was issued
+        asynchronously before the BPTT (world > 1, BPTT); the rest is reduced here, then both are
+        joined on the current stream."""
+        dp = self.tr.dp
+        work, self._grad_work = self._grad_work, None
+        if work is None:
+            dp.all_reduce_(self.tr.fp.grad)
+            return
+        lo, hi = self.grad_ranges["controller"]
+        dp.all_reduce_(self.tr.fp.grad[lo:hi])
+        work.wait()
 
     def _bdriver(self):
         """The native BPTT driver over this engine's persistent buffers (checked here once)."""

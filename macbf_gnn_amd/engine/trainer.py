@@ -171,7 +171,7 @@ class Trainer:
         obs = obs.to(self.device) if obs is not None else None
         tm.mark("sample")
         stats = self.engine.step(s0, g, obs)
-        self.dp.all_reduce_(self.fp.grad)
+        self.reduce_grad()
         tm.mark("allreduce")
         # failure detection: a non-finite reduced gradient is identical on every
         # rank, so every rank skips the same step; parameters and Adam state stay untouched
@@ -209,6 +209,15 @@ class Trainer:
         if tm.enabled:
             stats["phases_ms"] = tm.results()
         return stats
+
+    def reduce_grad(self):
+        """DP all-reduce of the flat gradient of the last engine.step (the HIP engine overlaps the
+        CBF range with its BPTT and joins it here)."""
+        red = getattr(self.engine, "reduce_grad", None)
+        if red is not None:
+            red()
+        else:
+            self.dp.all_reduce_(self.fp.grad)
 
     @property
     def skipped_steps(self) -> int:

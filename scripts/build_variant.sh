@@ -17,7 +17,7 @@ for K in "${KL[@]}"; do
 done
 for p in $PIDS; do wait $p; done      # set -e: a failed compile stops the script
 OBJS=""
-for o in scan scenario ctrl ctrl_f16 ctrl_x3 cbf cbf_f16 cbf_x3 dedup graph optim probe bindings runtime; do
+for o in scan scenario ctrl ctrl_f16 ctrl_x3 cbf cbf_f16 cbf_x3 dedup graph optim bindings runtime; do
   if [[ ",$KS," == *",$o,"* ]]; then OBJS="$OBJS $O/$o.o"; else OBJS="$OBJS $B/$o.o"; fi
 done
 TL=$(python3 -c "import os,importlib.util as u;print(os.path.join(os.path.dirname(u.find_spec('torch').origin),'lib'))")

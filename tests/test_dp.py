@@ -52,7 +52,7 @@ def _worker(rank, world, port, outdir, mode):
         torch.save(tr.fp.flat.clone(), os.path.join(outdir, f"flat{rank}.pt"))
     elif mode == "grad":
         tr.engine.step(s_all[sl], g_all[sl])
-        dp.all_reduce_(tr.fp.grad)
+        tr.reduce_grad()
         torch.save(tr.fp.grad.clone(), os.path.join(outdir, f"grad{rank}.pt"))
     else:
         for it in range(3):

@@ -46,7 +46,7 @@ def _worker(rank, world, port, outdir):
     tr = Trainer(_cfg(B), device=dev, dp=dp)
     sl = slice(rank * B, (rank + 1) * B)
     tr.engine.step(s_all[sl].to(dev), g_all[sl].to(dev))
-    dp.all_reduce_(tr.fp.grad)
+    tr.reduce_grad()
     torch.cuda.synchronize()
     torch.save(tr.fp.grad.cpu(), os.path.join(outdir, f"grad{rank}.pt"))
     dp.shutdown()

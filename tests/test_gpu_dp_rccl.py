@@ -69,7 +69,7 @@ def _worker(rank, world, port, outdir):
     tr = Trainer(_cfg(B), device=dev, dp=dp)
     sl = slice(rank * B, (rank + 1) * B)
     tr.engine.step(s_all[sl].to(dev), g_all[sl].to(dev))
-    dp.all_reduce_(tr.fp.grad)
+    tr.reduce_grad()
     grad = tr.fp.grad.cpu()
     for _ in range(3):
         tr.train_step()
