@@ -306,15 +306,6 @@ struct CombineArgs {
   float dt;
 };
 
-// Persistent small-scene BPTT (ctrl.hip bptt_small_kernel): one workgroup per env runs the whole
-// reverse-time recursion. The member structs hold time-major / env-major BASE pointers (step 0,
-// env 0); the kernel derives every (t, b) view. nb.partial / eb.partial: one slab row per env.
-struct BpttSmallArgs {
-  CtrlNodeBwdArgs nb;   // pooled (T,B,N,P), S (T+1,B,Nn), G, A (T,B,N,D), valid (T,B), dP / ego (B,N)
-  CtrlEdgeBwdArgs eb;   // idx (T,B,N,K), argmax (T,B,N,128), dEc (B,N,K)
-  CombineArgs cb;       // dS (T+1,B,N), ptr (T*B,Nn+1), edges (T*B,N*K), Gout = Gb (T+1,B,N)
-  int T, Nn;
-};
 
 struct RolloutStatsArgs {
   unsigned long long* dist;   // (T, B) per-env sum of |p_{t+1} - g| over the N agents (x FX_DIST)
@@ -382,9 +373,6 @@ int mb_ctrl_edge_bwd_x3(const mb::CtrlEdgeBwdArgs* a, int num_blocks, hipStream_
 int mb_k16_wg_per_cu(int kernel);
 int mb_k16_wg_per_cu_f16(int kernel);
 int mb_k16_wg_per_cu_x3(int kernel);
-int mb_bptt_small(const mb::BpttSmallArgs* a, hipStream_t st);
-int mb_bptt_small_f16(const mb::BpttSmallArgs* a, hipStream_t st);
-int mb_bptt_small_x3(const mb::BpttSmallArgs* a, hipStream_t st);
 int mb_rev_csr(const mb::CsrArgs* a, hipStream_t st);
 int mb_cbf_match(const mb::CbfMatchArgs* a, hipStream_t st);
 int mb_cbf_dh(const mb::CbfDhArgs* a, int num_blocks, hipStream_t st);

@@ -2202,93 +2202,6 @@ __global__ __launch_bounds__(SR_WAVES * 64) void rollout_small_kernel(RolloutSma
 
 size_t rollout_small_lds() { return (size_t)CTRL_FWD_FRAGS * FRAG_SZ + CTRL_VEC * 4; }
 
-// ---------------------------------------------------------------------------------------
-// Persistent small-scene BPTT (envs of <= NB_CH agents; the reverse-time loop of
-// train.py:58-103's autograd, BpttDriver's launches): one workgroup per env runs, for
-// t = T-1..0, the node backward, the edge backward and the BPTT combine of its env -- the same
-// device bodies as the per-step kernels over a B = 1 view of the env, so the results are those
-// of the launch-per-step path bit for bit. Envs never interact, so the only synchronisation is
-// the workgroup barrier between phases (the phases reuse the dynamic LDS). Weight gradients
-// accumulate in the env's slab row (first step writes).
-// ---------------------------------------------------------------------------------------
-// The phases are separate (non-inlined) functions here: inlined into the time loop the node
-// body's register allocation degrades (scratch spills); each call is one per step.
-template <int D>
-__device__ __noinline__ void node_bwd_call(const CtrlNodeBwdArgs& a, unsigned char* smem, float* P) {
-  node_bwd_body<D>(a, smem, 0, 1, P);
-}
-template <int D>
-__device__ __noinline__ void node_coop_call(const CtrlNodeBwdArgs& a, unsigned char* smem, float* P) {
-  node_bwd_coop<D>(a, smem, 0, 1, P);
-}
-template <int D>
-__device__ __noinline__ void edge_bwd_call(const CtrlEdgeBwdArgs& a, unsigned char* smem, float* P) {
-  edge_bwd_body<D, 0, true>(a, smem, 0, 1, P);    // one 32-agent group at a time over all waves
-}
-
-template <int D>
-__global__ __launch_bounds__(NB_WAVES * 64, 1) void bptt_small_kernel(BpttSmallArgs ba) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  constexpr int R = REC<D>;
-  const int b = blockIdx.x, T = ba.T, Nn = ba.Nn;
-  const int B = ba.nb.B, N = ba.nb.N, K = ba.eb.K;
-  const long nk = (long)N * K;
-  float* Pn = ba.nb.partial + (long)b * CTRL_NODE_PARTIAL;
-  float* Pe = ba.eb.partial + (long)b * CTRL_EDGE_PARTIAL;
-  h16* dPb = ba.nb.dP + (long)b * N * PROW;
-  float4* egb = ba.nb.ego + (long)b * N * R;
-  float4* dEcb = ba.eb.dEc + (long)b * nk * R;
-  for (int t = T - 1; t >= 0; --t) {
-    const long tb = (long)t * B + b;
-    // G_{t+1} = dL/ds_{t+1}: the direct terms dS_T for the last step, else combined in the node
-    // phase's prologue from step t+1's records (fused_combine) and written to Gb[t+1]
-    const float4* Gn = ba.cb.dS + (tb + B) * N * R;
-    const float4* St = ba.nb.S + tb * Nn * R;
-    {
-      CtrlNodeBwdArgs a = ba.nb;
-      a.cdS = nullptr;
-      a.K = K;
-      if (t < T - 1) {
-        a.cdS = ba.cb.dS + (tb + B) * N * R; a.cds_env = N;
-        a.cego = egb; a.cdEc = dEcb;
-        a.cptr = ba.cb.ptr + (tb + B) * (Nn + 1); a.cptr_env = Nn + 1;
-        a.cedges = ba.cb.edges + (tb + B) * nk; a.cedges_env = nk;
-        a.cGn = (t + 1 == T - 1 ? ba.cb.dS : ba.cb.Gout) + (tb + 2 * B) * N * R; a.cgn_env = N;
-        a.cGout = ba.cb.Gout + (tb + B) * N * R; a.cgo_env = N;
-      }
-      a.pooled = ba.nb.pooled + tb * N * PROW; a.p_env = (long)N * PROW;
-      a.S = St; a.s_env = Nn;
-      a.G = ba.nb.G + (long)b * N * D;
-      a.A = ba.nb.A + tb * N * D; a.a_env = N;
-      a.Gn = Gn; a.gn_env = N;
-      a.valid = ba.nb.valid ? ba.nb.valid + tb : nullptr; a.v_env = 1;
-      a.B = 1;
-      a.dP = dPb; a.dp_env = (long)N * PROW;
-      a.ego = egb;
-      a.init = t == T - 1;
-      if (a.coop) node_coop_call<D>(a, smem, Pn);
-      else node_bwd_call<D>(a, smem, Pn);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // dP / ego stores complete
-    __syncthreads();
-    {
-      CtrlEdgeBwdArgs a = ba.eb;
-      a.S = St; a.s_env = Nn;
-      a.idx = ba.eb.idx + tb * nk; a.i_env = nk;
-      a.argmax = ba.eb.argmax + tb * N * 128; a.am_env = (long)N * 128;
-      a.dP = dPb; a.dp_env = (long)N * PROW;
-      a.B = 1;
-      a.dEc = dEcb; a.de_env = nk;
-      a.qsplit = 1;
-      a.init = t == T - 1;
-      edge_bwd_call<D>(a, smem, Pe);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // dEc stores complete (read by the next node phase)
-    __syncthreads();
-  }
-}
-
-size_t bptt_small_lds() { return ctrl_node_bwd_lds() > ctrl_edge_bwd_lds() ? ctrl_node_bwd_lds() : ctrl_edge_bwd_lds(); }
 
 }  // namespace MB_PREC
 }  // namespace mb
@@ -2400,28 +2313,3 @@ extern "C" int MB_SYM(rollout_small)(const mb::RolloutSmallArgs* a, hipStream_t 
   return (int)hipGetLastError();
 }
 
-extern "C" int MB_SYM(bptt_small)(const mb::BpttSmallArgs* a, hipStream_t st) {
-  using namespace mb;
-  using namespace mb::MB_PREC;
-  const int B = a->nb.B, N = a->nb.N, K = a->eb.K;
-  if (K > 16 || K < 1 || N < 1 || N > NB_CH || a->eb.N != N || a->eb.B != B || a->cb.N != N || a->cb.K != K ||
-      a->Nn < N || a->T < 1 || B < 1)
-    return -1;
-  if (!a->nb.partial || !a->eb.partial || !a->nb.dP || !a->nb.ego || !a->eb.dEc || !a->cb.dS || !a->cb.Gout ||
-      !a->cb.ptr || !a->cb.edges)
-    return -2;
-  const size_t lds = bptt_small_lds();
-  {   // static + dynamic LDS must fit one workgroup: refuse before launching
-    hipFuncAttributes fa{};
-    const void* k = a->nb.dim == 3 ? (const void*)bptt_small_kernel<3> : (const void*)bptt_small_kernel<2>;
-    if (hipFuncGetAttributes(&fa, k) != hipSuccess || fa.sharedSizeBytes + lds > 160u * 1024u) return -4;
-  }
-  if (a->nb.dim == 3) {
-    (void)hipFuncSetAttribute((const void*)bptt_small_kernel<3>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL(bptt_small_kernel<3>, dim3(B), dim3(NB_WAVES * 64), lds, st, *a);
-  } else {
-    (void)hipFuncSetAttribute((const void*)bptt_small_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL(bptt_small_kernel<2>, dim3(B), dim3(NB_WAVES * 64), lds, st, *a);
-  }
-  return (int)hipGetLastError();
-}

@@ -353,7 +353,6 @@ class BpttDriver {
     part_node_ = U("part_node"); part_edge_ = U("part_edge");
     wpack_ = U("ctrl_w"); f_ew1f_ = (int)I("f_ew1f"); f_ew2tn_ = (int)I("f_ew2tn");
     dt_ = F("dt"); sqrt3_ = F("sqrt3");
-    small_ = (int)I("small");
     node_chunk_ = (int)I("node_chunk");
     fused_ = c.contains("fused_step") ? (int)I("fused_step") : 0;
     if (fused_ && (node_chunk_ != 32 || nb_node_ != nb_edge_))
@@ -366,31 +365,6 @@ class BpttDriver {
     if (B_ < 1 || N_ < 1 || Nn_ < N_ || K_ < 1 || K_ > 16 || (D_ != 2 && D_ != 3) || Tmax_ < 1 || nb_node_ < 1 ||
         nb_edge_ < 1)
       throw std::invalid_argument("BpttDriver: bad dimensions");
-  }
-
-  // Persistent small-scene BPTT (ctrl.hip bptt_small_kernel): the whole reverse-time loop in
-  // one launch, one workgroup per env; the env slabs are rows 0..B-1.
-  void run_small(int T, float act_coef, u64 stream) {
-    if (T < 1 || T > Tmax_) throw std::invalid_argument("BpttDriver: T out of range");
-    if (!small_) throw std::runtime_error("BpttDriver: built without the small-scene path");
-    mb::BpttSmallArgs a{};
-    a.T = T; a.Nn = Nn_;
-    mb::CtrlNodeBwdArgs& n = a.nb;
-    n.dim = D_; n.pooled = P<const h16>(pooled_); n.S = P<const float4>(S_); n.G = P<const float>(G_);
-    n.A = P<const float>(A_); n.valid = P<const uint8_t>(valid_); n.B = B_; n.N = N_;
-    n.wrm = P<const h16>(wrm_); n.o_w1 = o1_; n.o_w2 = o2_; n.o_w3 = o3_; n.o_w4 = o4_;
-    n.wvec = P<const float>(wvec_); n.act_coef = act_coef; n.act_scale = P<const float>(act_scale_);
-    n.gscale = P<const float>(gscale_);
-    n.dt = dt_; n.sqrt3 = sqrt3_; n.dP = P<h16>(dP_); n.ego = P<float4>(ego_); n.partial = P<float>(part_node_);
-    n.coop = mb::node_bwd_coop_enabled() && N_ <= 64;   // 32-agent chunks over the four waves
-    mb::CtrlEdgeBwdArgs& e = a.eb;
-    e.dim = D_; e.S = n.S; e.idx = P<const int>(idx_); e.argmax = P<const uint8_t>(argmax_); e.dP = n.dP;
-    e.B = B_; e.N = N_; e.K = K_; e.wpack = P<const h16>(wpack_); e.f_ew1f = f_ew1f_; e.f_ew2tn = f_ew2tn_;
-    e.dEc = P<float4>(dEc_); e.partial = P<float>(part_edge_); e.qsplit = 1;
-    mb::CombineArgs& c = a.cb;
-    c.dim = D_; c.dS = P<const float4>(dS_); c.ptr = P<const int>(rptr_); c.edges = P<const int>(redges_);
-    c.Gout = P<float4>(Gb_); c.B = B_; c.N = N_; c.K = K_; c.dt = dt_;
-    chk((prec_ == 2 ? mb_bptt_small_x3 : prec_ == 1 ? mb_bptt_small_f16 : mb_bptt_small)(&a, ST(stream)), "bptt_small");
   }
 
   void run(int T, float act_coef, u64 stream) {
@@ -464,7 +438,7 @@ class BpttDriver {
   }
 
  private:
-  int B_, N_, Nn_, K_, D_, R_, Tmax_, prec_, prow_, nb_node_, nb_edge_, qsplit_, small_ = 0, node_chunk_ = 0, fused_ = 0;
+  int B_, N_, Nn_, K_, D_, R_, Tmax_, prec_, prow_, nb_node_, nb_edge_, qsplit_, node_chunk_ = 0, fused_ = 0;
   u64 pooled_, S_, G_, A_, dS_, Gb_, valid_, idx_, argmax_, rptr_, redges_, wrm_, wvec_, act_scale_, dP_, ego_, dEc_;
   u64 part_node_, part_edge_, wpack_, gscale_ = 0, ew16_ = 0, nw16_ = 0;
   int o1_, o2_, o3_, o4_, f_ew1f_, f_ew2tn_;
@@ -476,8 +450,7 @@ class BpttDriver {
 void register_runtime(py::module& m) {
   py::class_<BpttDriver>(m, "BpttDriver")
       .def(py::init<py::dict>())
-      .def("run", &BpttDriver::run, py::arg("T"), py::arg("act_coef"), py::arg("stream"))
-      .def("run_small", &BpttDriver::run_small, py::arg("T"), py::arg("act_coef"), py::arg("stream"));
+      .def("run", &BpttDriver::run, py::arg("T"), py::arg("act_coef"), py::arg("stream"));
   py::class_<RolloutDriver>(m, "RolloutDriver")
       .def(py::init<py::dict>())
       .def("run_small", &RolloutDriver::run_small, py::arg("stream"), py::arg("early_stop"),

@@ -55,18 +55,11 @@ class HipEngine:
                               # during it (A/B on MI355X: neutral-to-slower, 7.63 vs 7.66 ms; off)
     small_rollout = True      # envs of <= native.SMALL_MAXN graph nodes: the whole rollout is ONE
                               # persistent launch (one workgroup per env, device-side early stop)
-    small_bptt = False        # envs of <= native.SMALL_MAXN agents: the BPTT recursion as ONE
-                              # persistent launch (one workgroup per env). Off: measured 3x slower
-                              # at 32 x 1 (2.17 vs 0.69 ms) -- the per-step launches spread a small
-                              # env's 16 edge tile rounds over 16 workgroups (qsplit), one
-                              # workgroup per env runs them in sequence
-
     def __init__(self, trainer):
         self.tr = trainer
         cfg = trainer.cfg
         # scheduling choices are class attributes (tests / A/B scripts set them); the environment
         # knobs that remain are listed in macbf_gnn_amd/knobs.py
-        self.small_bptt = bool(knobs.get_int("MACBF_SMALL_BPTT", int(self.small_bptt)))
         # instance snapshots of the class-level choices (a test may reset the class attribute)
         self.bptt_groups = int(self.bptt_groups) if cfg.num_envs % self.bptt_groups == 0 else 1
         self._drv = None
@@ -88,7 +81,6 @@ class HipEngine:
             raise ValueError(f"top_k <= {C.MAX_TOP_K} supported by the native kernels")
         self.Tmax = cfg.inner_loops
         self.small_rollout = self.small_rollout and self.native_rollout and self.Nn <= native.SMALL_MAXN
-        self.small_bptt = self.small_bptt and self.native_bptt and self.N <= native.SMALL_MAXN
         if self.small_rollout:
             self.overlap_hfwd = False     # the CBF h of all main slots runs after the one-launch rollout
         # kernel precision (csrc/prec.h): bf16 / fp16 MFMA inputs, or "fp32" -- the reference
@@ -210,7 +202,7 @@ class HipEngine:
             raise ValueError(f"bptt_groups={Gp} must divide num_envs={B}")
         self.grp_nb = native.ctrl_bwd_grids((B // Gp) * N, dev, self.prec, eb16=eb16)
         # slab rows each BPTT path writes (and the slab reduction reads): exactly those, so rows no
-        # path writes are never summed (the persistent small-scene BPTT: one row per env)
+        # path writes are never summed
         self.slab_rows = (self.nb_node, self.nb_edge) if Gp == 1 else (Gp * self.grp_nb[0], Gp * self.grp_nb[1])
         rows_n, rows_e = self.slab_rows
         self.part_node = torch.zeros(max(rows_n, B), native.CTRL_NODE_PARTIAL, dtype=f32, device=dev)
@@ -250,8 +242,7 @@ class HipEngine:
         # the no-BPTT launch T x B x N >= that, so every node launch of this engine takes the same kernel
         Gp = self.bptt_groups
         self.node16_w = (self.pw.node_rm16 if (knobs.get_int("MACBF_NODE16", 1)
-                                               and native.node_bwd_chunk((B // Gp) * N, dev) == 128
-                                               and not self.small_bptt) else None)
+                                               and native.node_bwd_chunk((B // Gp) * N, dev) == 128) else None)
         self.host_dist = torch.zeros(T, B, dtype=torch.int64, pin_memory=True)
         self.copy_stream = torch.cuda.Stream(device=dev)
         self.aux = torch.cuda.Stream(device=dev)      # reverse-CSR build overlaps the CBF kernel
@@ -629,11 +620,7 @@ class HipEngine:
             redges3 = redges[: T * B].view(T, B, N * K)
             Gp = self.bptt_groups
             slab_rows = self.slab_rows
-            if Gp == 1 and red_done is None and self.native_bptt and self.small_bptt:
-                # one persistent launch for the whole recursion (csrc/ctrl.hip bptt_small_kernel)
-                self._bdriver().run_small(T, gs * ACT_COEF, cur.cuda_stream)
-                slab_rows = (B, B)
-            elif Gp == 1 and red_done is None and self.native_bptt:
+            if Gp == 1 and red_done is None and self.native_bptt:
                 # the reverse-time launch loop in C++ (csrc/runtime.cpp): same launches, same order
                 self._bdriver().run(T, gs * ACT_COEF, cur.cuda_stream)
             elif Gp == 1:
@@ -748,7 +735,7 @@ class HipEngine:
                 ctrl_rm=native.ptr(pw.ctrl_rm), o_w1=int(pw.node_rm_off["w1"]), o_w2=int(pw.node_rm_off["w2"]),
                 o_w3=int(pw.node_rm_off["w3"]), o_w4=int(pw.node_rm_off["w4"]), ctrl_v=native.ptr(pw.ctrl_v),
                 ctrl_w=native.ptr(pw.ctrl_w), f_ew1f=int(pw.ctrl_off["ew1f"]), f_ew2tn=int(pw.ctrl_off["ew2tn"]),
-                dt=float(C.TIME_STEP), sqrt3=float(C.SQRT3), small=int(self.small_bptt),
+                dt=float(C.TIME_STEP), sqrt3=float(C.SQRT3),
                 node_chunk=int(native.node_bwd_chunk(B * N, self.dev)),
                 fused_step=int(native.bwd_step_fused(B * N, self.dev)),
                 ctrl_w16=native.ptr(self.eb16_w) if self.eb16_w is not None else 0,

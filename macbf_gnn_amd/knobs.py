@@ -11,9 +11,8 @@ removed (their decision is the code's default, the measurement is in docs/PERF.m
 | MACBF_EXT | -- | ops/native.py | load an alternative extension build (scripts/build_variant.sh A/B, no-barrier builds) |
 | MACBF_NATIVE_BPTT | 1 | engine/hip_engine.py | Python BPTT launch loop, so tests can spy on the calls |
 | MACBF_PREFETCH | 1 | engine/trainer.py | next-iteration scenario sampler: 0 inline, 1 side stream at once, 2 side stream after the enqueued work (A/B) |
-| MACBF_SMALL_BPTT | 0 | engine/hip_engine.py | persistent small-scene BPTT (scripts/gpu_ab_cfg2.sh) |
 | MACBF_CBF16 | 1 (fp32), 0 (bf16 / fp16) | engine/hip_engine.py | 16x16x32 vs 32x32x16 CBF backward (A/B, scripts/gpu_r4_validate.sh) |
-| MACBF_EB16 | 1 (fp32), 0 (bf16 / fp16) | engine/hip_engine.py | 16x16x32 vs 32x32x16 edge backward (tests/test_gpu_small.py compares the persistent kernels with the 32x32x16 one; A/B) |
+| MACBF_EB16 | 1 (fp32), 0 (bf16 / fp16) | engine/hip_engine.py | 16x16x32 vs 32x32x16 edge backward (tests and A/B runs) |
 | MACBF_NODE16 | 1 | engine/hip_engine.py | 32x32x16 node backward (tests/test_gpu_node16.py; bf16 / fp16 A/B) |
 | MACBF_NODE_CHUNK | by size | ops/native.py | agents per node-backward chunk (tests force 128 at small sizes) |
 | MACBF_BWD_FUSED | by size | ops/native.py | fused node + edge BPTT step on / off (tests) |

@@ -63,16 +63,15 @@ def _nan_slabs(tr):
         b.fill_(float("nan"))
 
 
-@pytest.mark.parametrize("mode", ["per_step", "groups", "no_bptt", "small_bptt"])
+@pytest.mark.parametrize("mode", ["per_step", "groups", "no_bptt", "small"])
 def test_stale_slab_rows_never_reach_the_gradient(mode):
     from macbf_gnn_amd.engine.hip_engine import HipEngine
-    old = HipEngine.bptt_groups, HipEngine.small_bptt
+    old = HipEngine.bptt_groups
     HipEngine.bptt_groups = 2 if mode == "groups" else 1
-    HipEngine.small_bptt = mode == "small_bptt"
     try:
-        tr = _trainer(N=32 if mode == "small_bptt" else 96, B=4, bptt=mode != "no_bptt")
+        tr = _trainer(N=32 if mode == "small" else 96, B=4, bptt=mode != "no_bptt")
     finally:
-        HipEngine.bptt_groups, HipEngine.small_bptt = old
+        HipEngine.bptt_groups = old
     s0, g, _ = tr.sample()
     tr.engine.step(s0, g)                       # sizes the lazily allocated slabs
     ref = tr.fp.grad.clone()

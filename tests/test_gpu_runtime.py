@@ -16,12 +16,12 @@ def _trainer(**kw):
     from macbf_gnn_amd.parallel import DP
     cfg = C.TrainConfig(num_agents=kw.pop("N", 64), num_envs=kw.pop("B", 4), inner_loops=kw.pop("T", 30),
                         seed=1, device="hip", **kw)
-    old = HipEngine.small_rollout, HipEngine.small_bptt
-    HipEngine.small_rollout = HipEngine.small_bptt = False
+    old = HipEngine.small_rollout
+    HipEngine.small_rollout = False
     try:
         return Trainer(cfg, device=DEV, dp=DP(device=DEV))
     finally:
-        HipEngine.small_rollout, HipEngine.small_bptt = old
+        HipEngine.small_rollout = old
 
 
 def _rollout(tr, native_rollout, s0, g, early_stop):

@@ -12,19 +12,18 @@ pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda")
 
 
-def _trainer(small, small_bptt=None, **kw):
+def _trainer(small, **kw):
     from macbf_gnn_amd.engine import Trainer
     from macbf_gnn_amd.engine.hip_engine import HipEngine
     from macbf_gnn_amd.parallel import DP
     cfg = C.TrainConfig(num_agents=kw.pop("N", 32), num_envs=kw.pop("B", 4), inner_loops=kw.pop("T", 40),
                         seed=kw.pop("seed", 3), device="hip", **kw)
-    old = HipEngine.small_rollout, HipEngine.small_bptt
+    old = HipEngine.small_rollout
     HipEngine.small_rollout = small
-    HipEngine.small_bptt = small if small_bptt is None else small_bptt
     try:
         tr = Trainer(cfg, device=DEV, dp=DP(device=DEV))
     finally:
-        HipEngine.small_rollout, HipEngine.small_bptt = old
+        HipEngine.small_rollout = old
     assert tr.engine.small_rollout == (small and tr.engine.Nn <= 64)
     return tr
 
@@ -73,7 +72,7 @@ def test_small_rollout_variants(kw):
 
 
 def test_small_rollout_training_step_matches():
-    a, b = _trainer(False, small_bptt=False, T=20), _trainer(True, small_bptt=False, T=20)
+    a, b = _trainer(False, T=20), _trainer(True, T=20)
     b.fp.flat.copy_(a.fp.flat)
     b.engine.after_update()
     s0, g, obs = a.sample()
@@ -99,33 +98,6 @@ def test_small_rollout_repeatable_and_trains():
     assert float(st["agent_steps"]) > 0
 
 
-@pytest.mark.parametrize("kw", [dict(dtype="fp32"), dict(dtype="bf16"), dict(dtype="fp32", dim=3, num_obstacles=2, N=24),
-                                dict(dtype="fp32", N=64, B=2), dict(dtype="bf16", N=10, B=5)])
-def test_small_bptt_matches_per_step_launches(kw, monkeypatch):
-    """Persistent BPTT (one workgroup per env, csrc/ctrl.hip bptt_small_kernel): the same device
-    bodies as the per-step kernels -> the same dL/ds_t recursion and weight gradients bit for bit
-    (slab rows differ: one per env, so the final slab sums may differ in rounding order). The
-    per-step side uses the 32x32x16 edge backward (MACBF_EB16=0), whose body the persistent kernel
-    shares; the 16x16x32 one is pinned to a float64 oracle in test_gpu_oracle16.py."""
-    monkeypatch.setenv("MACBF_EB16", "0")
-    a = _trainer(True, small_bptt=False, T=20, **kw)
-    b = _trainer(True, small_bptt=True, T=20, **kw)
-    assert b.engine.small_bptt and not a.engine.small_bptt
-    b.fp.flat.copy_(a.fp.flat)
-    b.engine.after_update()
-    s0, g, obs = a.sample()
-    a.engine.step(s0, g, obs)
-    b.engine.step(s0, g, obs)
-    torch.cuda.synchronize()
-    assert torch.equal(a.engine.Gb, b.engine.Gb)
-    assert torch.equal(a.engine.dP, b.engine.dP) and torch.equal(a.engine.ego, b.engine.ego)
-    torch.testing.assert_close(b.fp.grad, a.fp.grad, rtol=2e-5, atol=1e-8)
-    b.engine.step(s0, g, obs)           # deterministic run to run
-    g1 = b.fp.grad.clone()
-    b.engine.step(s0, g, obs)
-    assert torch.equal(g1, b.fp.grad)
-
-
 @pytest.mark.parametrize("native_bptt,N,B", [(True, 256, 8), (False, 256, 8), (True, 1024, 12), (False, 1024, 12)])
 def test_fused_bptt_step_matches_separate_launches(native_bptt, N, B, monkeypatch):
     """Fused node + edge backward per reverse step (csrc/ctrl.hip ctrl_bwd_step_kernel, the
@@ -141,7 +113,7 @@ def test_fused_bptt_step_matches_separate_launches(native_bptt, N, B, monkeypatc
     trs = []
     for fused in ("0", "1"):
         monkeypatch.setenv("MACBF_BWD_FUSED", fused)
-        trs.append(_trainer(False, small_bptt=False, N=N, B=B, T=12))
+        trs.append(_trainer(False, N=N, B=B, T=12))
     a, b = trs
     assert b.engine.nb_node == b.engine.nb_edge
     assert native.bwd_step_fused(B * N, b.engine.dev) and native.node_bwd_chunk(B * N, b.engine.dev) == 32
