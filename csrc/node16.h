@@ -27,6 +27,9 @@
 namespace mb {
 namespace MB_PREC {
 
+#ifndef N16_DIAG_NOSTORE
+#define N16_DIAG_NOSTORE 0      // diagnostics build only: skip the dL/dpooled stores (phase clocks)
+#endif
 constexpr int N16_NW = 8, N16_CH = 16 * N16_NW;           // waves, agents per chunk
 constexpr int N16_S1 = 176, N16_S2 = 80, N16_S3 = 144, N16_S4 = 80;   // layout.NODE16_STRIDES (bank model)
 constexpr int N16_O2 = 64 * N16_S1, N16_O3 = N16_O2 + 128 * N16_S2, N16_O4 = N16_O3 + 64 * N16_S3;
@@ -409,12 +412,14 @@ __global__ __launch_bounds__(N16_NW * 64) void ctrl_node_bwd16_kernel(CtrlNodeBw
         for (int s = 0; s < 2; ++s) c = mma16(n16_w1T(W1c, 16 * mt, s, lane), pk4_fr(dY1[2 * s], dY1[2 * s + 1]), c);
       }
       if (mt < 8) {
-        if (ok) {
+        if (ok && !N16_DIAG_NOSTORE) {
           h16* drow = a.dP + (long)b * a.dp_env + (long)i * PROW + 16 * mt + 4 * g;
           const Pk4 v = to_pk4(c);
           *reinterpret_cast<h16x4*>(drow) = v.h;
           if constexpr (X3) *reinterpret_cast<h16x4*>(drow + 128) = v.l;
         }
+        if (mt == 3) stamp(10);                // diagnostics: dP tiles 0..3 done
+        if (mt == 7) stamp(11);                // tiles 4..7 done
       } else {
         // rows 128 + 4g + q: the state slots [p - g, v] (hi: slots 0..2D-1; lane g = 0 holds rows
         // 0..3, lane g = 1 rows 4..7)

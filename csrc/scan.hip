@@ -628,11 +628,17 @@ static bool scan_boxes_global(const ScanArgs& a) {
   return (size_t)2 * (nch + nsc) * 16 > SCAN_BOX_LDS;
 }
 
+// 3-D scenes: lanes per agent of the big-block path (A/B build knob): the 2-D curve order leaves every
+// wave box spanning the whole z range, so fewer agents per wave (a smaller box) cull more
+#ifndef SCAN_LPA3
+#define SCAN_LPA3 SCAN_LPA
+#endif
+
 template <int K, int D>
 static void launch_kd(const ScanArgs& a, hipStream_t st) {
   if (scan_boxes_global(a)) launch_kdb<K, D, SCAN_BS_BIG>(a, st);
   else if (scan_lpa8(a)) launch_kdb<K, D, 256, 8>(a, st);
-  else if (a.Nn > 512 && !scan_small_grid(a)) launch_kdb<K, D, SCAN_BS_BIG>(a, st);
+  else if (a.Nn > 512 && !scan_small_grid(a)) launch_kdb<K, D, SCAN_BS_BIG, D == 3 ? SCAN_LPA3 : SCAN_LPA>(a, st);
   else launch_kdb<K, D, 256>(a, st);
 }
 

@@ -55,6 +55,12 @@ class HipEngine:
                               # during it (A/B on MI355X: neutral-to-slower, 7.63 vs 7.66 ms; off)
     small_rollout = True      # envs of <= native.SMALL_MAXN graph nodes: the whole rollout is ONE
                               # persistent launch (one workgroup per env, device-side early stop)
+    bwd_graph = True          # small scenes (the persistent rollout's <= 64-node envs): everything after
+                              # the rollout (counts, CBF losses + backward, BPTT, gradient assembly)
+                              # replayed from a HIP graph captured once per horizon T -- the host issues
+                              # ~30 launches there and the GPU waited for it (config #2: ~0.1 ms of host
+                              # gaps per iteration, profiles/r5_b2/)
+
     def __init__(self, trainer):
         self.tr = trainer
         cfg = trainer.cfg
@@ -134,6 +140,10 @@ class HipEngine:
         self.graph_mode = bool(getattr(cfg, "graph", False))
         self._graphs = None
         self._graph_gs = None
+        self.bwd_graph = bool(knobs.get_int("MACBF_BWD_GRAPH", int(self.bwd_graph)))
+        self._bwd_graphs = {}          # (T, grad scale) -> CUDAGraph of _counts + _backward
+        self._bwd_pool = None
+        self._bwd_capture = False
         # the 16x16x32 backward kernels this engine runs, once before training (ops/selfcheck.py: a
         # miscompiled schedule stops here instead of corrupting gradients): CBF / edge against their
         # float64 oracles (x3), the node kernel against the 32x32x16 one (every precision)
@@ -461,12 +471,58 @@ class HipEngine:
         # (a high-priority stream for this critical chain was measured slower: 7.62 -> 8.06 ms)
         T = self.rollout(s0, g, obs)
         tm.mark("rollout")
+        if self._bwd_graph_on():
+            return self._backward_graphed(T)
         valid = self._counts(T)
         # the count all-reduce (the only mid-step collective) overlaps the parts of the backward
         # that do not read the global counts (reverse CSR, match, extra h evaluations)
         work = self.tr.dp.all_reduce_async(self.counts)
         tm.mark("counts")
         return self._stats(*self._backward(T, valid, counts_work=work))
+
+    # ------------------------------------------------------------------ per-T backward graphs
+    def _bwd_graph_on(self):
+        return (self.bwd_graph and self.small_rollout and self.native_bptt and self.bptt and not self.graph_mode
+                and not self.tr.dp.enabled and not self.tr.timer.enabled and not torch.cuda.is_current_stream_capturing())
+
+    def _backward_graphed(self, T):
+        """_counts + _backward for horizon T from a HIP graph captured the first time T occurs (that
+        iteration runs eagerly, then the graph is captured: same kernels, same arguments -- every
+        buffer is allocated once per engine, the statistics row is the fixed raw_stats, copied to a
+        ring row after the replay)."""
+        # (the flat gradient's address too: a checkpoint load that rebinds the flat buffers gets a
+        # fresh graph; every other captured buffer lives as long as the engine)
+        key = (int(T), self._gscale()[0], self.tr.fp.grad.data_ptr(), self.tr.fp.flat.data_ptr())
+        g = self._bwd_graphs.get(key)
+        if g is None:
+            valid = self._counts(T)
+            out = self._stats(*self._backward(T, valid))
+            self._capture_bwd(T, key)
+            return out
+        g.replay()
+        self._sums_dirty = False                   # the captured rollout_stats zeroed the sums
+        row = self._next_row()
+        row.copy_(self.raw_stats)
+        return self._stats(row, T)
+
+    def _capture_bwd(self, T, key):
+        cur = torch.cuda.current_stream(self.dev)
+        side = torch.cuda.Stream(device=self.dev)
+        side.wait_stream(cur)
+        if self._bwd_pool is None:
+            self._bwd_pool = torch.cuda.graph_pool_handle()
+        g = torch.cuda.CUDAGraph()
+        dirty = self._sums_dirty
+        self._bwd_capture = True
+        try:
+            with torch.cuda.graph(g, pool=self._bwd_pool, stream=side):
+                valid = self._counts(T)
+                self._backward(T, valid)
+        finally:
+            self._bwd_capture = False
+            self._sums_dirty = dirty
+        cur.wait_stream(side)
+        self._bwd_graphs[key] = g
 
     # ------------------------------------------------------------------ graph mode
     def _step_graph(self, s0, g, obs):
@@ -673,7 +729,7 @@ class HipEngine:
         tm.mark("grad_reduce")
         # ---- stats: one raw device row per iteration (no per-statistic kernels), derived lazily on read
         sums = self.loss_red[:10] if self.dedup else self.red_cbf[native.CBF_P_LOSS: native.CBF_P_LOSS + 10]
-        row = self.raw_stats if self.graph_mode else self._next_row()
+        row = self.raw_stats if (self.graph_mode or self._bwd_capture) else self._next_row()
         native.stats_pack(sums, self.counts, self.local, row)
         Tv = T if not self.graph_mode else (valid != 0).any(1).sum()
         return row, Tv

@@ -17,7 +17,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 PHASES = ["start", "weights", "loads", "L1", "L2", "L3", "L4+gain", "dY3", "S4/S3+dY2", "S2+dY1",
           "S1 stage", "S1", "dP", "chunk end", "slab"]
 PHASES16 = ["start", "weights", "loads+combine", "forward", "gain+dY3", "stage1", "dY2+dY1", "stage2", "stage3",
-            "dP", "-", "-", "-", "chunk end", "slab"]
+            "dP ego tile", "dP tiles 0-3", "dP tiles 4-7", "-", "chunk end", "slab"]
+ORDER16 = [2, 3, 4, 5, 6, 7, 8, 10, 11, 9, 12, 13, 14]   # slots in time order (10, 11 inside the dP loop)
 
 
 def main():
@@ -65,7 +66,7 @@ def main():
     prev = s[:, :, 15].max(dim=1).values                   # (last) chunk start
     rows.append(("to chunk start", float((prev - w1).float().median()), float((prev - w1).float().max())))
     names = PHASES16 if a.node16 else PHASES
-    for k in range(2, 15):
+    for k in (ORDER16 if a.node16 else range(2, 15)):
         if names[k] == "-":
             continue
         tk = s[:, :, k].max(dim=1).values                  # slowest wave reaches phase end

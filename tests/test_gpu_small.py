@@ -128,3 +128,30 @@ def test_fused_bptt_step_matches_separate_launches(native_bptt, N, B, monkeypatc
     assert torch.equal(a.engine.Gb, b.engine.Gb)
     assert torch.equal(a.engine.dP, b.engine.dP) and torch.equal(a.engine.ego, b.engine.ego)
     torch.testing.assert_close(b.fp.grad, a.fp.grad, rtol=2e-5, atol=1e-8)
+
+
+@pytest.mark.parametrize("kw", [dict(dtype="fp32"), dict(dtype="bf16", N=32, B=1), dict(dtype="fp16", N=20, B=3),
+                                dict(dtype="fp32", dim=3, num_obstacles=2, N=24)])
+def test_backward_graph_matches_eager(kw, monkeypatch):
+    """Small scenes: the post-rollout work (counts, CBF losses + backward, BPTT, gradient assembly)
+    replayed from a HIP graph captured per horizon T gives the eager step's gradient and statistics
+    bit for bit -- the first occurrence of a T runs eagerly and captures, later ones replay."""
+    monkeypatch.setenv("MACBF_BWD_GRAPH", "0")
+    a = _trainer(True, T=20, **dict(kw))
+    monkeypatch.setenv("MACBF_BWD_GRAPH", "1")
+    b = _trainer(True, T=20, **dict(kw))
+    assert b.engine._bwd_graph_on() and not a.engine._bwd_graph_on()
+    b.fp.flat.copy_(a.fp.flat)
+    b.engine.after_update()
+    s0, g, obs = a.sample()
+    for it in range(3):
+        sa = a.engine.step(s0, g, obs)
+        ga = a.fp.grad.clone()
+        sb = b.engine.step(s0, g, obs)
+        gb = b.fp.grad.clone()
+        torch.cuda.synchronize()
+        assert torch.isfinite(ga).all()
+        assert torch.equal(ga, gb), it
+        assert torch.equal(sa.raw[:16], sb.raw[:16]), it
+        assert float(sa["T"]) == float(sb["T"])
+    assert len(b.engine._bwd_graphs) == 1
