@@ -27,6 +27,9 @@
 namespace mb {
 namespace MB_PREC {
 
+#ifndef N16_DP_PAIRED
+#define N16_DP_PAIRED 0         // dL/dpooled stores: 16 B per lane from tile pairs (A/B build knob)
+#endif
 #ifndef N16_DIAG_NOSTORE
 #define N16_DIAG_NOSTORE 0      // diagnostics build only: skip the dL/dpooled stores (phase clocks)
 #endif
@@ -412,7 +415,40 @@ __global__ __launch_bounds__(N16_NW * 64) void ctrl_node_bwd16_kernel(CtrlNodeBw
         for (int s = 0; s < 2; ++s) c = mma16(n16_w1T(W1c, 16 * mt, s, lane), pk4_fr(dY1[2 * s], dY1[2 * s + 1]), c);
       }
       if (mt < 8) {
-        if (ok && !N16_DIAG_NOSTORE) {
+        if constexpr (N16_DP_PAIRED) {
+          // tile pair (mt, mt + 1): lanes g and g ^ 1 swap one tile's 4 features, so every lane holds
+          // 8 consecutive ones -- g even: 16 mt + 4g .. +7, g odd: 16 (mt + 1) + 4 (g - 1) .. +7 --
+          // and stores 16 B per plane (a row gets 64 contiguous bytes per store, not 32)
+          if (mt % 2 == 0) {
+            const Pk4 va = to_pk4(c), vb = to_pk4(dpair);
+            const bool odd = (g & 1) != 0;
+            const Pk4 sd = odd ? va : vb;
+            Pk4 rv;
+            {
+              const u32x2v sh = __builtin_bit_cast(u32x2v, sd.h);
+              rv.h = __builtin_bit_cast(h16x4, u32x2v{lane_xor<16>(sh[0]), lane_xor<16>(sh[1])});
+              if constexpr (X3) {
+                const u32x2v sl = __builtin_bit_cast(u32x2v, sd.l);
+                rv.l = __builtin_bit_cast(h16x4, u32x2v{lane_xor<16>(sl[0]), lane_xor<16>(sl[1])});
+              }
+            }
+            const Pk4& lo4 = odd ? rv : va;          // features +0..3 of the 8
+            const Pk4& hi4 = odd ? vb : rv;          // features +4..7
+            if (ok && !N16_DIAG_NOSTORE) {
+              h16* drow = a.dP + (long)b * a.dp_env + (long)i * PROW + (odd ? 16 * (mt + 1) + 4 * (g - 1) : 16 * mt + 4 * g);
+              h16x8 oh;
+#pragma unroll
+              for (int q = 0; q < 4; ++q) { oh[q] = lo4.h[q]; oh[4 + q] = hi4.h[q]; }
+              *reinterpret_cast<h16x8*>(drow) = oh;
+              if constexpr (X3) {
+                h16x8 ol;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) { ol[q] = lo4.l[q]; ol[4 + q] = hi4.l[q]; }
+                *reinterpret_cast<h16x8*>(drow + 128) = ol;
+              }
+            }
+          }
+        } else if (ok && !N16_DIAG_NOSTORE) {
           h16* drow = a.dP + (long)b * a.dp_env + (long)i * PROW + 16 * mt + 4 * g;
           const Pk4 v = to_pk4(c);
           *reinterpret_cast<h16x4*>(drow) = v.h;

@@ -17,3 +17,4 @@ for rep in 1 2; do
   MACBF_EXT=alt_so/lpa3/_C.so timeout -k 10 300 python bench.py --dim 3 --num_obstacles 8 --dtype fp16 > $O/cfg5_lpa3_$rep.log 2>&1 || { echo STOP; exit 1; }
   echo "cfg5 lpa3 $rep $(ms $O/cfg5_lpa3_$rep.log)"
 done
+TAG=r5b7 bash scripts/gpu_r5_b7.sh
