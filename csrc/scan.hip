@@ -12,6 +12,7 @@
 // fp contraction is OFF in this file so distances / TTC decisions are bit-identical to the
 // PyTorch oracle (separately rounded products, same association order).
 #pragma clang fp contract(off)
+#include <algorithm>
 #include <cstdlib>
 #include "common.h"
 #include "args.h"
@@ -234,6 +235,15 @@ __global__ __launch_bounds__(STAGE_BLOCK) void scan_stage_kernel(ScanArgs a) {
   }
 }
 
+// SCAN_FUSE_PROBE (diagnostics): the scan at the occupancy a fused scan +
+// controller-step kernel would give it -- 8-wave blocks, one per CU (the x3 controller step holds
+// 233 registers per lane, two waves per SIMD, and 145 KB of LDS), each block scanning two 128-agent
+// ranges (the 256 agents of one controller block) after ONE staging of its env. Same results.
+#ifndef SCAN_FUSE_PROBE
+#define SCAN_FUSE_PROBE 0
+#endif
+constexpr int SCAN_PASSES = SCAN_FUSE_PROBE ? 2 : 1;
+
 // GLB: 0 = env staged in LDS; 1 = nodes in the global workspace, culling boxes copied to LDS;
 // 2 = boxes read from the workspace too (envs whose boxes exceed LDS: > ~36 K nodes)
 #ifndef SCAN_STAGE_BT
@@ -340,8 +350,10 @@ __global__ __launch_bounds__(BS) void scan_kernel(ScanArgs a) {
   // LPA lanes per agent: lane (r, h) owns curve position base + r and scans candidate slots
   // (SCH/LPA)h.. of every chunk; the partial lists are merged at the end (LPA x the waves of a
   // lane-per-agent layout, 1/LPA of the per-chunk work per lane).
+  // (SCAN_FUSE_PROBE: a block covers SCAN_PASSES consecutive agent ranges after one staging)
+  for (int pass = 0; pass < SCAN_PASSES; ++pass) {
   const int wave = threadIdx.x / WAVE, lane = threadIdx.x & 63, r = lane % APW, h = lane / APW;
-  const int pos = bx * SCAN_AG + wave * APW + r;              // my position on the curve
+  const int pos = (bx * SCAN_PASSES + pass) * SCAN_AG + wave * APW + r;   // my position on the curve
   float4 me = make_float4(0.f, 0.f, 0.f, 0.f), mv = make_float4(0.f, 0.f, 0.f, 0.f);
   int i = -1;
   if (pos < Nn) {
@@ -396,7 +408,7 @@ __global__ __launch_bounds__(BS) void scan_kernel(ScanArgs a) {
   }
   const float wvmax = wave_max(act ? mv.w : 0.f);
   const bool wave_live = __any(act);
-  int cc0 = (bx * SCAN_AG + wave * APW + APW / 2) / SCH;
+  int cc0 = ((bx * SCAN_PASSES + pass) * SCAN_AG + wave * APW + APW / 2) / SCH;
   if (cc0 >= nch) cc0 = nch - 1;
   float thr = wave_max(act ? bound : -INFINITY);   // bound on every agent's final K-th distance
   bool all_danger = false;
@@ -560,12 +572,17 @@ __global__ __launch_bounds__(BS) void scan_kernel(ScanArgs a) {
     }
     if (a.do_safety && a.safe) atomicAdd(a.safe + (long)b * a.sf_env, s2);
   }
+  if constexpr (SCAN_PASSES > 1) __syncthreads();   // red[] is rewritten by the next pass
+  }
 }
 
 #ifndef SCAN_LPA
 #define SCAN_LPA 4      // lanes per agent (A/B at 1024 x 64: 2 -> 4 lanes 65.4 -> 61.5 us per step)
 #endif
 
+#if SCAN_FUSE_PROBE
+#define SCAN_BS_BIG 512
+#endif
 #ifndef SCAN_BS_BIG
 #define SCAN_BS_BIG 1024  // block size above 512 nodes per env (4 lanes/agent: 512 -> 1024, 61.5 -> 60.5 us)
 #endif
@@ -573,7 +590,7 @@ constexpr size_t SCAN_BOX_LDS = 160 * 1024 - 1024;   // LDS budget of the cullin
 
 template <int K, int D, int BS, int LPA = SCAN_LPA>
 static void launch_kdb(const ScanArgs& a, hipStream_t st) {
-  dim3 grid((a.Nn + BS / LPA - 1) / (BS / LPA), a.B);
+  dim3 grid((a.Nn + SCAN_PASSES * BS / LPA - 1) / (SCAN_PASSES * BS / LPA), a.B);
   if (a.Nn > SCAN_MAXN) {
     const int Np = (a.Nn + SCH - 1) / SCH * SCH, nch = Np / SCH, nsc = (nch + SSC - 1) / SSC;
     hipLaunchKernelGGL(scan_stage_kernel<D>, dim3((nch + STAGE_BLOCK - 1) / STAGE_BLOCK, a.B), dim3(STAGE_BLOCK), 0,
@@ -588,7 +605,8 @@ static void launch_kdb(const ScanArgs& a, hipStream_t st) {
     hipLaunchKernelGGL((scan_kernel<K, D, BS, LPA, 1>), grid, dim3(BS), lds, st, a);
     return;
   }
-  const size_t lds = scan_lds_bytes(a.Nn);
+  // (SCAN_FUSE_PROBE: LDS padded to the controller step's 145 KB -> one block per CU)
+  const size_t lds = SCAN_FUSE_PROBE ? std::max(scan_lds_bytes(a.Nn), (size_t)145 * 1024) : scan_lds_bytes(a.Nn);
   (void)hipFuncSetAttribute((const void*)scan_kernel<K, D, BS, LPA, 0>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   hipLaunchKernelGGL((scan_kernel<K, D, BS, LPA, 0>), grid, dim3(BS), lds, st, a);
 }
