@@ -70,6 +70,7 @@ class RolloutDriver {
     // early-stop publication (ctrl.hip publish_step): per-step workgroup counters on the device,
     // the per-env sums and a flag per step in host-coherent memory
     publish_ = c.contains("publish") ? (int)I("publish") : 0;
+    poll_query_ms_ = c.contains("poll_query_ms") ? (int)I("poll_query_ms") : 0;
     if (publish_) {
       const size_t nd = (size_t)Tmax_ * B_, bytes = nd * sizeof(unsigned long long) + (size_t)Tmax_ * sizeof(unsigned);
       chk(hipHostMalloc((void**)&pub_host_, bytes, hipHostMallocMapped | hipHostMallocCoherent), "hipHostMalloc");
@@ -230,9 +231,15 @@ class RolloutDriver {
     const auto t0 = std::chrono::steady_clock::now();
     for (unsigned long n = 0; __atomic_load_n(flag, __ATOMIC_ACQUIRE) != gen_; ++n) {
       if ((n & 4095) == 4095) {
-        const hipError_t e = hipStreamQuery(st);
-        if (e != hipSuccess && e != hipErrorNotReady) chk(e, "rollout stream");
-        if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(60))
+        // the stream-error probe only after poll_query_ms_ of waiting: hipStreamQuery on a busy
+        // stream may enqueue a marker packet, which stalls the queue behind it (A/B knob
+        // MACBF_POLL_QUERY_MS; 0 = probe every 4096 polls)
+        const auto dt = std::chrono::steady_clock::now() - t0;
+        if (dt >= std::chrono::milliseconds(poll_query_ms_)) {
+          const hipError_t e = hipStreamQuery(st);
+          if (e != hipSuccess && e != hipErrorNotReady) chk(e, "rollout stream");
+        }
+        if (dt > std::chrono::seconds(60))
           throw std::runtime_error("RolloutDriver: early-stop flag of step " + std::to_string(t) + " not published");
       }
 #if defined(__x86_64__)
@@ -310,6 +317,7 @@ class RolloutDriver {
   int B_, N_, Nn_, K_, D_, W_, Tmax_, num_cu_, prec_, prow_, resort_, safety_, overlap_, hfwd_blocks_, check_, apw_;
   int publish_ = 0;
   unsigned gen_ = 0;
+  int poll_query_ms_ = 0;
   unsigned long long* pub_host_ = nullptr;   // host view: [Tmax][B] sums, then [Tmax] flags
   unsigned long long* pub_dev_ = nullptr;    // the same memory, device view
   unsigned* pub_ctr_ = nullptr;              // [Tmax] per-step workgroup counters (device)

@@ -15,3 +15,16 @@ for v in cur probe; do
   cp $(find $O/prof_$v -name "*kernel_stats.csv" | head -1) $O/kernel_stats_$v.csv
   python3 $GRAFT_REPO_ROOT/scripts/kstats.py $O/kernel_stats_$v.csv 8 | grep -i "scan\|ctrl_fwd"
 done
+# early-stop wait without the per-wait hipStreamQuery (MACBF_POLL_QUERY_MS=100): kernel trace
+# (gap after each controller step) and interleaved headline A/B
+unset MACBF_EXT
+MACBF_POLL_QUERY_MS=100 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_poll -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py --steps 4 --warmup 2 > $O/prof_poll.log 2>&1 || { tail -5 $O/prof_poll.log; exit 1; }
+cp $(find $O/prof_poll -name "*kernel_trace.csv" | head -1) $O/kernel_trace_poll.csv
+cp $(find $O/prof_cur -name "*kernel_trace.csv" | head -1) $O/kernel_trace_cur.csv
+cd $GRAFT_REPO_ROOT
+ms() { grep '^{' $1 | python -c 'import json,sys; print(round(json.loads(sys.stdin.read())["ms_per_step"],3))'; }
+for rep in 1 2 3; do
+  timeout -k 10 200 python bench.py > $O/poll0_$rep.log 2>&1 || { echo STOP; exit 1; }
+  MACBF_POLL_QUERY_MS=100 timeout -k 10 200 python bench.py > $O/poll100_$rep.log 2>&1 || { echo STOP; exit 1; }
+  echo "poll $rep q0 $(ms $O/poll0_$rep.log) q100 $(ms $O/poll100_$rep.log)"
+done

@@ -3,7 +3,7 @@
 # "transient": no box / slot free, nothing charged); any call that ran -- passed or failed -- is
 # final. Usage: scripts/gpurun_retry.sh TIMEOUT 'command'   (output: the gpurun client's)
 T=$1; shift
-for attempt in 1 2 3 4 5 6 7 8 9 10 11 12; do
+for attempt in $(seq 1 30); do
   /usr/local/graft/bin/gpurun --timeout "$T" -- "$@"
   rc=$?
   st=$(python3 -c "import json;d=json.load(open('gpurun_out/.last_call.json'));print(d.get('status'), d.get('rc'))" 2>/dev/null)
