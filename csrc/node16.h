@@ -27,8 +27,12 @@
 namespace mb {
 namespace MB_PREC {
 
+// dL/dpooled stores: lanes g / g^1 swap one tile's values (permlane16) so every lane stores 16 B
+// hi + 16 B lo of 8 consecutive features, instead of 8 B of 4 from each tile (default since round 5:
+// dP phase 11.9 -> 5.5 k cycles per chunk, headline 10.649-10.658 -> 10.602-10.636 ms fp32, 6.732-6.742
+// -> 6.705-6.724 bf16, interleaved, profiles/r5_b7/; 0 = the 8-byte stores)
 #ifndef N16_DP_PAIRED
-#define N16_DP_PAIRED 0         // dL/dpooled stores: 16 B per lane from tile pairs (A/B build knob)
+#define N16_DP_PAIRED 1
 #endif
 #ifndef N16_DIAG_NOSTORE
 #define N16_DIAG_NOSTORE 0      // diagnostics build only: skip the dL/dpooled stores (phase clocks)
