@@ -54,24 +54,6 @@ static_assert(C16_LDS <= 160 * 1024 / C16_WG_PER_CU - 64, "LDS budget");
 #ifndef CBF16_DBG
 #define CBF16_DBG 0    // 1: per-record forward sums to a.dbg (scripts/check_cbf16.py)
 #endif
-// CBF16_DB (A/B): the weight-gradient stages in four 32-row turns through two alternating
-// buffers with ONE barrier per turn (the two waves of the next turn store while the others
-// contract the current one), instead of two 64-row turns with a barrier pair each. Same number of
-// barriers per chunk, but no phase in which every wave waits for four waves' stores. Buffers (h16
-// elements from stg; a stage-BC buffer = C16_DB_B): stage BC t even [0, B), t odd [B, 2B); stage A
-// t even [0, A), t odd [B, B + A) -- stage A's odd buffer is disjoint from stage BC's even one and
-// vice versa, so the first turn of a stage never overwrites what the last turn of the other stage
-// may still be reading; a buffer is rewritten two turns after its reads, past a barrier.
-#ifndef CBF16_DB
-#define CBF16_DB 0
-#endif
-constexpr int C16_DB_PA = 32 * (S16_64 + S16_128);                  // stage A buffer lo-plane offset
-constexpr int C16_DB_PB = 32 * (S16_128 + 2 * S16_64);              // stage BC buffer lo-plane offset
-constexpr int C16_DB_B = C16_PLANES * C16_DB_PB + 32 * S16_F;       // stage BC buffer (elements)
-static_assert(2 * C16_DB_B <= C16_REGION && C16_DB_B + C16_PLANES * C16_DB_PA <= C16_REGION, "DB buffers fit");
-static_assert(C16_PLANES * C16_DB_PA <= C16_DB_B, "stage A even buffer inside stage BC even buffer");
-static_assert((C16_NW * 256 + 4 * 256) * 2 <= C16_DB_B, "final reduction inside stage BC even buffer");
-
 #ifndef CBF16_REC2
 #define CBF16_REC2 1   // records two chunks ahead, states one chunk ahead (0: record + states at the loop end)
 #endif
@@ -301,32 +283,6 @@ __global__ __launch_bounds__(C16_NW * 64, 2 * C16_WG_PER_CU) void cbf_bwd16_kern
       dw4acc += reduce_scatter16(v, n);
     }
     // ---- stage A: dW3 += dH3pre . H2^T, db3 (two turns of 64 evaluation rows)
-#if CBF16_DB
-    // four turns of 32 rows through two alternating buffers, one barrier each: the two waves of
-    // turn t+1 store while the others still contract turn t (buffer layout: see CBF16_DB)
-#pragma unroll
-    for (int turn = 0; turn < 4; ++turn) {
-      h16* imD = stg + ((turn & 1) ? C16_DB_B : 0);
-      h16* imH = imD + 32 * S16_64;
-      if ((wave >> 1) == turn) {
-        const int row = (wave & 1) * 16 + n;
-#pragma unroll
-        for (int mt = 0; mt < 4; ++mt) store4(imD, S16_64, C16_DB_PA, row, mt, g, D3[mt]);
-#pragma unroll
-        for (int mt = 0; mt < 8; ++mt) store4(imH, S16_128, C16_DB_PA, row, mt, g, H2[mt]);
-      }
-      __syncthreads();
-      const Fr B0 = tr16_fr(imH, S16_128, C16_DB_PA, 0, 16 * na0, lane);
-      const Fr B1 = tr16_fr(imH, S16_128, C16_DB_PA, 0, 16 * (na0 + 1), lane);
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const Fr A = tr16_fr(imD, S16_64, C16_DB_PA, 0, 16 * (ma0 + u), lane);
-        accA[u][0] = mma16(A, B0, accA[u][0]);
-        accA[u][1] = mma16(A, B1, accA[u][1]);
-        if (ua == u && (wave >> 2) == (turn >> 1)) biasA = mma16_bx(A, ones, biasA);
-      }
-    }
-#else
 #pragma unroll
     for (int turn = 0; turn < 2; ++turn) {
       h16* imD = stg;
@@ -353,7 +309,6 @@ __global__ __launch_bounds__(C16_NW * 64, 2 * C16_WG_PER_CU) void cbf_bwd16_kern
       }
       __syncthreads();
     }
-#endif
     stamp(1);
     // ---- dH2pre = (W3^T dH3pre) . relu'(H2); dH1pre = (W2^T dH2pre) . relu'(H1)
     Pk4 D2[8], D1[4];
@@ -396,40 +351,6 @@ __global__ __launch_bounds__(C16_NW * 64, 2 * C16_WG_PER_CU) void cbf_bwd16_kern
     }
     stamp(2);
     // ---- stage BC: dW2 += dH2pre . H1^T, db2; dW1f += dH1pre . F^T (two turns)
-#if CBF16_DB
-#pragma unroll
-    for (int turn = 0; turn < 4; ++turn) {
-      h16* imD2 = stg + (turn & 1) * C16_DB_B;
-      h16* imH1 = imD2 + 32 * S16_128;
-      h16* imD1 = imH1 + 32 * S16_64;
-      h16* imF = imD2 + C16_PLANES * C16_DB_PB;
-      if ((wave >> 1) == turn) {
-        const int row = (wave & 1) * 16 + n;
-#pragma unroll
-        for (int mt = 0; mt < 8; ++mt) store4(imD2, S16_128, C16_DB_PB, row, mt, g, D2[mt]);
-#pragma unroll
-        for (int mt = 0; mt < 4; ++mt) {
-          store4(imH1, S16_64, C16_DB_PB, row, mt, g, H1[mt]);
-          store4(imD1, S16_64, C16_DB_PB, row, mt, g, D1[mt]);
-        }
-        if (g < 2) *reinterpret_cast<h16x8*>(imF + row * S16_F + 8 * g) = F;
-      }
-      __syncthreads();
-      const Fr B0 = tr16_fr(imH1, S16_64, C16_DB_PB, 0, 16 * nb0, lane);
-      const Fr B1 = tr16_fr(imH1, S16_64, C16_DB_PB, 0, 16 * (nb0 + 1), lane);
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const Fr A = tr16_fr(imD2, S16_128, C16_DB_PB, 0, 16 * (mb0 + u), lane);
-        accB[u][0] = mma16(A, B0, accB[u][0]);
-        accB[u][1] = mma16(A, B1, accB[u][1]);
-        if (ub == u) biasB = mma16_bx(A, ones, biasB);
-      }
-      if ((wave >> 2) == (turn & 1)) {
-        const Fr Ac = tr16_fr(imD1, S16_64, C16_DB_PB, 0, 16 * (wave & 3), lane);
-        accC = mma16_bx(Ac, tr16(imF, S16_F, 0, 0, lane), accC);
-      }
-    }
-#else
 #pragma unroll
     for (int turn = 0; turn < 2; ++turn) {
       h16* imD2 = stg;
@@ -466,7 +387,6 @@ __global__ __launch_bounds__(C16_NW * 64, 2 * C16_WG_PER_CU) void cbf_bwd16_kern
       }
       __syncthreads();
     }
-#endif
     stamp(3);
 #if !CBF16_REC2
     ev16_issue<D>(a, rn, nx);

@@ -12,7 +12,6 @@
 // fp contraction is OFF in this file so distances / TTC decisions are bit-identical to the
 // PyTorch oracle (separately rounded products, same association order).
 #pragma clang fp contract(off)
-#include <algorithm>
 #include <cstdlib>
 #include "common.h"
 #include "args.h"
@@ -235,15 +234,6 @@ __global__ __launch_bounds__(STAGE_BLOCK) void scan_stage_kernel(ScanArgs a) {
   }
 }
 
-// SCAN_FUSE_PROBE (diagnostics): the scan at the occupancy a fused scan +
-// controller-step kernel would give it -- 8-wave blocks, one per CU (the x3 controller step holds
-// 233 registers per lane, two waves per SIMD, and 145 KB of LDS), each block scanning two 128-agent
-// ranges (the 256 agents of one controller block) after ONE staging of its env. Same results.
-#ifndef SCAN_FUSE_PROBE
-#define SCAN_FUSE_PROBE 0
-#endif
-constexpr int SCAN_PASSES = SCAN_FUSE_PROBE ? 2 : 1;
-
 // GLB: 0 = env staged in LDS; 1 = nodes in the global workspace, culling boxes copied to LDS;
 // 2 = boxes read from the workspace too (envs whose boxes exceed LDS: > ~36 K nodes)
 #ifndef SCAN_STAGE_BT
@@ -350,10 +340,8 @@ __global__ __launch_bounds__(BS) void scan_kernel(ScanArgs a) {
   // LPA lanes per agent: lane (r, h) owns curve position base + r and scans candidate slots
   // (SCH/LPA)h.. of every chunk; the partial lists are merged at the end (LPA x the waves of a
   // lane-per-agent layout, 1/LPA of the per-chunk work per lane).
-  // (SCAN_FUSE_PROBE: a block covers SCAN_PASSES consecutive agent ranges after one staging)
-  for (int pass = 0; pass < SCAN_PASSES; ++pass) {
   const int wave = threadIdx.x / WAVE, lane = threadIdx.x & 63, r = lane % APW, h = lane / APW;
-  const int pos = (bx * SCAN_PASSES + pass) * SCAN_AG + wave * APW + r;   // my position on the curve
+  const int pos = bx * SCAN_AG + wave * APW + r;              // my position on the curve
   float4 me = make_float4(0.f, 0.f, 0.f, 0.f), mv = make_float4(0.f, 0.f, 0.f, 0.f);
   int i = -1;
   if (pos < Nn) {
@@ -408,7 +396,7 @@ __global__ __launch_bounds__(BS) void scan_kernel(ScanArgs a) {
   }
   const float wvmax = wave_max(act ? mv.w : 0.f);
   const bool wave_live = __any(act);
-  int cc0 = ((bx * SCAN_PASSES + pass) * SCAN_AG + wave * APW + APW / 2) / SCH;
+  int cc0 = (bx * SCAN_AG + wave * APW + APW / 2) / SCH;
   if (cc0 >= nch) cc0 = nch - 1;
   float thr = wave_max(act ? bound : -INFINITY);   // bound on every agent's final K-th distance
   bool all_danger = false;
@@ -572,17 +560,12 @@ __global__ __launch_bounds__(BS) void scan_kernel(ScanArgs a) {
     }
     if (a.do_safety && a.safe) atomicAdd(a.safe + (long)b * a.sf_env, s2);
   }
-  if constexpr (SCAN_PASSES > 1) __syncthreads();   // red[] is rewritten by the next pass
-  }
 }
 
 #ifndef SCAN_LPA
 #define SCAN_LPA 4      // lanes per agent (A/B at 1024 x 64: 2 -> 4 lanes 65.4 -> 61.5 us per step)
 #endif
 
-#if SCAN_FUSE_PROBE
-#define SCAN_BS_BIG 512
-#endif
 #ifndef SCAN_BS_BIG
 #define SCAN_BS_BIG 1024  // block size above 512 nodes per env (4 lanes/agent: 512 -> 1024, 61.5 -> 60.5 us)
 #endif
@@ -590,7 +573,7 @@ constexpr size_t SCAN_BOX_LDS = 160 * 1024 - 1024;   // LDS budget of the cullin
 
 template <int K, int D, int BS, int LPA = SCAN_LPA>
 static void launch_kdb(const ScanArgs& a, hipStream_t st) {
-  dim3 grid((a.Nn + SCAN_PASSES * BS / LPA - 1) / (SCAN_PASSES * BS / LPA), a.B);
+  dim3 grid((a.Nn + BS / LPA - 1) / (BS / LPA), a.B);
   if (a.Nn > SCAN_MAXN) {
     const int Np = (a.Nn + SCH - 1) / SCH * SCH, nch = Np / SCH, nsc = (nch + SSC - 1) / SSC;
     hipLaunchKernelGGL(scan_stage_kernel<D>, dim3((nch + STAGE_BLOCK - 1) / STAGE_BLOCK, a.B), dim3(STAGE_BLOCK), 0,
@@ -605,8 +588,7 @@ static void launch_kdb(const ScanArgs& a, hipStream_t st) {
     hipLaunchKernelGGL((scan_kernel<K, D, BS, LPA, 1>), grid, dim3(BS), lds, st, a);
     return;
   }
-  // (SCAN_FUSE_PROBE: LDS padded to the controller step's 145 KB -> one block per CU)
-  const size_t lds = SCAN_FUSE_PROBE ? std::max(scan_lds_bytes(a.Nn), (size_t)145 * 1024) : scan_lds_bytes(a.Nn);
+  const size_t lds = scan_lds_bytes(a.Nn);
   (void)hipFuncSetAttribute((const void*)scan_kernel<K, D, BS, LPA, 0>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   hipLaunchKernelGGL((scan_kernel<K, D, BS, LPA, 0>), grid, dim3(BS), lds, st, a);
 }
@@ -646,17 +628,14 @@ static bool scan_boxes_global(const ScanArgs& a) {
   return (size_t)2 * (nch + nsc) * 16 > SCAN_BOX_LDS;
 }
 
-// 3-D scenes: lanes per agent of the big-block path (A/B build knob): the 2-D curve order leaves every
-// wave box spanning the whole z range, so fewer agents per wave (a smaller box) cull more
-#ifndef SCAN_LPA3
-#define SCAN_LPA3 SCAN_LPA
-#endif
+// (3-D scenes at 8 lanes per agent -- 8 agents per wave, a smaller wave box in x, y -- measured
+// slower in round 5: config #5 fp16 9.93 vs 9.50-9.52 ms, profiles/r5_b6/)
 
 template <int K, int D>
 static void launch_kd(const ScanArgs& a, hipStream_t st) {
   if (scan_boxes_global(a)) launch_kdb<K, D, SCAN_BS_BIG>(a, st);
   else if (scan_lpa8(a)) launch_kdb<K, D, 256, 8>(a, st);
-  else if (a.Nn > 512 && !scan_small_grid(a)) launch_kdb<K, D, SCAN_BS_BIG, D == 3 ? SCAN_LPA3 : SCAN_LPA>(a, st);
+  else if (a.Nn > 512 && !scan_small_grid(a)) launch_kdb<K, D, SCAN_BS_BIG>(a, st);
   else launch_kdb<K, D, 256>(a, st);
 }
 

@@ -350,7 +350,7 @@ class HipEngine:
                 fork_device_scope=1,
                 # early stop published by the controller kernels (no per-step queue marker / copy)
                 publish=knobs.get_int("MACBF_PUBLISH", 1),
-                poll_query_ms=knobs.get_int("MACBF_POLL_QUERY_MS", 0)))
+                poll_query_ms=knobs.get_int("MACBF_POLL_QUERY_MS", 100)))
             if pw.ctrl_v.numel() < 352 or pw.ctrl_w.numel() < (c["f_node"] + 54) * 512 * (2 if pw.x3 else 1):
                 raise native.NativeError("packed controller weights too small")
             if overlap and (self.hbuf.numel() < 2 * T * BNK or self.src.numel() < 2 * T * BNK):

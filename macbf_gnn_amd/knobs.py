@@ -20,7 +20,7 @@ removed (their decision is the code's default, the measurement is in docs/PERF.m
 | MACBF_EDGE_WG_PER_CU | 1 (x3) | ops/native.py | edge-backward workgroups per CU (tests) |
 | MACBF_BWD_GRAPH | 1 | engine/hip_engine.py | small scenes: post-rollout work replayed from per-T HIP graphs (0: eager, tests / A/B) |
 | MACBF_PUBLISH | 1 | engine/hip_engine.py | early stop through a queue marker instead of kernel publication (tests) |
-| MACBF_POLL_QUERY_MS | 0 | engine/hip_engine.py | early-stop wait: stream-error probe only after this many ms of waiting (A/B) |
+| MACBF_POLL_QUERY_MS | 100 | engine/hip_engine.py | early-stop wait: stream-error probe only after this many ms of waiting (0: every 4096 polls, the marker-per-wait A/B) |
 | MACBF_SELFCHECK | 1 | ops/selfcheck.py | skip the start-up self-check of the 16x16x32 kernels |
 | MACBF_ARCH | gfx950 | csrc/build.py | build target |
 """
