@@ -88,6 +88,7 @@ struct CtrlArgs {
   unsigned long long* pub_dist;       // host-coherent (B) slots of this step
   unsigned* pub_flag;                 // host-coherent flag of this step
   unsigned pub_gen;                   // the rollout's generation number
+  unsigned long long* stamps;         // diagnostics: phase clocks [block][wave][16] (x3 step; null = off)
 };
 
 // Persistent small-scene rollout (ctrl.hip rollout_small_kernel): one workgroup per env runs

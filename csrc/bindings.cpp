@@ -64,8 +64,9 @@ static int ctrl_fwd(u64 S, long s_env, u64 G, u64 idx, long i_env, int B, int N,
                     int f_node, u64 wvec, u64 A, long a_env, u64 Sn, long sn_env, u64 dist_sum, long d_env,
                     u64 act_sum, long ac_env, u64 noise, long n_env, float dt, float obs_r, float sqrt3,
                     u64 pooled, long p_env, u64 argmax, long am_env, int dim, int num_cu, int prec, int apw,
-                    u64 noise_key, float noise_prob, float noise_scale, int noise_t, u64 stream) {
+                    u64 noise_key, float noise_prob, float noise_scale, int noise_t, u64 stamps, u64 stream) {
   mb::CtrlArgs a{};
+  a.stamps = P<unsigned long long>(stamps);
   a.dim = dim;
   a.apw = apw;
   a.S = P<const float4>(S); a.s_env = s_env; a.G = P<const float>(G); a.idx = P<const int>(idx); a.i_env = i_env;

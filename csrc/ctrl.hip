@@ -470,10 +470,23 @@ constexpr int CTRL_FWD_DENSE = 1;
 // quads (an agent that straddles two tiles carries its partial max in a register). Pooled values
 // and argmax slots are bit-identical to the 2-agent x 16-slot path (same per-edge MFMA values,
 // same slot codes and tie rule).
-template <int D, bool SPLIT, bool GNODE = false, bool DENSE12 = false>
+// ST (diagnostics, x3 fused step): per-wave phase clocks to a.stamps[(block * 8 + wave) * 16 + k]:
+// 0 weight staging (from t0, the kernel start), 1 group prologue loads, per edge tile 2 load issue,
+// 3 edge features, 4 edge MLP, 5 pool + stores; 6 pooled-store wait, 7 node phase; 15 tile count
+// (scripts/stamps_ctrl.py). A separate instantiation: no runtime stamp branches in production.
+template <int D, bool SPLIT, bool GNODE = false, bool DENSE12 = false, bool ST = false>
 DEV void ctrl_fwd_groups(const CtrlArgs& a, const h16* wl, const h16* wn, const float* vl, h16* pools, int grp0,
-                         int gstride) {
+                         int gstride, unsigned long long t0 = 0) {
   constexpr bool GPOOL = X3 || SPLIT;
+  unsigned long long ph[16] = {}, tck = t0;
+  auto stamp = [&](int k) {
+    if constexpr (ST) {
+      const unsigned long long t = __builtin_amdgcn_s_memtime();
+      ph[k] += t - tck;
+      tck = t;
+    }
+  };
+  stamp(0);
   const float* eb2 = vl;
   const float* nb2 = vl + 128;
   const float* nb3 = vl + 256;
@@ -520,21 +533,27 @@ DEV void ctrl_fwd_groups(const CtrlArgs& a, const h16* wl, const h16* wn, const 
       ctrl_st_load<D>(a.S, a.s_env, xi0, xs0);
       idx_load(1, xi1);
     }
+    stamp(1);
     for (int q = 0; q < NTL; ++q) {
+      if constexpr (ST) ph[15] += 1;
       const EdgeSt<D> cur = xs0;
       ctrl_st_load<D>(a.S, a.s_env, xi1, xs0);                    // states of tile q+1
       idx_load(q + 2, xi1);                                        // idx of tile q+2
+      stamp(2);
       const bool ok = cur.ok;
       const float eye = (cur.j == cur.i) ? 1.f : 0.f;
       float rp[D], rv[D];
       edge_rel<D>(cur, rp, rv);
       const bool m = ok && (sqrtf(sqsum<D>(rp)) < a.obs_r);   // strict, un-eps'd (controller.py:38-39)
       const h16x8 F = ctrl_edge_frag<D>(rp, rv, eye, ok, h);
+      stamp(3);
       f32x16 Z[4];
       ctrl_edge_tile(F, wl + opaque_zero(), eb2, lane, Z, HOIST_EB ? zb : nullptr);
       const unsigned mask32 = (unsigned)(__ballot(m) & 0xffffffffull);
+      stamp(4);
       if constexpr (DENSE12) {
         pool_dense12<X3, GPOOL>(a, ab, g0, APW, total, q, mask32, Z, carry, pool, lane);
+        stamp(5);
         continue;
       }
       // Masked max-pool of relu(Z) over each agent's 16 rows with the first-occurrence argmax,
@@ -585,11 +604,13 @@ DEV void ctrl_fwd_groups(const CtrlArgs& a, const h16* wl, const h16* wn, const 
       // wrote to global memory (the stores are complete after the wait; the rows were not read
       // before, so no stale L1 line can hide them)
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      stamp(6);
       const int gi = min(g0 + min(r, APW - 1), total - 1);
       int bb, ii;
       agent_bi(ab, gi - g0, N, bb, ii);
       const h16* prow = a.pooled + (long)bb * a.p_env + (long)ii * PROW + 8 * h;
       node_phase<D>(a, g0, APW, total, [&](int kk) { return row_fr(prow + 16 * kk, 128); }, wn, nb2, nb3, nb4, lane);
+      stamp(7);
       continue;
     }
     if constexpr (GPOOL) continue;     // node phase: ctrl_node_groups
@@ -610,6 +631,11 @@ DEV void ctrl_fwd_groups(const CtrlArgs& a, const h16* wl, const h16* wn, const 
                   wn, nb2, nb3, nb4, lane);
     // the pool image is rewritten by the next group: finish all reads first
     lds_wave_sync();
+  }
+  if constexpr (ST) {
+    if ((threadIdx.x & 63) == 0)
+#pragma unroll
+      for (int k = 0; k < 16; ++k) a.stamps[((long)blockIdx.x * (blockDim.x / WAVE) + wave) * 16 + k] = ph[k];
   }
 }
 
@@ -665,9 +691,10 @@ DEV void publish_step(const CtrlArgs& a) {
 
 // FUSE (x3): all 72 fragments in LDS (145 KB) and the node phase of each group in the same
 // wave right after its edge phase (pooled rows through global memory): one launch per step.
-template <int WAVES, int D, bool FUSE = false>
+template <int WAVES, int D, bool FUSE = false, bool ST = false>
 __global__ __launch_bounds__(WAVES * 64) void ctrl_fwd_kernel(CtrlArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const unsigned long long t0 = ST ? __builtin_amdgcn_s_memtime() : 0ull;
   constexpr int NFR = (X3 && !FUSE) ? 18 : CTRL_FWD_FRAGS;          // fragments staged in LDS
   h16* wl = reinterpret_cast<h16*>(smem);                            // ew1f, ew2 (18 frags)
   h16* wn = wl + 18 * FRAG_ELEMS;                                     // nw1f..nw4 (54 frags)
@@ -684,9 +711,9 @@ __global__ __launch_bounds__(WAVES * 64) void ctrl_fwd_kernel(CtrlArgs a) {
   const int nact = min((int)gridDim.x, (ngrp + WAVES - 1) / WAVES);
   const int lb = (ROLL_XCD && (int)blockIdx.x < nact) ? xcd_block((int)blockIdx.x, nact) : (int)blockIdx.x;
   if (CTRL_FWD_DENSE && a.K == 12 && apw % 8 == 0)
-    ctrl_fwd_groups<D, false, FUSE, true>(a, wl, wn, vl, pools, lb * WAVES + wave_id(), gridDim.x * WAVES);
+    ctrl_fwd_groups<D, false, FUSE, true, ST>(a, wl, wn, vl, pools, lb * WAVES + wave_id(), gridDim.x * WAVES, t0);
   else
-    ctrl_fwd_groups<D, false, FUSE>(a, wl, wn, vl, pools, lb * WAVES + wave_id(), gridDim.x * WAVES);
+    ctrl_fwd_groups<D, false, FUSE, false, ST>(a, wl, wn, vl, pools, lb * WAVES + wave_id(), gridDim.x * WAVES, t0);
   if constexpr (!X3 || FUSE) publish_step(a);   // the x3 split path publishes from its node kernel
 }
 
@@ -745,12 +772,16 @@ extern "C" int MB_SYM(ctrl_fwd)(const mb::CtrlArgs* a, int num_cu, hipStream_t s
   // x3: one fused launch (edge + node phase per group, 145 KB of weights)
   if (X3) {
     const size_t ldf = (size_t)CTRL_FWD_FRAGS * FRAG_SZ + CTRL_VEC * 4;
+    auto go = [&](auto kern) {
+      (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ldf);
+      hipLaunchKernelGGL(kern, dim3(blocks), dim3(CTRL_WAVES * 64), ldf, st, b);
+    };
     if (a->dim == 3) {
-      (void)hipFuncSetAttribute((const void*)ctrl_fwd_kernel<CTRL_WAVES, 3, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ldf);
-      hipLaunchKernelGGL((ctrl_fwd_kernel<CTRL_WAVES, 3, true>), dim3(blocks), dim3(CTRL_WAVES * 64), ldf, st, b);
+      if (a->stamps) go(ctrl_fwd_kernel<CTRL_WAVES, 3, true, true>);
+      else go(ctrl_fwd_kernel<CTRL_WAVES, 3, true>);
     } else {
-      (void)hipFuncSetAttribute((const void*)ctrl_fwd_kernel<CTRL_WAVES, 2, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ldf);
-      hipLaunchKernelGGL((ctrl_fwd_kernel<CTRL_WAVES, 2, true>), dim3(blocks), dim3(CTRL_WAVES * 64), ldf, st, b);
+      if (a->stamps) go(ctrl_fwd_kernel<CTRL_WAVES, 2, true, true>);
+      else go(ctrl_fwd_kernel<CTRL_WAVES, 2, true>);
     }
     return (int)hipGetLastError();
   }

@@ -342,7 +342,7 @@ def _records(t, name, lead, W, min_rows=None):
 
 
 def ctrl_fwd(S, G, idx, wpack, f_edge, f_node, wvec, A, Sn, dist_sum, act_sum, noise=None, pooled=None, argmax=None,
-             prec=None, noise_key=None, noise_prob=0.0, noise_scale=0.0, noise_t=0):
+             prec=None, noise_key=None, noise_prob=0.0, noise_scale=0.0, noise_t=0, stamps=None):
     """Fused controller step on per-step views: S/Sn (B,Nn,W) node records (agents first),
     G (B,N,D), idx (B,N,K), A (B,N,D), dist_sum/act_sum (B,) int64 fixed point (x FX_DIST /
     x FX_ACT: order-independent integer atomics), pooled (B,N,128) bf16
@@ -377,6 +377,11 @@ def ctrl_fwd(S, G, idx, wpack, f_edge, f_node, wvec, A, Sn, dist_sum, act_sum, n
         _rows(argmax, 128, "argmax", (B, N))
         if argmax.dtype != torch.uint8:
             raise NativeError("argmax must be uint8")
+    if stamps is not None:   # diagnostics (scripts/stamps_ctrl.py): x3 step only, [blocks, 8 waves, 16]
+        if f16 != 2 or stamps.dtype != torch.int64 or not stamps.is_contiguous():
+            raise NativeError("ctrl_fwd stamps: int64 buffer of the x3 step")
+        if stamps.numel() < 16 * 8 * 2 * num_cu(S.device):       # the grid is at most 2 blocks per CU
+            raise NativeError("ctrl_fwd stamps buffer too small")
     rc = lib().ctrl_fwd(ptr(S), S.stride(0) // W, ptr(G), ptr(idx), idx.stride(0), B, N, K,
                         ptr(wpack), int(f_edge), int(f_node), ptr(wvec),
                         ptr(A), A.stride(0) // D if A is not None else 0,
@@ -388,7 +393,8 @@ def ctrl_fwd(S, G, idx, wpack, f_edge, f_node, wvec, A, Sn, dist_sum, act_sum, n
                         ptr(pooled), pooled.stride(0) if pooled is not None else 0,
                         ptr(argmax), argmax.stride(0) if argmax is not None else 0,
                         D, num_cu(S.device), f16, ctrl_fwd_apw(B * N, S.device, N),
-                        ptr(noise_key), float(noise_prob), float(noise_scale), int(noise_t), stream_handle())
+                        ptr(noise_key), float(noise_prob), float(noise_scale), int(noise_t), ptr(stamps),
+                        stream_handle())
     _ok(rc, "ctrl_fwd")
 
 
