@@ -388,67 +388,83 @@ DEV void pool_store(const PoolDst& d, int nt, int pw_) {
 }
 
 // DENSE12 pool of edge tile q (see ctrl_fwd_groups): Z = relu-free pre-activations of the tile's
-// 32 edges (rows) x 128 features (4 column tiles), mask32 = in-radius rows
-template <bool IS_X3, bool GPOOL>
-DEV void pool_dense12(const CtrlArgs& a, const AgentBase& ab, int g0, int APW, int total, int q, unsigned mask32,
-                      const f32x16 (&Z)[4], int (&carry)[4], h16* pool, int lane) {
+// 32 edges (rows) x 128 features (4 column tiles), mask32 = in-radius rows: the tile's context
+// (emission targets, per-row slot codes), then one step per column tile. (Issuing each column
+// tile's pool right after the next one's MFMA chain measured neutral in round 5: phase clocks
+// 6.8 -> 6.4 k cycles per tile, headline within noise, profiles/r5_b11/.)
+struct PoolCtx { PoolDst d1, d2; int crow[16]; int ph; };
+
+template <bool GPOOL>
+DEV PoolCtx pool_ctx12(const CtrlArgs& a, const AgentBase& ab, int g0, int APW, int total, int q, unsigned mask32,
+                       h16* pool, int lane) {
   const int r = lane & 31, h = lane >> 5;
-  const int ph = (2 * q) % 3;                  // tile phase (uniform)
+  PoolCtx c;
+  c.ph = (2 * q) % 3;                          // tile phase (uniform)
   const int af = (8 * q) / 3;                  // first agent (group-relative) with rows in the tile
-  const bool three = ph != 0;                  // agents completed in this tile: 2 (ph 0) or 3
+  const bool three = c.ph != 0;                // agents completed in this tile: 2 (ph 0) or 3
   // this lane's emissions: half 0 the tile's 1st and 3rd completed agent, half 1 the 2nd
-  const PoolDst d1 = pool_dst(a, ab, g0, APW, total, af + h, pool, GPOOL, r);
-  const PoolDst d2 = pool_dst(a, ab, g0, APW, total, (h == 0 && three) ? af + 2 : APW, pool, GPOOL, r);
+  c.d1 = pool_dst(a, ab, g0, APW, total, af + h, pool, GPOOL, r);
+  c.d2 = pool_dst(a, ab, g0, APW, total, (h == 0 && three) ? af + 2 : APW, pool, GPOOL, r);
   // slot code of every accumulator row: quad j = 2m + h holds slots 4 ((ph + j) mod 3) + i
-  int crow[16];
 #pragma unroll
   for (int m = 0; m < 4; ++m) {
-    const int sq = 4 * ((ph + 2 * m + h) % 3);
+    const int sq = 4 * ((c.ph + 2 * m + h) % 3);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int reg = 4 * m + i;
-      crow[reg] = ((mask32 >> acc_row(reg, h)) & 1u) ? (15 - (sq + i)) : INT_MIN;
+      c.crow[reg] = ((mask32 >> acc_row(reg, h)) & 1u) ? (15 - (sq + i)) : INT_MIN;
     }
   }
+  return c;
+}
+
+template <bool IS_X3, bool GPOOL>
+DEV void pool_step12(const PoolCtx& c, int nt, const f32x16& Zn, int& carry, int lane) {
+  const int h = lane >> 5;
+  int g[4];
 #pragma unroll
-  for (int nt = 0; nt < 4; ++nt) {
-    int g[4];
+  for (int m = 0; m < 4; ++m) {
+    int v[4];
 #pragma unroll
-    for (int m = 0; m < 4; ++m) {
-      int v[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) v[i] = (__float_as_int(Z[nt][4 * m + i]) & -16) | crow[4 * m + i];
-      g[m] = max(max(max(0, v[0]), max(v[1], v[2])), v[3]);
-    }
-    int Q[8];                                  // quad maxima of the whole tile, in row order
-#pragma unroll
-    for (int m = 0; m < 4; ++m) {
-      const int o = shfl_xor32i(g[m]);
-      Q[2 * m] = h ? o : g[m];
-      Q[2 * m + 1] = h ? g[m] : o;
-    }
-    // agents of the tile: ph 0: [0-2] [3-5] [6,7 -> carry]; ph 2: [carry, 0] [1-3] [4-6] [7 -> carry];
-    // ph 1: [carry, 0, 1] [2-4] [5-7]
-    int e0, e1, e2;
-    if (ph == 0) {
-      e0 = max(max(Q[0], Q[1]), Q[2]);
-      e1 = max(max(Q[3], Q[4]), Q[5]);
-      e2 = 0;
-      carry[nt] = max(Q[6], Q[7]);
-    } else if (ph == 2) {
-      e0 = max(carry[nt], Q[0]);
-      e1 = max(max(Q[1], Q[2]), Q[3]);
-      e2 = max(max(Q[4], Q[5]), Q[6]);
-      carry[nt] = Q[7];
-    } else {
-      e0 = max(max(carry[nt], Q[0]), Q[1]);
-      e1 = max(max(Q[2], Q[3]), Q[4]);
-      e2 = max(max(Q[5], Q[6]), Q[7]);
-      carry[nt] = 0;
-    }
-    pool_store<IS_X3, GPOOL>(d1, nt, h ? e1 : e0);
-    pool_store<IS_X3, GPOOL>(d2, nt, e2);
+    for (int i = 0; i < 4; ++i) v[i] = (__float_as_int(Zn[4 * m + i]) & -16) | c.crow[4 * m + i];
+    g[m] = max(max(max(0, v[0]), max(v[1], v[2])), v[3]);
   }
+  int Q[8];                                    // quad maxima of the whole tile, in row order
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    const int o = shfl_xor32i(g[m]);
+    Q[2 * m] = h ? o : g[m];
+    Q[2 * m + 1] = h ? g[m] : o;
+  }
+  // agents of the tile: ph 0: [0-2] [3-5] [6,7 -> carry]; ph 2: [carry, 0] [1-3] [4-6] [7 -> carry];
+  // ph 1: [carry, 0, 1] [2-4] [5-7]
+  int e0, e1, e2;
+  if (c.ph == 0) {
+    e0 = max(max(Q[0], Q[1]), Q[2]);
+    e1 = max(max(Q[3], Q[4]), Q[5]);
+    e2 = 0;
+    carry = max(Q[6], Q[7]);
+  } else if (c.ph == 2) {
+    e0 = max(carry, Q[0]);
+    e1 = max(max(Q[1], Q[2]), Q[3]);
+    e2 = max(max(Q[4], Q[5]), Q[6]);
+    carry = Q[7];
+  } else {
+    e0 = max(max(carry, Q[0]), Q[1]);
+    e1 = max(max(Q[2], Q[3]), Q[4]);
+    e2 = max(max(Q[5], Q[6]), Q[7]);
+    carry = 0;
+  }
+  pool_store<IS_X3, GPOOL>(c.d1, nt, h ? e1 : e0);
+  pool_store<IS_X3, GPOOL>(c.d2, nt, e2);
+}
+
+template <bool IS_X3, bool GPOOL>
+DEV void pool_dense12(const CtrlArgs& a, const AgentBase& ab, int g0, int APW, int total, int q, unsigned mask32,
+                      const f32x16 (&Z)[4], int (&carry)[4], h16* pool, int lane) {
+  const PoolCtx c = pool_ctx12<GPOOL>(a, ab, g0, APW, total, q, mask32, pool, lane);
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt) pool_step12<IS_X3, GPOOL>(c, nt, Z[nt], carry[nt], lane);
 }
 
 // Controller step. bf16 / fp16: edge and node phase in one kernel, the pooled features cross

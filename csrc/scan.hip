@@ -234,6 +234,13 @@ __global__ __launch_bounds__(STAGE_BLOCK) void scan_stage_kernel(ScanArgs a) {
   }
 }
 
+// SCAN_THR_SKIP (A/B build knob): the per-chunk threshold update (group min + wave max) only when
+// some lane of the wave inserted into its list in that chunk, the all-danger update only when some
+// lane's danger flag turned on; the same lists, bits and counts either way
+#ifndef SCAN_THR_SKIP
+#define SCAN_THR_SKIP 0
+#endif
+
 // GLB: 0 = env staged in LDS; 1 = nodes in the global workspace, culling boxes copied to LDS;
 // 2 = boxes read from the workspace too (envs whose boxes exceed LDS: > ~36 K nodes)
 #ifndef SCAN_STAGE_BT
@@ -441,6 +448,7 @@ __global__ __launch_bounds__(BS) void scan_kernel(ScanArgs a) {
         float4 c[HU];
 #pragma unroll
         for (int u = 0; u < HU; ++u) c[u] = tp[cur * SCH + hoff + u];
+        bool ins = false, dch = false;            // this lane's list / danger flag changed in this chunk
 #pragma unroll
         for (int u = 0; u < HU; ++u) {
           const int j = __float_as_int(c[u].w);
@@ -450,7 +458,10 @@ __global__ __launch_bounds__(BS) void scan_kernel(ScanArgs a) {
           if constexpr (D == 3) dp[2] = me.z - c[u].z;
           const float d2 = sqsum<D>(dp);
           const uint64_t key = knn_key(d2, (unsigned)j);
-          if (nk && act && d2 <= bound && key < bk[K - 1]) topk_insert<K>(bk, key);
+          if (nk && act && d2 <= bound && key < bk[K - 1]) {
+            topk_insert<K>(bk, key);
+            ins = true;
+          }
           if (ns && act && !danger) {
             const float4 cv = tv[cur * SCH + hoff + u];
             const float lim = 1.01f * (base_i + a.ttc_check * cv.w) + 1e-4f;
@@ -460,17 +471,19 @@ __global__ __launch_bounds__(BS) void scan_kernel(ScanArgs a) {
               dv[1] = mv.y - cv.y;
               if constexpr (D == 3) dv[2] = mv.z - cv.z;
               danger = ttc_danger<D>(dp, dv, a.r2_check, a.ttc_check);
+              dch = dch || danger;
             }
           }
         }
-        if (nk) {
+        // (SCAN_THR_SKIP: no list of the wave changed in this chunk -> kth and thr are unchanged)
+        if (nk && (!SCAN_THR_SKIP || __any(ins))) {
           // the merged list's K-th distance <= min of the partial lists' K-th distances
           float kth = __uint_as_float((unsigned)(bk[K - 1] >> 32));
 #pragma unroll
           for (int o = APW; o < WAVE; o <<= 1) kth = fminf(kth, grp_xor(kth, o));
           thr = wave_max(act ? fminf(kth, bound) : -INFINITY);
         }
-        if (ns) {
+        if (ns && (!SCAN_THR_SKIP || __any(dch))) {
           // the lane swaps must run on every lane: never inside a short-circuit '||'
           unsigned dg = danger ? 1u : 0u;
 #pragma unroll
