@@ -36,9 +36,10 @@ static int cell_sort(u64 S, long s_env, int B, int N, float L, u64 perm, int rec
 static int scan(u64 S, long s_env, u64 perm, int B, int N, int K, u64 idx, long i_env, u64 dang, u64 cnt, long c_env,
                 u64 safe, long sf_env, float r2_train, float ttc_train, float r2_check, float ttc_check,
                 int do_knn, int do_safety, int Nn, int dim, u64 prev_idx, long pi_env, u64 ws, long ws_env,
-                int lanes, u64 stream) {
+                int lanes, u64 stamps, u64 stream) {
   mb::ScanArgs a{};
   a.lanes = lanes;
+  a.stamps = P<unsigned long long>(stamps);
   a.ws = P<float4>(ws); a.ws_env = ws_env;
   a.prev_idx = P<const int>(prev_idx); a.pi_env = pi_env;
   a.Nn = Nn; a.dim = dim;

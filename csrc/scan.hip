@@ -234,11 +234,12 @@ __global__ __launch_bounds__(STAGE_BLOCK) void scan_stage_kernel(ScanArgs a) {
   }
 }
 
-// SCAN_THR_SKIP (A/B build knob): the per-chunk threshold update (group min + wave max) only when
-// some lane of the wave inserted into its list in that chunk, the all-danger update only when some
-// lane's danger flag turned on; the same lists, bits and counts either way
+// SCAN_THR_SKIP: the per-chunk threshold update (group min + wave max) only when some lane of the
+// wave inserted into its list in that chunk, the all-danger update only when some lane's danger
+// flag turned on; the same lists, bits and counts either way (default since round 5: scan 48.8 ->
+// 47.5 us, headline -0.04 ms, config #5 fp16 9.42-9.43 -> 9.30-9.33 ms, profiles/r5_b12/)
 #ifndef SCAN_THR_SKIP
-#define SCAN_THR_SKIP 0
+#define SCAN_THR_SKIP 1
 #endif
 
 // GLB: 0 = env staged in LDS; 1 = nodes in the global workspace, culling boxes copied to LDS;
@@ -246,8 +247,20 @@ __global__ __launch_bounds__(STAGE_BLOCK) void scan_stage_kernel(ScanArgs a) {
 #ifndef SCAN_STAGE_BT
 #define SCAN_STAGE_BT 4
 #endif
-template <int K, int D, int BS, int LPA, int GLB>
+// ST (diagnostics): per-wave phase clocks and chunk counts to a.stamps[(block * BS/64 + wave) * 16 + k]:
+// 0 env staging, 1 culling boxes, 2 wave setup + temporal bound, 3 candidate loop, 4 list merge,
+// 5 output slots, 6 counts; 8 superchunks visited, 9 chunks tested, 10 chunks evaluated,
+// 11 chunks with an insertion (scripts/stamps_scan.py). A separate instantiation.
+template <int K, int D, int BS, int LPA, int GLB, bool ST = false>
 __global__ __launch_bounds__(BS) void scan_kernel(ScanArgs a) {
+  unsigned long long ph[16] = {}, tck = ST ? __builtin_amdgcn_s_memtime() : 0ull;
+  auto stamp = [&](int k) {
+    if constexpr (ST) {
+      const unsigned long long t = __builtin_amdgcn_s_memtime();
+      ph[k] += t - tck;
+      tck = t;
+    }
+  };
   constexpr int APW = WAVE / LPA;                              // agents per wave
   constexpr int SCAN_AG = BS / LPA;                            // agents (curve positions) per block
   extern __shared__ float4 smem4[];
@@ -313,6 +326,7 @@ __global__ __launch_bounds__(BS) void scan_kernel(ScanArgs a) {
     }
   }
   __syncthreads();
+  stamp(0);
   if constexpr (!GLB) {
   for (int c = threadIdx.x; c < nch; c += BS) {
     float4 lo = make_float4(INFINITY, INFINITY, INFINITY, 0.f);
@@ -344,6 +358,7 @@ __global__ __launch_bounds__(BS) void scan_kernel(ScanArgs a) {
   }
   __syncthreads();
   }
+  stamp(1);
   // LPA lanes per agent: lane (r, h) owns curve position base + r and scans candidate slots
   // (SCH/LPA)h.. of every chunk; the partial lists are merged at the end (LPA x the waves of a
   // lane-per-agent layout, 1/LPA of the per-chunk work per lane).
@@ -407,6 +422,7 @@ __global__ __launch_bounds__(BS) void scan_kernel(ScanArgs a) {
   if (cc0 >= nch) cc0 = nch - 1;
   float thr = wave_max(act ? bound : -INFINITY);   // bound on every agent's final K-th distance
   bool all_danger = false;
+  stamp(2);
   if (wave_live) {
     // gap^2 (x0.999) between this wave's box and a chunk / superchunk box
     auto gap2 = [&](const float4& cl, const float4& chh) {
@@ -433,6 +449,7 @@ __global__ __launch_bounds__(BS) void scan_kernel(ScanArgs a) {
         const float slb = 1.01f * (rc + a.ttc_check * (wvmax + sl.w)) + 1e-4f;
         const bool snk = a.do_knn && !(sd2 > thr);
         const bool sns = a.do_safety && !all_danger && !(sd2 > slb * slb);
+        if constexpr (ST) ph[8] += 1;
         if (!snk && !sns) continue;
       }
       const int c_end = min(sc * SSC + SSC, nch);
@@ -442,7 +459,9 @@ __global__ __launch_bounds__(BS) void scan_kernel(ScanArgs a) {
         const bool nk = a.do_knn && !(bd2 > thr);
         const float lb = 1.01f * (rc + a.ttc_check * (wvmax + cl.w)) + 1e-4f;
         const bool ns = a.do_safety && !all_danger && !(bd2 > lb * lb);
+        if constexpr (ST) ph[9] += 1;
         if (!nk && !ns) continue;
+        if constexpr (ST) ph[10] += 1;
         constexpr int HU = SCH / LPA;
         const int hoff = HU * h;
         float4 c[HU];
@@ -476,6 +495,7 @@ __global__ __launch_bounds__(BS) void scan_kernel(ScanArgs a) {
           }
         }
         // (SCAN_THR_SKIP: no list of the wave changed in this chunk -> kth and thr are unchanged)
+        if constexpr (ST) ph[11] += __any(ins) ? 1 : 0;
         if (nk && (!SCAN_THR_SKIP || __any(ins))) {
           // the merged list's K-th distance <= min of the partial lists' K-th distances
           float kth = __uint_as_float((unsigned)(bk[K - 1] >> 32));
@@ -493,6 +513,7 @@ __global__ __launch_bounds__(BS) void scan_kernel(ScanArgs a) {
       }
     }
   }
+  stamp(3);
   // merge the partial lists (butterfly: every lane ends with the full list; keys are unique:
   // (d2, node id), and the partners' lists are disjoint)
   if (a.do_knn) {
@@ -513,6 +534,7 @@ __global__ __launch_bounds__(BS) void scan_kernel(ScanArgs a) {
     for (int o = APW; o < WAVE; o <<= 1) dg |= grp_xoru(dg, o);
     danger = dg != 0u;
   }
+  stamp(4);
   const bool own = act && h == 0;                              // one lane reports per agent
   float ndang = 0.f, nsafe_e = 0.f, safe_ag = 0.f;
   if (act && a.do_knn) {
@@ -559,6 +581,7 @@ __global__ __launch_bounds__(BS) void scan_kernel(ScanArgs a) {
     }
   }
   if (own && a.do_safety) safe_ag = danger ? 0.f : 1.f;
+  stamp(5);
   ndang = wave_sum(ndang);
   nsafe_e = wave_sum(nsafe_e);
   safe_ag = wave_sum(safe_ag);
@@ -572,6 +595,12 @@ __global__ __launch_bounds__(BS) void scan_kernel(ScanArgs a) {
       atomicAdd(a.cnt + (long)b * a.c_env + 1, s1);
     }
     if (a.do_safety && a.safe) atomicAdd(a.safe + (long)b * a.sf_env, s2);
+  }
+  stamp(6);
+  if constexpr (ST) {
+    if (lane == 0)
+#pragma unroll
+      for (int k = 0; k < 16; ++k) a.stamps[((long)lin0 * (BS / WAVE) + wave) * 16 + k] = ph[k];
   }
 }
 
@@ -602,6 +631,13 @@ static void launch_kdb(const ScanArgs& a, hipStream_t st) {
     return;
   }
   const size_t lds = scan_lds_bytes(a.Nn);
+  if constexpr (K == 12) {
+    if (a.stamps) {           // diagnostics: phase clocks (scripts/stamps_scan.py)
+      (void)hipFuncSetAttribute((const void*)scan_kernel<K, D, BS, LPA, 0, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      hipLaunchKernelGGL((scan_kernel<K, D, BS, LPA, 0, true>), grid, dim3(BS), lds, st, a);
+      return;
+    }
+  }
   (void)hipFuncSetAttribute((const void*)scan_kernel<K, D, BS, LPA, 0>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   hipLaunchKernelGGL((scan_kernel<K, D, BS, LPA, 0>), grid, dim3(BS), lds, st, a);
 }

@@ -218,7 +218,7 @@ def _perm_buf(B, N, device):
 
 
 def scan(S, idx, dang, cnt, safe, *, K, do_knn=True, do_safety=True, perm=None, n_agents=None, prev_idx=None,
-         sort=True, lanes=0):
+         sort=True, lanes=0, stamps=None):
     """K1 over one timestep. S: (B, N, 4) view with env stride (may be a slice of a (B,T+1,N,4)
     buffer); idx/dang: (B, N, K) views; cnt: (B, 2) view; safe: (B,) view.
 
@@ -233,6 +233,9 @@ def scan(S, idx, dang, cnt, safe, *, K, do_knn=True, do_safety=True, perm=None, 
     if lanes not in (0, 4, 8):
         raise NativeError("lanes must be 0 (auto), 4 or 8")
     B, Nn = S.shape[0], S.shape[1]
+    if stamps is not None:   # diagnostics (scripts/stamps_scan.py): [block][wave][16] int64, <= 512 waves per env
+        if K != 12 or stamps.dtype != torch.int64 or stamps.numel() < B * 8192 or not stamps.is_contiguous():
+            raise NativeError("scan stamps: K = 12 and a contiguous int64 buffer of B * 8192")
     D = dim_of(S)
     W = rec_width(D)
     N = Nn if n_agents is None else int(n_agents)     # centres = the first N nodes
@@ -275,7 +278,7 @@ def scan(S, idx, dang, cnt, safe, *, K, do_knn=True, do_safety=True, perm=None, 
                     float(C.DIST_MIN_CHECK * C.DIST_MIN_CHECK), float(C.TIME_TO_COLLISION_CHECK),
                     int(do_knn), int(do_safety), Nn, D, ptr(prev_idx),
                     prev_idx.stride(0) if prev_idx is not None else 0, ptr(ws), int(ws_f4), int(lanes),
-                    stream_handle())
+                    ptr(stamps), stream_handle())
     _ok(rc, "scan")
 
 
