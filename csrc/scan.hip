@@ -234,6 +234,12 @@ __global__ __launch_bounds__(STAGE_BLOCK) void scan_stage_kernel(ScanArgs a) {
   }
 }
 
+// SCAN_WAVE_ATOMIC (A/B build knob): the per-env counts added by every wave instead of one
+// block-level sum after a barrier
+#ifndef SCAN_WAVE_ATOMIC
+#define SCAN_WAVE_ATOMIC 0
+#endif
+
 // SCAN_THR_SKIP: the per-chunk threshold update (group min + wave max) only when some lane of the
 // wave inserted into its list in that chunk, the all-danger update only when some lane's danger
 // flag turned on; the same lists, bits and counts either way (default since round 5: scan 48.8 ->
@@ -585,6 +591,17 @@ __global__ __launch_bounds__(BS) void scan_kernel(ScanArgs a) {
   ndang = wave_sum(ndang);
   nsafe_e = wave_sum(nsafe_e);
   safe_ag = wave_sum(safe_ag);
+  if constexpr (SCAN_WAVE_ATOMIC) {
+    // per-wave atomics, no block barrier: a wave does not wait for the slowest wave of its block
+    // (the counts are sums of 0/1 values, exact in fp32 in any order)
+    if (lane == 0) {
+      if (a.do_knn && a.cnt) {
+        atomicAdd(a.cnt + (long)b * a.c_env + 0, ndang);
+        atomicAdd(a.cnt + (long)b * a.c_env + 1, nsafe_e);
+      }
+      if (a.do_safety && a.safe) atomicAdd(a.safe + (long)b * a.sf_env, safe_ag);
+    }
+  } else {
   if (lane == 0) { red[0][wave] = ndang; red[1][wave] = nsafe_e; red[2][wave] = safe_ag; }
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -595,6 +612,7 @@ __global__ __launch_bounds__(BS) void scan_kernel(ScanArgs a) {
       atomicAdd(a.cnt + (long)b * a.c_env + 1, s1);
     }
     if (a.do_safety && a.safe) atomicAdd(a.safe + (long)b * a.sf_env, s2);
+  }
   }
   stamp(6);
   if constexpr (ST) {
