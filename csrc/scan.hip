@@ -239,6 +239,9 @@ __global__ __launch_bounds__(STAGE_BLOCK) void scan_stage_kernel(ScanArgs a) {
 #ifndef SCAN_WAVE_ATOMIC
 #define SCAN_WAVE_ATOMIC 0
 #endif
+#ifndef SCAN_WAVE_ATOMIC3
+#define SCAN_WAVE_ATOMIC3 SCAN_WAVE_ATOMIC   // 3-D scenes
+#endif
 
 // SCAN_THR_SKIP: the per-chunk threshold update (group min + wave max) only when some lane of the
 // wave inserted into its list in that chunk, the all-danger update only when some lane's danger
@@ -591,7 +594,7 @@ __global__ __launch_bounds__(BS) void scan_kernel(ScanArgs a) {
   ndang = wave_sum(ndang);
   nsafe_e = wave_sum(nsafe_e);
   safe_ag = wave_sum(safe_ag);
-  if constexpr (SCAN_WAVE_ATOMIC) {
+  if constexpr (D == 3 ? SCAN_WAVE_ATOMIC3 : SCAN_WAVE_ATOMIC) {
     // per-wave atomics, no block barrier: a wave does not wait for the slowest wave of its block
     // (the counts are sums of 0/1 values, exact in fp32 in any order)
     if (lane == 0) {
@@ -628,6 +631,9 @@ __global__ __launch_bounds__(BS) void scan_kernel(ScanArgs a) {
 
 #ifndef SCAN_BS_BIG
 #define SCAN_BS_BIG 1024  // block size above 512 nodes per env (4 lanes/agent: 512 -> 1024, 61.5 -> 60.5 us)
+#endif
+#ifndef SCAN_BS_BIG3
+#define SCAN_BS_BIG3 SCAN_BS_BIG   // 3-D scenes
 #endif
 constexpr size_t SCAN_BOX_LDS = 160 * 1024 - 1024;   // LDS budget of the culling boxes (GLB 1)
 
@@ -702,7 +708,7 @@ template <int K, int D>
 static void launch_kd(const ScanArgs& a, hipStream_t st) {
   if (scan_boxes_global(a)) launch_kdb<K, D, SCAN_BS_BIG>(a, st);
   else if (scan_lpa8(a)) launch_kdb<K, D, 256, 8>(a, st);
-  else if (a.Nn > 512 && !scan_small_grid(a)) launch_kdb<K, D, SCAN_BS_BIG>(a, st);
+  else if (a.Nn > 512 && !scan_small_grid(a)) launch_kdb<K, D, D == 3 ? SCAN_BS_BIG3 : SCAN_BS_BIG>(a, st);
   else launch_kdb<K, D, 256>(a, st);
 }
 
