@@ -239,8 +239,12 @@ __global__ __launch_bounds__(STAGE_BLOCK) void scan_stage_kernel(ScanArgs a) {
 #ifndef SCAN_WAVE_ATOMIC
 #define SCAN_WAVE_ATOMIC 0
 #endif
+// 3-D scenes: on (round 5: the 3-D candidate loop varies 1.8x between waves of a block, and with
+// the barrier a wave waited for the block's slowest; with SCAN_BS_BIG3 = 512 config #5 fp16
+// 9.26-9.28 -> 8.54-8.56 ms, fp32 13.70 -> 13.05, interleaved, profiles/r5_b15/); 2-D: off
+// (+0.04 ms at the headline, profiles/r5_b14/)
 #ifndef SCAN_WAVE_ATOMIC3
-#define SCAN_WAVE_ATOMIC3 SCAN_WAVE_ATOMIC   // 3-D scenes
+#define SCAN_WAVE_ATOMIC3 1
 #endif
 
 // SCAN_THR_SKIP: the per-chunk threshold update (group min + wave max) only when some lane of the
@@ -632,8 +636,10 @@ __global__ __launch_bounds__(BS) void scan_kernel(ScanArgs a) {
 #ifndef SCAN_BS_BIG
 #define SCAN_BS_BIG 1024  // block size above 512 nodes per env (4 lanes/agent: 512 -> 1024, 61.5 -> 60.5 us)
 #endif
+// 3-D scenes: 512-thread blocks, two per CU, so one block's slow waves overlap the other block's
+// (with per-wave count atomics: see SCAN_WAVE_ATOMIC3)
 #ifndef SCAN_BS_BIG3
-#define SCAN_BS_BIG3 SCAN_BS_BIG   // 3-D scenes
+#define SCAN_BS_BIG3 512
 #endif
 constexpr size_t SCAN_BOX_LDS = 160 * 1024 - 1024;   // LDS budget of the culling boxes (GLB 1)
 
