@@ -159,7 +159,7 @@ __global__ __launch_bounds__(WAVES * 64) void cbf_fwd_kernel(CbfFwdArgs a) {
   h16* wl = reinterpret_cast<h16*>(smem);
   float* vl = reinterpret_cast<float*>(smem + CBF_FWD_FRAGS * FRAG_SZ);
   __shared__ float red[10][WAVES];
-  block_copy16(wl, a.wpack + (size_t)a.f_fwd * FRAG_ELEMS, CBF_FWD_FRAGS * FRAG_SZ);
+  block_copy16(wl, a.wpack + (size_t)a.f_fwd * FRAG_ELEMS, CBF_FWD_FRAGS * FRAG_SZ, !MB_COPY_ONEWAIT);
   block_copy16(vl, a.wvec, CBF_VEC * 4);
   __syncthreads();
   const int wave = wave_id(), lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
@@ -402,8 +402,8 @@ __global__ __launch_bounds__(NW * 64, CBF_HFWD_MINW) void cbf_hfwd_kernel(CbfFwd
   h16* W3 = W2 + RM_W2;
   h16* wf = W2 + RMP;                         // w1f (2 frags)
   float* vl = reinterpret_cast<float*>(smem + (size_t)RMP * 2 + 2 * FRAG_SZ);
-  block_copy16(W2, a.wrm, RMP * 2);
-  block_copy16(wf, a.wpack + (size_t)a.f_fwd * FRAG_ELEMS, 2 * FRAG_SZ);
+  block_copy16(W2, a.wrm, RMP * 2, !MB_COPY_ONEWAIT);
+  block_copy16(wf, a.wpack + (size_t)a.f_fwd * FRAG_ELEMS, 2 * FRAG_SZ, !MB_COPY_ONEWAIT);
   block_copy16(vl, a.wvec, CBF_VEC * 4);
   __syncthreads();
   const int wave = wave_id(), lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
@@ -589,9 +589,9 @@ __global__ __launch_bounds__(NW * 64, 1) void cbf_bwd_kernel(CbfBwdArgs a) {
   __shared__ float lacc[8][FUSED ? CH / 2 : 1];  // fused: per-lane loss partial sums (pass-0 lanes)
   __shared__ float lred[NW][10];
   __shared__ float red4[NW];
-  block_copy16(W2, a.wrm, RMP * 2);
-  block_copy16(wf, a.wpack + (size_t)a.f_bwd * FRAG_ELEMS, 2 * FRAG_SZ);
-  block_copy16(wf + 2 * FRAG_ELEMS, a.wpack + (size_t)(a.f_bwd + 66) * FRAG_ELEMS, 4 * FRAG_SZ);
+  block_copy16(W2, a.wrm, RMP * 2, !MB_COPY_ONEWAIT);
+  block_copy16(wf, a.wpack + (size_t)a.f_bwd * FRAG_ELEMS, 2 * FRAG_SZ, !MB_COPY_ONEWAIT);
+  block_copy16(wf + 2 * FRAG_ELEMS, a.wpack + (size_t)(a.f_bwd + 66) * FRAG_ELEMS, 4 * FRAG_SZ, !MB_COPY_ONEWAIT);
   block_copy16(vl, a.wvec, CBF_VEC * 4);
   if constexpr (FUSED)
     for (int q = threadIdx.x; q < 8 * CH / 2; q += blockDim.x) (&lacc[0][0])[q] = 0.f;

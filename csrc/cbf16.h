@@ -122,8 +122,8 @@ __global__ __launch_bounds__(C16_NW * 64, 2 * C16_WG_PER_CU) void cbf_bwd16_kern
   float* vl = reinterpret_cast<float*>(smem + C16_LDS_W + C16_LDS_F);
   h16* stg = reinterpret_cast<h16*>(smem + C16_LDS_W + C16_LDS_F + CBF_VEC * 4);
   __shared__ float red4[C16_NW];
-  block_copy16(W2, a.wrm16, (int)C16_LDS_W);
-  block_copy16(wft, a.w16 + 4 * FRAG_ELEMS, (int)C16_LDS_F);
+  block_copy16(W2, a.wrm16, (int)C16_LDS_W, !MB_COPY_ONEWAIT);
+  block_copy16(wft, a.w16 + 4 * FRAG_ELEMS, (int)C16_LDS_F, !MB_COPY_ONEWAIT);
   block_copy16(vl, a.wvec, CBF_VEC * 4);
   __syncthreads();
   const int wave = wave_id(), lane = threadIdx.x & 63, n = lane & 15, g = lane >> 4;

@@ -182,7 +182,13 @@ DEV void lds_wave_order() { asm volatile("" ::: "memory"); }
 #ifndef MB_GLDS_COPY
 #define MB_GLDS_COPY 1
 #endif
-DEV void block_copy16(void* dst, const void* src, int bytes) {
+// MB_COPY_ONEWAIT (A/B build knob): a kernel's back-to-back weight copies wait once, after the last
+#ifndef MB_COPY_ONEWAIT
+#define MB_COPY_ONEWAIT 0
+#endif
+// wait = false (LDS-DMA path): issue only -- consecutive copies then share one latency round trip;
+// the LAST copy before the caller's barrier must wait (vmcnt(0) covers every copy issued before)
+DEV void block_copy16(void* dst, const void* src, int bytes, bool wait = true) {
   const u32x4* s = reinterpret_cast<const u32x4*>(src);
   u32x4* d = reinterpret_cast<u32x4*>(dst);
   const int n = bytes / 16, bd = blockDim.x;
@@ -196,7 +202,7 @@ DEV void block_copy16(void* dst, const void* src, int bytes) {
             (const __attribute__((address_space(1))) void*)(s + i),
             (__attribute__((address_space(3))) void*)(d + (i - lane)), 16, 0, 0);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (wait) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     return;
   }
 #endif

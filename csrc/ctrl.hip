@@ -716,8 +716,8 @@ __global__ __launch_bounds__(WAVES * 64) void ctrl_fwd_kernel(CtrlArgs a) {
   h16* wn = wl + 18 * FRAG_ELEMS;                                     // nw1f..nw4 (54 frags)
   float* vl = reinterpret_cast<float*>(smem + NFR * FRAG_SZ);
   h16* pools = reinterpret_cast<h16*>(smem + NFR * FRAG_SZ + CTRL_VEC * 4);
-  block_copy16(wl, a.wpack + (size_t)a.f_edge * FRAG_ELEMS, 18 * FRAG_SZ);
-  if constexpr (!X3 || FUSE) block_copy16(wn, a.wpack + (size_t)a.f_node * FRAG_ELEMS, 54 * FRAG_SZ);
+  block_copy16(wl, a.wpack + (size_t)a.f_edge * FRAG_ELEMS, 18 * FRAG_SZ, !MB_COPY_ONEWAIT);
+  if constexpr (!X3 || FUSE) block_copy16(wn, a.wpack + (size_t)a.f_node * FRAG_ELEMS, 54 * FRAG_SZ, !MB_COPY_ONEWAIT);
   block_copy16(vl, a.wvec, CTRL_VEC * 4);
   __syncthreads();
   const int apw = (a.apw >= 2 && a.apw <= 32) ? a.apw : 32;
@@ -756,7 +756,7 @@ __global__ __launch_bounds__(WAVES * 64) void ctrl_node_fwd_kernel(CtrlArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   h16* wn = reinterpret_cast<h16*>(smem);                             // nw1f..nw4 (54 frags)
   float* vl = reinterpret_cast<float*>(smem + 54 * FRAG_SZ);
-  block_copy16(wn, a.wpack + (size_t)a.f_node * FRAG_ELEMS, 54 * FRAG_SZ);
+  block_copy16(wn, a.wpack + (size_t)a.f_node * FRAG_ELEMS, 54 * FRAG_SZ, !MB_COPY_ONEWAIT);
   block_copy16(vl, a.wvec, CTRL_VEC * 4);
   __syncthreads();
   ctrl_node_groups<D>(a, wn, vl, blockIdx.x * WAVES + wave_id(), gridDim.x * WAVES);
@@ -981,7 +981,7 @@ DEV void node_bwd_body(const CtrlNodeBwdArgs& a, unsigned char* smem, long c0, l
   h16* wr = reinterpret_cast<h16*>(smem);
   float* vl = reinterpret_cast<float*>(smem + RM * 2);
   h16* stg = reinterpret_cast<h16*>(smem + RM * 2 + CTRL_VEC * 4);
-  block_copy16(wr, a.wrm, RM * 2);
+  block_copy16(wr, a.wrm, RM * 2, !MB_COPY_ONEWAIT);
   block_copy16(vl, a.wvec, CTRL_VEC * 4);
   __syncthreads();
   const float* nb2 = vl + 128;
@@ -1749,7 +1749,7 @@ template <int D, int KC = 0, bool SPLIT = false>
 DEV void edge_bwd_body(const CtrlEdgeBwdArgs& a, unsigned char* smem, long w0, long wstride, float* P) {
   h16* wf = reinterpret_cast<h16*>(smem);                 // ew1f (2) | ew2tn (16) | ew1ft (4)
   h16* stg = reinterpret_cast<h16*>(smem + 22 * FRAG_SZ);
-  block_copy16(wf, a.wpack + (size_t)a.f_ew1f * FRAG_ELEMS, 2 * FRAG_SZ);
+  block_copy16(wf, a.wpack + (size_t)a.f_ew1f * FRAG_ELEMS, 2 * FRAG_SZ, !MB_COPY_ONEWAIT);
   block_copy16(wf + 2 * FRAG_ELEMS, a.wpack + (size_t)a.f_ew2tn * FRAG_ELEMS, 20 * FRAG_SZ);
   __syncthreads();
   const int wave = wave_id(), lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
@@ -2187,8 +2187,8 @@ __global__ __launch_bounds__(SR_WAVES * 64) void rollout_small_kernel(RolloutSma
   h16* wn = wl + 18 * FRAG_ELEMS;                                     // nw1f..nw4 (54 frags)
   float* vl = reinterpret_cast<float*>(smem + (size_t)CTRL_FWD_FRAGS * FRAG_SZ);
   const CtrlArgs& c = ra.c;
-  block_copy16(wl, c.wpack + (size_t)c.f_edge * FRAG_ELEMS, 18 * FRAG_SZ);
-  block_copy16(wn, c.wpack + (size_t)c.f_node * FRAG_ELEMS, 54 * FRAG_SZ);
+  block_copy16(wl, c.wpack + (size_t)c.f_edge * FRAG_ELEMS, 18 * FRAG_SZ, !MB_COPY_ONEWAIT);
+  block_copy16(wn, c.wpack + (size_t)c.f_node * FRAG_ELEMS, 54 * FRAG_SZ, !MB_COPY_ONEWAIT);
   block_copy16(vl, c.wvec, CTRL_VEC * 4);
   __syncthreads();
   const int b = blockIdx.x, B = c.B, N = c.N, K = c.K, Nn = ra.Nn, Tmax = ra.Tmax;
@@ -2276,7 +2276,8 @@ extern "C" int MB_SYM(ctrl_node_bwd)(const mb::CtrlNodeBwdArgs* a, int num_block
                                : (b.coop ? (const void*)ctrl_node_bwd_coop_kernel<2> : (const void*)ctrl_node_bwd_kernel<2>);
   (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   void* kargs[] = {&b};
-  hipLaunchKernel(fn, dim3(num_blocks), dim3(NB_WAVES * 64), kargs, lds, st);
+  const hipError_t rc = hipLaunchKernel(fn, dim3(num_blocks), dim3(NB_WAVES * 64), kargs, lds, st);
+  if (rc != hipSuccess) return (int)rc;
   return (int)hipGetLastError();
 }
 

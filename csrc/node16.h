@@ -123,7 +123,7 @@ __global__ __launch_bounds__(N16_NW * 64) void ctrl_node_bwd16_kernel(CtrlNodeBw
     }
   };
   stamp(0);
-  block_copy16(W1, a.wrm16, (int)N16_LDS_W);
+  block_copy16(W1, a.wrm16, (int)N16_LDS_W, !MB_COPY_ONEWAIT);
   block_copy16(vl, a.wvec + 128, N16_VEC * 4);
   __syncthreads();
   stamp(1);
