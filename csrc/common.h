@@ -182,9 +182,11 @@ DEV void lds_wave_order() { asm volatile("" ::: "memory"); }
 #ifndef MB_GLDS_COPY
 #define MB_GLDS_COPY 1
 #endif
-// MB_COPY_ONEWAIT (A/B build knob): a kernel's back-to-back weight copies wait once, after the last
+// MB_COPY_ONEWAIT: a kernel's back-to-back weight copies wait once, after the last (default since
+// round 5: controller-step staging 6.0 -> 4.7 k cycles, headline fp32 10.609-10.643 -> 10.557-10.587
+// ms interleaved, bf16 neutral, profiles/r5_b18/; 0 = a wait after every copy)
 #ifndef MB_COPY_ONEWAIT
-#define MB_COPY_ONEWAIT 0
+#define MB_COPY_ONEWAIT 1
 #endif
 // wait = false (LDS-DMA path): issue only -- consecutive copies then share one latency round trip;
 // the LAST copy before the caller's barrier must wait (vmcnt(0) covers every copy issued before)
