@@ -429,8 +429,8 @@ DEV PoolCtx pool_ctx12(const CtrlArgs& a, const AgentBase& ab, int g0, int APW, 
   return c;
 }
 
-// the tile's two emissions for column tile nt (pooled value | slot code, see pool_store)
-DEV void pool_vals12(const PoolCtx& c, const f32x16& Zn, int& carry, int lane, int& v1, int& v2) {
+template <bool IS_X3, bool GPOOL>
+DEV void pool_step12(const PoolCtx& c, int nt, const f32x16& Zn, int& carry, int lane) {
   const int h = lane >> 5;
   int g[4];
 #pragma unroll
@@ -466,72 +466,14 @@ DEV void pool_vals12(const PoolCtx& c, const f32x16& Zn, int& carry, int lane, i
     e2 = max(max(Q[5], Q[6]), Q[7]);
     carry = 0;
   }
-  v1 = h ? e1 : e0;
-  v2 = e2;
+  pool_store<IS_X3, GPOOL>(c.d1, nt, h ? e1 : e0);
+  pool_store<IS_X3, GPOOL>(c.d2, nt, e2);
 }
-
-template <bool IS_X3, bool GPOOL>
-DEV void pool_step12(const PoolCtx& c, int nt, const f32x16& Zn, int& carry, int lane) {
-  int v1, v2;
-  pool_vals12(c, Zn, carry, lane, v1, v2);
-  pool_store<IS_X3, GPOOL>(c.d1, nt, v1);
-  pool_store<IS_X3, GPOOL>(c.d2, nt, v2);
-}
-
-// CTRL_POOL_PACK (A/B build knob, global pooled rows): a lane's four emissions of a tile (features
-// r, 32 + r, 64 + r, 96 + r of one agent) are transposed inside each 4-lane quad, so every lane
-// stores four CONSECUTIVE features: one 8-byte hi, one 8-byte lo and one 4-byte argmax store per
-// agent and tile instead of four 2-byte / 1-byte stores each (the step's phase clocks without any
-// pooled stores: pool + stores 3.8 -> 2.9 k cycles per tile)
-#ifndef CTRL_POOL_PACK
-#define CTRL_POOL_PACK 0
-#endif
-template <bool IS_X3>
-DEV void pool_store_packed(const PoolDst& d, int (&v)[4], int lane) {
-  const int j = lane & 3;
-  // 4x4 transpose of (lane j of the quad, column tile n): swap the off-diagonal 2x2 blocks (xor 2),
-  // then the off-diagonal elements of each block (xor 1); afterwards lane j holds column tile j
-  // for the quad's four features. Every lane runs it (DPP partners), before the ok test.
-  {
-    int t[4];
-#pragma unroll
-    for (int n = 0; n < 4; ++n) t[n] = (int)lane_xor<2>((unsigned)v[n ^ 2]);
-#pragma unroll
-    for (int n = 0; n < 4; ++n) v[n] = ((n & 2) != (j & 2)) ? t[n] : v[n];
-#pragma unroll
-    for (int n = 0; n < 4; ++n) t[n] = (int)lane_xor<1>((unsigned)v[n ^ 1]);
-#pragma unroll
-    for (int n = 0; n < 4; ++n) v[n] = ((n & 1) != (j & 1)) ? t[n] : v[n];
-  }
-  if (!d.ok) return;
-  const int r = lane & 31, off = 32 * j + 4 * (r >> 2) - r;   // from feature r to 32j + 4q
-  h16x4 hi, lo;
-  unsigned am = 0;
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const float pv = __int_as_float(v[k] & -16);
-    hi[k] = (h16)pv;
-    lo[k] = (h16)(pv - (float)hi[k]);
-    am |= ((v[k] > 15) ? (15u - (unsigned)(v[k] & 15)) : 0xFFu) << (8 * k);
-  }
-  *reinterpret_cast<h16x4*>(d.prow + off) = hi;
-  if constexpr (IS_X3) *reinterpret_cast<h16x4*>(d.prow + off + 128) = lo;
-  if (d.arow) *reinterpret_cast<unsigned*>(d.arow + off) = am;
-}
-
 
 template <bool IS_X3, bool GPOOL>
 DEV void pool_dense12(const CtrlArgs& a, const AgentBase& ab, int g0, int APW, int total, int q, unsigned mask32,
                       const f32x16 (&Z)[4], int (&carry)[4], h16* pool, int lane) {
   const PoolCtx c = pool_ctx12<GPOOL>(a, ab, g0, APW, total, q, mask32, pool, lane);
-  if constexpr (GPOOL && CTRL_POOL_PACK) {
-    int v1[4], v2[4];
-#pragma unroll
-    for (int nt = 0; nt < 4; ++nt) pool_vals12(c, Z[nt], carry[nt], lane, v1[nt], v2[nt]);
-    pool_store_packed<IS_X3>(c.d1, v1, lane);
-    pool_store_packed<IS_X3>(c.d2, v2, lane);
-    return;
-  }
 #pragma unroll
   for (int nt = 0; nt < 4; ++nt) pool_step12<IS_X3, GPOOL>(c, nt, Z[nt], carry[nt], lane);
 }
