@@ -378,21 +378,10 @@ DEV PoolDst pool_dst(const CtrlArgs& a, const AgentBase& ab, int g0, int APW, in
 }
 
 template <bool IS_X3, bool GPOOL>
-// CTRL_DIAG_NOPOOLSTORE (diagnostics build only, wrong results): the pooled values and argmax
-// slots are computed but not stored (phase clocks of the store cost)
-#ifndef CTRL_DIAG_NOPOOLSTORE
-#define CTRL_DIAG_NOPOOLSTORE 0
-#endif
 DEV void pool_store(const PoolDst& d, int nt, int pw_) {
   if (!d.ok) return;
   const float pv = __int_as_float(pw_ & -16);
   const h16 ph = (h16)pv;
-#if CTRL_DIAG_NOPOOLSTORE
-  const h16 pl = (h16)(pv - (float)ph);
-  const unsigned am = (pw_ > 15) ? (15u - (unsigned)(pw_ & 15)) : 0xFFu;
-  asm volatile("" :: "v"(ph), "v"(pl), "v"(am));
-  return;
-#endif
   d.prow[32 * nt] = ph;
   if constexpr (IS_X3 && GPOOL) d.prow[32 * nt + 128] = (h16)(pv - (float)ph);
   if (d.arow) d.arow[32 * nt] = (pw_ > 15) ? (uint8_t)(15 - (pw_ & 15)) : (uint8_t)0xFF;
