@@ -263,7 +263,8 @@ __global__ __launch_bounds__(STAGE_BLOCK) void scan_stage_kernel(ScanArgs a) {
 // ST (diagnostics): per-wave phase clocks and chunk counts to a.stamps[(block * BS/64 + wave) * 16 + k]:
 // 0 env staging, 1 culling boxes, 2 wave setup + temporal bound, 3 candidate loop, 4 list merge,
 // 5 output slots, 6 counts; 8 superchunks visited, 9 chunks tested, 10 chunks evaluated,
-// 11 chunks with an insertion (scripts/stamps_scan.py). A separate instantiation.
+// 11 chunks with an insertion, 12 evaluated for the kNN, 13 for the safety test only
+// (scripts/stamps_scan.py). A separate instantiation.
 template <int K, int D, int BS, int LPA, int GLB, bool ST = false>
 __global__ __launch_bounds__(BS) void scan_kernel(ScanArgs a) {
   unsigned long long ph[16] = {}, tck = ST ? __builtin_amdgcn_s_memtime() : 0ull;
@@ -474,7 +475,7 @@ __global__ __launch_bounds__(BS) void scan_kernel(ScanArgs a) {
         const bool ns = a.do_safety && !all_danger && !(bd2 > lb * lb);
         if constexpr (ST) ph[9] += 1;
         if (!nk && !ns) continue;
-        if constexpr (ST) ph[10] += 1;
+        if constexpr (ST) { ph[10] += 1; ph[12] += nk ? 1 : 0; ph[13] += nk ? 0 : 1; }
         constexpr int HU = SCH / LPA;
         const int hoff = HU * h;
         float4 c[HU];
