@@ -247,6 +247,20 @@ __global__ __launch_bounds__(STAGE_BLOCK) void scan_stage_kernel(ScanArgs a) {
 #define SCAN_WAVE_ATOMIC3 1
 #endif
 
+// SCAN_CELL3 (A/B build knob): 3-D scenes with a temporal bound search a uniform 8^3 cell grid of
+// the env around each agent instead of the wave-uniform chunk culling. The 2-D curve order leaves
+// every chunk a full-height column and every wave box as tall as the env, so a 3-D wave evaluates
+// ~2x the chunks of a 2-D one (stamps_scan.py: 30 vs 14); with cells each agent's four lanes visit
+// only the cells within its own bound (the largest current distance of its previous K neighbours)
+// and safety reach. Same keys, same exact tests: the same lists, bits and counts.
+#ifndef SCAN_CELL3
+#define SCAN_CELL3 0
+#endif
+constexpr int CELL_G = 8, CELL_G3 = CELL_G * CELL_G * CELL_G;
+static inline size_t scan_cell_lds(int Np) { return (size_t)(2 * CELL_G3 + 1) * 4 + (size_t)Np * 2; }
+// cell coordinate of a scaled position (monotone; NaN and values below 0 -> 0, above -> G-1)
+DEV int cell_coord(float x) { return x >= 1.f ? (x < (float)(CELL_G - 1) ? (int)x : CELL_G - 1) : 0; }
+
 // SCAN_THR_SKIP: the per-chunk threshold update (group min + wave max) only when some lane of the
 // wave inserted into its list in that chunk, the all-danger update only when some lane's danger
 // flag turned on; the same lists, bits and counts either way (default since round 5: scan 48.8 ->
@@ -372,6 +386,70 @@ __global__ __launch_bounds__(BS) void scan_kernel(ScanArgs a) {
   }
   __syncthreads();
   }
+  // 3-D cell grid over the env's bounding box (SCAN_CELL3): counting sort of the staged curve
+  // positions by cell; the order inside a cell is irrelevant (the lists are exact for any order)
+  constexpr bool CELLS = D == 3 && SCAN_CELL3 && !GLB && BS >= CELL_G3;
+  const bool use_cells = CELLS && a.prev_idx && a.do_knn;      // uniform per launch
+  __shared__ float cgrid[8];                                   // lo.xyz, 1 / cell size.xyz, max |v|
+  int* cstart = reinterpret_cast<int*>(pinv + Np);             // [G^3 + 1] cell starts
+  int* cfill = cstart + CELL_G3 + 1;                           // [G^3] fill counters
+  unsigned short* clist = reinterpret_cast<unsigned short*>(cfill + CELL_G3);   // [Np] curve positions
+  auto cell_of = [&](float x, float y, float z) {
+    return (cell_coord((z - cgrid[2]) * cgrid[5]) * CELL_G + cell_coord((y - cgrid[1]) * cgrid[4])) * CELL_G +
+           cell_coord((x - cgrid[0]) * cgrid[3]);
+  };
+  if constexpr (CELLS) {
+    if (use_cells) {
+      if (threadIdx.x == 0) {
+        float lx = INFINITY, ly = INFINITY, lz = INFINITY, hx = -INFINITY, hy = -INFINITY, hz = -INFINITY, vm = 0.f;
+        for (int c = 0; c < nsc; ++c) {
+          const float4 l = sbl[c], u = sbh[c];
+          lx = fminf(lx, l.x); ly = fminf(ly, l.y); lz = fminf(lz, l.z); vm = fmaxf(vm, l.w);
+          hx = fmaxf(hx, u.x); hy = fmaxf(hy, u.y); hz = fmaxf(hz, u.z);
+        }
+        const float g = (float)CELL_G;
+        cgrid[0] = lx; cgrid[1] = ly; cgrid[2] = lz;
+        cgrid[3] = g / fmaxf(hx - lx, 1e-6f); cgrid[4] = g / fmaxf(hy - ly, 1e-6f); cgrid[5] = g / fmaxf(hz - lz, 1e-6f);
+        cgrid[6] = vm;
+      }
+      for (int c = threadIdx.x; c < CELL_G3; c += BS) { cstart[c] = 0; cfill[c] = 0; }
+      __syncthreads();
+      for (int q = threadIdx.x; q < Nn; q += BS) {
+        const float4 t = tp[q];
+        atomicAdd(&cfill[cell_of(t.x, t.y, t.z)], 1);
+      }
+      __syncthreads();
+      // exclusive scan of the G^3 counts: wave scans, then the wave totals (one thread per cell)
+      __shared__ int wtot[CELL_G3 / WAVE];
+      const int tid = threadIdx.x, ln = tid & 63, wv = tid / WAVE;
+      int v = 0, x = 0;
+      if (tid < CELL_G3) {
+        v = cfill[tid];
+        x = v;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+          const int y = __shfl_up(x, o);
+          if (ln >= o) x += y;
+        }
+        if (ln == 63) wtot[wv] = x;
+      }
+      __syncthreads();
+      if (tid < CELL_G3) {
+        int pre = 0;
+        for (int w = 0; w < wv; ++w) pre += wtot[w];
+        cstart[tid] = pre + x - v;
+        cfill[tid] = 0;
+        if (tid == CELL_G3 - 1) cstart[CELL_G3] = pre + x;
+      }
+      __syncthreads();
+      for (int q = threadIdx.x; q < Nn; q += BS) {
+        const float4 t = tp[q];
+        const int c = cell_of(t.x, t.y, t.z);
+        clist[cstart[c] + atomicAdd(&cfill[c], 1)] = (unsigned short)q;
+      }
+      __syncthreads();
+    }
+  }
   stamp(1);
   // LPA lanes per agent: lane (r, h) owns curve position base + r and scans candidate slots
   // (SCH/LPA)h.. of every chunk; the partial lists are merged at the end (LPA x the waves of a
@@ -437,7 +515,63 @@ __global__ __launch_bounds__(BS) void scan_kernel(ScanArgs a) {
   float thr = wave_max(act ? bound : -INFINITY);   // bound on every agent's final K-th distance
   bool all_danger = false;
   stamp(2);
-  if (wave_live) {
+  if constexpr (CELLS) {
+    if (use_cells && wave_live) {
+      // this agent's cell box: its bound (kNN) and safety reach, with a margin for the float
+      // rounding of d2 and of the cell mapping; lane h of the agent takes cells h, h + LPA, ...
+      const float Rk = sqrtf(fmaxf(bound, 0.f)) * 1.001f + 1e-5f;
+      const float Rs = a.do_safety ? (1.01f * (base_i + a.ttc_check * cgrid[6]) + 1e-4f) * 1.001f + 1e-5f : 0.f;
+      float R = fmaxf(Rk, Rs);
+      if (!(R < INFINITY) || !(me.x == me.x && me.y == me.y && me.z == me.z)) R = INFINITY;   // whole grid
+      int c0[3], c1[3];
+      {
+        const float pc[3] = {me.x, me.y, me.z};
+#pragma unroll
+        for (int d = 0; d < 3; ++d) {
+          c0[d] = R < INFINITY ? cell_coord((pc[d] - R - cgrid[d]) * cgrid[3 + d]) : 0;
+          c1[d] = R < INFINITY ? cell_coord((pc[d] + R - cgrid[d]) * cgrid[3 + d]) : CELL_G - 1;
+        }
+      }
+      const int nx = c1[0] - c0[0] + 1, ny = c1[1] - c0[1] + 1;
+      const int ncell = act ? nx * ny * (c1[2] - c0[2] + 1) : 0;
+      int ci = h, qi = 0, qe = 0;
+      while (true) {
+        while (qi == qe && ci < ncell) {          // next non-empty cell of this lane
+          const int cz = ci / (nx * ny), rem = ci - cz * nx * ny, cy = rem / nx, cx = rem - cy * nx;
+          const int cid = ((c0[2] + cz) * CELL_G + (c0[1] + cy)) * CELL_G + (c0[0] + cx);
+          qi = cstart[cid];
+          qe = cstart[cid + 1];
+          ci += LPA;
+        }
+        const bool has = qi < qe;
+        if (!__any(has)) break;
+        if (has) {
+          const int qn = clist[qi++];
+          const float4 cp = tp[qn];
+          const int j = __float_as_int(cp.w);
+          float dp[D];
+          dp[0] = me.x - cp.x;
+          dp[1] = me.y - cp.y;
+          dp[2] = me.z - cp.z;
+          const float d2 = sqsum<D>(dp);
+          const uint64_t key = knn_key(d2, (unsigned)j);
+          if (d2 <= bound && key < bk[K - 1]) topk_insert<K>(bk, key);
+          if (a.do_safety && !danger) {
+            const float4 cv = tv[qn];
+            const float lim = 1.01f * (base_i + a.ttc_check * cv.w) + 1e-4f;
+            if (d2 < lim * lim && j != i) {
+              float dv[D];
+              dv[0] = mv.x - cv.x;
+              dv[1] = mv.y - cv.y;
+              dv[2] = mv.z - cv.z;
+              danger = ttc_danger<D>(dp, dv, a.r2_check, a.ttc_check);
+            }
+          }
+        }
+      }
+    }
+  }
+  if (wave_live && !use_cells) {
     // gap^2 (x0.999) between this wave's box and a chunk / superchunk box
     auto gap2 = [&](const float4& cl, const float4& chh) {
       const float gx = fmaxf(0.f, fmaxf(cl.x - wmaxx, wminx - chh.x));
@@ -661,7 +795,7 @@ static void launch_kdb(const ScanArgs& a, hipStream_t st) {
     hipLaunchKernelGGL((scan_kernel<K, D, BS, LPA, 1>), grid, dim3(BS), lds, st, a);
     return;
   }
-  const size_t lds = scan_lds_bytes(a.Nn);
+  const size_t lds = scan_lds_bytes(a.Nn) + ((D == 3 && SCAN_CELL3 && BS >= CELL_G3) ? scan_cell_lds((a.Nn + SCH - 1) / SCH * SCH) : 0);
   if constexpr (K == 12) {
     if (a.stamps) {           // diagnostics: phase clocks (scripts/stamps_scan.py)
       (void)hipFuncSetAttribute((const void*)scan_kernel<K, D, BS, LPA, 0, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);

@@ -53,6 +53,36 @@ def test_scan_nd_obstacles(dim, nobs, N):
     assert torch.equal(safe, O.safe_agent_count(s, nodes).float())
 
 
+@pytest.mark.parametrize("nobs,lattice", [(8, False), (0, True)])
+def test_scan_3d_temporal_bound_large(nobs, lattice):
+    """Config #5 scale (1,024 agents, the big-block 3-D scan) with the previous step's kNN as the
+    temporal bound, step after step on moving states: lists, danger bits, counts and safety equal
+    the oracle (the path that searches the 3-D cell grid when SCAN_CELL3 is on, the chunk culling
+    otherwise). lattice: positions on a coarse grid, many equal distances (exact tie order)."""
+    B, N, K = 3, 1024, C.TOP_K
+    s, g, obs = _scene(B, N, 3, nobs, seed=11 + nobs)
+    if lattice:
+        s[..., :3] = torch.round(s[..., :3] * 2) / 2
+    prev = None
+    for step in range(3):
+        S = graph.node_records(s, obs)
+        idx = torch.empty(B, N, K, dtype=torch.int32, device=DEV)
+        dang = torch.empty(B, N, K, dtype=torch.uint8, device=DEV)
+        cnt = torch.zeros(B, 2, device=DEV)
+        safe = torch.zeros(B, device=DEV)
+        native.scan(S, idx, dang, cnt, safe, K=K, n_agents=N, prev_idx=prev)
+        torch.cuda.synchronize()
+        nodes = O.with_obstacles(s, obs)
+        ref = O.knn_idx(s, K, nodes)
+        assert torch.equal(idx.long(), ref), step
+        dref = O.ttc_mask_knn(s, ref, nodes)
+        assert torch.equal(dang.bool(), dref), step
+        assert torch.equal(cnt[:, 0], dref.sum((1, 2)).float()), step
+        assert torch.equal(safe, O.safe_agent_count(s, nodes).float()), step
+        prev = idx
+        s = (s + torch.cat([s[..., 3:], torch.zeros_like(s[..., 3:])], -1) * 0.1).contiguous()
+
+
 def test_scenario_sampler_3d_obstacles():
     s, g, obs = scenario.generate(3, 256, seed=4, device=DEV, dim=3, num_obstacles=5)
     assert s.shape == (3, 256, 6) and g.shape == (3, 256, 3) and obs.shape == (3, 60, 3)
