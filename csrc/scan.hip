@@ -247,19 +247,31 @@ __global__ __launch_bounds__(STAGE_BLOCK) void scan_stage_kernel(ScanArgs a) {
 #define SCAN_WAVE_ATOMIC3 1
 #endif
 
-// SCAN_CELL3 (A/B build knob): 3-D scenes with a temporal bound search a uniform 8^3 cell grid of
+// SCAN_CELL3 / SCAN_CELL2 (A/B build knobs): with a temporal bound, search a uniform cell grid of
 // the env around each agent instead of the wave-uniform chunk culling. The 2-D curve order leaves
-// every chunk a full-height column and every wave box as tall as the env, so a 3-D wave evaluates
-// ~2x the chunks of a 2-D one (stamps_scan.py: 30 vs 14); with cells each agent's four lanes visit
+// every 3-D chunk a full-height column and every 3-D wave box as tall as the env, so a 3-D wave
+// evaluates ~2x the chunks of a 2-D one (stamps_scan.py: 30 vs 14); and in either dimension a wave
+// evaluates a chunk when ANY of its 16 agents needs it. With cells, each agent's four lanes visit
 // only the cells within its own bound (the largest current distance of its previous K neighbours)
 // and safety reach. Same keys, same exact tests: the same lists, bits and counts.
 #ifndef SCAN_CELL3
 #define SCAN_CELL3 0
 #endif
-constexpr int CELL_G = 8, CELL_G3 = CELL_G * CELL_G * CELL_G;
-static inline size_t scan_cell_lds(int Np) { return (size_t)(2 * CELL_G3 + 1) * 4 + (size_t)Np * 2; }
+#ifndef SCAN_CELL2
+#define SCAN_CELL2 0
+#endif
+#ifndef SCAN_CELL_G3
+#define SCAN_CELL_G3 8        // 8^3 cells: ~2.2 graph nodes per cell at config #5
+#endif
+#ifndef SCAN_CELL_G2
+#define SCAN_CELL_G2 16       // 16^2 cells: 4 agents per cell at the headline
+#endif
+template <int D> constexpr int cell_g() { return D == 3 ? SCAN_CELL_G3 : SCAN_CELL_G2; }
+template <int D> constexpr int cell_n() { return D == 3 ? cell_g<3>() * cell_g<3>() * cell_g<3>() : cell_g<2>() * cell_g<2>(); }
+template <int D> constexpr bool cell_on() { return D == 3 ? SCAN_CELL3 != 0 : SCAN_CELL2 != 0; }
+template <int D> static inline size_t scan_cell_lds(int Np) { return (size_t)(2 * cell_n<D>() + 1) * 4 + (size_t)Np * 2; }
 // cell coordinate of a scaled position (monotone; NaN and values below 0 -> 0, above -> G-1)
-DEV int cell_coord(float x) { return x >= 1.f ? (x < (float)(CELL_G - 1) ? (int)x : CELL_G - 1) : 0; }
+template <int G> DEV int cell_coord(float x) { return x >= 1.f ? (x < (float)(G - 1) ? (int)x : G - 1) : 0; }
 
 // SCAN_THR_SKIP: the per-chunk threshold update (group min + wave max) only when some lane of the
 // wave inserted into its list in that chunk, the all-danger update only when some lane's danger
@@ -386,44 +398,49 @@ __global__ __launch_bounds__(BS) void scan_kernel(ScanArgs a) {
   }
   __syncthreads();
   }
-  // 3-D cell grid over the env's bounding box (SCAN_CELL3): counting sort of the staged curve
-  // positions by cell; the order inside a cell is irrelevant (the lists are exact for any order)
-  constexpr bool CELLS = D == 3 && SCAN_CELL3 && !GLB && BS >= CELL_G3;
+  // cell grid over the env's bounding box (SCAN_CELL2 / SCAN_CELL3): counting sort of the staged
+  // curve positions by cell; the order inside a cell is irrelevant (the lists are exact for any order)
+  constexpr int CG = cell_g<D>(), NCELL = cell_n<D>();
+  constexpr bool CELLS = cell_on<D>() && !GLB && BS >= NCELL;
   const bool use_cells = CELLS && a.prev_idx && a.do_knn;      // uniform per launch
-  __shared__ float cgrid[8];                                   // lo.xyz, 1 / cell size.xyz, max |v|
-  int* cstart = reinterpret_cast<int*>(pinv + Np);             // [G^3 + 1] cell starts
-  int* cfill = cstart + CELL_G3 + 1;                           // [G^3] fill counters
-  unsigned short* clist = reinterpret_cast<unsigned short*>(cfill + CELL_G3);   // [Np] curve positions
-  auto cell_of = [&](float x, float y, float z) {
-    return (cell_coord((z - cgrid[2]) * cgrid[5]) * CELL_G + cell_coord((y - cgrid[1]) * cgrid[4])) * CELL_G +
-           cell_coord((x - cgrid[0]) * cgrid[3]);
+  __shared__ float cgrid[8];                                   // lo.xyz, cells per unit.xyz, max |v|
+  int* cstart = reinterpret_cast<int*>(pinv + Np);             // [NCELL + 1] cell starts
+  int* cfill = cstart + NCELL + 1;                             // [NCELL] fill counters
+  unsigned short* clist = reinterpret_cast<unsigned short*>(cfill + NCELL);   // [Np] curve positions
+  auto cell_of = [&](const float4& t) {
+    const int cx = cell_coord<CG>((t.x - cgrid[0]) * cgrid[3]), cy = cell_coord<CG>((t.y - cgrid[1]) * cgrid[4]);
+    if constexpr (D == 3) return (cell_coord<CG>((t.z - cgrid[2]) * cgrid[5]) * CG + cy) * CG + cx;
+    return cy * CG + cx;
   };
   if constexpr (CELLS) {
     if (use_cells) {
-      if (threadIdx.x == 0) {
-        float lx = INFINITY, ly = INFINITY, lz = INFINITY, hx = -INFINITY, hy = -INFINITY, hz = -INFINITY, vm = 0.f;
-        for (int c = 0; c < nsc; ++c) {
-          const float4 l = sbl[c], u = sbh[c];
-          lx = fminf(lx, l.x); ly = fminf(ly, l.y); lz = fminf(lz, l.z); vm = fmaxf(vm, l.w);
-          hx = fmaxf(hx, u.x); hy = fmaxf(hy, u.y); hz = fmaxf(hz, u.z);
+      if (threadIdx.x < WAVE) {               // wave 0: bounding box and max speed of the env's nodes
+        const int l = threadIdx.x;
+        float4 lo = make_float4(INFINITY, INFINITY, INFINITY, 0.f), hi = make_float4(-INFINITY, -INFINITY, -INFINITY, 0.f);
+        for (int c = l; c < nsc; c += WAVE) {
+          const float4 u = sbl[c], w = sbh[c];
+          lo.x = fminf(lo.x, u.x); lo.y = fminf(lo.y, u.y); lo.z = fminf(lo.z, u.z); lo.w = fmaxf(lo.w, u.w);
+          hi.x = fmaxf(hi.x, w.x); hi.y = fmaxf(hi.y, w.y); hi.z = fmaxf(hi.z, w.z);
         }
-        const float g = (float)CELL_G;
-        cgrid[0] = lx; cgrid[1] = ly; cgrid[2] = lz;
-        cgrid[3] = g / fmaxf(hx - lx, 1e-6f); cgrid[4] = g / fmaxf(hy - ly, 1e-6f); cgrid[5] = g / fmaxf(hz - lz, 1e-6f);
-        cgrid[6] = vm;
+        lo.x = wave_min(lo.x); lo.y = wave_min(lo.y); lo.z = wave_min(lo.z); lo.w = wave_max(lo.w);
+        hi.x = wave_max(hi.x); hi.y = wave_max(hi.y); hi.z = wave_max(hi.z);
+        if (l == 0) {
+          const float g = (float)CG;
+          cgrid[0] = lo.x; cgrid[1] = lo.y; cgrid[2] = lo.z;
+          cgrid[3] = g / fmaxf(hi.x - lo.x, 1e-6f); cgrid[4] = g / fmaxf(hi.y - lo.y, 1e-6f);
+          cgrid[5] = g / fmaxf(hi.z - lo.z, 1e-6f);
+          cgrid[6] = lo.w;
+        }
       }
-      for (int c = threadIdx.x; c < CELL_G3; c += BS) { cstart[c] = 0; cfill[c] = 0; }
+      for (int c = threadIdx.x; c < NCELL; c += BS) cfill[c] = 0;
       __syncthreads();
-      for (int q = threadIdx.x; q < Nn; q += BS) {
-        const float4 t = tp[q];
-        atomicAdd(&cfill[cell_of(t.x, t.y, t.z)], 1);
-      }
+      for (int q = threadIdx.x; q < Nn; q += BS) atomicAdd(&cfill[cell_of(tp[q])], 1);
       __syncthreads();
-      // exclusive scan of the G^3 counts: wave scans, then the wave totals (one thread per cell)
-      __shared__ int wtot[CELL_G3 / WAVE];
+      // exclusive scan of the cell counts: wave scans, then the wave totals (one thread per cell)
+      __shared__ int wtot[NCELL / WAVE];
       const int tid = threadIdx.x, ln = tid & 63, wv = tid / WAVE;
       int v = 0, x = 0;
-      if (tid < CELL_G3) {
+      if (tid < NCELL) {
         v = cfill[tid];
         x = v;
 #pragma unroll
@@ -434,17 +451,16 @@ __global__ __launch_bounds__(BS) void scan_kernel(ScanArgs a) {
         if (ln == 63) wtot[wv] = x;
       }
       __syncthreads();
-      if (tid < CELL_G3) {
+      if (tid < NCELL) {
         int pre = 0;
         for (int w = 0; w < wv; ++w) pre += wtot[w];
         cstart[tid] = pre + x - v;
         cfill[tid] = 0;
-        if (tid == CELL_G3 - 1) cstart[CELL_G3] = pre + x;
+        if (tid == NCELL - 1) cstart[NCELL] = pre + x;
       }
       __syncthreads();
       for (int q = threadIdx.x; q < Nn; q += BS) {
-        const float4 t = tp[q];
-        const int c = cell_of(t.x, t.y, t.z);
+        const int c = cell_of(tp[q]);
         clist[cstart[c] + atomicAdd(&cfill[c], 1)] = (unsigned short)q;
       }
       __syncthreads();
@@ -522,26 +538,32 @@ __global__ __launch_bounds__(BS) void scan_kernel(ScanArgs a) {
       const float Rk = sqrtf(fmaxf(bound, 0.f)) * 1.001f + 1e-5f;
       const float Rs = a.do_safety ? (1.01f * (base_i + a.ttc_check * cgrid[6]) + 1e-4f) * 1.001f + 1e-5f : 0.f;
       float R = fmaxf(Rk, Rs);
-      if (!(R < INFINITY) || !(me.x == me.x && me.y == me.y && me.z == me.z)) R = INFINITY;   // whole grid
-      int c0[3], c1[3];
-      {
+      bool fin = R < INFINITY && me.x == me.x && me.y == me.y;
+      if constexpr (D == 3) fin = fin && me.z == me.z;
+      int c0[3] = {0, 0, 0}, c1[3] = {CG - 1, CG - 1, D == 3 ? CG - 1 : 0};
+      if (fin) {
         const float pc[3] = {me.x, me.y, me.z};
 #pragma unroll
-        for (int d = 0; d < 3; ++d) {
-          c0[d] = R < INFINITY ? cell_coord((pc[d] - R - cgrid[d]) * cgrid[3 + d]) : 0;
-          c1[d] = R < INFINITY ? cell_coord((pc[d] + R - cgrid[d]) * cgrid[3 + d]) : CELL_G - 1;
+        for (int d = 0; d < D; ++d) {
+          c0[d] = cell_coord<CG>((pc[d] - R - cgrid[d]) * cgrid[3 + d]);
+          c1[d] = cell_coord<CG>((pc[d] + R - cgrid[d]) * cgrid[3 + d]);
         }
       }
-      const int nx = c1[0] - c0[0] + 1, ny = c1[1] - c0[1] + 1;
-      const int ncell = act ? nx * ny * (c1[2] - c0[2] + 1) : 0;
-      int ci = h, qi = 0, qe = 0;
+      const int nx = c1[0] - c0[0] + 1, ny = c1[1] - c0[1] + 1, nz = c1[2] - c0[2] + 1;
+      const int ncell = act ? nx * ny * nz : 0;
+      // this lane's cells ci = h, h + LPA, ... in (x, y, z) order, decoded incrementally
+      int ci = h, cx = h, cy = 0, cz = 0;
+      while (cx >= nx && ny > 0) { cx -= nx; if (++cy == ny) { cy = 0; ++cz; } }
+      int qi = 0, qe = 0;
       while (true) {
         while (qi == qe && ci < ncell) {          // next non-empty cell of this lane
-          const int cz = ci / (nx * ny), rem = ci - cz * nx * ny, cy = rem / nx, cx = rem - cy * nx;
-          const int cid = ((c0[2] + cz) * CELL_G + (c0[1] + cy)) * CELL_G + (c0[0] + cx);
+          int cid = (c0[1] + cy) * CG + (c0[0] + cx);
+          if constexpr (D == 3) cid += (c0[2] + cz) * CG * CG;
           qi = cstart[cid];
           qe = cstart[cid + 1];
           ci += LPA;
+          cx += LPA;
+          while (cx >= nx) { cx -= nx; if (++cy == ny) { cy = 0; ++cz; } }
         }
         const bool has = qi < qe;
         if (!__any(has)) break;
@@ -552,7 +574,7 @@ __global__ __launch_bounds__(BS) void scan_kernel(ScanArgs a) {
           float dp[D];
           dp[0] = me.x - cp.x;
           dp[1] = me.y - cp.y;
-          dp[2] = me.z - cp.z;
+          if constexpr (D == 3) dp[2] = me.z - cp.z;
           const float d2 = sqsum<D>(dp);
           const uint64_t key = knn_key(d2, (unsigned)j);
           if (d2 <= bound && key < bk[K - 1]) topk_insert<K>(bk, key);
@@ -563,7 +585,7 @@ __global__ __launch_bounds__(BS) void scan_kernel(ScanArgs a) {
               float dv[D];
               dv[0] = mv.x - cv.x;
               dv[1] = mv.y - cv.y;
-              dv[2] = mv.z - cv.z;
+              if constexpr (D == 3) dv[2] = mv.z - cv.z;
               danger = ttc_danger<D>(dp, dv, a.r2_check, a.ttc_check);
             }
           }
@@ -795,7 +817,7 @@ static void launch_kdb(const ScanArgs& a, hipStream_t st) {
     hipLaunchKernelGGL((scan_kernel<K, D, BS, LPA, 1>), grid, dim3(BS), lds, st, a);
     return;
   }
-  const size_t lds = scan_lds_bytes(a.Nn) + ((D == 3 && SCAN_CELL3 && BS >= CELL_G3) ? scan_cell_lds((a.Nn + SCH - 1) / SCH * SCH) : 0);
+  const size_t lds = scan_lds_bytes(a.Nn) + ((cell_on<D>() && BS >= cell_n<D>()) ? scan_cell_lds<D>((a.Nn + SCH - 1) / SCH * SCH) : 0);
   if constexpr (K == 12) {
     if (a.stamps) {           // diagnostics: phase clocks (scripts/stamps_scan.py)
       (void)hipFuncSetAttribute((const void*)scan_kernel<K, D, BS, LPA, 0, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
