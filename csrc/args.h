@@ -42,6 +42,7 @@ struct ScanArgs {
   float4* ws; long ws_env;           // Nn > 4096: per-env global staging (float4s per env), else null
   int lanes;                         // lanes per agent: 0 = by grid size (scan.hip scan_lpa8), 4 or 8
   unsigned long long* stamps;        // diagnostics: phase clocks [block][wave][16] (K = 12 LDS path; null = off)
+  int cells;                         // set by the launcher: the cell-grid LDS was allocated (scan.hip SCAN_CELL*)
 };
 
 struct ScenArgs {

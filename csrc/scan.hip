@@ -402,7 +402,7 @@ __global__ __launch_bounds__(BS) void scan_kernel(ScanArgs a) {
   // curve positions by cell; the order inside a cell is irrelevant (the lists are exact for any order)
   constexpr int CG = cell_g<D>(), NCELL = cell_n<D>();
   constexpr bool CELLS = cell_on<D>() && !GLB && BS >= NCELL;
-  const bool use_cells = CELLS && a.prev_idx && a.do_knn;      // uniform per launch
+  const bool use_cells = CELLS && a.cells && a.prev_idx && a.do_knn;      // uniform per launch
   __shared__ float cgrid[8];                                   // lo.xyz, cells per unit.xyz, max |v|
   int* cstart = reinterpret_cast<int*>(pinv + Np);             // [NCELL + 1] cell starts
   int* cfill = cstart + NCELL + 1;                             // [NCELL] fill counters
@@ -817,16 +817,26 @@ static void launch_kdb(const ScanArgs& a, hipStream_t st) {
     hipLaunchKernelGGL((scan_kernel<K, D, BS, LPA, 1>), grid, dim3(BS), lds, st, a);
     return;
   }
-  const size_t lds = scan_lds_bytes(a.Nn) + ((cell_on<D>() && BS >= cell_n<D>()) ? scan_cell_lds<D>((a.Nn + SCH - 1) / SCH * SCH) : 0);
+  // the cell grid's LDS (SCAN_CELL*) only when the env still fits the 160 KB with it
+  ScanArgs b = a;
+  size_t lds = scan_lds_bytes(a.Nn);
+  b.cells = 0;
+  if constexpr (cell_on<D>() && BS >= cell_n<D>()) {
+    const size_t lc = scan_cell_lds<D>((a.Nn + SCH - 1) / SCH * SCH);
+    if (lds + lc + 1024 <= 160 * 1024) {
+      lds += lc;
+      b.cells = 1;
+    }
+  }
   if constexpr (K == 12) {
     if (a.stamps) {           // diagnostics: phase clocks (scripts/stamps_scan.py)
       (void)hipFuncSetAttribute((const void*)scan_kernel<K, D, BS, LPA, 0, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-      hipLaunchKernelGGL((scan_kernel<K, D, BS, LPA, 0, true>), grid, dim3(BS), lds, st, a);
+      hipLaunchKernelGGL((scan_kernel<K, D, BS, LPA, 0, true>), grid, dim3(BS), lds, st, b);
       return;
     }
   }
   (void)hipFuncSetAttribute((const void*)scan_kernel<K, D, BS, LPA, 0>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL((scan_kernel<K, D, BS, LPA, 0>), grid, dim3(BS), lds, st, a);
+  hipLaunchKernelGGL((scan_kernel<K, D, BS, LPA, 0>), grid, dim3(BS), lds, st, b);
 }
 
 
