@@ -257,8 +257,10 @@ __global__ __launch_bounds__(STAGE_BLOCK) void scan_stage_kernel(ScanArgs a) {
 #ifndef SCAN_CELL3
 #define SCAN_CELL3 0
 #endif
+// 2-D: on (round 5: scan 47.1 -> 33.8 us per call, candidate loop 50 -> 25 k cycles per wave,
+// headline fp32 10.52-10.53 -> 10.26-10.27 ms, bf16 6.65 -> 6.39, interleaved, profiles/r5_b25/)
 #ifndef SCAN_CELL2
-#define SCAN_CELL2 0
+#define SCAN_CELL2 1
 #endif
 #ifndef SCAN_CELL_G3
 #define SCAN_CELL_G3 8        // 8^3 cells: ~2.2 graph nodes per cell at config #5
