@@ -254,8 +254,10 @@ __global__ __launch_bounds__(STAGE_BLOCK) void scan_stage_kernel(ScanArgs a) {
 // evaluates a chunk when ANY of its 16 agents needs it. With cells, each agent's four lanes visit
 // only the cells within its own bound (the largest current distance of its previous K neighbours)
 // and safety reach. Same keys, same exact tests: the same lists, bits and counts.
+// 3-D: on (round 5: config #5 scan 93.6 -> 89.3 us per call, fp16 8.56-8.58 -> 8.52-8.53 ms,
+// interleaved, profiles/r5_b27/)
 #ifndef SCAN_CELL3
-#define SCAN_CELL3 0
+#define SCAN_CELL3 1
 #endif
 // 2-D: on (round 5: scan 47.1 -> 33.8 us per call, candidate loop 50 -> 25 k cycles per wave,
 // headline fp32 10.52-10.53 -> 10.26-10.27 ms, bf16 6.65 -> 6.39, interleaved, profiles/r5_b25/)
@@ -271,7 +273,11 @@ __global__ __launch_bounds__(STAGE_BLOCK) void scan_stage_kernel(ScanArgs a) {
 template <int D> constexpr int cell_g() { return D == 3 ? SCAN_CELL_G3 : SCAN_CELL_G2; }
 template <int D> constexpr int cell_n() { return D == 3 ? cell_g<3>() * cell_g<3>() * cell_g<3>() : cell_g<2>() * cell_g<2>(); }
 template <int D> constexpr bool cell_on() { return D == 3 ? SCAN_CELL3 != 0 : SCAN_CELL2 != 0; }
-template <int D> static inline size_t scan_cell_lds(int Np) { return (size_t)(2 * cell_n<D>() + 1) * 4 + (size_t)Np * 2; }
+// cell arrays: [NCELL + 1] starts | [NCELL] fill counters | [Np] curve positions (u16) | [Np]
+// node records (x, y, z, id) in cell order (16-byte aligned: one LDS read per candidate)
+template <int D> static inline size_t scan_cell_lds(int Np) {
+  return ((size_t)(2 * cell_n<D>() + 1) * 4 + (size_t)Np * 2 + 15) / 16 * 16 + (size_t)Np * 16 + 16;
+}
 // cell coordinate of a scaled position (monotone; NaN and values below 0 -> 0, above -> G-1)
 template <int G> DEV int cell_coord(float x) { return x >= 1.f ? (x < (float)(G - 1) ? (int)x : G - 1) : 0; }
 
@@ -337,6 +343,13 @@ __global__ __launch_bounds__(BS) void scan_kernel(ScanArgs a) {
   unsigned short* pinv = reinterpret_cast<unsigned short*>(sbh + nsc);
   const float4* Sb = a.S + (long)b * a.s_env * REC<D>;
   const int* perm = a.perm + (long)b * Nn;
+  constexpr int CG = cell_g<D>(), NCELL = cell_n<D>();
+  constexpr bool CELLS = cell_on<D>() && !GLB && BS >= NCELL;
+  const bool use_cells = CELLS && a.cells && a.prev_idx && a.do_knn;      // uniform per launch
+  __shared__ float cgrid[8];                                   // lo.xyz, cells per unit.xyz, max |v|
+  __shared__ float wbox[BS / WAVE][8];                         // per-wave bounding boxes (cell path)
+  // this thread's running bounding box of its staged nodes (cell path: replaces the chunk boxes)
+  float bx0 = INFINITY, by0 = INFINITY, bz0 = INFINITY, bx1 = -INFINITY, by1 = -INFINITY, bz1 = -INFINITY, bvm = 0.f;
   if constexpr (GLB == 2) {
   } else if constexpr (GLB == 1) {
     const float4* gb = tv + Np;
@@ -358,18 +371,35 @@ __global__ __launch_bounds__(BS) void scan_kernel(ScanArgs a) {
       if (q < Nn) {
         const float z = (D == 3) ? p[u][D - 1] : 0.f;
         const float vz = (D == 3) ? v[u][D - 1] : 0.f;
+        const float vm = sqrtf(sqsum<D>(v[u]));
         tp[q] = make_float4(p[u][0], p[u][1], z, __int_as_float(ids[u]));
-        tv[q] = make_float4(v[u][0], v[u][1], vz, sqrtf(sqsum<D>(v[u])));
+        tv[q] = make_float4(v[u][0], v[u][1], vz, vm);
         pinv[ids[u]] = (unsigned short)q;
+        if constexpr (CELLS) {
+          bx0 = fminf(bx0, p[u][0]); by0 = fminf(by0, p[u][1]); bz0 = fminf(bz0, z);
+          bx1 = fmaxf(bx1, p[u][0]); by1 = fmaxf(by1, p[u][1]); bz1 = fmaxf(bz1, z);
+          bvm = fmaxf(bvm, vm);
+        }
       } else {
         tp[q] = make_float4(INFINITY, INFINITY, INFINITY, __int_as_float(-1));   // key == KEY_EMPTY
         tv[q] = make_float4(0.f, 0.f, 0.f, 0.f);
       }
     }
   }
+  if constexpr (CELLS) {
+    if (use_cells) {                          // every wave: its box to wbox (all lanes take part)
+      bx0 = wave_min(bx0); by0 = wave_min(by0); bz0 = wave_min(bz0);
+      bx1 = wave_max(bx1); by1 = wave_max(by1); bz1 = wave_max(bz1); bvm = wave_max(bvm);
+      if ((threadIdx.x & (WAVE - 1)) == 0) {
+        float* w = wbox[threadIdx.x / WAVE];
+        w[0] = bx0; w[1] = by0; w[2] = bz0; w[3] = bx1; w[4] = by1; w[5] = bz1; w[6] = bvm;
+      }
+    }
+  }
   __syncthreads();
   stamp(0);
   if constexpr (!GLB) {
+  if (!use_cells) {                           // the chunk culling's boxes (the cell path needs none)
   for (int c = threadIdx.x; c < nch; c += BS) {
     float4 lo = make_float4(INFINITY, INFINITY, INFINITY, 0.f);
     float4 hi = make_float4(-INFINITY, -INFINITY, -INFINITY, 0.f);
@@ -400,15 +430,13 @@ __global__ __launch_bounds__(BS) void scan_kernel(ScanArgs a) {
   }
   __syncthreads();
   }
+  }
   // cell grid over the env's bounding box (SCAN_CELL2 / SCAN_CELL3): counting sort of the staged
   // curve positions by cell; the order inside a cell is irrelevant (the lists are exact for any order)
-  constexpr int CG = cell_g<D>(), NCELL = cell_n<D>();
-  constexpr bool CELLS = cell_on<D>() && !GLB && BS >= NCELL;
-  const bool use_cells = CELLS && a.cells && a.prev_idx && a.do_knn;      // uniform per launch
-  __shared__ float cgrid[8];                                   // lo.xyz, cells per unit.xyz, max |v|
   int* cstart = reinterpret_cast<int*>(pinv + Np);             // [NCELL + 1] cell starts
   int* cfill = cstart + NCELL + 1;                             // [NCELL] fill counters
   unsigned short* clist = reinterpret_cast<unsigned short*>(cfill + NCELL);   // [Np] curve positions
+  float4* ctp = reinterpret_cast<float4*>((reinterpret_cast<uintptr_t>(clist + Np) + 15) & ~(uintptr_t)15);   // [Np]
   auto cell_of = [&](const float4& t) {
     const int cx = cell_coord<CG>((t.x - cgrid[0]) * cgrid[3]), cy = cell_coord<CG>((t.y - cgrid[1]) * cgrid[4]);
     if constexpr (D == 3) return (cell_coord<CG>((t.z - cgrid[2]) * cgrid[5]) * CG + cy) * CG + cx;
@@ -419,10 +447,10 @@ __global__ __launch_bounds__(BS) void scan_kernel(ScanArgs a) {
       if (threadIdx.x < WAVE) {               // wave 0: bounding box and max speed of the env's nodes
         const int l = threadIdx.x;
         float4 lo = make_float4(INFINITY, INFINITY, INFINITY, 0.f), hi = make_float4(-INFINITY, -INFINITY, -INFINITY, 0.f);
-        for (int c = l; c < nsc; c += WAVE) {
-          const float4 u = sbl[c], w = sbh[c];
-          lo.x = fminf(lo.x, u.x); lo.y = fminf(lo.y, u.y); lo.z = fminf(lo.z, u.z); lo.w = fmaxf(lo.w, u.w);
-          hi.x = fmaxf(hi.x, w.x); hi.y = fmaxf(hi.y, w.y); hi.z = fmaxf(hi.z, w.z);
+        if (l < BS / WAVE) {
+          const float* w = wbox[l];
+          lo = make_float4(w[0], w[1], w[2], w[6]);
+          hi = make_float4(w[3], w[4], w[5], 0.f);
         }
         lo.x = wave_min(lo.x); lo.y = wave_min(lo.y); lo.z = wave_min(lo.z); lo.w = wave_max(lo.w);
         hi.x = wave_max(hi.x); hi.y = wave_max(hi.y); hi.z = wave_max(hi.z);
@@ -462,8 +490,11 @@ __global__ __launch_bounds__(BS) void scan_kernel(ScanArgs a) {
       }
       __syncthreads();
       for (int q = threadIdx.x; q < Nn; q += BS) {
-        const int c = cell_of(tp[q]);
-        clist[cstart[c] + atomicAdd(&cfill[c], 1)] = (unsigned short)q;
+        const float4 t = tp[q];
+        const int c = cell_of(t);
+        const int dst = cstart[c] + atomicAdd(&cfill[c], 1);
+        clist[dst] = (unsigned short)q;
+        ctp[dst] = t;
       }
       __syncthreads();
     }
@@ -570,8 +601,9 @@ __global__ __launch_bounds__(BS) void scan_kernel(ScanArgs a) {
         const bool has = qi < qe;
         if (!__any(has)) break;
         if (has) {
-          const int qn = clist[qi++];
-          const float4 cp = tp[qn];
+          const int qn = clist[qi];               // (for the velocity record, read only when needed)
+          const float4 cp = ctp[qi];
+          ++qi;
           const int j = __float_as_int(cp.w);
           float dp[D];
           dp[0] = me.x - cp.x;

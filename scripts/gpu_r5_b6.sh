@@ -7,7 +7,7 @@ cd $GRAFT_REPO_ROOT
 O=gpurun_out/${TAG:-r5b6}
 mkdir -p $O
 ms() { grep '^{' $1 | python -c 'import json,sys; print(round(json.loads(sys.stdin.read())["ms_per_step"],3))'; }
-MACBF_EXT=alt_so/nostore/_C.so timeout -k 10 200 python scripts/stamps_node.py --node16 --envs 64 > $O/stamps_node16_nostore.log 2>&1 && tail -14 $O/stamps_node16_nostore.log || { echo STOP stamps; exit 1; }
+MACBF_SELFCHECK=0 MACBF_EXT=alt_so/nostore/_C.so timeout -k 10 200 python scripts/stamps_node.py --node16 --envs 64 > $O/stamps_node16_nostore.log 2>&1 && tail -14 $O/stamps_node16_nostore.log || { echo STOP stamps; exit 1; }
 MACBF_EXT=$GRAFT_REPO_ROOT/alt_so/nofence/_C.so TAG=${TAG:-r5b6}/nofence STEPS=6 bash scripts/gpu_prof.sh > $O/nofence_summary.txt 2>&1 || { echo STOP prof; tail -3 $O/nofence_summary.txt; exit 1; }
 MACBF_EXT=alt_so/lpa3/_C.so timeout -k 10 300 python -u -m pytest tests/test_gpu_nd.py tests/test_gpu_forward.py -q -p no:cacheprovider --timeout 120 --timeout-method thread > $O/lpa3_tests.log 2>&1
 rc=$?; tail -2 $O/lpa3_tests.log; if [ $rc -ne 0 ]; then echo "STOP lpa3 tests"; exit $rc; fi
