@@ -345,7 +345,8 @@ __global__ __launch_bounds__(BS) void scan_kernel(ScanArgs a) {
   const int* perm = a.perm + (long)b * Nn;
   constexpr int CG = cell_g<D>(), NCELL = cell_n<D>();
   constexpr bool CELLS = cell_on<D>() && !GLB && BS >= NCELL;
-  const bool use_cells = CELLS && a.cells && a.prev_idx && a.do_knn;      // uniform per launch
+  constexpr int MQ = (4096 + BS - 1) / BS;                     // cell path: staged nodes per thread
+  const bool use_cells = CELLS && a.cells && a.prev_idx && a.do_knn && Nn <= MQ * BS;   // uniform per launch
   __shared__ float cgrid[8];                                   // lo.xyz, cells per unit.xyz, max |v|
   __shared__ float wbox[BS / WAVE][8];                         // per-wave bounding boxes (cell path)
   // this thread's running bounding box of its staged nodes (cell path: replaces the chunk boxes)
@@ -464,7 +465,16 @@ __global__ __launch_bounds__(BS) void scan_kernel(ScanArgs a) {
       }
       for (int c = threadIdx.x; c < NCELL; c += BS) cfill[c] = 0;
       __syncthreads();
-      for (int q = threadIdx.x; q < Nn; q += BS) atomicAdd(&cfill[cell_of(tp[q])], 1);
+      // each node's cell and rank inside it (the atomic's return), kept for the scatter
+      int crk[MQ];
+#pragma unroll
+      for (int u = 0; u < MQ; ++u) {
+        const int q = threadIdx.x + u * BS;
+        if (q < Nn) {
+          const int c = cell_of(tp[q]);
+          crk[u] = (c << 16) | atomicAdd(&cfill[c], 1);
+        }
+      }
       __syncthreads();
       // exclusive scan of the cell counts: wave scans, then the wave totals (one thread per cell)
       __shared__ int wtot[NCELL / WAVE];
@@ -485,16 +495,17 @@ __global__ __launch_bounds__(BS) void scan_kernel(ScanArgs a) {
         int pre = 0;
         for (int w = 0; w < wv; ++w) pre += wtot[w];
         cstart[tid] = pre + x - v;
-        cfill[tid] = 0;
         if (tid == NCELL - 1) cstart[NCELL] = pre + x;
       }
       __syncthreads();
-      for (int q = threadIdx.x; q < Nn; q += BS) {
-        const float4 t = tp[q];
-        const int c = cell_of(t);
-        const int dst = cstart[c] + atomicAdd(&cfill[c], 1);
-        clist[dst] = (unsigned short)q;
-        ctp[dst] = t;
+#pragma unroll
+      for (int u = 0; u < MQ; ++u) {
+        const int q = threadIdx.x + u * BS;
+        if (q < Nn) {
+          const int dst = cstart[crk[u] >> 16] + (crk[u] & 0xffff);
+          clist[dst] = (unsigned short)q;
+          ctp[dst] = tp[q];
+        }
       }
       __syncthreads();
     }
@@ -582,28 +593,71 @@ __global__ __launch_bounds__(BS) void scan_kernel(ScanArgs a) {
           c1[d] = cell_coord<CG>((pc[d] + R - cgrid[d]) * cgrid[3 + d]);
         }
       }
-      const int nx = c1[0] - c0[0] + 1, ny = c1[1] - c0[1] + 1, nz = c1[2] - c0[2] + 1;
-      const int ncell = act ? nx * ny * nz : 0;
-      // this lane's cells ci = h, h + LPA, ... in (x, y, z) order, decoded incrementally
-      int ci = h, cx = h, cy = 0, cz = 0;
-      while (cx >= nx && ny > 0) { cx -= nx; if (++cy == ny) { cy = 0; ++cz; } }
-      int qi = 0, qe = 0;
+      const int ny = c1[1] - c0[1] + 1, nz = c1[2] - c0[2] + 1;
+      const int nrow = act ? ny * nz : 0;
+      // the box's cells in rows along x: a row's cells are consecutive cell ids, so its nodes are
+      // one contiguous range of the cell-ordered arrays. Each row is trimmed to the x extent the
+      // sphere of radius R leaves at the row's (y, z) distance (a disc / ball instead of the box),
+      // and rows beyond R are skipped; the agent's LPA lanes take every LPA-th candidate of the
+      // concatenated ranges (balanced lanes, one range read per row instead of one per cell)
+      float uc[3] = {0.f, 0.f, 0.f}, csz[3] = {0.f, 0.f, 0.f};
+      const float R2 = fin ? R * R : INFINITY;
+      {
+        const float pc[3] = {me.x, me.y, me.z};
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+          uc[d] = (pc[d] - cgrid[d]) * cgrid[3 + d];
+          csz[d] = 1.f / cgrid[3 + d];
+        }
+      }
+      // distance from the agent to cell row / layer c along axis d (the edge cells are open:
+      // cell_coord clamps), less a 1e-4-cell slack for the rounding of the cell mapping
+      auto gap = [&](int c, int d) {
+        const float lo = c == 0 ? -INFINITY : (float)c, hi = c == CG - 1 ? INFINITY : (float)(c + 1);
+        return fmaxf(0.f, fmaxf(lo - uc[d], uc[d] - hi) - 1e-4f) * csz[d];
+      };
+      if constexpr (ST) {                     // counters: 12 = rows in the wave's agents' boxes
+        int sc = h == 0 ? nrow : 0;
+#pragma unroll
+        for (int o = 1; o < WAVE; o <<= 1) sc += __shfl_xor(sc, o);
+        ph[12] = sc;
+      }
+      int ry = 0, rz = 0, off = 0, qi = 0, qe = 0;  // next row; candidates before it, mod LPA
       while (true) {
-        while (qi == qe && ci < ncell) {          // next non-empty cell of this lane
-          int cid = (c0[1] + cy) * CG + (c0[0] + cx);
-          if constexpr (D == 3) cid += (c0[2] + cz) * CG * CG;
-          qi = cstart[cid];
-          qe = cstart[cid + 1];
-          ci += LPA;
-          cx += LPA;
-          while (cx >= nx) { cx -= nx; if (++cy == ny) { cy = 0; ++cz; } }
+        while (qi >= qe && rz < nz && nrow > 0) {    // this lane's next candidate in a later row
+          const int cy = c0[1] + ry, cz = c0[2] + rz;
+          if (++ry == ny) { ry = 0; ++rz; }
+          float g2 = 0.f;
+          {
+            const float gy = gap(cy, 1);
+            g2 = gy * gy;
+          }
+          if constexpr (D == 3) {
+            const float gz = gap(cz, 2);
+            g2 += gz * gz;
+          }
+          if (g2 > R2) continue;
+          int x0 = c0[0], x1 = c1[0];
+          if (fin) {
+            // +1e-6 R^2: the cancellation in R^2 - g2 (R already carries the rounding margins)
+            const float rx = sqrtf(fmaxf(R2 - g2, 0.f) + 1e-6f * R2);
+            x0 = cell_coord<CG>((me.x - rx - cgrid[0]) * cgrid[3]);
+            x1 = cell_coord<CG>((me.x + rx - cgrid[0]) * cgrid[3]);
+          }
+          int rb = cy * CG;
+          if constexpr (D == 3) rb += cz * CG * CG;
+          const int s0 = cstart[rb + x0], e0 = cstart[rb + x1 + 1];
+          qi = s0 + ((h - off) & (LPA - 1));
+          qe = e0;
+          off = (off + e0 - s0) & (LPA - 1);
         }
         const bool has = qi < qe;
         if (!__any(has)) break;
+        if constexpr (ST) { ph[9] += 1; ph[10] += __popcll(__ballot(has)); }   // steps, candidates
         if (has) {
           const int qn = clist[qi];               // (for the velocity record, read only when needed)
           const float4 cp = ctp[qi];
-          ++qi;
+          qi += LPA;
           const int j = __float_as_int(cp.w);
           float dp[D];
           dp[0] = me.x - cp.x;

@@ -16,8 +16,10 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 PHASES = {0: "env staging", 1: "culling boxes", 2: "setup + bound", 3: "candidate loop", 4: "list merge",
           5: "output slots", 6: "counts"}
-COUNTS = {8: "superchunks visited", 9: "chunks tested", 10: "chunks evaluated", 11: "chunks w/ insertion",
-          12: "evaluated for kNN", 13: "evaluated, safety only"}
+# chunk path | cell path (steps of the wave's candidate loop, candidates over its lanes, cell rows in
+# its agents' search boxes)
+COUNTS = {8: "superchunks visited", 9: "chunks tested|cell steps", 10: "chunks eval.|candidates",
+          11: "chunks w/ insertion", 12: "eval. for kNN|rows", 13: "evaluated, safety only"}
 
 
 def main():
