@@ -275,8 +275,17 @@ template <int D> constexpr int cell_n() { return D == 3 ? cell_g<3>() * cell_g<3
 template <int D> constexpr bool cell_on() { return D == 3 ? SCAN_CELL3 != 0 : SCAN_CELL2 != 0; }
 // cell arrays: [NCELL + 1] starts | [NCELL] fill counters | [Np] curve positions (u16) | [Np]
 // node records (x, y, z, id) in cell order (16-byte aligned: one LDS read per candidate)
-template <int D> static inline size_t scan_cell_lds(int Np) {
-  return ((size_t)(2 * cell_n<D>() + 1) * 4 + (size_t)Np * 2 + 15) / 16 * 16 + (size_t)Np * 16 + 16;
+// SCAN_CELL_VZ: cell records carry the node's speed (2-D: in the unused z slot; 3-D: rounded up to
+// bf16 beside a 16-bit node id), so the safety pre-test of a candidate needs no second (dependent)
+// LDS read
+#ifndef SCAN_CELL_VZ
+#define SCAN_CELL_VZ 1
+#endif
+// rows of an agent's search box per row-table batch (SCAN_ROWTAB; 2-D boxes have at most CG2)
+constexpr int SCAN_RT = 16;
+template <int D> static inline size_t scan_cell_lds(int Np, int nag) {
+  return ((size_t)(2 * cell_n<D>() + 1) * 4 + (size_t)Np * 2 + 15) / 16 * 16 + (size_t)Np * 16 + 16 +
+         (size_t)nag * SCAN_RT * 4;
 }
 // cell coordinate of a scaled position (monotone; NaN and values below 0 -> 0, above -> G-1)
 template <int G> DEV int cell_coord(float x) { return x >= 1.f ? (x < (float)(G - 1) ? (int)x : G - 1) : 0; }
@@ -438,6 +447,7 @@ __global__ __launch_bounds__(BS) void scan_kernel(ScanArgs a) {
   int* cfill = cstart + NCELL + 1;                             // [NCELL] fill counters
   unsigned short* clist = reinterpret_cast<unsigned short*>(cfill + NCELL);   // [Np] curve positions
   float4* ctp = reinterpret_cast<float4*>((reinterpret_cast<uintptr_t>(clist + Np) + 15) & ~(uintptr_t)15);   // [Np]
+  unsigned* rtab = reinterpret_cast<unsigned*>(ctp + Np);      // [SCAN_AG][SCAN_RT] row ranges (s | e << 16)
   auto cell_of = [&](const float4& t) {
     const int cx = cell_coord<CG>((t.x - cgrid[0]) * cgrid[3]), cy = cell_coord<CG>((t.y - cgrid[1]) * cgrid[4]);
     if constexpr (D == 3) return (cell_coord<CG>((t.z - cgrid[2]) * cgrid[5]) * CG + cy) * CG + cx;
@@ -504,7 +514,12 @@ __global__ __launch_bounds__(BS) void scan_kernel(ScanArgs a) {
         if (q < Nn) {
           const int dst = cstart[crk[u] >> 16] + (crk[u] & 0xffff);
           clist[dst] = (unsigned short)q;
-          ctp[dst] = tp[q];
+          float4 t = tp[q];
+          if constexpr (D == 2 && SCAN_CELL_VZ) t.z = tv[q].w;     // 2-D: the speed in the unused z
+          if constexpr (D == 3 && SCAN_CELL_VZ)   // 3-D: id (16 bits) | speed rounded up to bf16
+            t.w = __uint_as_float((unsigned)(__float_as_int(t.w) & 0xffff) |
+                                  ((__float_as_uint(tv[q].w) + 0xffffu) & 0xffff0000u));
+          ctp[dst] = t;
         }
       }
       __syncthreads();
@@ -622,43 +637,64 @@ __global__ __launch_bounds__(BS) void scan_kernel(ScanArgs a) {
         for (int o = 1; o < WAVE; o <<= 1) sc += __shfl_xor(sc, o);
         ph[12] = sc;
       }
-      int ry = 0, rz = 0, off = 0, qi = 0, qe = 0;  // next row; candidates before it, mod LPA
-      while (true) {
-        while (qi >= qe && rz < nz && nrow > 0) {    // this lane's next candidate in a later row
-          const int cy = c0[1] + ry, cz = c0[2] + rz;
-          if (++ry == ny) { ry = 0; ++rz; }
-          float g2 = 0.f;
+      // row table: the agent's LPA lanes compute the ranges of SCAN_RT rows at a time (lane h rows
+      // h, h + LPA, ...; a skipped row is an empty range) into the agent's LDS slots, then every
+      // lane walks them in order -- the row work leaves the divergent candidate loop
+      unsigned* rt = rtab + (wave * APW + r) * SCAN_RT;
+      int off = 0;                                 // candidates of the rows before, mod LPA
+      for (int r0 = 0; __any(r0 < nrow); r0 += SCAN_RT) {
+#pragma unroll
+        for (int k = h; k < SCAN_RT; k += LPA) {
+          const int rr = r0 + k;
+          if (rr >= nrow) break;
+          unsigned pk = 0;
           {
-            const float gy = gap(cy, 1);
-            g2 = gy * gy;
+            const int rz = D == 3 ? rr / ny : 0;
+            const int cy = c0[1] + rr - rz * ny, cz = c0[2] + rz;
+            float g2 = 0.f;
+            {
+              const float gy = gap(cy, 1);
+              g2 = gy * gy;
+            }
+            if constexpr (D == 3) {
+              const float gz = gap(cz, 2);
+              g2 += gz * gz;
+            }
+            if (!(g2 > R2)) {
+              int x0 = c0[0], x1 = c1[0];
+              if (fin) {
+                // +1e-6 R^2: the cancellation in R^2 - g2 (R already carries the rounding margins)
+                const float rx = sqrtf(fmaxf(R2 - g2, 0.f) + 1e-6f * R2);
+                x0 = cell_coord<CG>((me.x - rx - cgrid[0]) * cgrid[3]);
+                x1 = cell_coord<CG>((me.x + rx - cgrid[0]) * cgrid[3]);
+              }
+              int rb = cy * CG;
+              if constexpr (D == 3) rb += cz * CG * CG;
+              pk = (unsigned)cstart[rb + x0] | ((unsigned)cstart[rb + x1 + 1] << 16);
+            }
           }
-          if constexpr (D == 3) {
-            const float gz = gap(cz, 2);
-            g2 += gz * gz;
-          }
-          if (g2 > R2) continue;
-          int x0 = c0[0], x1 = c1[0];
-          if (fin) {
-            // +1e-6 R^2: the cancellation in R^2 - g2 (R already carries the rounding margins)
-            const float rx = sqrtf(fmaxf(R2 - g2, 0.f) + 1e-6f * R2);
-            x0 = cell_coord<CG>((me.x - rx - cgrid[0]) * cgrid[3]);
-            x1 = cell_coord<CG>((me.x + rx - cgrid[0]) * cgrid[3]);
-          }
-          int rb = cy * CG;
-          if constexpr (D == 3) rb += cz * CG * CG;
-          const int s0 = cstart[rb + x0], e0 = cstart[rb + x1 + 1];
-          qi = s0 + ((h - off) & (LPA - 1));
-          qe = e0;
-          off = (off + e0 - s0) & (LPA - 1);
+          rt[k] = pk;
         }
+        __builtin_amdgcn_wave_barrier();           // the wave's own LDS writes, read back in order
+        const int kn = min(SCAN_RT, nrow - r0);    // this agent's rows in the batch
+        int k = 0, qi = 0, qe = 0;
+        while (true) {
+          while (qi >= qe && k < kn) {             // this lane's next candidate in a later row
+            const unsigned pk = rt[k++];
+            const int s0 = (int)(pk & 0xffffu), e0 = (int)(pk >> 16);
+            qi = s0 + ((h - off) & (LPA - 1));
+            qe = e0;
+            off = (off + e0 - s0) & (LPA - 1);
+          }
         const bool has = qi < qe;
         if (!__any(has)) break;
         if constexpr (ST) { ph[9] += 1; ph[10] += __popcll(__ballot(has)); }   // steps, candidates
         if (has) {
-          const int qn = clist[qi];               // (for the velocity record, read only when needed)
+          const int qo = qi;
           const float4 cp = ctp[qi];
           qi += LPA;
-          const int j = __float_as_int(cp.w);
+          constexpr bool PK3 = D == 3 && SCAN_CELL_VZ;
+          const int j = PK3 ? (__float_as_int(cp.w) & 0xffff) : __float_as_int(cp.w);
           float dp[D];
           dp[0] = me.x - cp.x;
           dp[1] = me.y - cp.y;
@@ -667,9 +703,14 @@ __global__ __launch_bounds__(BS) void scan_kernel(ScanArgs a) {
           const uint64_t key = knn_key(d2, (unsigned)j);
           if (d2 <= bound && key < bk[K - 1]) topk_insert<K>(bk, key);
           if (a.do_safety && !danger) {
-            const float4 cv = tv[qn];
-            const float lim = 1.01f * (base_i + a.ttc_check * cv.w) + 1e-4f;
+            // the pre-test's speed from the cell-ordered record (SCAN_CELL_VZ; 3-D: rounded up, a
+            // looser pre-test), the velocity record only for the candidates that pass it
+            const float vw = !SCAN_CELL_VZ ? tv[clist[qo]].w
+                             : D == 2   ? cp.z
+                                        : __uint_as_float(__float_as_uint(cp.w) & 0xffff0000u);
+            const float lim = 1.01f * (base_i + a.ttc_check * vw) + 1e-4f;
             if (d2 < lim * lim && j != i) {
+              const float4 cv = tv[clist[qo]];
               float dv[D];
               dv[0] = mv.x - cv.x;
               dv[1] = mv.y - cv.y;
@@ -678,6 +719,8 @@ __global__ __launch_bounds__(BS) void scan_kernel(ScanArgs a) {
             }
           }
         }
+        }
+        __builtin_amdgcn_wave_barrier();           // the batch's reads before the next batch's writes
       }
     }
   }
@@ -910,7 +953,7 @@ static void launch_kdb(const ScanArgs& a, hipStream_t st) {
   size_t lds = scan_lds_bytes(a.Nn);
   b.cells = 0;
   if constexpr (cell_on<D>() && BS >= cell_n<D>()) {
-    const size_t lc = scan_cell_lds<D>((a.Nn + SCH - 1) / SCH * SCH);
+    const size_t lc = scan_cell_lds<D>((a.Nn + SCH - 1) / SCH * SCH, BS / LPA);
     if (lds + lc + 1024 <= 160 * 1024) {
       lds += lc;
       b.cells = 1;
