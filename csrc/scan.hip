@@ -252,10 +252,10 @@ __global__ __launch_bounds__(STAGE_BLOCK) void scan_stage_kernel(ScanArgs a) {
 // every 3-D chunk a full-height column and every 3-D wave box as tall as the env, so a 3-D wave
 // evaluates ~2x the chunks of a 2-D one (stamps_scan.py: 30 vs 14); and in either dimension a wave
 // evaluates a chunk when ANY of its 16 agents needs it. With cells, each agent's four lanes visit
-// only the cells within its own bound (the largest current distance of its previous K neighbours)
-// and safety reach. Same keys, same exact tests: the same lists, bits and counts.
-// 3-D: on (round 5: config #5 scan 93.6 -> 89.3 us per call, fp16 8.56-8.58 -> 8.52-8.53 ms,
-// interleaved, profiles/r5_b27/)
+// only the cell rows within its own bound (the largest current distance of its previous K
+// neighbours) and safety reach. Same keys, same exact tests: the same lists, bits and counts.
+// 3-D: on (round 5: config #5 scan 93.6 -> 72.0 us per call, fp16 8.57 -> 8.12 ms over the cell
+// versions, interleaved, profiles/r5_b27/ - r5_b32/)
 #ifndef SCAN_CELL3
 #define SCAN_CELL3 1
 #endif
@@ -267,11 +267,20 @@ __global__ __launch_bounds__(STAGE_BLOCK) void scan_stage_kernel(ScanArgs a) {
 #ifndef SCAN_CELL_G3
 #define SCAN_CELL_G3 8        // 8^3 cells: ~2.2 graph nodes per cell at config #5
 #endif
+// 2-D: 24^2 cells (~1.8 agents per cell at the headline) in blocks of >= 576 threads (one thread
+// per cell in the prefix sum), 16^2 in smaller blocks. Round 5, with the row-table walk, headline
+// fp32 interleaved: 16^2 10.205 / 10.190, 24^2 10.173 / 10.150, 32^2 10.184 / 10.152 ms
+// (candidates per wave 479 / 372 / 323, profiles/r5_b33/); on a second box 10.118 / 10.152 vs
+// 10.122 / 10.112, bf16 6.255 vs 6.238, slice unchanged (profiles/r5_b34/)
 #ifndef SCAN_CELL_G2
-#define SCAN_CELL_G2 16       // 16^2 cells: 4 agents per cell at the headline
+#define SCAN_CELL_G2 24
 #endif
-template <int D> constexpr int cell_g() { return D == 3 ? SCAN_CELL_G3 : SCAN_CELL_G2; }
-template <int D> constexpr int cell_n() { return D == 3 ? cell_g<3>() * cell_g<3>() * cell_g<3>() : cell_g<2>() * cell_g<2>(); }
+template <int D, int BS> constexpr int cell_g() {
+  return D == 3 ? SCAN_CELL_G3 : (BS >= SCAN_CELL_G2 * SCAN_CELL_G2 ? SCAN_CELL_G2 : 16);
+}
+template <int D, int BS> constexpr int cell_n() {
+  return D == 3 ? cell_g<3, BS>() * cell_g<3, BS>() * cell_g<3, BS>() : cell_g<2, BS>() * cell_g<2, BS>();
+}
 template <int D> constexpr bool cell_on() { return D == 3 ? SCAN_CELL3 != 0 : SCAN_CELL2 != 0; }
 // cell arrays: [NCELL + 1] starts | [NCELL] fill counters | [Np] curve positions (u16) | [Np]
 // node records (x, y, z, id) in cell order (16-byte aligned: one LDS read per candidate)
@@ -281,10 +290,10 @@ template <int D> constexpr bool cell_on() { return D == 3 ? SCAN_CELL3 != 0 : SC
 #ifndef SCAN_CELL_VZ
 #define SCAN_CELL_VZ 1
 #endif
-// rows of an agent's search box per row-table batch (SCAN_ROWTAB; 2-D boxes have at most CG2)
+// rows of an agent's search box per row-table batch (more rows: further batches)
 constexpr int SCAN_RT = 16;
-template <int D> static inline size_t scan_cell_lds(int Np, int nag) {
-  return ((size_t)(2 * cell_n<D>() + 1) * 4 + (size_t)Np * 2 + 15) / 16 * 16 + (size_t)Np * 16 + 16 +
+template <int D, int BS> static inline size_t scan_cell_lds(int Np, int nag) {
+  return ((size_t)(2 * cell_n<D, BS>() + 1) * 4 + (size_t)Np * 2 + 15) / 16 * 16 + (size_t)Np * 16 + 16 +
          (size_t)nag * SCAN_RT * 4;
 }
 // cell coordinate of a scaled position (monotone; NaN and values below 0 -> 0, above -> G-1)
@@ -352,7 +361,7 @@ __global__ __launch_bounds__(BS) void scan_kernel(ScanArgs a) {
   unsigned short* pinv = reinterpret_cast<unsigned short*>(sbh + nsc);
   const float4* Sb = a.S + (long)b * a.s_env * REC<D>;
   const int* perm = a.perm + (long)b * Nn;
-  constexpr int CG = cell_g<D>(), NCELL = cell_n<D>();
+  constexpr int CG = cell_g<D, BS>(), NCELL = cell_n<D, BS>();
   constexpr bool CELLS = cell_on<D>() && !GLB && BS >= NCELL;
   constexpr int MQ = (4096 + BS - 1) / BS;                     // cell path: staged nodes per thread
   const bool use_cells = CELLS && a.cells && a.prev_idx && a.do_knn && Nn <= MQ * BS;   // uniform per launch
@@ -593,7 +602,7 @@ __global__ __launch_bounds__(BS) void scan_kernel(ScanArgs a) {
   if constexpr (CELLS) {
     if (use_cells && wave_live) {
       // this agent's cell box: its bound (kNN) and safety reach, with a margin for the float
-      // rounding of d2 and of the cell mapping; lane h of the agent takes cells h, h + LPA, ...
+      // rounding of d2 and of the cell mapping; its rows are tabulated below
       const float Rk = sqrtf(fmaxf(bound, 0.f)) * 1.001f + 1e-5f;
       const float Rs = a.do_safety ? (1.01f * (base_i + a.ttc_check * cgrid[6]) + 1e-4f) * 1.001f + 1e-5f : 0.f;
       float R = fmaxf(Rk, Rs);
@@ -952,8 +961,8 @@ static void launch_kdb(const ScanArgs& a, hipStream_t st) {
   ScanArgs b = a;
   size_t lds = scan_lds_bytes(a.Nn);
   b.cells = 0;
-  if constexpr (cell_on<D>() && BS >= cell_n<D>()) {
-    const size_t lc = scan_cell_lds<D>((a.Nn + SCH - 1) / SCH * SCH, BS / LPA);
+  if constexpr (cell_on<D>() && BS >= cell_n<D, BS>()) {
+    const size_t lc = scan_cell_lds<D, BS>((a.Nn + SCH - 1) / SCH * SCH, BS / LPA);
     if (lds + lc + 1024 <= 160 * 1024) {
       lds += lc;
       b.cells = 1;
