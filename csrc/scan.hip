@@ -264,8 +264,12 @@ __global__ __launch_bounds__(STAGE_BLOCK) void scan_stage_kernel(ScanArgs a) {
 #ifndef SCAN_CELL2
 #define SCAN_CELL2 1
 #endif
+// 3-D: 10^3 cells (~1.1 graph nodes per cell at config #5; two cells per thread in the prefix sum
+// of the 512-thread blocks). Config #5 fp16, interleaved: 8^3 8.144 / 8.093, 10^3 8.083 / 8.101,
+// 12^3 8.565 / 8.575 ms (its LDS leaves one block per CU); candidates per wave 674 -> 552
+// (profiles/r5_b35/)
 #ifndef SCAN_CELL_G3
-#define SCAN_CELL_G3 8        // 8^3 cells: ~2.2 graph nodes per cell at config #5
+#define SCAN_CELL_G3 10
 #endif
 // 2-D: 24^2 cells (~1.8 agents per cell at the headline) in blocks of >= 576 threads (one thread
 // per cell in the prefix sum), 16^2 in smaller blocks. Round 5, with the row-table walk, headline
@@ -362,7 +366,7 @@ __global__ __launch_bounds__(BS) void scan_kernel(ScanArgs a) {
   const float4* Sb = a.S + (long)b * a.s_env * REC<D>;
   const int* perm = a.perm + (long)b * Nn;
   constexpr int CG = cell_g<D, BS>(), NCELL = cell_n<D, BS>();
-  constexpr bool CELLS = cell_on<D>() && !GLB && BS >= NCELL;
+  constexpr bool CELLS = cell_on<D>() && !GLB;
   constexpr int MQ = (4096 + BS - 1) / BS;                     // cell path: staged nodes per thread
   const bool use_cells = CELLS && a.cells && a.prev_idx && a.do_knn && Nn <= MQ * BS;   // uniform per launch
   __shared__ float cgrid[8];                                   // lo.xyz, cells per unit.xyz, max |v|
@@ -495,26 +499,36 @@ __global__ __launch_bounds__(BS) void scan_kernel(ScanArgs a) {
         }
       }
       __syncthreads();
-      // exclusive scan of the cell counts: wave scans, then the wave totals (one thread per cell)
-      __shared__ int wtot[NCELL / WAVE];
+      // exclusive scan of the cell counts: PC consecutive cells per thread, wave scans of the
+      // thread sums, then the wave totals
+      constexpr int PC = (NCELL + BS - 1) / BS;
+      __shared__ int wtot[BS / WAVE];
       const int tid = threadIdx.x, ln = tid & 63, wv = tid / WAVE;
-      int v = 0, x = 0;
-      if (tid < NCELL) {
-        v = cfill[tid];
-        x = v;
+      int loc[PC];
+      int v = 0;
 #pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-          const int y = __shfl_up(x, o);
-          if (ln >= o) x += y;
-        }
-        if (ln == 63) wtot[wv] = x;
+      for (int p = 0; p < PC; ++p) {
+        const int c = tid * PC + p;
+        loc[p] = v;
+        v += c < NCELL ? cfill[c] : 0;
       }
+      int x = v;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(x, o);
+        if (ln >= o) x += y;
+      }
+      if (ln == 63) wtot[wv] = x;
       __syncthreads();
-      if (tid < NCELL) {
+      {
         int pre = 0;
         for (int w = 0; w < wv; ++w) pre += wtot[w];
-        cstart[tid] = pre + x - v;
-        if (tid == NCELL - 1) cstart[NCELL] = pre + x;
+#pragma unroll
+        for (int p = 0; p < PC; ++p) {
+          const int c = tid * PC + p;
+          if (c < NCELL) cstart[c] = pre + x - v + loc[p];
+        }
+        if (tid == BS - 1) cstart[NCELL] = pre + x;
       }
       __syncthreads();
 #pragma unroll
@@ -961,7 +975,7 @@ static void launch_kdb(const ScanArgs& a, hipStream_t st) {
   ScanArgs b = a;
   size_t lds = scan_lds_bytes(a.Nn);
   b.cells = 0;
-  if constexpr (cell_on<D>() && BS >= cell_n<D, BS>()) {
+  if constexpr (cell_on<D>()) {
     const size_t lc = scan_cell_lds<D, BS>((a.Nn + SCH - 1) / SCH * SCH, BS / LPA);
     if (lds + lc + 1024 <= 160 * 1024) {
       lds += lc;
