@@ -7,10 +7,11 @@ One timed step = a full training iteration on every rank: on-device scenario sam
 rollout (kNN scan + fused controller, until every env is done or INNER_LOOPS), CBF losses,
 hand-written backward through the CBF and BPTT through the rollout, RCCL all-reduce of the
 flat gradient, fused Adam. agent-steps = sum over envs of N x valid rollout steps.
-Weak scaling (default): every rank trains --envs environments of --agents agents. Strong scaling
-(--global_envs G, BASELINE config #3 as stated: G = 64 envs over all ranks): every rank trains
-G / world of them. Random-init weights, synthetic scenarios from the on-device sampler (keyed by
-seed, iteration and rank).
+Default: BASELINE config #3 as stated -- 64 batched envs of 1024 agents over ALL ranks (strong
+scaling: every rank trains 64 / world of them; --global_envs G changes the total). Weak scaling
+(every rank trains its own --envs environments, 64 unless given) with --weak or an explicit
+--envs. The JSON carries "scaling" and "global_batch" either way. Random-init weights, synthetic
+scenarios from the on-device sampler (keyed by seed, iteration and rank).
 
 Precision (--dtype): fp32 (default) is the reference precision (/root/reference is fp32 end to
 end): the near-fp32 3-term split-bf16 MFMA kernels (each operand hi + lo, ~16 significant bits;
@@ -18,7 +19,7 @@ hi*hi + hi*lo + lo*hi, fp32 accumulation: ~2^-16 relative per product, tighter t
 cuDNN uses for the reference's Conv1d layers). bf16 / fp16 are the faster 16-bit-input modes (fp16
 with dynamic loss scaling). Default window: 20 timed steps after 5 warm-up steps.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--dtype fp32|bf16|fp16] [--global_envs G]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--dtype fp32|bf16|fp16] [--global_envs G | --weak | --envs E]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
 
 `python bench.py --gpus N` without a launcher starts the N ranks itself (parallel/launch.py): one
@@ -52,9 +53,12 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--agents", type=int, default=1024)
-    ap.add_argument("--envs", type=int, default=64, help="environments per rank (weak scaling)")
-    ap.add_argument("--global_envs", type=int, default=0,
-                    help="strong scaling: environments over all ranks (BASELINE config #3: 64), sharded per rank")
+    ap.add_argument("--envs", type=int, default=None,
+                    help="environments per rank: weak scaling (default 64 with --weak)")
+    ap.add_argument("--weak", action="store_true", help="weak scaling: --envs (default 64) environments per rank")
+    ap.add_argument("--global_envs", type=int, default=64,
+                    help="strong scaling (the default; BASELINE config #3: 64): environments over all ranks, "
+                         "sharded per rank")
     ap.add_argument("--inner_loops", type=int, default=50)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no_early_stop", action="store_true", help="fixed-T (=inner_loops) throughput")
@@ -102,10 +106,10 @@ def main():
     if not cpu and not plan.share_devices and len({u for _, u in dev_ids}) != world:
         raise SystemExit(f"launch error: ranks share devices {dev_ids}; RCCL needs one device per rank")
     sync = (lambda: None) if cpu else torch.cuda.synchronize
-    strong = args.global_envs > 0
-    if strong and args.global_envs % world:
-        raise SystemExit(f"--global_envs {args.global_envs} must be divisible by the world size {world}")
-    envs = args.global_envs // world if strong else args.envs
+    strong = not args.weak and args.envs is None
+    if strong and (args.global_envs < world or args.global_envs % world):
+        raise SystemExit(f"--global_envs {args.global_envs} must be a positive multiple of the world size {world}")
+    envs = args.global_envs // world if strong else (args.envs or 64)
     cfg = C.TrainConfig(num_agents=args.agents, num_envs=envs, inner_loops=args.inner_loops,
                         seed=args.seed, device="cpu" if cpu else "hip", early_stop=not args.no_early_stop,
                         display_steps=10 ** 9, save_steps=10 ** 9, dim=args.dim, num_obstacles=args.num_obstacles,

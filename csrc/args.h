@@ -346,6 +346,7 @@ struct AdamArgs {
 
 extern "C" {
 int mb_scan(const mb::ScanArgs* a, hipStream_t st);
+int mb_scan_plan(const mb::ScanArgs* a, long* out);
 int mb_cell_sort(const mb::CellSortArgs* a, hipStream_t st);
 int mb_scenario(const mb::ScenArgs* a, hipStream_t st);
 int mb_ctrl_fwd(const mb::CtrlArgs* a, int num_cu, hipStream_t st);

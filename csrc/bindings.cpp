@@ -51,6 +51,19 @@ static int scan(u64 S, long s_env, u64 perm, int B, int N, int K, u64 idx, long 
   return mb_scan(&a, ST(stream));
 }
 
+// the launch plan mb_scan picks for a call of this shape (tests assert the instantiation they hit)
+static py::tuple scan_plan(int B, int N, int K, int Nn, int dim, int has_prev, int do_knn, int do_safety, int lanes) {
+  mb::ScanArgs a{};
+  a.B = B; a.N = N; a.K = K; a.Nn = Nn; a.dim = dim; a.lanes = lanes;
+  a.do_knn = do_knn; a.do_safety = do_safety;
+  static const int dummy = 0;
+  a.prev_idx = has_prev ? &dummy : nullptr;
+  long out[9] = {};
+  const int rc = mb_scan_plan(&a, out);
+  if (rc) throw std::runtime_error("scan_plan: bad arguments");
+  return py::make_tuple(out[0], out[1], out[2], out[3], out[4], out[5], out[6], out[7], out[8]);
+}
+
 static int scenario(u64 S, long s_env, u64 G, u64 obs, int M, int dim, int B, int N, float L, float r, float spread,
                     u64 seed, int max_rounds, u64 status, u64 ws, long ws_env, u64 stream) {
   mb::ScenArgs a{};
@@ -364,6 +377,7 @@ PYBIND11_MODULE(_C, m) {
   m.doc() = "macbf_gnn_amd native gfx950 kernels";
   register_runtime(m);
   m.def("scan", &scan);
+  m.def("scan_plan", &scan_plan);
   m.def("cell_sort", &cell_sort);
   m.def("scenario", &scenario);
   m.def("ctrl_fwd", &ctrl_fwd);

@@ -620,6 +620,9 @@ __global__ __launch_bounds__(BS) void scan_kernel(ScanArgs a) {
       const float Rk = sqrtf(fmaxf(bound, 0.f)) * 1.001f + 1e-5f;
       const float Rs = a.do_safety ? (1.01f * (base_i + a.ttc_check * cgrid[6]) + 1e-4f) * 1.001f + 1e-5f : 0.f;
       float R = fmaxf(Rk, Rs);
+#ifdef MB_DIAG_SCAN_SHRINK
+      R *= 0.7f;      // negative check only (build_variant.sh): a too-small box must fail the oracle tests
+#endif
       bool fin = R < INFINITY && me.x == me.x && me.y == me.y;
       if constexpr (D == 3) fin = fin && me.z == me.z;
       int c0[3] = {0, 0, 0}, c1[3] = {CG - 1, CG - 1, D == 3 ? CG - 1 : 0};
@@ -954,43 +957,77 @@ __global__ __launch_bounds__(BS) void scan_kernel(ScanArgs a) {
 #endif
 constexpr size_t SCAN_BOX_LDS = 160 * 1024 - 1024;   // LDS budget of the culling boxes (GLB 1)
 
-template <int K, int D, int BS, int LPA = SCAN_LPA>
-static void launch_kdb(const ScanArgs& a, hipStream_t st) {
-  dim3 grid((a.Nn + BS / LPA - 1) / (BS / LPA), a.B);
+// The launch plan of one scan call (mb_scan_plan reports it, so the tests can assert which
+// instantiation they exercised): block size, lanes per agent, staging mode, whether the block
+// allocates the cell grid's LDS and uses it, the grid side, per-wave count atomics, the block count
+// and the dynamic LDS.
+struct ScanPlan { int bs, lpa, glb, cells, use_cells, cell_g, wave_atomic, blocks; long lds; };
+
+template <int D, int BS, int LPA>
+static ScanPlan plan_kdb(const ScanArgs& a) {
+  ScanPlan p{};
+  p.bs = BS;
+  p.lpa = LPA;
+  p.blocks = (a.Nn + BS / LPA - 1) / (BS / LPA) * a.B;
+  p.wave_atomic = (D == 3 ? SCAN_WAVE_ATOMIC3 : SCAN_WAVE_ATOMIC) != 0;
   if (a.Nn > SCAN_MAXN) {
     const int Np = (a.Nn + SCH - 1) / SCH * SCH, nch = Np / SCH, nsc = (nch + SSC - 1) / SSC;
+    p.lds = (long)2 * (nch + nsc) * 16;
+    p.glb = (size_t)p.lds > SCAN_BOX_LDS ? 2 : 1;
+    if (p.glb == 2) p.lds = 0;
+    return p;
+  }
+  // the cell grid's LDS (SCAN_CELL*) only for calls that search it (a temporal bound and a kNN
+  // pass: not the first step of a rollout, not the safety-only tail scans -- ADVICE r5), and only
+  // when the env still fits the 160 KB with it
+  p.lds = (long)scan_lds_bytes(a.Nn);
+  if constexpr (cell_on<D>()) {
+    if (a.prev_idx && a.do_knn) {
+      const size_t lc = scan_cell_lds<D, BS>((a.Nn + SCH - 1) / SCH * SCH, BS / LPA);
+      if ((size_t)p.lds + lc + 1024 <= 160 * 1024) {
+        p.lds += (long)lc;
+        p.cells = 1;
+        p.cell_g = cell_g<D, BS>();
+      }
+    }
+  }
+  constexpr int MQ = (4096 + BS - 1) / BS;
+  p.use_cells = p.cells && a.Nn <= MQ * BS;       // the kernel's use_cells condition
+  return p;
+}
+
+template <int K, int D, int BS, int LPA = SCAN_LPA>
+static void launch_kdb(const ScanArgs& a, hipStream_t st, ScanPlan* plan) {
+  const ScanPlan p = plan_kdb<D, BS, LPA>(a);
+  if (plan) {                // mb_scan_plan: report, do not launch
+    *plan = p;
+    return;
+  }
+  dim3 grid((a.Nn + BS / LPA - 1) / (BS / LPA), a.B);
+  if (p.glb) {
+    const int Np = (a.Nn + SCH - 1) / SCH * SCH, nch = Np / SCH;
     hipLaunchKernelGGL(scan_stage_kernel<D>, dim3((nch + STAGE_BLOCK - 1) / STAGE_BLOCK, a.B), dim3(STAGE_BLOCK), 0,
                        st, a);
-    const size_t lds = (size_t)2 * (nch + nsc) * 16;
-    if (lds > SCAN_BOX_LDS) {                // huge envs: the boxes stay in the global workspace
+    if (p.glb == 2) {                // huge envs: the boxes stay in the global workspace
       if constexpr (BS == SCAN_BS_BIG && LPA == SCAN_LPA)
         hipLaunchKernelGGL((scan_kernel<K, D, BS, LPA, 2>), grid, dim3(BS), 0, st, a);
       return;
     }
-    (void)hipFuncSetAttribute((const void*)scan_kernel<K, D, BS, LPA, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL((scan_kernel<K, D, BS, LPA, 1>), grid, dim3(BS), lds, st, a);
+    (void)hipFuncSetAttribute((const void*)scan_kernel<K, D, BS, LPA, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)p.lds);
+    hipLaunchKernelGGL((scan_kernel<K, D, BS, LPA, 1>), grid, dim3(BS), p.lds, st, a);
     return;
   }
-  // the cell grid's LDS (SCAN_CELL*) only when the env still fits the 160 KB with it
   ScanArgs b = a;
-  size_t lds = scan_lds_bytes(a.Nn);
-  b.cells = 0;
-  if constexpr (cell_on<D>()) {
-    const size_t lc = scan_cell_lds<D, BS>((a.Nn + SCH - 1) / SCH * SCH, BS / LPA);
-    if (lds + lc + 1024 <= 160 * 1024) {
-      lds += lc;
-      b.cells = 1;
-    }
-  }
+  b.cells = p.cells;
   if constexpr (K == 12) {
     if (a.stamps) {           // diagnostics: phase clocks (scripts/stamps_scan.py)
-      (void)hipFuncSetAttribute((const void*)scan_kernel<K, D, BS, LPA, 0, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-      hipLaunchKernelGGL((scan_kernel<K, D, BS, LPA, 0, true>), grid, dim3(BS), lds, st, b);
+      (void)hipFuncSetAttribute((const void*)scan_kernel<K, D, BS, LPA, 0, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)p.lds);
+      hipLaunchKernelGGL((scan_kernel<K, D, BS, LPA, 0, true>), grid, dim3(BS), p.lds, st, b);
       return;
     }
   }
-  (void)hipFuncSetAttribute((const void*)scan_kernel<K, D, BS, LPA, 0>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL((scan_kernel<K, D, BS, LPA, 0>), grid, dim3(BS), lds, st, b);
+  (void)hipFuncSetAttribute((const void*)scan_kernel<K, D, BS, LPA, 0>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)p.lds);
+  hipLaunchKernelGGL((scan_kernel<K, D, BS, LPA, 0>), grid, dim3(BS), p.lds, st, b);
 }
 
 
@@ -1005,8 +1042,9 @@ static int scan_num_cu() {
 
 // Small scans (a strong-scaling slice: few envs) would fill only some CUs with big blocks: use
 // 256-thread blocks whenever the big-block grid has fewer blocks than CUs.
+template <int D>
 static bool scan_small_grid(const ScanArgs& a) {
-  constexpr int AG = SCAN_BS_BIG / SCAN_LPA;      // agents per big block
+  constexpr int AG = (D == 3 ? SCAN_BS_BIG3 : SCAN_BS_BIG) / SCAN_LPA;      // agents per big block
   return (long)a.B * ((a.Nn + AG - 1) / AG) < scan_num_cu();
 }
 
@@ -1032,17 +1070,17 @@ static bool scan_boxes_global(const ScanArgs& a) {
 // slower in round 5: config #5 fp16 9.93 vs 9.50-9.52 ms, profiles/r5_b6/)
 
 template <int K, int D>
-static void launch_kd(const ScanArgs& a, hipStream_t st) {
-  if (scan_boxes_global(a)) launch_kdb<K, D, SCAN_BS_BIG>(a, st);
-  else if (scan_lpa8(a)) launch_kdb<K, D, 256, 8>(a, st);
-  else if (a.Nn > 512 && !scan_small_grid(a)) launch_kdb<K, D, D == 3 ? SCAN_BS_BIG3 : SCAN_BS_BIG>(a, st);
-  else launch_kdb<K, D, 256>(a, st);
+static void launch_kd(const ScanArgs& a, hipStream_t st, ScanPlan* plan) {
+  if (scan_boxes_global(a)) launch_kdb<K, D, SCAN_BS_BIG>(a, st, plan);
+  else if (scan_lpa8(a)) launch_kdb<K, D, 256, 8>(a, st, plan);
+  else if (a.Nn > 512 && !scan_small_grid<D>(a)) launch_kdb<K, D, D == 3 ? SCAN_BS_BIG3 : SCAN_BS_BIG>(a, st, plan);
+  else launch_kdb<K, D, 256>(a, st, plan);
 }
 
 template <int K>
-static void launch_k(const ScanArgs& a, hipStream_t st) {
-  if (a.dim == 3) launch_kd<K, 3>(a, st);
-  else launch_kd<K, 2>(a, st);
+static void launch_k(const ScanArgs& a, hipStream_t st, ScanPlan* plan = nullptr) {
+  if (a.dim == 3) launch_kd<K, 3>(a, st, plan);
+  else launch_kd<K, 2>(a, st, plan);
 }
 
 }  // namespace mb
@@ -1068,4 +1106,17 @@ extern "C" int mb_scan(const mb::ScanArgs* a, hipStream_t st) {
     default: return -1;
   }
   return (int)hipGetLastError();
+}
+
+// The plan mb_scan would launch for these arguments (no launch; the plan does not depend on K):
+// out = {block size, lanes per agent, staging mode (0 LDS, 1 global records, 2 global boxes),
+// cell LDS allocated, cell grid searched, cell grid side, per-wave count atomics, blocks, LDS bytes}
+extern "C" int mb_scan_plan(const mb::ScanArgs* a, long* out) {
+  using namespace mb;
+  if (a->Nn < a->N) return -3;
+  ScanPlan p{};
+  launch_k<1>(*a, nullptr, &p);
+  const long v[9] = {p.bs, p.lpa, p.glb, p.cells, p.use_cells, p.cell_g, p.wave_atomic, p.blocks, p.lds};
+  for (int k = 0; k < 9; ++k) out[k] = v[k];
+  return 0;
 }

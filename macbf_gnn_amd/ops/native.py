@@ -282,6 +282,19 @@ def scan(S, idx, dang, cnt, safe, *, K, do_knn=True, do_safety=True, perm=None, 
     _ok(rc, "scan")
 
 
+def scan_plan(B: int, N: int, K: int, *, Nn: int | None = None, dim: int = 2, prev: bool = True, do_knn: bool = True,
+              do_safety: bool = True, lanes: int = 0) -> dict:
+    """The launch plan ``scan`` picks for a call of this shape, without launching (csrc/scan.hip
+    mb_scan_plan): block size ``bs``, lanes per agent ``lpa``, staging mode ``glb`` (0 LDS, 1 global
+    records, 2 global boxes), cell-grid LDS allocated ``cells`` / searched ``use_cells``, grid side
+    ``cell_g``, per-wave count atomics ``wave_atomic``, ``blocks`` and dynamic ``lds`` bytes. Tests
+    use it to assert the instantiation they exercise."""
+    Nn = N if Nn is None else int(Nn)
+    v = lib().scan_plan(int(B), int(N), int(K), Nn, int(dim), int(bool(prev)), int(bool(do_knn)),
+                        int(bool(do_safety)), int(lanes))
+    return dict(zip(("bs", "lpa", "glb", "cells", "use_cells", "cell_g", "wave_atomic", "blocks", "lds"), v))
+
+
 def scenario(S, G, *, seed, L, r=C.DIST_MIN_THRES, spread=C.GOAL_SPREAD, max_rounds=256, status=None, obs=None):
     """S (B, >=N, W) agent records out (velocity 0), G (B, N, D) goals out; obs (B, M, D) static
     obstacle points kept > r from every start and goal."""

@@ -1,7 +1,7 @@
 #!/usr/bin/env bash
 # DP scaling sweep of the headline in ONE allocation (VERDICT r3 missing #3): N = 1/2/4/8 ranks,
-# one per GPU over RCCL, weak (64 envs per GPU) and strong (BASELINE config #3 as stated:
-# --global_envs 64 sharded over the ranks). One JSON line per run (bench.py's, with world,
+# one per GPU over RCCL, weak (--weak: 64 envs per GPU) and strong (BASELINE config #3 as stated,
+# bench.py's default: --global_envs 64 sharded over the ranks). One JSON line per run (bench.py's, with world,
 # dp_backend, device ids) appended to $OUT. N larger than the visible device count is skipped
 # (bench.py would refuse it anyway).
 #
@@ -23,8 +23,8 @@ for mode in weak strong; do
       echo "skip $mode N=$n (only $NDEV devices)" | tee -a "${OUT%.jsonl}.log"
       continue
     fi
-    extra=()
-    [ "$mode" = strong ] && extra=(--global_envs 64)
+    extra=(--global_envs 64)
+    [ "$mode" = weak ] && extra=(--weak)
     echo "== $mode N=$n" | tee -a "${OUT%.jsonl}.log"
     line=$(timeout -k 10 600 python bench.py --gpus "$n" --steps "$STEPS" --warmup "$WARMUP" --dtype "$DTYPE" \
            "${extra[@]}" 2>>"${OUT%.jsonl}.log" | grep '^{')

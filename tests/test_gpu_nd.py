@@ -55,8 +55,9 @@ def test_scan_nd_obstacles(dim, nobs, N):
 
 @pytest.mark.parametrize("nobs,lattice", [(8, False), (0, True)])
 def test_scan_3d_temporal_bound_large(nobs, lattice):
-    """Config #5 scale (1,024 agents, the big-block 3-D scan) with the previous step's kNN as the
-    temporal bound, step after step on moving states: lists, danger bits, counts and safety equal
+    """Config #5 env size (1,024 agents; at B = 3 the launcher picks the 256-thread, 8-lane
+    layout -- the production 512-thread config #5 plan is pinned in test_gpu_scan_plans.py) with
+    the previous step's kNN as the temporal bound, step after step on moving states: lists, danger bits, counts and safety equal
     the oracle (the path that searches the 3-D cell grid when SCAN_CELL3 is on, the chunk culling
     otherwise). lattice: positions on a coarse grid, many equal distances (exact tie order)."""
     B, N, K = 3, 1024, C.TOP_K

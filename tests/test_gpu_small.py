@@ -155,3 +155,39 @@ def test_backward_graph_matches_eager(kw, monkeypatch):
         assert torch.equal(sa.raw[:16], sb.raw[:16]), it
         assert float(sa["T"]) == float(sb["T"])
     assert len(b.engine._bwd_graphs) == 1
+
+
+def test_backward_graphs_of_several_horizons_replay_exactly(monkeypatch):
+    """Early stop changes the horizon T between iterations, so several per-T backward graphs are
+    captured into ONE memory pool and replayed in any order. Scenarios of different
+    horizons, visited as A B A B A, through the graphed engine give the eager engine's gradient and
+    statistics bit for bit, with one graph per horizon."""
+    monkeypatch.setenv("MACBF_BWD_GRAPH", "0")
+    a = _trainer(True, T=40, B=1, N=32)
+    monkeypatch.setenv("MACBF_BWD_GRAPH", "1")
+    b = _trainer(True, T=40, B=1, N=32)
+    b.fp.flat.copy_(a.fp.flat)
+    b.engine.after_update()
+    # scenarios with distinct horizons (eager probe runs; the parameters never change: no Adam step)
+    scen, horizons = [], set()
+    for it in range(40):
+        s0, g, obs = a.sample(it)
+        T = int(a.engine.rollout(s0, g, obs))
+        if T not in horizons:
+            horizons.add(T)
+            scen.append((s0.clone(), g.clone(), None if obs is None else obs.clone()))
+        if len(scen) == 2:
+            break
+    assert len(scen) == 2, f"no two horizons among the sampled scenarios: {horizons}"
+    for it, k in enumerate((0, 1, 0, 1, 0)):
+        s0, g, obs = scen[k]
+        sa = a.engine.step(s0, g, obs)
+        ga = a.fp.grad.clone()
+        sb = b.engine.step(s0, g, obs)
+        gb = b.fp.grad.clone()
+        torch.cuda.synchronize()
+        assert torch.isfinite(ga).all()
+        assert float(sa["T"]) == float(sb["T"])
+        assert torch.equal(ga, gb), (it, k)
+        assert torch.equal(sa.raw[:16], sb.raw[:16]), (it, k)
+    assert len(b.engine._bwd_graphs) == 2

@@ -76,7 +76,20 @@ def test_bench_gpus2_spawns_two_ranks_cpu():
     out = json.loads(lines[0])
     assert out["n_gpus"] == 2 and out["world"] == 2 and out["dp_backend"] == "gloo"
     assert out["config"]["parallelism"] == "dp2" and out["config"]["global_batch"] == 4
+    assert out["scaling"] == "weak"             # an explicit --envs is per rank
     assert len(out["device_ids"]) == 2
+
+
+@pytest.mark.timeout(600)
+def test_bench_default_is_the_stated_config_strong_scaled_cpu():
+    """Without --envs / --weak, bench.py runs BASELINE config #3 as stated: 64 envs over ALL ranks
+    (32 per rank at --gpus 2), reported as strong scaling with global_batch 64."""
+    r = _bench(["--gpus", "2", "--device", "cpu", "--agents", "6", "--steps", "1", "--warmup", "0",
+                "--inner_loops", "2"], {"MACBF_DP_BACKEND": "gloo"})
+    assert r.returncode == 0, r.stderr[-2000:]
+    out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    assert out["scaling"] == "strong" and out["config"]["global_batch"] == 64
+    assert out["config"]["envs_per_gpu"] == 32 and out["config"]["parallelism"] == "dp2"
 
 
 @pytest.mark.timeout(300)
