@@ -18,13 +18,9 @@
 #include "args.h"
 #include "state.h"
 
-#ifndef CBF_NW
-#if MB_X3
-#define CBF_NW 4   // x3: one wave per SIMD (split activations double the register footprint)
-#else
-#define CBF_NW 8   // waves per CBF-backward workgroup (4: one per SIMD, 8: two per SIMD)
-#endif
-#endif
+// waves per 32x32x16 CBF-backward workgroup: x3 4 (one per SIMD: the split activations double
+// the register footprint), 1-pass 8 (two per SIMD)
+constexpr int CBF_NW = MB_X3 ? 4 : 8;
 
 namespace mb {
 namespace MB_PREC {
@@ -159,7 +155,7 @@ __global__ __launch_bounds__(WAVES * 64) void cbf_fwd_kernel(CbfFwdArgs a) {
   h16* wl = reinterpret_cast<h16*>(smem);
   float* vl = reinterpret_cast<float*>(smem + CBF_FWD_FRAGS * FRAG_SZ);
   __shared__ float red[10][WAVES];
-  block_copy16(wl, a.wpack + (size_t)a.f_fwd * FRAG_ELEMS, CBF_FWD_FRAGS * FRAG_SZ, !MB_COPY_ONEWAIT);
+  block_copy16(wl, a.wpack + (size_t)a.f_fwd * FRAG_ELEMS, CBF_FWD_FRAGS * FRAG_SZ, false);
   block_copy16(vl, a.wvec, CBF_VEC * 4);
   __syncthreads();
   const int wave = wave_id(), lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
@@ -388,13 +384,7 @@ DEV void cbf_load(const CbfBwdArgs& a, long chunk, int wave, int r, long E, long
 // x3: without the next-tile prefetch the kernel fits 122 VGPRs -> two 8-wave workgroups
 // (4 waves/SIMD, LDS 2 x 70 KB) per CU instead of one: 1.31 -> 1.22 ms per iteration's h
 // (profiles/r2_hfwd/); the 16-bit builds keep the prefetch (40 KB LDS, more resident waves)
-#ifndef CBF_HFWD_MINW
-#if MB_X3
-#define CBF_HFWD_MINW 4
-#else
-#define CBF_HFWD_MINW 1
-#endif
-#endif
+constexpr int CBF_HFWD_MINW = MB_X3 ? 4 : 1;
 template <int NW, int D>
 __global__ __launch_bounds__(NW * 64, CBF_HFWD_MINW) void cbf_hfwd_kernel(CbfFwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -402,8 +392,8 @@ __global__ __launch_bounds__(NW * 64, CBF_HFWD_MINW) void cbf_hfwd_kernel(CbfFwd
   h16* W3 = W2 + RM_W2;
   h16* wf = W2 + RMP;                         // w1f (2 frags)
   float* vl = reinterpret_cast<float*>(smem + (size_t)RMP * 2 + 2 * FRAG_SZ);
-  block_copy16(W2, a.wrm, RMP * 2, !MB_COPY_ONEWAIT);
-  block_copy16(wf, a.wpack + (size_t)a.f_fwd * FRAG_ELEMS, 2 * FRAG_SZ, !MB_COPY_ONEWAIT);
+  block_copy16(W2, a.wrm, RMP * 2, false);
+  block_copy16(wf, a.wpack + (size_t)a.f_fwd * FRAG_ELEMS, 2 * FRAG_SZ, false);
   block_copy16(vl, a.wvec, CBF_VEC * 4);
   __syncthreads();
   const int wave = wave_id(), lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
@@ -420,24 +410,11 @@ __global__ __launch_bounds__(NW * 64, CBF_HFWD_MINW) void cbf_hfwd_kernel(CbfFwd
     cbf_edge<D>(a.S, a.s_env, a.s_step, pass ? a.idx1 : a.idx, a.B, a.N, a.K, e, in ? E : 0, pass, a.obs_r,
                 a.dist_thr, a.dist_eps, c);
   };
-#ifndef CBF_HFWD_PREFETCH
-#if MB_X3
-#define CBF_HFWD_PREFETCH 0
-#else
-#define CBF_HFWD_PREFETCH 1
-#endif
-#endif
 // 1-pass builds: the three-stage gather pipeline below (bf16 headline 6.86-6.88 vs 6.89-6.91 ms,
 // profiles/r4_loads/); x3: no prefetch at all -- the pipeline's registers spill at the 128 of four
-// waves per SIMD (10.91-10.94 vs 10.93 ms, 3 waves per SIMD 10.96-10.98 ms)
-#ifndef CBF_HFWD_PIPE
-#if MB_X3
-#define CBF_HFWD_PIPE 0
-#else
-#define CBF_HFWD_PIPE 1
-#endif
-#endif
-#if CBF_HFWD_PIPE
+// waves per SIMD (10.91-10.94 vs 10.93 ms, 3 waves per SIMD 10.96-10.98 ms; the one-tile-ahead
+// prefetch variant is in the git history, round 5)
+#if !MB_X3
   // Gather pipeline over a wave's tiles k, k + stride, ...: the chain src[u] (extras) -> idx[e] ->
   // S[i], S[j] is three dependent loads, so each runs one tile apart -- src three tiles ahead, idx
   // two ahead, the two node records one ahead -- every load unconditional (clamped indices) and
@@ -509,17 +486,10 @@ __global__ __launch_bounds__(NW * 64, CBF_HFWD_MINW) void cbf_hfwd_kernel(CbfFwd
       c.mask = cur.in && c.d <= a.obs_r;
     }
 #else
-  EdgeCtx<D> nx;
   unsigned tile = (CBF_XCD ? xcd_block((int)blockIdx.x, (int)gridDim.x) : (int)blockIdx.x) * NW + wave;
-  if (CBF_HFWD_PREFETCH && tile < ntiles) load(tile, nx);
   for (; tile < ntiles; tile += stride) {
-#if CBF_HFWD_PREFETCH
-    const EdgeCtx<D> c = nx;
-    if (tile + stride < ntiles) load(tile + stride, nx);
-#else
     EdgeCtx<D> c;
     load(tile, c);
-#endif
 #endif
     const h16x8 F = cbf_edge_frag<D>(c.rp, c.rv, c.eye, c.dfeat, c.ok, h);
     const h16* wt = wf + opaque_zero();
@@ -567,10 +537,7 @@ __global__ __launch_bounds__(NW * 64, CBF_HFWD_MINW) void cbf_hfwd_kernel(CbfFwd
   }
 }
 
-#ifndef CBF_HFWD_WAVES
-#define CBF_HFWD_WAVES 8
-#endif
-constexpr int HFWD_WAVES = CBF_HFWD_WAVES;
+constexpr int HFWD_WAVES = 8;
 constexpr size_t HFWD_LDS = (size_t)RMP * 2 + 2 * FRAG_SZ + CBF_VEC * 4;
 
 template <bool FUSED, int NW, int D>
@@ -589,9 +556,9 @@ __global__ __launch_bounds__(NW * 64, 1) void cbf_bwd_kernel(CbfBwdArgs a) {
   __shared__ float lacc[8][FUSED ? CH / 2 : 1];  // fused: per-lane loss partial sums (pass-0 lanes)
   __shared__ float lred[NW][10];
   __shared__ float red4[NW];
-  block_copy16(W2, a.wrm, RMP * 2, !MB_COPY_ONEWAIT);
-  block_copy16(wf, a.wpack + (size_t)a.f_bwd * FRAG_ELEMS, 2 * FRAG_SZ, !MB_COPY_ONEWAIT);
-  block_copy16(wf + 2 * FRAG_ELEMS, a.wpack + (size_t)(a.f_bwd + 66) * FRAG_ELEMS, 4 * FRAG_SZ, !MB_COPY_ONEWAIT);
+  block_copy16(W2, a.wrm, RMP * 2, false);
+  block_copy16(wf, a.wpack + (size_t)a.f_bwd * FRAG_ELEMS, 2 * FRAG_SZ, false);
+  block_copy16(wf + 2 * FRAG_ELEMS, a.wpack + (size_t)(a.f_bwd + 66) * FRAG_ELEMS, 4 * FRAG_SZ, false);
   block_copy16(vl, a.wvec, CBF_VEC * 4);
   if constexpr (FUSED)
     for (int q = threadIdx.x; q < 8 * CH / 2; q += blockDim.x) (&lacc[0][0])[q] = 0.f;

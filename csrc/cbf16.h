@@ -51,12 +51,7 @@ constexpr int C16_WG_PER_CU = CBF16_WGPC;
 static_assert(C16_REGION >= C16_PLANES * C16_PLA, "stage A fits the region");
 static_assert(C16_LDS <= 160 * 1024 / C16_WG_PER_CU - 64, "LDS budget");
 
-#ifndef CBF16_DBG
-#define CBF16_DBG 0    // 1: per-record forward sums to a.dbg (scripts/check_cbf16.py)
-#endif
-#ifndef CBF16_REC2
-#define CBF16_REC2 1   // records two chunks ahead, states one chunk ahead (0: record + states at the loop end)
-#endif
+#define CBF16_DBG ((MB_DIAG & 2) != 0)    // per-record forward sums to a.dbg (scripts/check_cbf16.py)
 
 DEV f32x4 bias4(const float* b, int row0, int g) {
   const float4 v = *reinterpret_cast<const float4*>(b + row0 + 4 * g);
@@ -122,8 +117,8 @@ __global__ __launch_bounds__(C16_NW * 64, 2 * C16_WG_PER_CU) void cbf_bwd16_kern
   float* vl = reinterpret_cast<float*>(smem + C16_LDS_W + C16_LDS_F);
   h16* stg = reinterpret_cast<h16*>(smem + C16_LDS_W + C16_LDS_F + CBF_VEC * 4);
   __shared__ float red4[C16_NW];
-  block_copy16(W2, a.wrm16, (int)C16_LDS_W, !MB_COPY_ONEWAIT);
-  block_copy16(wft, a.w16 + 4 * FRAG_ELEMS, (int)C16_LDS_F, !MB_COPY_ONEWAIT);
+  block_copy16(W2, a.wrm16, (int)C16_LDS_W, false);
+  block_copy16(wft, a.w16 + 4 * FRAG_ELEMS, (int)C16_LDS_F, false);
   block_copy16(vl, a.wvec, CBF_VEC * 4);
   __syncthreads();
   const int wave = wave_id(), lane = threadIdx.x & 63, n = lane & 15, g = lane >> 4;
@@ -174,20 +169,14 @@ __global__ __launch_bounds__(C16_NW * 64, 2 * C16_WG_PER_CU) void cbf_bwd16_kern
   if (c0 < nchunks) {   // else no chunk for this workgroup (EV may be 0): zero slab
   Ev16<D> nx;
   ev16_issue<D>(a, rec_at(c0), nx);
-#if CBF16_REC2
   int4 r2 = rec_at(c0 + stride);
-#endif
 
   for (long chunk = c0; chunk < nchunks; chunk += stride) {
     if constexpr (ST) { tck = __builtin_amdgcn_s_memtime(); ph[7] += 1; }
     const Ev16<D> cur = nx;
     const bool in = in_at(chunk);
-#if CBF16_REC2
     ev16_issue<D>(a, r2, nx);                                 // state records of the next chunk
     r2 = rec_at(chunk + 2 * stride);                          // records two chunks ahead
-#else
-    const int4 rn = rec_at(chunk + stride);                   // next chunk's record (states: loop end)
-#endif
     // ---- edge features of this lane's evaluation (all four g-lanes of column n hold it)
     float rp[D], rv[D];
     {
@@ -388,9 +377,6 @@ __global__ __launch_bounds__(C16_NW * 64, 2 * C16_WG_PER_CU) void cbf_bwd16_kern
       __syncthreads();
     }
     stamp(3);
-#if !CBF16_REC2
-    ev16_issue<D>(a, rn, nx);
-#endif
   }
   }
   if (ST && lane == 0)

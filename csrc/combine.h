@@ -11,10 +11,7 @@ namespace mb {
 // node are one coalesced 16*K-byte segment (lane k reads slot k), the incoming edges are
 // spread over the lanes (independent random 16-byte loads, L2-resident per step graph), and
 // a fixed xor butterfly combines the lane partials -> deterministic, no atomics.
-#ifndef CMB_RG
-#define CMB_RG 16
-#endif
-constexpr int RG = CMB_RG;             // lanes per node
+constexpr int RG = 16;             // lanes per node
 
 DEV float grp_sum(float v) {
   static_assert(RG == 16, "16-lane groups");

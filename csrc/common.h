@@ -105,9 +105,15 @@ DEV int opaque_zero() {
 // after an MFMA chain is a branch whose taken path reaches the MFMA's VALU consumers with too few
 // wait states (scripts/check_mfma_exec.py; the round-3 "miscompile" of the 16x16x32 CBF kernel, whose
 // stamps are now a template instantiation)
-#ifndef MB_STAMPS
-#define MB_STAMPS 0
+// Diagnostics builds: ONE switch, MB_DIAG (a bit mask; scripts/build_variant.sh NAME KERNELS
+// "-DMB_DIAG=<bits>"), never set in production: 1 phase clocks of the 32x32x16 backward kernels
+// (MB_STAMPS), 2 per-record forward sums of the 16x16x32 CBF backward (scripts/check_cbf16.py), 4 the
+// 16x16x32 node backward without its dL/dpooled stores (phase clocks), 8 the kNN scan's cell search
+// box shrunk to 0.7x (negative check: the oracle tests must fail, tests/test_gpu_scan_plans.py).
+#ifndef MB_DIAG
+#define MB_DIAG 0
 #endif
+#define MB_STAMPS ((MB_DIAG & 1) != 0)
 
 // The wave's index in its workgroup as a wave-uniform (SGPR) value. Every branch on it is then a
 // scalar branch (s_cbranch_scc) rather than an EXEC-masked region. This matters for MFMAs: the
@@ -135,17 +141,11 @@ DEV int xcd_block(int bid, int nwg) {
 // 10.85 -> 10.69 ms, bf16 6.85 -> 6.74, profiles/r4_xcd/). ROLL_XCD: the same for the rollout's
 // forward step and kNN scan (blocks of one env on one XCD: 10.68-10.69 -> 10.67-10.68 ms, bf16
 // 6.73 -> 6.72). node_reduce (graph.hip NODE_RED_XCD): neutral, kept for the same locality.
-#ifndef BPTT_XCD
-#define BPTT_XCD 1
-#endif
-#ifndef ROLL_XCD
-#define ROLL_XCD 1
-#endif
+constexpr bool BPTT_XCD = true;
+constexpr bool ROLL_XCD = true;
 // CBF_XCD: the CBF h forward / backward over the evaluation list, x3 builds (10.77 -> 10.74 ms;
 // bf16 6.74 vs 6.75: off there)
-#ifndef CBF_XCD
-#define CBF_XCD MB_X3
-#endif
+constexpr bool CBF_XCD = MB_X3 != 0;
 
 // lane l <- lane l^32 with v_permlane32_swap (CDNA4, VALU) instead of ds_bpermute (LDS path)
 DEV unsigned xor32u(unsigned u) {
@@ -174,20 +174,14 @@ DEV void lds_wave_order() { asm volatile("" ::: "memory"); }
 // (8 independent 16-byte loads in flight per thread before the stores: the weight staging at
 // kernel start is latency-bound, which dominates small launches -- a 120 KB x3 image is 30
 // loads per thread of a 256-thread block)
-// MB_GLDS_COPY (default): LDS-DMA instead -- every wave issues all of its 16-byte
+// LDS-DMA (the VGPR copy it replaced is in the git history, round 5) -- every wave issues all of its 16-byte
 // global_load_lds_dwordx4 copies back to back (no VGPR staging, one latency round trip for the
 // whole image instead of one per 8 loads), then waits for them before the caller's barrier.
 // The destination of one wave instruction is its wave-uniform base + lane x 16: a lane-linear
 // image, which a plain copy is. Callers pass LDS destinations and global sources.
-#ifndef MB_GLDS_COPY
-#define MB_GLDS_COPY 1
-#endif
-// MB_COPY_ONEWAIT: a kernel's back-to-back weight copies wait once, after the last (default since
-// round 5: controller-step staging 6.0 -> 4.7 k cycles, headline fp32 10.609-10.643 -> 10.557-10.587
-// ms interleaved, bf16 neutral, profiles/r5_b18/; 0 = a wait after every copy)
-#ifndef MB_COPY_ONEWAIT
-#define MB_COPY_ONEWAIT 1
-#endif
+// A kernel's back-to-back weight copies wait once, after the last (pass wait = false to all but
+// the last; round 5: controller-step staging 6.0 -> 4.7 k cycles, headline fp32 10.609-10.643 -> 10.557-10.587
+// ms interleaved, bf16 neutral, profiles/r5_b18/)
 // wait = false (LDS-DMA path): issue only -- consecutive copies then share one latency round trip;
 // the LAST copy before the caller's barrier must wait (vmcnt(0) covers every copy issued before)
 DEV void block_copy16(void* dst, const void* src, int bytes, bool wait = true) {
@@ -195,31 +189,14 @@ DEV void block_copy16(void* dst, const void* src, int bytes, bool wait = true) {
   u32x4* d = reinterpret_cast<u32x4*>(dst);
   const int n = bytes / 16, bd = blockDim.x;
   int i = threadIdx.x;
-#if MB_GLDS_COPY
-  {
-    const int lane = threadIdx.x & 63;
-    for (; i - lane < n; i += bd) {       // wave-uniform trip count (the wave's first index)
-      if (i < n)
-        __builtin_amdgcn_global_load_lds(
-            (const __attribute__((address_space(1))) void*)(s + i),
-            (__attribute__((address_space(3))) void*)(d + (i - lane)), 16, 0, 0);
-    }
-    if (wait) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    return;
+  const int lane = threadIdx.x & 63;
+  for (; i - lane < n; i += bd) {       // wave-uniform trip count (the wave's first index)
+    if (i < n)
+      __builtin_amdgcn_global_load_lds(
+          (const __attribute__((address_space(1))) void*)(s + i),
+          (__attribute__((address_space(3))) void*)(d + (i - lane)), 16, 0, 0);
   }
-#endif
-  for (; i + 7 * bd < n; i += 8 * bd) {
-    u32x4 v[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) v[u] = s[i + u * bd];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) d[i + u * bd] = v[u];
-  }
-  for (; i + 3 * bd < n; i += 4 * bd) {
-    const u32x4 v0 = s[i], v1 = s[i + bd], v2 = s[i + 2 * bd], v3 = s[i + 3 * bd];
-    d[i] = v0; d[i + bd] = v1; d[i + 2 * bd] = v2; d[i + 3 * bd] = v3;
-  }
-  for (; i < n; i += bd) d[i] = s[i];
+  if (wait) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 // ---- lane exchanges without the LDS crossbar. __shfl_xor is a ds_bpermute_b32: an LDS-unit

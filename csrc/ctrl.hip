@@ -15,6 +15,7 @@
 // pre-packed 1 KiB fragments (ops/layout.py); all intermediate activations stay in VGPRs.
 #pragma clang fp contract(off)
 #include <climits>
+#include <cstdlib>
 #include "common.h"
 #include "args.h"
 #include "state.h"
@@ -716,8 +717,8 @@ __global__ __launch_bounds__(WAVES * 64) void ctrl_fwd_kernel(CtrlArgs a) {
   h16* wn = wl + 18 * FRAG_ELEMS;                                     // nw1f..nw4 (54 frags)
   float* vl = reinterpret_cast<float*>(smem + NFR * FRAG_SZ);
   h16* pools = reinterpret_cast<h16*>(smem + NFR * FRAG_SZ + CTRL_VEC * 4);
-  block_copy16(wl, a.wpack + (size_t)a.f_edge * FRAG_ELEMS, 18 * FRAG_SZ, !MB_COPY_ONEWAIT);
-  if constexpr (!X3 || FUSE) block_copy16(wn, a.wpack + (size_t)a.f_node * FRAG_ELEMS, 54 * FRAG_SZ, !MB_COPY_ONEWAIT);
+  block_copy16(wl, a.wpack + (size_t)a.f_edge * FRAG_ELEMS, 18 * FRAG_SZ, false);
+  if constexpr (!X3 || FUSE) block_copy16(wn, a.wpack + (size_t)a.f_node * FRAG_ELEMS, 54 * FRAG_SZ, false);
   block_copy16(vl, a.wvec, CTRL_VEC * 4);
   __syncthreads();
   const int apw = (a.apw >= 2 && a.apw <= 32) ? a.apw : 32;
@@ -756,7 +757,7 @@ __global__ __launch_bounds__(WAVES * 64) void ctrl_node_fwd_kernel(CtrlArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   h16* wn = reinterpret_cast<h16*>(smem);                             // nw1f..nw4 (54 frags)
   float* vl = reinterpret_cast<float*>(smem + 54 * FRAG_SZ);
-  block_copy16(wn, a.wpack + (size_t)a.f_node * FRAG_ELEMS, 54 * FRAG_SZ, !MB_COPY_ONEWAIT);
+  block_copy16(wn, a.wpack + (size_t)a.f_node * FRAG_ELEMS, 54 * FRAG_SZ, false);
   block_copy16(vl, a.wvec, CTRL_VEC * 4);
   __syncthreads();
   ctrl_node_groups<D>(a, wn, vl, blockIdx.x * WAVES + wave_id(), gridDim.x * WAVES);
@@ -785,18 +786,26 @@ extern "C" int MB_SYM(ctrl_fwd)(const mb::CtrlArgs* a, int num_cu, hipStream_t s
   if (blocks > maxb) blocks = maxb;
   CtrlArgs b = *a;
   b.apw = apw;
-  // x3: one fused launch (edge + node phase per group, 145 KB of weights)
+  // x3: one fused launch (edge + node phase per group, 145 KB of weights: one workgroup per CU)
   if (X3) {
     const size_t ldf = (size_t)CTRL_FWD_FRAGS * FRAG_SZ + CTRL_VEC * 4;
+    // small grids (strong-scaling slices): 4-wave workgroups when the 8-wave grid would leave at
+    // least half of the CUs without a workgroup -- twice the workgroups, one wave per SIMD
+    static const int wv_env = [] { const char* e = getenv("MACBF_CTRL_WAVES"); return e ? atoi(e) : 0; }();
+    const bool w4 = !a->stamps && (wv_env == 4 || (wv_env == 0 && num_cu > 0 && 2 * blocks <= num_cu));
+    const int wv = w4 ? 4 : CTRL_WAVES;
+    const int nb = w4 ? (groups + 3) / 4 < maxb ? (groups + 3) / 4 : maxb : blocks;
     auto go = [&](auto kern) {
       (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ldf);
-      hipLaunchKernelGGL(kern, dim3(blocks), dim3(CTRL_WAVES * 64), ldf, st, b);
+      hipLaunchKernelGGL(kern, dim3(nb), dim3(wv * 64), ldf, st, b);
     };
     if (a->dim == 3) {
       if (a->stamps) go(ctrl_fwd_kernel<CTRL_WAVES, 3, true, true>);
+      else if (w4) go(ctrl_fwd_kernel<4, 3, true>);
       else go(ctrl_fwd_kernel<CTRL_WAVES, 3, true>);
     } else {
       if (a->stamps) go(ctrl_fwd_kernel<CTRL_WAVES, 2, true, true>);
+      else if (w4) go(ctrl_fwd_kernel<4, 2, true>);
       else go(ctrl_fwd_kernel<CTRL_WAVES, 2, true>);
     }
     return (int)hipGetLastError();
@@ -899,9 +908,7 @@ DEV void store_tile_add(float* dst, int ncols, int mt, int nt, const f32x16& old
 // stores it (the next reverse step's Euler term).
 // XO: lane distance between the two halves of an agent (32: lane halves h; 16: the g = 0 / 1
 // lanes of the 16x16x32 node kernel)
-#ifndef CMB_BT
-#define CMB_BT 4
-#endif
+constexpr int CMB_BT = 4;        // edge records per batch of the fused combine's gathers
 template <int D, int XO = 32>
 DEV void fused_combine(const CtrlNodeBwdArgs& a, bool ok, int b, int i, int h, float (&gp)[D], float (&gv)[D]) {
   constexpr int R = REC<D>;
@@ -981,7 +988,7 @@ DEV void node_bwd_body(const CtrlNodeBwdArgs& a, unsigned char* smem, long c0, l
   h16* wr = reinterpret_cast<h16*>(smem);
   float* vl = reinterpret_cast<float*>(smem + RM * 2);
   h16* stg = reinterpret_cast<h16*>(smem + RM * 2 + CTRL_VEC * 4);
-  block_copy16(wr, a.wrm, RM * 2, !MB_COPY_ONEWAIT);
+  block_copy16(wr, a.wrm, RM * 2, false);
   block_copy16(vl, a.wvec, CTRL_VEC * 4);
   __syncthreads();
   const float* nb2 = vl + 128;
@@ -1749,7 +1756,7 @@ template <int D, int KC = 0, bool SPLIT = false>
 DEV void edge_bwd_body(const CtrlEdgeBwdArgs& a, unsigned char* smem, long w0, long wstride, float* P) {
   h16* wf = reinterpret_cast<h16*>(smem);                 // ew1f (2) | ew2tn (16) | ew1ft (4)
   h16* stg = reinterpret_cast<h16*>(smem + 22 * FRAG_SZ);
-  block_copy16(wf, a.wpack + (size_t)a.f_ew1f * FRAG_ELEMS, 2 * FRAG_SZ, !MB_COPY_ONEWAIT);
+  block_copy16(wf, a.wpack + (size_t)a.f_ew1f * FRAG_ELEMS, 2 * FRAG_SZ, false);
   block_copy16(wf + 2 * FRAG_ELEMS, a.wpack + (size_t)a.f_ew2tn * FRAG_ELEMS, 20 * FRAG_SZ);
   __syncthreads();
   const int wave = wave_id(), lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
@@ -2187,8 +2194,8 @@ __global__ __launch_bounds__(SR_WAVES * 64) void rollout_small_kernel(RolloutSma
   h16* wn = wl + 18 * FRAG_ELEMS;                                     // nw1f..nw4 (54 frags)
   float* vl = reinterpret_cast<float*>(smem + (size_t)CTRL_FWD_FRAGS * FRAG_SZ);
   const CtrlArgs& c = ra.c;
-  block_copy16(wl, c.wpack + (size_t)c.f_edge * FRAG_ELEMS, 18 * FRAG_SZ, !MB_COPY_ONEWAIT);
-  block_copy16(wn, c.wpack + (size_t)c.f_node * FRAG_ELEMS, 54 * FRAG_SZ, !MB_COPY_ONEWAIT);
+  block_copy16(wl, c.wpack + (size_t)c.f_edge * FRAG_ELEMS, 18 * FRAG_SZ, false);
+  block_copy16(wn, c.wpack + (size_t)c.f_node * FRAG_ELEMS, 54 * FRAG_SZ, false);
   block_copy16(vl, c.wvec, CTRL_VEC * 4);
   __syncthreads();
   const int b = blockIdx.x, B = c.B, N = c.N, K = c.K, Nn = ra.Nn, Tmax = ra.Tmax;

@@ -30,9 +30,7 @@ namespace mb {
 constexpr int MATCH_BLOCK = 256;
 constexpr int DH_BLOCK = 256;
 constexpr int DH_PARTIAL = 12;
-#ifndef DH_UNROLL
-#define DH_UNROLL 4
-#endif   // loss partials per block: [0, 0, 8 sums, 0, 0] (rows padded to 4)
+constexpr int DH_UNROLL = 4;   // loss partials per block: [0, 0, 8 sums, 0, 0] (rows padded to 4)
 
 // Block-wide exclusive scan of one int per thread (NT threads, wave64): returns the exclusive
 // prefix of this thread, *total = the block sum. Two barriers.

@@ -171,22 +171,13 @@ __global__ __launch_bounds__(CSR_BLOCK) void rev_csr_glb_kernel(CsrArgs a) {
 // gated record accumulation: a zero gate selects zero (the record may hold stale data). The
 // gate is read first and inactive evaluations skip the record load (CMB_GATE_FIRST: one more
 // dependent round trip, but most evaluations are inactive: node_reduce 330 -> 297 us per
-// iteration at the headline, profiles/r2_gather/); 0 loads both together
-#ifndef CMB_GATE_FIRST
-#define CMB_GATE_FIRST 1
-#endif
+// iteration at the headline, profiles/r2_gather/; loading both together: history, round 4)
 template <int R, int SIGN>
 DEV void acc_rec_g(float4 (&g)[R], const float4* src, const float* gate) {
   float4 v[R];
-#if CMB_GATE_FIRST      // inactive evaluations: no record load (one more dependent round trip)
-  const bool on = !gate || *gate != 0.f;
+  const bool on = !gate || *gate != 0.f;     // inactive evaluations: no record load
 #pragma unroll
   for (int q = 0; q < R; ++q) v[q] = on ? src[q] : make_float4(0.f, 0.f, 0.f, 0.f);
-#else
-#pragma unroll
-  for (int q = 0; q < R; ++q) v[q] = src[q];
-  const bool on = !gate || *gate != 0.f;
-#endif
 #pragma unroll
   for (int q = 0; q < R; ++q) {
     if (!on) v[q] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -194,9 +185,7 @@ DEV void acc_rec_g(float4 (&g)[R], const float4* src, const float* gate) {
   }
 }
 
-#ifndef NODE_RED_XCD
-#define NODE_RED_XCD 1
-#endif
+constexpr bool NODE_RED_XCD = true;
 // out[t', b, i] (+)= sum over passes p of [ sum_k dE_p[t'-p, b, i, k] - sum_{e in in(i)} dE_p[e] ]
 // for the N agents (obstacle nodes receive no gradient). Records of REC<D> float4.
 template <int D>

@@ -11,14 +11,10 @@
 // Workgroups per CU of the 8-wave CBF (cbf16.h) and edge (ctrl16.h) backward kernels: one (two
 // waves per SIMD at <= 256 registers). The 1-pass builds fit two in LDS (<= 80 KiB each) but only
 // at <= 128 registers: the CBF kernel then spills 96 registers, the edge kernel 6, and both run
-// slower (bf16 headline 6.48 vs 6.25 ms, profiles/r4_k16/) -- -DCBF16_WGPC=2 / -DE16_WGPC=2 build
-// that variant (scripts/build_variant.sh). The launch grids follow (mb_k16_wg_per_cu).
-#ifndef CBF16_WGPC
-#define CBF16_WGPC 1
-#endif
-#ifndef E16_WGPC
-#define E16_WGPC 1
-#endif
+// slower (bf16 headline 6.48 vs 6.25 ms, profiles/r4_k16/) -- CBF16_WGPC / E16_WGPC = 2 build
+// that variant. The launch grids follow (mb_k16_wg_per_cu).
+constexpr int CBF16_WGPC = 1;
+constexpr int E16_WGPC = 1;
 
 namespace mb {
 namespace MB_PREC {

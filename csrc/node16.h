@@ -31,12 +31,8 @@ namespace MB_PREC {
 // hi + 16 B lo of 8 consecutive features, instead of 8 B of 4 from each tile (default since round 5:
 // dP phase 11.9 -> 5.5 k cycles per chunk, headline 10.649-10.658 -> 10.602-10.636 ms fp32, 6.732-6.742
 // -> 6.705-6.724 bf16, interleaved, profiles/r5_b7/; 0 = the 8-byte stores)
-#ifndef N16_DP_PAIRED
-#define N16_DP_PAIRED 1
-#endif
-#ifndef N16_DIAG_NOSTORE
-#define N16_DIAG_NOSTORE 0      // diagnostics build only: skip the dL/dpooled stores (phase clocks)
-#endif
+constexpr bool N16_DP_PAIRED = true;
+constexpr bool N16_DIAG_NOSTORE = (MB_DIAG & 4) != 0;   // diagnostics build only: skip the dL/dpooled stores
 constexpr int N16_NW = 8, N16_CH = 16 * N16_NW;           // waves, agents per chunk
 constexpr int N16_S1 = 176, N16_S2 = 80, N16_S3 = 144, N16_S4 = 80;   // layout.NODE16_STRIDES (bank model)
 constexpr int N16_O2 = 64 * N16_S1, N16_O3 = N16_O2 + 128 * N16_S2, N16_O4 = N16_O3 + 64 * N16_S3;
@@ -123,7 +119,7 @@ __global__ __launch_bounds__(N16_NW * 64) void ctrl_node_bwd16_kernel(CtrlNodeBw
     }
   };
   stamp(0);
-  block_copy16(W1, a.wrm16, (int)N16_LDS_W, !MB_COPY_ONEWAIT);
+  block_copy16(W1, a.wrm16, (int)N16_LDS_W, false);
   block_copy16(vl, a.wvec + 128, N16_VEC * 4);
   __syncthreads();
   stamp(1);

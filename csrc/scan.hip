@@ -236,16 +236,12 @@ __global__ __launch_bounds__(STAGE_BLOCK) void scan_stage_kernel(ScanArgs a) {
 
 // SCAN_WAVE_ATOMIC (A/B build knob): the per-env counts added by every wave instead of one
 // block-level sum after a barrier
-#ifndef SCAN_WAVE_ATOMIC
-#define SCAN_WAVE_ATOMIC 0
-#endif
+constexpr int SCAN_WAVE_ATOMIC = 0;
 // 3-D scenes: on (round 5: the 3-D candidate loop varies 1.8x between waves of a block, and with
 // the barrier a wave waited for the block's slowest; with SCAN_BS_BIG3 = 512 config #5 fp16
 // 9.26-9.28 -> 8.54-8.56 ms, fp32 13.70 -> 13.05, interleaved, profiles/r5_b15/); 2-D: off
 // (+0.04 ms at the headline, profiles/r5_b14/)
-#ifndef SCAN_WAVE_ATOMIC3
-#define SCAN_WAVE_ATOMIC3 1
-#endif
+constexpr int SCAN_WAVE_ATOMIC3 = 1;
 
 // SCAN_CELL3 / SCAN_CELL2 (A/B build knobs): with a temporal bound, search a uniform cell grid of
 // the env around each agent instead of the wave-uniform chunk culling. The 2-D curve order leaves
@@ -256,29 +252,21 @@ __global__ __launch_bounds__(STAGE_BLOCK) void scan_stage_kernel(ScanArgs a) {
 // neighbours) and safety reach. Same keys, same exact tests: the same lists, bits and counts.
 // 3-D: on (round 5: config #5 scan 93.6 -> 72.0 us per call, fp16 8.57 -> 8.12 ms over the cell
 // versions, interleaved, profiles/r5_b27/ - r5_b32/)
-#ifndef SCAN_CELL3
-#define SCAN_CELL3 1
-#endif
+constexpr int SCAN_CELL3 = 1;
 // 2-D: on (round 5: scan 47.1 -> 33.8 us per call, candidate loop 50 -> 25 k cycles per wave,
 // headline fp32 10.52-10.53 -> 10.26-10.27 ms, bf16 6.65 -> 6.39, interleaved, profiles/r5_b25/)
-#ifndef SCAN_CELL2
-#define SCAN_CELL2 1
-#endif
+constexpr int SCAN_CELL2 = 1;
 // 3-D: 10^3 cells (~1.1 graph nodes per cell at config #5; two cells per thread in the prefix sum
 // of the 512-thread blocks). Config #5 fp16, interleaved: 8^3 8.144 / 8.093, 10^3 8.083 / 8.101,
 // 12^3 8.565 / 8.575 ms (its LDS leaves one block per CU); candidates per wave 674 -> 552
 // (profiles/r5_b35/)
-#ifndef SCAN_CELL_G3
-#define SCAN_CELL_G3 10
-#endif
+constexpr int SCAN_CELL_G3 = 10;
 // 2-D: 24^2 cells (~1.8 agents per cell at the headline) in blocks of >= 576 threads (one thread
 // per cell in the prefix sum), 16^2 in smaller blocks. Round 5, with the row-table walk, headline
 // fp32 interleaved: 16^2 10.205 / 10.190, 24^2 10.173 / 10.150, 32^2 10.184 / 10.152 ms
 // (candidates per wave 479 / 372 / 323, profiles/r5_b33/); on a second box 10.118 / 10.152 vs
 // 10.122 / 10.112, bf16 6.255 vs 6.238, slice unchanged (profiles/r5_b34/)
-#ifndef SCAN_CELL_G2
-#define SCAN_CELL_G2 24
-#endif
+constexpr int SCAN_CELL_G2 = 24;
 template <int D, int BS> constexpr int cell_g() {
   return D == 3 ? SCAN_CELL_G3 : (BS >= SCAN_CELL_G2 * SCAN_CELL_G2 ? SCAN_CELL_G2 : 16);
 }
@@ -291,9 +279,7 @@ template <int D> constexpr bool cell_on() { return D == 3 ? SCAN_CELL3 != 0 : SC
 // SCAN_CELL_VZ: cell records carry the node's speed (2-D: in the unused z slot; 3-D: rounded up to
 // bf16 beside a 16-bit node id), so the safety pre-test of a candidate needs no second (dependent)
 // LDS read
-#ifndef SCAN_CELL_VZ
-#define SCAN_CELL_VZ 1
-#endif
+constexpr int SCAN_CELL_VZ = 1;
 // rows of an agent's search box per row-table batch (more rows: further batches)
 constexpr int SCAN_RT = 16;
 template <int D, int BS> static inline size_t scan_cell_lds(int Np, int nag) {
@@ -307,15 +293,10 @@ template <int G> DEV int cell_coord(float x) { return x >= 1.f ? (x < (float)(G 
 // wave inserted into its list in that chunk, the all-danger update only when some lane's danger
 // flag turned on; the same lists, bits and counts either way (default since round 5: scan 48.8 ->
 // 47.5 us, headline -0.04 ms, config #5 fp16 9.42-9.43 -> 9.30-9.33 ms, profiles/r5_b12/)
-#ifndef SCAN_THR_SKIP
-#define SCAN_THR_SKIP 1
-#endif
 
 // GLB: 0 = env staged in LDS; 1 = nodes in the global workspace, culling boxes copied to LDS;
 // 2 = boxes read from the workspace too (envs whose boxes exceed LDS: > ~36 K nodes)
-#ifndef SCAN_STAGE_BT
-#define SCAN_STAGE_BT 4
-#endif
+constexpr int SCAN_STAGE_BT = 4;
 // ST (diagnostics): per-wave phase clocks and chunk counts to a.stamps[(block * BS/64 + wave) * 16 + k]:
 // 0 env staging, 1 culling boxes, 2 wave setup + temporal bound, 3 candidate loop, 4 list merge,
 // 5 output slots, 6 counts; 8 superchunks visited, 9 chunks tested, 10 chunks evaluated,
@@ -620,9 +601,7 @@ __global__ __launch_bounds__(BS) void scan_kernel(ScanArgs a) {
       const float Rk = sqrtf(fmaxf(bound, 0.f)) * 1.001f + 1e-5f;
       const float Rs = a.do_safety ? (1.01f * (base_i + a.ttc_check * cgrid[6]) + 1e-4f) * 1.001f + 1e-5f : 0.f;
       float R = fmaxf(Rk, Rs);
-#ifdef MB_DIAG_SCAN_SHRINK
-      R *= 0.7f;      // negative check only (build_variant.sh): a too-small box must fail the oracle tests
-#endif
+      if constexpr ((MB_DIAG & 8) != 0) R *= 0.7f;   // negative check only: a too-small box must fail the oracle tests
       bool fin = R < INFINITY && me.x == me.x && me.y == me.y;
       if constexpr (D == 3) fin = fin && me.z == me.z;
       int c0[3] = {0, 0, 0}, c1[3] = {CG - 1, CG - 1, D == 3 ? CG - 1 : 0};
@@ -823,14 +802,14 @@ __global__ __launch_bounds__(BS) void scan_kernel(ScanArgs a) {
         }
         // (SCAN_THR_SKIP: no list of the wave changed in this chunk -> kth and thr are unchanged)
         if constexpr (ST) ph[11] += __any(ins) ? 1 : 0;
-        if (nk && (!SCAN_THR_SKIP || __any(ins))) {
+        if (nk && __any(ins)) {
           // the merged list's K-th distance <= min of the partial lists' K-th distances
           float kth = __uint_as_float((unsigned)(bk[K - 1] >> 32));
 #pragma unroll
           for (int o = APW; o < WAVE; o <<= 1) kth = fminf(kth, grp_xor(kth, o));
           thr = wave_max(act ? fminf(kth, bound) : -INFINITY);
         }
-        if (ns && (!SCAN_THR_SKIP || __any(dch))) {
+        if (ns && __any(dch)) {
           // the lane swaps must run on every lane: never inside a short-circuit '||'
           unsigned dg = danger ? 1u : 0u;
 #pragma unroll
@@ -943,18 +922,12 @@ __global__ __launch_bounds__(BS) void scan_kernel(ScanArgs a) {
   }
 }
 
-#ifndef SCAN_LPA
-#define SCAN_LPA 4      // lanes per agent (A/B at 1024 x 64: 2 -> 4 lanes 65.4 -> 61.5 us per step)
-#endif
+constexpr int SCAN_LPA = 4;      // lanes per agent (A/B at 1024 x 64: 2 -> 4 lanes 65.4 -> 61.5 us per step)
 
-#ifndef SCAN_BS_BIG
-#define SCAN_BS_BIG 1024  // block size above 512 nodes per env (4 lanes/agent: 512 -> 1024, 61.5 -> 60.5 us)
-#endif
+constexpr int SCAN_BS_BIG = 1024;  // block size above 512 nodes per env (4 lanes/agent: 512 -> 1024, 61.5 -> 60.5 us)
 // 3-D scenes: 512-thread blocks, two per CU, so one block's slow waves overlap the other block's
 // (with per-wave count atomics: see SCAN_WAVE_ATOMIC3)
-#ifndef SCAN_BS_BIG3
-#define SCAN_BS_BIG3 512
-#endif
+constexpr int SCAN_BS_BIG3 = 512;
 constexpr size_t SCAN_BOX_LDS = 160 * 1024 - 1024;   // LDS budget of the culling boxes (GLB 1)
 
 // The launch plan of one scan call (mb_scan_plan reports it, so the tests can assert which

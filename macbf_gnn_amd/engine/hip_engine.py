@@ -236,8 +236,8 @@ class HipEngine:
             # x3: the 16x16x32 backward (csrc/cbf16.h, two waves per SIMD) reads cbf_compact's
             # 16-byte records of the active evaluations; bf16 / fp16: the 32x32x16 kernel on the
             # index list (already two waves per SIMD there; 1635 vs 1791 us per call in bf16,
-            # profiles/r4_validate/). MACBF_CBF16=0/1 forces either (A/B runs)
-            self.cbf16 = bool(knobs.get_int("MACBF_CBF16", int(self.prec == "fp32")))
+            # profiles/r4_validate/)
+            self.cbf16 = self.prec == "fp32"
             self.act_list = torch.zeros(2 * E, dtype=i32, device=dev) if not self.cbf16 else None
             self.rec_list = torch.zeros(2 * E, 4, dtype=i32, device=dev) if self.cbf16 else None
             self.loss_red = torch.zeros(native.DH_PARTIAL, dtype=f32, device=dev)
@@ -350,7 +350,7 @@ class HipEngine:
                 fork_device_scope=1,
                 # early stop published by the controller kernels (no per-step queue marker / copy)
                 publish=knobs.get_int("MACBF_PUBLISH", 1),
-                poll_query_ms=knobs.get_int("MACBF_POLL_QUERY_MS", 100)))
+                poll_query_ms=100))
             if pw.ctrl_v.numel() < 352 or pw.ctrl_w.numel() < (c["f_node"] + 54) * 512 * (2 if pw.x3 else 1):
                 raise native.NativeError("packed controller weights too small")
             if overlap and (self.hbuf.numel() < 2 * T * BNK or self.src.numel() < 2 * T * BNK):

@@ -80,13 +80,11 @@ class Trainer:
             self.gscale_dev = torch.full((1,), float(cfg.loss_scale_init), dtype=torch.float32, device=self.device)
             self._good_dev = torch.zeros(1, dtype=torch.int32, device=self.device)
         self._next = None
-        from .. import knobs
-        # 0: sample inline; 1: side stream, launched as soon as enqueued (it then runs beside the
-        # previous iteration's CBF backward); 2: side stream gated on the end of the work enqueued
-        # so far (it runs beside the next rollout's first kernels)
-        self._prefetch_mode = knobs.get_int("MACBF_PREFETCH", 1) if cfg.prefetch_data else 0
+        # the next iteration's scenarios on a side stream, launched as soon as enqueued: it runs in
+        # the idle issue slots of the current iteration's CBF backward (inline sampling and a side
+        # stream gated on the enqueued work both measured slower, docs/PERF.md round 5)
         self._side = (torch.cuda.Stream(device=self.device)
-                      if (self.device.type == "cuda" and self._prefetch_mode) else None)
+                      if (self.device.type == "cuda" and cfg.prefetch_data) else None)
         if self.device.type == "cuda":
             from .hip_engine import HipEngine
             self._ok = torch.ones(1, dtype=torch.int32, device=self.device)
@@ -111,8 +109,6 @@ class Trainer:
     def _sample_async(self, it: int):
         """Launch the (parameter-independent) scenario sampler for iteration ``it`` on a side
         stream: it overlaps the current iteration's rollout instead of serialising with it."""
-        if self._prefetch_mode == 2:
-            self._side.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(self._side):
             data = self.sample(it)
             ev = torch.cuda.Event()

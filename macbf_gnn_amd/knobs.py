@@ -10,8 +10,6 @@ removed (their decision is the code's default, the measurement is in docs/PERF.m
 | MACBF_DP_FORCE_PG | 0 | parallel/dist.py | RCCL process group at world 1 (tests/test_gpu_dp.py) |
 | MACBF_EXT | -- | ops/native.py | load an alternative extension build (scripts/build_variant.sh A/B, no-barrier builds) |
 | MACBF_NATIVE_BPTT | 1 | engine/hip_engine.py | Python BPTT launch loop, so tests can spy on the calls |
-| MACBF_PREFETCH | 1 | engine/trainer.py | next-iteration scenario sampler: 0 inline, 1 side stream at once, 2 side stream after the enqueued work (A/B) |
-| MACBF_CBF16 | 1 (fp32), 0 (bf16 / fp16) | engine/hip_engine.py | 16x16x32 vs 32x32x16 CBF backward (A/B, scripts/gpu_r4_validate.sh) |
 | MACBF_EB16 | 1 (fp32), 0 (bf16 / fp16) | engine/hip_engine.py | 16x16x32 vs 32x32x16 edge backward (tests and A/B runs) |
 | MACBF_NODE16 | 1 | engine/hip_engine.py | 32x32x16 node backward (tests/test_gpu_node16.py; bf16 / fp16 A/B) |
 | MACBF_NODE_CHUNK | by size | ops/native.py | agents per node-backward chunk (tests force 128 at small sizes) |
@@ -20,7 +18,6 @@ removed (their decision is the code's default, the measurement is in docs/PERF.m
 | MACBF_EDGE_WG_PER_CU | 1 (x3) | ops/native.py | edge-backward workgroups per CU (tests) |
 | MACBF_BWD_GRAPH | 1 | engine/hip_engine.py | small scenes: post-rollout work replayed from per-T HIP graphs (0: eager, tests / A/B) |
 | MACBF_PUBLISH | 1 | engine/hip_engine.py | early stop through a queue marker instead of kernel publication (tests) |
-| MACBF_POLL_QUERY_MS | 100 | engine/hip_engine.py | early-stop wait: stream-error probe only after this many ms of waiting (0: every 4096 polls, the marker-per-wait A/B) |
 | MACBF_SELFCHECK | 1 | ops/selfcheck.py | skip the start-up self-check of the 16x16x32 kernels |
 | MACBF_ARCH | gfx950 | csrc/build.py | build target |
 """
