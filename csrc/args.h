@@ -342,11 +342,32 @@ struct AdamArgs {
   float lr;
 };
 
+// several parameter groups' Adam steps in one launch (block offsets filled by the launcher)
+constexpr int AM_GROUPS = 4;
+struct AdamMultiArgs { AdamArgs g[AM_GROUPS]; int blk0[AM_GROUPS]; int ngroups; };
+
+// several slab reductions in one launch (block offsets filled by the launcher)
+constexpr int RM_JOBS = 4;
+struct ReduceMultiArgs {
+  const float* partial[RM_JOBS]; float* out[RM_JOBS];
+  int rows[RM_JOBS], cols[RM_JOBS], accumulate[RM_JOBS], blk0[RM_JOBS];
+  int njobs;
+};
+
+// flat gradient assembly (+ optional finite check and statistics row)
+struct GradAssembleArgs {
+  const float* red; const int* ptr; const int* src; int n; float scale; const float* gscale; float* grad;
+  int* ok;                                            // null: no check (an all-reduce follows)
+  const float* sums; const float* counts; const float* local; float* row;   // row null: no stats
+};
+
 }  // namespace mb
 
 extern "C" {
 int mb_scan(const mb::ScanArgs* a, hipStream_t st);
 int mb_scan_plan(const mb::ScanArgs* a, long* out);
+int mb_reduce_multi(const mb::ReduceMultiArgs* a, hipStream_t st);
+int mb_adam_multi(const mb::AdamMultiArgs* a, hipStream_t st);
 int mb_cell_sort(const mb::CellSortArgs* a, hipStream_t st);
 int mb_scenario(const mb::ScenArgs* a, hipStream_t st);
 int mb_ctrl_fwd(const mb::CtrlArgs* a, int num_cu, hipStream_t st);
@@ -389,10 +410,9 @@ int mb_reduce_rows(const float* partial, int rows, int cols, float* out, int acc
 int mb_adam(const mb::AdamArgs* a, hipStream_t st);
 int mb_rollout_stats(const mb::RolloutStatsArgs* a, hipStream_t st);
 int mb_grad_check(const float* g, int n, int* ok, hipStream_t st);
-int mb_grad_assemble(const float* red, const int* ptr, const int* src, int n, float scale, const float* gscale, float* grad,
-                     hipStream_t st);
+int mb_grad_assemble(const mb::GradAssembleArgs* a, hipStream_t st);
 int mb_pack_gather(const float* src, int n, const int* idx16, int m16, unsigned short* out16, int f16,
-                   const int* idx32, int m32, float* out32, hipStream_t st);
+                   const int* idx32, int m32, float* out32, const mb::StepCommitArgs* commit, hipStream_t st);
 int mb_step_commit(const mb::StepCommitArgs* a, hipStream_t st);
 int mb_stats_pack(const float* sums, const float* counts, const float* local, float* row, hipStream_t st);
 int mb_probe_mfma16(const void* a, const void* b, float* d, hipStream_t st);

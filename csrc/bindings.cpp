@@ -215,25 +215,74 @@ static int reduce_rows(u64 partial, int rows, int cols, u64 out, int accumulate,
   return mb_reduce_rows(P<const float>(partial), rows, cols, P<float>(out), accumulate, ST(stream));
 }
 
-static int pack_gather(u64 src, int n, u64 idx16, int m16, u64 out16, int f16, u64 idx32, int m32, u64 out32,
-                       u64 stream) {
-  return mb_pack_gather(P<const float>(src), n, P<const int>(idx16), m16, P<unsigned short>(out16), f16,
-                        P<const int>(idx32), m32, P<float>(out32), ST(stream));
+static mb::StepCommitArgs commit_args(u64 ok, u64 steps, int mask, int ngroups, u64 skipped, u64 gscale, u64 good,
+                                      int growth, float max_scale, u64 stats_row) {
+  mb::StepCommitArgs a{};
+  a.ok = P<int>(ok); a.steps = P<int>(steps); a.mask = mask; a.ngroups = ngroups; a.skipped = P<int>(skipped);
+  a.gscale = P<float>(gscale); a.good = P<int>(good); a.growth = growth; a.max_scale = max_scale;
+  a.stats_row = P<float>(stats_row);
+  return a;
 }
 
-static int grad_assemble(u64 red, u64 ptr, u64 src, int n, float scale, u64 gscale, u64 grad, u64 stream) {
-  return mb_grad_assemble(P<const float>(red), P<const int>(ptr), P<const int>(src), n, scale, P<const float>(gscale),
-                          P<float>(grad), ST(stream));
+// commit: None, or the step_commit arguments (ok, steps, mask, ngroups, skipped, gscale, good, growth,
+// max_scale, stats_row) -- the optimizer step's commit runs inside the gather launch
+static int pack_gather(u64 src, int n, u64 idx16, int m16, u64 out16, int f16, u64 idx32, int m32, u64 out32,
+                       py::object commit, u64 stream) {
+  mb::StepCommitArgs c{};
+  const bool has = !commit.is_none();
+  if (has) {
+    const py::tuple t = commit.cast<py::tuple>();
+    c = commit_args(t[0].cast<u64>(), t[1].cast<u64>(), t[2].cast<int>(), t[3].cast<int>(), t[4].cast<u64>(),
+                    t[5].cast<u64>(), t[6].cast<u64>(), t[7].cast<int>(), t[8].cast<float>(), t[9].cast<u64>());
+  }
+  return mb_pack_gather(P<const float>(src), n, P<const int>(idx16), m16, P<unsigned short>(out16), f16,
+                        P<const int>(idx32), m32, P<float>(out32), has ? &c : nullptr, ST(stream));
+}
+
+static int grad_assemble(u64 red, u64 ptr, u64 src, int n, float scale, u64 gscale, u64 grad, u64 ok, u64 sums,
+                         u64 counts, u64 local, u64 row, u64 stream) {
+  mb::GradAssembleArgs a{};
+  a.red = P<const float>(red); a.ptr = P<const int>(ptr); a.src = P<const int>(src); a.n = n; a.scale = scale;
+  a.gscale = P<const float>(gscale); a.grad = P<float>(grad); a.ok = P<int>(ok);
+  a.sums = P<const float>(sums); a.counts = P<const float>(counts); a.local = P<const float>(local); a.row = P<float>(row);
+  return mb_grad_assemble(&a, ST(stream));
+}
+
+// jobs: [(partial, rows, cols, out, accumulate)] (at most mb::RM_JOBS), one launch
+static int reduce_multi(py::list jobs, u64 stream) {
+  mb::ReduceMultiArgs a{};
+  a.njobs = (int)py::len(jobs);
+  if (a.njobs < 1 || a.njobs > mb::RM_JOBS) return -1;
+  for (int j = 0; j < a.njobs; ++j) {
+    const py::tuple t = jobs[j].cast<py::tuple>();
+    a.partial[j] = P<const float>(t[0].cast<u64>()); a.rows[j] = t[1].cast<int>(); a.cols[j] = t[2].cast<int>();
+    a.out[j] = P<float>(t[3].cast<u64>()); a.accumulate[j] = t[4].cast<int>();
+  }
+  return mb_reduce_multi(&a, ST(stream));
+}
+
+// groups: [(lo, hi, step_ptr)] (at most mb::AM_GROUPS); the rest as adam()
+static int adam_multi(u64 param, u64 grad, u64 m, u64 v, py::list groups, float b1, float b2, float eps, float wd,
+                      u64 ok, float lr, u64 stream) {
+  mb::AdamMultiArgs a{};
+  a.ngroups = (int)py::len(groups);
+  if (a.ngroups < 1 || a.ngroups > mb::AM_GROUPS) return -1;
+  for (int g = 0; g < a.ngroups; ++g) {
+    const py::tuple t = groups[g].cast<py::tuple>();
+    mb::AdamArgs& x = a.g[g];
+    x.param = P<float>(param); x.grad = P<const float>(grad); x.m = P<float>(m); x.v = P<float>(v);
+    x.lo = t[0].cast<int>(); x.hi = t[1].cast<int>(); x.step = P<const int>(t[2].cast<u64>());
+    x.b1 = b1; x.b2 = b2; x.eps = eps; x.wd = wd; x.ok = P<const int>(ok); x.lr = lr;
+    if (!x.step) return -2;          // device step counters only (bias corrections on the device)
+  }
+  return mb_adam_multi(&a, ST(stream));
 }
 
 static int grad_check(u64 g, int n, u64 ok, u64 stream) { return mb_grad_check(P<const float>(g), n, P<int>(ok), ST(stream)); }
 
 static int step_commit(u64 ok, u64 steps, int mask, int ngroups, u64 skipped, u64 gscale, u64 good, int growth,
                        float max_scale, u64 stats_row, u64 stream) {
-  mb::StepCommitArgs a{};
-  a.ok = P<int>(ok); a.steps = P<int>(steps); a.mask = mask; a.ngroups = ngroups; a.skipped = P<int>(skipped);
-  a.gscale = P<float>(gscale); a.good = P<int>(good); a.growth = growth; a.max_scale = max_scale;
-  a.stats_row = P<float>(stats_row);
+  const mb::StepCommitArgs a = commit_args(ok, steps, mask, ngroups, skipped, gscale, good, growth, max_scale, stats_row);
   return mb_step_commit(&a, ST(stream));
 }
 
@@ -397,6 +446,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("rollout_stats", &rollout_stats);
   m.def("grad_check", &grad_check);
   m.def("grad_assemble", &grad_assemble);
+  m.def("reduce_multi", &reduce_multi);
+  m.def("adam_multi", &adam_multi);
   m.def("pack_gather", &pack_gather);
   m.def("step_commit", &step_commit);
   m.def("stats_pack", &stats_pack);

@@ -15,7 +15,6 @@
 // pre-packed 1 KiB fragments (ops/layout.py); all intermediate activations stay in VGPRs.
 #pragma clang fp contract(off)
 #include <climits>
-#include <cstdlib>
 #include "common.h"
 #include "args.h"
 #include "state.h"
@@ -789,23 +788,17 @@ extern "C" int MB_SYM(ctrl_fwd)(const mb::CtrlArgs* a, int num_cu, hipStream_t s
   // x3: one fused launch (edge + node phase per group, 145 KB of weights: one workgroup per CU)
   if (X3) {
     const size_t ldf = (size_t)CTRL_FWD_FRAGS * FRAG_SZ + CTRL_VEC * 4;
-    // small grids (strong-scaling slices): 4-wave workgroups when the 8-wave grid would leave at
-    // least half of the CUs without a workgroup -- twice the workgroups, one wave per SIMD
-    static const int wv_env = [] { const char* e = getenv("MACBF_CTRL_WAVES"); return e ? atoi(e) : 0; }();
-    const bool w4 = !a->stamps && (wv_env == 4 || (wv_env == 0 && num_cu > 0 && 2 * blocks <= num_cu));
-    const int wv = w4 ? 4 : CTRL_WAVES;
-    const int nb = w4 ? (groups + 3) / 4 < maxb ? (groups + 3) / 4 : maxb : blocks;
     auto go = [&](auto kern) {
       (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ldf);
-      hipLaunchKernelGGL(kern, dim3(nb), dim3(wv * 64), ldf, st, b);
+      hipLaunchKernelGGL(kern, dim3(blocks), dim3(CTRL_WAVES * 64), ldf, st, b);
     };
+    // (4-wave workgroups for the slices' small grids -- one wave per SIMD on twice the CUs --
+    // measured no faster: 8-env slice 2.825-2.833 vs 2.797-2.820 ms, profiles/r6b/)
     if (a->dim == 3) {
       if (a->stamps) go(ctrl_fwd_kernel<CTRL_WAVES, 3, true, true>);
-      else if (w4) go(ctrl_fwd_kernel<4, 3, true>);
       else go(ctrl_fwd_kernel<CTRL_WAVES, 3, true>);
     } else {
       if (a->stamps) go(ctrl_fwd_kernel<CTRL_WAVES, 2, true, true>);
-      else if (w4) go(ctrl_fwd_kernel<4, 2, true>);
       else go(ctrl_fwd_kernel<CTRL_WAVES, 2, true>);
     }
     return (int)hipGetLastError();
@@ -1377,6 +1370,9 @@ constexpr int NB_PREFETCH = 1;
 constexpr int NC_SW = 296;                           // 148 dwords: row reads spread over the banks
 static_assert(NC_SW * 32 <= NB_PL, "cooperative region must fit the stage plane");
 
+#ifndef NB_SLAB_EARLY
+#define NB_SLAB_EARLY 0
+#endif
 template <int D>
 DEV void node_bwd_coop(const CtrlNodeBwdArgs& a, unsigned char* smem, long c0, long cstride, float* P) {
   constexpr int RM = (X3 ? 2 : 1) * NODE_RM_ELEMS;
@@ -1418,6 +1414,32 @@ DEV void node_bwd_coop(const CtrlNodeBwdArgs& a, unsigned char* smem, long c0, l
   const int n1 = (wave < 2) ? 3 : 2;
   // B fragment (natural k) of image columns c0 + 16kk.. for this lane's agent row
   auto img_fr = [&](int col0, int kk) { return row_fr(stg + r * SW + col0 + 16 * kk + 8 * h, PLN); };
+  // the slab's old values (read-modify-write at the end), loaded by slab_loads()
+  f32x16 o1[3], o2[2], o3[2], o4 = zero16();
+  float ob2[2] = {0.f, 0.f}, ob3[2] = {0.f, 0.f}, ob4 = 0.f;
+  o1[0] = o1[1] = o1[2] = o2[0] = o2[1] = o3[0] = o3[1] = zero16();
+  bool loaded = false;
+  auto slab_loads = [&]() {
+    loaded = true;
+    if (a.init) return;
+#pragma unroll
+    for (int u = 0; u < 3; ++u) {
+      const int t = wave + 4 * u;
+      if (u < n1) load_tile(o1[u], P + NP_W1, 160, t / 5, t % 5, lane);
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int t = wave + 4 * u;
+      load_tile(o2[u], P + NP_W2, 64, t / 2, t % 2, lane);
+      load_tile(o3[u], P + NP_W3, 128, t / 4, t % 4, lane);
+      ob2[u] = P[NP_B2 + 32 * (t / 2) + r];
+      ob3[u] = P[NP_B3 + 32 * (t / 4) + r];
+    }
+    if (wave < 2) {
+      load_tile(o4, P + NP_W4, 64, 0, wave, lane);
+      ob4 = P[NP_B4 + r];
+    }
+  };
 
   for (long chunk = c0; chunk < nchunks; chunk += cstride) {
     stamp(15);
@@ -1596,6 +1618,9 @@ DEV void node_bwd_coop(const CtrlNodeBwdArgs& a, unsigned char* smem, long c0, l
     }
     __syncthreads();                                   // S2 images and d2 read by every wave
     stamp(9);
+    // NB_SLAB_EARLY: the workgroup's last chunk requests the slab's old values here, so their
+    // latency hides behind the S1 stage and the dP tiles instead of opening the tail
+    if (NB_SLAB_EARLY && chunk + cstride >= nchunks) slab_loads();
     // ---- S1 images: d1 (cols 0..63), [P | s | 0] (cols 64..223: pooled 128, state fragment 16, zeros 16)
     if (wave < 2) store_pk(stg, SW, r, 32 * wave, d1b, h, PLN);
 #pragma unroll
@@ -1663,28 +1688,7 @@ DEV void node_bwd_coop(const CtrlNodeBwdArgs& a, unsigned char* smem, long c0, l
   }
   stamp(13);
   // ---- slab += this workgroup's partial (fixed tile owners: deterministic); loads first
-  f32x16 o1[3], o2[2], o3[2], o4 = zero16();
-  float ob2[2] = {0.f, 0.f}, ob3[2] = {0.f, 0.f}, ob4 = 0.f;
-  o1[0] = o1[1] = o1[2] = o2[0] = o2[1] = o3[0] = o3[1] = zero16();
-  if (!a.init) {
-#pragma unroll
-    for (int u = 0; u < 3; ++u) {
-      const int t = wave + 4 * u;
-      if (u < n1) load_tile(o1[u], P + NP_W1, 160, t / 5, t % 5, lane);
-    }
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int t = wave + 4 * u;
-      load_tile(o2[u], P + NP_W2, 64, t / 2, t % 2, lane);
-      load_tile(o3[u], P + NP_W3, 128, t / 4, t % 4, lane);
-      ob2[u] = P[NP_B2 + 32 * (t / 2) + r];
-      ob3[u] = P[NP_B3 + 32 * (t / 4) + r];
-    }
-    if (wave < 2) {
-      load_tile(o4, P + NP_W4, 64, 0, wave, lane);
-      ob4 = P[NP_B4 + r];
-    }
-  }
+  if (!loaded) slab_loads();
 #pragma unroll
   for (int u = 0; u < 3; ++u) {
     const int t = wave + 4 * u;

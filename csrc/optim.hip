@@ -12,18 +12,25 @@ namespace mb {
 // the 16 slice sums are added in slice order through LDS. ~300 workgroups for the CBF slab
 // instead of 19 with one serial thread per column.
 constexpr int RR_COLS = 16, RR_SLICES = 16;
-__global__ __launch_bounds__(RR_COLS * RR_SLICES) void reduce_rows_kernel(const float* partial, int rows, int cols,
-                                                                          float* out, int accumulate) {
+DEV void reduce_rows_block(const float* partial, int rows, int cols, float* out, int accumulate, int bx) {
   __shared__ float4 red[RR_SLICES][RR_COLS];
   const int cx = threadIdx.x % RR_COLS, sy = threadIdx.x / RR_COLS;
-  const int c4 = blockIdx.x * RR_COLS + cx;
+  const int c4 = bx * RR_COLS + cx;
   const bool ok = c4 * 4 < cols;
   float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
   if (ok) {
-#pragma unroll 4
-    for (int r = sy; r < rows; r += RR_SLICES) {
-      const float4 v = *reinterpret_cast<const float4*>(partial + (long)r * cols + c4 * 4);
-      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    // 8 rows' loads in flight before their (in-order) adds: the slabs come from HBM / MALL, and
+    // one dependent round trip per 4 rows made the reduction latency-bound (~1 TB/s)
+    for (int r = sy; r < rows; r += 8 * RR_SLICES) {
+      float4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int rr = min(r + u * RR_SLICES, rows - 1);
+        v[u] = *reinterpret_cast<const float4*>(partial + (long)rr * cols + c4 * 4);
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (r + u * RR_SLICES < rows) { s.x += v[u].x; s.y += v[u].y; s.z += v[u].z; s.w += v[u].w; }
     }
   }
   red[sy][cx] = s;
@@ -43,8 +50,22 @@ __global__ __launch_bounds__(RR_COLS * RR_SLICES) void reduce_rows_kernel(const 
   }
 }
 
-__global__ __launch_bounds__(256) void adam_kernel(AdamArgs a) {
-  const int i = a.lo + blockIdx.x * blockDim.x + threadIdx.x;
+__global__ __launch_bounds__(RR_COLS * RR_SLICES) void reduce_rows_kernel(const float* partial, int rows, int cols,
+                                                                          float* out, int accumulate) {
+  reduce_rows_block(partial, rows, cols, out, accumulate, blockIdx.x);
+}
+
+// Several independent slab reductions in ONE launch (the CBF, node and edge weight-gradient slabs
+// and the loss partials after the backward): job j owns blocks [blk0[j], blk0[j + 1]), each block
+// the same fixed-order column-group reduction as reduce_rows_kernel (bitwise the same sums)
+__global__ __launch_bounds__(RR_COLS * RR_SLICES) void reduce_multi_kernel(ReduceMultiArgs a) {
+  int j = 0;
+  while (j + 1 < a.njobs && (int)blockIdx.x >= a.blk0[j + 1]) ++j;
+  reduce_rows_block(a.partial[j], a.rows[j], a.cols[j], a.out[j], a.accumulate[j], (int)blockIdx.x - a.blk0[j]);
+}
+
+DEV void adam_block(const AdamArgs& a, int bx) {
+  const int i = a.lo + bx * blockDim.x + threadIdx.x;
   if (i >= a.hi) return;
   // device-side failure guard: a non-finite reduced gradient skips the whole step (the flag is
   // the same on every rank after the all-reduce), with no host round trip
@@ -67,14 +88,29 @@ __global__ __launch_bounds__(256) void adam_kernel(AdamArgs a) {
   a.param[i] = p - step_size * (m / denom);
 }
 
+__global__ __launch_bounds__(256) void adam_kernel(AdamArgs a) { adam_block(a, blockIdx.x); }
+
+// The Adam steps of several parameter groups (the two reference optimizers, train.py:36-37) in
+// ONE launch: group g owns blocks [blk0[g], blk0[g + 1]); same per-element arithmetic
+__global__ __launch_bounds__(256) void adam_multi_kernel(AdamMultiArgs a) {
+  int g = 0;
+  while (g + 1 < a.ngroups && (int)blockIdx.x >= a.blk0[g + 1]) ++g;
+  adam_block(a.g[g], (int)blockIdx.x - a.blk0[g]);
+}
+
 // Weight repacking after an optimizer step: every MFMA fragment / row-major image / side vector
 // of both networks is a gather of the flat fp32 master parameters (index maps from
 // ops/layout.py; index n = constant 0, n + 1 = constant 1), in ONE launch: 16-bit outputs
 // (bf16 RNE or fp16) then fp32 outputs.
+DEV void step_commit_body(const StepCommitArgs& a);
+// commit (optional): the optimizer step's commit (step_commit_kernel's work) by one thread -- the
+// gather runs after the Adam launch, whose reads of the step counters and the guard flag are then
+// complete (kernel boundary): one launch fewer per iteration
 __global__ __launch_bounds__(256) void pack_gather_kernel(const float* src, int n, const int* idx16, int m16,
                                                           unsigned short* out16, int f16, const int* idx32, int m32,
-                                                          float* out32) {
+                                                          float* out32, StepCommitArgs commit) {
   const int i = blockIdx.x * 256 + threadIdx.x;
+  if (commit.ok && i == 0) step_commit_body(commit);
   if (i < m16) {
     // bit 30 of an index selects the bf16 residual v - bf16(v) (the lo plane of the x3 split)
     const int k0 = idx16[i];
@@ -98,14 +134,27 @@ __global__ __launch_bounds__(256) void pack_gather_kernel(const float* src, int 
 
 // Flat gradient assembly: grad[p] = scale * sum of the reduced slab entries that map to
 // parameter p (CSR by p, fixed order: deterministic, no atomics, no zero-fill)
-__global__ __launch_bounds__(256) void grad_assemble_kernel(const float* red, const int* ptr, const int* src, int n,
-                                                            float scale, const float* gscale, float* grad) {
+// Optional in the same launch (single-process runs: no all-reduce follows): ok <- 0 if any assembled
+// element is not finite (grad_check_kernel's test), and one extra block writes the iteration's
+// statistics row (stats_pack_kernel's work) -- two launches fewer per iteration
+DEV void stats_pack_body(const float* sums, const float* counts, const float* local, float* row, int t);
+__global__ __launch_bounds__(256) void grad_assemble_kernel(GradAssembleArgs a) {
   const int p = blockIdx.x * 256 + threadIdx.x;
-  if (p >= n) return;
-  if (gscale) scale /= *gscale;     // fp16: unscale by the device loss scale
-  float t = 0.f;
-  for (int q = ptr[p]; q < ptr[p + 1]; ++q) t += red[src[q]];
-  grad[p] = t * scale;
+  if (a.row && (int)blockIdx.x == (a.n + 255) / 256) {
+    stats_pack_body(a.sums, a.counts, a.local, a.row, threadIdx.x);
+    return;
+  }
+  float scale = a.scale;
+  if (a.gscale) scale /= *a.gscale;     // fp16: unscale by the device loss scale
+  bool bad = false;
+  if (p < a.n) {
+    float t = 0.f;
+    for (int q = a.ptr[p]; q < a.ptr[p + 1]; ++q) t += a.red[a.src[q]];
+    const float v = t * scale;
+    a.grad[p] = v;
+    bad = !isfinite(v);
+  }
+  if (a.ok && __any(bad) && (threadIdx.x % WAVE) == 0) *a.ok = 0;
 }
 
 // ok = 0 if any gradient element is not finite (ok is 1 between steps: step_commit resets it)
@@ -117,8 +166,7 @@ __global__ __launch_bounds__(256) void grad_check_kernel(const float* g, int n, 
 
 // after the Adam launches of one iteration (see StepCommitArgs): no host round trip, no
 // torch glue kernels between the optimizer and the next iteration
-__global__ void step_commit_kernel(StepCommitArgs a) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+DEV void step_commit_body(const StepCommitArgs& a) {
   const int ok = *a.ok;
   if (ok) {
     for (int g = 0; g < a.ngroups; ++g)
@@ -149,10 +197,17 @@ __global__ void step_commit_kernel(StepCommitArgs a) {
   *a.ok = 1;
 }
 
+__global__ void step_commit_kernel(StepCommitArgs a) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  step_commit_body(a);
+}
+
 // One iteration's statistics row (utils.metrics.StepStats): [10 loss sums | counts 3 | local 3 |
 // skipped | loss scale] -- written into a ring of rows instead of torch.cat + clone
 __global__ void stats_pack_kernel(const float* sums, const float* counts, const float* local, float* row) {
-  const int t = threadIdx.x;
+  stats_pack_body(sums, counts, local, row, threadIdx.x);
+}
+DEV void stats_pack_body(const float* sums, const float* counts, const float* local, float* row, int t) {
   if (t < 10) row[t] = sums[t];
   else if (t < 13) row[t] = counts[t - 10];
   else if (t < 16) row[t] = local[t - 13];
@@ -220,19 +275,50 @@ __global__ __launch_bounds__(RS_BLOCK) void rollout_stats_kernel(RolloutStatsArg
 }  // namespace mb
 
 extern "C" int mb_pack_gather(const float* src, int n, const int* idx16, int m16, unsigned short* out16, int f16,
-                              const int* idx32, int m32, float* out32, hipStream_t st) {
+                              const int* idx32, int m32, float* out32, const mb::StepCommitArgs* commit,
+                              hipStream_t st) {
   using namespace mb;
   const int tot = m16 + m32;
-  hipLaunchKernelGGL(pack_gather_kernel, dim3((tot + 255) / 256), dim3(256), 0, st, src, n, idx16, m16, out16, f16,
-                     idx32, m32, out32);
+  StepCommitArgs c{};
+  if (commit) c = *commit;
+  hipLaunchKernelGGL(pack_gather_kernel, dim3(tot > 0 ? (tot + 255) / 256 : 1), dim3(256), 0, st, src, n, idx16, m16,
+                     out16, f16, idx32, m32, out32, c);
   return (int)hipGetLastError();
 }
 
-extern "C" int mb_grad_assemble(const float* red, const int* ptr, const int* src, int n, float scale,
-                                const float* gscale, float* grad, hipStream_t st) {
+extern "C" int mb_grad_assemble(const mb::GradAssembleArgs* a, hipStream_t st) {
   using namespace mb;
-  hipLaunchKernelGGL(grad_assemble_kernel, dim3((n + 255) / 256), dim3(256), 0, st, red, ptr, src, n, scale, gscale,
-                     grad);
+  const int blocks = (a->n + 255) / 256 + (a->row ? 1 : 0);
+  hipLaunchKernelGGL(grad_assemble_kernel, dim3(blocks > 0 ? blocks : 1), dim3(256), 0, st, *a);
+  return (int)hipGetLastError();
+}
+
+extern "C" int mb_reduce_multi(const mb::ReduceMultiArgs* a, hipStream_t st) {
+  using namespace mb;
+  if (a->njobs < 1 || a->njobs > RM_JOBS) return -1;
+  ReduceMultiArgs b = *a;
+  int blk = 0;
+  for (int j = 0; j < b.njobs; ++j) {
+    if (b.cols[j] % 4) return -1;
+    b.blk0[j] = blk;
+    blk += (b.cols[j] / 4 + RR_COLS - 1) / RR_COLS;
+  }
+  hipLaunchKernelGGL(reduce_multi_kernel, dim3(blk), dim3(RR_COLS * RR_SLICES), 0, st, b);
+  return (int)hipGetLastError();
+}
+
+extern "C" int mb_adam_multi(const mb::AdamMultiArgs* a, hipStream_t st) {
+  using namespace mb;
+  if (a->ngroups < 1 || a->ngroups > AM_GROUPS) return -1;
+  AdamMultiArgs b = *a;
+  int blk = 0;
+  for (int g = 0; g < b.ngroups; ++g) {
+    b.blk0[g] = blk;
+    const int n = b.g[g].hi - b.g[g].lo;
+    blk += n > 0 ? (n + 255) / 256 : 0;
+  }
+  if (blk == 0) return 0;
+  hipLaunchKernelGGL(adam_multi_kernel, dim3(blk), dim3(256), 0, st, b);
   return (int)hipGetLastError();
 }
 

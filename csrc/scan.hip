@@ -768,8 +768,10 @@ __global__ __launch_bounds__(BS) void scan_kernel(ScanArgs a) {
         if constexpr (ST) ph[9] += 1;
         if (!nk && !ns) continue;
         if constexpr (ST) { ph[10] += 1; ph[12] += nk ? 1 : 0; ph[13] += nk ? 0 : 1; }
-        constexpr int HU = SCH / LPA;
-        const int hoff = HU * h;
+        // LPA <= 8: 8 / LPA candidates per lane; LPA = 16: one per lane, lanes h >= 8 idle
+        constexpr int HU = SCH / LPA > 0 ? SCH / LPA : 1;
+        const bool hact = LPA <= SCH || h < SCH;
+        const int hoff = hact ? HU * h : 0;
         float4 c[HU];
 #pragma unroll
         for (int u = 0; u < HU; ++u) c[u] = tp[cur * SCH + hoff + u];
@@ -783,11 +785,11 @@ __global__ __launch_bounds__(BS) void scan_kernel(ScanArgs a) {
           if constexpr (D == 3) dp[2] = me.z - c[u].z;
           const float d2 = sqsum<D>(dp);
           const uint64_t key = knn_key(d2, (unsigned)j);
-          if (nk && act && d2 <= bound && key < bk[K - 1]) {
+          if (hact && nk && act && d2 <= bound && key < bk[K - 1]) {
             topk_insert<K>(bk, key);
             ins = true;
           }
-          if (ns && act && !danger) {
+          if (hact && ns && act && !danger) {
             const float4 cv = tv[cur * SCH + hoff + u];
             const float lim = 1.01f * (base_i + a.ttc_check * cv.w) + 1e-4f;
             if (d2 < lim * lim && j != i) {
@@ -1026,7 +1028,7 @@ static bool scan_small_grid(const ScanArgs& a) {
 // chunk work -> twice the blocks. Same keys and tie order: the merged lists are identical for
 // any LPA (tests/test_gpu_forward.py forces lanes = 4 / 8 through ScanArgs.lanes).
 static bool scan_lpa8(const ScanArgs& a) {
-  if (a.lanes == 4 || a.lanes == 8) return a.lanes == 8;
+  if (a.lanes == 4 || a.lanes == 8 || a.lanes == 16) return a.lanes == 8;
   constexpr int AG = 256 / SCAN_LPA;
   return SCAN_LPA < 8 && (long)a.B * ((a.Nn + AG - 1) / AG) < scan_num_cu();
 }
@@ -1042,9 +1044,21 @@ static bool scan_boxes_global(const ScanArgs& a) {
 // (3-D scenes at 8 lanes per agent -- 8 agents per wave, a smaller wave box in x, y -- measured
 // slower in round 5: config #5 fp16 9.93 vs 9.50-9.52 ms, profiles/r5_b6/)
 
+// Strong-scaling slices (8 envs x 1024 agents: the 8-lane grid has no more blocks than CUs) whose
+// calls search the cell grid: 16 lanes per agent in 512-thread blocks -- the same blocks, twice
+// the threads for the per-block env staging and cell-grid build, half the candidates per lane
+// (ScanArgs.lanes = 16 forces it; MACBF_SCAN_L16 = 0 / 1 for the A/B)
+static bool scan_lpa16(const ScanArgs& a) {
+  if (a.lanes) return a.lanes == 16;
+  static const int env = [] { const char* e = getenv("MACBF_SCAN_L16"); return e ? atoi(e) : 0; }();
+  if (!env) return false;
+  return a.prev_idx && a.do_knn && a.Nn <= SCAN_MAXN && (long)a.B * ((a.Nn + 31) / 32) <= scan_num_cu();
+}
+
 template <int K, int D>
 static void launch_kd(const ScanArgs& a, hipStream_t st, ScanPlan* plan) {
   if (scan_boxes_global(a)) launch_kdb<K, D, SCAN_BS_BIG>(a, st, plan);
+  else if (scan_lpa16(a)) launch_kdb<K, D, 512, 16>(a, st, plan);
   else if (scan_lpa8(a)) launch_kdb<K, D, 256, 8>(a, st, plan);
   else if (a.Nn > 512 && !scan_small_grid<D>(a)) launch_kdb<K, D, D == 3 ? SCAN_BS_BIG3 : SCAN_BS_BIG>(a, st, plan);
   else launch_kdb<K, D, 256>(a, st, plan);

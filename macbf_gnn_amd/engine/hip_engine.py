@@ -144,6 +144,9 @@ class HipEngine:
         self._bwd_graphs = {}          # (T, grad scale) -> CUDAGraph of _counts + _backward
         self._bwd_pool = None
         self._bwd_capture = False
+        # int32 guard flag the gradient-assembly launch clears on a non-finite element (set by the
+        # trainer for single-process runs; with DP the check follows the all-reduce)
+        self.check_ok = None
         # the 16x16x32 backward kernels this engine runs, once before training (ops/selfcheck.py: a
         # miscompiled schedule stops here instead of corrupting gradients): CBF / edge against their
         # float64 oracles (x3), the node kernel against the 32x32x16 one (every precision)
@@ -260,8 +263,8 @@ class HipEngine:
         self._part_cbf = {}
         self._part_cbf_nb = {}
 
-    def after_update(self):
-        self.pw.update()
+    def after_update(self, commit=None):
+        self.pw.update(commit=commit)
 
     # ------------------------------------------------------------------ rollout
     def _noise_args(self):
@@ -634,7 +637,7 @@ class HipEngine:
                 native.cbf_bwd(S, idx, dh.view(2, T, B, N, K), pw.cbf_w, pw.cbf_off["w1f"], pw.cbf_rm, pw.cbf_v,
                                passes=2, dE=dE, partial=part_cbf, num_blocks=nbb, idx1=idx if self.reuse else idx1,
                                src=src, nev=nev, act=act, nact=nact, prec=self.prec)
-            native.reduce_rows(self.loss_part, self.loss_red)
+            # (the loss partials are reduced with the weight-gradient slabs after the BPTT)
         else:
             # ---- CBF: h, h', hinge losses, upstream grads and the full backward in ONE kernel
             self._counts_ready(counts_work)
@@ -717,21 +720,27 @@ class HipEngine:
                                  init=True)
             self._nb_parts = (pn, pe)
         tm.mark("bptt")
-        # ---- weight-gradient slabs -> flat grad
+        # ---- weight-gradient slabs (+ the loss partials) -> flat grad, one reduction launch
         pnode, pedge = (self.part_node[: slab_rows[0]], self.part_edge[: slab_rows[1]]) if self.bptt else self._nb_parts
-        for part, red in (((part_cbf, self.red_cbf),) if not split else ()) + ((pnode, self.red_node), (pedge, self.red_edge)):
-            native.reduce_rows(part, red)
+        jobs = ([(part_cbf, self.red_cbf, False)] if not split else []) + [(pnode, self.red_node, False),
+                                                                           (pedge, self.red_edge, False)]
+        if self.dedup:
+            jobs.append((self.loss_part, self.loss_red, False))
+        native.reduce_multi(jobs)
+        # ---- stats: one raw device row per iteration (no per-statistic kernels), derived lazily on
+        #      read; written by the assembly launch, which (single process) also runs the finite check
+        sums = self.loss_red[:10] if self.dedup else self.red_cbf[native.CBF_P_LOSS: native.CBF_P_LOSS + 10]
+        row = self.raw_stats if (self.graph_mode or self._bwd_capture) else self._next_row()
+        stats = (sums, self.counts, self.local, row)
+        ok = None if split else self.check_ok
         if split:
             lo, hi = self.grad_ranges["controller"]
             native.grad_assemble(self.red_all, self.g_ptr[lo: hi + 1], self.g_src, tr.fp.grad[lo:hi], scale=1.0 / gs,
-                                 gscale=gsd)
+                                 gscale=gsd, stats=stats)
         else:
-            native.grad_assemble(self.red_all, self.g_ptr, self.g_src, tr.fp.grad, scale=1.0 / gs, gscale=gsd)
+            native.grad_assemble(self.red_all, self.g_ptr, self.g_src, tr.fp.grad, scale=1.0 / gs, gscale=gsd, ok=ok,
+                                 stats=stats)
         tm.mark("grad_reduce")
-        # ---- stats: one raw device row per iteration (no per-statistic kernels), derived lazily on read
-        sums = self.loss_red[:10] if self.dedup else self.red_cbf[native.CBF_P_LOSS: native.CBF_P_LOSS + 10]
-        row = self.raw_stats if (self.graph_mode or self._bwd_capture) else self._next_row()
-        native.stats_pack(sums, self.counts, self.local, row)
         Tv = T if not self.graph_mode else (valid != 0).any(1).sum()
         return row, Tv
 

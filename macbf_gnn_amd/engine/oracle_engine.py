@@ -18,8 +18,10 @@ class OracleEngine:
     def __init__(self, trainer):
         self.tr = trainer
 
-    def after_update(self):
-        pass
+    def after_update(self, commit=None):
+        if commit is not None:          # a trainer on a HIP device: the deferred optimizer commit
+            from ..ops import native
+            native.step_commit_raw(commit)
 
     def step(self, s0, g, obs=None, forced=None):
         """``forced``: replay a trajectory (``oracle.rollout``), e.g. ``HipEngine.trajectory()``."""

@@ -89,6 +89,8 @@ class Trainer:
             from .hip_engine import HipEngine
             self._ok = torch.ones(1, dtype=torch.int32, device=self.device)
             self.engine = HipEngine(self)
+            if (cfg.nan_guard or self.fp16) and not self.dp.enabled:
+                self.engine.check_ok = self._ok      # the finite check runs in the assembly launch
         else:
             from .oracle_engine import OracleEngine
             self.engine = OracleEngine(self)
@@ -177,16 +179,18 @@ class Trainer:
             # this step's statistics row and re-arms the flag -- no host round trip, no torch glue
             from ..ops import native
             guard = self.cfg.nan_guard or self.fp16
-            if guard:
-                native.grad_check(self.fp.grad, self._ok)
+            if guard and getattr(self.engine, "check_ok", None) is None:
+                native.grad_check(self.fp.grad, self._ok)        # after the all-reduce (DP)
             row = getattr(stats, "raw", None)
             row = row if (row is not None and row.numel() >= 18) else None
             # without a stats row the skip flag is read before the commit kernel re-arms it
             ok_snap = self._ok.clone() if (row is None and guard) else None
-            self.opt.step(self.groups_to_step(), ok=self._ok if guard else None, gscale=self.gscale_dev,
-                          good=self._good_dev if self.fp16 else None, growth=self.cfg.loss_scale_growth,
-                          stats_row=row)
-            self.engine.after_update()
+            # Adam of every group in one launch; its commit (step counts, skip count, loss scale,
+            # flag re-arm) runs inside the weight repack launch that follows
+            commit = self.opt.step(self.groups_to_step(), ok=self._ok if guard else None, gscale=self.gscale_dev,
+                                   good=self._good_dev if self.fp16 else None, growth=self.cfg.loss_scale_growth,
+                                   stats_row=row, defer_commit=True)
+            self.engine.after_update(commit=commit)
             if row is None:
                 stats["skipped"] = 1 - ok_snap[0] if ok_snap is not None else 0
             elif self.fp16:

@@ -228,10 +228,10 @@ def scan(S, idx, dang, cnt, safe, *, K, do_knn=True, do_safety=True, perm=None, 
     agents; their current distances bound the K-th distance (tighter culling, same result).
     sort=False reuses the curve order of the previous call on the same perm buffer (the agents
     moved one step: slightly looser culling, identical results). lanes: lanes per agent (0: by
-    grid size -- 8 when 4-lane 256-thread blocks leave CUs idle; 4 or 8 forces the layout; the
-    lists, bits and counts are identical for either)."""
-    if lanes not in (0, 4, 8):
-        raise NativeError("lanes must be 0 (auto), 4 or 8")
+    grid size -- 8 when 4-lane 256-thread blocks leave CUs idle; 4, 8 or 16 (512-thread blocks)
+    forces the layout; the lists, bits and counts are identical for any)."""
+    if lanes not in (0, 4, 8, 16):
+        raise NativeError("lanes must be 0 (auto), 4, 8 or 16")
     B, Nn = S.shape[0], S.shape[1]
     if stamps is not None:   # diagnostics (scripts/stamps_scan.py): [block][wave][16] int64, <= 512 waves per env
         if K != 12 or stamps.dtype != torch.int64 or stamps.numel() < B * 8192 or not stamps.is_contiguous():
@@ -983,6 +983,22 @@ def bwd_step_fused(total_agents: int, device) -> bool:
     return BWD_FUSED_DEFAULT and node_bwd_chunk(total_agents, device) == 32 and (total_agents + 31) // 32 >= num_cu(device) // 2
 
 
+def reduce_multi(jobs):
+    """Several reduce_rows in ONE launch: jobs = [(partial (rows, cols), out (cols,), accumulate)]
+    (at most 4; the same fixed-order sums as reduce_rows)."""
+    if not 1 <= len(jobs) <= 4:
+        raise NativeError("reduce_multi takes 1..4 jobs")
+    spec = []
+    for partial, out, acc in jobs:
+        rows, cols = partial.shape
+        check(partial, torch.float32, None, "partial")
+        check(out, torch.float32, (cols,), "out")
+        if cols % 4:
+            raise NativeError("cols must be a multiple of 4")
+        spec.append((ptr(partial), rows, cols, ptr(out), int(bool(acc))))
+    _ok(lib().reduce_multi(spec, stream_handle()), "reduce_multi")
+
+
 def reduce_rows(partial, out, accumulate=False):
     rows, cols = partial.shape
     check(partial, torch.float32, None, "partial")
@@ -1026,6 +1042,24 @@ def rollout_stats(dist, cnt, safe, act, valid, counts, local, *, N, reset=None):
                             ptr(valid), ptr(counts), ptr(local), int(reset_T), stream_handle()), "rollout_stats")
 
 
+def adam_multi(param, grad, m, v, groups, lr, b1, b2, eps, wd, ok=None):
+    """Fused Adam over several ranges in ONE launch: groups = [(lo, hi, step_dev)] (at most 4; each
+    step_dev a 1-element device int32 counter, step = *step_dev + 1); ok as in adam."""
+    for t, n in ((param, "param"), (grad, "grad"), (m, "m"), (v, "v")):
+        check(t, torch.float32, (param.numel(),), n)
+    check(ok, torch.int32, None, "ok")
+    if not 1 <= len(groups) <= 4:
+        raise NativeError("adam_multi takes 1..4 groups")
+    spec = []
+    for lo, hi, sd in groups:
+        if not (0 <= lo <= hi <= param.numel()):
+            raise NativeError("bad Adam range")
+        check(sd, torch.int32, (1,), "step_dev")
+        spec.append((int(lo), int(hi), ptr(sd)))
+    _ok(lib().adam_multi(ptr(param), ptr(grad), ptr(m), ptr(v), spec, float(b1), float(b2), float(eps), float(wd),
+                         ptr(ok), float(lr), stream_handle()), "adam_multi")
+
+
 def adam(param, grad, m, v, lo, hi, lr, b1, b2, eps, wd, step, ok=None, step_dev=None):
     """Fused Adam over param[lo:hi]. step: host step count (bias corrections), or step_dev: a
     1-element device int32 counter (step = *step_dev + 1, read by the kernel); ok: optional
@@ -1043,9 +1077,10 @@ def adam(param, grad, m, v, lo, hi, lr, b1, b2, eps, wd, step, ok=None, step_dev
                    stream_handle()), "adam")
 
 
-def pack_gather(src, idx16, out16, idx32, out32):
+def pack_gather(src, idx16, out16, idx32, out32, commit=None):
     """out16[i] = h16(src'[idx16[i]]), out32[j] = src'[idx32[j]] with src' = [src, 0, 1]: all
-    packed weight buffers of both networks in one launch."""
+    packed weight buffers of both networks in one launch. commit: step_commit_args(...) of the
+    optimizer step just enqueued -- its commit then runs in this launch (one launch fewer)."""
     check(src, torch.float32, None, "src")
     check(idx16, torch.int32, None, "idx16")
     check(idx32, torch.int32, None, "idx32")
@@ -1054,21 +1089,38 @@ def pack_gather(src, idx16, out16, idx32, out32):
         raise NativeError("out16 must be a contiguous bf16/fp16 buffer matching idx16")
     n = src.numel()    # index range (<= n + 1) is validated once by ops.weights.PackedWeights
     _ok(lib().pack_gather(ptr(src), n, ptr(idx16), idx16.numel(), ptr(out16), int(out16.dtype == torch.float16),
-                          ptr(idx32), idx32.numel(), ptr(out32), stream_handle()), "pack_gather")
+                          ptr(idx32), idx32.numel(), ptr(out32), commit, stream_handle()), "pack_gather")
 
 
-def grad_assemble(red, ptr_, src, grad, scale=1.0, gscale=None):
+def grad_assemble(red, ptr_, src, grad, scale=1.0, gscale=None, ok=None, stats=None):
     """grad[p] = scale * sum(red[src[ptr[p]:ptr[p+1]]]) (/ *gscale: the device loss scale) for
     every flat parameter p (one launch, fixed order). ptr (n+1,) / src int32 from a host-built CSR
-    (validated by the caller)."""
+    (validated by the caller). In the same launch (single-process runs): ok (int32 flag) <- 0 if an
+    assembled element is not finite (grad_check's test); stats = (sums, counts, local, row): the
+    iteration's statistics row (stats_pack's work)."""
     n = grad.numel()
     check(red, torch.float32, None, "red")
     check(ptr_, torch.int32, (n + 1,), "ptr")
     check(src, torch.int32, None, "src")
     check(grad, torch.float32, None, "grad")
     check(gscale, torch.float32, (1,), "gscale")
-    _ok(lib().grad_assemble(ptr(red), ptr(ptr_), ptr(src), n, float(scale), ptr(gscale), ptr(grad), stream_handle()),
-        "grad_assemble")
+    check(ok, torch.int32, (1,), "ok")
+    sums = counts = local = row = None
+    if stats is not None:
+        sums, counts, local, row = stats
+        _stats_args(sums, counts, local, row)
+    _ok(lib().grad_assemble(ptr(red), ptr(ptr_), ptr(src), n, float(scale), ptr(gscale), ptr(grad), ptr(ok),
+                            ptr(sums), ptr(counts), ptr(local), ptr(row), stream_handle()), "grad_assemble")
+
+
+def _stats_args(sums, counts, local, row):
+    check(sums, torch.float32, None, "sums")
+    check(counts, torch.float32, None, "counts")
+    check(local, torch.float32, None, "local")
+    if sums.numel() < 10 or counts.numel() < 3 or local.numel() < 3:
+        raise NativeError("stats_pack needs 10 sums, 3 counts, 3 local values")
+    if row.dtype != torch.float32 or row.numel() < 18 or not row.is_contiguous():
+        raise NativeError("row must be a contiguous float32 row of >= 18")
 
 
 def grad_check(g, ok):
@@ -1077,6 +1129,28 @@ def grad_check(g, ok):
     check(g, torch.float32, None, "g")
     check(ok, torch.int32, None, "ok")
     _ok(lib().grad_check(ptr(g), g.numel(), ptr(ok), stream_handle()), "grad_check")
+
+
+def step_commit_args(ok, steps, mask, skipped, *, gscale=None, good=None, growth=1000, max_scale=2.0 ** 24,
+                     stats_row=None):
+    """Validated step_commit arguments as the tuple pack_gather(commit=...) takes."""
+    check(ok, torch.int32, (1,), "ok")
+    check(steps, torch.int32, None, "steps")
+    check(skipped, torch.int32, (1,), "skipped")
+    check(gscale, torch.float32, (1,), "gscale")
+    check(good, torch.int32, (1,), "good")
+    if (gscale is None) != (good is None):
+        raise NativeError("gscale and good go together")
+    if stats_row is not None and (stats_row.dtype != torch.float32 or stats_row.numel() < 18
+                                  or not stats_row.is_contiguous()):
+        raise NativeError("stats_row must be a contiguous float32 row of >= 18")
+    return (ptr(ok), ptr(steps), int(mask), steps.numel(), ptr(skipped), ptr(gscale), ptr(good), int(growth),
+            float(max_scale), ptr(stats_row))
+
+
+def step_commit_raw(args):
+    """step_commit from a step_commit_args tuple (its own launch)."""
+    _ok(lib().step_commit(*args, stream_handle()), "step_commit")
 
 
 def step_commit(ok, steps, mask, skipped, *, gscale=None, good=None, growth=1000, max_scale=2.0 ** 24,

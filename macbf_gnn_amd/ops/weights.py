@@ -79,10 +79,12 @@ class PackedWeights:
         return np.concatenate(out), views
 
     @torch.no_grad()
-    def update(self):
+    def update(self, commit=None):
+        """Repack every weight image from the flat parameters. commit (HIP): the deferred commit of
+        the optimizer step just enqueued (FlatAdam.step(defer_commit=True)), run in the same launch."""
         if self._buf16.is_cuda:
             from . import native
-            native.pack_gather(self.fp.flat, self._idx16, self._buf16, self._idx32, self._buf32)
+            native.pack_gather(self.fp.flat, self._idx16, self._buf16, self._idx32, self._buf32, commit=commit)
             return
         n = self.fp.numel
         src = torch.cat([self.fp.flat, torch.tensor([0.0, 1.0], device=self.fp.flat.device)])

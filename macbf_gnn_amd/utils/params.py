@@ -115,27 +115,32 @@ class FlatAdam:
         else:
             self._steps[name] = int(step)
 
-    def step(self, groups=None, ok=None, gscale=None, good=None, growth=1000, stats_row=None):
+    def step(self, groups=None, ok=None, gscale=None, good=None, growth=1000, stats_row=None, defer_commit=False):
         """One Adam step of the named ranges. On HIP, ok (device int32 flag, optional) gates the
         whole step on the device: 0 leaves parameters, moments and step counts untouched and
         counts a skipped step; the commit kernel then re-arms the flag. gscale / good (fp16): the
         device loss scale and finite-step count, updated by the commit kernel (``native.step_commit``);
-        stats_row: the iteration's statistics row (skipped flag and loss scale written into it)."""
+        stats_row: the iteration's statistics row (skipped flag and loss scale written into it).
+        All groups update in ONE launch; defer_commit: return the commit's arguments instead of
+        launching it (the weight repack runs it: ``PackedWeights.update(commit=...)``)."""
         groups = list(self.fp.ranges) if groups is None else list(groups)
         if self.on_device:
             from ..ops import native
             flag = self._one if ok is None else ok
-            mask = 0
+            mask, spec = 0, []
             for name in groups:
                 a, b = self.fp.ranges[name]
                 gi = self._names.index(name)
-                native.adam(self.fp.flat, self.fp.grad, self.exp_avg, self.exp_avg_sq, a, b,
-                            self.lr, self.betas[0], self.betas[1], self.eps, self.wd, 1, ok=flag,
-                            step_dev=self._dsteps[gi:gi + 1])
+                spec.append((a, b, self._dsteps[gi:gi + 1]))
                 mask |= 1 << gi
-            native.step_commit(flag, self._dsteps, mask, self.dskipped, gscale=gscale, good=good, growth=growth,
-                               stats_row=stats_row)
-            return
+            if spec:
+                native.adam_multi(self.fp.flat, self.fp.grad, self.exp_avg, self.exp_avg_sq, spec, self.lr,
+                                  self.betas[0], self.betas[1], self.eps, self.wd, ok=flag)
+            kw = dict(gscale=gscale, good=good, growth=growth, stats_row=stats_row)
+            if defer_commit:
+                return native.step_commit_args(flag, self._dsteps, mask, self.dskipped, **kw)
+            native.step_commit(flag, self._dsteps, mask, self.dskipped, **kw)
+            return None
         for name in groups:
             a, b = self.fp.ranges[name]
             self._steps[name] += 1

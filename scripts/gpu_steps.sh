@@ -16,7 +16,10 @@
 # ab:<NAME>    interleaved headline+slice A/B of alt_so/NAME/_C.so vs the in-tree build (REPS, ABARGS)
 # prof         kernel trace of the headline    -> prof/kernel_stats.csv, prof_summary.txt
 # prof_slice   kernel trace of the slice       -> prof_slice/...
+# sol / sol_slice / sol_cfg4 / sol_cfg5   two-pass PMC speed-of-light table (scripts/gpu_sol.sh) -> sol_*/sol.md
 # neg          scan oracle tests against alt_so/shrink (search box 0.7x): must FAIL -> neg.log
+# py:S,ARGS    python scripts/S with comma-separated ARGS (e.g. py:stamps_scan.py,--envs,8) -> py_S.log
+# sl:K=V       the slice bench with the env var K=V (A/B of a runtime choice)   -> sl_K_V.log
 # env:K=V      export K=V for the following steps
 set -o pipefail
 cd $GRAFT_REPO_ROOT
@@ -75,10 +78,23 @@ for s in ${STEPS:-tests smoke bench}; do
       done ;;
     prof) prof prof ;;
     prof_slice) prof prof_slice --envs 8 ;;
+    sol) TAG=${TAG:-r6}/sol ARGS="" bash scripts/gpu_sol.sh > $O/sol.log 2>&1 || { echo "STOP sol"; tail -5 $O/sol.log; exit 1; }; head -30 $O/sol/sol.md ;;
+    sol_slice) TAG=${TAG:-r6}/sol_slice ARGS="--envs 8" bash scripts/gpu_sol.sh > $O/sol_slice.log 2>&1 || { echo "STOP sol_slice"; tail -5 $O/sol_slice.log; exit 1; }; head -30 $O/sol_slice/sol.md ;;
+    sol_cfg4) TAG=${TAG:-r6}/sol_cfg4 ARGS="--agents 4096 --envs 16" bash scripts/gpu_sol.sh > $O/sol_cfg4.log 2>&1 || { echo "STOP sol_cfg4"; tail -5 $O/sol_cfg4.log; exit 1; }; head -30 $O/sol_cfg4/sol.md ;;
+    sol_cfg5) TAG=${TAG:-r6}/sol_cfg5 ARGS="--agents 1024 --envs 64 --dim 3 --num_obstacles 8 --dtype fp16" bash scripts/gpu_sol.sh > $O/sol_cfg5.log 2>&1 || { echo "STOP sol_cfg5"; tail -5 $O/sol_cfg5.log; exit 1; }; head -30 $O/sol_cfg5/sol.md ;;
     neg)
       MACBF_EXT=alt_so/shrink/_C.so timeout -k 10 600 python -u -m pytest tests/test_gpu_scan_plans.py -q -m gpu -p no:cacheprovider --timeout 240 --timeout-method thread > $O/neg.log 2>&1
       rc=$?; tail -3 $O/neg.log
       if [ $rc -eq 1 ]; then echo "neg: the shrunk search box FAILS the oracle tests (expected)"; else echo "STOP neg rc=$rc (expected 1)"; exit 1; fi ;;
+    py:*)
+      spec=${s#py:}; scr=${spec%%,*}; args=""; [ "$spec" != "$scr" ] && args=${spec#*,}
+      L=$O/py_${scr%.py}_$(echo "$args" | tr -c 'a-zA-Z0-9' _).log
+      timeout -k 10 300 python -u scripts/$scr ${args//,/ } > $L 2>&1 || { echo "STOP $s"; tail -5 $L; exit 1; }
+      echo "== $s"; tail -25 $L ;;
+    sl:*)
+      kv=${s#sl:}; n=sl_$(echo "$kv" | tr -c 'a-zA-Z0-9' _)
+      env "$kv" timeout -k 10 300 $B --envs 8 > $O/$n.log 2>&1 || { echo "STOP $n"; tail -5 $O/$n.log; exit 1; }
+      echo "$n: $(ms $O/$n.log)" ;;
     env:*) export "${s#env:}" ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac

@@ -1,7 +1,7 @@
 """Kernels of one training iteration from a rocprofv3 kernel_trace.csv.
 
-Iterations are split at the optimizer's commit kernel (``step_commit_kernel``, the last launch of
-a step). Prints, for the last complete iteration: per-kernel-name launch counts and total device
+Iterations are split at the weight repack (``pack_gather_kernel``, the last launch of a step; it
+runs the optimizer's commit since round 6). Prints, for the last complete iteration: per-kernel-name launch counts and total device
 time, the glue kernels (anything not in the ``mb::`` namespace, e.g. ``at::native`` fills / copies)
 and the sum of the gaps between consecutive kernels on the compute queue.
 
@@ -13,7 +13,7 @@ import json
 from collections import OrderedDict
 
 
-def iterations(path, marker="step_commit_kernel"):
+def iterations(path, marker="pack_gather_kernel"):
     rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
     its, cur = [], []
     for r in rows:

@@ -2,7 +2,7 @@
 then one ctrl_node_bwd call with the stamps buffer and prints, per phase, the median over
 workgroups of the slowest wave's shader-clock delta (cycles). Default: the cooperative 32-agent
 kernel, whose stamps are compiled only into a diagnostics build (MACBF_EXT=alt_so/stamps/_C.so from
-scripts/build_variant.sh stamps ctrl_x3 "-DMB_STAMPS=1"); --node16: the 16x16x32 kernel
+scripts/build_variant.sh stamps ctrl_x3 "-DMB_DIAG=1"); --node16: the 16x16x32 kernel
 (csrc/node16.h, 128-agent chunks, 8 waves; its stamps instantiation ships in every build).
 
     python scripts/stamps_node.py [--agents 1024 --envs 8] [--node16 --envs 64]

@@ -349,18 +349,34 @@ def test_graph_mode_training_runs():
     assert 1 <= float(st["T"]) <= 10
 
 
-def test_device_nan_guard_skips_step_without_host_sync():
+@pytest.mark.parametrize("where", ["assemble", "after"])
+def test_device_nan_guard_skips_step_without_host_sync(where, monkeypatch):
     """HIP bf16 path: a non-finite reduced gradient is caught on the device (flag -> fused
-    Adam), parameters / moments / step counts stay untouched, the skip is counted."""
+    Adam), parameters / moments / step counts stay untouched, the skip is counted. assemble: the
+    single-process check inside the gradient-assembly launch (a reduced slab entry poisoned);
+    after: the separate check that follows a DP all-reduce (the assembled gradient poisoned)."""
+    from macbf_gnn_amd.ops import native
     tr = _trainer(DEV, N=32, B=2, T=4)
+    tr.engine.bwd_graph = False                    # eager launches (no graph captures the poison)
+    assert tr.engine.check_ok is not None          # single process: the fused check
     before = tr.fp.flat.clone()
     m_before = tr.opt.exp_avg.clone()
     real_step = tr.engine.step
+    if where == "assemble":
+        real_reduce = native.reduce_multi
 
-    def poisoned(s0, g0, obs=None):
-        st = real_step(s0, g0, obs)
-        tr.fp.grad[5] = float("inf")
-        return st
+        def poisoned_reduce(jobs):
+            real_reduce(jobs)
+            tr.engine.red_all.fill_(float("nan"))
+        monkeypatch.setattr(native, "reduce_multi", poisoned_reduce)
+        poisoned = real_step
+    else:
+        tr.engine.check_ok = None                  # the DP path: grad_check after the all-reduce
+
+        def poisoned(s0, g0, obs=None):
+            st = real_step(s0, g0, obs)
+            tr.fp.grad[5] = float("inf")
+            return st
 
     tr.engine.step = poisoned
     st = tr.train_step()
@@ -369,6 +385,7 @@ def test_device_nan_guard_skips_step_without_host_sync():
     assert torch.equal(before, tr.fp.flat) and torch.equal(m_before, tr.opt.exp_avg)
     assert tr.opt.steps == {"controller": 0, "cbf": 0}
     tr.engine.step = real_step
+    monkeypatch.undo()
     st = tr.train_step()
     assert int(st["skipped"]) == 0 and tr.skipped_steps == 1
     assert not torch.equal(before, tr.fp.flat)
