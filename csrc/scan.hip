@@ -1028,7 +1028,7 @@ static bool scan_small_grid(const ScanArgs& a) {
 // chunk work -> twice the blocks. Same keys and tie order: the merged lists are identical for
 // any LPA (tests/test_gpu_forward.py forces lanes = 4 / 8 through ScanArgs.lanes).
 static bool scan_lpa8(const ScanArgs& a) {
-  if (a.lanes == 4 || a.lanes == 8 || a.lanes == 16) return a.lanes == 8;
+  if (a.lanes == 4 || a.lanes == 8) return a.lanes == 8;
   constexpr int AG = 256 / SCAN_LPA;
   return SCAN_LPA < 8 && (long)a.B * ((a.Nn + AG - 1) / AG) < scan_num_cu();
 }
@@ -1044,21 +1044,13 @@ static bool scan_boxes_global(const ScanArgs& a) {
 // (3-D scenes at 8 lanes per agent -- 8 agents per wave, a smaller wave box in x, y -- measured
 // slower in round 5: config #5 fp16 9.93 vs 9.50-9.52 ms, profiles/r5_b6/)
 
-// Strong-scaling slices (8 envs x 1024 agents: the 8-lane grid has no more blocks than CUs) whose
-// calls search the cell grid: 16 lanes per agent in 512-thread blocks -- the same blocks, twice
-// the threads for the per-block env staging and cell-grid build, half the candidates per lane
-// (ScanArgs.lanes = 16 forces it; MACBF_SCAN_L16 = 0 / 1 for the A/B)
-static bool scan_lpa16(const ScanArgs& a) {
-  if (a.lanes) return a.lanes == 16;
-  static const int env = [] { const char* e = getenv("MACBF_SCAN_L16"); return e ? atoi(e) : 0; }();
-  if (!env) return false;
-  return a.prev_idx && a.do_knn && a.Nn <= SCAN_MAXN && (long)a.B * ((a.Nn + 31) / 32) <= scan_num_cu();
-}
+// (16 lanes per agent in 512-thread blocks for the slices -- twice the threads for the per-block
+// staging and cell-grid build, half the candidates per lane, a fourth merge level: oracle tests
+// pass, 8-env slice 2.826 / 2.829 vs 2.830 / 2.809 ms, neutral; removed, profiles/r6c/)
 
 template <int K, int D>
 static void launch_kd(const ScanArgs& a, hipStream_t st, ScanPlan* plan) {
   if (scan_boxes_global(a)) launch_kdb<K, D, SCAN_BS_BIG>(a, st, plan);
-  else if (scan_lpa16(a)) launch_kdb<K, D, 512, 16>(a, st, plan);
   else if (scan_lpa8(a)) launch_kdb<K, D, 256, 8>(a, st, plan);
   else if (a.Nn > 512 && !scan_small_grid<D>(a)) launch_kdb<K, D, D == 3 ? SCAN_BS_BIG3 : SCAN_BS_BIG>(a, st, plan);
   else launch_kdb<K, D, 256>(a, st, plan);

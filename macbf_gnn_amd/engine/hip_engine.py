@@ -140,6 +140,8 @@ class HipEngine:
         self.graph_mode = bool(getattr(cfg, "graph", False))
         self._graphs = None
         self._graph_gs = None
+        # (per-T backward graphs for every scene size, not only small ones: headline 10.125-10.135
+        # vs 10.141-10.165 ms, 8-env slice 2.798-2.803 vs 2.793-2.815 -- within noise, profiles/r6d/)
         self.bwd_graph = bool(knobs.get_int("MACBF_BWD_GRAPH", int(self.bwd_graph)))
         self._bwd_graphs = {}          # (T, grad scale) -> CUDAGraph of _counts + _backward
         self._bwd_pool = None

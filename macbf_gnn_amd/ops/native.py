@@ -228,10 +228,10 @@ def scan(S, idx, dang, cnt, safe, *, K, do_knn=True, do_safety=True, perm=None, 
     agents; their current distances bound the K-th distance (tighter culling, same result).
     sort=False reuses the curve order of the previous call on the same perm buffer (the agents
     moved one step: slightly looser culling, identical results). lanes: lanes per agent (0: by
-    grid size -- 8 when 4-lane 256-thread blocks leave CUs idle; 4, 8 or 16 (512-thread blocks)
-    forces the layout; the lists, bits and counts are identical for any)."""
-    if lanes not in (0, 4, 8, 16):
-        raise NativeError("lanes must be 0 (auto), 4, 8 or 16")
+    grid size -- 8 when 4-lane 256-thread blocks leave CUs idle; 4 or 8 forces the layout; the
+    lists, bits and counts are identical for either)."""
+    if lanes not in (0, 4, 8):
+        raise NativeError("lanes must be 0 (auto), 4 or 8")
     B, Nn = S.shape[0], S.shape[1]
     if stamps is not None:   # diagnostics (scripts/stamps_scan.py): [block][wave][16] int64, <= 512 waves per env
         if K != 12 or stamps.dtype != torch.int64 or stamps.numel() < B * 8192 or not stamps.is_contiguous():

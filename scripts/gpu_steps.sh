@@ -20,6 +20,7 @@
 # neg          scan oracle tests against alt_so/shrink (search box 0.7x): must FAIL -> neg.log
 # py:S,ARGS    python scripts/S with comma-separated ARGS (e.g. py:stamps_scan.py,--envs,8) -> py_S.log
 # sl:K=V       the slice bench with the env var K=V (A/B of a runtime choice)   -> sl_K_V.log
+# e:K=V:STEP   run STEP (a bench step) with the env var K=V        -> K_V_STEP.log
 # env:K=V      export K=V for the following steps
 set -o pipefail
 cd $GRAFT_REPO_ROOT
@@ -28,7 +29,7 @@ mkdir -p $O
 B="python -u bench.py"
 ms() { grep '^{' $1 | tail -1 | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(round(d["ms_per_step"],3), "ms", round(d["value"]/1e6,2), "M/s", d["scaling"], d["config"]["global_batch"])'; }
 bench() {   # name limit args...
-  local n=$1 t=$2; shift 2
+  local n=${PFX:-}$1 t=$2; shift 2
   timeout -k 10 $t $B "$@" > $O/$n.log 2>&1 || { echo "STOP $n rc=$?"; tail -5 $O/$n.log; exit 1; }
   echo "$n: $(ms $O/$n.log)"
 }
@@ -95,6 +96,9 @@ for s in ${STEPS:-tests smoke bench}; do
       kv=${s#sl:}; n=sl_$(echo "$kv" | tr -c 'a-zA-Z0-9' _)
       env "$kv" timeout -k 10 300 $B --envs 8 > $O/$n.log 2>&1 || { echo "STOP $n"; tail -5 $O/$n.log; exit 1; }
       echo "$n: $(ms $O/$n.log)" ;;
+    e:*)
+      spec=${s#e:}; kv=${spec%%:*}; sub=${spec#*:}
+      PFX="$(echo "$kv" | tr -c 'a-zA-Z0-9' _)_" STEPS="$sub" TAG=${TAG:-r6} env "$kv" bash scripts/gpu_steps.sh | grep -v '^DONE' || exit 1 ;;
     env:*) export "${s#env:}" ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac

@@ -33,7 +33,7 @@ def _nets(seed=0):
     return ctrl, cbf, fp, PackedWeights(fp)
 
 
-@pytest.mark.parametrize("lanes", [4, 8, 16])
+@pytest.mark.parametrize("lanes", [4, 8])
 @pytest.mark.parametrize("B,N", [(2, 8), (3, 13), (2, 64), (1, 1100)])
 def test_scan_knn_ttc_safety(B, N, lanes):
     _scan_vs_oracle(B, N, lanes)
@@ -64,7 +64,7 @@ def _scan_vs_oracle(B, N, lanes):
     assert torch.equal(safe, O.safe_agent_count(s).float())
 
 
-@pytest.mark.parametrize("lanes", [4, 8, 16])
+@pytest.mark.parametrize("lanes", [4, 8])
 @pytest.mark.parametrize("resort", [True, False])
 @pytest.mark.parametrize("B,N,steps", [(2, 13, 3), (2, 300, 4), (1, 1100, 3), (1, 4096, 2)])
 def test_scan_temporal_bound_is_exact(B, N, steps, resort, lanes):

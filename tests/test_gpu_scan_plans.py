@@ -9,8 +9,8 @@ danger bits, counts and safety counts with the oracle (reference semantics: /roo
 core.py:187-209 kNN + TTC mask, core.py:234-250 safety check). ``lattice`` rounds the positions
 to a coarse grid: many exactly equal distances, so the (distance, index) tie order is checked.
 
-Negative check (one-off, recorded in profiles/r6_scan_neg/): the same tests run against a build
-whose cell search box is shrunk to 0.7x (``-DMB_DIAG_SCAN_SHRINK``) and fail.
+Negative check (one-off, recorded in profiles/r6_runs/r6c/neg.log: 12 of 12 fail): the same tests run against a build
+whose cell search box is shrunk to 0.7x (``scripts/build_variant.sh shrink scan "-DMB_DIAG=8"``).
 """
 import pytest
 import torch
@@ -30,8 +30,6 @@ PLANS = [
     ("cfg5_3d_obstacles", 64, 1024, 3, 96, 0, dict(bs=512, lpa=4, glb=0, use_cells=1, cell_g=10, wave_atomic=1)),
     # the DP=8 slice of config #3 (8 envs per rank): 256-thread blocks, 8 lanes per agent, 16^2 grid
     ("slice8_2d", 8, 1024, 2, 0, 0, dict(bs=256, lpa=8, glb=0, use_cells=1, cell_g=16, wave_atomic=0)),
-    # the slice's 16-lane layout (512-thread blocks, 4 agents per wave, four merge levels)
-    ("slice8_2d_l16", 8, 1024, 2, 0, 16, dict(bs=512, lpa=16, glb=0, use_cells=1, cell_g=16, wave_atomic=0)),
     # small 3-D scenes: 256-thread blocks with 4 cells per thread in the prefix sum,
     # at the auto layout (8 lanes) and forced 4 lanes
     ("small_3d_auto", 2, 300, 3, 0, 0, dict(bs=256, lpa=8, glb=0, use_cells=1, cell_g=10, wave_atomic=1)),
