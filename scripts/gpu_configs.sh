@@ -27,9 +27,11 @@ echo "cfg1_train     ok: $(grep -c loss $O/cfg1_train.log) log line(s)"
 run cfg1_cpu 300 --device cpu --agents 8 --envs 1 --steps 3 --warmup 1
 run cfg2_bf16 300 --agents 32 --envs 1 --steps 30 --warmup 5 --dtype bf16
 run cfg2_fp32 300 --agents 32 --envs 1 --steps 30 --warmup 5
-run cfg3_fp32 300 --agents 1024 --envs 64
-run cfg3_bf16 300 --agents 1024 --envs 64 --dtype bf16
+run cfg3_fp32 300 --agents 1024                  # bench.py's default: 64 envs over the ranks (here one)
+run cfg3_bf16 300 --agents 1024 --dtype bf16
 run cfg3_slice8_fp32 300 --agents 1024 --envs 8
 run cfg4_fp32 300 --agents 4096 --envs 16
 run cfg5_fp16 300 --agents 1024 --envs 64 --dim 3 --num_obstacles 8 --dtype fp16
 run cfg5_fp32 300 --agents 1024 --envs 64 --dim 3 --num_obstacles 8
+run cfg3_fixedT_fp32 300 --agents 1024 --no_early_stop
+run cfg3_fixedT_bf16 300 --agents 1024 --no_early_stop --dtype bf16

@@ -17,6 +17,8 @@
 # prof         kernel trace of the headline    -> prof/kernel_stats.csv, prof_summary.txt
 # prof_slice   kernel trace of the slice       -> prof_slice/...
 # sol / sol_slice / sol_cfg4 / sol_cfg5   two-pass PMC speed-of-light table (scripts/gpu_sol.sh) -> sol_*/sol.md
+# configs      every BASELINE config (scripts/gpu_configs.sh)   -> configs/configs.jsonl
+# dp:N         N ranks of the bench on this one GPU over gloo (launch / DP rehearsal, strong default)
 # neg          scan oracle tests against alt_so/shrink (search box 0.7x): must FAIL -> neg.log
 # py:S,ARGS    python scripts/S with comma-separated ARGS (e.g. py:stamps_scan.py,--envs,8) -> py_S.log
 # sl:K=V       the slice bench with the env var K=V (A/B of a runtime choice)   -> sl_K_V.log
@@ -83,6 +85,10 @@ for s in ${STEPS:-tests smoke bench}; do
     sol_slice) TAG=${TAG:-r6}/sol_slice ARGS="--envs 8" bash scripts/gpu_sol.sh > $O/sol_slice.log 2>&1 || { echo "STOP sol_slice"; tail -5 $O/sol_slice.log; exit 1; }; head -30 $O/sol_slice/sol.md ;;
     sol_cfg4) TAG=${TAG:-r6}/sol_cfg4 ARGS="--agents 4096 --envs 16" bash scripts/gpu_sol.sh > $O/sol_cfg4.log 2>&1 || { echo "STOP sol_cfg4"; tail -5 $O/sol_cfg4.log; exit 1; }; head -30 $O/sol_cfg4/sol.md ;;
     sol_cfg5) TAG=${TAG:-r6}/sol_cfg5 ARGS="--agents 1024 --envs 64 --dim 3 --num_obstacles 8 --dtype fp16" bash scripts/gpu_sol.sh > $O/sol_cfg5.log 2>&1 || { echo "STOP sol_cfg5"; tail -5 $O/sol_cfg5.log; exit 1; }; head -30 $O/sol_cfg5/sol.md ;;
+    configs) TAG=${TAG:-r6}/configs bash scripts/gpu_configs.sh || { echo "STOP configs"; exit 1; } ;;
+    dp:*)
+      NR=${s#dp:} STEPS=3 bash scripts/gpu_dp_rehearsal.sh || { echo "STOP $s"; exit 1; }
+      mv gpurun_out/dp${s#dp:}_rehearsal.log $O/ ;;
     neg)
       MACBF_EXT=alt_so/shrink/_C.so timeout -k 10 600 python -u -m pytest tests/test_gpu_scan_plans.py -q -m gpu -p no:cacheprovider --timeout 240 --timeout-method thread > $O/neg.log 2>&1
       rc=$?; tail -3 $O/neg.log
