@@ -320,7 +320,6 @@ __global__ __launch_bounds__(DH_BLOCK) void cbf_compact_kernel(const float* dh, 
   const unsigned U = (unsigned)*nev;
   const unsigned span = dh_span(U, gridDim.x);
   const unsigned u_lo = blockIdx.x * span, u_hi = min(U, u_lo + span);
-  __shared__ int wcnt[DH_BLOCK / WAVE];
   const int wave = threadIdx.x / WAVE, lane = threadIdx.x % WAVE;
   int base;
   if (blk_off) {
@@ -329,31 +328,64 @@ __global__ __launch_bounds__(DH_BLOCK) void cbf_compact_kernel(const float* dh, 
     base = block_sum_prefix<DH_BLOCK>(blk_active, blockIdx.x);
     if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0 && nact) *nact = base + blk_active[blockIdx.x];
   }
-  for (unsigned u0 = u_lo; u0 < u_hi; u0 += DH_BLOCK) {
-    const unsigned u = u0 + threadIdx.x;
-    const float dv = u < u_hi ? dh[u] : 0.f;
-    const bool f = dv != 0.f;
-    const unsigned long long bal = __ballot(f);
-    const int below = __popcll(bal & ((1ull << lane) - 1ull));
-    if (lane == 0) wcnt[wave] = __popcll(bal);
-    __syncthreads();
-    int wo = 0, tot = 0;
-    for (int w = 0; w < DH_BLOCK / WAVE; ++w) {
-      const int c = wcnt[w];
-      wo += (w < wave) ? c : 0;
-      tot += c;
+  // CP_U rows of DH_BLOCK evaluations per round: their dh loads, then (for the active ones) the
+  // source and neighbour-index loads, are in flight together, and one barrier pair serves the
+  // round -- the same output order (u ascending) as one row per round (round 6: a row per round
+  // was one dependent chain of three loads and two barriers per 256 evaluations, ~75 us at the
+  // headline)
+  constexpr int CP_U = 4;
+  __shared__ int wcu[CP_U][DH_BLOCK / WAVE];
+  for (unsigned u0 = u_lo; u0 < u_hi; u0 += CP_U * DH_BLOCK) {
+    float dv[CP_U];
+    bool f[CP_U];
+    int below[CP_U];
+#pragma unroll
+    for (int r = 0; r < CP_U; ++r) {
+      const unsigned u = u0 + r * DH_BLOCK + threadIdx.x;
+      dv[r] = u < u_hi ? dh[u] : 0.f;
     }
-    if (f) {
-      if (rec) {
+#pragma unroll
+    for (int r = 0; r < CP_U; ++r) {
+      f[r] = dv[r] != 0.f;
+      const unsigned long long bal = __ballot(f[r]);
+      below[r] = __popcll(bal & ((1ull << lane) - 1ull));
+      if (lane == 0) wcu[r][wave] = __popcll(bal);
+    }
+    // the records' source / neighbour indices, requested before the barrier
+    unsigned ev[CP_U];
+    int jn[CP_U];
+    if (rec) {
+      unsigned e0[CP_U];
+#pragma unroll
+      for (int r = 0; r < CP_U; ++r) {
+        const unsigned u = u0 + r * DH_BLOCK + threadIdx.x;
         const unsigned pass = u >= E ? 1u : 0u;
-        const unsigned e = pass ? (unsigned)src[u] : u;
-        const int j = ((pass && idx1) ? idx1 : idx)[e];
-        rec[base + wo + below] = int4{(int)u, (int)(e | (pass << 31)), j, __float_as_int(dv)};
-      } else {
-        act[base + wo + below] = (int)u;
+        e0[r] = (f[r] && pass) ? (unsigned)src[u] : (f[r] ? u : 0u);
+      }
+#pragma unroll
+      for (int r = 0; r < CP_U; ++r) {
+        const unsigned u = u0 + r * DH_BLOCK + threadIdx.x;
+        const unsigned pass = u >= E ? 1u : 0u;
+        ev[r] = e0[r] | (pass << 31);
+        jn[r] = f[r] ? ((pass && idx1) ? idx1 : idx)[e0[r]] : 0;
       }
     }
-    base += tot;
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < CP_U; ++r) {
+      int wo = 0, tot = 0;
+      for (int w = 0; w < DH_BLOCK / WAVE; ++w) {
+        const int c = wcu[r][w];
+        wo += (w < wave) ? c : 0;
+        tot += c;
+      }
+      if (f[r]) {
+        const unsigned u = u0 + r * DH_BLOCK + threadIdx.x;
+        if (rec) rec[base + wo + below[r]] = int4{(int)u, (int)ev[r], jn[r], __float_as_int(dv[r])};
+        else act[base + wo + below[r]] = (int)u;
+      }
+      base += tot;
+    }
     __syncthreads();
   }
 }

@@ -168,36 +168,27 @@ __global__ __launch_bounds__(CSR_BLOCK) void rev_csr_glb_kernel(CsrArgs a) {
   }
 }
 
-// gated record accumulation: a zero gate selects zero (the record may hold stale data). The
-// gate is read first and inactive evaluations skip the record load (CMB_GATE_FIRST: one more
-// dependent round trip, but most evaluations are inactive: node_reduce 330 -> 297 us per
-// iteration at the headline, profiles/r2_gather/; loading both together: history, round 4)
-template <int R, int SIGN>
-DEV void acc_rec_g(float4 (&g)[R], const float4* src, const float* gate) {
-  float4 v[R];
-  const bool on = !gate || *gate != 0.f;     // inactive evaluations: no record load
-#pragma unroll
-  for (int q = 0; q < R; ++q) v[q] = on ? src[q] : make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-  for (int q = 0; q < R; ++q) {
-    if (!on) v[q] = make_float4(0.f, 0.f, 0.f, 0.f);
-    g[q].x += SIGN * v[q].x; g[q].y += SIGN * v[q].y; g[q].z += SIGN * v[q].z; g[q].w += SIGN * v[q].w;
-  }
-}
-
 constexpr bool NODE_RED_XCD = true;
 // out[t', b, i] (+)= sum over passes p of [ sum_k dE_p[t'-p, b, i, k] - sum_{e in in(i)} dE_p[e] ]
 // for the N agents (obstacle nodes receive no gradient). Records of REC<D> float4.
+// NRL lanes per node (round 6; was 16): a node's K out-slots and its in-edges form one slot list,
+// dealt to the lanes NRL apart and consumed NRB slots per lane at a time -- every load of a batch
+// (in-edge index -> dedup map -> gate -> record) is requested for all NRB slots before the next
+// stage needs it, so a lane keeps up to NRB records in flight instead of one dependent chain per
+// slot, and the grid has a quarter of the threads (the 16-lane version ran ~38 rounds of full
+// occupancy at the headline, 297 us, each paying the chain's 4-5 memory latencies). Fixed slot
+// order per lane and a fixed xor butterfly: deterministic.
+constexpr int NRL = 4, NRB = 4;
 template <int D>
 __global__ __launch_bounds__(256) void node_reduce_kernel(NodeRedArgs a) {
   const int t_hi = a.t_hi ? a.t_hi : a.T + 1;
   // one graph's nodes on one XCD: the in-edge gathers read the records the graph's out-edge reads
   // just brought into that XCD's L2
   const int lb = NODE_RED_XCD ? xcd_block((int)blockIdx.x, (int)gridDim.x) : (int)blockIdx.x;
-  const long node = (long)a.t_lo * a.B * a.N + ((long)lb * blockDim.x + threadIdx.x) / RG;
-  const int l = threadIdx.x % RG;
+  const long node = (long)a.t_lo * a.B * a.N + ((long)lb * blockDim.x + threadIdx.x) / NRL;
+  const int l = threadIdx.x % NRL;
   const long total = (long)a.B * t_hi * a.N;
-  if (node >= total) return;             // whole 16-lane groups
+  if (node >= total) return;             // whole lane groups
   // time-major: out[(t'*B + b)*N + i], graphs g = t*B + b
   const int i = (int)(node % a.N);
   const long tb = node / a.N;
@@ -206,6 +197,7 @@ __global__ __launch_bounds__(256) void node_reduce_kernel(NodeRedArgs a) {
   const int N = a.N, K = a.K;
   const int Nt = a.Nn > 0 ? a.Nn : N;
   const long E = (long)a.B * a.T * N * K;
+  const int NK = N * K;
   constexpr int R = REC<D>;
   float4 g[R];
 #pragma unroll
@@ -217,33 +209,62 @@ __global__ __launch_bounds__(256) void node_reduce_kernel(NodeRedArgs a) {
     const long ge = (long)t * a.B + b;                          // edge block of step t
     const long gi = ge + (pass == 1 ? (long)a.shift1 * a.B : 0);  // graph (CSR) the edges live in
     const int* ptr = a.ptr + gi * (Nt + 1);
-    const int* edges = a.edges + gi * (long)N * K;
+    const int* edges = a.edges + gi * (long)NK;
     const int q0 = ptr[i], q1 = ptr[i + 1];
-    if (pass == 1 && a.map1) {
-      // deduplicated evaluations: only the extras (map1 >= E) carry a pass-1 gradient; the
-      // matched slots' h' gradient is part of the next step's main evaluation (pass 0)
-      const int* mp = a.map1 + ge * N * K;
-      for (int k = l; k < K; k += RG) {
-        const int m = mp[i * K + k];
-        if (m >= E) acc_rec_g<R, 1>(g, a.dE + (long)m * R, a.gate ? a.gate + m : nullptr);
+    // deduplicated evaluations: only the extras (map1 >= E) carry a pass-1 gradient; the matched
+    // slots' h' gradient is part of the next step's main evaluation (pass 0)
+    const bool dd = pass == 1 && a.map1;
+    const int* mp = dd ? a.map1 + ge * NK : nullptr;
+    const long eb = pass * E + ge * NK;                          // (non-dedup) record base of this block
+    const int nsl = K + (q1 - q0);                              // out-slots, then in-edges
+    for (int s0 = 0; s0 < nsl; s0 += NRL * NRB) {
+      int loc[NRB];
+      bool on[NRB], outs[NRB];
+#pragma unroll
+      for (int u = 0; u < NRB; ++u) {              // slot -> local edge index (in-edges: a load)
+        const int sl = s0 + l + u * NRL;
+        outs[u] = sl < K;
+        on[u] = sl < nsl;
+        const int q = min(q0 + max(sl - K, 0), NK - 1);
+        const int e = edges[q];                    // clamped, unconditional
+        loc[u] = outs[u] ? i * K + sl : e;
       }
-      for (int q = q0 + l; q < q1; q += RG) {
-        const int m = mp[edges[q]];
-        if (m >= E) acc_rec_g<R, -1>(g, a.dE + (long)m * R, a.gate ? a.gate + m : nullptr);
+      long x[NRB];
+#pragma unroll
+      for (int u = 0; u < NRB; ++u) {              // local edge -> evaluation index (dedup: a load)
+        if (dd) {
+          const int m = mp[min(max(loc[u], 0), NK - 1)];
+          on[u] = on[u] && m >= E;
+          x[u] = on[u] ? (long)m : 0;
+        } else {
+          x[u] = eb + loc[u];
+        }
       }
-      continue;
-    }
-    const long eb = pass * E + ge * N * K;
-    const float4* dE = a.dE + eb * R;
-    const float* gt = a.gate ? a.gate + eb : nullptr;
-    for (int k = l; k < K; k += RG)
-      acc_rec_g<R, 1>(g, dE + ((long)i * K + k) * R, gt ? gt + i * K + k : nullptr);
-    for (int q = q0 + l; q < q1; q += RG) {
-      const int e = edges[q];
-      acc_rec_g<R, -1>(g, dE + (long)e * R, gt ? gt + e : nullptr);
+      float gv[NRB];
+#pragma unroll
+      for (int u = 0; u < NRB; ++u) gv[u] = a.gate ? a.gate[on[u] ? x[u] : 0] : 1.f;
+      float4 v[NRB][R];
+#pragma unroll
+      for (int u = 0; u < NRB; ++u) {
+        // a zero gate: the record was never written (the active-list backward skips it)
+        const bool rd = on[u] && gv[u] != 0.f;
+#pragma unroll
+        for (int q = 0; q < R; ++q) v[u][q] = rd ? a.dE[x[u] * R + q] : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+      for (int u = 0; u < NRB; ++u) {
+        if (outs[u]) acc_rec_v<R, 1>(g, v[u]);
+        else acc_rec_v<R, -1>(g, v[u]);
+      }
     }
   }
-  grp_sum<R>(g);
+#pragma unroll
+  for (int q = 0; q < R; ++q) {
+    g[q].x += lane_xorf<2>(g[q].x); g[q].y += lane_xorf<2>(g[q].y);
+    g[q].z += lane_xorf<2>(g[q].z); g[q].w += lane_xorf<2>(g[q].w);
+    g[q].x += lane_xorf<1>(g[q].x); g[q].y += lane_xorf<1>(g[q].y);
+    g[q].z += lane_xorf<1>(g[q].z); g[q].w += lane_xorf<1>(g[q].w);
+  }
   if (l != 0) return;
   float4* o = a.out + (((long)tp * a.B + b) * N + i) * R;
   if (a.accumulate) acc_rec<R, 1>(g, o);
@@ -283,7 +304,7 @@ extern "C" int mb_node_reduce(const mb::NodeRedArgs* a, hipStream_t st) {
   using namespace mb;
   const int t_hi = a->t_hi ? a->t_hi : a->T + 1;
   if (a->t_lo < 0 || t_hi > a->T + 1 || a->t_lo >= t_hi) return -1;
-  const long total = (long)a->B * (t_hi - a->t_lo) * a->N * RG;
+  const long total = (long)a->B * (t_hi - a->t_lo) * a->N * NRL;
   if (a->dim == 3) hipLaunchKernelGGL(node_reduce_kernel<3>, dim3((total + 255) / 256), dim3(256), 0, st, *a);
   else hipLaunchKernelGGL(node_reduce_kernel<2>, dim3((total + 255) / 256), dim3(256), 0, st, *a);
   return (int)hipGetLastError();

@@ -50,9 +50,49 @@ DEV void reduce_rows_block(const float* partial, int rows, int cols, float* out,
   }
 }
 
+// Narrow slabs (<= 16 columns: the CBF loss partials, 12 floats x 16 rows per CU): one block, 64 row
+// slices x 4 column groups -- the wide layout's 16 slices left each thread 1/16 of thousands of rows
+// in a dependent chain, the iteration's slowest block
+constexpr int RN_SLICES = RR_COLS * RR_SLICES / 4;
+DEV void reduce_rows_narrow(const float* partial, int rows, int cols, float* out, int accumulate) {
+  __shared__ float4 redn[RN_SLICES][4];
+  const int cx = threadIdx.x % 4, sy = threadIdx.x / 4;
+  const bool ok = cx * 4 < cols;
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (ok) {
+    for (int r = sy; r < rows; r += 8 * RN_SLICES) {
+      float4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int rr = min(r + u * RN_SLICES, rows - 1);
+        v[u] = *reinterpret_cast<const float4*>(partial + (long)rr * cols + cx * 4);
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (r + u * RN_SLICES < rows) { s.x += v[u].x; s.y += v[u].y; s.z += v[u].z; s.w += v[u].w; }
+    }
+  }
+  redn[sy][cx] = s;
+  __syncthreads();
+  if (sy == 0 && ok) {
+    float4 t = redn[0][cx];
+    for (int y = 1; y < RN_SLICES; ++y) {
+      const float4 v = redn[y][cx];
+      t.x += v.x; t.y += v.y; t.z += v.z; t.w += v.w;
+    }
+    float4* o = reinterpret_cast<float4*>(out + cx * 4);
+    if (accumulate) {
+      const float4 p = *o;
+      t.x += p.x; t.y += p.y; t.z += p.z; t.w += p.w;
+    }
+    *o = t;
+  }
+}
+
 __global__ __launch_bounds__(RR_COLS * RR_SLICES) void reduce_rows_kernel(const float* partial, int rows, int cols,
                                                                           float* out, int accumulate) {
-  reduce_rows_block(partial, rows, cols, out, accumulate, blockIdx.x);
+  if (cols <= 16) reduce_rows_narrow(partial, rows, cols, out, accumulate);
+  else reduce_rows_block(partial, rows, cols, out, accumulate, blockIdx.x);
 }
 
 // Several independent slab reductions in ONE launch (the CBF, node and edge weight-gradient slabs
@@ -61,7 +101,8 @@ __global__ __launch_bounds__(RR_COLS * RR_SLICES) void reduce_rows_kernel(const 
 __global__ __launch_bounds__(RR_COLS * RR_SLICES) void reduce_multi_kernel(ReduceMultiArgs a) {
   int j = 0;
   while (j + 1 < a.njobs && (int)blockIdx.x >= a.blk0[j + 1]) ++j;
-  reduce_rows_block(a.partial[j], a.rows[j], a.cols[j], a.out[j], a.accumulate[j], (int)blockIdx.x - a.blk0[j]);
+  if (a.cols[j] <= 16) reduce_rows_narrow(a.partial[j], a.rows[j], a.cols[j], a.out[j], a.accumulate[j]);
+  else reduce_rows_block(a.partial[j], a.rows[j], a.cols[j], a.out[j], a.accumulate[j], (int)blockIdx.x - a.blk0[j]);
 }
 
 DEV void adam_block(const AdamArgs& a, int bx) {
@@ -223,22 +264,40 @@ DEV void stats_pack_body(const float* sums, const float* counts, const float* lo
 constexpr int RS_BLOCK = 256;
 __global__ __launch_bounds__(RS_BLOCK) void rollout_stats_kernel(RolloutStatsArgs a) {
   float v[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  // the step records of RS_T steps are requested together (clamped, unconditional), then consumed
+  // in step order: one memory round trip per RS_T steps instead of one per step (the per-env
+  // chain was ~30 us at the headline, on the critical path between the rollout and the backward)
+  constexpr int RS_T = 8;
   for (int b = threadIdx.x; b < a.B; b += RS_BLOCK) {
     bool done = false;
-    for (int t = 0; t < a.T; ++t) {
-      const bool vl = !done;
-      a.valid[t * a.B + b] = vl ? 1 : 0;
-      if (vl) {
-        v[0] += a.cnt[(t * a.B + b) * 2];
-        v[1] += a.cnt[(t * a.B + b) * 2 + 1];
-        v[2] += (float)a.N;
-        if (a.safe) v[3] += a.safe[(t + 1) * a.B + b];
-        if (a.act) {   // a saturated (diverged) agent term: the action loss is not a number
-          const unsigned long long q = a.act[t * a.B + b];
-          v[4] += (double)q >= FX_SAT ? __builtin_nanf("") : (float)((double)q / FX_ACT);
-        }
+    for (int t0 = 0; t0 < a.T; t0 += RS_T) {
+      float c0[RS_T], c1[RS_T], sf[RS_T];
+      unsigned long long dq[RS_T], aq[RS_T];
+#pragma unroll
+      for (int u = 0; u < RS_T; ++u) {
+        const int t = min(t0 + u, a.T - 1);
+        c0[u] = a.cnt[(t * a.B + b) * 2];
+        c1[u] = a.cnt[(t * a.B + b) * 2 + 1];
+        sf[u] = a.safe ? a.safe[(t + 1) * a.B + b] : 0.f;
+        aq[u] = a.act ? a.act[t * a.B + b] : 0ull;
+        dq[u] = a.dist[t * a.B + b];
       }
-      done = done || ((float)((double)a.dist[t * a.B + b] / FX_DIST) / (float)a.N < a.thr);
+#pragma unroll
+      for (int u = 0; u < RS_T; ++u) {
+        const int t = t0 + u;
+        if (t >= a.T) break;
+        const bool vl = !done;
+        a.valid[t * a.B + b] = vl ? 1 : 0;
+        if (vl) {
+          v[0] += c0[u];
+          v[1] += c1[u];
+          v[2] += (float)a.N;
+          if (a.safe) v[3] += sf[u];
+          if (a.act)     // a saturated (diverged) agent term: the action loss is not a number
+            v[4] += (double)aq[u] >= FX_SAT ? __builtin_nanf("") : (float)((double)aq[u] / FX_ACT);
+        }
+        done = done || ((float)((double)dq[u] / FX_DIST) / (float)a.N < a.thr);
+      }
     }
   }
   __shared__ float red[6][RS_BLOCK];
