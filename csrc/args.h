@@ -192,12 +192,12 @@ struct CbfMatchArgs {
   const int* idx;        // (T+G1, B, N, K) neighbour slots (G1 = 1: h' on the recomputed kNN)
   int T, B, N, K;
   int mode;              // 0: reuse_nbr_idx (match by neighbour id), 1: recomputed kNN (slot k <-> k)
-  int phase;             // 0: count extras per row, 1: write map1 / src
-  int* cnt;              // (T*B*N) extras per (t,b,i) row (phase 0 out, optional)
+  int phase;             // 0: match, counts, map1 / src except the extras' offsets; 1: the extras' offsets
+  int* cnt;              // (T*B*N) extras per (t,b,i) row (phase 0 out, phase 1 in)
   const int* off;        // (T*B*N) exclusive offsets (phase 1 in; null: computed in-kernel from bsum)
   int* bsum;             // (gridDim.x) extras per block (phase 0 out, phase 1 in)
   int* nev;              // [E + extras] (phase 1 out, written by the last block)
-  int* map1;             // (E) evaluation index of the h' partner of main slot e
+  int* map1;             // (E) evaluation index of the h' partner of main slot e (phase 0 null: counts only)
   int* src;              // (2E) source slot whose h' is evaluation u, or -1
 };
 

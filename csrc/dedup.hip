@@ -57,20 +57,33 @@ DEV int block_excl_scan(int v, int* total) {
   return pre + x - v;
 }
 
-// Sum of p[0..n) by the whole block (fixed order per thread + fixed tree: deterministic).
+// Sum of p[0..n) by the whole block (integer sums: exact in any order). Every block of a grid
+// sums the counts of all blocks before it, so the loads are issued 8 per thread at a time (one
+// dependent round trip per 8 x NT counts; the 4,608 match blocks at the headline took ~20 us
+// with one load per round trip).
 template <int NT>
 DEV int block_sum_prefix(const int* p, int n) {
   int s = 0;
-  for (int q = threadIdx.x; q < n; q += NT) s += p[q];
+  for (int q0 = threadIdx.x; q0 < n; q0 += 8 * NT) {
+    int v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = q0 + u * NT < n ? p[q0 + u * NT] : 0;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s += v[u];
+  }
   int tot;
   (void)block_excl_scan<NT>(s, &tot);
   return tot;
 }
 
-// One thread per (t,b,i) row, MATCH_BLOCK consecutive rows per block: the block's slot rows of
-// step t and step t+1 (each one contiguous segment) are staged in LDS with coalesced loads, the
-// matching runs in registers, and map1 / the next row's src go back through LDS as coalesced
-// segments (extras are written directly: a few percent of the slots).
+// One thread per (t,b,i) row, MATCH_BLOCK consecutive rows per block. Phase 0 stages the block's
+// slot rows of step t and step t+1 (each one contiguous segment) in LDS with coalesced loads,
+// matches in registers and writes everything that does not need the global extras offsets:
+// map1 of the matched slots (final), a placeholder -1 - x for the row's x-th unmatched slot, the
+// next step's src (final), the per-row extras counts and the block sums. Phase 1 turns the
+// placeholders of the rows that have extras (a quarter of the rows at the headline) into
+// E + offset and writes their src entries -- it reads one count per row instead of re-staging and
+// re-matching both steps' slot rows (round 6; the two phases were 2 x 75 us at the headline).
 __global__ __launch_bounds__(MATCH_BLOCK) void cbf_match_kernel(CbfMatchArgs a) {
   __shared__ int s0[MATCH_BLOCK * 16], s1[MATCH_BLOCK * 16];
   const long BN = (long)a.B * a.N;
@@ -82,14 +95,44 @@ __global__ __launch_bounds__(MATCH_BLOCK) void cbf_match_kernel(CbfMatchArgs a) 
   const int nr = (int)min((long)MATCH_BLOCK, rows - row0);
   const long e00 = row0 * K;
   const int ns = nr * K;
+  const int lr = threadIdx.x;
+  const long row = row0 + lr;
+  const bool live = lr < nr;
+  if (a.phase == 1) {
+    // extras offset of this row: exclusive scan over the rows (in-kernel when off is null: block
+    // prefix from the phase-0 block sums + the block-local scan; exact integers, deterministic)
+    const int cnt = live ? a.cnt[row] : 0;
+    long roff = 0;
+    if (a.off) {
+      roff = live ? a.off[row] : 0;
+    } else {
+      const int pre = block_sum_prefix<MATCH_BLOCK>(a.bsum, blockIdx.x);
+      int tot;
+      const int ex = block_excl_scan<MATCH_BLOCK>(cnt, &tot);
+      roff = (long)pre + ex;
+      if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0 && a.nev) *a.nev = (int)(E + pre + tot);
+    }
+    if (live && cnt > 0) {
+      const long e0 = row * K, off = E + roff;
+      int mv[16];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) mv[k] = k < K ? a.map1[e0 + k] : 0;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        if (k < K && mv[k] < 0) {
+          const long u = off - 1 - mv[k];          // placeholder -1 - x -> extra x of the row
+          a.map1[e0 + k] = (int)u;
+          a.src[u] = (int)(e0 + k);
+        }
+      }
+    }
+    return;
+  }
   // next-step rows exist for rows < (T-1)*BN
   const int nn = (int)max(0L, min((long)nr, (long)(a.T - 1) * BN - row0));
   for (int q = threadIdx.x; q < ns; q += MATCH_BLOCK) s0[q] = a.idx[e00 + q];
   for (int q = threadIdx.x; q < nn * K; q += MATCH_BLOCK) s1[q] = a.idx[e00 + NKB + q];
   __syncthreads();
-  const int lr = threadIdx.x;
-  const long row = row0 + lr;
-  const bool live = lr < nr;
   const bool has_next = lr < nn;
   int m[16];
 #pragma unroll
@@ -118,29 +161,13 @@ __global__ __launch_bounds__(MATCH_BLOCK) void cbf_match_kernel(CbfMatchArgs a) 
     }
   }
   const int cnt = live ? K - nmatch : 0;
-  if (a.phase == 0) {
-    if (live && a.cnt) a.cnt[row] = cnt;
-    int tot;
-    (void)block_excl_scan<MATCH_BLOCK>(cnt, &tot);
-    if (threadIdx.x == 0 && a.bsum) a.bsum[blockIdx.x] = tot;
-    return;
-  }
-  // extras offset of this row: exclusive scan over the rows (in-kernel when off is null: block
-  // prefix from the phase-0 block sums + the block-local scan; exact integers, deterministic)
-  long roff = 0;
-  if (a.off) {
-    roff = live ? a.off[row] : 0;
-  } else {
-    const int pre = block_sum_prefix<MATCH_BLOCK>(a.bsum, blockIdx.x);
-    int tot;
-    const int ex = block_excl_scan<MATCH_BLOCK>(cnt, &tot);
-    roff = (long)pre + ex;
-    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0 && a.nev) *a.nev = (int)(E + pre + tot);
-  }
-  __syncthreads();                         // s0 / s1 are reused as output staging
+  if (live && a.cnt) a.cnt[row] = cnt;
+  int tot;
+  (void)block_excl_scan<MATCH_BLOCK>(cnt, &tot);   // (its barriers also end the reads of s0 / s1)
+  if (threadIdx.x == 0 && a.bsum) a.bsum[blockIdx.x] = tot;
+  if (!a.map1) return;                             // counts only
   const long e0 = row * K;
   if (live) {
-    const long off = E + roff;
     int x = 0;
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
@@ -148,8 +175,7 @@ __global__ __launch_bounds__(MATCH_BLOCK) void cbf_match_kernel(CbfMatchArgs a) 
       if (m[k] >= 0) {
         s0[lr * K + k] = (int)(e0 + NKB + m[k]);
       } else {
-        s0[lr * K + k] = (int)(off + x);
-        a.src[off + x] = (int)(e0 + k);
+        s0[lr * K + k] = -1 - x;                   // phase 1: E + the row's offset + x
         ++x;
       }
     }

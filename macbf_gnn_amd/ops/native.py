@@ -523,9 +523,12 @@ def cbf_match(idx, T, map1, src, cnt, *, recomputed=False, nev=None):
         nev = torch.empty(1, dtype=torch.int32, device=idx.device)
     check(nev, torch.int32, (1,), "nev")
     mode = 1 if recomputed else 0
-    _ok(lib().cbf_match(ptr(idx), T, B, N, K, mode, 0, 0, 0, 0, 0, ptr(cnt), 0, stream_handle()), "cbf_match/count")
-    _ok(lib().cbf_match(ptr(idx), T, B, N, K, mode, 1, 0, 0, ptr(map1), ptr(src), ptr(cnt), ptr(nev),
-                        stream_handle()), "cbf_match/fill")
+    rowcnt = _workspace("match_rows", rows * 4, idx.device).view(torch.int32)
+    # phase 0: match + everything but the extras' offsets; phase 1: the offsets (rows with extras)
+    _ok(lib().cbf_match(ptr(idx), T, B, N, K, mode, 0, ptr(rowcnt), 0, ptr(map1), ptr(src), ptr(cnt), 0,
+                        stream_handle()), "cbf_match/match")
+    _ok(lib().cbf_match(ptr(idx), T, B, N, K, mode, 1, ptr(rowcnt), 0, ptr(map1), ptr(src), ptr(cnt), ptr(nev),
+                        stream_handle()), "cbf_match/extras")
     return nev
 
 
