@@ -10,6 +10,7 @@
 # smoke        __graft_entry__.smoke()                          -> smoke.log
 # bench        bench.py defaults (config #3 as stated)          -> bench.log
 # slice        bench.py --envs 8 (the DP=8 per-rank slice)      -> slice.log
+# e16 / e32    bench.py --envs 16 / 32 (the DP=4 / DP=2 per-rank work)
 # cfg2         bench.py --agents 32 --envs 1 --dtype bf16       -> cfg2.log
 # cfg4 / cfg5  config #4 (4096 x 16 fp32) / #5 (3-D + 8 obstacles, fp16)
 # bf16         the headline in bf16
@@ -62,6 +63,8 @@ for s in ${STEPS:-tests smoke bench}; do
       tail -1 $O/smoke.log ;;
     bench) bench bench 300 ;;
     slice) bench slice 300 --envs 8 ;;
+    e16) bench e16 300 --envs 16 ;;              # the per-rank work of config #3 at DP 4
+    e32) bench e32 300 --envs 32 ;;              # ... at DP 2
     cfg2) bench cfg2 300 --agents 32 --envs 1 --steps 30 --dtype bf16 ;;
     cfg2f) bench cfg2f 300 --agents 32 --envs 1 --steps 30 ;;
     cfg4) bench cfg4 300 --agents 4096 --envs 16 ;;
