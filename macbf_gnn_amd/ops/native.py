@@ -295,9 +295,13 @@ def scan_plan(B: int, N: int, K: int, *, Nn: int | None = None, dim: int = 2, pr
     return dict(zip(("bs", "lpa", "glb", "cells", "use_cells", "cell_g", "wave_atomic", "blocks", "lds"), v))
 
 
-def scenario(S, G, *, seed, L, r=C.DIST_MIN_THRES, spread=C.GOAL_SPREAD, max_rounds=256, status=None, obs=None):
+def scenario(S, G, *, seed, L, r=C.DIST_MIN_THRES, spread=C.GOAL_SPREAD, max_rounds=256, status=None, obs=None,
+             lds_free=False):
     """S (B, >=N, W) agent records out (velocity 0), G (B, N, D) goals out; obs (B, M, D) static
-    obstacle points kept > r from every start and goal."""
+    obstacle points kept > r from every start and goal. lds_free: the per-env arrays and cell grid
+    in a global workspace even when they fit LDS (same results) -- a background launch then holds
+    no LDS, so it shares CUs with the 1-workgroup-per-CU kernels it overlaps instead of taking a
+    whole CU's LDS for the grid."""
     B, N, D = G.shape
     W = rec_width(D)
     _records(S, "S", (B, N), W)
@@ -309,7 +313,7 @@ def scenario(S, G, *, seed, L, r=C.DIST_MIN_THRES, spread=C.GOAL_SPREAD, max_rou
         check(obs, torch.float32, (B, M, D), "obs")
     base = (3 * N + M) * D * 4 + 5 * N + 16
     ws, ws_env = None, 0
-    if base + 4 * 2 ** D > 160 * 1024 - 64:
+    if lds_free or base + 4 * 2 ** D > 160 * 1024 - 64:
         # env too large for LDS: the sampler's arrays live in a per-env global workspace with a
         # full-resolution cell grid (same results: acceptance does not depend on the grid)
         span = float(L) + 2.0 * (float(spread) + float(r))

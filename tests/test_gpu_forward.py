@@ -227,3 +227,14 @@ def test_scenario_invariants():
     a = scenario.generate(2, 64, seed=5, iteration=7, device=DEV)
     b = scenario.generate(2, 64, seed=5, iteration=7, device=DEV)
     assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
+
+
+@pytest.mark.parametrize("dim,nobs", [(2, 0), (3, 2)])
+def test_scenario_lds_free_path_is_bitwise_the_lds_path(dim, nobs):
+    """The background sampler keeps its arrays and cell grid in global memory (lds_free): the same
+    starts and goals, bit for bit, as the LDS path (acceptance does not depend on the grid)."""
+    from macbf_gnn_amd.ops import scenario
+    a = scenario.generate(4, 1024, seed=3, iteration=5, device=DEV, dim=dim, num_obstacles=nobs)
+    b = scenario.generate(4, 1024, seed=3, iteration=5, device=DEV, dim=dim, num_obstacles=nobs, background=True)
+    torch.cuda.synchronize()
+    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
