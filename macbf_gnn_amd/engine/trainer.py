@@ -85,8 +85,8 @@ class Trainer:
         # stream gated on the enqueued work both measured slower, docs/PERF.md round 5)
         self._side = (torch.cuda.Stream(device=self.device)
                       if (self.device.type == "cuda" and cfg.prefetch_data) else None)
-        from .. import knobs
-        self._bg_lds_free = bool(knobs.get_int("MACBF_SAMPLER_LDS_FREE", 0))     # A/B
+        # (the sampler's arrays in global memory -- no LDS, so it would share CUs with the kernels it
+        # overlaps -- measured much slower: headline 12.10 vs 10.23-10.28 ms, profiles/r6_runs/r6l/)
         if self.device.type == "cuda":
             from .hip_engine import HipEngine
             self._ok = torch.ones(1, dtype=torch.int32, device=self.device)
@@ -100,7 +100,7 @@ class Trainer:
             ckpt.load(self, cfg.model_path)
 
     # ------------------------------------------------------------------ data
-    def sample(self, it: Optional[int] = None, background: bool = False):
+    def sample(self, it: Optional[int] = None):
         """B scenarios for this rank -> (s0, g, obstacles or None): the parallel RSA sampler, on
         the device (HIP kernel) or in the host runtime (C++), identical for one seed."""
         it = self.step_count if it is None else it
@@ -108,14 +108,13 @@ class Trainer:
         B, N = cfg.num_envs, cfg.num_agents
         from ..ops import scenario
         return scenario.generate(B, N, seed=cfg.seed, iteration=it, rank=self.dp.rank, device=self.device,
-                                 dim=cfg.dim, num_obstacles=cfg.num_obstacles, obstacle_points=cfg.obstacle_points,
-                                 background=background)
+                                 dim=cfg.dim, num_obstacles=cfg.num_obstacles, obstacle_points=cfg.obstacle_points)
 
     def _sample_async(self, it: int):
         """Launch the (parameter-independent) scenario sampler for iteration ``it`` on a side
         stream: it overlaps the current iteration's rollout instead of serialising with it."""
         with torch.cuda.stream(self._side):
-            data = self.sample(it, background=self._bg_lds_free)
+            data = self.sample(it)
             ev = torch.cuda.Event()
             ev.record(self._side)
         return it, data, ev

@@ -299,9 +299,7 @@ def scenario(S, G, *, seed, L, r=C.DIST_MIN_THRES, spread=C.GOAL_SPREAD, max_rou
              lds_free=False):
     """S (B, >=N, W) agent records out (velocity 0), G (B, N, D) goals out; obs (B, M, D) static
     obstacle points kept > r from every start and goal. lds_free: the per-env arrays and cell grid
-    in a global workspace even when they fit LDS (same results) -- a background launch then holds
-    no LDS, so it shares CUs with the 1-workgroup-per-CU kernels it overlaps instead of taking a
-    whole CU's LDS for the grid."""
+    in a global workspace even when they fit LDS (the large-env path; same results)."""
     B, N, D = G.shape
     W = rec_width(D)
     _records(S, "S", (B, N), W)

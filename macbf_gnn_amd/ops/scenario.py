@@ -38,7 +38,7 @@ def obstacles(B, N, *, dim, num_obstacles, points, seed, device):
 
 
 def generate(B, N, *, seed=0, iteration=0, rank=0, device=None, out=None, dim=2, num_obstacles=0,
-             obstacle_points=12, background=False):
+             obstacle_points=12):
     """-> (s0 (B,N,2D), g (B,N,D), obstacles (B,M,D) or None). HIP device: the on-device
     parallel RSA kernel; CPU: the same process in the host runtime (bit-identical output).
     Obstacle points are fixed conflict points for starts and goals."""
@@ -57,6 +57,5 @@ def generate(B, N, *, seed=0, iteration=0, rank=0, device=None, out=None, dim=2,
         G = torch.empty(B, N, dim, dtype=torch.float32, device=device)
     else:
         S, G = out
-    native.scenario(S, G, seed=key, L=E.side_length(N, dim), r=C.DIST_MIN_THRES, spread=C.GOAL_SPREAD, obs=obs,
-                    lds_free=background)
+    native.scenario(S, G, seed=key, L=E.side_length(N, dim), r=C.DIST_MIN_THRES, spread=C.GOAL_SPREAD, obs=obs)
     return native.from_records(S), G, obs

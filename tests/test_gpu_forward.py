@@ -230,11 +230,19 @@ def test_scenario_invariants():
 
 
 @pytest.mark.parametrize("dim,nobs", [(2, 0), (3, 2)])
-def test_scenario_lds_free_path_is_bitwise_the_lds_path(dim, nobs):
-    """The background sampler keeps its arrays and cell grid in global memory (lds_free): the same
-    starts and goals, bit for bit, as the LDS path (acceptance does not depend on the grid)."""
+def test_scenario_global_workspace_path_is_bitwise_the_lds_path(dim, nobs):
+    """The sampler's global-workspace path (large envs; forced here with lds_free) gives the same
+    starts and goals, bit for bit, as the LDS path at 1,024 agents (acceptance does not depend on
+    the grid)."""
+    from macbf_gnn_amd import env as E
     from macbf_gnn_amd.ops import scenario
-    a = scenario.generate(4, 1024, seed=3, iteration=5, device=DEV, dim=dim, num_obstacles=nobs)
-    b = scenario.generate(4, 1024, seed=3, iteration=5, device=DEV, dim=dim, num_obstacles=nobs, background=True)
+    B, N = 4, 1024
+    obs = (scenario.obstacles(B, N, dim=dim, num_obstacles=nobs, points=12, seed=9, device=DEV) if nobs else None)
+    out = []
+    for lds_free in (False, True):
+        S = torch.empty(B, N, native.rec_width(dim), device=DEV)
+        G = torch.empty(B, N, dim, device=DEV)
+        native.scenario(S, G, seed=1234, L=E.side_length(N, dim), obs=obs, lds_free=lds_free)
+        out.append((S, G))
     torch.cuda.synchronize()
-    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
+    assert torch.equal(out[0][0], out[1][0]) and torch.equal(out[0][1], out[1][1])
