@@ -17,6 +17,7 @@
 # ab:<NAME>    interleaved headline+slice A/B of alt_so/NAME/_C.so vs the in-tree build (REPS, ABARGS)
 # prof         kernel trace of the headline    -> prof/kernel_stats.csv, prof_summary.txt
 # prof_slice   kernel trace of the slice       -> prof_slice/...
+# prof_cfg2    kernel trace of config #2 (bf16) -> prof_cfg2/...
 # sol / sol_slice / sol_cfg4 / sol_cfg5   two-pass PMC speed-of-light table (scripts/gpu_sol.sh) -> sol_*/sol.md
 # configs      every BASELINE config (scripts/gpu_configs.sh)   -> configs/configs.jsonl
 # dp:N         N ranks of the bench on this one GPU over gloo (launch / DP rehearsal, strong default)
@@ -84,6 +85,7 @@ for s in ${STEPS:-tests smoke bench}; do
       done ;;
     prof) prof prof ;;
     prof_slice) prof prof_slice --envs 8 ;;
+    prof_cfg2) prof prof_cfg2 --agents 32 --envs 1 --dtype bf16 ;;
     sol) TAG=${TAG:-r6}/sol ARGS="" bash scripts/gpu_sol.sh > $O/sol.log 2>&1 || { echo "STOP sol"; tail -5 $O/sol.log; exit 1; }; head -30 $O/sol/sol.md ;;
     sol_slice) TAG=${TAG:-r6}/sol_slice ARGS="--envs 8" bash scripts/gpu_sol.sh > $O/sol_slice.log 2>&1 || { echo "STOP sol_slice"; tail -5 $O/sol_slice.log; exit 1; }; head -30 $O/sol_slice/sol.md ;;
     sol_cfg4) TAG=${TAG:-r6}/sol_cfg4 ARGS="--agents 4096 --envs 16" bash scripts/gpu_sol.sh > $O/sol_cfg4.log 2>&1 || { echo "STOP sol_cfg4"; tail -5 $O/sol_cfg4.log; exit 1; }; head -30 $O/sol_cfg4/sol.md ;;

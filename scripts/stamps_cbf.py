@@ -15,7 +15,8 @@ import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
-PHASES = ["p0", "p1", "p2", "p3", "p4", "p5"]   # cbf_bwd: fwd A dH2 B dH1 CD; cbf_bwd16: fwd A dH2+dH1+dF BC
+PHASES = ["p0", "p1", "p2", "p3", "p4", "p5"]   # cbf_bwd: fwd A dH2 B dH1 CD; cbf_bwd16: fwd A dH2+dH1+dF BC;
+#                                                 cbf_bwd_pw: fwd, head + image A + dW3, dH2 + dH1 + dF, image B + dW2 + dW1f
 
 
 def main():
@@ -63,13 +64,19 @@ def main():
         orig(*x, **k)
         orig(*x, stamps=st, **k)
         torch.cuda.synchronize()
-        st = st.view(-1, 8).double().cpu()
+        st = st.view(nb, nw, 8).double().cpu()
+        busy_w = int((st[:, :, 7].sum(0) > 0).sum())    # the per-wave-dW kernel runs 4 waves
+        st = st[:, :busy_w].reshape(-1, 8)
+        st = st[st[:, 7] > 0]
         nch = st[:, 7].clamp(min=1)
         per = st[:, :6] / nch[:, None]
         med = per.median(dim=0).values
         tot = st[:, :6].sum(1)
         res = {p: round(float(v)) for p, v in zip(PHASES, med)}
         res["sum_per_chunk"] = round(float(med.sum()))
+        # a chunk is 16 evaluations per wave: per CU 16 x (waves) evaluations per chunk time
+        res["waves"] = busy_w
+        res["cu_cycles_per_128_evals"] = round(float(med.sum()) * 128 / (16 * busy_w))
         res["chunks_per_wave"] = float(nch.median())
         res["slowest_wave_cycles"] = round(float(tot.max()))
         out[mode] = res
