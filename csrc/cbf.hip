@@ -911,13 +911,8 @@ static void launch_cbf_bwd(const CbfBwdArgs& a, int num_blocks, hipStream_t st) 
 }  // namespace mb
 
 #include "cbf16.h"
-#include "cbfpw.h"
-
-// CBF backward over the active records: per-wave weight gradients (cbfpw.h) or the 8-wave
-// cross-wave stage kernel (cbf16.h)
-#ifndef MB_CBF_PW
-#define MB_CBF_PW 0
-#endif
+// (A barrier-free variant with per-wave, register-resident weight gradients -- 4 waves, one per
+// SIMD -- passed the oracle tests and lost 12.3 vs 10.2 ms: docs/PERF.md round 6, git history.)
 
 extern "C" int MB_SYM(cbf_bwd)(const mb::CbfBwdArgs* a, int num_blocks, hipStream_t st) {
   using namespace mb;
@@ -925,13 +920,8 @@ extern "C" int MB_SYM(cbf_bwd)(const mb::CbfBwdArgs* a, int num_blocks, hipStrea
   if (a->K > 16 || a->K < 1 || a->passes < 1 || a->passes > 2) return -1;
   if (a->rec) {   // 16x16x32 backward over cbf_compact's records (csrc/cbf16.h)
     if (a->fused || !a->nact || !a->wrm16 || !a->w16) return -5;
-    if constexpr (MB_CBF_PW != 0) {
-      if (a->dim == 3) launch_cbf_bwd_pw<3>(*a, num_blocks, st);
-      else launch_cbf_bwd_pw<2>(*a, num_blocks, st);
-    } else {
-      if (a->dim == 3) launch_cbf_bwd16<3>(*a, num_blocks, st);
-      else launch_cbf_bwd16<2>(*a, num_blocks, st);
-    }
+    if (a->dim == 3) launch_cbf_bwd16<3>(*a, num_blocks, st);
+    else launch_cbf_bwd16<2>(*a, num_blocks, st);
     return (int)hipGetLastError();
   }
   if (a->fused && (a->passes != 2 || !a->dang || !a->counts)) return -2;
