@@ -295,10 +295,12 @@ def test_full_step_4096_agents_matches_oracle():
     assert torch.isfinite(torch.as_tensor(float(stats["loss_total"])))
 
 
-@pytest.mark.parametrize("G,N,K,Nn", [(3, 40, 12, 40), (2, 1024, 12, 1120), (1, 6000, 12, 6000)])
+@pytest.mark.parametrize("G,N,K,Nn", [(3, 40, 12, 40), (2, 1024, 12, 1120), (1, 6000, 12, 6000), (2, 64, 1, 64),
+                                       (3, 700, 16, 700), (2, 4096, 12, 4096)])
 def test_rev_csr_matches_sorted_reference(G, N, K, Nn):
-    """Reverse CSR (incoming non-self edges per target node, sorted by edge id): the LDS-sorted
-    path (N*K <= 65536) and the global-memory path (larger graphs) against torch."""
+    """Reverse CSR (incoming non-self edges per target node, sorted by edge id): the register-held
+    path (N*K <= 16384: the headline's 1024 x 12 graphs), the LDS insertion-sort path (4096 x 12)
+    and the global-memory path (larger graphs) against torch."""
     gen = torch.Generator().manual_seed(G * N)
     idx = torch.randint(0, Nn, (G, N, K), generator=gen, dtype=torch.int32)
     idx[:, :, 0] = torch.arange(N, dtype=torch.int32)          # self at slot 0
