@@ -109,7 +109,8 @@ DEV int opaque_zero() {
 // "-DMB_DIAG=<bits>"), never set in production: 1 phase clocks of the 32x32x16 backward kernels
 // (MB_STAMPS), 2 per-record forward sums of the 16x16x32 CBF backward (scripts/check_cbf16.py), 4 the
 // 16x16x32 node backward without its dL/dpooled stores (phase clocks), 8 the kNN scan's cell search
-// box shrunk to 0.7x (negative check: the oracle tests must fail, tests/test_gpu_scan_plans.py).
+// box shrunk to 0.7x (negative check: the oracle tests must fail, tests/test_gpu_scan_plans.py), 16
+// the controller step without its pooled / argmax stores (phase clocks).
 #ifndef MB_DIAG
 #define MB_DIAG 0
 #endif

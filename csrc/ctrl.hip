@@ -379,6 +379,10 @@ DEV PoolDst pool_dst(const CtrlArgs& a, const AgentBase& ab, int g0, int APW, in
 
 template <bool IS_X3, bool GPOOL>
 DEV void pool_store(const PoolDst& d, int nt, int pw_) {
+  if constexpr ((MB_DIAG & 16) != 0) {           // diagnostics build: no pooled / argmax stores
+    if (d.ok && pw_ == 0x7ffffff0) d.prow[32 * nt] = (h16)0.f;   // (keeps the pool computed)
+    return;
+  }
   if (!d.ok) return;
   const float pv = __int_as_float(pw_ & -16);
   const h16 ph = (h16)pv;
