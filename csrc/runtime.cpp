@@ -363,6 +363,13 @@ class BpttDriver {
     wpack_ = U("ctrl_w"); f_ew1f_ = (int)I("f_ew1f"); f_ew2tn_ = (int)I("f_ew2tn");
     dt_ = F("dt"); sqrt3_ = F("sqrt3");
     node_chunk_ = (int)I("node_chunk");
+    // per-step slab rows (small grids): step t's node / edge workgroups write rows (T-1-t) x grid
+    // of the slabs instead of accumulating into one row per workgroup
+    step_rows_ = c.contains("step_rows") ? (int)I("step_rows") : 0;
+    node_part_ = c.contains("node_part") ? I("node_part") : 0;
+    edge_part_ = c.contains("edge_part") ? I("edge_part") : 0;
+    if (step_rows_ && (node_part_ <= 0 || edge_part_ <= 0))
+      throw std::invalid_argument("BpttDriver: step_rows needs the slab row sizes");
     fused_ = c.contains("fused_step") ? (int)I("fused_step") : 0;
     if (fused_ && (node_chunk_ != 32 || nb_node_ != nb_edge_))
       throw std::invalid_argument("BpttDriver: the fused step needs 32-agent chunks and one grid");
@@ -401,6 +408,10 @@ class BpttDriver {
         a.dt = dt_; a.sqrt3 = sqrt3_;
         a.dP = P<h16>(dP_); a.dp_env = (long)N_ * prow_; a.ego = P<float4>(ego_); a.partial = P<float>(part_node_);
         a.init = t == T - 1;     // the first step of the reverse loop writes the slabs
+        if (step_rows_) {
+          a.partial += (long)(T - 1 - t) * nb_node_ * node_part_;
+          a.init = 1;
+        }
         a.chunk = node_chunk_;
         a.wrm16 = P<const h16>(nw16_);
         a.K = K_;
@@ -430,6 +441,10 @@ class BpttDriver {
         a.dEc = P<float4>(dEc_) + (long)(t & 1) * BN * K_ * R_; a.de_env = nk; a.partial = P<float>(part_edge_);
         a.qsplit = qsplit_;
         a.init = t == T - 1;
+        if (step_rows_) {
+          a.partial += (long)(T - 1 - t) * nb_edge_ * edge_part_;
+          a.init = 1;
+        }
         a.w16 = fused_ ? nullptr : P<const h16>(ew16_);   // (the fused step keeps its own edge phase)
       }
       if (fused_) {      // node + edge backward of the same 32-agent chunks in one launch
@@ -448,6 +463,8 @@ class BpttDriver {
 
  private:
   int B_, N_, Nn_, K_, D_, R_, Tmax_, prec_, prow_, nb_node_, nb_edge_, qsplit_, node_chunk_ = 0, fused_ = 0;
+  int step_rows_ = 0;
+  long node_part_ = 0, edge_part_ = 0;
   u64 pooled_, S_, G_, A_, dS_, Gb_, valid_, idx_, argmax_, rptr_, redges_, wrm_, wvec_, act_scale_, dP_, ego_, dEc_;
   u64 part_node_, part_edge_, wpack_, gscale_ = 0, ew16_ = 0, nw16_ = 0;
   int o1_, o2_, o3_, o4_, f_ew1f_, f_ew2tn_;

@@ -34,6 +34,7 @@ from ..ops.weights import PackedWeights
 # action-loss weight of the total loss (core.py:174-184 via train.py:93,98); the node backward
 # divides it by the all-reduced action count on the device
 ACT_COEF = C.LOSS_SCALE * C.LOSS_WEIGHTS[4]
+STEP_ROWS_BYTES = 64 << 20      # per-step slab rows for BPTT grids whose T x rows fit this (HipEngine.step_rows)
 STATS_COLS = 18       # StepStats row: 10 loss sums | 3 counts | 3 local | skipped | loss scale
 STATS_RING = 256
 
@@ -219,7 +220,16 @@ class HipEngine:
         # slab rows each BPTT path writes (and the slab reduction reads): exactly those, so rows no
         # path writes are never summed
         self.slab_rows = (self.nb_node, self.nb_edge) if Gp == 1 else (Gp * self.grp_nb[0], Gp * self.grp_nb[1])
+        # small grids (config #2: one node and 16 edge workgroups): every reverse step writes its own
+        # slab rows (no read-modify-write of the previous step's partial at each kernel's end) and
+        # the tail reduction sums T x rows -- at most a few MB; large grids keep one accumulated row
+        # per workgroup (T x 256 rows would cost the reduction more than the RMW costs the chain)
+        self.step_rows = bool(Gp == 1 and self.bptt and
+                              T * (self.nb_node * native.CTRL_NODE_PARTIAL + self.nb_edge * native.CTRL_EDGE_PARTIAL) * 4
+                              <= STEP_ROWS_BYTES)
         rows_n, rows_e = self.slab_rows
+        if self.step_rows:
+            rows_n, rows_e = T * rows_n, T * rows_e
         self.part_node = torch.zeros(max(rows_n, B), native.CTRL_NODE_PARTIAL, dtype=f32, device=dev)
         self.part_edge = torch.zeros(max(rows_e, B), native.CTRL_EDGE_PARTIAL, dtype=f32, device=dev)
         self.gstreams = [torch.cuda.Stream(device=dev) for _ in range(Gp - 1)]
@@ -723,7 +733,13 @@ class HipEngine:
             self._nb_parts = (pn, pe)
         tm.mark("bptt")
         # ---- weight-gradient slabs (+ the loss partials) -> flat grad, one reduction launch
-        pnode, pedge = (self.part_node[: slab_rows[0]], self.part_edge[: slab_rows[1]]) if self.bptt else self._nb_parts
+        if self.bptt:
+            rn, re_ = slab_rows
+            if self.step_rows:
+                rn, re_ = T * rn, T * re_
+            pnode, pedge = self.part_node[:rn], self.part_edge[:re_]
+        else:
+            pnode, pedge = self._nb_parts
         jobs = ([(part_cbf, self.red_cbf, False)] if not split else []) + [(pnode, self.red_node, False),
                                                                            (pedge, self.red_edge, False)]
         if self.dedup:
@@ -791,7 +807,8 @@ class HipEngine:
                    "ego": (self.ego, torch.float32, (B, N, W)), "dEc": (self.dEc, torch.float32, (2, B, N, K, W))}
             for name, (t, dt, shape) in exp.items():
                 native.check(t, dt, shape, name)
-            if self.part_node.shape[0] < self.nb_node or self.part_edge.shape[0] < self.nb_edge:
+            rows = T if self.step_rows else 1
+            if self.part_node.shape[0] < rows * self.nb_node or self.part_edge.shape[0] < rows * self.nb_edge:
                 raise native.NativeError("controller slab buffers too small")
             pw = self.pw
             c = {k: native.ptr(v[0]) for k, v in exp.items()}
@@ -805,6 +822,7 @@ class HipEngine:
                 ctrl_w=native.ptr(pw.ctrl_w), f_ew1f=int(pw.ctrl_off["ew1f"]), f_ew2tn=int(pw.ctrl_off["ew2tn"]),
                 dt=float(C.TIME_STEP), sqrt3=float(C.SQRT3),
                 node_chunk=int(native.node_bwd_chunk(B * N, self.dev)),
+                step_rows=int(self.step_rows), node_part=native.CTRL_NODE_PARTIAL, edge_part=native.CTRL_EDGE_PARTIAL,
                 fused_step=int(native.bwd_step_fused(B * N, self.dev)),
                 ctrl_w16=native.ptr(self.eb16_w) if self.eb16_w is not None else 0,
                 node_rm16=native.ptr(self._node16(B * N)),
@@ -815,7 +833,12 @@ class HipEngine:
     def _bptt_chain(self, T, sl, valid_u8, gs, rptr3, redges3, part_node, part_edge, nbn, nbe, red_done, ts, st):
         """Reverse-time BPTT over the envs `sl` on stream `st`: G_t = dL/ds_t from G_{t+1}."""
         pw, K = self.pw, self.K
+        step_rows = self.step_rows and sl == slice(0, self.B)
         for t in range(T - 1, -1, -1):
+            pn, pe, init = part_node, part_edge, t == T - 1
+            if step_rows:            # this step's own slab rows, written (not accumulated)
+                r = T - 1 - t
+                pn, pe, init = self.part_node[r * nbn:(r + 1) * nbn], self.part_edge[r * nbe:(r + 1) * nbe], True
             if red_done is not None and t == ts - 1:
                 st.wait_event(red_done)                                # dS[0..ts) from the aux stream
             # G_{t+1}: the direct terms dS_T for t = T-1; else formed in the node kernel's prologue
@@ -827,12 +850,12 @@ class HipEngine:
                            Gout=self.Gb[t + 1][sl], K=K)
             node = dict(pooled=self.pooled[t][sl], S=self.S[t][sl], G=self.G[sl], A=self.A[t][sl], Gn=self.dS[T][sl],
                         valid_t=valid_u8[t][sl], wrm=pw.ctrl_rm, offs=pw.node_rm_off, wvec=pw.ctrl_v,
-                        act_coef=gs * ACT_COEF, dP=self.dP[sl], ego=self.ego[sl], partial=part_node,
-                        act_cnt=self.counts[2:3], prec=self.prec, init=t == T - 1,
+                        act_coef=gs * ACT_COEF, dP=self.dP[sl], ego=self.ego[sl], partial=pn,
+                        act_cnt=self.counts[2:3], prec=self.prec, init=init,
                         gscale=getattr(self.tr, "gscale_dev", None), combine=cmb)
             edge = dict(S=self.S[t][sl], idx=self.idx[t][sl], argmax=self.argmax[t][sl], dP=self.dP[sl], wpack=pw.ctrl_w,
-                        f_ew1f=pw.ctrl_off["ew1f"], f_ew2tn=pw.ctrl_off["ew2tn"], dEc=self.dEc[t & 1][sl], partial=part_edge,
-                        prec=self.prec, init=t == T - 1)
+                        f_ew1f=pw.ctrl_off["ew1f"], f_ew2tn=pw.ctrl_off["ew2tn"], dEc=self.dEc[t & 1][sl], partial=pe,
+                        prec=self.prec, init=init)
             if nbn == nbe and native.bwd_step_fused(self.G[sl].shape[0] * self.N, self.dev):
                 native.ctrl_bwd_step(node, edge, nbn)            # node + edge backward: one launch
             else:
