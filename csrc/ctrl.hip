@@ -2207,7 +2207,18 @@ __global__ __launch_bounds__(SR_WAVES * 64) void rollout_small_kernel(RolloutSma
   const int wave = wave_id();
   int T = -1;                  // horizon, once every env has published its first done step
   bool done = false;           // (thread 0) this env has published
+  // diagnostics builds (MB_STAMPS, c.stamps set): per-wave cycles of each phase summed over the
+  // steps -- 0 scan, 1 edge phase, 2 barrier, 3 node phase, 4 step tail; 15 steps
+  unsigned long long ph[16] = {}, tck = 0;
+  auto stamp = [&](int k) {
+    if constexpr (MB_STAMPS) {
+      const unsigned long long tn = __builtin_amdgcn_s_memtime();
+      ph[k] += tn - tck;
+      tck = tn;
+    }
+  };
   for (int t = 0; t <= Tmax; ++t) {
+    if constexpr (MB_STAMPS) { tck = __builtin_amdgcn_s_memtime(); ph[15] += 1; }
     // one relaxed poll of the done count per step; once it reads B, ONE agent-scope acquire
     // (pairs with the publishers' release adds below) before ctl[1] is read
     if (threadIdx.x == 0) {
@@ -2225,6 +2236,7 @@ __global__ __launch_bounds__(SR_WAVES * 64) void rollout_small_kernel(RolloutSma
     const float4* St = c.S + tb * Nn * REC<D>;
     small_scan<D>(ra, St, N, Nn, K, t < Tmax || ra.knn_tail, t < Tmax, ra.idx + tb * nk, ra.dang + tb * nk,
                   ra.cnt + tb * 2, ra.safe ? ra.safe + tb : nullptr, L);
+    stamp(0);
     if (tail) break;
     // env b's view of step t: the per-step controller bodies over this env's agents only
     CtrlArgs e = c;
@@ -2240,8 +2252,11 @@ __global__ __launch_bounds__(SR_WAVES * 64) void rollout_small_kernel(RolloutSma
     e.argmax = c.argmax + tb * N * 128; e.am_env = (long)N * 128;
     e.noise_t = t;
     ctrl_fwd_groups<D, true>(e, wl, wn, vl, nullptr, wave, SR_WAVES);
+    stamp(1);
     __syncthreads();                                // the env's pooled rows -> node phase
+    stamp(2);
     ctrl_node_groups<D>(e, wn, vl, wave, SR_WAVES);
+    stamp(3);
     // s_{t+1} (read by this workgroup only) and the env's sum atomics (device scope) complete
     // before the barrier; the workgroup-scope barrier is enough for both
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -2255,6 +2270,11 @@ __global__ __launch_bounds__(SR_WAVES * 64) void rollout_small_kernel(RolloutSma
         __hip_atomic_fetch_add(ra.ctl, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
+    stamp(4);
+  }
+  if constexpr (MB_STAMPS) {
+    if (c.stamps && (threadIdx.x & 63) == 0)
+      for (int k = 0; k < 16; ++k) c.stamps[((long)b * SR_WAVES + wave) * 16 + k] = ph[k];
   }
 }
 

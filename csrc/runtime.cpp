@@ -66,6 +66,7 @@ class RolloutDriver {
     scan_ws_ = U("scan_ws"); scan_ws_env_ = I("scan_ws_env");
     apw_ = (int)I("apw");
     small_ctl_ = U("small_ctl"); small_apw_ = (int)I("small_apw"); knn_tail_ = (int)I("knn_tail");
+    small_stamps_ = c.contains("small_stamps") ? U("small_stamps") : 0;
     if (small_ctl_) chk(hipHostMalloc((void**)&host_ctl_, 2 * sizeof(int), hipHostMallocDefault), "hipHostMalloc");
     // early-stop publication (ctrl.hip publish_step): per-step workgroup counters on the device,
     // the per-env sums and a flag per step in host-coherent memory
@@ -192,6 +193,7 @@ class RolloutDriver {
     c.dt = dt_; c.obs_r = obs_r_; c.sqrt3 = sqrt3_;
     c.pooled = P<h16>(pooled_); c.argmax = P<uint8_t>(argmax_);
     c.apw = small_apw_;
+    c.stamps = reinterpret_cast<unsigned long long*>(small_stamps_);   // diagnostics builds only (else 0)
     a.idx = P<int>(idx_); a.dang = P<uint8_t>(dang_); a.cnt = P<float>(cnt_);
     a.safe = safety_ ? P<float>(safe_) : nullptr;
     a.Nn = Nn_; a.Tmax = Tmax_; a.knn_tail = knn_tail_;
@@ -328,7 +330,7 @@ class RolloutDriver {
   float noise_prob_, noise_scale_;
   u64 scan_ws_;
   long scan_ws_env_;
-  u64 small_ctl_ = 0;
+  u64 small_ctl_ = 0, small_stamps_ = 0;
   int small_apw_ = 0, knn_tail_ = 0;
   int* host_ctl_ = nullptr;
   int f_edge_, f_node_, f_fwd_;

@@ -205,6 +205,7 @@ class HipEngine:
         # exploration noise (reference train.py:65-67): counter-based device RNG keyed per iteration
         self.noise_key = torch.zeros(1, dtype=torch.int64, device=dev)
         self.small_ctl = torch.zeros(2, dtype=i32, device=dev)     # persistent rollout: [envs done, max step]
+        self.small_stamps = None          # diagnostics: [env][wave][16] phase clocks of the persistent rollout
         # K = 12, x3: the 16x16x32 controller edge backward (csrc/ctrl16.h, 8-wave workgroups); the
         # 1-pass builds keep the 32x32x16 kernel (70 vs 78 us per call in bf16, 74 vs 89 us fp16 3-D,
         # profiles/r4_validate/). MACBF_EB16=0/1 forces either. Decided before the grids (per-CU residency)
@@ -361,6 +362,7 @@ class HipEngine:
                 scan_ws=native.ptr(scan_ws), scan_ws_env=int(scan_f4),
                 small_ctl=native.ptr(self.small_ctl) if self.small_rollout else 0,
                 small_apw=int(native.small_apw(N)), knn_tail=int(not self.reuse),
+                small_stamps=native.ptr(self.small_stamps),     # diagnostics builds (scripts/stamps_small.py)
                 noise_prob=float(cfg.add_noise_prob), noise_scale=float(cfg.noise_scale),
                 fork_device_scope=1,
                 # early stop published by the controller kernels (no per-step queue marker / copy)
