@@ -2087,7 +2087,11 @@ __global__ __launch_bounds__(NB_WAVES * 64, 1) void ctrl_bwd_step_kernel(CtrlNod
 // =======================================================================================
 constexpr int SR_WAVES = 8;
 constexpr int SMALL_MAXN = 64;
-constexpr int SR_JG = 8;                       // kNN candidates per work item
+// kNN candidates per work item (JG of small_scan): 8 amortise each key over more compares, 2
+// spread a 32-agent env's 32 x 32 pairs over all 512 threads (8 leaves 3 of 4 waves idle: the
+// rank loop was half of the config-#2 step, profiles/r6_runs/r6y/); the rollout takes 2 when the
+// env's work items fit one pass of the workgroup, else 8
+constexpr int SR_JG = 8, SR_JG_SMALL = 2;
 
 struct SmallScanLds {
   float4 tp[SMALL_MAXN], tv[SMALL_MAXN];       // positions / velocities of s_t (z = 0 in 2-D)
@@ -2107,7 +2111,7 @@ DEV void rel_d2(const float4& a, const float4& c, float (&dp)[D]) {
 // kNN / danger / counts / safety of one env's s_t (Sb: the env's records) by the whole workgroup.
 // Same keys, arithmetic and tie order as scan_kernel: (d2 bits, node id) ranks, so the lists are
 // those of the all-pairs oracle; the safety test runs on every pair (no culling pre-test).
-template <int D>
+template <int D, int JG>
 DEV void small_scan(const RolloutSmallArgs& ra, const float4* Sb, int N, int Nn, int K, bool knn, bool dng,
                     int* idx_out, uint8_t* dang_out, float* cnt_out, float* safe_out, SmallScanLds& L) {
   const int tid = threadIdx.x, wave = tid / WAVE, lane = tid & 63;
@@ -2122,14 +2126,14 @@ DEV void small_scan(const RolloutSmallArgs& ra, const float4* Sb, int N, int Nn,
   __syncthreads();
   if (knn) {
     // slot of candidate j in agent i's list = #{j' : key(i, j') < key(i, j)}; keys are unique
-    const int ng = (Nn + SR_JG - 1) / SR_JG;
+    const int ng = (Nn + JG - 1) / JG;
     for (int w = tid; w < N * ng; w += NTH) {
-      const int i = w / ng, j0 = (w - i * ng) * SR_JG;
+      const int i = w / ng, j0 = (w - i * ng) * JG;
       const float4 me = L.tp[i];
-      uint64_t key[SR_JG];
-      int rank[SR_JG];
+      uint64_t key[JG];
+      int rank[JG];
 #pragma unroll
-      for (int u = 0; u < SR_JG; ++u) {
+      for (int u = 0; u < JG; ++u) {
         float dp[D];
         rel_d2<D>(me, L.tp[min(j0 + u, Nn - 1)], dp);
         key[u] = j0 + u < Nn ? knn_key(sqsum<D>(dp), (unsigned)(j0 + u)) : ~0ull;
@@ -2140,10 +2144,10 @@ DEV void small_scan(const RolloutSmallArgs& ra, const float4* Sb, int N, int Nn,
         rel_d2<D>(me, L.tp[jp], dp);
         const uint64_t kp = knn_key(sqsum<D>(dp), (unsigned)jp);
 #pragma unroll
-        for (int u = 0; u < SR_JG; ++u) rank[u] += kp < key[u] ? 1 : 0;
+        for (int u = 0; u < JG; ++u) rank[u] += kp < key[u] ? 1 : 0;
       }
 #pragma unroll
-      for (int u = 0; u < SR_JG; ++u)
+      for (int u = 0; u < JG; ++u)
         if (j0 + u < Nn && rank[u] < K) {
           L.nbr[i * K + rank[u]] = j0 + u;
           idx_out[i * K + rank[u]] = j0 + u;
@@ -2234,8 +2238,12 @@ __global__ __launch_bounds__(SR_WAVES * 64) void rollout_small_kernel(RolloutSma
     const bool tail = t == Tmax || t == T;       // s_T: scan only
     const long tb = (long)t * B + b;
     const float4* St = c.S + tb * Nn * REC<D>;
-    small_scan<D>(ra, St, N, Nn, K, t < Tmax || ra.knn_tail, t < Tmax, ra.idx + tb * nk, ra.dang + tb * nk,
-                  ra.cnt + tb * 2, ra.safe ? ra.safe + tb : nullptr, L);
+    if (N * ((Nn + SR_JG_SMALL - 1) / SR_JG_SMALL) <= SR_WAVES * WAVE)
+      small_scan<D, SR_JG_SMALL>(ra, St, N, Nn, K, t < Tmax || ra.knn_tail, t < Tmax, ra.idx + tb * nk,
+                                 ra.dang + tb * nk, ra.cnt + tb * 2, ra.safe ? ra.safe + tb : nullptr, L);
+    else
+      small_scan<D, SR_JG>(ra, St, N, Nn, K, t < Tmax || ra.knn_tail, t < Tmax, ra.idx + tb * nk, ra.dang + tb * nk,
+                           ra.cnt + tb * 2, ra.safe ? ra.safe + tb : nullptr, L);
     stamp(0);
     if (tail) break;
     // env b's view of step t: the per-step controller bodies over this env's agents only

@@ -14,7 +14,8 @@
 # cfg2         bench.py --agents 32 --envs 1 --dtype bf16       -> cfg2.log
 # cfg4 / cfg5  config #4 (4096 x 16 fp32) / #5 (3-D + 8 obstacles, fp16)
 # bf16         the headline in bf16
-# ab:<NAME>    interleaved headline+slice A/B of alt_so/NAME/_C.so vs the in-tree build (REPS, ABARGS)
+# ab:<NAME>    interleaved headline+slice A/B of alt_so/NAME/_C.so vs the in-tree build (REPS; ABARGS
+#              replaces the headline's bench args, '+' for spaces: env:ABARGS=--agents+32+--envs+1)
 # prof         kernel trace of the headline    -> prof/kernel_stats.csv, prof_summary.txt
 # prof_slice   kernel trace of the slice       -> prof_slice/...
 # prof_cfg2    kernel trace of config #2 (bf16) -> prof_cfg2/...
@@ -75,7 +76,7 @@ for s in ${STEPS:-tests smoke bench}; do
       alt=alt_so/${s#ab:}/_C.so
       for rep in $(seq 1 ${REPS:-2}); do
         for v in cur alt; do
-          for a in "${ABARGS:-}" "--envs 8"; do
+          for a in "${ABARGS//+/ }" "--envs 8"; do
             tag=${s#ab:}_${v}_$(echo "x$a" | tr -c 'a-zA-Z0-9' _)_$rep
             if [ $v = cur ]; then E=X=1; else E=MACBF_EXT=$alt; fi
             env $E timeout -k 10 300 $B $a > $O/$tag.log 2>&1 || { echo "STOP $tag"; tail -3 $O/$tag.log; exit 1; }
