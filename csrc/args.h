@@ -91,6 +91,9 @@ struct CtrlArgs {
   unsigned* pub_flag;                 // host-coherent flag of this step
   unsigned pub_gen;                   // the rollout's generation number
   unsigned long long* stamps;         // diagnostics: phase clocks [block][wave][16] (x3 step; null = off)
+  // the node MLP's activations out, for the cooperative node backward to reuse instead of
+  // recomputing them: agent (b,i) -> acts + (b*na_env + i) * NODE_ACT_BYTES (ctrl.hip), or null
+  unsigned char* acts; long na_env;
 };
 
 // Persistent small-scene rollout (ctrl.hip rollout_small_kernel): one workgroup per env runs
@@ -234,6 +237,8 @@ struct CtrlNodeBwdArgs {
   h16* dP;            long dp_env;    // (b,i,128) dL/dpooled out
   float4* ego;                         // (B,N) records: dL/ds_t from the node path + gain law + action loss
   float* partial;                      // (gridDim.x, CTRL_NODE_PARTIAL) slabs, accumulated
+  const unsigned char* acts; long na_env;   // step t's node activations from the rollout (CtrlArgs.acts)
+                                            // or null: the cooperative kernel recomputes them
   int init;                            // 1: the slabs are written, not accumulated (first BPTT step)
   int chunk;                           // agents per workgroup chunk: 32, 64 or 128 (0 = 128); small
                                        // scenes use smaller chunks to spread over more CUs
@@ -398,6 +403,9 @@ int mb_ctrl_edge_bwd_x3(const mb::CtrlEdgeBwdArgs* a, int num_blocks, hipStream_
 int mb_k16_wg_per_cu(int kernel);
 int mb_k16_wg_per_cu_f16(int kernel);
 int mb_k16_wg_per_cu_x3(int kernel);
+int mb_node_act_bytes();
+int mb_node_act_bytes_f16();
+int mb_node_act_bytes_x3();
 int mb_rev_csr(const mb::CsrArgs* a, hipStream_t st);
 int mb_cbf_match(const mb::CbfMatchArgs* a, hipStream_t st);
 int mb_cbf_dh(const mb::CbfDhArgs* a, int num_blocks, hipStream_t st);

@@ -416,6 +416,10 @@ static py::dict device_info(int dev) {
 static std::string err_str(int e) { return hipGetErrorString((hipError_t)e); }
 
 // workgroups per CU of the 16x16x32 backward kernels of build `prec` (kernel 0 CBF, 1 edge, 2 node)
+static int node_act_bytes(int prec) {
+  return (prec == 2 ? mb_node_act_bytes_x3 : prec == 1 ? mb_node_act_bytes_f16 : mb_node_act_bytes)();
+}
+
 static int k16_wg_per_cu(int prec, int kernel) {
   return (prec == 2 ? mb_k16_wg_per_cu_x3 : prec == 1 ? mb_k16_wg_per_cu_f16 : mb_k16_wg_per_cu)(kernel);
 }
@@ -455,5 +459,6 @@ PYBIND11_MODULE(_C, m) {
   m.def("device_info", &device_info);
   m.def("err_str", &err_str);
   m.def("k16_wg_per_cu", &k16_wg_per_cu);
+  m.def("node_act_bytes", &node_act_bytes);
   m.attr("ARCH") = "gfx950";
 }

@@ -120,6 +120,32 @@ DEV void ctrl_edge_tile(const h16x8& F, const h16* wl, const float* eb2, int lan
 // node MLP forward for 32 agents; returns Y4 (rows 0..3 = the 4 gain pre-activations)
 struct NodeActs { f32x16 Y1[2], Y2[4], Y3[2], Y4; };
 
+// Node activations kept from the rollout (CtrlArgs.acts) for the cooperative node backward: per
+// agent, tiles 0..7 = Y1[2] | Y2[4] | Y3[2] (relu'd, packed hi [| lo] as the backward's to_pk) per
+// lane half h of the 32x32 C layout, then Y4 (raw fp32, 16 per half) -- the C-layout lane (agent r,
+// half h) stores and loads exactly its own registers
+constexpr int NODE_ACT_PKB = X3 ? 64 : 32;
+constexpr int NODE_ACT_BYTES = 16 * NODE_ACT_PKB + 128;
+DEV h16x16 zero_h16x16() {
+  h16x16 z;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) z[j] = (h16)0.f;
+  return z;
+}
+DEV void act_store_pk(unsigned char* base, int tile, int h, const f32x16& c) {
+  const Pk p = to_pk(c);
+  unsigned char* q = base + (tile * 2 + h) * NODE_ACT_PKB;
+  *reinterpret_cast<h16x16*>(q) = p.h;
+  if constexpr (X3) *reinterpret_cast<h16x16*>(q + 32) = p.l;
+}
+DEV Pk act_load_pk(const unsigned char* base, int tile, int h) {
+  const unsigned char* q = base + (tile * 2 + h) * NODE_ACT_PKB;
+  Pk p;
+  p.h = *reinterpret_cast<const h16x16*>(q);
+  if constexpr (X3) p.l = *reinterpret_cast<const h16x16*>(q + 32);
+  return p;
+}
+
 // pool(kk): the pooled-feature B fragment of k-step kk (features 16kk + 8h + j of agent r)
 template <typename PoolFr>
 DEV void node_forward(PoolFr pool, const h16x8& sfrag, const h16* wn, const float* nb2,
@@ -267,7 +293,9 @@ DEV void edge_rel(const EdgeSt<D>& c, float (&rp)[D], float (&rv)[D]) {
 // Node phase of the controller step for the 32-column group at g0 (lane column r = agent
 // g0 + r, r < APW): node MLP (pooled fragments from `pool`), gains 2*sigmoid+0.2, PD law, Euler
 // step, per-env goal-distance and action-loss sums.
-template <int D, typename PoolFr>
+// ACTS: the activations go to a.acts (a separate instantiation: the stores' registers would make
+// the fused x3 step kernel spill where they are not wanted)
+template <int D, bool ACTS, typename PoolFr>
 DEV void node_phase(const CtrlArgs& a, int g0, int APW, int total, PoolFr pool, const h16* wn, const float* nb2,
                     const float* nb3, const float* nb4, int lane) {
   const int r = lane & 31, h = lane >> 5;
@@ -290,6 +318,17 @@ DEV void node_phase(const CtrlArgs& a, int g0, int APW, int total, PoolFr pool, 
   const h16x8 sf = node_state_frag<D>(ex, sv, ok, h);
   NodeActs na;
   node_forward(pool, sf, wn + opaque_zero(), nb2, nb3, nb4, lane, na);
+  if (ACTS && ok) {            // kept for the cooperative node backward (NODE_ACT_BYTES layout)
+    unsigned char* ab = a.acts + ((long)b * a.na_env + i) * NODE_ACT_BYTES;
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt) {
+      act_store_pk(ab, mt, h, na.Y1[mt]);
+      act_store_pk(ab, 6 + mt, h, na.Y3[mt]);
+    }
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) act_store_pk(ab, 2 + mt, h, na.Y2[mt]);
+    *reinterpret_cast<f32x16*>(ab + 16 * NODE_ACT_PKB + 64 * h) = na.Y4;
+  }
   float y4r[8];
   acc_rows8(na.Y4, y4r);                                     // gain pre-activations 0..2D-1
   float dsum = 0.f, asum = 0.f;
@@ -494,7 +533,7 @@ constexpr int CTRL_FWD_DENSE = 1;
 // 0 weight staging (from t0, the kernel start), 1 group prologue loads, per edge tile 2 load issue,
 // 3 edge features, 4 edge MLP, 5 pool + stores; 6 pooled-store wait, 7 node phase; 15 tile count
 // (scripts/stamps_ctrl.py). A separate instantiation: no runtime stamp branches in production.
-template <int D, bool SPLIT, bool GNODE = false, bool DENSE12 = false, bool ST = false>
+template <int D, bool SPLIT, bool GNODE = false, bool DENSE12 = false, bool ST = false, bool ACTS = false>
 DEV void ctrl_fwd_groups(const CtrlArgs& a, const h16* wl, const h16* wn, const float* vl, h16* pools, int grp0,
                          int gstride, unsigned long long t0 = 0) {
   constexpr bool GPOOL = X3 || SPLIT;
@@ -629,7 +668,7 @@ DEV void ctrl_fwd_groups(const CtrlArgs& a, const h16* wl, const h16* wn, const 
       int bb, ii;
       agent_bi(ab, gi - g0, N, bb, ii);
       const h16* prow = a.pooled + (long)bb * a.p_env + (long)ii * PROW + 8 * h;
-      node_phase<D>(a, g0, APW, total, [&](int kk) { return row_fr(prow + 16 * kk, 128); }, wn, nb2, nb3, nb4, lane);
+      node_phase<D, ACTS>(a, g0, APW, total, [&](int kk) { return row_fr(prow + 16 * kk, 128); }, wn, nb2, nb3, nb4, lane);
       stamp(7);
       continue;
     }
@@ -647,7 +686,7 @@ DEV void ctrl_fwd_groups(const CtrlArgs& a, const h16* wl, const h16* wn, const 
       }
     }
     // ---------------- node phase: lane column r = agent g0 + r
-    node_phase<D>(a, g0, APW, total, [&](int kk) { return row_fr(pool + r * PSTR + 16 * kk + 8 * h, 0); },
+    node_phase<D, ACTS>(a, g0, APW, total, [&](int kk) { return row_fr(pool + r * PSTR + 16 * kk + 8 * h, 0); },
                   wn, nb2, nb3, nb4, lane);
     // the pool image is rewritten by the next group: finish all reads first
     lds_wave_sync();
@@ -711,8 +750,8 @@ DEV void publish_step(const CtrlArgs& a) {
 
 // FUSE (x3): all 72 fragments in LDS (145 KB) and the node phase of each group in the same
 // wave right after its edge phase (pooled rows through global memory): one launch per step.
-template <int WAVES, int D, bool FUSE = false, bool ST = false>
-__global__ __launch_bounds__(WAVES * 64) void ctrl_fwd_kernel(CtrlArgs a) {
+template <int WAVES, int D, bool FUSE, bool ST, bool ACTS>
+DEV void ctrl_fwd_body(const CtrlArgs& a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const unsigned long long t0 = ST ? __builtin_amdgcn_s_memtime() : 0ull;
   constexpr int NFR = (X3 && !FUSE) ? 18 : CTRL_FWD_FRAGS;          // fragments staged in LDS
@@ -731,15 +770,26 @@ __global__ __launch_bounds__(WAVES * 64) void ctrl_fwd_kernel(CtrlArgs a) {
   const int nact = min((int)gridDim.x, (ngrp + WAVES - 1) / WAVES);
   const int lb = (ROLL_XCD && (int)blockIdx.x < nact) ? xcd_block((int)blockIdx.x, nact) : (int)blockIdx.x;
   if (CTRL_FWD_DENSE && a.K == 12 && apw % 8 == 0)
-    ctrl_fwd_groups<D, false, FUSE, true, ST>(a, wl, wn, vl, pools, lb * WAVES + wave_id(), gridDim.x * WAVES, t0);
+    ctrl_fwd_groups<D, false, FUSE, true, ST, ACTS>(a, wl, wn, vl, pools, lb * WAVES + wave_id(), gridDim.x * WAVES, t0);
   else
-    ctrl_fwd_groups<D, false, FUSE, false, ST>(a, wl, wn, vl, pools, lb * WAVES + wave_id(), gridDim.x * WAVES, t0);
+    ctrl_fwd_groups<D, false, FUSE, false, ST, ACTS>(a, wl, wn, vl, pools, lb * WAVES + wave_id(), gridDim.x * WAVES, t0);
   if constexpr (!X3 || FUSE) publish_step(a);   // the x3 split path publishes from its node kernel
+}
+
+template <int WAVES, int D, bool FUSE = false, bool ST = false>
+__global__ __launch_bounds__(WAVES * 64) void ctrl_fwd_kernel(CtrlArgs a) {
+  ctrl_fwd_body<WAVES, D, FUSE, ST, false>(a);
+}
+
+// the same step, also storing each agent's node activations for the backward (node_acts)
+template <int WAVES, int D, bool FUSE = false>
+__global__ __launch_bounds__(WAVES * 64) void ctrl_fwd_acts_kernel(CtrlArgs a) {
+  ctrl_fwd_body<WAVES, D, FUSE, false, true>(a);
 }
 
 // Node phase of the controller step over the pooled rows in global memory, 32-agent groups
 // grp0, grp0 + gstride, ... (x3 steps, and the persistent small-scene rollout)
-template <int D>
+template <int D, bool ACTS = false>
 DEV void ctrl_node_groups(const CtrlArgs& a, const h16* wn, const float* vl, int grp0, int gstride) {
   const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
   const int N = a.N;
@@ -749,13 +799,13 @@ DEV void ctrl_node_groups(const CtrlArgs& a, const h16* wn, const float* vl, int
     const int gi = min(g0 + r, total - 1);
     const int b = gi / N, i = gi - b * N;
     const h16* prow = a.pooled + (long)b * a.p_env + (long)i * PROW + 8 * h;
-    node_phase<D>(a, g0, 32, total, [&](int kk) { return row_fr(prow + 16 * kk, 128); }, wn, vl + 128, vl + 256,
+    node_phase<D, ACTS>(a, g0, 32, total, [&](int kk) { return row_fr(prow + 16 * kk, 128); }, wn, vl + 128, vl + 256,
                   vl + 320, lane);
   }
 }
 
 // x3 node phase of the controller step over the pooled rows written by ctrl_fwd_kernel
-template <int WAVES, int D>
+template <int WAVES, int D, bool ACTS = false>
 __global__ __launch_bounds__(WAVES * 64) void ctrl_node_fwd_kernel(CtrlArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   h16* wn = reinterpret_cast<h16*>(smem);                             // nw1f..nw4 (54 frags)
@@ -763,7 +813,7 @@ __global__ __launch_bounds__(WAVES * 64) void ctrl_node_fwd_kernel(CtrlArgs a) {
   block_copy16(wn, a.wpack + (size_t)a.f_node * FRAG_ELEMS, 54 * FRAG_SZ, false);
   block_copy16(vl, a.wvec, CTRL_VEC * 4);
   __syncthreads();
-  ctrl_node_groups<D>(a, wn, vl, blockIdx.x * WAVES + wave_id(), gridDim.x * WAVES);
+  ctrl_node_groups<D, ACTS>(a, wn, vl, blockIdx.x * WAVES + wave_id(), gridDim.x * WAVES);
   publish_step(a);
 }
 
@@ -800,20 +850,26 @@ extern "C" int MB_SYM(ctrl_fwd)(const mb::CtrlArgs* a, int num_cu, hipStream_t s
     // measured no faster: 8-env slice 2.825-2.833 vs 2.797-2.820 ms, profiles/r6b/)
     if (a->dim == 3) {
       if (a->stamps) go(ctrl_fwd_kernel<CTRL_WAVES, 3, true, true>);
+      else if (a->acts) go(ctrl_fwd_acts_kernel<CTRL_WAVES, 3, true>);
       else go(ctrl_fwd_kernel<CTRL_WAVES, 3, true>);
     } else {
       if (a->stamps) go(ctrl_fwd_kernel<CTRL_WAVES, 2, true, true>);
+      else if (a->acts) go(ctrl_fwd_acts_kernel<CTRL_WAVES, 2, true>);
       else go(ctrl_fwd_kernel<CTRL_WAVES, 2, true>);
     }
     return (int)hipGetLastError();
   }
   const size_t lds = ctrl_fwd_lds();
+  auto go1 = [&](auto kern) {
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(kern, dim3(blocks), dim3(CTRL_WAVES * 64), lds, st, b);
+  };
   if (a->dim == 3) {
-    (void)hipFuncSetAttribute((const void*)ctrl_fwd_kernel<CTRL_WAVES, 3>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL((ctrl_fwd_kernel<CTRL_WAVES, 3>), dim3(blocks), dim3(CTRL_WAVES * 64), lds, st, b);
+    if (a->acts) go1(ctrl_fwd_acts_kernel<CTRL_WAVES, 3>);
+    else go1(ctrl_fwd_kernel<CTRL_WAVES, 3>);
   } else {
-    (void)hipFuncSetAttribute((const void*)ctrl_fwd_kernel<CTRL_WAVES, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL((ctrl_fwd_kernel<CTRL_WAVES, 2>), dim3(blocks), dim3(CTRL_WAVES * 64), lds, st, b);
+    if (a->acts) go1(ctrl_fwd_acts_kernel<CTRL_WAVES, 2>);
+    else go1(ctrl_fwd_kernel<CTRL_WAVES, 2>);
   }
   if constexpr (X3) {
     const size_t ldn = (size_t)54 * FRAG_SZ + CTRL_VEC * 4;
@@ -1474,8 +1530,22 @@ DEV void node_bwd_coop(const CtrlNodeBwdArgs& a, unsigned char* smem, long c0, l
     const h16* W2 = W1 + 64 * NS1;
     const h16* W3 = W2 + 128 * NS2;
     const h16* W4 = W3 + 64 * NS3;
-    // ---- L1 (waves 0, 1): Y1 tile `wave` = relu(W1f [P; s])
     Pk Y1b, Y2b, Y3b;
+    // the rollout's activations of this step (a.acts): Y1 / Y2 / Y3 tiles and y4 loaded instead of
+    // the L1..L4 recompute; the stage images end up as after L3 (Y2 cols 0..127, Y3 128..191)
+    const unsigned char* abase = a.acts ? a.acts + ((long)b * a.na_env + i) * NODE_ACT_BYTES : nullptr;
+    if (a.acts) {
+      const Pk zp = {zero_h16x16(), zero_h16x16()};
+      if (wave < 2) Y1b = ok ? act_load_pk(abase, wave, h) : zp;
+      Y2b = ok ? act_load_pk(abase, 2 + wave, h) : zp;
+      if (wave >= 2) Y3b = ok ? act_load_pk(abase, 6 + wave - 2, h) : zp;
+      store_pk(stg, SW, r, 32 * wave, Y2b, h, PLN);
+      if (wave >= 2) store_pk(stg, SW, r, 128 + 32 * (wave - 2), Y3b, h, PLN);
+      __syncthreads();
+      stamp(3);
+      stamp(4);
+    } else {
+    // ---- L1 (waves 0, 1): Y1 tile `wave` = relu(W1f [P; s])
     if (wave < 2) {
       f32x16 c = zero16();
 #pragma unroll
@@ -1515,15 +1585,21 @@ DEV void node_bwd_coop(const CtrlNodeBwdArgs& a, unsigned char* smem, long c0, l
       store_pk(stg, SW, r, 128 + 32 * mt, Y3b, h, PLN);
     }
     __syncthreads();
+    }
     stamp(5);
     // ---- L4 + gain law + action-loss backward (wave 0) -> d4, ego terms
     float egp[D], egv[D];
 #pragma unroll
     for (int q = 0; q < D; ++q) { egp[q] = 0.f; egv[q] = 0.f; }
     if (wave == 0) {
-      f32x16 y4 = bias_rows(nb4, 0, h);
+      f32x16 y4;
+      if (a.acts) {
+        y4 = ok ? *reinterpret_cast<const f32x16*>(abase + 16 * NODE_ACT_PKB + 64 * h) : zero16();
+      } else {
+        y4 = bias_rows(nb4, 0, h);
 #pragma unroll
-      for (int kk = 0; kk < 4; ++kk) y4 = mma(wrm_nat_fr(W4, NS4, 0, kk, lane, LO), img_fr(128, kk), y4);
+        for (int kk = 0; kk < 4; ++kk) y4 = mma(wrm_nat_fr(W4, NS4, 0, kk, lane, LO), img_fr(128, kk), y4);
+      }
       float y4r[8];
       acc_rows8(y4, y4r);
       float d4r[8];
@@ -2194,7 +2270,7 @@ DEV void small_scan(const RolloutSmallArgs& ra, const float4* Sb, int N, int Nn,
   }
 }
 
-template <int D>
+template <int D, bool ACTS>
 __global__ __launch_bounds__(SR_WAVES * 64) void rollout_small_kernel(RolloutSmallArgs ra) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ SmallScanLds L;
@@ -2258,12 +2334,13 @@ __global__ __launch_bounds__(SR_WAVES * 64) void rollout_small_kernel(RolloutSma
     e.act_sum = c.act_sum ? c.act_sum + tb : nullptr; e.ac_env = 1;
     e.pooled = c.pooled + tb * N * PROW; e.p_env = (long)N * PROW;
     e.argmax = c.argmax + tb * N * 128; e.am_env = (long)N * 128;
+    e.acts = c.acts ? c.acts + tb * N * NODE_ACT_BYTES : nullptr; e.na_env = N;
     e.noise_t = t;
     ctrl_fwd_groups<D, true>(e, wl, wn, vl, nullptr, wave, SR_WAVES);
     stamp(1);
     __syncthreads();                                // the env's pooled rows -> node phase
     stamp(2);
-    ctrl_node_groups<D>(e, wn, vl, wave, SR_WAVES);
+    ctrl_node_groups<D, ACTS>(e, wn, vl, wave, SR_WAVES);
     stamp(3);
     // s_{t+1} (read by this workgroup only) and the env's sum atomics (device scope) complete
     // before the barrier; the workgroup-scope barrier is enough for both
@@ -2294,6 +2371,8 @@ size_t rollout_small_lds() { return (size_t)CTRL_FWD_FRAGS * FRAG_SZ + CTRL_VEC 
 
 #include "ctrl16.h"
 #include "node16.h"
+
+extern "C" int MB_SYM(node_act_bytes)() { return mb::MB_PREC::NODE_ACT_BYTES; }
 
 // kernel 0: CBF backward (cbf16.h), 1: edge backward (ctrl16.h), 2: node backward (node16.h)
 extern "C" int MB_SYM(k16_wg_per_cu)(int kernel) {
@@ -2390,12 +2469,16 @@ extern "C" int MB_SYM(rollout_small)(const mb::RolloutSmallArgs* a, hipStream_t 
   if (!a->ctl || !a->idx || !a->dang || !a->cnt || !c.pooled || !c.argmax || !c.dist_sum || !c.S) return -2;
   if (c.apw < 2 || c.apw > 32 || (c.apw & 1)) return -3;
   const size_t lds = rollout_small_lds();
+  auto go = [&](auto kern) {
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(kern, dim3(c.B), dim3(SR_WAVES * 64), lds, st, *a);
+  };
   if (c.dim == 3) {
-    (void)hipFuncSetAttribute((const void*)rollout_small_kernel<3>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL(rollout_small_kernel<3>, dim3(c.B), dim3(SR_WAVES * 64), lds, st, *a);
+    if (c.acts) go(rollout_small_kernel<3, true>);
+    else go(rollout_small_kernel<3, false>);
   } else {
-    (void)hipFuncSetAttribute((const void*)rollout_small_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL(rollout_small_kernel<2>, dim3(c.B), dim3(SR_WAVES * 64), lds, st, *a);
+    if (c.acts) go(rollout_small_kernel<2, true>);
+    else go(rollout_small_kernel<2, false>);
   }
   return (int)hipGetLastError();
 }

@@ -67,6 +67,10 @@ class RolloutDriver {
     apw_ = (int)I("apw");
     small_ctl_ = U("small_ctl"); small_apw_ = (int)I("small_apw"); knn_tail_ = (int)I("knn_tail");
     small_stamps_ = c.contains("small_stamps") ? U("small_stamps") : 0;
+    // the node MLP's activations per step (T, B*N, node_act_bytes), kept for the cooperative node
+    // backward (0 = not kept)
+    acts_ = c.contains("node_acts") ? U("node_acts") : 0;
+    act_bytes_ = c.contains("node_act_bytes") ? I("node_act_bytes") : 0;
     if (small_ctl_) chk(hipHostMalloc((void**)&host_ctl_, 2 * sizeof(int), hipHostMallocDefault), "hipHostMalloc");
     // early-stop publication (ctrl.hip publish_step): per-step workgroup counters on the device,
     // the per-env sums and a flag per step in host-coherent memory
@@ -194,6 +198,7 @@ class RolloutDriver {
     c.pooled = P<h16>(pooled_); c.argmax = P<uint8_t>(argmax_);
     c.apw = small_apw_;
     c.stamps = reinterpret_cast<unsigned long long*>(small_stamps_);   // diagnostics builds only (else 0)
+    c.acts = P<unsigned char>(acts_); c.na_env = N_;     // per-step views offset in the kernel
     a.idx = P<int>(idx_); a.dang = P<uint8_t>(dang_); a.cnt = P<float>(cnt_);
     a.safe = safety_ ? P<float>(safe_) : nullptr;
     a.Nn = Nn_; a.Tmax = Tmax_; a.knn_tail = knn_tail_;
@@ -285,6 +290,7 @@ class RolloutDriver {
     a.G = P<const float>(G_);
     const long nk = (long)N_ * K_;
     a.idx = P<const int>(idx_) + (long)t * B_ * nk; a.i_env = nk;
+    a.acts = acts_ ? P<unsigned char>(acts_) + (long)t * B_ * N_ * act_bytes_ : nullptr; a.na_env = N_;
     a.B = B_; a.N = N_; a.K = K_;
     a.wpack = P<const h16>(ctrl_w_); a.f_edge = f_edge_; a.f_node = f_node_; a.wvec = P<const float>(ctrl_v_);
     a.A = P<float>(A_) + (long)t * B_ * N_ * D_; a.a_env = N_;
@@ -330,7 +336,8 @@ class RolloutDriver {
   float noise_prob_, noise_scale_;
   u64 scan_ws_;
   long scan_ws_env_;
-  u64 small_ctl_ = 0, small_stamps_ = 0;
+  u64 small_ctl_ = 0, small_stamps_ = 0, acts_ = 0;
+  long act_bytes_ = 0;
   int small_apw_ = 0, knn_tail_ = 0;
   int* host_ctl_ = nullptr;
   int f_edge_, f_node_, f_fwd_;
@@ -368,6 +375,8 @@ class BpttDriver {
     // per-step slab rows (small grids): step t's node / edge workgroups write rows (T-1-t) x grid
     // of the slabs instead of accumulating into one row per workgroup
     step_rows_ = c.contains("step_rows") ? (int)I("step_rows") : 0;
+    acts_ = c.contains("node_acts") ? U("node_acts") : 0;
+    act_bytes_ = c.contains("node_act_bytes") ? I("node_act_bytes") : 0;
     node_part_ = c.contains("node_part") ? I("node_part") : 0;
     edge_part_ = c.contains("edge_part") ? I("edge_part") : 0;
     if (step_rows_ && (node_part_ <= 0 || edge_part_ <= 0))
@@ -385,7 +394,8 @@ class BpttDriver {
       throw std::invalid_argument("BpttDriver: bad dimensions");
   }
 
-  void run(int T, float act_coef, u64 stream) {
+  // use_acts: this iteration's rollout kept the node activations (RolloutDriver with node_acts)
+  void run(int T, float act_coef, u64 stream, bool use_acts) {
     if (T < 1 || T > Tmax_) throw std::invalid_argument("BpttDriver: T out of range");
     hipStream_t st = ST(stream);
     const long BN = (long)B_ * N_;
@@ -415,6 +425,8 @@ class BpttDriver {
           a.init = 1;
         }
         a.chunk = node_chunk_;
+        a.acts = (use_acts && acts_) ? P<const unsigned char>(acts_) + (long)t * BN * act_bytes_ : nullptr;
+        a.na_env = N_;
         a.wrm16 = P<const h16>(nw16_);
         a.K = K_;
         if (t < T - 1) {
@@ -466,7 +478,8 @@ class BpttDriver {
  private:
   int B_, N_, Nn_, K_, D_, R_, Tmax_, prec_, prow_, nb_node_, nb_edge_, qsplit_, node_chunk_ = 0, fused_ = 0;
   int step_rows_ = 0;
-  long node_part_ = 0, edge_part_ = 0;
+  long node_part_ = 0, edge_part_ = 0, act_bytes_ = 0;
+  u64 acts_ = 0;
   u64 pooled_, S_, G_, A_, dS_, Gb_, valid_, idx_, argmax_, rptr_, redges_, wrm_, wvec_, act_scale_, dP_, ego_, dEc_;
   u64 part_node_, part_edge_, wpack_, gscale_ = 0, ew16_ = 0, nw16_ = 0;
   int o1_, o2_, o3_, o4_, f_ew1f_, f_ew2tn_;
@@ -478,7 +491,7 @@ class BpttDriver {
 void register_runtime(py::module& m) {
   py::class_<BpttDriver>(m, "BpttDriver")
       .def(py::init<py::dict>())
-      .def("run", &BpttDriver::run, py::arg("T"), py::arg("act_coef"), py::arg("stream"));
+      .def("run", &BpttDriver::run, py::arg("T"), py::arg("act_coef"), py::arg("stream"), py::arg("use_acts") = false);
   py::class_<RolloutDriver>(m, "RolloutDriver")
       .def(py::init<py::dict>())
       .def("run_small", &RolloutDriver::run_small, py::arg("stream"), py::arg("early_stop"),

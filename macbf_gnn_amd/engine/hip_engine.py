@@ -228,6 +228,15 @@ class HipEngine:
         self.step_rows = bool(Gp == 1 and self.bptt and
                               T * (self.nb_node * native.CTRL_NODE_PARTIAL + self.nb_edge * native.CTRL_EDGE_PARTIAL) * 4
                               <= STEP_ROWS_BYTES)
+        # small scenes: the persistent rollout keeps the node MLP's activations for the cooperative
+        # (32-agent chunk) node backward, which then skips its L1..L4 recompute (native drivers
+        # only). Config #2 bf16 0.88-0.91 vs 0.97 ms; the 8-env slice (launch-per-step x3 path,
+        # whose store-keeping step kernel spills) 2.87 vs 2.78-2.83 ms: off there (docs/PERF.md)
+        self.node_acts = None
+        self._acts_valid = False
+        if (self.bptt and self.small_rollout and native.node_bwd_chunk(B * N, dev) == 32
+                and knobs.get_int("MACBF_NODE_ACTS", 1)):
+            self.node_acts = torch.empty(T * B * N * native.node_act_bytes(self.prec), dtype=torch.uint8, device=dev)
         rows_n, rows_e = self.slab_rows
         if self.step_rows:
             rows_n, rows_e = T * rows_n, T * rows_e
@@ -363,6 +372,7 @@ class HipEngine:
                 small_ctl=native.ptr(self.small_ctl) if self.small_rollout else 0,
                 small_apw=int(native.small_apw(N)), knn_tail=int(not self.reuse),
                 small_stamps=native.ptr(self.small_stamps),     # diagnostics builds (scripts/stamps_small.py)
+                node_acts=native.ptr(self.node_acts), node_act_bytes=native.node_act_bytes(self.prec),
                 noise_prob=float(cfg.add_noise_prob), noise_scale=float(cfg.noise_scale),
                 fork_device_scope=1,
                 # early stop published by the controller kernels (no per-step queue marker / copy)
@@ -392,6 +402,9 @@ class HipEngine:
         tail_scanned = False
         cur = torch.cuda.current_stream(self.dev)
         overlap = self.dedup and self.overlap_hfwd
+        # the native drivers keep the node activations (node_acts); the Python loop does not
+        self._acts_valid = bool(self.node_acts is not None and self.native_rollout and
+                                not torch.cuda.is_current_stream_capturing())
         if self.native_rollout and not torch.cuda.is_current_stream_capturing():
             if self.small_rollout:
                 # one persistent launch for the whole rollout (csrc/ctrl.hip rollout_small_kernel)
@@ -696,7 +709,7 @@ class HipEngine:
             slab_rows = self.slab_rows
             if Gp == 1 and red_done is None and self.native_bptt:
                 # the reverse-time launch loop in C++ (csrc/runtime.cpp): same launches, same order
-                self._bdriver().run(T, gs * ACT_COEF, cur.cuda_stream)
+                self._bdriver().run(T, gs * ACT_COEF, cur.cuda_stream, use_acts=self._acts_valid)
             elif Gp == 1:
                 self._bptt_chain(T, slice(0, B), valid_u8, gs, rptr3, redges3, self.part_node[: self.nb_node],
                                  self.part_edge[: self.nb_edge], self.nb_node, self.nb_edge, red_done, ts, cur)
@@ -825,6 +838,7 @@ class HipEngine:
                 dt=float(C.TIME_STEP), sqrt3=float(C.SQRT3),
                 node_chunk=int(native.node_bwd_chunk(B * N, self.dev)),
                 step_rows=int(self.step_rows), node_part=native.CTRL_NODE_PARTIAL, edge_part=native.CTRL_EDGE_PARTIAL,
+                node_acts=native.ptr(self.node_acts), node_act_bytes=native.node_act_bytes(self.prec),
                 fused_step=int(native.bwd_step_fused(B * N, self.dev)),
                 ctrl_w16=native.ptr(self.eb16_w) if self.eb16_w is not None else 0,
                 node_rm16=native.ptr(self._node16(B * N)),

@@ -16,6 +16,7 @@ removed (their decision is the code's default, the measurement is in docs/PERF.m
 | MACBF_BWD_FUSED | by size | ops/native.py | fused node + edge BPTT step on / off (tests) |
 | MACBF_CTRL_APW | by size | ops/native.py | agents per wave of the controller step (tests/test_gpu_fp32.py dense-row equality) |
 | MACBF_EDGE_WG_PER_CU | 1 (x3) | ops/native.py | edge-backward workgroups per CU (tests) |
+| MACBF_NODE_ACTS | 1 | engine/hip_engine.py | 0: the cooperative node backward recomputes the node MLP instead of reusing the rollout's activations (A/B, tests) |
 | MACBF_BWD_GRAPH | 1 | engine/hip_engine.py | small scenes: post-rollout work replayed from per-T HIP graphs (0: eager, tests / A/B) |
 | MACBF_PUBLISH | 1 | engine/hip_engine.py | early stop through a queue marker instead of kernel publication (tests) |
 | MACBF_SELFCHECK | 1 | ops/selfcheck.py | skip the start-up self-check of the 16x16x32 kernels |

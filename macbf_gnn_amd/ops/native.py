@@ -652,6 +652,12 @@ def cbf_active(dh, nev, blk_active, act, nact=None, *, rec=None, src=None, idx=N
     return nact
 
 
+def node_act_bytes(prec) -> int:
+    """Bytes per agent and step of the node activations the rollout keeps for the cooperative node
+    backward (csrc/ctrl.hip NODE_ACT_BYTES: 1152 x3, 640 in the 16-bit builds)."""
+    return int(lib().node_act_bytes(L.PREC_CODE[prec]))
+
+
 def k16_wg_per_cu(prec, kernel: int) -> int:
     """Workgroups per CU of the 16x16x32 backward kernel `kernel` (0 CBF, 1 edge, 2 node) of the
     build of `prec` (csrc/mfma16.h: x3 one, the 1-pass builds two)."""

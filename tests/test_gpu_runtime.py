@@ -9,19 +9,24 @@ pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda")
 
 
-def _trainer(**kw):
-    """Launch-per-step paths (the persistent small-scene rollout is tested in test_gpu_small.py)."""
+def _trainer(acts=False, small=False, **kw):
+    """Launch-per-step paths (the persistent small-scene rollout is tested in test_gpu_small.py).
+    acts=False: the cooperative node backward recomputes the node MLP (the Python loops always do,
+    so the bitwise comparisons below need the recompute on the native path too)."""
     from macbf_gnn_amd.engine import Trainer
     from macbf_gnn_amd.engine.hip_engine import HipEngine
     from macbf_gnn_amd.parallel import DP
     cfg = C.TrainConfig(num_agents=kw.pop("N", 64), num_envs=kw.pop("B", 4), inner_loops=kw.pop("T", 30),
                         seed=1, device="hip", **kw)
     old = HipEngine.small_rollout
-    HipEngine.small_rollout = False
+    HipEngine.small_rollout = small
     try:
-        return Trainer(cfg, device=DEV, dp=DP(device=DEV))
+        tr = Trainer(cfg, device=DEV, dp=DP(device=DEV))
     finally:
         HipEngine.small_rollout = old
+    if not acts:
+        tr.engine.node_acts = None      # before the drivers are built (lazily, at the first step)
+    return tr
 
 
 def _rollout(tr, native_rollout, s0, g, early_stop):
@@ -94,6 +99,27 @@ def test_native_bptt_matches_python_loop(dim):
     tr.engine.step(s0, g, obs)
     assert torch.equal(g_py, tr.fp.grad)
     assert torch.equal(gb_py, tr.engine.Gb)
+
+
+@pytest.mark.parametrize("dtype,tol", [("fp32", 2e-5), ("bf16", 3e-2), ("fp16", 3e-2)])
+def test_node_activations_reuse_matches_recompute(dtype, tol):
+    """The cooperative node backward on the node activations the persistent small-scene rollout
+    kept (HipEngine.node_acts) against its own recompute: the same gradients up to the forward's
+    summation order (the rollout's fragment-layout products vs the backward's row-major ones)."""
+    grads = []
+    for acts in (True, False):
+        tr = _trainer(acts=acts, small=True, T=12, dtype=dtype, N=32, B=2)
+        assert (tr.engine.node_acts is not None) == acts
+        s0, g, _ = tr.sample()
+        tr.engine.step(s0, g)
+        torch.cuda.synchronize()
+        if acts:
+            assert tr.engine._acts_valid
+        grads.append(tr.fp.grad.clone())
+    a, b = grads
+    assert torch.isfinite(a).all()
+    err = (a - b).norm() / b.norm()
+    assert err < tol, float(err)
 
 
 @pytest.mark.parametrize("every", [2, 3, 5])

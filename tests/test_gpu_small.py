@@ -73,6 +73,9 @@ def test_small_rollout_variants(kw):
 
 def test_small_rollout_training_step_matches():
     a, b = _trainer(False, T=20), _trainer(True, T=20)
+    # bit-for-bit: the stored node activations round the backward differently from the per-step
+    # recompute (covered with a tolerance by test_gpu_runtime's node-activation test)
+    b.engine.node_acts = None
     b.fp.flat.copy_(a.fp.flat)
     b.engine.after_update()
     s0, g, obs = a.sample()
