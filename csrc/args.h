@@ -108,7 +108,10 @@ struct RolloutSmallArgs {
   int Nn, Tmax, knn_tail;
   float r2_train, ttc_train, r2_check, ttc_check;
   float done_thr;       // early stop: mean goal distance < done_thr (-inf: run all Tmax steps)
-  int* ctl;             // [envs done, max first-done step]: zeroed before the launch
+  int* ctl;             // [envs done, max first-done step, finished workgroups]: zero at the launch
+                        // (with res: re-armed by the kernel's last workgroup)
+  int* res;             // optional host-coherent [T, flag]: the horizon, then flag = res_gen
+  int res_gen;
 };
 
 struct LossConsts {
@@ -336,6 +339,7 @@ struct StepCommitArgs {
   int* ok; int* steps; int mask, ngroups; int* skipped;
   float* gscale; int* good; int growth; float max_scale;   // gscale null: no loss scaling
   float* stats_row;                                        // null: no statistics row
+  const float* stats_src;   // optional: stats_row[0:16] copied from here first (graph-replayed backward)
 };
 
 struct AdamArgs {

@@ -216,16 +216,17 @@ static int reduce_rows(u64 partial, int rows, int cols, u64 out, int accumulate,
 }
 
 static mb::StepCommitArgs commit_args(u64 ok, u64 steps, int mask, int ngroups, u64 skipped, u64 gscale, u64 good,
-                                      int growth, float max_scale, u64 stats_row) {
+                                      int growth, float max_scale, u64 stats_row, u64 stats_src = 0) {
   mb::StepCommitArgs a{};
   a.ok = P<int>(ok); a.steps = P<int>(steps); a.mask = mask; a.ngroups = ngroups; a.skipped = P<int>(skipped);
   a.gscale = P<float>(gscale); a.good = P<int>(good); a.growth = growth; a.max_scale = max_scale;
   a.stats_row = P<float>(stats_row);
+  a.stats_src = P<const float>(stats_src);
   return a;
 }
 
 // commit: None, or the step_commit arguments (ok, steps, mask, ngroups, skipped, gscale, good, growth,
-// max_scale, stats_row) -- the optimizer step's commit runs inside the gather launch
+// max_scale, stats_row[, stats_src]) -- the optimizer step's commit runs inside the gather launch
 static int pack_gather(u64 src, int n, u64 idx16, int m16, u64 out16, int f16, u64 idx32, int m32, u64 out32,
                        py::object commit, u64 stream) {
   mb::StepCommitArgs c{};
@@ -233,7 +234,8 @@ static int pack_gather(u64 src, int n, u64 idx16, int m16, u64 out16, int f16, u
   if (has) {
     const py::tuple t = commit.cast<py::tuple>();
     c = commit_args(t[0].cast<u64>(), t[1].cast<u64>(), t[2].cast<int>(), t[3].cast<int>(), t[4].cast<u64>(),
-                    t[5].cast<u64>(), t[6].cast<u64>(), t[7].cast<int>(), t[8].cast<float>(), t[9].cast<u64>());
+                    t[5].cast<u64>(), t[6].cast<u64>(), t[7].cast<int>(), t[8].cast<float>(), t[9].cast<u64>(),
+                    t.size() > 10 ? t[10].cast<u64>() : 0);
   }
   return mb_pack_gather(P<const float>(src), n, P<const int>(idx16), m16, P<unsigned short>(out16), f16,
                         P<const int>(idx32), m32, P<float>(out32), has ? &c : nullptr, ST(stream));
@@ -281,8 +283,9 @@ static int adam_multi(u64 param, u64 grad, u64 m, u64 v, py::list groups, float 
 static int grad_check(u64 g, int n, u64 ok, u64 stream) { return mb_grad_check(P<const float>(g), n, P<int>(ok), ST(stream)); }
 
 static int step_commit(u64 ok, u64 steps, int mask, int ngroups, u64 skipped, u64 gscale, u64 good, int growth,
-                       float max_scale, u64 stats_row, u64 stream) {
-  const mb::StepCommitArgs a = commit_args(ok, steps, mask, ngroups, skipped, gscale, good, growth, max_scale, stats_row);
+                       float max_scale, u64 stats_row, u64 stats_src, u64 stream) {
+  const mb::StepCommitArgs a = commit_args(ok, steps, mask, ngroups, skipped, gscale, good, growth, max_scale, stats_row,
+                                           stats_src);
   return mb_step_commit(&a, ST(stream));
 }
 

@@ -2361,6 +2361,22 @@ __global__ __launch_bounds__(SR_WAVES * 64) void rollout_small_kernel(RolloutSma
     if (c.stamps && (threadIdx.x & 63) == 0)
       for (int k = 0; k < 16; ++k) c.stamps[((long)b * SR_WAVES + wave) * 16 + k] = ph[k];
   }
+  // The last workgroup to finish hands the horizon to the host (host-coherent memory, polled by
+  // csrc/runtime.cpp run_small) and re-arms the control words for the next launch: no memset,
+  // read-back copy or stream synchronisation around the launch.
+  if (ra.res && threadIdx.x == 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (__hip_atomic_fetch_add(ra.ctl + 2, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT) == B - 1) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      const int nd = __hip_atomic_load(ra.ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int mx = __hip_atomic_load(ra.ctl + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      for (int q = 0; q < 3; ++q) __hip_atomic_store(ra.ctl + q, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(ra.res, nd == B ? min(Tmax, mx + 1) : Tmax, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(ra.res + 1, ra.res_gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
 }
 
 size_t rollout_small_lds() { return (size_t)CTRL_FWD_FRAGS * FRAG_SZ + CTRL_VEC * 4; }

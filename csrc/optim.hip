@@ -232,6 +232,8 @@ DEV void step_commit_body(const StepCommitArgs& a) {
     *a.gscale = s;
   }
   if (a.stats_row) {
+    if (a.stats_src)
+      for (int q = 0; q < 16; ++q) a.stats_row[q] = a.stats_src[q];
     a.stats_row[16] = ok ? 0.f : 1.f;
     a.stats_row[17] = a.gscale ? *a.gscale : 1.f;
   }

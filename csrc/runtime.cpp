@@ -20,6 +20,7 @@
 #include <cmath>
 #include <cstring>
 #include <stdexcept>
+#include <tuple>
 #include <vector>
 
 #include "args.h"
@@ -71,7 +72,11 @@ class RolloutDriver {
     // backward (0 = not kept)
     acts_ = c.contains("node_acts") ? U("node_acts") : 0;
     act_bytes_ = c.contains("node_act_bytes") ? I("node_act_bytes") : 0;
-    if (small_ctl_) chk(hipHostMalloc((void**)&host_ctl_, 2 * sizeof(int), hipHostMallocDefault), "hipHostMalloc");
+    if (small_ctl_) {
+      chk(hipHostMalloc((void**)&small_res_, 2 * sizeof(int), hipHostMallocMapped | hipHostMallocCoherent), "hipHostMalloc");
+      small_res_[0] = small_res_[1] = 0;
+      chk(hipHostGetDevicePointer((void**)&small_res_dev_, small_res_, 0), "hipHostGetDevicePointer");
+    }
     // early-stop publication (ctrl.hip publish_step): per-step workgroup counters on the device,
     // the per-env sums and a flag per step in host-coherent memory
     publish_ = c.contains("publish") ? (int)I("publish") : 0;
@@ -100,7 +105,7 @@ class RolloutDriver {
     for (auto e : ev_copy_) (void)hipEventDestroy(e);
     (void)hipEventDestroy(ev_main_);
     (void)hipEventDestroy(ev_side_);
-    if (host_ctl_) (void)hipHostFree(host_ctl_);
+    if (small_res_) (void)hipHostFree(small_res_);
     if (pub_host_) (void)hipHostFree(pub_host_);
     if (pub_ctr_) (void)hipFree(pub_ctr_);
   }
@@ -177,13 +182,18 @@ class RolloutDriver {
     return {T, tail};     // converted to a tuple after the GIL is re-acquired
   }
 
+  // Executable graphs of the post-rollout work per horizon (index T; 0: none), captured by the
+  // engine (hip_engine.py _capture_bwd): run_small(..., launch_graph) launches graph T as soon as
+  // the horizon arrives, without a return to Python in between.
+  void set_bwd_graphs(std::vector<u64> execs) { bwd_execs_ = std::move(execs); }
+
   // Persistent small-scene rollout (ctrl.hip rollout_small_kernel): the whole rollout in one
-  // launch, early stop decided on the device; returns (T, true) -- the kernel also scanned s_T.
-  std::pair<int, bool> run_small(u64 stream, bool early_stop) {
+  // launch, early stop decided on the device; returns (T, true, launched) -- the kernel also scanned
+  // s_T; launched: the registered graph of horizon T was launched on `stream`.
+  std::tuple<int, bool, bool> run_small(u64 stream, bool early_stop, bool launch_graph) {
     if (!small_ctl_) throw std::runtime_error("RolloutDriver: no small-scene control buffer");
     hipStream_t st = ST(stream);
     int* ctl = P<int>(small_ctl_);
-    chk(hipMemsetAsync(ctl, 0, 2 * sizeof(int), st), "hipMemsetAsync");
     mb::RolloutSmallArgs a{};
     mb::CtrlArgs& c = a.c;
     c.dim = D_;
@@ -204,12 +214,38 @@ class RolloutDriver {
     a.Nn = Nn_; a.Tmax = Tmax_; a.knn_tail = knn_tail_;
     a.r2_train = r2_train_; a.ttc_train = ttc_train_; a.r2_check = r2_check_; a.ttc_check = ttc_check_;
     a.done_thr = early_stop ? done_thr_ : -INFINITY;
-    a.ctl = ctl;
+    a.ctl = ctl;      // zero at allocation; the kernel's last workgroup re-arms it
+    a.res = small_res_dev_;
+    a.res_gen = (int)++small_gen_;
     chk((prec_ == 2 ? mb_rollout_small_x3 : prec_ == 1 ? mb_rollout_small_f16 : mb_rollout_small)(&a, st), "rollout_small");
-    chk(hipMemcpyAsync(host_ctl_, ctl, 2 * sizeof(int), hipMemcpyDeviceToHost, st), "hipMemcpyAsync");
-    chk(hipStreamSynchronize(st), "hipStreamSynchronize");
-    const int T = host_ctl_[0] == B_ ? std::min(Tmax_, host_ctl_[1] + 1) : Tmax_;
-    return {T, true};
+    // the horizon arrives in host-coherent memory when the last workgroup finishes: poll it (a
+    // stream synchronisation added a memset, a read-back copy and the blocking wake-up to every
+    // iteration of the small configurations)
+    const volatile int* res = small_res_;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (unsigned long n = 0; __atomic_load_n(&res[1], __ATOMIC_ACQUIRE) != a.res_gen; ++n) {
+      if ((n & 4095) == 4095) {
+        const auto dt = std::chrono::steady_clock::now() - t0;
+        if (dt >= std::chrono::milliseconds(poll_query_ms_)) {
+          const hipError_t e = hipStreamQuery(st);
+          if (e != hipSuccess && e != hipErrorNotReady) chk(e, "rollout_small stream");
+          // the stream drained without the flag: the launch did not run (never spin forever)
+          if (e == hipSuccess && __atomic_load_n(&res[1], __ATOMIC_ACQUIRE) != a.res_gen)
+            throw std::runtime_error("RolloutDriver: rollout_small finished without publishing its horizon");
+        }
+        if (dt > std::chrono::seconds(60)) throw std::runtime_error("RolloutDriver: rollout_small horizon not published");
+      }
+#if defined(__x86_64__)
+      __builtin_ia32_pause();
+#endif
+    }
+    const int T = res[0];
+    bool launched = false;
+    if (launch_graph && T >= 1 && T < (int)bwd_execs_.size() && bwd_execs_[T]) {
+      chk(hipGraphLaunch(reinterpret_cast<hipGraphExec_t>(static_cast<uintptr_t>(bwd_execs_[T])), st), "hipGraphLaunch");
+      launched = true;
+    }
+    return {T, true, launched};
   }
 
  private:
@@ -339,7 +375,10 @@ class RolloutDriver {
   u64 small_ctl_ = 0, small_stamps_ = 0, acts_ = 0;
   long act_bytes_ = 0;
   int small_apw_ = 0, knn_tail_ = 0;
-  int* host_ctl_ = nullptr;
+  std::vector<u64> bwd_execs_;
+  int* small_res_ = nullptr;                 // host-coherent [T, flag] of the persistent rollout
+  int* small_res_dev_ = nullptr;             // its device view
+  unsigned small_gen_ = 0;
   int f_edge_, f_node_, f_fwd_;
   float r2_train_, ttc_train_, r2_check_, ttc_check_, dt_, obs_r_, sqrt3_, dist_thr_, dist_eps_, done_thr_;
   std::vector<hipEvent_t> ev_copy_;
@@ -494,8 +533,9 @@ void register_runtime(py::module& m) {
       .def("run", &BpttDriver::run, py::arg("T"), py::arg("act_coef"), py::arg("stream"), py::arg("use_acts") = false);
   py::class_<RolloutDriver>(m, "RolloutDriver")
       .def(py::init<py::dict>())
+      .def("set_bwd_graphs", &RolloutDriver::set_bwd_graphs, py::arg("execs"))
       .def("run_small", &RolloutDriver::run_small, py::arg("stream"), py::arg("early_stop"),
-           py::call_guard<py::gil_scoped_release>())
+           py::arg("launch_graph") = false, py::call_guard<py::gil_scoped_release>())
       .def("run", &RolloutDriver::run, py::arg("stream"), py::arg("hstream"), py::arg("copy_stream"),
            py::arg("early_stop"),
            // the loop blocks on hipEventSynchronize: let other Python threads run meanwhile

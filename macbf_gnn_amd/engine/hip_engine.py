@@ -145,6 +145,10 @@ class HipEngine:
         # vs 10.141-10.165 ms, 8-env slice 2.798-2.803 vs 2.793-2.815 -- within noise, profiles/r6d/)
         self.bwd_graph = bool(knobs.get_int("MACBF_BWD_GRAPH", int(self.bwd_graph)))
         self._bwd_graphs = {}          # (T, grad scale) -> CUDAGraph of _counts + _backward
+        self._graph_table = None       # key suffix of the graphs registered with the rollout driver
+        self._graph_launch = False     # the next run_small launches the registered graph of its T
+        self._launched_T = None
+        self._drv_launch = bool(knobs.get_int("MACBF_GRAPH_LAUNCH", 1))
         self._bwd_pool = None
         self._bwd_capture = False
         # int32 guard flag the gradient-assembly launch clears on a non-finite element (set by the
@@ -193,6 +197,7 @@ class HipEngine:
         self.counts = torch.zeros(3, dtype=f32, device=dev)
         self.local = torch.zeros(3, dtype=f32, device=dev)        # agent-steps, safe agents, action-loss sum
         self.raw_stats = torch.zeros(STATS_COLS, dtype=f32, device=dev)   # graph mode (fixed address)
+        self._stats_pending = None
         # per-iteration statistics rows (utils.metrics.StepStats layout), written by one kernel per
         # iteration into a ring; a full ring is replaced by a fresh one (torch.empty: no kernel), so
         # a StepStats keeps its row for as long as it is referenced
@@ -204,7 +209,8 @@ class HipEngine:
         self.valid_buf = torch.zeros(T, B, dtype=u8, device=dev)
         # exploration noise (reference train.py:65-67): counter-based device RNG keyed per iteration
         self.noise_key = torch.zeros(1, dtype=torch.int64, device=dev)
-        self.small_ctl = torch.zeros(2, dtype=i32, device=dev)     # persistent rollout: [envs done, max step]
+        # persistent rollout: [envs done, max step, finished workgroups] (re-armed by the kernel)
+        self.small_ctl = torch.zeros(3, dtype=i32, device=dev)
         self.small_stamps = None          # diagnostics: [env][wave][16] phase clocks of the persistent rollout
         # K = 12, x3: the 16x16x32 controller edge backward (csrc/ctrl16.h, 8-wave workgroups); the
         # 1-pass builds keep the 32x32x16 kernel (70 vs 78 us per call in bf16, 74 vs 89 us fp16 3-D,
@@ -408,7 +414,11 @@ class HipEngine:
         if self.native_rollout and not torch.cuda.is_current_stream_capturing():
             if self.small_rollout:
                 # one persistent launch for the whole rollout (csrc/ctrl.hip rollout_small_kernel)
-                T, tail_scanned = self._driver().run_small(cur.cuda_stream, bool(early_stop))
+                # (step(): the registered backward graph of the horizon is launched by the driver
+                # as soon as the horizon arrives -- _backward_graphed then skips its replay)
+                T, tail_scanned, launched = self._driver().run_small(cur.cuda_stream, bool(early_stop),
+                                                                    self._graph_launch)
+                self._launched_T = T if launched else None
                 return self._tail_scan(T, tail_scanned)
             # the per-step launch loop in C++ (csrc/runtime.cpp): same launches, same order
             T, tail_scanned = self._driver().run(cur.cuda_stream, self.hstream.cuda_stream if overlap else 0,
@@ -499,10 +509,17 @@ class HipEngine:
         if self.graph_mode:
             return self._step_graph(s0, g, obs)
         tm = self.tr.timer
-        # (a high-priority stream for this critical chain was measured slower: 7.62 -> 8.06 ms)
-        T = self.rollout(s0, g, obs)
+        graphed = self._bwd_graph_on()
+        if graphed:
+            self.flush_stats()                      # a replay rewrites raw_stats
+            self._graph_launch = self._graph_table == self._graph_suffix() and self._drv_launch
+        try:
+            # (a high-priority stream for this critical chain was measured slower: 7.62 -> 8.06 ms)
+            T = self.rollout(s0, g, obs)
+        finally:
+            self._graph_launch = False
         tm.mark("rollout")
-        if self._bwd_graph_on():
+        if graphed:
             return self._backward_graphed(T)
         valid = self._counts(T)
         # the count all-reduce (the only mid-step collective) overlaps the parts of the backward
@@ -521,20 +538,38 @@ class HipEngine:
         iteration runs eagerly, then the graph is captured: same kernels, same arguments -- every
         buffer is allocated once per engine, the statistics row is the fixed raw_stats, copied to a
         ring row after the replay)."""
-        # (the flat gradient's address too: a checkpoint load that rebinds the flat buffers gets a
-        # fresh graph; every other captured buffer lives as long as the engine)
-        key = (int(T), self._gscale()[0], self.tr.fp.grad.data_ptr(), self.tr.fp.flat.data_ptr())
+        key = (int(T),) + self._graph_suffix()
+        launched, self._launched_T = self._launched_T == T, None
         g = self._bwd_graphs.get(key)
         if g is None:
             valid = self._counts(T)
             out = self._stats(*self._backward(T, valid))
             self._capture_bwd(T, key)
             return out
-        g.replay()
+        if not launched:
+            self.flush_stats()                      # the replay rewrites raw_stats
+            g.replay()
         self._sums_dirty = False                   # the captured rollout_stats zeroed the sums
         row = self._next_row()
-        row.copy_(self.raw_stats)
-        return self._stats(row, T)
+        # raw_stats -> row: by the optimizer's commit launch when the trainer takes it
+        # (take_stats_src), else before the row is read or raw_stats is rewritten (flush_stats)
+        self._stats_pending = row
+        st = self._stats(row, T)
+        st.flush = self.flush_stats
+        return st
+
+    def take_stats_src(self, row):
+        """The fixed buffer the pending statistics row is still to be copied from (the caller's
+        launch copies it), or None."""
+        if self._stats_pending is not None and self._stats_pending is row:
+            self._stats_pending = None
+            return self.raw_stats
+        return None
+
+    def flush_stats(self):
+        if self._stats_pending is not None:
+            self._stats_pending.copy_(self.raw_stats)
+            self._stats_pending = None
 
     def _capture_bwd(self, T, key):
         cur = torch.cuda.current_stream(self.dev)
@@ -554,6 +589,19 @@ class HipEngine:
             self._sums_dirty = dirty
         cur.wait_stream(side)
         self._bwd_graphs[key] = g
+        if self.small_rollout and self.native_rollout:
+            # the driver's table of this key suffix: launched right after the rollout (run_small)
+            execs = [0] * (self.Tmax + 1)
+            for k, gk in self._bwd_graphs.items():
+                if k[1:] == key[1:]:
+                    execs[k[0]] = int(gk.raw_cuda_graph_exec())
+            self._driver().set_bwd_graphs(execs)
+            self._graph_table = key[1:]
+
+    def _graph_suffix(self):
+        # (the flat gradient's address too: a checkpoint load that rebinds the flat buffers gets a
+        # fresh graph; every other captured buffer lives as long as the engine)
+        return (self._gscale()[0], self.tr.fp.grad.data_ptr(), self.tr.fp.flat.data_ptr())
 
     # ------------------------------------------------------------------ graph mode
     def _step_graph(self, s0, g, obs):

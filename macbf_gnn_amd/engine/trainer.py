@@ -183,15 +183,18 @@ class Trainer:
             guard = self.cfg.nan_guard or self.fp16
             if guard and getattr(self.engine, "check_ok", None) is None:
                 native.grad_check(self.fp.grad, self._ok)        # after the all-reduce (DP)
-            row = getattr(stats, "raw", None)
+            row = getattr(stats, "row", None)
             row = row if (row is not None and row.numel() >= 18) else None
             # without a stats row the skip flag is read before the commit kernel re-arms it
             ok_snap = self._ok.clone() if (row is None and guard) else None
+            # a graph-replayed backward leaves the row's values in its fixed buffer: the commit copies
+            take = getattr(self.engine, "take_stats_src", None)
+            src = take(row) if (take is not None and row is not None) else None
             # Adam of every group in one launch; its commit (step counts, skip count, loss scale,
             # flag re-arm) runs inside the weight repack launch that follows
             commit = self.opt.step(self.groups_to_step(), ok=self._ok if guard else None, gscale=self.gscale_dev,
                                    good=self._good_dev if self.fp16 else None, growth=self.cfg.loss_scale_growth,
-                                   stats_row=row, defer_commit=True)
+                                   stats_row=row, defer_commit=True, stats_src=src)
             self.engine.after_update(commit=commit)
             if row is None:
                 stats["skipped"] = 1 - ok_snap[0] if ok_snap is not None else 0

@@ -1142,9 +1142,20 @@ def grad_check(g, ok):
     _ok(lib().grad_check(ptr(g), g.numel(), ptr(ok), stream_handle()), "grad_check")
 
 
+def _check_stats_src(stats_src, stats_row):
+    if stats_src is None:
+        return
+    if stats_row is None:
+        raise NativeError("stats_src needs stats_row")
+    if stats_src.dtype != torch.float32 or stats_src.numel() < 16 or not stats_src.is_contiguous():
+        raise NativeError("stats_src must be a contiguous float32 row of >= 16")
+
+
 def step_commit_args(ok, steps, mask, skipped, *, gscale=None, good=None, growth=1000, max_scale=2.0 ** 24,
-                     stats_row=None):
-    """Validated step_commit arguments as the tuple pack_gather(commit=...) takes."""
+                     stats_row=None, stats_src=None):
+    """Validated step_commit arguments as the tuple pack_gather(commit=...) takes; stats_src: the
+    commit first copies stats_row[0:16] from it (the graph-replayed backward's fixed row)."""
+    _check_stats_src(stats_src, stats_row)
     check(ok, torch.int32, (1,), "ok")
     check(steps, torch.int32, None, "steps")
     check(skipped, torch.int32, (1,), "skipped")
@@ -1156,7 +1167,7 @@ def step_commit_args(ok, steps, mask, skipped, *, gscale=None, good=None, growth
                                   or not stats_row.is_contiguous()):
         raise NativeError("stats_row must be a contiguous float32 row of >= 18")
     return (ptr(ok), ptr(steps), int(mask), steps.numel(), ptr(skipped), ptr(gscale), ptr(good), int(growth),
-            float(max_scale), ptr(stats_row))
+            float(max_scale), ptr(stats_row), ptr(stats_src))
 
 
 def step_commit_raw(args):
@@ -1165,7 +1176,7 @@ def step_commit_raw(args):
 
 
 def step_commit(ok, steps, mask, skipped, *, gscale=None, good=None, growth=1000, max_scale=2.0 ** 24,
-                stats_row=None):
+                stats_row=None, stats_src=None):
     """End of an optimizer step on the device: steps[g] += 1 for the groups in mask if *ok, else
     skipped += 1; fp16 (gscale, good): the dynamic loss scale halves on a skipped step and doubles
     after `growth` finite ones; stats_row[16:18] = [skipped, loss scale]; *ok reset to 1."""
@@ -1179,8 +1190,9 @@ def step_commit(ok, steps, mask, skipped, *, gscale=None, good=None, growth=1000
     if stats_row is not None and (stats_row.dtype != torch.float32 or stats_row.numel() < 18
                                   or not stats_row.is_contiguous()):
         raise NativeError("stats_row must be a contiguous float32 row of >= 18")
+    _check_stats_src(stats_src, stats_row)
     _ok(lib().step_commit(ptr(ok), ptr(steps), int(mask), steps.numel(), ptr(skipped), ptr(gscale), ptr(good),
-                          int(growth), float(max_scale), ptr(stats_row), stream_handle()), "step_commit")
+                          int(growth), float(max_scale), ptr(stats_row), ptr(stats_src), stream_handle()), "step_commit")
 
 
 def stats_pack(sums, counts, local, row):

@@ -38,11 +38,19 @@ class StepStats(collections.abc.MutableMapping):
     RAW = 16
 
     def __init__(self, raw: torch.Tensor, T, extra=None):
-        self.raw = raw
+        self.row = raw               # the device row as written so far (the optimizer's commit completes it)
         self.scaled = False          # fp16: report the loss scale (raw[17])
         self._T = T
         self.extra = dict(extra or {})
         self._host = None
+        self.flush = None            # set by a graph-replayed backward: completes the row first
+
+    @property
+    def raw(self) -> torch.Tensor:
+        """The complete device row (a graph-replayed backward's pending values copied in first)."""
+        if self.flush is not None:
+            self.flush()
+        return self.row
 
     def _compute(self):
         if self._host is None:

@@ -115,12 +115,14 @@ class FlatAdam:
         else:
             self._steps[name] = int(step)
 
-    def step(self, groups=None, ok=None, gscale=None, good=None, growth=1000, stats_row=None, defer_commit=False):
+    def step(self, groups=None, ok=None, gscale=None, good=None, growth=1000, stats_row=None, defer_commit=False,
+             stats_src=None):
         """One Adam step of the named ranges. On HIP, ok (device int32 flag, optional) gates the
         whole step on the device: 0 leaves parameters, moments and step counts untouched and
         counts a skipped step; the commit kernel then re-arms the flag. gscale / good (fp16): the
         device loss scale and finite-step count, updated by the commit kernel (``native.step_commit``);
-        stats_row: the iteration's statistics row (skipped flag and loss scale written into it).
+        stats_row: the iteration's statistics row (skipped flag and loss scale written into it;
+        stats_src: its first 16 values are copied from there first).
         All groups update in ONE launch; defer_commit: return the commit's arguments instead of
         launching it (the weight repack runs it: ``PackedWeights.update(commit=...)``)."""
         groups = list(self.fp.ranges) if groups is None else list(groups)
@@ -136,7 +138,7 @@ class FlatAdam:
             if spec:
                 native.adam_multi(self.fp.flat, self.fp.grad, self.exp_avg, self.exp_avg_sq, spec, self.lr,
                                   self.betas[0], self.betas[1], self.eps, self.wd, ok=flag)
-            kw = dict(gscale=gscale, good=good, growth=growth, stats_row=stats_row)
+            kw = dict(gscale=gscale, good=good, growth=growth, stats_row=stats_row, stats_src=stats_src)
             if defer_commit:
                 return native.step_commit_args(flag, self._dsteps, mask, self.dskipped, **kw)
             native.step_commit(flag, self._dsteps, mask, self.dskipped, **kw)

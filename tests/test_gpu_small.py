@@ -160,6 +160,28 @@ def test_backward_graph_matches_eager(kw, monkeypatch):
     assert len(b.engine._bwd_graphs) == 1
 
 
+def test_backward_graph_statistics_through_the_optimizer_commit(monkeypatch):
+    """Under train_step the replayed graph's statistics reach the iteration's row through the
+    optimizer's commit launch (no separate copy): rows, skipped flags, gradients and parameters
+    equal the eager trainer's, iteration by iteration."""
+    monkeypatch.setenv("MACBF_BWD_GRAPH", "0")
+    a = _trainer(True, T=20)
+    monkeypatch.setenv("MACBF_BWD_GRAPH", "1")
+    b = _trainer(True, T=20)
+    b.fp.flat.copy_(a.fp.flat)
+    b.engine.after_update()
+    s0, g, obs = a.sample()
+    for it in range(4):
+        sa = a.train_step(s0, g, obs)
+        sb = b.train_step(s0, g, obs)
+        assert sb.flush is not None or it == 0
+        assert b.engine._stats_pending is None        # taken by the commit
+        torch.cuda.synchronize()
+        assert torch.equal(sa.row, sb.row), it
+        assert torch.equal(a.fp.flat, b.fp.flat), it
+        assert sa["loss_total"] == sb["loss_total"]
+
+
 def test_backward_graphs_of_several_horizons_replay_exactly(monkeypatch):
     """Early stop changes the horizon T between iterations, so several per-T backward graphs are
     captured into ONE memory pool and replayed in any order. Scenarios of different
