@@ -112,6 +112,8 @@ struct RolloutSmallArgs {
                         // (with res: re-armed by the kernel's last workgroup)
   int* res;             // optional host-coherent [T, flag]: the horizon, then flag = res_gen
   int res_gen;
+  const float* s0;      // optional (B, N, 2D) start states: written into the S[0] records first
+  const float* g0;      // optional (B, N, D) goals: copied into c.G first
 };
 
 struct LossConsts {

@@ -2281,9 +2281,26 @@ __global__ __launch_bounds__(SR_WAVES * 64) void rollout_small_kernel(RolloutSma
   block_copy16(wl, c.wpack + (size_t)c.f_edge * FRAG_ELEMS, 18 * FRAG_SZ, false);
   block_copy16(wn, c.wpack + (size_t)c.f_node * FRAG_ELEMS, 54 * FRAG_SZ, false);
   block_copy16(vl, c.wvec, CTRL_VEC * 4);
-  __syncthreads();
   const int b = blockIdx.x, B = c.B, N = c.N, K = c.K, Nn = ra.Nn, Tmax = ra.Tmax;
   const long nk = (long)N * K;
+  if (ra.s0) {
+    // this env's scenario straight from the sampler's buffers (no copy launches before the
+    // rollout): S[0] agent records and goals, read back below by this workgroup only
+    float4* S0 = const_cast<float4*>(c.S) + (long)b * Nn * REC<D>;
+    for (int q = threadIdx.x; q < N; q += blockDim.x) {
+      const float* x = ra.s0 + ((long)b * N + q) * 2 * D;
+      if constexpr (D == 2) {
+        S0[q] = make_float4(x[0], x[1], x[2], x[3]);
+      } else {
+        S0[2 * q] = make_float4(x[0], x[1], x[2], 0.f);
+        S0[2 * q + 1] = make_float4(x[3], x[4], x[5], 0.f);
+      }
+    }
+    float* Gb = const_cast<float*>(c.G) + (long)b * N * D;
+    for (int q = threadIdx.x; q < N * D; q += blockDim.x) Gb[q] = ra.g0[(long)b * N * D + q];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
   const int wave = wave_id();
   int T = -1;                  // horizon, once every env has published its first done step
   bool done = false;           // (thread 0) this env has published

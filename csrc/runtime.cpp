@@ -190,7 +190,9 @@ class RolloutDriver {
   // Persistent small-scene rollout (ctrl.hip rollout_small_kernel): the whole rollout in one
   // launch, early stop decided on the device; returns (T, true, launched) -- the kernel also scanned
   // s_T; launched: the registered graph of horizon T was launched on `stream`.
-  std::tuple<int, bool, bool> run_small(u64 stream, bool early_stop, bool launch_graph) {
+  // s0 / g0 (optional): the scenario's start states (B, N, 2D) and goals (B, N, D), loaded by the
+  // kernel itself.
+  std::tuple<int, bool, bool> run_small(u64 stream, bool early_stop, bool launch_graph, u64 s0, u64 g0) {
     if (!small_ctl_) throw std::runtime_error("RolloutDriver: no small-scene control buffer");
     hipStream_t st = ST(stream);
     int* ctl = P<int>(small_ctl_);
@@ -217,6 +219,8 @@ class RolloutDriver {
     a.ctl = ctl;      // zero at allocation; the kernel's last workgroup re-arms it
     a.res = small_res_dev_;
     a.res_gen = (int)++small_gen_;
+    a.s0 = P<const float>(s0); a.g0 = P<const float>(g0);
+    if ((s0 == 0) != (g0 == 0)) throw std::invalid_argument("run_small: s0 and g0 go together");
     chk((prec_ == 2 ? mb_rollout_small_x3 : prec_ == 1 ? mb_rollout_small_f16 : mb_rollout_small)(&a, st), "rollout_small");
     // the horizon arrives in host-coherent memory when the last workgroup finishes: poll it (a
     // stream synchronisation added a memset, a read-back copy and the blocking wake-up to every
@@ -535,7 +539,8 @@ void register_runtime(py::module& m) {
       .def(py::init<py::dict>())
       .def("set_bwd_graphs", &RolloutDriver::set_bwd_graphs, py::arg("execs"))
       .def("run_small", &RolloutDriver::run_small, py::arg("stream"), py::arg("early_stop"),
-           py::arg("launch_graph") = false, py::call_guard<py::gil_scoped_release>())
+           py::arg("launch_graph") = false, py::arg("s0") = 0, py::arg("g0") = 0,
+           py::call_guard<py::gil_scoped_release>())
       .def("run", &RolloutDriver::run, py::arg("stream"), py::arg("hstream"), py::arg("copy_stream"),
            py::arg("early_stop"),
            // the loop blocks on hipEventSynchronize: let other Python threads run meanwhile

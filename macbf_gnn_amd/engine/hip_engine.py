@@ -146,6 +146,8 @@ class HipEngine:
         self.bwd_graph = bool(knobs.get_int("MACBF_BWD_GRAPH", int(self.bwd_graph)))
         self._bwd_graphs = {}          # (T, grad scale) -> CUDAGraph of _counts + _backward
         self._graph_table = None       # key suffix of the graphs registered with the rollout driver
+        self._scenario = None          # (s0, g) the next small-scene rollout loads itself
+        self._kernel_scenario = bool(knobs.get_int("MACBF_KERNEL_SCENARIO", 1))
         self._graph_launch = False     # the next run_small launches the registered graph of its T
         self._launched_T = None
         self._drv_launch = bool(knobs.get_int("MACBF_GRAPH_LAUNCH", 1))
@@ -301,14 +303,23 @@ class HipEngine:
             return dict(noise_key=None)
         return dict(noise_key=self.noise_key, noise_prob=float(cfg.add_noise_prob), noise_scale=float(cfg.noise_scale))
 
-    def load_inputs(self, s0, g, obs=None):
+    def load_inputs(self, s0, g, obs=None, defer=False):
         """Scenario -> the static input buffers (start records, goals, obstacle rows) and the
-        exploration-noise key of this iteration (seed, iteration, rank)."""
+        exploration-noise key of this iteration (seed, iteration, rank). defer: the persistent
+        small-scene rollout loads the start records and goals itself (self._scenario)."""
         if self.tr.cfg.add_noise_prob > 0:
             from ..ops.scenario import iteration_key
             self.noise_key.fill_(iteration_key(self.tr.cfg.seed, int(self.tr.step_count), self.tr.dp.rank, salt=0x4E4F4953))
         B, N, D = self.B, self.N, self.D
-        if D == 2:
+        self._scenario = None
+        # (inputs the kernel cannot read as they are -- host tensors, other dtypes or layouts -- take
+        # the copies below)
+        defer = (defer and all(t.device == self.S.device and t.dtype == torch.float32 and t.is_contiguous()
+                               for t in (s0, g))
+                 and tuple(s0.shape) == (B, N, 2 * D) and tuple(g.shape) == (B, N, D))
+        if defer:
+            self._scenario = (s0, g)
+        elif D == 2:
             self.S[0, :, :N].copy_(s0)
         else:
             # 3-D records (x, y, z, 0 | vx, vy, vz, 0): two strided copies into the record halves
@@ -322,10 +333,14 @@ class HipEngine:
             # static obstacle nodes in every time slice: one strided copy of the positions (their
             # velocity and pad lanes stay zero: no kernel writes them)
             self.S[:, :, N:, :D].copy_(obs.unsqueeze(0).expand(self.Tmax + 1, B, self.M, D))
-        self.G.copy_(g)
+        if not defer:
+            self.G.copy_(g)
+        return defer
 
     def rollout(self, s0, g, obs=None, early_stop=None):
-        self.load_inputs(s0, g, obs)
+        small = (self.small_rollout and self.native_rollout and not self.graph_mode and self._kernel_scenario
+                 and not torch.cuda.is_current_stream_capturing())
+        self.load_inputs(s0, g, obs, defer=small)
         return self._rollout_steps(self.tr.cfg.early_stop if early_stop is None else early_stop)
 
     def _driver(self):
@@ -416,8 +431,11 @@ class HipEngine:
                 # one persistent launch for the whole rollout (csrc/ctrl.hip rollout_small_kernel)
                 # (step(): the registered backward graph of the horizon is launched by the driver
                 # as soon as the horizon arrives -- _backward_graphed then skips its replay)
-                T, tail_scanned, launched = self._driver().run_small(cur.cuda_stream, bool(early_stop),
-                                                                    self._graph_launch)
+                # (sc None: load_inputs already wrote S[0] / G -- graph mode's warm-up)
+                sc, self._scenario = self._scenario, None
+                T, tail_scanned, launched = self._driver().run_small(
+                    cur.cuda_stream, bool(early_stop), self._graph_launch,
+                    native.ptr(sc[0]) if sc else 0, native.ptr(sc[1]) if sc else 0)
                 self._launched_T = T if launched else None
                 return self._tail_scan(T, tail_scanned)
             # the per-step launch loop in C++ (csrc/runtime.cpp): same launches, same order
