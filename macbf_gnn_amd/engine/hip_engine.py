@@ -88,6 +88,9 @@ class HipEngine:
             raise ValueError(f"top_k <= {C.MAX_TOP_K} supported by the native kernels")
         self.Tmax = cfg.inner_loops
         self.small_rollout = self.small_rollout and self.native_rollout and self.Nn <= native.SMALL_MAXN
+        ov = knobs.get_int("MACBF_OVERLAP_HFWD", -1)
+        if ov >= 0:
+            self.overlap_hfwd = bool(ov)
         if self.small_rollout:
             self.overlap_hfwd = False     # the CBF h of all main slots runs after the one-launch rollout
         # kernel precision (csrc/prec.h): bf16 / fp16 MFMA inputs, or "fp32" -- the reference
