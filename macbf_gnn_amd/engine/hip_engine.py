@@ -91,6 +91,12 @@ class HipEngine:
         ov = knobs.get_int("MACBF_OVERLAP_HFWD", -1)
         if ov >= 0:
             self.overlap_hfwd = bool(ov)
+        elif cfg.dtype == "fp32" and 12288 <= self.B * self.N <= 24576:
+            # the 16-env per-rank work of config #3 at DP 4 (16,384 agents): the h slices fill CUs the
+            # controller step leaves idle -- 3.987-3.998 vs 4.044-4.076 ms interleaved; at 8 envs
+            # neutral (2.806-2.862 vs 2.821-2.870), at 32 envs slower (6.55-6.58 vs 6.25),
+            # profiles/r6_runs/r6ar/, r6as/
+            self.overlap_hfwd = True
         if self.small_rollout:
             self.overlap_hfwd = False     # the CBF h of all main slots runs after the one-launch rollout
         # kernel precision (csrc/prec.h): bf16 / fp16 MFMA inputs, or "fp32" -- the reference

@@ -19,7 +19,7 @@ removed (their decision is the code's default, the measurement is in docs/PERF.m
 | MACBF_NODE_ACTS | 1 | engine/hip_engine.py | 0: the cooperative node backward recomputes the node MLP instead of reusing the rollout's activations (A/B, tests) |
 | MACBF_BWD_GRAPH | 1 | engine/hip_engine.py | small scenes: post-rollout work replayed from per-T HIP graphs (0: eager, tests / A/B) |
 | MACBF_KERNEL_SCENARIO | 1 | engine/hip_engine.py | small scenes: the persistent rollout loads the start states and goals itself (0: copy launches, A/B) |
-| MACBF_OVERLAP_HFWD | (class default) | engine/hip_engine.py | 1 / 0: CBF h of each step's main slots on a side stream during the rollout (A/B) |
+| MACBF_OVERLAP_HFWD | by size | engine/hip_engine.py | 1 / 0: CBF h of each step's main slots on a side stream during the rollout (default: on for fp32 ranks of 12,288-24,576 agents, off otherwise; A/B) |
 | MACBF_GRAPH_LAUNCH | 1 | engine/hip_engine.py | small scenes: the rollout driver launches the horizon's backward graph itself (0: replay from Python, A/B) |
 | MACBF_PUBLISH | 1 | engine/hip_engine.py | early stop through a queue marker instead of kernel publication (tests) |
 | MACBF_SELFCHECK | 1 | ops/selfcheck.py | skip the start-up self-check of the 16x16x32 kernels |
