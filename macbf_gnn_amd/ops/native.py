@@ -418,16 +418,19 @@ def ctrl_fwd(S, G, idx, wpack, f_edge, f_node, wvec, A, Sn, dist_sum, act_sum, n
 
 def ctrl_fwd_apw(total_agents: int, device, n_agents: int | None = None) -> int:
     """Agents per wave of the controller step's edge phase: 32, halved (down to 4) while the
-    scene has fewer groups than four per CU, so small scenes spread the edge phase over more
-    waves (8-env strong-scaling slice, fp32: 16 / 8 / 4 agents per wave -> 4.36 / 3.82 / 3.95 ms
-    per iteration with the other small-grid choices). Any grouping gives the same results (the
-    per-env sums are per-agent fixed-point integers). MACBF_CTRL_APW overrides (A/B runs)."""
+    scene has fewer groups than eight per CU, so smaller scenes spread the edge phase over more
+    waves; scenes of >= 8,192 agents stop at 8. Measured per-rank work of config #3 (fp32,
+    interleaved, profiles/r6_runs/r6au/, r6av/, r6ap/): 65,536 agents 32 / 16 / 8 -> 10.08-10.27 /
+    10.41-10.43 / 11.02 ms; 32,768: 16 -> 5.79 vs 6.17-6.24 (32) and 6.19 (8); 16,384: 8 -> 3.88-3.90
+    vs 3.97-4.27 (16) and 4.17 (4); 8,192: 8 -> 2.80-2.82 vs 2.91-2.98 (4) and 2.91-2.96 (16). Any
+    grouping gives the same results (the per-env sums are per-agent fixed-point integers).
+    MACBF_CTRL_APW overrides (A/B runs)."""
     env = os.environ.get("MACBF_CTRL_APW")
     if env:
         return int(env)
-    apw, cap = 32, 4 * num_cu(device)
+    apw, cap = 32, 8 * num_cu(device)
     for cand in (16, 8, 4):
-        if (total_agents + apw - 1) // apw >= cap:
+        if (total_agents + apw - 1) // apw >= cap or (cand == 4 and total_agents >= 8192):
             break
         apw = cand
     return apw
