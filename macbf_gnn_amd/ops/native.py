@@ -834,16 +834,19 @@ def ctrl_edge_qsplit(total_agents: int, device) -> int:
 
 
 def node_bwd_chunk(total_agents: int, device) -> int:
-    """Agents per node-backward workgroup chunk: 128 while the chunks fill the CUs, else 64 / 32
-    (small scenes and strong-scaling slices: more, shorter workgroups; a chunk's empty stage
-    turns are skipped). MACBF_NODE_CHUNK overrides."""
+    """Agents per node-backward workgroup chunk: 128 while the chunks fill half the CUs, else 64
+    while they fill the CUs, else 32 (small scenes and strong-scaling slices: more, shorter
+    workgroups; a chunk's empty stage turns are skipped). At 16,384 agents (config #3 per rank at
+    DP 4) 128 over 64: 3.815-3.853 vs 3.873-3.888 ms interleaved (profiles/r6_runs/r6ax/, r6ay/).
+    MACBF_NODE_CHUNK overrides."""
     env = os.environ.get("MACBF_NODE_CHUNK")
     if env:
         return int(env)
     cu = num_cu(device)
-    for ca in (128, 64):
-        if (total_agents + ca - 1) // ca >= cu:
-            return ca
+    if (total_agents + 127) // 128 >= cu // 2:
+        return 128
+    if (total_agents + 63) // 64 >= cu:
+        return 64
     return 32
 
 
